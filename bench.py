@@ -1,0 +1,158 @@
+#!/usr/bin/env python
+"""Headline benchmark: LDA variational-EM throughput on a synthetic 1-day netflow corpus.
+
+Metric (BASELINE.json): "LDA docs/sec to convergence + ml_ops.sh wall-clock, 1-day netflow".
+One step = one full EM iteration of the oni-lda-c algorithm (length-bucketed fused
+E-step to per-doc convergence, deterministic sufficient statistics, RCCL all-reduce
+when N > 1, M-step, alpha Newton).  value = documents processed per second summed
+over all ranks (docs x timed EM iterations / max-over-ranks wall time).
+
+Scaling is weak: every rank holds its own synthetic 1-day netflow corpus (same
+generator, rank-specific seed), i.e. N GPUs model an N-day corpus with per-day
+documents.  Data are synthetic, weights random-init (lda-c "random" start).
+
+  python bench.py --gpus N --steps K --warmup W
+  (N > 1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...)
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "LDA docs/sec to convergence + ml_ops.sh wall-clock, 1-day netflow"
+BASELINE_DOCS_PER_SEC = None  # filled from BASELINE.md once the CPU reference baseline is measured
+
+
+def _baseline():
+    try:
+        with open(os.path.join(ROOT, "BASELINE.json")) as f:
+            b = json.load(f)
+        v = b.get("measured_baseline", {}).get("lda_docs_per_sec")
+        return float(v) if v else None
+    except Exception:
+        return None
+
+
+def build_corpus(args, rank):
+    seed = args.seed + 1000 * rank
+    if args.corpus == "planted":
+        from oni_ml_amd.synth.corpus import planted_corpus
+        return planted_corpus(num_docs=args.docs, num_terms=args.vocab, num_topics=24, mean_tokens=25,
+                              tail=1.1, max_tokens=300_000, seed=seed), {}
+    from oni_ml_amd.pipeline.flow import synthetic_flow_corpus
+    c, info = synthetic_flow_corpus(events=args.events, seed=seed)
+    return c, info
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--topics", type=int, default=20)
+    ap.add_argument("--events", type=int, default=1_000_000)
+    ap.add_argument("--corpus", choices=["flow", "planted"], default="flow")
+    ap.add_argument("--docs", type=int, default=80_000)
+    ap.add_argument("--vocab", type=int, default=8_000)
+    ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--converge", type=int, default=1, help="also time a full random-init run to convergence")
+    args = ap.parse_args()
+
+    from oni_ml_amd.parallel import dist as D
+    ctx = D.init_from_env(expected_world=args.gpus)
+    rank, world = ctx.rank, ctx.world_size
+    dev = ctx.device
+
+    from oni_ml_amd.models.lda.em import LDAEngine
+    from oni_ml_amd.models.lda.settings import LDASettings
+
+    t0 = time.perf_counter()
+    corpus, info = build_corpus(args, rank)
+    t_corpus = time.perf_counter() - t0
+    # weak scaling: each rank's corpus is its own shard
+    eng = LDAEngine(corpus, args.topics, LDASettings(), backend="hip", device=dev,
+                    dist=ctx if world > 1 else None, seed=args.seed, local_shard=True)
+    eng.init_random()
+    docs_global = ctx.allreduce_int(corpus.num_docs)
+
+    def step():
+        sc = eng.e_step()
+        if world > 1:
+            sc = ctx.allreduce_suffstats(eng.cw, sc)
+        host = sc.cpu().tolist()
+        eng.m_step(True, float(host[1]), docs_global)
+        return host[0]
+
+    for _ in range(args.warmup):
+        step()
+    ctx.barrier()
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    for _ in range(args.steps):
+        lik = step()
+    torch.cuda.synchronize()
+    ctx.barrier()
+    dt = time.perf_counter() - t1
+    dt = ctx.allreduce_max(dt)
+    ms = dt / args.steps * 1e3
+    value = docs_global * args.steps / dt
+
+    extra = {}
+    if args.converge:
+        eng2 = LDAEngine(corpus, args.topics, LDASettings(), backend="hip", device=dev,
+                         dist=ctx if world > 1 else None, seed=args.seed + 1, local_shard=True)
+        ctx.barrier()
+        torch.cuda.synchronize()
+        t2 = time.perf_counter()
+        res = eng2.run()
+        torch.cuda.synchronize()
+        tc = ctx.allreduce_max(time.perf_counter() - t2)
+        extra = dict(converge_seconds=round(tc, 4), converge_em_iters=res.em_iterations,
+                     converge_docs_per_sec=round(docs_global * res.em_iterations / tc, 1),
+                     final_likelihood=res.likelihoods[-1][0])
+    base = _baseline()
+    if rank == 0:
+        out = {
+            "metric": METRIC,
+            "value": round(value, 1),
+            "unit": "docs/s (docs x EM iterations / s, all ranks)",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": (round(value / base, 2) if base else None),
+            "dtype": "fp32 E-step / fp64 likelihood+alpha (reference lda-c: fp64)",
+            "data": "synthetic (1-day netflow per GPU, random-init topics)",
+            "config": {
+                "model": f"oni-lda-c variational EM LDA, K={args.topics}",
+                "global_batch": docs_global,
+                "seq_len": int(round(corpus.nnz / max(1, corpus.num_docs))),
+                "parallelism": f"dp{world}",
+                "corpus": args.corpus,
+                "events_per_gpu": args.events if args.corpus == "flow" else None,
+                "docs_per_gpu": corpus.num_docs,
+                "vocab": corpus.num_terms,
+                "nnz_per_gpu": corpus.nnz,
+                "max_doc_len": int(corpus.lengths().max()),
+            },
+            "corpus_build_s": round(t_corpus, 3),
+            **info,
+            **extra,
+        }
+        print(json.dumps(out), flush=True)
+    ctx.shutdown()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,123 @@
+// pybind11 module `_onihip`: thin launch bindings for the gfx950 kernels.
+//
+// Arguments are raw device addresses (torch tensor .data_ptr()) and the HIP
+// stream handle of the caller (torch.cuda.current_stream().cuda_stream), so
+// launches join torch's stream order and can be captured into hipGraphs.
+// Shape/dtype/contiguity validation happens in oni_ml_amd/ops/hip.py before
+// any launch.
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "common.h"
+#include "kernels.h"
+
+namespace py = pybind11;
+using u = uintptr_t;
+
+template <typename T>
+static T* P(u x) {
+  return reinterpret_cast<T*>(x);
+}
+static hipStream_t S(u x) { return reinterpret_cast<hipStream_t>(x); }
+
+PYBIND11_MODULE(_onihip, m) {
+  m.doc() = "oni_ml_amd CDNA4 (gfx950) HIP kernels";
+
+  m.def("compiled_ks", []() {
+    std::vector<int> v;
+#define ONI_KS(X) v.push_back(X);
+    ONI_FOR_EACH_KS(ONI_KS)
+#undef ONI_KS
+    return v;
+  });
+
+  m.def("device_name", []() {
+    hipDeviceProp_t p;
+    int dev = 0;
+    ONI_HIP_CHECK(hipGetDevice(&dev));
+    ONI_HIP_CHECK(hipGetDeviceProperties(&p, dev));
+    return std::string(p.gcnArchName);
+  });
+
+  m.def(
+      "lda_estep",
+      [](u doc_ptr, u word_idx, u counts, u order, int n_items, u beta, int K, int KS, float alpha,
+         double lik_const, int var_max_iter, float var_conv, u gamma, u e_out, u r_out, u lik, u alpha_ss,
+         u iters, int variant, u stream) {
+        oni::EStepArgs a{P<const int>(doc_ptr), P<const int>(word_idx), P<const float>(counts),
+                         P<const int>(order),   n_items,              P<const float>(beta),
+                         K,                     alpha,                lik_const,
+                         var_max_iter,          var_conv,             P<float>(gamma),
+                         P<float>(e_out),       P<float>(r_out),      P<double>(lik),
+                         P<double>(alpha_ss),   P<int>(iters)};
+        oni::launch_lda_estep(a, variant, KS, S(stream));
+      });
+
+  m.def("lda_suffstats", [](u word_ptr, u csc_ent, u csc_doc, u order, int n_items, u e, u r, u beta, u cw,
+                            int KS, int variant, u stream) {
+    oni::SuffArgs a{P<const int>(word_ptr), P<const int>(csc_ent), P<const int>(csc_doc),
+                    P<const int>(order),    n_items,               P<const float>(e),
+                    P<const float>(r),      P<const float>(beta),  P<float>(cw)};
+    oni::launch_lda_suffstats(a, variant, KS, S(stream));
+  });
+
+  m.def("lda_mstep", [](u cw, u class_total, u beta, int V, int K, int KS, u stream) {
+    oni::launch_lda_mstep(P<const float>(cw), P<const double>(class_total), P<float>(beta), V, K, KS,
+                          S(stream));
+  });
+
+  m.def("score_events", [](u theta, u phi, int K, double dflt, u doc_a, u word_a, u doc_b, u word_b,
+                           int64_t n, double tol, u score_a, u score_b, u key, u flag, u stream) {
+    oni::ScoreArgs a{P<const double>(theta), P<const double>(phi), K, dflt,
+                     P<const int>(doc_a),    P<const int>(word_a), P<const int>(doc_b),
+                     P<const int>(word_b),   n,                    tol,
+                     P<double>(score_a),     P<double>(score_b),   P<double>(key),
+                     P<uint8_t>(flag)};
+    oni::launch_score_events(a, S(stream));
+  });
+
+  m.def("flow_words", [](u hour, u minute, u second, u port_a, u port_b, u ipkt, u ibyt, u time_cuts,
+                         int n_time, u ibyt_cuts, int n_ibyt, u ipkt_cuts, int n_ipkt, int64_t n, u time_out,
+                         u time_bin, u ibyt_bin, u ipkt_bin, u word_port, u p_case, u src_prefix,
+                         u dst_prefix, u stream) {
+    oni::FlowWordArgs a{};
+    a.hour = P<const double>(hour);
+    a.minute = P<const double>(minute);
+    a.second = P<const double>(second);
+    a.port_a = P<const double>(port_a);
+    a.port_b = P<const double>(port_b);
+    a.ipkt = P<const double>(ipkt);
+    a.ibyt = P<const double>(ibyt);
+    a.time_cuts = P<const double>(time_cuts);
+    a.ibyt_cuts = P<const double>(ibyt_cuts);
+    a.ipkt_cuts = P<const double>(ipkt_cuts);
+    a.n_time_cuts = n_time;
+    a.n_ibyt_cuts = n_ibyt;
+    a.n_ipkt_cuts = n_ipkt;
+    a.n = n;
+    a.time_out = P<double>(time_out);
+    a.time_bin = P<int8_t>(time_bin);
+    a.ibyt_bin = P<int8_t>(ibyt_bin);
+    a.ipkt_bin = P<int8_t>(ipkt_bin);
+    a.word_port = P<double>(word_port);
+    a.p_case = P<int8_t>(p_case);
+    a.src_prefix = P<int8_t>(src_prefix);
+    a.dst_prefix = P<int8_t>(dst_prefix);
+    oni::launch_flow_words(a, S(stream));
+  });
+
+  m.def("bin_columns", [](std::vector<u> values, std::vector<u> cuts, std::vector<int> ncuts, int64_t n,
+                          u bins, u stream) {
+    if (values.size() != cuts.size() || values.size() != ncuts.size())
+      throw std::runtime_error("bin_columns: column lists differ in length");
+    std::vector<const double*> v, c;
+    for (auto x : values) v.push_back(P<const double>(x));
+    for (auto x : cuts) c.push_back(P<const double>(x));
+    oni::launch_bin_columns(v.data(), c.data(), ncuts.data(), (int)values.size(), n, P<int8_t>(bins),
+                            S(stream));
+  });
+}

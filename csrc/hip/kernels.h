@@ -1,0 +1,113 @@
+// Host-visible launch interface of the oni_ml_amd HIP kernels (gfx950).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace oni {
+
+// Padded topic counts (row stride of word-major beta, multiple of 4) that have
+// compiled kernel instantiations.  Any K is served by the next larger entry;
+// padding topics carry beta = 0 and are masked in the per-topic phase.
+#define ONI_FOR_EACH_KS(X) X(8) X(12) X(16) X(20) X(24) X(32) X(52) X(64) X(100) X(128)
+
+// ---------------------------------------------------------------- E-step ---
+enum EStepVariant : int {
+  kEStepG16 = 0,   // 16 lanes/doc, 16 docs per 256-thread block
+  kEStepG32 = 1,   // 32 lanes/doc
+  kEStepG64 = 2,   // one wave per doc
+  kEStepG64C = 3,  // one wave per doc, several beta rows cached per lane
+  kEStepB4 = 4,    // one doc per 4-wave workgroup
+  kEStepB8 = 5,    // one doc per 8-wave workgroup (longest docs)
+};
+
+struct EStepArgs {
+  const int* doc_ptr;     // [D+1] CSR offsets
+  const int* word_idx;    // [nnz]
+  const float* counts;    // [nnz]
+  const int* order;       // [n_items] doc ids of this bucket
+  int n_items;
+  const float* beta;      // [V][KS]  exp(log p(w|z)), word-major
+  int K;                  // real topic count
+  float alpha;
+  double lik_const;       // lgamma(K*alpha) - K*lgamma(alpha)
+  int var_max_iter;       // -1 = unbounded
+  float var_conv;
+  float* gamma;           // [D][KS]
+  float* e_out;           // [D][KS]
+  float* r_out;           // [nnz]
+  double* lik;            // [D]
+  double* alpha_ss;       // [D]
+  int* iters;             // [D]
+};
+void launch_lda_estep(const EStepArgs& a, int variant, int KS, hipStream_t s);
+
+// ------------------------------------------------------------ suff stats ---
+enum SuffVariant : int { kSuffG16 = 0, kSuffG64 = 1, kSuffB8 = 2 };
+
+struct SuffArgs {
+  const int* word_ptr;    // [V+1] CSC offsets (entries of each word)
+  const int* csc_ent;     // [nnz] CSR entry index of each CSC slot
+  const int* csc_doc;     // [nnz] document of each CSC slot
+  const int* order;       // [n_items] word ids of this bucket
+  int n_items;
+  const float* e;         // [D][KS]
+  const float* r;         // [nnz]
+  const float* beta;      // [V][KS]
+  float* cw;              // [V][KS] class_word (word-major), written for listed words
+};
+void launch_lda_suffstats(const SuffArgs& a, int variant, int KS, hipStream_t s);
+
+// ----------------------------------------------------------------- M-step ---
+// beta[w][k] = cw/ct_k if cw > 0 else exp(-100) (k < K); 0 for padding topics.
+void launch_lda_mstep(const float* cw, const double* class_total, float* beta, int V, int K, int KS,
+                      hipStream_t s);
+
+// ---------------------------------------------------------------- scoring ---
+struct ScoreArgs {
+  const double* theta;    // [D][K] p(z|d)
+  const double* phi;      // [V][K] p(w|z)
+  int K;                  // topics summed (reference: 20)
+  double dflt;            // value of the default vector used for misses
+  const int* doc_a;       // [n] doc index or -1
+  const int* word_a;      // [n] word index or -1
+  const int* doc_b;       // [n] (flow: destination side) or nullptr
+  const int* word_b;      // [n]
+  int64_t n;
+  double tol;
+  double* score_a;        // [n]
+  double* score_b;        // [n] or nullptr
+  double* key;            // [n] min(score_a, score_b) (or score_a)
+  uint8_t* flag;          // [n] key < tol
+};
+void launch_score_events(const ScoreArgs& a, hipStream_t s);
+
+// ------------------------------------------------------------ flow words ---
+struct FlowWordArgs {
+  const double* hour;      // [n] col 4
+  const double* minute;    // [n] col 5
+  const double* second;    // [n] col 6
+  const double* port_a;    // [n] col 10 (reference variable name: dport)
+  const double* port_b;    // [n] col 11 (reference variable name: sport)
+  const double* ipkt;      // [n] col 16
+  const double* ibyt;      // [n] col 17
+  const double* time_cuts; // [n_time_cuts]
+  const double* ibyt_cuts;
+  const double* ipkt_cuts;
+  int n_time_cuts, n_ibyt_cuts, n_ipkt_cuts;
+  int64_t n;
+  double* time_out;        // [n] col 27
+  int8_t* time_bin;        // [n]
+  int8_t* ibyt_bin;        // [n]
+  int8_t* ipkt_bin;        // [n]
+  double* word_port;       // [n]
+  int8_t* p_case;          // [n]
+  int8_t* src_prefix;      // [n] 1 if src word carries "-1_"
+  int8_t* dst_prefix;      // [n]
+};
+void launch_flow_words(const FlowWordArgs& a, hipStream_t s);
+
+// bins[i*ncols + c] = #{cut in cuts_c : value_c[i] > cut}   (generic binning)
+void launch_bin_columns(const double* const* values, const double* const* cuts, const int* ncuts,
+                        int ncols, int64_t n, int8_t* bins, hipStream_t s);
+
+}  // namespace oni

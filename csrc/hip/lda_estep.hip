@@ -1,0 +1,510 @@
+// Fused variational E-step for LDA on CDNA4 (gfx950).
+//
+// Reference semantics: oni-lda-c `lda_inference` + `compute_likelihood`
+// (call site /root/reference/ml_ops.sh:80).  lda-c updates
+// gamma after every word (Gauss-Seidel, K digammas per word).  Here the doc is
+// updated in Jacobi form, which has the same fixed point:
+//
+//   E_k      = exp(psi(gamma_k) - m)               (m = max_k psi, scale-free)
+//   P_n      = sum_k E_k * beta[w_n][k]            (phinorm, scaled by e^-m)
+//   gamma'_k = alpha + E_k * sum_n (c_n / P_n) beta[w_n][k]
+//
+// and the per-doc likelihood is evaluated in closed form (no per-(n,k) log):
+//
+//   L = lnG(K a) - K lnG(a) - lnG(S') + sum_k [(a-1)Y_k + lnG(g'_k) - (g'_k-1)Y_k
+//       + (g'_k - a)(psi(g'_k) - psi(g_k))] + sum_n c_n (ln P_n + m) - T psi(S')
+//   Y_k = psi(g'_k) - psi(S'),  S' = sum_k g'_k,  T = sum_n c_n
+//
+// which equals lda-c's compute_likelihood(phi(g), g') exactly in exact arithmetic.
+// Convergence follows lda-c: iterate while (L_old - L)/L_old > var_conv and
+// it < var_max_iter (-1 = unbounded), L_old starting at 0.
+//
+// Work decomposition (length-bucketed):
+//   lda_estep_group<KS,G,CW>: G lanes (16/32/64) per document, 256/G docs per
+//     block; lanes stride over words; the doc's first CW*G beta rows stay in
+//     VGPRs across all variational iterations; per-topic transcendentals are
+//     spread over lanes (topic k on lane k mod G); E is broadcast through LDS.
+//   lda_estep_block<KS,NW,CW>: one long document per NW-wave workgroup (the
+//     "long-context" analogue): words striped over NW*64 lanes, cross-wave
+//     sums through LDS, wave 0 owns the per-topic state.
+// Outputs per doc: gamma, the E vector of the final phi, r_n = c_n/P_n (so the
+// sufficient statistics can be formed deterministically in lda_suffstats),
+// likelihood, alpha sufficient statistic and the variational iteration count.
+#include <stdexcept>
+#include <string>
+
+#include "common.h"
+#include "kernels.h"
+
+namespace oni {
+
+namespace {
+
+template <int KS>
+__device__ __forceinline__ void load_row(const float* __restrict__ beta, int w, float (&row)[KS]) {
+  const float4* p = reinterpret_cast<const float4*>(beta + (size_t)w * KS);
+#pragma unroll
+  for (int j = 0; j < KS / 4; ++j) {
+    float4 v = p[j];
+    row[4 * j + 0] = v.x;
+    row[4 * j + 1] = v.y;
+    row[4 * j + 2] = v.z;
+    row[4 * j + 3] = v.w;
+  }
+}
+
+// P = sum_k E_k * row_k with E read from LDS (broadcast: every lane of a group
+// reads the same address).
+template <int KS>
+__device__ __forceinline__ float dot_lds(const float* sE, const float (&row)[KS]) {
+  const float4* e4 = reinterpret_cast<const float4*>(sE);
+  float p0 = 0.f, p1 = 0.f;
+#pragma unroll
+  for (int j = 0; j < KS / 4; ++j) {
+    float4 e = e4[j];
+    p0 = fmaf(e.x, row[4 * j + 0], p0);
+    p1 = fmaf(e.y, row[4 * j + 1], p1);
+    p0 = fmaf(e.z, row[4 * j + 2], p0);
+    p1 = fmaf(e.w, row[4 * j + 3], p1);
+  }
+  return p0 + p1;
+}
+
+constexpr float kPMin = 1e-30f;
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// Group kernel: G lanes per document.
+// ---------------------------------------------------------------------------
+template <int KS, int G, int CW>
+__global__ __launch_bounds__(256) void lda_estep_group(EStepArgs a) {
+  constexpr int GPB = 256 / G;
+  constexpr int TJ = (KS + G - 1) / G;
+  __shared__ float4 sE4[GPB][KS / 4];
+
+  const int t = threadIdx.x % G;
+  const int g = threadIdx.x / G;
+  const int item = blockIdx.x * GPB + g;
+  if (item >= a.n_items) return;  // group-uniform exit
+  float* sE = reinterpret_cast<float*>(&sE4[g][0]);
+
+  const int d = a.order[item];
+  const int beg = a.doc_ptr[d];
+  const int N = a.doc_ptr[d + 1] - beg;
+  const int K = a.K;
+  const float alpha = a.alpha;
+
+  // ---- stage this lane's first CW words in registers ----
+  float bc[CW][KS];
+  float cc[CW];
+  double tot_l = 0.0;
+#pragma unroll
+  for (int c = 0; c < CW; ++c) {
+    const int n = t + G * c;
+    if (n < N) {
+      const int w = a.word_idx[beg + n];
+      cc[c] = a.counts[beg + n];
+      load_row<KS>(a.beta, w, bc[c]);
+    } else {
+      cc[c] = 0.f;
+#pragma unroll
+      for (int k = 0; k < KS; ++k) bc[c][k] = 0.f;
+    }
+    tot_l += cc[c];
+  }
+  for (int n = t + G * CW; n < N; n += G) tot_l += a.counts[beg + n];
+  const double total = group_sum<G>(tot_l);
+  const float totalf = (float)total;
+
+  // ---- per-topic state (topic k = t + G*j) ----
+  float gam[TJ], psi[TJ], e[TJ];
+  const float g0 = alpha + (float)(total / K);
+#pragma unroll
+  for (int j = 0; j < TJ; ++j) {
+    const int k = t + G * j;
+    gam[j] = (k < K) ? g0 : 0.f;
+    psi[j] = (k < K) ? digammaf_ldac(g0) : -INFINITY;
+    e[j] = 0.f;
+  }
+
+  double lik_old = 0.0, L = 0.0, conv = 1.0, dsum_last = 0.0;
+  int it = 0;
+  float m = 0.f;
+  const bool unbounded = a.var_max_iter < 0;
+
+  while (conv > (double)a.var_conv && (unbounded || it < a.var_max_iter)) {
+    ++it;
+    // E_k = exp(psi_k - m)
+    float mx = -INFINITY;
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) mx = fmaxf(mx, psi[j]);
+    m = group_max<G>(mx);
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) {
+      const int k = t + G * j;
+      e[j] = (k < K) ? __expf(psi[j] - m) : 0.f;
+      if (k < KS) sE[k] = e[j];
+    }
+    wave_lds_sync();
+
+    // ---- word pass ----
+    float acc[KS];
+#pragma unroll
+    for (int k = 0; k < KS; ++k) acc[k] = 0.f;
+    float lsum = 0.f;
+#pragma unroll
+    for (int c = 0; c < CW; ++c) {
+      if (t + G * c < N) {
+        const float P = fmaxf(dot_lds<KS>(sE, bc[c]), kPMin);
+        const float r = cc[c] / P;
+        lsum = fmaf(cc[c], __logf(P), lsum);
+#pragma unroll
+        for (int k = 0; k < KS; ++k) acc[k] = fmaf(r, bc[c][k], acc[k]);
+      }
+    }
+    for (int n = t + G * CW; n < N; n += G) {
+      float row[KS];
+      const int w = a.word_idx[beg + n];
+      const float cnt = a.counts[beg + n];
+      load_row<KS>(a.beta, w, row);
+      const float P = fmaxf(dot_lds<KS>(sE, row), kPMin);
+      const float r = cnt / P;
+      lsum = fmaf(cnt, __logf(P), lsum);
+#pragma unroll
+      for (int k = 0; k < KS; ++k) acc[k] = fmaf(r, row[k], acc[k]);
+    }
+    group_sum_vec<G, KS>(acc);
+    const double lsum_d = group_sum<G>((double)lsum);
+
+    // ---- topic phase: gamma update + likelihood ----
+    float gn[TJ];
+    float sg = 0.f;
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) {
+      const int k = t + G * j;
+      float ak = 0.f;
+#pragma unroll
+      for (int i = 0; i < KS; ++i) ak = (i == k) ? acc[i] : ak;
+      gn[j] = (k < K) ? fmaf(e[j], ak, alpha) : 0.f;
+      sg += gn[j];
+    }
+    const float S = group_sum<G>(sg);
+    const float dS = digammaf_ldac(S);
+    double term = 0.0;
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) {
+      const int k = t + G * j;
+      if (k < K) {
+        const float pn = digammaf_ldac(gn[j]);
+        const float y = pn - dS;
+        term += (double)((alpha - 1.f) * y) + (double)lgammaf(gn[j]) - (double)((gn[j] - 1.f) * y) +
+                (double)((gn[j] - alpha) * (pn - psi[j]));
+        psi[j] = pn;
+        gam[j] = gn[j];
+      }
+    }
+    term = group_sum<G>(term);
+    L = a.lik_const - (double)lgammaf(S) + term + (lsum_d + (double)m * total) - total * (double)dS;
+    conv = (lik_old - L) / lik_old;
+    lik_old = L;
+    dsum_last = dS;
+  }
+
+  if (it == 0) {  // var_max_iter == 0: phi from the initial gamma
+    float mx = -INFINITY;
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) mx = fmaxf(mx, psi[j]);
+    m = group_max<G>(mx);
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) {
+      const int k = t + G * j;
+      e[j] = (k < K) ? __expf(psi[j] - m) : 0.f;
+      if (k < KS) sE[k] = e[j];
+    }
+    float sg = 0.f;
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) sg += gam[j];
+    dsum_last = digammaf_ldac(group_sum<G>(sg));
+    wave_lds_sync();
+  }
+
+  // ---- outputs ----
+  double ass = 0.0;
+#pragma unroll
+  for (int j = 0; j < TJ; ++j) {
+    const int k = t + G * j;
+    if (k < KS) {
+      a.gamma[(size_t)d * KS + k] = gam[j];
+      a.e_out[(size_t)d * KS + k] = e[j];
+    }
+    if (k < K) ass += (double)psi[j];
+  }
+  ass = group_sum<G>(ass);
+#pragma unroll
+  for (int c = 0; c < CW; ++c) {
+    const int n = t + G * c;
+    if (n < N) a.r_out[beg + n] = cc[c] / fmaxf(dot_lds<KS>(sE, bc[c]), kPMin);
+  }
+  for (int n = t + G * CW; n < N; n += G) {
+    float row[KS];
+    load_row<KS>(a.beta, a.word_idx[beg + n], row);
+    a.r_out[beg + n] = a.counts[beg + n] / fmaxf(dot_lds<KS>(sE, row), kPMin);
+  }
+  if (t == 0) {
+    a.lik[d] = L;
+    a.alpha_ss[d] = ass - (double)K * dsum_last;
+    a.iters[d] = it;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Block kernel: one long document per workgroup of NW waves.
+// ---------------------------------------------------------------------------
+template <int KS, int NW, int CW>
+__global__ __launch_bounds__(NW * 64) void lda_estep_block(EStepArgs a) {
+  constexpr int NT = NW * 64;
+  constexpr int TJ = (KS + 63) / 64;  // topics per lane of wave 0
+  __shared__ float4 sE4[KS / 4];
+  __shared__ float sRed[NW][KS];
+  __shared__ double sRedD[NW][2];
+  __shared__ int sFlag;
+
+  const int t = threadIdx.x;
+  const int lane = t & 63;
+  const int wv = t >> 6;
+  const int d = a.order[blockIdx.x];
+  const int beg = a.doc_ptr[d];
+  const int N = a.doc_ptr[d + 1] - beg;
+  const int K = a.K;
+  const float alpha = a.alpha;
+  float* sE = reinterpret_cast<float*>(&sE4[0]);
+
+  float bc[CW][KS];
+  float cc[CW];
+  double tot_l = 0.0;
+#pragma unroll
+  for (int c = 0; c < CW; ++c) {
+    const int n = t + NT * c;
+    if (n < N) {
+      cc[c] = a.counts[beg + n];
+      load_row<KS>(a.beta, a.word_idx[beg + n], bc[c]);
+    } else {
+      cc[c] = 0.f;
+#pragma unroll
+      for (int k = 0; k < KS; ++k) bc[c][k] = 0.f;
+    }
+    tot_l += cc[c];
+  }
+  for (int n = t + NT * CW; n < N; n += NT) tot_l += a.counts[beg + n];
+  tot_l = group_sum<64>(tot_l);
+  if (lane == 0) sRedD[wv][0] = tot_l;
+  __syncthreads();
+  double total = 0.0;
+#pragma unroll
+  for (int w = 0; w < NW; ++w) total += sRedD[w][0];
+  __syncthreads();
+
+  // wave 0 owns topic state
+  float gam[TJ], psi[TJ], e[TJ];
+  const float g0 = alpha + (float)(total / K);
+  double lik_old = 0.0, L = 0.0, conv = 1.0, dsum_last = 0.0;
+  float m = 0.f;
+  int it = 0;
+  const bool unbounded = a.var_max_iter < 0;
+  if (wv == 0) {
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) {
+      const int k = lane + 64 * j;
+      gam[j] = (k < K) ? g0 : 0.f;
+      psi[j] = (k < K) ? digammaf_ldac(g0) : -INFINITY;
+      e[j] = 0.f;
+    }
+    // first E
+    float mx = -INFINITY;
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) mx = fmaxf(mx, psi[j]);
+    m = group_max<64>(mx);
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) {
+      const int k = lane + 64 * j;
+      e[j] = (k < K) ? __expf(psi[j] - m) : 0.f;
+      if (k < KS) sE[k] = e[j];
+    }
+    float sg = 0.f;
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) sg += gam[j];
+    dsum_last = digammaf_ldac(group_sum<64>(sg));
+    if (lane == 0) sFlag = (unbounded || a.var_max_iter > 0) ? 1 : 0;
+  }
+  __syncthreads();
+
+  while (sFlag) {
+    // ---- word pass (all waves) ----
+    float acc[KS];
+#pragma unroll
+    for (int k = 0; k < KS; ++k) acc[k] = 0.f;
+    float lsum = 0.f;
+#pragma unroll
+    for (int c = 0; c < CW; ++c) {
+      if (t + NT * c < N) {
+        const float P = fmaxf(dot_lds<KS>(sE, bc[c]), kPMin);
+        const float r = cc[c] / P;
+        lsum = fmaf(cc[c], __logf(P), lsum);
+#pragma unroll
+        for (int k = 0; k < KS; ++k) acc[k] = fmaf(r, bc[c][k], acc[k]);
+      }
+    }
+    for (int n = t + NT * CW; n < N; n += NT) {
+      float row[KS];
+      const float cnt = a.counts[beg + n];
+      load_row<KS>(a.beta, a.word_idx[beg + n], row);
+      const float P = fmaxf(dot_lds<KS>(sE, row), kPMin);
+      const float r = cnt / P;
+      lsum = fmaf(cnt, __logf(P), lsum);
+#pragma unroll
+      for (int k = 0; k < KS; ++k) acc[k] = fmaf(r, row[k], acc[k]);
+    }
+    group_sum_vec<64, KS>(acc);
+    const double lsum_w = group_sum<64>((double)lsum);
+    if (lane == 0) {
+#pragma unroll
+      for (int k = 0; k < KS; ++k) sRed[wv][k] = acc[k];
+      sRedD[wv][1] = lsum_w;
+    }
+    __syncthreads();
+
+    // ---- topic phase (wave 0) ----
+    if (wv == 0) {
+      ++it;
+      double lsum_d = 0.0;
+#pragma unroll
+      for (int w = 0; w < NW; ++w) lsum_d += sRedD[w][1];
+      float gn[TJ];
+      float sg = 0.f;
+#pragma unroll
+      for (int j = 0; j < TJ; ++j) {
+        const int k = lane + 64 * j;
+        float ak = 0.f;
+        if (k < KS) {
+#pragma unroll
+          for (int w = 0; w < NW; ++w) ak += sRed[w][k];
+        }
+        gn[j] = (k < K) ? fmaf(e[j], ak, alpha) : 0.f;
+        sg += gn[j];
+      }
+      const float S = group_sum<64>(sg);
+      const float dS = digammaf_ldac(S);
+      double term = 0.0;
+#pragma unroll
+      for (int j = 0; j < TJ; ++j) {
+        const int k = lane + 64 * j;
+        if (k < K) {
+          const float pn = digammaf_ldac(gn[j]);
+          const float y = pn - dS;
+          term += (double)((alpha - 1.f) * y) + (double)lgammaf(gn[j]) - (double)((gn[j] - 1.f) * y) +
+                  (double)((gn[j] - alpha) * (pn - psi[j]));
+          psi[j] = pn;
+          gam[j] = gn[j];
+        }
+      }
+      term = group_sum<64>(term);
+      L = a.lik_const - (double)lgammaf(S) + term + (lsum_d + (double)m * total) - total * (double)dS;
+      conv = (lik_old - L) / lik_old;
+      lik_old = L;
+      dsum_last = dS;
+      const bool cont = conv > (double)a.var_conv && (unbounded || it < a.var_max_iter);
+      if (cont) {  // next E (keeps sE = E of the final phi when stopping)
+        float mx = -INFINITY;
+#pragma unroll
+        for (int j = 0; j < TJ; ++j) mx = fmaxf(mx, psi[j]);
+        m = group_max<64>(mx);
+#pragma unroll
+        for (int j = 0; j < TJ; ++j) {
+          const int k = lane + 64 * j;
+          e[j] = (k < K) ? __expf(psi[j] - m) : 0.f;
+          if (k < KS) sE[k] = e[j];
+        }
+      }
+      if (lane == 0) sFlag = cont ? 1 : 0;
+    }
+    __syncthreads();
+  }
+
+  // ---- outputs ----
+#pragma unroll
+  for (int c = 0; c < CW; ++c) {
+    const int n = t + NT * c;
+    if (n < N) a.r_out[beg + n] = cc[c] / fmaxf(dot_lds<KS>(sE, bc[c]), kPMin);
+  }
+  for (int n = t + NT * CW; n < N; n += NT) {
+    float row[KS];
+    load_row<KS>(a.beta, a.word_idx[beg + n], row);
+    a.r_out[beg + n] = a.counts[beg + n] / fmaxf(dot_lds<KS>(sE, row), kPMin);
+  }
+  if (wv == 0) {
+    double ass = 0.0;
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) {
+      const int k = lane + 64 * j;
+      if (k < KS) {
+        a.gamma[(size_t)d * KS + k] = gam[j];
+        a.e_out[(size_t)d * KS + k] = sE[k];
+      }
+      if (k < K) ass += (double)psi[j];
+    }
+    ass = group_sum<64>(ass);
+    if (lane == 0) {
+      a.lik[d] = L;
+      a.alpha_ss[d] = ass - (double)K * dsum_last;
+      a.iters[d] = it;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Host launcher
+// ---------------------------------------------------------------------------
+template <int KS>
+static void launch_ks(const EStepArgs& a, int variant, hipStream_t s) {
+  if (a.n_items <= 0) return;
+  constexpr int CWS = KS <= 32 ? 4 : (KS <= 64 ? 2 : 1);
+  switch (variant) {
+    case kEStepG16:
+      hipLaunchKernelGGL((lda_estep_group<KS, 16, 1>), dim3((a.n_items + 15) / 16), dim3(256), 0, s, a);
+      break;
+    case kEStepG32:
+      hipLaunchKernelGGL((lda_estep_group<KS, 32, 1>), dim3((a.n_items + 7) / 8), dim3(256), 0, s, a);
+      break;
+    case kEStepG64:
+      hipLaunchKernelGGL((lda_estep_group<KS, 64, 1>), dim3((a.n_items + 3) / 4), dim3(256), 0, s, a);
+      break;
+    case kEStepG64C:
+      hipLaunchKernelGGL((lda_estep_group<KS, 64, CWS>), dim3((a.n_items + 3) / 4), dim3(256), 0, s, a);
+      break;
+    case kEStepB4:
+      hipLaunchKernelGGL((lda_estep_block<KS, 4, CWS>), dim3(a.n_items), dim3(256), 0, s, a);
+      break;
+    case kEStepB8:
+      hipLaunchKernelGGL((lda_estep_block<KS, 8, (CWS > 2 ? 2 : CWS)>), dim3(a.n_items), dim3(512), 0, s, a);
+      break;
+    default:
+      throw std::runtime_error("lda_estep: unknown variant");
+  }
+  ONI_HIP_CHECK(hipGetLastError());
+}
+
+void launch_lda_estep(const EStepArgs& a, int variant, int KS, hipStream_t s) {
+  switch (KS) {
+#define ONI_KS(X) \
+  case X:         \
+    launch_ks<X>(a, variant, s); \
+    break;
+    ONI_FOR_EACH_KS(ONI_KS)
+#undef ONI_KS
+    default:
+      throw std::runtime_error("lda_estep: unsupported padded topic count " + std::to_string(KS));
+  }
+}
+
+}  // namespace oni

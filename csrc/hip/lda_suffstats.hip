@@ -1,0 +1,148 @@
+// Deterministic LDA sufficient statistics (lda-c doc_e_step):
+//
+//   class_word[w][k] = sum_{(d,n): w_n = w} c_n phi_nk
+//                    = beta[w][k] * sum_{d in docs(w)} E[d][k] * r_{d,n}
+//
+// where E and r = c/P come from the fused E-step.  Instead of nnz*K float
+// atomics (an order-dependent, atomic-rate-bound scatter), the corpus is also
+// held in CSC (word-major) order and each word's topic vector is produced by
+// exactly one group as a gather-reduce: bitwise reproducible run to run.
+// Words are length-bucketed: light words share a wave (16 lanes each), heavy
+// (Zipf-head) words get an 8-wave workgroup with a cross-wave LDS reduction.
+#include <stdexcept>
+#include <string>
+
+#include "common.h"
+#include "kernels.h"
+
+namespace oni {
+
+template <int KS>
+__device__ __forceinline__ void axpy_row(const float* __restrict__ e, int d, float r, float (&acc)[KS]) {
+  const float4* p = reinterpret_cast<const float4*>(e + (size_t)d * KS);
+#pragma unroll
+  for (int j = 0; j < KS / 4; ++j) {
+    float4 v = p[j];
+    acc[4 * j + 0] = fmaf(r, v.x, acc[4 * j + 0]);
+    acc[4 * j + 1] = fmaf(r, v.y, acc[4 * j + 1]);
+    acc[4 * j + 2] = fmaf(r, v.z, acc[4 * j + 2]);
+    acc[4 * j + 3] = fmaf(r, v.w, acc[4 * j + 3]);
+  }
+}
+
+template <int KS>
+__device__ __forceinline__ void store_cw(const SuffArgs& a, int w, const float (&acc)[KS]) {
+  const float4* b = reinterpret_cast<const float4*>(a.beta + (size_t)w * KS);
+  float4* o = reinterpret_cast<float4*>(a.cw + (size_t)w * KS);
+#pragma unroll
+  for (int j = 0; j < KS / 4; ++j) {
+    float4 bv = b[j];
+    o[j] = make_float4(bv.x * acc[4 * j + 0], bv.y * acc[4 * j + 1], bv.z * acc[4 * j + 2],
+                       bv.w * acc[4 * j + 3]);
+  }
+}
+
+template <int KS, int G>
+__global__ __launch_bounds__(256) void lda_suff_group(SuffArgs a) {
+  constexpr int GPB = 256 / G;
+  const int t = threadIdx.x % G;
+  const int item = blockIdx.x * GPB + threadIdx.x / G;
+  if (item >= a.n_items) return;
+  const int w = a.order[item];
+  const int beg = a.word_ptr[w], end = a.word_ptr[w + 1];
+  float acc[KS];
+#pragma unroll
+  for (int k = 0; k < KS; ++k) acc[k] = 0.f;
+  for (int i = beg + t; i < end; i += G) axpy_row<KS>(a.e, a.csc_doc[i], a.r[a.csc_ent[i]], acc);
+  group_sum_vec<G, KS>(acc);
+  if (t == 0) store_cw<KS>(a, w, acc);
+}
+
+template <int KS, int NW>
+__global__ __launch_bounds__(NW * 64) void lda_suff_block(SuffArgs a) {
+  __shared__ float sRed[NW][KS];
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const int w = a.order[blockIdx.x];
+  const int beg = a.word_ptr[w], end = a.word_ptr[w + 1];
+  float acc[KS];
+#pragma unroll
+  for (int k = 0; k < KS; ++k) acc[k] = 0.f;
+  for (int i = beg + t; i < end; i += NW * 64) axpy_row<KS>(a.e, a.csc_doc[i], a.r[a.csc_ent[i]], acc);
+  group_sum_vec<64, KS>(acc);
+  if (lane == 0) {
+#pragma unroll
+    for (int k = 0; k < KS; ++k) sRed[wv][k] = acc[k];
+  }
+  __syncthreads();
+  if (t < KS) {
+    float s = 0.f;
+#pragma unroll
+    for (int v = 0; v < NW; ++v) s += sRed[v][t];
+    a.cw[(size_t)w * KS + t] = a.beta[(size_t)w * KS + t] * s;
+  }
+}
+
+template <int KS>
+static void suff_ks(const SuffArgs& a, int variant, hipStream_t s) {
+  if (a.n_items <= 0) return;
+  switch (variant) {
+    case kSuffG16:
+      hipLaunchKernelGGL((lda_suff_group<KS, 16>), dim3((a.n_items + 15) / 16), dim3(256), 0, s, a);
+      break;
+    case kSuffG64:
+      hipLaunchKernelGGL((lda_suff_group<KS, 64>), dim3((a.n_items + 3) / 4), dim3(256), 0, s, a);
+      break;
+    case kSuffB8:
+      hipLaunchKernelGGL((lda_suff_block<KS, 8>), dim3(a.n_items), dim3(512), 0, s, a);
+      break;
+    default:
+      throw std::runtime_error("lda_suffstats: unknown variant");
+  }
+  ONI_HIP_CHECK(hipGetLastError());
+}
+
+void launch_lda_suffstats(const SuffArgs& a, int variant, int KS, hipStream_t s) {
+  switch (KS) {
+#define ONI_KS(X) \
+  case X:         \
+    suff_ks<X>(a, variant, s); \
+    break;
+    ONI_FOR_EACH_KS(ONI_KS)
+#undef ONI_KS
+    default:
+      throw std::runtime_error("lda_suffstats: unsupported KS " + std::to_string(KS));
+  }
+}
+
+// ----------------------------------------------------------------- M-step ---
+// lda-c lda_mle: log p(w|z) = log cw - log ct, floor -100 where
+// cw == 0.  The E-step consumes exp(log p) directly, so this writes
+// beta = cw / ct (exact division) or exp(-100).
+__global__ __launch_bounds__(256) void lda_mstep_kernel(const float* __restrict__ cw,
+                                                        const double* __restrict__ ct,
+                                                        float* __restrict__ beta, int V, int K, int KS) {
+  const int64_t total = (int64_t)V * KS;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    const int k = (int)(i % KS);
+    float out = 0.f;
+    if (k < K) {
+      const float c = cw[i];
+      out = c > 0.f ? (float)((double)c / ct[k]) : kExpMinus100;
+    }
+    beta[i] = out;
+  }
+}
+
+void launch_lda_mstep(const float* cw, const double* class_total, float* beta, int V, int K, int KS,
+                      hipStream_t s) {
+  const int64_t total = (int64_t)V * KS;
+  if (total == 0) return;
+  int64_t blocks = (total + 255) / 256;
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(lda_mstep_kernel, dim3((unsigned)blocks), dim3(256), 0, s, cw, class_total, beta, V,
+                     K, KS);
+  ONI_HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace oni

@@ -1,0 +1,193 @@
+"""Native build driver: compiles the CDNA4 HIP kernels and the C++ host runtime in-tree.
+
+No torch.utils.cpp_extension / hipify is involved: HIP sources are compiled with
+``hipcc --offload-arch=gfx950`` and linked with pybind11 bindings into
+``oni_ml_amd/_lib/_onihip*.so``; the C++ host runtime (CSV parser, formatters,
+lda-c reference EM, DNS parser) is compiled with ``g++`` into
+``oni_ml_amd/_lib/_oninative*.so`` plus the standalone ``lda`` executable that
+mirrors oni-lda-c's command line (reference call site ``ml_ops.sh:80``).
+
+Builds are incremental: every artefact carries a stamp holding the hash of its
+inputs (sources, headers, flags, compiler); an unchanged hash skips the step.
+"""
+from __future__ import annotations
+
+import hashlib
+import os
+import shutil
+import subprocess
+import sys
+import sysconfig
+import threading
+from concurrent.futures import ThreadPoolExecutor
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent.parent
+CSRC = ROOT / "csrc"
+LIB = Path(__file__).resolve().parent / "_lib"
+OBJ = ROOT / "build" / "obj"
+
+ROCM = Path(os.environ.get("ROCM_PATH", "/opt/rocm"))
+HIPCC = str(ROCM / "bin" / "hipcc")
+ARCH = os.environ.get("ONI_OFFLOAD_ARCH", "gfx950")
+
+_lock = threading.Lock()
+
+
+def _ext_suffix() -> str:
+    return sysconfig.get_config_var("EXT_SUFFIX") or ".so"
+
+
+def _pybind_inc() -> str:
+    import pybind11
+
+    return pybind11.get_include()
+
+
+def _py_inc() -> str:
+    return sysconfig.get_paths()["include"]
+
+
+def _hash(files, flags) -> str:
+    h = hashlib.sha256()
+    for f in sorted(str(x) for x in files):
+        h.update(f.encode())
+        h.update(Path(f).read_bytes())
+    h.update(" ".join(flags).encode())
+    return h.hexdigest()
+
+
+def _run(cmd, verbose):
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"build failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+    return r
+
+
+def _stale(out: Path, digest: str) -> bool:
+    stamp = out.with_name(out.name + ".stamp")
+    if not out.exists() or not stamp.exists():
+        return True
+    return stamp.read_text().strip() != digest
+
+
+def _stamp(out: Path, digest: str):
+    out.with_name(out.name + ".stamp").write_text(digest)
+
+
+def _compile(src: Path, out: Path, cmd_prefix, flags, deps, verbose):
+    digest = _hash([src] + list(deps), cmd_prefix + flags)
+    if not _stale(out, digest):
+        return out
+    out.parent.mkdir(parents=True, exist_ok=True)
+    _run(cmd_prefix + flags + ["-c", str(src), "-o", str(out)], verbose)
+    _stamp(out, digest)
+    return out
+
+
+def hip_flags():
+    return [
+        "-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}",
+        "-D__HIP_PLATFORM_AMD__", "-Wno-unused-result",
+        "-munsafe-fp-atomics",
+        f"-I{CSRC / 'hip'}",
+    ]
+
+
+def native_flags():
+    return ["-O3", "-std=c++17", "-fPIC", "-march=x86-64-v2", "-pthread",
+            "-Wall", "-Wno-unused-function", "-Wno-sign-compare", f"-I{CSRC / 'native'}"]
+
+
+def build_hip(verbose=False, jobs=8) -> Path:
+    """Compile csrc/hip/*.hip (device kernels, gfx950) + bind_hip.cpp into _onihip."""
+    out = LIB / ("_onihip" + _ext_suffix())
+    hdrs = sorted((CSRC / "hip").glob("*.h"))
+    srcs = sorted((CSRC / "hip").glob("*.hip"))
+    bind = CSRC / "hip" / "bind_hip.cpp"
+    flags = hip_flags()
+    objs = []
+
+    def one(src):
+        o = OBJ / "hip" / (src.stem + ".o")
+        extra = [f"-I{_pybind_inc()}", f"-I{_py_inc()}"] if src == bind else []
+        return _compile(src, o, [HIPCC], flags + extra, hdrs, verbose)
+
+    with ThreadPoolExecutor(max_workers=jobs) as ex:
+        objs = list(ex.map(one, srcs + [bind]))
+    link = [HIPCC, "-shared", f"--offload-arch={ARCH}", "-fPIC", "-o", str(out)] + [str(o) for o in objs]
+    digest = _hash(objs, link)
+    if _stale(out, digest):
+        LIB.mkdir(parents=True, exist_ok=True)
+        _run(link, verbose)
+        _stamp(out, digest)
+    return out
+
+
+def build_native(verbose=False, jobs=8) -> Path:
+    """Compile csrc/native/*.cpp (host runtime) into _oninative + the `lda` CLI binary."""
+    cxx = os.environ.get("CXX", "g++")
+    out = LIB / ("_oninative" + _ext_suffix())
+    hdrs = sorted((CSRC / "native").glob("*.h"))
+    srcs = [s for s in sorted((CSRC / "native").glob("*.cpp")) if s.name not in ("lda_main.cpp",)]
+    bind = CSRC / "native" / "bind_native.cpp"
+    if not bind.exists():
+        return None
+    lib_srcs = [s for s in srcs if s != bind]
+    flags = native_flags()
+
+    def one(src):
+        o = OBJ / "native" / (src.stem + ".o")
+        extra = [f"-I{_pybind_inc()}", f"-I{_py_inc()}"] if src == bind else []
+        return _compile(src, o, [cxx], flags + extra, hdrs, verbose)
+
+    with ThreadPoolExecutor(max_workers=jobs) as ex:
+        objs = list(ex.map(one, lib_srcs + [bind]))
+    link = [cxx, "-shared", "-fPIC", "-pthread", "-o", str(out)] + [str(o) for o in objs]
+    digest = _hash(objs, link)
+    if _stale(out, digest):
+        LIB.mkdir(parents=True, exist_ok=True)
+        _run(link, verbose)
+        _stamp(out, digest)
+    # standalone lda-c compatible executable
+    main = CSRC / "native" / "lda_main.cpp"
+    if main.exists():
+        mo = one(main)
+        exe = LIB / "lda"
+        lib_objs = [o for o in objs if o.stem != "bind_native"]
+        cmd = [cxx, "-pthread", "-o", str(exe), str(mo)] + [str(o) for o in lib_objs]
+        digest = _hash([mo] + lib_objs, cmd)
+        if _stale(exe, digest):
+            _run(cmd, verbose)
+            _stamp(exe, digest)
+    return out
+
+
+def build_all(verbose=False, hip=True, native=True):
+    with _lock:
+        outs = []
+        if native:
+            o = build_native(verbose)
+            if o is not None:
+                outs.append(o)
+        if hip:
+            if not Path(HIPCC).exists():
+                raise RuntimeError(f"hipcc not found at {HIPCC}")
+            outs.append(build_hip(verbose))
+        return outs
+
+
+def clean():
+    shutil.rmtree(ROOT / "build", ignore_errors=True)
+    for p in LIB.glob("*"):
+        if p.name != "__init__.py":
+            p.unlink()
+
+
+if __name__ == "__main__":
+    v = "-v" in sys.argv
+    if "clean" in sys.argv:
+        clean()
+    print(build_all(verbose=v))

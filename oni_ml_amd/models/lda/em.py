@@ -1,0 +1,344 @@
+"""Variational-EM LDA engine (replacement for the MPI oni-lda-c core).
+
+Reference behaviour: oni-lda-c `lda est` (ml_ops.sh:80):
+random/seeded/model init -> EM loop { zero ss; E-step over docs; M-step (lda_mle,
+optional alpha Newton); conv = (L_old - L)/L_old; if conv < 0: VAR_MAX_ITER *= 2 }
+while (conv < 0 or conv > EM_CONV or i <= 2) and i <= EM_MAX_ITER.
+
+MI355X design:
+* the corpus (CSR + CSC) and the model (word-major beta, f32) stay resident in
+  HBM for the whole run; one EM iteration = length-bucketed fused E-step
+  kernels (launched on up to 3 HIP streams so the long-document buckets overlap
+  the short ones) -> deterministic CSC sufficient statistics -> (RCCL all-reduce
+  of the flat [class_word | scalars] buffer when data-parallel) -> M-step kernel.
+  The only host sync per iteration is the 3-scalar read the convergence test
+  and alpha Newton need.
+* backends: "hip" (gfx950 kernels), "torch" (vectorised reference, any device),
+  "cpu" (lda-c semantics C++ reference, Gauss-Seidel).
+"""
+from __future__ import annotations
+
+import math
+import time
+from dataclasses import dataclass, field
+from typing import Callable, List, Optional
+
+import numpy as np
+import torch
+
+from ...corpus.csr import Corpus, DeviceCorpus
+from ...utils.trace import range_push, range_pop
+from . import special
+from .settings import LDASettings, LOG_FLOOR, NUM_INIT
+
+
+@dataclass
+class EMIterStats:
+    iteration: int
+    likelihood: float
+    converged: float
+    alpha: float
+    seconds: float
+    var_iter_mean: float
+    var_iter_max: int
+    var_max_iter: int
+
+
+@dataclass
+class LDAResult:
+    log_beta: np.ndarray            # [K, V] float64 (lda-c .beta content)
+    gamma: np.ndarray               # [D, K] float64 (lda-c .gamma content)
+    alpha: float
+    num_topics: int
+    num_terms: int
+    likelihoods: List[tuple] = field(default_factory=list)   # (L, conv) per EM iteration
+    stats: List[EMIterStats] = field(default_factory=list)
+    em_iterations: int = 0
+    seconds: float = 0.0
+
+
+class _Buckets:
+    """Length-bucket plan: (variant, int32 order tensor) launched per E-step."""
+
+    def __init__(self, lengths: np.ndarray, ks: int, device, kind: str):
+        from ...ops import hip as H
+        order = np.argsort(-lengths, kind="stable").astype(np.int32)
+        L = lengths[order]
+        plan = []
+        if kind == "doc":
+            cws = 4 if ks <= 32 else (2 if ks <= 64 else 1)
+            edges = [(H.ESTEP_B8, 256 * cws, None), (H.ESTEP_B4, 64 * cws, 256 * cws),
+                     (H.ESTEP_G64C, 64, 64 * cws), (H.ESTEP_G64, 32, 64), (H.ESTEP_G32, 16, 32),
+                     (H.ESTEP_G16, 0, 16)]
+            L = np.where(L == 0, 1, L)
+        else:
+            edges = [(H.SUFF_B8, 2048, None), (H.SUFF_G64, 64, 2048), (H.SUFF_G16, 0, 64)]
+        for var, lo, hi in edges:
+            m = (L > lo) if hi is None else ((L > lo) & (L <= hi))
+            if kind == "word" and var == H.SUFF_G16:
+                m = (L > 0) & (L <= 64)
+            if m.any():
+                plan.append((var, torch.from_numpy(order[m].copy()).to(device)))
+        self.plan = plan
+
+
+class LDAEngine:
+    def __init__(self, corpus: Corpus, num_topics: int, settings: Optional[LDASettings] = None,
+                 alpha_init: float = 2.5, backend: str = "auto", device=None, dist=None, seed: int = 0,
+                 streams: int = 3, local_shard: bool = False):
+        self.settings = settings or LDASettings()
+        self.K = int(num_topics)
+        self.V = corpus.num_terms
+        self.alpha = float(alpha_init)
+        self.alpha_init = float(alpha_init)
+        self.dist = dist
+        self.seed = seed
+        self.var_max_iter = self.settings.var_max_iter
+        if backend == "auto":
+            from ...ops import hip as H
+            backend = "hip" if H.available() else "torch"
+        self.backend = backend
+        if device is None:
+            device = torch.device("cuda", torch.cuda.current_device()) if (
+                backend == "hip" or torch.cuda.is_available()) and torch.cuda.is_available() else torch.device("cpu")
+        self.device = torch.device(device)
+        # shard (data parallel over documents)
+        self.global_docs = corpus.num_docs
+        if local_shard:
+            # caller already hands this rank its own shard (weak-scaling bench)
+            self.doc_range = (0, corpus.num_docs)
+            if dist is not None:
+                self.global_docs = dist.allreduce_int(corpus.num_docs)
+        elif dist is not None and dist.world_size > 1:
+            d0, d1 = dist.shard_range(corpus)
+            self.doc_range = (d0, d1)
+            corpus = corpus.slice_docs(d0, d1)
+        else:
+            self.doc_range = (0, corpus.num_docs)
+        self.corpus = corpus
+        self.D = corpus.num_docs
+        if backend == "hip":
+            from ...ops import hip as H
+            self.KS = H.padded_topics(self.K)
+            self.dc = DeviceCorpus.build(corpus, self.device)
+            self.doc_buckets = _Buckets(self.dc.doc_len, self.KS, self.device, "doc")
+            self.word_buckets = _Buckets(self.dc.word_len, self.KS, self.device, "word")
+            dev, D, V, KS, nnz = self.device, self.D, self.V, self.KS, corpus.nnz
+            self.beta = torch.zeros(V, KS, dtype=torch.float32, device=dev)
+            self.cw = torch.zeros(V, KS, dtype=torch.float32, device=dev)
+            self.gamma = torch.zeros(D, KS, dtype=torch.float32, device=dev)
+            self.e = torch.zeros(D, KS, dtype=torch.float32, device=dev)
+            self.r = torch.zeros(max(nnz, 1), dtype=torch.float32, device=dev)[:nnz]
+            self.lik = torch.zeros(D, dtype=torch.float64, device=dev)
+            self.ass = torch.zeros(D, dtype=torch.float64, device=dev)
+            self.iters = torch.zeros(D, dtype=torch.int32, device=dev)
+            # flat reduce buffer view: [cw (V*KS) | lik_sum | ass_sum | ndocs]
+            self._streams = [torch.cuda.Stream(device=dev) for _ in range(max(0, streams - 1))]
+        elif backend == "torch":
+            dev = self.device
+            self.KS = self.K
+            self.t_doc_ptr = torch.from_numpy(corpus.doc_ptr).to(dev)
+            self.t_word = torch.from_numpy(corpus.word_idx.astype(np.int64)).to(dev)
+            self.t_cnt = torch.from_numpy(corpus.counts.astype(np.float64)).to(dev)
+            self.beta = torch.zeros(self.V, self.K, dtype=torch.float64, device=dev)
+            self.cw = torch.zeros(self.V, self.K, dtype=torch.float64, device=dev)
+            self.gamma = torch.zeros(self.D, self.K, dtype=torch.float64, device=dev)
+        elif backend == "cpu":
+            from ...ops import native
+            self._native = native.lib()
+            self.KS = self.K
+            self.beta = torch.zeros(self.V, self.K, dtype=torch.float64)
+            self.cw = torch.zeros(self.V, self.K, dtype=torch.float64)
+            self.gamma = torch.zeros(self.D, self.K, dtype=torch.float64)
+        else:
+            raise ValueError(f"unknown backend {backend}")
+        self.class_total = torch.zeros(self.KS, dtype=torch.float64, device=self.cw.device)
+
+    # ------------------------------------------------------------------ init
+    def init_random(self, seed: Optional[int] = None):
+        """random_initialize_ss + lda_mle(..., 0): cw[k][w] = 1/V + U(0,1)."""
+        rng = np.random.default_rng(self.seed if seed is None else seed)
+        cw = 1.0 / self.V + rng.random((self.K, self.V))
+        self._set_ss_host(cw)
+        self.alpha = self.alpha_init
+
+    def init_seeded(self, corpus_global: Corpus, seed: Optional[int] = None):
+        """corpus_initialize_ss: NUM_INIT random docs per topic + 1 smoothing."""
+        rng = np.random.default_rng(self.seed if seed is None else seed)
+        cw = np.zeros((self.K, self.V))
+        for k in range(self.K):
+            for _ in range(NUM_INIT):
+                d = int(math.floor(rng.random() * corpus_global.num_docs))
+                a, b = corpus_global.doc_ptr[d], corpus_global.doc_ptr[d + 1]
+                np.add.at(cw[k], corpus_global.word_idx[a:b], corpus_global.counts[a:b])
+            cw[k] += 1.0
+        self._set_ss_host(cw)
+        self.alpha = self.alpha_init
+
+    def init_from_model(self, log_beta: np.ndarray, alpha: float):
+        """Resume path (lda-c `load_lda_model`): beta from log p(w|z)."""
+        lb = np.asarray(log_beta, dtype=np.float64)
+        if lb.shape != (self.K, self.V):
+            raise ValueError(f"model shape {lb.shape} != ({self.K}, {self.V})")
+        cw = np.exp(lb)
+        self._set_ss_host(cw, normalized=True)
+        self.alpha = float(alpha)
+
+    def _set_ss_host(self, cw_kv: np.ndarray, normalized=False):
+        ct = np.cumsum(cw_kv, axis=1)[:, -1] if cw_kv.shape[1] else np.zeros(self.K)
+        if normalized:
+            ct = np.ones(self.K)
+        cw_t = torch.zeros(self.V, self.KS, dtype=self.cw.dtype)
+        cw_t[:, :self.K] = torch.from_numpy(cw_kv.T.copy()).to(self.cw.dtype)
+        self.cw.copy_(cw_t.to(self.cw.device))
+        ctt = torch.zeros(self.KS, dtype=torch.float64)
+        ctt[:self.K] = torch.from_numpy(ct)
+        self.class_total.copy_(ctt.to(self.class_total.device))
+        self._mstep_beta()
+
+    # ------------------------------------------------------------- E / M steps
+    def _mstep_beta(self):
+        if self.backend == "hip":
+            from ...ops import hip as H
+            H.lda_mstep(self.cw, self.class_total, self.beta, self.K)
+        else:
+            from ...ops import reference as R
+            self.beta.copy_(R.mstep(self.cw, self.class_total, self.K))
+
+    def e_step(self):
+        """One E-step over the local shard. Returns (lik_sum, alpha_ss_sum) as a device f64 tensor [2]."""
+        if self.backend == "hip":
+            return self._e_step_hip()
+        if self.backend == "torch":
+            from ...ops import reference as R
+            out = R.estep_jacobi(self.t_doc_ptr, self.t_word, self.t_cnt, self.beta, self.K, self.alpha,
+                                 self.var_max_iter, self.settings.var_converged)
+            self.gamma = out["gamma"]
+            self.iters = out["iters"]
+            self.cw = R.suffstats(self.t_doc_ptr, self.t_word, out["e"], out["r"], self.beta, self.V, self.K)
+            return torch.stack([out["lik"].sum(), out["alpha_ss"].sum()])
+        # cpu: lda-c Gauss-Seidel reference (C++)
+        lb = torch.where(self.beta > 0, torch.log(self.beta), torch.full_like(self.beta, LOG_FLOOR))
+        res = self._native.lda_estep_ldac(
+            self.corpus.doc_ptr, self.corpus.word_idx, self.corpus.counts,
+            np.ascontiguousarray(lb.T.numpy()), self.alpha, self.var_max_iter, self.settings.var_converged, 0)
+        self.gamma = torch.from_numpy(res["gamma"])
+        self.iters = torch.from_numpy(res["iters"])
+        self.cw = torch.from_numpy(np.ascontiguousarray(res["class_word"].T))
+        return torch.tensor([res["likelihood"], res["alpha_ss"]], dtype=torch.float64)
+
+    def _e_step_hip(self):
+        from ...ops import hip as H
+        dc = self.dc
+        lc = special.lik_const(self.alpha, self.K)
+        main = torch.cuda.current_stream(self.device)
+        streams = [main] + self._streams
+        plan = self.doc_buckets.plan
+        # fork: largest buckets on side streams so they overlap the short-doc bulk
+        ev = torch.cuda.Event()
+        ev.record(main)
+        for i, (var, order) in enumerate(plan):
+            s = streams[i % len(streams)]
+            if s is not main:
+                s.wait_event(ev)
+            with torch.cuda.stream(s):
+                H.lda_estep(dc.doc_ptr, dc.word_idx, dc.counts, order, self.beta, self.K, self.alpha, lc,
+                            self.var_max_iter, self.settings.var_converged, self.gamma, self.e, self.r,
+                            self.lik, self.ass, self.iters, var)
+        for s in streams[1:]:
+            e2 = torch.cuda.Event()
+            e2.record(s)
+            main.wait_event(e2)
+        # sufficient statistics (deterministic CSC gather-reduce)
+        self.cw.zero_()
+        for var, order in self.word_buckets.plan:
+            H.lda_suffstats(dc.word_ptr, dc.csc_ent, dc.csc_doc, order, self.e, self.r, self.beta, self.cw, var)
+        return torch.stack([self.lik.sum(), self.ass.sum()])
+
+    def m_step(self, estimate_alpha: bool, alpha_ss: float, num_docs: int):
+        self.class_total = self.cw.sum(0, dtype=torch.float64)
+        self._mstep_beta()
+        if estimate_alpha:
+            self.alpha = special.opt_alpha(alpha_ss, num_docs, self.K)
+
+    # -------------------------------------------------------------- outputs
+    def log_beta(self) -> np.ndarray:
+        """[K, V] float64 log p(w|z) as lda-c would save it (-100 floor)."""
+        cw = self.cw[:, :self.K].double()
+        ct = self.class_total[:self.K]
+        lb = torch.where(cw > 0, torch.log(cw) - torch.log(ct), torch.full_like(cw, LOG_FLOOR))
+        return lb.T.contiguous().cpu().numpy()
+
+    def local_gamma(self) -> np.ndarray:
+        return self.gamma[:, :self.K].double().cpu().numpy()
+
+    def gather_gamma(self) -> np.ndarray:
+        g = self.local_gamma()
+        if self.dist is not None and self.dist.world_size > 1:
+            return self.dist.gather_rows(g, self.global_docs)
+        return g
+
+    # ----------------------------------------------------------------- driver
+    def run(self, start: str = "random", corpus_global: Optional[Corpus] = None,
+            on_iteration: Optional[Callable] = None, on_save: Optional[Callable] = None,
+            start_iteration: int = 0, likelihood_old: float = 0.0, verbose: bool = False) -> LDAResult:
+        """Run EM to convergence. `on_save(tag, engine)` fires for '000', every LAG and 'final'."""
+        from .settings import LAG
+        st = self.settings
+        t0 = time.perf_counter()
+        if start == "random":
+            self.init_random()
+        elif start == "seeded":
+            self.init_seeded(corpus_global if corpus_global is not None else self.corpus)
+        elif start == "resume":
+            pass  # state restored by caller (checkpoint.restore)
+        else:
+            raise ValueError(start)
+        if on_save is not None and start_iteration == 0:
+            on_save("000", self)
+        i = start_iteration
+        L_old = likelihood_old
+        conv = 1.0
+        hist = []
+        stats = []
+        n_docs_global = self.global_docs
+        while ((conv < 0) or (conv > st.em_converged) or (i <= 2)) and (i <= st.em_max_iter):
+            i += 1
+            ti = time.perf_counter()
+            range_push(f"em_iter_{i}")
+            range_push("e_step")
+            sc = self.e_step()
+            range_pop()
+            if self.dist is not None and self.dist.world_size > 1:
+                range_push("allreduce")
+                sc = self.dist.allreduce_suffstats(self.cw, sc)
+                range_pop()
+            range_push("m_step")
+            host = sc.cpu().tolist()
+            lik, ass = float(host[0]), float(host[1])
+            self.m_step(st.estimate_alpha, ass, n_docs_global)
+            range_pop()
+            range_pop()
+            conv = (L_old - lik) / L_old if L_old != 0 else (math.inf if lik < 0 else (-math.inf if lik > 0 else math.nan))
+            if conv < 0:
+                self.var_max_iter = self.var_max_iter * 2
+            L_old = lik
+            hist.append((lik, conv))
+            it_np = self.iters.cpu().numpy() if isinstance(self.iters, torch.Tensor) else np.asarray(self.iters)
+            stt = EMIterStats(i, lik, conv, self.alpha, time.perf_counter() - ti,
+                              float(it_np.mean()) if it_np.size else 0.0, int(it_np.max()) if it_np.size else 0,
+                              self.var_max_iter)
+            stats.append(stt)
+            if verbose:
+                print(f"**** em iteration {i} **** L={lik:.6f} conv={conv:.5e} alpha={self.alpha:.5f} "
+                      f"var_iters(mean/max)={stt.var_iter_mean:.2f}/{stt.var_iter_max} {stt.seconds*1e3:.2f} ms",
+                      flush=True)
+            if on_iteration is not None:
+                on_iteration(self, i, lik, conv)
+            if on_save is not None and (i % LAG) == 0:
+                on_save(f"{i:03d}", self)
+        if on_save is not None:
+            on_save("final", self)
+        res = LDAResult(log_beta=None, gamma=None, alpha=self.alpha, num_topics=self.K, num_terms=self.V,
+                        likelihoods=hist, stats=stats, em_iterations=i, seconds=time.perf_counter() - t0)
+        return res

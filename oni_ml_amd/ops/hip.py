@@ -1,0 +1,231 @@
+"""Loader + validated launch wrappers for the gfx950 HIP kernels (`_onihip`).
+
+Every wrapper checks dtype / device / contiguity / shape on the host before it
+hands raw addresses to the kernel (a wrong shape on a hand-written kernel can
+fault the whole GPU), then launches on torch's current stream so the launch is
+ordered with torch work and capturable in a hipGraph.
+
+On a machine with a GPU the extension is mandatory: :func:`lib` raises if it
+cannot be imported instead of silently falling back to eager torch.
+"""
+from __future__ import annotations
+
+import importlib
+import os
+import sys
+
+import torch
+
+_LIB = None
+_ERR = None
+
+# estep / suffstats variant ids (csrc/hip/kernels.h)
+ESTEP_G16, ESTEP_G32, ESTEP_G64, ESTEP_G64C, ESTEP_B4, ESTEP_B8 = range(6)
+SUFF_G16, SUFF_G64, SUFF_B8 = range(3)
+
+
+def _import():
+    global _LIB, _ERR
+    if _LIB is not None or _ERR is not None:
+        return
+    try:
+        here = os.path.join(os.path.dirname(os.path.dirname(__file__)), "_lib")
+        if here not in sys.path:
+            sys.path.insert(0, here)
+        _LIB = importlib.import_module("_onihip")
+    except Exception as e:  # pragma: no cover - depends on build state
+        _ERR = e
+
+
+def available() -> bool:
+    _import()
+    return _LIB is not None and torch.cuda.is_available()
+
+
+def lib():
+    """Return the extension module; raise loudly if it is missing."""
+    _import()
+    if _LIB is None:
+        raise RuntimeError(
+            "oni_ml_amd HIP extension (_onihip) is not built or failed to load: "
+            f"{_ERR!r}. Run `python -m oni_ml_amd._build` (needs hipcc, gfx950)."
+        )
+    return _LIB
+
+
+def compiled_ks():
+    return list(lib().compiled_ks())
+
+
+def padded_topics(K: int) -> int:
+    """Smallest compiled row stride >= K (multiple of 4)."""
+    for ks in (8, 12, 16, 20, 24, 32, 52, 64, 100, 128):
+        if ks >= K:
+            return ks
+    raise ValueError(f"K={K} exceeds the largest compiled topic count (128)")
+
+
+def _stream() -> int:
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _chk(t: torch.Tensor, dtype, name, shape=None, device=None):
+    if not isinstance(t, torch.Tensor):
+        raise TypeError(f"{name}: expected tensor")
+    if t.dtype != dtype:
+        raise TypeError(f"{name}: expected {dtype}, got {t.dtype}")
+    if not t.is_cuda:
+        raise ValueError(f"{name}: must be a GPU tensor")
+    if device is not None and t.device != device:
+        raise ValueError(f"{name}: on {t.device}, expected {device}")
+    if not t.is_contiguous():
+        raise ValueError(f"{name}: must be contiguous")
+    if shape is not None and tuple(t.shape) != tuple(shape):
+        raise ValueError(f"{name}: shape {tuple(t.shape)} != {tuple(shape)}")
+    return t.data_ptr()
+
+
+def lda_estep(doc_ptr, word_idx, counts, order, beta, K, alpha, lik_const, var_max_iter, var_conv,
+              gamma, e_out, r_out, lik, alpha_ss, iters, variant):
+    D = doc_ptr.numel() - 1
+    nnz = word_idx.numel()
+    V, KS = beta.shape
+    if KS not in compiled_ks():
+        raise ValueError(f"beta row stride {KS} has no compiled kernel")
+    if not (0 < K <= KS):
+        raise ValueError("K out of range")
+    dev = beta.device
+    args = [
+        _chk(doc_ptr, torch.int32, "doc_ptr", (D + 1,), dev),
+        _chk(word_idx, torch.int32, "word_idx", (nnz,), dev),
+        _chk(counts, torch.float32, "counts", (nnz,), dev),
+        _chk(order, torch.int32, "order", None, dev),
+        order.numel(),
+        _chk(beta, torch.float32, "beta", (V, KS), dev),
+        int(K), int(KS), float(alpha), float(lik_const), int(var_max_iter), float(var_conv),
+        _chk(gamma, torch.float32, "gamma", (D, KS), dev),
+        _chk(e_out, torch.float32, "e_out", (D, KS), dev),
+        _chk(r_out, torch.float32, "r_out", (nnz,), dev),
+        _chk(lik, torch.float64, "lik", (D,), dev),
+        _chk(alpha_ss, torch.float64, "alpha_ss", (D,), dev),
+        _chk(iters, torch.int32, "iters", (D,), dev),
+        int(variant), _stream(),
+    ]
+    if order.numel() == 0:
+        return
+    lib().lda_estep(*args)
+
+
+def lda_suffstats(word_ptr, csc_ent, csc_doc, order, e, r, beta, cw, variant):
+    V, KS = beta.shape
+    nnz = csc_ent.numel()
+    D = e.shape[0]
+    dev = beta.device
+    args = [
+        _chk(word_ptr, torch.int32, "word_ptr", (V + 1,), dev),
+        _chk(csc_ent, torch.int32, "csc_ent", (nnz,), dev),
+        _chk(csc_doc, torch.int32, "csc_doc", (nnz,), dev),
+        _chk(order, torch.int32, "order", None, dev),
+        order.numel(),
+        _chk(e, torch.float32, "e", (D, KS), dev),
+        _chk(r, torch.float32, "r", (nnz,), dev),
+        _chk(beta, torch.float32, "beta", (V, KS), dev),
+        _chk(cw, torch.float32, "cw", (V, KS), dev),
+        int(KS), int(variant), _stream(),
+    ]
+    if order.numel() == 0:
+        return
+    lib().lda_suffstats(*args)
+
+
+def lda_mstep(cw, class_total, beta, K):
+    V, KS = cw.shape
+    dev = cw.device
+    lib().lda_mstep(
+        _chk(cw, torch.float32, "cw", (V, KS), dev),
+        _chk(class_total, torch.float64, "class_total", (KS,), dev),
+        _chk(beta, torch.float32, "beta", (V, KS), dev),
+        int(V), int(K), int(KS), _stream(),
+    )
+
+
+def score_events(theta, phi, K, dflt, doc_a, word_a, doc_b, word_b, tol):
+    """Returns (score_a, score_b|None, key, flag) as new device tensors."""
+    n = doc_a.numel()
+    dev = doc_a.device
+    D = theta.shape[0]
+    V = phi.shape[0]
+    if theta.dim() != 2 or phi.dim() != 2 or theta.shape[1] < K or phi.shape[1] < K:
+        raise ValueError("theta/phi must be [*, >=K]")
+    if theta.shape[1] != phi.shape[1]:
+        raise ValueError("theta and phi row strides differ")
+    Kr = theta.shape[1]
+    if Kr != K:
+        theta = theta[:, :K].contiguous()
+        phi = phi[:, :K].contiguous()
+    # index bounds (host check before a gather kernel touches memory)
+    for name, idx, lim in (("doc_a", doc_a, D), ("word_a", word_a, V), ("doc_b", doc_b, D), ("word_b", word_b, V)):
+        if idx is None:
+            continue
+        if idx.numel() != n:
+            raise ValueError(f"{name}: length mismatch")
+        if n and (int(idx.max()) >= lim or int(idx.min()) < -1):
+            raise ValueError(f"{name}: index out of range")
+    sa = torch.empty(n, dtype=torch.float64, device=dev)
+    sb = torch.empty(n, dtype=torch.float64, device=dev) if doc_b is not None else None
+    key = torch.empty(n, dtype=torch.float64, device=dev)
+    flag = torch.empty(n, dtype=torch.uint8, device=dev)
+    if n == 0:
+        return sa, sb, key, flag
+    lib().score_events(
+        _chk(theta, torch.float64, "theta", (D, K), dev), _chk(phi, torch.float64, "phi", (V, K), dev),
+        int(K), float(dflt),
+        _chk(doc_a, torch.int32, "doc_a", (n,), dev), _chk(word_a, torch.int32, "word_a", (n,), dev),
+        _chk(doc_b, torch.int32, "doc_b", (n,), dev) if doc_b is not None else 0,
+        _chk(word_b, torch.int32, "word_b", (n,), dev) if word_b is not None else 0,
+        int(n), float(tol), sa.data_ptr(), sb.data_ptr() if sb is not None else 0, key.data_ptr(),
+        flag.data_ptr(), _stream(),
+    )
+    return sa, sb, key, flag
+
+
+def flow_words(hour, minute, second, port_a, port_b, ipkt, ibyt, time_cuts, ibyt_cuts, ipkt_cuts):
+    n = hour.numel()
+    dev = hour.device
+    cols = [hour, minute, second, port_a, port_b, ipkt, ibyt]
+    names = ["hour", "minute", "second", "port_a", "port_b", "ipkt", "ibyt"]
+    ptrs = [_chk(c, torch.float64, nm, (n,), dev) for c, nm in zip(cols, names)]
+    cuts = [time_cuts, ibyt_cuts, ipkt_cuts]
+    cptr = [_chk(c, torch.float64, "cuts", None, dev) for c in cuts]
+    out = dict(
+        time=torch.empty(n, dtype=torch.float64, device=dev),
+        time_bin=torch.empty(n, dtype=torch.int8, device=dev),
+        ibyt_bin=torch.empty(n, dtype=torch.int8, device=dev),
+        ipkt_bin=torch.empty(n, dtype=torch.int8, device=dev),
+        word_port=torch.empty(n, dtype=torch.float64, device=dev),
+        p_case=torch.empty(n, dtype=torch.int8, device=dev),
+        src_prefix=torch.empty(n, dtype=torch.int8, device=dev),
+        dst_prefix=torch.empty(n, dtype=torch.int8, device=dev),
+    )
+    if n == 0:
+        return out
+    lib().flow_words(
+        *ptrs, cptr[0], time_cuts.numel(), cptr[1], ibyt_cuts.numel(), cptr[2], ipkt_cuts.numel(), int(n),
+        out["time"].data_ptr(), out["time_bin"].data_ptr(), out["ibyt_bin"].data_ptr(),
+        out["ipkt_bin"].data_ptr(), out["word_port"].data_ptr(), out["p_case"].data_ptr(),
+        out["src_prefix"].data_ptr(), out["dst_prefix"].data_ptr(), _stream(),
+    )
+    return out
+
+
+def bin_columns(values, cuts):
+    """bins[i, c] = #{cut in cuts[c] : values[c][i] > cut} (int8 [n, ncols])."""
+    n = values[0].numel()
+    dev = values[0].device
+    vp = [_chk(v, torch.float64, "values", (n,), dev) for v in values]
+    cp = [_chk(c, torch.float64, "cuts", None, dev) for c in cuts]
+    out = torch.empty((n, len(values)), dtype=torch.int8, device=dev)
+    if n == 0:
+        return out
+    lib().bin_columns(vp, cp, [int(c.numel()) for c in cuts], int(n), out.data_ptr(), _stream())
+    return out
