@@ -30,8 +30,8 @@ def _random_beta(V, K, KS, seed=0, dev="cuda"):
     return out.to(dev)
 
 
-@pytest.mark.parametrize("K", [20, 7, 50, 100])
-def test_estep_matches_reference(hip, K):
+@pytest.mark.parametrize("K,vconv", [(20, -1e30), (7, -1e30), (50, -1e30), (100, -1e30), (20, 1e-6)])
+def test_estep_matches_reference(hip, K, vconv):
     c = _corpus_with_long_docs()
     dev = torch.device("cuda")
     KS = hip.padded_topics(K)
@@ -44,7 +44,10 @@ def test_estep_matches_reference(hip, K):
     lik = torch.zeros(D, dtype=torch.float64, device=dev)
     ass = torch.zeros(D, dtype=torch.float64, device=dev)
     iters = torch.zeros(D, dtype=torch.int32, device=dev)
-    alpha, vmax, vconv = 0.7, 20, 1e-6
+    # vconv = -1e30 runs exactly vmax Jacobi iterations per doc (tight fp32-vs-fp64
+    # numerics); vconv = 1e-6 is the lda-c convergence rule, where a doc may stop one
+    # iteration apart in fp32 and fp64, so gamma is compared loosely there.
+    alpha, vmax = 0.7, 20
     lc = special.lik_const(alpha, K)
     plan = _Buckets(dc.doc_len, KS, dev, "doc").plan
     assert len(plan) >= 4
@@ -55,15 +58,16 @@ def test_estep_matches_reference(hip, K):
     ref = R.estep_jacobi(dc.doc_ptr, dc.word_idx, dc.counts, beta.double(), K, alpha, vmax, vconv)
     g, gr = gamma[:, :K].double(), ref["gamma"]
     rel = ((g - gr).abs() / gr.abs().clamp_min(1e-3)).max().item()
-    assert rel < 2e-3, rel
+    assert rel < (2e-3 if vconv < 0 else 2e-2), rel
     lrel = ((lik - ref["lik"]).abs() / ref["lik"].abs()).max().item()
     assert lrel < 1e-4, lrel
+    assert abs(lik.sum().item() - ref["lik"].sum().item()) / abs(ref["lik"].sum().item()) < 1e-5
     # padding topics stay zero
     if KS > K:
         assert gamma[:, K:].abs().max().item() == 0
     # iteration counts agree for the vast majority of documents
     agree = (iters.cpu() == ref["iters"].cpu()).float().mean().item()
-    assert agree > 0.9, agree
+    assert agree > (0.999 if vconv < 0 else 0.9), agree
     # alpha sufficient statistic
     arel = ((ass - ref["alpha_ss"]).abs() / ref["alpha_ss"].abs().clamp_min(1.0)).max().item()
     assert arel < 1e-3, arel
