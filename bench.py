@@ -42,15 +42,38 @@ def _baseline():
         return None
 
 
-def build_corpus(args, rank):
+def build_corpus(args, rank, dev=None):
     seed = args.seed + 1000 * rank
     if args.corpus == "planted":
         from oni_ml_amd.synth.corpus import planted_corpus
         return planted_corpus(num_docs=args.docs, num_terms=args.vocab, num_topics=24, mean_tokens=25,
                               tail=1.1, max_tokens=300_000, seed=seed), {}
     from oni_ml_amd.pipeline.flow import synthetic_flow_corpus
-    c, info = synthetic_flow_corpus(events=args.events, seed=seed)
+    c, info = synthetic_flow_corpus(events=args.events, seed=seed, device=dev)
     return c, info
+
+
+def _e2e(args, dev):
+    """Wall-clock of the full pipeline (ml_ops.sh YYYYMMDD flow TOL equivalent) on a synthetic day."""
+    import shutil
+    import tempfile
+    from oni_ml_amd import config as CFG
+    from oni_ml_amd.pipeline import run
+    from oni_ml_amd.synth.flow import generate_flow_day
+    tmp = tempfile.mkdtemp(prefix="oni_e2e_")
+    try:
+        generate_flow_day(os.path.join(tmp, "in/"), events=args.events, seed=args.seed + 7)
+        cfg = CFG.resolve("20160122", "flow", tol=1e-20, conf_path=None, environ={}, lpath=os.path.join(tmp, "ml"),
+                          flow_path=os.path.join(tmp, "in"), backend="hip", topics=args.topics, verbose=False)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        s = run(cfg, device=dev, log=lambda *a, **k: None)
+        torch.cuda.synchronize()
+        wall = time.perf_counter() - t0
+        return dict(e2e_wall_s=round(wall, 3), e2e_stage_s={k: round(v, 3) for k, v in s["stage_seconds"].items()},
+                    e2e_em_iters=s["lda"]["em_iterations"], e2e_flagged=s.get("scored"), e2e_corpus=s.get("corpus"))
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
 
 
 def main():
@@ -65,6 +88,7 @@ def main():
     ap.add_argument("--vocab", type=int, default=8_000)
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--converge", type=int, default=1, help="also time a full random-init run to convergence")
+    ap.add_argument("--e2e", type=int, default=1, help="N=1: also time the whole ml_ops flow pipeline on the day")
     args = ap.parse_args()
 
     from oni_ml_amd.parallel import dist as D
@@ -76,7 +100,7 @@ def main():
     from oni_ml_amd.models.lda.settings import LDASettings
 
     t0 = time.perf_counter()
-    corpus, info = build_corpus(args, rank)
+    corpus, info = build_corpus(args, rank, dev)
     t_corpus = time.perf_counter() - t0
     # weak scaling: each rank's corpus is its own shard
     eng = LDAEngine(corpus, args.topics, LDASettings(), backend="hip", device=dev,
@@ -119,6 +143,8 @@ def main():
         extra = dict(converge_seconds=round(tc, 4), converge_em_iters=res.em_iterations,
                      converge_docs_per_sec=round(docs_global * res.em_iterations / tc, 1),
                      final_likelihood=res.likelihoods[-1][0])
+    if args.e2e and world == 1 and args.corpus == "flow":
+        extra.update(_e2e(args, dev))
     base = _baseline()
     if rank == 0:
         out = {

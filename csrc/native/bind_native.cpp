@@ -1,0 +1,299 @@
+// pybind11 module `_oninative`: the C++ host runtime of oni_ml_amd.
+//   * TextTable     - multithreaded CSV ingest with the reference's semantics
+//   * write_rows    - multithreaded formatted writer (Java / Python-2 / lda-c formats)
+//   * dns_features  - DNS query-name parsing + Scala-order entropy
+//   * lda_estep_ldac / opt_alpha / digamma - lda-c reference numerics
+//   * java_double / py2_float - formatting helpers (tests, small outputs)
+#include <pybind11/numpy.h>
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include <thread>
+
+#include "dns.h"
+#include "fmt.h"
+#include "lda_ref.h"
+#include "table.h"
+
+namespace py = pybind11;
+using namespace onin;
+
+template <typename T>
+static py::array_t<T> to_np(const std::vector<T>& v) {
+  py::array_t<T> a(v.size());
+  if (!v.empty()) std::memcpy(a.mutable_data(), v.data(), v.size() * sizeof(T));
+  return a;
+}
+
+static int default_threads() {
+  unsigned n = std::thread::hardware_concurrency();
+  return n ? (int)std::min(n, 16u) : 4;
+}
+
+// Keeps numpy arrays / name lists alive while the writer runs.
+struct ColHolder {
+  std::vector<py::object> keep;
+  std::vector<std::vector<std::string>> names;
+};
+
+static std::vector<OutCol> build_cols(const py::list& spec, ColHolder& h, int64_t n_rows_needed) {
+  std::vector<OutCol> cols;
+  h.names.reserve(spec.size());
+  for (auto item : spec) {
+    py::tuple t = item.cast<py::tuple>();
+    std::string kind = t[0].cast<std::string>();
+    OutCol c{};
+    if (kind == "table") {
+      c.kind = OutCol::kTable;
+      c.table = t[1].cast<TextTable*>();
+      h.keep.push_back(t[1]);
+      if (t.size() > 2) {
+        auto m = py::array_t<int64_t, py::array::c_style | py::array::forcecast>::ensure(t[2]);
+        if (!m || m.size() < n_rows_needed) throw std::invalid_argument("table row map too short");
+        const int64_t nr = (int64_t)c.table->rows.size();
+        for (py::ssize_t i = 0; i < m.size(); ++i)
+          if (m.data()[i] < 0 || m.data()[i] >= nr) throw std::invalid_argument("table row map out of range");
+        h.keep.push_back(m);
+        c.rowmap = m.data();
+      }
+    } else if (kind == "java" || kind == "py2row" || kind == "fixedrow") {
+      auto a = py::array_t<double, py::array::c_style | py::array::forcecast>::ensure(t[1]);
+      if (!a) throw std::invalid_argument("float64 array expected");
+      h.keep.push_back(a);
+      c.f64 = a.data();
+      if (kind == "java") {
+        c.kind = OutCol::kJava;
+        if (a.size() < n_rows_needed) throw std::invalid_argument("java column too short");
+      } else {
+        c.kind = kind == "py2row" ? OutCol::kPy2Row : OutCol::kFixedRow;
+        if (a.ndim() != 2) throw std::invalid_argument("row column needs a 2-D array");
+        c.width = (int)a.shape(1);
+        if (a.shape(0) < n_rows_needed) throw std::invalid_argument("row column too short");
+        c.text = t.size() > 2 ? t[2].cast<std::string>() : std::string(" ");
+      }
+    } else if (kind == "int") {
+      auto a = py::array_t<int64_t, py::array::c_style | py::array::forcecast>::ensure(t[1]);
+      if (!a) throw std::invalid_argument("int64 array expected");
+      if (a.size() < n_rows_needed) throw std::invalid_argument("int column too short");
+      h.keep.push_back(a);
+      c.kind = OutCol::kInt;
+      c.i64 = a.data();
+    } else if (kind == "dict" || kind == "pair") {
+      h.names.push_back(t[1].cast<std::vector<std::string>>());
+      c.names = &h.names.back();
+      auto a = py::array_t<int32_t, py::array::c_style | py::array::forcecast>::ensure(t[2]);
+      if (!a || a.size() < n_rows_needed) throw std::invalid_argument("index column too short");
+      h.keep.push_back(a);
+      c.idx = a.data();
+      const int64_t nn = (int64_t)c.names->size();
+      for (py::ssize_t i = 0; i < a.size(); ++i)
+        if (c.idx[i] >= nn || (kind == "pair" && c.idx[i] < 0)) throw std::invalid_argument("index out of range");
+      c.kind = kind == "dict" ? OutCol::kDict : OutCol::kPair;
+      if (kind == "pair") {
+        auto b = py::array_t<int32_t, py::array::c_style | py::array::forcecast>::ensure(t[3]);
+        if (!b || b.size() < n_rows_needed) throw std::invalid_argument("pair column too short");
+        for (py::ssize_t i = 0; i < b.size(); ++i)
+          if (b.data()[i] >= nn || b.data()[i] < 0) throw std::invalid_argument("index out of range");
+        h.keep.push_back(b);
+        c.idx2 = b.data();
+      }
+    } else if (kind == "const") {
+      c.kind = OutCol::kConst;
+      c.text = t[1].cast<std::string>();
+    } else {
+      throw std::invalid_argument("unknown column kind " + kind);
+    }
+    cols.push_back(std::move(c));
+  }
+  return cols;
+}
+
+PYBIND11_MODULE(_oninative, m) {
+  m.doc() = "oni_ml_amd C++ host runtime";
+
+  py::class_<TextTable>(m, "TextTable")
+      .def(py::init<int, std::vector<int>, std::vector<std::vector<int>>>(), py::arg("ncols"),
+           py::arg("numeric_cols"), py::arg("dict_groups"))
+      .def("load_files", &TextTable::load_files, py::arg("paths"), py::arg("drop_header") = true,
+           py::arg("threads") = default_threads(), py::call_guard<py::gil_scoped_release>())
+      .def("append_text", &TextTable::append_text, py::arg("text"), py::arg("weight") = 1,
+           py::arg("threads") = default_threads(), py::call_guard<py::gil_scoped_release>())
+      .def_property_readonly("num_rows", [](const TextTable& t) { return (int64_t)t.rows.size(); })
+      .def_readonly("header", &TextTable::header)
+      .def_readonly("n_bad_fields", &TextTable::n_bad_fields)
+      .def_readonly("n_bad_numeric", &TextTable::n_bad_numeric)
+      .def_readonly("n_header", &TextTable::n_header)
+      .def("numeric", [](const TextTable& t, int col) {
+        int s = t.numeric_slot(col);
+        if (s < 0) throw std::invalid_argument("column not parsed as numeric");
+        return to_np(t.num[s]);
+      })
+      .def("dict_ids", [](const TextTable& t, int col) {
+        int s = t.dict_slot(col);
+        if (s < 0) throw std::invalid_argument("column not dictionary-encoded");
+        return to_np(t.ids[s]);
+      })
+      .def("dict_names", [](const TextTable& t, int group) {
+        if (group < 0 || group >= (int)t.dicts.size()) throw std::invalid_argument("bad group");
+        return t.dicts[group].names;
+      })
+      .def("weights", [](const TextTable& t) { return to_np(t.weight); })
+      .def("row_text", [](const TextTable& t, int64_t i) {
+        if (i < 0 || i >= (int64_t)t.rows.size()) throw std::out_of_range("row");
+        return std::string(t.row_text((size_t)i));
+      });
+
+  m.def(
+      "write_rows",
+      [](const std::string& path, py::object order, py::list spec, const std::string& sep, bool append,
+         int threads, int64_t n) {
+        ColHolder h;
+        const int64_t* ord = nullptr;
+        py::array_t<int64_t, py::array::c_style | py::array::forcecast> oa;
+        int64_t max_row = n - 1;
+        if (!order.is_none()) {
+          oa = py::array_t<int64_t, py::array::c_style | py::array::forcecast>::ensure(order);
+          ord = oa.data();
+          n = oa.size();
+          max_row = -1;
+          for (int64_t i = 0; i < n; ++i) max_row = std::max(max_row, ord[i]);
+          for (int64_t i = 0; i < n; ++i)
+            if (ord[i] < 0) throw std::invalid_argument("negative row index");
+        }
+        auto cols = build_cols(spec, h, max_row + 1);
+        for (auto& c : cols)
+          if (c.kind == OutCol::kTable && !c.rowmap && max_row >= (int64_t)c.table->rows.size())
+            throw std::invalid_argument("row index beyond table");
+        py::gil_scoped_release rel;
+        return write_rows(path, ord, n, cols, sep, append, threads);
+      },
+      py::arg("path"), py::arg("order"), py::arg("cols"), py::arg("sep") = ",", py::arg("append") = false,
+      py::arg("threads") = default_threads(), py::arg("n") = -1);
+
+  m.def(
+      "dns_features",
+      [](py::buffer data, py::array_t<int64_t, py::array::c_style | py::array::forcecast> offsets,
+         std::vector<std::string> cc, std::vector<std::string> top, std::string special, int threads) {
+        py::buffer_info bi = data.request();
+        const int64_t n = offsets.size() - 1;
+        if (n < 0) throw std::invalid_argument("offsets must have n+1 entries");
+        const int64_t* off = offsets.data();
+        for (int64_t i = 0; i < n; ++i)
+          if (off[i] > off[i + 1] || off[i] < 0) throw std::invalid_argument("non-monotone offsets");
+        if (n >= 0 && off[n] > (int64_t)(bi.size * bi.itemsize)) throw std::invalid_argument("offsets beyond data");
+        DnsFeatures F;
+        {
+          py::gil_scoped_release rel;
+          F = dns_features((const char*)bi.ptr, off, n, cc, top, special, threads);
+        }
+        py::dict d;
+        d["domain_id"] = to_np(F.domain_id);
+        d["subdomain_id"] = to_np(F.sub_id);
+        d["subdomain_length"] = to_np(F.sub_len);
+        d["num_periods"] = to_np(F.num_parts);
+        d["entropy"] = to_np(F.entropy);
+        d["top_domain"] = to_np(F.top);
+        d["domains"] = F.domains;
+        d["subdomains"] = F.subs;
+        return d;
+      },
+      py::arg("data"), py::arg("offsets"), py::arg("country_codes"), py::arg("top_domains"),
+      py::arg("special") = "intel", py::arg("threads") = default_threads());
+
+  m.def("scala_entropy", [](const std::string& s) { return scala_entropy(s); });
+  m.def("java_double", [](double d) { return java_double(d); });
+  m.def("py2_float", [](double d) {
+    std::string s;
+    append_py2_float(s, d);
+    return s;
+  });
+  m.def("java_parse_double", [](const std::string& s) -> py::object {
+    double v;
+    if (!java_parse_double(s.data(), s.data() + s.size(), &v)) return py::none();
+    return py::float_(v);
+  });
+  m.def("java_double_array", [](py::array_t<double, py::array::c_style | py::array::forcecast> a) {
+    std::vector<std::string> out;
+    out.reserve(a.size());
+    for (py::ssize_t i = 0; i < a.size(); ++i) out.push_back(java_double(a.data()[i]));
+    return out;
+  });
+
+  // Value round trips through the reference's text hand-offs: "%5.10f"
+  // (final.gamma / final.beta read back by lda_post.py) and Python-2 str
+  // (doc_results.csv / word_results.csv read back by the Scala scorers).
+  auto roundtrip = [](py::array_t<double, py::array::c_style | py::array::forcecast> a, int mode, int threads) {
+    py::array_t<double> out(a.request().shape);
+    const double* src = a.data();
+    double* dst = out.mutable_data();
+    const int64_t n = a.size();
+    if (threads <= 0) threads = default_threads();
+    if (n < 65536) threads = 1;
+    {
+      py::gil_scoped_release rel;
+      auto work = [&](int t) {
+        std::string s;
+        for (int64_t i = n * t / threads; i < n * (t + 1) / threads; ++i) {
+          s.clear();
+          if (mode == 0) append_fixed10(s, src[i]);
+          else append_py2_float(s, src[i]);
+          dst[i] = std::strtod(s.c_str(), nullptr);
+        }
+      };
+      std::vector<std::thread> th;
+      for (int t = 1; t < threads; ++t) th.emplace_back(work, t);
+      work(0);
+      for (auto& x : th) x.join();
+    }
+    return out;
+  };
+  m.def("roundtrip_fixed10", [roundtrip](py::array_t<double, py::array::c_style | py::array::forcecast> a, int threads) {
+    return roundtrip(a, 0, threads);
+  }, py::arg("a"), py::arg("threads") = 0);
+  m.def("roundtrip_py2", [roundtrip](py::array_t<double, py::array::c_style | py::array::forcecast> a, int threads) {
+    return roundtrip(a, 1, threads);
+  }, py::arg("a"), py::arg("threads") = 0);
+
+  // ---------------------------------------------------------------- lda-c --
+  m.def("digamma", &ldac_digamma);
+  m.def("trigamma", &ldac_trigamma);
+  m.def("log_sum", &ldac_log_sum);
+  m.def("opt_alpha", &ldac_opt_alpha, py::arg("ss"), py::arg("D"), py::arg("K"));
+  m.def(
+      "lda_estep_ldac",
+      [](py::array_t<int64_t, py::array::c_style | py::array::forcecast> doc_ptr,
+         py::array_t<int32_t, py::array::c_style | py::array::forcecast> words,
+         py::array_t<double, py::array::c_style | py::array::forcecast> counts,
+         py::array_t<double, py::array::c_style | py::array::forcecast> log_beta, double alpha, int var_max_iter,
+         double var_conv, int nshards, int threads) {
+        const int D = (int)doc_ptr.size() - 1;
+        if (log_beta.ndim() != 2) throw std::invalid_argument("log_beta must be [K, V]");
+        const int K = (int)log_beta.shape(0), V = (int)log_beta.shape(1);
+        if (words.size() != counts.size() || doc_ptr.data()[D] != words.size())
+          throw std::invalid_argument("inconsistent corpus arrays");
+        for (py::ssize_t i = 0; i < words.size(); ++i)
+          if (words.data()[i] < 0 || words.data()[i] >= V) throw std::invalid_argument("word id out of range");
+        if (threads <= 0) threads = default_threads();
+        EStepOut r;
+        {
+          py::gil_scoped_release rel;
+          r = ldac_estep(doc_ptr.data(), words.data(), counts.data(), D, V, K, log_beta.data(), alpha,
+                         var_max_iter, (float)var_conv, nshards, threads);
+        }
+        py::dict d;
+        d["likelihood"] = r.likelihood;
+        d["alpha_ss"] = r.alpha_ss;
+        py::array_t<double> cw({K, V});
+        std::memcpy(cw.mutable_data(), r.class_word.data(), r.class_word.size() * sizeof(double));
+        d["class_word"] = cw;
+        d["class_total"] = to_np(r.class_total);
+        py::array_t<double> g({D, K});
+        if (!r.gamma.empty()) std::memcpy(g.mutable_data(), r.gamma.data(), r.gamma.size() * sizeof(double));
+        d["gamma"] = g;
+        d["iters"] = to_np(r.iters);
+        d["doc_likelihood"] = to_np(r.doc_lik);
+        return d;
+      },
+      py::arg("doc_ptr"), py::arg("words"), py::arg("counts"), py::arg("log_beta"), py::arg("alpha"),
+      py::arg("var_max_iter"), py::arg("var_conv"), py::arg("nshards") = 1, py::arg("threads") = 0);
+}

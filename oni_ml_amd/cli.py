@@ -1,0 +1,222 @@
+"""Command line: ``python -m oni_ml_amd <command> ...`` (and scripts/ml_ops.sh).
+
+  ml_ops YYYYMMDD {flow|dns} [TOL] [options]   end-to-end run (reference ml_ops.sh:1-123)
+  lda est <alpha> <k> <settings> <nproc> <corpus> <random|seeded|prefix> <dir>
+                                               oni-lda-c command line (ml_ops.sh:80) on the MI355X engine
+  lda inf <settings> <model-prefix> <corpus> <name>
+  lda_pre <LPATH>/                             lda_pre.py equivalent (doc_wc.dat -> words/doc/model.dat)
+  lda_post <LPATH>/                            lda_post.py equivalent (final.* -> doc/word_results.csv)
+  synth {flow|dns} --out DIR ...               synthetic inputs (flow CSV day, DNS parquet, top-1m.csv)
+  qtiles <flow_qtiles>                         print cuts of the legacy qtiles format
+
+Multi-GPU: launch with torchrun (one process per GPU); ranks share the LDA
+stage over RCCL, rank 0 runs featurization, export and scoring.
+"""
+from __future__ import annotations
+
+import argparse
+import glob
+import json
+import os
+import shutil
+import subprocess
+import sys
+import time
+
+SYNTAX = """ml_ops.sh syntax error
+Please run ml_ops.sh again with the correct syntax:
+./ml_ops.sh YYYYMMDD TYPE [TOL]
+for example:
+./ml_ops.sh 20160122 dns 1e-6
+./ml_ops.sh 20160122 flow"""
+
+
+def _common_lda_args(ap):
+    ap.add_argument("--backend", default="auto", choices=["auto", "hip", "torch", "cpu"])
+    ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--verbose", action="store_true")
+
+
+def clean_workdir(lpath: str):
+    """ml_ops.sh:53-54: remove stale *.dat,*.beta,*.gamma,*.other,*.pkl; keep *.csv (analyst feedback)."""
+    for pat in ("*.dat", "*.beta", "*.gamma", "*.other", "*.pkl", "checkpoint.npz"):
+        for f in glob.glob(os.path.join(lpath, pat)):
+            os.unlink(f)
+    shutil.rmtree(os.path.join(lpath, ".stages"), ignore_errors=True)
+
+
+def cmd_ml_ops(argv):
+    ap = argparse.ArgumentParser(prog="ml_ops", description="suspicious-connects end-to-end run")
+    ap.add_argument("fdate", nargs="?", default="")
+    ap.add_argument("dsource", nargs="?", default="")
+    ap.add_argument("tol", nargs="?", default=None)
+    ap.add_argument("--conf", default=os.environ.get("ONI_CONF", "/etc/duxbay.conf"))
+    ap.add_argument("--lpath")
+    ap.add_argument("--flow-path")
+    ap.add_argument("--dns-path")
+    ap.add_argument("--top1m")
+    ap.add_argument("--topics", type=int, default=20)
+    ap.add_argument("--alpha", type=float, default=2.5)
+    ap.add_argument("--settings", help="lda-c settings.txt (default: upstream lda-c defaults)")
+    ap.add_argument("--dupfactor", type=int)
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--compat", default="strict", choices=["strict", "fixed"])
+    ap.add_argument("--start", default="random")
+    ap.add_argument("--resume", action="store_true")
+    ap.add_argument("--keep-doc-wc", action="store_true", help="keep doc_wc.dat (the reference deletes it)")
+    ap.add_argument("--word-assignments", action="store_true")
+    ap.add_argument("--rank-gamma", action="store_true", help="also write <rank>.gamma per GPU")
+    ap.add_argument("--threads", type=int, default=8)
+    ap.add_argument("--deliver", action="store_true", help="scp -r LPATH UINODE:RPATH (ml_ops.sh:121)")
+    ap.add_argument("--quiet", action="store_true")
+    _common_lda_args(ap)
+    a = ap.parse_args(argv)
+    if len(a.fdate) != 8 or not a.dsource:
+        print(SYNTAX)
+        return 1
+    from . import config as CFG
+    from .models.lda.settings import LDASettings
+    from .parallel import dist as D
+
+    ctx = D.init_from_env(expected_world=a.gpus if a.gpus > 1 else None)
+    cfg = CFG.resolve(a.fdate, a.dsource, tol=float(a.tol) if a.tol is not None else None, conf_path=a.conf,
+                      lpath=a.lpath, flow_path=a.flow_path, dns_path=a.dns_path, top1m=a.top1m, topics=a.topics,
+                      alpha=a.alpha, dupfactor=a.dupfactor, gpus=ctx.world_size, backend=a.backend, compat=a.compat,
+                      seed=a.seed, start=a.start, resume=a.resume, threads=a.threads, write_doc_wc=a.keep_doc_wc,
+                      word_assignments=a.word_assignments, rank_gamma=a.rank_gamma, verbose=not a.quiet)
+    if a.settings:
+        cfg.settings = LDASettings.load(a.settings)
+    cfg.validate()
+    from .pipeline import run
+    from .pipeline.runner import RunLock
+    log = (lambda *x, **k: None) if (a.quiet or ctx.rank != 0) else print
+    t0 = time.perf_counter()
+    lock = None
+    if ctx.rank == 0:
+        os.makedirs(cfg.lpath, exist_ok=True)
+        if not cfg.resume:
+            clean_workdir(cfg.lpath)
+        lock = RunLock(os.path.join(cfg.lpath, ".lock")).__enter__()
+    ctx.barrier()
+    try:
+        summary = run(cfg, dist=ctx if ctx.world_size > 1 else None, device=ctx.device, log=log)
+    finally:
+        if lock is not None:
+            lock.__exit__(None, None, None)
+    if ctx.rank == 0:
+        summary["wall_seconds"] = time.perf_counter() - t0
+        with open(os.path.join(cfg.lpath, "run_summary.json"), "w") as f:
+            json.dump(summary, f, indent=1, default=str)
+        log(json.dumps(summary, default=str))
+        if a.deliver:
+            ui, rp = cfg.extra.get("UINODE"), cfg.extra.get("RPATH")
+            if ui and rp:
+                subprocess.run(["scp", "-r", cfg.lpath, f"{ui}:{rp}"], check=True)
+    ctx.shutdown()
+    return 0
+
+
+def cmd_lda(argv):
+    if not argv or argv[0] not in ("est", "inf"):
+        print("usage: lda est [initial alpha] [k] [settings] [nproc] [data] [random/seeded/*] [directory]\n"
+              "       lda inf [settings] [model] [data] [name]")
+        return 1
+    from .io import ldac
+    from .models.lda.settings import LDASettings
+    if argv[0] == "est":
+        ap = argparse.ArgumentParser(prog="lda est")
+        for n in ("alpha", "k", "settings", "nproc", "data", "start", "directory"):
+            ap.add_argument(n)
+        ap.add_argument("--resume", action="store_true")
+        ap.add_argument("--word-assignments", action="store_true", default=True)
+        _common_lda_args(ap)
+        a = ap.parse_args(argv[1:])
+        from .models.lda.estimate import estimate
+        from .parallel import dist as D
+        ctx = D.init_from_env()
+        corpus = ldac.read_model_dat(a.data)
+        st = LDASettings.load(a.settings)
+        res = estimate(corpus, int(a.k), float(a.alpha), st, a.start, a.directory, backend=a.backend,
+                       device=ctx.device, dist=ctx if ctx.world_size > 1 else None, seed=a.seed, resume=a.resume,
+                       write_word_assignments=a.word_assignments, verbose=True)
+        if ctx.rank == 0:
+            print(f"em iterations: {res.em_iterations}  seconds: {res.seconds:.3f}")
+        ctx.shutdown()
+        return 0
+    ap = argparse.ArgumentParser(prog="lda inf")
+    for n in ("settings", "model", "data", "name"):
+        ap.add_argument(n)
+    _common_lda_args(ap)
+    a = ap.parse_args(argv[1:])
+    from .models.lda.inference import infer_files
+    infer_files(a.settings, a.model, a.data, a.name, backend=a.backend)
+    return 0
+
+
+def cmd_lda_pre(argv):
+    """lda_pre.py <LPATH>/ : doc_wc.dat -> words.dat, doc.dat, model.dat."""
+    rpath = argv[0]
+    from .corpus.builder import lda_pre, read_doc_wc
+    from .pipeline.common import write_corpus_files
+    dwc, ips, words = read_doc_wc(os.path.join(rpath, "doc_wc.dat"))
+    built = lda_pre(dwc)
+    write_corpus_files(rpath, built, [ips[i] for i in built.doc_keys.tolist()], [words[i] for i in built.word_keys.tolist()])
+    print(f"docs {built.corpus.num_docs} words {built.corpus.num_terms} entries {built.corpus.nnz}")
+    return 0
+
+
+def cmd_lda_post(argv):
+    """lda_post.py <LPATH>/ : final.gamma + final.beta + doc.dat + words.dat -> doc/word_results.csv."""
+    ap = argparse.ArgumentParser(prog="lda_post")
+    ap.add_argument("rpath")
+    ap.add_argument("--compat", default="strict", choices=["strict", "fixed"])
+    a = ap.parse_args(argv)
+    from .export import lda_post
+    from .io import ldac
+    r = a.rpath
+    gamma = ldac.load_gamma(os.path.join(r, "final.gamma"))
+    lb = ldac.load_beta(os.path.join(r, "final.beta"))
+    lda_post.export(ldac.read_index_file(os.path.join(r, "doc.dat")), gamma, ldac.read_index_file(os.path.join(r, "words.dat")),
+                    lb, os.path.join(r, "doc_results.csv"), os.path.join(r, "word_results.csv"), strict=a.compat == "strict")
+    return 0
+
+
+def cmd_synth(argv):
+    ap = argparse.ArgumentParser(prog="synth")
+    ap.add_argument("kind", choices=["flow", "dns"])
+    ap.add_argument("--out", required=True)
+    ap.add_argument("--events", type=int, default=1_000_000)
+    ap.add_argument("--files", type=int, default=1)
+    ap.add_argument("--seed", type=int, default=0)
+    a = ap.parse_args(argv)
+    if a.kind == "flow":
+        from .synth.flow import generate_flow_day
+        print(generate_flow_day(a.out, a.events, a.seed, files=a.files))
+    else:
+        from .synth.dns import generate_dns_day
+        print(generate_dns_day(a.out, a.events, a.seed, files=a.files))
+    return 0
+
+
+def cmd_qtiles(argv):
+    from .features.quantiles import parse_qtiles
+    with open(argv[0]) as f:
+        q = parse_qtiles(f.read())
+    print(json.dumps({k: v.tolist() for k, v in q.items()}))
+    return 0
+
+
+COMMANDS = dict(ml_ops=cmd_ml_ops, lda=cmd_lda, lda_pre=cmd_lda_pre, lda_post=cmd_lda_post, synth=cmd_synth,
+                qtiles=cmd_qtiles)
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    if not argv or argv[0] not in COMMANDS:
+        print(__doc__)
+        return 1
+    return COMMANDS[argv[0]](argv[1:])
+
+
+if __name__ == "__main__":
+    sys.exit(main())

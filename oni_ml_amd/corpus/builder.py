@@ -1,0 +1,142 @@
+"""Corpus builder: (doc, word) event pairs -> doc_wc -> lda-c corpus (lda_pre.py equivalent).
+
+Reference pipeline:
+* the pre-LDA stage counts (ip, word) pairs with reduceByKey -- twice for flow
+  (source side and destination side, flow_pre_lda.scala:366-373) and unions the
+  two results WITHOUT merging, so one (ip, word) can appear twice;
+* lda_pre.py reads the resulting ``ip,word,count`` lines and assigns word ids
+  in first-appearance order (0-based, words.dat), doc ids in first-appearance
+  order (1-based, doc.dat), and writes each doc's entries in line order
+  (model.dat).
+
+Here the counting is a sort-based group-by on packed int64 keys on the device
+(torch.unique), and the lda_pre dictionaries are first-appearance ranks
+computed with scatter-min; nothing is materialised as text unless asked.
+The reference's doc_wc line order is Spark hash-partition order (not
+reproducible); ours is deterministic: section by section, pairs sorted by
+(ip dictionary id, word key).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import List, Optional, Sequence, Tuple
+
+import numpy as np
+import torch
+
+from .csr import Corpus
+
+_SHIFT = 32
+
+
+@dataclass
+class DocWordCounts:
+    """doc_wc in line order (device tensors)."""
+    doc: torch.Tensor      # int64 ip/doc dictionary ids
+    word: torch.Tensor     # int64 word keys
+    count: torch.Tensor    # int64
+
+    @property
+    def n(self) -> int:
+        return int(self.doc.numel())
+
+
+def count_pairs(doc: torch.Tensor, word: torch.Tensor, weight: Optional[torch.Tensor] = None) -> DocWordCounts:
+    """reduceByKey((doc, word), +weight) with output sorted by (doc, word)."""
+    if doc.numel() and (int(word.min()) < 0 or int(word.max()) >= (1 << _SHIFT)):
+        raise ValueError("word keys must fit in 32 bits")
+    pk = (doc.to(torch.int64) << _SHIFT) | word.to(torch.int64)
+    uniq, inv = torch.unique(pk, sorted=True, return_inverse=True)
+    w = torch.ones_like(pk) if weight is None else weight.to(device=pk.device, dtype=torch.int64)
+    cnt = torch.zeros(uniq.numel(), dtype=torch.int64, device=pk.device).index_add_(0, inv, w)
+    return DocWordCounts(uniq >> _SHIFT, uniq & ((1 << _SHIFT) - 1), cnt)
+
+
+def concat(parts: Sequence[DocWordCounts], merge: bool = False) -> DocWordCounts:
+    """Union of sections; merge=True sums duplicate (doc, word) pairs across sections."""
+    doc = torch.cat([p.doc for p in parts])
+    word = torch.cat([p.word for p in parts])
+    cnt = torch.cat([p.count for p in parts])
+    if merge:
+        return count_pairs(doc, word, cnt)
+    return DocWordCounts(doc, word, cnt)
+
+
+def _first_appearance_ids(keys: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+    """ids[i] = rank of keys[i]'s first appearance; returns (ids, distinct keys in rank order)."""
+    n = keys.numel()
+    uniq, inv = torch.unique(keys, sorted=True, return_inverse=True)
+    pos = torch.arange(n, device=keys.device, dtype=torch.int64)
+    first = torch.full((uniq.numel(),), n, dtype=torch.int64, device=keys.device)
+    first.scatter_reduce_(0, inv, pos, reduce="amin", include_self=True)
+    order = torch.argsort(first)
+    rank = torch.empty_like(order)
+    rank[order] = torch.arange(order.numel(), device=keys.device)
+    return rank[inv], uniq[order]
+
+
+@dataclass
+class BuiltCorpus:
+    corpus: Corpus
+    doc_keys: np.ndarray     # [D] ip dictionary id of each doc (doc.dat order)
+    word_keys: np.ndarray    # [V] word key of each word id (words.dat order)
+
+
+def lda_pre(dwc: DocWordCounts) -> BuiltCorpus:
+    """lda_pre.py semantics on device: first-appearance word / doc ids, entries grouped by doc in line order."""
+    if dwc.n == 0:
+        raise ValueError("empty doc_wc: no (ip, word) pairs survived featurization")
+    wid, wkeys = _first_appearance_ids(dwc.word)
+    did, dkeys = _first_appearance_ids(dwc.doc)
+    order = torch.sort(did, stable=True).indices
+    d_sorted = did[order]
+    D = int(dkeys.numel())
+    lens = torch.bincount(d_sorted, minlength=D)
+    ptr = torch.zeros(D + 1, dtype=torch.int64, device=lens.device)
+    ptr[1:] = torch.cumsum(lens, 0)
+    corpus = Corpus(
+        doc_ptr=ptr.cpu().numpy(),
+        word_idx=wid[order].to(torch.int32).cpu().numpy(),
+        counts=dwc.count[order].cpu().numpy(),
+        num_terms=int(wkeys.numel()),
+    )
+    return BuiltCorpus(corpus, dkeys.cpu().numpy(), wkeys.cpu().numpy())
+
+
+def lda_pre_reference(lines: List[Tuple[str, str, int]]):
+    """Literal lda_pre.py (test oracle): returns (words list, docs list, model lines)."""
+    wcdict, words = {}, []
+    for ip, w, c in lines:
+        if w not in wcdict:
+            wcdict[w] = len(words)
+            words.append(w)
+    docdict, docs = {}, []
+    for ip, w, c in lines:
+        if ip in docdict:
+            docdict[ip][1] += 1
+            docdict[ip][2].append(" %s:%s" % (wcdict[w], c))
+        else:
+            docdict[ip] = [len(docs) + 1, 1, [" %s:%s" % (wcdict[w], c)]]
+            docs.append(ip)
+    model = ["%s%s" % (docdict[ip][1], "".join(docdict[ip][2])) for ip in docs]
+    return words, docs, model
+
+
+def read_doc_wc(path: str, threads: int = 8):
+    """Parse a doc_wc.dat (``ip,word,count``) with the C++ ingest: returns (DocWordCounts on CPU, ip names, word names)."""
+    from ..ops import native
+    t = native.lib().TextTable(3, [2], [[0], [1]])
+    t.load_files([path], drop_header=False, threads=threads)
+    dwc = DocWordCounts(torch.from_numpy(t.dict_ids(0).astype(np.int64)),
+                        torch.from_numpy(t.dict_ids(1).astype(np.int64)),
+                        torch.from_numpy(t.numeric(2).astype(np.int64)))
+    return dwc, t.dict_names(0), t.dict_names(1)
+
+
+def write_doc_wc(path: str, dwc: DocWordCounts, doc_names: Sequence[str], word_names_of_key):
+    """Write doc_wc.dat lines ``ip,word,count`` (word_names_of_key: callable keys -> (names list, index array))."""
+    from ..ops import native
+    names, idx = word_names_of_key(dwc.word.cpu().numpy())
+    native.lib().write_rows(path, None, [("dict", list(doc_names), dwc.doc.cpu().numpy().astype(np.int32)),
+                                         ("dict", names, idx.astype(np.int32)),
+                                         ("int", dwc.count.cpu().numpy())], n=dwc.n)

@@ -1,0 +1,104 @@
+"""Model export: the lda_post.py equivalent (reference lda_post.py:1-123).
+
+* doc_results.csv  - ``ip,θ1 θ2 … θK``: θ = γ/Σγ per document (20 zeros when
+  Σγ <= 0), the document name taken from doc.dat line j (lda_post.py:35-63).
+* word_results.csv - ``word,p1 … pK``: per topic p(w|z) = exp(logβ)/Σ_w exp(logβ),
+  transposed to one line per word (lda_post.py:70-122).
+
+Values are Python-2 ``str(float)`` text ("%.12g"); sums run sequentially like
+Python's builtin ``sum`` over numpy float64.  In ``strict`` compat mode the
+inputs are first rounded through the "%5.10f" text lda-c writes (lda_post.py
+reads final.gamma / final.beta back from disk), words are truncated to 20
+bytes (the ``dtype="S20"`` array, lda_post.py:78-84) and K must be 20
+(the hard-coded 20-column format, lda_post.py:42,115).
+"""
+from __future__ import annotations
+
+from typing import Sequence, Tuple
+
+import numpy as np
+
+from ..ops import native
+
+
+def doc_topics(gamma: np.ndarray, strict: bool = True) -> np.ndarray:
+    """θ [D, K] float64 from γ [D, K]."""
+    g = np.asarray(gamma, np.float64)
+    if strict:
+        g = native.lib().roundtrip_fixed10(np.ascontiguousarray(g))
+    if g.size == 0:
+        return g.copy()
+    total = np.cumsum(g, axis=1)[:, -1]
+    theta = np.zeros_like(g)
+    pos = total > 0
+    theta[pos] = g[pos] / total[pos, None]
+    return theta
+
+
+def word_topics(log_beta: np.ndarray, strict: bool = True) -> np.ndarray:
+    """p(w|z) [V, K] float64 from log β [K, V]."""
+    lb = np.asarray(log_beta, np.float64)
+    if strict:
+        lb = native.lib().roundtrip_fixed10(np.ascontiguousarray(lb))
+    raw = np.exp(lb)
+    total = np.cumsum(raw, axis=1)[:, -1:]
+    return np.ascontiguousarray((raw / total).T)
+
+
+def truncate_s20(names: Sequence[str]) -> list:
+    """numpy dtype 'S20' assignment: the UTF-8 bytes cut to 20 (trailing NULs dropped on read)."""
+    out = []
+    for n in names:
+        b = n.encode("utf-8")[:20].rstrip(b"\x00")
+        out.append(b.decode("utf-8", errors="ignore"))
+    return out
+
+
+def check_strict_k(K: int, strict: bool):
+    if strict and K != 20:
+        raise ValueError("compat=strict reproduces lda_post.py's hard-coded 20 topics; use compat=fixed for K != 20")
+
+
+def write_doc_results(path: str, doc_names: Sequence[str], theta: np.ndarray, threads: int = 8) -> int:
+    n = len(doc_names)
+    if theta.shape[0] != n:
+        raise ValueError("doc names / theta rows differ")
+    return native.lib().write_rows(path, None, [("dict", list(doc_names), np.arange(n, dtype=np.int32)),
+                                                ("py2row", np.ascontiguousarray(theta, np.float64), " ")],
+                                   threads=threads, n=n)
+
+
+def write_word_results(path: str, word_names: Sequence[str], phi: np.ndarray, threads: int = 8) -> int:
+    n = len(word_names)
+    if phi.shape[0] != n:
+        raise ValueError("word names / phi rows differ")
+    return native.lib().write_rows(path, None, [("dict", list(word_names), np.arange(n, dtype=np.int32)),
+                                                ("py2row", np.ascontiguousarray(phi, np.float64), " ")],
+                                   threads=threads, n=n)
+
+
+def export(doc_names, gamma, word_names, log_beta, doc_path, word_path, strict=True) -> Tuple[np.ndarray, np.ndarray, list]:
+    """Write both files; returns (θ, φ, word keys as written) as the scorers will read them back."""
+    check_strict_k(gamma.shape[1], strict)
+    theta = doc_topics(gamma, strict)
+    phi = word_topics(log_beta, strict)
+    wnames = truncate_s20(word_names) if strict else list(word_names)
+    write_doc_results(doc_path, doc_names, theta)
+    write_word_results(word_path, wnames, phi)
+    return theta, phi, wnames
+
+
+def read_results(path: str):
+    """doc_results.csv / word_results.csv -> (keys, values [n, K]) as the Scala scorers parse them
+    (key = field 0, values = field 1 with quotes removed, split on ' ', toDouble;
+    flow_post_lda.scala:107-123).  Later duplicate keys win (collectAsMap)."""
+    keys, vals = [], []
+    with open(path, "r", encoding="utf-8") as f:
+        for line in f:
+            line = line.rstrip("\n")
+            if not line:
+                continue
+            parts = line.split(",")
+            keys.append(parts[0])
+            vals.append([float(x) for x in parts[1].replace('"', "").split(" ")])
+    return keys, np.asarray(vals, np.float64)

@@ -1,0 +1,272 @@
+"""DNS featurization: parquet -> per-query words -> (ip_dst, word) counts.
+
+Reference: dns_pre_lda.scala (pre-LDA) and dns_post_lda.scala:108-297 (repeated
+before scoring); SURVEY.md C6a-C6i, C7b.
+
+* input: Hive/parquet paths (comma-separated DNS_PATH); the reference reads
+  path 0 and then only paths with index > 1, silently skipping index 1
+  (dns_pre_lda.scala:142-148) -- reproduced in compat=strict;
+* rows with null frame_len / unix_tstamp are dropped; each row is printed with
+  Row.mkString(",") (nulls become "null") and kept only if it splits back
+  into exactly 8 fields (a comma inside any value drops the row);
+* analyst feedback: dns_scores.csv rows with dns_sev == 3 (24-col schema,
+  dns_pre_lda.scala:84-139), weight DUPFACTOR;
+* per-name features (domain / subdomain / lengths / Scala-order entropy /
+  top-1m flag) in the multithreaded C++ parser (csrc/native/dns.cpp);
+* cuts: deciles of unix_tstamp and frame_len, quintiles of subdomain length,
+  entropy and label count over values > 0 only; bins on the device;
+* word = top _ bin(frame_len) _ bin(tstamp) _ bin(sublen) _ bin(entropy) _
+  bin(labels) _ qry_type _ qry_rcode (integers, dns_pre_lda.scala:320-327).
+"""
+from __future__ import annotations
+
+import os
+from dataclasses import dataclass, field
+from typing import Dict, List, Optional, Sequence
+
+import numpy as np
+import torch
+
+from ..ops import native
+from .dns_data import COUNTRY_CODES, SPECIAL_DOMAIN
+from .quantiles import DECILES, QUINTILES, ecdf_cuts
+
+COLUMNS = ["frame_time", "unix_tstamp", "frame_len", "ip_dst", "dns_qry_name", "dns_qry_class", "dns_qry_type",
+           "dns_qry_rcode"]
+FEEDBACK_IDX = dict(frame_time=0, unix_tstamp=23, frame_len=1, ip_dst=2, dns_qry_name=3, dns_qry_class=4,
+                    dns_qry_type=5, dns_qry_rcode=6, dns_sev=18)
+
+
+def _pa():
+    import pyarrow as pa
+    import pyarrow.compute as pc
+    import pyarrow.parquet as pq
+    return pa, pc, pq
+
+
+def select_paths(dns_path: str, strict: bool) -> List[str]:
+    paths = [p for p in dns_path.split(",")]
+    if strict:
+        return [p for i, p in enumerate(paths) if i == 0 or i > 1]
+    return [p for p in paths if p]
+
+
+def _java_split_len(line: str) -> int:
+    parts = line.split(",")
+    while parts and parts[-1] == "":
+        parts.pop()
+    return len(parts) if line else 1
+
+
+def read_dns_feedback(path: str) -> List[List[str]]:
+    """dns_scores.csv rows with dns_sev == 3 as the 8 selected string fields."""
+    if not path or not os.path.exists(path):
+        return []
+    with open(path, "r", encoding="utf-8", newline="") as fh:
+        lines = fh.read().split("\n")
+    if lines and lines[-1] == "":
+        lines.pop()
+    out = []
+    for l in lines[1:]:
+        f = l.rstrip("\r").split(",")
+        while f and f[-1] == "":
+            f.pop()
+        if len(f) < 24:
+            continue   # the reference would throw ArrayIndexOutOfBounds
+        try:
+            flen = int(f[FEEDBACK_IDX["frame_len"]].strip())
+            sev = int(f[FEEDBACK_IDX["dns_sev"]].strip())
+        except ValueError:
+            continue
+        if sev != 3:
+            continue
+        row = [f[FEEDBACK_IDX[c]] for c in COLUMNS]
+        row[2] = str(flen)
+        out.append(row)
+    return out
+
+
+def _java_double(s: str) -> Optional[float]:
+    return native.lib().java_parse_double(s)
+
+
+@dataclass
+class DnsTable:
+    """The 8 selected columns as strings (mkString semantics) + weights; feedback rows last."""
+    cols: Dict[str, list]          # name -> list[str] (kept for output, dictionary-encoded lazily)
+    frame_len: np.ndarray          # f64
+    unix_tstamp: np.ndarray        # f64
+    weight: np.ndarray             # int64
+    n_raw: int
+    n_feedback: int
+    dropped: int = 0
+
+    @property
+    def n(self) -> int:
+        return self.n_raw + self.n_feedback
+
+
+def _arrow_strings(pa, pc, col):
+    if not pa.types.is_string(col.type) and not pa.types.is_large_string(col.type):
+        col = pc.cast(col, pa.string())
+    return pc.fill_null(col, "null")
+
+
+def load_dns(dns_path: str, feedback_path: Optional[str] = None, dupfactor: int = 1000, strict: bool = True) -> DnsTable:
+    pa, pc, pq = _pa()
+    tables = []
+    for p in select_paths(dns_path, strict):
+        if not p:
+            continue
+        t = pq.read_table(p, columns=COLUMNS)
+        t = t.filter(pc.and_(pc.is_valid(t["frame_len"]), pc.is_valid(t["unix_tstamp"])))
+        tables.append(t)
+    if not tables:
+        raise FileNotFoundError(f"no DNS input in {dns_path!r}")
+    t = pa.concat_tables(tables, promote_options="permissive") if len(tables) > 1 else tables[0]
+    strs = {c: _arrow_strings(pa, pc, t[c]).combine_chunks() for c in COLUMNS}
+    # Row.mkString(",").split(",") must give back 8 fields: no comma anywhere; trailing empty fields vanish
+    bad = None
+    for c in COLUMNS:
+        m = pc.match_substring(strs[c], ",")
+        bad = m if bad is None else pc.or_(bad, m)
+    bad = pc.or_(bad, pc.equal(pc.utf8_length(strs[COLUMNS[-1]]), 0))
+    keep = pc.invert(bad)
+    n_before = len(t)
+    strs = {c: pc.filter(v, keep) for c, v in strs.items()}
+    flen = pc.filter(t["frame_len"], keep).to_numpy(zero_copy_only=False).astype(np.float64)
+    tst = pc.filter(t["unix_tstamp"], keep).to_numpy(zero_copy_only=False).astype(np.float64)
+    cols = {c: v.to_pylist() for c, v in strs.items()}
+    n_raw = len(flen)
+    fb = read_dns_feedback(feedback_path) if feedback_path else []
+    fb_ok = []
+    for r in fb:
+        if any("," in x for x in r) or r[-1] == "":
+            continue
+        a, b = _java_double(r[2]), _java_double(r[1])
+        if a is None or b is None:
+            continue
+        fb_ok.append((r, a, b))
+    for r, a, b in fb_ok:
+        for c, v in zip(COLUMNS, r):
+            cols[c].append(v)
+    if fb_ok:
+        flen = np.concatenate([flen, np.array([a for _, a, _ in fb_ok])])
+        tst = np.concatenate([tst, np.array([b for _, _, b in fb_ok])])
+    w = np.ones(len(flen), np.int64)
+    w[n_raw:] = dupfactor
+    return DnsTable(cols, flen, tst, w, n_raw, len(fb_ok), dropped=n_before - n_raw)
+
+
+def load_top_domains(path: Optional[str]) -> List[str]:
+    """top-1m.csv (`rank,domain`) -> first label of each domain (dns_pre_lda.scala:62-66)."""
+    if not path or not os.path.exists(path):
+        return []
+    out = []
+    with open(path, "r", encoding="utf-8", errors="replace") as f:
+        for line in f:
+            parts = line.rstrip("\n").split(",")
+            if len(parts) < 2:
+                continue
+            out.append(parts[1].split(".")[0])
+    return out
+
+
+def _offsets(names: List[str]):
+    enc = [s.encode("utf-8") for s in names]
+    off = np.zeros(len(enc) + 1, np.int64)
+    np.cumsum([len(b) for b in enc], out=off[1:])
+    return b"".join(enc), off
+
+
+@dataclass
+class DnsFeatures:
+    rows: np.ndarray                  # table rows featurized
+    ip: torch.Tensor                  # int64 ip_dst dictionary id
+    ip_names: List[str]
+    word_key: torch.Tensor            # int64
+    weight: torch.Tensor
+    bins: Dict[str, torch.Tensor]
+    cuts: Dict[str, np.ndarray]
+    host: dict                        # C++ name features (host arrays)
+    qpairs: List[str]                 # "type_rcode" dictionary
+
+
+def dictionary_encode(values: List[str]):
+    """First-appearance ids + names."""
+    d = {}
+    ids = np.empty(len(values), np.int32)
+    for i, v in enumerate(values):
+        j = d.get(v)
+        if j is None:
+            j = len(d)
+            d[v] = j
+        ids[i] = j
+    return ids, list(d.keys())
+
+
+def featurize(tab: DnsTable, device, top_domains: Sequence[str], cuts: Optional[Dict[str, np.ndarray]] = None,
+              raw_only: bool = False, threads: int = 8) -> DnsFeatures:
+    device = torch.device(device)
+    n = tab.n_raw if raw_only else tab.n
+    names = tab.cols["dns_qry_name"][:n]
+    data, off = _offsets(names)
+    F = native.lib().dns_features(data, off, list(COUNTRY_CODES), list(top_domains), SPECIAL_DOMAIN, threads)
+    w = torch.from_numpy(tab.weight[:n]).to(device)
+    vals = dict(
+        frame_len=torch.from_numpy(tab.frame_len[:n]).to(device),
+        unix_tstamp=torch.from_numpy(tab.unix_tstamp[:n]).to(device),
+        subdomain_length=torch.from_numpy(F["subdomain_length"].astype(np.float64)).to(device),
+        entropy=torch.from_numpy(F["entropy"]).to(device),
+        num_periods=torch.from_numpy(F["num_periods"].astype(np.float64)).to(device),
+    )
+    if cuts is None:
+        cuts_t = {}
+        for k, q in (("unix_tstamp", DECILES), ("frame_len", DECILES)):
+            cuts_t[k] = ecdf_cuts(vals[k], q, w)
+        for k in ("subdomain_length", "entropy", "num_periods"):
+            m = vals[k] > 0
+            cuts_t[k] = ecdf_cuts(vals[k][m], QUINTILES, w[m])
+    else:
+        cuts_t = {k: torch.as_tensor(np.asarray(v, np.float64), device=device) for k, v in cuts.items()}
+    bins = {k: (vals[k].unsqueeze(-1) > cuts_t[k].unsqueeze(0)).sum(-1) for k in vals}
+    qp = [f"{a}_{b}" for a, b in zip(tab.cols["dns_qry_type"][:n], tab.cols["dns_qry_rcode"][:n])]
+    qid, qnames = dictionary_encode(qp)
+    top = torch.from_numpy(F["top_domain"].astype(np.int64)).to(device)
+    key = top
+    radix = dict(frame_len=len(cuts_t["frame_len"]) + 1, unix_tstamp=len(cuts_t["unix_tstamp"]) + 1,
+                 subdomain_length=len(cuts_t["subdomain_length"]) + 1, entropy=len(cuts_t["entropy"]) + 1,
+                 num_periods=len(cuts_t["num_periods"]) + 1)
+    for k in ("frame_len", "unix_tstamp", "subdomain_length", "entropy", "num_periods"):
+        key = key * radix[k] + bins[k]
+    key = key * max(1, len(qnames)) + torch.from_numpy(qid.astype(np.int64)).to(device)
+    ip_ids, ip_names = dictionary_encode(tab.cols["ip_dst"][:n])
+    return DnsFeatures(rows=np.arange(n, dtype=np.int64), ip=torch.from_numpy(ip_ids.astype(np.int64)).to(device),
+                       ip_names=ip_names, word_key=key, weight=w, bins=bins,
+                       cuts={k: v.cpu().numpy() for k, v in cuts_t.items()}, host=F, qpairs=qnames)
+
+
+class DnsWordSpace:
+    """Decodes DNS word keys to the reference's word strings."""
+
+    ORDER = ("frame_len", "unix_tstamp", "subdomain_length", "entropy", "num_periods")
+
+    def __init__(self, cuts: Dict[str, np.ndarray], qpairs: List[str]):
+        self.radix = [len(cuts[k]) + 1 for k in self.ORDER]
+        self.qpairs = list(qpairs)
+
+    def decode(self, keys: np.ndarray) -> List[str]:
+        k = np.asarray(keys, np.int64)
+        nq = max(1, len(self.qpairs))
+        q = k % nq
+        k = k // nq
+        parts = []
+        for r in reversed(self.radix):
+            parts.append(k % r)
+            k = k // r
+        top = k
+        parts = parts[::-1]
+        out = []
+        for i in range(len(top)):
+            out.append("_".join([str(int(top[i]))] + [str(int(p[i])) for p in parts] + [self.qpairs[int(q[i])]]))
+        return out

@@ -215,6 +215,7 @@ class LDAEngine:
                                  self.var_max_iter, self.settings.var_converged)
             self.gamma = out["gamma"]
             self.iters = out["iters"]
+            self.lik = out["lik"]
             self.cw = R.suffstats(self.t_doc_ptr, self.t_word, out["e"], out["r"], self.beta, self.V, self.K)
             return torch.stack([out["lik"].sum(), out["alpha_ss"].sum()])
         # cpu: lda-c Gauss-Seidel reference (C++)
@@ -224,6 +225,7 @@ class LDAEngine:
             np.ascontiguousarray(lb.T.numpy()), self.alpha, self.var_max_iter, self.settings.var_converged, 0)
         self.gamma = torch.from_numpy(res["gamma"])
         self.iters = torch.from_numpy(res["iters"])
+        self.lik = torch.from_numpy(res["doc_likelihood"])
         self.cw = torch.from_numpy(np.ascontiguousarray(res["class_word"].T))
         return torch.tensor([res["likelihood"], res["alpha_ss"]], dtype=torch.float64)
 

@@ -1,0 +1,136 @@
+"""`lda est` driver on the MI355X engine: EM run + lda-c output files + checkpoint/resume.
+
+Reference call site: ``mpiexec -n 20 -f machinefile ./lda est 2.5 20 settings.txt 20 model.dat random <dir>``
+(ml_ops.sh:80).  Outputs (README.md:116-121):
+
+  000.beta/.other           model before the first EM iteration
+  %03d.beta/.other/.gamma   every LAG=5 iterations
+  final.beta/.other/.gamma  at convergence
+  likelihood.dat            "%10.10f\\t%5.5e" per EM iteration
+  word-assignments.dat      (optional) per-word argmax topic under the final model
+  <rank>.gamma              (optional) each rank's contiguous gamma block
+
+plus ``checkpoint.npz`` every LAG iterations (log beta, alpha, iteration,
+likelihood history, VAR_MAX_ITER, RNG-free) for exact ``--resume``.
+Only rank 0 writes combined files; gamma is gathered in rank order, so
+final.gamma line j is corpus document j (lda_post.py pairs it with doc.dat).
+"""
+from __future__ import annotations
+
+import json
+import os
+import time
+from typing import Optional
+
+import numpy as np
+
+from ...corpus.csr import Corpus
+from ...io import ldac
+from .em import LDAEngine, LDAResult
+from .settings import LAG, LDASettings
+
+CKPT = "checkpoint.npz"
+
+
+def save_checkpoint(outdir: str, eng: LDAEngine, iteration: int, L_old: float, history):
+    tmp = os.path.join(outdir, CKPT + ".tmp.npz")
+    np.savez(tmp, log_beta=eng.log_beta(), alpha=np.float64(eng.alpha), iteration=np.int64(iteration),
+             likelihood_old=np.float64(L_old), var_max_iter=np.int64(eng.var_max_iter),
+             history=np.asarray(history, np.float64).reshape(-1, 2))
+    os.replace(tmp, os.path.join(outdir, CKPT))
+
+
+def load_checkpoint(outdir: str) -> Optional[dict]:
+    p = os.path.join(outdir, CKPT)
+    if not os.path.exists(p):
+        return None
+    with np.load(p, allow_pickle=False) as z:
+        return {k: z[k] for k in z.files}
+
+
+def estimate(corpus: Corpus, num_topics: int, alpha_init: float, settings: LDASettings, start: str, outdir: str,
+             backend: str = "auto", device=None, dist=None, seed: int = 0, resume: bool = False,
+             write_word_assignments: bool = False, write_rank_gamma: bool = False, verbose: bool = False,
+             fault_at_iteration: Optional[int] = None) -> LDAResult:
+    """Run EM and write lda-c files.  `start`: random | seeded | <model prefix>.
+
+    `fault_at_iteration` raises after that EM iteration (fault-injection hook for the resume tests)."""
+    rank0 = dist is None or dist.rank == 0
+    if rank0:
+        os.makedirs(outdir, exist_ok=True)
+    eng = LDAEngine(corpus, num_topics, settings, alpha_init=alpha_init, backend=backend, device=device, dist=dist,
+                    seed=seed)
+    start_it, L_old, hist = 0, 0.0, []
+    ck = load_checkpoint(outdir) if resume else None
+    if ck is not None:
+        eng.init_from_model(ck["log_beta"], float(ck["alpha"]))
+        eng.var_max_iter = int(ck["var_max_iter"])
+        start_it, L_old = int(ck["iteration"]), float(ck["likelihood_old"])
+        hist = [tuple(x) for x in ck["history"].tolist()]
+        mode = "resume"
+        if rank0:  # likelihood.dat holds exactly the checkpointed iterations
+            with open(os.path.join(outdir, "likelihood.dat"), "w") as f:
+                for L, c in hist:
+                    f.write(ldac.format_likelihood_line(L, c))
+    elif start in ("random", "seeded"):
+        mode = start
+        if rank0:
+            open(os.path.join(outdir, "likelihood.dat"), "w").close()
+    else:
+        lb, a = ldac.load_model(start)
+        eng.init_from_model(lb, a)
+        mode = "resume"
+        if rank0:
+            open(os.path.join(outdir, "likelihood.dat"), "w").close()
+
+    history = list(hist)
+
+    def on_iteration(e, i, lik, conv):
+        history.append((lik, conv))
+        if rank0:
+            ldac.append_likelihood(os.path.join(outdir, "likelihood.dat"), lik, conv)
+        if fault_at_iteration is not None and i >= fault_at_iteration:
+            raise RuntimeError(f"injected fault after EM iteration {i}")
+
+    def on_save(tag, e):
+        lb = e.log_beta()
+        g = e.gather_gamma() if tag != "000" else None
+        if write_rank_gamma and tag == "final":
+            r = 0 if dist is None else dist.rank
+            ldac.save_gamma(os.path.join(outdir, f"{r}.gamma"), e.local_gamma())
+        if not rank0:
+            return
+        ldac.save_model(os.path.join(outdir, tag), lb, e.alpha)
+        if g is not None:
+            ldac.save_gamma(os.path.join(outdir, f"{tag}.gamma"), g)
+        if tag not in ("000", "final"):
+            save_checkpoint(outdir, e, int(tag), history[-1][0] if history else 0.0, history)
+
+    res = eng.run(start=mode, corpus_global=corpus, on_iteration=on_iteration, on_save=on_save,
+                  start_iteration=start_it, likelihood_old=L_old, verbose=verbose and rank0)
+    res.likelihoods = history
+    res.log_beta = eng.log_beta()
+    res.gamma = eng.gather_gamma()
+    if write_word_assignments and rank0:
+        write_assignments(os.path.join(outdir, "word-assignments.dat"), corpus, res.log_beta, res.gamma)
+    if rank0:
+        with open(os.path.join(outdir, "lda_stats.json"), "w") as f:
+            json.dump(dict(em_iterations=res.em_iterations, seconds=res.seconds, alpha=res.alpha,
+                           backend=eng.backend, docs=corpus.num_docs, terms=corpus.num_terms, nnz=corpus.nnz,
+                           per_iter=[s.__dict__ for s in res.stats]), f)
+    res.engine = eng
+    return res
+
+
+def write_assignments(path: str, corpus: Corpus, log_beta: np.ndarray, gamma: np.ndarray):
+    """word-assignments.dat: per doc ``%03d`` length then `` %04d:%02d`` word:argmax-topic.
+
+    The argmax of φ_nk ∝ exp(ψ(γ_k)) β_{k,w} is argmax_k (ψ(γ_k) + log β_{k,w}) (lda-c write_word_assignment)."""
+    from .special import digamma
+    psi = digamma(gamma)                                  # [D, K]
+    with open(path, "w") as f:
+        for d in range(corpus.num_docs):
+            a, b = corpus.doc_ptr[d], corpus.doc_ptr[d + 1]
+            w = corpus.word_idx[a:b]
+            z = np.argmax(psi[d][None, :] + log_beta[:, w].T, axis=1)
+            f.write("%03d" % (b - a) + "".join(" %04d:%02d" % (wi, zi) for wi, zi in zip(w.tolist(), z.tolist())) + "\n")

@@ -118,3 +118,29 @@ def score(theta, phi, K, dflt, doc_a, word_a, doc_b=None, word_b=None, tol=float
     sb = one(doc_b.long(), word_b.long()) if doc_b is not None else None
     key = torch.minimum(sa, sb) if sb is not None else sa
     return sa, sb, key, (key < tol).to(torch.uint8)
+
+
+def flow_words(hour, minute, second, port_a, port_b, ipkt, ibyt, time_cuts, ibyt_cuts, ipkt_cuts):
+    """Torch transcription of csrc/hip/flow_words.hip (flow_pre_lda.scala:272-358)."""
+    t = (hour + minute / 60) + second / 3600
+    def nb(v, c):
+        return (v.unsqueeze(-1) > c.to(v.device).unsqueeze(0)).sum(-1).to(torch.int8)
+    dp, sp = port_a, port_b                    # reference names: dport = col 10, sport = col 11
+    mn, mx = torch.minimum(dp, sp), torch.maximum(dp, sp)
+    c2 = ((dp <= 1024) | (sp <= 1024)) & ((dp > 1024) | (sp > 1024)) & (mn != 0)
+    c3 = ~c2 & (dp > 1024) & (sp > 1024)
+    c4a = ~c2 & ~c3 & (dp == 0) & (sp != 0)
+    c4b = ~c2 & ~c3 & ~c4a & (sp == 0) & (dp != 0)
+    c1 = ~(c2 | c3 | c4a | c4b)
+    wp = torch.where(c2, mn, torch.where(c3, torch.full_like(mn, 333333.0), torch.where(
+        c4a, sp, torch.where(c4b, dp, torch.where(mn == 0, mx, torch.full_like(mn, 111111.0))))))
+    pc = torch.where(c2, 2, torch.where(c3, 3, torch.where(c4a | c4b, 4, 1))).to(torch.int8)
+    # the reference's if / else-if chain for the "-1_" side
+    r1 = c2 & (dp < sp)
+    r2 = ~r1 & c2 & (sp < dp)
+    r3 = ~r1 & ~r2 & (pc == 4) & (dp == 0)
+    r4 = ~r1 & ~r2 & ~r3 & (pc == 4) & (sp == 0)
+    dpre = r1 | r4
+    spre = r2 | r3
+    return dict(time=t, time_bin=nb(t, time_cuts), ibyt_bin=nb(ibyt, ibyt_cuts), ipkt_bin=nb(ipkt, ipkt_cuts),
+                word_port=wp, p_case=pc, src_prefix=spre.to(torch.int8), dst_prefix=dpre.to(torch.int8))

@@ -95,6 +95,33 @@ class DistContext:
         assert res.shape[0] == total_rows, (res.shape, total_rows)
         return res
 
+    def broadcast_corpus(self, corpus):
+        """Rank 0's Corpus on every rank (arrays via the collective backend, not pickles)."""
+        if not self.initialized:
+            return corpus
+        import torch.distributed as td
+        from ..corpus.csr import Corpus
+
+        meta = [None]
+        if self.rank == 0:
+            meta = [(corpus.num_docs, corpus.nnz, corpus.num_terms)]
+        td.broadcast_object_list(meta, src=0)
+        D, nnz, V = meta[0]
+        dev = self._coll_device()
+        if self.rank == 0:
+            ptr = torch.from_numpy(corpus.doc_ptr).to(dev)
+            w = torch.from_numpy(corpus.word_idx).to(dev)
+            c = torch.from_numpy(corpus.counts).to(dev)
+        else:
+            ptr = torch.empty(D + 1, dtype=torch.int64, device=dev)
+            w = torch.empty(nnz, dtype=torch.int32, device=dev)
+            c = torch.empty(nnz, dtype=torch.int64, device=dev)
+        for t in (ptr, w, c):
+            td.broadcast(t, src=0)
+        if self.rank == 0:
+            return corpus
+        return Corpus(ptr.cpu().numpy(), w.cpu().numpy(), c.cpu().numpy(), V)
+
     def barrier(self):
         if self.initialized:
             import torch.distributed as td

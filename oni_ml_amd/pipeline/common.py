@@ -1,0 +1,96 @@
+"""Stages shared by the flow and DNS pipelines: corpus files, LDA, model export, model reload."""
+from __future__ import annotations
+
+import json
+import os
+from dataclasses import dataclass
+from typing import List, Optional
+
+import numpy as np
+import torch
+
+from ..corpus.builder import BuiltCorpus, lda_pre
+from ..corpus.csr import Corpus
+from ..export import lda_post
+from ..io import ldac
+from ..models.lda.estimate import estimate
+
+
+@dataclass
+class ModelTables:
+    """What the scorers consume: θ / φ and their row names (as written to the result files)."""
+    doc_names: List[str]
+    theta: np.ndarray          # [D, K]
+    word_names: List[str]      # keys as written (strict: truncated to 20 bytes)
+    phi: np.ndarray            # [V, K]
+
+    def doc_index(self) -> dict:
+        return {n: i for i, n in enumerate(self.doc_names)}      # later duplicates win (collectAsMap)
+
+    def word_index(self) -> dict:
+        return {n: i for i, n in enumerate(self.word_names)}
+
+
+def write_corpus_files(lpath: str, built: BuiltCorpus, doc_names: List[str], word_names: List[str]):
+    ldac.write_words_dat(os.path.join(lpath, "words.dat"), word_names)
+    ldac.write_doc_dat(os.path.join(lpath, "doc.dat"), doc_names)
+    ldac.write_model_dat(os.path.join(lpath, "model.dat"), built.corpus)
+
+
+def load_corpus_files(lpath: str):
+    c = ldac.read_model_dat(os.path.join(lpath, "model.dat"))
+    docs = ldac.read_index_file(os.path.join(lpath, "doc.dat"))
+    words = ldac.read_index_file(os.path.join(lpath, "words.dat"))
+    c.num_terms = max(c.num_terms, len(words))
+    return c, docs, words
+
+
+def run_lda(cfg, corpus: Corpus, dist=None, device=None, log=print):
+    outdir = cfg.lpath
+    settings_path = os.path.join(outdir, "settings.txt")
+    if dist is None or dist.rank == 0:
+        ldac.write_settings(settings_path, cfg.settings)
+    return estimate(corpus, cfg.topics, cfg.alpha, cfg.settings, cfg.start, outdir, backend=cfg.backend,
+                    device=device, dist=dist, seed=cfg.seed, resume=cfg.resume,
+                    write_word_assignments=cfg.word_assignments, write_rank_gamma=cfg.rank_gamma,
+                    verbose=cfg.verbose, fault_at_iteration=cfg.extra.get("fault_at_iteration"))
+
+
+def run_export(cfg, doc_names, gamma, word_names, log_beta) -> ModelTables:
+    th, ph, wn = lda_post.export(doc_names, gamma, word_names, log_beta,
+                                 os.path.join(cfg.lpath, "doc_results.csv"),
+                                 os.path.join(cfg.lpath, "word_results.csv"), strict=cfg.strict)
+    return ModelTables(list(doc_names), th, wn, ph)
+
+
+def load_model_tables(lpath: str) -> ModelTables:
+    """Read doc_results.csv / word_results.csv exactly as the Scala scorers do."""
+    dn, th = lda_post.read_results(os.path.join(lpath, "doc_results.csv"))
+    wn, ph = lda_post.read_results(os.path.join(lpath, "word_results.csv"))
+    return ModelTables(dn, th, wn, ph)
+
+
+def strict_tables(mt: ModelTables, strict: bool) -> ModelTables:
+    """θ/φ as the scorers see them after the text hand-off (Python-2 str -> toDouble)."""
+    if not strict:
+        return mt
+    from ..ops import native
+    n = native.lib()
+    return ModelTables(mt.doc_names, n.roundtrip_py2(np.ascontiguousarray(mt.theta)), mt.word_names,
+                       n.roundtrip_py2(np.ascontiguousarray(mt.phi)))
+
+
+def map_names(names: List[str], index: dict, device) -> torch.Tensor:
+    """Name list -> row ids through a {name: row} map (-1 when absent), as a device int64 tensor."""
+    ids = np.fromiter((index.get(n, -1) for n in names), dtype=np.int64, count=len(names))
+    return torch.from_numpy(ids).to(device)
+
+
+def save_json(path: str, obj):
+    with open(path, "w") as f:
+        json.dump(obj, f, indent=1, default=lambda o: o.tolist() if hasattr(o, "tolist") else str(o))
+
+
+def load_json(path: str):
+    with open(path) as f:
+        return json.load(f)

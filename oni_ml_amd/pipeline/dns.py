@@ -1,0 +1,143 @@
+"""DNS suspicious-connects pipeline (ml_ops.sh YYYYMMDD dns [TOL]).
+
+Stages: load -> dns_pre -> lda_pre -> lda -> lda_post -> dns_post
+(reference: dns_pre_lda.scala, lda_pre.py, oni-lda-c, lda_post.py,
+dns_post_lda.scala).  Output dns_results.csv has 16
+columns: the 8 input fields, domain, subdomain, subdomain.length,
+num.periods, subdomain.entropy, top_domain, word, score (dns_post_lda.scala:326-331).
+"""
+from __future__ import annotations
+
+import os
+
+import numpy as np
+import torch
+
+from ..corpus.builder import count_pairs, lda_pre
+from ..features import dns as FD
+from ..score import scorer as S
+from . import common as C
+from .runner import StageRunner
+
+
+def run(cfg, dist=None, device=None, log=print) -> dict:
+    rank = 0 if dist is None else dist.rank
+    device = torch.device(device or ("cuda" if torch.cuda.is_available() else "cpu"))
+    R = StageRunner(cfg.lpath, resume=cfg.resume, rank=rank, log=log,
+                    sync=(torch.cuda.synchronize if device.type == "cuda" else None))
+    summary = {}
+    tab = built = None
+    doc_names = word_names = None
+    top = None
+    need_pre = not (R.done("lda_pre") and R.done("dns_pre"))
+    if rank == 0 and (need_pre or not R.done("dns_post")):
+        with R.stage("load") as res:
+            tab = FD.load_dns(cfg.dns_path, cfg.feedback_path(), cfg.dupfactor, strict=cfg.strict)
+            top = FD.load_top_domains(cfg.top1m)
+            if not top:
+                log(f"warning: top-1m list {cfg.top1m!r} not found; every domain gets top_domain 0/2")
+            res.update(rows=tab.n, raw_rows=tab.n_raw, feedback_rows=tab.n_feedback, dropped=tab.dropped,
+                       top_domains=len(top))
+            summary["input"] = dict(rows=tab.n, feedback_rows=tab.n_feedback, dropped=tab.dropped)
+    if need_pre:
+        if rank == 0:
+            with R.stage("dns_pre") as res:
+                feat = FD.featurize(tab, device, top, threads=cfg.threads)
+                wsp = FD.DnsWordSpace(feat.cuts, feat.qpairs)
+                dwc = count_pairs(feat.ip, feat.word_key, feat.weight)
+                C.save_json(os.path.join(cfg.lpath, "dns_cuts.json"), dict(cuts={k: v.tolist() for k, v in feat.cuts.items()}))
+                res["pairs"] = dwc.n
+                log("cuts: " + " ".join(f"{k}={v.tolist()}" for k, v in feat.cuts.items()))
+            with R.stage("lda_pre") as res:
+                built = lda_pre(dwc)
+                doc_names = [feat.ip_names[i] for i in built.doc_keys.tolist()]
+                word_names = wsp.decode(built.word_keys)
+                if cfg.write_doc_wc:
+                    from ..corpus.builder import write_doc_wc
+                    write_doc_wc(os.path.join(cfg.lpath, "doc_wc.dat"), dwc, feat.ip_names,
+                                 lambda keys: (lambda u: (wsp.decode(u[0]), u[1]))(np.unique(keys, return_inverse=True)))
+                C.write_corpus_files(cfg.lpath, built, doc_names, word_names)
+                res.update(docs=built.corpus.num_docs, terms=built.corpus.num_terms, nnz=built.corpus.nnz)
+                summary["corpus"] = dict(docs=built.corpus.num_docs, terms=built.corpus.num_terms, nnz=built.corpus.nnz)
+    else:
+        R.skip("dns_pre")
+        R.skip("lda_pre")
+
+    corpus = built.corpus if built is not None else None
+    if not R.done("lda"):
+        if corpus is None and rank == 0:
+            corpus, doc_names, word_names = C.load_corpus_files(cfg.lpath)
+        if dist is not None and dist.world_size > 1:
+            corpus = dist.broadcast_corpus(corpus)
+        with R.stage("lda") as res:
+            lres = C.run_lda(cfg, corpus, dist=dist, device=device, log=log)
+            res.update(em_iterations=lres.em_iterations, alpha=lres.alpha)
+            summary["lda"] = dict(em_iterations=lres.em_iterations, seconds=lres.seconds, alpha=lres.alpha,
+                                  likelihood=lres.likelihoods[-1][0] if lres.likelihoods else None)
+        gamma, log_beta = lres.gamma, lres.log_beta
+    else:
+        R.skip("lda")
+        gamma = log_beta = None
+    if rank != 0:
+        return summary
+
+    if not R.done("lda_post"):
+        if doc_names is None:
+            _, doc_names, word_names = C.load_corpus_files(cfg.lpath)
+        if gamma is None:
+            from ..io import ldac
+            gamma = ldac.load_gamma(os.path.join(cfg.lpath, "final.gamma"))
+            log_beta, _ = ldac.load_model(os.path.join(cfg.lpath, "final"))
+        with R.stage("lda_post"):
+            tables = C.strict_tables(C.run_export(cfg, doc_names, gamma, word_names, log_beta), cfg.strict)
+    else:
+        R.skip("lda_post")
+        tables = C.load_model_tables(cfg.lpath)
+
+    if not R.done("dns_post"):
+        with R.stage("dns_post") as res:
+            res.update(score_dns(cfg, tab, top, tables, device, log))
+            summary["scored"] = res.get("flagged")
+    else:
+        R.skip("dns_post")
+    summary["stage_seconds"] = dict(R.times)
+    return summary
+
+
+def score_dns(cfg, tab: FD.DnsTable, top, tables: C.ModelTables, device, log=print) -> dict:
+    cuts = None
+    if not cfg.strict:
+        cuts = {k: np.asarray(v, np.float64) for k, v in C.load_json(os.path.join(cfg.lpath, "dns_cuts.json"))["cuts"].items()}
+    feat = FD.featurize(tab, device, top, cuts=cuts, raw_only=True, threads=cfg.threads)
+    wsp = FD.DnsWordSpace(feat.cuts, feat.qpairs)
+    uk, inv = torch.unique(feat.word_key, return_inverse=True)
+    unames = wsp.decode(uk.cpu().numpy())
+    widx = C.map_names(unames, tables.word_index(), device)[inv]
+    didx = C.map_names(feat.ip_names, tables.doc_index(), device)[feat.ip]
+    K = tables.theta.shape[1]
+    if cfg.strict and K != 20:
+        raise ValueError("compat=strict scores over exactly 20 topics (dns_post_lda.scala:316)")
+    model = S.TopicModel.build(tables.theta, tables.phi, S.default_value("dns", K, cfg.strict), device)
+    sc, _, key, flag = S.score(model, didx, widx, None, None, cfg.tol)
+    order = S.rank_flagged(key, flag)
+    n = int(order.size)
+    out = os.path.join(cfg.lpath, "dns_results.csv")
+    cols = []
+    for c in FD.COLUMNS:
+        ids, names = FD.dictionary_encode([tab.cols[c][i] for i in order.tolist()])
+        cols.append(("dict", names, ids))
+    H = feat.host
+    cols += [
+        ("dict", H["domains"], H["domain_id"][order]),
+        ("dict", H["subdomains"], H["subdomain_id"][order]),
+        ("int", H["subdomain_length"][order].astype(np.int64)),
+        ("int", H["num_periods"][order].astype(np.int64)),
+        ("java", H["entropy"][order]),
+        ("int", H["top_domain"][order].astype(np.int64)),
+        ("dict", unames, inv[torch.from_numpy(order).to(inv.device)].cpu().numpy().astype(np.int32)),
+        ("java", sc[torch.from_numpy(order).to(sc.device)].cpu().numpy()),
+    ]
+    from ..ops import native
+    native.lib().write_rows(out, None, cols, threads=cfg.threads, n=n)
+    log(f"dns_post: {n} queries with score < {cfg.tol} written to {out}")
+    return dict(flagged=n, events=int(feat.word_key.numel()))

@@ -1,0 +1,201 @@
+"""Netflow suspicious-connects pipeline (ml_ops.sh YYYYMMDD flow [TOL]).
+
+Stages (reference call stack SURVEY.md §3.1):
+  flow_pre   featurize FLOW_PATH (+ analyst feedback x DUPFACTOR) -> (ip, word) counts   [flow_pre_lda.scala]
+  lda_pre    words.dat / doc.dat / model.dat (+ doc_wc.dat)                               [lda_pre.py]
+  lda        variational EM on the GPU(s) -> final.{beta,gamma,other}, likelihood.dat    [oni-lda-c]
+  lda_post   doc_results.csv / word_results.csv                                          [lda_post.py]
+  flow_post  re-featurize raw rows, score, filter < TOL, sort -> flow_results.csv        [flow_post_lda.scala]
+
+Everything between stages stays in memory (device tensors / host arrays); the
+text files are written as the compatibility contract and are what `--resume`
+reloads when earlier stages are already complete.
+"""
+from __future__ import annotations
+
+import os
+from typing import Optional
+
+import numpy as np
+import torch
+
+from ..corpus.builder import concat, count_pairs, lda_pre
+from ..features import flow as FF
+from ..score import scorer as S
+from . import common as C
+from .runner import StageRunner
+
+
+def _word_names(ws: FF.FlowWordSpace, keys: np.ndarray):
+    return ws.decode(keys)
+
+
+def run(cfg, dist=None, device=None, log=print) -> dict:
+    rank = 0 if dist is None else dist.rank
+    device = torch.device(device or ("cuda" if torch.cuda.is_available() else "cpu"))
+    R = StageRunner(cfg.lpath, resume=cfg.resume, rank=rank, log=log,
+                    sync=(torch.cuda.synchronize if device.type == "cuda" else None))
+    summary = {}
+    ft = feat = ws = built = None
+    doc_names = word_names = None
+
+    # ------------------------------------------------------------------ pre
+    need_pre = not (R.done("lda_pre") and R.done("flow_pre"))
+    if rank == 0 and (need_pre or not R.done("flow_post")):
+        with R.stage("load") as res:
+            ft = FF.load_flow(cfg.flow_path, cfg.feedback_path(), cfg.dupfactor, cfg.threads)
+            res.update(ft.stats())
+            summary["input"] = ft.stats()
+    if need_pre:
+        if rank == 0:
+            with R.stage("flow_pre") as res:
+                feat = FF.featurize(ft, device)
+                ws = FF.word_space_for(feat)
+                src, dst = FF.word_keys(feat, ws)
+                dwc = concat([count_pairs(feat.sip, src, feat.weight), count_pairs(feat.dip, dst, feat.weight)],
+                             merge=not cfg.strict)
+                C.save_json(os.path.join(cfg.lpath, "flow_cuts.json"),
+                            dict(cuts={k: v.tolist() for k, v in feat.cuts.items()}, ports=ws.ports.tolist()))
+                res["pairs"] = dwc.n
+                log(f"cuts: time={feat.cuts['time'].tolist()} ibyt={feat.cuts['ibyt'].tolist()} "
+                    f"ipkt={feat.cuts['ipkt'].tolist()}")
+            with R.stage("lda_pre") as res:
+                built = lda_pre(dwc)
+                ipn = ft.ip_names
+                doc_names = [ipn[i] for i in built.doc_keys.tolist()]
+                word_names = _word_names(ws, built.word_keys)
+                if cfg.write_doc_wc:
+                    from ..corpus.builder import write_doc_wc
+                    write_doc_wc(os.path.join(cfg.lpath, "doc_wc.dat"), dwc, ipn,
+                                 lambda keys: (lambda u: (_word_names(ws, u[0]), u[1]))(np.unique(keys, return_inverse=True)))
+                C.write_corpus_files(cfg.lpath, built, doc_names, word_names)
+                res.update(docs=built.corpus.num_docs, terms=built.corpus.num_terms, nnz=built.corpus.nnz)
+                summary["corpus"] = dict(docs=built.corpus.num_docs, terms=built.corpus.num_terms, nnz=built.corpus.nnz)
+    else:
+        R.skip("flow_pre")
+        R.skip("lda_pre")
+
+    # ------------------------------------------------------------------ lda
+    corpus = built.corpus if built is not None else None
+    if not R.done("lda"):
+        if corpus is None and rank == 0:
+            corpus, doc_names, word_names = C.load_corpus_files(cfg.lpath)
+        if dist is not None and dist.world_size > 1:
+            corpus = dist.broadcast_corpus(corpus)
+        with R.stage("lda") as res:
+            lres = C.run_lda(cfg, corpus, dist=dist, device=device, log=log)
+            res.update(em_iterations=lres.em_iterations, likelihood=lres.likelihoods[-1][0] if lres.likelihoods else 0.0,
+                       alpha=lres.alpha)
+            summary["lda"] = dict(em_iterations=lres.em_iterations, seconds=lres.seconds, alpha=lres.alpha,
+                                  likelihood=lres.likelihoods[-1][0] if lres.likelihoods else None)
+        gamma, log_beta = lres.gamma, lres.log_beta
+    else:
+        R.skip("lda")
+        gamma = log_beta = None
+    if rank != 0:
+        return summary
+
+    # ------------------------------------------------------------- lda_post
+    if not R.done("lda_post"):
+        if doc_names is None:
+            _, doc_names, word_names = C.load_corpus_files(cfg.lpath)
+        if gamma is None:
+            from ..io import ldac
+            gamma = ldac.load_gamma(os.path.join(cfg.lpath, "final.gamma"))
+            log_beta, _ = ldac.load_model(os.path.join(cfg.lpath, "final"))
+        with R.stage("lda_post") as res:
+            tables = C.strict_tables(C.run_export(cfg, doc_names, gamma, word_names, log_beta), cfg.strict)
+    else:
+        R.skip("lda_post")
+        tables = C.load_model_tables(cfg.lpath)
+
+    # ------------------------------------------------------------ flow_post
+    if not R.done("flow_post"):
+        with R.stage("flow_post") as res:
+            res.update(score_flow(cfg, ft, tables, device, log))
+            summary["scored"] = res.get("flagged")
+    else:
+        R.skip("flow_post")
+    summary["stage_seconds"] = dict(R.times)
+    return summary
+
+
+def score_flow(cfg, ft: FF.FlowTable, tables: C.ModelTables, device, log=print) -> dict:
+    """flow_post_lda.scala: features of raw rows, θ·φ per side, min, < TOL, ascending, 37-column rows."""
+    cuts = None
+    if not cfg.strict:
+        saved = C.load_json(os.path.join(cfg.lpath, "flow_cuts.json"))
+        cuts = {k: np.asarray(v, np.float64) for k, v in saved["cuts"].items()}
+    feat = FF.featurize(ft, device, cuts=cuts, raw_only=True)
+    ws = FF.word_space_for(feat)
+    src, dst = FF.word_keys(feat, ws)
+    # word keys -> names -> word_results rows (names as written; strict: 20-byte keys never match long words)
+    both = torch.cat([src, dst])
+    uk, inv = torch.unique(both, return_inverse=True)
+    uk_np = uk.cpu().numpy()
+    unames = ws.decode(uk_np)
+    widx = C.map_names(unames, tables.word_index(), device)[inv]
+    w_src, w_dst = widx[: src.numel()], widx[src.numel():]
+    ipn = ft.ip_names
+    didx = C.map_names(ipn, tables.doc_index(), device)
+    K = tables.theta.shape[1]
+    if cfg.strict and K != 20:
+        raise ValueError("compat=strict scores over exactly 20 topics (flow_post_lda.scala:232)")
+    model = S.TopicModel.build(tables.theta, tables.phi, S.default_value("flow", K, cfg.strict), device)
+    sa, sb, key, flag = S.score(model, didx[feat.sip.long()], w_src, didx[feat.dip.long()], w_dst, cfg.tol)
+    order = S.rank_flagged(key, flag)
+    n = int(order.size)
+    out = os.path.join(cfg.lpath, "flow_results.csv")
+    # output columns: 27 raw + time + ibyt_bin + ipkt_bin + time_bin + word_port + ip_pair + src/dest word + scores
+    o_t = torch.from_numpy(order).to(device)
+    inv_src = inv[: src.numel()][o_t].cpu().numpy().astype(np.int32)
+    inv_dst = inv[src.numel():][o_t].cpu().numpy().astype(np.int32)
+    sel = lambda t: t[o_t].cpu().numpy()
+    cols = [
+        ("table", ft.table, order),
+        ("java", sel(feat.time)),
+        ("int", sel(feat.ibyt_bin).astype(np.int64)),
+        ("int", sel(feat.ipkt_bin).astype(np.int64)),
+        ("int", sel(feat.time_bin).astype(np.int64)),
+        ("java", sel(feat.word_port)),
+        ("pair", ipn, sel(feat.sip).astype(np.int32), sel(feat.dip).astype(np.int32)),
+        ("dict", unames, inv_src),
+        ("dict", unames, inv_dst),
+        ("java", sel(sa)),
+        ("java", sel(sb)),
+    ]
+    from ..ops import native
+    native.lib().write_rows(out, None, cols, threads=cfg.threads, n=n)
+    log(f"flow_post: {n} events with score < {cfg.tol} written to {out}")
+    return dict(flagged=n, events=int(feat.time.numel()))
+
+
+
+def synthetic_flow_corpus(events: int = 1_000_000, seed: int = 0, workdir: Optional[str] = None, device=None,
+                          strict: bool = True, threads: int = 8):
+    """Synthetic netflow day -> featurized -> lda-c corpus (the bench / test input path).
+
+    Returns (Corpus, info dict with stage timings)."""
+    import tempfile
+    import time
+    from ..synth.flow import generate_flow_day
+    device = torch.device(device or ("cuda" if torch.cuda.is_available() else "cpu"))
+    tmp = tempfile.mkdtemp(prefix="oni_flow_") if workdir is None else workdir
+    t0 = time.perf_counter()
+    gen = generate_flow_day(os.path.join(tmp, "in/"), events=events, seed=seed, threads=threads)
+    t1 = time.perf_counter()
+    ft = FF.load_flow(os.path.join(tmp, "in"), None, 1000, threads)
+    t2 = time.perf_counter()
+    feat = FF.featurize(ft, device)
+    ws = FF.word_space_for(feat)
+    src, dst = FF.word_keys(feat, ws)
+    dwc = concat([count_pairs(feat.sip, src, feat.weight), count_pairs(feat.dip, dst, feat.weight)], merge=not strict)
+    built = lda_pre(dwc)
+    if device.type == "cuda":
+        torch.cuda.synchronize()
+    t3 = time.perf_counter()
+    if workdir is None:
+        import shutil
+        shutil.rmtree(tmp, ignore_errors=True)
+    info = dict(events=events, synth_s=round(t1 - t0, 3), ingest_s=round(t2 - t1, 3), featurize_corpus_s=round(t3 - t2, 3))
+    return built.corpus, info

@@ -1,11 +1,13 @@
 #!/bin/bash
-# GPU-box check: tests, a short bench, and a rocprofv3 kernel profile.
+# GPU-box check: tests, the default bench, and a rocprofv3 kernel profile of the bench.
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 600 python -m pytest tests -m gpu -x -q > gpurun_out/pytest_gpu.log 2>&1
+python -m oni_ml_amd._build > gpurun_out/build.log 2>&1 || { echo "build failed"; tail -20 gpurun_out/build.log; exit 1; }
+timeout -k 10 900 python -m pytest tests -m gpu -x -q > gpurun_out/pytest_gpu.log 2>&1
 echo "pytest exit $?" ; tail -5 gpurun_out/pytest_gpu.log
-timeout -k 10 300 python bench.py --corpus planted --steps 5 --warmup 2 --converge 0 > gpurun_out/bench_planted.log 2>&1 || exit 1
-cat gpurun_out/bench_planted.log
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run -- python3 bench.py --corpus planted --steps 3 --warmup 1 --converge 0 > gpurun_out/prof.log 2>&1 || exit 1
-find gpurun_out/prof -name '*stats*' | head
+timeout -k 10 600 python bench.py > gpurun_out/bench.log 2>&1 || { echo "bench failed"; tail -30 gpurun_out/bench.log; exit 1; }
+tail -3 gpurun_out/bench.log
+timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run -- python3 bench.py --steps 5 --warmup 2 --converge 0 --e2e 0 > gpurun_out/prof.log 2>&1 || { echo "prof failed"; tail -20 gpurun_out/prof.log; exit 1; }
+python scripts/prof_summary.py gpurun_out/prof/run_results.db --md gpurun_out/prof_summary.md > /dev/null
+echo done
