@@ -104,7 +104,8 @@ def test_suffstats_and_mstep(hip):
     refb = R.mstep(cw.double(), ct, K)
     assert torch.allclose(b2[:, :K].double(), refb, rtol=1e-6, atol=1e-45)
     assert b2[5, 3].item() == pytest.approx(math.exp(-100), rel=1e-5)
-    assert b2[:, K:].abs().max().item() == 0
+    if KS > K:
+        assert b2[:, K:].abs().max().item() == 0
 
 
 def test_em_hip_tracks_torch_reference():
