@@ -1,0 +1,137 @@
+"""Text formats: Java Double.toString, Python-2 str(float), lda-c %5.10f, Java parseDouble, CSV ingest rules."""
+import math
+import os
+import random
+import struct
+
+import numpy as np
+import pytest
+
+from oni_ml_amd.io.javafmt import java_double, py2_float
+from oni_ml_amd.ops import native
+
+N = native.lib()
+
+
+@pytest.mark.parametrize("x,s", [
+    (80.0, "80.0"), (0.05, "0.05"), (1e-20, "1.0E-20"), (1234567.0, "1234567.0"), (1e7, "1.0E7"),
+    (12345678.0, "1.2345678E7"), (0.001, "0.001"), (0.0001, "1.0E-4"), (-0.0, "-0.0"), (0.0, "0.0"),
+    (23.983333333333334, "23.983333333333334"), (333333.0, "333333.0"), (float("nan"), "NaN"),
+    (float("inf"), "Infinity"), (-1.5e-300, "-1.5E-300"), (9999999.0, "9999999.0"),
+])
+def test_java_double_known(x, s):
+    assert java_double(x) == s
+    assert N.java_double(x) == s
+
+
+def test_java_double_native_matches_python_random():
+    rng = random.Random(1)
+    vals = []
+    for _ in range(20000):
+        v = struct.unpack("d", struct.pack("Q", rng.getrandbits(64)))[0]
+        if v == v:
+            vals.append(v)
+        vals.append(rng.random() * 10 ** rng.randint(-12, 12))
+    for v in vals:
+        assert N.java_double(v) == java_double(v), v
+        assert float(java_double(v).replace("E", "e")) == v
+
+
+@pytest.mark.parametrize("x,s", [(1 / 3, "0.333333333333"), (1.0, "1.0"), (1e-5, "1e-05"), (0.05, "0.05"),
+                                 (123456789012345.0, "1.23456789012e+14"), (0.0, "0.0"), (5e-324, "4.94065645841e-324")])
+def test_py2_float(x, s):
+    assert py2_float(x) == s
+    assert N.py2_float(x) == s
+
+
+def test_roundtrips():
+    a = np.array([1 / 3, -100.0, 2.5e-11, 0.123456789012345678])
+    assert np.array_equal(N.roundtrip_fixed10(a), np.array([float("%5.10f" % x) for x in a]))
+    assert np.array_equal(N.roundtrip_py2(a), np.array([float(py2_float(x)) for x in a]))
+
+
+@pytest.mark.parametrize("s,v", [(" 12.5 ", 12.5), ("1e3", 1000.0), ("5d", 5.0), ("-2", -2.0), ("+7", 7.0),
+                                 (".5", 0.5), ("NaN", None), ("##", None), ("", None), ("abc", None)])
+def test_java_parse(s, v):
+    r = N.java_parse_double(s)
+    if s == "NaN":
+        assert r != r
+    elif v is None:
+        assert r is None
+    else:
+        assert r == v
+
+
+def test_table_ingest_rules(tmp_path):
+    hdr = "a,b,c,d"
+    lines = [
+        hdr,
+        "1,2,x,4",           # ok
+        "  5,6,y,7  ",        # trimmed
+        "1,2,3",             # 3 fields -> dropped
+        "1,2,3,4,",          # trailing empty field vanishes -> 4 fields, kept as "1,2,3,4"
+        "1,2,,4",            # empty middle field kept (non-numeric col 2 is a string col)
+        "q,2,x,4",           # non-numeric col 0 -> dropped
+        hdr,                 # every header copy dropped
+        "8,9,z,10\r",        # CRLF
+        "",
+    ]
+    p = tmp_path / "in.csv"
+    p.write_text("\n".join(lines) + "\n")
+    t = N.TextTable(4, [0, 1, 3], [[2]])
+    t.load_files([str(p)], drop_header=True, threads=2)
+    assert t.num_rows == 5
+    assert [t.row_text(i) for i in range(t.num_rows)] == ["1,2,x,4", "5,6,y,7", "1,2,3,4", "1,2,,4", "8,9,z,10"]
+    assert t.numeric(0).tolist() == [1, 5, 1, 1, 8]
+    assert t.dict_names(0) == ["x", "y", "3", "", "z"]
+    assert t.n_header == 2 and t.n_bad_numeric == 1 and t.n_bad_fields == 2
+    t.append_text("3,3,x,3", weight=1000)
+    assert t.weights().tolist() == [1, 1, 1, 1, 1, 1000]
+    assert t.dict_ids(2).tolist()[-1] == 0
+
+
+def test_table_ingest_thread_invariance(tmp_path):
+    rng = np.random.default_rng(0)
+    n = 60000
+    names = [f"10.0.{i // 256}.{i % 256}" for i in range(3000)]
+    rows = [f"{rng.integers(0, 100)},{names[rng.integers(0, 3000)]},{names[rng.integers(0, 3000)]}" for _ in range(n)]
+    p = tmp_path / "big.csv"
+    p.write_text("h,s,d\n" + "\n".join(rows) + "\n")
+    outs = []
+    for th in (1, 7):
+        t = N.TextTable(3, [0], [[1, 2]])
+        t.load_files([str(p)], drop_header=True, threads=th)
+        outs.append((t.numeric(0).tolist(), t.dict_ids(1).tolist(), t.dict_ids(2).tolist(), t.dict_names(0)))
+    assert outs[0] == outs[1]
+
+
+def test_writer_kinds(tmp_path):
+    t = N.TextTable(2, [0], [[1]])
+    p = tmp_path / "t.csv"
+    p.write_text("1,a\n2,b\n3,c\n")
+    t.load_files([str(p)], drop_header=False)
+    out = tmp_path / "o.csv"
+    order = np.array([2, 0], np.int64)
+    N.write_rows(str(out), None, [("table", t, order), ("java", np.array([1e-20, 80.0])),
+                                  ("int", np.array([3, 4])), ("dict", ["x", "y"], np.array([1, 0], np.int32)),
+                                  ("pair", ["10.0.0.2", "10.0.0.10"], np.array([0, 1], np.int32), np.array([1, 0], np.int32)),
+                                  ("py2row", np.array([[1 / 3, 0.5], [1.0, 2.0]]), " "), ("const", "k")], n=2)
+    assert out.read_text().splitlines() == [
+        "3,c,1.0E-20,3,y,10.0.0.10 10.0.0.2,0.333333333333 0.5,k",
+        "1,a,80.0,4,x,10.0.0.10 10.0.0.2,1.0 2.0,k",
+    ]
+
+
+def test_ldac_files_roundtrip(tmp_path):
+    from oni_ml_amd.io import ldac
+    lb = np.array([[-1.5, -100.0, -0.25], [-2.0, -3.0, -4.0]])
+    ldac.save_model(str(tmp_path / "final"), lb, 0.1234)
+    txt = (tmp_path / "final.beta").read_text().splitlines()
+    assert txt[0] == " -1.5000000000 -100.0000000000 -0.2500000000"
+    lb2, a = ldac.load_model(str(tmp_path / "final"))
+    assert np.array_equal(lb, lb2) and a == pytest.approx(0.1234)
+    g = np.array([[1.0, 2.5], [3.25, 0.125]])
+    ldac.save_gamma(str(tmp_path / "final.gamma"), g)
+    assert (tmp_path / "final.gamma").read_text() == "1.0000000000 2.5000000000\n3.2500000000 0.1250000000\n"
+    assert ldac.format_likelihood_line(-12345.678, 0.00123) == "-12345.6780000000\t1.23000e-03\n"
+    assert ldac.format_likelihood_line(-1.0, math.inf) == "-1.0000000000\t  inf\n"
