@@ -40,6 +40,16 @@ def save_checkpoint(outdir: str, eng: LDAEngine, iteration: int, L_old: float, h
     os.replace(tmp, os.path.join(outdir, CKPT))
 
 
+def load_final(outdir: str):
+    """(gamma, log_beta) of a finished run: the binary copy when present, else the lda-c text files."""
+    p = os.path.join(outdir, "final_model.npz")
+    if os.path.exists(p):
+        with np.load(p, allow_pickle=False) as z:
+            return z["gamma"], z["log_beta"]
+    lb, _ = ldac.load_model(os.path.join(outdir, "final"))
+    return ldac.load_gamma(os.path.join(outdir, "final.gamma")), lb
+
+
 def load_checkpoint(outdir: str) -> Optional[dict]:
     p = os.path.join(outdir, CKPT)
     if not os.path.exists(p):
@@ -105,6 +115,8 @@ def estimate(corpus: Corpus, num_topics: int, alpha_init: float, settings: LDASe
             ldac.save_gamma(os.path.join(outdir, f"{tag}.gamma"), g)
         if tag not in ("000", "final"):
             save_checkpoint(outdir, e, int(tag), history[-1][0] if history else 0.0, history)
+        if tag == "final":  # exact binary copy of what final.* hold as text (stage resume reloads this)
+            np.savez(os.path.join(outdir, "final_model.npz"), log_beta=lb, gamma=g, alpha=np.float64(e.alpha))
 
     res = eng.run(start=mode, corpus_global=corpus, on_iteration=on_iteration, on_save=on_save,
                   start_iteration=start_it, likelihood_old=L_old, verbose=verbose and rank0)

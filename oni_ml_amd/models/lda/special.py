@@ -66,7 +66,7 @@ def opt_alpha(ss: float, D: int, K: int, init_a: float = 100.0) -> float:
     it = 0
     while True:
         it += 1
-        a = math.exp(log_a)
+        a = math.exp(log_a) if log_a < 709.78 else (math.nan if math.isnan(log_a) else math.inf)
         if math.isnan(a):
             init_a = init_a * 10
             a = init_a
@@ -76,7 +76,7 @@ def opt_alpha(ss: float, D: int, K: int, init_a: float = 100.0) -> float:
         log_a = log_a - df / (d2f * a + df)
         if not (abs(df) > NEWTON_THRESH and it < MAX_ALPHA_ITER):
             break
-    return math.exp(log_a)
+    return math.exp(log_a) if log_a < 709.78 else (math.nan if math.isnan(log_a) else math.inf)
 
 
 def lik_const(alpha: float, K: int) -> float:

@@ -70,10 +70,11 @@ def load_model_tables(lpath: str) -> ModelTables:
     return ModelTables(dn, th, wn, ph)
 
 
-def strict_tables(mt: ModelTables, strict: bool) -> ModelTables:
-    """θ/φ as the scorers see them after the text hand-off (Python-2 str -> toDouble)."""
-    if not strict:
-        return mt
+def strict_tables(mt: ModelTables, strict: bool = True) -> ModelTables:
+    """θ/φ as the scorers see them after the text hand-off (Python-2 str -> toDouble).
+
+    Applied in both compat modes: the result files are the stage contract, so an
+    in-memory run and a run resumed from the files score identically."""
     from ..ops import native
     n = native.lib()
     return ModelTables(mt.doc_names, n.roundtrip_py2(np.ascontiguousarray(mt.theta)), mt.word_names,

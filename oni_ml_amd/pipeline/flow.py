@@ -100,9 +100,8 @@ def run(cfg, dist=None, device=None, log=print) -> dict:
         if doc_names is None:
             _, doc_names, word_names = C.load_corpus_files(cfg.lpath)
         if gamma is None:
-            from ..io import ldac
-            gamma = ldac.load_gamma(os.path.join(cfg.lpath, "final.gamma"))
-            log_beta, _ = ldac.load_model(os.path.join(cfg.lpath, "final"))
+            from ..models.lda.estimate import load_final
+            gamma, log_beta = load_final(cfg.lpath)
         with R.stage("lda_post") as res:
             tables = C.strict_tables(C.run_export(cfg, doc_names, gamma, word_names, log_beta), cfg.strict)
     else:

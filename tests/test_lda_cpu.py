@@ -1,0 +1,179 @@
+"""LDA core on the CPU: lda-c reference numerics, Jacobi torch engine, lda CLI, resume."""
+import math
+import os
+import subprocess
+
+import numpy as np
+import pytest
+import scipy.special as sp
+import torch
+
+from oni_ml_amd.corpus.csr import Corpus
+from oni_ml_amd.io import ldac
+from oni_ml_amd.models.lda import special
+from oni_ml_amd.models.lda.em import LDAEngine
+from oni_ml_amd.models.lda.estimate import estimate
+from oni_ml_amd.models.lda.settings import LDASettings
+from oni_ml_amd.ops import native
+from oni_ml_amd.ops import reference as R
+from oni_ml_amd.synth.corpus import planted_corpus
+
+N = native.lib()
+
+
+def test_special_functions():
+    for x in (0.05, 0.3, 1.0, 2.5, 17.0, 1234.5):
+        assert N.digamma(x) == pytest.approx(sp.digamma(x), rel=1e-9, abs=1e-9)
+        assert special.digamma(x) == pytest.approx(N.digamma(x), rel=1e-15)
+        assert N.trigamma(x) == pytest.approx(sp.polygamma(1, x), rel=1e-8)
+        assert special.trigamma(x) == pytest.approx(N.trigamma(x), rel=1e-14)
+    assert N.log_sum(-3.0, -2.0) == pytest.approx(math.log(math.exp(-3) + math.exp(-2)))
+
+
+@pytest.mark.parametrize("D,K,ss", [(100, 20, -8000.0), (5000, 10, -150000.0), (50, 5, -600.0)])
+def test_opt_alpha_is_newton_root(D, K, ss):
+    a = N.opt_alpha(ss, D, K)
+    assert special.opt_alpha(ss, D, K) == pytest.approx(a, rel=1e-12)
+    # stationary point of alhood(a) = D(lnG(Ka) - K lnG(a)) + (a-1) ss
+    d = D * (K * sp.digamma(K * a) - K * sp.digamma(a)) + ss
+    assert abs(d) < 1e-4 * D
+
+
+def _ldac_inference_py(words, counts, lb, alpha, var_max_iter, var_conv):
+    """Literal lda-c lda_inference + compute_likelihood (tiny inputs)."""
+    K = lb.shape[0]
+    N_ = len(words)
+    total = sum(counts)
+    gam = [alpha + total / K] * K
+    dig = [special.digamma(g) for g in gam]
+    phi = [[1.0 / K] * K for _ in range(N_)]
+    conv, L_old, it = 1.0, 0.0, 0
+    while conv > var_conv and (it < var_max_iter or var_max_iter == -1):
+        it += 1
+        for n in range(N_):
+            old = list(phi[n])
+            s = 0.0
+            for k in range(K):
+                phi[n][k] = dig[k] + lb[k, words[n]]
+                s = special.log_sum(s, phi[n][k]) if k > 0 else phi[n][k]
+            for k in range(K):
+                phi[n][k] = math.exp(phi[n][k] - s)
+                gam[k] = gam[k] + counts[n] * (phi[n][k] - old[k])
+                dig[k] = special.digamma(gam[k])
+        gsum = sum(gam)
+        dsum = special.digamma(gsum)
+        L = math.lgamma(alpha * K) - K * math.lgamma(alpha) - math.lgamma(gsum)
+        for k in range(K):
+            L += (alpha - 1) * (dig[k] - dsum) + math.lgamma(gam[k]) - (gam[k] - 1) * (dig[k] - dsum)
+            for n in range(N_):
+                if phi[n][k] > 0:
+                    L += counts[n] * (phi[n][k] * ((dig[k] - dsum) - math.log(phi[n][k]) + lb[k, words[n]]))
+        conv = (L_old - L) / L_old
+        L_old = L
+    return gam, L, it
+
+
+def test_cpu_estep_matches_literal_ldac():
+    c = planted_corpus(num_docs=12, num_terms=30, num_topics=3, mean_tokens=8, seed=5)
+    K = 4
+    rng = np.random.default_rng(0)
+    cw = 1.0 / c.num_terms + rng.random((K, c.num_terms))
+    lb = np.log(cw / cw.sum(1, keepdims=True))
+    r = N.lda_estep_ldac(c.doc_ptr, c.word_idx, c.counts.astype(float), lb, 0.7, 20, float(np.float32(1e-6)), 1, 1)
+    for d in range(c.num_docs):
+        a, b = c.doc_ptr[d], c.doc_ptr[d + 1]
+        g, L, it = _ldac_inference_py(c.word_idx[a:b].tolist(), c.counts[a:b].tolist(), lb, 0.7, 20,
+                                      float(np.float32(1e-6)))
+        assert np.allclose(r["gamma"][d], g, rtol=1e-12)
+        assert r["doc_likelihood"][d] == pytest.approx(L, rel=1e-12)
+        assert r["iters"][d] == it
+
+
+def test_cpu_estep_thread_invariance():
+    c = planted_corpus(num_docs=400, num_terms=300, num_topics=5, seed=1)
+    rng = np.random.default_rng(0)
+    lb = np.log(rng.dirichlet(np.ones(300), size=8))
+    outs = [N.lda_estep_ldac(c.doc_ptr, c.word_idx, c.counts.astype(float), lb, 0.5, 20, 1e-6, 4, t) for t in (1, 3, 8)]
+    for o in outs[1:]:
+        assert np.array_equal(o["class_word"], outs[0]["class_word"]) and o["likelihood"] == outs[0]["likelihood"]
+        assert np.array_equal(o["gamma"], outs[0]["gamma"])
+
+
+def test_jacobi_and_gauss_seidel_reach_the_same_fixed_point():
+    c = planted_corpus(num_docs=200, num_terms=100, num_topics=4, mean_tokens=15, seed=2)
+    K = 6
+    rng = np.random.default_rng(1)
+    lb = np.log(rng.dirichlet(np.ones(100), size=K))
+    gs = N.lda_estep_ldac(c.doc_ptr, c.word_idx, c.counts.astype(float), lb, 0.3, -1, 1e-12, 1, 4)
+    jc = R.estep_jacobi(torch.from_numpy(c.doc_ptr), torch.from_numpy(c.word_idx), torch.from_numpy(c.counts).double(),
+                        torch.from_numpy(np.exp(lb).T.copy()), K, 0.3, -1, 1e-12)
+    # per-document variational problem is non-convex: compare the corpus objective and most docs
+    assert jc["lik"].sum().item() == pytest.approx(gs["likelihood"], rel=2e-3)
+    close = np.isclose(jc["gamma"].numpy(), gs["gamma"], rtol=1e-3, atol=1e-2).all(1).mean()
+    assert close > 0.8
+
+
+def test_torch_engine_em_runs_and_is_monotone():
+    c = planted_corpus(num_docs=300, num_terms=200, num_topics=4, seed=3)
+    eng = LDAEngine(c, 8, LDASettings(em_max_iter=10), backend="torch", device="cpu", seed=0)
+    res = eng.run()
+    L = [x[0] for x in res.likelihoods]
+    assert all(np.diff(L) > -1e-6 * abs(L[0]))
+    assert res.em_iterations <= 11 and eng.alpha > 0
+
+
+def test_cpu_backend_engine_matches_native_estimate(tmp_path):
+    c = planted_corpus(num_docs=150, num_terms=120, num_topics=4, seed=4)
+    st = LDASettings(em_max_iter=3)
+    eng = LDAEngine(c, 5, st, backend="cpu", seed=2)
+    res = eng.run()
+    assert len(res.likelihoods) == 4 and all(np.isfinite(x[0]) for x in res.likelihoods)
+
+
+def test_lda_executable(tmp_path):
+    exe = os.path.join(os.path.dirname(native.__file__), "..", "_lib", "lda")
+    c = planted_corpus(num_docs=60, num_terms=50, num_topics=3, seed=6)
+    ldac.write_model_dat(str(tmp_path / "model.dat"), c)
+    (tmp_path / "settings.txt").write_text(LDASettings(em_max_iter=4).dumps())
+    out = tmp_path / "out"
+    r = subprocess.run([exe, "est", "2.5", "5", str(tmp_path / "settings.txt"), "3", str(tmp_path / "model.dat"),
+                        "random", str(out)], capture_output=True, text=True, env=dict(os.environ, ONI_THREADS="2"))
+    assert r.returncode == 0, r.stderr
+    for f in ("000.beta", "000.other", "005.beta", "005.gamma", "final.beta", "final.gamma", "final.other",
+              "likelihood.dat", "word-assignments.dat"):
+        assert (out / f).exists(), f
+    lb, a = ldac.load_model(str(out / "final"))
+    assert lb.shape == (5, c.num_terms) and a > 0
+    assert len((out / "likelihood.dat").read_text().splitlines()) == 5
+    g = ldac.load_gamma(str(out / "final.gamma"))
+    assert g.shape == (60, 5)
+    # lda inf with the trained model
+    r = subprocess.run([exe, "inf", str(tmp_path / "settings.txt"), str(out / "final"), str(tmp_path / "model.dat"),
+                        str(tmp_path / "inf")], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    assert ldac.load_gamma(str(tmp_path / "inf-gamma.dat")).shape == (60, 5)
+
+
+def test_estimate_files_and_exact_resume(tmp_path):
+    c = planted_corpus(num_docs=200, num_terms=150, num_topics=4, seed=7)
+    st = LDASettings(em_max_iter=12, em_converged=1e-12)
+    full = estimate(c, 6, 2.5, st, "random", str(tmp_path / "full"), backend="torch", device="cpu", seed=3)
+    with pytest.raises(RuntimeError):
+        estimate(c, 6, 2.5, LDASettings(em_max_iter=12, em_converged=1e-12), "random", str(tmp_path / "part"),
+                 backend="torch", device="cpu", seed=3, fault_at_iteration=7)
+    assert (tmp_path / "part" / "checkpoint.npz").exists()
+    resumed = estimate(c, 6, 2.5, LDASettings(em_max_iter=12, em_converged=1e-12), "random", str(tmp_path / "part"),
+                       backend="torch", device="cpu", seed=3, resume=True)
+    assert resumed.em_iterations == full.em_iterations
+    assert (tmp_path / "part" / "likelihood.dat").read_text() == (tmp_path / "full" / "likelihood.dat").read_text()
+    assert np.allclose(resumed.gamma, full.gamma, rtol=1e-9)
+    assert (tmp_path / "part" / "final.beta").read_text() == (tmp_path / "full" / "final.beta").read_text()
+
+
+def test_settings_roundtrip(tmp_path):
+    s = LDASettings(var_max_iter=30, var_converged=1e-5, em_max_iter=50, em_converged=1e-3, estimate_alpha=False)
+    p = tmp_path / "settings.txt"
+    p.write_text(s.dumps())
+    s2 = LDASettings.load(str(p))
+    assert (s2.var_max_iter, s2.em_max_iter, s2.estimate_alpha) == (30, 50, False)
+    assert s2.var_converged == s.var_converged

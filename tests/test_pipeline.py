@@ -1,0 +1,175 @@
+"""End-to-end pipelines on the CPU (torch LDA backend): file contract, stage resume, locking, CLI, config."""
+import json
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+from oni_ml_amd import config as CFG
+from oni_ml_amd.models.lda.settings import LDASettings
+from oni_ml_amd.pipeline import run
+from oni_ml_amd.pipeline.runner import RunLock
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+FLOW_FILES = ["doc.dat", "words.dat", "model.dat", "final.beta", "final.gamma", "final.other", "likelihood.dat",
+              "doc_results.csv", "word_results.csv", "flow_results.csv"]
+
+
+def _flow_cfg(tmp_path, events=4000, **kw):
+    from oni_ml_amd.synth.flow import generate_flow_day
+    if not (tmp_path / "in").exists():
+        generate_flow_day(str(tmp_path / "in") + "/", events=events, seed=11, n_internal=300, n_external=600)
+    cfg = CFG.resolve("20160122", "flow", tol=kw.pop("tol", 1e-3), conf_path=None, environ={},
+                      lpath=str(tmp_path / "ml"), flow_path=str(tmp_path / "in"), backend="torch", threads=2,
+                      verbose=False, **kw)
+    cfg.settings = LDASettings(em_max_iter=3)
+    return cfg
+
+
+def test_flow_pipeline_file_contract(tmp_path):
+    cfg = _flow_cfg(tmp_path)
+    s = run(cfg, device="cpu", log=lambda *a, **k: None)
+    for f in FLOW_FILES:
+        assert (tmp_path / "ml" / f).exists(), f
+    res = (tmp_path / "ml" / "flow_results.csv").read_text().splitlines()
+    assert len(res) == s["scored"] > 0
+    keys = []
+    for line in res:
+        f = line.split(",")
+        assert len(f) == 37
+        keys.append(min(float(f[35]), float(f[36])))
+        assert float(f[35]) < 1e-3 or float(f[36]) < 1e-3
+    assert keys == sorted(keys)
+    docs = (tmp_path / "ml" / "doc.dat").read_text().splitlines()
+    dres = (tmp_path / "ml" / "doc_results.csv").read_text().splitlines()
+    assert [d.split(",")[1] for d in docs] == [r.split(",")[0] for r in dres]
+    assert len((tmp_path / "ml" / "final.gamma").read_text().splitlines()) == len(docs)
+    for r in dres[:20]:
+        vals = [float(x) for x in r.split(",")[1].split(" ")]
+        assert len(vals) == 20 and abs(sum(vals) - 1) < 1e-9
+    wres = (tmp_path / "ml" / "word_results.csv").read_text().splitlines()
+    phi = np.array([[float(x) for x in r.split(",")[1].split(" ")] for r in wres])
+    assert np.allclose(phi.sum(0), 1.0, atol=1e-8)
+    assert all(len(r.split(",")[0]) <= 20 for r in wres)   # strict: S20 truncation
+
+
+def test_flow_pipeline_fixed_mode_and_resume(tmp_path):
+    cfg = _flow_cfg(tmp_path, compat="fixed", topics=7)
+    run(cfg, device="cpu", log=lambda *a, **k: None)
+    first = (tmp_path / "ml" / "flow_results.csv").read_text()
+    assert len((tmp_path / "ml" / "doc_results.csv").read_text().splitlines()[0].split(",")[1].split(" ")) == 7
+    # resume after lda: only lda_post + flow_post rerun, same results
+    os.unlink(tmp_path / "ml" / ".stages" / "lda_post.done")
+    os.unlink(tmp_path / "ml" / ".stages" / "flow_post.done")
+    os.unlink(tmp_path / "ml" / "flow_results.csv")
+    cfg2 = _flow_cfg(tmp_path, compat="fixed", topics=7, resume=True)
+    logs = []
+    run(cfg2, device="cpu", log=logs.append)
+    again = (tmp_path / "ml" / "flow_results.csv").read_text()
+    assert again.splitlines() == first.splitlines() if len(first) < 2000 else hash(again) == hash(first)
+    assert any("lda] already complete" in l for l in logs)
+
+
+def test_flow_feedback_changes_corpus_weights(tmp_path):
+    from oni_ml_amd.synth.flow import generate_flow_day, generate_flow_feedback
+    r = generate_flow_day(str(tmp_path / "in") + "/", events=3000, seed=5, n_internal=200, n_external=300)
+    rows = open(r["paths"][0]).read().splitlines()[1:]
+    os.makedirs(tmp_path / "ml", exist_ok=True)
+    generate_flow_feedback(str(tmp_path / "ml" / "flow_scores.csv"), rows, n=4)
+    cfg = _flow_cfg(tmp_path)
+    s = run(cfg, device="cpu", log=lambda *a, **k: None)
+    assert s["input"]["feedback_rows"] == 4
+    counts = [int(tok.split(":")[1]) for line in (tmp_path / "ml" / "model.dat").read_text().splitlines()
+              for tok in line.split()[1:]]
+    assert max(counts) >= 1000
+
+
+def test_dns_pipeline(tmp_path):
+    from oni_ml_amd.synth.dns import generate_dns_day
+    r = generate_dns_day(str(tmp_path / "in"), events=6000, seed=3, files=3, n_names=800, n_clients=300)
+    cfg = CFG.resolve("20160122", "dns", tol=1e-2, conf_path=None, environ={}, lpath=str(tmp_path / "ml"),
+                      dns_path=r["dns_path"], top1m=r["top1m"], backend="torch", threads=2, verbose=False)
+    cfg.settings = LDASettings(em_max_iter=2)
+    s = run(cfg, device="cpu", log=lambda *a, **k: None)
+    rows = (tmp_path / "ml" / "dns_results.csv").read_text().splitlines()
+    assert len(rows) == s["scored"] > 0
+    for line in rows[:50]:
+        f = line.split(",")
+        assert len(f) == 16
+        assert f[14].count("_") == 7 and float(f[15]) < 1e-2
+    # strict: path index 1 skipped
+    assert s["input"]["rows"] < 6000 * 0.7
+
+
+def test_run_lock(tmp_path):
+    p = str(tmp_path / ".lock")
+    with RunLock(p):
+        with pytest.raises(RuntimeError):
+            RunLock(p).__enter__()
+    with RunLock(p):
+        pass
+
+
+def test_duxbay_parser():
+    text = """
+# site config
+NODES=('node01' 'node02')
+UINODE='ui01'
+LUSER=/home/duxbay
+HPATH=${LUSER}/ml/${DSOURCE}/${FDATE}
+LPATH=${LUSER}/ml/${FDATE}
+FLOW_PATH="/user/duxbay/flow/csv/y=${YR}/m=${MH}/d=${DY}/"
+export TOL=1e-20
+RAW='${LUSER}'
+"""
+    d = CFG.parse_duxbay(text, CFG.run_vars("20160122", "flow"))
+    assert d["NODES"] == ["node01", "node02"] and d["UINODE"] == "ui01"
+    assert d["HPATH"] == "/home/duxbay/ml/flow/20160122"
+    assert d["FLOW_PATH"] == "/user/duxbay/flow/csv/y=2016/m=01/d=22/"
+    assert d["TOL"] == "1e-20" and d["RAW"] == "${LUSER}"
+
+
+def test_config_layering(tmp_path):
+    conf = tmp_path / "duxbay.conf"
+    conf.write_text("LUSER=/data/u\nLPATH=${LUSER}/ml/${FDATE}\nFLOW_PATH=/a\nTOL=1e-5\n")
+    c = CFG.resolve("20160122", "flow", conf_path=str(conf), environ={"FLOW_PATH": "/b"})
+    assert c.lpath == "/data/u/ml/20160122" and c.flow_path == "/b" and c.tol == 1e-5
+    c = CFG.resolve("20160122", "flow", tol=1e-9, conf_path=str(conf), environ={}, topics=30)
+    assert c.tol == 1e-9 and c.topics == 30 and c.flow_path == "/a"
+
+
+def test_cli_syntax_error():
+    r = subprocess.run([sys.executable, "-m", "oni_ml_amd", "ml_ops", "2016", "flow"], cwd=ROOT, capture_output=True,
+                       text=True)
+    assert "ml_ops.sh syntax error" in r.stdout
+
+
+def test_cli_end_to_end_and_lda_est(tmp_path):
+    from oni_ml_amd.synth.flow import generate_flow_day
+    generate_flow_day(str(tmp_path / "in") + "/", events=3000, seed=2, n_internal=200, n_external=300)
+    st = tmp_path / "settings.txt"
+    st.write_text(LDASettings(em_max_iter=2).dumps())
+    env = dict(os.environ, ONI_CONF=str(tmp_path / "none.conf"))
+    r = subprocess.run([sys.executable, "-m", "oni_ml_amd", "ml_ops", "20160122", "flow", "1e-3", "--lpath",
+                        str(tmp_path / "ml"), "--flow-path", str(tmp_path / "in"), "--backend", "torch", "--settings",
+                        str(st), "--threads", "2", "--quiet"], cwd=ROOT, capture_output=True, text=True, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    summ = json.load(open(tmp_path / "ml" / "run_summary.json"))
+    assert summ["scored"] > 0 and (tmp_path / "ml" / "flow_results.csv").exists()
+    assert not (tmp_path / "ml" / "doc_wc.dat").exists()
+    # lda est on the produced corpus (GPU engine's CLI, torch backend here)
+    r = subprocess.run([sys.executable, "-m", "oni_ml_amd", "lda", "est", "2.5", "20", str(st), "1",
+                        str(tmp_path / "ml" / "model.dat"), "random", str(tmp_path / "lda"), "--backend", "torch"],
+                       cwd=ROOT, capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert (tmp_path / "lda" / "final.gamma").exists() and (tmp_path / "lda" / "word-assignments.dat").exists()
+    # lda_post on that directory with the reference's file names
+    import shutil
+    for f in ("doc.dat", "words.dat"):
+        shutil.copy(tmp_path / "ml" / f, tmp_path / "lda" / f)
+    r = subprocess.run([sys.executable, "-m", "oni_ml_amd", "lda_post", str(tmp_path / "lda") + "/"], cwd=ROOT,
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert (tmp_path / "lda" / "word_results.csv").exists()
