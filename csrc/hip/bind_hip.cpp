@@ -57,6 +57,25 @@ PYBIND11_MODULE(_onihip, m) {
         oni::launch_lda_estep(a, variant, KS, S(stream));
       });
 
+  m.def("split_segment_words", [](int KS) { return oni::split_segment_words(KS); });
+  m.def("split_max_blocks", []() { return oni::kSplitMaxBlocks; });
+  m.def(
+      "lda_estep_split",
+      [](u doc_ptr, u word_idx, u counts, u beta, int K, int KS, float alpha, double lik_const, int var_max_iter,
+         float var_conv, u gamma, u e_out, u r_out, u lik, u alpha_ss, u iters, u seg_doc, u seg_index, u seg_count,
+         u seg_base, u doc_slot, int n_blocks, int seg_words, u partial, u partial_l, u counter, u error, u stream) {
+        oni::EStepArgs a{P<const int>(doc_ptr), P<const int>(word_idx), P<const float>(counts),
+                         nullptr,               n_blocks,             P<const float>(beta),
+                         K,                     alpha,                lik_const,
+                         var_max_iter,          var_conv,             P<float>(gamma),
+                         P<float>(e_out),       P<float>(r_out),      P<double>(lik),
+                         P<double>(alpha_ss),   P<int>(iters)};
+        oni::SplitArgs s{P<const int>(seg_doc), P<const int>(seg_index), P<const int>(seg_count),
+                         P<const int>(seg_base), P<const int>(doc_slot), n_blocks, seg_words, P<float>(partial),
+                         P<double>(partial_l), P<int>(counter), P<int>(error)};
+        oni::launch_lda_estep_split(a, s, KS, S(stream));
+      });
+
   m.def("lda_suffstats", [](u word_ptr, u csc_ent, u csc_doc, u order, int n_items, u e, u r, u beta, u cw,
                             int KS, int variant, u stream) {
     oni::SuffArgs a{P<const int>(word_ptr), P<const int>(csc_ent), P<const int>(csc_doc),

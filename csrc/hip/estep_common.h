@@ -1,0 +1,40 @@
+// Device helpers shared by the E-step kernels (lda_estep.hip, lda_estep_split.hip).
+#pragma once
+#include "common.h"
+
+namespace oni {
+
+// One word-major beta row (KS topics, 16-byte aligned) into registers.
+template <int KS>
+__device__ __forceinline__ void load_row(const float* __restrict__ beta, int w, float (&row)[KS]) {
+  const float4* p = reinterpret_cast<const float4*>(beta + (size_t)w * KS);
+#pragma unroll
+  for (int j = 0; j < KS / 4; ++j) {
+    float4 v = p[j];
+    row[4 * j + 0] = v.x;
+    row[4 * j + 1] = v.y;
+    row[4 * j + 2] = v.z;
+    row[4 * j + 3] = v.w;
+  }
+}
+
+// P = sum_k E_k * row_k with E read from LDS (broadcast: every lane of a group
+// reads the same address).
+template <int KS>
+__device__ __forceinline__ float dot_lds(const float* sE, const float (&row)[KS]) {
+  const float4* e4 = reinterpret_cast<const float4*>(sE);
+  float p0 = 0.f, p1 = 0.f;
+#pragma unroll
+  for (int j = 0; j < KS / 4; ++j) {
+    float4 e = e4[j];
+    p0 = fmaf(e.x, row[4 * j + 0], p0);
+    p1 = fmaf(e.y, row[4 * j + 1], p1);
+    p0 = fmaf(e.z, row[4 * j + 2], p0);
+    p1 = fmaf(e.w, row[4 * j + 3], p1);
+  }
+  return p0 + p1;
+}
+
+constexpr float kPMin = 1e-30f;
+
+}  // namespace oni

@@ -20,6 +20,28 @@ enum EStepVariant : int {
   kEStepB8 = 5,    // one doc per 8-wave workgroup (longest docs)
 };
 
+// Huge documents (the long-context analogue): one document is
+// split into `nseg` contiguous word segments, one 4-wave workgroup each; every
+// variational iteration the segments exchange their partial
+// (sum_n c_n beta_n / P_n, sum_n c_n log P_n) through global memory behind a
+// per-document arrival counter, and each workgroup then runs the identical
+// (deterministic) topic update.  All workgroups of one launch must be
+// co-resident: the host caps a launch at kSplitMaxBlocks workgroups.
+constexpr int kSplitMaxBlocks = 256;
+struct SplitArgs {
+  const int* seg_doc;     // [n_blocks] document of each workgroup
+  const int* seg_index;   // [n_blocks] segment number within its document
+  const int* seg_count;   // [n_blocks] segments of that document
+  const int* seg_base;    // [n_blocks] block id of the document's segment 0
+  const int* doc_slot;    // [n_blocks] counter slot of the document
+  int n_blocks;
+  int seg_words;          // words per segment
+  float* partial;         // [2][n_blocks][KS]  partial accumulators (parity double-buffer)
+  double* partial_l;      // [2][n_blocks]      partial sum_n c_n log P_n
+  int* counter;           // [n_docs_in_launch] arrival counters, zeroed before the launch
+  int* error;             // set to 1 if a barrier wait times out (never hangs the GPU)
+};
+
 struct EStepArgs {
   const int* doc_ptr;     // [D+1] CSR offsets
   const int* word_idx;    // [nnz]
@@ -40,6 +62,8 @@ struct EStepArgs {
   int* iters;             // [D]
 };
 void launch_lda_estep(const EStepArgs& a, int variant, int KS, hipStream_t s);
+void launch_lda_estep_split(const EStepArgs& a, const SplitArgs& s, int KS, hipStream_t st);
+int split_segment_words(int KS);   // words one split workgroup keeps in registers
 
 // ------------------------------------------------------------ suff stats ---
 enum SuffVariant : int { kSuffG16 = 0, kSuffG64 = 1, kSuffB8 = 2 };

@@ -1,0 +1,304 @@
+// Split-document E-step: one huge document over several workgroups
+// (the sequence-/context-parallel analogue of SURVEY.md §5.7(a)).
+//
+// A document with N >> 1024 distinct words (NAT gateways, resolvers, busy
+// servers: the heavy tail of IP "documents") would serialise its whole
+// variational loop on one workgroup.  Here it is cut into `nseg` segments of
+// `seg_words` words; workgroup s keeps its segment's beta rows in VGPRs for all
+// variational iterations and every iteration
+//
+//   1. computes E from its (replicated) topic state,
+//   2. reduces its segment's sum_n (c_n/P_n) beta_n  and  sum_n c_n log P_n
+//      over its 4 waves (LDS),
+//   3. publishes them to partial[it & 1][block] and arrives on the document's
+//      counter (agent-scope release; microarch guide "Valid forms": storing
+//      wave waits vmcnt(0), release fence, vmcnt(0), relaxed atomic add),
+//   4. waits until all nseg segments arrived (relaxed agent-scope poll with
+//      s_sleep, then one agent-scope acquire; the spin is bounded and reports
+//      a timeout through `error` instead of hanging the GPU),
+//   5. sums the nseg partials in segment order -- identical bits in every
+//      workgroup -- and runs the same deterministic topic update, so all
+//      segments agree on gamma and on the convergence decision without a
+//      second barrier.
+// Parity double-buffering makes one barrier per iteration sufficient: a
+// workgroup can only overwrite buffer (it & 1) again at iteration it + 2, after
+// every segment has passed barrier it + 1, i.e. finished reading iteration it.
+// The launch is capped at kSplitMaxBlocks workgroups (one per CU), so all
+// segments are co-resident and the barrier cannot deadlock.
+#include <stdexcept>
+#include <string>
+
+#include "common.h"
+#include "estep_common.h"
+#include "kernels.h"
+
+namespace oni {
+
+namespace {
+
+constexpr int kNW = 4;
+constexpr int kNT = kNW * 64;
+constexpr long kSpinLimit = 1L << 26;   // ~ seconds of polling, then give up (error flag)
+
+__device__ __forceinline__ void publish_arrive(int* counter) {
+  // caller: the storing wave, after its partial stores
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_add(counter, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ bool wait_count(int* counter, int target, int* error) {
+  bool ok = true;
+  if ((threadIdx.x & 63) == 0) {
+    long spins = 0;
+    while (__hip_atomic_load(counter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+      __builtin_amdgcn_s_sleep(2);
+      if (++spins > kSpinLimit) {
+        ok = false;
+        __hip_atomic_store(error, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+    }
+  }
+  ok = __shfl(ok ? 1 : 0, 0) != 0;
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  return ok;
+}
+
+}  // namespace
+
+template <int KS, int CW>
+__global__ __launch_bounds__(kNT) void lda_estep_split(EStepArgs a, SplitArgs s) {
+  constexpr int TJ = (KS + 63) / 64;
+  __shared__ float4 sE4[KS / 4];
+  __shared__ float sRed[kNW][KS];
+  __shared__ double sRedD[kNW];
+  __shared__ int sFlag;
+
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const int b = blockIdx.x;
+  const int d = s.seg_doc[b];
+  const int seg = s.seg_index[b];
+  const int nseg = s.seg_count[b];
+  const int base = s.seg_base[b];
+  int* counter = s.counter + s.doc_slot[b];
+  const int dbeg = a.doc_ptr[d];
+  const int Ndoc = a.doc_ptr[d + 1] - dbeg;
+  const int beg = dbeg + seg * s.seg_words;
+  const int N = min(s.seg_words, Ndoc - seg * s.seg_words);
+  const int K = a.K;
+  const float alpha = a.alpha;
+  float* sE = reinterpret_cast<float*>(&sE4[0]);
+
+  // ---- this workgroup's words in registers (seg_words <= kNT * CW) ----
+  float bc[CW][KS];
+  float cc[CW];
+#pragma unroll
+  for (int c = 0; c < CW; ++c) {
+    const int n = t + kNT * c;
+    if (n < N) {
+      cc[c] = a.counts[beg + n];
+      load_row<KS>(a.beta, a.word_idx[beg + n], bc[c]);
+    } else {
+      cc[c] = 0.f;
+#pragma unroll
+      for (int k = 0; k < KS; ++k) bc[c][k] = 0.f;
+    }
+  }
+  // document total (every workgroup reads the whole doc's counts: O(N) once)
+  double tot_l = 0.0;
+  for (int n = t; n < Ndoc; n += kNT) tot_l += a.counts[dbeg + n];
+  tot_l = group_sum<64>(tot_l);
+  if (lane == 0) sRedD[wv] = tot_l;
+  __syncthreads();
+  double total = 0.0;
+#pragma unroll
+  for (int w = 0; w < kNW; ++w) total += sRedD[w];
+  __syncthreads();
+
+  float gam[TJ], psi[TJ], e[TJ];
+  const float g0 = alpha + (float)(total / K);
+  double lik_old = 0.0, L = 0.0, conv = 1.0, dsum_last = 0.0;
+  float m = 0.f;
+  int it = 0;
+  const bool unbounded = a.var_max_iter < 0;
+  if (wv == 0) {
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) {
+      const int k = lane + 64 * j;
+      gam[j] = (k < K) ? g0 : 0.f;
+      psi[j] = (k < K) ? digammaf_ldac(g0) : -INFINITY;
+    }
+    float mx = -INFINITY;
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) mx = fmaxf(mx, psi[j]);
+    m = group_max<64>(mx);
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) {
+      const int k = lane + 64 * j;
+      e[j] = (k < K) ? __expf(psi[j] - m) : 0.f;
+      if (k < KS) sE[k] = e[j];
+    }
+    float sg = 0.f;
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) sg += gam[j];
+    dsum_last = digammaf_ldac(group_sum<64>(sg));
+    if (lane == 0) sFlag = (unbounded || a.var_max_iter > 0) ? 1 : 0;
+  }
+  __syncthreads();
+
+  while (sFlag) {
+    // ---- word pass over this segment ----
+    float acc[KS];
+#pragma unroll
+    for (int k = 0; k < KS; ++k) acc[k] = 0.f;
+    float lsum = 0.f;
+#pragma unroll
+    for (int c = 0; c < CW; ++c) {
+      if (t + kNT * c < N) {
+        const float P = fmaxf(dot_lds<KS>(sE, bc[c]), kPMin);
+        const float r = cc[c] / P;
+        lsum = fmaf(cc[c], __logf(P), lsum);
+#pragma unroll
+        for (int k = 0; k < KS; ++k) acc[k] = fmaf(r, bc[c][k], acc[k]);
+      }
+    }
+    group_sum_vec<64, KS>(acc);
+    const double lsum_w = group_sum<64>((double)lsum);
+    if (lane == 0) {
+#pragma unroll
+      for (int k = 0; k < KS; ++k) sRed[wv][k] = acc[k];
+      sRedD[wv] = lsum_w;
+    }
+    __syncthreads();
+
+    if (wv == 0) {
+      ++it;
+      const int par = it & 1;
+      // publish this segment's partial, arrive, wait for all segments
+      float* prow = s.partial + ((size_t)par * s.n_blocks + b) * KS;
+#pragma unroll
+      for (int j = 0; j < TJ; ++j) {
+        const int k = lane + 64 * j;
+        if (k < KS) {
+          float v = 0.f;
+#pragma unroll
+          for (int w = 0; w < kNW; ++w) v += sRed[w][k];
+          prow[k] = v;
+        }
+      }
+      if (lane == 0) {
+        double l = 0.0;
+#pragma unroll
+        for (int w = 0; w < kNW; ++w) l += sRedD[w];
+        s.partial_l[(size_t)par * s.n_blocks + b] = l;
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      publish_arrive(counter);
+      const bool ok = wait_count(counter, nseg * it, s.error);
+      // all segments' partials, summed in segment order (bitwise identical in every workgroup)
+      double lsum_d = 0.0;
+      float gn[TJ];
+      float sg = 0.f;
+#pragma unroll
+      for (int j = 0; j < TJ; ++j) {
+        const int k = lane + 64 * j;
+        float ak = 0.f;
+        if (k < KS) {
+          for (int q = 0; q < nseg; ++q) ak += s.partial[((size_t)par * s.n_blocks + base + q) * KS + k];
+        }
+        gn[j] = (k < K) ? fmaf(e[j], ak, alpha) : 0.f;
+        sg += gn[j];
+      }
+      for (int q = 0; q < nseg; ++q) lsum_d += s.partial_l[(size_t)par * s.n_blocks + base + q];
+      const float S = group_sum<64>(sg);
+      const float dS = digammaf_ldac(S);
+      double term = 0.0;
+#pragma unroll
+      for (int j = 0; j < TJ; ++j) {
+        const int k = lane + 64 * j;
+        if (k < K) {
+          const float pn = digammaf_ldac(gn[j]);
+          const float y = pn - dS;
+          term += (double)((alpha - 1.f) * y) + (double)lgammaf(gn[j]) - (double)((gn[j] - 1.f) * y) +
+                  (double)((gn[j] - alpha) * (pn - psi[j]));
+          psi[j] = pn;
+          gam[j] = gn[j];
+        }
+      }
+      term = group_sum<64>(term);
+      L = a.lik_const - (double)lgammaf(S) + term + (lsum_d + (double)m * total) - total * (double)dS;
+      conv = (lik_old - L) / lik_old;
+      lik_old = L;
+      dsum_last = dS;
+      const bool cont = ok && conv > (double)a.var_conv && (unbounded || it < a.var_max_iter);
+      if (cont) {
+        float mx = -INFINITY;
+#pragma unroll
+        for (int j = 0; j < TJ; ++j) mx = fmaxf(mx, psi[j]);
+        m = group_max<64>(mx);
+#pragma unroll
+        for (int j = 0; j < TJ; ++j) {
+          const int k = lane + 64 * j;
+          e[j] = (k < K) ? __expf(psi[j] - m) : 0.f;
+          if (k < KS) sE[k] = e[j];
+        }
+      }
+      if (lane == 0) sFlag = cont ? 1 : 0;
+    }
+    __syncthreads();
+  }
+
+  // ---- outputs: r for this segment; the document state from segment 0 ----
+#pragma unroll
+  for (int c = 0; c < CW; ++c) {
+    const int n = t + kNT * c;
+    if (n < N) a.r_out[beg + n] = cc[c] / fmaxf(dot_lds<KS>(sE, bc[c]), kPMin);
+  }
+  if (wv == 0 && seg == 0) {
+    double ass = 0.0;
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) {
+      const int k = lane + 64 * j;
+      if (k < KS) {
+        a.gamma[(size_t)d * KS + k] = gam[j];
+        a.e_out[(size_t)d * KS + k] = sE[k];
+      }
+      if (k < K) ass += (double)psi[j];
+    }
+    ass = group_sum<64>(ass);
+    if (lane == 0) {
+      a.lik[d] = L;
+      a.alpha_ss[d] = ass - (double)K * dsum_last;
+      a.iters[d] = it;
+    }
+  }
+}
+
+template <int KS>
+static void split_ks(const EStepArgs& a, const SplitArgs& s, hipStream_t st) {
+  constexpr int CW = KS <= 32 ? 4 : (KS <= 64 ? 2 : 1);
+  if (s.n_blocks <= 0) return;
+  if (s.n_blocks > kSplitMaxBlocks) throw std::runtime_error("lda_estep_split: too many workgroups in one launch");
+  if (s.seg_words > kNT * CW) throw std::runtime_error("lda_estep_split: segment larger than the register cache");
+  hipLaunchKernelGGL((lda_estep_split<KS, CW>), dim3(s.n_blocks), dim3(kNT), 0, st, a, s);
+  ONI_HIP_CHECK(hipGetLastError());
+}
+
+int split_segment_words(int KS) { return kNT * (KS <= 32 ? 4 : (KS <= 64 ? 2 : 1)); }
+
+void launch_lda_estep_split(const EStepArgs& a, const SplitArgs& s, int KS, hipStream_t st) {
+  switch (KS) {
+#define ONI_KS(X) \
+  case X:         \
+    split_ks<X>(a, s, st); \
+    break;
+    ONI_FOR_EACH_KS(ONI_KS)
+#undef ONI_KS
+    default:
+      throw std::runtime_error("lda_estep_split: unsupported KS " + std::to_string(KS));
+  }
+}
+
+}  // namespace oni

@@ -60,13 +60,23 @@ class LDAResult:
 class _Buckets:
     """Length-bucket plan: (variant, int32 order tensor) launched per E-step."""
 
-    def __init__(self, lengths: np.ndarray, ks: int, device, kind: str):
+    def __init__(self, lengths: np.ndarray, ks: int, device, kind: str, doc_ptr: Optional[np.ndarray] = None,
+                 split: bool = True):
         from ...ops import hip as H
         order = np.argsort(-lengths, kind="stable").astype(np.int32)
         L = lengths[order]
         plan = []
+        self.split = None
         if kind == "doc":
             cws = 4 if ks <= 32 else (2 if ks <= 64 else 1)
+            if split and doc_ptr is not None:
+                # documents beyond one workgroup's register cache: split over several workgroups
+                huge = order[L > 256 * cws]
+                if huge.size:
+                    self.split = H.SplitPlan(huge, doc_ptr, ks, device)
+                    rest = np.asarray(self.split.leftover, np.int32)
+                    keep = ~np.isin(order, huge) | np.isin(order, rest)
+                    order, L = order[keep], L[keep]
             edges = [(H.ESTEP_B8, 256 * cws, None), (H.ESTEP_B4, 64 * cws, 256 * cws),
                      (H.ESTEP_G64C, 64, 64 * cws), (H.ESTEP_G64, 32, 64), (H.ESTEP_G32, 16, 32),
                      (H.ESTEP_G16, 0, 16)]
@@ -85,7 +95,7 @@ class _Buckets:
 class LDAEngine:
     def __init__(self, corpus: Corpus, num_topics: int, settings: Optional[LDASettings] = None,
                  alpha_init: float = 2.5, backend: str = "auto", device=None, dist=None, seed: int = 0,
-                 streams: int = 3, local_shard: bool = False):
+                 streams: int = 3, local_shard: bool = False, split_docs: bool = True):
         self.settings = settings or LDASettings()
         self.K = int(num_topics)
         self.V = corpus.num_terms
@@ -121,7 +131,8 @@ class LDAEngine:
             from ...ops import hip as H
             self.KS = H.padded_topics(self.K)
             self.dc = DeviceCorpus.build(corpus, self.device)
-            self.doc_buckets = _Buckets(self.dc.doc_len, self.KS, self.device, "doc")
+            self.doc_buckets = _Buckets(self.dc.doc_len, self.KS, self.device, "doc",
+                                        doc_ptr=corpus.doc_ptr, split=split_docs)
             self.word_buckets = _Buckets(self.dc.word_len, self.KS, self.device, "word")
             dev, D, V, KS, nnz = self.device, self.D, self.V, self.KS, corpus.nnz
             self.beta = torch.zeros(V, KS, dtype=torch.float32, device=dev)
@@ -184,6 +195,20 @@ class LDAEngine:
         self._set_ss_host(cw, normalized=True)
         self.alpha = float(alpha)
 
+    def state_arrays(self) -> dict:
+        """Exact engine state (sufficient statistics in the engine's own precision) for checkpoints."""
+        return dict(cw=self.cw.cpu().numpy(), class_total=self.class_total.cpu().numpy())
+
+    def load_state_arrays(self, cw: np.ndarray, class_total: np.ndarray, alpha: float):
+        """Restore `state_arrays()` output; beta is re-derived by the same M-step, so a resumed run is
+        bit-identical to an uninterrupted one."""
+        if tuple(cw.shape) != tuple(self.cw.shape):
+            raise ValueError(f"checkpoint statistics {cw.shape} != engine {tuple(self.cw.shape)}")
+        self.cw.copy_(torch.from_numpy(cw).to(self.cw.device, self.cw.dtype))
+        self.class_total = torch.from_numpy(class_total).to(self.cw.device, torch.float64)
+        self._mstep_beta()
+        self.alpha = float(alpha)
+
     def _set_ss_host(self, cw_kv: np.ndarray, normalized=False):
         ct = np.cumsum(cw_kv, axis=1)[:, -1] if cw_kv.shape[1] else np.zeros(self.K)
         if normalized:
@@ -239,6 +264,16 @@ class LDAEngine:
         # fork: largest buckets on side streams so they overlap the short-doc bulk
         ev = torch.cuda.Event()
         ev.record(main)
+        sp = self.doc_buckets.split
+        if sp is not None:  # huge documents first, on their own stream (critical path)
+            s = streams[-1]
+            if s is not main:
+                s.wait_event(ev)
+            with torch.cuda.stream(s):
+                for batch in sp.batches:
+                    H.lda_estep_split(dc.doc_ptr, dc.word_idx, dc.counts, self.beta, self.K, self.alpha, lc,
+                                      self.var_max_iter, self.settings.var_converged, self.gamma, self.e, self.r,
+                                      self.lik, self.ass, self.iters, batch, sp.seg_words)
         for i, (var, order) in enumerate(plan):
             s = streams[i % len(streams)]
             if s is not main:

@@ -36,7 +36,7 @@ def save_checkpoint(outdir: str, eng: LDAEngine, iteration: int, L_old: float, h
     tmp = os.path.join(outdir, CKPT + ".tmp.npz")
     np.savez(tmp, log_beta=eng.log_beta(), alpha=np.float64(eng.alpha), iteration=np.int64(iteration),
              likelihood_old=np.float64(L_old), var_max_iter=np.int64(eng.var_max_iter),
-             history=np.asarray(history, np.float64).reshape(-1, 2))
+             history=np.asarray(history, np.float64).reshape(-1, 2), **eng.state_arrays())
     os.replace(tmp, os.path.join(outdir, CKPT))
 
 
@@ -73,7 +73,10 @@ def estimate(corpus: Corpus, num_topics: int, alpha_init: float, settings: LDASe
     start_it, L_old, hist = 0, 0.0, []
     ck = load_checkpoint(outdir) if resume else None
     if ck is not None:
-        eng.init_from_model(ck["log_beta"], float(ck["alpha"]))
+        if "cw" in ck and tuple(ck["cw"].shape) == tuple(eng.cw.shape):
+            eng.load_state_arrays(ck["cw"], ck["class_total"], float(ck["alpha"]))
+        else:
+            eng.init_from_model(ck["log_beta"], float(ck["alpha"]))
         eng.var_max_iter = int(ck["var_max_iter"])
         start_it, L_old = int(ck["iteration"]), float(ck["likelihood_old"])
         hist = [tuple(x) for x in ck["history"].tolist()]

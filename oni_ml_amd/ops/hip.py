@@ -116,6 +116,75 @@ def lda_estep(doc_ptr, word_idx, counts, order, beta, K, alpha, lik_const, var_m
     lib().lda_estep(*args)
 
 
+class SplitPlan:
+    """Launch batches for the split-document E-step (huge documents over several workgroups).
+
+    Each batch holds <= split_max_blocks() workgroups so every segment of a batch is
+    co-resident (the per-iteration cross-workgroup barrier cannot deadlock)."""
+
+    def __init__(self, doc_ids, doc_ptr_host, KS: int, device):
+        L = lib()
+        self.seg_words = int(L.split_segment_words(KS))
+        self.max_blocks = int(L.split_max_blocks())
+        self.batches = []
+        self.leftover = []          # docs needing more segments than a batch holds
+        cur = []
+        used = 0
+        for d in doc_ids:
+            n = int(doc_ptr_host[d + 1] - doc_ptr_host[d])
+            nseg = (n + self.seg_words - 1) // self.seg_words
+            if nseg > self.max_blocks:
+                self.leftover.append(int(d))
+                continue
+            if used + nseg > self.max_blocks:
+                self.batches.append(self._make(cur, doc_ptr_host, KS, device))
+                cur, used = [], 0
+            cur.append((int(d), nseg))
+            used += nseg
+        if cur:
+            self.batches.append(self._make(cur, doc_ptr_host, KS, device))
+
+    def _make(self, docs, doc_ptr_host, KS, device):
+        import numpy as np
+        sd, si, sc, sb, slot = [], [], [], [], []
+        for j, (d, nseg) in enumerate(docs):
+            base = len(sd)
+            for q in range(nseg):
+                sd.append(d), si.append(q), sc.append(nseg), sb.append(base), slot.append(j)
+        t = lambda a: torch.tensor(np.asarray(a, np.int32), device=device)
+        nb = len(sd)
+        return dict(seg_doc=t(sd), seg_index=t(si), seg_count=t(sc), seg_base=t(sb), doc_slot=t(slot), n_blocks=nb,
+                    partial=torch.zeros(2 * nb * KS, dtype=torch.float32, device=device),
+                    partial_l=torch.zeros(2 * nb, dtype=torch.float64, device=device),
+                    counter=torch.zeros(len(docs), dtype=torch.int32, device=device),
+                    error=torch.zeros(1, dtype=torch.int32, device=device), docs=len(docs))
+
+
+def lda_estep_split(doc_ptr, word_idx, counts, beta, K, alpha, lik_const, var_max_iter, var_conv, gamma, e_out, r_out,
+                    lik, alpha_ss, iters, batch, seg_words):
+    D = doc_ptr.numel() - 1
+    nnz = word_idx.numel()
+    V, KS = beta.shape
+    dev = beta.device
+    nb = batch["n_blocks"]
+    for k in ("seg_doc", "seg_index", "seg_count", "seg_base", "doc_slot"):
+        _chk(batch[k], torch.int32, k, (nb,), dev)
+    batch["counter"].zero_()
+    lib().lda_estep_split(
+        _chk(doc_ptr, torch.int32, "doc_ptr", (D + 1,), dev), _chk(word_idx, torch.int32, "word_idx", (nnz,), dev),
+        _chk(counts, torch.float32, "counts", (nnz,), dev), _chk(beta, torch.float32, "beta", (V, KS), dev),
+        int(K), int(KS), float(alpha), float(lik_const), int(var_max_iter), float(var_conv),
+        _chk(gamma, torch.float32, "gamma", (D, KS), dev), _chk(e_out, torch.float32, "e_out", (D, KS), dev),
+        _chk(r_out, torch.float32, "r_out", (nnz,), dev), _chk(lik, torch.float64, "lik", (D,), dev),
+        _chk(alpha_ss, torch.float64, "alpha_ss", (D,), dev), _chk(iters, torch.int32, "iters", (D,), dev),
+        batch["seg_doc"].data_ptr(), batch["seg_index"].data_ptr(), batch["seg_count"].data_ptr(),
+        batch["seg_base"].data_ptr(), batch["doc_slot"].data_ptr(), int(nb), int(seg_words),
+        _chk(batch["partial"], torch.float32, "partial", (2 * nb * KS,), dev),
+        _chk(batch["partial_l"], torch.float64, "partial_l", (2 * nb,), dev),
+        _chk(batch["counter"], torch.int32, "counter", None, dev), _chk(batch["error"], torch.int32, "error", (1,), dev),
+        _stream())
+
+
 def lda_suffstats(word_ptr, csc_ent, csc_doc, order, e, r, beta, cw, variant):
     V, KS = beta.shape
     nnz = csc_ent.numel()

@@ -1,0 +1,92 @@
+"""GPU (gfx950) end-to-end: HIP featurization/scoring kernels and the pipelines on cuda:0."""
+import json
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+from oni_ml_amd import config as CFG
+from oni_ml_amd.models.lda.settings import LDASettings
+from oni_ml_amd.ops import reference as R
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_flow_words_kernel_bitwise(hip):
+    rng = np.random.default_rng(0)
+    n = 200_000
+    ports = np.array([0, 1, 22, 53, 80, 443, 1023, 1024, 1025, 8080, 49152, 65535], np.float64)
+    cols = [rng.integers(0, 24, n) * 1.0, rng.integers(0, 60, n) * 1.0, rng.integers(0, 60, n) * 1.0,
+            rng.choice(ports, n), rng.choice(ports, n), rng.integers(1, 100, n) * 1.0, rng.integers(28, 9000, n) * 1.0]
+    cuts = [torch.tensor([0.0, 2.3, 4.78, 7.41, 9.68, 12.0, 14.2, 16.6, 19.1, 21.6], dtype=torch.float64),
+            torch.tensor([0.0, 52, 76, 104, 152, 207, 293, 573, 1234, 3569], dtype=torch.float64),
+            torch.tensor([0.0, 1, 1, 2, 4], dtype=torch.float64)]
+    g = hip.flow_words(*[torch.from_numpy(c).cuda() for c in cols], *[c.cuda() for c in cuts])
+    r = R.flow_words(*[torch.from_numpy(c) for c in cols], *cuts)
+    for k in ("time", "time_bin", "ibyt_bin", "ipkt_bin", "word_port", "src_prefix", "dst_prefix"):
+        assert torch.equal(g[k].cpu(), r[k]), k
+
+
+def _flow(tmp_path, backend, device, events=20000, topics=20):
+    from oni_ml_amd.pipeline import run
+    from oni_ml_amd.synth.flow import generate_flow_day
+    if not (tmp_path / "in").exists():
+        generate_flow_day(str(tmp_path / "in") + "/", events=events, seed=4, n_internal=1500, n_external=3000)
+    lp = tmp_path / f"ml_{backend}"
+    cfg = CFG.resolve("20160122", "flow", tol=1e-4, conf_path=None, environ={}, lpath=str(lp),
+                      flow_path=str(tmp_path / "in"), backend=backend, threads=4, verbose=False, topics=topics)
+    cfg.settings = LDASettings(em_max_iter=6)
+    return run(cfg, device=device, log=lambda *a, **k: None), lp
+
+
+def test_flow_pipeline_gpu_matches_cpu_path(tmp_path):
+    s_gpu, lg = _flow(tmp_path, "hip", "cuda")
+    s_cpu, lc = _flow(tmp_path, "torch", "cpu")
+    for f in ("doc.dat", "words.dat", "model.dat"):   # featurization + corpus identical on both devices
+        assert (lg / f).read_text() == (lc / f).read_text(), f
+    Lg = [float(l.split()[0]) for l in (lg / "likelihood.dat").read_text().splitlines()]
+    Lc = [float(l.split()[0]) for l in (lc / "likelihood.dat").read_text().splitlines()]
+    assert len(Lg) == len(Lc) and np.allclose(Lg, Lc, rtol=1e-3)
+    fg = [l.split(",")[:27] for l in (lg / "flow_results.csv").read_text().splitlines()]
+    fc = [l.split(",")[:27] for l in (lc / "flow_results.csv").read_text().splitlines()]
+    sg, sc = set(map(tuple, fg)), set(map(tuple, fc))
+    assert len(sg) > 0 and len(sg & sc) / max(len(sg | sc), 1) > 0.9
+
+
+def test_dns_pipeline_gpu(tmp_path):
+    from oni_ml_amd.pipeline import run
+    from oni_ml_amd.synth.dns import generate_dns_day
+    r = generate_dns_day(str(tmp_path / "in"), events=30000, seed=1, files=2)
+    cfg = CFG.resolve("20160122", "dns", tol=1e-3, conf_path=None, environ={}, lpath=str(tmp_path / "ml"),
+                      dns_path=r["dns_path"], top1m=r["top1m"], backend="hip", threads=4, verbose=False)
+    cfg.settings = LDASettings(em_max_iter=5)
+    s = run(cfg, device="cuda", log=lambda *a, **k: None)
+    rows = (tmp_path / "ml" / "dns_results.csv").read_text().splitlines()
+    assert len(rows) == s["scored"] and all(len(l.split(",")) == 16 for l in rows[:100])
+
+
+def test_hip_estimate_resume_exact(tmp_path):
+    from oni_ml_amd.models.lda.estimate import estimate
+    from oni_ml_amd.synth.corpus import planted_corpus
+    c = planted_corpus(num_docs=3000, num_terms=800, num_topics=6, seed=2)
+    st = lambda: LDASettings(em_max_iter=11, em_converged=1e-12)
+    full = estimate(c, 20, 2.5, st(), "random", str(tmp_path / "a"), backend="hip", device="cuda", seed=5)
+    with pytest.raises(RuntimeError):
+        estimate(c, 20, 2.5, st(), "random", str(tmp_path / "b"), backend="hip", device="cuda", seed=5,
+                 fault_at_iteration=6)
+    res = estimate(c, 20, 2.5, st(), "random", str(tmp_path / "b"), backend="hip", device="cuda", seed=5, resume=True)
+    assert (tmp_path / "a" / "likelihood.dat").read_text() == (tmp_path / "b" / "likelihood.dat").read_text()
+    assert np.array_equal(res.gamma, full.gamma)
+
+
+def test_bench_smoke():
+    r = subprocess.run([sys.executable, "bench.py", "--steps", "3", "--warmup", "1", "--events", "200000",
+                        "--converge", "0", "--e2e", "0"], cwd=ROOT, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = [l for l in r.stdout.splitlines() if l.startswith("{")][-1]
+    out = json.loads(line)
+    assert out["n_gpus"] == 1 and out["value"] > 0 and out["steps"] == 3

@@ -139,3 +139,33 @@ def test_score_kernel_bitwise(hip):
     ref = R.score(theta, phi, K, 0.05, da, wa, db, wb, 1e-4)
     for a, b in zip(out, ref):
         assert torch.equal(a.cpu(), b), "scores must match the sequential f64 reference bit for bit"
+
+
+@pytest.mark.parametrize("K", [20, 50])
+def test_split_documents_match_single_workgroup(hip, K):
+    """Huge documents split across workgroups (per-iteration cross-workgroup reduction) give the
+    same E-step as the one-workgroup kernel and the fp64 reference."""
+    c = planted_corpus(num_docs=400, num_terms=20000, num_topics=6, mean_tokens=400, tail=0.7,
+                       max_tokens=2_000_000, seed=8)
+    assert c.lengths().max() > 4 * 1024
+    st = LDASettings(var_max_iter=15, var_converged=-1e30)
+    outs = []
+    for split in (True, False):
+        eng = LDAEngine(c, K, st, backend="hip", seed=1, split_docs=split)
+        eng.init_random()
+        if split:
+            assert eng.doc_buckets.split is not None and eng.doc_buckets.split.batches
+        sc = eng.e_step()
+        torch.cuda.synchronize()
+        if split:
+            assert int(eng.doc_buckets.split.batches[0]["error"].item()) == 0
+        outs.append((eng.gamma[:, :K].double().cpu(), eng.lik.cpu(), sc.cpu(), eng.cw.cpu(), eng.iters.cpu()))
+    (g1, l1, s1, cw1, i1), (g0, l0, s0, cw0, i0) = outs
+    assert torch.equal(i1, i0)
+    rel = ((g1 - g0).abs() / g0.abs().clamp_min(1e-3)).max().item()
+    assert rel < 2e-3, rel
+    assert ((l1 - l0).abs() / l0.abs()).max().item() < 1e-5
+    assert ((cw1 - cw0).abs().max() / cw0.abs().max()).item() < 1e-3
+    ref = R.estep_jacobi(torch.from_numpy(c.doc_ptr), torch.from_numpy(c.word_idx), torch.from_numpy(c.counts).double(),
+                         eng.beta.double().cpu(), K, eng.alpha, 15, -1e30)
+    assert ((g1 - ref["gamma"]).abs() / ref["gamma"].abs().clamp_min(1e-3)).max().item() < 2e-3
