@@ -47,13 +47,13 @@ PYBIND11_MODULE(_onihip, m) {
       "lda_estep",
       [](u doc_ptr, u word_idx, u counts, u order, int n_items, u beta, int K, int KS, float alpha,
          double lik_const, int var_max_iter, float var_conv, u gamma, u e_out, u r_out, u lik, u alpha_ss,
-         u iters, int variant, u stream) {
+         u iters, int variant, u params, u stream) {
         oni::EStepArgs a{P<const int>(doc_ptr), P<const int>(word_idx), P<const float>(counts),
                          P<const int>(order),   n_items,              P<const float>(beta),
                          K,                     alpha,                lik_const,
                          var_max_iter,          var_conv,             P<float>(gamma),
                          P<float>(e_out),       P<float>(r_out),      P<double>(lik),
-                         P<double>(alpha_ss),   P<int>(iters)};
+                         P<double>(alpha_ss),   P<int>(iters),        P<const double>(params)};
         oni::launch_lda_estep(a, variant, KS, S(stream));
       });
 
@@ -63,13 +63,13 @@ PYBIND11_MODULE(_onihip, m) {
       "lda_estep_split",
       [](u doc_ptr, u word_idx, u counts, u beta, int K, int KS, float alpha, double lik_const, int var_max_iter,
          float var_conv, u gamma, u e_out, u r_out, u lik, u alpha_ss, u iters, u seg_doc, u seg_index, u seg_count,
-         u seg_base, u doc_slot, int n_blocks, int seg_words, u partial, u partial_l, u counter, u error, u stream) {
+         u seg_base, u doc_slot, int n_blocks, int seg_words, u partial, u partial_l, u counter, u error, u params, u stream) {
         oni::EStepArgs a{P<const int>(doc_ptr), P<const int>(word_idx), P<const float>(counts),
                          nullptr,               n_blocks,             P<const float>(beta),
                          K,                     alpha,                lik_const,
                          var_max_iter,          var_conv,             P<float>(gamma),
                          P<float>(e_out),       P<float>(r_out),      P<double>(lik),
-                         P<double>(alpha_ss),   P<int>(iters)};
+                         P<double>(alpha_ss),   P<int>(iters),        P<const double>(params)};
         oni::SplitArgs s{P<const int>(seg_doc), P<const int>(seg_index), P<const int>(seg_count),
                          P<const int>(seg_base), P<const int>(doc_slot), n_blocks, seg_words, P<float>(partial),
                          P<double>(partial_l), P<int>(counter), P<int>(error)};
@@ -82,6 +82,14 @@ PYBIND11_MODULE(_onihip, m) {
                     P<const int>(order),    n_items,               P<const float>(e),
                     P<const float>(r),      P<const float>(beta),  P<float>(cw)};
     oni::launch_lda_suffstats(a, variant, KS, S(stream));
+  });
+
+  m.def("reduce_scratch_doubles", [](int cols) { return oni::reduce_scratch_doubles(cols); });
+  m.def("colsum", [](u mat, int rows, int cols, u out, u scratch, u stream) {
+    oni::launch_colsum(P<const float>(mat), rows, cols, P<double>(out), P<double>(scratch), S(stream));
+  });
+  m.def("sum2", [](u a, u b, int n, u out, u scratch, u stream) {
+    oni::launch_sum2(P<const double>(a), P<const double>(b), n, P<double>(out), P<double>(scratch), S(stream));
   });
 
   m.def("lda_mstep", [](u cw, u class_total, u beta, int V, int K, int KS, u stream) {

@@ -37,4 +37,15 @@ __device__ __forceinline__ float dot_lds(const float* sE, const float (&row)[KS]
 
 constexpr float kPMin = 1e-30f;
 
+// Per-launch scalars from device memory when the launch is graph-replayed.
+template <typename Args>
+__device__ __forceinline__ void load_params(Args& a) {
+  if (a.params) {
+    a.alpha = (float)a.params[0];
+    a.lik_const = a.params[1];
+    a.var_max_iter = (int)a.params[2];
+    a.var_conv = (float)a.params[3];
+  }
+}
+
 }  // namespace oni

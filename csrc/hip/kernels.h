@@ -18,6 +18,7 @@ enum EStepVariant : int {
   kEStepG64C = 3,  // one wave per doc, several beta rows cached per lane
   kEStepB4 = 4,    // one doc per 4-wave workgroup
   kEStepB8 = 5,    // one doc per 8-wave workgroup (longest docs)
+  kEStepT1 = 6,    // one thread per document (tiny documents, KS <= 32)
 };
 
 // Huge documents (the long-context analogue): one document is
@@ -60,6 +61,10 @@ struct EStepArgs {
   double* lik;            // [D]
   double* alpha_ss;       // [D]
   int* iters;             // [D]
+  // Optional device copy of {alpha, lik_const, var_max_iter, var_conv}: when set
+  // it overrides those four fields, so a captured hipGraph of the E-step can be
+  // replayed every EM iteration while alpha / VAR_MAX_ITER change.
+  const double* params = nullptr;
 };
 void launch_lda_estep(const EStepArgs& a, int variant, int KS, hipStream_t s);
 void launch_lda_estep_split(const EStepArgs& a, const SplitArgs& s, int KS, hipStream_t st);
@@ -85,6 +90,13 @@ void launch_lda_suffstats(const SuffArgs& a, int variant, int KS, hipStream_t s)
 // beta[w][k] = cw/ct_k if cw > 0 else exp(-100) (k < K); 0 for padding topics.
 void launch_lda_mstep(const float* cw, const double* class_total, float* beta, int V, int K, int KS,
                       hipStream_t s);
+
+// ------------------------------------------------------------- reductions ---
+// Deterministic two-pass reductions (reduce.hip).  scratch holds
+// reduce_scratch_doubles(cols) doubles.
+int reduce_scratch_doubles(int cols);
+void launch_colsum(const float* m, int rows, int cols, double* out, double* scratch, hipStream_t s);
+void launch_sum2(const double* a, const double* b, int n, double* out, double* scratch, hipStream_t s);
 
 // ---------------------------------------------------------------- scoring ---
 struct ScoreArgs {

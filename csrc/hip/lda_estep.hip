@@ -45,6 +45,7 @@ namespace oni {
 // ---------------------------------------------------------------------------
 template <int KS, int G, int CW>
 __global__ __launch_bounds__(256) void lda_estep_group(EStepArgs a) {
+  load_params(a);
   constexpr int GPB = 256 / G;
   constexpr int TJ = (KS + G - 1) / G;
   __shared__ float4 sE4[GPB][KS / 4];
@@ -164,14 +165,14 @@ __global__ __launch_bounds__(256) void lda_estep_group(EStepArgs a) {
       if (k < K) {
         const float pn = digammaf_ldac(gn[j]);
         const float y = pn - dS;
-        term += (double)((alpha - 1.f) * y) + (double)lgammaf(gn[j]) - (double)((gn[j] - 1.f) * y) +
+        term += (double)((alpha - 1.f) * y) + (double)lgammaf_fast(gn[j]) - (double)((gn[j] - 1.f) * y) +
                 (double)((gn[j] - alpha) * (pn - psi[j]));
         psi[j] = pn;
         gam[j] = gn[j];
       }
     }
     term = group_sum<G>(term);
-    L = a.lik_const - (double)lgammaf(S) + term + (lsum_d + (double)m * total) - total * (double)dS;
+    L = a.lik_const - (double)lgammaf_fast(S) + term + (lsum_d + (double)m * total) - total * (double)dS;
     conv = (lik_old - L) / lik_old;
     lik_old = L;
     dsum_last = dS;
@@ -229,6 +230,7 @@ __global__ __launch_bounds__(256) void lda_estep_group(EStepArgs a) {
 // ---------------------------------------------------------------------------
 template <int KS, int NW, int CW>
 __global__ __launch_bounds__(NW * 64) void lda_estep_block(EStepArgs a) {
+  load_params(a);
   constexpr int NT = NW * 64;
   constexpr int TJ = (KS + 63) / 64;  // topics per lane of wave 0
   __shared__ float4 sE4[KS / 4];
@@ -368,14 +370,14 @@ __global__ __launch_bounds__(NW * 64) void lda_estep_block(EStepArgs a) {
         if (k < K) {
           const float pn = digammaf_ldac(gn[j]);
           const float y = pn - dS;
-          term += (double)((alpha - 1.f) * y) + (double)lgammaf(gn[j]) - (double)((gn[j] - 1.f) * y) +
+          term += (double)((alpha - 1.f) * y) + (double)lgammaf_fast(gn[j]) - (double)((gn[j] - 1.f) * y) +
                   (double)((gn[j] - alpha) * (pn - psi[j]));
           psi[j] = pn;
           gam[j] = gn[j];
         }
       }
       term = group_sum<64>(term);
-      L = a.lik_const - (double)lgammaf(S) + term + (lsum_d + (double)m * total) - total * (double)dS;
+      L = a.lik_const - (double)lgammaf_fast(S) + term + (lsum_d + (double)m * total) - total * (double)dS;
       conv = (lik_old - L) / lik_old;
       lik_old = L;
       dsum_last = dS;
@@ -429,6 +431,123 @@ __global__ __launch_bounds__(NW * 64) void lda_estep_block(EStepArgs a) {
 }
 
 // ---------------------------------------------------------------------------
+// Thread kernel: one document per thread (tiny documents: half of all IP
+// documents hold 1-2 distinct words).  No cross-lane traffic at all: the
+// thread keeps gamma / psi / E / the accumulator in registers, streams its few
+// beta rows from L2 and runs the whole variational loop serially.  64 documents
+// share a wave; the plan sorts documents by length so a wave's documents have
+// similar word counts.
+// ---------------------------------------------------------------------------
+template <int KS>
+__global__ __launch_bounds__(256) void lda_estep_thread(EStepArgs a) {
+  load_params(a);
+  const int item = blockIdx.x * 256 + threadIdx.x;
+  if (item >= a.n_items) return;
+  const int d = a.order[item];
+  const int beg = a.doc_ptr[d];
+  const int N = a.doc_ptr[d + 1] - beg;
+  const int K = a.K;
+  const float alpha = a.alpha;
+  double total = 0.0;
+  for (int n = 0; n < N; ++n) total += a.counts[beg + n];
+  float gam[KS], psi[KS], e[KS];
+  const float g0 = alpha + (float)(total / K);
+  const float p0 = digammaf_ldac(g0);
+#pragma unroll
+  for (int k = 0; k < KS; ++k) {
+    gam[k] = k < K ? g0 : 0.f;
+    psi[k] = k < K ? p0 : -INFINITY;
+  }
+  double lik_old = 0.0, L = 0.0, conv = 1.0, dsum_last = 0.0;
+  float m = p0;
+  int it = 0;
+  const bool unbounded = a.var_max_iter < 0;
+  auto compute_e = [&]() {
+    float mx = -INFINITY;
+#pragma unroll
+    for (int k = 0; k < KS; ++k) mx = fmaxf(mx, psi[k]);
+    m = mx;
+#pragma unroll
+    for (int k = 0; k < KS; ++k) e[k] = k < K ? __expf(psi[k] - m) : 0.f;
+  };
+  compute_e();
+  {
+    float sg = 0.f;
+#pragma unroll
+    for (int k = 0; k < KS; ++k) sg += gam[k];
+    dsum_last = digammaf_ldac(sg);
+  }
+  while (conv > (double)a.var_conv && (unbounded || it < a.var_max_iter)) {
+    ++it;
+    float acc[KS];
+#pragma unroll
+    for (int k = 0; k < KS; ++k) acc[k] = 0.f;
+    float lsum = 0.f;
+    for (int n = 0; n < N; ++n) {
+      float row[KS];
+      load_row<KS>(a.beta, a.word_idx[beg + n], row);
+      const float cnt = a.counts[beg + n];
+      float p0_ = 0.f, p1_ = 0.f;
+#pragma unroll
+      for (int k = 0; k < KS; k += 2) {
+        p0_ = fmaf(e[k], row[k], p0_);
+        p1_ = fmaf(e[k + 1], row[k + 1], p1_);
+      }
+      const float P = fmaxf(p0_ + p1_, kPMin);
+      const float r = cnt / P;
+      lsum = fmaf(cnt, __logf(P), lsum);
+#pragma unroll
+      for (int k = 0; k < KS; ++k) acc[k] = fmaf(r, row[k], acc[k]);
+    }
+    float gn[KS];
+    float S = 0.f;
+#pragma unroll
+    for (int k = 0; k < KS; ++k) {
+      gn[k] = k < K ? fmaf(e[k], acc[k], alpha) : 0.f;
+      S += gn[k];
+    }
+    const float dS = digammaf_ldac(S);
+    double term = 0.0;
+#pragma unroll
+    for (int k = 0; k < KS; ++k) {
+      if (k < K) {
+        const float pn = digammaf_ldac(gn[k]);
+        const float y = pn - dS;
+        term += (double)((alpha - 1.f) * y) + (double)lgammaf_fast(gn[k]) - (double)((gn[k] - 1.f) * y) +
+                (double)((gn[k] - alpha) * (pn - psi[k]));
+        psi[k] = pn;
+        gam[k] = gn[k];
+      }
+    }
+    L = a.lik_const - (double)lgammaf_fast(S) + term + ((double)lsum + (double)m * total) - total * (double)dS;
+    conv = (lik_old - L) / lik_old;
+    lik_old = L;
+    dsum_last = dS;
+    const bool cont = conv > (double)a.var_conv && (unbounded || it < a.var_max_iter);
+    if (cont) compute_e();
+  }
+  // outputs (E of the final phi; r_n = c_n / P_n under it)
+  double ass = 0.0;
+#pragma unroll
+  for (int k = 0; k < KS; ++k) {
+    a.gamma[(size_t)d * KS + k] = gam[k];
+    a.e_out[(size_t)d * KS + k] = e[k];
+    if (k < K) ass += (double)psi[k];
+  }
+  for (int n = 0; n < N; ++n) {
+    float row[KS];
+    load_row<KS>(a.beta, a.word_idx[beg + n], row);
+    float P = 0.f;
+#pragma unroll
+    for (int k = 0; k < KS; ++k) P = fmaf(e[k], row[k], P);
+    a.r_out[beg + n] = a.counts[beg + n] / fmaxf(P, kPMin);
+  }
+  a.lik[d] = L;
+  a.alpha_ss[d] = ass - (double)K * dsum_last;
+  a.iters[d] = it;
+}
+
+// ---------------------------------------------------------------------------
 // Host launcher
 // ---------------------------------------------------------------------------
 template <int KS>
@@ -453,6 +572,13 @@ static void launch_ks(const EStepArgs& a, int variant, hipStream_t s) {
       break;
     case kEStepB8:
       hipLaunchKernelGGL((lda_estep_block<KS, 8, (CWS > 2 ? 2 : CWS)>), dim3(a.n_items), dim3(512), 0, s, a);
+      break;
+    case kEStepT1:
+      if constexpr (KS <= 32) {
+        hipLaunchKernelGGL((lda_estep_thread<KS>), dim3((a.n_items + 255) / 256), dim3(256), 0, s, a);
+      } else {
+        throw std::runtime_error("lda_estep: thread-per-document variant needs KS <= 32");
+      }
       break;
     default:
       throw std::runtime_error("lda_estep: unknown variant");

@@ -41,8 +41,8 @@ constexpr int kNT = kNW * 64;
 constexpr long kSpinLimit = 1L << 26;   // ~ seconds of polling, then give up (error flag)
 
 __device__ __forceinline__ void publish_arrive(int* counter) {
-  // caller: the storing wave, after its partial stores
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+  // caller: the storing wave, after its write-through (sc1) partial stores; those
+  // need no release fence (microarch guide, split-K "Equally valid" form): drain, then arrive
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_add(counter, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -66,10 +66,28 @@ __device__ __forceinline__ bool wait_count(int* counter, int target, int* error)
   return ok;
 }
 
+// sum_{q < n} x[q * stride] in order q = 0, 1, ... with 8 loads in flight per
+// round trip; loads are unconditional (clamped index) so hipcc does not branch
+// around each one and wait per element.
+template <typename T>
+__device__ __forceinline__ T ordered_sum(const T* x, int n, int stride) {
+  T s = T(0);
+  for (int q0 = 0; q0 < n; q0 += 8) {
+    T v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = x[(size_t)min(q0 + u, n - 1) * stride];
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      if (q0 + u < n) s += v[u];
+  }
+  return s;
+}
+
 }  // namespace
 
 template <int KS, int CW>
 __global__ __launch_bounds__(kNT) void lda_estep_split(EStepArgs a, SplitArgs s) {
+  load_params(a);
   constexpr int TJ = (KS + 63) / 64;
   __shared__ float4 sE4[KS / 4];
   __shared__ float sRed[kNW][KS];
@@ -185,16 +203,15 @@ __global__ __launch_bounds__(kNT) void lda_estep_split(EStepArgs a, SplitArgs s)
           float v = 0.f;
 #pragma unroll
           for (int w = 0; w < kNW; ++w) v += sRed[w][k];
-          prow[k] = v;
+          __hip_atomic_store(prow + k, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // sc1 write-through
         }
       }
       if (lane == 0) {
         double l = 0.0;
 #pragma unroll
         for (int w = 0; w < kNW; ++w) l += sRedD[w];
-        s.partial_l[(size_t)par * s.n_blocks + b] = l;
+        __hip_atomic_store(s.partial_l + (size_t)par * s.n_blocks + b, l, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       publish_arrive(counter);
       const bool ok = wait_count(counter, nseg * it, s.error);
       // all segments' partials, summed in segment order (bitwise identical in every workgroup)
@@ -206,12 +223,12 @@ __global__ __launch_bounds__(kNT) void lda_estep_split(EStepArgs a, SplitArgs s)
         const int k = lane + 64 * j;
         float ak = 0.f;
         if (k < KS) {
-          for (int q = 0; q < nseg; ++q) ak += s.partial[((size_t)par * s.n_blocks + base + q) * KS + k];
+          ak = ordered_sum(s.partial + ((size_t)par * s.n_blocks + base) * KS + k, nseg, KS);
         }
         gn[j] = (k < K) ? fmaf(e[j], ak, alpha) : 0.f;
         sg += gn[j];
       }
-      for (int q = 0; q < nseg; ++q) lsum_d += s.partial_l[(size_t)par * s.n_blocks + base + q];
+      lsum_d = ordered_sum(s.partial_l + (size_t)par * s.n_blocks + base, nseg, 1);
       const float S = group_sum<64>(sg);
       const float dS = digammaf_ldac(S);
       double term = 0.0;
@@ -221,14 +238,14 @@ __global__ __launch_bounds__(kNT) void lda_estep_split(EStepArgs a, SplitArgs s)
         if (k < K) {
           const float pn = digammaf_ldac(gn[j]);
           const float y = pn - dS;
-          term += (double)((alpha - 1.f) * y) + (double)lgammaf(gn[j]) - (double)((gn[j] - 1.f) * y) +
+          term += (double)((alpha - 1.f) * y) + (double)lgammaf_fast(gn[j]) - (double)((gn[j] - 1.f) * y) +
                   (double)((gn[j] - alpha) * (pn - psi[j]));
           psi[j] = pn;
           gam[j] = gn[j];
         }
       }
       term = group_sum<64>(term);
-      L = a.lik_const - (double)lgammaf(S) + term + (lsum_d + (double)m * total) - total * (double)dS;
+      L = a.lik_const - (double)lgammaf_fast(S) + term + (lsum_d + (double)m * total) - total * (double)dS;
       conv = (lik_old - L) / lik_old;
       lik_old = L;
       dsum_last = dS;

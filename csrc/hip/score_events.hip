@@ -20,13 +20,16 @@ namespace oni {
 
 __device__ __forceinline__ double score_one(const double* __restrict__ theta, const double* __restrict__ phi,
                                             int K, double dflt, int d, int w) {
+  // HIP compiles with -ffp-contract=fast; the JVM rounds the product and the sum separately.
+#pragma clang fp contract(off)
   const double* tr = d >= 0 ? theta + (size_t)d * K : nullptr;
   const double* pr = w >= 0 ? phi + (size_t)w * K : nullptr;
   double s = 0.0;
   for (int k = 0; k < K; ++k) {
     const double tk = tr ? tr[k] : dflt;
     const double pk = pr ? pr[k] : dflt;
-    s = __dadd_rn(s, __dmul_rn(tk, pk));
+    const double prod = tk * pk;  // contract(off): rounded product, then rounded sum
+    s = s + prod;
   }
   return s;
 }

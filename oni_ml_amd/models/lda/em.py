@@ -61,7 +61,7 @@ class _Buckets:
     """Length-bucket plan: (variant, int32 order tensor) launched per E-step."""
 
     def __init__(self, lengths: np.ndarray, ks: int, device, kind: str, doc_ptr: Optional[np.ndarray] = None,
-                 split: bool = True):
+                 split: bool = True, split_min: Optional[int] = None):
         from ...ops import hip as H
         order = np.argsort(-lengths, kind="stable").astype(np.int32)
         L = lengths[order]
@@ -71,15 +71,17 @@ class _Buckets:
             cws = 4 if ks <= 32 else (2 if ks <= 64 else 1)
             if split and doc_ptr is not None:
                 # documents beyond one workgroup's register cache: split over several workgroups
-                huge = order[L > 256 * cws]
+                huge = order[L > max(256 * cws, split_min or 0)]
                 if huge.size:
                     self.split = H.SplitPlan(huge, doc_ptr, ks, device)
                     rest = np.asarray(self.split.leftover, np.int32)
                     keep = ~np.isin(order, huge) | np.isin(order, rest)
                     order, L = order[keep], L[keep]
+            # tiny documents: one thread each while the topic state fits the registers (KS <= 24)
+            tiny = H.ESTEP_T1 if ks <= 24 else H.ESTEP_G16
             edges = [(H.ESTEP_B8, 256 * cws, None), (H.ESTEP_B4, 64 * cws, 256 * cws),
                      (H.ESTEP_G64C, 64, 64 * cws), (H.ESTEP_G64, 32, 64), (H.ESTEP_G32, 16, 32),
-                     (H.ESTEP_G16, 0, 16)]
+                     (tiny, 0, 16)]
             L = np.where(L == 0, 1, L)
         else:
             edges = [(H.SUFF_B8, 2048, None), (H.SUFF_G64, 64, 2048), (H.SUFF_G16, 0, 64)]
@@ -95,7 +97,8 @@ class _Buckets:
 class LDAEngine:
     def __init__(self, corpus: Corpus, num_topics: int, settings: Optional[LDASettings] = None,
                  alpha_init: float = 2.5, backend: str = "auto", device=None, dist=None, seed: int = 0,
-                 streams: int = 3, local_shard: bool = False, split_docs: bool = True):
+                 streams: int = 3, local_shard: bool = False, split_docs: bool = True,
+                 split_min: Optional[int] = 4096, use_graph: bool = True):
         self.settings = settings or LDASettings()
         self.K = int(num_topics)
         self.V = corpus.num_terms
@@ -132,7 +135,7 @@ class LDAEngine:
             self.KS = H.padded_topics(self.K)
             self.dc = DeviceCorpus.build(corpus, self.device)
             self.doc_buckets = _Buckets(self.dc.doc_len, self.KS, self.device, "doc",
-                                        doc_ptr=corpus.doc_ptr, split=split_docs)
+                                        doc_ptr=corpus.doc_ptr, split=split_docs, split_min=split_min)
             self.word_buckets = _Buckets(self.dc.word_len, self.KS, self.device, "word")
             dev, D, V, KS, nnz = self.device, self.D, self.V, self.KS, corpus.nnz
             self.beta = torch.zeros(V, KS, dtype=torch.float32, device=dev)
@@ -143,8 +146,18 @@ class LDAEngine:
             self.lik = torch.zeros(D, dtype=torch.float64, device=dev)
             self.ass = torch.zeros(D, dtype=torch.float64, device=dev)
             self.iters = torch.zeros(D, dtype=torch.int32, device=dev)
-            # flat reduce buffer view: [cw (V*KS) | lik_sum | ass_sum | ndocs]
             self._streams = [torch.cuda.Stream(device=dev) for _ in range(max(0, streams - 1))]
+            self._scalars = torch.zeros(2, dtype=torch.float64, device=dev)
+            self._red_scratch = torch.zeros(H.lib().reduce_scratch_doubles(KS), dtype=torch.float64, device=dev)
+            self._red_scratch2 = torch.zeros(H.lib().reduce_scratch_doubles(2), dtype=torch.float64, device=dev)
+            self._ct_fresh = False
+            self._params = torch.zeros(4, dtype=torch.float64, device=dev)
+            self._params_host = torch.zeros(4, dtype=torch.float64).pin_memory()
+            self._ev_fork = torch.cuda.Event()
+            self._ev_join = [torch.cuda.Event() for _ in range(1 + len(self._streams))]
+            self.use_graph = use_graph
+            self._graph = None
+            self._build_schedule()
         elif backend == "torch":
             dev = self.device
             self.KS = self.K
@@ -205,7 +218,8 @@ class LDAEngine:
         if tuple(cw.shape) != tuple(self.cw.shape):
             raise ValueError(f"checkpoint statistics {cw.shape} != engine {tuple(self.cw.shape)}")
         self.cw.copy_(torch.from_numpy(cw).to(self.cw.device, self.cw.dtype))
-        self.class_total = torch.from_numpy(class_total).to(self.cw.device, torch.float64)
+        # in place: a captured E-step graph holds this buffer's address
+        self.class_total.copy_(torch.from_numpy(class_total).to(self.cw.device, torch.float64))
         self._mstep_beta()
         self.alpha = float(alpha)
 
@@ -255,45 +269,101 @@ class LDAEngine:
         return torch.tensor([res["likelihood"], res["alpha_ss"]], dtype=torch.float64)
 
     def _e_step_hip(self):
+        """One E-step on the GPU.  The launch sequence (all buckets on their streams, suff-stats,
+        reductions) is captured once into a hipGraph and replayed every EM iteration; the
+        per-iteration scalars (alpha, lgamma constant, VAR_MAX_ITER) travel in a device buffer."""
+        p = self._params_host
+        p[0] = self.alpha
+        p[1] = special.lik_const(self.alpha, self.K)
+        p[2] = float(self.var_max_iter)
+        p[3] = float(self.settings.var_converged)
+        self._params.copy_(p, non_blocking=True)
+        if self.use_graph:
+            if self._graph is None:
+                self._launch_estep()          # warm-up (first launches JIT-load code objects)
+                torch.cuda.synchronize(self.device)
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g):
+                    self._launch_estep()
+                self._graph = g
+            self._graph.replay()
+        else:
+            self._launch_estep()
+        self._ct_fresh = True
+        return self._scalars
+
+    def _launch_estep(self):
         from ...ops import hip as H
         dc = self.dc
-        lc = special.lik_const(self.alpha, self.K)
+        prm = self._params
+        a = self.alpha
         main = torch.cuda.current_stream(self.device)
         streams = [main] + self._streams
-        plan = self.doc_buckets.plan
-        # fork: largest buckets on side streams so they overlap the short-doc bulk
-        ev = torch.cuda.Event()
-        ev.record(main)
-        sp = self.doc_buckets.split
-        if sp is not None:  # huge documents first, on their own stream (critical path)
-            s = streams[-1]
+        self._ev_fork.record(main)
+        used = set()
+        # Stream schedule (critical path first): the split-document batches and the long-document
+        # buckets each get a side stream; the short-document bulk shares the main stream.
+        for si, work in enumerate(self._schedule):
+            if not work:
+                continue
+            s = streams[si % len(streams)]
+            used.add(si % len(streams))
             if s is not main:
-                s.wait_event(ev)
+                s.wait_event(self._ev_fork)
             with torch.cuda.stream(s):
-                for batch in sp.batches:
-                    H.lda_estep_split(dc.doc_ptr, dc.word_idx, dc.counts, self.beta, self.K, self.alpha, lc,
-                                      self.var_max_iter, self.settings.var_converged, self.gamma, self.e, self.r,
-                                      self.lik, self.ass, self.iters, batch, sp.seg_words)
-        for i, (var, order) in enumerate(plan):
-            s = streams[i % len(streams)]
-            if s is not main:
-                s.wait_event(ev)
-            with torch.cuda.stream(s):
-                H.lda_estep(dc.doc_ptr, dc.word_idx, dc.counts, order, self.beta, self.K, self.alpha, lc,
-                            self.var_max_iter, self.settings.var_converged, self.gamma, self.e, self.r,
-                            self.lik, self.ass, self.iters, var)
-        for s in streams[1:]:
-            e2 = torch.cuda.Event()
-            e2.record(s)
-            main.wait_event(e2)
-        # sufficient statistics (deterministic CSC gather-reduce)
+                for kind, item in work:
+                    if kind == "split":
+                        sp = self.doc_buckets.split
+                        H.lda_estep_split(dc.doc_ptr, dc.word_idx, dc.counts, self.beta, self.K, a, 0.0, 0, 0.0,
+                                          self.gamma, self.e, self.r, self.lik, self.ass, self.iters, item,
+                                          sp.seg_words, params=prm)
+                    else:
+                        var, order = item
+                        H.lda_estep(dc.doc_ptr, dc.word_idx, dc.counts, order, self.beta, self.K, a, 0.0, 0, 0.0,
+                                    self.gamma, self.e, self.r, self.lik, self.ass, self.iters, var, params=prm)
+        for si in sorted(used):
+            s = streams[si]
+            if s is main:
+                continue
+            self._ev_join[si].record(s)
+            main.wait_event(self._ev_join[si])
+        # sufficient statistics (deterministic CSC gather-reduce) + their per-topic totals
         self.cw.zero_()
         for var, order in self.word_buckets.plan:
             H.lda_suffstats(dc.word_ptr, dc.csc_ent, dc.csc_doc, order, self.e, self.r, self.beta, self.cw, var)
-        return torch.stack([self.lik.sum(), self.ass.sum()])
+        H.colsum(self.cw, self.class_total, self._red_scratch)
+        H.sum2(self.lik, self.ass, self._scalars, self._red_scratch2)
+
+    def _build_schedule(self):
+        """Assign E-step work to streams: [main: short docs], [side 1: split batches], [side 2: B8 + B4], ..."""
+        from ...ops import hip as H
+        nstreams = 1 + len(self._streams)
+        long_vars = (H.ESTEP_B8, H.ESTEP_B4)
+        sched = [[] for _ in range(max(nstreams, 1))]
+        sp = self.doc_buckets.split
+        split_work = [("split", b) for b in sp.batches] if sp is not None else []
+        long_work = [("bucket", (v, o)) for v, o in self.doc_buckets.plan if v in long_vars]
+        short_work = [("bucket", (v, o)) for v, o in self.doc_buckets.plan if v not in long_vars]
+        if nstreams >= 3:
+            sched[1] = split_work
+            sched[2] = long_work
+            sched[0] = short_work
+        elif nstreams == 2:
+            sched[1] = split_work + long_work
+            sched[0] = short_work
+        else:
+            sched[0] = split_work + long_work + short_work
+        self._schedule = sched
 
     def m_step(self, estimate_alpha: bool, alpha_ss: float, num_docs: int):
-        self.class_total = self.cw.sum(0, dtype=torch.float64)
+        if self.backend == "hip":
+            from ...ops import hip as H
+            distributed = self.dist is not None and self.dist.world_size > 1
+            if not self._ct_fresh or distributed:   # class_word was all-reduced: re-total it
+                H.colsum(self.cw, self.class_total, self._red_scratch)
+            self._ct_fresh = False
+        else:
+            self.class_total = self.cw.sum(0, dtype=torch.float64)
         self._mstep_beta()
         if estimate_alpha:
             self.alpha = special.opt_alpha(alpha_ss, num_docs, self.K)

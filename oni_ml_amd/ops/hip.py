@@ -20,7 +20,7 @@ _LIB = None
 _ERR = None
 
 # estep / suffstats variant ids (csrc/hip/kernels.h)
-ESTEP_G16, ESTEP_G32, ESTEP_G64, ESTEP_G64C, ESTEP_B4, ESTEP_B8 = range(6)
+ESTEP_G16, ESTEP_G32, ESTEP_G64, ESTEP_G64C, ESTEP_B4, ESTEP_B8, ESTEP_T1 = range(7)
 SUFF_G16, SUFF_G64, SUFF_B8 = range(3)
 
 
@@ -86,7 +86,9 @@ def _chk(t: torch.Tensor, dtype, name, shape=None, device=None):
 
 
 def lda_estep(doc_ptr, word_idx, counts, order, beta, K, alpha, lik_const, var_max_iter, var_conv,
-              gamma, e_out, r_out, lik, alpha_ss, iters, variant):
+              gamma, e_out, r_out, lik, alpha_ss, iters, variant, params=None):
+    """`params`: optional device f64[4] {alpha, lik_const, var_max_iter, var_conv} overriding the scalars
+    (graph-replayed E-steps)."""
     D = doc_ptr.numel() - 1
     nnz = word_idx.numel()
     V, KS = beta.shape
@@ -109,7 +111,7 @@ def lda_estep(doc_ptr, word_idx, counts, order, beta, K, alpha, lik_const, var_m
         _chk(lik, torch.float64, "lik", (D,), dev),
         _chk(alpha_ss, torch.float64, "alpha_ss", (D,), dev),
         _chk(iters, torch.int32, "iters", (D,), dev),
-        int(variant), _stream(),
+        int(variant), _params_ptr(params, dev), _stream(),
     ]
     if order.numel() == 0:
         return
@@ -161,7 +163,7 @@ class SplitPlan:
 
 
 def lda_estep_split(doc_ptr, word_idx, counts, beta, K, alpha, lik_const, var_max_iter, var_conv, gamma, e_out, r_out,
-                    lik, alpha_ss, iters, batch, seg_words):
+                    lik, alpha_ss, iters, batch, seg_words, params=None):
     D = doc_ptr.numel() - 1
     nnz = word_idx.numel()
     V, KS = beta.shape
@@ -182,7 +184,11 @@ def lda_estep_split(doc_ptr, word_idx, counts, beta, K, alpha, lik_const, var_ma
         _chk(batch["partial"], torch.float32, "partial", (2 * nb * KS,), dev),
         _chk(batch["partial_l"], torch.float64, "partial_l", (2 * nb,), dev),
         _chk(batch["counter"], torch.int32, "counter", None, dev), _chk(batch["error"], torch.int32, "error", (1,), dev),
-        _stream())
+        _params_ptr(params, dev), _stream())
+
+
+def _params_ptr(params, dev) -> int:
+    return 0 if params is None else _chk(params, torch.float64, "params", (4,), dev)
 
 
 def lda_suffstats(word_ptr, csc_ent, csc_doc, order, e, r, beta, cw, variant):
@@ -205,6 +211,31 @@ def lda_suffstats(word_ptr, csc_ent, csc_doc, order, e, r, beta, cw, variant):
     if order.numel() == 0:
         return
     lib().lda_suffstats(*args)
+
+
+def colsum(mat, out, scratch):
+    """out[k] = sum_r mat[r, k] (f32 -> f64, deterministic)."""
+    rows, cols = mat.shape
+    dev = mat.device
+    need = lib().reduce_scratch_doubles(cols)
+    lib().colsum(_chk(mat, torch.float32, "mat", None, dev), int(rows), int(cols),
+                 _chk(out, torch.float64, "out", (cols,), dev),
+                 _chk(scratch, torch.float64, "scratch", None, dev) if scratch.numel() >= need else _bad("scratch"),
+                 _stream())
+
+
+def sum2(a, b, out, scratch):
+    """out = [sum(a), sum(b)] (f64, deterministic)."""
+    n = a.numel()
+    dev = a.device
+    lib().sum2(_chk(a, torch.float64, "a", (n,), dev), _chk(b, torch.float64, "b", (n,), dev), int(n),
+               _chk(out, torch.float64, "out", (2,), dev),
+               _chk(scratch, torch.float64, "scratch", None, dev) if scratch.numel() >= lib().reduce_scratch_doubles(2)
+               else _bad("scratch"), _stream())
+
+
+def _bad(name):
+    raise ValueError(f"{name}: buffer too small")
 
 
 def lda_mstep(cw, class_total, beta, K):

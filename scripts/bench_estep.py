@@ -1,0 +1,102 @@
+#!/usr/bin/env python
+"""Per-bucket timing of the HIP E-step on the synthetic 1-day netflow corpus.
+
+For each length bucket (and each split-document batch) it reports the number of
+documents, their length range, variational iterations (mean / max) and the
+kernel time measured with HIP events (median of repeats, one bucket at a time on
+one stream), plus the suff-stats and M-step kernels and the whole EM step.
+
+  python scripts/bench_estep.py [--events N] [--topics K] [--split-min W ...]
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def timed(fn, reps=5):
+    ts = []
+    for _ in range(reps):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        fn()
+        b.record()
+        b.synchronize()
+        ts.append(a.elapsed_time(b))
+    return float(np.median(ts))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--events", type=int, default=1_000_000)
+    ap.add_argument("--topics", type=int, default=20)
+    ap.add_argument("--split-min", type=int, nargs="*", default=[1024, 4096, 1 << 30])
+    ap.add_argument("--warm-em", type=int, default=3)
+    a = ap.parse_args()
+    from oni_ml_amd.models.lda import special
+    from oni_ml_amd.models.lda.em import LDAEngine
+    from oni_ml_amd.models.lda.settings import LDASettings
+    from oni_ml_amd.ops import hip as H
+    from oni_ml_amd.pipeline.flow import synthetic_flow_corpus
+    c, info = synthetic_flow_corpus(events=a.events, seed=0, device="cuda")
+    lens = c.lengths()
+    print(json.dumps(dict(docs=c.num_docs, nnz=c.nnz, V=c.num_terms, max_len=int(lens.max()),
+                          len_pct={p: int(np.percentile(lens, p)) for p in (50, 90, 99, 99.9)})), flush=True)
+    for smin in a.split_min:
+        eng = LDAEngine(c, a.topics, LDASettings(), backend="hip", seed=0, split_min=smin)
+        eng.init_random()
+        for _ in range(a.warm_em):
+            sc = eng.e_step()
+            host = sc.cpu().tolist()
+            eng.m_step(True, host[1], c.num_docs)
+        torch.cuda.synchronize()
+        dc = eng.dc
+        lc = special.lik_const(eng.alpha, eng.K)
+        it = eng.iters.cpu().numpy()
+        rows = []
+        sp = eng.doc_buckets.split
+        if sp is not None:
+            for bi, batch in enumerate(sp.batches):
+                docs = batch["seg_doc"].cpu().numpy()
+                ud = np.unique(docs)
+                ms = timed(lambda: H.lda_estep_split(dc.doc_ptr, dc.word_idx, dc.counts, eng.beta, eng.K, eng.alpha, lc,
+                                                     eng.var_max_iter, eng.settings.var_converged, eng.gamma, eng.e,
+                                                     eng.r, eng.lik, eng.ass, eng.iters, batch, sp.seg_words))
+                rows.append(dict(bucket=f"split[{bi}]", docs=int(ud.size), blocks=int(batch["n_blocks"]),
+                                 len_min=int(lens[ud].min()), len_max=int(lens[ud].max()),
+                                 it_mean=round(float(it[ud].mean()), 2), it_max=int(it[ud].max()), ms=round(ms, 4)))
+        for var, order in eng.doc_buckets.plan:
+            o = order.cpu().numpy()
+            ms = timed(lambda: H.lda_estep(dc.doc_ptr, dc.word_idx, dc.counts, order, eng.beta, eng.K, eng.alpha, lc,
+                                           eng.var_max_iter, eng.settings.var_converged, eng.gamma, eng.e, eng.r,
+                                           eng.lik, eng.ass, eng.iters, var))
+            rows.append(dict(bucket=["G16", "G32", "G64", "G64C", "B4", "B8", "T1"][var], docs=int(o.size),
+                             len_min=int(lens[o].min()), len_max=int(lens[o].max()),
+                             it_mean=round(float(it[o].mean()), 2), it_max=int(it[o].max()), ms=round(ms, 4)))
+
+        def suff():
+            eng.cw.zero_()
+            for var, order in eng.word_buckets.plan:
+                H.lda_suffstats(dc.word_ptr, dc.csc_ent, dc.csc_doc, order, eng.e, eng.r, eng.beta, eng.cw, var)
+        rows.append(dict(bucket="suffstats", ms=round(timed(suff), 4)))
+        rows.append(dict(bucket="mstep", ms=round(timed(lambda: eng.m_step(False, 0.0, c.num_docs)), 4)))
+
+        def step():
+            sc = eng.e_step()
+            host = sc.cpu().tolist()
+            eng.m_step(True, host[1], c.num_docs)
+        rows.append(dict(bucket="EM step (hipGraph)", ms=round(timed(step, 10), 4), var_max_iter=eng.var_max_iter))
+        eng.use_graph = False
+        rows.append(dict(bucket="EM step (eager launches)", ms=round(timed(step, 10), 4)))
+        eng.use_graph = True
+        print(json.dumps(dict(split_min=smin, rows=rows)), flush=True)
+
+
+if __name__ == "__main__":
+    main()
