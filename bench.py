@@ -2,17 +2,23 @@
 """Headline benchmark: LDA variational-EM throughput on a synthetic 1-day netflow corpus.
 
 Metric (BASELINE.json): "LDA docs/sec to convergence + ml_ops.sh wall-clock, 1-day netflow".
-One step = one full EM iteration of the oni-lda-c algorithm (length-bucketed fused
-E-step to per-doc convergence, deterministic sufficient statistics, RCCL all-reduce
-when N > 1, M-step, alpha Newton).  value = documents processed per second summed
-over all ranks (docs x timed EM iterations / max-over-ranks wall time).
 
-Scaling is weak: every rank holds its own synthetic 1-day netflow corpus (same
-generator, rank-specific seed), i.e. N GPUs model an N-day corpus with per-day
-documents.  Data are synthetic, weights random-init (lda-c "random" start).
+One step = one full EM iteration of the oni-lda-c algorithm: the length-bucketed
+fused E-step run to per-document convergence (hipGraph replay), deterministic
+sufficient statistics, RCCL all-reduce of class_word when N > 1, M-step and
+the alpha Newton step.  value = documents processed per second summed over
+all ranks (docs x timed EM iterations / max-over-ranks wall time).
+
+Scaling is weak: rank r featurizes its own synthetic netflow day (1M events,
+seed r) through the real pipeline (CSV -> C++ ingest -> GPU featurization ->
+corpus), the ranks agree on the union vocabulary, and the N days are trained
+as one N-day corpus with documents sharded by rank.  Weights are random-init
+(lda-c "random" start).  Extras: time to EM convergence from a fresh random
+init, and (N = 1) the wall-clock of the whole ml_ops flow pipeline on the day.
 
   python bench.py --gpus N --steps K --warmup W
   (N > 1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...)
+  CPU rehearsal of the multi-rank path: --device cpu (gloo, torch backend).
 """
 from __future__ import annotations
 
@@ -29,7 +35,6 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 METRIC = "LDA docs/sec to convergence + ml_ops.sh wall-clock, 1-day netflow"
-BASELINE_DOCS_PER_SEC = None  # filled from BASELINE.md once the CPU reference baseline is measured
 
 
 def _baseline():
@@ -42,14 +47,20 @@ def _baseline():
         return None
 
 
-def build_corpus(args, rank, dev=None):
+def build_corpus(args, rank, ctx, dev):
     seed = args.seed + 1000 * rank
     if args.corpus == "planted":
         from oni_ml_amd.synth.corpus import planted_corpus
-        return planted_corpus(num_docs=args.docs, num_terms=args.vocab, num_topics=24, mean_tokens=25,
-                              tail=1.1, max_tokens=300_000, seed=seed), {}
-    from oni_ml_amd.pipeline.flow import synthetic_flow_corpus
-    c, info = synthetic_flow_corpus(events=args.events, seed=seed, device=dev)
+        c = planted_corpus(num_docs=args.docs, num_terms=args.vocab, num_topics=24, mean_tokens=25, tail=1.1,
+                           max_tokens=300_000, seed=seed)
+        names = [str(i) for i in range(c.num_terms)]
+        info = {}
+    else:
+        from oni_ml_amd.pipeline.flow import synthetic_flow_corpus
+        c, info, names = synthetic_flow_corpus(events=args.events, seed=seed, device=dev, return_names=True)
+    if ctx.world_size > 1:
+        from oni_ml_amd.pipeline.flow import unify_vocabulary
+        c, _ = unify_vocabulary(ctx, c, names)
     return c, info
 
 
@@ -62,18 +73,26 @@ def _e2e(args, dev):
     from oni_ml_amd.synth.flow import generate_flow_day
     tmp = tempfile.mkdtemp(prefix="oni_e2e_")
     try:
+        t0 = time.perf_counter()
         generate_flow_day(os.path.join(tmp, "in/"), events=args.events, seed=args.seed + 7)
+        t_gen = time.perf_counter() - t0
         cfg = CFG.resolve("20160122", "flow", tol=1e-20, conf_path=None, environ={}, lpath=os.path.join(tmp, "ml"),
-                          flow_path=os.path.join(tmp, "in"), backend="hip", topics=args.topics, verbose=False)
-        torch.cuda.synchronize()
+                          flow_path=os.path.join(tmp, "in"), backend=args.backend, topics=args.topics, verbose=False)
+        _sync(dev)
         t0 = time.perf_counter()
         s = run(cfg, device=dev, log=lambda *a, **k: None)
-        torch.cuda.synchronize()
+        _sync(dev)
         wall = time.perf_counter() - t0
-        return dict(e2e_wall_s=round(wall, 3), e2e_stage_s={k: round(v, 3) for k, v in s["stage_seconds"].items()},
+        return dict(e2e_wall_s=round(wall, 3), e2e_synth_input_s=round(t_gen, 3),
+                    e2e_stage_s={k: round(v, 3) for k, v in s["stage_seconds"].items()},
                     e2e_em_iters=s["lda"]["em_iterations"], e2e_flagged=s.get("scored"), e2e_corpus=s.get("corpus"))
     finally:
         shutil.rmtree(tmp, ignore_errors=True)
+
+
+def _sync(dev):
+    if torch.device(dev).type == "cuda":
+        torch.cuda.synchronize()
 
 
 def main():
@@ -89,22 +108,25 @@ def main():
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--converge", type=int, default=1, help="also time a full random-init run to convergence")
     ap.add_argument("--e2e", type=int, default=1, help="N=1: also time the whole ml_ops flow pipeline on the day")
+    ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"], help="cpu: gloo/torch rehearsal")
     args = ap.parse_args()
+    args.backend = "hip" if args.device == "cuda" else "torch"
 
     from oni_ml_amd.parallel import dist as D
-    ctx = D.init_from_env(expected_world=args.gpus)
+    ctx = D.init_from_env(expected_world=args.gpus, backend=None if args.device == "cuda" else "gloo")
     rank, world = ctx.rank, ctx.world_size
-    dev = ctx.device
+    dev = ctx.device if args.device == "cuda" else torch.device("cpu")
 
     from oni_ml_amd.models.lda.em import LDAEngine
     from oni_ml_amd.models.lda.settings import LDASettings
 
     t0 = time.perf_counter()
-    corpus, info = build_corpus(args, rank, dev)
+    corpus, info = build_corpus(args, rank, ctx, dev)
     t_corpus = time.perf_counter() - t0
-    # weak scaling: each rank's corpus is its own shard
-    eng = LDAEngine(corpus, args.topics, LDASettings(), backend="hip", device=dev,
-                    dist=ctx if world > 1 else None, seed=args.seed, local_shard=True)
+    dist = ctx if world > 1 else None
+    # weak scaling: each rank's corpus is its own document shard of the N-day corpus
+    eng = LDAEngine(corpus, args.topics, LDASettings(), backend=args.backend, device=dev, dist=dist, seed=args.seed,
+                    local_shard=True)
     eng.init_random()
     docs_global = ctx.allreduce_int(corpus.num_docs)
 
@@ -119,28 +141,29 @@ def main():
     for _ in range(args.warmup):
         step()
     ctx.barrier()
-    torch.cuda.synchronize()
+    _sync(dev)
     t1 = time.perf_counter()
     for _ in range(args.steps):
-        lik = step()
-    torch.cuda.synchronize()
+        step()
+    _sync(dev)
     ctx.barrier()
     dt = time.perf_counter() - t1
     dt = ctx.allreduce_max(dt)
     ms = dt / args.steps * 1e3
     value = docs_global * args.steps / dt
+    it = eng.iters.cpu().numpy()
 
-    extra = {}
+    extra = dict(var_iter_mean=round(float(it.mean()), 3), var_iter_max=int(it.max()), var_max_iter=eng.var_max_iter)
     if args.converge:
-        eng2 = LDAEngine(corpus, args.topics, LDASettings(), backend="hip", device=dev,
-                         dist=ctx if world > 1 else None, seed=args.seed + 1, local_shard=True)
+        eng2 = LDAEngine(corpus, args.topics, LDASettings(), backend=args.backend, device=dev, dist=dist,
+                         seed=args.seed + 1, local_shard=True)
         ctx.barrier()
-        torch.cuda.synchronize()
+        _sync(dev)
         t2 = time.perf_counter()
         res = eng2.run()
-        torch.cuda.synchronize()
+        _sync(dev)
         tc = ctx.allreduce_max(time.perf_counter() - t2)
-        extra = dict(converge_seconds=round(tc, 4), converge_em_iters=res.em_iterations,
+        extra.update(converge_seconds=round(tc, 4), converge_em_iters=res.em_iterations,
                      converge_docs_per_sec=round(docs_global * res.em_iterations / tc, 1),
                      final_likelihood=res.likelihoods[-1][0])
     if args.e2e and world == 1 and args.corpus == "flow":
@@ -158,8 +181,8 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": (round(value / base, 2) if base else None),
-            "dtype": "fp32 E-step / fp64 likelihood+alpha (reference lda-c: fp64)",
-            "data": "synthetic (1-day netflow per GPU, random-init topics)",
+            "dtype": "fp32 E-step / fp64 likelihood, alpha, sufficient-statistic totals (reference lda-c: fp64)",
+            "data": "synthetic (1-day netflow per GPU through the real featurizer, random-init topics)",
             "config": {
                 "model": f"oni-lda-c variational EM LDA, K={args.topics}",
                 "global_batch": docs_global,
@@ -171,6 +194,7 @@ def main():
                 "vocab": corpus.num_terms,
                 "nnz_per_gpu": corpus.nnz,
                 "max_doc_len": int(corpus.lengths().max()),
+                "device": args.device,
             },
             "corpus_build_s": round(t_corpus, 3),
             **info,

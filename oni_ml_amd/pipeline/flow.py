@@ -171,10 +171,10 @@ def score_flow(cfg, ft: FF.FlowTable, tables: C.ModelTables, device, log=print) 
 
 
 def synthetic_flow_corpus(events: int = 1_000_000, seed: int = 0, workdir: Optional[str] = None, device=None,
-                          strict: bool = True, threads: int = 8):
+                          strict: bool = True, threads: int = 8, return_names: bool = False):
     """Synthetic netflow day -> featurized -> lda-c corpus (the bench / test input path).
 
-    Returns (Corpus, info dict with stage timings)."""
+    Returns (Corpus, info dict with stage timings[, word names])."""
     import tempfile
     import time
     from ..synth.flow import generate_flow_day
@@ -197,4 +197,28 @@ def synthetic_flow_corpus(events: int = 1_000_000, seed: int = 0, workdir: Optio
         import shutil
         shutil.rmtree(tmp, ignore_errors=True)
     info = dict(events=events, synth_s=round(t1 - t0, 3), ingest_s=round(t2 - t1, 3), featurize_corpus_s=round(t3 - t2, 3))
+    if return_names:
+        return built.corpus, info, ws.decode(built.word_keys)
     return built.corpus, info
+
+
+def unify_vocabulary(ctx, corpus, word_names):
+    """Map a rank-local corpus onto the union vocabulary of all ranks (sorted word strings).
+
+    Data-parallel EM all-reduces class_word [V, K]: every rank must index the
+    same words the same way.  Ranks that featurize different days (weak-scaling
+    bench, multi-day runs) see different word sets; their union, ordered by the
+    word string, is the shared dictionary."""
+    from ..corpus.csr import Corpus
+    names = list(word_names)
+    if ctx is not None and ctx.initialized:
+        import torch.distributed as td
+        gathered = [None] * ctx.world_size
+        td.all_gather_object(gathered, names)
+    else:
+        gathered = [names]
+    vocab = sorted(set().union(*[set(g) for g in gathered]))
+    index = {w: i for i, w in enumerate(vocab)}
+    remap = np.fromiter((index[w] for w in names), dtype=np.int32, count=len(names))
+    c = Corpus(corpus.doc_ptr, remap[corpus.word_idx], corpus.counts, len(vocab), meta=dict(corpus.meta))
+    return c, vocab

@@ -76,3 +76,18 @@ def test_two_rank_em_matches_single_rank(tmp_path):
     # per-rank gamma blocks concatenate to final.gamma (README.md:121)
     parts = np.concatenate([np.atleast_2d(np.loadtxt(tmp_path / "w2" / f"{r}.gamma")) for r in range(2)])
     assert np.allclose(parts, g2, atol=1e-9)
+
+
+def test_bench_two_rank_cpu_rehearsal():
+    """bench.py's multi-rank path (vocabulary union, sharded EM, max-over-ranks timing) on gloo."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "bench.py", "--gpus", "2",
+                        "--steps", "1", "--warmup", "1", "--events", "5000", "--device", "cpu", "--converge", "0"],
+                       cwd=root, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    assert out["n_gpus"] == 2 and out["config"]["parallelism"] == "dp2" and out["value"] > 0
