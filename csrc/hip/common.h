@@ -77,21 +77,75 @@ __device__ __forceinline__ double digamma_ldac(double x) {
 // Wavefront / group reductions.  G must be a power of two <= 64; all lanes of
 // the group must be active (callers keep loop conditions group-uniform).
 // ---------------------------------------------------------------------------
-template <int G, typename T>
-__device__ __forceinline__ T group_sum(T x) {
-#pragma unroll
-  for (int o = G / 2; o > 0; o >>= 1) x += __shfl_xor(x, o, G);
+//
+// Within a 16-lane row the exchanges are DPP modifiers on the VALU op itself
+// (quad_perm xor1 / xor2, row_half_mirror, row_mirror: no LDS crossbar), the
+// 32-lane step is one ds_swizzle (xor 16), the 64-lane step two v_readlane.
+// Every step combines a lane with its partner commutatively, so all lanes of
+// a group finish with bitwise the same total (the kernels rely on that:
+// replicated topic state must not diverge between lanes).
+
+namespace detail {
+template <int CTRL>
+__device__ __forceinline__ int dpp(int x) {
+  return __builtin_amdgcn_update_dpp(0, x, CTRL, 0xF, 0xF, true);
+}
+constexpr int kQuadXor1 = 0xB1;   // quad_perm [1,0,3,2]
+constexpr int kQuadXor2 = 0x4E;   // quad_perm [2,3,0,1]
+constexpr int kRowHalfMirror = 0x141;
+constexpr int kRowMirror = 0x140;
+constexpr int kSwzXor16 = 0x401F; // ds_swizzle bitmask mode: and 0x1f, or 0, xor 0x10
+
+template <int CTRL>
+__device__ __forceinline__ float xchg(float x) { return __int_as_float(dpp<CTRL>(__float_as_int(x))); }
+template <int CTRL>
+__device__ __forceinline__ double xchg(double x) {
+  const long long b = __double_as_longlong(x);
+  const int lo = dpp<CTRL>((int)(b & 0xffffffffLL)), hi = dpp<CTRL>((int)(b >> 32));
+  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+__device__ __forceinline__ float swz16(float x) {
+  return __int_as_float(__builtin_amdgcn_ds_swizzle(__float_as_int(x), kSwzXor16));
+}
+__device__ __forceinline__ double swz16(double x) {
+  const long long b = __double_as_longlong(x);
+  const int lo = __builtin_amdgcn_ds_swizzle((int)(b & 0xffffffffLL), kSwzXor16);
+  const int hi = __builtin_amdgcn_ds_swizzle((int)(b >> 32), kSwzXor16);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+__device__ __forceinline__ float rdlane(float x, int l) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(x), l)); }
+__device__ __forceinline__ double rdlane(double x, int l) {
+  const long long b = __double_as_longlong(x);
+  const int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffffLL), l), hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+template <typename T>
+__device__ __forceinline__ T add(T a, T b) { return a + b; }
+template <typename T>
+__device__ __forceinline__ T mx(T a, T b) { return a > b ? a : b; }
+}  // namespace detail
+
+template <int G, typename T, typename Op>
+__device__ __forceinline__ T group_reduce(T x, Op op) {
+  static_assert(G == 16 || G == 32 || G == 64, "group size must be 16, 32 or 64");
+  using namespace detail;
+  x = op(x, xchg<kQuadXor1>(x));
+  x = op(x, xchg<kQuadXor2>(x));
+  x = op(x, xchg<kRowHalfMirror>(x));
+  x = op(x, xchg<kRowMirror>(x));
+  if constexpr (G >= 32) x = op(x, swz16(x));
+  if constexpr (G == 64) x = op(rdlane(x, 0), rdlane(x, 32));
   return x;
 }
 
 template <int G, typename T>
+__device__ __forceinline__ T group_sum(T x) {
+  return group_reduce<G>(x, [](T a, T b) { return a + b; });
+}
+
+template <int G, typename T>
 __device__ __forceinline__ T group_max(T x) {
-#pragma unroll
-  for (int o = G / 2; o > 0; o >>= 1) {
-    T y = __shfl_xor(x, o, G);
-    x = x > y ? x : y;
-  }
-  return x;
+  return group_reduce<G>(x, [](T a, T b) { return a > b ? a : b; });
 }
 
 // Wave-level LDS hand-off between lanes of ONE wavefront: orders the
@@ -103,15 +157,12 @@ __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// Multi-value butterfly: reduces v[0..N) over the G lanes of a group and
-// leaves the total of value i in EVERY lane's v[i].  N*log2(G) shuffles.
+// Multi-value all-reduce: the total of value i over the G lanes of a group in
+// EVERY lane's v[i] (N independent DPP chains: good ILP, no LDS traffic).
 template <int G, int N>
 __device__ __forceinline__ void group_sum_vec(float (&v)[N]) {
 #pragma unroll
-  for (int o = G / 2; o > 0; o >>= 1) {
-#pragma unroll
-    for (int i = 0; i < N; ++i) v[i] += __shfl_xor(v[i], o, G);
-  }
+  for (int i = 0; i < N; ++i) v[i] = group_sum<G>(v[i]);
 }
 
 // Bijective XCD-aware remap of a 1-D grid (cdna_hip_programming.md §5 T1):

@@ -165,7 +165,8 @@ def init_from_env(expected_world: int = None, backend: str = None, timeout_s: fl
     if expected_world is not None and expected_world != world and world != 1:
         raise RuntimeError(f"--gpus {expected_world} but WORLD_SIZE={world}")
     if backend is None:
-        backend = "nccl" if torch.cuda.is_available() else "gloo"
+        # ONI_DIST_BACKEND=gloo rehearses several ranks on one GPU (RCCL needs one GPU per rank)
+        backend = os.environ.get("ONI_DIST_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
     if torch.cuda.is_available() and backend == "nccl":
         torch.cuda.set_device(local)
         dev = torch.device("cuda", local)
