@@ -131,12 +131,10 @@ def main():
     docs_global = ctx.allreduce_int(corpus.num_docs)
 
     def step():
-        sc = eng.e_step()
-        if world > 1:
-            sc = ctx.allreduce_suffstats(eng.cw, sc)
-        host = sc.cpu().tolist()
-        eng.m_step(True, float(host[1]), docs_global)
-        return host[0]
+        # E-step graph -> (RCCL all-reduce of class_word + scalars when N > 1) -> M-step graph with the
+        # alpha Newton on the device; one host read-back of (likelihood, alpha_ss, alpha)
+        lik, _ = eng.em_iteration(True, docs_global)
+        return lik
 
     for _ in range(args.warmup):
         step()

@@ -92,6 +92,11 @@ PYBIND11_MODULE(_onihip, m) {
     oni::launch_sum2(P<const double>(a), P<const double>(b), n, P<double>(out), P<double>(scratch), S(stream));
   });
 
+  m.def("alpha_newton", [](u scalars, double num_docs, int K, bool estimate, u params, u alpha_out, u stream) {
+    oni::launch_alpha_newton(P<const double>(scalars), num_docs, K, estimate, P<double>(params), P<double>(alpha_out),
+                             S(stream));
+  });
+
   m.def("lda_mstep", [](u cw, u class_total, u beta, int V, int K, int KS, u stream) {
     oni::launch_lda_mstep(P<const float>(cw), P<const double>(class_total), P<float>(beta), V, K, KS,
                           S(stream));

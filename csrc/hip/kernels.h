@@ -91,6 +91,11 @@ void launch_lda_suffstats(const SuffArgs& a, int variant, int KS, hipStream_t s)
 void launch_lda_mstep(const float* cw, const double* class_total, float* beta, int V, int K, int KS,
                       hipStream_t s);
 
+// alpha Newton on the device: reads scalars[1] (alpha_ss), writes params[0..1]
+// (alpha, lgamma(K alpha) - K lgamma(alpha)) and alpha_out[0].
+void launch_alpha_newton(const double* scalars, double num_docs, int K, bool estimate, double* params,
+                         double* alpha_out, hipStream_t s);
+
 // ------------------------------------------------------------- reductions ---
 // Deterministic two-pass reductions (reduce.hip).  scratch holds
 // reduce_scratch_doubles(cols) doubles.

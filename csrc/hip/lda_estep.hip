@@ -231,6 +231,9 @@ __global__ __launch_bounds__(256) void lda_estep_group(EStepArgs a) {
 template <int KS, int NW, int CW>
 __global__ __launch_bounds__(NW * 64) void lda_estep_block(EStepArgs a) {
   load_params(a);
+  // long documents are the EM step's critical path: win SIMD issue arbitration
+  // against the short-document waves that share the CU (microarch guide, s_setprio)
+  __builtin_amdgcn_s_setprio(2);
   constexpr int NT = NW * 64;
   constexpr int TJ = (KS + 63) / 64;  // topics per lane of wave 0
   __shared__ float4 sE4[KS / 4];

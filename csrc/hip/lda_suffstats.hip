@@ -134,6 +134,61 @@ __global__ __launch_bounds__(256) void lda_mstep_kernel(const float* __restrict_
   }
 }
 
+// ------------------------------------------------------- alpha on device ---
+// lda-c opt_alpha (lda-alpha.c): Newton on log(alpha) for
+//   alhood(a) = D (lnG(K a) - K lnG(a)) + (a - 1) ss
+// started at 100, x10 restart on NaN, |df| <= 1e-5 or 1000 iterations, in
+// double exactly as the host version (models/lda/special.py).  One thread;
+// it reads alpha_ss from the E-step's reduction output and writes the next
+// E-step's {alpha, lgamma(K a) - K lgamma(a)} into the device parameter block,
+// so an EM iteration needs no host round trip besides the likelihood read-back.
+__device__ double trigamma_ldac(double x) {
+  x = x + 6.0;
+  double p = 1.0 / (x * x);
+  p = (((((0.075757575757576 * p - 0.033333333333333) * p + 0.0238095238095238) * p - 0.033333333333333) * p +
+        0.166666666666667) * p + 1) / x + 0.5 * p;
+  for (int i = 0; i < 6; ++i) {
+    x = x - 1.0;
+    p = 1.0 / (x * x) + p;
+  }
+  return p;
+}
+
+__global__ void alpha_newton_kernel(const double* __restrict__ scalars, double num_docs, int K, int estimate,
+                                    double* __restrict__ params, double* __restrict__ alpha_out) {
+  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  double a = params[0];
+  if (estimate) {
+    const double ss = scalars[1];
+    const double D = num_docs;
+    double init_a = 100.0, log_a = log(init_a), df;
+    int iter = 0;
+    do {
+      ++iter;
+      a = exp(log_a);
+      if (isnan(a)) {
+        init_a = init_a * 10.0;
+        a = init_a;
+        log_a = log(a);
+      }
+      df = D * (K * digamma_ldac(K * a) - K * digamma_ldac(a)) + ss;
+      const double d2f = D * (K * K * trigamma_ldac(K * a) - K * trigamma_ldac(a));
+      log_a = log_a - df / (d2f * a + df);
+    } while (fabs(df) > 1e-5 && iter < 1000);
+    a = exp(log_a);
+  }
+  params[0] = a;
+  params[1] = lgamma(a * K) - K * lgamma(a);
+  alpha_out[0] = a;
+}
+
+void launch_alpha_newton(const double* scalars, double num_docs, int K, bool estimate, double* params,
+                         double* alpha_out, hipStream_t s) {
+  hipLaunchKernelGGL(alpha_newton_kernel, dim3(1), dim3(64), 0, s, scalars, num_docs, K, estimate ? 1 : 0, params,
+                     alpha_out);
+  ONI_HIP_CHECK(hipGetLastError());
+}
+
 void launch_lda_mstep(const float* cw, const double* class_total, float* beta, int V, int K, int KS,
                       hipStream_t s) {
   const int64_t total = (int64_t)V * KS;

@@ -107,6 +107,7 @@ class LDAEngine:
         self.dist = dist
         self.seed = seed
         self.var_max_iter = self.settings.var_max_iter
+        self.collect_iter_stats = False
         if backend == "auto":
             from ...ops import hip as H
             backend = "hip" if H.available() else "torch"
@@ -157,6 +158,11 @@ class LDAEngine:
             self._ev_join = [torch.cuda.Event() for _ in range(1 + len(self._streams))]
             self.use_graph = use_graph
             self._graph = None
+            self._mgraph, self._mgraph_key = None, None
+            self._alpha_dev = torch.zeros(1, dtype=torch.float64, device=dev)
+            self._out_host = torch.zeros(3, dtype=torch.float64).pin_memory()
+            self._out_ev = torch.cuda.Event()
+            self._pushed = None
             self._build_schedule()
         elif backend == "torch":
             dev = self.device
@@ -278,17 +284,13 @@ class LDAEngine:
         p[2] = float(self.var_max_iter)
         p[3] = float(self.settings.var_converged)
         self._params.copy_(p, non_blocking=True)
-        if self.use_graph:
-            if self._graph is None:
-                self._launch_estep()          # warm-up (first launches JIT-load code objects)
-                torch.cuda.synchronize(self.device)
-                g = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g):
-                    self._launch_estep()
-                self._graph = g
+        if self.use_graph and self._graph is None:
+            self._capture_estep()             # its warm-up launch is this call's E-step
+        elif self.use_graph:
             self._graph.replay()
         else:
             self._launch_estep()
+        self._pushed = None                   # params now hold host values; em_iteration re-checks
         self._ct_fresh = True
         return self._scalars
 
@@ -303,7 +305,11 @@ class LDAEngine:
         used = set()
         # Stream schedule (critical path first): the split-document batches and the long-document
         # buckets each get a side stream; the short-document bulk shares the main stream.
-        for si, work in enumerate(self._schedule):
+        # side streams first: the long-document kernels (the critical path) are dispatched before the
+        # short-document bulk floods the CUs
+        order = list(range(1, len(self._schedule))) + [0]
+        for si in order:
+            work = self._schedule[si]
             if not work:
                 continue
             s = streams[si % len(streams)]
@@ -331,8 +337,70 @@ class LDAEngine:
         self.cw.zero_()
         for var, order in self.word_buckets.plan:
             H.lda_suffstats(dc.word_ptr, dc.csc_ent, dc.csc_doc, order, self.e, self.r, self.beta, self.cw, var)
-        H.colsum(self.cw, self.class_total, self._red_scratch)
         H.sum2(self.lik, self.ass, self._scalars, self._red_scratch2)
+
+    def _launch_mstep(self, estimate_alpha: bool, num_docs: int):
+        """M-step on the device: class totals, beta, alpha Newton (lda-c opt_alpha) -> next E-step params."""
+        from ...ops import hip as H
+        H.colsum(self.cw, self.class_total, self._red_scratch)
+        H.lda_mstep(self.cw, self.class_total, self.beta, self.K)
+        H.alpha_newton(self._scalars, num_docs, self.K, estimate_alpha, self._params, self._alpha_dev)
+
+    def em_iteration(self, estimate_alpha: bool, num_docs: int):
+        """One device-resident EM iteration (hip backend): E-step graph -> [RCCL all-reduce] -> M-step graph.
+
+        alpha and the lgamma constant never leave the device between iterations; the host reads back
+        (likelihood, alpha_ss, alpha) once, for the convergence test.  Returns (likelihood, alpha_ss)."""
+        if self.backend != "hip":
+            sc = self.e_step()
+            if self.dist is not None and self.dist.world_size > 1:
+                sc = self.dist.allreduce_suffstats(self.cw, sc)
+            host = sc.cpu().tolist()
+            self.m_step(estimate_alpha, float(host[1]), num_docs)
+            return float(host[0]), float(host[1])
+        p = self._params_host
+        if self._pushed != (self.alpha, self.var_max_iter):   # host changed alpha / VAR_MAX_ITER
+            p[0] = self.alpha
+            p[1] = special.lik_const(self.alpha, self.K)
+            p[2] = float(self.var_max_iter)
+            p[3] = float(self.settings.var_converged)
+            self._params.copy_(p, non_blocking=True)
+        if self.use_graph and self._graph is None:
+            self._capture_estep()             # its warm-up launch is this iteration's E-step
+        elif self.use_graph:
+            self._graph.replay()
+        else:
+            self._launch_estep()
+        if self.dist is not None and self.dist.world_size > 1:
+            self.dist.allreduce_suffstats(self.cw, self._scalars)
+        key = (bool(estimate_alpha), int(num_docs))
+        if self.use_graph:
+            if self._mgraph_key != key:
+                self._launch_mstep(*key)                       # warm-up, then capture
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g):
+                    self._launch_mstep(*key)
+                self._mgraph, self._mgraph_key = g, key
+            else:
+                self._mgraph.replay()
+        else:
+            self._launch_mstep(*key)
+        self._out_host[0:2].copy_(self._scalars, non_blocking=True)
+        self._out_host[2:3].copy_(self._alpha_dev, non_blocking=True)
+        self._out_ev.record()
+        self._out_ev.synchronize()
+        lik, ass, alpha = self._out_host.tolist()
+        self.alpha = alpha
+        self._pushed = (self.alpha, self.var_max_iter)
+        return lik, ass
+
+    def _capture_estep(self):
+        self._launch_estep()                  # warm-up (first launches load code objects)
+        torch.cuda.synchronize(self.device)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            self._launch_estep()
+        self._graph = g
 
     def _build_schedule(self):
         """Assign E-step work to streams: [main: short docs], [side 1: split batches], [side 2: B8 + B4], ..."""
@@ -358,10 +426,7 @@ class LDAEngine:
     def m_step(self, estimate_alpha: bool, alpha_ss: float, num_docs: int):
         if self.backend == "hip":
             from ...ops import hip as H
-            distributed = self.dist is not None and self.dist.world_size > 1
-            if not self._ct_fresh or distributed:   # class_word was all-reduced: re-total it
-                H.colsum(self.cw, self.class_total, self._red_scratch)
-            self._ct_fresh = False
+            H.colsum(self.cw, self.class_total, self._red_scratch)
         else:
             self.class_total = self.cw.sum(0, dtype=torch.float64)
         self._mstep_beta()
@@ -413,28 +478,20 @@ class LDAEngine:
             i += 1
             ti = time.perf_counter()
             range_push(f"em_iter_{i}")
-            range_push("e_step")
-            sc = self.e_step()
-            range_pop()
-            if self.dist is not None and self.dist.world_size > 1:
-                range_push("allreduce")
-                sc = self.dist.allreduce_suffstats(self.cw, sc)
-                range_pop()
-            range_push("m_step")
-            host = sc.cpu().tolist()
-            lik, ass = float(host[0]), float(host[1])
-            self.m_step(st.estimate_alpha, ass, n_docs_global)
-            range_pop()
+            lik, ass = self.em_iteration(st.estimate_alpha, n_docs_global)
             range_pop()
             conv = (L_old - lik) / L_old if L_old != 0 else (math.inf if lik < 0 else (-math.inf if lik > 0 else math.nan))
             if conv < 0:
                 self.var_max_iter = self.var_max_iter * 2
             L_old = lik
             hist.append((lik, conv))
-            it_np = self.iters.cpu().numpy() if isinstance(self.iters, torch.Tensor) else np.asarray(self.iters)
-            stt = EMIterStats(i, lik, conv, self.alpha, time.perf_counter() - ti,
-                              float(it_np.mean()) if it_np.size else 0.0, int(it_np.max()) if it_np.size else 0,
-                              self.var_max_iter)
+            if verbose or self.collect_iter_stats:   # an extra D2H copy per iteration: opt-in
+                it_np = self.iters.cpu().numpy() if isinstance(self.iters, torch.Tensor) else np.asarray(self.iters)
+                it_mean = float(it_np.mean()) if it_np.size else 0.0
+                it_max = int(it_np.max()) if it_np.size else 0
+            else:
+                it_mean, it_max = -1.0, -1
+            stt = EMIterStats(i, lik, conv, self.alpha, time.perf_counter() - ti, it_mean, it_max, self.var_max_iter)
             stats.append(stt)
             if verbose:
                 print(f"**** em iteration {i} **** L={lik:.6f} conv={conv:.5e} alpha={self.alpha:.5f} "

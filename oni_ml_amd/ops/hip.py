@@ -213,6 +213,14 @@ def lda_suffstats(word_ptr, csc_ent, csc_doc, order, e, r, beta, cw, variant):
     lib().lda_suffstats(*args)
 
 
+def alpha_newton(scalars, num_docs, K, estimate, params, alpha_out):
+    """Device lda-c opt_alpha: params[0:2] <- (alpha, lgamma(K alpha) - K lgamma(alpha))."""
+    dev = params.device
+    lib().alpha_newton(_chk(scalars, torch.float64, "scalars", (2,), dev), float(num_docs), int(K), bool(estimate),
+                       _chk(params, torch.float64, "params", (4,), dev),
+                       _chk(alpha_out, torch.float64, "alpha_out", (1,), dev), _stream())
+
+
 def colsum(mat, out, scratch):
     """out[k] = sum_r mat[r, k] (f32 -> f64, deterministic)."""
     rows, cols = mat.shape
