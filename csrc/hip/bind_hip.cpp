@@ -59,6 +59,7 @@ PYBIND11_MODULE(_onihip, m) {
 
   m.def("split_segment_words", [](int KS) { return oni::split_segment_words(KS); });
   m.def("split_max_blocks", []() { return oni::kSplitMaxBlocks; });
+  m.def("block_words", [](int KS, int waves) { return oni::block_words(KS, waves); });
   m.def(
       "lda_estep_split",
       [](u doc_ptr, u word_idx, u counts, u beta, int K, int KS, float alpha, double lik_const, int var_max_iter,

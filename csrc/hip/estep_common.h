@@ -37,6 +37,12 @@ __device__ __forceinline__ float dot_lds(const float* sE, const float (&row)[KS]
 
 constexpr float kPMin = 1e-30f;
 
+// Beta rows each lane keeps in VGPRs across the variational iterations:
+// 4-wave kernels (G64C, B4) and 8-wave kernels (B8, split segments; 2 waves per
+// SIMD leave ~256 VGPRs per lane, so up to 8 rows of 20 topics fit).
+constexpr int rows_per_lane_4w(int KS) { return KS <= 32 ? 4 : (KS <= 64 ? 2 : 1); }
+constexpr int rows_per_lane_8w(int KS) { return KS <= 20 ? 6 : (KS <= 32 ? 3 : 1); }
+
 // Per-launch scalars from device memory when the launch is graph-replayed.
 template <typename Args>
 __device__ __forceinline__ void load_params(Args& a) {

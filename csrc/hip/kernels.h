@@ -28,7 +28,7 @@ enum EStepVariant : int {
 // per-document arrival counter, and each workgroup then runs the identical
 // (deterministic) topic update.  All workgroups of one launch must be
 // co-resident: the host caps a launch at kSplitMaxBlocks workgroups.
-constexpr int kSplitMaxBlocks = 256;
+constexpr int kSplitMaxBlocks = 192;   // 8-wave workgroups, ~1 per CU: keep a margin below 256 CUs
 struct SplitArgs {
   const int* seg_doc;     // [n_blocks] document of each workgroup
   const int* seg_index;   // [n_blocks] segment number within its document
@@ -69,6 +69,7 @@ struct EStepArgs {
 void launch_lda_estep(const EStepArgs& a, int variant, int KS, hipStream_t s);
 void launch_lda_estep_split(const EStepArgs& a, const SplitArgs& s, int KS, hipStream_t st);
 int split_segment_words(int KS);   // words one split workgroup keeps in registers
+int block_words(int KS, int waves); // register-cached words of a 4- or 8-wave document workgroup
 
 // ------------------------------------------------------------ suff stats ---
 enum SuffVariant : int { kSuffG16 = 0, kSuffG64 = 1, kSuffB8 = 2 };

@@ -556,7 +556,8 @@ __global__ __launch_bounds__(256) void lda_estep_thread(EStepArgs a) {
 template <int KS>
 static void launch_ks(const EStepArgs& a, int variant, hipStream_t s) {
   if (a.n_items <= 0) return;
-  constexpr int CWS = KS <= 32 ? 4 : (KS <= 64 ? 2 : 1);
+  constexpr int CWS = rows_per_lane_4w(KS);
+  constexpr int CW8 = rows_per_lane_8w(KS);
   switch (variant) {
     case kEStepG16:
       hipLaunchKernelGGL((lda_estep_group<KS, 16, 1>), dim3((a.n_items + 15) / 16), dim3(256), 0, s, a);
@@ -574,7 +575,7 @@ static void launch_ks(const EStepArgs& a, int variant, hipStream_t s) {
       hipLaunchKernelGGL((lda_estep_block<KS, 4, CWS>), dim3(a.n_items), dim3(256), 0, s, a);
       break;
     case kEStepB8:
-      hipLaunchKernelGGL((lda_estep_block<KS, 8, (CWS > 2 ? 2 : CWS)>), dim3(a.n_items), dim3(512), 0, s, a);
+      hipLaunchKernelGGL((lda_estep_block<KS, 8, CW8>), dim3(a.n_items), dim3(512), 0, s, a);
       break;
     case kEStepT1:
       if constexpr (KS <= 32) {

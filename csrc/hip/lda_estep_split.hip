@@ -36,7 +36,7 @@ namespace oni {
 
 namespace {
 
-constexpr int kNW = 4;
+constexpr int kNW = 8;      // 8 waves x rows_per_lane_8w rows: 4096 words per segment at K <= 20
 constexpr int kNT = kNW * 64;
 constexpr long kSpinLimit = 1L << 26;   // ~ seconds of polling, then give up (error flag)
 
@@ -296,7 +296,7 @@ __global__ __launch_bounds__(kNT) void lda_estep_split(EStepArgs a, SplitArgs s)
 
 template <int KS>
 static void split_ks(const EStepArgs& a, const SplitArgs& s, hipStream_t st) {
-  constexpr int CW = KS <= 32 ? 4 : (KS <= 64 ? 2 : 1);
+  constexpr int CW = rows_per_lane_8w(KS);
   if (s.n_blocks <= 0) return;
   if (s.n_blocks > kSplitMaxBlocks) throw std::runtime_error("lda_estep_split: too many workgroups in one launch");
   if (s.seg_words > kNT * CW) throw std::runtime_error("lda_estep_split: segment larger than the register cache");
@@ -304,7 +304,8 @@ static void split_ks(const EStepArgs& a, const SplitArgs& s, hipStream_t st) {
   ONI_HIP_CHECK(hipGetLastError());
 }
 
-int split_segment_words(int KS) { return kNT * (KS <= 32 ? 4 : (KS <= 64 ? 2 : 1)); }
+int split_segment_words(int KS) { return kNT * rows_per_lane_8w(KS); }
+int block_words(int KS, int waves) { return waves * 64 * (waves == 8 ? rows_per_lane_8w(KS) : rows_per_lane_4w(KS)); }
 
 void launch_lda_estep_split(const EStepArgs& a, const SplitArgs& s, int KS, hipStream_t st) {
   switch (KS) {

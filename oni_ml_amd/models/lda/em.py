@@ -69,9 +69,11 @@ class _Buckets:
         self.split = None
         if kind == "doc":
             cws = 4 if ks <= 32 else (2 if ks <= 64 else 1)
+            b4_words = H.lib().block_words(ks, 4)       # 4-wave workgroup, all words in registers
+            b8_words = H.lib().block_words(ks, 8)       # 8-wave workgroup, all words in registers
             if split and doc_ptr is not None:
                 # documents beyond one workgroup's register cache: split over several workgroups
-                huge = order[L > max(256 * cws, split_min or 0)]
+                huge = order[L > max(b8_words, split_min or 0)]
                 if huge.size:
                     self.split = H.SplitPlan(huge, doc_ptr, ks, device)
                     rest = np.asarray(self.split.leftover, np.int32)
@@ -79,7 +81,7 @@ class _Buckets:
                     order, L = order[keep], L[keep]
             # tiny documents: one thread each while the topic state fits the registers (KS <= 24)
             tiny = H.ESTEP_T1 if ks <= 24 else H.ESTEP_G16
-            edges = [(H.ESTEP_B8, 256 * cws, None), (H.ESTEP_B4, 64 * cws, 256 * cws),
+            edges = [(H.ESTEP_B8, b4_words, None), (H.ESTEP_B4, 64 * cws, b4_words),
                      (H.ESTEP_G64C, 64, 64 * cws), (H.ESTEP_G64, 32, 64), (H.ESTEP_G32, 16, 32),
                      (tiny, 0, 16)]
             L = np.where(L == 0, 1, L)
