@@ -131,7 +131,7 @@ def build_native(verbose=False, jobs=8) -> Path:
     cxx = os.environ.get("CXX", "g++")
     out = LIB / ("_oninative" + _ext_suffix())
     hdrs = sorted((CSRC / "native").glob("*.h"))
-    srcs = [s for s in sorted((CSRC / "native").glob("*.cpp")) if s.name not in ("lda_main.cpp",)]
+    srcs = [s for s in sorted((CSRC / "native").glob("*.cpp")) if s.name not in ("lda_main.cpp", "selftest.cpp")]
     bind = CSRC / "native" / "bind_native.cpp"
     if not bind.exists():
         return None
@@ -163,6 +163,26 @@ def build_native(verbose=False, jobs=8) -> Path:
             _run(cmd, verbose)
             _stamp(exe, digest)
     return out
+
+
+def build_sanitized(kind: str = "thread", verbose=False) -> Path:
+    """Native self-test executable under a host sanitizer (thread | address).
+
+    GPU sanitizers are not available on this pool, so race / memory checking
+    covers the multithreaded C++ runtime; the HIP kernels get
+    their checks from host-side shape/index validation before every launch."""
+    cxx = os.environ.get("CXX", "g++")
+    san = {"thread": ["-fsanitize=thread"], "address": ["-fsanitize=address,undefined"]}[kind]
+    outdir = ROOT / "build" / f"san_{kind}"
+    outdir.mkdir(parents=True, exist_ok=True)
+    srcs = [CSRC / "native" / f for f in ("table.cpp", "dns.cpp", "lda_ref.cpp", "selftest.cpp")]
+    exe = outdir / "native_selftest"
+    flags = ["-O1", "-g", "-fno-omit-frame-pointer", "-std=c++17", "-pthread", f"-I{CSRC / 'native'}"] + san
+    digest = _hash(srcs + sorted((CSRC / "native").glob("*.h")), flags)
+    if _stale(exe, digest):
+        _run([cxx] + flags + [str(s) for s in srcs] + ["-o", str(exe)], verbose)
+        _stamp(exe, digest)
+    return exe
 
 
 def build_all(verbose=False, hip=True, native=True):
