@@ -106,6 +106,7 @@ def main():
     ap.add_argument("--docs", type=int, default=80_000)
     ap.add_argument("--vocab", type=int, default=8_000)
     ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--streams", type=int, default=4, help="HIP streams for the E-step buckets")
     ap.add_argument("--converge", type=int, default=1, help="also time a full random-init run to convergence")
     ap.add_argument("--e2e", type=int, default=1, help="N=1: also time the whole ml_ops flow pipeline on the day")
     ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"], help="cpu: gloo/torch rehearsal")
@@ -126,7 +127,7 @@ def main():
     dist = ctx if world > 1 else None
     # weak scaling: each rank's corpus is its own document shard of the N-day corpus
     eng = LDAEngine(corpus, args.topics, LDASettings(), backend=args.backend, device=dev, dist=dist, seed=args.seed,
-                    local_shard=True)
+                    local_shard=True, streams=args.streams)
     eng.init_random()
     docs_global = ctx.allreduce_int(corpus.num_docs)
 

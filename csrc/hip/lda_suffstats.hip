@@ -30,6 +30,42 @@ __device__ __forceinline__ void axpy_row(const float* __restrict__ e, int d, flo
   }
 }
 
+// acc += sum over this lane's CSC entries i = beg, beg + STRIDE, ... of r_i * E[doc_i].
+// Four entries are in flight per lane (index loads, then the r / E-row gathers,
+// then the FMAs): the gather chain is latency-bound, not bandwidth-bound.
+template <int KS, int STRIDE>
+__device__ __forceinline__ void gather_axpy(const SuffArgs& a, int i, int end, float (&acc)[KS]) {
+  constexpr int U = KS <= 32 ? 4 : (KS <= 64 ? 2 : 1);   // registers: U rows of KS in flight
+  for (; i + (U - 1) * STRIDE < end; i += U * STRIDE) {
+    int d[U], ent[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      d[u] = a.csc_doc[i + u * STRIDE];
+      ent[u] = a.csc_ent[i + u * STRIDE];
+    }
+    float r[U];
+    float4 v[U][KS / 4];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      r[u] = a.r[ent[u]];
+      const float4* p = reinterpret_cast<const float4*>(a.e + (size_t)d[u] * KS);
+#pragma unroll
+      for (int j = 0; j < KS / 4; ++j) v[u][j] = p[j];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+#pragma unroll
+      for (int j = 0; j < KS / 4; ++j) {
+        acc[4 * j + 0] = fmaf(r[u], v[u][j].x, acc[4 * j + 0]);
+        acc[4 * j + 1] = fmaf(r[u], v[u][j].y, acc[4 * j + 1]);
+        acc[4 * j + 2] = fmaf(r[u], v[u][j].z, acc[4 * j + 2]);
+        acc[4 * j + 3] = fmaf(r[u], v[u][j].w, acc[4 * j + 3]);
+      }
+    }
+  }
+  for (; i < end; i += STRIDE) axpy_row<KS>(a.e, a.csc_doc[i], a.r[a.csc_ent[i]], acc);
+}
+
 template <int KS>
 __device__ __forceinline__ void store_cw(const SuffArgs& a, int w, const float (&acc)[KS]) {
   const float4* b = reinterpret_cast<const float4*>(a.beta + (size_t)w * KS);
@@ -53,7 +89,7 @@ __global__ __launch_bounds__(256) void lda_suff_group(SuffArgs a) {
   float acc[KS];
 #pragma unroll
   for (int k = 0; k < KS; ++k) acc[k] = 0.f;
-  for (int i = beg + t; i < end; i += G) axpy_row<KS>(a.e, a.csc_doc[i], a.r[a.csc_ent[i]], acc);
+  gather_axpy<KS, G>(a, beg + t, end, acc);
   group_sum_vec<G, KS>(acc);
   if (t == 0) store_cw<KS>(a, w, acc);
 }
@@ -67,7 +103,7 @@ __global__ __launch_bounds__(NW * 64) void lda_suff_block(SuffArgs a) {
   float acc[KS];
 #pragma unroll
   for (int k = 0; k < KS; ++k) acc[k] = 0.f;
-  for (int i = beg + t; i < end; i += NW * 64) axpy_row<KS>(a.e, a.csc_doc[i], a.r[a.csc_ent[i]], acc);
+  gather_axpy<KS, NW * 64>(a, beg + t, end, acc);
   group_sum_vec<64, KS>(acc);
   if (lane == 0) {
 #pragma unroll

@@ -86,11 +86,10 @@ class _Buckets:
                      (tiny, 0, 16)]
             L = np.where(L == 0, 1, L)
         else:
-            edges = [(H.SUFF_B8, 2048, None), (H.SUFF_G64, 64, 2048), (H.SUFF_G16, 0, 64)]
+            # every word gets a row (empty words write zeros), so class_word needs no clearing
+            edges = [(H.SUFF_B8, 1024, None), (H.SUFF_G64, 64, 1024), (H.SUFF_G16, -1, 64)]
         for var, lo, hi in edges:
             m = (L > lo) if hi is None else ((L > lo) & (L <= hi))
-            if kind == "word" and var == H.SUFF_G16:
-                m = (L > 0) & (L <= 64)
             if m.any():
                 plan.append((var, torch.from_numpy(order[m].copy()).to(device)))
         self.plan = plan
@@ -99,7 +98,7 @@ class _Buckets:
 class LDAEngine:
     def __init__(self, corpus: Corpus, num_topics: int, settings: Optional[LDASettings] = None,
                  alpha_init: float = 2.5, backend: str = "auto", device=None, dist=None, seed: int = 0,
-                 streams: int = 3, local_shard: bool = False, split_docs: bool = True,
+                 streams: int = 4, local_shard: bool = False, split_docs: bool = True,
                  split_min: Optional[int] = 4096, use_graph: bool = True):
         self.settings = settings or LDASettings()
         self.K = int(num_topics)
@@ -150,7 +149,7 @@ class LDAEngine:
             self.ass = torch.zeros(D, dtype=torch.float64, device=dev)
             self.iters = torch.zeros(D, dtype=torch.int32, device=dev)
             self._streams = [torch.cuda.Stream(device=dev) for _ in range(max(0, streams - 1))]
-            self._scalars = torch.zeros(2, dtype=torch.float64, device=dev)
+            self._scalars = torch.zeros(3, dtype=torch.float64, device=dev)   # likelihood, alpha_ss, alpha
             self._red_scratch = torch.zeros(H.lib().reduce_scratch_doubles(KS), dtype=torch.float64, device=dev)
             self._red_scratch2 = torch.zeros(H.lib().reduce_scratch_doubles(2), dtype=torch.float64, device=dev)
             self._ct_fresh = False
@@ -161,7 +160,9 @@ class LDAEngine:
             self.use_graph = use_graph
             self._graph = None
             self._mgraph, self._mgraph_key = None, None
-            self._alpha_dev = torch.zeros(1, dtype=torch.float64, device=dev)
+            self._fgraph, self._fgraph_key = None, None
+            self._ev_red = torch.cuda.Event()
+            self._ev_side = torch.cuda.Event()
             self._out_host = torch.zeros(3, dtype=torch.float64).pin_memory()
             self._out_ev = torch.cuda.Event()
             self._pushed = None
@@ -294,9 +295,13 @@ class LDAEngine:
             self._launch_estep()
         self._pushed = None                   # params now hold host values; em_iteration re-checks
         self._ct_fresh = True
-        return self._scalars
+        return self._scalars[:2]
 
-    def _launch_estep(self):
+    def _launch_estep(self, newton_key=None):
+        """Enqueue one E-step: document buckets on their streams, then suff-stats (main stream) and
+        the likelihood / alpha_ss reduction (side stream).  With ``newton_key`` = (estimate_alpha,
+        num_docs) the M-step follows in the same launch sequence (single-rank fused EM iteration):
+        alpha Newton on the side stream right after the reduction, beta on the main stream."""
         from ...ops import hip as H
         dc = self.dc
         prm = self._params
@@ -305,8 +310,6 @@ class LDAEngine:
         streams = [main] + self._streams
         self._ev_fork.record(main)
         used = set()
-        # Stream schedule (critical path first): the split-document batches and the long-document
-        # buckets each get a side stream; the short-document bulk shares the main stream.
         # side streams first: the long-document kernels (the critical path) are dispatched before the
         # short-document bulk floods the CUs
         order = list(range(1, len(self._schedule))) + [0]
@@ -335,22 +338,59 @@ class LDAEngine:
                 continue
             self._ev_join[si].record(s)
             main.wait_event(self._ev_join[si])
-        # sufficient statistics (deterministic CSC gather-reduce) + their per-topic totals
-        self.cw.zero_()
+        side = self._streams[0] if self._streams else None
+        if side is not None:
+            # the scalar reduction (and the alpha Newton) overlap the suff-stats gather
+            self._ev_red.record(main)
+            side.wait_event(self._ev_red)
+            with torch.cuda.stream(side):
+                self._launch_scalars(newton_key)
+        else:
+            self._launch_scalars(newton_key)
+        # sufficient statistics: deterministic CSC gather-reduce; every word row is written
+        # (empty words included), so cw needs no clearing
         for var, order in self.word_buckets.plan:
             H.lda_suffstats(dc.word_ptr, dc.csc_ent, dc.csc_doc, order, self.e, self.r, self.beta, self.cw, var)
-        H.sum2(self.lik, self.ass, self._scalars, self._red_scratch2)
+        if newton_key is not None:
+            self._launch_beta()
+        if side is not None:
+            self._ev_side.record(side)
+            main.wait_event(self._ev_side)
 
-    def _launch_mstep(self, estimate_alpha: bool, num_docs: int):
-        """M-step on the device: class totals, beta, alpha Newton (lda-c opt_alpha) -> next E-step params."""
+    def _launch_scalars(self, newton_key):
+        from ...ops import hip as H
+        H.sum2(self.lik, self.ass, self._scalars[:2], self._red_scratch2)
+        if newton_key is not None:
+            H.alpha_newton(self._scalars[:2], newton_key[1], self.K, newton_key[0], self._params, self._scalars[2:3])
+
+    def _launch_beta(self):
         from ...ops import hip as H
         H.colsum(self.cw, self.class_total, self._red_scratch)
         H.lda_mstep(self.cw, self.class_total, self.beta, self.K)
-        H.alpha_newton(self._scalars, num_docs, self.K, estimate_alpha, self._params, self._alpha_dev)
+
+    def _launch_mstep(self, estimate_alpha: bool, num_docs: int):
+        """M-step on the device after the cross-rank all-reduce: class totals + beta (main stream)
+        alongside the alpha Newton (side stream) -> next E-step params."""
+        from ...ops import hip as H
+        main = torch.cuda.current_stream(self.device)
+        side = self._streams[0] if self._streams else None
+        if side is None:
+            self._launch_beta()
+            H.alpha_newton(self._scalars[:2], num_docs, self.K, estimate_alpha, self._params, self._scalars[2:3])
+            return
+        self._ev_red.record(main)
+        side.wait_event(self._ev_red)
+        with torch.cuda.stream(side):
+            H.alpha_newton(self._scalars[:2], num_docs, self.K, estimate_alpha, self._params, self._scalars[2:3])
+        self._launch_beta()
+        self._ev_side.record(side)
+        main.wait_event(self._ev_side)
 
     def em_iteration(self, estimate_alpha: bool, num_docs: int):
-        """One device-resident EM iteration (hip backend): E-step graph -> [RCCL all-reduce] -> M-step graph.
+        """One device-resident EM iteration (hip backend).
 
+        Single rank: one hipGraph holds the whole iteration (E-step, suff-stats, M-step, alpha).
+        Several ranks: E-step graph -> RCCL all-reduce of (class_word, scalars) -> M-step graph.
         alpha and the lgamma constant never leave the device between iterations; the host reads back
         (likelihood, alpha_ss, alpha) once, for the convergence test.  Returns (likelihood, alpha_ss)."""
         if self.backend != "hip":
@@ -367,28 +407,32 @@ class LDAEngine:
             p[2] = float(self.var_max_iter)
             p[3] = float(self.settings.var_converged)
             self._params.copy_(p, non_blocking=True)
-        if self.use_graph and self._graph is None:
-            self._capture_estep()             # its warm-up launch is this iteration's E-step
-        elif self.use_graph:
-            self._graph.replay()
-        else:
-            self._launch_estep()
-        if self.dist is not None and self.dist.world_size > 1:
-            self.dist.allreduce_suffstats(self.cw, self._scalars)
         key = (bool(estimate_alpha), int(num_docs))
-        if self.use_graph:
-            if self._mgraph_key != key:
-                self._launch_mstep(*key)                       # warm-up, then capture
-                g = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g):
-                    self._launch_mstep(*key)
-                self._mgraph, self._mgraph_key = g, key
+        distributed = self.dist is not None and self.dist.world_size > 1
+        if not distributed:
+            if not self.use_graph:
+                self._launch_estep(newton_key=key)
+            elif self._fgraph_key != key:
+                self._fgraph = self._capture(lambda: self._launch_estep(newton_key=key))
+                self._fgraph_key = key
+            else:
+                self._fgraph.replay()
+        else:
+            if self.use_graph and self._graph is None:
+                self._capture_estep()             # its warm-up launch is this iteration's E-step
+            elif self.use_graph:
+                self._graph.replay()
+            else:
+                self._launch_estep()
+            self.dist.allreduce_suffstats(self.cw, self._scalars)
+            if not self.use_graph:
+                self._launch_mstep(*key)
+            elif self._mgraph_key != key:
+                self._mgraph = self._capture(lambda: self._launch_mstep(*key))
+                self._mgraph_key = key
             else:
                 self._mgraph.replay()
-        else:
-            self._launch_mstep(*key)
-        self._out_host[0:2].copy_(self._scalars, non_blocking=True)
-        self._out_host[2:3].copy_(self._alpha_dev, non_blocking=True)
+        self._out_host.copy_(self._scalars, non_blocking=True)
         self._out_ev.record()
         self._out_ev.synchronize()
         lik, ass, alpha = self._out_host.tolist()
@@ -396,33 +440,41 @@ class LDAEngine:
         self._pushed = (self.alpha, self.var_max_iter)
         return lik, ass
 
-    def _capture_estep(self):
-        self._launch_estep()                  # warm-up (first launches load code objects)
+    def _capture(self, launch):
+        """Run ``launch`` once (this call's real work; first launches also load code objects),
+        then capture the same launch sequence into a graph for the following iterations."""
+        launch()
         torch.cuda.synchronize(self.device)
         g = torch.cuda.CUDAGraph()
         with torch.cuda.graph(g):
-            self._launch_estep()
-        self._graph = g
+            launch()
+        return g
+
+    def _capture_estep(self):
+        self._graph = self._capture(self._launch_estep)
 
     def _build_schedule(self):
-        """Assign E-step work to streams: [main: short docs], [side 1: split batches], [side 2: B8 + B4], ..."""
+        """Assign E-step work to streams (critical path first): [side 1: split batches],
+        [side 2: B8 + B4], [side 3: G64C/G64/G32], [main: thread-per-document bulk]."""
         from ...ops import hip as H
         nstreams = 1 + len(self._streams)
         long_vars = (H.ESTEP_B8, H.ESTEP_B4)
+        tiny_vars = (H.ESTEP_T1, H.ESTEP_G16)
         sched = [[] for _ in range(max(nstreams, 1))]
         sp = self.doc_buckets.split
         split_work = [("split", b) for b in sp.batches] if sp is not None else []
-        long_work = [("bucket", (v, o)) for v, o in self.doc_buckets.plan if v in long_vars]
-        short_work = [("bucket", (v, o)) for v, o in self.doc_buckets.plan if v not in long_vars]
-        if nstreams >= 3:
-            sched[1] = split_work
-            sched[2] = long_work
-            sched[0] = short_work
+        plan = self.doc_buckets.plan
+        long_work = [("bucket", (v, o)) for v, o in plan if v in long_vars]
+        mid_work = [("bucket", (v, o)) for v, o in plan if v not in long_vars and v not in tiny_vars]
+        tiny_work = [("bucket", (v, o)) for v, o in plan if v in tiny_vars]
+        if nstreams >= 4:
+            sched[1], sched[2], sched[3], sched[0] = split_work, long_work, mid_work, tiny_work
+        elif nstreams == 3:
+            sched[1], sched[2], sched[0] = split_work, long_work, mid_work + tiny_work
         elif nstreams == 2:
-            sched[1] = split_work + long_work
-            sched[0] = short_work
+            sched[1], sched[0] = split_work + long_work, mid_work + tiny_work
         else:
-            sched[0] = split_work + long_work + short_work
+            sched[0] = split_work + long_work + mid_work + tiny_work
         self._schedule = sched
 
     def m_step(self, estimate_alpha: bool, alpha_ss: float, num_docs: int):

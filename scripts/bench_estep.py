@@ -38,6 +38,7 @@ def main():
     ap.add_argument("--topics", type=int, default=20)
     ap.add_argument("--split-min", type=int, nargs="*", default=[1024, 4096, 1 << 30])
     ap.add_argument("--warm-em", type=int, default=3)
+    ap.add_argument("--streams", type=int, nargs="+", default=[4], help="E-step stream counts to compare")
     a = ap.parse_args()
     from oni_ml_amd.models.lda import special
     from oni_ml_amd.models.lda.em import LDAEngine
@@ -49,7 +50,7 @@ def main():
     print(json.dumps(dict(docs=c.num_docs, nnz=c.nnz, V=c.num_terms, max_len=int(lens.max()),
                           len_pct={p: int(np.percentile(lens, p)) for p in (50, 90, 99, 99.9)})), flush=True)
     for smin in a.split_min:
-        eng = LDAEngine(c, a.topics, LDASettings(), backend="hip", seed=0, split_min=smin)
+        eng = LDAEngine(c, a.topics, LDASettings(), backend="hip", seed=0, split_min=smin, streams=a.streams[0])
         eng.init_random()
         for _ in range(a.warm_em):
             sc = eng.e_step()
@@ -81,17 +82,23 @@ def main():
                              it_mean=round(float(it[o].mean()), 2), it_max=int(it[o].max()), ms=round(ms, 4)))
 
         def suff():
-            eng.cw.zero_()
             for var, order in eng.word_buckets.plan:
                 H.lda_suffstats(dc.word_ptr, dc.csc_ent, dc.csc_doc, order, eng.e, eng.r, eng.beta, eng.cw, var)
         rows.append(dict(bucket="suffstats", ms=round(timed(suff), 4)))
         rows.append(dict(bucket="mstep", ms=round(timed(lambda: eng.m_step(False, 0.0, c.num_docs)), 4)))
 
         def step():
-            sc = eng.e_step()
-            host = sc.cpu().tolist()
-            eng.m_step(True, host[1], c.num_docs)
-        rows.append(dict(bucket="EM step (hipGraph)", ms=round(timed(step, 10), 4), var_max_iter=eng.var_max_iter))
+            eng.em_iteration(True, c.num_docs)
+        rows.append(dict(bucket="EM step (hipGraph)", ms=round(timed(step, 10), 4), var_max_iter=eng.var_max_iter,
+                         streams=a.streams[0]))
+        for ns in a.streams[1:]:
+            e2 = LDAEngine(c, a.topics, LDASettings(), backend="hip", seed=0, split_min=smin, streams=ns)
+            e2.init_random()
+            for _ in range(a.warm_em):
+                e2.em_iteration(True, c.num_docs)
+            rows.append(dict(bucket="EM step (hipGraph)", streams=ns,
+                             ms=round(timed(lambda: e2.em_iteration(True, c.num_docs), 10), 4)))
+            del e2
         eng.use_graph = False
         rows.append(dict(bucket="EM step (eager launches)", ms=round(timed(step, 10), 4)))
         eng.use_graph = True
