@@ -62,6 +62,27 @@ __device__ __forceinline__ float lgammaf_fast(float x) {
   return (xs - 0.5f) * __logf(xs) - xs + 0.918938533204673f + ser - __logf(p) - __logf(q);
 }
 
+// psi(x) and lnGamma(x) together, x > 0, in the shift-by-6 forms above.  The
+// six reciprocals 1/(x+i), i < 6, collapse into two: sum_{i<3} 1/(x+i) = A'/A
+// with A = x(x+1)(x+2) (likewise B over x+3..x+5), and log A, log B, log(x+6),
+// 1/(x+6) are shared with lnGamma: 3 v_rcp + 3 v_log instead of 8 + 4.
+// A, B stay finite for x < 6e12 (gamma values are bounded by document counts).
+__device__ __forceinline__ void digamma_lgamma(float x, float& psi, float& lg) {
+  const float xs = x + 6.0f;
+  const float ix = frcp(xs);
+  const float z = ix * ix;
+  const float x1 = x + 1.0f, x2 = x + 2.0f, x3 = x + 3.0f, x4 = x + 4.0f, x5 = x + 5.0f;
+  const float A = x * x1 * x2, dA = fmaf(x, x1 + x2, x1 * x2);
+  const float B = x3 * x4 * x5, dB = fmaf(x3, x4 + x5, x4 * x5);
+  const float lxs = __logf(xs), lA = __logf(A), lB = __logf(B);
+  const float pser = (((0.004166666666667f * z - 0.003968253986254f) * z + 0.008333333333333f) * z -
+                      0.083333333333333f) * z;
+  psi = pser + lxs - 0.5f * ix - dA * frcp(A) - dB * frcp(B);
+  const float lser = (((-0.000595238095238f * z + 0.000793650793651f) * z - 0.002777777777778f) * z +
+                      0.083333333333333f) * ix;
+  lg = (xs - 0.5f) * lxs - xs + 0.918938533204673f + lser - lA - lB;
+}
+
 __device__ __forceinline__ double digamma_ldac(double x) {
   double p;
   x = x + 6.0;

@@ -39,7 +39,9 @@ struct SplitArgs {
   int seg_words;          // words per segment
   float* partial;         // [2][n_blocks][KS]  partial accumulators (parity double-buffer)
   double* partial_l;      // [2][n_blocks]      partial sum_n c_n log P_n
-  int* counter;           // [n_docs_in_launch] arrival counters, zeroed before the launch
+  int* counter;           // [2][n_docs] arrival / exit counts; zero before the first launch, and the
+                          // kernel leaves them zero again (the last workgroup of a document resets them)
+  int n_docs;             // documents in this launch
   int* error;             // set to 1 if a barrier wait times out (never hangs the GPU)
 };
 

@@ -157,22 +157,23 @@ __global__ __launch_bounds__(256) void lda_estep_group(EStepArgs a) {
       sg += gn[j];
     }
     const float S = group_sum<G>(sg);
-    const float dS = digammaf_ldac(S);
+    float dS, lgS;
+    digamma_lgamma(S, dS, lgS);
     double term = 0.0;
 #pragma unroll
     for (int j = 0; j < TJ; ++j) {
       const int k = t + G * j;
       if (k < K) {
-        const float pn = digammaf_ldac(gn[j]);
-        const float y = pn - dS;
-        term += (double)((alpha - 1.f) * y) + (double)lgammaf_fast(gn[j]) - (double)((gn[j] - 1.f) * y) +
-                (double)((gn[j] - alpha) * (pn - psi[j]));
+        float pn, lg;
+        digamma_lgamma(gn[j], pn, lg);
+        // (a-1)Y + lnG(g') - (g'-1)Y + (g'-a)(psi(g') - psi(g)) with Y = psi(g') - psi(S')
+        term += (double)lg + (double)((gn[j] - alpha) * (dS - psi[j]));
         psi[j] = pn;
         gam[j] = gn[j];
       }
     }
     term = group_sum<G>(term);
-    L = a.lik_const - (double)lgammaf_fast(S) + term + (lsum_d + (double)m * total) - total * (double)dS;
+    L = a.lik_const - (double)lgS + term + (lsum_d + (double)m * total) - total * (double)dS;
     conv = (lik_old - L) / lik_old;
     lik_old = L;
     dsum_last = dS;
@@ -365,22 +366,23 @@ __global__ __launch_bounds__(NW * 64) void lda_estep_block(EStepArgs a) {
         sg += gn[j];
       }
       const float S = group_sum<64>(sg);
-      const float dS = digammaf_ldac(S);
+      float dS, lgS;
+      digamma_lgamma(S, dS, lgS);
       double term = 0.0;
 #pragma unroll
       for (int j = 0; j < TJ; ++j) {
         const int k = lane + 64 * j;
         if (k < K) {
-          const float pn = digammaf_ldac(gn[j]);
-          const float y = pn - dS;
-          term += (double)((alpha - 1.f) * y) + (double)lgammaf_fast(gn[j]) - (double)((gn[j] - 1.f) * y) +
-                  (double)((gn[j] - alpha) * (pn - psi[j]));
+          float pn, lg;
+          digamma_lgamma(gn[j], pn, lg);
+          // (a-1)Y + lnG(g') - (g'-1)Y + (g'-a)(psi(g') - psi(g)) with Y = psi(g') - psi(S')
+          term += (double)lg + (double)((gn[j] - alpha) * (dS - psi[j]));
           psi[j] = pn;
           gam[j] = gn[j];
         }
       }
       term = group_sum<64>(term);
-      L = a.lik_const - (double)lgammaf_fast(S) + term + (lsum_d + (double)m * total) - total * (double)dS;
+      L = a.lik_const - (double)lgS + term + (lsum_d + (double)m * total) - total * (double)dS;
       conv = (lik_old - L) / lik_old;
       lik_old = L;
       dsum_last = dS;
@@ -443,6 +445,10 @@ __global__ __launch_bounds__(NW * 64) void lda_estep_block(EStepArgs a) {
 // ---------------------------------------------------------------------------
 template <int KS>
 __global__ __launch_bounds__(256) void lda_estep_thread(EStepArgs a) {
+  // The first TC beta rows stay in VGPRs across the variational iterations (the
+  // median document has 2 words, so most threads never touch memory in the loop);
+  // further words are fetched two rows at a time so their loads overlap.
+  constexpr int TC = KS <= 12 ? 4 : (KS <= 20 ? 3 : 1);
   load_params(a);
   const int item = blockIdx.x * 256 + threadIdx.x;
   if (item >= a.n_items) return;
@@ -451,8 +457,21 @@ __global__ __launch_bounds__(256) void lda_estep_thread(EStepArgs a) {
   const int N = a.doc_ptr[d + 1] - beg;
   const int K = a.K;
   const float alpha = a.alpha;
+  float bc[TC][KS], cc[TC];
   double total = 0.0;
-  for (int n = 0; n < N; ++n) total += a.counts[beg + n];
+#pragma unroll
+  for (int c = 0; c < TC; ++c) {
+    if (c < N) {
+      cc[c] = a.counts[beg + c];
+      load_row<KS>(a.beta, a.word_idx[beg + c], bc[c]);
+    } else {
+      cc[c] = 0.f;
+#pragma unroll
+      for (int k = 0; k < KS; ++k) bc[c][k] = 0.f;
+    }
+    total += cc[c];
+  }
+  for (int n = TC; n < N; ++n) total += a.counts[beg + n];
   float gam[KS], psi[KS], e[KS];
   const float g0 = alpha + (float)(total / K);
   const float p0 = digammaf_ldac(g0);
@@ -486,10 +505,9 @@ __global__ __launch_bounds__(256) void lda_estep_thread(EStepArgs a) {
 #pragma unroll
     for (int k = 0; k < KS; ++k) acc[k] = 0.f;
     float lsum = 0.f;
-    for (int n = 0; n < N; ++n) {
-      float row[KS];
-      load_row<KS>(a.beta, a.word_idx[beg + n], row);
-      const float cnt = a.counts[beg + n];
+    // one word: P = E . beta_w, r = c / P, acc += r beta_w.  r_n is written every
+    // iteration; the last write is r under the final E (no reload pass at the end).
+    auto word = [&](const float (&row)[KS], float cnt, int n) {
       float p0_ = 0.f, p1_ = 0.f;
 #pragma unroll
       for (int k = 0; k < KS; k += 2) {
@@ -501,6 +519,20 @@ __global__ __launch_bounds__(256) void lda_estep_thread(EStepArgs a) {
       lsum = fmaf(cnt, __logf(P), lsum);
 #pragma unroll
       for (int k = 0; k < KS; ++k) acc[k] = fmaf(r, row[k], acc[k]);
+      a.r_out[beg + n] = r;
+    };
+#pragma unroll
+    for (int c = 0; c < TC; ++c)
+      if (c < N) word(bc[c], cc[c], c);
+    for (int n = TC; n < N; n += 2) {
+      const bool two = n + 1 < N;
+      float r0[KS], r1[KS];
+      load_row<KS>(a.beta, a.word_idx[beg + n], r0);
+      load_row<KS>(a.beta, a.word_idx[beg + (two ? n + 1 : n)], r1);
+      const float c0 = a.counts[beg + n];
+      const float c1 = two ? a.counts[beg + n + 1] : 0.f;
+      word(r0, c0, n);
+      if (two) word(r1, c1, n + 1);
     }
     float gn[KS];
     float S = 0.f;
@@ -509,41 +541,34 @@ __global__ __launch_bounds__(256) void lda_estep_thread(EStepArgs a) {
       gn[k] = k < K ? fmaf(e[k], acc[k], alpha) : 0.f;
       S += gn[k];
     }
-    const float dS = digammaf_ldac(S);
+    float dS, lgS;
+    digamma_lgamma(S, dS, lgS);
     double term = 0.0;
 #pragma unroll
     for (int k = 0; k < KS; ++k) {
       if (k < K) {
-        const float pn = digammaf_ldac(gn[k]);
-        const float y = pn - dS;
-        term += (double)((alpha - 1.f) * y) + (double)lgammaf_fast(gn[k]) - (double)((gn[k] - 1.f) * y) +
-                (double)((gn[k] - alpha) * (pn - psi[k]));
+        float pn, lg;
+        digamma_lgamma(gn[k], pn, lg);
+        // (a-1)Y + lnG(g') - (g'-1)Y + (g'-a)(psi(g') - psi(g)) with Y = psi(g') - psi(S')
+        term += (double)lg + (double)((gn[k] - alpha) * (dS - psi[k]));
         psi[k] = pn;
         gam[k] = gn[k];
       }
     }
-    L = a.lik_const - (double)lgammaf_fast(S) + term + ((double)lsum + (double)m * total) - total * (double)dS;
+    L = a.lik_const - (double)lgS + term + ((double)lsum + (double)m * total) - total * (double)dS;
     conv = (lik_old - L) / lik_old;
     lik_old = L;
     dsum_last = dS;
     const bool cont = conv > (double)a.var_conv && (unbounded || it < a.var_max_iter);
     if (cont) compute_e();
   }
-  // outputs (E of the final phi; r_n = c_n / P_n under it)
+  // outputs (E of the final phi; r_n was written by the last word pass)
   double ass = 0.0;
 #pragma unroll
   for (int k = 0; k < KS; ++k) {
     a.gamma[(size_t)d * KS + k] = gam[k];
     a.e_out[(size_t)d * KS + k] = e[k];
     if (k < K) ass += (double)psi[k];
-  }
-  for (int n = 0; n < N; ++n) {
-    float row[KS];
-    load_row<KS>(a.beta, a.word_idx[beg + n], row);
-    float P = 0.f;
-#pragma unroll
-    for (int k = 0; k < KS; ++k) P = fmaf(e[k], row[k], P);
-    a.r_out[beg + n] = a.counts[beg + n] / fmaxf(P, kPMin);
   }
   a.lik[d] = L;
   a.alpha_ss[d] = ass - (double)K * dsum_last;

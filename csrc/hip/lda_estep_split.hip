@@ -231,22 +231,23 @@ __global__ __launch_bounds__(kNT) void lda_estep_split(EStepArgs a, SplitArgs s)
       }
       lsum_d = ordered_sum(s.partial_l + (size_t)par * s.n_blocks + base, nseg, 1);
       const float S = group_sum<64>(sg);
-      const float dS = digammaf_ldac(S);
+      float dS, lgS;
+      digamma_lgamma(S, dS, lgS);
       double term = 0.0;
 #pragma unroll
       for (int j = 0; j < TJ; ++j) {
         const int k = lane + 64 * j;
         if (k < K) {
-          const float pn = digammaf_ldac(gn[j]);
-          const float y = pn - dS;
-          term += (double)((alpha - 1.f) * y) + (double)lgammaf_fast(gn[j]) - (double)((gn[j] - 1.f) * y) +
-                  (double)((gn[j] - alpha) * (pn - psi[j]));
+          float pn, lg;
+          digamma_lgamma(gn[j], pn, lg);
+          // (a-1)Y + lnG(g') - (g'-1)Y + (g'-a)(psi(g') - psi(g)) with Y = psi(g') - psi(S')
+          term += (double)lg + (double)((gn[j] - alpha) * (dS - psi[j]));
           psi[j] = pn;
           gam[j] = gn[j];
         }
       }
       term = group_sum<64>(term);
-      L = a.lik_const - (double)lgammaf_fast(S) + term + (lsum_d + (double)m * total) - total * (double)dS;
+      L = a.lik_const - (double)lgS + term + (lsum_d + (double)m * total) - total * (double)dS;
       conv = (lik_old - L) / lik_old;
       lik_old = L;
       dsum_last = dS;
@@ -268,6 +269,18 @@ __global__ __launch_bounds__(kNT) void lda_estep_split(EStepArgs a, SplitArgs s)
     __syncthreads();
   }
 
+  // Every wave of this workgroup has passed its last barrier (the loop ends on a
+  // __syncthreads).  The last workgroup of the document to get here zeroes the
+  // arrival and exit counts for the next launch, so a replayed graph needs no memset.
+  if (t == 0) {
+    int* exits = counter + s.n_docs;
+    if (__hip_atomic_fetch_add(exits, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nseg - 1) {
+      __hip_atomic_store(counter, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(exits, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  const bool failed = __hip_atomic_load(s.error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
+
   // ---- outputs: r for this segment; the document state from segment 0 ----
 #pragma unroll
   for (int c = 0; c < CW; ++c) {
@@ -287,7 +300,7 @@ __global__ __launch_bounds__(kNT) void lda_estep_split(EStepArgs a, SplitArgs s)
     }
     ass = group_sum<64>(ass);
     if (lane == 0) {
-      a.lik[d] = L;
+      a.lik[d] = failed ? __builtin_nan("") : L;   // a timed-out barrier surfaces as a NaN likelihood
       a.alpha_ss[d] = ass - (double)K * dsum_last;
       a.iters[d] = it;
     }

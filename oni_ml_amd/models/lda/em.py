@@ -154,7 +154,6 @@ class LDAEngine:
             self._red_scratch2 = torch.zeros(H.lib().reduce_scratch_doubles(2), dtype=torch.float64, device=dev)
             self._ct_fresh = False
             self._params = torch.zeros(4, dtype=torch.float64, device=dev)
-            self._params_host = torch.zeros(4, dtype=torch.float64).pin_memory()
             self._ev_fork = torch.cuda.Event()
             self._ev_join = [torch.cuda.Event() for _ in range(1 + len(self._streams))]
             self.use_graph = use_graph
@@ -281,12 +280,7 @@ class LDAEngine:
         """One E-step on the GPU.  The launch sequence (all buckets on their streams, suff-stats,
         reductions) is captured once into a hipGraph and replayed every EM iteration; the
         per-iteration scalars (alpha, lgamma constant, VAR_MAX_ITER) travel in a device buffer."""
-        p = self._params_host
-        p[0] = self.alpha
-        p[1] = special.lik_const(self.alpha, self.K)
-        p[2] = float(self.var_max_iter)
-        p[3] = float(self.settings.var_converged)
-        self._params.copy_(p, non_blocking=True)
+        self._push_params()
         if self.use_graph and self._graph is None:
             self._capture_estep()             # its warm-up launch is this call's E-step
         elif self.use_graph:
@@ -400,13 +394,8 @@ class LDAEngine:
             host = sc.cpu().tolist()
             self.m_step(estimate_alpha, float(host[1]), num_docs)
             return float(host[0]), float(host[1])
-        p = self._params_host
         if self._pushed != (self.alpha, self.var_max_iter):   # host changed alpha / VAR_MAX_ITER
-            p[0] = self.alpha
-            p[1] = special.lik_const(self.alpha, self.K)
-            p[2] = float(self.var_max_iter)
-            p[3] = float(self.settings.var_converged)
-            self._params.copy_(p, non_blocking=True)
+            self._push_params()
         key = (bool(estimate_alpha), int(num_docs))
         distributed = self.dist is not None and self.dist.world_size > 1
         if not distributed:
@@ -436,9 +425,29 @@ class LDAEngine:
         self._out_ev.record()
         self._out_ev.synchronize()
         lik, ass, alpha = self._out_host.tolist()
+        if lik != lik:
+            self._check_split_error()
         self.alpha = alpha
         self._pushed = (self.alpha, self.var_max_iter)
         return lik, ass
+
+    def _push_params(self):
+        """Host alpha / VAR_MAX_ITER -> device parameter block.  The lgamma constant is derived
+        on the device by the same code the alpha Newton uses, so a run that restarts from host
+        values (resume, VAR_MAX_ITER doubling) sees bit-identical parameters."""
+        from ...ops import hip as H
+        p = torch.tensor([self.alpha, 0.0, float(self.var_max_iter), float(self.settings.var_converged)],
+                         dtype=torch.float64)
+        self._params.copy_(p)            # pageable source: no pending read of a reused host buffer
+        H.alpha_newton(self._scalars[:2], 1.0, self.K, False, self._params, self._scalars[2:3])
+
+    def _check_split_error(self):
+        """A NaN likelihood: if a split-document barrier timed out, fail loudly (the kernel
+        flags it instead of hanging the GPU)."""
+        sp = self.doc_buckets.split
+        if sp is not None and any(int(b["error"].item()) for b in sp.batches):
+            raise RuntimeError("split-document E-step: a cross-workgroup barrier timed out "
+                               "(segments of one document were not co-resident)")
 
     def _capture(self, launch):
         """Run ``launch`` once (this call's real work; first launches also load code objects),

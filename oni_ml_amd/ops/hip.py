@@ -158,7 +158,7 @@ class SplitPlan:
         return dict(seg_doc=t(sd), seg_index=t(si), seg_count=t(sc), seg_base=t(sb), doc_slot=t(slot), n_blocks=nb,
                     partial=torch.zeros(2 * nb * KS, dtype=torch.float32, device=device),
                     partial_l=torch.zeros(2 * nb, dtype=torch.float64, device=device),
-                    counter=torch.zeros(len(docs), dtype=torch.int32, device=device),
+                    counter=torch.zeros(2 * len(docs), dtype=torch.int32, device=device),   # kernel re-zeroes
                     error=torch.zeros(1, dtype=torch.int32, device=device), docs=len(docs))
 
 
@@ -171,7 +171,6 @@ def lda_estep_split(doc_ptr, word_idx, counts, beta, K, alpha, lik_const, var_ma
     nb = batch["n_blocks"]
     for k in ("seg_doc", "seg_index", "seg_count", "seg_base", "doc_slot"):
         _chk(batch[k], torch.int32, k, (nb,), dev)
-    batch["counter"].zero_()
     lib().lda_estep_split(
         _chk(doc_ptr, torch.int32, "doc_ptr", (D + 1,), dev), _chk(word_idx, torch.int32, "word_idx", (nnz,), dev),
         _chk(counts, torch.float32, "counts", (nnz,), dev), _chk(beta, torch.float32, "beta", (V, KS), dev),
@@ -183,7 +182,8 @@ def lda_estep_split(doc_ptr, word_idx, counts, beta, K, alpha, lik_const, var_ma
         batch["seg_base"].data_ptr(), batch["doc_slot"].data_ptr(), int(nb), int(seg_words),
         _chk(batch["partial"], torch.float32, "partial", (2 * nb * KS,), dev),
         _chk(batch["partial_l"], torch.float64, "partial_l", (2 * nb,), dev),
-        _chk(batch["counter"], torch.int32, "counter", None, dev), _chk(batch["error"], torch.int32, "error", (1,), dev),
+        _chk(batch["counter"], torch.int32, "counter", (2 * batch["docs"],), dev), int(batch["docs"]),
+        _chk(batch["error"], torch.int32, "error", (1,), dev),
         _params_ptr(params, dev), _stream())
 
 
