@@ -107,6 +107,8 @@ def main():
     ap.add_argument("--vocab", type=int, default=8_000)
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--streams", type=int, default=4, help="HIP streams for the E-step buckets")
+    ap.add_argument("--batch", type=int, default=5,
+                    help="EM iterations per host read-back (LDAEngine.run() uses LAG=5 when saving)")
     ap.add_argument("--converge", type=int, default=1, help="also time a full random-init run to convergence")
     ap.add_argument("--e2e", type=int, default=1, help="N=1: also time the whole ml_ops flow pipeline on the day")
     ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"], help="cpu: gloo/torch rehearsal")
@@ -131,19 +133,24 @@ def main():
     eng.init_random()
     docs_global = ctx.allreduce_int(corpus.num_docs)
 
-    def step():
-        # E-step graph -> (RCCL all-reduce of class_word + scalars when N > 1) -> M-step graph with the
-        # alpha Newton on the device; one host read-back of (likelihood, alpha_ss, alpha)
-        lik, _ = eng.em_iteration(True, docs_global)
-        return lik
+    def run_iters(n):
+        # EM iterations exactly as LDAEngine.run() issues them: batches of --batch iterations
+        # (one hipGraph replay each on one rank; E-step graph -> RCCL all-reduce -> M-step graph on
+        # several) with the lda-c convergence test evaluated on the device and one host read-back of
+        # the per-iteration (likelihood, conv, alpha) history per batch.  stop=False: every one of
+        # the n iterations runs in full (none is skipped by a converged loop).
+        done = 0
+        while done < n:
+            m = min(args.batch, n - done)
+            recs = eng.em_iterations(m, True, docs_global, stop=False)
+            assert len(recs) == m, (len(recs), m)
+            done += m
 
-    for _ in range(args.warmup):
-        step()
+    run_iters(args.warmup)
     ctx.barrier()
     _sync(dev)
     t1 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
+    run_iters(args.steps)
     _sync(dev)
     ctx.barrier()
     dt = time.perf_counter() - t1

@@ -78,29 +78,57 @@ PYBIND11_MODULE(_onihip, m) {
       });
 
   m.def("lda_suffstats", [](u word_ptr, u csc_ent, u csc_doc, u order, int n_items, u e, u r, u beta, u cw,
-                            int KS, int variant, u stream) {
+                            int KS, int variant, u gate, u stream) {
     oni::SuffArgs a{P<const int>(word_ptr), P<const int>(csc_ent), P<const int>(csc_doc),
                     P<const int>(order),    n_items,               P<const float>(e),
-                    P<const float>(r),      P<const float>(beta),  P<float>(cw)};
+                    P<const float>(r),      P<const float>(beta),  P<float>(cw),
+                    P<const double>(gate)};
     oni::launch_lda_suffstats(a, variant, KS, S(stream));
   });
 
+  m.def("suff_fused_blocks", [](int h, int m_, int l) { return oni::suff_fused_blocks(h, m_, l); });
+  m.def("lda_suffstats_fused", [](u word_ptr, u csc_ent, u csc_doc, u order, int n_heavy, int n_medium, int n_light,
+                                  u e, u r, u beta, u cw, u part, int KS, u gate, u stream) {
+    oni::SuffArgs a{P<const int>(word_ptr), P<const int>(csc_ent),  P<const int>(csc_doc),
+                    P<const int>(order),    n_heavy + n_medium + n_light, P<const float>(e),
+                    P<const float>(r),      P<const float>(beta),   P<float>(cw),
+                    P<const double>(gate)};
+    oni::launch_lda_suffstats_fused(a, n_heavy, n_medium, n_light, P<double>(part), KS, S(stream));
+  });
+  m.def("colsum_partials", [](u part, int nb, int cols, u out, u gate, u stream) {
+    oni::launch_colsum_partials(P<const double>(part), nb, cols, P<double>(out), P<const double>(gate), S(stream));
+  });
+  m.def("lda_mstep_control", [](u cw, u class_total, u beta, int V, int K, int KS, u scalars, u params, u ctl,
+                                u hist, int hist_slots, u done_count, u stream) {
+    oni::EMControlArgs c{P<const double>(scalars), P<double>(params), P<double>(ctl), P<double>(hist), hist_slots,
+                         P<int>(done_count)};
+    oni::launch_lda_mstep_control(P<const float>(cw), P<const double>(class_total), P<float>(beta), V, K, KS, c,
+                                  S(stream));
+  });
   m.def("reduce_scratch_doubles", [](int cols) { return oni::reduce_scratch_doubles(cols); });
-  m.def("colsum", [](u mat, int rows, int cols, u out, u scratch, u stream) {
-    oni::launch_colsum(P<const float>(mat), rows, cols, P<double>(out), P<double>(scratch), S(stream));
+  m.def("colsum", [](u mat, int rows, int cols, u out, u scratch, u gate, u stream) {
+    oni::launch_colsum(P<const float>(mat), rows, cols, P<double>(out), P<double>(scratch), P<const double>(gate),
+                       S(stream));
   });
-  m.def("sum2", [](u a, u b, int n, u out, u scratch, u stream) {
-    oni::launch_sum2(P<const double>(a), P<const double>(b), n, P<double>(out), P<double>(scratch), S(stream));
+  m.def("sum2", [](u a, u b, int n, u out, u scratch, u gate, u stream) {
+    oni::launch_sum2(P<const double>(a), P<const double>(b), n, P<double>(out), P<double>(scratch),
+                     P<const double>(gate), S(stream));
   });
+  m.def("em_control", [](u scalars, u params, u ctl, u hist, int hist_slots, u stream) {
+    oni::launch_em_control(P<const double>(scalars), P<double>(params), P<double>(ctl), P<double>(hist), hist_slots,
+                           S(stream));
+  });
+  m.def("param_count", []() { return oni::kParamCount; });
+  m.def("hist_cols", []() { return oni::kHistCols; });
 
   m.def("alpha_newton", [](u scalars, double num_docs, int K, bool estimate, u params, u alpha_out, u stream) {
     oni::launch_alpha_newton(P<const double>(scalars), num_docs, K, estimate, P<double>(params), P<double>(alpha_out),
                              S(stream));
   });
 
-  m.def("lda_mstep", [](u cw, u class_total, u beta, int V, int K, int KS, u stream) {
+  m.def("lda_mstep", [](u cw, u class_total, u beta, int V, int K, int KS, u gate, u stream) {
     oni::launch_lda_mstep(P<const float>(cw), P<const double>(class_total), P<float>(beta), V, K, KS,
-                          S(stream));
+                          P<const double>(gate), S(stream));
   });
 
   m.def("score_events", [](u theta, u phi, int K, double dflt, u doc_a, u word_a, u doc_b, u word_b,

@@ -35,6 +35,10 @@ constexpr float kExpMinus100 = 3.7200759760208e-44f;
 // dominated by these.
 __device__ __forceinline__ float frcp(float x) { return __builtin_amdgcn_rcpf(x); }
 
+// Device-side EM loop control (em_control.hip): once the convergence test has
+// fired, every kernel of the iterations still queued behind it returns at once.
+__device__ __forceinline__ bool gated(const double* gate) { return gate != nullptr && *gate != 0.0; }
+
 __device__ __forceinline__ float digammaf_ldac(float x) {
   float p;
   x = x + 6.0f;

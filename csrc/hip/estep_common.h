@@ -1,6 +1,7 @@
 // Device helpers shared by the E-step kernels (lda_estep.hip, lda_estep_split.hip).
 #pragma once
 #include "common.h"
+#include "kernels.h"
 
 namespace oni {
 
@@ -43,15 +44,19 @@ constexpr float kPMin = 1e-30f;
 constexpr int rows_per_lane_4w(int KS) { return KS <= 32 ? 4 : (KS <= 64 ? 2 : 1); }
 constexpr int rows_per_lane_8w(int KS) { return KS <= 20 ? 6 : (KS <= 32 ? 3 : 1); }
 
-// Per-launch scalars from device memory when the launch is graph-replayed.
+// Per-launch scalars from device memory when the launch is graph-replayed:
+// params = {alpha, lgamma(K alpha) - K lgamma(alpha), VAR_MAX_ITER, VAR_CONVERGED,
+// done}.  Returns true when the EM loop has already converged (skip the launch).
 template <typename Args>
-__device__ __forceinline__ void load_params(Args& a) {
+__device__ __forceinline__ bool load_params(Args& a) {
   if (a.params) {
+    if (a.params[kParamDone] != 0.0) return true;
     a.alpha = (float)a.params[0];
     a.lik_const = a.params[1];
     a.var_max_iter = (int)a.params[2];
     a.var_conv = (float)a.params[3];
   }
+  return false;
 }
 
 }  // namespace oni

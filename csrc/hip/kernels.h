@@ -8,6 +8,13 @@ namespace oni {
 // Padded topic counts (row stride of word-major beta, multiple of 4) that have
 // compiled kernel instantiations.  Any K is served by the next larger entry;
 // padding topics carry beta = 0 and are masked in the per-topic phase.
+// Device parameter block (double[kParamCount]) read by the E-step kernels and
+// written by the alpha Newton / EM control kernels; kParamDone != 0 gates every
+// kernel of the EM iteration (device-side convergence, em_control.hip).
+constexpr int kParamDone = 4;
+constexpr int kParamCount = 8;
+constexpr int kHistCols = 6;
+
 #define ONI_FOR_EACH_KS(X) X(8) X(12) X(16) X(20) X(24) X(32) X(52) X(64) X(100) X(128)
 
 // ---------------------------------------------------------------- E-step ---
@@ -63,9 +70,10 @@ struct EStepArgs {
   double* lik;            // [D]
   double* alpha_ss;       // [D]
   int* iters;             // [D]
-  // Optional device copy of {alpha, lik_const, var_max_iter, var_conv}: when set
-  // it overrides those four fields, so a captured hipGraph of the E-step can be
-  // replayed every EM iteration while alpha / VAR_MAX_ITER change.
+  // Optional device parameter block (kParamCount doubles): when set, its
+  // {alpha, lik_const, var_max_iter, var_conv} override those four fields, so a
+  // captured hipGraph of the E-step can be replayed every EM iteration while alpha
+  // / VAR_MAX_ITER change, and params[kParamDone] != 0 skips the launch.
   const double* params = nullptr;
 };
 void launch_lda_estep(const EStepArgs& a, int variant, int KS, hipStream_t s);
@@ -86,25 +94,64 @@ struct SuffArgs {
   const float* r;         // [nnz]
   const float* beta;      // [V][KS]
   float* cw;              // [V][KS] class_word (word-major), written for listed words
+  const double* gate;     // nullable: skip when *gate != 0 (converged EM loop)
 };
 void launch_lda_suffstats(const SuffArgs& a, int variant, int KS, hipStream_t s);
+// All words in one launch: a.order = [heavy | medium | light] word ids (heavy first);
+// part receives suff_fused_blocks(...) x KS per-workgroup column sums (double).
+int suff_fused_blocks(int n_heavy, int n_medium, int n_light);
+void launch_lda_suffstats_fused(const SuffArgs& a, int n_heavy, int n_medium, int n_light, double* part, int KS,
+                                hipStream_t s);
 
 // ----------------------------------------------------------------- M-step ---
 // beta[w][k] = cw/ct_k if cw > 0 else exp(-100) (k < K); 0 for padding topics.
 void launch_lda_mstep(const float* cw, const double* class_total, float* beta, int V, int K, int KS,
-                      hipStream_t s);
+                      const double* gate, hipStream_t s);
 
 // alpha Newton on the device: reads scalars[1] (alpha_ss), writes params[0..1]
 // (alpha, lgamma(K alpha) - K lgamma(alpha)) and alpha_out[0].
+// Skipped once params[kParamDone] is set.
 void launch_alpha_newton(const double* scalars, double num_docs, int K, bool estimate, double* params,
                          double* alpha_out, hipStream_t s);
+
+// Device-side EM convergence test (em_control.hip), the lda-c driver loop
+//   while ((conv < 0 || conv > EM_CONVERGED || i <= 2) && i <= EM_MAX_ITER)
+// evaluated after each iteration without a host round trip.  ctl (double[8]):
+//   [0] previous likelihood  [1] EM_CONVERGED  [2] history slot  [3] iteration i
+//   [4] EM_MAX_ITER  [5] stop allowed (0: never set done)
+// scalars = {likelihood, alpha_ss}.  It appends {likelihood, conv, alpha (params[0]),
+// VAR_MAX_ITER, alpha_ss, -} (kHistCols
+// doubles) to hist[slot], doubles
+// VAR_MAX_ITER in params when the likelihood decreased (lda-c), and sets
+// params[kParamDone] when the loop ends.
+void launch_em_control(const double* scalars, double* params, double* ctl, double* hist, int hist_slots,
+                       hipStream_t s);
+
+// M-step fused with the EM control step: the last workgroup to finish (every
+// other one has read the gate) runs em_control_step.  done_count: one int,
+// zero before the first launch, left zero by the kernel.
+struct EMControlArgs {
+  const double* scalars;
+  double* params;
+  double* ctl;
+  double* hist;
+  int hist_slots;
+  int* done_count;
+};
+void launch_lda_mstep_control(const float* cw, const double* class_total, float* beta, int V, int K, int KS,
+                              const EMControlArgs& c, hipStream_t s);
 
 // ------------------------------------------------------------- reductions ---
 // Deterministic two-pass reductions (reduce.hip).  scratch holds
 // reduce_scratch_doubles(cols) doubles.
 int reduce_scratch_doubles(int cols);
-void launch_colsum(const float* m, int rows, int cols, double* out, double* scratch, hipStream_t s);
-void launch_sum2(const double* a, const double* b, int n, double* out, double* scratch, hipStream_t s);
+// gate (nullable): skip when *gate != 0.
+void launch_colsum(const float* m, int rows, int cols, double* out, double* scratch, const double* gate,
+                   hipStream_t s);
+void launch_sum2(const double* a, const double* b, int n, double* out, double* scratch, const double* gate,
+                 hipStream_t s);
+// out[k] = sum_b part[b][k] (b in order), the second pass of the fused suff-stats.
+void launch_colsum_partials(const double* part, int nb, int cols, double* out, const double* gate, hipStream_t s);
 
 // ---------------------------------------------------------------- scoring ---
 struct ScoreArgs {

@@ -45,7 +45,7 @@ namespace oni {
 // ---------------------------------------------------------------------------
 template <int KS, int G, int CW>
 __global__ __launch_bounds__(256) void lda_estep_group(EStepArgs a) {
-  load_params(a);
+  if (load_params(a)) return;
   constexpr int GPB = 256 / G;
   constexpr int TJ = (KS + G - 1) / G;
   __shared__ float4 sE4[GPB][KS / 4];
@@ -231,7 +231,7 @@ __global__ __launch_bounds__(256) void lda_estep_group(EStepArgs a) {
 // ---------------------------------------------------------------------------
 template <int KS, int NW, int CW>
 __global__ __launch_bounds__(NW * 64) void lda_estep_block(EStepArgs a) {
-  load_params(a);
+  if (load_params(a)) return;
   // long documents are the EM step's critical path: win SIMD issue arbitration
   // against the short-document waves that share the CU (microarch guide, s_setprio)
   __builtin_amdgcn_s_setprio(2);
@@ -449,7 +449,7 @@ __global__ __launch_bounds__(256) void lda_estep_thread(EStepArgs a) {
   // median document has 2 words, so most threads never touch memory in the loop);
   // further words are fetched two rows at a time so their loads overlap.
   constexpr int TC = KS <= 12 ? 4 : (KS <= 20 ? 3 : 1);
-  load_params(a);
+  if (load_params(a)) return;
   const int item = blockIdx.x * 256 + threadIdx.x;
   if (item >= a.n_items) return;
   const int d = a.order[item];

@@ -87,7 +87,7 @@ __device__ __forceinline__ T ordered_sum(const T* x, int n, int stride) {
 
 template <int KS, int CW>
 __global__ __launch_bounds__(kNT) void lda_estep_split(EStepArgs a, SplitArgs s) {
-  load_params(a);
+  if (load_params(a)) return;
   __builtin_amdgcn_s_setprio(3);   // the longest serial chain of the EM step
   constexpr int TJ = (KS + 63) / 64;
   __shared__ float4 sE4[KS / 4];

@@ -14,6 +14,7 @@
 
 #include "common.h"
 #include "kernels.h"
+#include "em_control.h"
 
 namespace oni {
 
@@ -83,7 +84,7 @@ __global__ __launch_bounds__(256) void lda_suff_group(SuffArgs a) {
   constexpr int GPB = 256 / G;
   const int t = threadIdx.x % G;
   const int item = blockIdx.x * GPB + threadIdx.x / G;
-  if (item >= a.n_items) return;
+  if (item >= a.n_items || gated(a.gate)) return;
   const int w = a.order[item];
   const int beg = a.word_ptr[w], end = a.word_ptr[w + 1];
   float acc[KS];
@@ -97,6 +98,7 @@ __global__ __launch_bounds__(256) void lda_suff_group(SuffArgs a) {
 template <int KS, int NW>
 __global__ __launch_bounds__(NW * 64) void lda_suff_block(SuffArgs a) {
   __shared__ float sRed[NW][KS];
+  if (gated(a.gate)) return;
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const int w = a.order[blockIdx.x];
   const int beg = a.word_ptr[w], end = a.word_ptr[w + 1];
@@ -115,6 +117,106 @@ __global__ __launch_bounds__(NW * 64) void lda_suff_block(SuffArgs a) {
 #pragma unroll
     for (int v = 0; v < NW; ++v) s += sRed[v][t];
     a.cw[(size_t)w * KS + t] = a.beta[(size_t)w * KS + t] * s;
+  }
+}
+
+// One launch for all words (heavy words first), 256 threads per workgroup:
+//   heavy  (> 1024 entries): one word per workgroup, 4 waves, cross-wave LDS sum
+//   medium (65..1024):       one word per wave
+//   light  (<= 64, empty):   one word per 16 lanes
+// Each workgroup also writes the column sums of the class_word rows it produced
+// (in double, fixed group order) to part[blockIdx.x][0..KS), so the per-topic
+// totals need only a small second pass over the partials (colsum_partials)
+// instead of a re-read of the whole [V][KS] matrix.
+template <int KS>
+__global__ __launch_bounds__(256) void lda_suff_fused(SuffArgs a, int n_heavy, int n_medium, int n_light,
+                                                      double* __restrict__ part) {
+  __shared__ float sRow[16][KS];
+  if (gated(a.gate)) return;
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const int nbM = (n_medium + 3) / 4;
+  const int b = blockIdx.x;
+  float acc[KS];
+#pragma unroll
+  for (int k = 0; k < KS; ++k) acc[k] = 0.f;
+  int ngroups;
+  if (b < n_heavy) {
+    const int w = a.order[b];
+    gather_axpy<KS, 256>(a, a.word_ptr[w] + t, a.word_ptr[w + 1], acc);
+    group_sum_vec<64, KS>(acc);
+    if (lane == 0) {
+#pragma unroll
+      for (int k = 0; k < KS; ++k) sRow[wv][k] = acc[k];
+    }
+    __syncthreads();
+    if (t < KS) {
+      float s = 0.f;
+#pragma unroll
+      for (int v = 0; v < 4; ++v) s += sRow[v][t];
+      const float c = a.beta[(size_t)w * KS + t] * s;
+      a.cw[(size_t)w * KS + t] = c;
+      part[(size_t)b * KS + t] = (double)c;
+    }
+    return;
+  } else if (b < n_heavy + nbM) {
+    const int item = (b - n_heavy) * 4 + wv;
+    const bool valid = item < n_medium;
+    const int w = valid ? a.order[n_heavy + item] : 0;
+    if (valid) gather_axpy<KS, 64>(a, a.word_ptr[w] + lane, a.word_ptr[w + 1], acc);
+    group_sum_vec<64, KS>(acc);
+    if (lane == 0) {
+      if (valid) store_cw<KS>(a, w, acc);
+      const float* bw = a.beta + (size_t)w * KS;
+#pragma unroll
+      for (int k = 0; k < KS; ++k) sRow[wv][k] = valid ? bw[k] * acc[k] : 0.f;
+    }
+    ngroups = 4;
+  } else {
+    const int g = t >> 4, q = t & 15;
+    const int item = (b - n_heavy - nbM) * 16 + g;
+    const bool valid = item < n_light;
+    const int w = valid ? a.order[n_heavy + n_medium + item] : 0;
+    if (valid) gather_axpy<KS, 16>(a, a.word_ptr[w] + q, a.word_ptr[w + 1], acc);
+    group_sum_vec<16, KS>(acc);
+    if (q == 0) {
+      if (valid) store_cw<KS>(a, w, acc);
+      const float* bw = a.beta + (size_t)w * KS;
+#pragma unroll
+      for (int k = 0; k < KS; ++k) sRow[g][k] = valid ? bw[k] * acc[k] : 0.f;
+    }
+    ngroups = 16;
+  }
+  __syncthreads();
+  if (t < KS) {
+    double s = 0.0;
+    for (int g = 0; g < ngroups; ++g) s += (double)sRow[g][t];
+    part[(size_t)b * KS + t] = s;
+  }
+}
+
+int suff_fused_blocks(int n_heavy, int n_medium, int n_light) {
+  return n_heavy + (n_medium + 3) / 4 + (n_light + 15) / 16;
+}
+
+template <int KS>
+static void suff_fused_ks(const SuffArgs& a, int n_heavy, int n_medium, int n_light, double* part, hipStream_t s) {
+  const int nb = suff_fused_blocks(n_heavy, n_medium, n_light);
+  if (nb <= 0) return;
+  hipLaunchKernelGGL((lda_suff_fused<KS>), dim3(nb), dim3(256), 0, s, a, n_heavy, n_medium, n_light, part);
+  ONI_HIP_CHECK(hipGetLastError());
+}
+
+void launch_lda_suffstats_fused(const SuffArgs& a, int n_heavy, int n_medium, int n_light, double* part, int KS,
+                                hipStream_t s) {
+  switch (KS) {
+#define ONI_KS(X) \
+  case X:         \
+    suff_fused_ks<X>(a, n_heavy, n_medium, n_light, part, s); \
+    break;
+    ONI_FOR_EACH_KS(ONI_KS)
+#undef ONI_KS
+    default:
+      throw std::runtime_error("lda_suffstats_fused: unsupported KS " + std::to_string(KS));
   }
 }
 
@@ -156,7 +258,9 @@ void launch_lda_suffstats(const SuffArgs& a, int variant, int KS, hipStream_t s)
 // beta = cw / ct (exact division) or exp(-100).
 __global__ __launch_bounds__(256) void lda_mstep_kernel(const float* __restrict__ cw,
                                                         const double* __restrict__ ct,
-                                                        float* __restrict__ beta, int V, int K, int KS) {
+                                                        float* __restrict__ beta, int V, int K, int KS,
+                                                        const double* gate) {
+  if (gated(gate)) return;
   const int64_t total = (int64_t)V * KS;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total;
        i += (int64_t)gridDim.x * blockDim.x) {
@@ -168,6 +272,52 @@ __global__ __launch_bounds__(256) void lda_mstep_kernel(const float* __restrict_
     }
     beta[i] = out;
   }
+}
+
+__global__ __launch_bounds__(256) void lda_mstep_control_kernel(const float* __restrict__ cw,
+                                                                const double* __restrict__ ct,
+                                                                float* __restrict__ beta, int V, int K, int KS,
+                                                                EMControlArgs c) {
+  if (c.params[kParamDone] != 0.0) return;
+  // float4 granules of the word-major [V][KS] matrices (KS % 4 == 0)
+  const int q = KS / 4;
+  const int total4 = V * q;
+  const float4* cw4 = reinterpret_cast<const float4*>(cw);
+  float4* beta4 = reinterpret_cast<float4*>(beta);
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total4; i += gridDim.x * blockDim.x) {
+    const int k0 = (i % q) * 4;
+    const float4 v = cw4[i];
+    float o[4];
+    const float vv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int k = k0 + j;
+      o[j] = k < K ? (vv[j] > 0.f ? (float)((double)vv[j] / ct[k]) : kExpMinus100) : 0.f;
+    }
+    beta4[i] = make_float4(o[0], o[1], o[2], o[3]);
+  }
+  // Relaxed is enough: the control step reads only what earlier kernels wrote (scalars,
+  // params, ctl); the count just has to see every workgroup past its gate read.
+  // (An acq_rel agent-scope RMW per workgroup costs an L2 writeback + invalidate each.)
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    if (__hip_atomic_fetch_add(c.done_count, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (int)gridDim.x - 1) {
+      __hip_atomic_store(c.done_count, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      em_control_step(c.scalars, c.params, c.ctl, c.hist, c.hist_slots);
+    }
+  }
+}
+
+void launch_lda_mstep_control(const float* cw, const double* class_total, float* beta, int V, int K, int KS,
+                              const EMControlArgs& c, hipStream_t s) {
+  const int64_t total = (int64_t)V * KS;
+  // 2 workgroups per CU: the completion count is a same-address atomic per workgroup
+  int64_t blocks = (total / 4 + 255) / 256;
+  if (blocks > 512) blocks = 512;
+  if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL(lda_mstep_control_kernel, dim3((unsigned)blocks), dim3(256), 0, s, cw, class_total, beta, V,
+                     K, KS, c);
+  ONI_HIP_CHECK(hipGetLastError());
 }
 
 // ------------------------------------------------------- alpha on device ---
@@ -192,7 +342,7 @@ __device__ double trigamma_ldac(double x) {
 
 __global__ void alpha_newton_kernel(const double* __restrict__ scalars, double num_docs, int K, int estimate,
                                     double* __restrict__ params, double* __restrict__ alpha_out) {
-  if (threadIdx.x != 0 || blockIdx.x != 0) return;
+  if (threadIdx.x != 0 || blockIdx.x != 0 || params[kParamDone] != 0.0) return;
   double a = params[0];
   if (estimate) {
     const double ss = scalars[1];
@@ -226,13 +376,13 @@ void launch_alpha_newton(const double* scalars, double num_docs, int K, bool est
 }
 
 void launch_lda_mstep(const float* cw, const double* class_total, float* beta, int V, int K, int KS,
-                      hipStream_t s) {
+                      const double* gate, hipStream_t s) {
   const int64_t total = (int64_t)V * KS;
   if (total == 0) return;
   int64_t blocks = (total + 255) / 256;
   if (blocks > 4096) blocks = 4096;
   hipLaunchKernelGGL(lda_mstep_kernel, dim3((unsigned)blocks), dim3(256), 0, s, cw, class_total, beta, V,
-                     K, KS);
+                     K, KS, gate);
   ONI_HIP_CHECK(hipGetLastError());
 }
 

@@ -18,7 +18,8 @@ constexpr int kRT = 256;   // threads per workgroup
 }  // namespace
 
 __global__ __launch_bounds__(kRT) void colsum_pass1(const float* __restrict__ m, int rows, int cols,
-                                                    double* __restrict__ part) {
+                                                    double* __restrict__ part, const double* gate) {
+  if (gated(gate)) return;
   __shared__ double sh[kRT];
   const int groups = kRT / cols;                   // row groups per workgroup
   const int t = threadIdx.x;
@@ -40,7 +41,8 @@ __global__ __launch_bounds__(kRT) void colsum_pass1(const float* __restrict__ m,
 // One wave per column (columns round-robin over the 4 waves): lane l adds the
 // partials l, l+64, l+128, l+192 (independent loads), then a fixed butterfly.
 __global__ __launch_bounds__(kRT) void colsum_pass2(const double* __restrict__ part, int nb, int cols,
-                                                    double* __restrict__ out) {
+                                                    double* __restrict__ out, const double* gate) {
+  if (gated(gate)) return;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   for (int k = wv; k < cols; k += kRT / 64) {
     double v[kRB / 64];
@@ -58,7 +60,8 @@ __global__ __launch_bounds__(kRT) void colsum_pass2(const double* __restrict__ p
 }
 
 __global__ __launch_bounds__(kRT) void sum2_pass1(const double* __restrict__ a, const double* __restrict__ b, int n,
-                                                  double* __restrict__ part) {
+                                                  double* __restrict__ part, const double* gate) {
+  if (gated(gate)) return;
   __shared__ double sa[kRT / 64], sb[kRT / 64];
   const int per = (n + gridDim.x - 1) / gridDim.x;
   const int i0 = blockIdx.x * per, i1 = min(n, i0 + per);
@@ -85,7 +88,9 @@ __global__ __launch_bounds__(kRT) void sum2_pass1(const double* __restrict__ a, 
   }
 }
 
-__global__ __launch_bounds__(64) void sum2_pass2(const double* __restrict__ part, int nb, double* __restrict__ out) {
+__global__ __launch_bounds__(64) void sum2_pass2(const double* __restrict__ part, int nb, double* __restrict__ out,
+                                                 const double* gate) {
+  if (gated(gate)) return;
   const int lane = threadIdx.x;
   double u[kRB / 64], v[kRB / 64];
 #pragma unroll
@@ -108,18 +113,56 @@ __global__ __launch_bounds__(64) void sum2_pass2(const double* __restrict__ part
   }
 }
 
-int reduce_scratch_doubles(int cols) { return kRB * (cols > 2 ? cols : 2); }
+// out[k] = sum_b part[b][k] over the per-workgroup column sums of the fused
+// suff-stats kernel: one workgroup per column, rows strided over 256 lanes with
+// 8 loads in flight, fixed-order wave and cross-wave combination.
+__global__ __launch_bounds__(kRT) void colsum_partials_kernel(const double* __restrict__ part, int nb, int cols,
+                                                              double* __restrict__ out, const double* gate) {
+  if (gated(gate)) return;
+  __shared__ double sw[kRT / 64];
+  const int k = blockIdx.x, t = threadIdx.x;
+  double s = 0.0;
+  for (int b0 = t; b0 < nb; b0 += 8 * kRT) {
+    double v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int b = b0 + u * kRT;
+      v[u] = b < nb ? part[(size_t)b * cols + k] : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) s += v[u];
+  }
+  s = group_sum<64>(s);
+  if ((t & 63) == 0) sw[t >> 6] = s;
+  __syncthreads();
+  if (t == 0) {
+    double r = 0.0;
+#pragma unroll
+    for (int w = 0; w < kRT / 64; ++w) r += sw[w];
+    out[k] = r;
+  }
+}
 
-void launch_colsum(const float* m, int rows, int cols, double* out, double* scratch, hipStream_t s) {
-  if (cols <= 0 || cols > kRT) throw std::runtime_error("colsum: cols out of range");
-  hipLaunchKernelGGL(colsum_pass1, dim3(kRB), dim3(kRT), 0, s, m, rows, cols, scratch);
-  hipLaunchKernelGGL(colsum_pass2, dim3(1), dim3(kRT), 0, s, scratch, kRB, cols, out);
+void launch_colsum_partials(const double* part, int nb, int cols, double* out, const double* gate, hipStream_t s) {
+  if (cols <= 0) return;
+  hipLaunchKernelGGL(colsum_partials_kernel, dim3(cols), dim3(kRT), 0, s, part, nb, cols, out, gate);
   ONI_HIP_CHECK(hipGetLastError());
 }
 
-void launch_sum2(const double* a, const double* b, int n, double* out, double* scratch, hipStream_t s) {
-  hipLaunchKernelGGL(sum2_pass1, dim3(kRB), dim3(kRT), 0, s, a, b, n, scratch);
-  hipLaunchKernelGGL(sum2_pass2, dim3(1), dim3(64), 0, s, scratch, kRB, out);
+int reduce_scratch_doubles(int cols) { return kRB * (cols > 2 ? cols : 2); }
+
+void launch_colsum(const float* m, int rows, int cols, double* out, double* scratch, const double* gate,
+                   hipStream_t s) {
+  if (cols <= 0 || cols > kRT) throw std::runtime_error("colsum: cols out of range");
+  hipLaunchKernelGGL(colsum_pass1, dim3(kRB), dim3(kRT), 0, s, m, rows, cols, scratch, gate);
+  hipLaunchKernelGGL(colsum_pass2, dim3(1), dim3(kRT), 0, s, scratch, kRB, cols, out, gate);
+  ONI_HIP_CHECK(hipGetLastError());
+}
+
+void launch_sum2(const double* a, const double* b, int n, double* out, double* scratch, const double* gate,
+                 hipStream_t s) {
+  hipLaunchKernelGGL(sum2_pass1, dim3(kRB), dim3(kRT), 0, s, a, b, n, scratch, gate);
+  hipLaunchKernelGGL(sum2_pass2, dim3(1), dim3(64), 0, s, scratch, kRB, out, gate);
   ONI_HIP_CHECK(hipGetLastError());
 }
 

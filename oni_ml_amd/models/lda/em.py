@@ -109,6 +109,7 @@ class LDAEngine:
         self.seed = seed
         self.var_max_iter = self.settings.var_max_iter
         self.collect_iter_stats = False
+        self.max_batch = 8          # EM iterations enqueued per host read-back (run())
         if backend == "auto":
             from ...ops import hip as H
             backend = "hip" if H.available() else "torch"
@@ -138,7 +139,6 @@ class LDAEngine:
             self.dc = DeviceCorpus.build(corpus, self.device)
             self.doc_buckets = _Buckets(self.dc.doc_len, self.KS, self.device, "doc",
                                         doc_ptr=corpus.doc_ptr, split=split_docs, split_min=split_min)
-            self.word_buckets = _Buckets(self.dc.word_len, self.KS, self.device, "word")
             dev, D, V, KS, nnz = self.device, self.D, self.V, self.KS, corpus.nnz
             self.beta = torch.zeros(V, KS, dtype=torch.float32, device=dev)
             self.cw = torch.zeros(V, KS, dtype=torch.float32, device=dev)
@@ -149,11 +149,28 @@ class LDAEngine:
             self.ass = torch.zeros(D, dtype=torch.float64, device=dev)
             self.iters = torch.zeros(D, dtype=torch.int32, device=dev)
             self._streams = [torch.cuda.Stream(device=dev) for _ in range(max(0, streams - 1))]
-            self._scalars = torch.zeros(3, dtype=torch.float64, device=dev)   # likelihood, alpha_ss, alpha
+            # [likelihood, alpha_ss, class_total[0..KS)]: the doubles one EM iteration reduces
+            self._red = torch.zeros(2 + KS, dtype=torch.float64, device=dev)
+            self._scalars = self._red[:2]
+            self.class_total = self._red[2:]
+            # Several ranks: the E-step writes rank-local statistics, the all-reduce works on copies
+            # (re-reducing unchanged locals after the device loop has converged is then a no-op).
+            self._distributed = dist is not None and dist.world_size > 1
+            self._cw_local = torch.zeros_like(self.cw) if self._distributed else self.cw
+            self._red_local = torch.zeros_like(self._red) if self._distributed else self._red
+            self.suff_plan = H.SuffPlan(self.dc.word_len, dev)
+            self._suff_part = torch.zeros(max(self.suff_plan.n_blocks, 1), KS, dtype=torch.float64, device=dev)
+            self._done_count = torch.zeros(1, dtype=torch.int32, device=dev)
+            self._alpha_dummy = torch.zeros(1, dtype=torch.float64, device=dev)
             self._red_scratch = torch.zeros(H.lib().reduce_scratch_doubles(KS), dtype=torch.float64, device=dev)
             self._red_scratch2 = torch.zeros(H.lib().reduce_scratch_doubles(2), dtype=torch.float64, device=dev)
             self._ct_fresh = False
-            self._params = torch.zeros(4, dtype=torch.float64, device=dev)
+            self._params = torch.zeros(H.PARAM_COUNT, dtype=torch.float64, device=dev)
+            self._gate = self._params[H.PARAM_DONE:H.PARAM_DONE + 1]
+            # device EM loop control block + per-iteration history (em_control.hip)
+            self._hist_cap = 64
+            self._ctlhist = torch.zeros(8 + H.HIST_COLS * self._hist_cap, dtype=torch.float64, device=dev)
+            self._ctl, self._hist = self._ctlhist[:8], self._ctlhist[8:]
             self._ev_fork = torch.cuda.Event()
             self._ev_join = [torch.cuda.Event() for _ in range(1 + len(self._streams))]
             self.use_graph = use_graph
@@ -162,7 +179,7 @@ class LDAEngine:
             self._fgraph, self._fgraph_key = None, None
             self._ev_red = torch.cuda.Event()
             self._ev_side = torch.cuda.Event()
-            self._out_host = torch.zeros(3, dtype=torch.float64).pin_memory()
+            self._out_host = torch.zeros(self._ctlhist.numel(), dtype=torch.float64).pin_memory()
             self._out_ev = torch.cuda.Event()
             self._pushed = None
             self._build_schedule()
@@ -184,7 +201,8 @@ class LDAEngine:
             self.gamma = torch.zeros(self.D, self.K, dtype=torch.float64)
         else:
             raise ValueError(f"unknown backend {backend}")
-        self.class_total = torch.zeros(self.KS, dtype=torch.float64, device=self.cw.device)
+        if backend != "hip":
+            self.class_total = torch.zeros(self.KS, dtype=torch.float64, device=self.cw.device)
 
     # ------------------------------------------------------------------ init
     def init_random(self, seed: Optional[int] = None):
@@ -289,16 +307,18 @@ class LDAEngine:
             self._launch_estep()
         self._pushed = None                   # params now hold host values; em_iteration re-checks
         self._ct_fresh = True
-        return self._scalars[:2]
+        return self._scalars
 
     def _launch_estep(self, newton_key=None):
         """Enqueue one E-step: document buckets on their streams, then suff-stats (main stream) and
         the likelihood / alpha_ss reduction (side stream).  With ``newton_key`` = (estimate_alpha,
-        num_docs) the M-step follows in the same launch sequence (single-rank fused EM iteration):
-        alpha Newton on the side stream right after the reduction, beta on the main stream."""
+        num_docs) the M-step and the EM convergence test follow in the same launch sequence
+        (single-rank fused EM iteration): alpha Newton on the side stream right after the reduction,
+        beta on the main stream.  Every kernel is gated on params[DONE] (device-side convergence)."""
         from ...ops import hip as H
         dc = self.dc
         prm = self._params
+        gate = self._gate
         a = self.alpha
         main = torch.cuda.current_stream(self.device)
         streams = [main] + self._streams
@@ -341,52 +361,42 @@ class LDAEngine:
                 self._launch_scalars(newton_key)
         else:
             self._launch_scalars(newton_key)
-        # sufficient statistics: deterministic CSC gather-reduce; every word row is written
-        # (empty words included), so cw needs no clearing
-        for var, order in self.word_buckets.plan:
-            H.lda_suffstats(dc.word_ptr, dc.csc_ent, dc.csc_doc, order, self.e, self.r, self.beta, self.cw, var)
-        if newton_key is not None:
-            self._launch_beta()
+        # sufficient statistics: one deterministic CSC gather-reduce launch over every word (empty
+        # words included, so cw needs no clearing) + per-workgroup column sums -> class totals
+        sp = self.suff_plan
+        H.lda_suffstats_fused(dc.word_ptr, dc.csc_ent, dc.csc_doc, sp, self.e, self.r, self.beta, self._cw_local,
+                              self._suff_part, gate=gate)
+        H.colsum_partials(self._suff_part, sp.n_blocks, self._red_local[2:], gate=gate)
         if side is not None:
             self._ev_side.record(side)
             main.wait_event(self._ev_side)
+        if self._distributed:
+            # all-reduce inputs (see __init__): the collectives then run on self.cw / self._red
+            self.cw.copy_(self._cw_local)
+            self._red.copy_(self._red_local)
+        if newton_key is not None:
+            self._launch_beta_control()
 
     def _launch_scalars(self, newton_key):
         from ...ops import hip as H
-        H.sum2(self.lik, self.ass, self._scalars[:2], self._red_scratch2)
+        H.sum2(self.lik, self.ass, self._red_local[:2], self._red_scratch2, gate=self._gate)
         if newton_key is not None:
-            H.alpha_newton(self._scalars[:2], newton_key[1], self.K, newton_key[0], self._params, self._scalars[2:3])
+            H.alpha_newton(self._scalars, newton_key[1], self.K, newton_key[0], self._params, self._alpha_dummy)
 
-    def _launch_beta(self):
+    def _launch_beta_control(self):
         from ...ops import hip as H
-        H.colsum(self.cw, self.class_total, self._red_scratch)
-        H.lda_mstep(self.cw, self.class_total, self.beta, self.K)
+        H.lda_mstep_control(self.cw, self.class_total, self.beta, self.K, self._scalars, self._params, self._ctl,
+                            self._hist, self._done_count)
 
     def _launch_mstep(self, estimate_alpha: bool, num_docs: int):
-        """M-step on the device after the cross-rank all-reduce: class totals + beta (main stream)
-        alongside the alpha Newton (side stream) -> next E-step params."""
+        """M-step on the device after the cross-rank all-reduce: alpha Newton, then beta and the
+        EM convergence step (fused kernel)."""
         from ...ops import hip as H
-        main = torch.cuda.current_stream(self.device)
-        side = self._streams[0] if self._streams else None
-        if side is None:
-            self._launch_beta()
-            H.alpha_newton(self._scalars[:2], num_docs, self.K, estimate_alpha, self._params, self._scalars[2:3])
-            return
-        self._ev_red.record(main)
-        side.wait_event(self._ev_red)
-        with torch.cuda.stream(side):
-            H.alpha_newton(self._scalars[:2], num_docs, self.K, estimate_alpha, self._params, self._scalars[2:3])
-        self._launch_beta()
-        self._ev_side.record(side)
-        main.wait_event(self._ev_side)
+        H.alpha_newton(self._scalars, num_docs, self.K, estimate_alpha, self._params, self._alpha_dummy)
+        self._launch_beta_control()
 
     def em_iteration(self, estimate_alpha: bool, num_docs: int):
-        """One device-resident EM iteration (hip backend).
-
-        Single rank: one hipGraph holds the whole iteration (E-step, suff-stats, M-step, alpha).
-        Several ranks: E-step graph -> RCCL all-reduce of (class_word, scalars) -> M-step graph.
-        alpha and the lgamma constant never leave the device between iterations; the host reads back
-        (likelihood, alpha_ss, alpha) once, for the convergence test.  Returns (likelihood, alpha_ss)."""
+        """One EM iteration (E-step, [all-reduce], M-step, alpha).  Returns (likelihood, alpha_ss)."""
         if self.backend != "hip":
             sc = self.e_step()
             if self.dist is not None and self.dist.world_size > 1:
@@ -394,52 +404,95 @@ class LDAEngine:
             host = sc.cpu().tolist()
             self.m_step(estimate_alpha, float(host[1]), num_docs)
             return float(host[0]), float(host[1])
+        rec = self.em_iterations(1, estimate_alpha, num_docs, stop=False)[0]
+        return rec[0], rec[4]
+
+    def em_iterations(self, n: int, estimate_alpha: bool, num_docs: int, likelihood_old: float = 0.0,
+                      iteration: int = 0, stop: bool = True, em_converged: Optional[float] = None,
+                      em_max_iter: Optional[int] = None) -> List[tuple]:
+        """Run up to ``n`` EM iterations with the lda-c convergence test evaluated on the device.
+
+        hip backend: the host enqueues the n iterations (one hipGraph replay each on one rank; E-step
+        graph -> RCCL all-reduce -> M-step graph on several) without waiting; after the iteration that
+        ends the lda-c loop (``stop``), em_control sets params[DONE] and the kernels of the remaining
+        queued iterations return at once.  One read-back per batch returns the executed iterations as
+        (likelihood, conv, alpha, var_max_iter, alpha_ss); self.alpha / self.var_max_iter follow the
+        last one.  ``likelihood_old`` / ``iteration`` are the loop state before the batch."""
+        from ...ops import hip as H
+        st = self.settings
+        emc = st.em_converged if em_converged is None else em_converged
+        emx = st.em_max_iter if em_max_iter is None else em_max_iter
+        if self.backend != "hip":
+            recs = []
+            L_old, i = likelihood_old, iteration
+            for _ in range(n):
+                lik, ass = self.em_iteration(estimate_alpha, num_docs)
+                i += 1
+                conv = _conv(L_old, lik)
+                if conv < 0:
+                    self.var_max_iter = self.var_max_iter * 2
+                L_old = lik
+                recs.append((lik, conv, self.alpha, self.var_max_iter, ass))
+                if stop and not _em_continue(conv, i, emc, emx):
+                    break
+            return recs
+        if n > self._hist_cap:
+            raise ValueError(f"batch of {n} EM iterations > history capacity {self._hist_cap}")
         if self._pushed != (self.alpha, self.var_max_iter):   # host changed alpha / VAR_MAX_ITER
             self._push_params()
-        key = (bool(estimate_alpha), int(num_docs))
-        distributed = self.dist is not None and self.dist.world_size > 1
-        if not distributed:
-            if not self.use_graph:
-                self._launch_estep(newton_key=key)
-            elif self._fgraph_key != key:
-                self._fgraph = self._capture(lambda: self._launch_estep(newton_key=key))
-                self._fgraph_key = key
-            else:
-                self._fgraph.replay()
         else:
-            if self.use_graph and self._graph is None:
-                self._capture_estep()             # its warm-up launch is this iteration's E-step
-            elif self.use_graph:
-                self._graph.replay()
+            self._gate.zero_()
+        self._ctl.copy_(torch.tensor([likelihood_old, emc, 0.0, float(iteration), float(emx),
+                                      1.0 if stop else 0.0, 0.0, 0.0], dtype=torch.float64))
+        key = (bool(estimate_alpha), int(num_docs))
+        for _ in range(n):
+            if not self._distributed:
+                if not self.use_graph:
+                    self._launch_estep(newton_key=key)
+                elif self._fgraph_key != key:
+                    self._fgraph = self._capture(lambda: self._launch_estep(newton_key=key))
+                    self._fgraph_key = key
+                else:
+                    self._fgraph.replay()
             else:
-                self._launch_estep()
-            self.dist.allreduce_suffstats(self.cw, self._scalars)
-            if not self.use_graph:
-                self._launch_mstep(*key)
-            elif self._mgraph_key != key:
-                self._mgraph = self._capture(lambda: self._launch_mstep(*key))
-                self._mgraph_key = key
-            else:
-                self._mgraph.replay()
-        self._out_host.copy_(self._scalars, non_blocking=True)
+                if self.use_graph and self._graph is None:
+                    self._capture_estep()             # its warm-up launch is this iteration's E-step
+                elif self.use_graph:
+                    self._graph.replay()
+                else:
+                    self._launch_estep()
+                self.dist.allreduce_suffstats(self.cw, self._red)
+                if not self.use_graph:
+                    self._launch_mstep(*key)
+                elif self._mgraph_key != key:
+                    self._mgraph = self._capture(lambda: self._launch_mstep(*key))
+                    self._mgraph_key = key
+                else:
+                    self._mgraph.replay()
+        m = 8 + H.HIST_COLS * n
+        self._out_host[:m].copy_(self._ctlhist[:m], non_blocking=True)
         self._out_ev.record()
         self._out_ev.synchronize()
-        lik, ass, alpha = self._out_host.tolist()
-        if lik != lik:
+        out = self._out_host[:m].tolist()
+        done = int(out[2])
+        rows = [tuple(out[8 + H.HIST_COLS * j: 8 + H.HIST_COLS * j + 5]) for j in range(min(done, n))]
+        recs = [(r[0], r[1], r[2], int(r[3]), r[4]) for r in rows]
+        if any(r[0] != r[0] for r in recs):
             self._check_split_error()
-        self.alpha = alpha
+        if recs:
+            self.alpha, self.var_max_iter = recs[-1][2], recs[-1][3]
         self._pushed = (self.alpha, self.var_max_iter)
-        return lik, ass
+        return recs
 
     def _push_params(self):
         """Host alpha / VAR_MAX_ITER -> device parameter block.  The lgamma constant is derived
         on the device by the same code the alpha Newton uses, so a run that restarts from host
         values (resume, VAR_MAX_ITER doubling) sees bit-identical parameters."""
         from ...ops import hip as H
-        p = torch.tensor([self.alpha, 0.0, float(self.var_max_iter), float(self.settings.var_converged)],
-                         dtype=torch.float64)
+        p = torch.zeros(H.PARAM_COUNT, dtype=torch.float64)
+        p[0], p[2], p[3] = self.alpha, float(self.var_max_iter), float(self.settings.var_converged)
         self._params.copy_(p)            # pageable source: no pending read of a reused host buffer
-        H.alpha_newton(self._scalars[:2], 1.0, self.K, False, self._params, self._scalars[2:3])
+        H.alpha_newton(self._scalars, 1.0, self.K, False, self._params, self._alpha_dummy)
 
     def _check_split_error(self):
         """A NaN likelihood: if a split-document barrier timed out, fail loudly (the kernel
@@ -462,6 +515,7 @@ class LDAEngine:
     def _capture_estep(self):
         self._graph = self._capture(self._launch_estep)
 
+
     def _build_schedule(self):
         """Assign E-step work to streams (critical path first): [side 1: split batches],
         [side 2: B8 + B4], [side 3: G64C/G64/G32], [main: thread-per-document bulk]."""
@@ -476,8 +530,11 @@ class LDAEngine:
         long_work = [("bucket", (v, o)) for v, o in plan if v in long_vars]
         mid_work = [("bucket", (v, o)) for v, o in plan if v not in long_vars and v not in tiny_vars]
         tiny_work = [("bucket", (v, o)) for v, o in plan if v in tiny_vars]
+        b8_work = [w for w in long_work if w[1][0] == H.ESTEP_B8]
+        b4_work = [w for w in long_work if w[1][0] != H.ESTEP_B8]
         if nstreams >= 4:
-            sched[1], sched[2], sched[3], sched[0] = split_work, long_work, mid_work, tiny_work
+            # B4 queues behind the split batches: B8 alone is about as long as split + B4
+            sched[1], sched[2], sched[3], sched[0] = split_work + b4_work, b8_work, mid_work, tiny_work
         elif nstreams == 3:
             sched[1], sched[2], sched[0] = split_work, long_work, mid_work + tiny_work
         elif nstreams == 2:
@@ -537,31 +594,39 @@ class LDAEngine:
         hist = []
         stats = []
         n_docs_global = self.global_docs
-        while ((conv < 0) or (conv > st.em_converged) or (i <= 2)) and (i <= st.em_max_iter):
-            i += 1
+        per_iter_stats = verbose or self.collect_iter_stats   # an extra D2H copy per iteration: opt-in
+        while _em_continue(conv, i, st.em_converged, st.em_max_iter):
+            # One batch = the iterations up to the next LAG save (the saved state must be that
+            # iteration's), at most max_batch; the device stops the batch itself on convergence.
+            n = 1 if per_iter_stats else self.max_batch
+            if on_save is not None:
+                n = min(n, LAG - (i % LAG))
+            n = max(1, min(n, st.em_max_iter - i + 1))
             ti = time.perf_counter()
-            range_push(f"em_iter_{i}")
-            lik, ass = self.em_iteration(st.estimate_alpha, n_docs_global)
+            range_push(f"em_iters_{i + 1}_{i + n}")
+            recs = self.em_iterations(n, st.estimate_alpha, n_docs_global, likelihood_old=L_old, iteration=i)
             range_pop()
-            conv = (L_old - lik) / L_old if L_old != 0 else (math.inf if lik < 0 else (-math.inf if lik > 0 else math.nan))
-            if conv < 0:
-                self.var_max_iter = self.var_max_iter * 2
-            L_old = lik
-            hist.append((lik, conv))
-            if verbose or self.collect_iter_stats:   # an extra D2H copy per iteration: opt-in
+            dt = (time.perf_counter() - ti) / max(len(recs), 1)
+            if per_iter_stats:
                 it_np = self.iters.cpu().numpy() if isinstance(self.iters, torch.Tensor) else np.asarray(self.iters)
                 it_mean = float(it_np.mean()) if it_np.size else 0.0
                 it_max = int(it_np.max()) if it_np.size else 0
             else:
                 it_mean, it_max = -1.0, -1
-            stt = EMIterStats(i, lik, conv, self.alpha, time.perf_counter() - ti, it_mean, it_max, self.var_max_iter)
-            stats.append(stt)
-            if verbose:
-                print(f"**** em iteration {i} **** L={lik:.6f} conv={conv:.5e} alpha={self.alpha:.5f} "
-                      f"var_iters(mean/max)={stt.var_iter_mean:.2f}/{stt.var_iter_max} {stt.seconds*1e3:.2f} ms",
-                      flush=True)
-            if on_iteration is not None:
-                on_iteration(self, i, lik, conv)
+            for lik, conv, alpha, vmi, _ass in recs:
+                i += 1
+                L_old = lik
+                hist.append((lik, conv))
+                stt = EMIterStats(i, lik, conv, alpha, dt, it_mean, it_max, vmi)
+                stats.append(stt)
+                if verbose:
+                    print(f"**** em iteration {i} **** L={lik:.6f} conv={conv:.5e} alpha={alpha:.5f} "
+                          f"var_iters(mean/max)={stt.var_iter_mean:.2f}/{stt.var_iter_max} {dt*1e3:.2f} ms",
+                          flush=True)
+                if on_iteration is not None:
+                    on_iteration(self, i, lik, conv)
+            if not recs:
+                break
             if on_save is not None and (i % LAG) == 0:
                 on_save(f"{i:03d}", self)
         if on_save is not None:
@@ -569,3 +634,15 @@ class LDAEngine:
         res = LDAResult(log_beta=None, gamma=None, alpha=self.alpha, num_topics=self.K, num_terms=self.V,
                         likelihoods=hist, stats=stats, em_iterations=i, seconds=time.perf_counter() - t0)
         return res
+
+
+def _conv(L_old: float, lik: float) -> float:
+    """lda-c: converged = (likelihood_old - likelihood) / likelihood_old (IEEE semantics at 0)."""
+    if L_old != 0:
+        return (L_old - lik) / L_old
+    return math.inf if lik < 0 else (-math.inf if lik > 0 else math.nan)
+
+
+def _em_continue(conv: float, i: int, em_converged: float, em_max_iter: int) -> bool:
+    """lda-c run_em loop condition after iteration i."""
+    return ((conv < 0) or (conv > em_converged) or (i <= 2)) and (i <= em_max_iter)

@@ -187,11 +187,21 @@ def lda_estep_split(doc_ptr, word_idx, counts, beta, K, alpha, lik_const, var_ma
         _params_ptr(params, dev), _stream())
 
 
+PARAM_COUNT = 8      # device parameter block (csrc/hip/kernels.h kParamCount)
+PARAM_DONE = 4       # params[PARAM_DONE] != 0: the EM loop converged, kernels skip
+HIST_COLS = 6        # em_control history row: likelihood, conv, alpha, VAR_MAX_ITER, alpha_ss, -
+
+
 def _params_ptr(params, dev) -> int:
-    return 0 if params is None else _chk(params, torch.float64, "params", (4,), dev)
+    return 0 if params is None else _chk(params, torch.float64, "params", (PARAM_COUNT,), dev)
 
 
-def lda_suffstats(word_ptr, csc_ent, csc_doc, order, e, r, beta, cw, variant):
+def _gate_ptr(gate, dev) -> int:
+    """Pointer to a float64 flag (e.g. params[PARAM_DONE:PARAM_DONE+1]) or 0."""
+    return 0 if gate is None else _chk(gate, torch.float64, "gate", (1,), dev)
+
+
+def lda_suffstats(word_ptr, csc_ent, csc_doc, order, e, r, beta, cw, variant, gate=None):
     V, KS = beta.shape
     nnz = csc_ent.numel()
     D = e.shape[0]
@@ -206,22 +216,88 @@ def lda_suffstats(word_ptr, csc_ent, csc_doc, order, e, r, beta, cw, variant):
         _chk(r, torch.float32, "r", (nnz,), dev),
         _chk(beta, torch.float32, "beta", (V, KS), dev),
         _chk(cw, torch.float32, "cw", (V, KS), dev),
-        int(KS), int(variant), _stream(),
+        int(KS), int(variant), _gate_ptr(gate, dev), _stream(),
     ]
     if order.numel() == 0:
         return
     lib().lda_suffstats(*args)
 
 
+class SuffPlan:
+    """Word order for the single-launch suff-stats kernel: [heavy | medium | light] (heavy first)."""
+    HEAVY, LIGHT = 1024, 64
+
+    def __init__(self, word_len, device):
+        import numpy as np
+        order = np.argsort(-np.asarray(word_len), kind="stable").astype(np.int32)
+        L = np.asarray(word_len)[order]
+        self.n_heavy = int((L > self.HEAVY).sum())
+        self.n_medium = int(((L > self.LIGHT) & (L <= self.HEAVY)).sum())
+        self.n_light = int((L <= self.LIGHT).sum())
+        self.order = torch.from_numpy(order).to(device)
+        self.n_blocks = int(lib().suff_fused_blocks(self.n_heavy, self.n_medium, self.n_light))
+
+
+def lda_suffstats_fused(word_ptr, csc_ent, csc_doc, plan: "SuffPlan", e, r, beta, cw, part, gate=None):
+    """class_word for every word (one launch) + per-workgroup column sums into part [n_blocks, KS]."""
+    V, KS = beta.shape
+    nnz = csc_ent.numel()
+    D = e.shape[0]
+    dev = beta.device
+    if plan.order.numel() != V:
+        raise ValueError("suff plan does not cover the vocabulary")
+    lib().lda_suffstats_fused(
+        _chk(word_ptr, torch.int32, "word_ptr", (V + 1,), dev), _chk(csc_ent, torch.int32, "csc_ent", (nnz,), dev),
+        _chk(csc_doc, torch.int32, "csc_doc", (nnz,), dev), _chk(plan.order, torch.int32, "order", (V,), dev),
+        plan.n_heavy, plan.n_medium, plan.n_light,
+        _chk(e, torch.float32, "e", (D, KS), dev), _chk(r, torch.float32, "r", (nnz,), dev),
+        _chk(beta, torch.float32, "beta", (V, KS), dev), _chk(cw, torch.float32, "cw", (V, KS), dev),
+        _chk(part, torch.float64, "part", (max(plan.n_blocks, 1), KS), dev), int(KS), _gate_ptr(gate, dev), _stream())
+
+
+def colsum_partials(part, n_blocks, out, gate=None):
+    """out[k] = sum_b part[b, k] for b < n_blocks (deterministic order)."""
+    dev = part.device
+    cols = part.shape[1]
+    if n_blocks > part.shape[0]:
+        raise ValueError("n_blocks exceeds partial rows")
+    lib().colsum_partials(_chk(part, torch.float64, "part", None, dev), int(n_blocks), int(cols),
+                          _chk(out, torch.float64, "out", (cols,), dev), _gate_ptr(gate, dev), _stream())
+
+
+def lda_mstep_control(cw, class_total, beta, K, scalars, params, ctl, hist, done_count):
+    """M-step (beta = cw / class_total) + the device EM convergence step in the last workgroup."""
+    V, KS = cw.shape
+    dev = cw.device
+    slots = hist.numel() // HIST_COLS
+    lib().lda_mstep_control(
+        _chk(cw, torch.float32, "cw", (V, KS), dev), _chk(class_total, torch.float64, "class_total", (KS,), dev),
+        _chk(beta, torch.float32, "beta", (V, KS), dev), int(V), int(K), int(KS),
+        _chk(scalars, torch.float64, "scalars", (2,), dev), _chk(params, torch.float64, "params", (PARAM_COUNT,), dev),
+        _chk(ctl, torch.float64, "ctl", (8,), dev), _chk(hist, torch.float64, "hist", (slots * HIST_COLS,), dev),
+        int(slots), _chk(done_count, torch.int32, "done_count", (1,), dev), _stream())
+
+
 def alpha_newton(scalars, num_docs, K, estimate, params, alpha_out):
     """Device lda-c opt_alpha: params[0:2] <- (alpha, lgamma(K alpha) - K lgamma(alpha))."""
     dev = params.device
     lib().alpha_newton(_chk(scalars, torch.float64, "scalars", (2,), dev), float(num_docs), int(K), bool(estimate),
-                       _chk(params, torch.float64, "params", (4,), dev),
+                       _chk(params, torch.float64, "params", (PARAM_COUNT,), dev),
                        _chk(alpha_out, torch.float64, "alpha_out", (1,), dev), _stream())
 
 
-def colsum(mat, out, scratch):
+def em_control(scalars, params, ctl, hist):
+    """Device EM convergence test after one iteration (csrc/hip/em_control.hip)."""
+    dev = params.device
+    slots = hist.numel() // HIST_COLS
+    lib().em_control(_chk(scalars, torch.float64, "scalars", (2,), dev),
+                     _chk(params, torch.float64, "params", (PARAM_COUNT,), dev),
+                     _chk(ctl, torch.float64, "ctl", (8,), dev),
+                     _chk(hist, torch.float64, "hist", (slots * HIST_COLS,), dev),
+                     int(slots), _stream())
+
+
+def colsum(mat, out, scratch, gate=None):
     """out[k] = sum_r mat[r, k] (f32 -> f64, deterministic)."""
     rows, cols = mat.shape
     dev = mat.device
@@ -229,31 +305,31 @@ def colsum(mat, out, scratch):
     lib().colsum(_chk(mat, torch.float32, "mat", None, dev), int(rows), int(cols),
                  _chk(out, torch.float64, "out", (cols,), dev),
                  _chk(scratch, torch.float64, "scratch", None, dev) if scratch.numel() >= need else _bad("scratch"),
-                 _stream())
+                 _gate_ptr(gate, dev), _stream())
 
 
-def sum2(a, b, out, scratch):
+def sum2(a, b, out, scratch, gate=None):
     """out = [sum(a), sum(b)] (f64, deterministic)."""
     n = a.numel()
     dev = a.device
     lib().sum2(_chk(a, torch.float64, "a", (n,), dev), _chk(b, torch.float64, "b", (n,), dev), int(n),
                _chk(out, torch.float64, "out", (2,), dev),
                _chk(scratch, torch.float64, "scratch", None, dev) if scratch.numel() >= lib().reduce_scratch_doubles(2)
-               else _bad("scratch"), _stream())
+               else _bad("scratch"), _gate_ptr(gate, dev), _stream())
 
 
 def _bad(name):
     raise ValueError(f"{name}: buffer too small")
 
 
-def lda_mstep(cw, class_total, beta, K):
+def lda_mstep(cw, class_total, beta, K, gate=None):
     V, KS = cw.shape
     dev = cw.device
     lib().lda_mstep(
         _chk(cw, torch.float32, "cw", (V, KS), dev),
         _chk(class_total, torch.float64, "class_total", (KS,), dev),
         _chk(beta, torch.float32, "beta", (V, KS), dev),
-        int(V), int(K), int(KS), _stream(),
+        int(V), int(K), int(KS), _gate_ptr(gate, dev), _stream(),
     )
 
 

@@ -82,8 +82,9 @@ def main():
                              it_mean=round(float(it[o].mean()), 2), it_max=int(it[o].max()), ms=round(ms, 4)))
 
         def suff():
-            for var, order in eng.word_buckets.plan:
-                H.lda_suffstats(dc.word_ptr, dc.csc_ent, dc.csc_doc, order, eng.e, eng.r, eng.beta, eng.cw, var)
+            H.lda_suffstats_fused(dc.word_ptr, dc.csc_ent, dc.csc_doc, eng.suff_plan, eng.e, eng.r, eng.beta, eng.cw,
+                                  eng._suff_part)
+            H.colsum_partials(eng._suff_part, eng.suff_plan.n_blocks, eng.class_total)
         rows.append(dict(bucket="suffstats", ms=round(timed(suff), 4)))
         rows.append(dict(bucket="mstep", ms=round(timed(lambda: eng.m_step(False, 0.0, c.num_docs)), 4)))
 
@@ -91,6 +92,8 @@ def main():
             eng.em_iteration(True, c.num_docs)
         rows.append(dict(bucket="EM step (hipGraph)", ms=round(timed(step, 10), 4), var_max_iter=eng.var_max_iter,
                          streams=a.streams[0]))
+        rows.append(dict(bucket="EM step (hipGraph, 5 per read-back)", streams=a.streams[0],
+                         ms=round(timed(lambda: eng.em_iterations(5, True, c.num_docs, stop=False), 5) / 5, 4)))
         for ns in a.streams[1:]:
             e2 = LDAEngine(c, a.topics, LDASettings(), backend="hip", seed=0, split_min=smin, streams=ns)
             e2.init_random()
