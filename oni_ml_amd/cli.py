@@ -7,7 +7,9 @@
   lda_pre <LPATH>/                             lda_pre.py equivalent (doc_wc.dat -> words/doc/model.dat)
   lda_post <LPATH>/                            lda_post.py equivalent (final.* -> doc/word_results.csv)
   synth {flow|dns} --out DIR ...               synthetic inputs (flow CSV day, DNS parquet, top-1m.csv)
-  qtiles <flow_qtiles>                         print cuts of the legacy qtiles format
+  qtiles [show] <flow_qtiles>                  print cuts of the legacy qtiles format
+  qtiles gen <FLOW_PATH> [--out DIR]           gen_qtiles.sh + qtiles.py: sample ntile cuts -> flow_qtiles
+  install [--nodes a,b] [--dry-run]            install_ml.sh: rsync the framework to NODES:${LUSER}/ml
 
 Multi-GPU: launch with torchrun (one process per GPU); ranks share the LDA
 stage over RCCL, rank 0 runs featurization, export and scoring.
@@ -68,6 +70,10 @@ def cmd_ml_ops(argv):
     ap.add_argument("--rank-gamma", action="store_true", help="also write <rank>.gamma per GPU")
     ap.add_argument("--threads", type=int, default=8)
     ap.add_argument("--deliver", action="store_true", help="scp -r LPATH UINODE:RPATH (ml_ops.sh:121)")
+    ap.add_argument("--cuts", help="fixed flow cuts: a flow_qtiles file or its text (the reference's CUT)")
+    ap.add_argument("--hdfs", action="store_true",
+                    help="stage hdfs:// inputs locally and publish results to HPATH (ml_ops.sh HDFS steps)")
+    ap.add_argument("--hadoop", default="hadoop", help="hadoop CLI for --hdfs")
     ap.add_argument("--quiet", action="store_true")
     _common_lda_args(ap)
     a = ap.parse_args(argv)
@@ -83,7 +89,8 @@ def cmd_ml_ops(argv):
                       lpath=a.lpath, flow_path=a.flow_path, dns_path=a.dns_path, top1m=a.top1m, topics=a.topics,
                       alpha=a.alpha, dupfactor=a.dupfactor, gpus=ctx.world_size, backend=a.backend, compat=a.compat,
                       seed=a.seed, start=a.start, resume=a.resume, threads=a.threads, write_doc_wc=a.keep_doc_wc,
-                      word_assignments=a.word_assignments, rank_gamma=a.rank_gamma, verbose=not a.quiet)
+                      word_assignments=a.word_assignments, rank_gamma=a.rank_gamma, verbose=not a.quiet,
+                      cuts=a.cuts, hdfs=a.hdfs or None, hadoop=a.hadoop)
     if a.settings:
         cfg.settings = LDASettings.load(a.settings)
     cfg.validate()
@@ -199,15 +206,87 @@ def cmd_synth(argv):
 
 
 def cmd_qtiles(argv):
+    """qtiles show <flow_qtiles>  |  qtiles gen <FLOW_PATH> [--out DIR] [--sample-rows N] [--keep-tsv]
+
+    gen = gen_qtiles.sh + qtiles.py: per input file the first N data rows stand in
+    for Hive's TABLESAMPLE(N ROWS); ibyt deciles, ipkt ntile(3), time deciles -> qtiles.tsv ->
+    <out>/flow_qtiles (consumable by ml_ops --cuts / the CUT variable)."""
+    if argv and argv[0] == "gen":
+        ap = argparse.ArgumentParser(prog="qtiles gen")
+        ap.add_argument("flow_path")
+        ap.add_argument("--out", default=".")
+        ap.add_argument("--sample-rows", type=int, default=100)
+        ap.add_argument("--keep-tsv", action="store_true", help="keep qtiles.tsv (gen_qtiles.sh deletes it)")
+        a = ap.parse_args(argv[1:])
+        import numpy as np
+        from .features.flow import list_inputs
+        from .features.quantiles import gen_qtiles_tsv, qtiles_from_tsv
+        cols = {4: [], 5: [], 16: [], 17: []}          # hour, minute, ipkt, ibyt (27-column flow CSV)
+        for path in list_inputs(a.flow_path):
+            with open(path) as f:
+                header = f.readline()
+                n = 0
+                for line in f:
+                    if line == header:
+                        continue
+                    parts = line.rstrip("\n").split(",")
+                    if len(parts) != 27:
+                        continue
+                    try:
+                        vals = {c: float(parts[c]) for c in cols}
+                    except ValueError:
+                        continue
+                    for c, v in vals.items():
+                        cols[c].append(v)
+                    n += 1
+                    if n >= a.sample_rows:
+                        break
+        tsv = gen_qtiles_tsv(np.asarray(cols[17]), np.asarray(cols[16]), np.asarray(cols[4]), np.asarray(cols[5]))
+        os.makedirs(a.out, exist_ok=True)
+        if a.keep_tsv:
+            with open(os.path.join(a.out, "qtiles.tsv"), "w") as f:
+                f.write(tsv)
+        out = os.path.join(a.out, "flow_qtiles")
+        with open(out, "w") as f:
+            f.write(qtiles_from_tsv(tsv))
+        print(out)
+        return 0
     from .features.quantiles import parse_qtiles
-    with open(argv[0]) as f:
+    path = argv[1] if argv and argv[0] == "show" else argv[0]
+    with open(path) as f:
         q = parse_qtiles(f.read())
     print(json.dumps({k: v.tolist() for k, v in q.items()}))
     return 0
 
 
+def cmd_install(argv):
+    """install_ml.sh: rsync the framework (dot-files excluded) to every node in NODES:${LUSER}/ml."""
+    ap = argparse.ArgumentParser(prog="install")
+    ap.add_argument("--conf", default=os.environ.get("ONI_CONF", "/etc/duxbay.conf"))
+    ap.add_argument("--nodes", help="comma-separated node list (default: NODES from the config)")
+    ap.add_argument("--luser", help="remote base dir (default: LUSER from the config)")
+    ap.add_argument("--src", default=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    ap.add_argument("--dry-run", action="store_true", help="print the rsync commands only")
+    a = ap.parse_args(argv)
+    from . import config as CFG
+    cfg = CFG.resolve("00000000", "flow", conf_path=a.conf)
+    nodes = a.nodes.split(",") if a.nodes else cfg.extra.get("NODES") or []
+    if isinstance(nodes, str):
+        nodes = nodes.split()
+    luser = a.luser or cfg.extra.get("LUSER")
+    if not nodes or not luser:
+        print("install: NODES and LUSER are required (config or --nodes/--luser)", file=sys.stderr)
+        return 1
+    for d in nodes:
+        cmd = ["rsync", "-v", "-a", "--exclude=.*", a.src.rstrip("/") + "/", f"{d}:{luser}/ml"]
+        print(" ".join(cmd))
+        if not a.dry_run:
+            subprocess.run(cmd, check=True)
+    return 0
+
+
 COMMANDS = dict(ml_ops=cmd_ml_ops, lda=cmd_lda, lda_pre=cmd_lda_pre, lda_post=cmd_lda_post, synth=cmd_synth,
-                qtiles=cmd_qtiles)
+                qtiles=cmd_qtiles, install=cmd_install)
 
 
 def main(argv=None):

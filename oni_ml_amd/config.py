@@ -26,7 +26,7 @@ from typing import Dict, List, Optional
 from .models.lda.settings import LDASettings
 
 ENV_KEYS = ("FLOW_PATH", "DNS_PATH", "HPATH", "LPATH", "LUSER", "TOL", "DUPFACTOR", "KRB_AUTH", "NODES", "UINODE",
-            "RPATH", "LDAPATH", "SPK_EXEC", "SPK_EXEC_MEM", "TOP1M")
+            "RPATH", "LDAPATH", "SPK_EXEC", "SPK_EXEC_MEM", "TOP1M", "CUT")
 
 _VAR = re.compile(r"\$\{([A-Za-z_][A-Za-z0-9_]*)\}|\$([A-Za-z_][A-Za-z0-9_]*)")
 
@@ -97,8 +97,23 @@ class RunConfig:
     word_assignments: bool = False
     rank_gamma: bool = False
     verbose: bool = True
+    cuts: str = ""                        # fixed flow cuts in flow_qtiles form ("ibyt,ipkt,time"; the
+                                          # reference's commented-out CUT consumer, flow_pre_lda.scala:95-98)
+    hdfs: bool = False                    # stage hdfs:// inputs locally and publish results to HPATH
+    hadoop: str = "hadoop"                # hadoop CLI used for the HDFS steps
     settings: LDASettings = field(default_factory=LDASettings)
     extra: Dict[str, object] = field(default_factory=dict)
+
+    def fixed_cuts(self):
+        """Cuts from `cuts` (flow_qtiles text or a path to such a file), else None."""
+        if not self.cuts:
+            return None
+        from .features.quantiles import parse_qtiles
+        text = self.cuts
+        if os.path.exists(text):
+            with open(text) as f:
+                text = f.read()
+        return parse_qtiles(text)
 
     @property
     def strict(self) -> bool:
@@ -163,6 +178,8 @@ def _apply(cfg: RunConfig, layer: Dict[str, object]):
         cfg.tol = float(layer["TOL"])
     if "DUPFACTOR" in layer and layer["DUPFACTOR"] not in ("", None):
         cfg.dupfactor = int(layer["DUPFACTOR"])
+    if "CUT" in layer and isinstance(layer["CUT"], str) and layer["CUT"].strip():
+        cfg.cuts = layer["CUT"]
     for k in ("NODES", "UINODE", "RPATH", "LDAPATH", "LUSER", "KRB_AUTH", "SPK_EXEC", "SPK_EXEC_MEM"):
         if k in layer:
             cfg.extra[k] = layer[k]

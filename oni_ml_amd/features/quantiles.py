@@ -97,3 +97,71 @@ def dump_qtiles(ibyt, ipkt, time) -> str:
             out.append(str(int(x)) if x.is_integer() else repr(x))
         return " ".join(out)
     return ",".join(fmt(a) for a in (ibyt, ipkt, time))
+
+
+# ---------------------------------------------------------------------------
+# gen_qtiles.sh + qtiles.py (reference gen_qtiles.sh:9-19, qtiles.py:9-21)
+# ---------------------------------------------------------------------------
+def hive_ntile_max(values, n: int, order_key=None):
+    """``SELECT max(v), qtile FROM (SELECT v, ntile(n) OVER (ORDER BY key) AS qtile ...) GROUP BY qtile``.
+
+    Hive's ntile puts rows (ordered by ``order_key``, default the values) into n buckets whose
+    sizes differ by at most one, the first N mod n buckets holding the extra row; with fewer
+    rows than buckets every row is its own bucket.  Returns [(max, tile)] in tile order."""
+    v = np.asarray(values, np.float64)
+    key = v if order_key is None else np.asarray(order_key)
+    N = v.size
+    if N == 0:
+        return []
+    order = np.lexsort(key.T[::-1]) if key.ndim == 2 else np.argsort(key, kind="stable")
+    vs = v[order]
+    tiles = min(n, N)
+    base, extra = divmod(N, tiles)
+    out, start = [], 0
+    for t in range(tiles):
+        size = base + (1 if t < extra else 0)
+        out.append((float(vs[start:start + size].max()), t + 1))
+        start += size
+    return out
+
+
+def _hive_num(x: float, integral: bool) -> str:
+    """Hive CLI rendering: bigint columns as integers, double columns as Java Double.toString."""
+    from ..io.javafmt import java_double
+    return str(int(x)) if integral else java_double(x)
+
+
+def gen_qtiles_tsv(ibyt, ipkt, hour, minute) -> str:
+    """qtiles.tsv of gen_qtiles.sh: ibyt deciles, ipkt ntile(3), time deciles over (hour, minute),
+    one ``max<TAB>qtile`` line per tile; a ``|`` line separates the three queries (the separator
+    qtiles.py splits groups on)."""
+    hour = np.asarray(hour, np.float64)
+    minute = np.asarray(minute, np.float64)
+    dectime = hour + minute / 60.0
+    groups = [
+        [(_hive_num(m, True), t) for m, t in hive_ntile_max(ibyt, 10)],
+        [(_hive_num(m, True), t) for m, t in hive_ntile_max(ipkt, 3)],
+        [(_hive_num(m, False), t) for m, t in hive_ntile_max(dectime, 10, np.stack([hour, minute], 1))],
+    ]
+    lines = []
+    for gi, g in enumerate(groups):
+        if gi:
+            lines.append("|")
+        lines.extend(f"{m}\t{t}" for m, t in g)
+    return "\n".join(lines) + "\n"
+
+
+def qtiles_from_tsv(tsv: str) -> str:
+    """qtiles.py: "0 " then each first column + " "; a "|" row closes the group with ",0 "."""
+    import csv
+    import io
+    out = "0 "
+    for row in csv.reader(io.StringIO(tsv), delimiter="\t", quotechar='"'):
+        if not row:
+            continue
+        if row[0] == "|":
+            out = out[:-1]
+            out += ",0 "
+        else:
+            out += "%s " % (row[0])
+    return out

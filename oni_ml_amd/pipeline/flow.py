@@ -49,7 +49,7 @@ def run(cfg, dist=None, device=None, log=print) -> dict:
     if need_pre:
         if rank == 0:
             with R.stage("flow_pre") as res:
-                feat = FF.featurize(ft, device)
+                feat = FF.featurize(ft, device, cuts=cfg.fixed_cuts())
                 ws = FF.word_space_for(feat)
                 src, dst = FF.word_keys(feat, ws)
                 dwc = concat([count_pairs(feat.sip, src, feat.weight), count_pairs(feat.dip, dst, feat.weight)],
@@ -121,8 +121,8 @@ def run(cfg, dist=None, device=None, log=print) -> dict:
 
 def score_flow(cfg, ft: FF.FlowTable, tables: C.ModelTables, device, log=print) -> dict:
     """flow_post_lda.scala: features of raw rows, θ·φ per side, min, < TOL, ascending, 37-column rows."""
-    cuts = None
-    if not cfg.strict:
+    cuts = cfg.fixed_cuts()          # fixed CUT cuts apply to both stages (flow_pre_lda.scala:95-98)
+    if cuts is None and not cfg.strict:
         saved = C.load_json(os.path.join(cfg.lpath, "flow_cuts.json"))
         cuts = {k: np.asarray(v, np.float64) for k, v in saved["cuts"].items()}
     feat = FF.featurize(ft, device, cuts=cuts, raw_only=True)

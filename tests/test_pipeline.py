@@ -173,3 +173,69 @@ def test_cli_end_to_end_and_lda_est(tmp_path):
                        capture_output=True, text=True)
     assert r.returncode == 0, r.stderr[-2000:]
     assert (tmp_path / "lda" / "word_results.csv").exists()
+
+
+def test_hive_ntile_semantics():
+    from oni_ml_amd.features.quantiles import hive_ntile_max
+    rng = np.random.default_rng(3)
+    for N, n in [(100, 10), (101, 10), (7, 3), (2, 10), (1, 3)]:
+        v = rng.integers(0, 50, N).astype(float)
+        got = hive_ntile_max(v, n)
+        # literal ntile: row i (0-based, sorted) goes to tile 1 + i // ceil-ish split
+        s = np.sort(v, kind="stable")
+        tiles = min(n, N)
+        base, extra = divmod(N, tiles)
+        tile_of = []
+        for t in range(tiles):
+            tile_of += [t + 1] * (base + (t < extra))
+        want = [(max(s[i] for i in range(N) if tile_of[i] == t), t) for t in range(1, tiles + 1)]
+        assert got == want
+
+
+def test_qtiles_gen_cli_and_fixed_cuts(tmp_path):
+    """gen_qtiles.sh + qtiles.py -> flow_qtiles, then a run with those fixed cuts (the CUT consumer)."""
+    from oni_ml_amd.cli import main
+    from oni_ml_amd.features.quantiles import parse_qtiles
+    cfg = _flow_cfg(tmp_path)
+    assert main(["qtiles", "gen", cfg.flow_path, "--out", str(tmp_path / "q"), "--keep-tsv"]) == 0
+    text = (tmp_path / "q" / "flow_qtiles").read_text()
+    q = parse_qtiles(text)
+    assert q["ibyt"][0] == 0 and len(q["ibyt"]) == 11 and len(q["ipkt"]) == 4 and len(q["time"]) == 11
+    assert all(np.diff(q[k]).min() >= 0 for k in q)
+    tsv = (tmp_path / "q" / "qtiles.tsv").read_text().splitlines()
+    assert tsv.count("|") == 2 and tsv[0].endswith("\t1")
+    cfg.cuts = str(tmp_path / "q" / "flow_qtiles")
+    run(cfg, device="cpu", log=lambda *a, **k: None)
+    saved = json.loads((tmp_path / "ml" / "flow_cuts.json").read_text())["cuts"]
+    for k in ("ibyt", "ipkt", "time"):
+        assert saved[k] == q[k].tolist()
+
+
+def test_cut_environment_variable():
+    c = CFG.resolve("20160122", "flow", conf_path=None, environ={"CUT": "0 10 20,0 1,0 5.5", "FLOW_PATH": "/x",
+                                                                   "LPATH": "/y"})
+    assert c.fixed_cuts()["time"].tolist() == [0.0, 5.5]
+
+
+def test_install_dry_run(tmp_path, capsys):
+    from oni_ml_amd.cli import main
+    conf = tmp_path / "duxbay.conf"
+    conf.write_text('NODES=(node01 node02)\nLUSER=/home/oni\n')
+    assert main(["install", "--conf", str(conf), "--dry-run"]) == 0
+    out = capsys.readouterr().out.splitlines()
+    assert len(out) == 2 and out[0].startswith("rsync -v -a --exclude=.* ") and out[1].endswith("node02:/home/oni/ml")
+
+
+def test_hdfs_hooks_command_sequence(tmp_path):
+    from oni_ml_amd.io.hdfs import Hdfs
+    calls = []
+    h = Hdfs("hadoop", runner=lambda cmd: calls.append(cmd))
+    local = h.stage_inputs("hdfs://nn/flow/2016/01/22,/local/x", str(tmp_path / "st"))
+    assert local.split(",")[1] == "/local/x" and local.split(",")[0].endswith("in000")
+    assert calls[0][:3] == ["hadoop", "fs", "-copyToLocal"] and calls[0][3] == "hdfs://nn/flow/2016/01/22/*"
+    calls.clear()
+    h.publish("/lp", "/hp", "flow")
+    flat = [" ".join(c[2:]) for c in calls]
+    assert flat == ["-rm /hp/doc_results.csv", "-put /lp/doc_results.csv /hp/.", "-rm /hp/word_results.csv",
+                    "-put /lp/word_results.csv /hp/.", "-rm -R -f /hp/word_counts", "-rm -R -f /hp/scored",
+                    "-mkdir -p /hp/scored", "-put /lp/flow_results.csv /hp/scored/part-00000"]
