@@ -8,8 +8,10 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
+#include <charconv>
 #include <thread>
 
+#include "corpus_io.h"
 #include "dns.h"
 #include "fmt.h"
 #include "lda_ref.h"
@@ -237,7 +239,7 @@ PYBIND11_MODULE(_oninative, m) {
           s.clear();
           if (mode == 0) append_fixed10(s, src[i]);
           else append_py2_float(s, src[i]);
-          dst[i] = std::strtod(s.c_str(), nullptr);
+          std::from_chars(s.data(), s.data() + s.size(), dst[i]);
         }
       };
       std::vector<std::thread> th;
@@ -253,6 +255,37 @@ PYBIND11_MODULE(_oninative, m) {
   m.def("roundtrip_py2", [roundtrip](py::array_t<double, py::array::c_style | py::array::forcecast> a, int threads) {
     return roundtrip(a, 1, threads);
   }, py::arg("a"), py::arg("threads") = 0);
+
+  // lda-c corpus text (model.dat)
+  m.def(
+      "write_ldac_corpus",
+      [](const std::string& path, py::array_t<int64_t, py::array::c_style | py::array::forcecast> ptr,
+         py::array_t<int32_t, py::array::c_style | py::array::forcecast> words,
+         py::array_t<int64_t, py::array::c_style | py::array::forcecast> counts, int threads) {
+        const int64_t D = (int64_t)ptr.size() - 1;
+        if (D < 0) throw std::invalid_argument("doc_ptr must have D+1 entries");
+        const int64_t* p = ptr.data();
+        if (p[0] != 0 || p[D] != (int64_t)words.size() || words.size() != counts.size())
+          throw std::invalid_argument("inconsistent corpus arrays");
+        for (int64_t d = 0; d < D; ++d)
+          if (p[d] > p[d + 1]) throw std::invalid_argument("non-monotone doc_ptr");
+        if (threads <= 0) threads = default_threads();
+        py::gil_scoped_release rel;
+        return write_corpus_text(path, p, D, words.data(), counts.data(), threads);
+      },
+      py::arg("path"), py::arg("doc_ptr"), py::arg("words"), py::arg("counts"), py::arg("threads") = 0);
+  m.def(
+      "read_ldac_corpus",
+      [](const std::string& path, int threads) {
+        if (threads <= 0) threads = default_threads();
+        TextCorpus c;
+        {
+          py::gil_scoped_release rel;
+          c = read_corpus_text(path, threads);
+        }
+        return py::make_tuple(to_np(c.doc_ptr), to_np(c.words), to_np(c.counts));
+      },
+      py::arg("path"), py::arg("threads") = 0);
 
   // ---------------------------------------------------------------- lda-c --
   m.def("digamma", &ldac_digamma);

@@ -69,11 +69,14 @@ inline std::string java_double(double d) {
 }
 
 // Python 2 str(float): repr-free "%.12g" plus ".0" on integral-looking output.
+// std::to_chars(general, 12) is specified as printf("%.12g") in the C locale and
+// is exact (Ryu-printf in libstdc++), ~4x faster than snprintf.
 inline void append_py2_float(std::string& out, double d) {
   if (std::isnan(d)) { out += "nan"; return; }
   if (std::isinf(d)) { out += d > 0 ? "inf" : "-inf"; return; }
   char buf[40];
-  int n = std::snprintf(buf, sizeof(buf), "%.12g", d);
+  auto r = std::to_chars(buf, buf + sizeof(buf), d, std::chars_format::general, 12);
+  const int n = (int)(r.ptr - buf);
   out.append(buf, n);
   bool has = false;
   for (int i = 0; i < n; ++i)
@@ -81,10 +84,18 @@ inline void append_py2_float(std::string& out, double d) {
   if (!has) out += ".0";
 }
 
+// printf("%5.10f"): finite values always exceed the 5-character field width, so
+// to_chars(fixed, 10) (exact, same digits as glibc) is the whole conversion;
+// nan / inf keep printf's padded spelling.
 inline void append_fixed10(std::string& out, double d) {
-  char buf[64];
-  int n = std::snprintf(buf, sizeof(buf), "%5.10f", d);
-  out.append(buf, n);
+  char buf[352];
+  if (!std::isfinite(d)) {
+    int n = std::snprintf(buf, sizeof(buf), "%5.10f", d);
+    out.append(buf, n);
+    return;
+  }
+  auto r = std::to_chars(buf, buf + sizeof(buf), d, std::chars_format::fixed, 10);
+  out.append(buf, r.ptr - buf);
 }
 
 inline void append_int(std::string& out, long long v) {

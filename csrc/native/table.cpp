@@ -268,7 +268,11 @@ int64_t write_rows(const std::string& path, const int64_t* order, int64_t n, con
   FILE* f = std::fopen(path.c_str(), append ? "ab" : "wb");
   if (!f) throw std::runtime_error("cannot open for writing: " + path);
   if (threads < 1) threads = 1;
-  const int64_t block = 1 << 16;
+  // Rows per thread block: ~2^16 cells of work per block, so wide rows (a K x V
+  // .beta file has K rows of V values) still spread over every thread.
+  int64_t cells = 0;
+  for (const OutCol& c : cols) cells += (c.kind == OutCol::kPy2Row || c.kind == OutCol::kFixedRow) ? c.width : 1;
+  const int64_t block = std::max<int64_t>(1, (int64_t(1) << 16) / std::max<int64_t>(1, cells));
   int64_t written = 0;
   std::vector<std::string> bufs(threads);
   for (int64_t b0 = 0; b0 < n; b0 += block * threads) {

@@ -167,7 +167,8 @@ class FlowWordSpace:
         k = k // self.NB
         tb = k % self.NT
         port = k // self.NT
-        pstr = [java_double(float(x)) for x in self.ports]
+        from ..ops import native
+        pstr = native.lib().java_double_array(np.asarray(self.ports, np.float64))
         bstr = [java_double(float(i)) for i in range(max(self.NT, self.NB, self.NP))]
         return [("-1_" if pr else "") + f"{pstr[po]}_{bstr[t]}_{bstr[b]}_{bstr[p]}"
                 for pr, po, t, b, p in zip(prefix.tolist(), port.tolist(), tb.tolist(), bb.tolist(), pb.tolist())]

@@ -52,41 +52,15 @@ def read_index_file(path: str) -> List[str]:
 
 
 def write_model_dat(path: str, c: Corpus):
-    """lda-c corpus format, one document per line."""
-    with open(path, "w") as f:
-        ptr, w, cnt = c.doc_ptr, c.word_idx, c.counts
-        buf = []
-        for d in range(c.num_docs):
-            a, b = ptr[d], ptr[d + 1]
-            parts = [str(b - a)]
-            parts.extend(f"{wi}:{ci}" for wi, ci in zip(w[a:b].tolist(), cnt[a:b].tolist()))
-            buf.append(" ".join(parts))
-            if len(buf) >= 65536:
-                f.write("\n".join(buf) + "\n")
-                buf = []
-        if buf:
-            f.write("\n".join(buf) + "\n")
+    """lda-c corpus format, one document per line (multithreaded C++ writer)."""
+    _n().write_ldac_corpus(path, np.asarray(c.doc_ptr, np.int64), np.asarray(c.word_idx, np.int32),
+                           np.asarray(c.counts, np.int64))
 
 
 def read_model_dat(path: str) -> Corpus:
     """Parse lda-c corpus format; num_terms = max word id + 1 (lda-c read_data)."""
-    ptr = [0]
-    words, counts = [], []
-    with open(path, "r") as f:
-        for line in f:
-            parts = line.split()
-            if not parts:
-                continue
-            n = int(parts[0])
-            if len(parts) != n + 1:
-                raise ValueError(f"model.dat line declares {n} entries, has {len(parts) - 1}")
-            for tok in parts[1:]:
-                a, b = tok.split(":")
-                words.append(int(a))
-                counts.append(int(b))
-            ptr.append(len(words))
-    w = np.asarray(words, np.int32)
-    return Corpus(np.asarray(ptr, np.int64), w, np.asarray(counts, np.int64), int(w.max()) + 1 if w.size else 0)
+    ptr, w, cnt = _n().read_ldac_corpus(path)
+    return Corpus(ptr, w, cnt, int(w.max()) + 1 if w.size else 0)
 
 
 def save_beta(path: str, log_beta: np.ndarray):

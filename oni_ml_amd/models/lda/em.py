@@ -236,7 +236,9 @@ class LDAEngine:
 
     def state_arrays(self) -> dict:
         """Exact engine state (sufficient statistics in the engine's own precision) for checkpoints."""
-        return dict(cw=self.cw.cpu().numpy(), class_total=self.class_total.cpu().numpy())
+        # copy=True: host arrays never alias live engine buffers (CPU backend), since files are written
+        # by a background thread while EM continues
+        return dict(cw=self.cw.to("cpu", copy=True).numpy(), class_total=self.class_total.to("cpu", copy=True).numpy())
 
     def load_state_arrays(self, cw: np.ndarray, class_total: np.ndarray, alpha: float):
         """Restore `state_arrays()` output; beta is re-derived by the same M-step, so a resumed run is
@@ -562,7 +564,7 @@ class LDAEngine:
         return lb.T.contiguous().cpu().numpy()
 
     def local_gamma(self) -> np.ndarray:
-        return self.gamma[:, :self.K].double().cpu().numpy()
+        return self.gamma[:, :self.K].to("cpu", torch.float64, copy=True).numpy()
 
     def gather_gamma(self) -> np.ndarray:
         g = self.local_gamma()

@@ -19,6 +19,8 @@ from __future__ import annotations
 
 import json
 import os
+import queue
+import threading
 import time
 from typing import Optional
 
@@ -32,11 +34,53 @@ from .settings import LAG, LDASettings
 CKPT = "checkpoint.npz"
 
 
+class AsyncWriter:
+    """One background thread for the LAG-period model files.
+
+    lda-c writes %03d.beta/.gamma every LAG iterations inside its EM loop; here
+    the host copies are handed to this thread (the C++ writers release the GIL)
+    so the device keeps iterating while text is formatted.  Jobs run in
+    submission order; `close()` drains the queue and re-raises the first error."""
+
+    def __init__(self):
+        self._q: "queue.Queue" = queue.Queue()
+        self._err: Optional[BaseException] = None
+        self._t = threading.Thread(target=self._loop, name="oni-lda-writer", daemon=True)
+        self._t.start()
+
+    def _loop(self):
+        while True:
+            job = self._q.get()
+            if job is None:
+                return
+            if self._err is None:
+                try:
+                    job()
+                except BaseException as e:  # surfaced by close()
+                    self._err = e
+
+    def submit(self, fn, *args, **kw):
+        if self._err is not None:
+            raise self._err
+        self._q.put(lambda: fn(*args, **kw))
+
+    def close(self):
+        self._q.put(None)
+        self._t.join()
+        if self._err is not None:
+            raise self._err
+
+
 def save_checkpoint(outdir: str, eng: LDAEngine, iteration: int, L_old: float, history):
+    _write_checkpoint(outdir, dict(log_beta=eng.log_beta(), alpha=np.float64(eng.alpha), iteration=np.int64(iteration),
+                                   likelihood_old=np.float64(L_old), var_max_iter=np.int64(eng.var_max_iter),
+                                   history=np.asarray(history, np.float64).reshape(-1, 2), **eng.state_arrays()))
+
+
+def _write_checkpoint(outdir: str, arrays: dict):
+    """Atomic checkpoint.npz (temp file + rename): a crash never leaves a torn checkpoint."""
     tmp = os.path.join(outdir, CKPT + ".tmp.npz")
-    np.savez(tmp, log_beta=eng.log_beta(), alpha=np.float64(eng.alpha), iteration=np.int64(iteration),
-             likelihood_old=np.float64(L_old), var_max_iter=np.int64(eng.var_max_iter),
-             history=np.asarray(history, np.float64).reshape(-1, 2), **eng.state_arrays())
+    np.savez(tmp, **arrays)
     os.replace(tmp, os.path.join(outdir, CKPT))
 
 
@@ -105,24 +149,35 @@ def estimate(corpus: Corpus, num_topics: int, alpha_init: float, settings: LDASe
         if fault_at_iteration is not None and i >= fault_at_iteration:
             raise RuntimeError(f"injected fault after EM iteration {i}")
 
+    writer = AsyncWriter()
+
     def on_save(tag, e):
         lb = e.log_beta()
         g = e.gather_gamma() if tag != "000" else None
         if write_rank_gamma and tag == "final":
             r = 0 if dist is None else dist.rank
-            ldac.save_gamma(os.path.join(outdir, f"{r}.gamma"), e.local_gamma())
+            writer.submit(ldac.save_gamma, os.path.join(outdir, f"{r}.gamma"), e.local_gamma())
         if not rank0:
             return
-        ldac.save_model(os.path.join(outdir, tag), lb, e.alpha)
+        writer.submit(ldac.save_model, os.path.join(outdir, tag), lb, e.alpha)
         if g is not None:
-            ldac.save_gamma(os.path.join(outdir, f"{tag}.gamma"), g)
+            writer.submit(ldac.save_gamma, os.path.join(outdir, f"{tag}.gamma"), g)
         if tag not in ("000", "final"):
-            save_checkpoint(outdir, e, int(tag), history[-1][0] if history else 0.0, history)
+            # engine state is read now (host copies); only the file write is deferred
+            ck = dict(log_beta=lb, alpha=np.float64(e.alpha), iteration=np.int64(int(tag)),
+                      likelihood_old=np.float64(history[-1][0] if history else 0.0),
+                      var_max_iter=np.int64(e.var_max_iter), history=np.asarray(history, np.float64).reshape(-1, 2),
+                      **e.state_arrays())
+            writer.submit(_write_checkpoint, outdir, ck)
         if tag == "final":  # exact binary copy of what final.* hold as text (stage resume reloads this)
-            np.savez(os.path.join(outdir, "final_model.npz"), log_beta=lb, gamma=g, alpha=np.float64(e.alpha))
+            writer.submit(np.savez, os.path.join(outdir, "final_model.npz"), log_beta=lb, gamma=g,
+                          alpha=np.float64(e.alpha))
 
-    res = eng.run(start=mode, corpus_global=corpus, on_iteration=on_iteration, on_save=on_save,
-                  start_iteration=start_it, likelihood_old=L_old, verbose=verbose and rank0)
+    try:
+        res = eng.run(start=mode, corpus_global=corpus, on_iteration=on_iteration, on_save=on_save,
+                      start_iteration=start_it, likelihood_old=L_old, verbose=verbose and rank0)
+    finally:
+        writer.close()
     res.likelihoods = history
     res.log_beta = eng.log_beta()
     res.gamma = eng.gather_gamma()

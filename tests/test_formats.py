@@ -135,3 +135,70 @@ def test_ldac_files_roundtrip(tmp_path):
     assert (tmp_path / "final.gamma").read_text() == "1.0000000000 2.5000000000\n3.2500000000 0.1250000000\n"
     assert ldac.format_likelihood_line(-12345.678, 0.00123) == "-12345.6780000000\t1.23000e-03\n"
     assert ldac.format_likelihood_line(-1.0, math.inf) == "-1.0000000000\t  inf\n"
+
+
+def _edge_values(n=20000, seed=3):
+    rng = np.random.default_rng(seed)
+    v = np.concatenate([
+        rng.uniform(-120, 30, n), -100.0 * np.ones(4), np.ldexp(rng.integers(0, 1 << 20, n).astype(np.float64),
+                                                                -rng.integers(0, 45, n)),
+        [0.0, -0.0, -1e-12, 1e-12, 0.5e-10, -0.5e-10, 2.0 ** -11, -(2.0 ** -11), 1e15, -3.3e19, 123456789.0000000005,
+         5e-324, 1.7976931348623157e308],
+        rng.standard_normal(n) * 1e-6,
+    ])
+    return v
+
+
+def test_fixed10_and_py2_match_printf(tmp_path):
+    """The C++ writers' "%5.10f" (lda-c .beta/.gamma) and "%.12g" (Python-2 str) equal C printf exactly,
+    including ties, tiny negatives (-0.0000000000), huge and subnormal values."""
+    v = _edge_values()
+    p = tmp_path / "g.txt"
+    native.lib().write_rows(str(p), None, [("fixedrow", v.reshape(1, -1), " ")], n=1)
+    got = p.read_text().rstrip("\n").split(" ")
+    assert got == ["%5.10f" % x for x in v]
+    p2 = tmp_path / "p.txt"
+    native.lib().write_rows(str(p2), None, [("py2row", v.reshape(-1, 1), " ")], n=v.size)
+    want = []
+    for x in v:
+        s = "%.12g" % x
+        want.append(s if ("." in s or "e" in s or "n" in s) else s + ".0")
+    assert p2.read_text().splitlines() == want
+
+
+def test_wide_rows_thread_invariant(tmp_path):
+    """A K x V .beta file (few, very wide rows) is split over threads; output is identical to 1 thread."""
+    lb = np.random.default_rng(0).uniform(-100, 0, (7, 50_001))
+    a, b = tmp_path / "a.beta", tmp_path / "b.beta"
+    native.lib().write_rows(str(a), None, [("const", ""), ("fixedrow", lb, " ")], sep=" ", n=7, threads=1)
+    native.lib().write_rows(str(b), None, [("const", ""), ("fixedrow", lb, " ")], sep=" ", n=7, threads=8)
+    assert a.read_bytes() == b.read_bytes()
+    assert np.allclose(np.loadtxt(str(a)), lb, atol=1e-10)
+
+
+def test_ldac_corpus_text_native(tmp_path):
+    """model.dat writer/reader (C++, multithreaded): python-formatted equality, blank lines, bad lines."""
+    from oni_ml_amd.corpus.csr import Corpus
+    from oni_ml_amd.io import ldac
+    rng = np.random.default_rng(1)
+    lens = rng.zipf(1.6, 30_000).clip(1, 3000)
+    ptr = np.concatenate([[0], np.cumsum(lens)]).astype(np.int64)
+    w = rng.integers(0, 9000, ptr[-1]).astype(np.int32)
+    c = rng.integers(1, 5000, ptr[-1]).astype(np.int64)
+    p = tmp_path / "model.dat"
+    ldac.write_model_dat(str(p), Corpus(ptr, w, c, 9000))
+    lines = p.read_text().splitlines()
+    assert len(lines) == lens.size
+    for d in (0, 1, 777, lens.size - 1):
+        a, b = ptr[d], ptr[d + 1]
+        assert lines[d] == " ".join([str(b - a)] + [f"{x}:{y}" for x, y in zip(w[a:b], c[a:b])])
+    r = ldac.read_model_dat(str(p))
+    assert np.array_equal(r.doc_ptr, ptr) and np.array_equal(r.word_idx, w) and np.array_equal(r.counts, c)
+    assert r.num_terms == int(w.max()) + 1
+    q = tmp_path / "m2.dat"
+    q.write_text("2 0:1 3:2\n\n1 5:7\r\n")
+    r = ldac.read_model_dat(str(q))
+    assert r.doc_ptr.tolist() == [0, 2, 3] and r.word_idx.tolist() == [0, 3, 5] and r.counts.tolist() == [1, 2, 7]
+    q.write_text("3 0:1 3:2\n")
+    with pytest.raises(RuntimeError, match="declares 3 entries"):
+        ldac.read_model_dat(str(q))
