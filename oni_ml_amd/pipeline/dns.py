@@ -140,3 +140,40 @@ def score_dns(cfg, tab: FD.DnsTable, top, tables: C.ModelTables, device, log=pri
     native.lib().write_rows(out, None, cols, threads=cfg.threads, n=n)
     log(f"dns_post: {n} queries with score < {cfg.tol} written to {out}")
     return dict(flagged=n, events=int(feat.word_key.numel()))
+
+
+def synthetic_dns_corpus(events: int = 2_000_000, seed: int = 0, device=None, strict: bool = True, threads: int = 8,
+                         return_names: bool = False, n_names: int = None, n_clients: int = None):
+    """Synthetic DNS day -> featurized (dns_pre_lda semantics) -> lda-c corpus: the bench / test input path.
+
+    Name and client populations grow with the day's size (a 2M-query day: 200k names, 50k clients)."""
+    import shutil
+    import tempfile
+    import time
+    from ..synth.dns import generate_dns_day
+    device = torch.device(device or ("cuda" if torch.cuda.is_available() else "cpu"))
+    n_names = n_names or max(20_000, events // 10)
+    n_clients = n_clients or max(5_000, events // 40)
+    tmp = tempfile.mkdtemp(prefix="oni_dns_")
+    try:
+        t0 = time.perf_counter()
+        gen = generate_dns_day(os.path.join(tmp, "in/"), events=events, seed=seed, n_names=n_names,
+                               n_clients=n_clients, with_edge_rows=False)
+        t1 = time.perf_counter()
+        tab = FD.load_dns(gen["dns_path"], None, 1000, strict=strict)
+        top = FD.load_top_domains(gen["top1m"])
+        t2 = time.perf_counter()
+        feat = FD.featurize(tab, device, top, threads=threads)
+        wsp = FD.DnsWordSpace(feat.cuts, feat.qpairs)
+        dwc = count_pairs(feat.ip, feat.word_key, feat.weight)
+        built = lda_pre(dwc)
+        if device.type == "cuda":
+            torch.cuda.synchronize()
+        t3 = time.perf_counter()
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
+    info = dict(events=events, synth_s=round(t1 - t0, 3), ingest_s=round(t2 - t1, 3),
+                featurize_corpus_s=round(t3 - t2, 3))
+    if return_names:
+        return built.corpus, info, wsp.decode(built.word_keys)
+    return built.corpus, info

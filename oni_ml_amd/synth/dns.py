@@ -73,16 +73,20 @@ def generate_dns_day(path: str, events: int = 100_000, seed: int = 0, files: int
     ts = np.sort(t0 + rng.integers(0, 86400, size=events))
     qtype = rng.choice([1, 28, 5, 12, 15, 16, 33, 2, 255], size=events, p=[.55, .18, .06, .1, .04, .03, .02, .01, .01])
     rcode = rng.choice([0, 3, 2, 5], size=events, p=[.86, .1, .03, .01])
-    flen = (60 + np.array([len(names[i]) for i in qn]) + rng.integers(0, 200, size=events) * (rng.random(events) < 0.3)).astype(np.int32)
-    ft = [np.datetime_as_string(np.datetime64(int(x), "s")).replace("T", " ") + ".000000000" for x in ts.tolist()]
+    name_len = np.fromiter((len(x) for x in names), np.int64, count=len(names))
+    flen = (60 + name_len[qn] + rng.integers(0, 200, size=events) * (rng.random(events) < 0.3)).astype(np.int32)
+    import pyarrow.compute as pc
+    ft = np.char.add(np.char.replace(np.datetime_as_string(ts.astype("datetime64[s]")), "T", " "), ".000000000")
+    # dictionary columns: one string per distinct value, indices per event (vectorised; millions of rows)
+    take = lambda vals, idx: pc.take(pa.array(vals, pa.string()), pa.array(idx.astype(np.int64)))
     cols = dict(
         frame_time=pa.array(ft, pa.string()),
         unix_tstamp=pa.array(ts.astype(np.int64), pa.int64()),
         frame_len=pa.array(flen, pa.int32()),
-        ip_dst=pa.array([clients[i] for i in cl], pa.string()),
-        ip_src=pa.array(["10.0.0.53"] * events, pa.string()),
-        dns_qry_name=pa.array([names[i] for i in qn], pa.string()),
-        dns_qry_class=pa.array(["0x00000001"] * events, pa.string()),
+        ip_dst=take(clients, cl),
+        ip_src=take(["10.0.0.53"], np.zeros(events, np.int64)),
+        dns_qry_name=take(names, qn),
+        dns_qry_class=take(["0x00000001"], np.zeros(events, np.int64)),
         dns_qry_type=pa.array(qtype.astype(np.int32), pa.int32()),
         dns_qry_rcode=pa.array(rcode.astype(np.int32), pa.int32()),
         dns_a=pa.array(["93.184.216.34"] * events, pa.string()),
