@@ -166,6 +166,16 @@ def main():
     it = eng.iters.cpu().numpy()
 
     extra = dict(var_iter_mean=round(float(it.mean()), 3), var_iter_max=int(it.max()), var_max_iter=eng.var_max_iter)
+    # variational iterations of the last E-step by document length (the long documents' share
+    # of the E-step is words x iterations)
+    lens = corpus.lengths()
+    by_len = {}
+    for lo, hi in ((0, 16), (16, 64), (64, 256), (256, 1024), (1024, 4096), (4096, 1 << 40)):
+        m = (lens > lo) & (lens <= hi)
+        if m.any():
+            by_len[f"{lo + 1}-{hi if hi < 1 << 40 else 'inf'}"] = [int(m.sum()), round(float(it[m].mean()), 2),
+                                                                  int(it[m].max())]
+    extra["var_iter_by_len"] = by_len
     if args.converge:
         eng2 = LDAEngine(corpus, args.topics, LDASettings(), backend=args.backend, device=dev, dist=dist,
                          seed=args.seed + 1, local_shard=True)

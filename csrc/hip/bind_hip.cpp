@@ -60,9 +60,11 @@ PYBIND11_MODULE(_onihip, m) {
   m.def("split_segment_words", [](int KS) { return oni::split_segment_words(KS); });
   m.def("split_max_blocks", []() { return oni::kSplitMaxBlocks; });
   m.def("block_words", [](int KS, int waves) { return oni::block_words(KS, waves); });
+  m.def("wide_words", [](int KS, int lanes) { return oni::wide_words(KS, lanes); });
+  m.def("wide_slots", [](int KS, int lanes) { return oni::wide_slots(KS, lanes); });
   m.def(
       "lda_estep_split",
-      [](u doc_ptr, u word_idx, u counts, u beta, int K, int KS, float alpha, double lik_const, int var_max_iter,
+      [](bool wide, u doc_ptr, u word_idx, u counts, u beta, int K, int KS, float alpha, double lik_const, int var_max_iter,
          float var_conv, u gamma, u e_out, u r_out, u lik, u alpha_ss, u iters, u seg_doc, u seg_index, u seg_count,
          u seg_base, u doc_slot, int n_blocks, int seg_words, u partial, u partial_l, u counter, int n_docs, u error, u params, u stream) {
         oni::EStepArgs a{P<const int>(doc_ptr), P<const int>(word_idx), P<const float>(counts),
@@ -74,7 +76,10 @@ PYBIND11_MODULE(_onihip, m) {
         oni::SplitArgs s{P<const int>(seg_doc), P<const int>(seg_index), P<const int>(seg_count),
                          P<const int>(seg_base), P<const int>(doc_slot), n_blocks, seg_words, P<float>(partial),
                          P<double>(partial_l), P<int>(counter), n_docs, P<int>(error)};
-        oni::launch_lda_estep_split(a, s, KS, S(stream));
+        if (wide)
+          oni::launch_lda_estep_wsplit(a, s, KS, S(stream));
+        else
+          oni::launch_lda_estep_split(a, s, KS, S(stream));
       });
 
   m.def("lda_suffstats", [](u word_ptr, u csc_ent, u csc_doc, u order, int n_items, u e, u r, u beta, u cw,
@@ -88,12 +93,12 @@ PYBIND11_MODULE(_onihip, m) {
 
   m.def("suff_fused_blocks", [](int h, int m_, int l) { return oni::suff_fused_blocks(h, m_, l); });
   m.def("lda_suffstats_fused", [](u word_ptr, u csc_ent, u csc_doc, u order, int n_heavy, int n_medium, int n_light,
-                                  u e, u r, u beta, u cw, u part, int KS, u gate, u stream) {
+                                  u e, u r, u beta, u cw, u part, int KS, u gate, u stream, bool wide) {
     oni::SuffArgs a{P<const int>(word_ptr), P<const int>(csc_ent),  P<const int>(csc_doc),
                     P<const int>(order),    n_heavy + n_medium + n_light, P<const float>(e),
                     P<const float>(r),      P<const float>(beta),   P<float>(cw),
                     P<const double>(gate)};
-    oni::launch_lda_suffstats_fused(a, n_heavy, n_medium, n_light, P<double>(part), KS, S(stream));
+    oni::launch_lda_suffstats_fused(a, n_heavy, n_medium, n_light, P<double>(part), KS, wide, S(stream));
   });
   m.def("colsum_partials", [](u part, int nb, int cols, u out, u gate, u stream) {
     oni::launch_colsum_partials(P<const double>(part), nb, cols, P<double>(out), P<const double>(gate), S(stream));

@@ -16,6 +16,9 @@ constexpr int kParamCount = 8;
 constexpr int kHistCols = 6;
 
 #define ONI_FOR_EACH_KS(X) X(8) X(12) X(16) X(20) X(24) X(32) X(52) X(64) X(100) X(128)
+// Padded topic counts with wide-topic E-step kernels (lda_estep_wide.hip): a word's
+// topics split over 4 lanes; the host uses them for K > 32.
+#define ONI_FOR_EACH_WIDE_KS(X) X(32) X(52) X(64) X(100) X(128)
 
 // ---------------------------------------------------------------- E-step ---
 enum EStepVariant : int {
@@ -26,6 +29,12 @@ enum EStepVariant : int {
   kEStepB4 = 4,    // one doc per 4-wave workgroup
   kEStepB8 = 5,    // one doc per 8-wave workgroup (longest docs)
   kEStepT1 = 6,    // one thread per document (tiny documents, KS <= 32)
+  // wide-topic layout (lda_estep_wide.hip): 4 lanes share a word's topics
+  kEStepW16 = 7,   // 16 lanes (4 word slots) per doc
+  kEStepW32 = 8,   // 32 lanes (8 slots) per doc
+  kEStepW64 = 9,   // one wave (16 slots) per doc
+  kEStepWB4 = 10,  // one doc per 4-wave workgroup (64 slots)
+  kEStepWB8 = 11,  // one doc per 8-wave workgroup (128 slots)
 };
 
 // Huge documents (the long-context analogue): one document is
@@ -78,6 +87,10 @@ struct EStepArgs {
 };
 void launch_lda_estep(const EStepArgs& a, int variant, int KS, hipStream_t s);
 void launch_lda_estep_split(const EStepArgs& a, const SplitArgs& s, int KS, hipStream_t st);
+void launch_lda_estep_wide(const EStepArgs& a, int variant, int KS, hipStream_t s);
+void launch_lda_estep_wsplit(const EStepArgs& a, const SplitArgs& s, int KS, hipStream_t st);
+int wide_words(int KS, int lanes);  // register-cached words of a wide kernel with `lanes` lanes per doc
+int wide_slots(int KS, int lanes);  // word slots (lanes / topic-group width) of a wide kernel
 int split_segment_words(int KS);   // words one split workgroup keeps in registers
 int block_words(int KS, int waves); // register-cached words of a 4- or 8-wave document workgroup
 
@@ -100,8 +113,9 @@ void launch_lda_suffstats(const SuffArgs& a, int variant, int KS, hipStream_t s)
 // All words in one launch: a.order = [heavy | medium | light] word ids (heavy first);
 // part receives suff_fused_blocks(...) x KS per-workgroup column sums (double).
 int suff_fused_blocks(int n_heavy, int n_medium, int n_light);
+// wide: the wide-topic layout (KS >= 32; lda_suff_wide), used with the wide E-step.
 void launch_lda_suffstats_fused(const SuffArgs& a, int n_heavy, int n_medium, int n_light, double* part, int KS,
-                                hipStream_t s);
+                                bool wide, hipStream_t s);
 
 // ----------------------------------------------------------------- M-step ---
 // beta[w][k] = cw/ct_k if cw > 0 else exp(-100) (k < K); 0 for padding topics.

@@ -616,6 +616,10 @@ static void launch_ks(const EStepArgs& a, int variant, hipStream_t s) {
 }
 
 void launch_lda_estep(const EStepArgs& a, int variant, int KS, hipStream_t s) {
+  if (variant >= kEStepW16) {
+    launch_lda_estep_wide(a, variant, KS, s);
+    return;
+  }
   switch (KS) {
 #define ONI_KS(X) \
   case X:         \

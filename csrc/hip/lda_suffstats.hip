@@ -194,24 +194,144 @@ __global__ __launch_bounds__(256) void lda_suff_fused(SuffArgs a, int n_heavy, i
   }
 }
 
+// Wide-topic variant (K > 32) of lda_suff_fused: a CSC entry's KS topics are split
+// over TG lanes (E-row chunk c on lane c mod TG, as in lda_estep_wide.hip), so a
+// lane holds ceil(KS/4/TG) float4 accumulators instead of KS floats and the
+// kernel runs at 3-4 waves per SIMD instead of spilling at one.  Same group
+// shapes as lda_suff_fused (heavy: one word per workgroup; medium: per wave;
+// light: per 16 lanes), S = G/TG entry slots per word.  The slot partials meet in
+// LDS and are added in slot order (bitwise reproducible); the word's row is then
+// scaled by beta and written with the per-workgroup column sums.
+template <int KS, int TG>
+__global__ __launch_bounds__(256) void lda_suff_wide(SuffArgs a, int n_heavy, int n_medium, int n_light,
+                                                     double* __restrict__ part) {
+  constexpr int C = KS / 4;
+  constexpr int CPL = (C + TG - 1) / TG;
+  constexpr int NSLOT = 256 / TG;
+  constexpr int U = 4;   // entries in flight per lane
+  __shared__ float4 sAcc4[NSLOT][C];
+  __shared__ float sRow[16][KS];
+  if (gated(a.gate)) return;
+  const int t = threadIdx.x;
+  const int b = blockIdx.x;
+  const int nbM = (n_medium + 3) / 4;
+  int G, item, nitems, base;
+  if (b < n_heavy) {
+    G = 256, item = b, nitems = n_heavy, base = 0;
+  } else if (b < n_heavy + nbM) {
+    G = 64, item = (b - n_heavy) * 4 + t / 64, nitems = n_medium, base = n_heavy;
+  } else {
+    G = 16, item = (b - n_heavy - nbM) * 16 + t / 16, nitems = n_light, base = n_heavy + n_medium;
+  }
+  const int S = G / TG;
+  const int gi = t / G;                      // word group of this thread within the block
+  const int s = (t % G) / TG, q = t % TG;
+  const bool valid = item < nitems;
+  const int w = valid ? a.order[base + item] : 0;
+  float4 acc[CPL];
+#pragma unroll
+  for (int j = 0; j < CPL; ++j) acc[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (valid) {
+    int i = a.word_ptr[w] + s;
+    const int end = a.word_ptr[w + 1];
+    for (; i + (U - 1) * S < end; i += U * S) {
+      int d[U];
+      float r[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        d[u] = a.csc_doc[i + u * S];
+        r[u] = a.r[a.csc_ent[i + u * S]];
+      }
+      float4 v[U][CPL];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const float4* p = reinterpret_cast<const float4*>(a.e + (size_t)d[u] * KS);
+#pragma unroll
+        for (int j = 0; j < CPL; ++j) v[u][j] = (q + TG * j < C) ? p[q + TG * j] : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+#pragma unroll
+        for (int j = 0; j < CPL; ++j) {
+          acc[j].x = fmaf(r[u], v[u][j].x, acc[j].x);
+          acc[j].y = fmaf(r[u], v[u][j].y, acc[j].y);
+          acc[j].z = fmaf(r[u], v[u][j].z, acc[j].z);
+          acc[j].w = fmaf(r[u], v[u][j].w, acc[j].w);
+        }
+      }
+    }
+    for (; i < end; i += S) {
+      const float r = a.r[a.csc_ent[i]];
+      const float4* p = reinterpret_cast<const float4*>(a.e + (size_t)a.csc_doc[i] * KS);
+#pragma unroll
+      for (int j = 0; j < CPL; ++j) {
+        if (q + TG * j < C) {
+          const float4 v = p[q + TG * j];
+          acc[j].x = fmaf(r, v.x, acc[j].x);
+          acc[j].y = fmaf(r, v.y, acc[j].y);
+          acc[j].z = fmaf(r, v.z, acc[j].z);
+          acc[j].w = fmaf(r, v.w, acc[j].w);
+        }
+      }
+    }
+  }
+  // slot partials -> LDS (global slot index t / TG)
+#pragma unroll
+  for (int j = 0; j < CPL; ++j)
+    if (q + TG * j < C) sAcc4[t / TG][q + TG * j] = acc[j];
+  __syncthreads();
+  const float* sAcc = reinterpret_cast<const float*>(&sAcc4[0][0]);
+  const int ngroups = 256 / G;
+  for (int idx = t; idx < ngroups * KS; idx += 256) {
+    const int g = idx / KS, k = idx % KS;
+    const int it = (G == 256 ? item : item - gi + g);   // the item of word group g
+    float v = 0.f;
+    for (int u = 0; u < S; ++u) v += sAcc[(g * S + u) * KS + k];
+    float c = 0.f;
+    if (it < nitems) {
+      const int wg = a.order[base + it];
+      c = a.beta[(size_t)wg * KS + k] * v;
+      a.cw[(size_t)wg * KS + k] = c;
+    }
+    sRow[g][k] = c;
+  }
+  __syncthreads();
+  if (t < KS) {
+    double sum = 0.0;
+    for (int g = 0; g < ngroups; ++g) sum += (double)sRow[g][t];
+    part[(size_t)b * KS + t] = sum;
+  }
+}
+
 int suff_fused_blocks(int n_heavy, int n_medium, int n_light) {
   return n_heavy + (n_medium + 3) / 4 + (n_light + 15) / 16;
 }
 
 template <int KS>
-static void suff_fused_ks(const SuffArgs& a, int n_heavy, int n_medium, int n_light, double* part, hipStream_t s) {
+static void suff_fused_ks(const SuffArgs& a, int n_heavy, int n_medium, int n_light, double* part, bool wide,
+                          hipStream_t s) {
   const int nb = suff_fused_blocks(n_heavy, n_medium, n_light);
   if (nb <= 0) return;
+  if (wide) {
+    if constexpr (KS >= 32) {
+      hipLaunchKernelGGL((lda_suff_wide<KS, (KS >= 100 ? 8 : 4)>), dim3(nb), dim3(256), 0, s, a, n_heavy, n_medium,
+                         n_light, part);
+      ONI_HIP_CHECK(hipGetLastError());
+      return;
+    } else {
+      throw std::runtime_error("lda_suffstats_fused: wide layout needs KS >= 32");
+    }
+  }
   hipLaunchKernelGGL((lda_suff_fused<KS>), dim3(nb), dim3(256), 0, s, a, n_heavy, n_medium, n_light, part);
   ONI_HIP_CHECK(hipGetLastError());
 }
 
 void launch_lda_suffstats_fused(const SuffArgs& a, int n_heavy, int n_medium, int n_light, double* part, int KS,
-                                hipStream_t s) {
+                                bool wide, hipStream_t s) {
   switch (KS) {
 #define ONI_KS(X) \
   case X:         \
-    suff_fused_ks<X>(a, n_heavy, n_medium, n_light, part, s); \
+    suff_fused_ks<X>(a, n_heavy, n_medium, n_light, part, wide, s); \
     break;
     ONI_FOR_EACH_KS(ONI_KS)
 #undef ONI_KS

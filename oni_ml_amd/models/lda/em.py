@@ -18,6 +18,8 @@ MI355X design:
 """
 from __future__ import annotations
 
+import os
+
 import math
 import time
 from dataclasses import dataclass, field
@@ -57,6 +59,17 @@ class LDAResult:
     seconds: float = 0.0
 
 
+def _use_wide(ks: int) -> bool:
+    """Wide-topic E-step kernels for K > 32 (ONI_ESTEP_WIDE=0 / 1 forces narrow / wide)."""
+    from ...ops import hip as H
+    env = os.environ.get("ONI_ESTEP_WIDE")
+    if ks not in H.WIDE_KS:
+        return False
+    if env is not None:
+        return env == "1"
+    return ks > 32
+
+
 class _Buckets:
     """Length-bucket plan: (variant, int32 order tensor) launched per E-step."""
 
@@ -67,7 +80,21 @@ class _Buckets:
         L = lengths[order]
         plan = []
         self.split = None
-        if kind == "doc":
+        if kind == "doc" and _use_wide(ks):
+            # wide-topic kernels (K > 32): 4 lanes per word; WB8 and split segments stream the
+            # words beyond their register cache, so the split threshold is a tuning knob only
+            wb8 = H.lib().wide_words(ks, 512)
+            if split and doc_ptr is not None:
+                huge = order[L > max(wb8, split_min or 0)]
+                if huge.size:
+                    self.split = H.SplitPlan(huge, doc_ptr, ks, device, wide=True, seg_words=2 * wb8)
+                    rest = np.asarray(self.split.leftover, np.int32)
+                    keep = ~np.isin(order, huge) | np.isin(order, rest)
+                    order, L = order[keep], L[keep]
+            edges = [(H.ESTEP_WB8, 256, None), (H.ESTEP_WB4, 64, 256), (H.ESTEP_W64, 32, 64),
+                     (H.ESTEP_W32, 16, 32), (H.ESTEP_W16, 0, 16)]
+            L = np.where(L == 0, 1, L)
+        elif kind == "doc":
             cws = 4 if ks <= 32 else (2 if ks <= 64 else 1)
             b4_words = H.lib().block_words(ks, 4)       # 4-wave workgroup, all words in registers
             b8_words = H.lib().block_words(ks, 8)       # 8-wave workgroup, all words in registers
@@ -158,7 +185,7 @@ class LDAEngine:
             self._distributed = dist is not None and dist.world_size > 1
             self._cw_local = torch.zeros_like(self.cw) if self._distributed else self.cw
             self._red_local = torch.zeros_like(self._red) if self._distributed else self._red
-            self.suff_plan = H.SuffPlan(self.dc.word_len, dev)
+            self.suff_plan = H.SuffPlan(self.dc.word_len, dev, wide=_use_wide(self.KS))
             self._suff_part = torch.zeros(max(self.suff_plan.n_blocks, 1), KS, dtype=torch.float64, device=dev)
             self._done_count = torch.zeros(1, dtype=torch.int32, device=dev)
             self._alpha_dummy = torch.zeros(1, dtype=torch.float64, device=dev)
@@ -343,7 +370,7 @@ class LDAEngine:
                         sp = self.doc_buckets.split
                         H.lda_estep_split(dc.doc_ptr, dc.word_idx, dc.counts, self.beta, self.K, a, 0.0, 0, 0.0,
                                           self.gamma, self.e, self.r, self.lik, self.ass, self.iters, item,
-                                          sp.seg_words, params=prm)
+                                          sp.seg_words, params=prm, wide=sp.wide)
                     else:
                         var, order = item
                         H.lda_estep(dc.doc_ptr, dc.word_idx, dc.counts, order, self.beta, self.K, a, 0.0, 0, 0.0,
@@ -523,8 +550,8 @@ class LDAEngine:
         [side 2: B8 + B4], [side 3: G64C/G64/G32], [main: thread-per-document bulk]."""
         from ...ops import hip as H
         nstreams = 1 + len(self._streams)
-        long_vars = (H.ESTEP_B8, H.ESTEP_B4)
-        tiny_vars = (H.ESTEP_T1, H.ESTEP_G16)
+        long_vars = (H.ESTEP_B8, H.ESTEP_B4, H.ESTEP_WB8, H.ESTEP_WB4)
+        tiny_vars = (H.ESTEP_T1, H.ESTEP_G16, H.ESTEP_W16)
         sched = [[] for _ in range(max(nstreams, 1))]
         sp = self.doc_buckets.split
         split_work = [("split", b) for b in sp.batches] if sp is not None else []
@@ -532,8 +559,8 @@ class LDAEngine:
         long_work = [("bucket", (v, o)) for v, o in plan if v in long_vars]
         mid_work = [("bucket", (v, o)) for v, o in plan if v not in long_vars and v not in tiny_vars]
         tiny_work = [("bucket", (v, o)) for v, o in plan if v in tiny_vars]
-        b8_work = [w for w in long_work if w[1][0] == H.ESTEP_B8]
-        b4_work = [w for w in long_work if w[1][0] != H.ESTEP_B8]
+        b8_work = [w for w in long_work if w[1][0] in (H.ESTEP_B8, H.ESTEP_WB8)]
+        b4_work = [w for w in long_work if w[1][0] not in (H.ESTEP_B8, H.ESTEP_WB8)]
         if nstreams >= 4:
             # B4 queues behind the split batches: B8 alone is about as long as split + B4
             sched[1], sched[2], sched[3], sched[0] = split_work + b4_work, b8_work, mid_work, tiny_work

@@ -21,6 +21,9 @@ _ERR = None
 
 # estep / suffstats variant ids (csrc/hip/kernels.h)
 ESTEP_G16, ESTEP_G32, ESTEP_G64, ESTEP_G64C, ESTEP_B4, ESTEP_B8, ESTEP_T1 = range(7)
+# wide-topic variants (lda_estep_wide.hip): 4 lanes share one word's topics
+ESTEP_W16, ESTEP_W32, ESTEP_W64, ESTEP_WB4, ESTEP_WB8 = range(7, 12)
+WIDE_KS = (32, 52, 64, 100, 128)   # kernels.h ONI_FOR_EACH_WIDE_KS
 SUFF_G16, SUFF_G64, SUFF_B8 = range(3)
 
 
@@ -124,10 +127,20 @@ class SplitPlan:
     Each batch holds <= split_max_blocks() workgroups so every segment of a batch is
     co-resident (the per-iteration cross-workgroup barrier cannot deadlock)."""
 
-    def __init__(self, doc_ids, doc_ptr_host, KS: int, device):
+    def __init__(self, doc_ids, doc_ptr_host, KS: int, device, wide: bool = False, seg_words: int = None):
         L = lib()
-        self.seg_words = int(L.split_segment_words(KS))
         self.max_blocks = int(L.split_max_blocks())
+        self.wide = bool(wide)
+        # narrow kernel: a segment is exactly its register cache; wide kernel: any size
+        # (the first wide_words(KS, 512) words in registers, the rest streamed)
+        self.seg_words = int(L.split_segment_words(KS))
+        if wide:
+            # wide kernel segments stream their words, so the size is free: pick it to minimise
+            # the split path's critical path, sum over launches of (longest segment + barrier)
+            lens = [int(doc_ptr_host[d + 1] - doc_ptr_host[d]) for d in doc_ids]
+            self.seg_words = self.plan_segments(lens, int(L.wide_slots(KS, 512)), self.max_blocks,
+                                                int(seg_words or 0))
+
         self.batches = []
         self.leftover = []          # docs needing more segments than a batch holds
         cur = []
@@ -146,6 +159,36 @@ class SplitPlan:
         if cur:
             self.batches.append(self._make(cur, doc_ptr_host, KS, device))
 
+    @staticmethod
+    def plan_segments(lens, unit: int, max_blocks: int, min_words: int = 0, barrier_words: int = 2500) -> int:
+        """Segment size (a multiple of `unit`) minimising sum_batches(max segment words + barrier_words):
+        per variational iteration a launch costs its longest segment's streaming time plus one
+        cross-workgroup barrier (~10 us ~ 2.5k words of K = 100 rows at one CU's L2 bandwidth)."""
+        if not lens:
+            return max(unit, min_words)
+        mx = max(lens)
+        lo = max(unit, min_words, -(-mx // max_blocks))
+        best = None
+        seg = -(-lo // unit) * unit
+        cands = set()
+        while seg < mx:
+            cands.add(seg)
+            seg = -(-int(seg * 1.25) // unit) * unit
+        cands.add(-(-mx // unit) * unit)
+        for seg in sorted(cands):
+            cost, used, cur = 0, 0, 0
+            for n in lens:
+                k = -(-n // seg)
+                if used + k > max_blocks:
+                    cost += cur + barrier_words
+                    used, cur = 0, 0
+                used += k
+                cur = max(cur, min(n, seg))
+            cost += cur + barrier_words
+            if best is None or cost < best[0]:
+                best = (cost, seg)
+        return best[1]
+
     def _make(self, docs, doc_ptr_host, KS, device):
         import numpy as np
         sd, si, sc, sb, slot = [], [], [], [], []
@@ -163,7 +206,7 @@ class SplitPlan:
 
 
 def lda_estep_split(doc_ptr, word_idx, counts, beta, K, alpha, lik_const, var_max_iter, var_conv, gamma, e_out, r_out,
-                    lik, alpha_ss, iters, batch, seg_words, params=None):
+                    lik, alpha_ss, iters, batch, seg_words, params=None, wide=False):
     D = doc_ptr.numel() - 1
     nnz = word_idx.numel()
     V, KS = beta.shape
@@ -171,8 +214,10 @@ def lda_estep_split(doc_ptr, word_idx, counts, beta, K, alpha, lik_const, var_ma
     nb = batch["n_blocks"]
     for k in ("seg_doc", "seg_index", "seg_count", "seg_base", "doc_slot"):
         _chk(batch[k], torch.int32, k, (nb,), dev)
+    if wide and KS not in WIDE_KS:
+        raise ValueError(f"no wide split kernel for KS={KS}")
     lib().lda_estep_split(
-        _chk(doc_ptr, torch.int32, "doc_ptr", (D + 1,), dev), _chk(word_idx, torch.int32, "word_idx", (nnz,), dev),
+        bool(wide), _chk(doc_ptr, torch.int32, "doc_ptr", (D + 1,), dev), _chk(word_idx, torch.int32, "word_idx", (nnz,), dev),
         _chk(counts, torch.float32, "counts", (nnz,), dev), _chk(beta, torch.float32, "beta", (V, KS), dev),
         int(K), int(KS), float(alpha), float(lik_const), int(var_max_iter), float(var_conv),
         _chk(gamma, torch.float32, "gamma", (D, KS), dev), _chk(e_out, torch.float32, "e_out", (D, KS), dev),
@@ -227,8 +272,9 @@ class SuffPlan:
     """Word order for the single-launch suff-stats kernel: [heavy | medium | light] (heavy first)."""
     HEAVY, LIGHT = 1024, 64
 
-    def __init__(self, word_len, device):
+    def __init__(self, word_len, device, wide: bool = False):
         import numpy as np
+        self.wide = bool(wide)      # wide-topic kernel (lda_suff_wide), KS >= 32
         order = np.argsort(-np.asarray(word_len), kind="stable").astype(np.int32)
         L = np.asarray(word_len)[order]
         self.n_heavy = int((L > self.HEAVY).sum())
@@ -246,13 +292,16 @@ def lda_suffstats_fused(word_ptr, csc_ent, csc_doc, plan: "SuffPlan", e, r, beta
     dev = beta.device
     if plan.order.numel() != V:
         raise ValueError("suff plan does not cover the vocabulary")
+    if plan.wide and KS < 32:
+        raise ValueError(f"wide suff-stats layout needs KS >= 32 (got {KS})")
     lib().lda_suffstats_fused(
         _chk(word_ptr, torch.int32, "word_ptr", (V + 1,), dev), _chk(csc_ent, torch.int32, "csc_ent", (nnz,), dev),
         _chk(csc_doc, torch.int32, "csc_doc", (nnz,), dev), _chk(plan.order, torch.int32, "order", (V,), dev),
         plan.n_heavy, plan.n_medium, plan.n_light,
         _chk(e, torch.float32, "e", (D, KS), dev), _chk(r, torch.float32, "r", (nnz,), dev),
         _chk(beta, torch.float32, "beta", (V, KS), dev), _chk(cw, torch.float32, "cw", (V, KS), dev),
-        _chk(part, torch.float64, "part", (max(plan.n_blocks, 1), KS), dev), int(KS), _gate_ptr(gate, dev), _stream())
+        _chk(part, torch.float64, "part", (max(plan.n_blocks, 1), KS), dev), int(KS), _gate_ptr(gate, dev), _stream(),
+        bool(plan.wide))
 
 
 def colsum_partials(part, n_blocks, out, gate=None):

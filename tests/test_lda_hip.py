@@ -30,8 +30,14 @@ def _random_beta(V, K, KS, seed=0, dev="cuda"):
     return out.to(dev)
 
 
-@pytest.mark.parametrize("K,vconv", [(20, -1e30), (7, -1e30), (50, -1e30), (100, -1e30), (20, 1e-6)])
-def test_estep_matches_reference(hip, K, vconv):
+@pytest.mark.parametrize("K,vconv,wide", [(20, -1e30, None), (7, -1e30, None), (50, -1e30, None), (100, -1e30, None),
+                                          (20, 1e-6, None), (30, -1e30, "1"), (30, -1e30, "0"), (64, -1e30, None),
+                                          (128, -1e30, None), (100, 1e-6, None), (50, -1e30, "0")])
+def test_estep_matches_reference(hip, K, vconv, wide, monkeypatch):
+    """Every length bucket of the narrow (K <= 32) and wide-topic (K > 32, lda_estep_wide.hip)
+    E-step kernels against the fp64 Jacobi oracle; ``wide`` forces a layout (ONI_ESTEP_WIDE)."""
+    if wide is not None:
+        monkeypatch.setenv("ONI_ESTEP_WIDE", wide)
     c = _corpus_with_long_docs()
     dev = torch.device("cuda")
     KS = hip.padded_topics(K)
@@ -73,6 +79,12 @@ def test_estep_matches_reference(hip, K, vconv):
     # alpha sufficient statistic
     arel = ((ass - ref["alpha_ss"]).abs() / ref["alpha_ss"].abs().clamp_min(1.0)).max().item()
     assert arel < 1e-3, arel
+    if vconv < 0:
+        # E of the final phi and r_n = c_n / P_n under it (the suff-stats inputs)
+        erel = ((e[:, :K].double() - ref["e"]).abs() / ref["e"].abs().clamp_min(1e-6)).max().item()
+        assert erel < 2e-3, erel
+        rrel = ((r.double() - ref["r"]).abs() / ref["r"].abs().clamp_min(1e-30)).max().item()
+        assert rrel < 2e-3, rrel
 
 
 def test_suffstats_and_mstep(hip):
@@ -110,9 +122,11 @@ def test_suffstats_and_mstep(hip):
         assert b2[:, K:].abs().max().item() == 0
 
 
-def test_suffstats_fused_and_partial_colsums(hip):
+@pytest.mark.parametrize("K,wide", [(20, False), (30, True), (50, True), (100, True), (128, True)])
+def test_suffstats_fused_and_partial_colsums(hip, K, wide):
     """Single-launch suff-stats (heavy / medium / light words, empty words included) against the
-    fp64 reference, bitwise reproducible; the per-workgroup column sums give the class totals."""
+    fp64 reference, bitwise reproducible; the per-workgroup column sums give the class totals.
+    wide: the wide-topic layout (lda_suff_wide, 4 or 8 lanes per CSC entry) used for K > 32."""
     # Zipf-like word usage: a few "stop words" in most documents (heavy), a middle band, a long
     # tail of rare words and some never-used ones (empty)
     rng = np.random.default_rng(6)
@@ -128,7 +142,6 @@ def test_suffstats_fused_and_partial_colsums(hip):
         ptr.append(ptr[-1] + w.size)
     idx = np.concatenate(idx)
     c = Corpus(np.array(ptr), idx, rng.integers(1, 5, idx.size), V)
-    K = 20
     dev = torch.device("cuda")
     KS = hip.padded_topics(K)
     dc = DeviceCorpus.build(c, dev)
@@ -138,7 +151,7 @@ def test_suffstats_fused_and_partial_colsums(hip):
     e = torch.rand(D, KS, generator=gen).to(dev)
     e[:, K:] = 0
     r = torch.rand(nnz, generator=gen).to(dev)
-    plan = hip.SuffPlan(dc.word_len, dev)
+    plan = hip.SuffPlan(dc.word_len, dev, wide=wide)
     assert plan.n_heavy > 0 and plan.n_medium > 0 and plan.n_light > 0 and int((dc.word_len == 0).sum()) > 0
     part = torch.zeros(plan.n_blocks, KS, dtype=torch.float64, device=dev)
     cw = torch.full((V, KS), float("nan"), device=dev)          # every row must be written
@@ -217,8 +230,8 @@ def test_score_kernel_bitwise(hip):
         assert torch.equal(a.cpu(), b), "scores must match the sequential f64 reference bit for bit"
 
 
-@pytest.mark.parametrize("K", [20, 50])
-def test_split_documents_match_single_workgroup(hip, K):
+@pytest.mark.parametrize("K", [20, 50, 100])
+def test_split_documents_match_single_workgroup(hip, K):  # K = 50, 100: wide-topic split kernel
     """Huge documents split across workgroups (per-iteration cross-workgroup reduction) give the
     same E-step as the one-workgroup kernel and the fp64 reference."""
     c = planted_corpus(num_docs=400, num_terms=20000, num_topics=6, mean_tokens=400, tail=0.7,
