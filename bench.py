@@ -212,6 +212,7 @@ def main():
                 "global_batch": docs_global,
                 "seq_len": int(round(corpus.nnz / max(1, corpus.num_docs))),
                 "parallelism": f"dp{world}",
+                "class_word_reduction": eng.exchange_mode,
                 "corpus": args.corpus,
                 "events_per_gpu": args.events if args.corpus in ("flow", "dns") else None,
                 "docs_per_gpu": corpus.num_docs,

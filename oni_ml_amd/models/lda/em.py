@@ -230,6 +230,35 @@ class LDAEngine:
             raise ValueError(f"unknown backend {backend}")
         if backend != "hip":
             self.class_total = torch.zeros(self.KS, dtype=torch.float64, device=self.cw.device)
+        self._xchg = self._make_exchange(corpus)
+
+    def _make_exchange(self, corpus: Corpus):
+        """Sparse class_word exchange (parallel/dist.py VocabExchange) when the ranks' vocabularies
+        overlap little; ONI_DIST_EXCHANGE = auto (default) | sparse | dense.  Collective: every rank
+        builds it (or none does)."""
+        d = self.dist
+        if d is None or d.world_size <= 1 or self.backend == "cpu":
+            return None
+        mode = os.environ.get("ONI_DIST_EXCHANGE", "auto")
+        if mode == "dense":
+            return None
+        from ...parallel.dist import VocabExchange
+        words = np.unique(corpus.word_idx) if corpus.nnz else np.zeros(0, np.int64)
+        x = VocabExchange(d, words, self.V, self.KS, self.cw.device, self.cw.dtype)
+        return x if (mode == "sparse" or x.worthwhile()) else None
+
+    @property
+    def exchange_mode(self) -> str:
+        if self.dist is None or self.dist.world_size <= 1:
+            return "none"
+        return "sparse-alltoall" if self._xchg is not None else "dense-allreduce"
+
+    def global_cw(self) -> torch.Tensor:
+        """class_word summed over all ranks for every word (collective under the sparse exchange,
+        where a rank only holds its own words' rows)."""
+        if self._xchg is None:
+            return self.cw
+        return self._xchg.global_rows(self.cw)
 
     # ------------------------------------------------------------------ init
     def init_random(self, seed: Optional[int] = None):
@@ -265,7 +294,8 @@ class LDAEngine:
         """Exact engine state (sufficient statistics in the engine's own precision) for checkpoints."""
         # copy=True: host arrays never alias live engine buffers (CPU backend), since files are written
         # by a background thread while EM continues
-        return dict(cw=self.cw.to("cpu", copy=True).numpy(), class_total=self.class_total.to("cpu", copy=True).numpy())
+        return dict(cw=self.global_cw().to("cpu", copy=True).numpy(),
+                    class_total=self.class_total.to("cpu", copy=True).numpy())
 
     def load_state_arrays(self, cw: np.ndarray, class_total: np.ndarray, alpha: float):
         """Restore `state_arrays()` output; beta is re-derived by the same M-step, so a resumed run is
@@ -400,8 +430,12 @@ class LDAEngine:
             self._ev_side.record(side)
             main.wait_event(self._ev_side)
         if self._distributed:
-            # all-reduce inputs (see __init__): the collectives then run on self.cw / self._red
-            self.cw.copy_(self._cw_local)
+            # collective inputs (see __init__): the dense all-reduce runs on self.cw / self._red;
+            # the sparse exchange packs the shared rows here and accumulates in the M graph
+            if self._xchg is not None:
+                self._xchg.pack(self._cw_local)
+            else:
+                self.cw.copy_(self._cw_local)
             self._red.copy_(self._red_local)
         if newton_key is not None:
             self._launch_beta_control()
@@ -417,10 +451,24 @@ class LDAEngine:
         H.lda_mstep_control(self.cw, self.class_total, self.beta, self.K, self._scalars, self._params, self._ctl,
                             self._hist, self._done_count)
 
+    def _reduce_stats(self):
+        """Cross-rank reduction of one EM iteration's statistics (outside the graphs): the packed
+        [likelihood, alpha_ss, class_total] doubles by all-reduce, class_word densely by all-reduce
+        or sparsely by the all-to-all of shared rows, both in flight together."""
+        if self._xchg is None:
+            self.dist.allreduce_suffstats(self.cw, self._red)
+            return
+        import torch.distributed as td
+        work = td.all_reduce(self._red, async_op=True)
+        self._xchg.exchange()
+        work.wait()
+
     def _launch_mstep(self, estimate_alpha: bool, num_docs: int):
-        """M-step on the device after the cross-rank all-reduce: alpha Newton, then beta and the
-        EM convergence step (fused kernel)."""
+        """M-step on the device after the cross-rank reduction: (sparse exchange: sum the received
+        rows), alpha Newton, then beta and the EM convergence step (fused kernel)."""
         from ...ops import hip as H
+        if self._xchg is not None:
+            self._xchg.accumulate(self.cw, self._cw_local)
         H.alpha_newton(self._scalars, num_docs, self.K, estimate_alpha, self._params, self._alpha_dummy)
         self._launch_beta_control()
 
@@ -428,6 +476,22 @@ class LDAEngine:
         """One EM iteration (E-step, [all-reduce], M-step, alpha).  Returns (likelihood, alpha_ss)."""
         if self.backend != "hip":
             sc = self.e_step()
+            if self._xchg is not None:
+                import torch.distributed as td
+                red = torch.cat([sc.to(torch.float64), self.cw.sum(0, dtype=torch.float64)])
+                work = td.all_reduce(red, async_op=True)
+                local = self.cw
+                self._xchg.pack(local)
+                self._xchg.exchange()
+                self.cw = torch.empty_like(local)
+                self._xchg.accumulate(self.cw, local)
+                work.wait()
+                host = red[:2].cpu().tolist()
+                self.class_total = red[2:].clone()
+                self._mstep_beta()
+                if estimate_alpha:
+                    self.alpha = special.opt_alpha(float(host[1]), num_docs, self.K)
+                return float(host[0]), float(host[1])
             if self.dist is not None and self.dist.world_size > 1:
                 sc = self.dist.allreduce_suffstats(self.cw, sc)
             host = sc.cpu().tolist()
@@ -490,7 +554,7 @@ class LDAEngine:
                     self._graph.replay()
                 else:
                     self._launch_estep()
-                self.dist.allreduce_suffstats(self.cw, self._red)
+                self._reduce_stats()
                 if not self.use_graph:
                     self._launch_mstep(*key)
                 elif self._mgraph_key != key:
@@ -583,9 +647,10 @@ class LDAEngine:
             self.alpha = special.opt_alpha(alpha_ss, num_docs, self.K)
 
     # -------------------------------------------------------------- outputs
-    def log_beta(self) -> np.ndarray:
-        """[K, V] float64 log p(w|z) as lda-c would save it (-100 floor)."""
-        cw = self.cw[:, :self.K].double()
+    def log_beta(self, cw: Optional[torch.Tensor] = None) -> np.ndarray:
+        """[K, V] float64 log p(w|z) as lda-c would save it (-100 floor).  Collective under the
+        sparse exchange unless ``cw`` (a ``global_cw()`` result) is given."""
+        cw = (self.global_cw() if cw is None else cw)[:, :self.K].double()
         ct = self.class_total[:self.K]
         lb = torch.where(cw > 0, torch.log(cw) - torch.log(ct), torch.full_like(cw, LOG_FLOOR))
         return lb.T.contiguous().cpu().numpy()

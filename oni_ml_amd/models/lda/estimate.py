@@ -25,6 +25,7 @@ import time
 from typing import Optional
 
 import numpy as np
+import torch
 
 from ...corpus.csr import Corpus
 from ...io import ldac
@@ -72,9 +73,14 @@ class AsyncWriter:
 
 
 def save_checkpoint(outdir: str, eng: LDAEngine, iteration: int, L_old: float, history):
-    _write_checkpoint(outdir, dict(log_beta=eng.log_beta(), alpha=np.float64(eng.alpha), iteration=np.int64(iteration),
+    """Collective under the sparse class_word exchange: every rank calls it (rank 0 writes)."""
+    st = eng.state_arrays()
+    lb = eng.log_beta(torch.from_numpy(st["cw"]).to(eng.cw.device))
+    if eng.dist is not None and eng.dist.rank != 0:
+        return
+    _write_checkpoint(outdir, dict(log_beta=lb, alpha=np.float64(eng.alpha), iteration=np.int64(iteration),
                                    likelihood_old=np.float64(L_old), var_max_iter=np.int64(eng.var_max_iter),
-                                   history=np.asarray(history, np.float64).reshape(-1, 2), **eng.state_arrays()))
+                                   history=np.asarray(history, np.float64).reshape(-1, 2), **st))
 
 
 def _write_checkpoint(outdir: str, arrays: dict):
@@ -152,7 +158,9 @@ def estimate(corpus: Corpus, num_topics: int, alpha_init: float, settings: LDASe
     writer = AsyncWriter()
 
     def on_save(tag, e):
-        lb = e.log_beta()
+        # collectives first, on every rank: global class_word (sparse exchange) and the gamma gather
+        st = e.state_arrays()
+        lb = e.log_beta(torch.from_numpy(st["cw"]).to(e.cw.device))
         g = e.gather_gamma() if tag != "000" else None
         if write_rank_gamma and tag == "final":
             r = 0 if dist is None else dist.rank
@@ -167,7 +175,7 @@ def estimate(corpus: Corpus, num_topics: int, alpha_init: float, settings: LDASe
             ck = dict(log_beta=lb, alpha=np.float64(e.alpha), iteration=np.int64(int(tag)),
                       likelihood_old=np.float64(history[-1][0] if history else 0.0),
                       var_max_iter=np.int64(e.var_max_iter), history=np.asarray(history, np.float64).reshape(-1, 2),
-                      **e.state_arrays())
+                      **st)
             writer.submit(_write_checkpoint, outdir, ck)
         if tag == "final":  # exact binary copy of what final.* hold as text (stage resume reloads this)
             writer.submit(np.savez, os.path.join(outdir, "final_model.npz"), log_beta=lb, gamma=g,

@@ -6,9 +6,13 @@ ml_ops.sh:80):
 * documents are sharded CONTIGUOUSLY and balanced by nnz (not doc count), so the
   per-rank gamma blocks concatenate in corpus order exactly like lda-c's
   per-worker <rank>.gamma files combined into final.gamma (README.md:121);
-* per EM iteration the only collective is one all-reduce of the flat class_word
-  buffer [V x KS] f32 plus a 2-scalar f64 all-reduce (likelihood, alpha ss) —
-  ring all-reduce over the 7 xGMI links of a node, K*V*4 bytes;
+* per EM iteration the collectives are the class_word reduction and one small
+  f64 all-reduce ([likelihood, alpha ss, class_total]).  class_word is reduced
+  either densely (ring all-reduce of [V x KS] f32, K*V*4 bytes) or -- when the
+  ranks' vocabularies overlap little, as IP/port "words" of different days do --
+  by `VocabExchange`: an all-to-all of only the rows two ranks share.  On the
+  fully connected xGMI mesh an all-to-all uses every link at once, while a ring
+  all-reduce is bound by one link per step;
 * the CPU test path runs the same code over gloo.
 """
 from __future__ import annotations
@@ -139,6 +143,110 @@ class DistContext:
 
     def _coll_device(self):
         return self.device if self.backend == "nccl" else torch.device("cpu")
+
+
+class VocabExchange:
+    """Sparse cross-rank reduction of class_word rows.
+
+    A rank's E-step only produces class_word rows for words of its own documents,
+    and its next E-step only reads beta rows of those words; beta[w] needs the
+    global sum of row w over the ranks that hold w.  With L_r the sorted word list
+    of rank r, the plan (built once) is the intersections L_r ∩ L_s; every EM
+    iteration each rank
+
+      1. packs its rows of L_r ∩ L_s for every s (``pack``, graph-capturable),
+      2. exchanges them with one ``all_to_all_single`` (``exchange``),
+      3. sums, for its own words, the contributions in global rank order
+         (``accumulate``: 0 + c_0 + c_1 + ... -- every rank that holds w
+         therefore gets bitwise the same sum, like an all-reduce).
+
+    Rows of words a rank does not hold are left zero; ``global_rows`` (dense,
+    masked by a single owner per word) rebuilds the full matrix for model files.
+    Traffic per rank: sum_s |L_r ∩ L_s| rows instead of 2 (N-1)/N V rows."""
+
+    def __init__(self, ctx: "DistContext", local_words: np.ndarray, V: int, width: int, device, dtype):
+        import torch.distributed as td
+
+        self.ctx, self.V, self.width = ctx, int(V), int(width)
+        self.device, self.dtype = torch.device(device), dtype
+        cdev = ctx._coll_device()
+        lw = torch.as_tensor(np.asarray(local_words, dtype=np.int64), device=cdev)
+        n = torch.tensor([lw.numel()], dtype=torch.int64, device=cdev)
+        sizes = [torch.zeros_like(n) for _ in range(ctx.world_size)]
+        td.all_gather(sizes, n)
+        sizes = [int(x.item()) for x in sizes]
+        pad = torch.full((max(sizes),), -1, dtype=torch.int64, device=cdev)
+        pad[: lw.numel()] = lw
+        lists = [torch.empty_like(pad) for _ in range(ctx.world_size)]
+        td.all_gather(lists, pad)
+        lists = [l[:k].cpu() for l, k in zip(lists, sizes)]
+        mine = lists[ctx.rank]
+        self.common = []
+        for s_, other in enumerate(lists):
+            if s_ == ctx.rank:
+                self.common.append(torch.zeros(0, dtype=torch.int64))
+            else:
+                self.common.append(mine[torch.isin(mine, other)])
+        self.splits = [int(c.numel()) for c in self.common]
+        self.rows = sum(self.splits)
+        # single owner per word (lowest rank holding it): the dense model-file reduction
+        owner = torch.full((self.V,), ctx.world_size, dtype=torch.int64)
+        for s_ in reversed(range(ctx.world_size)):
+            owner[lists[s_]] = s_
+        self.owned = (owner == ctx.rank).to(self.device)
+        self.send_idx = torch.cat(self.common).to(self.device)
+        self.recv_idx = [c.to(self.device) for c in self.common]
+        self.offsets = np.concatenate([[0], np.cumsum(self.splits)]).tolist()
+        self.send = torch.zeros(max(self.rows, 1), self.width, dtype=dtype, device=self.device)
+        self.recv = torch.zeros_like(self.send)
+        self.local_words = int(mine.numel())
+        mx = torch.tensor([self.rows], dtype=torch.int64, device=cdev)
+        td.all_reduce(mx, op=td.ReduceOp.MAX)
+        self.max_rows = int(mx.item())
+
+    def worthwhile(self) -> bool:
+        """The busiest rank's all-to-all rows (sent = received) against a ring all-reduce's
+        2 (N-1)/N V rows per rank, with a margin for the all-to-all's per-peer latency.
+        Identical on every rank (max over ranks)."""
+        N = self.ctx.world_size
+        return self.max_rows < 0.7 * 2.0 * (N - 1) / N * self.V
+
+    def pack(self, cw_local: torch.Tensor):
+        if self.rows:
+            torch.index_select(cw_local, 0, self.send_idx, out=self.send[: self.rows])
+
+    def exchange(self, async_op: bool = False):
+        """Collective: every rank calls it every EM iteration (possibly with no rows)."""
+        import torch.distributed as td
+
+        if self.ctx.backend != "nccl" and self.send.device.type == "cuda":
+            # gloo rehearsal of several ranks on one GPU: stage through host memory
+            s_cpu = self.send[: self.rows].cpu()
+            r_cpu = torch.empty_like(s_cpu)
+            td.all_to_all_single(r_cpu, s_cpu, self.splits, self.splits)
+            self.recv[: self.rows].copy_(r_cpu)
+            return None
+        return td.all_to_all_single(self.recv[: self.rows], self.send[: self.rows], self.splits, self.splits,
+                                    async_op=async_op)
+
+    def accumulate(self, cw_out: torch.Tensor, cw_local: torch.Tensor):
+        cw_out.zero_()
+        for s_ in range(self.ctx.world_size):
+            if s_ == self.ctx.rank:
+                cw_out.add_(cw_local)
+            elif self.splits[s_]:
+                a, b = self.offsets[s_], self.offsets[s_ + 1]
+                cw_out.index_add_(0, self.recv_idx[s_], self.recv[a:b])
+
+    def global_rows(self, cw: torch.Tensor) -> torch.Tensor:
+        """Full [V, width] matrix of global sums (collective: every rank must call it)."""
+        import torch.distributed as td
+
+        g = cw * self.owned.unsqueeze(1).to(cw.dtype)
+        cdev = self.ctx._coll_device()
+        gc = g.to(cdev)
+        td.all_reduce(gc)
+        return gc.to(cw.device)
 
 
 def shard_bounds(doc_ptr: np.ndarray, world: int):

@@ -18,9 +18,9 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, outdir, q):
+def _worker(rank, world, port, outdir, q, exchange="auto"):
     os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
-                      MASTER_PORT=str(port))
+                      MASTER_PORT=str(port), ONI_DIST_EXCHANGE=exchange)
     torch.set_num_threads(1)
     try:
         from oni_ml_amd.parallel import dist as D
@@ -30,21 +30,35 @@ def _worker(rank, world, port, outdir, q):
         ctx = D.init_from_env(backend="gloo")
         c = planted_corpus(num_docs=240, num_terms=120, num_topics=4, seed=9) if rank == 0 else None
         c = ctx.broadcast_corpus(c)
+        if exchange == "sparse":
+            # disjoint-ish vocabularies per shard (as IP/port words of different days): words of the
+            # second half of the documents are shifted, so the shards share only a few words
+            c = _shifted_vocab(c)
         res = estimate(c, 6, 2.5, LDASettings(em_max_iter=4), "random", outdir, backend="torch", device="cpu",
                        dist=ctx, seed=1, write_rank_gamma=True)
         g = ctx.gather_rows(np.full((rank + 1, 2), float(rank)), sum(range(1, world + 1)))
-        q.put((rank, [x[0] for x in res.likelihoods], res.alpha, g.tolist(), res.gamma.shape))
+        q.put((rank, [x[0] for x in res.likelihoods], res.alpha, g.tolist(), res.gamma.shape, res.log_beta))
         ctx.shutdown()
     except Exception as e:  # pragma: no cover
         import traceback
-        q.put((rank, "ERR", traceback.format_exc(), None, None))
+        q.put((rank, "ERR", traceback.format_exc(), None, None, None))
 
 
-def _run(world, outdir):
+def _shifted_vocab(c):
+    """Documents of the second half use word ids shifted by V (plus every 10th word kept shared)."""
+    from oni_ml_amd.corpus.csr import Corpus
+    w = c.word_idx.copy()
+    half = c.doc_ptr[c.num_docs // 2]
+    tail = w[half:]
+    w[half:] = np.where(tail % 10 == 0, tail, tail + c.num_terms)
+    return Corpus(c.doc_ptr.copy(), w, c.counts.copy(), 2 * c.num_terms)
+
+
+def _run(world, outdir, exchange="auto"):
     port = _free_port()
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    ps = [ctx.Process(target=_worker, args=(r, world, port, outdir, q)) for r in range(world)]
+    ps = [ctx.Process(target=_worker, args=(r, world, port, outdir, q, exchange)) for r in range(world)]
     for p in ps:
         p.start()
     out = [q.get(timeout=300) for _ in ps]
@@ -62,9 +76,11 @@ def test_shard_bounds_balanced_and_contiguous():
     assert b[0][0] == 0 and b[-1][1] == 100 and all(b[i][1] == b[i + 1][0] for i in range(3))
 
 
-def test_two_rank_em_matches_single_rank(tmp_path):
-    one = _run(1, str(tmp_path / "w1"))
-    two = _run(2, str(tmp_path / "w2"))
+@pytest.mark.parametrize("exchange", ["dense", "sparse"])
+def test_two_rank_em_matches_single_rank(tmp_path, exchange):
+    """dense: ring all-reduce of class_word; sparse: VocabExchange all-to-all of the shared rows."""
+    one = _run(1, str(tmp_path / "w1"), exchange)
+    two = _run(2, str(tmp_path / "w2"), exchange)
     L1, L2 = np.array(one[0][1]), np.array(two[0][1])
     assert L1.shape == L2.shape
     assert np.allclose(L1, L2, rtol=1e-10), (L1, L2)             # all-reduce order only
@@ -73,6 +89,9 @@ def test_two_rank_em_matches_single_rank(tmp_path):
     g1 = np.loadtxt(tmp_path / "w1" / "final.gamma")
     g2 = np.loadtxt(tmp_path / "w2" / "final.gamma")
     assert g1.shape == g2.shape and np.allclose(g1, g2, rtol=1e-6)
+    # the full model (final.beta) agrees: the sparse exchange rebuilds the non-local rows for saves
+    assert np.allclose(one[0][5], two[0][5], rtol=1e-9, atol=1e-12)
+    assert np.array_equal(two[0][5], two[1][5])
     # per-rank gamma blocks concatenate to final.gamma (README.md:121)
     parts = np.concatenate([np.atleast_2d(np.loadtxt(tmp_path / "w2" / f"{r}.gamma")) for r in range(2)])
     assert np.allclose(parts, g2, atol=1e-9)
