@@ -112,7 +112,7 @@ def main():
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--streams", type=int, default=4, help="HIP streams for the E-step buckets")
     ap.add_argument("--batch", type=int, default=5,
-                    help="EM iterations per host read-back (LDAEngine.run() uses LAG=5 when saving)")
+                    help="EM iterations per host read-back (LDAEngine.run() batches LAG=5 when saving, 8 otherwise)")
     ap.add_argument("--converge", type=int, default=1, help="also time a full random-init run to convergence")
     ap.add_argument("--e2e", type=int, default=1, help="N=1: also time the whole ml_ops flow pipeline on the day")
     ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"], help="cpu: gloo/torch rehearsal")
@@ -140,17 +140,15 @@ def main():
     docs_global = ctx.allreduce_int(corpus.num_docs)
 
     def run_iters(n):
-        # EM iterations exactly as LDAEngine.run() issues them: batches of --batch iterations
-        # (one hipGraph replay each on one rank; E-step graph -> RCCL all-reduce -> M-step graph on
-        # several) with the lda-c convergence test evaluated on the device and one host read-back of
-        # the per-iteration (likelihood, conv, alpha) history per batch.  stop=False: every one of
-        # the n iterations runs in full (none is skipped by a converged loop).
-        done = 0
-        while done < n:
-            m = min(args.batch, n - done)
-            recs = eng.em_iterations(m, True, docs_global, stop=False)
-            assert len(recs) == m, (len(recs), m)
-            done += m
+        # EM iterations exactly as LDAEngine.run() issues them without LAG saves: batches of --batch
+        # iterations (one hipGraph replay each on one rank; E-step graph -> RCCL collectives -> M-step
+        # graph on several), one batch always queued ahead of the host's read-back of the previous
+        # batch's (likelihood, conv, alpha) history, the lda-c convergence test evaluated on the
+        # device.  stop=False: every one of the n iterations runs in full (none is skipped by a
+        # converged loop).
+        batches = [min(args.batch, n - b) for b in range(0, n, args.batch)]
+        recs = eng.em_iterations_pipelined(batches, True, docs_global, stop=False)
+        assert len(recs) == n, (len(recs), n)
 
     run_iters(args.warmup)
     ctx.barrier()

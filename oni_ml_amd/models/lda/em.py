@@ -529,14 +529,61 @@ class LDAEngine:
                 if stop and not _em_continue(conv, i, emc, emx):
                     break
             return recs
+        ticket = self._enqueue_batch(n, estimate_alpha, num_docs, likelihood_old, iteration, stop, emc, emx,
+                                     cont=False)
+        return self._collect_batch(ticket)
+
+    def em_iterations_pipelined(self, batches: List[int], estimate_alpha: bool, num_docs: int,
+                                likelihood_old: float = 0.0, iteration: int = 0, stop: bool = True) -> List[tuple]:
+        """``em_iterations`` over several batches with one batch always queued ahead: batch k+1 is
+        enqueued before batch k's history is read back, so the GPU never idles on the host's
+        read-back, Python bookkeeping and the next batch's launches.  Continuation batches take
+        their loop state (previous likelihood, iteration, done flag, alpha, VAR_MAX_ITER) from the
+        device, where em_control keeps it; the host sends nothing.  Batches queued after the
+        device loop converged are no-ops (every kernel checks params[DONE]).  Not for runs that
+        read engine state between batches (LAG saves)."""
+        if self.backend != "hip":
+            recs = []
+            for n in batches:
+                r = self.em_iterations(n, estimate_alpha, num_docs, likelihood_old, iteration + len(recs), stop)
+                recs += r
+                if r:
+                    likelihood_old = r[-1][0]
+                if len(r) < n:
+                    break
+            return recs
+        st = self.settings
+        emc, emx = st.em_converged, st.em_max_iter
+        bufs = [self._out_host, torch.zeros_like(self._out_host).pin_memory()]
+        recs, pending = [], None
+        for j, n in enumerate(batches):
+            t = self._enqueue_batch(n, estimate_alpha, num_docs, likelihood_old, iteration, stop, emc, emx,
+                                    cont=j > 0, buf=bufs[j % 2])
+            if pending is not None:
+                r = self._collect_batch(pending)
+                recs += r
+                if len(r) < pending[2]:       # the device loop ended in that batch: stop enqueuing
+                    pending = t
+                    break
+            pending = t
+        if pending is not None:
+            recs += self._collect_batch(pending)
+        return recs
+
+    def _enqueue_batch(self, n, estimate_alpha, num_docs, likelihood_old, iteration, stop, emc, emx, cont=False,
+                       buf=None):
+        from ...ops import hip as H
         if n > self._hist_cap:
             raise ValueError(f"batch of {n} EM iterations > history capacity {self._hist_cap}")
-        if self._pushed != (self.alpha, self.var_max_iter):   # host changed alpha / VAR_MAX_ITER
-            self._push_params()
+        if cont:
+            self._ctl[2:3].zero_()   # history slot; loop state and params stay as the device left them
         else:
-            self._gate.zero_()
-        self._ctl.copy_(torch.tensor([likelihood_old, emc, 0.0, float(iteration), float(emx),
-                                      1.0 if stop else 0.0, 0.0, 0.0], dtype=torch.float64))
+            if self._pushed != (self.alpha, self.var_max_iter):   # host changed alpha / VAR_MAX_ITER
+                self._push_params()
+            else:
+                self._gate.zero_()
+            self._ctl.copy_(torch.tensor([likelihood_old, emc, 0.0, float(iteration), float(emx),
+                                          1.0 if stop else 0.0, 0.0, 0.0], dtype=torch.float64))
         key = (bool(estimate_alpha), int(num_docs))
         for _ in range(n):
             if not self._distributed:
@@ -562,11 +609,19 @@ class LDAEngine:
                     self._mgraph_key = key
                 else:
                     self._mgraph.replay()
+        buf = self._out_host if buf is None else buf
         m = 8 + H.HIST_COLS * n
-        self._out_host[:m].copy_(self._ctlhist[:m], non_blocking=True)
-        self._out_ev.record()
-        self._out_ev.synchronize()
-        out = self._out_host[:m].tolist()
+        buf[:m].copy_(self._ctlhist[:m], non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        return ev, buf, n
+
+    def _collect_batch(self, ticket) -> List[tuple]:
+        from ...ops import hip as H
+        ev, buf, n = ticket
+        ev.synchronize()
+        m = 8 + H.HIST_COLS * n
+        out = buf[:m].tolist()
         done = int(out[2])
         rows = [tuple(out[8 + H.HIST_COLS * j: 8 + H.HIST_COLS * j + 5]) for j in range(min(done, n))]
         recs = [(r[0], r[1], r[2], int(r[3]), r[4]) for r in rows]
@@ -689,7 +744,26 @@ class LDAEngine:
         stats = []
         n_docs_global = self.global_docs
         per_iter_stats = verbose or self.collect_iter_stats   # an extra D2H copy per iteration: opt-in
-        while _em_continue(conv, i, st.em_converged, st.em_max_iter):
+        if on_save is None and not per_iter_stats and self.backend == "hip" and \
+                _em_continue(conv, i, st.em_converged, st.em_max_iter):
+            # no saves: batches run back to back with one queued ahead (em_iterations_pipelined)
+            left = st.em_max_iter - i + 1
+            batches = [min(self.max_batch, left - b) for b in range(0, max(left, 0), self.max_batch)]
+            ti = time.perf_counter()
+            recs = self.em_iterations_pipelined(batches, st.estimate_alpha, n_docs_global, likelihood_old=L_old,
+                                                iteration=i)
+            dt = (time.perf_counter() - ti) / max(len(recs), 1)
+            for lik, conv, alpha, vmi, _ass in recs:
+                i += 1
+                L_old = lik
+                hist.append((lik, conv))
+                stats.append(EMIterStats(i, lik, conv, alpha, dt, -1.0, -1, vmi))
+                if on_iteration is not None:
+                    on_iteration(self, i, lik, conv)
+            conv = 0.0 if not recs else conv
+        while on_save is not None or per_iter_stats or self.backend != "hip":
+            if not _em_continue(conv, i, st.em_converged, st.em_max_iter):
+                break
             # One batch = the iterations up to the next LAG save (the saved state must be that
             # iteration's), at most max_batch; the device stops the batch itself on convergence.
             n = 1 if per_iter_stats else self.max_batch
