@@ -92,8 +92,12 @@ def _java_double(s: str) -> Optional[float]:
 
 @dataclass
 class DnsTable:
-    """The 8 selected columns as strings (mkString semantics) + weights; feedback rows last."""
-    cols: Dict[str, list]          # name -> list[str] (kept for output, dictionary-encoded lazily)
+    """The 8 selected columns as strings (mkString semantics) + weights; feedback rows last.
+
+    Columns stay Arrow string arrays (one chunk each): featurization reads the name bytes and
+    offsets zero-copy and dictionary-encodes with Arrow kernels; only the flagged output rows are
+    ever turned into Python strings (``take``)."""
+    arrays: Dict[str, object]      # name -> pyarrow StringArray over all n rows
     frame_len: np.ndarray          # f64
     unix_tstamp: np.ndarray        # f64
     weight: np.ndarray             # int64
@@ -104,6 +108,19 @@ class DnsTable:
     @property
     def n(self) -> int:
         return self.n_raw + self.n_feedback
+
+    def column(self, name: str, n: Optional[int] = None):
+        a = self.arrays[name]
+        return a if n is None or n == len(a) else a.slice(0, n)
+
+    def take(self, name: str, rows) -> List[str]:
+        pa, pc, _ = _pa()
+        return pc.take(self.arrays[name], pa.array(np.asarray(rows, np.int64))).to_pylist()
+
+    @property
+    def cols(self) -> Dict[str, list]:
+        """All columns as Python lists (tests / small tables only)."""
+        return {c: a.to_pylist() for c, a in self.arrays.items()}
 
 
 def _arrow_strings(pa, pc, col):
@@ -136,7 +153,6 @@ def load_dns(dns_path: str, feedback_path: Optional[str] = None, dupfactor: int 
     strs = {c: pc.filter(v, keep) for c, v in strs.items()}
     flen = pc.filter(t["frame_len"], keep).to_numpy(zero_copy_only=False).astype(np.float64)
     tst = pc.filter(t["unix_tstamp"], keep).to_numpy(zero_copy_only=False).astype(np.float64)
-    cols = {c: v.to_pylist() for c, v in strs.items()}
     n_raw = len(flen)
     fb = read_dns_feedback(feedback_path) if feedback_path else []
     fb_ok = []
@@ -147,15 +163,18 @@ def load_dns(dns_path: str, feedback_path: Optional[str] = None, dupfactor: int 
         if a is None or b is None:
             continue
         fb_ok.append((r, a, b))
-    for r, a, b in fb_ok:
-        for c, v in zip(COLUMNS, r):
-            cols[c].append(v)
+    arrays = {}
+    for j, c in enumerate(COLUMNS):
+        a = strs[c]
+        if fb_ok:
+            a = pa.concat_arrays([a.cast(pa.large_string()), pa.array([r[j] for r, _, _ in fb_ok], pa.large_string())])
+        arrays[c] = a.combine_chunks() if hasattr(a, "combine_chunks") else a
     if fb_ok:
         flen = np.concatenate([flen, np.array([a for _, a, _ in fb_ok])])
         tst = np.concatenate([tst, np.array([b for _, _, b in fb_ok])])
     w = np.ones(len(flen), np.int64)
     w[n_raw:] = dupfactor
-    return DnsTable(cols, flen, tst, w, n_raw, len(fb_ok), dropped=n_before - n_raw)
+    return DnsTable(arrays, flen, tst, w, n_raw, len(fb_ok), dropped=n_before - n_raw)
 
 
 def load_top_domains(path: Optional[str]) -> List[str]:
@@ -172,11 +191,28 @@ def load_top_domains(path: Optional[str]) -> List[str]:
     return out
 
 
-def _offsets(names: List[str]):
-    enc = [s.encode("utf-8") for s in names]
-    off = np.zeros(len(enc) + 1, np.int64)
-    np.cumsum([len(b) for b in enc], out=off[1:])
-    return b"".join(enc), off
+def _offsets(names):
+    """(bytes buffer, int64 offsets) of a list of str or an Arrow string array (zero-copy data)."""
+    if isinstance(names, list):
+        enc = [s.encode("utf-8") for s in names]
+        off = np.zeros(len(enc) + 1, np.int64)
+        np.cumsum([len(b) for b in enc], out=off[1:])
+        return b"".join(enc), off
+    pa, _, _ = _pa()
+    a = names
+    wide = pa.types.is_large_string(a.type)
+    bufs = a.buffers()
+    off = np.frombuffer(bufs[1], dtype=np.int64 if wide else np.int32)[a.offset: a.offset + len(a) + 1]
+    data = bufs[2] if bufs[2] is not None else b""
+    return data, off.astype(np.int64)
+
+
+def arrow_dictionary_encode(arr):
+    """First-appearance ids + names of an Arrow string array (Arrow's hash memo assigns codes in
+    order of first occurrence, like ``dictionary_encode``)."""
+    _, pc, _ = _pa()
+    d = pc.dictionary_encode(arr)
+    return d.indices.to_numpy(zero_copy_only=False).astype(np.int32), d.dictionary.to_pylist()
 
 
 @dataclass
@@ -209,8 +245,7 @@ def featurize(tab: DnsTable, device, top_domains: Sequence[str], cuts: Optional[
               raw_only: bool = False, threads: int = 8) -> DnsFeatures:
     device = torch.device(device)
     n = tab.n_raw if raw_only else tab.n
-    names = tab.cols["dns_qry_name"][:n]
-    data, off = _offsets(names)
+    data, off = _offsets(tab.column("dns_qry_name", n))
     F = native.lib().dns_features(data, off, list(COUNTRY_CODES), list(top_domains), SPECIAL_DOMAIN, threads)
     w = torch.from_numpy(tab.weight[:n]).to(device)
     vals = dict(
@@ -230,8 +265,9 @@ def featurize(tab: DnsTable, device, top_domains: Sequence[str], cuts: Optional[
     else:
         cuts_t = {k: torch.as_tensor(np.asarray(v, np.float64), device=device) for k, v in cuts.items()}
     bins = {k: (vals[k].unsqueeze(-1) > cuts_t[k].unsqueeze(0)).sum(-1) for k in vals}
-    qp = [f"{a}_{b}" for a, b in zip(tab.cols["dns_qry_type"][:n], tab.cols["dns_qry_rcode"][:n])]
-    qid, qnames = dictionary_encode(qp)
+    _, pc, _ = _pa()
+    qid, qnames = arrow_dictionary_encode(
+        pc.binary_join_element_wise(tab.column("dns_qry_type", n), tab.column("dns_qry_rcode", n), "_"))
     top = torch.from_numpy(F["top_domain"].astype(np.int64)).to(device)
     key = top
     radix = dict(frame_len=len(cuts_t["frame_len"]) + 1, unix_tstamp=len(cuts_t["unix_tstamp"]) + 1,
@@ -240,7 +276,7 @@ def featurize(tab: DnsTable, device, top_domains: Sequence[str], cuts: Optional[
     for k in ("frame_len", "unix_tstamp", "subdomain_length", "entropy", "num_periods"):
         key = key * radix[k] + bins[k]
     key = key * max(1, len(qnames)) + torch.from_numpy(qid.astype(np.int64)).to(device)
-    ip_ids, ip_names = dictionary_encode(tab.cols["ip_dst"][:n])
+    ip_ids, ip_names = arrow_dictionary_encode(tab.column("ip_dst", n))
     return DnsFeatures(rows=np.arange(n, dtype=np.int64), ip=torch.from_numpy(ip_ids.astype(np.int64)).to(device),
                        ip_names=ip_names, word_key=key, weight=w, bins=bins,
                        cuts={k: v.cpu().numpy() for k, v in cuts_t.items()}, host=F, qpairs=qnames)

@@ -106,11 +106,16 @@ class _Buckets:
                     rest = np.asarray(self.split.leftover, np.int32)
                     keep = ~np.isin(order, huge) | np.isin(order, rest)
                     order, L = order[keep], L[keep]
-            # tiny documents: one thread each while the topic state fits the registers (KS <= 24)
-            tiny = H.ESTEP_T1 if ks <= 24 else H.ESTEP_G16
+            # tiny documents: one thread each while the topic state fits the registers (KS <= 24) and
+            # the document fits the thread's row cache (t1_max words); longer tiny documents would
+            # re-stream their rows every variational iteration from one thread, so they take 16 lanes
+            t1_max = int(os.environ.get("ONI_T1_MAX", "16"))
+            if ks <= 24:
+                tiny = [(H.ESTEP_G16, t1_max, 16), (H.ESTEP_T1, 0, min(t1_max, 16))]
+            else:
+                tiny = [(H.ESTEP_G16, 0, 16)]
             edges = [(H.ESTEP_B8, b4_words, None), (H.ESTEP_B4, 64 * cws, b4_words),
-                     (H.ESTEP_G64C, 64, 64 * cws), (H.ESTEP_G64, 32, 64), (H.ESTEP_G32, 16, 32),
-                     (tiny, 0, 16)]
+                     (H.ESTEP_G64C, 64, 64 * cws), (H.ESTEP_G64, 32, 64), (H.ESTEP_G32, 16, 32)] + tiny
             L = np.where(L == 0, 1, L)
         else:
             # every word gets a row (empty words write zeros), so class_word needs no clearing

@@ -123,7 +123,7 @@ def score_dns(cfg, tab: FD.DnsTable, top, tables: C.ModelTables, device, log=pri
     out = os.path.join(cfg.lpath, "dns_results.csv")
     cols = []
     for c in FD.COLUMNS:
-        ids, names = FD.dictionary_encode([tab.cols[c][i] for i in order.tolist()])
+        ids, names = FD.dictionary_encode(tab.take(c, order))
         cols.append(("dict", names, ids))
     H = feat.host
     cols += [
