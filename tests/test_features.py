@@ -151,3 +151,23 @@ def test_dns_feedback(tmp_path):
     p.write_text("\n".join([hdr, ",".join(row), ",".join(row2)]) + "\n")
     out = read_dns_feedback(str(p))
     assert out == [["2016-01-22 00:00:01", "1453420801", "120", "10.0.0.5", "www.x.com", "1", "1", "0"]]
+
+
+def test_arrow_dictionary_encode_first_appearance():
+    """Arrow's dictionary encoding (DNS ingest) assigns ids in first-appearance order, exactly like
+    the Python encoder the corpus order was defined with."""
+    import pyarrow as pa
+    from oni_ml_amd.features.dns import arrow_dictionary_encode, dictionary_encode, _offsets
+    rng = np.random.default_rng(3)
+    vals = [f"10.0.{x // 250}.{x % 250}" for x in rng.integers(0, 3000, 20000)]
+    a_ids, a_names = arrow_dictionary_encode(pa.array(vals))
+    p_ids, p_names = dictionary_encode(vals)
+    assert np.array_equal(a_ids, p_ids) and a_names == p_names
+    # zero-copy name buffers equal the encoded list form, also for sliced / large_string arrays
+    arr = pa.array(vals).slice(5, 1000)
+    d1, o1 = _offsets(arr)
+    d2, o2 = _offsets(vals[5:1005])
+    assert [bytes(d1)[o1[i]:o1[i + 1]] for i in range(1000)] == [d2[o2[i]:o2[i + 1]] for i in range(1000)]
+    arrl = pa.array(vals, pa.large_string())
+    d3, o3 = _offsets(arrl)
+    assert bytes(d3)[o3[7]:o3[8]].decode() == vals[7]
