@@ -1,4 +1,5 @@
 """Document data parallelism over torch.distributed (gloo on the CPU; the same code runs RCCL on GPUs)."""
+import json
 import os
 import socket
 
@@ -110,3 +111,43 @@ def test_bench_two_rank_cpu_rehearsal():
     assert r.returncode == 0, r.stderr[-3000:]
     out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
     assert out["n_gpus"] == 2 and out["config"]["parallelism"] == "dp2" and out["value"] > 0
+
+
+@pytest.mark.parametrize("exchange", ["dense", "sparse"])
+def test_two_rank_ml_ops_pipeline_matches_one_rank(tmp_path, exchange):
+    """`ml_ops` under torchrun with 2 ranks (gloo, torch backend): rank 0 featurizes and broadcasts the
+    corpus, the ranks share the LDA stage (dense all-reduce or sparse all-to-all of class_word rows),
+    rank 0 exports and scores.  The output files match a single-rank run."""
+    import subprocess
+    import sys
+    from oni_ml_amd.models.lda.settings import LDASettings
+    from oni_ml_amd.synth.flow import generate_flow_day
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    generate_flow_day(str(tmp_path / "in") + "/", events=3000, seed=2, n_internal=200, n_external=300)
+    st = tmp_path / "settings.txt"
+    st.write_text(LDASettings(em_max_iter=3).dumps())
+    env = dict(os.environ, ONI_CONF=str(tmp_path / "none.conf"), ONI_DIST_EXCHANGE=exchange)
+    args = ["ml_ops", "20160122", "flow", "1e-3", "--flow-path", str(tmp_path / "in"), "--backend", "torch",
+            "--settings", str(st), "--threads", "2", "--quiet"]
+    r1 = subprocess.run([sys.executable, "-m", "oni_ml_amd"] + args + ["--lpath", str(tmp_path / "one")], cwd=root,
+                        capture_output=True, text=True, env=env, timeout=600)
+    assert r1.returncode == 0, r1.stderr[-2000:]
+    r2 = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                         "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "-m", "oni_ml_amd"] + args +
+                        ["--lpath", str(tmp_path / "two"), "--gpus", "2"], cwd=root, capture_output=True, text=True,
+                        env=env, timeout=600)
+    assert r2.returncode == 0, r2.stderr[-3000:]
+    for f in ("doc.dat", "words.dat", "model.dat"):
+        assert (tmp_path / "one" / f).read_text() == (tmp_path / "two" / f).read_text(), f
+    g1, g2 = np.loadtxt(tmp_path / "one" / "final.gamma"), np.loadtxt(tmp_path / "two" / "final.gamma")
+    assert g1.shape == g2.shape and np.allclose(g1, g2, rtol=1e-6, atol=1e-7)
+    b1, b2 = np.loadtxt(tmp_path / "one" / "final.beta"), np.loadtxt(tmp_path / "two" / "final.beta")
+    assert np.allclose(b1, b2, rtol=1e-8, atol=1e-9)
+    l1 = [l.split("\t")[0] for l in (tmp_path / "one" / "likelihood.dat").read_text().splitlines()]
+    l2 = [l.split("\t")[0] for l in (tmp_path / "two" / "likelihood.dat").read_text().splitlines()]
+    assert np.allclose(np.array(l1, float), np.array(l2, float), rtol=1e-10)
+    s1 = json.load(open(tmp_path / "one" / "run_summary.json"))
+    s2 = json.load(open(tmp_path / "two" / "run_summary.json"))
+    assert s1["scored"] == s2["scored"] > 0
+    assert (tmp_path / "one" / "flow_results.csv").read_text().splitlines()[:20] == \
+        (tmp_path / "two" / "flow_results.csv").read_text().splitlines()[:20]
