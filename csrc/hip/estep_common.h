@@ -38,6 +38,11 @@ __device__ __forceinline__ float dot_lds(const float* sE, const float (&row)[KS]
 
 constexpr float kPMin = 1e-30f;
 
+// r = c / P with v_rcp_f32 (1 ulp) instead of IEEE division: the correctly rounded
+// f32 divide is a ~10-instruction div_scale / fmas / fixup sequence, a large share
+// of the per-word work (P >= kPMin is a normal float, so rcp is exact to 1 ulp).
+__device__ __forceinline__ float rdiv(float c, float P) { return c * __builtin_amdgcn_rcpf(P); }
+
 // Beta rows each lane keeps in VGPRs across the variational iterations:
 // 4-wave kernels (G64C, B4) and 8-wave kernels (B8, split segments; 2 waves per
 // SIMD leave ~256 VGPRs per lane, so up to 8 rows of 20 topics fit).

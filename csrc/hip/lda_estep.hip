@@ -124,7 +124,7 @@ __global__ __launch_bounds__(256) void lda_estep_group(EStepArgs a) {
     for (int c = 0; c < CW; ++c) {
       if (t + G * c < N) {
         const float P = fmaxf(dot_lds<KS>(sE, bc[c]), kPMin);
-        const float r = cc[c] / P;
+        const float r = rdiv(cc[c], P);
         lsum = fmaf(cc[c], __logf(P), lsum);
 #pragma unroll
         for (int k = 0; k < KS; ++k) acc[k] = fmaf(r, bc[c][k], acc[k]);
@@ -136,7 +136,7 @@ __global__ __launch_bounds__(256) void lda_estep_group(EStepArgs a) {
       const float cnt = a.counts[beg + n];
       load_row<KS>(a.beta, w, row);
       const float P = fmaxf(dot_lds<KS>(sE, row), kPMin);
-      const float r = cnt / P;
+      const float r = rdiv(cnt, P);
       lsum = fmaf(cnt, __logf(P), lsum);
 #pragma unroll
       for (int k = 0; k < KS; ++k) acc[k] = fmaf(r, row[k], acc[k]);
@@ -212,12 +212,12 @@ __global__ __launch_bounds__(256) void lda_estep_group(EStepArgs a) {
 #pragma unroll
   for (int c = 0; c < CW; ++c) {
     const int n = t + G * c;
-    if (n < N) a.r_out[beg + n] = cc[c] / fmaxf(dot_lds<KS>(sE, bc[c]), kPMin);
+    if (n < N) a.r_out[beg + n] = rdiv(cc[c], fmaxf(dot_lds<KS>(sE, bc[c]), kPMin));
   }
   for (int n = t + G * CW; n < N; n += G) {
     float row[KS];
     load_row<KS>(a.beta, a.word_idx[beg + n], row);
-    a.r_out[beg + n] = a.counts[beg + n] / fmaxf(dot_lds<KS>(sE, row), kPMin);
+    a.r_out[beg + n] = rdiv(a.counts[beg + n], fmaxf(dot_lds<KS>(sE, row), kPMin));
   }
   if (t == 0) {
     a.lik[d] = L;
@@ -321,7 +321,7 @@ __global__ __launch_bounds__(NW * 64) void lda_estep_block(EStepArgs a) {
     for (int c = 0; c < CW; ++c) {
       if (t + NT * c < N) {
         const float P = fmaxf(dot_lds<KS>(sE, bc[c]), kPMin);
-        const float r = cc[c] / P;
+        const float r = rdiv(cc[c], P);
         lsum = fmaf(cc[c], __logf(P), lsum);
 #pragma unroll
         for (int k = 0; k < KS; ++k) acc[k] = fmaf(r, bc[c][k], acc[k]);
@@ -332,7 +332,7 @@ __global__ __launch_bounds__(NW * 64) void lda_estep_block(EStepArgs a) {
       const float cnt = a.counts[beg + n];
       load_row<KS>(a.beta, a.word_idx[beg + n], row);
       const float P = fmaxf(dot_lds<KS>(sE, row), kPMin);
-      const float r = cnt / P;
+      const float r = rdiv(cnt, P);
       lsum = fmaf(cnt, __logf(P), lsum);
 #pragma unroll
       for (int k = 0; k < KS; ++k) acc[k] = fmaf(r, row[k], acc[k]);
@@ -408,12 +408,12 @@ __global__ __launch_bounds__(NW * 64) void lda_estep_block(EStepArgs a) {
 #pragma unroll
   for (int c = 0; c < CW; ++c) {
     const int n = t + NT * c;
-    if (n < N) a.r_out[beg + n] = cc[c] / fmaxf(dot_lds<KS>(sE, bc[c]), kPMin);
+    if (n < N) a.r_out[beg + n] = rdiv(cc[c], fmaxf(dot_lds<KS>(sE, bc[c]), kPMin));
   }
   for (int n = t + NT * CW; n < N; n += NT) {
     float row[KS];
     load_row<KS>(a.beta, a.word_idx[beg + n], row);
-    a.r_out[beg + n] = a.counts[beg + n] / fmaxf(dot_lds<KS>(sE, row), kPMin);
+    a.r_out[beg + n] = rdiv(a.counts[beg + n], fmaxf(dot_lds<KS>(sE, row), kPMin));
   }
   if (wv == 0) {
     double ass = 0.0;
@@ -515,7 +515,7 @@ __global__ __launch_bounds__(256) void lda_estep_thread(EStepArgs a) {
         p1_ = fmaf(e[k + 1], row[k + 1], p1_);
       }
       const float P = fmaxf(p0_ + p1_, kPMin);
-      const float r = cnt / P;
+      const float r = rdiv(cnt, P);
       lsum = fmaf(cnt, __logf(P), lsum);
 #pragma unroll
       for (int k = 0; k < KS; ++k) acc[k] = fmaf(r, row[k], acc[k]);

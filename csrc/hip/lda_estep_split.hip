@@ -177,7 +177,7 @@ __global__ __launch_bounds__(kNT) void lda_estep_split(EStepArgs a, SplitArgs s)
     for (int c = 0; c < CW; ++c) {
       if (t + kNT * c < N) {
         const float P = fmaxf(dot_lds<KS>(sE, bc[c]), kPMin);
-        const float r = cc[c] / P;
+        const float r = rdiv(cc[c], P);
         lsum = fmaf(cc[c], __logf(P), lsum);
 #pragma unroll
         for (int k = 0; k < KS; ++k) acc[k] = fmaf(r, bc[c][k], acc[k]);
@@ -285,7 +285,7 @@ __global__ __launch_bounds__(kNT) void lda_estep_split(EStepArgs a, SplitArgs s)
 #pragma unroll
   for (int c = 0; c < CW; ++c) {
     const int n = t + kNT * c;
-    if (n < N) a.r_out[beg + n] = cc[c] / fmaxf(dot_lds<KS>(sE, bc[c]), kPMin);
+    if (n < N) a.r_out[beg + n] = rdiv(cc[c], fmaxf(dot_lds<KS>(sE, bc[c]), kPMin));
   }
   if (wv == 0 && seg == 0) {
     double ass = 0.0;

@@ -162,7 +162,7 @@ __device__ __forceinline__ void word_pass(const EStepArgs& a, int beg, int N, in
   for (int i = 0; i < CW; ++i) {
     if (s + S * i < N) {   // slot-uniform
       const float P = fmaxf(tg_sum<TG>(dot4<CPL>(e, c.bc[i])), kPMin);
-      const float r = c.cc[i] / P;
+      const float r = rdiv(c.cc[i], P);
       if (q == 0) lsum = fmaf(c.cc[i], __logf(P), lsum);
       axpy4<CPL>(r, c.bc[i], acc);
     }
@@ -179,7 +179,7 @@ __device__ __forceinline__ void word_pass(const EStepArgs& a, int beg, int N, in
 #pragma unroll
     for (int u = 0; u < UNR; ++u) {
       const float P = fmaxf(tg_sum<TG>(dot4<CPL>(e, rows[u])), kPMin);
-      const float x = cn[u] / P;
+      const float x = rdiv(cn[u], P);
       if (q == 0) {
         lsum = fmaf(cn[u], __logf(P), lsum);
         a.r_out[beg + n + u * S] = x;
@@ -192,7 +192,7 @@ __device__ __forceinline__ void word_pass(const EStepArgs& a, int beg, int N, in
     const float c0 = a.counts[beg + n];
     load_chunks<KS, TG>(a.beta, a.word_idx[beg + n], q, r0);
     const float P0 = fmaxf(tg_sum<TG>(dot4<CPL>(e, r0)), kPMin);
-    const float x0 = c0 / P0;
+    const float x0 = rdiv(c0, P0);
     if (q == 0) {
       lsum = fmaf(c0, __logf(P0), lsum);
       a.r_out[beg + n] = x0;
@@ -213,7 +213,7 @@ __device__ __forceinline__ void write_r(const EStepArgs& a, int beg, int N, int 
     const int n = s + S * i;
     if (n < N) {
       const float P = fmaxf(tg_sum<TG>(dot4<CPL>(e, c.bc[i])), kPMin);
-      if (q == 0) a.r_out[beg + n] = c.cc[i] / P;
+      if (q == 0) a.r_out[beg + n] = rdiv(c.cc[i], P);
     }
   }
   if (streamed) {
@@ -221,7 +221,7 @@ __device__ __forceinline__ void write_r(const EStepArgs& a, int beg, int N, int 
       float4 row[CPL];
       load_chunks<KS, TG>(a.beta, a.word_idx[beg + n], q, row);
       const float P = fmaxf(tg_sum<TG>(dot4<CPL>(e, row)), kPMin);
-      if (q == 0) a.r_out[beg + n] = a.counts[beg + n] / P;
+      if (q == 0) a.r_out[beg + n] = rdiv(a.counts[beg + n], P);
     }
   }
 }
