@@ -64,4 +64,103 @@ __device__ __forceinline__ bool load_params(Args& a) {
   return false;
 }
 
+// ---------------------------------------------------------------------------
+// Split-document hand-off: iteration-tagged 8-byte granules {float, uint32 tag}.
+// A 64-bit aligned relaxed atomic store / load is single-copy atomic, so a reader
+// that sees the tag sees the value; agent scope makes the accesses coherent
+// across XCDs (sc1, no stale L2 / L1 lines).  Tag = (launch epoch << 12) |
+// (iteration & 0xfff): iteration bits separate it from it - 2 (the previous use
+// of the parity buffer), the epoch separates launches.
+// ---------------------------------------------------------------------------
+constexpr long kSplitSpinLimit = 1L << 24;   // ~seconds of polling, then give up (error flag)
+
+__device__ __forceinline__ unsigned split_tag(int epoch, int it) {
+  return ((unsigned)(epoch & 0xfffff) << 12) | (unsigned)(it & 0xfff);
+}
+
+__device__ __forceinline__ void put_tagged(unsigned long long* p, float v, unsigned tag) {
+  const unsigned long long g = ((unsigned long long)tag << 32) | (unsigned long long)__float_as_uint(v);
+  __hip_atomic_store(p, g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// sum_{q < n} value(x[q * stride]) in order q = 0, 1, ..., each granule awaited until it
+// carries `tag`; 8 loads in flight per round trip.  Returns false on a timeout.
+__device__ __forceinline__ bool tagged_sum(const unsigned long long* x, int n, int stride, unsigned tag, float& out) {
+  float s = 0.f;
+  long spins = 0;
+  for (int q0 = 0; q0 < n; q0 += 8) {
+    unsigned long long v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      v[u] = __hip_atomic_load(x + (size_t)min(q0 + u, n - 1) * stride, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      if (q0 + u >= n) continue;
+      while ((unsigned)(v[u] >> 32) != tag) {
+        if (++spins > kSplitSpinLimit) {
+          out = __builtin_nanf("");
+          return false;
+        }
+        __builtin_amdgcn_s_sleep(1);
+        v[u] = __hip_atomic_load(x + (size_t)(q0 + u) * stride, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      s += __uint_as_float((unsigned)(v[u] & 0xffffffffu));
+    }
+  }
+  out = s;
+  return true;
+}
+
+// The same for the (hi, lo) float pairs of a double: sum_q ((double)hi_q + (double)lo_q).
+__device__ __forceinline__ bool tagged_sum2(const unsigned long long* x, int n, int stride, unsigned tag, double& out) {
+  double s = 0.0;
+  long spins = 0;
+  for (int q = 0; q < n; ++q) {
+    unsigned long long h, l;
+    do {
+      h = __hip_atomic_load(x + (size_t)q * stride, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      l = __hip_atomic_load(x + (size_t)q * stride + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if ((unsigned)(h >> 32) == tag && (unsigned)(l >> 32) == tag) break;
+      if (++spins > kSplitSpinLimit) {
+        out = __builtin_nan("");
+        return false;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    } while (true);
+    s += (double)__uint_as_float((unsigned)(h & 0xffffffffu)) + (double)__uint_as_float((unsigned)(l & 0xffffffffu));
+  }
+  out = s;
+  return true;
+}
+
+// Publish one segment's iteration partials: lanes 0..63 of the calling wave write the
+// KS topic granules (acc_of(k)), lane 0 also the log-sum pair.
+template <int KS, typename AccOf>
+__device__ __forceinline__ void publish_tagged(unsigned long long* row, AccOf acc_of, double lsum, int lane,
+                                               unsigned tag) {
+#pragma unroll
+  for (int j = 0; j < (KS + 63) / 64; ++j) {
+    const int k = lane + 64 * j;
+    if (k < KS) put_tagged(row + k, acc_of(j), tag);
+  }
+  if (lane == 0) {
+    const float hi = (float)lsum;
+    const float lo = (float)(lsum - (double)hi);
+    put_tagged(row + KS, hi, tag);
+    put_tagged(row + KS + 1, lo, tag);
+  }
+}
+
+// End of a split launch: the last segment of the document to get here bumps the
+// document's epoch and resets the exit count (graph replays need no memset).
+__device__ __forceinline__ void split_exit(int* counter, int n_docs, int nseg) {
+  if (threadIdx.x == 0) {
+    int* exits = counter + n_docs;
+    if (__hip_atomic_fetch_add(exits, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nseg - 1) {
+      __hip_atomic_store(exits, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_fetch_add(counter, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
 }  // namespace oni

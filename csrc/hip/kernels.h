@@ -38,12 +38,14 @@ enum EStepVariant : int {
 };
 
 // Huge documents (the long-context analogue): one document is
-// split into `nseg` contiguous word segments, one 4-wave workgroup each; every
+// split into `nseg` contiguous word segments, one workgroup each; every
 // variational iteration the segments exchange their partial
-// (sum_n c_n beta_n / P_n, sum_n c_n log P_n) through global memory behind a
-// per-document arrival counter, and each workgroup then runs the identical
-// (deterministic) topic update.  All workgroups of one launch must be
-// co-resident: the host caps a launch at kSplitMaxBlocks workgroups.
+// (sum_n c_n beta_n / P_n, sum_n c_n log P_n) through global memory as
+// iteration-tagged 8-byte granules {float value, uint32 tag} -- a reader polls
+// the granules themselves, so a hand-off costs one write and the polling reads
+// (no arrival counter, no store-completion wait) -- and each workgroup then runs
+// the identical (deterministic) topic update.  All workgroups of one launch must
+// be co-resident: the host caps a launch at kSplitMaxBlocks workgroups.
 constexpr int kSplitMaxBlocks = 192;   // 8-wave workgroups, ~1 per CU: keep a margin below 256 CUs
 struct SplitArgs {
   const int* seg_doc;     // [n_blocks] document of each workgroup
@@ -53,12 +55,12 @@ struct SplitArgs {
   const int* doc_slot;    // [n_blocks] counter slot of the document
   int n_blocks;
   int seg_words;          // words per segment
-  float* partial;         // [2][n_blocks][KS]  partial accumulators (parity double-buffer)
-  double* partial_l;      // [2][n_blocks]      partial sum_n c_n log P_n
-  int* counter;           // [2][n_docs] arrival / exit counts; zero before the first launch, and the
-                          // kernel leaves them zero again (the last workgroup of a document resets them)
+  unsigned long long* xchg;  // [2][n_blocks][KS + 2] tagged granules (parity double-buffer): KS topic
+                             // partials, then sum_n c_n log P_n as a float pair (hi, lo)
+  int* counter;           // [2][n_docs] per document: launch epoch (tags of different launches never
+                          // match), exit count (the last segment out bumps the epoch, resets the count)
   int n_docs;             // documents in this launch
-  int* error;             // set to 1 if a barrier wait times out (never hangs the GPU)
+  int* error;             // set to 1 if a wait times out (never hangs the GPU)
 };
 
 struct EStepArgs {

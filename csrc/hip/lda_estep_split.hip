@@ -9,22 +9,24 @@
 //
 //   1. computes E from its (replicated) topic state,
 //   2. reduces its segment's sum_n (c_n/P_n) beta_n  and  sum_n c_n log P_n
-//      over its 4 waves (LDS),
-//   3. publishes them to partial[it & 1][block] and arrives on the document's
-//      counter (agent-scope release; microarch guide "Valid forms": storing
-//      wave waits vmcnt(0), release fence, vmcnt(0), relaxed atomic add),
-//   4. waits until all nseg segments arrived (relaxed agent-scope poll with
-//      s_sleep, then one agent-scope acquire; the spin is bounded and reports
-//      a timeout through `error` instead of hanging the GPU),
-//   5. sums the nseg partials in segment order -- identical bits in every
-//      workgroup -- and runs the same deterministic topic update, so all
-//      segments agree on gamma and on the convergence decision without a
-//      second barrier.
-// Parity double-buffering makes one barrier per iteration sufficient: a
+//      over its waves (LDS),
+//   3. publishes them as iteration-tagged 8-byte granules {value, tag} to
+//      xchg[it & 1][block] (relaxed agent-scope 64-bit stores: single-copy
+//      atomic, so a reader that sees the tag sees the value),
+//   4. polls the nseg segments' granules of this iteration directly (8 loads in
+//      flight, s_sleep between rounds, bounded: a timeout sets `error`) and sums
+//      them in segment order -- identical bits in every workgroup --
+//   5. runs the same deterministic topic update, so all segments agree on gamma
+//      and on the convergence decision without a second barrier.
+// One write + the polling reads per iteration: no arrival counter and no wait for
+// store completion (a counter-based barrier costs about two more fabric round
+// trips per iteration -- the split chain is the E-step's critical path).
+// Parity double-buffering makes one exchange per iteration sufficient: a
 // workgroup can only overwrite buffer (it & 1) again at iteration it + 2, after
-// every segment has passed barrier it + 1, i.e. finished reading iteration it.
-// The launch is capped at kSplitMaxBlocks workgroups (one per CU), so all
-// segments are co-resident and the barrier cannot deadlock.
+// every segment has read iteration it.  The tag holds the document's launch
+// epoch, bumped by its last segment on exit, so granules of an earlier launch
+// never match.  The launch is capped at kSplitMaxBlocks workgroups (one per CU),
+// so all segments are co-resident and the exchange cannot deadlock.
 #include <stdexcept>
 #include <string>
 
@@ -38,50 +40,6 @@ namespace {
 
 constexpr int kNW = 8;      // 8 waves x rows_per_lane_8w rows: 4096 words per segment at K <= 20
 constexpr int kNT = kNW * 64;
-constexpr long kSpinLimit = 1L << 26;   // ~ seconds of polling, then give up (error flag)
-
-__device__ __forceinline__ void publish_arrive(int* counter) {
-  // caller: the storing wave, after its write-through (sc1) partial stores; those
-  // need no release fence (microarch guide, split-K "Equally valid" form): drain, then arrive
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_add(counter, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-__device__ __forceinline__ bool wait_count(int* counter, int target, int* error) {
-  bool ok = true;
-  if ((threadIdx.x & 63) == 0) {
-    long spins = 0;
-    while (__hip_atomic_load(counter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
-      __builtin_amdgcn_s_sleep(2);
-      if (++spins > kSpinLimit) {
-        ok = false;
-        __hip_atomic_store(error, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        break;
-      }
-    }
-  }
-  ok = __shfl(ok ? 1 : 0, 0) != 0;
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  return ok;
-}
-
-// sum_{q < n} x[q * stride] in order q = 0, 1, ... with 8 loads in flight per
-// round trip; loads are unconditional (clamped index) so hipcc does not branch
-// around each one and wait per element.
-template <typename T>
-__device__ __forceinline__ T ordered_sum(const T* x, int n, int stride) {
-  T s = T(0);
-  for (int q0 = 0; q0 < n; q0 += 8) {
-    T v[8];
-#pragma unroll
-    for (int u = 0; u < 8; ++u) v[u] = x[(size_t)min(q0 + u, n - 1) * stride];
-#pragma unroll
-    for (int u = 0; u < 8; ++u)
-      if (q0 + u < n) s += v[u];
-  }
-  return s;
-}
 
 }  // namespace
 
@@ -102,6 +60,7 @@ __global__ __launch_bounds__(kNT) void lda_estep_split(EStepArgs a, SplitArgs s)
   const int nseg = s.seg_count[b];
   const int base = s.seg_base[b];
   int* counter = s.counter + s.doc_slot[b];
+  const int epoch = __hip_atomic_load(counter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const int dbeg = a.doc_ptr[d];
   const int Ndoc = a.doc_ptr[d + 1] - dbeg;
   const int beg = dbeg + seg * s.seg_words;
@@ -195,27 +154,26 @@ __global__ __launch_bounds__(kNT) void lda_estep_split(EStepArgs a, SplitArgs s)
     if (wv == 0) {
       ++it;
       const int par = it & 1;
-      // publish this segment's partial, arrive, wait for all segments
-      float* prow = s.partial + ((size_t)par * s.n_blocks + b) * KS;
+      const unsigned tag = split_tag(epoch, it);
+      constexpr int GR = KS + 2;
+      // publish this segment's partials, then gather every segment's (in segment order)
+      float part[TJ];
 #pragma unroll
       for (int j = 0; j < TJ; ++j) {
         const int k = lane + 64 * j;
+        float v = 0.f;
         if (k < KS) {
-          float v = 0.f;
 #pragma unroll
           for (int w = 0; w < kNW; ++w) v += sRed[w][k];
-          __hip_atomic_store(prow + k, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // sc1 write-through
         }
+        part[j] = v;
       }
-      if (lane == 0) {
-        double l = 0.0;
+      double lpart = 0.0;
 #pragma unroll
-        for (int w = 0; w < kNW; ++w) l += sRedD[w];
-        __hip_atomic_store(s.partial_l + (size_t)par * s.n_blocks + b, l, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-      publish_arrive(counter);
-      const bool ok = wait_count(counter, nseg * it, s.error);
-      // all segments' partials, summed in segment order (bitwise identical in every workgroup)
+      for (int w = 0; w < kNW; ++w) lpart += sRedD[w];
+      unsigned long long* xb = s.xchg + (size_t)par * s.n_blocks * GR;
+      publish_tagged<KS>(xb + (size_t)b * GR, [&](int j) { return part[j]; }, lpart, lane, tag);
+      bool ok = true;
       double lsum_d = 0.0;
       float gn[TJ];
       float sg = 0.f;
@@ -223,13 +181,14 @@ __global__ __launch_bounds__(kNT) void lda_estep_split(EStepArgs a, SplitArgs s)
       for (int j = 0; j < TJ; ++j) {
         const int k = lane + 64 * j;
         float ak = 0.f;
-        if (k < KS) {
-          ak = ordered_sum(s.partial + ((size_t)par * s.n_blocks + base) * KS + k, nseg, KS);
-        }
+        if (k < KS) ok &= tagged_sum(xb + (size_t)base * GR + k, nseg, GR, tag, ak);
         gn[j] = (k < K) ? fmaf(e[j], ak, alpha) : 0.f;
         sg += gn[j];
       }
-      lsum_d = ordered_sum(s.partial_l + (size_t)par * s.n_blocks + base, nseg, 1);
+      if (lane == 0) ok &= tagged_sum2(xb + (size_t)base * GR + KS, nseg, GR, tag, lsum_d);
+      lsum_d = __shfl(lsum_d, 0);
+      ok = __all(ok);
+      if (!ok && lane == 0) __hip_atomic_store(s.error, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       const float S = group_sum<64>(sg);
       float dS, lgS;
       digamma_lgamma(S, dS, lgS);
@@ -269,16 +228,8 @@ __global__ __launch_bounds__(kNT) void lda_estep_split(EStepArgs a, SplitArgs s)
     __syncthreads();
   }
 
-  // Every wave of this workgroup has passed its last barrier (the loop ends on a
-  // __syncthreads).  The last workgroup of the document to get here zeroes the
-  // arrival and exit counts for the next launch, so a replayed graph needs no memset.
-  if (t == 0) {
-    int* exits = counter + s.n_docs;
-    if (__hip_atomic_fetch_add(exits, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nseg - 1) {
-      __hip_atomic_store(counter, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(exits, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
+  // Every wave of this workgroup has passed its last exchange (the loop ends on a __syncthreads).
+  split_exit(counter, s.n_docs, nseg);
   const bool failed = __hip_atomic_load(s.error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
 
   // ---- outputs: r for this segment; the document state from segment 0 ----

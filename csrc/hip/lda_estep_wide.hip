@@ -516,45 +516,6 @@ __global__ __launch_bounds__(NW * 64) void lda_estep_wblock(EStepArgs a) {
 namespace {
 constexpr int kWNW = 8;
 constexpr int kWNT = kWNW * 64;
-constexpr long kWSpinLimit = 1L << 26;
-
-__device__ __forceinline__ void w_publish_arrive(int* counter) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  if ((threadIdx.x & 63) == 0) __hip_atomic_fetch_add(counter, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-__device__ __forceinline__ bool w_wait_count(int* counter, int target, int* error) {
-  bool ok = true;
-  if ((threadIdx.x & 63) == 0) {
-    long spins = 0;
-    while (__hip_atomic_load(counter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
-      __builtin_amdgcn_s_sleep(2);
-      if (++spins > kWSpinLimit) {
-        ok = false;
-        __hip_atomic_store(error, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        break;
-      }
-    }
-  }
-  ok = __shfl(ok ? 1 : 0, 0) != 0;
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  return ok;
-}
-
-template <typename T>
-__device__ __forceinline__ T w_ordered_sum(const T* x, int n, int stride) {
-  T s = T(0);
-  for (int q0 = 0; q0 < n; q0 += 8) {
-    T v[8];
-#pragma unroll
-    for (int u = 0; u < 8; ++u) v[u] = x[(size_t)min(q0 + u, n - 1) * stride];
-#pragma unroll
-    for (int u = 0; u < 8; ++u)
-      if (q0 + u < n) s += v[u];
-  }
-  return s;
-}
 }  // namespace
 
 template <int KS, int TG, int CW, int UNR>
@@ -581,6 +542,7 @@ __global__ __launch_bounds__(kWNT) void lda_estep_wsplit(EStepArgs a, SplitArgs 
   const int nseg = sp.seg_count[b];
   const int base = sp.seg_base[b];
   int* counter = sp.counter + sp.doc_slot[b];
+  const int epoch = __hip_atomic_load(counter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const int dbeg = a.doc_ptr[d];
   const int Ndoc = a.doc_ptr[d + 1] - dbeg;
   const int beg = dbeg + seg * sp.seg_words;
@@ -640,34 +602,38 @@ __global__ __launch_bounds__(kWNT) void lda_estep_wsplit(EStepArgs a, SplitArgs 
     if (wv == 0) {
       ++it;
       const int par = it & 1;
-      float* prow = sp.partial + ((size_t)par * sp.n_blocks + b) * KS;
+      const unsigned tag = split_tag(epoch, it);
+      constexpr int GR = KS + 2;
+      float part[TP::TJ];
 #pragma unroll
       for (int j = 0; j < TP::TJ; ++j) {
         const int k = lane + 64 * j;
+        float v = 0.f;
         if (k < KS) {
-          float v = 0.f;
 #pragma unroll
           for (int h = 0; h < H; ++h) v += sPart[h][k];
-          __hip_atomic_store(prow + k, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // sc1 write-through
         }
+        part[j] = v;
       }
-      if (lane == 0) {
-        double l = 0.0;
+      double lpart = 0.0;
 #pragma unroll
-        for (int w = 0; w < kWNW; ++w) l += sRedD[w];
-        __hip_atomic_store(sp.partial_l + (size_t)par * sp.n_blocks + b, l, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-      }
-      w_publish_arrive(counter);
-      const bool ok = w_wait_count(counter, nseg * it, sp.error);
+      for (int w = 0; w < kWNW; ++w) lpart += sRedD[w];
+      unsigned long long* xb = sp.xchg + (size_t)par * sp.n_blocks * GR;
+      publish_tagged<KS>(xb + (size_t)b * GR, [&](int j) { return part[j]; }, lpart, lane, tag);
       // every segment's partials in segment order: identical bits in every workgroup
+      bool ok = true;
       float acc[TP::TJ];
 #pragma unroll
       for (int j = 0; j < TP::TJ; ++j) {
         const int k = lane + 64 * j;
-        acc[j] = (k < KS) ? w_ordered_sum(sp.partial + ((size_t)par * sp.n_blocks + base) * KS + k, nseg, KS) : 0.f;
+        acc[j] = 0.f;
+        if (k < KS) ok &= tagged_sum(xb + (size_t)base * GR + k, nseg, GR, tag, acc[j]);
       }
-      const double lsum_d = w_ordered_sum(sp.partial_l + (size_t)par * sp.n_blocks + base, nseg, 1);
+      double lsum_d = 0.0;
+      if (lane == 0) ok &= tagged_sum2(xb + (size_t)base * GR + KS, nseg, GR, tag, lsum_d);
+      lsum_d = __shfl(lsum_d, 0);
+      ok = __all(ok);
+      if (!ok && lane == 0) __hip_atomic_store(sp.error, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       L = topics_update<KS, 64>(T, acc, lane, K, alpha, a.lik_const, lsum_d, m, total, dsum);
       conv = (lik_old - L) / lik_old;
       lik_old = L;
@@ -679,14 +645,7 @@ __global__ __launch_bounds__(kWNT) void lda_estep_wsplit(EStepArgs a, SplitArgs 
     load_e<KS, TG>(sE, q, e4);
   }
 
-  // the last workgroup of the document out re-zeroes its counters (graph replays need no memset)
-  if (t == 0) {
-    int* exits = counter + sp.n_docs;
-    if (__hip_atomic_fetch_add(exits, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == nseg - 1) {
-      __hip_atomic_store(counter, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(exits, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
+  split_exit(counter, sp.n_docs, nseg);
   const bool failed = __hip_atomic_load(sp.error, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0;
   write_r<KS, TG, CW>(a, beg, N, s, S, q, cache, e4, !ran);
   if (wv == 0 && seg == 0) topics_out<KS, 64>(a, T, d, lane, K, failed ? __builtin_nan("") : L, dsum, it);

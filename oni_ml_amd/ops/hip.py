@@ -199,9 +199,10 @@ class SplitPlan:
         t = lambda a: torch.tensor(np.asarray(a, np.int32), device=device)
         nb = len(sd)
         return dict(seg_doc=t(sd), seg_index=t(si), seg_count=t(sc), seg_base=t(sb), doc_slot=t(slot), n_blocks=nb,
-                    partial=torch.zeros(2 * nb * KS, dtype=torch.float32, device=device),
-                    partial_l=torch.zeros(2 * nb, dtype=torch.float64, device=device),
-                    counter=torch.zeros(2 * len(docs), dtype=torch.int32, device=device),   # kernel re-zeroes
+                    # tagged hand-off granules {float, uint32 tag}: [2][n_blocks][KS + 2]
+                    xchg=torch.zeros(2 * nb * (KS + 2), dtype=torch.int64, device=device),
+                    # per document: launch epoch, exit count (the kernel keeps both consistent)
+                    counter=torch.zeros(2 * len(docs), dtype=torch.int32, device=device),
                     error=torch.zeros(1, dtype=torch.int32, device=device), docs=len(docs))
 
 
@@ -225,8 +226,7 @@ def lda_estep_split(doc_ptr, word_idx, counts, beta, K, alpha, lik_const, var_ma
         _chk(alpha_ss, torch.float64, "alpha_ss", (D,), dev), _chk(iters, torch.int32, "iters", (D,), dev),
         batch["seg_doc"].data_ptr(), batch["seg_index"].data_ptr(), batch["seg_count"].data_ptr(),
         batch["seg_base"].data_ptr(), batch["doc_slot"].data_ptr(), int(nb), int(seg_words),
-        _chk(batch["partial"], torch.float32, "partial", (2 * nb * KS,), dev),
-        _chk(batch["partial_l"], torch.float64, "partial_l", (2 * nb,), dev),
+        _chk(batch["xchg"], torch.int64, "xchg", (2 * nb * (KS + 2),), dev),
         _chk(batch["counter"], torch.int32, "counter", (2 * batch["docs"],), dev), int(batch["docs"]),
         _chk(batch["error"], torch.int32, "error", (1,), dev),
         _params_ptr(params, dev), _stream())

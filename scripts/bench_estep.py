@@ -68,7 +68,8 @@ def main():
                 ud = np.unique(docs)
                 ms = timed(lambda: H.lda_estep_split(dc.doc_ptr, dc.word_idx, dc.counts, eng.beta, eng.K, eng.alpha, lc,
                                                      eng.var_max_iter, eng.settings.var_converged, eng.gamma, eng.e,
-                                                     eng.r, eng.lik, eng.ass, eng.iters, batch, sp.seg_words))
+                                                     eng.r, eng.lik, eng.ass, eng.iters, batch, sp.seg_words,
+                                                     wide=sp.wide))
                 rows.append(dict(bucket=f"split[{bi}]", docs=int(ud.size), blocks=int(batch["n_blocks"]),
                                  len_min=int(lens[ud].min()), len_max=int(lens[ud].max()),
                                  it_mean=round(float(it[ud].mean()), 2), it_max=int(it[ud].max()), ms=round(ms, 4)))
@@ -77,7 +78,7 @@ def main():
             ms = timed(lambda: H.lda_estep(dc.doc_ptr, dc.word_idx, dc.counts, order, eng.beta, eng.K, eng.alpha, lc,
                                            eng.var_max_iter, eng.settings.var_converged, eng.gamma, eng.e, eng.r,
                                            eng.lik, eng.ass, eng.iters, var))
-            rows.append(dict(bucket=["G16", "G32", "G64", "G64C", "B4", "B8", "T1"][var], docs=int(o.size),
+            rows.append(dict(bucket=["G16", "G32", "G64", "G64C", "B4", "B8", "T1", "W16", "W32", "W64", "WB4", "WB8"][var], docs=int(o.size),
                              len_min=int(lens[o].min()), len_max=int(lens[o].max()),
                              it_mean=round(float(it[o].mean()), 2), it_max=int(it[o].max()), ms=round(ms, 4)))
 
