@@ -111,10 +111,13 @@ def load_checkpoint(outdir: str) -> Optional[dict]:
 def estimate(corpus: Corpus, num_topics: int, alpha_init: float, settings: LDASettings, start: str, outdir: str,
              backend: str = "auto", device=None, dist=None, seed: int = 0, resume: bool = False,
              write_word_assignments: bool = False, write_rank_gamma: bool = False, verbose: bool = False,
-             fault_at_iteration: Optional[int] = None) -> LDAResult:
+             fault_at_iteration: Optional[int] = None, defer_files: bool = False) -> LDAResult:
     """Run EM and write lda-c files.  `start`: random | seeded | <model prefix>.
 
-    `fault_at_iteration` raises after that EM iteration (fault-injection hook for the resume tests)."""
+    `fault_at_iteration` raises after that EM iteration (fault-injection hook for the resume tests).
+    `defer_files`: return while the background writer is still formatting the LAG / final model
+    files; the caller must call ``res.close_files()`` (which re-raises a write error).  Without it
+    the files are complete when this returns."""
     rank0 = dist is None or dist.rank == 0
     if rank0:
         os.makedirs(outdir, exist_ok=True)
@@ -181,11 +184,15 @@ def estimate(corpus: Corpus, num_topics: int, alpha_init: float, settings: LDASe
             writer.submit(np.savez, os.path.join(outdir, "final_model.npz"), log_beta=lb, gamma=g,
                           alpha=np.float64(e.alpha))
 
+    ok = False
     try:
         res = eng.run(start=mode, corpus_global=corpus, on_iteration=on_iteration, on_save=on_save,
                       start_iteration=start_it, likelihood_old=L_old, verbose=verbose and rank0)
+        ok = True
     finally:
-        writer.close()
+        if not (ok and defer_files):
+            writer.close()
+    res.close_files = writer.close if defer_files else (lambda: None)
     res.likelihoods = history
     res.log_beta = eng.log_beta()
     res.gamma = eng.gather_gamma()

@@ -53,7 +53,8 @@ def run_lda(cfg, corpus: Corpus, dist=None, device=None, log=print):
     return estimate(corpus, cfg.topics, cfg.alpha, cfg.settings, cfg.start, outdir, backend=cfg.backend,
                     device=device, dist=dist, seed=cfg.seed, resume=cfg.resume,
                     write_word_assignments=cfg.word_assignments, write_rank_gamma=cfg.rank_gamma,
-                    verbose=cfg.verbose, fault_at_iteration=cfg.extra.get("fault_at_iteration"))
+                    verbose=cfg.verbose, fault_at_iteration=cfg.extra.get("fault_at_iteration"),
+                    defer_files=dist is None or dist.world_size <= 1)
 
 
 def run_export(cfg, doc_names, gamma, word_names, log_beta) -> ModelTables:

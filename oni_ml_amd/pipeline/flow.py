@@ -84,6 +84,7 @@ def run(cfg, dist=None, device=None, log=print) -> dict:
             corpus = dist.broadcast_corpus(corpus)
         with R.stage("lda") as res:
             lres = C.run_lda(cfg, corpus, dist=dist, device=device, log=log)
+            res["_defer"] = lres.close_files   # LAG / final model files: written while later stages run
             res.update(em_iterations=lres.em_iterations, likelihood=lres.likelihoods[-1][0] if lres.likelihoods else 0.0,
                        alpha=lres.alpha)
             summary["lda"] = dict(em_iterations=lres.em_iterations, seconds=lres.seconds, alpha=lres.alpha,
@@ -93,28 +94,34 @@ def run(cfg, dist=None, device=None, log=print) -> dict:
         R.skip("lda")
         gamma = log_beta = None
     if rank != 0:
+        R.finish_deferred()
         return summary
+    try:
 
-    # ------------------------------------------------------------- lda_post
-    if not R.done("lda_post"):
-        if doc_names is None:
-            _, doc_names, word_names = C.load_corpus_files(cfg.lpath)
-        if gamma is None:
-            from ..models.lda.estimate import load_final
-            gamma, log_beta = load_final(cfg.lpath)
-        with R.stage("lda_post") as res:
-            tables = C.strict_tables(C.run_export(cfg, doc_names, gamma, word_names, log_beta), cfg.strict)
-    else:
-        R.skip("lda_post")
-        tables = C.load_model_tables(cfg.lpath)
+        # ------------------------------------------------------------- lda_post
+        if not R.done("lda_post"):
+            if doc_names is None:
+                _, doc_names, word_names = C.load_corpus_files(cfg.lpath)
+            if gamma is None:
+                from ..models.lda.estimate import load_final
+                gamma, log_beta = load_final(cfg.lpath)
+            with R.stage("lda_post") as res:
+                tables = C.strict_tables(C.run_export(cfg, doc_names, gamma, word_names, log_beta), cfg.strict)
+        else:
+            R.skip("lda_post")
+            tables = C.load_model_tables(cfg.lpath)
 
-    # ------------------------------------------------------------ flow_post
-    if not R.done("flow_post"):
-        with R.stage("flow_post") as res:
-            res.update(score_flow(cfg, ft, tables, device, log))
-            summary["scored"] = res.get("flagged")
-    else:
-        R.skip("flow_post")
+        # ------------------------------------------------------------ flow_post
+        if not R.done("flow_post"):
+            with R.stage("flow_post") as res:
+                res.update(score_flow(cfg, ft, tables, device, log))
+                summary["scored"] = res.get("flagged")
+        else:
+            R.skip("flow_post")
+    except BaseException:
+        R.finish_deferred(suppress=True)
+        raise
+    R.finish_deferred()
     summary["stage_seconds"] = dict(R.times)
     return summary
 

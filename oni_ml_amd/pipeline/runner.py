@@ -80,6 +80,7 @@ class StageRunner:
         self.log = log
         self.sync = sync
         self.times = {}
+        self._pending = []          # (name, record, join): stages whose outputs are still being written
         if rank == 0:
             os.makedirs(self.mdir, exist_ok=True)
 
@@ -126,13 +127,45 @@ class StageRunner:
             range_pop()
         dt = time.perf_counter() - t0
         self.times[name] = self.times.get(name, 0.0) + dt
+        join = result.pop("_defer", None)
         rec = dict(stage=name, status="ok", seconds=dt, ts=time.time(), **meta,
                    **{k: v for k, v in result.items() if isinstance(v, (int, float, str, bool))})
         self.emit(rec)
+        if join is not None:
+            # the stage's results are in memory (later stages use them now); its files are still
+            # being written in the background: the completion marker waits for them (finish_deferred)
+            self._pending.append((name, rec, join))
+            if self.rank == 0:
+                self.log(f"[stage {name}] {dt:.3f}s (files pending)")
+            return
+        self._mark(name, rec)
+        if self.rank == 0:
+            self.log(f"[stage {name}] {dt:.3f}s")
+
+    def _mark(self, name: str, rec: dict):
         if self.rank == 0:
             with open(os.path.join(self.mdir, name + ".done"), "w") as f:
                 json.dump(rec, f)
-            self.log(f"[stage {name}] {dt:.3f}s")
+
+    def finish_deferred(self, suppress: bool = False):
+        """Wait for background output writers; a stage is marked complete only once its files are.
+        ``suppress``: another error is already propagating -- drain the writers, raise nothing."""
+        pending, self._pending = self._pending, []
+        err = None
+        for name, rec, join in pending:
+            t0 = time.perf_counter()
+            try:
+                join()
+            except Exception as e:  # noqa: BLE001 -- re-raised after the other writers finished
+                self.emit(dict(stage=name, status="failed", seconds=0.0, error=repr(e), ts=time.time()))
+                err = err or e
+                continue
+            wait = time.perf_counter() - t0
+            rec = dict(rec, files_wait_seconds=wait)
+            self.emit(dict(stage=name + ".files", status="ok", seconds=wait, ts=time.time()))
+            self._mark(name, rec)
+        if err is not None and not suppress:
+            raise StageFailed(f"background writes failed: {err!r}") from err
 
     def skip(self, name: str):
         if self.rank == 0:

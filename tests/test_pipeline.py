@@ -239,3 +239,31 @@ def test_hdfs_hooks_command_sequence(tmp_path):
     assert flat == ["-rm /hp/doc_results.csv", "-put /lp/doc_results.csv /hp/.", "-rm /hp/word_results.csv",
                     "-put /lp/word_results.csv /hp/.", "-rm -R -f /hp/word_counts", "-rm -R -f /hp/scored",
                     "-mkdir -p /hp/scored", "-put /lp/flow_results.csv /hp/scored/part-00000"]
+
+
+def test_stage_runner_deferred_markers(tmp_path):
+    """A stage whose files are written in the background is marked complete only after its writer
+    finished; a failed writer raises StageFailed at finish_deferred and leaves no marker."""
+    from oni_ml_amd.pipeline.runner import StageFailed, StageRunner
+    R = StageRunner(str(tmp_path), resume=True, log=lambda *a, **k: None)
+    done = []
+    with R.stage("a") as res:
+        res["_defer"] = lambda: done.append(1)
+    assert not R.done("a")                     # marker waits for the files
+    with R.stage("b"):
+        pass
+    assert R.done("b")
+    R.finish_deferred()
+    assert done == [1] and R.done("a")
+
+    def boom():
+        raise OSError("disk full")
+    with R.stage("c") as res:
+        res["_defer"] = boom
+    with pytest.raises(StageFailed):
+        R.finish_deferred()
+    assert not R.done("c")
+    with R.stage("d") as res:
+        res["_defer"] = boom
+    R.finish_deferred(suppress=True)           # another error already propagating
+    assert not R.done("d")
