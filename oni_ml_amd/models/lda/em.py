@@ -235,6 +235,20 @@ class LDAEngine:
         if backend != "hip":
             self.class_total = torch.zeros(self.KS, dtype=torch.float64, device=self.cw.device)
         self._xchg = self._make_exchange(corpus)
+        # sparse exchange on the GPU: suff-stats of the shared words first, so their all-to-all runs
+        # while the suff-stats of the rank's private words (the bulk) are computed
+        self._overlap = self._xchg is not None and backend == "hip" and \
+            os.environ.get("ONI_DIST_OVERLAP", "1") != "0"
+        if self._overlap:
+            from ...ops import hip as H
+            shared = np.unique(self._xchg.send_idx.cpu().numpy())
+            private = np.setdiff1d(np.arange(self.V, dtype=np.int64), shared, assume_unique=True)
+            wide = _use_wide(self.KS)
+            self._plan_a = H.SuffPlan(self.dc.word_len, self.device, wide=wide, words=shared)
+            self._plan_b = H.SuffPlan(self.dc.word_len, self.device, wide=wide, words=private)
+            nb = max(self._plan_a.n_blocks + self._plan_b.n_blocks, self.suff_plan.n_blocks, 1)
+            self._suff_part = torch.zeros(nb, self.KS, dtype=torch.float64, device=self.device)
+            self._graph_a = self._graph_b = None
 
     def _make_exchange(self, corpus: Corpus):
         """Sparse class_word exchange (parallel/dist.py VocabExchange) when the ranks' vocabularies
@@ -372,7 +386,7 @@ class LDAEngine:
         self._ct_fresh = True
         return self._scalars
 
-    def _launch_estep(self, newton_key=None):
+    def _launch_estep(self, newton_key=None, phase: str = "all"):
         """Enqueue one E-step: document buckets on their streams, then suff-stats (main stream) and
         the likelihood / alpha_ss reduction (side stream).  With ``newton_key`` = (estimate_alpha,
         num_docs) the M-step and the EM convergence test follow in the same launch sequence
@@ -384,6 +398,15 @@ class LDAEngine:
         gate = self._gate
         a = self.alpha
         main = torch.cuda.current_stream(self.device)
+        if phase == "B":
+            # overlap mode, after the shared rows left: the private words' suff-stats, then the class
+            # totals of both launches and the all-reduce input
+            pa, pb = self._plan_a, self._plan_b
+            H.lda_suffstats_fused(dc.word_ptr, dc.csc_ent, dc.csc_doc, pb, self.e, self.r, self.beta,
+                                  self._cw_local, self._suff_part[pa.n_blocks:pa.n_blocks + pb.n_blocks], gate=gate)
+            H.colsum_partials(self._suff_part, pa.n_blocks + pb.n_blocks, self._red_local[2:], gate=gate)
+            self._red.copy_(self._red_local)
+            return
         streams = [main] + self._streams
         self._ev_fork.record(main)
         used = set()
@@ -426,9 +449,18 @@ class LDAEngine:
             self._launch_scalars(newton_key)
         # sufficient statistics: one deterministic CSC gather-reduce launch over every word (empty
         # words included, so cw needs no clearing) + per-workgroup column sums -> class totals
+        if phase == "A":
+            # overlap mode: the shared words' rows first, packed for the all-to-all
+            H.lda_suffstats_fused(dc.word_ptr, dc.csc_ent, dc.csc_doc, self._plan_a, self.e, self.r, self.beta,
+                                  self._cw_local, self._suff_part[:max(self._plan_a.n_blocks, 1)], gate=gate)
+            self._xchg.pack(self._cw_local)
+            if side is not None:
+                self._ev_side.record(side)
+                main.wait_event(self._ev_side)
+            return
         sp = self.suff_plan
         H.lda_suffstats_fused(dc.word_ptr, dc.csc_ent, dc.csc_doc, sp, self.e, self.r, self.beta, self._cw_local,
-                              self._suff_part, gate=gate)
+                              self._suff_part[:max(sp.n_blocks, 1)], gate=gate)
         H.colsum_partials(self._suff_part, sp.n_blocks, self._red_local[2:], gate=gate)
         if side is not None:
             self._ev_side.record(side)
@@ -598,6 +630,22 @@ class LDAEngine:
                     self._fgraph_key = key
                 else:
                     self._fgraph.replay()
+            elif self._overlap:
+                self._run_phase("A")
+                work = self._xchg.exchange(async_op=True)      # shared rows in flight ...
+                self._run_phase("B")                           # ... while the private rows are computed
+                import torch.distributed as td
+                w2 = td.all_reduce(self._red, async_op=True)
+                if work is not None:
+                    work.wait()
+                w2.wait()
+                if not self.use_graph:
+                    self._launch_mstep(*key)
+                elif self._mgraph_key != key:
+                    self._mgraph = self._capture(lambda: self._launch_mstep(*key))
+                    self._mgraph_key = key
+                else:
+                    self._mgraph.replay()
             else:
                 if self.use_graph and self._graph is None:
                     self._capture_estep()             # its warm-up launch is this iteration's E-step
@@ -663,6 +711,17 @@ class LDAEngine:
         with torch.cuda.graph(g):
             launch()
         return g
+
+    def _run_phase(self, phase: str):
+        """One of the two E-step graphs of the overlap mode (captured on first use)."""
+        attr = "_graph_a" if phase == "A" else "_graph_b"
+        g = getattr(self, attr)
+        if not self.use_graph:
+            self._launch_estep(phase=phase)
+        elif g is None:
+            setattr(self, attr, self._capture(lambda: self._launch_estep(phase=phase)))
+        else:
+            g.replay()
 
     def _capture_estep(self):
         self._graph = self._capture(self._launch_estep)

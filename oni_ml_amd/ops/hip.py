@@ -269,14 +269,22 @@ def lda_suffstats(word_ptr, csc_ent, csc_doc, order, e, r, beta, cw, variant, ga
 
 
 class SuffPlan:
-    """Word order for the single-launch suff-stats kernel: [heavy | medium | light] (heavy first)."""
+    """Word order for the single-launch suff-stats kernel: [heavy | medium | light] (heavy first).
+
+    ``words``: restrict the plan to these word ids (a sub-plan; several sub-plans must together
+    cover the vocabulary, since every word's class_word row is written by exactly one launch)."""
     HEAVY, LIGHT = 1024, 64
 
-    def __init__(self, word_len, device, wide: bool = False):
+    def __init__(self, word_len, device, wide: bool = False, words=None):
         import numpy as np
         self.wide = bool(wide)      # wide-topic kernel (lda_suff_wide), KS >= 32
-        order = np.argsort(-np.asarray(word_len), kind="stable").astype(np.int32)
-        L = np.asarray(word_len)[order]
+        wl = np.asarray(word_len)
+        ids = np.arange(wl.size, dtype=np.int64) if words is None else np.asarray(words, np.int64)
+        if ids.size and (ids.min() < 0 or ids.max() >= wl.size):
+            raise ValueError("suff sub-plan word ids out of range")
+        self.covers_all = words is None
+        order = ids[np.argsort(-wl[ids], kind="stable")].astype(np.int32)
+        L = wl[order]
         self.n_heavy = int((L > self.HEAVY).sum())
         self.n_medium = int(((L > self.LIGHT) & (L <= self.HEAVY)).sum())
         self.n_light = int((L <= self.LIGHT).sum())
@@ -290,13 +298,16 @@ def lda_suffstats_fused(word_ptr, csc_ent, csc_doc, plan: "SuffPlan", e, r, beta
     nnz = csc_ent.numel()
     D = e.shape[0]
     dev = beta.device
-    if plan.order.numel() != V:
+    if plan.covers_all and plan.order.numel() != V:
         raise ValueError("suff plan does not cover the vocabulary")
+    if plan.order.numel() == 0:
+        return
     if plan.wide and KS < 32:
         raise ValueError(f"wide suff-stats layout needs KS >= 32 (got {KS})")
     lib().lda_suffstats_fused(
         _chk(word_ptr, torch.int32, "word_ptr", (V + 1,), dev), _chk(csc_ent, torch.int32, "csc_ent", (nnz,), dev),
-        _chk(csc_doc, torch.int32, "csc_doc", (nnz,), dev), _chk(plan.order, torch.int32, "order", (V,), dev),
+        _chk(csc_doc, torch.int32, "csc_doc", (nnz,), dev),
+        _chk(plan.order, torch.int32, "order", (plan.order.numel(),), dev),
         plan.n_heavy, plan.n_medium, plan.n_light,
         _chk(e, torch.float32, "e", (D, KS), dev), _chk(r, torch.float32, "r", (nnz,), dev),
         _chk(beta, torch.float32, "beta", (V, KS), dev), _chk(cw, torch.float32, "cw", (V, KS), dev),

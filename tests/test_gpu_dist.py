@@ -21,8 +21,8 @@ def _port():
     return p
 
 
-def _run(world, exchange):
-    env = dict(os.environ, ONI_DIST_EXCHANGE=exchange, ONI_DIST_BACKEND="gloo")
+def _run(world, exchange, overlap="1"):
+    env = dict(os.environ, ONI_DIST_EXCHANGE=exchange, ONI_DIST_BACKEND="gloo", ONI_DIST_OVERLAP=overlap)
     if world == 1:
         cmd = [sys.executable, "scripts/dist_check.py"]
     else:
@@ -36,9 +36,11 @@ def _run(world, exchange):
 def test_two_rank_hip_exchanges_match_single_rank():
     one = _run(1, "auto")
     dense = _run(2, "dense")
-    sparse = _run(2, "sparse")
+    sparse = _run(2, "sparse")                 # shared rows in flight during the private suff-stats
+    sparse_seq = _run(2, "sparse", overlap="0")
     assert one["exchange"] == "none" and dense["exchange"] == "dense-allreduce"
     assert sparse["exchange"] == "sparse-alltoall" and 0 < sparse["rows"] < 4000
+    assert sparse_seq["likelihoods"] == sparse["likelihoods"]      # same arithmetic, other schedule
     for o in (dense, sparse):
         assert len(o["likelihoods"]) == len(one["likelihoods"])
         assert np.allclose(o["likelihoods"], one["likelihoods"], rtol=2e-6), (o["likelihoods"], one["likelihoods"])
