@@ -258,3 +258,47 @@ def test_split_documents_match_single_workgroup(hip, K):  # K = 50, 100: wide-to
     ref = R.estep_jacobi(torch.from_numpy(c.doc_ptr), torch.from_numpy(c.word_idx), torch.from_numpy(c.counts).double(),
                          eng.beta.double().cpu(), K, eng.alpha, 15, -1e30)
     assert ((g1 - ref["gamma"]).abs() / ref["gamma"].abs().clamp_min(1e-3)).max().item() < 2e-3
+
+
+@pytest.mark.parametrize("K", [3, 13, 24, 33, 77, 128])
+def test_estep_random_corpora_edge_cases(hip, K):
+    """Randomised corpora with the shapes real featurization produces: empty documents, duplicate
+    (doc, word) entries (strict mode keeps the src/dst halves apart), counts > 1, words never used,
+    every length bucket (and split documents); odd K (padding topics).  Every E-step kernel and
+    the suff-stats against the fp64 references, fixed variational iterations."""
+    rng = np.random.default_rng(K)
+    V, D = 1500, 900
+    lens = np.minimum(rng.zipf(1.4, D), 9000)
+    lens[rng.choice(D, 25, replace=False)] = 0                      # empty documents
+    ptr = np.concatenate([[0], np.cumsum(lens)])
+    words = rng.integers(0, V - 100, int(ptr[-1]))                  # the last 100 words never occur
+    for d in rng.choice(np.flatnonzero(lens > 3), 40, replace=False):  # duplicated entries
+        a = ptr[d]
+        words[a + 1] = words[a]
+    counts = rng.integers(1, 4, words.size)
+    c = Corpus(ptr.astype(np.int64), words.astype(np.int32), counts.astype(np.int64), V)
+    dev = torch.device("cuda")
+    eng = LDAEngine(c, K, LDASettings(var_max_iter=8, var_converged=-1e30), backend="hip", seed=K, split_min=2048)
+    eng.init_random()
+    eng.e_step()
+    torch.cuda.synchronize()
+    dc = eng.dc
+    ref = R.estep_jacobi(dc.doc_ptr, dc.word_idx, dc.counts, eng.beta.double(), K, eng.alpha, 8, -1e30)
+    g, gr = eng.gamma[:, :K].double(), ref["gamma"]
+    assert ((g - gr).abs() / gr.abs().clamp_min(1e-3)).max().item() < 2e-3
+    lik = eng.lik
+    # per-document likelihoods near 0 (empty documents: lnG(Ka) - K lnG(a) - lnG(Ka) + K lnG(a)) carry the
+    # fp32 rounding of the K-term topic phase, ~1e-4 absolute at K = 77: compare them absolutely
+    assert ((lik - ref["lik"]).abs() / ref["lik"].abs().clamp_min(10.0)).max().item() < 1e-4
+    nz = lens > 0
+    rr = (eng.r.double() - ref["r"]).abs() / ref["r"].abs().clamp_min(1e-30)
+    assert rr.max().item() < 2e-3
+    if eng.KS > K:
+        assert eng.gamma[:, K:].abs().max().item() == 0
+    # suff-stats of that E-step (local statistics) against the fp64 scatter
+    cw_ref = R.suffstats(dc.doc_ptr, dc.word_idx, eng.e[:, :K].double(), eng.r.double(), eng.beta.double(), V, K)
+    cw = eng._cw_local[:, :K].double()
+    rel = ((cw - cw_ref).abs() / cw_ref.abs().clamp_min(1e-20)).max().item()
+    assert rel < 1e-4, rel
+    assert cw[V - 100:].abs().max().item() == 0                      # unused words: zero rows
+    assert int(nz.sum()) < D
