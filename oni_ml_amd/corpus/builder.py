@@ -46,10 +46,24 @@ def count_pairs(doc: torch.Tensor, word: torch.Tensor, weight: Optional[torch.Te
     if doc.numel() and (int(word.min()) < 0 or int(word.max()) >= (1 << _SHIFT)):
         raise ValueError("word keys must fit in 32 bits")
     pk = (doc.to(torch.int64) << _SHIFT) | word.to(torch.int64)
-    uniq, inv = torch.unique(pk, sorted=True, return_inverse=True)
-    w = torch.ones_like(pk) if weight is None else weight.to(device=pk.device, dtype=torch.int64)
-    cnt = torch.zeros(uniq.numel(), dtype=torch.int64, device=pk.device).index_add_(0, inv, w)
+    if weight is None:
+        uniq, cnt = torch.unique(pk, sorted=True, return_counts=True)
+        cnt = cnt.to(torch.int64)
+    else:
+        uniq, cnt = segment_sums(pk, weight.to(device=pk.device, dtype=torch.int64))
     return DocWordCounts(uniq >> _SHIFT, uniq & ((1 << _SHIFT) - 1), cnt)
+
+
+def segment_sums(keys: torch.Tensor, w: torch.Tensor):
+    """(sorted distinct keys, sum of w per key) by a radix sort and a prefix sum -- no atomics, so
+    heavily repeated keys (a handful of port words, hour-of-day values) cost nothing extra; an
+    int64 index_add_ over them serialises on a few contended addresses."""
+    sk, perm = torch.sort(keys)
+    uniq, counts = torch.unique_consecutive(sk, return_counts=True)
+    cw = torch.cumsum(w[perm], 0)
+    ends = torch.cumsum(counts, 0) - 1
+    tot = cw[ends]
+    return uniq, torch.diff(tot, prepend=tot.new_zeros(1))
 
 
 def concat(parts: Sequence[DocWordCounts], merge: bool = False) -> DocWordCounts:
@@ -64,11 +78,13 @@ def concat(parts: Sequence[DocWordCounts], merge: bool = False) -> DocWordCounts
 
 def _first_appearance_ids(keys: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
     """ids[i] = rank of keys[i]'s first appearance; returns (ids, distinct keys in rank order)."""
-    n = keys.numel()
-    uniq, inv = torch.unique(keys, sorted=True, return_inverse=True)
-    pos = torch.arange(n, device=keys.device, dtype=torch.int64)
-    first = torch.full((uniq.numel(),), n, dtype=torch.int64, device=keys.device)
-    first.scatter_reduce_(0, inv, pos, reduce="amin", include_self=True)
+    # stable sort: the first element of each run of equal keys is the key's first appearance
+    sk, perm = torch.sort(keys, stable=True)
+    uniq, counts = torch.unique_consecutive(sk, return_counts=True)
+    starts = torch.cumsum(counts, 0) - counts
+    first = perm[starts]
+    inv = torch.empty_like(perm)
+    inv[perm] = torch.repeat_interleave(torch.arange(uniq.numel(), device=keys.device), counts)
     order = torch.argsort(first)
     rank = torch.empty_like(order)
     rank[order] = torch.arange(order.numel(), device=keys.device)
@@ -91,9 +107,9 @@ def lda_pre(dwc: DocWordCounts) -> BuiltCorpus:
     order = torch.sort(did, stable=True).indices
     d_sorted = did[order]
     D = int(dkeys.numel())
-    lens = torch.bincount(d_sorted, minlength=D)
-    ptr = torch.zeros(D + 1, dtype=torch.int64, device=lens.device)
-    ptr[1:] = torch.cumsum(lens, 0)
+    # d_sorted is sorted: the CSR offsets are a binary search per document (a bincount would be
+    # an atomic histogram over the entries)
+    ptr = torch.searchsorted(d_sorted, torch.arange(D + 1, device=d_sorted.device, dtype=d_sorted.dtype))
     corpus = Corpus(
         doc_ptr=ptr.cpu().numpy(),
         word_idx=wid[order].to(torch.int32).cpu().numpy(),

@@ -34,9 +34,8 @@ def ecdf_cuts(values: torch.Tensor, quantiles: Sequence[float], weights: Optiona
         uniq, counts = torch.unique(v, sorted=True, return_counts=True)
         counts = counts.to(torch.int64)
     else:
-        w = weights.to(device=v.device, dtype=torch.int64).reshape(-1)
-        uniq, inv = torch.unique(v, sorted=True, return_inverse=True)
-        counts = torch.zeros(uniq.numel(), dtype=torch.int64, device=v.device).index_add_(0, inv, w)
+        from ..corpus.builder import segment_sums
+        uniq, counts = segment_sums(v, weights.to(device=v.device, dtype=torch.int64).reshape(-1))
     cum = torch.cumsum(counts, 0)
     F = cum.to(torch.float64) / cum[-1].to(torch.float64)
     # largest index with F < q  (F is non-decreasing)
