@@ -104,11 +104,11 @@ PYBIND11_MODULE(_onihip, m) {
     oni::launch_colsum_partials(P<const double>(part), nb, cols, P<double>(out), P<const double>(gate), S(stream));
   });
   m.def("lda_mstep_control", [](u cw, u class_total, u beta, int V, int K, int KS, u scalars, u params, u ctl,
-                                u hist, int hist_slots, u done_count, u stream) {
+                                u hist, int hist_slots, u done_count, u stream, u rows, int n_rows) {
     oni::EMControlArgs c{P<const double>(scalars), P<double>(params), P<double>(ctl), P<double>(hist), hist_slots,
                          P<int>(done_count)};
-    oni::launch_lda_mstep_control(P<const float>(cw), P<const double>(class_total), P<float>(beta), V, K, KS, c,
-                                  S(stream));
+    oni::launch_lda_mstep_control(P<const float>(cw), P<const double>(class_total), P<float>(beta), V, K, KS,
+                                  P<const int>(rows), n_rows, c, S(stream));
   });
   m.def("reduce_scratch_doubles", [](int cols) { return oni::reduce_scratch_doubles(cols); });
   m.def("colsum", [](u mat, int rows, int cols, u out, u scratch, u gate, u stream) {

@@ -155,7 +155,7 @@ struct EMControlArgs {
   int* done_count;
 };
 void launch_lda_mstep_control(const float* cw, const double* class_total, float* beta, int V, int K, int KS,
-                              const EMControlArgs& c, hipStream_t s);
+                              const int* rows, int n_rows, const EMControlArgs& c, hipStream_t s);
 
 // ------------------------------------------------------------- reductions ---
 // Deterministic two-pass reductions (reduce.hip).  scratch holds

@@ -394,18 +394,22 @@ __global__ __launch_bounds__(256) void lda_mstep_kernel(const float* __restrict_
   }
 }
 
+// rows != nullptr: only those word rows (a rank's own words under the sparse class_word
+// exchange -- the other rows of beta are never read on that rank).
 __global__ __launch_bounds__(256) void lda_mstep_control_kernel(const float* __restrict__ cw,
                                                                 const double* __restrict__ ct,
                                                                 float* __restrict__ beta, int V, int K, int KS,
+                                                                const int* __restrict__ rows, int n_rows,
                                                                 EMControlArgs c) {
   if (c.params[kParamDone] != 0.0) return;
   // float4 granules of the word-major [V][KS] matrices (KS % 4 == 0)
   const int q = KS / 4;
-  const int total4 = V * q;
+  const int total4 = (rows ? n_rows : V) * q;
   const float4* cw4 = reinterpret_cast<const float4*>(cw);
   float4* beta4 = reinterpret_cast<float4*>(beta);
-  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < total4; i += gridDim.x * blockDim.x) {
-    const int k0 = (i % q) * 4;
+  for (int g = blockIdx.x * blockDim.x + threadIdx.x; g < total4; g += gridDim.x * blockDim.x) {
+    const int k0 = (g % q) * 4;
+    const int i = rows ? rows[g / q] * q + g % q : g;
     const float4 v = cw4[i];
     float o[4];
     const float vv[4] = {v.x, v.y, v.z, v.w};
@@ -429,14 +433,14 @@ __global__ __launch_bounds__(256) void lda_mstep_control_kernel(const float* __r
 }
 
 void launch_lda_mstep_control(const float* cw, const double* class_total, float* beta, int V, int K, int KS,
-                              const EMControlArgs& c, hipStream_t s) {
-  const int64_t total = (int64_t)V * KS;
+                              const int* rows, int n_rows, const EMControlArgs& c, hipStream_t s) {
+  const int64_t total = (int64_t)(rows ? n_rows : V) * KS;
   // 2 workgroups per CU: the completion count is a same-address atomic per workgroup
   int64_t blocks = (total / 4 + 255) / 256;
   if (blocks > 512) blocks = 512;
   if (blocks < 1) blocks = 1;
   hipLaunchKernelGGL(lda_mstep_control_kernel, dim3((unsigned)blocks), dim3(256), 0, s, cw, class_total, beta, V,
-                     K, KS, c);
+                     K, KS, rows, n_rows, c);
   ONI_HIP_CHECK(hipGetLastError());
 }
 

@@ -241,8 +241,11 @@ class LDAEngine:
             os.environ.get("ONI_DIST_OVERLAP", "1") != "0"
         if self._overlap:
             from ...ops import hip as H
+            # only this rank's words: rows of other words stay zero in cw_local and are never read
+            # (the E-step touches only local words; the M-step is restricted to them below)
             shared = np.unique(self._xchg.send_idx.cpu().numpy())
-            private = np.setdiff1d(np.arange(self.V, dtype=np.int64), shared, assume_unique=True)
+            local = self._xchg.local_ids.cpu().numpy()
+            private = np.setdiff1d(local, shared, assume_unique=True)
             wide = _use_wide(self.KS)
             self._plan_a = H.SuffPlan(self.dc.word_len, self.device, wide=wide, words=shared)
             self._plan_b = H.SuffPlan(self.dc.word_len, self.device, wide=wide, words=private)
@@ -484,8 +487,9 @@ class LDAEngine:
 
     def _launch_beta_control(self):
         from ...ops import hip as H
+        rows = self._xchg.local_rows32 if self._xchg is not None else None
         H.lda_mstep_control(self.cw, self.class_total, self.beta, self.K, self._scalars, self._params, self._ctl,
-                            self._hist, self._done_count)
+                            self._hist, self._done_count, rows=rows)
 
     def _reduce_stats(self):
         """Cross-rank reduction of one EM iteration's statistics (outside the graphs): the packed
@@ -519,7 +523,7 @@ class LDAEngine:
                 local = self.cw
                 self._xchg.pack(local)
                 self._xchg.exchange()
-                self.cw = torch.empty_like(local)
+                self.cw = torch.zeros_like(local)     # rows of other ranks' words stay 0 (global_rows masks)
                 self._xchg.accumulate(self.cw, local)
                 work.wait()
                 host = red[:2].cpu().tolist()

@@ -325,17 +325,20 @@ def colsum_partials(part, n_blocks, out, gate=None):
                           _chk(out, torch.float64, "out", (cols,), dev), _gate_ptr(gate, dev), _stream())
 
 
-def lda_mstep_control(cw, class_total, beta, K, scalars, params, ctl, hist, done_count):
-    """M-step (beta = cw / class_total) + the device EM convergence step in the last workgroup."""
+def lda_mstep_control(cw, class_total, beta, K, scalars, params, ctl, hist, done_count, rows=None):
+    """M-step (beta = cw / class_total) + the device EM convergence step in the last workgroup.
+    ``rows``: int32 word ids, restrict the M-step to them (validated host-side once by the caller)."""
     V, KS = cw.shape
     dev = cw.device
     slots = hist.numel() // HIST_COLS
+    n_rows = 0 if rows is None else int(rows.numel())
+    rows_ptr = 0 if rows is None else _chk(rows, torch.int32, "rows", (n_rows,), dev)
     lib().lda_mstep_control(
         _chk(cw, torch.float32, "cw", (V, KS), dev), _chk(class_total, torch.float64, "class_total", (KS,), dev),
         _chk(beta, torch.float32, "beta", (V, KS), dev), int(V), int(K), int(KS),
         _chk(scalars, torch.float64, "scalars", (2,), dev), _chk(params, torch.float64, "params", (PARAM_COUNT,), dev),
         _chk(ctl, torch.float64, "ctl", (8,), dev), _chk(hist, torch.float64, "hist", (slots * HIST_COLS,), dev),
-        int(slots), _chk(done_count, torch.int32, "done_count", (1,), dev), _stream())
+        int(slots), _chk(done_count, torch.int32, "done_count", (1,), dev), _stream(), rows_ptr, n_rows)
 
 
 def alpha_newton(scalars, num_docs, K, estimate, params, alpha_out):

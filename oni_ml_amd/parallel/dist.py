@@ -196,6 +196,9 @@ class VocabExchange:
         self.owned = (owner == ctx.rank).to(self.device)
         self.send_idx = torch.cat(self.common).to(self.device)
         self.recv_idx = [c.to(self.device) for c in self.common]
+        # this rank's own words: the rows accumulate() writes and the M-step needs
+        self.local_ids = mine.to(self.device)
+        self.local_rows32 = self.local_ids.to(torch.int32)
         self.offsets = np.concatenate([[0], np.cumsum(self.splits)]).tolist()
         self.send = torch.zeros(max(self.rows, 1), self.width, dtype=dtype, device=self.device)
         self.recv = torch.zeros_like(self.send)
@@ -230,10 +233,13 @@ class VocabExchange:
                                     async_op=async_op)
 
     def accumulate(self, cw_out: torch.Tensor, cw_local: torch.Tensor):
-        cw_out.zero_()
+        """cw_out[w] = 0 + c_0[w] + c_1[w] + ... for this rank's words w (rank order); rows of other
+        words are not touched (never read on this rank).  Cost ~ local rows, not the union vocabulary."""
+        li = self.local_ids
+        cw_out.index_fill_(0, li, 0)
         for s_ in range(self.ctx.world_size):
             if s_ == self.ctx.rank:
-                cw_out.add_(cw_local)
+                cw_out.index_add_(0, li, cw_local.index_select(0, li))
             elif self.splits[s_]:
                 a, b = self.offsets[s_], self.offsets[s_ + 1]
                 cw_out.index_add_(0, self.recv_idx[s_], self.recv[a:b])
