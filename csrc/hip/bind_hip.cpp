@@ -47,13 +47,14 @@ PYBIND11_MODULE(_onihip, m) {
       "lda_estep",
       [](u doc_ptr, u word_idx, u counts, u order, int n_items, u beta, int K, int KS, float alpha,
          double lik_const, int var_max_iter, float var_conv, u gamma, u e_out, u r_out, u lik, u alpha_ss,
-         u iters, int variant, u params, u stream) {
+         u iters, int variant, u params, u stream, u dbg) {
         oni::EStepArgs a{P<const int>(doc_ptr), P<const int>(word_idx), P<const float>(counts),
                          P<const int>(order),   n_items,              P<const float>(beta),
                          K,                     alpha,                lik_const,
                          var_max_iter,          var_conv,             P<float>(gamma),
                          P<float>(e_out),       P<float>(r_out),      P<double>(lik),
-                         P<double>(alpha_ss),   P<int>(iters),        P<const double>(params)};
+                         P<double>(alpha_ss),   P<int>(iters),        P<const double>(params),
+                         P<long long>(dbg)};
         oni::launch_lda_estep(a, variant, KS, S(stream));
       });
 

@@ -38,6 +38,15 @@ __device__ __forceinline__ float dot_lds(const float* sE, const float (&row)[KS]
 
 constexpr float kPMin = 1e-30f;
 
+// lda-c's variational loop test  (L_old - L) / L_old > VAR_CONVERGED  with IEEE semantics
+// (L_old == 0 on the first iteration: +-inf or NaN), evaluated without the f64 division:
+// the sign of L_old decides the direction of the inequality.
+__device__ __forceinline__ bool var_more(double lik_old, double L, double c) {
+  if (lik_old < 0.0) return (lik_old - L) < c * lik_old;
+  if (lik_old > 0.0) return (lik_old - L) > c * lik_old;
+  return L < 0.0 && c < INFINITY;   // (0 - L) / 0 = +inf (L < 0), -inf or NaN otherwise
+}
+
 // r = c / P with v_rcp_f32 (1 ulp) instead of IEEE division: the correctly rounded
 // f32 divide is a ~10-instruction div_scale / fmas / fixup sequence, a large share
 // of the per-word work (P >= kPMin is a normal float, so rcp is exact to 1 ulp).

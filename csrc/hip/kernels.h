@@ -86,6 +86,9 @@ struct EStepArgs {
   // captured hipGraph of the E-step can be replayed every EM iteration while alpha
   // / VAR_MAX_ITER change, and params[kParamDone] != 0 skips the launch.
   const double* params = nullptr;
+  // Optional phase timer (diagnostics, scripts/bench_estep.py --phases): block 0, thread 0 of the
+  // block kernels accumulate clock64() cycles per phase of the variational loop into dbg[0..7].
+  long long* dbg = nullptr;
 };
 void launch_lda_estep(const EStepArgs& a, int variant, int KS, hipStream_t s);
 void launch_lda_estep_split(const EStepArgs& a, const SplitArgs& s, int KS, hipStream_t st);

@@ -95,12 +95,13 @@ __global__ __launch_bounds__(256) void lda_estep_group(EStepArgs a) {
     e[j] = 0.f;
   }
 
-  double lik_old = 0.0, L = 0.0, conv = 1.0, dsum_last = 0.0;
+  double lik_old = 0.0, L = 0.0, dsum_last = 0.0;
+  bool more = 1.0 > (double)a.var_conv;   // lda-c starts with converged = 1
   int it = 0;
   float m = 0.f;
   const bool unbounded = a.var_max_iter < 0;
 
-  while (conv > (double)a.var_conv && (unbounded || it < a.var_max_iter)) {
+  while (more && (unbounded || it < a.var_max_iter)) {
     ++it;
     // E_k = exp(psi_k - m)
     float mx = -INFINITY;
@@ -156,25 +157,27 @@ __global__ __launch_bounds__(256) void lda_estep_group(EStepArgs a) {
       gn[j] = (k < K) ? fmaf(e[j], ak, alpha) : 0.f;
       sg += gn[j];
     }
-    const float S = group_sum<G>(sg);
-    float dS, lgS;
-    digamma_lgamma(S, dS, lgS);
-    double term = 0.0;
+    // sum_k [lnG(g'_k) + (g'_k - a)(psi(S') - psi(g_k))]
+    //   = sum_k [lnG(g'_k) - (g'_k - a) psi(g_k)] + psi(S') (S' - K a): no wait for psi(S')
+    double part = 0.0;
 #pragma unroll
     for (int j = 0; j < TJ; ++j) {
       const int k = t + G * j;
       if (k < K) {
         float pn, lg;
         digamma_lgamma(gn[j], pn, lg);
-        // (a-1)Y + lnG(g') - (g'-1)Y + (g'-a)(psi(g') - psi(g)) with Y = psi(g') - psi(S')
-        term += (double)lg + (double)((gn[j] - alpha) * (dS - psi[j]));
+        part += (double)lg - (double)(gn[j] - alpha) * (double)psi[j];
         psi[j] = pn;
         gam[j] = gn[j];
       }
     }
-    term = group_sum<G>(term);
+    const float S = group_sum<G>(sg);
+    const double termp = group_sum<G>(part);
+    float dS, lgS;
+    digamma_lgamma(S, dS, lgS);
+    const double term = termp + (double)dS * ((double)S - (double)K * (double)alpha);
     L = a.lik_const - (double)lgS + term + (lsum_d + (double)m * total) - total * (double)dS;
-    conv = (lik_old - L) / lik_old;
+    more = var_more(lik_old, L, (double)a.var_conv);
     lik_old = L;
     dsum_last = dS;
   }
@@ -280,7 +283,7 @@ __global__ __launch_bounds__(NW * 64) void lda_estep_block(EStepArgs a) {
   // wave 0 owns topic state
   float gam[TJ], psi[TJ], e[TJ];
   const float g0 = alpha + (float)(total / K);
-  double lik_old = 0.0, L = 0.0, conv = 1.0, dsum_last = 0.0;
+  double lik_old = 0.0, L = 0.0, dsum_last = 0.0;
   float m = 0.f;
   int it = 0;
   const bool unbounded = a.var_max_iter < 0;
@@ -311,7 +314,10 @@ __global__ __launch_bounds__(NW * 64) void lda_estep_block(EStepArgs a) {
   }
   __syncthreads();
 
+  const bool timed = a.dbg != nullptr && blockIdx.x == 0 && t == 0;
+  long long tm[4] = {0, 0, 0, 0}, t0 = 0, t1 = 0;
   while (sFlag) {
+    if (timed) t0 = clock64();
     // ---- word pass (all waves) ----
     float acc[KS];
 #pragma unroll
@@ -337,6 +343,7 @@ __global__ __launch_bounds__(NW * 64) void lda_estep_block(EStepArgs a) {
 #pragma unroll
       for (int k = 0; k < KS; ++k) acc[k] = fmaf(r, row[k], acc[k]);
     }
+    if (timed) { t1 = clock64(); tm[0] += t1 - t0; t0 = t1; }
     group_sum_vec<64, KS>(acc);
     const double lsum_w = group_sum<64>((double)lsum);
     if (lane == 0) {
@@ -344,7 +351,9 @@ __global__ __launch_bounds__(NW * 64) void lda_estep_block(EStepArgs a) {
       for (int k = 0; k < KS; ++k) sRed[wv][k] = acc[k];
       sRedD[wv][1] = lsum_w;
     }
+    if (timed) { t1 = clock64(); tm[1] += t1 - t0; t0 = t1; }
     __syncthreads();
+    if (timed) { t1 = clock64(); tm[2] += t1 - t0; t0 = t1; }
 
     // ---- topic phase (wave 0) ----
     if (wv == 0) {
@@ -365,33 +374,39 @@ __global__ __launch_bounds__(NW * 64) void lda_estep_block(EStepArgs a) {
         gn[j] = (k < K) ? fmaf(e[j], ak, alpha) : 0.f;
         sg += gn[j];
       }
-      const float S = group_sum<64>(sg);
-      float dS, lgS;
-      digamma_lgamma(S, dS, lgS);
-      double term = 0.0;
+      // The topic-dependent part of the likelihood does not need psi(S'):
+      //   sum_k [lnG(g'_k) + (g'_k - a)(psi(S') - psi(g_k))]
+      //     = sum_k [lnG(g'_k) - (g'_k - a) psi(g_k)] + psi(S') (S' - K a)
+      // so its reduction runs beside the S' reduction and psi(S') (shorter serial chain).  With
+      // KS <= 32 every topic lives in the low half-wave: 32-lane reductions (no v_readlane step).
+      constexpr int GR = KS <= 32 ? 32 : 64;
+      double part = 0.0;
 #pragma unroll
       for (int j = 0; j < TJ; ++j) {
         const int k = lane + 64 * j;
         if (k < K) {
           float pn, lg;
           digamma_lgamma(gn[j], pn, lg);
-          // (a-1)Y + lnG(g') - (g'-1)Y + (g'-a)(psi(g') - psi(g)) with Y = psi(g') - psi(S')
-          term += (double)lg + (double)((gn[j] - alpha) * (dS - psi[j]));
+          part += (double)lg - (double)(gn[j] - alpha) * (double)psi[j];
           psi[j] = pn;
           gam[j] = gn[j];
         }
       }
-      term = group_sum<64>(term);
+      const float S = group_sum<GR>(sg);
+      const double termp = group_sum<GR>(part);
+      float dS, lgS;
+      digamma_lgamma(S, dS, lgS);
+      const double term = termp + (double)dS * ((double)S - (double)K * (double)alpha);
       L = a.lik_const - (double)lgS + term + (lsum_d + (double)m * total) - total * (double)dS;
-      conv = (lik_old - L) / lik_old;
+      const bool more = var_more(lik_old, L, (double)a.var_conv);
       lik_old = L;
       dsum_last = dS;
-      const bool cont = conv > (double)a.var_conv && (unbounded || it < a.var_max_iter);
+      const bool cont = more && (unbounded || it < a.var_max_iter);
       if (cont) {  // next E (keeps sE = E of the final phi when stopping)
         float mx = -INFINITY;
 #pragma unroll
         for (int j = 0; j < TJ; ++j) mx = fmaxf(mx, psi[j]);
-        m = group_max<64>(mx);
+        m = group_max<GR>(mx);
 #pragma unroll
         for (int j = 0; j < TJ; ++j) {
           const int k = lane + 64 * j;
@@ -401,7 +416,15 @@ __global__ __launch_bounds__(NW * 64) void lda_estep_block(EStepArgs a) {
       }
       if (lane == 0) sFlag = cont ? 1 : 0;
     }
+    if (timed) { t1 = clock64(); tm[3] += t1 - t0; t0 = t1; }
     __syncthreads();
+  }
+  if (timed) {
+    // [0] word pass  [1] cross-lane / LDS reductions  [2] barrier wait  [3] topic phase (wave 0)
+    // [4] variational iterations  [5] words
+    for (int i = 0; i < 4; ++i) a.dbg[i] = tm[i];
+    a.dbg[4] = it;
+    a.dbg[5] = N;
   }
 
   // ---- outputs ----
@@ -480,7 +503,8 @@ __global__ __launch_bounds__(256) void lda_estep_thread(EStepArgs a) {
     gam[k] = k < K ? g0 : 0.f;
     psi[k] = k < K ? p0 : -INFINITY;
   }
-  double lik_old = 0.0, L = 0.0, conv = 1.0, dsum_last = 0.0;
+  double lik_old = 0.0, L = 0.0, dsum_last = 0.0;
+  bool more = 1.0 > (double)a.var_conv;   // lda-c starts with converged = 1
   float m = p0;
   int it = 0;
   const bool unbounded = a.var_max_iter < 0;
@@ -499,7 +523,7 @@ __global__ __launch_bounds__(256) void lda_estep_thread(EStepArgs a) {
     for (int k = 0; k < KS; ++k) sg += gam[k];
     dsum_last = digammaf_ldac(sg);
   }
-  while (conv > (double)a.var_conv && (unbounded || it < a.var_max_iter)) {
+  while (more && (unbounded || it < a.var_max_iter)) {
     ++it;
     float acc[KS];
 #pragma unroll
@@ -543,23 +567,24 @@ __global__ __launch_bounds__(256) void lda_estep_thread(EStepArgs a) {
     }
     float dS, lgS;
     digamma_lgamma(S, dS, lgS);
-    double term = 0.0;
+    // sum_k [lnG(g'_k) - (g'_k - a) psi(g_k)] + psi(S') (S' - K a): independent of psi(S')
+    double part = 0.0;
 #pragma unroll
     for (int k = 0; k < KS; ++k) {
       if (k < K) {
         float pn, lg;
         digamma_lgamma(gn[k], pn, lg);
-        // (a-1)Y + lnG(g') - (g'-1)Y + (g'-a)(psi(g') - psi(g)) with Y = psi(g') - psi(S')
-        term += (double)lg + (double)((gn[k] - alpha) * (dS - psi[k]));
+        part += (double)lg - (double)(gn[k] - alpha) * (double)psi[k];
         psi[k] = pn;
         gam[k] = gn[k];
       }
     }
+    const double term = part + (double)dS * ((double)S - (double)K * (double)alpha);
     L = a.lik_const - (double)lgS + term + ((double)lsum + (double)m * total) - total * (double)dS;
-    conv = (lik_old - L) / lik_old;
+    more = var_more(lik_old, L, (double)a.var_conv);
     lik_old = L;
     dsum_last = dS;
-    const bool cont = conv > (double)a.var_conv && (unbounded || it < a.var_max_iter);
+    const bool cont = more && (unbounded || it < a.var_max_iter);
     if (cont) compute_e();
   }
   // outputs (E of the final phi; r_n was written by the last word pass)

@@ -97,7 +97,7 @@ __global__ __launch_bounds__(kNT) void lda_estep_split(EStepArgs a, SplitArgs s)
 
   float gam[TJ], psi[TJ], e[TJ];
   const float g0 = alpha + (float)(total / K);
-  double lik_old = 0.0, L = 0.0, conv = 1.0, dsum_last = 0.0;
+  double lik_old = 0.0, L = 0.0, dsum_last = 0.0;
   float m = 0.f;
   int it = 0;
   const bool unbounded = a.var_max_iter < 0;
@@ -189,33 +189,36 @@ __global__ __launch_bounds__(kNT) void lda_estep_split(EStepArgs a, SplitArgs s)
       lsum_d = __shfl(lsum_d, 0);
       ok = __all(ok);
       if (!ok && lane == 0) __hip_atomic_store(s.error, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const float S = group_sum<64>(sg);
-      float dS, lgS;
-      digamma_lgamma(S, dS, lgS);
-      double term = 0.0;
+      // sum_k [lnG(g'_k) - (g'_k - a) psi(g_k)] + psi(S') (S' - K a): independent of psi(S');
+      // KS <= 32: every topic in the low half-wave, 32-lane reductions
+      constexpr int GL = KS <= 32 ? 32 : 64;
+      double partl = 0.0;
 #pragma unroll
       for (int j = 0; j < TJ; ++j) {
         const int k = lane + 64 * j;
         if (k < K) {
           float pn, lg;
           digamma_lgamma(gn[j], pn, lg);
-          // (a-1)Y + lnG(g') - (g'-1)Y + (g'-a)(psi(g') - psi(g)) with Y = psi(g') - psi(S')
-          term += (double)lg + (double)((gn[j] - alpha) * (dS - psi[j]));
+          partl += (double)lg - (double)(gn[j] - alpha) * (double)psi[j];
           psi[j] = pn;
           gam[j] = gn[j];
         }
       }
-      term = group_sum<64>(term);
+      const float S = group_sum<GL>(sg);
+      const double termp = group_sum<GL>(partl);
+      float dS, lgS;
+      digamma_lgamma(S, dS, lgS);
+      const double term = termp + (double)dS * ((double)S - (double)K * (double)alpha);
       L = a.lik_const - (double)lgS + term + (lsum_d + (double)m * total) - total * (double)dS;
-      conv = (lik_old - L) / lik_old;
+      const bool more = var_more(lik_old, L, (double)a.var_conv);
       lik_old = L;
       dsum_last = dS;
-      const bool cont = ok && conv > (double)a.var_conv && (unbounded || it < a.var_max_iter);
+      const bool cont = ok && more && (unbounded || it < a.var_max_iter);
       if (cont) {
         float mx = -INFINITY;
 #pragma unroll
         for (int j = 0; j < TJ; ++j) mx = fmaxf(mx, psi[j]);
-        m = group_max<64>(mx);
+        m = group_max<GL>(mx);
 #pragma unroll
         for (int j = 0; j < TJ; ++j) {
           const int k = lane + 64 * j;

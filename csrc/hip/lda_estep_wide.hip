@@ -284,23 +284,25 @@ __device__ __forceinline__ double topics_update(Topics<KS, GT>& T, const float (
     gn[j] = (k < K) ? fmaf(T.e[j], acc[j], alpha) : 0.f;
     sg += gn[j];
   }
-  const float S = group_sum<GT>(sg);
-  float dS, lgS;
-  digamma_lgamma(S, dS, lgS);
-  double term = 0.0;
+  // sum_k [lnG(g'_k) + (g'_k - a)(psi(S') - psi(g_k))]
+  //   = sum_k [lnG(g'_k) - (g'_k - a) psi(g_k)] + psi(S') (S' - K a): no wait for psi(S')
+  double part = 0.0;
 #pragma unroll
   for (int j = 0; j < TJ; ++j) {
     const int k = lane + GT * j;
     if (k < K) {
       float pn, lg;
       digamma_lgamma(gn[j], pn, lg);
-      // (a-1)Y + lnG(g') - (g'-1)Y + (g'-a)(psi(g') - psi(g)) with Y = psi(g') - psi(S')
-      term += (double)lg + (double)((gn[j] - alpha) * (dS - T.psi[j]));
+      part += (double)lg - (double)(gn[j] - alpha) * (double)T.psi[j];
       T.psi[j] = pn;
       T.gam[j] = gn[j];
     }
   }
-  term = group_sum<GT>(term);
+  const float S = group_sum<GT>(sg);
+  const double termp = group_sum<GT>(part);
+  float dS, lgS;
+  digamma_lgamma(S, dS, lgS);
+  const double term = termp + (double)dS * ((double)S - (double)K * (double)alpha);
   dsum = dS;
   return lik_const - (double)lgS + term + (lsum + (double)m * total) - total * (double)dS;
 }
@@ -367,10 +369,11 @@ __global__ __launch_bounds__(256) void lda_estep_wgroup(EStepArgs a) {
   float4 e4[W::CPL];
   load_e<KS, TG>(sE, q, e4);
 
-  double lik_old = 0.0, L = 0.0, conv = 1.0;
+  double lik_old = 0.0, L = 0.0;
+  bool more = 1.0 > (double)a.var_conv;   // lda-c starts with converged = 1
   int it = 0;
   const bool unbounded = a.var_max_iter < 0;
-  while (conv > (double)a.var_conv && (unbounded || it < a.var_max_iter)) {
+  while (more && (unbounded || it < a.var_max_iter)) {
     ++it;
     float4 acc4[W::CPL];
     float lsum = 0.f;
@@ -390,9 +393,9 @@ __global__ __launch_bounds__(256) void lda_estep_wgroup(EStepArgs a) {
       acc[j] = v;
     }
     L = topics_update<KS, G>(T, acc, t, K, alpha, a.lik_const, lsum_d, m, total, dsum);
-    conv = (lik_old - L) / lik_old;
+    more = var_more(lik_old, L, (double)a.var_conv);
     lik_old = L;
-    if (conv > (double)a.var_conv && (unbounded || it < a.var_max_iter)) {
+    if (more && (unbounded || it < a.var_max_iter)) {
       m = topics_e<KS, G>(T, t, K, sE);
       wave_lds_sync();
       load_e<KS, TG>(sE, q, e4);
@@ -445,7 +448,7 @@ __global__ __launch_bounds__(NW * 64) void lda_estep_wblock(EStepArgs a) {
   __syncthreads();
 
   TP T;
-  double lik_old = 0.0, L = 0.0, conv = 1.0, dsum = 0.0;
+  double lik_old = 0.0, L = 0.0, dsum = 0.0;
   float m = 0.f;
   int it = 0;
   const bool unbounded = a.var_max_iter < 0;
@@ -495,9 +498,9 @@ __global__ __launch_bounds__(NW * 64) void lda_estep_wblock(EStepArgs a) {
         acc[j] = v;
       }
       L = topics_update<KS, 64>(T, acc, lane, K, alpha, a.lik_const, lsum_d, m, total, dsum);
-      conv = (lik_old - L) / lik_old;
+      const bool more = var_more(lik_old, L, (double)a.var_conv);
       lik_old = L;
-      const bool cont = conv > (double)a.var_conv && (unbounded || it < a.var_max_iter);
+      const bool cont = more && (unbounded || it < a.var_max_iter);
       if (cont) m = topics_e<KS, 64>(T, lane, K, sE);
       if (lane == 0) sFlag = cont ? 1 : 0;
     }
@@ -566,7 +569,7 @@ __global__ __launch_bounds__(kWNT) void lda_estep_wsplit(EStepArgs a, SplitArgs 
   __syncthreads();
 
   TP T;
-  double lik_old = 0.0, L = 0.0, conv = 1.0, dsum = 0.0;
+  double lik_old = 0.0, L = 0.0, dsum = 0.0;
   float m = 0.f;
   int it = 0;
   const bool unbounded = a.var_max_iter < 0;
@@ -635,9 +638,9 @@ __global__ __launch_bounds__(kWNT) void lda_estep_wsplit(EStepArgs a, SplitArgs 
       ok = __all(ok);
       if (!ok && lane == 0) __hip_atomic_store(sp.error, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       L = topics_update<KS, 64>(T, acc, lane, K, alpha, a.lik_const, lsum_d, m, total, dsum);
-      conv = (lik_old - L) / lik_old;
+      const bool more = var_more(lik_old, L, (double)a.var_conv);
       lik_old = L;
-      const bool cont = ok && conv > (double)a.var_conv && (unbounded || it < a.var_max_iter);
+      const bool cont = ok && more && (unbounded || it < a.var_max_iter);
       if (cont) m = topics_e<KS, 64>(T, lane, K, sE);
       if (lane == 0) sFlag = cont ? 1 : 0;
     }

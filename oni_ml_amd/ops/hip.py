@@ -89,7 +89,7 @@ def _chk(t: torch.Tensor, dtype, name, shape=None, device=None):
 
 
 def lda_estep(doc_ptr, word_idx, counts, order, beta, K, alpha, lik_const, var_max_iter, var_conv,
-              gamma, e_out, r_out, lik, alpha_ss, iters, variant, params=None):
+              gamma, e_out, r_out, lik, alpha_ss, iters, variant, params=None, dbg=None):
     """`params`: optional device f64[4] {alpha, lik_const, var_max_iter, var_conv} overriding the scalars
     (graph-replayed E-steps)."""
     D = doc_ptr.numel() - 1
@@ -115,6 +115,7 @@ def lda_estep(doc_ptr, word_idx, counts, order, beta, K, alpha, lik_const, var_m
         _chk(alpha_ss, torch.float64, "alpha_ss", (D,), dev),
         _chk(iters, torch.int32, "iters", (D,), dev),
         int(variant), _params_ptr(params, dev), _stream(),
+        0 if dbg is None else _chk(dbg, torch.int64, "dbg", (8,), dev),
     ]
     if order.numel() == 0:
         return
