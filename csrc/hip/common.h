@@ -173,6 +173,47 @@ __device__ __forceinline__ T group_max(T x) {
   return group_reduce<G>(x, [](T a, T b) { return a > b ? a : b; });
 }
 
+// Sum over the 64 lanes of a wave delivered to lane 63 only, all in DPP (no
+// ds_swizzle, no v_readlane): the four row steps of group_reduce, then
+// row_bcast:15 (rows 1, 3 add the last lane of rows 0, 2) and row_bcast:31
+// (rows 2, 3 add lane 31).  For reductions whose result one lane stores: the
+// ds_swizzle + readlane tail of group_reduce costs LDS-pipe round trips and
+// readlane hazards per value (~2,000 cycles per variational iteration for the
+// KS accumulators of the 4/8-wave document kernels, scripts/estep_phases.py).
+namespace detail {
+constexpr int kRowBcast15 = 0x142;
+constexpr int kRowBcast31 = 0x143;
+template <int CTRL, int ROWS>
+__device__ __forceinline__ float bcast(float x) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), CTRL, ROWS, 0xF, false));
+}
+template <int CTRL, int ROWS>
+__device__ __forceinline__ double bcast(double x) {
+  const long long b = __double_as_longlong(x);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)(b & 0xffffffffLL), CTRL, ROWS, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), CTRL, ROWS, 0xF, false);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+}  // namespace detail
+
+template <typename T>
+__device__ __forceinline__ T wave_sum_last(T x) {
+  using namespace detail;
+  x += xchg<kQuadXor1>(x);
+  x += xchg<kQuadXor2>(x);
+  x += xchg<kRowHalfMirror>(x);
+  x += xchg<kRowMirror>(x);
+  x += bcast<kRowBcast15, 0xA>(x);
+  x += bcast<kRowBcast31, 0xC>(x);
+  return x;   // lane 63: the total
+}
+
+template <int N>
+__device__ __forceinline__ void wave_sum_last_vec(float (&v)[N]) {
+#pragma unroll
+  for (int i = 0; i < N; ++i) v[i] = wave_sum_last(v[i]);
+}
+
 // Wave-level LDS hand-off between lanes of ONE wavefront: orders the
 // ds_writes before the ds_reads (same wave, so no s_barrier is needed and
 // divergent groups never deadlock).

@@ -49,6 +49,7 @@ __global__ __launch_bounds__(256) void lda_estep_group(EStepArgs a) {
   constexpr int GPB = 256 / G;
   constexpr int TJ = (KS + G - 1) / G;
   __shared__ float4 sE4[GPB][KS / 4];
+  __shared__ float sAcc[G == 64 ? GPB : 1][G == 64 ? KS : 1];   // one-wave documents: lane 63 -> topic lanes
 
   const int t = threadIdx.x % G;
   const int g = threadIdx.x / G;
@@ -142,8 +143,21 @@ __global__ __launch_bounds__(256) void lda_estep_group(EStepArgs a) {
 #pragma unroll
       for (int k = 0; k < KS; ++k) acc[k] = fmaf(r, row[k], acc[k]);
     }
-    group_sum_vec<G, KS>(acc);
-    const double lsum_d = group_sum<G>((double)lsum);
+    double lsum_d;
+    if constexpr (G == 64) {
+      // one document per wave: DPP sums into lane 63 (no swizzle / readlane per value), handed to
+      // the topic lanes through LDS
+      wave_sum_last_vec<KS>(acc);
+      lsum_d = __shfl(wave_sum_last((double)lsum), 63);
+      if (t == 63) {
+#pragma unroll
+        for (int k = 0; k < KS; ++k) sAcc[g][k] = acc[k];
+      }
+      wave_lds_sync();
+    } else {
+      group_sum_vec<G, KS>(acc);
+      lsum_d = group_sum<G>((double)lsum);
+    }
 
     // ---- topic phase: gamma update + likelihood ----
     float gn[TJ];
@@ -152,8 +166,12 @@ __global__ __launch_bounds__(256) void lda_estep_group(EStepArgs a) {
     for (int j = 0; j < TJ; ++j) {
       const int k = t + G * j;
       float ak = 0.f;
+      if constexpr (G == 64) {
+        if (k < KS) ak = sAcc[g][k];
+      } else {
 #pragma unroll
-      for (int i = 0; i < KS; ++i) ak = (i == k) ? acc[i] : ak;
+        for (int i = 0; i < KS; ++i) ak = (i == k) ? acc[i] : ak;
+      }
       gn[j] = (k < K) ? fmaf(e[j], ak, alpha) : 0.f;
       sg += gn[j];
     }
@@ -344,9 +362,9 @@ __global__ __launch_bounds__(NW * 64) void lda_estep_block(EStepArgs a) {
       for (int k = 0; k < KS; ++k) acc[k] = fmaf(r, row[k], acc[k]);
     }
     if (timed) { t1 = clock64(); tm[0] += t1 - t0; t0 = t1; }
-    group_sum_vec<64, KS>(acc);
-    const double lsum_w = group_sum<64>((double)lsum);
-    if (lane == 0) {
+    wave_sum_last_vec<KS>(acc);   // totals in lane 63
+    const double lsum_w = wave_sum_last((double)lsum);
+    if (lane == 63) {
 #pragma unroll
       for (int k = 0; k < KS; ++k) sRed[wv][k] = acc[k];
       sRedD[wv][1] = lsum_w;

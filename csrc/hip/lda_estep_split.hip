@@ -142,9 +142,9 @@ __global__ __launch_bounds__(kNT) void lda_estep_split(EStepArgs a, SplitArgs s)
         for (int k = 0; k < KS; ++k) acc[k] = fmaf(r, bc[c][k], acc[k]);
       }
     }
-    group_sum_vec<64, KS>(acc);
-    const double lsum_w = group_sum<64>((double)lsum);
-    if (lane == 0) {
+    wave_sum_last_vec<KS>(acc);   // totals in lane 63
+    const double lsum_w = wave_sum_last((double)lsum);
+    if (lane == 63) {
 #pragma unroll
       for (int k = 0; k < KS; ++k) sRed[wv][k] = acc[k];
       sRedD[wv] = lsum_w;
