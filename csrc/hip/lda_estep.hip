@@ -102,9 +102,7 @@ __global__ __launch_bounds__(256) void lda_estep_group(EStepArgs a) {
   float m = 0.f;
   const bool unbounded = a.var_max_iter < 0;
 
-  while (more && (unbounded || it < a.var_max_iter)) {
-    ++it;
-    // E_k = exp(psi_k - m)
+  {  // E_k = exp(psi_k - m) of the initial gamma; later E's come from the previous topic phase
     float mx = -INFINITY;
 #pragma unroll
     for (int j = 0; j < TJ; ++j) mx = fmaxf(mx, psi[j]);
@@ -115,7 +113,10 @@ __global__ __launch_bounds__(256) void lda_estep_group(EStepArgs a) {
       e[j] = (k < K) ? __expf(psi[j] - m) : 0.f;
       if (k < KS) sE[k] = e[j];
     }
-    wave_lds_sync();
+  }
+  while (more && (unbounded || it < a.var_max_iter)) {
+    ++it;
+    wave_lds_sync();   // sE of this iteration
 
     // ---- word pass ----
     float acc[KS];
@@ -189,8 +190,15 @@ __global__ __launch_bounds__(256) void lda_estep_group(EStepArgs a) {
         gam[j] = gn[j];
       }
     }
+    float mx = -INFINITY;
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) mx = fmaxf(mx, psi[j]);
     const float S = group_sum<G>(sg);
     const double termp = group_sum<G>(part);
+    const float m_new = group_max<G>(mx);   // next E beside the likelihood chain
+    float e_new[TJ];
+#pragma unroll
+    for (int j = 0; j < TJ; ++j) e_new[j] = (t + G * j < K) ? __expf(psi[j] - m_new) : 0.f;
     float dS, lgS;
     digamma_lgamma(S, dS, lgS);
     const double term = termp + (double)dS * ((double)S - (double)K * (double)alpha);
@@ -198,6 +206,15 @@ __global__ __launch_bounds__(256) void lda_estep_group(EStepArgs a) {
     more = var_more(lik_old, L, (double)a.var_conv);
     lik_old = L;
     dsum_last = dS;
+    if (more && (unbounded || it < a.var_max_iter)) {   // commit (E of the final phi stays otherwise)
+      m = m_new;
+#pragma unroll
+      for (int j = 0; j < TJ; ++j) {
+        const int k = t + G * j;
+        e[j] = e_new[j];
+        if (k < KS) sE[k] = e[j];
+      }
+    }
   }
 
   if (it == 0) {  // var_max_iter == 0: phi from the initial gamma
@@ -410,8 +427,17 @@ __global__ __launch_bounds__(NW * 64) void lda_estep_block(EStepArgs a) {
           gam[j] = gn[j];
         }
       }
+      // the next E (max + exp of the new psi) is computed beside the likelihood chain and committed
+      // only if the loop continues (E of the final phi stays otherwise)
+      float mx = -INFINITY;
+#pragma unroll
+      for (int j = 0; j < TJ; ++j) mx = fmaxf(mx, psi[j]);
       const float S = group_sum<GR>(sg);
       const double termp = group_sum<GR>(part);
+      const float m_new = group_max<GR>(mx);
+      float e_new[TJ];
+#pragma unroll
+      for (int j = 0; j < TJ; ++j) e_new[j] = (lane + 64 * j < K) ? __expf(psi[j] - m_new) : 0.f;
       float dS, lgS;
       digamma_lgamma(S, dS, lgS);
       const double term = termp + (double)dS * ((double)S - (double)K * (double)alpha);
@@ -421,14 +447,11 @@ __global__ __launch_bounds__(NW * 64) void lda_estep_block(EStepArgs a) {
       dsum_last = dS;
       const bool cont = more && (unbounded || it < a.var_max_iter);
       if (cont) {  // next E (keeps sE = E of the final phi when stopping)
-        float mx = -INFINITY;
-#pragma unroll
-        for (int j = 0; j < TJ; ++j) mx = fmaxf(mx, psi[j]);
-        m = group_max<GR>(mx);
+        m = m_new;
 #pragma unroll
         for (int j = 0; j < TJ; ++j) {
           const int k = lane + 64 * j;
-          e[j] = (k < K) ? __expf(psi[j] - m) : 0.f;
+          e[j] = e_new[j];
           if (k < KS) sE[k] = e[j];
         }
       }

@@ -204,8 +204,15 @@ __global__ __launch_bounds__(kNT) void lda_estep_split(EStepArgs a, SplitArgs s)
           gam[j] = gn[j];
         }
       }
+      float mx = -INFINITY;
+#pragma unroll
+      for (int j = 0; j < TJ; ++j) mx = fmaxf(mx, psi[j]);
       const float S = group_sum<GL>(sg);
       const double termp = group_sum<GL>(partl);
+      const float m_new = group_max<GL>(mx);   // next E beside the likelihood chain
+      float e_new[TJ];
+#pragma unroll
+      for (int j = 0; j < TJ; ++j) e_new[j] = (lane + 64 * j < K) ? __expf(psi[j] - m_new) : 0.f;
       float dS, lgS;
       digamma_lgamma(S, dS, lgS);
       const double term = termp + (double)dS * ((double)S - (double)K * (double)alpha);
@@ -215,14 +222,11 @@ __global__ __launch_bounds__(kNT) void lda_estep_split(EStepArgs a, SplitArgs s)
       dsum_last = dS;
       const bool cont = ok && more && (unbounded || it < a.var_max_iter);
       if (cont) {
-        float mx = -INFINITY;
-#pragma unroll
-        for (int j = 0; j < TJ; ++j) mx = fmaxf(mx, psi[j]);
-        m = group_max<GL>(mx);
+        m = m_new;
 #pragma unroll
         for (int j = 0; j < TJ; ++j) {
           const int k = lane + 64 * j;
-          e[j] = (k < K) ? __expf(psi[j] - m) : 0.f;
+          e[j] = e_new[j];
           if (k < KS) sE[k] = e[j];
         }
       }
