@@ -92,10 +92,11 @@ __device__ __forceinline__ void put_tagged(unsigned long long* p, float v, unsig
   __hip_atomic_store(p, g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// sum_{q < n} value(x[q * stride]) in order q = 0, 1, ..., each granule awaited until it
-// carries `tag`; 8 loads in flight per round trip.  Returns false on a timeout.
-__device__ __forceinline__ bool tagged_sum(const unsigned long long* x, int n, int stride, unsigned tag, float& out) {
-  float s = 0.f;
+// sum_{q < n} value(x[q * stride]) in order q = 0, 1, ..., in double, each granule
+// awaited until it carries `tag`; 8 loads in flight per round trip.  Returns false
+// on a timeout.
+__device__ __forceinline__ bool tagged_sum(const unsigned long long* x, int n, int stride, unsigned tag, double& out) {
+  double s = 0.0;
   long spins = 0;
   for (int q0 = 0; q0 < n; q0 += 8) {
     unsigned long long v[8];
@@ -107,39 +108,40 @@ __device__ __forceinline__ bool tagged_sum(const unsigned long long* x, int n, i
       if (q0 + u >= n) continue;
       while ((unsigned)(v[u] >> 32) != tag) {
         if (++spins > kSplitSpinLimit) {
-          out = __builtin_nanf("");
+          out = __builtin_nan("");
           return false;
         }
         __builtin_amdgcn_s_sleep(1);
         v[u] = __hip_atomic_load(x + (size_t)(q0 + u) * stride, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
-      s += __uint_as_float((unsigned)(v[u] & 0xffffffffu));
+      s += (double)__uint_as_float((unsigned)(v[u] & 0xffffffffu));
     }
   }
   out = s;
   return true;
 }
 
-// The same for the (hi, lo) float pairs of a double: sum_q ((double)hi_q + (double)lo_q).
-__device__ __forceinline__ bool tagged_sum2(const unsigned long long* x, int n, int stride, unsigned tag, double& out) {
-  double s = 0.0;
-  long spins = 0;
-  for (int q = 0; q < n; ++q) {
-    unsigned long long h, l;
-    do {
-      h = __hip_atomic_load(x + (size_t)q * stride, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      l = __hip_atomic_load(x + (size_t)q * stride + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if ((unsigned)(h >> 32) == tag && (unsigned)(l >> 32) == tag) break;
-      if (++spins > kSplitSpinLimit) {
-        out = __builtin_nan("");
-        return false;
-      }
-      __builtin_amdgcn_s_sleep(1);
-    } while (true);
-    s += (double)__uint_as_float((unsigned)(h & 0xffffffffu)) + (double)__uint_as_float((unsigned)(l & 0xffffffffu));
+// Gather every segment's row (KS topic granules + the log-sum hi/lo pair) in segment
+// order: lane-column k < KS + 2 of the calling wave sums its column over the n
+// segments, all columns in flight together (one round-trip chain, not one per
+// segment for the log-sum).  acc[j] = topic lane + 64 j (0 past KS), lsum = the
+// document's log-sum; the same bits in every workgroup of the document.
+template <int KS, int TJ>
+__device__ __forceinline__ bool tagged_gather(const unsigned long long* x, int n, int stride, unsigned tag, int lane,
+                                              float (&acc)[TJ], double& lsum) {
+  constexpr int TX = (KS + 2 + 63) / 64;
+  double v[TX];
+  bool ok = true;
+#pragma unroll
+  for (int j = 0; j < TX; ++j) {
+    const int k = lane + 64 * j;
+    v[j] = 0.0;
+    if (k < KS + 2) ok &= tagged_sum(x + k, n, stride, tag, v[j]);
   }
-  out = s;
-  return true;
+#pragma unroll
+  for (int j = 0; j < TJ; ++j) acc[j] = (lane + 64 * j < KS) ? (float)v[j] : 0.f;
+  lsum = __shfl(v[KS / 64], KS % 64) + __shfl(v[(KS + 1) / 64], (KS + 1) % 64);
+  return ok;
 }
 
 // Publish one segment's iteration partials: lanes 0..63 of the calling wave write the

@@ -173,20 +173,16 @@ __global__ __launch_bounds__(kNT) void lda_estep_split(EStepArgs a, SplitArgs s)
       for (int w = 0; w < kNW; ++w) lpart += sRedD[w];
       unsigned long long* xb = s.xchg + (size_t)par * s.n_blocks * GR;
       publish_tagged<KS>(xb + (size_t)b * GR, [&](int j) { return part[j]; }, lpart, lane, tag);
-      bool ok = true;
-      double lsum_d = 0.0;
+      float ak[TJ];
+      double lsum_d;
+      bool ok = tagged_gather<KS>(xb + (size_t)base * GR, nseg, GR, tag, lane, ak, lsum_d);
       float gn[TJ];
       float sg = 0.f;
 #pragma unroll
       for (int j = 0; j < TJ; ++j) {
-        const int k = lane + 64 * j;
-        float ak = 0.f;
-        if (k < KS) ok &= tagged_sum(xb + (size_t)base * GR + k, nseg, GR, tag, ak);
-        gn[j] = (k < K) ? fmaf(e[j], ak, alpha) : 0.f;
+        gn[j] = (lane + 64 * j < K) ? fmaf(e[j], ak[j], alpha) : 0.f;
         sg += gn[j];
       }
-      if (lane == 0) ok &= tagged_sum2(xb + (size_t)base * GR + KS, nseg, GR, tag, lsum_d);
-      lsum_d = __shfl(lsum_d, 0);
       ok = __all(ok);
       if (!ok && lane == 0) __hip_atomic_store(s.error, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       // sum_k [lnG(g'_k) - (g'_k - a) psi(g_k)] + psi(S') (S' - K a): independent of psi(S');

@@ -624,17 +624,9 @@ __global__ __launch_bounds__(kWNT) void lda_estep_wsplit(EStepArgs a, SplitArgs 
       unsigned long long* xb = sp.xchg + (size_t)par * sp.n_blocks * GR;
       publish_tagged<KS>(xb + (size_t)b * GR, [&](int j) { return part[j]; }, lpart, lane, tag);
       // every segment's partials in segment order: identical bits in every workgroup
-      bool ok = true;
       float acc[TP::TJ];
-#pragma unroll
-      for (int j = 0; j < TP::TJ; ++j) {
-        const int k = lane + 64 * j;
-        acc[j] = 0.f;
-        if (k < KS) ok &= tagged_sum(xb + (size_t)base * GR + k, nseg, GR, tag, acc[j]);
-      }
-      double lsum_d = 0.0;
-      if (lane == 0) ok &= tagged_sum2(xb + (size_t)base * GR + KS, nseg, GR, tag, lsum_d);
-      lsum_d = __shfl(lsum_d, 0);
+      double lsum_d;
+      bool ok = tagged_gather<KS>(xb + (size_t)base * GR, nseg, GR, tag, lane, acc, lsum_d);
       ok = __all(ok);
       if (!ok && lane == 0) __hip_atomic_store(sp.error, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       L = topics_update<KS, 64>(T, acc, lane, K, alpha, a.lik_const, lsum_d, m, total, dsum);
