@@ -67,13 +67,15 @@ PYBIND11_MODULE(_onihip, m) {
       "lda_estep_split",
       [](bool wide, u doc_ptr, u word_idx, u counts, u beta, int K, int KS, float alpha, double lik_const, int var_max_iter,
          float var_conv, u gamma, u e_out, u r_out, u lik, u alpha_ss, u iters, u seg_doc, u seg_index, u seg_count,
-         u seg_base, u doc_slot, int n_blocks, int seg_words, u xchg, u counter, int n_docs, u error, u params, u stream) {
+         u seg_base, u doc_slot, int n_blocks, int seg_words, u xchg, u counter, int n_docs, u error, u params, u stream,
+         u dbg) {
         oni::EStepArgs a{P<const int>(doc_ptr), P<const int>(word_idx), P<const float>(counts),
                          nullptr,               n_blocks,             P<const float>(beta),
                          K,                     alpha,                lik_const,
                          var_max_iter,          var_conv,             P<float>(gamma),
                          P<float>(e_out),       P<float>(r_out),      P<double>(lik),
-                         P<double>(alpha_ss),   P<int>(iters),        P<const double>(params)};
+                         P<double>(alpha_ss),   P<int>(iters),        P<const double>(params),
+                         P<long long>(dbg)};
         oni::SplitArgs s{P<const int>(seg_doc), P<const int>(seg_index), P<const int>(seg_count),
                          P<const int>(seg_base), P<const int>(doc_slot), n_blocks, seg_words,
                          P<unsigned long long>(xchg), P<int>(counter), n_docs, P<int>(error)};

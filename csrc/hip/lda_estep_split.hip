@@ -126,6 +126,18 @@ __global__ __launch_bounds__(kNT) void lda_estep_split(EStepArgs a, SplitArgs s)
   }
   __syncthreads();
 
+  // optional phase timer (scripts/estep_phases.py): thread 0 of workgroup 0
+  const bool timed = a.dbg != nullptr && b == 0 && t == 0;
+  long long tm[6] = {0, 0, 0, 0, 0, 0}, t0 = 0;
+  auto lap = [&](int i) {
+    if (timed) {
+      const long long t1 = clock64();
+      tm[i] += t1 - t0;
+      t0 = t1;
+    }
+  };
+  if (timed) t0 = clock64();
+
   while (sFlag) {
     // ---- word pass over this segment ----
     float acc[KS];
@@ -142,6 +154,7 @@ __global__ __launch_bounds__(kNT) void lda_estep_split(EStepArgs a, SplitArgs s)
         for (int k = 0; k < KS; ++k) acc[k] = fmaf(r, bc[c][k], acc[k]);
       }
     }
+    lap(0);
     wave_sum_last_vec<KS>(acc);   // totals in lane 63
     const double lsum_w = wave_sum_last((double)lsum);
     if (lane == 63) {
@@ -150,6 +163,7 @@ __global__ __launch_bounds__(kNT) void lda_estep_split(EStepArgs a, SplitArgs s)
       sRedD[wv] = lsum_w;
     }
     __syncthreads();
+    lap(1);
 
     if (wv == 0) {
       ++it;
@@ -173,9 +187,11 @@ __global__ __launch_bounds__(kNT) void lda_estep_split(EStepArgs a, SplitArgs s)
       for (int w = 0; w < kNW; ++w) lpart += sRedD[w];
       unsigned long long* xb = s.xchg + (size_t)par * s.n_blocks * GR;
       publish_tagged<KS>(xb + (size_t)b * GR, [&](int j) { return part[j]; }, lpart, lane, tag);
+      lap(2);
       float ak[TJ];
       double lsum_d;
       bool ok = tagged_gather<KS>(xb + (size_t)base * GR, nseg, GR, tag, lane, ak, lsum_d);
+      lap(3);
       float gn[TJ];
       float sg = 0.f;
 #pragma unroll
@@ -227,8 +243,16 @@ __global__ __launch_bounds__(kNT) void lda_estep_split(EStepArgs a, SplitArgs s)
         }
       }
       if (lane == 0) sFlag = cont ? 1 : 0;
+      lap(4);
     }
     __syncthreads();
+    lap(5);
+  }
+  if (timed) {
+#pragma unroll
+    for (int i = 0; i < 6; ++i) a.dbg[i] = tm[i];
+    a.dbg[6] = it;
+    a.dbg[7] = nseg;
   }
 
   // Every wave of this workgroup has passed its last exchange (the loop ends on a __syncthreads).

@@ -747,7 +747,20 @@ class LDAEngine:
         tiny_work = [("bucket", (v, o)) for v, o in plan if v in tiny_vars]
         b8_work = [w for w in long_work if w[1][0] in (H.ESTEP_B8, H.ESTEP_WB8)]
         b4_work = [w for w in long_work if w[1][0] not in (H.ESTEP_B8, H.ESTEP_WB8)]
-        if nstreams >= 4:
+        spec = os.environ.get("ONI_ESTEP_SCHED")
+        if spec and nstreams >= 4:
+            # experiment hook: "split+B4|B8|G64C+G64+G32|T1" = side streams 1..3 | main
+            names = {"split": None, "B8": (H.ESTEP_B8, H.ESTEP_WB8), "B4": (H.ESTEP_B4, H.ESTEP_WB4),
+                     "G64C": (H.ESTEP_G64C,), "G64": (H.ESTEP_G64, H.ESTEP_W64), "G32": (H.ESTEP_G32, H.ESTEP_W32),
+                     "T1": tiny_vars}
+            lanes = spec.split("|")
+            for si, lane in zip([1, 2, 3, 0], lanes):
+                for tok in lane.split("+"):
+                    if tok == "split":
+                        sched[si] += split_work
+                    else:
+                        sched[si] += [("bucket", (v, o)) for v, o in plan if v in names[tok]]
+        elif nstreams >= 4:
             # B4 queues behind the split batches: B8 alone is about as long as split + B4 (measured
             # against moving B4 behind B8 and the short-document buckets behind split: 3-7 % slower)
             sched[1], sched[2], sched[3], sched[0] = split_work + b4_work, b8_work, mid_work, tiny_work

@@ -208,7 +208,9 @@ class SplitPlan:
 
 
 def lda_estep_split(doc_ptr, word_idx, counts, beta, K, alpha, lik_const, var_max_iter, var_conv, gamma, e_out, r_out,
-                    lik, alpha_ss, iters, batch, seg_words, params=None, wide=False):
+                    lik, alpha_ss, iters, batch, seg_words, params=None, wide=False, dbg=None):
+    """dbg: optional int64[8] phase timer of workgroup 0 (narrow kernel): cycles in word pass, reductions,
+    publish, gather wait, topic phase, loop barrier; iterations; segments of its document."""
     D = doc_ptr.numel() - 1
     nnz = word_idx.numel()
     V, KS = beta.shape
@@ -230,7 +232,7 @@ def lda_estep_split(doc_ptr, word_idx, counts, beta, K, alpha, lik_const, var_ma
         _chk(batch["xchg"], torch.int64, "xchg", (2 * nb * (KS + 2),), dev),
         _chk(batch["counter"], torch.int32, "counter", (2 * batch["docs"],), dev), int(batch["docs"]),
         _chk(batch["error"], torch.int32, "error", (1,), dev),
-        _params_ptr(params, dev), _stream())
+        _params_ptr(params, dev), _stream(), 0 if dbg is None else _chk(dbg, torch.int64, "dbg", (8,), dev))
 
 
 PARAM_COUNT = 8      # device parameter block (csrc/hip/kernels.h kParamCount)

@@ -1,7 +1,8 @@
 #!/usr/bin/env python
-"""Phase timing of the block E-step kernels (B4 / B8) on the 1-day netflow corpus: thread 0 of
-block 0 (the bucket's longest document) accumulates clock64() cycles per phase of the variational
-loop -- word pass, cross-lane/LDS reductions, barrier wait, topic phase (wave 0).
+"""Phase timing of the block E-step kernels (B4 / B8) and the split-document kernel on the 1-day
+netflow corpus: thread 0 of block 0 (the bucket's longest document) accumulates clock64() cycles
+per phase of the variational loop -- word pass, cross-lane/LDS reductions, barrier wait, topic
+phase (wave 0); split: word pass, reductions, publish, gather wait, topic phase, loop barrier.
 
   python scripts/estep_phases.py [--topics K]
 """
@@ -33,6 +34,20 @@ def main():
     torch.cuda.synchronize()
     dc = eng.dc
     lc = special.lik_const(eng.alpha, eng.K)
+    sp = eng.doc_buckets.split
+    if sp is not None and not sp.wide:
+        for bi, batch in enumerate(sp.batches):
+            dbg = torch.zeros(8, dtype=torch.int64, device="cuda")
+            H.lda_estep_split(dc.doc_ptr, dc.word_idx, dc.counts, eng.beta, eng.K, eng.alpha, lc, eng.var_max_iter,
+                              eng.settings.var_converged, eng.gamma, eng.e, eng.r, eng.lik, eng.ass, eng.iters, batch,
+                              sp.seg_words, dbg=dbg)
+            torch.cuda.synchronize()
+            d = dbg.cpu().tolist()
+            it = max(d[6], 1)
+            ph = ("word_pass", "reductions", "publish", "gather_wait", "topic_phase", "loop_barrier")
+            print(json.dumps(dict(bucket=f"split[{bi}]", segments=d[7], blocks=int(batch["n_blocks"]), iterations=d[6],
+                                  cycles_per_iteration={n: d[i] // it for i, n in enumerate(ph)},
+                                  total_cycles=sum(d[:6]))), flush=True)
     names = {H.ESTEP_B4: "B4", H.ESTEP_B8: "B8"}
     for var, order in eng.doc_buckets.plan:
         if var not in names:
