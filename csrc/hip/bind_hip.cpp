@@ -103,6 +103,10 @@ PYBIND11_MODULE(_onihip, m) {
                     P<const double>(gate)};
     oni::launch_lda_suffstats_fused(a, n_heavy, n_medium, n_light, P<double>(part), KS, wide, S(stream));
   });
+  m.def("rows_accumulate", [](u rows, u ptr, u src, u own, u recv, u out, int n_rows, int width, u stream) {
+    oni::launch_rows_accumulate(P<const int>(rows), P<const int>(ptr), P<const int>(src), P<const float>(own),
+                                P<const float>(recv), P<float>(out), n_rows, width, S(stream));
+  });
   m.def("colsum_partials", [](u part, int nb, int cols, u out, u gate, u stream) {
     oni::launch_colsum_partials(P<const double>(part), nb, cols, P<double>(out), P<const double>(gate), S(stream));
   });

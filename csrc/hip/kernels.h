@@ -171,6 +171,10 @@ void launch_sum2(const double* a, const double* b, int n, double* out, double* s
                  hipStream_t s);
 // out[k] = sum_b part[b][k] (b in order), the second pass of the fused suff-stats.
 void launch_colsum_partials(const double* part, int nb, int cols, double* out, const double* gate, hipStream_t s);
+// Sparse class_word exchange: out[rows[i]] = 0 + src_0 + src_1 + ... over row i's sources
+// (CSR ptr/src; src >= 0: recv row, src < 0: the rank's own row own[rows[i]]), float4 granules.
+void launch_rows_accumulate(const int* rows, const int* ptr, const int* src, const float* own, const float* recv,
+                            float* out, int n_rows, int width, hipStream_t s);
 
 // ---------------------------------------------------------------- scoring ---
 struct ScoreArgs {

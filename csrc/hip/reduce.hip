@@ -149,6 +149,42 @@ void launch_colsum_partials(const double* part, int nb, int cols, double* out, c
   ONI_HIP_CHECK(hipGetLastError());
 }
 
+// Sparse class_word exchange (parallel/dist.py VocabExchange.accumulate): one launch
+// for the whole rank-order sum instead of a fill + one index_add per peer.  The
+// fp32 adds run in source order (own row at the rank's own position), so every
+// rank holding a word computes bitwise the same row.
+__global__ __launch_bounds__(kRT) void rows_accumulate_kernel(const int* __restrict__ rows, const int* __restrict__ ptr,
+                                                              const int* __restrict__ src,
+                                                              const float4* __restrict__ own,
+                                                              const float4* __restrict__ recv,
+                                                              float4* __restrict__ out, int n_rows, int q) {
+  const long g = (long)blockIdx.x * kRT + threadIdx.x;
+  if (g >= (long)n_rows * q) return;
+  const int i = (int)(g / q), c = (int)(g % q);
+  const size_t dst = (size_t)rows[i] * q + c;
+  float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int j = ptr[i]; j < ptr[i + 1]; ++j) {
+    const int from = src[j];
+    const float4 v = from < 0 ? own[dst] : recv[(size_t)from * q + c];
+    s.x += v.x;
+    s.y += v.y;
+    s.z += v.z;
+    s.w += v.w;
+  }
+  out[dst] = s;
+}
+
+void launch_rows_accumulate(const int* rows, const int* ptr, const int* src, const float* own, const float* recv,
+                            float* out, int n_rows, int width, hipStream_t s) {
+  if (width % 4 != 0) throw std::runtime_error("rows_accumulate: width must be a multiple of 4");
+  const long n = (long)n_rows * (width / 4);
+  if (n <= 0) return;
+  hipLaunchKernelGGL(rows_accumulate_kernel, dim3((unsigned)((n + kRT - 1) / kRT)), dim3(kRT), 0, s, rows, ptr, src,
+                     reinterpret_cast<const float4*>(own), reinterpret_cast<const float4*>(recv),
+                     reinterpret_cast<float4*>(out), n_rows, width / 4);
+  ONI_HIP_CHECK(hipGetLastError());
+}
+
 int reduce_scratch_doubles(int cols) { return kRB * (cols > 2 ? cols : 2); }
 
 void launch_colsum(const float* m, int rows, int cols, double* out, double* scratch, const double* gate,

@@ -318,6 +318,21 @@ def lda_suffstats_fused(word_ptr, csc_ent, csc_doc, plan: "SuffPlan", e, r, beta
         bool(plan.wide))
 
 
+def rows_accumulate(rows, ptr, src, own, recv, out):
+    """out[rows[i]] = 0 + sum over j in [ptr[i], ptr[i+1]) of (own[rows[i]] if src[j] < 0 else recv[src[j]]),
+    fp32, in j order (parallel/dist.py VocabExchange.accumulate)."""
+    dev = out.device
+    V, W = out.shape
+    n = rows.numel()
+    if n == 0:
+        return
+    # ptr / src are built and bounds-checked once on the host (VocabExchange.__init__)
+    lib().rows_accumulate(_chk(rows, torch.int32, "rows", (n,), dev), _chk(ptr, torch.int32, "ptr", (n + 1,), dev),
+                          _chk(src, torch.int32, "src", None, dev), _chk(own, torch.float32, "own", (V, W), dev),
+                          _chk(recv, torch.float32, "recv", None, dev), _chk(out, torch.float32, "out", (V, W), dev),
+                          int(n), int(W), _stream())
+
+
 def colsum_partials(part, n_blocks, out, gate=None):
     """out[k] = sum_b part[b, k] for b < n_blocks (deterministic order)."""
     dev = part.device

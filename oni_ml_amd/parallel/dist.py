@@ -200,6 +200,32 @@ class VocabExchange:
         self.local_ids = mine.to(self.device)
         self.local_rows32 = self.local_ids.to(torch.int32)
         self.offsets = np.concatenate([[0], np.cumsum(self.splits)]).tolist()
+        # accumulate() plan, CSR over this rank's words: each row's sources in rank order
+        # (src >= 0: a received row, -1: the rank's own row)
+        n_loc = int(mine.numel())
+        if n_loc > 1 and not bool((mine[1:] > mine[:-1]).all()):
+            raise ValueError("VocabExchange: local word list must be sorted and unique")
+        r_rows, r_key, r_src = [], [], []
+        for s_ in range(ctx.world_size):
+            if s_ == ctx.rank:
+                rr = torch.arange(n_loc, dtype=torch.int64)
+                ss = torch.full((n_loc,), -1, dtype=torch.int64)
+            else:
+                rr = torch.searchsorted(mine, self.common[s_])
+                ss = int(self.offsets[s_]) + torch.arange(self.splits[s_], dtype=torch.int64)
+            r_rows.append(rr)
+            r_key.append(rr * ctx.world_size + s_)
+            r_src.append(ss)
+        key = torch.cat(r_key)
+        order = torch.argsort(key, stable=True)
+        rows_sorted = torch.cat(r_rows)[order]
+        src = torch.cat(r_src)[order]
+        ptr = torch.zeros(n_loc + 1, dtype=torch.int64)
+        ptr[1:] = torch.cumsum(torch.bincount(rows_sorted, minlength=n_loc), 0)
+        if src.numel() and int(src.max()) >= max(self.rows, 1):
+            raise RuntimeError("VocabExchange: accumulate plan out of range")
+        self.acc_ptr = ptr.to(torch.int32).to(self.device)
+        self.acc_src = src.to(torch.int32).to(self.device)
         self.send = torch.zeros(max(self.rows, 1), self.width, dtype=dtype, device=self.device)
         self.recv = torch.zeros_like(self.send)
         self.local_words = int(mine.numel())
@@ -235,6 +261,10 @@ class VocabExchange:
     def accumulate(self, cw_out: torch.Tensor, cw_local: torch.Tensor):
         """cw_out[w] = 0 + c_0[w] + c_1[w] + ... for this rank's words w (rank order); rows of other
         words are not touched (never read on this rank).  Cost ~ local rows, not the union vocabulary."""
+        if cw_out.is_cuda and cw_out.dtype == torch.float32 and self.width % 4 == 0:
+            from ..ops import hip as H
+            H.rows_accumulate(self.local_rows32, self.acc_ptr, self.acc_src, cw_local, self.recv, cw_out)
+            return
         li = self.local_ids
         cw_out.index_fill_(0, li, 0)
         for s_ in range(self.ctx.world_size):

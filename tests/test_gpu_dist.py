@@ -47,3 +47,50 @@ def test_two_rank_hip_exchanges_match_single_rank():
         assert o["gamma_shape"] == one["gamma_shape"]
         assert abs(o["gamma_sum"] - one["gamma_sum"]) / one["gamma_sum"] < 1e-5
         assert abs(o["beta_checksum"] - one["beta_checksum"]) / abs(one["beta_checksum"]) < 1e-5
+
+
+def test_rows_accumulate_kernel_matches_rank_order_sum():
+    """HIP rows_accumulate (VocabExchange.accumulate's one-launch form) == fill + index_add per
+    source in rank order, bit for bit (fp32 adds in the same order)."""
+    import torch
+    from oni_ml_amd.ops import hip as H
+    g = torch.Generator().manual_seed(3)
+    V, W, world, me = 5000, 20, 4, 2
+    mine = torch.unique(torch.randint(0, V, (1800,), generator=g))
+    own = torch.rand(V, W, generator=g)
+    commons, recv_parts = [], []
+    for s in range(world):
+        if s == me:
+            commons.append(torch.zeros(0, dtype=torch.int64))
+            continue
+        c = mine[torch.rand(mine.numel(), generator=g) < 0.4]
+        commons.append(c)
+        recv_parts.append(torch.rand(c.numel(), W, generator=g))
+    recv = torch.cat(recv_parts)
+    offsets = np.concatenate([[0], np.cumsum([c.numel() for c in commons])]).tolist()
+    # reference: fill + index_add in rank order
+    ref = torch.full((V, W), 7.0)
+    ref.index_fill_(0, mine, 0)
+    for s in range(world):
+        if s == me:
+            ref.index_add_(0, mine, own.index_select(0, mine))
+        elif commons[s].numel():
+            ref.index_add_(0, commons[s], recv[offsets[s]:offsets[s + 1]])
+    # CSR plan as VocabExchange builds it
+    rows, keys, srcs = [], [], []
+    for s in range(world):
+        if s == me:
+            rr, ss = torch.arange(mine.numel()), torch.full((mine.numel(),), -1)
+        else:
+            rr, ss = torch.searchsorted(mine, commons[s]), offsets[s] + torch.arange(commons[s].numel())
+        rows.append(rr), keys.append(rr * world + s), srcs.append(ss)
+    order = torch.argsort(torch.cat(keys), stable=True)
+    rs, src = torch.cat(rows)[order], torch.cat(srcs)[order]
+    ptr = torch.zeros(mine.numel() + 1, dtype=torch.int64)
+    ptr[1:] = torch.cumsum(torch.bincount(rs, minlength=mine.numel()), 0)
+    d = torch.device("cuda")
+    out = torch.full((V, W), 7.0, device=d)
+    H.rows_accumulate(mine.to(d, torch.int32), ptr.to(d, torch.int32), src.to(d, torch.int32), own.to(d),
+                      recv.to(d), out)
+    torch.cuda.synchronize()
+    assert torch.equal(out.cpu(), ref)
