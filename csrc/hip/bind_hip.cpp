@@ -96,12 +96,14 @@ PYBIND11_MODULE(_onihip, m) {
 
   m.def("suff_fused_blocks", [](int h, int m_, int l) { return oni::suff_fused_blocks(h, m_, l); });
   m.def("lda_suffstats_fused", [](u word_ptr, u csc_ent, u csc_doc, u order, int n_heavy, int n_medium, int n_light,
-                                  u e, u r, u beta, u cw, u part, int KS, u gate, u stream, bool wide) {
+                                  u e, u r, u beta, u cw, u part, int KS, u gate, u stream, bool wide, int pstride,
+                                  u lik, u ass, int lo, int hi) {
     oni::SuffArgs a{P<const int>(word_ptr), P<const int>(csc_ent),  P<const int>(csc_doc),
                     P<const int>(order),    n_heavy + n_medium + n_light, P<const float>(e),
                     P<const float>(r),      P<const float>(beta),   P<float>(cw),
                     P<const double>(gate)};
-    oni::launch_lda_suffstats_fused(a, n_heavy, n_medium, n_light, P<double>(part), KS, wide, S(stream));
+    const oni::SuffPartLayout lay{pstride, pstride == KS ? 0 : 2, P<const double>(lik), P<const double>(ass), lo, hi};
+    oni::launch_lda_suffstats_fused(a, n_heavy, n_medium, n_light, P<double>(part), KS, wide, lay, S(stream));
   });
   m.def("rows_accumulate", [](u rows, u ptr, u src, u own, u recv, u out, int n_rows, int width, u stream) {
     oni::launch_rows_accumulate(P<const int>(rows), P<const int>(ptr), P<const int>(src), P<const float>(own),
@@ -111,11 +113,14 @@ PYBIND11_MODULE(_onihip, m) {
     oni::launch_colsum_partials(P<const double>(part), nb, cols, P<double>(out), P<const double>(gate), S(stream));
   });
   m.def("lda_mstep_control", [](u cw, u class_total, u beta, int V, int K, int KS, u scalars, u params, u ctl,
-                                u hist, int hist_slots, u done_count, u stream, u rows, int n_rows) {
+                                u hist, int hist_slots, u done_count, u stream, u rows, int n_rows, int newton,
+                                int estimate, double num_docs, u alpha_out) {
     oni::EMControlArgs c{P<const double>(scalars), P<double>(params), P<double>(ctl), P<double>(hist), hist_slots,
                          P<int>(done_count)};
+    const oni::NewtonArgs nw{newton, estimate, num_docs, P<double>(alpha_out)};
+    if (newton && !alpha_out) throw std::runtime_error("lda_mstep_control: alpha_out required with newton");
     oni::launch_lda_mstep_control(P<const float>(cw), P<const double>(class_total), P<float>(beta), V, K, KS,
-                                  P<const int>(rows), n_rows, c, S(stream));
+                                  P<const int>(rows), n_rows, c, nw, S(stream));
   });
   m.def("reduce_scratch_doubles", [](int cols) { return oni::reduce_scratch_doubles(cols); });
   m.def("colsum", [](u mat, int rows, int cols, u out, u scratch, u gate, u stream) {

@@ -7,7 +7,8 @@
 namespace oni {
 
 __device__ inline void em_control_step(const double* __restrict__ scalars, double* __restrict__ params,
-                                double* __restrict__ ctl, double* __restrict__ hist, int hist_slots) {
+                                double* __restrict__ ctl, double* __restrict__ hist, int hist_slots,
+                                double alpha_now) {
   const double lik = scalars[0];
   const double L_old = ctl[0];
   // IEEE division reproduces the host's L_old == 0 conventions (+-inf / nan)
@@ -21,7 +22,7 @@ __device__ inline void em_control_step(const double* __restrict__ scalars, doubl
     double* h = hist + (size_t)kHistCols * slot;
     h[0] = lik;
     h[1] = conv;
-    h[2] = params[0];   // alpha after this iteration's Newton
+    h[2] = alpha_now;   // alpha after this iteration's Newton
     h[3] = params[2];
     h[4] = scalars[1];
   }

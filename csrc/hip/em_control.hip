@@ -21,7 +21,7 @@ namespace oni {
 __global__ void em_control_kernel(const double* __restrict__ scalars, double* __restrict__ params,
                                   double* __restrict__ ctl, double* __restrict__ hist, int hist_slots) {
   if (threadIdx.x != 0 || blockIdx.x != 0 || params[kParamDone] != 0.0) return;
-  em_control_step(scalars, params, ctl, hist, hist_slots);
+  em_control_step(scalars, params, ctl, hist, hist_slots, params[0]);
 }
 
 void launch_em_control(const double* scalars, double* params, double* ctl, double* hist, int hist_slots,

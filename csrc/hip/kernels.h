@@ -119,8 +119,19 @@ void launch_lda_suffstats(const SuffArgs& a, int variant, int KS, hipStream_t s)
 // part receives suff_fused_blocks(...) x KS per-workgroup column sums (double).
 int suff_fused_blocks(int n_heavy, int n_medium, int n_light);
 // wide: the wide-topic layout (KS >= 32; lda_suff_wide), used with the wide E-step.
+// Partial-row layout of the fused suff-stats launch: row stride `stride` doubles, topic
+// column sums at [off, off + KS); with off == 2 columns 0 / 1 receive this workgroup's
+// slice sums of lik[] / alpha_ss[] over documents [lo, hi) (zeros when lik == nullptr), so
+// one colsum_partials pass yields {likelihood, alpha_ss, class_total[KS]}.
+struct SuffPartLayout {
+  int stride;
+  int off;
+  const double* lik;
+  const double* ass;
+  int lo, hi;
+};
 void launch_lda_suffstats_fused(const SuffArgs& a, int n_heavy, int n_medium, int n_light, double* part, int KS,
-                                bool wide, hipStream_t s);
+                                bool wide, const SuffPartLayout& lay, hipStream_t s);
 
 // ----------------------------------------------------------------- M-step ---
 // beta[w][k] = cw/ct_k if cw > 0 else exp(-100) (k < K); 0 for padding topics.
@@ -157,8 +168,17 @@ struct EMControlArgs {
   int hist_slots;
   int* done_count;
 };
+// alpha Newton fused into the M-step: workgroup 0 runs it (lanes 0-1) beside the beta
+// rows of the other workgroups; the control step (last workgroup) reads its alpha.
+struct NewtonArgs {
+  int enabled;            // 0: params[0..1] are left as they are
+  int estimate;           // lda-c "alpha estimate" (else only the lgamma constant is refreshed)
+  double num_docs;
+  double* alpha_out;      // [1]
+};
 void launch_lda_mstep_control(const float* cw, const double* class_total, float* beta, int V, int K, int KS,
-                              const int* rows, int n_rows, const EMControlArgs& c, hipStream_t s);
+                              const int* rows, int n_rows, const EMControlArgs& c, const NewtonArgs& nw,
+                              hipStream_t s);
 
 // ------------------------------------------------------------- reductions ---
 // Deterministic two-pass reductions (reduce.hip).  scratch holds

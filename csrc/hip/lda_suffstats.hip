@@ -128,12 +128,38 @@ __global__ __launch_bounds__(NW * 64) void lda_suff_block(SuffArgs a) {
 // (in double, fixed group order) to part[blockIdx.x][0..KS), so the per-topic
 // totals need only a small second pass over the partials (colsum_partials)
 // instead of a re-read of the whole [V][KS] matrix.
+// Columns 0 / 1 of this workgroup's partial row (layout off == 2): its slice of the
+// per-document likelihood and alpha_ss sums (wave 0; fixed order, so colsum_partials
+// gives bitwise the same totals every run).  Called by every thread before any barrier.
+__device__ __forceinline__ void scalar_slice(const SuffPartLayout& L, double* row) {
+  if (L.off != 2 || threadIdx.x >= 64) return;
+  const int t = threadIdx.x;
+  double x = 0.0, y = 0.0;
+  if (L.lik) {
+    const int n = L.hi - L.lo, nb = (int)gridDim.x;
+    const int per = (n + nb - 1) / nb;
+    const int i0 = L.lo + (int)blockIdx.x * per, i1 = min(L.hi, i0 + per);
+    for (int i = i0 + t; i < i1; i += 64) {
+      x += L.lik[i];
+      y += L.ass[i];
+    }
+  }
+  x = group_sum<64>(x);
+  y = group_sum<64>(y);
+  if (t == 0) {
+    row[0] = x;
+    row[1] = y;
+  }
+}
+
 template <int KS>
 __global__ __launch_bounds__(256) void lda_suff_fused(SuffArgs a, int n_heavy, int n_medium, int n_light,
-                                                      double* __restrict__ part) {
+                                                      double* __restrict__ part, SuffPartLayout lay) {
   __shared__ float sRow[16][KS];
   if (gated(a.gate)) return;
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  scalar_slice(lay, part + (size_t)blockIdx.x * lay.stride);
+  part += lay.off;
   const int nbM = (n_medium + 3) / 4;
   const int b = blockIdx.x;
   float acc[KS];
@@ -155,7 +181,7 @@ __global__ __launch_bounds__(256) void lda_suff_fused(SuffArgs a, int n_heavy, i
       for (int v = 0; v < 4; ++v) s += sRow[v][t];
       const float c = a.beta[(size_t)w * KS + t] * s;
       a.cw[(size_t)w * KS + t] = c;
-      part[(size_t)b * KS + t] = (double)c;
+      part[(size_t)b * lay.stride + t] = (double)c;
     }
     return;
   } else if (b < n_heavy + nbM) {
@@ -190,7 +216,7 @@ __global__ __launch_bounds__(256) void lda_suff_fused(SuffArgs a, int n_heavy, i
   if (t < KS) {
     double s = 0.0;
     for (int g = 0; g < ngroups; ++g) s += (double)sRow[g][t];
-    part[(size_t)b * KS + t] = s;
+    part[(size_t)b * lay.stride + t] = s;
   }
 }
 
@@ -204,7 +230,7 @@ __global__ __launch_bounds__(256) void lda_suff_fused(SuffArgs a, int n_heavy, i
 // scaled by beta and written with the per-workgroup column sums.
 template <int KS, int TG>
 __global__ __launch_bounds__(256) void lda_suff_wide(SuffArgs a, int n_heavy, int n_medium, int n_light,
-                                                     double* __restrict__ part) {
+                                                     double* __restrict__ part, SuffPartLayout lay) {
   constexpr int C = KS / 4;
   constexpr int CPL = (C + TG - 1) / TG;
   constexpr int NSLOT = 256 / TG;
@@ -212,6 +238,8 @@ __global__ __launch_bounds__(256) void lda_suff_wide(SuffArgs a, int n_heavy, in
   __shared__ float4 sAcc4[NSLOT][C];
   __shared__ float sRow[16][KS];
   if (gated(a.gate)) return;
+  scalar_slice(lay, part + (size_t)blockIdx.x * lay.stride);
+  part += lay.off;
   const int t = threadIdx.x;
   const int b = blockIdx.x;
   const int nbM = (n_medium + 3) / 4;
@@ -299,7 +327,7 @@ __global__ __launch_bounds__(256) void lda_suff_wide(SuffArgs a, int n_heavy, in
   if (t < KS) {
     double sum = 0.0;
     for (int g = 0; g < ngroups; ++g) sum += (double)sRow[g][t];
-    part[(size_t)b * KS + t] = sum;
+    part[(size_t)b * lay.stride + t] = sum;
   }
 }
 
@@ -309,29 +337,31 @@ int suff_fused_blocks(int n_heavy, int n_medium, int n_light) {
 
 template <int KS>
 static void suff_fused_ks(const SuffArgs& a, int n_heavy, int n_medium, int n_light, double* part, bool wide,
-                          hipStream_t s) {
+                          const SuffPartLayout& lay, hipStream_t s) {
   const int nb = suff_fused_blocks(n_heavy, n_medium, n_light);
   if (nb <= 0) return;
   if (wide) {
     if constexpr (KS >= 32) {
       hipLaunchKernelGGL((lda_suff_wide<KS, (KS >= 100 ? 8 : 4)>), dim3(nb), dim3(256), 0, s, a, n_heavy, n_medium,
-                         n_light, part);
+                         n_light, part, lay);
       ONI_HIP_CHECK(hipGetLastError());
       return;
     } else {
       throw std::runtime_error("lda_suffstats_fused: wide layout needs KS >= 32");
     }
   }
-  hipLaunchKernelGGL((lda_suff_fused<KS>), dim3(nb), dim3(256), 0, s, a, n_heavy, n_medium, n_light, part);
+  hipLaunchKernelGGL((lda_suff_fused<KS>), dim3(nb), dim3(256), 0, s, a, n_heavy, n_medium, n_light, part, lay);
   ONI_HIP_CHECK(hipGetLastError());
 }
 
 void launch_lda_suffstats_fused(const SuffArgs& a, int n_heavy, int n_medium, int n_light, double* part, int KS,
-                                bool wide, hipStream_t s) {
+                                bool wide, const SuffPartLayout& lay, hipStream_t s) {
+  if (!((lay.off == 0 && lay.stride == KS) || (lay.off == 2 && lay.stride == KS + 2)))
+    throw std::runtime_error("lda_suffstats_fused: partial layout must be [KS] or [2 + KS]");
   switch (KS) {
 #define ONI_KS(X) \
   case X:         \
-    suff_fused_ks<X>(a, n_heavy, n_medium, n_light, part, wide, s); \
+    suff_fused_ks<X>(a, n_heavy, n_medium, n_light, part, wide, lay, s); \
     break;
     ONI_FOR_EACH_KS(ONI_KS)
 #undef ONI_KS
@@ -394,14 +424,82 @@ __global__ __launch_bounds__(256) void lda_mstep_kernel(const float* __restrict_
   }
 }
 
+// ------------------------------------------------------- alpha on device ---
+// lda-c opt_alpha (lda-alpha.c; SURVEY.md C9g): Newton on log(alpha) for
+//   alhood(a) = D (lnG(K a) - K lnG(a)) + (a - 1) ss
+// started at 100, x10 restart on NaN, |df| <= 1e-5 or 1000 iterations, in
+// double exactly as the host version (models/lda/special.py).  Two lanes;
+// it reads alpha_ss from the E-step's reduction output and writes the next
+// E-step's {alpha, lgamma(K a) - K lgamma(a)} into the device parameter block,
+// so an EM iteration needs no host round trip besides the likelihood read-back.
+__device__ double trigamma_ldac(double x) {
+  x = x + 6.0;
+  double p = 1.0 / (x * x);
+  p = (((((0.075757575757576 * p - 0.033333333333333) * p + 0.0238095238095238) * p - 0.033333333333333) * p +
+        0.166666666666667) * p + 1) / x + 0.5 * p;
+  for (int i = 0; i < 6; ++i) {
+    x = x - 1.0;
+    p = 1.0 / (x * x) + p;
+  }
+  return p;
+}
+
+// Lanes 0 and 1 of the calling wave (both must call it): they evaluate each step's
+// special functions at K a and a side by side (one digamma + one trigamma latency per
+// Newton step instead of two of each) and carry the same scalar state.  Lane 0 writes
+// params[0..1] and alpha_out with agent-scope (write-through) stores, so a workgroup of
+// the same launch can read them after its own agent-scope loads (fused M-step).
+__device__ __forceinline__ void alpha_newton_lanes(const double* __restrict__ scalars, double num_docs, int K,
+                                                   int estimate, double* __restrict__ params,
+                                                   double* __restrict__ alpha_out, int lane) {
+  double a = params[0];
+  if (estimate) {
+    const double ss = scalars[1];
+    const double D = num_docs;
+    double init_a = 100.0, log_a = log(init_a), df;
+    int iter = 0;
+    do {
+      ++iter;
+      a = exp(log_a);
+      if (isnan(a)) {
+        init_a = init_a * 10.0;
+        a = init_a;
+        log_a = log(a);
+      }
+      const double x = lane == 0 ? K * a : a;
+      const double dg = digamma_ldac(x), tg = trigamma_ldac(x);
+      const double dg_ka = __shfl(dg, 0, 2), dg_a = __shfl(dg, 1, 2);
+      const double tg_ka = __shfl(tg, 0, 2), tg_a = __shfl(tg, 1, 2);
+      df = D * (K * dg_ka - K * dg_a) + ss;
+      const double d2f = D * (K * K * tg_ka - K * tg_a);
+      log_a = log_a - df / (d2f * a + df);
+    } while (fabs(df) > 1e-5 && iter < 1000);
+    a = exp(log_a);
+  }
+  const double lg = lgamma(lane == 0 ? a * K : a);
+  const double lg_ka = __shfl(lg, 0, 2), lg_a = __shfl(lg, 1, 2);
+  if (lane == 0) {
+    __hip_atomic_store(params, a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(params + 1, lg_ka - K * lg_a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(alpha_out, a, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
 // rows != nullptr: only those word rows (a rank's own words under the sparse class_word
 // exchange -- the other rows of beta are never read on that rank).
 __global__ __launch_bounds__(256) void lda_mstep_control_kernel(const float* __restrict__ cw,
                                                                 const double* __restrict__ ct,
                                                                 float* __restrict__ beta, int V, int K, int KS,
                                                                 const int* __restrict__ rows, int n_rows,
-                                                                EMControlArgs c) {
+                                                                EMControlArgs c, NewtonArgs nw) {
   if (c.params[kParamDone] != 0.0) return;
+  // alpha Newton (lanes 0-1 of workgroup 0) beside the other workgroups' beta rows; its
+  // agent-scope stores drain before this workgroup's completion count below
+  if (nw.enabled && blockIdx.x == 0 && threadIdx.x < 64) {
+    if (threadIdx.x < 2)
+      alpha_newton_lanes(c.scalars, nw.num_docs, K, nw.estimate, c.params, nw.alpha_out, threadIdx.x);
+    __builtin_amdgcn_s_waitcnt(0);
+  }
   // float4 granules of the word-major [V][KS] matrices (KS % 4 == 0)
   const int q = KS / 4;
   const int total4 = (rows ? n_rows : V) * q;
@@ -420,76 +518,38 @@ __global__ __launch_bounds__(256) void lda_mstep_control_kernel(const float* __r
     }
     beta4[i] = make_float4(o[0], o[1], o[2], o[3]);
   }
-  // Relaxed is enough: the control step reads only what earlier kernels wrote (scalars,
-  // params, ctl); the count just has to see every workgroup past its gate read.
+  // Relaxed is enough: the control step reads what earlier kernels wrote (scalars, params,
+  // ctl) plus this launch's alpha, which it loads at agent scope after the count has
+  // seen workgroup 0 (whose write-through stores drained before its add).
   // (An acq_rel agent-scope RMW per workgroup costs an L2 writeback + invalidate each.)
   __syncthreads();
   if (threadIdx.x == 0) {
     if (__hip_atomic_fetch_add(c.done_count, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (int)gridDim.x - 1) {
       __hip_atomic_store(c.done_count, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      em_control_step(c.scalars, c.params, c.ctl, c.hist, c.hist_slots);
+      const double alpha_now = __hip_atomic_load(c.params, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      em_control_step(c.scalars, c.params, c.ctl, c.hist, c.hist_slots, alpha_now);
     }
   }
 }
 
 void launch_lda_mstep_control(const float* cw, const double* class_total, float* beta, int V, int K, int KS,
-                              const int* rows, int n_rows, const EMControlArgs& c, hipStream_t s) {
+                              const int* rows, int n_rows, const EMControlArgs& c, const NewtonArgs& nw,
+                              hipStream_t s) {
   const int64_t total = (int64_t)(rows ? n_rows : V) * KS;
   // 2 workgroups per CU: the completion count is a same-address atomic per workgroup
   int64_t blocks = (total / 4 + 255) / 256;
   if (blocks > 512) blocks = 512;
   if (blocks < 1) blocks = 1;
   hipLaunchKernelGGL(lda_mstep_control_kernel, dim3((unsigned)blocks), dim3(256), 0, s, cw, class_total, beta, V,
-                     K, KS, rows, n_rows, c);
+                     K, KS, rows, n_rows, c, nw);
   ONI_HIP_CHECK(hipGetLastError());
-}
-
-// ------------------------------------------------------- alpha on device ---
-// lda-c opt_alpha (lda-alpha.c; SURVEY.md C9g): Newton on log(alpha) for
-//   alhood(a) = D (lnG(K a) - K lnG(a)) + (a - 1) ss
-// started at 100, x10 restart on NaN, |df| <= 1e-5 or 1000 iterations, in
-// double exactly as the host version (models/lda/special.py).  One thread;
-// it reads alpha_ss from the E-step's reduction output and writes the next
-// E-step's {alpha, lgamma(K a) - K lgamma(a)} into the device parameter block,
-// so an EM iteration needs no host round trip besides the likelihood read-back.
-__device__ double trigamma_ldac(double x) {
-  x = x + 6.0;
-  double p = 1.0 / (x * x);
-  p = (((((0.075757575757576 * p - 0.033333333333333) * p + 0.0238095238095238) * p - 0.033333333333333) * p +
-        0.166666666666667) * p + 1) / x + 0.5 * p;
-  for (int i = 0; i < 6; ++i) {
-    x = x - 1.0;
-    p = 1.0 / (x * x) + p;
-  }
-  return p;
 }
 
 __global__ void alpha_newton_kernel(const double* __restrict__ scalars, double num_docs, int K, int estimate,
                                     double* __restrict__ params, double* __restrict__ alpha_out) {
-  if (threadIdx.x != 0 || blockIdx.x != 0 || params[kParamDone] != 0.0) return;
-  double a = params[0];
-  if (estimate) {
-    const double ss = scalars[1];
-    const double D = num_docs;
-    double init_a = 100.0, log_a = log(init_a), df;
-    int iter = 0;
-    do {
-      ++iter;
-      a = exp(log_a);
-      if (isnan(a)) {
-        init_a = init_a * 10.0;
-        a = init_a;
-        log_a = log(a);
-      }
-      df = D * (K * digamma_ldac(K * a) - K * digamma_ldac(a)) + ss;
-      const double d2f = D * (K * K * trigamma_ldac(K * a) - K * trigamma_ldac(a));
-      log_a = log_a - df / (d2f * a + df);
-    } while (fabs(df) > 1e-5 && iter < 1000);
-    a = exp(log_a);
-  }
-  params[0] = a;
-  params[1] = lgamma(a * K) - K * lgamma(a);
-  alpha_out[0] = a;
+  const int lane = threadIdx.x;
+  if (blockIdx.x != 0 || lane >= 2 || params[kParamDone] != 0.0) return;
+  alpha_newton_lanes(scalars, num_docs, K, estimate, params, alpha_out, lane);
 }
 
 void launch_alpha_newton(const double* scalars, double num_docs, int K, bool estimate, double* params,

@@ -191,11 +191,11 @@ class LDAEngine:
             self._cw_local = torch.zeros_like(self.cw) if self._distributed else self.cw
             self._red_local = torch.zeros_like(self._red) if self._distributed else self._red
             self.suff_plan = H.SuffPlan(self.dc.word_len, dev, wide=_use_wide(self.KS))
-            self._suff_part = torch.zeros(max(self.suff_plan.n_blocks, 1), KS, dtype=torch.float64, device=dev)
+            # per-workgroup partial rows {lik, alpha_ss, class_total[KS]} -> one colsum pass -> _red
+            self._suff_part = torch.zeros(max(self.suff_plan.n_blocks, 1), 2 + KS, dtype=torch.float64, device=dev)
             self._done_count = torch.zeros(1, dtype=torch.int32, device=dev)
             self._alpha_dummy = torch.zeros(1, dtype=torch.float64, device=dev)
             self._red_scratch = torch.zeros(H.lib().reduce_scratch_doubles(KS), dtype=torch.float64, device=dev)
-            self._red_scratch2 = torch.zeros(H.lib().reduce_scratch_doubles(2), dtype=torch.float64, device=dev)
             self._ct_fresh = False
             self._params = torch.zeros(H.PARAM_COUNT, dtype=torch.float64, device=dev)
             self._gate = self._params[H.PARAM_DONE:H.PARAM_DONE + 1]
@@ -209,8 +209,6 @@ class LDAEngine:
             self._graph = None
             self._mgraph, self._mgraph_key = None, None
             self._fgraph, self._fgraph_key = None, None
-            self._ev_red = torch.cuda.Event()
-            self._ev_side = torch.cuda.Event()
             self._out_host = torch.zeros(self._ctlhist.numel(), dtype=torch.float64).pin_memory()
             self._pushed = None
             self._build_schedule()
@@ -250,7 +248,7 @@ class LDAEngine:
             self._plan_a = H.SuffPlan(self.dc.word_len, self.device, wide=wide, words=shared)
             self._plan_b = H.SuffPlan(self.dc.word_len, self.device, wide=wide, words=private)
             nb = max(self._plan_a.n_blocks + self._plan_b.n_blocks, self.suff_plan.n_blocks, 1)
-            self._suff_part = torch.zeros(nb, self.KS, dtype=torch.float64, device=self.device)
+            self._suff_part = torch.zeros(nb, 2 + self.KS, dtype=torch.float64, device=self.device)
             self._graph_a = self._graph_b = None
 
     def _make_exchange(self, corpus: Corpus):
@@ -407,7 +405,7 @@ class LDAEngine:
             pa, pb = self._plan_a, self._plan_b
             H.lda_suffstats_fused(dc.word_ptr, dc.csc_ent, dc.csc_doc, pb, self.e, self.r, self.beta,
                                   self._cw_local, self._suff_part[pa.n_blocks:pa.n_blocks + pb.n_blocks], gate=gate)
-            H.colsum_partials(self._suff_part, pa.n_blocks + pb.n_blocks, self._red_local[2:], gate=gate)
+            H.colsum_partials(self._suff_part, pa.n_blocks + pb.n_blocks, self._red_local, gate=gate)
             self._red.copy_(self._red_local)
             return
         streams = [main] + self._streams
@@ -441,33 +439,22 @@ class LDAEngine:
                 continue
             self._ev_join[si].record(s)
             main.wait_event(self._ev_join[si])
-        side = self._streams[0] if self._streams else None
-        if side is not None:
-            # the scalar reduction (and the alpha Newton) overlap the suff-stats gather
-            self._ev_red.record(main)
-            side.wait_event(self._ev_red)
-            with torch.cuda.stream(side):
-                self._launch_scalars(newton_key)
-        else:
-            self._launch_scalars(newton_key)
         # sufficient statistics: one deterministic CSC gather-reduce launch over every word (empty
-        # words included, so cw needs no clearing) + per-workgroup column sums -> class totals
+        # words included, so cw needs no clearing); each workgroup also sums a slice of the
+        # documents' likelihood / alpha_ss, so one column pass over the partial rows gives
+        # {likelihood, alpha_ss, class_total} (no side-stream reduction, no stream join)
+        scal = (self.lik, self.ass, 0, self.lik.numel())
         if phase == "A":
             # overlap mode: the shared words' rows first, packed for the all-to-all
             H.lda_suffstats_fused(dc.word_ptr, dc.csc_ent, dc.csc_doc, self._plan_a, self.e, self.r, self.beta,
-                                  self._cw_local, self._suff_part[:max(self._plan_a.n_blocks, 1)], gate=gate)
+                                  self._cw_local, self._suff_part[:max(self._plan_a.n_blocks, 1)], gate=gate,
+                                  scalars=scal)
             self._xchg.pack(self._cw_local)
-            if side is not None:
-                self._ev_side.record(side)
-                main.wait_event(self._ev_side)
             return
         sp = self.suff_plan
         H.lda_suffstats_fused(dc.word_ptr, dc.csc_ent, dc.csc_doc, sp, self.e, self.r, self.beta, self._cw_local,
-                              self._suff_part[:max(sp.n_blocks, 1)], gate=gate)
-        H.colsum_partials(self._suff_part, sp.n_blocks, self._red_local[2:], gate=gate)
-        if side is not None:
-            self._ev_side.record(side)
-            main.wait_event(self._ev_side)
+                              self._suff_part[:max(sp.n_blocks, 1)], gate=gate, scalars=scal)
+        H.colsum_partials(self._suff_part, sp.n_blocks, self._red_local, gate=gate)
         if self._distributed:
             # collective inputs (see __init__): the dense all-reduce runs on self.cw / self._red;
             # the sparse exchange packs the shared rows here and accumulates in the M graph
@@ -477,19 +464,15 @@ class LDAEngine:
                 self.cw.copy_(self._cw_local)
             self._red.copy_(self._red_local)
         if newton_key is not None:
-            self._launch_beta_control()
+            self._launch_beta_control(newton_key)
 
-    def _launch_scalars(self, newton_key):
-        from ...ops import hip as H
-        H.sum2(self.lik, self.ass, self._red_local[:2], self._red_scratch2, gate=self._gate)
-        if newton_key is not None:
-            H.alpha_newton(self._scalars, newton_key[1], self.K, newton_key[0], self._params, self._alpha_dummy)
-
-    def _launch_beta_control(self):
+    def _launch_beta_control(self, newton_key):
+        """beta, the alpha Newton (workgroup 0 of the same launch) and the EM convergence step."""
         from ...ops import hip as H
         rows = self._xchg.local_rows32 if self._xchg is not None else None
         H.lda_mstep_control(self.cw, self.class_total, self.beta, self.K, self._scalars, self._params, self._ctl,
-                            self._hist, self._done_count, rows=rows)
+                            self._hist, self._done_count, rows=rows,
+                            newton=(newton_key[0], newton_key[1], self._alpha_dummy))
 
     def _reduce_stats(self):
         """Cross-rank reduction of one EM iteration's statistics (outside the graphs): the packed
@@ -505,12 +488,10 @@ class LDAEngine:
 
     def _launch_mstep(self, estimate_alpha: bool, num_docs: int):
         """M-step on the device after the cross-rank reduction: (sparse exchange: sum the received
-        rows), alpha Newton, then beta and the EM convergence step (fused kernel)."""
-        from ...ops import hip as H
+        rows), then beta, the alpha Newton and the EM convergence step (one fused launch)."""
         if self._xchg is not None:
             self._xchg.accumulate(self.cw, self._cw_local)
-        H.alpha_newton(self._scalars, num_docs, self.K, estimate_alpha, self._params, self._alpha_dummy)
-        self._launch_beta_control()
+        self._launch_beta_control((estimate_alpha, num_docs))
 
     def em_iteration(self, estimate_alpha: bool, num_docs: int):
         """One EM iteration (E-step, [all-reduce], M-step, alpha).  Returns (likelihood, alpha_ss)."""

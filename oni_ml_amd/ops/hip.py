@@ -295,8 +295,13 @@ class SuffPlan:
         self.n_blocks = int(lib().suff_fused_blocks(self.n_heavy, self.n_medium, self.n_light))
 
 
-def lda_suffstats_fused(word_ptr, csc_ent, csc_doc, plan: "SuffPlan", e, r, beta, cw, part, gate=None):
-    """class_word for every word (one launch) + per-workgroup column sums into part [n_blocks, KS]."""
+def lda_suffstats_fused(word_ptr, csc_ent, csc_doc, plan: "SuffPlan", e, r, beta, cw, part, gate=None, scalars=None):
+    """class_word for every word (one launch) + per-workgroup column sums into part.
+
+    part [n_blocks, KS]: topic sums only.  part [n_blocks, 2 + KS]: columns 0 / 1 hold the
+    workgroup's slice sums of ``scalars`` = (lik, alpha_ss, lo, hi) over documents [lo, hi)
+    (zeros without ``scalars``), topics follow -- colsum_partials then yields
+    {likelihood, alpha_ss, class_total} in one pass."""
     V, KS = beta.shape
     nnz = csc_ent.numel()
     D = e.shape[0]
@@ -307,6 +312,8 @@ def lda_suffstats_fused(word_ptr, csc_ent, csc_doc, plan: "SuffPlan", e, r, beta
         return
     if plan.wide and KS < 32:
         raise ValueError(f"wide suff-stats layout needs KS >= 32 (got {KS})")
+    if part.dim() != 2 or part.shape[1] not in (KS, KS + 2) or part.shape[0] < max(plan.n_blocks, 1):
+        raise ValueError(f"part: shape {tuple(part.shape)}, expected [>= {plan.n_blocks}, {KS} or {KS + 2}]")
     lib().lda_suffstats_fused(
         _chk(word_ptr, torch.int32, "word_ptr", (V + 1,), dev), _chk(csc_ent, torch.int32, "csc_ent", (nnz,), dev),
         _chk(csc_doc, torch.int32, "csc_doc", (nnz,), dev),
@@ -314,8 +321,18 @@ def lda_suffstats_fused(word_ptr, csc_ent, csc_doc, plan: "SuffPlan", e, r, beta
         plan.n_heavy, plan.n_medium, plan.n_light,
         _chk(e, torch.float32, "e", (D, KS), dev), _chk(r, torch.float32, "r", (nnz,), dev),
         _chk(beta, torch.float32, "beta", (V, KS), dev), _chk(cw, torch.float32, "cw", (V, KS), dev),
-        _chk(part, torch.float64, "part", (max(plan.n_blocks, 1), KS), dev), int(KS), _gate_ptr(gate, dev), _stream(),
-        bool(plan.wide))
+        _chk(part, torch.float64, "part", None, dev), int(KS), _gate_ptr(gate, dev), _stream(),
+        bool(plan.wide), int(part.shape[1]), *_scalar_slice(scalars, D, dev))
+
+
+def _scalar_slice(scalars, D, dev):
+    if scalars is None:
+        return 0, 0, 0, 0
+    lik, ass, lo, hi = scalars
+    if not 0 <= lo <= hi <= D:
+        raise ValueError(f"scalar slice [{lo}, {hi}) outside [0, {D}]")
+    return (_chk(lik, torch.float64, "lik", (D,), dev), _chk(ass, torch.float64, "alpha_ss", (D,), dev),
+            int(lo), int(hi))
 
 
 def rows_accumulate(rows, ptr, src, own, recv, out):
@@ -343,9 +360,11 @@ def colsum_partials(part, n_blocks, out, gate=None):
                           _chk(out, torch.float64, "out", (cols,), dev), _gate_ptr(gate, dev), _stream())
 
 
-def lda_mstep_control(cw, class_total, beta, K, scalars, params, ctl, hist, done_count, rows=None):
+def lda_mstep_control(cw, class_total, beta, K, scalars, params, ctl, hist, done_count, rows=None, newton=None):
     """M-step (beta = cw / class_total) + the device EM convergence step in the last workgroup.
-    ``rows``: int32 word ids, restrict the M-step to them (validated host-side once by the caller)."""
+    ``rows``: int32 word ids, restrict the M-step to them (validated host-side once by the caller).
+    ``newton`` = (estimate_alpha, num_docs, alpha_out): the lda-c alpha Newton runs in workgroup 0 of
+    the same launch (params[0:2] <- alpha, lgamma constant) beside the beta rows."""
     V, KS = cw.shape
     dev = cw.device
     slots = hist.numel() // HIST_COLS
@@ -356,7 +375,10 @@ def lda_mstep_control(cw, class_total, beta, K, scalars, params, ctl, hist, done
         _chk(beta, torch.float32, "beta", (V, KS), dev), int(V), int(K), int(KS),
         _chk(scalars, torch.float64, "scalars", (2,), dev), _chk(params, torch.float64, "params", (PARAM_COUNT,), dev),
         _chk(ctl, torch.float64, "ctl", (8,), dev), _chk(hist, torch.float64, "hist", (slots * HIST_COLS,), dev),
-        int(slots), _chk(done_count, torch.int32, "done_count", (1,), dev), _stream(), rows_ptr, n_rows)
+        int(slots), _chk(done_count, torch.int32, "done_count", (1,), dev), _stream(), rows_ptr, n_rows,
+        0 if newton is None else 1, 0 if newton is None else int(bool(newton[0])),
+        0.0 if newton is None else float(newton[1]),
+        0 if newton is None else _chk(newton[2], torch.float64, "alpha_out", (1,), dev))
 
 
 def alpha_newton(scalars, num_docs, K, estimate, params, alpha_out):

@@ -84,8 +84,8 @@ def main():
 
         def suff():
             H.lda_suffstats_fused(dc.word_ptr, dc.csc_ent, dc.csc_doc, eng.suff_plan, eng.e, eng.r, eng.beta, eng.cw,
-                                  eng._suff_part)
-            H.colsum_partials(eng._suff_part, eng.suff_plan.n_blocks, eng.class_total)
+                                  eng._suff_part, scalars=(eng.lik, eng.ass, 0, eng.lik.numel()))
+            H.colsum_partials(eng._suff_part, eng.suff_plan.n_blocks, eng._red_local)
         rows.append(dict(bucket="suffstats", ms=round(timed(suff), 4)))
         rows.append(dict(bucket="mstep", ms=round(timed(lambda: eng.m_step(False, 0.0, c.num_docs)), 4)))
 

@@ -40,7 +40,9 @@ def test_two_rank_hip_exchanges_match_single_rank():
     sparse_seq = _run(2, "sparse", overlap="0")
     assert one["exchange"] == "none" and dense["exchange"] == "dense-allreduce"
     assert sparse["exchange"] == "sparse-alltoall" and 0 < sparse["rows"] < 4000
-    assert sparse_seq["likelihoods"] == sparse["likelihoods"]      # same arithmetic, other schedule
+    # same arithmetic, other schedule; the document-likelihood sum is sliced over the grid of the
+    # launch that carries it (plan A vs the whole vocabulary), so only its last bits may differ
+    assert np.allclose(sparse_seq["likelihoods"], sparse["likelihoods"], rtol=1e-13, atol=0)
     for o in (dense, sparse):
         assert len(o["likelihoods"]) == len(one["likelihoods"])
         assert np.allclose(o["likelihoods"], one["likelihoods"], rtol=2e-6), (o["likelihoods"], one["likelihoods"])

@@ -167,6 +167,20 @@ def test_suffstats_fused_and_partial_colsums(hip, K, wide):
     part2 = torch.zeros_like(part)
     hip.lda_suffstats_fused(dc.word_ptr, dc.csc_ent, dc.csc_doc, plan, e, r, beta, cw2, part2)
     assert torch.equal(cw, cw2) and torch.equal(part, part2)
+    # [lik, alpha_ss | topics] partial layout: the document-slice sums ride in columns 0 / 1
+    lik = torch.rand(D, generator=gen, dtype=torch.float64).to(dev) - 0.5
+    ass = torch.rand(D, generator=gen, dtype=torch.float64).to(dev) * -3.0
+    part3 = torch.full((plan.n_blocks, KS + 2), float("nan"), dtype=torch.float64, device=dev)
+    cw4 = torch.zeros_like(cw)
+    hip.lda_suffstats_fused(dc.word_ptr, dc.csc_ent, dc.csc_doc, plan, e, r, beta, cw4, part3, scalars=(lik, ass, 0, D))
+    assert torch.equal(cw4, cw) and torch.equal(part3[:, 2:], part)
+    red = torch.zeros(KS + 2, dtype=torch.float64, device=dev)
+    hip.colsum_partials(part3, plan.n_blocks, red)
+    assert torch.equal(red[2:], ct)
+    assert red[0].item() == pytest.approx(lik.sum().item(), rel=1e-12)
+    assert red[1].item() == pytest.approx(ass.sum().item(), rel=1e-12)
+    hip.lda_suffstats_fused(dc.word_ptr, dc.csc_ent, dc.csc_doc, plan, e, r, beta, cw4, part3)   # no slice: zeros
+    assert part3[:, :2].abs().max().item() == 0
     # a set gate skips the launch
     gate = torch.ones(1, dtype=torch.float64, device=dev)
     cw3 = torch.zeros_like(cw)
@@ -302,3 +316,22 @@ def test_estep_random_corpora_edge_cases(hip, K):
     assert rel < 1e-4, rel
     assert cw[V - 100:].abs().max().item() == 0                      # unused words: zero rows
     assert int(nz.sum()) < D
+
+
+@pytest.mark.parametrize("K", [20, 50, 100])
+def test_alpha_newton_device_matches_host(K):
+    """Device lda-c opt_alpha (two lanes) == host special.opt_alpha, and the lgamma constant."""
+    from oni_ml_amd.ops import hip as H
+    D = 124451
+    for astar in (0.03, 0.2, 1.0, 2.5, 7.0):
+        ss = -D * (K * special.digamma(K * astar) - K * special.digamma(astar)) * 1.01
+        scal = torch.tensor([0.0, ss], dtype=torch.float64, device="cuda")
+        params = torch.zeros(H.PARAM_COUNT, dtype=torch.float64, device="cuda")
+        params[0] = 2.5
+        out = torch.zeros(1, dtype=torch.float64, device="cuda")
+        H.alpha_newton(scal, D, K, True, params, out)
+        torch.cuda.synchronize()
+        host = special.opt_alpha(ss, D, K)
+        a = float(out.item())
+        assert a == pytest.approx(host, rel=1e-9), (astar, a, host)
+        assert float(params[1].item()) == pytest.approx(special.lik_const(a, K), rel=1e-9, abs=1e-9)
