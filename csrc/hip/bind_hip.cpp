@@ -127,10 +127,6 @@ PYBIND11_MODULE(_onihip, m) {
     oni::launch_colsum(P<const float>(mat), rows, cols, P<double>(out), P<double>(scratch), P<const double>(gate),
                        S(stream));
   });
-  m.def("sum2", [](u a, u b, int n, u out, u scratch, u gate, u stream) {
-    oni::launch_sum2(P<const double>(a), P<const double>(b), n, P<double>(out), P<double>(scratch),
-                     P<const double>(gate), S(stream));
-  });
   m.def("em_control", [](u scalars, u params, u ctl, u hist, int hist_slots, u stream) {
     oni::launch_em_control(P<const double>(scalars), P<double>(params), P<double>(ctl), P<double>(hist), hist_slots,
                            S(stream));

@@ -187,8 +187,6 @@ int reduce_scratch_doubles(int cols);
 // gate (nullable): skip when *gate != 0.
 void launch_colsum(const float* m, int rows, int cols, double* out, double* scratch, const double* gate,
                    hipStream_t s);
-void launch_sum2(const double* a, const double* b, int n, double* out, double* scratch, const double* gate,
-                 hipStream_t s);
 // out[k] = sum_b part[b][k] (b in order), the second pass of the fused suff-stats.
 void launch_colsum_partials(const double* part, int nb, int cols, double* out, const double* gate, hipStream_t s);
 // Sparse class_word exchange: out[rows[i]] = 0 + src_0 + src_1 + ... over row i's sources

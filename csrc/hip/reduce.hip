@@ -1,7 +1,6 @@
 // Deterministic two-pass reductions for the EM step (replacing generic torch
 // reductions that cost 12-25 us each at these sizes):
 //   * colsum: class_total[k] = sum_w class_word[w][k]  (f32 [V][KS] -> f64 [KS])
-//   * sum2:   (sum_d lik[d], sum_d alpha_ss[d])         (f64 [D] x 2 -> f64 [2])
 // Pass 1 writes one partial per workgroup, pass 2 (one workgroup) adds the
 // partials in workgroup order, so results are bitwise reproducible run to run
 // and independent of stream scheduling.
@@ -56,60 +55,6 @@ __global__ __launch_bounds__(kRT) void colsum_pass2(const double* __restrict__ p
     for (int j = 0; j < kRB / 64; ++j) s += v[j];
     s = group_sum<64>(s);
     if (lane == 0) out[k] = s;
-  }
-}
-
-__global__ __launch_bounds__(kRT) void sum2_pass1(const double* __restrict__ a, const double* __restrict__ b, int n,
-                                                  double* __restrict__ part, const double* gate) {
-  if (gated(gate)) return;
-  __shared__ double sa[kRT / 64], sb[kRT / 64];
-  const int per = (n + gridDim.x - 1) / gridDim.x;
-  const int i0 = blockIdx.x * per, i1 = min(n, i0 + per);
-  double x = 0.0, y = 0.0;
-  for (int i = i0 + threadIdx.x; i < i1; i += kRT) {
-    x += a[i];
-    y += b[i];
-  }
-  x = group_sum<64>(x);
-  y = group_sum<64>(y);
-  if ((threadIdx.x & 63) == 0) {
-    sa[threadIdx.x >> 6] = x;
-    sb[threadIdx.x >> 6] = y;
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    double u = 0.0, v = 0.0;
-    for (int w = 0; w < kRT / 64; ++w) {
-      u += sa[w];
-      v += sb[w];
-    }
-    part[2 * blockIdx.x] = u;
-    part[2 * blockIdx.x + 1] = v;
-  }
-}
-
-__global__ __launch_bounds__(64) void sum2_pass2(const double* __restrict__ part, int nb, double* __restrict__ out,
-                                                 const double* gate) {
-  if (gated(gate)) return;
-  const int lane = threadIdx.x;
-  double u[kRB / 64], v[kRB / 64];
-#pragma unroll
-  for (int j = 0; j < kRB / 64; ++j) {
-    const int b = lane + 64 * j;
-    u[j] = b < nb ? part[2 * b] : 0.0;
-    v[j] = b < nb ? part[2 * b + 1] : 0.0;
-  }
-  double x = 0.0, y = 0.0;
-#pragma unroll
-  for (int j = 0; j < kRB / 64; ++j) {
-    x += u[j];
-    y += v[j];
-  }
-  x = group_sum<64>(x);
-  y = group_sum<64>(y);
-  if (lane == 0) {
-    out[0] = x;
-    out[1] = y;
   }
 }
 
@@ -192,13 +137,6 @@ void launch_colsum(const float* m, int rows, int cols, double* out, double* scra
   if (cols <= 0 || cols > kRT) throw std::runtime_error("colsum: cols out of range");
   hipLaunchKernelGGL(colsum_pass1, dim3(kRB), dim3(kRT), 0, s, m, rows, cols, scratch, gate);
   hipLaunchKernelGGL(colsum_pass2, dim3(1), dim3(kRT), 0, s, scratch, kRB, cols, out, gate);
-  ONI_HIP_CHECK(hipGetLastError());
-}
-
-void launch_sum2(const double* a, const double* b, int n, double* out, double* scratch, const double* gate,
-                 hipStream_t s) {
-  hipLaunchKernelGGL(sum2_pass1, dim3(kRB), dim3(kRT), 0, s, a, b, n, scratch, gate);
-  hipLaunchKernelGGL(sum2_pass2, dim3(1), dim3(64), 0, s, scratch, kRB, out, gate);
   ONI_HIP_CHECK(hipGetLastError());
 }
 

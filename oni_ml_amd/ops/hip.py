@@ -411,16 +411,6 @@ def colsum(mat, out, scratch, gate=None):
                  _gate_ptr(gate, dev), _stream())
 
 
-def sum2(a, b, out, scratch, gate=None):
-    """out = [sum(a), sum(b)] (f64, deterministic)."""
-    n = a.numel()
-    dev = a.device
-    lib().sum2(_chk(a, torch.float64, "a", (n,), dev), _chk(b, torch.float64, "b", (n,), dev), int(n),
-               _chk(out, torch.float64, "out", (2,), dev),
-               _chk(scratch, torch.float64, "scratch", None, dev) if scratch.numel() >= lib().reduce_scratch_doubles(2)
-               else _bad("scratch"), _gate_ptr(gate, dev), _stream())
-
-
 def _bad(name):
     raise ValueError(f"{name}: buffer too small")
 
