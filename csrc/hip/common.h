@@ -105,7 +105,7 @@ __device__ __forceinline__ double digamma_ldac(double x) {
 //
 // Within a 16-lane row the exchanges are DPP modifiers on the VALU op itself
 // (quad_perm xor1 / xor2, row_half_mirror, row_mirror: no LDS crossbar), the
-// 32-lane step is one ds_swizzle (xor 16), the 64-lane step two v_readlane.
+// 32-lane step a v_permlane16_swap, the 64-lane step a v_permlane32_swap (gfx950).
 // Every step combines a lane with its partner commutatively, so all lanes of
 // a group finish with bitwise the same total (the kernels rely on that:
 // replicated topic state must not diverge between lanes).
@@ -144,6 +144,39 @@ __device__ __forceinline__ double rdlane(double x, int l) {
   const int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffffLL), l), hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
   return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
 }
+// gfx950 v_permlane16_swap / v_permlane32_swap with both operands = x: returns
+// (x of the even rows / lower half, x of the odd rows / upper half) in EVERY lane,
+// so op(first, second) is the xor-16 / xor-32 combination with the same operand
+// order in both partner lanes (bitwise identical) -- a VALU exchange, no LDS
+// crossbar (ds_swizzle) and no v_readlane / SGPR round trip.
+template <bool HALF>
+__device__ __forceinline__ void swap_pair(unsigned x, unsigned& lo_part, unsigned& hi_part) {
+  if constexpr (HALF) {
+    const auto r = __builtin_amdgcn_permlane32_swap(x, x, false, false);
+    lo_part = r[0];
+    hi_part = r[1];
+  } else {
+    const auto r = __builtin_amdgcn_permlane16_swap(x, x, false, false);
+    lo_part = r[0];
+    hi_part = r[1];
+  }
+}
+template <bool HALF, typename Op>
+__device__ __forceinline__ float swap_combine(float x, Op op) {
+  unsigned a, b;
+  swap_pair<HALF>(__float_as_uint(x), a, b);
+  return op(__uint_as_float(a), __uint_as_float(b));
+}
+template <bool HALF, typename Op>
+__device__ __forceinline__ double swap_combine(double x, Op op) {
+  const unsigned long long u = (unsigned long long)__double_as_longlong(x);
+  unsigned alo, blo, ahi, bhi;
+  swap_pair<HALF>((unsigned)(u & 0xffffffffULL), alo, blo);
+  swap_pair<HALF>((unsigned)(u >> 32), ahi, bhi);
+  const double a = __longlong_as_double((long long)(((unsigned long long)ahi << 32) | alo));
+  const double b = __longlong_as_double((long long)(((unsigned long long)bhi << 32) | blo));
+  return op(a, b);
+}
 template <typename T>
 __device__ __forceinline__ T add(T a, T b) { return a + b; }
 template <typename T>
@@ -158,8 +191,8 @@ __device__ __forceinline__ T group_reduce(T x, Op op) {
   x = op(x, xchg<kQuadXor2>(x));
   x = op(x, xchg<kRowHalfMirror>(x));
   x = op(x, xchg<kRowMirror>(x));
-  if constexpr (G >= 32) x = op(x, swz16(x));
-  if constexpr (G == 64) x = op(rdlane(x, 0), rdlane(x, 32));
+  if constexpr (G >= 32) x = swap_combine<false>(x, op);
+  if constexpr (G == 64) x = swap_combine<true>(x, op);
   return x;
 }
 
