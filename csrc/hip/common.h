@@ -78,7 +78,10 @@ __device__ __forceinline__ void digamma_lgamma(float x, float& psi, float& lg) {
   const float x1 = x + 1.0f, x2 = x + 2.0f, x3 = x + 3.0f, x4 = x + 4.0f, x5 = x + 5.0f;
   const float A = x * x1 * x2, dA = fmaf(x, x1 + x2, x1 * x2);
   const float B = x3 * x4 * x5, dB = fmaf(x3, x4 + x5, x4 * x5);
-  const float lxs = __logf(xs), lA = __logf(A), lB = __logf(B);
+  // v_log_f32 (log2) x ln 2: xs >= 6 and A, B > 0 are normal floats, so the denormal
+  // scaling and extended-precision ln 2 of the library logf only lengthen the chain
+  const float lxs = __builtin_amdgcn_logf(xs) * 0.693147180559945f, lA = __builtin_amdgcn_logf(A) * 0.693147180559945f,
+              lB = __builtin_amdgcn_logf(B) * 0.693147180559945f;
   const float pser = (((0.004166666666667f * z - 0.003968253986254f) * z + 0.008333333333333f) * z -
                       0.083333333333333f) * z;
   psi = pser + lxs - 0.5f * ix - dA * frcp(A) - dB * frcp(B);

@@ -42,9 +42,13 @@ constexpr float kPMin = 1e-30f;
 // (L_old == 0 on the first iteration: +-inf or NaN), evaluated without the f64 division:
 // the sign of L_old decides the direction of the inequality.
 __device__ __forceinline__ bool var_more(double lik_old, double L, double c) {
-  if (lik_old < 0.0) return (lik_old - L) < c * lik_old;
-  if (lik_old > 0.0) return (lik_old - L) > c * lik_old;
-  return L < 0.0 && c < INFINITY;   // (0 - L) / 0 = +inf (L < 0), -inf or NaN otherwise
+  // branch-free (selects, no exec-mask branches on the topic-phase chain):
+  //   lik_old < 0: (lik_old - L) < c lik_old;  lik_old > 0: (lik_old - L) > c lik_old;
+  //   lik_old == 0: (0 - L) / 0 = +inf (L < 0), -inf or NaN otherwise
+  const double d = lik_old - L, t = c * lik_old;
+  const bool neg = lik_old < 0.0, pos = lik_old > 0.0;
+  const bool zero_case = !neg & !pos & (L < 0.0) & (c < INFINITY);
+  return (neg & (d < t)) | (pos & (d > t)) | zero_case;
 }
 
 // r = c / P with v_rcp_f32 (1 ulp) instead of IEEE division: the correctly rounded
