@@ -71,6 +71,10 @@ __device__ __forceinline__ float lgammaf_fast(float x) {
 // with A = x(x+1)(x+2) (likewise B over x+3..x+5), and log A, log B, log(x+6),
 // 1/(x+6) are shared with lnGamma: 3 v_rcp + 3 v_log instead of 8 + 4.
 // A, B stay finite for x < 6e12 (gamma values are bounded by document counts).
+// Natural log of a positive NORMAL float: v_log_f32 (log2, ~1 ulp) x ln 2, without the
+// denormal scaling and extended-precision ln 2 of the library logf (a shorter chain).
+__device__ __forceinline__ float log_normal(float x) { return __builtin_amdgcn_logf(x) * 0.693147180559945f; }
+
 __device__ __forceinline__ void digamma_lgamma(float x, float& psi, float& lg) {
   const float xs = x + 6.0f;
   const float ix = frcp(xs);
@@ -80,8 +84,7 @@ __device__ __forceinline__ void digamma_lgamma(float x, float& psi, float& lg) {
   const float B = x3 * x4 * x5, dB = fmaf(x3, x4 + x5, x4 * x5);
   // v_log_f32 (log2) x ln 2: xs >= 6 and A, B > 0 are normal floats, so the denormal
   // scaling and extended-precision ln 2 of the library logf only lengthen the chain
-  const float lxs = __builtin_amdgcn_logf(xs) * 0.693147180559945f, lA = __builtin_amdgcn_logf(A) * 0.693147180559945f,
-              lB = __builtin_amdgcn_logf(B) * 0.693147180559945f;
+  const float lxs = log_normal(xs), lA = log_normal(A), lB = log_normal(B);
   const float pser = (((0.004166666666667f * z - 0.003968253986254f) * z + 0.008333333333333f) * z -
                       0.083333333333333f) * z;
   psi = pser + lxs - 0.5f * ix - dA * frcp(A) - dB * frcp(B);

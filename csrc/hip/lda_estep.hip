@@ -128,7 +128,7 @@ __global__ __launch_bounds__(256) void lda_estep_group(EStepArgs a) {
       if (t + G * c < N) {
         const float P = fmaxf(dot_lds<KS>(sE, bc[c]), kPMin);
         const float r = rdiv(cc[c], P);
-        lsum = fmaf(cc[c], __logf(P), lsum);
+        lsum = fmaf(cc[c], log_normal(P), lsum);
 #pragma unroll
         for (int k = 0; k < KS; ++k) acc[k] = fmaf(r, bc[c][k], acc[k]);
       }
@@ -140,7 +140,7 @@ __global__ __launch_bounds__(256) void lda_estep_group(EStepArgs a) {
       load_row<KS>(a.beta, w, row);
       const float P = fmaxf(dot_lds<KS>(sE, row), kPMin);
       const float r = rdiv(cnt, P);
-      lsum = fmaf(cnt, __logf(P), lsum);
+      lsum = fmaf(cnt, log_normal(P), lsum);
 #pragma unroll
       for (int k = 0; k < KS; ++k) acc[k] = fmaf(r, row[k], acc[k]);
     }
@@ -363,7 +363,7 @@ __global__ __launch_bounds__(NW * 64) void lda_estep_block(EStepArgs a) {
       if (t + NT * c < N) {
         const float P = fmaxf(dot_lds<KS>(sE, bc[c]), kPMin);
         const float r = rdiv(cc[c], P);
-        lsum = fmaf(cc[c], __logf(P), lsum);
+        lsum = fmaf(cc[c], log_normal(P), lsum);
 #pragma unroll
         for (int k = 0; k < KS; ++k) acc[k] = fmaf(r, bc[c][k], acc[k]);
       }
@@ -374,7 +374,7 @@ __global__ __launch_bounds__(NW * 64) void lda_estep_block(EStepArgs a) {
       load_row<KS>(a.beta, a.word_idx[beg + n], row);
       const float P = fmaxf(dot_lds<KS>(sE, row), kPMin);
       const float r = rdiv(cnt, P);
-      lsum = fmaf(cnt, __logf(P), lsum);
+      lsum = fmaf(cnt, log_normal(P), lsum);
 #pragma unroll
       for (int k = 0; k < KS; ++k) acc[k] = fmaf(r, row[k], acc[k]);
     }
@@ -581,7 +581,7 @@ __global__ __launch_bounds__(256) void lda_estep_thread(EStepArgs a) {
       }
       const float P = fmaxf(p0_ + p1_, kPMin);
       const float r = rdiv(cnt, P);
-      lsum = fmaf(cnt, __logf(P), lsum);
+      lsum = fmaf(cnt, log_normal(P), lsum);
 #pragma unroll
       for (int k = 0; k < KS; ++k) acc[k] = fmaf(r, row[k], acc[k]);
       a.r_out[beg + n] = r;

@@ -149,7 +149,7 @@ __global__ __launch_bounds__(kNT) void lda_estep_split(EStepArgs a, SplitArgs s)
       if (t + kNT * c < N) {
         const float P = fmaxf(dot_lds<KS>(sE, bc[c]), kPMin);
         const float r = rdiv(cc[c], P);
-        lsum = fmaf(cc[c], __logf(P), lsum);
+        lsum = fmaf(cc[c], log_normal(P), lsum);
 #pragma unroll
         for (int k = 0; k < KS; ++k) acc[k] = fmaf(r, bc[c][k], acc[k]);
       }

@@ -163,7 +163,7 @@ __device__ __forceinline__ void word_pass(const EStepArgs& a, int beg, int N, in
     if (s + S * i < N) {   // slot-uniform
       const float P = fmaxf(tg_sum<TG>(dot4<CPL>(e, c.bc[i])), kPMin);
       const float r = rdiv(c.cc[i], P);
-      if (q == 0) lsum = fmaf(c.cc[i], __logf(P), lsum);
+      if (q == 0) lsum = fmaf(c.cc[i], log_normal(P), lsum);
       axpy4<CPL>(r, c.bc[i], acc);
     }
   }
@@ -181,7 +181,7 @@ __device__ __forceinline__ void word_pass(const EStepArgs& a, int beg, int N, in
       const float P = fmaxf(tg_sum<TG>(dot4<CPL>(e, rows[u])), kPMin);
       const float x = rdiv(cn[u], P);
       if (q == 0) {
-        lsum = fmaf(cn[u], __logf(P), lsum);
+        lsum = fmaf(cn[u], log_normal(P), lsum);
         a.r_out[beg + n + u * S] = x;
       }
       axpy4<CPL>(x, rows[u], acc);
@@ -194,7 +194,7 @@ __device__ __forceinline__ void word_pass(const EStepArgs& a, int beg, int N, in
     const float P0 = fmaxf(tg_sum<TG>(dot4<CPL>(e, r0)), kPMin);
     const float x0 = rdiv(c0, P0);
     if (q == 0) {
-      lsum = fmaf(c0, __logf(P0), lsum);
+      lsum = fmaf(c0, log_normal(P0), lsum);
       a.r_out[beg + n] = x0;
     }
     axpy4<CPL>(x0, r0, acc);
