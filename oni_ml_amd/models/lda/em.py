@@ -388,11 +388,12 @@ class LDAEngine:
         return self._scalars
 
     def _launch_estep(self, newton_key=None, phase: str = "all"):
-        """Enqueue one E-step: document buckets on their streams, then suff-stats (main stream) and
-        the likelihood / alpha_ss reduction (side stream).  With ``newton_key`` = (estimate_alpha,
-        num_docs) the M-step and the EM convergence test follow in the same launch sequence
-        (single-rank fused EM iteration): alpha Newton on the side stream right after the reduction,
-        beta on the main stream.  Every kernel is gated on params[DONE] (device-side convergence)."""
+        """Enqueue one E-step: document buckets on their streams, one join, then (main stream) the
+        suff-stats launch, which also sums slices of the per-document likelihood / alpha_ss, and one
+        column pass giving {likelihood, alpha_ss, class_total}.  With ``newton_key`` =
+        (estimate_alpha, num_docs) the M-step follows in the same launch sequence (single-rank fused
+        EM iteration): beta, the alpha Newton (workgroup 0) and the EM convergence test in one launch.
+        Every kernel is gated on params[DONE] (device-side convergence)."""
         from ...ops import hip as H
         dc = self.dc
         prm = self._params
