@@ -1,0 +1,161 @@
+#!/usr/bin/env python
+"""Precision parity of the fp32 HIP E-step against fp64 engines on the headline bench corpus.
+
+The reference core (oni-lda-c) computes in double.  The HIP engine
+keeps phi / gamma / E rows in fp32 and the likelihood, alpha_ss, class totals and the alpha
+Newton step in fp64.  This script trains the SAME corpus (bench.py's 1-day synthetic netflow,
+seed 0) from the SAME random init with three engines and compares what the pipeline consumes:
+
+  hip    fp32 Jacobi E-step (HIP kernels, the bench path)
+  torch  fp64 Jacobi E-step (PyTorch on the same GPU, ops/reference.py)
+  cpu    fp64 Gauss-Seidel E-step, a literal transcription of lda-c's lda_inference
+         (csrc/native/lda_ref.cpp; the engine BASELINE.json's docs/s was measured with)
+
+Compared: per-EM-iteration likelihood, EM iterations to convergence, final alpha, the
+exported doc topics theta = gamma / sum(gamma) and word topics phi = softmax(log beta) rows
+(lda_post.py semantics), and the scorer's ranking of (doc, word) entries by
+theta_d . phi_w (flow_post_lda.scala:227-239: the lowest scores are the flagged events).
+
+A fourth run, `cpu@1`, is lda-c's own run-to-run spread: the same fp64 engine from another
+random init (oni-lda-c seeds its MT19937 from the clock, so no two reference runs agree).
+
+  python scripts/precision_parity.py [--events 1000000] [--topics 20] [--engines hip,torch,cpu,cpu@1]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def _train(corpus, K, backend, dev, seed):
+    from oni_ml_amd.models.lda.em import LDAEngine
+    from oni_ml_amd.models.lda.settings import LDASettings
+    eng = LDAEngine(corpus, K, LDASettings(), backend=backend, device=dev, seed=seed)
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    res = eng.run(start="random", on_iteration=lambda e, i, L, c: print(f"  {backend} it {i} L={L:.6f}", flush=True))
+    if dev.type == "cuda":
+        torch.cuda.synchronize()
+    sec = time.perf_counter() - t0
+    res.gamma = np.asarray(eng.gather_gamma(), dtype=np.float64)
+    res.log_beta = np.asarray(eng.log_beta(), dtype=np.float64)
+    return res, sec
+
+
+def _theta(gamma):
+    s = gamma.sum(1, keepdims=True)
+    return np.where(s > 0, gamma / np.where(s > 0, s, 1.0), 0.0)
+
+
+def _phi(log_beta):
+    x = log_beta - log_beta.max(1, keepdims=True)
+    p = np.exp(x)
+    return (p / p.sum(1, keepdims=True)).T          # [V, K]
+
+
+def _entry_scores(corpus, theta, phi):
+    doc = np.repeat(np.arange(corpus.num_docs), np.diff(corpus.doc_ptr))
+    return np.einsum("ek,ek->e", theta[doc], phi[corpus.word_idx])
+
+
+def _topk_overlap(a, b, k):
+    ia = set(np.argsort(a, kind="stable")[:k].tolist())
+    ib = set(np.argsort(b, kind="stable")[:k].tolist())
+    return len(ia & ib) / k
+
+
+def _spearman(a, b):
+    ra = np.empty(len(a)); ra[np.argsort(a, kind="stable")] = np.arange(len(a))
+    rb = np.empty(len(b)); rb[np.argsort(b, kind="stable")] = np.arange(len(b))
+    return float(np.corrcoef(ra, rb)[0, 1])
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--events", type=int, default=1_000_000)
+    ap.add_argument("--topics", type=int, default=20)
+    ap.add_argument("--seed", type=int, default=0)
+    ap.add_argument("--engines", default="hip,torch,cpu,cpu@1")
+    ap.add_argument("--json", default=None)
+    ap.add_argument("--md", default=None)
+    args = ap.parse_args()
+
+    from oni_ml_amd.pipeline.flow import synthetic_flow_corpus
+    dev = torch.device("cuda", 0) if torch.cuda.is_available() else torch.device("cpu")
+    corpus, _ = synthetic_flow_corpus(events=args.events, seed=args.seed, device=dev)
+    print(f"corpus: {corpus.num_docs} docs, {corpus.num_terms} words, {len(corpus.word_idx)} entries", flush=True)
+
+    runs = {}
+    for name in args.engines.split(","):
+        backend, _, seed = name.partition("@")        # "cpu@1": the cpu engine from another random init
+        d = torch.device("cpu") if backend == "cpu" else dev
+        res, sec = _train(corpus, args.topics, backend, d, int(seed) if seed else args.seed)
+        runs[name] = dict(res=res, sec=sec)
+        print(f"{name}: {res.em_iterations} EM iterations, {sec:.2f} s, L={res.likelihoods[-1][0]:.6f}, "
+              f"alpha={res.alpha:.8f}", flush=True)
+
+    names = list(runs)
+    ref_name = "cpu" if "cpu" in runs else names[-1]
+    derived = {}
+    for name, r in runs.items():
+        th, ph = _theta(r["res"].gamma), _phi(r["res"].log_beta)
+        derived[name] = dict(theta=th, phi=ph, score=_entry_scores(corpus, th, ph),
+                             L=np.array([x[0] for x in r["res"].likelihoods]))
+    k_top = max(1, len(corpus.word_idx) // 1000)
+    out = dict(corpus=dict(docs=corpus.num_docs, words=corpus.num_terms, entries=int(len(corpus.word_idx)),
+                           events=args.events, seed=args.seed), topics=args.topics, engines={}, pairs={})
+    for name, r in runs.items():
+        res = r["res"]
+        out["engines"][name] = dict(seconds=round(r["sec"], 3), em_iterations=res.em_iterations,
+                                    final_likelihood=float(derived[name]["L"][-1]), alpha=float(res.alpha),
+                                    likelihood_trajectory=[float(x) for x in derived[name]["L"]])
+    for i, a in enumerate(names):
+        for b in names[i + 1:]:
+            A, B = derived[a], derived[b]
+            n = min(len(A["L"]), len(B["L"]))
+            out["pairs"][f"{a} vs {b}"] = dict(
+                likelihood_rel_diff_max=float(np.max(np.abs(A["L"][:n] - B["L"][:n]) / np.abs(B["L"][:n]))),
+                final_likelihood_rel_diff=float(abs(A["L"][-1] - B["L"][-1]) / abs(B["L"][-1])),
+                alpha_rel_diff=float(abs(runs[a]["res"].alpha - runs[b]["res"].alpha) / runs[b]["res"].alpha),
+                theta_max_abs_diff=float(np.abs(A["theta"] - B["theta"]).max()),
+                theta_mean_abs_diff=float(np.abs(A["theta"] - B["theta"]).mean()),
+                theta_doc_argmax_agree=float((A["theta"].argmax(1) == B["theta"].argmax(1)).mean()),
+                phi_max_abs_diff=float(np.abs(A["phi"] - B["phi"]).max()),
+                score_spearman=_spearman(A["score"], B["score"]),
+                lowest_0p1pct_overlap=_topk_overlap(A["score"], B["score"], k_top),
+            )
+    print(json.dumps(dict(engines={k: {kk: vv for kk, vv in v.items() if kk != "likelihood_trajectory"}
+                                   for k, v in out["engines"].items()}, pairs=out["pairs"]), indent=1), flush=True)
+    if args.json:
+        with open(args.json, "w") as f:
+            json.dump(out, f, indent=1)
+    if args.md:
+        ecols = ["seconds", "em_iterations", "final_likelihood", "alpha"]
+        pcols = list(next(iter(out["pairs"].values())).keys()) if out["pairs"] else []
+        fmt = lambda v: f"{v:.6g}" if isinstance(v, float) else str(v)
+        lines = ["# Precision parity: fp32 HIP E-step vs fp64 engines", "",
+                 f"Corpus: bench.py's 1-day synthetic netflow ({args.events} events, seed {args.seed}): "
+                 f"{corpus.num_docs} docs, {corpus.num_terms} words, {len(corpus.word_idx)} entries; "
+                 f"K = {args.topics}, lda-c default settings, same random init (seed {args.seed}). "
+                 f"Scores = theta_d . phi_w over every corpus entry; overlap = shared fraction of the "
+                 f"{k_top} lowest-scoring (most suspicious) entries.", "",
+                 "| engine | " + " | ".join(ecols) + " |", "|---" * (len(ecols) + 1) + "|"]
+        lines += [f"| {n} | " + " | ".join(fmt(e[c]) for c in ecols) + " |" for n, e in out["engines"].items()]
+        lines += ["", "| pair | " + " | ".join(pcols) + " |", "|---" * (len(pcols) + 1) + "|"]
+        lines += [f"| {n} | " + " | ".join(fmt(e[c]) for c in pcols) + " |" for n, e in out["pairs"].items()]
+        with open(args.md, "w") as f:
+            f.write("\n".join(lines) + "\n")
+
+
+if __name__ == "__main__":
+    main()
