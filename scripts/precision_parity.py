@@ -7,7 +7,7 @@ Newton step in fp64.  This script trains the SAME corpus (bench.py's 1-day synth
 seed 0) from the SAME random init with three engines and compares what the pipeline consumes:
 
   hip    fp32 Jacobi E-step (HIP kernels, the bench path)
-  torch  fp64 Jacobi E-step (PyTorch on the same GPU, ops/reference.py)
+  torch  fp64 Jacobi E-step (PyTorch on the host CPU, ops/reference.py)
   cpu    fp64 Gauss-Seidel E-step, a literal transcription of lda-c's lda_inference
          (csrc/native/lda_ref.cpp; the engine BASELINE.json's docs/s was measured with)
 
@@ -36,10 +36,13 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
-def _train(corpus, K, backend, dev, seed):
+def _train(corpus, K, backend, dev, seed, var_max_iter=None):
     from oni_ml_amd.models.lda.em import LDAEngine
     from oni_ml_amd.models.lda.settings import LDASettings
-    eng = LDAEngine(corpus, K, LDASettings(), backend=backend, device=dev, seed=seed)
+    st = LDASettings()
+    if var_max_iter is not None:
+        st.var_max_iter = var_max_iter
+    eng = LDAEngine(corpus, K, st, backend=backend, device=dev, seed=seed)
     if dev.type == "cuda":
         torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -86,6 +89,7 @@ def main():
     ap.add_argument("--topics", type=int, default=20)
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--engines", default="hip,torch,cpu,cpu@1")
+    ap.add_argument("--var-max-iter", type=int, default=None, help="override settings.txt var max iter (20)")
     ap.add_argument("--json", default=None)
     ap.add_argument("--md", default=None)
     args = ap.parse_args()
@@ -98,8 +102,9 @@ def main():
     runs = {}
     for name in args.engines.split(","):
         backend, _, seed = name.partition("@")        # "cpu@1": the cpu engine from another random init
-        d = torch.device("cpu") if backend == "cpu" else dev
-        res, sec = _train(corpus, args.topics, backend, d, int(seed) if seed else args.seed)
+        # the fp64 PyTorch Jacobi engine runs on the host: its per-bucket launches make it slower on the GPU
+        d = dev if backend == "hip" else torch.device("cpu")
+        res, sec = _train(corpus, args.topics, backend, d, int(seed) if seed else args.seed, args.var_max_iter)
         runs[name] = dict(res=res, sec=sec)
         print(f"{name}: {res.em_iterations} EM iterations, {sec:.2f} s, L={res.likelihoods[-1][0]:.6f}, "
               f"alpha={res.alpha:.8f}", flush=True)
