@@ -1,0 +1,45 @@
+"""scripts/precision_parity.py: the engine-comparison harness behind profiles/r1_precision_parity.md.
+
+CPU: the two fp64 engines (PyTorch Jacobi, literal lda-c Gauss-Seidel) on a small synthetic day; the
+harness must report the pairwise metrics in range and write both outputs.
+GPU: the fp32 HIP engine against the fp64 Jacobi engine (same update schedule), which must agree to
+the tolerances the README quotes for the headline corpus (loosened for the small corpus)."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SCRIPT = os.path.join(ROOT, "scripts", "precision_parity.py")
+
+
+def _run(tmp_path, engines, events):
+    out = tmp_path / "parity.json"
+    r = subprocess.run([sys.executable, SCRIPT, "--events", str(events), "--engines", engines, "--json", str(out),
+                        "--md", str(tmp_path / "parity.md")], capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-2000:]
+    return json.loads(out.read_text())
+
+
+def test_parity_harness_fp64_engines(tmp_path):
+    res = _run(tmp_path, "torch,cpu", 8000)
+    e = res["engines"]
+    assert set(e) == {"torch", "cpu"} and set(res["pairs"]) == {"torch vs cpu"}
+    p = res["pairs"]["torch vs cpu"]
+    assert 0.0 <= p["final_likelihood_rel_diff"] < 1e-2
+    assert 0.5 < p["score_spearman"] <= 1.0
+    assert 0.0 <= p["lowest_0p1pct_overlap"] <= 1.0
+    for v in e.values():
+        assert v["final_likelihood"] < 0 and v["alpha"] > 0 and len(v["likelihood_trajectory"]) == v["em_iterations"]
+    assert (tmp_path / "parity.md").read_text().startswith("# Precision parity")
+
+
+@pytest.mark.gpu
+def test_fp32_hip_engine_tracks_fp64_jacobi(tmp_path):
+    p = _run(tmp_path, "hip,torch", 50000)["pairs"]["hip vs torch"]
+    assert p["likelihood_rel_diff_max"] < 1e-5
+    assert p["alpha_rel_diff"] < 1e-3
+    assert p["theta_doc_argmax_agree"] > 0.99
+    assert p["score_spearman"] > 0.999
