@@ -144,6 +144,39 @@ PYBIND11_MODULE(_onihip, m) {
                           P<const double>(gate), S(stream));
   });
 
+
+  // ---------------------------------------------- fp64 block Gauss-Seidel ---
+  m.def("gs_umax", []() { return oni::kGsUMax; });
+  m.def("gs_tiny_max", [](int KS) { return oni::gs_tiny_max(KS); });
+  m.def("gs_estep", [](u doc_ptr, u word_idx, u counts, u order, int n_items, u beta, int K, int KS, int gs_updates,
+                       u params, u gamma, u cphi, u lik, u alpha_ss, u iters, int variant, u stream) {
+    oni::GSArgs a{P<const int>(doc_ptr), P<const int>(word_idx), P<const float>(counts), P<const int>(order),
+                  n_items,               P<const double>(beta),  K,                      gs_updates,
+                  P<const double>(params), P<double>(gamma),     P<double>(cphi),        P<double>(lik),
+                  P<double>(alpha_ss),   P<int>(iters)};
+    oni::launch_gs_estep(a, variant, KS, S(stream));
+  });
+  m.def("gs_suff64", [](u word_ptr, u csc_ent, u order, int n_heavy, int n_medium, int n_light, u cphi, u cw, u part,
+                        u lik, u ass, int lo, int hi, int KS, u gate, u stream) {
+    oni::launch_gs_suff64(P<const int>(word_ptr), P<const int>(csc_ent), P<const int>(order), n_heavy, n_medium,
+                          n_light, P<const double>(cphi), P<double>(cw), P<double>(part), P<const double>(lik),
+                          P<const double>(ass), lo, hi, KS, P<const double>(gate), S(stream));
+  });
+  m.def("gs_mstep_control", [](u cw, u class_total, u beta, int V, int K, int KS, u scalars, u params, u ctl,
+                               u hist, int hist_slots, u done_count, u stream, u rows, int n_rows, int newton,
+                               int estimate, double num_docs, u alpha_out) {
+    oni::EMControlArgs c{P<const double>(scalars), P<double>(params), P<double>(ctl), P<double>(hist), hist_slots,
+                         P<int>(done_count)};
+    const oni::NewtonArgs nw{newton, estimate, num_docs, P<double>(alpha_out)};
+    if (newton && !alpha_out) throw std::runtime_error("gs_mstep_control: alpha_out required with newton");
+    oni::launch_gs_mstep_control(P<const double>(cw), P<const double>(class_total), P<double>(beta), V, K, KS,
+                                 P<const int>(rows), n_rows, c, nw, S(stream));
+  });
+  m.def("gs_mstep", [](u cw, u class_total, u beta, int V, int K, int KS, u gate, u stream) {
+    oni::launch_gs_mstep(P<const double>(cw), P<const double>(class_total), P<double>(beta), V, K, KS,
+                         P<const double>(gate), S(stream));
+  });
+
   m.def("score_events", [](u theta, u phi, int K, double dflt, u doc_a, u word_a, u doc_b, u word_b,
                            int64_t n, double tol, u score_a, u score_b, u key, u flag, u stream) {
     oni::ScoreArgs a{P<const double>(theta), P<const double>(phi), K, dflt,

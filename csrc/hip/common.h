@@ -25,7 +25,10 @@
 namespace oni {
 
 // exp(-100): the value lda-c's M-step floor (log_prob_w = -100) contributes in
-// the E-step.  It is an f32 subnormal; hipcc keeps f32 denormals by default.
+// the E-step.  It is an f32 subnormal; hipcc keeps f32 denormals by default.  The
+// literal rounds to the nearest subnormal, 27 * 2^-149 = 3.7835e-44 (1.7 % above
+// exp(-100) = 3.7201e-44): the fp32 engine's floor.  The fp64 engine (lda_gs64.hip)
+// keeps exp(-100) exactly.
 constexpr float kExpMinus100 = 3.7200759760208e-44f;
 
 // lda-c digamma (utils.c): x+6 shift, 4-term asymptotic series, then the six

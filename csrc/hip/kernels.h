@@ -180,6 +180,49 @@ void launch_lda_mstep_control(const float* cw, const double* class_total, float*
                               const int* rows, int n_rows, const EMControlArgs& c, const NewtonArgs& nw,
                               hipStream_t s);
 
+// ------------------------------------------------- fp64 block Gauss-Seidel ---
+// lda-c-faithful E-step (lda_gs64.hip): everything in double, gamma / digamma refreshed
+// after every chunk of W = ceil(n / U) words (U = gs_updates refreshes per sweep; a
+// document of n <= U words is lda-c's literal per-word schedule).  The CPU oracle is
+// csrc/native/lda_ref.cpp lda_inference(..., gs_updates).
+constexpr int kGsUMax = 32;          // largest U (chunk tables live in LDS)
+enum GsVariant : int {
+  kGsTiny = 0,     // TG lanes per document, literal schedule, n <= gs_tiny_max(KS)
+  kGsTeam1 = 1,    // one wave per document
+  kGsTeam4 = 2,    // one 4-wave workgroup per document
+  kGsTeam16 = 3,   // one 16-wave workgroup per document
+};
+struct GSArgs {
+  const int* doc_ptr;     // [D+1]
+  const int* word_idx;    // [nnz]
+  const float* counts;    // [nnz] (integer valued)
+  const int* order;       // [n_items] documents of this launch
+  int n_items;
+  const double* beta;     // [V][KS] p(w|z) = exp(log_prob_w), word-major; 0 for padding topics
+  int K;
+  int gs_updates;         // U, 1 <= U <= kGsUMax
+  const double* params;   // {alpha, lgamma(K a) - K lgamma(a), VAR_MAX_ITER, VAR_CONVERGED, done, ...}
+  double* gamma;          // [D][KS]
+  double* cphi;           // [nnz][KS] c_n * phi_nk of the final sweep (sufficient-statistic input)
+  double* lik;            // [D]
+  double* alpha_ss;       // [D]
+  int* iters;             // [D]
+};
+void launch_gs_estep(const GSArgs& a, int variant, int KS, hipStream_t s);
+int gs_tiny_max(int KS);   // longest document of the kGsTiny kernel
+
+// class_word[w] = sum over w's CSC entries of cphi rows (fixed order, no atomics); part
+// [nb][2 + KS] per-workgroup {lik slice, alpha_ss slice, column sums} for colsum_partials.
+void launch_gs_suff64(const int* word_ptr, const int* csc_ent, const int* order, int n_heavy, int n_medium,
+                      int n_light, const double* cphi, double* cw, double* part, const double* lik,
+                      const double* ass, int lo, int hi, int KS, const double* gate, hipStream_t s);
+// fp64 M-step + alpha Newton + EM control (as launch_lda_mstep_control)
+void launch_gs_mstep_control(const double* cw, const double* class_total, double* beta, int V, int K, int KS,
+                             const int* rows, int n_rows, const EMControlArgs& c, const NewtonArgs& nw,
+                             hipStream_t s);
+void launch_gs_mstep(const double* cw, const double* class_total, double* beta, int V, int K, int KS,
+                     const double* gate, hipStream_t s);
+
 // ------------------------------------------------------------- reductions ---
 // Deterministic two-pass reductions (reduce.hip).  scratch holds
 // reduce_scratch_doubles(cols) doubles.

@@ -1,0 +1,786 @@
+// fp64 block Gauss-Seidel E-step, sufficient statistics and M-step (gfx950).
+//
+// Reference: oni-lda-c's lda_inference (call site /root/reference/ml_ops.sh:80;
+// SURVEY.md C9c-C9h) computes in double and refreshes gamma and digamma(gamma)
+// after EVERY word.  This engine keeps lda-c's arithmetic (double, lda-c's series
+// digamma, lgamma, the -100 floor) and its schedule up to the block size: a
+// document of n words is walked in chunks of W = ceil(n / U) words (U = gs_updates
+// refreshes per sweep); a chunk's words take phi from one digamma vector, then
+// gamma and digamma are refreshed.  n <= U is exactly lda-c's per-word schedule.
+// The CPU oracle is csrc/native/lda_ref.cpp lda_inference(..., gs_updates).
+//
+// Chunk algebra (why no per-word phi state is needed): with E_k = exp(psi_k - m)
+// (m = psi of the initial gamma, a per-document constant), P_n = sum_k E_k b_nk,
+// r_n = c_n / P_n, the chunk's contribution to gamma is
+//     new_jk = sum_{n in j} c_n phi_nk = E_k * S_k,   S_k = sum_{n in j} r_n b_nk,
+// so a chunk update is gamma_k += new_jk - C_jk; C_jk = new_jk (C = the chunk's
+// previous contribution, c_total/K before the first sweep), one table of U x KS
+// doubles per document in LDS.  The per-sweep likelihood (lda-c compute_likelihood)
+// collapses to
+//     L = lgG(K a) - K lgG(a) - lgG(sum g) + sum_k lgG(g_k)
+//         + sum_n c_n (m + log P_n) - sum_j sum_k psi_jk new_jk
+// (the (a - 1), (g - 1) and (g - a) psi terms cancel exactly; psi_jk is the digamma
+// the chunk's words saw).  The final sweep's c_n phi_nk = E_jk b_nk r_n rows are
+// written per corpus entry; the suff-stats kernel gathers them in CSC order.
+//
+// Kernel shapes:
+//   gs_tiny   TG lanes per document (KPL = KS / TG topics per lane), n <= NMAX words,
+//             literal per-word schedule; the per-word contributions C[n][.] live in VGPRs.
+//   gs_team   one wave / 4-wave / 16-wave workgroup per document.  Lanes are
+//             (topic group q) x (word slot sl) with the slot in the low lane bits:
+//             a word's P is an xor-16/32 (permlane swap) reduction over q, the slot
+//             reduction of S is a row DPP reduction; cross-wave sums go through LDS in
+//             wave order (bitwise reproducible).  Topic owners (one thread per topic)
+//             run the refresh and broadcast E through LDS.
+#include <stdexcept>
+#include <string>
+
+#include "alpha_newton.h"
+#include "common.h"
+#include "em_control.h"
+#include "kernels.h"
+
+namespace oni {
+namespace gs {
+
+constexpr double kExpM100 = 3.720075976020836e-44;   // exp(-100), lda-c's log-probability floor
+
+constexpr int ilog2(int x) { return x <= 1 ? 0 : 1 + ilog2(x / 2); }
+constexpr int tg_of(int KS) { return KS <= 32 ? 4 : (KS <= 64 ? 8 : 16); }
+constexpr int kpl_of(int KS) { return (KS + tg_of(KS) - 1) / tg_of(KS); }
+// tiny kernel: wider topic groups than the team kernels (fewer topics, hence fewer
+// digamma/exp chains and queue registers per lane)
+constexpr int tiny_tg(int KS) { return KS <= 32 ? 8 : 16; }
+constexpr int tiny_kpl(int KS) { return (KS + tiny_tg(KS) - 1) / tiny_tg(KS); }
+constexpr int tiny_max(int KS) { return tiny_kpl(KS) <= 4 ? 8 : 4; }
+
+// 1/x for a positive normal double: v_rcp_f64 and two Newton steps (~1 ulp).
+__device__ __forceinline__ double drcp(double x) {
+  double r = __builtin_amdgcn_rcp(x);
+  double e = fma(-x, r, 1.0);
+  r = fma(r, e, r);
+  e = fma(-x, r, 1.0);
+  return fma(r, e, r);
+}
+
+// Natural log of a positive normal double in ~25 instructions (OCML's log is ~100): y =
+// 2^e m with m in [sqrt(1/2), sqrt(2)), log m = 2 atanh(f), f = (m - 1) / (m + 1),
+// |f| <= 0.1716, series through f^21 (truncation < 1e-17), ln 2 split hi / lo.  ~2 ulp.
+__device__ __forceinline__ double flog(double y) {
+  int e = __builtin_amdgcn_frexp_exp(y);
+  double mt = __builtin_amdgcn_frexp_mant(y);            // [0.5, 1)
+  const bool lo = mt < 0.70710678118654752;
+  mt = lo ? mt + mt : mt;
+  e = lo ? e - 1 : e;
+  const double f = (mt - 1.0) * drcp(mt + 1.0);
+  const double s = f * f;
+  double p = 0.086956521739130435;                        // 2/23 ... 2/3
+  p = fma(p, s, 0.095238095238095238);
+  p = fma(p, s, 0.10526315789473684);
+  p = fma(p, s, 0.11764705882352941);
+  p = fma(p, s, 0.13333333333333333);
+  p = fma(p, s, 0.15384615384615385);
+  p = fma(p, s, 0.18181818181818182);
+  p = fma(p, s, 0.22222222222222222);
+  p = fma(p, s, 0.28571428571428571);
+  p = fma(p, s, 0.4);
+  p = fma(p, s, 0.66666666666666667);
+  const double de = (double)e;
+  // 2f + f s p  +  e ln2 (hi exact in e * hi for |e| < 2^11)
+  return fma(de, 6.93147180369123816490e-01, fma(de, 1.90821492927058770002e-10, fma(f * s, p, f + f)));
+}
+
+// exp(x) for |x| < 700 in ~20 instructions: x = k ln 2 + r, |r| <= ln2 / 2,
+// degree-12 Taylor polynomial (truncation < 2e-16 relative), 2^k by ldexp.
+__device__ __forceinline__ double fexp(double x) {
+  const double k = __builtin_rint(x * 1.44269504088896340736);
+  const double r = fma(-k, 1.90821492927058770002e-10, fma(-k, 6.93147180369123816490e-01, x));
+  double p = 2.08767569878680989792e-09;                  // 1/12! ... 1/2!
+  p = fma(p, r, 2.50521083854417187751e-08);
+  p = fma(p, r, 2.75573192239858906526e-07);
+  p = fma(p, r, 2.75573192239858906526e-06);
+  p = fma(p, r, 2.48015873015873015873e-05);
+  p = fma(p, r, 1.98412698412698412698e-04);
+  p = fma(p, r, 1.38888888888888888889e-03);
+  p = fma(p, r, 8.33333333333333333333e-03);
+  p = fma(p, r, 4.16666666666666666667e-02);
+  p = fma(p, r, 1.66666666666666666667e-01);
+  p = fma(p, r, 0.5);
+  p = fma(p, r, 1.0);
+  p = fma(p, r, 1.0);
+  return __builtin_amdgcn_ldexp(p, (int)k);
+}
+
+// lda-c digamma (x + 6 shift, 4-term series, six recurrence terms) and
+// E = exp(psi - m).  The six reciprocals 1/(x+i) are dA/A + dB/B with
+// A = x(x+1)(x+2), B = (x+3)(x+4)(x+5); E = (x+6) exp(rest - m) does not wait on the log.
+__device__ __forceinline__ void psi_exp(double x, double m, double& psi, double& e) {
+  const double y = x + 6.0;
+  const double iy = drcp(y);
+  const double z = iy * iy;
+  const double x1 = x + 1.0, x2 = x + 2.0, x3 = x + 3.0, x4 = x + 4.0, x5 = x + 5.0;
+  const double A = x * x1 * x2, dA = fma(x, x1 + x2, x1 * x2);
+  const double B = x3 * x4 * x5, dB = fma(x3, x4 + x5, x4 * x5);
+  const double ser = (((0.004166666666667 * z - 0.003968253986254) * z + 0.008333333333333) * z -
+                      0.083333333333333) * z;
+  const double rest = ser - 0.5 * iy - dA * drcp(A) - dB * drcp(B);
+  psi = flog(y) + rest;
+  e = y * fexp(rest - m);
+}
+
+// ln Gamma(x), x > 0: Stirling series at y = x + 6 (terms through 1/y^13, truncation
+// < 1e-13 absolute) and the recurrence lnG(x) = lnG(x + 6) - ln(x (x+1) ... (x+5)).
+// Same accuracy class as the libm lgamma lda-c calls, at a fraction of OCML's cost.
+__device__ __forceinline__ double lgamma_pos(double x) {
+  const double y = x + 6.0;
+  const double iy = drcp(y);
+  const double z = iy * iy;
+  const double ser = ((((((0.0064102564102564103 * z - 0.0019175269175269175) * z + 0.00084175084175084175) * z -
+                         0.00059523809523809524) * z + 0.00079365079365079365) * z - 0.0027777777777777778) * z +
+                      0.083333333333333333) * iy;
+  const double p = x * (x + 1.0) * (x + 2.0) * ((x + 3.0) * (x + 4.0) * (x + 5.0));
+  return (y - 0.5) * flog(y) - y + 0.91893853320467274 + ser - flog(p);
+}
+
+__device__ __forceinline__ double psi_only(double x) {
+  double p, e;
+  psi_exp(x, 0.0, p, e);
+  return p;
+}
+
+// ---- symmetric lane reductions (every participating lane ends with the same bits) ----
+template <int MASK>
+__device__ __forceinline__ double xsum(double x) {
+  using namespace detail;
+  if constexpr (MASK == 1) {
+    return x + xchg<kQuadXor1>(x);
+  } else if constexpr (MASK == 2) {
+    return x + xchg<kQuadXor2>(x);
+  } else if constexpr (MASK == 4) {
+    const long long b = __double_as_longlong(x);
+    const int lo = __builtin_amdgcn_ds_swizzle((int)(b & 0xffffffffLL), 0x101F);
+    const int hi = __builtin_amdgcn_ds_swizzle((int)(b >> 32), 0x101F);
+    return x + __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+  } else if constexpr (MASK == 8) {
+    return x + xchg<0x128>(x);   // row_ror:8 == xor 8 inside a 16-lane row
+  } else if constexpr (MASK == 16) {
+    return swap_combine<false>(x, add<double>);
+  } else {
+    static_assert(MASK == 32, "lane mask");
+    return swap_combine<true>(x, add<double>);
+  }
+}
+
+// sum over lane bits [LO, HI)
+template <int LO, int HI>
+__device__ __forceinline__ double bits_sum(double x) {
+  if constexpr (LO >= HI) {
+    return x;
+  } else {
+    return bits_sum<LO + 1, HI>(xsum<(1 << LO)>(x));
+  }
+}
+
+__device__ __forceinline__ double params_vconv(const double* p) { return (double)(float)p[3]; }
+
+// lda-c: converged = (L_old - L) / L_old; the loop runs while converged > VAR_CONVERGED
+// and (var_iter < VAR_MAX_ITER or VAR_MAX_ITER == -1).
+__device__ __forceinline__ bool var_continue(double conv, double vconv, int it, int vmi) {
+  return conv > vconv && (it < vmi || vmi == -1);
+}
+
+// ------------------------------------------------------------------ tiny ----
+// C[j][.] (the current contribution of word j) is a register queue: word j always
+// uses C[0], then the queue rotates left by one with the new value at the back, so
+// the word loop is a runtime loop (one copy of the digamma/exp code, ~160 VGPRs)
+// instead of an unrolled one (>256 VGPRs + scratch).  After a sweep of n words the
+// queue is rotated back by (-n) mod NMAX in log2(NMAX) conditional stages.
+template <int N, int KPL>
+__device__ __forceinline__ void rotl1(double (&C)[N][KPL]) {
+#pragma unroll
+  for (int i = 0; i < KPL; ++i) {
+    const double t0 = C[0][i];
+#pragma unroll
+    for (int j = 0; j < N - 1; ++j) C[j][i] = C[j + 1][i];
+    C[N - 1][i] = t0;
+  }
+}
+
+template <int N, int KPL, int B>
+__device__ __forceinline__ void rotl_if(double (&C)[N][KPL], bool on) {
+#pragma unroll
+  for (int i = 0; i < KPL; ++i) {
+    double T[N];
+#pragma unroll
+    for (int j = 0; j < N; ++j) T[j] = C[(j + B) % N][i];
+#pragma unroll
+    for (int j = 0; j < N; ++j) C[j][i] = on ? T[j] : C[j][i];
+  }
+}
+
+template <int KS>
+__global__ __launch_bounds__(256) void gs_tiny(GSArgs a) {
+  constexpr int TG = tiny_tg(KS), KPL = tiny_kpl(KS), NMAX = tiny_max(KS);
+  constexpr int LTG = ilog2(TG);
+  static_assert(NMAX == 4 || NMAX == 8, "tiny queue length");
+  if (a.params[kParamDone] != 0.0) return;
+  const int t = threadIdx.x, q = t & (TG - 1);
+  const int item = blockIdx.x * (256 / TG) + t / TG;
+  if (item >= a.n_items) return;   // whole TG groups leave together
+  const double alpha = a.params[0], lik_const = a.params[1];
+  const int vmi = (int)a.params[2];
+  const double vconv = params_vconv(a.params);
+  const int K = a.K;
+  const int d = a.order[item];
+  const int s0 = a.doc_ptr[d];
+  const int n = min(a.doc_ptr[d + 1] - s0, NMAX);
+  const int* __restrict__ wrow = a.word_idx + s0;
+  const float* __restrict__ crow = a.counts + s0;
+  double total = 0.0;
+  for (int j = 0; j < n; ++j) total += (double)crow[j];
+  const double g0 = alpha + total / K;
+  const double m = psi_only(g0);
+  double gam[KPL], psi[KPL], E[KPL], C[NMAX][KPL];
+#pragma unroll
+  for (int i = 0; i < KPL; ++i) {
+    const bool real = q + TG * i < K;
+    gam[i] = real ? g0 : 0.0;
+    psi[i] = m;
+    E[i] = real ? 1.0 : 0.0;
+  }
+#pragma unroll
+  for (int j = 0; j < NMAX; ++j) {
+    const double cj = j < n ? (double)crow[j] : 0.0;
+#pragma unroll
+    for (int i = 0; i < KPL; ++i) C[j][i] = (q + TG * i < K) ? cj / K : 0.0;
+  }
+  double L = 0.0, L_old = 0.0, conv = 1.0, GS = 0.0;
+  int it = 0;
+  while (var_continue(conv, vconv, it, vmi)) {
+    ++it;
+    double lw = 0.0, lp = 0.0;
+#pragma unroll 1
+    for (int j = 0; j < n; ++j) {
+      const double* brow = a.beta + (size_t)wrow[j] * KS;
+      const double c = (double)crow[j];
+      double b[KPL];
+#pragma unroll
+      for (int i = 0; i < KPL; ++i) b[i] = (q + TG * i < KS) ? brow[q + TG * i] : 0.0;
+      double pp = 0.0;
+#pragma unroll
+      for (int i = 0; i < KPL; ++i) pp = fma(E[i], b[i], pp);
+      const double P = bits_sum<0, LTG>(pp);
+      const double r = c * drcp(P);
+      lw = fma(c, flog(P), lw);
+#pragma unroll
+      for (int i = 0; i < KPL; ++i) {
+        if (q + TG * i < K) {
+          const double nw = E[i] * b[i] * r;
+          lp = fma(psi[i], nw, lp);
+          gam[i] += nw - C[0][i];
+          C[0][i] = nw;
+          psi_exp(gam[i], m, psi[i], E[i]);
+        }
+      }
+      rotl1(C);
+    }
+    // n rotations so far: rotate by (-n) mod NMAX back to word order
+    const int rb = (NMAX - n) & (NMAX - 1);
+    rotl_if<NMAX, KPL, 1>(C, rb & 1);
+    rotl_if<NMAX, KPL, 2>(C, rb & 2);
+    if constexpr (NMAX == 8) rotl_if<NMAX, KPL, 4>(C, rb & 4);
+    double gs = 0.0, lg = 0.0;
+#pragma unroll
+    for (int i = 0; i < KPL; ++i) {
+      if (q + TG * i < K) {
+        gs += gam[i];
+        lg += lgamma_pos(gam[i]);
+      }
+    }
+    GS = bits_sum<0, LTG>(gs);
+    lg = bits_sum<0, LTG>(lg);
+    lp = bits_sum<0, LTG>(lp);
+    L = lik_const - lgamma_pos(GS) + lg + fma(m, total, lw) - lp;
+    conv = (L_old - L) / L_old;
+    L_old = L;
+  }
+  double ps = 0.0;
+#pragma unroll
+  for (int i = 0; i < KPL; ++i) {
+    const int k = q + TG * i;
+    if (k < K) ps += psi[i];
+    if (k < KS) a.gamma[(size_t)d * KS + k] = gam[i];
+  }
+  ps = bits_sum<0, LTG>(ps);
+#pragma unroll
+  for (int j = 0; j < NMAX; ++j) {
+    if (j < n) {
+      double* row = a.cphi + (size_t)(s0 + j) * KS;
+#pragma unroll
+      for (int i = 0; i < KPL; ++i)
+        if (q + TG * i < KS) row[q + TG * i] = C[j][i];
+    }
+  }
+  if (q == 0) {
+    a.lik[d] = L;
+    a.alpha_ss[d] = ps - K * psi_only(GS);
+    a.iters[d] = it;
+  }
+}
+
+// ------------------------------------------------------------------ team ----
+template <int NW>
+__device__ __forceinline__ void team_sync() {
+  if constexpr (NW == 1)
+    wave_lds_sync();
+  else
+    __syncthreads();
+}
+
+constexpr int team_threads(int KS, int NW) { return ((NW == 1 && KS <= 32) ? 4 : 1) * NW * 64; }
+
+template <int KS, int NW>
+struct TeamShape {
+  static constexpr int DPB = (NW == 1 && KS <= 32) ? 4 : 1;   // documents per workgroup
+  static constexpr int NTD = NW * 64;                          // threads per document
+  static constexpr int TG = tg_of(KS), KPL = kpl_of(KS);
+  static constexpr int NSW = 64 / TG;                          // word slots per wave
+  static constexpr int LSW = ilog2(NSW);
+  static constexpr int NS = NW * NSW;                          // word slots per document
+  static constexpr int TO = (KS + NTD - 1) / NTD;              // topics owned per thread
+};
+
+template <int KS, int NW>
+__global__ __launch_bounds__(team_threads(KS, NW)) void gs_team(GSArgs a) {
+  using T = TeamShape<KS, NW>;
+  constexpr int DPB = T::DPB, NTD = T::NTD, TG = T::TG, KPL = T::KPL, NSW = T::NSW, LSW = T::LSW, NS = T::NS,
+                TO = T::TO;
+  __shared__ double sC[DPB][kGsUMax][KS];    // chunk contributions (previous sweep)
+  __shared__ double sEt[DPB][kGsUMax][KS];   // E each chunk used (final pass)
+  __shared__ double sE[DPB][KS];             // current E, broadcast
+  __shared__ double sRed[DPB][NW][KS];       // per-wave slot sums
+  __shared__ double sCs[DPB][kGsUMax];       // chunk count sums
+  __shared__ double sScal[DPB][NW][4];       // per-wave sweep partials
+  if (a.params[kParamDone] != 0.0) return;
+  const int t = threadIdx.x % NTD, ds = threadIdx.x / NTD;
+  const int item = blockIdx.x * DPB + ds;
+  if (item >= a.n_items) return;             // NW == 1: one wave per document (no block barriers)
+  const double alpha = a.params[0], lik_const = a.params[1];
+  const int vmi = (int)a.params[2];
+  const double vconv = params_vconv(a.params);
+  const int K = a.K;
+  const int lane = t & 63, wv = t >> 6;
+  const int q = lane >> LSW, sl = lane & (NSW - 1);
+  const int slot = wv * NSW + sl;
+  const int d = a.order[item];
+  const int s0 = a.doc_ptr[d], n = a.doc_ptr[d + 1] - s0;
+  const int U = a.gs_updates;
+  const int W = n > 0 ? (n + U - 1) / U : 1;
+  const int nch = (n + W - 1) / W;           // <= U <= kGsUMax (host-checked)
+  double(*C)[KS] = sC[ds];
+  double(*Et)[KS] = sEt[ds];
+  double* E_ = sE[ds];
+  double* Cs = sCs[ds];
+  for (int j = t; j < nch; j += NTD) Cs[j] = 0.0;
+  team_sync<NW>();
+  // integer counts: the LDS double atomics are exact in any order
+  for (int p = t; p < n; p += NTD) atomicAdd(&Cs[p / W], (double)a.counts[s0 + p]);
+  team_sync<NW>();
+  double total = 0.0;
+  for (int j = 0; j < nch; ++j) total += Cs[j];
+  const double g0 = alpha + total / K;
+  const double m = psi_only(g0);
+  double gam[TO], psi[TO], lps[TO];
+#pragma unroll
+  for (int o = 0; o < TO; ++o) {
+    const int k = t + NTD * o;
+    gam[o] = k < K ? g0 : 0.0;
+    psi[o] = m;
+    lps[o] = 0.0;
+    if (k < KS) {
+      E_[k] = k < K ? 1.0 : 0.0;
+      for (int j = 0; j < nch; ++j) C[j][k] = k < K ? Cs[j] / K : 0.0;
+    }
+  }
+  team_sync<NW>();
+  double L = 0.0, L_old = 0.0, conv = 1.0, GS = 0.0;
+  int it = 0;
+  while (var_continue(conv, vconv, it, vmi)) {
+    ++it;
+    double lw = 0.0;
+#pragma unroll
+    for (int o = 0; o < TO; ++o) lps[o] = 0.0;
+    for (int j = 0; j < nch; ++j) {
+      const int n0 = j * W, n1 = min(n, n0 + W);
+      double E[KPL], acc[KPL];
+#pragma unroll
+      for (int i = 0; i < KPL; ++i) {
+        E[i] = (q + TG * i < KS) ? E_[q + TG * i] : 0.0;
+        acc[i] = 0.0;
+      }
+      for (int p = n0 + slot; p < n1; p += NS) {
+        const int e = s0 + p;
+        const double* brow = a.beta + (size_t)a.word_idx[e] * KS;
+        const double c = (double)a.counts[e];
+        double b[KPL];
+#pragma unroll
+        for (int i = 0; i < KPL; ++i) b[i] = (q + TG * i < KS) ? brow[q + TG * i] : 0.0;
+        double pp = 0.0;
+#pragma unroll
+        for (int i = 0; i < KPL; ++i) pp = fma(E[i], b[i], pp);
+        const double P = bits_sum<LSW, 6>(pp);
+        const double r = c * drcp(P);
+        lw = fma(c, flog(P), lw);
+#pragma unroll
+        for (int i = 0; i < KPL; ++i) acc[i] = fma(r, b[i], acc[i]);
+      }
+#pragma unroll
+      for (int i = 0; i < KPL; ++i) acc[i] = bits_sum<0, LSW>(acc[i]);
+      if (sl == 0) {
+#pragma unroll
+        for (int i = 0; i < KPL; ++i)
+          if (q + TG * i < KS) sRed[ds][wv][q + TG * i] = acc[i];
+      }
+      team_sync<NW>();
+#pragma unroll
+      for (int o = 0; o < TO; ++o) {
+        const int k = t + NTD * o;
+        if (k < KS) {
+          double S = 0.0;
+#pragma unroll
+          for (int v = 0; v < NW; ++v) S += sRed[ds][v][k];
+          const double Eo = E_[k];
+          const double nw = Eo * S;
+          double En = 0.0;
+          if (k < K) {
+            lps[o] = fma(psi[o], nw, lps[o]);
+            gam[o] += nw - C[j][k];
+            psi_exp(gam[o], m, psi[o], En);
+          }
+          C[j][k] = nw;
+          Et[j][k] = Eo;
+          E_[k] = En;
+        }
+      }
+      team_sync<NW>();
+    }
+    // sweep likelihood: wave partials -> LDS -> every thread sums in wave order
+    double gs = 0.0, lg = 0.0, lp = 0.0;
+#pragma unroll
+    for (int o = 0; o < TO; ++o) {
+      if (t + NTD * o < K) {
+        gs += gam[o];
+        lg += lgamma_pos(gam[o]);
+        lp += lps[o];
+      }
+    }
+    const double w0 = group_sum<64>(q == 0 ? lw : 0.0);
+    const double w1 = group_sum<64>(gs), w2 = group_sum<64>(lg), w3 = group_sum<64>(lp);
+    if (lane == 0) {
+      sScal[ds][wv][0] = w0;
+      sScal[ds][wv][1] = w1;
+      sScal[ds][wv][2] = w2;
+      sScal[ds][wv][3] = w3;
+    }
+    team_sync<NW>();
+    double LW = 0.0, LG = 0.0, LP = 0.0;
+    GS = 0.0;
+#pragma unroll
+    for (int v = 0; v < NW; ++v) {
+      LW += sScal[ds][v][0];
+      GS += sScal[ds][v][1];
+      LG += sScal[ds][v][2];
+      LP += sScal[ds][v][3];
+    }
+    L = lik_const - lgamma_pos(GS) + LG + fma(m, total, LW) - LP;
+    conv = (L_old - L) / L_old;
+    L_old = L;
+    team_sync<NW>();
+  }
+  // outputs
+  double ps = 0.0;
+#pragma unroll
+  for (int o = 0; o < TO; ++o) {
+    const int k = t + NTD * o;
+    if (k < K) ps += psi[o];
+    if (k < KS) a.gamma[(size_t)d * KS + k] = gam[o];
+  }
+  ps = group_sum<64>(ps);
+  if (lane == 0) sScal[ds][wv][0] = ps;
+  team_sync<NW>();
+  if (t == 0) {
+    double PS = 0.0;
+    for (int v = 0; v < NW; ++v) PS += sScal[ds][v][0];
+    a.lik[d] = L;
+    a.alpha_ss[d] = PS - K * psi_only(GS);
+    a.iters[d] = it;
+  }
+  // final pass: c_n phi_nk = E_jk b_nk r_n with the final sweep's chunk E (same P as the sweep)
+  for (int j = 0; j < nch; ++j) {
+    const int n0 = j * W, n1 = min(n, n0 + W);
+    double E[KPL];
+#pragma unroll
+    for (int i = 0; i < KPL; ++i) E[i] = (q + TG * i < KS) ? Et[j][q + TG * i] : 0.0;
+    for (int p = n0 + slot; p < n1; p += NS) {
+      const int e = s0 + p;
+      const double* brow = a.beta + (size_t)a.word_idx[e] * KS;
+      const double c = (double)a.counts[e];
+      double b[KPL];
+#pragma unroll
+      for (int i = 0; i < KPL; ++i) b[i] = (q + TG * i < KS) ? brow[q + TG * i] : 0.0;
+      double pp = 0.0;
+#pragma unroll
+      for (int i = 0; i < KPL; ++i) pp = fma(E[i], b[i], pp);
+      const double r = c * drcp(bits_sum<LSW, 6>(pp));
+      double* row = a.cphi + (size_t)e * KS;
+#pragma unroll
+      for (int i = 0; i < KPL; ++i)
+        if (q + TG * i < KS) row[q + TG * i] = E[i] * b[i] * r;
+    }
+  }
+}
+
+// ------------------------------------------------------------ suff stats ----
+// One word per workgroup (heavy) / wave (medium) / 16 lanes (light); a CSC entry's
+// row is read by TG lanes (KPL topics each), S = G / TG entries in flight per group.
+template <int KS>
+__global__ __launch_bounds__(256) void gs_suff64(const int* __restrict__ word_ptr, const int* __restrict__ csc_ent,
+                                                 const int* __restrict__ order, int n_heavy, int n_medium,
+                                                 int n_light, const double* __restrict__ cphi,
+                                                 double* __restrict__ cw, double* __restrict__ part,
+                                                 const double* __restrict__ lik, const double* __restrict__ ass,
+                                                 int lo, int hi, const double* gate) {
+  constexpr int TG = tg_of(KS), KPL = kpl_of(KS), NSLOT = 256 / TG;
+  __shared__ double sAcc[NSLOT][KS];
+  __shared__ double sRow[16][KS];
+  if (gated(gate)) return;
+  const int t = threadIdx.x, b = blockIdx.x;
+  double* prow = part + (size_t)b * (KS + 2);
+  // likelihood / alpha_ss slice of this workgroup (wave 0, fixed order)
+  if (t < 64) {
+    const int nd = hi - lo, nb = (int)gridDim.x;
+    const int per = (nd + nb - 1) / nb;
+    const int i0 = lo + b * per, i1 = min(hi, i0 + per);
+    double x = 0.0, y = 0.0;
+    if (lik)
+      for (int i = i0 + t; i < i1; i += 64) {
+        x += lik[i];
+        y += ass[i];
+      }
+    x = group_sum<64>(x);
+    y = group_sum<64>(y);
+    if (t == 0) {
+      prow[0] = x;
+      prow[1] = y;
+    }
+  }
+  const int nbM = (n_medium + 3) / 4;
+  int G, item, nitems, base;
+  if (b < n_heavy) {
+    G = 256, item = b, nitems = n_heavy, base = 0;
+  } else if (b < n_heavy + nbM) {
+    G = 64, item = (b - n_heavy) * 4 + t / 64, nitems = n_medium, base = n_heavy;
+  } else {
+    G = 16, item = (b - n_heavy - nbM) * 16 + t / 16, nitems = n_light, base = n_heavy + n_medium;
+  }
+  const int S = G / TG, gi = t / G;
+  const int sidx = (t % G) / TG, q = t % TG;
+  const bool valid = item < nitems;
+  double acc[KPL];
+#pragma unroll
+  for (int i = 0; i < KPL; ++i) acc[i] = 0.0;
+  if (valid) {
+    const int w = order[base + item];
+    int e = word_ptr[w] + sidx;
+    const int end = word_ptr[w + 1];
+    for (; e + 3 * S < end; e += 4 * S) {
+      const double* rr[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) rr[u] = cphi + (size_t)csc_ent[e + u * S] * KS;
+      double v[4][KPL];
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int i = 0; i < KPL; ++i) v[u][i] = (q + TG * i < KS) ? rr[u][q + TG * i] : 0.0;
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int i = 0; i < KPL; ++i) acc[i] += v[u][i];
+    }
+    for (; e < end; e += S) {
+      const double* rr = cphi + (size_t)csc_ent[e] * KS;
+#pragma unroll
+      for (int i = 0; i < KPL; ++i)
+        if (q + TG * i < KS) acc[i] += rr[q + TG * i];
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < KPL; ++i)
+    if (q + TG * i < KS) sAcc[t / TG][q + TG * i] = acc[i];
+  __syncthreads();
+  const int ngroups = 256 / G;
+  for (int idx = t; idx < ngroups * KS; idx += 256) {
+    const int g = idx / KS, k = idx % KS;
+    const int it = (G == 256 ? item : item - gi + g);
+    double v = 0.0;
+    for (int u = 0; u < S; ++u) v += sAcc[g * S + u][k];
+    if (it < nitems) cw[(size_t)order[base + it] * KS + k] = v;
+    else v = 0.0;
+    sRow[g][k] = v;
+  }
+  __syncthreads();
+  if (t < KS) {
+    double s = 0.0;
+    for (int g = 0; g < ngroups; ++g) s += sRow[g][t];
+    prow[2 + t] = s;
+  }
+}
+
+// ----------------------------------------------------------------- M-step ---
+__device__ __forceinline__ double mle(double c, double ct) { return c > 0.0 ? c / ct : kExpM100; }
+
+__global__ __launch_bounds__(256) void gs_mstep_control_kernel(const double* __restrict__ cw,
+                                                               const double* __restrict__ ct,
+                                                               double* __restrict__ beta, int V, int K, int KS,
+                                                               const int* __restrict__ rows, int n_rows,
+                                                               EMControlArgs c, NewtonArgs nw) {
+  if (c.params[kParamDone] != 0.0) return;
+  if (nw.enabled && blockIdx.x == 0 && threadIdx.x < 64) {
+    if (threadIdx.x < 2)
+      alpha_newton_lanes(c.scalars, nw.num_docs, K, nw.estimate, c.params, nw.alpha_out, threadIdx.x);
+    __builtin_amdgcn_s_waitcnt(0);
+  }
+  const int hq = KS / 2;
+  const int total2 = (rows ? n_rows : V) * hq;
+  const double2* cw2 = reinterpret_cast<const double2*>(cw);
+  double2* beta2 = reinterpret_cast<double2*>(beta);
+  for (int g = blockIdx.x * blockDim.x + threadIdx.x; g < total2; g += gridDim.x * blockDim.x) {
+    const int k0 = (g % hq) * 2;
+    const int i = rows ? rows[g / hq] * hq + g % hq : g;
+    const double2 v = cw2[i];
+    double2 o;
+    o.x = k0 < K ? mle(v.x, ct[k0]) : 0.0;
+    o.y = k0 + 1 < K ? mle(v.y, ct[k0 + 1]) : 0.0;
+    beta2[i] = o;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    if (__hip_atomic_fetch_add(c.done_count, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (int)gridDim.x - 1) {
+      __hip_atomic_store(c.done_count, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const double alpha_now = __hip_atomic_load(c.params, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      em_control_step(c.scalars, c.params, c.ctl, c.hist, c.hist_slots, alpha_now);
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void gs_mstep_kernel(const double* __restrict__ cw, const double* __restrict__ ct,
+                                                       double* __restrict__ beta, int V, int K, int KS,
+                                                       const double* gate) {
+  if (gated(gate)) return;
+  const int64_t total = (int64_t)V * KS;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (int64_t)gridDim.x * blockDim.x) {
+    const int k = (int)(i % KS);
+    beta[i] = k < K ? mle(cw[i], ct[k]) : 0.0;
+  }
+}
+
+}  // namespace gs
+
+// ------------------------------------------------------------------ launch ---
+template <int KS>
+static void gs_estep_ks(const GSArgs& a, int variant, hipStream_t s) {
+  if (a.n_items <= 0) return;
+  switch (variant) {
+    case kGsTiny: {
+      constexpr int per = 256 / gs::tiny_tg(KS);
+      hipLaunchKernelGGL((gs::gs_tiny<KS>), dim3((a.n_items + per - 1) / per), dim3(256), 0, s, a);
+      break;
+    }
+    case kGsTeam1: {
+      constexpr int dpb = gs::TeamShape<KS, 1>::DPB;
+      hipLaunchKernelGGL((gs::gs_team<KS, 1>), dim3((a.n_items + dpb - 1) / dpb), dim3(dpb * 64), 0, s, a);
+      break;
+    }
+    case kGsTeam4:
+      hipLaunchKernelGGL((gs::gs_team<KS, 4>), dim3(a.n_items), dim3(256), 0, s, a);
+      break;
+    case kGsTeam16:
+      hipLaunchKernelGGL((gs::gs_team<KS, 16>), dim3(a.n_items), dim3(1024), 0, s, a);
+      break;
+    default:
+      throw std::runtime_error("gs_estep: unknown variant");
+  }
+  ONI_HIP_CHECK(hipGetLastError());
+}
+
+void launch_gs_estep(const GSArgs& a, int variant, int KS, hipStream_t s) {
+  if (a.gs_updates < 1 || a.gs_updates > kGsUMax)
+    throw std::runtime_error("gs_estep: gs_updates must be in [1, " + std::to_string(kGsUMax) + "]");
+  if (!a.params) throw std::runtime_error("gs_estep: params block required");
+  switch (KS) {
+#define ONI_KS(X)                       \
+  case X:                               \
+    gs_estep_ks<X>(a, variant, s);      \
+    break;
+    ONI_FOR_EACH_KS(ONI_KS)
+#undef ONI_KS
+    default:
+      throw std::runtime_error("gs_estep: unsupported KS " + std::to_string(KS));
+  }
+}
+
+int gs_tiny_max(int KS) {
+  switch (KS) {
+#define ONI_KS(X) \
+  case X:         \
+    return gs::tiny_max(X);
+    ONI_FOR_EACH_KS(ONI_KS)
+#undef ONI_KS
+    default:
+      throw std::runtime_error("gs_tiny_max: unsupported KS " + std::to_string(KS));
+  }
+}
+
+void launch_gs_suff64(const int* word_ptr, const int* csc_ent, const int* order, int n_heavy, int n_medium,
+                      int n_light, const double* cphi, double* cw, double* part, const double* lik,
+                      const double* ass, int lo, int hi, int KS, const double* gate, hipStream_t s) {
+  const int nb = suff_fused_blocks(n_heavy, n_medium, n_light);
+  if (nb <= 0) return;
+  switch (KS) {
+#define ONI_KS(X)                                                                                        \
+  case X:                                                                                                \
+    hipLaunchKernelGGL((gs::gs_suff64<X>), dim3(nb), dim3(256), 0, s, word_ptr, csc_ent, order, n_heavy, \
+                       n_medium, n_light, cphi, cw, part, lik, ass, lo, hi, gate);                       \
+    break;
+    ONI_FOR_EACH_KS(ONI_KS)
+#undef ONI_KS
+    default:
+      throw std::runtime_error("gs_suff64: unsupported KS " + std::to_string(KS));
+  }
+  ONI_HIP_CHECK(hipGetLastError());
+}
+
+void launch_gs_mstep_control(const double* cw, const double* class_total, double* beta, int V, int K, int KS,
+                             const int* rows, int n_rows, const EMControlArgs& c, const NewtonArgs& nw,
+                             hipStream_t s) {
+  const int64_t total = (int64_t)(rows ? n_rows : V) * KS;
+  int64_t blocks = (total / 2 + 255) / 256;
+  if (blocks > 512) blocks = 512;
+  if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL(gs::gs_mstep_control_kernel, dim3((unsigned)blocks), dim3(256), 0, s, cw, class_total, beta, V,
+                     K, KS, rows, n_rows, c, nw);
+  ONI_HIP_CHECK(hipGetLastError());
+}
+
+void launch_gs_mstep(const double* cw, const double* class_total, double* beta, int V, int K, int KS,
+                     const double* gate, hipStream_t s) {
+  const int64_t total = (int64_t)V * KS;
+  if (total == 0) return;
+  int64_t blocks = (total + 255) / 256;
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(gs::gs_mstep_kernel, dim3((unsigned)blocks), dim3(256), 0, s, cw, class_total, beta, V, K, KS,
+                     gate);
+  ONI_HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace oni

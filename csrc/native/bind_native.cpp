@@ -298,7 +298,7 @@ PYBIND11_MODULE(_oninative, m) {
          py::array_t<int32_t, py::array::c_style | py::array::forcecast> words,
          py::array_t<double, py::array::c_style | py::array::forcecast> counts,
          py::array_t<double, py::array::c_style | py::array::forcecast> log_beta, double alpha, int var_max_iter,
-         double var_conv, int nshards, int threads) {
+         double var_conv, int nshards, int threads, int gs_updates) {
         const int D = (int)doc_ptr.size() - 1;
         if (log_beta.ndim() != 2) throw std::invalid_argument("log_beta must be [K, V]");
         const int K = (int)log_beta.shape(0), V = (int)log_beta.shape(1);
@@ -311,7 +311,7 @@ PYBIND11_MODULE(_oninative, m) {
         {
           py::gil_scoped_release rel;
           r = ldac_estep(doc_ptr.data(), words.data(), counts.data(), D, V, K, log_beta.data(), alpha,
-                         var_max_iter, (float)var_conv, nshards, threads);
+                         var_max_iter, (float)var_conv, nshards, threads, gs_updates);
         }
         py::dict d;
         d["likelihood"] = r.likelihood;
@@ -328,5 +328,6 @@ PYBIND11_MODULE(_oninative, m) {
         return d;
       },
       py::arg("doc_ptr"), py::arg("words"), py::arg("counts"), py::arg("log_beta"), py::arg("alpha"),
-      py::arg("var_max_iter"), py::arg("var_conv"), py::arg("nshards") = 1, py::arg("threads") = 0);
+      py::arg("var_max_iter"), py::arg("var_conv"), py::arg("nshards") = 1, py::arg("threads") = 0,
+      py::arg("gs_updates") = 0);
 }

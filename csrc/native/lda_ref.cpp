@@ -93,7 +93,7 @@ struct Workspace {
   std::vector<double> phi, oldphi, dig;
   void ensure(int n, int K) {
     if ((int)phi.size() < n * K) phi.resize((size_t)n * K);
-    oldphi.resize(K);
+    if ((int)oldphi.size() < K) oldphi.resize(K);
     dig.resize(K);
   }
 };
@@ -125,9 +125,17 @@ double compute_likelihood(const DocView& d, const double* lb, int V, int K, doub
 }
 
 // lda_inference: returns the document likelihood; gam/phi hold the final state.
+// gs_updates = 0: lda-c's literal schedule (gamma and digamma refreshed after every
+// word).  gs_updates = U > 0: block Gauss-Seidel, the schedule of the fp64 HIP
+// engine -- a document of n words is walked in chunks of W = ceil(n / U) words;
+// the words of a chunk take their phi from the same digamma vector, then gamma and
+// digamma are refreshed (at most U refreshes per sweep; n <= U is the literal
+// schedule).  Everything else (init, likelihood, convergence test) is lda-c's.
 double lda_inference(const DocView& d, const double* lb, int V, int K, double alpha, int var_max_iter,
-                     float var_converged, double* gam, Workspace& ws, int* iters) {
+                     float var_converged, double* gam, Workspace& ws, int* iters, int gs_updates) {
   ws.ensure(d.n, K);
+  const int W = gs_updates > 0 ? std::max(1, (d.n + gs_updates - 1) / gs_updates) : 1;
+  if ((int)ws.oldphi.size() < W * K) ws.oldphi.resize((size_t)W * K);
   double* phi = ws.phi.data();
   double* dig = ws.dig.data();
   double* old = ws.oldphi.data();
@@ -140,19 +148,25 @@ double lda_inference(const DocView& d, const double* lb, int V, int K, double al
   int it = 0;
   while (converged > var_converged && (it < var_max_iter || var_max_iter == -1)) {
     it++;
-    for (int n = 0; n < d.n; n++) {
-      double* ph = phi + (size_t)n * K;
-      double phisum = 0;
-      for (int k = 0; k < K; k++) {
-        old[k] = ph[k];
-        ph[k] = dig[k] + lb[(size_t)k * V + d.w[n]];
-        phisum = k > 0 ? ldac_log_sum(phisum, ph[k]) : ph[k];
+    for (int n0 = 0; n0 < d.n; n0 += W) {
+      const int n1 = std::min(d.n, n0 + W);
+      for (int n = n0; n < n1; n++) {
+        double* ph = phi + (size_t)n * K;
+        double* o = old + (size_t)(n - n0) * K;
+        double phisum = 0;
+        for (int k = 0; k < K; k++) {
+          o[k] = ph[k];
+          ph[k] = dig[k] + lb[(size_t)k * V + d.w[n]];
+          phisum = k > 0 ? ldac_log_sum(phisum, ph[k]) : ph[k];
+        }
+        for (int k = 0; k < K; k++) ph[k] = std::exp(ph[k] - phisum);
       }
-      for (int k = 0; k < K; k++) {
-        ph[k] = std::exp(ph[k] - phisum);
-        gam[k] = gam[k] + d.c[n] * (ph[k] - old[k]);
-        dig[k] = ldac_digamma(gam[k]);
+      for (int n = n0; n < n1; n++) {
+        const double* ph = phi + (size_t)n * K;
+        const double* o = old + (size_t)(n - n0) * K;
+        for (int k = 0; k < K; k++) gam[k] = gam[k] + d.c[n] * (ph[k] - o[k]);
       }
+      for (int k = 0; k < K; k++) dig[k] = ldac_digamma(gam[k]);
     }
     L = compute_likelihood(d, lb, V, K, alpha, phi, gam, dig);
     converged = (L_old - L) / L_old;
@@ -184,7 +198,7 @@ std::vector<std::pair<int, int>> shard_ranges(const int64_t* doc_ptr, int D, int
 
 EStepOut ldac_estep(const int64_t* doc_ptr, const int32_t* words, const double* counts, int D, int V, int K,
                     const double* log_beta, double alpha, int var_max_iter, float var_converged, int nshards,
-                    int threads) {
+                    int threads, int gs_updates) {
   // Shards (emulated MPI ranks) are processed one after another; inside a shard
   // documents are inferred in parallel chunks that keep their final phi, and
   // the statistics are then accumulated in document order (words partitioned
@@ -219,7 +233,8 @@ EStepOut ldac_estep(const int64_t* doc_ptr, const int32_t* words, const double* 
           DocView d{words + doc_ptr[di], counts + doc_ptr[di], (int)(doc_ptr[di + 1] - doc_ptr[di]), 0.0};
           for (int n = 0; n < d.n; n++) d.total += d.c[n];
           double* gam = out.gamma.data() + (size_t)di * K;
-          lik[di] = lda_inference(d, log_beta, V, K, alpha, var_max_iter, var_converged, gam, ws[t], &out.iters[di]);
+          lik[di] = lda_inference(d, log_beta, V, K, alpha, var_max_iter, var_converged, gam, ws[t], &out.iters[di],
+                                  gs_updates);
           std::memcpy(phi.data() + (size_t)(doc_ptr[di] - e0) * K, ws[t].phi.data(), sizeof(double) * d.n * K);
           double gsum = 0, dsum = 0;
           for (int k = 0; k < K; k++) {
@@ -439,7 +454,7 @@ int ldac_estimate(const LdacCorpus& c, int K, double alpha_init, const LdacSetti
     i++;
     auto t0 = std::chrono::steady_clock::now();
     r = ldac_estep(c.doc_ptr.data(), c.words.data(), cnt.data(), D, V, K, lb.data(), alpha, st.var_max_iter,
-                   st.var_converged, nshards, threads);
+                   st.var_converged, nshards, threads, st.gs_updates);
     mle(r.class_word, r.class_total, K, V, lb);
     if (st.estimate_alpha) alpha = ldac_opt_alpha(r.alpha_ss, D, K);
     conv = (L_old - r.likelihood) / L_old;
@@ -469,7 +484,8 @@ int ldac_estimate(const LdacCorpus& c, int K, double alpha_init, const LdacSetti
   for (int d = 0; d < D; d++) {
     DocView dv{c.words.data() + c.doc_ptr[d], cnt.data() + c.doc_ptr[d], (int)(c.doc_ptr[d + 1] - c.doc_ptr[d]), 0};
     for (int n = 0; n < dv.n; n++) dv.total += dv.c[n];
-    lda_inference(dv, lb.data(), V, K, alpha, st.var_max_iter, st.var_converged, gam.data(), ws, nullptr);
+    lda_inference(dv, lb.data(), V, K, alpha, st.var_max_iter, st.var_converged, gam.data(), ws, nullptr,
+                  st.gs_updates);
     std::fprintf(wf, "%03d", dv.n);
     for (int n = 0; n < dv.n; n++) {
       int best = 0;
@@ -504,7 +520,7 @@ int ldac_infer(const LdacCorpus& c, const std::string& model_prefix, const LdacS
         DocView dv{c.words.data() + c.doc_ptr[d], cnt.data() + c.doc_ptr[d], (int)(c.doc_ptr[d + 1] - c.doc_ptr[d]), 0};
         for (int n = 0; n < dv.n; n++) dv.total += dv.c[n];
         lik[d] = lda_inference(dv, lb.data(), V, K, alpha, st.var_max_iter, st.var_converged,
-                               gamma.data() + (size_t)d * K, ws, nullptr);
+                               gamma.data() + (size_t)d * K, ws, nullptr, st.gs_updates);
       }
     });
   }

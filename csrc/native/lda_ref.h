@@ -24,6 +24,7 @@ struct LdacSettings {
   int em_max_iter = 100;
   float em_converged = 1e-4f;
   bool estimate_alpha = true;
+  int gs_updates = 0;   // 0: lda-c's per-word schedule; U > 0: block Gauss-Seidel (lda_ref.cpp)
 };
 
 // Result of one E-step over a document range.
@@ -48,7 +49,7 @@ double ldac_opt_alpha(double ss, int D, int K);
 // order, so the result depends on nshards but never on threads.
 EStepOut ldac_estep(const int64_t* doc_ptr, const int32_t* words, const double* counts, int D, int V, int K,
                     const double* log_beta, double alpha, int var_max_iter, float var_converged, int nshards,
-                    int threads);
+                    int threads, int gs_updates = 0);
 
 LdacCorpus read_ldac_corpus(const std::string& path);
 LdacSettings read_ldac_settings(const std::string& path);

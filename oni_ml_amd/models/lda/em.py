@@ -131,8 +131,13 @@ class LDAEngine:
     def __init__(self, corpus: Corpus, num_topics: int, settings: Optional[LDASettings] = None,
                  alpha_init: float = 2.5, backend: str = "auto", device=None, dist=None, seed: int = 0,
                  streams: int = 4, local_shard: bool = False, split_docs: bool = True,
-                 split_min: Optional[int] = 4096, use_graph: bool = True):
+                 split_min: Optional[int] = 4096, use_graph: bool = True, precision: str = "fp64"):
+        """precision (hip backend): "fp64" = lda-c arithmetic with the block Gauss-Seidel schedule
+        (lda_gs64.hip, the default); "fp32" = the fp32 Jacobi engine (opt-in fast mode)."""
         self.settings = settings or LDASettings()
+        if precision not in ("fp64", "fp32"):
+            raise ValueError(f"precision must be fp64 or fp32, got {precision!r}")
+        self.precision = precision
         self.K = int(num_topics)
         self.V = corpus.num_terms
         self.alpha = float(alpha_init)
@@ -144,7 +149,14 @@ class LDAEngine:
         self.max_batch = 8          # EM iterations enqueued per host read-back (run())
         if backend == "auto":
             from ...ops import hip as H
-            backend = "hip" if H.available() else "torch"
+            if H.available():
+                backend = "hip"
+            elif torch.cuda.is_available():
+                # a GPU without the kernels is a broken install, not a reason to run 2500x slower
+                H.lib()
+                raise RuntimeError("HIP extension loaded but unusable on this GPU")
+            else:
+                backend = "torch"
         self.backend = backend
         if device is None:
             device = torch.device("cuda", torch.cuda.current_device()) if (
@@ -165,7 +177,11 @@ class LDAEngine:
             self.doc_range = (0, corpus.num_docs)
         self.corpus = corpus
         self.D = corpus.num_docs
-        if backend == "hip":
+        self.fp64 = backend == "hip" and precision == "fp64"
+        self.use_graph = use_graph
+        if self.fp64:
+            self._init_gs64(corpus)
+        elif backend == "hip":
             from ...ops import hip as H
             self.KS = H.padded_topics(self.K)
             self.dc = DeviceCorpus.build(corpus, self.device)
@@ -244,12 +260,112 @@ class LDAEngine:
             shared = np.unique(self._xchg.send_idx.cpu().numpy())
             local = self._xchg.local_ids.cpu().numpy()
             private = np.setdiff1d(local, shared, assume_unique=True)
-            wide = _use_wide(self.KS)
+            wide = _use_wide(self.KS) and not self.fp64
             self._plan_a = H.SuffPlan(self.dc.word_len, self.device, wide=wide, words=shared)
             self._plan_b = H.SuffPlan(self.dc.word_len, self.device, wide=wide, words=private)
             nb = max(self._plan_a.n_blocks + self._plan_b.n_blocks, self.suff_plan.n_blocks, 1)
             self._suff_part = torch.zeros(nb, 2 + self.KS, dtype=torch.float64, device=self.device)
             self._graph_a = self._graph_b = None
+
+    # ------------------------------------------------- fp64 block Gauss-Seidel
+    def gs_updates(self) -> int:
+        """U: gamma refreshes per sweep of the fp64 engine (settings.gs_updates, 0 = the default 32)."""
+        from ...ops import hip as H
+        u = int(self.settings.gs_updates) or min(32, H.gs_umax())
+        if not 1 <= u <= H.gs_umax():
+            raise ValueError(f"gs_updates={u}: the GPU engine supports 1..{H.gs_umax()}")
+        return u
+
+    def _init_gs64(self, corpus: Corpus):
+        """Buffers of the fp64 engine (csrc/hip/lda_gs64.hip): everything lda-c keeps in double is double
+        here (beta, class_word, gamma, the per-entry c*phi rows, likelihood and alpha terms)."""
+        from ...ops import hip as H
+        self.KS = KS = H.padded_topics(self.K)
+        self.dc = DeviceCorpus.build(corpus, self.device)
+        dev, D, V, nnz = self.device, self.D, self.V, corpus.nnz
+        self._U = self.gs_updates()
+        self.gs_plan = H.GSPlan(self.dc.doc_len, KS, self._U, dev)
+        f64 = torch.float64
+        self.beta = torch.zeros(V, KS, dtype=f64, device=dev)
+        self.cw = torch.zeros(V, KS, dtype=f64, device=dev)
+        self.gamma = torch.zeros(D, KS, dtype=f64, device=dev)
+        self.cphi = torch.zeros(max(nnz, 1), KS, dtype=f64, device=dev)[:nnz]
+        self.lik = torch.zeros(D, dtype=f64, device=dev)
+        self.ass = torch.zeros(D, dtype=f64, device=dev)
+        self.iters = torch.zeros(D, dtype=torch.int32, device=dev)
+        self._streams = [torch.cuda.Stream(device=dev) for _ in range(3)]
+        self._red = torch.zeros(2 + KS, dtype=f64, device=dev)
+        self._scalars = self._red[:2]
+        self.class_total = self._red[2:]
+        self._distributed = self.dist is not None and self.dist.world_size > 1
+        self._cw_local = torch.zeros_like(self.cw) if self._distributed else self.cw
+        self._red_local = torch.zeros_like(self._red) if self._distributed else self._red
+        self.suff_plan = H.SuffPlan(self.dc.word_len, dev)
+        self._suff_part = torch.zeros(max(self.suff_plan.n_blocks, 1), 2 + KS, dtype=f64, device=dev)
+        self._done_count = torch.zeros(1, dtype=torch.int32, device=dev)
+        self._alpha_dummy = torch.zeros(1, dtype=f64, device=dev)
+        self._ct_fresh = False
+        self._params = torch.zeros(H.PARAM_COUNT, dtype=f64, device=dev)
+        self._gate = self._params[H.PARAM_DONE:H.PARAM_DONE + 1]
+        self._hist_cap = 64
+        self._ctlhist = torch.zeros(8 + H.HIST_COLS * self._hist_cap, dtype=f64, device=dev)
+        self._ctl, self._hist = self._ctlhist[:8], self._ctlhist[8:]
+        self._ev_fork = torch.cuda.Event()
+        self._ev_join = [torch.cuda.Event() for _ in range(4)]
+        self._graph = None
+        self._mgraph, self._mgraph_key = None, None
+        self._fgraph, self._fgraph_key = None, None
+        self._out_host = torch.zeros(self._ctlhist.numel(), dtype=f64).pin_memory()
+        self._pushed = None
+        self.doc_buckets = None
+
+    def _launch_estep64(self, newton_key=None, phase: str = "all"):
+        """fp64 E-step: length buckets on 4 streams (longest first), one join, then the CSC
+        suff-stats (+ likelihood / alpha_ss slices), one column pass, [M-step + Newton + control]."""
+        from ...ops import hip as H
+        dc, prm, gate = self.dc, self._params, self._gate
+        main = torch.cuda.current_stream(self.device)
+        if phase == "B":
+            pa, pb = self._plan_a, self._plan_b
+            H.gs_suff64(dc.word_ptr, dc.csc_ent, pb, self.cphi, self._cw_local,
+                        self._suff_part[pa.n_blocks:pa.n_blocks + pb.n_blocks], gate=gate)
+            H.colsum_partials(self._suff_part, pa.n_blocks + pb.n_blocks, self._red_local, gate=gate)
+            self._red.copy_(self._red_local)
+            return
+        streams = [main] + self._streams
+        self._ev_fork.record(main)
+        used = []
+        # side streams: the long-document buckets (critical path) are dispatched first
+        work = list(self.gs_plan.plan)
+        for si, (var, order) in zip(range(len(work)), work):
+            s = streams[(si + 1) % len(streams)] if si < len(work) - 1 else main
+            if s is not main:
+                s.wait_event(self._ev_fork)
+                used.append(s)
+            with torch.cuda.stream(s):
+                H.gs_estep(dc.doc_ptr, dc.word_idx, dc.counts, order, self.beta, self.K, self._U, prm, self.gamma,
+                           self.cphi, self.lik, self.ass, self.iters, var)
+        for j, s in enumerate(used):
+            self._ev_join[j].record(s)
+            main.wait_event(self._ev_join[j])
+        scal = (self.lik, self.ass, 0, self.lik.numel())
+        if phase == "A":
+            H.gs_suff64(dc.word_ptr, dc.csc_ent, self._plan_a, self.cphi, self._cw_local,
+                        self._suff_part[:max(self._plan_a.n_blocks, 1)], gate=gate, scalars=scal)
+            self._xchg.pack(self._cw_local)
+            return
+        sp = self.suff_plan
+        H.gs_suff64(dc.word_ptr, dc.csc_ent, sp, self.cphi, self._cw_local, self._suff_part[:max(sp.n_blocks, 1)],
+                    gate=gate, scalars=scal)
+        H.colsum_partials(self._suff_part, sp.n_blocks, self._red_local, gate=gate)
+        if self._distributed:
+            if self._xchg is not None:
+                self._xchg.pack(self._cw_local)
+            else:
+                self.cw.copy_(self._cw_local)
+            self._red.copy_(self._red_local)
+        if newton_key is not None:
+            self._launch_beta_control(newton_key)
 
     def _make_exchange(self, corpus: Corpus):
         """Sparse class_word exchange (parallel/dist.py VocabExchange) when the ranks' vocabularies
@@ -343,7 +459,10 @@ class LDAEngine:
     def _mstep_beta(self):
         if self.backend == "hip":
             from ...ops import hip as H
-            H.lda_mstep(self.cw, self.class_total, self.beta, self.K)
+            if self.fp64:
+                H.gs_mstep(self.cw, self.class_total, self.beta, self.K)
+            else:
+                H.lda_mstep(self.cw, self.class_total, self.beta, self.K)
         else:
             from ...ops import reference as R
             self.beta.copy_(R.mstep(self.cw, self.class_total, self.K))
@@ -365,7 +484,8 @@ class LDAEngine:
         lb = torch.where(self.beta > 0, torch.log(self.beta), torch.full_like(self.beta, LOG_FLOOR))
         res = self._native.lda_estep_ldac(
             self.corpus.doc_ptr, self.corpus.word_idx, self.corpus.counts,
-            np.ascontiguousarray(lb.T.numpy()), self.alpha, self.var_max_iter, self.settings.var_converged, 0)
+            np.ascontiguousarray(lb.T.numpy()), self.alpha, self.var_max_iter, self.settings.var_converged, 0,
+            gs_updates=self.settings.gs_updates)
         self.gamma = torch.from_numpy(res["gamma"])
         self.iters = torch.from_numpy(res["iters"])
         self.lik = torch.from_numpy(res["doc_likelihood"])
@@ -394,6 +514,8 @@ class LDAEngine:
         (estimate_alpha, num_docs) the M-step follows in the same launch sequence (single-rank fused
         EM iteration): beta, the alpha Newton (workgroup 0) and the EM convergence test in one launch.
         Every kernel is gated on params[DONE] (device-side convergence)."""
+        if self.fp64:
+            return self._launch_estep64(newton_key, phase)
         from ...ops import hip as H
         dc = self.dc
         prm = self._params
@@ -471,6 +593,11 @@ class LDAEngine:
         """beta, the alpha Newton (workgroup 0 of the same launch) and the EM convergence step."""
         from ...ops import hip as H
         rows = self._xchg.local_rows32 if self._xchg is not None else None
+        if self.fp64:
+            H.gs_mstep_control(self.cw, self.class_total, self.beta, self.K, self._scalars, self._params, self._ctl,
+                               self._hist, self._done_count, rows=rows,
+                               newton=(newton_key[0], newton_key[1], self._alpha_dummy))
+            return
         H.lda_mstep_control(self.cw, self.class_total, self.beta, self.K, self._scalars, self._params, self._ctl,
                             self._hist, self._done_count, rows=rows,
                             newton=(newton_key[0], newton_key[1], self._alpha_dummy))
@@ -683,7 +810,7 @@ class LDAEngine:
     def _check_split_error(self):
         """A NaN likelihood: if a split-document barrier timed out, fail loudly (the kernel
         flags it instead of hanging the GPU)."""
-        sp = self.doc_buckets.split
+        sp = self.doc_buckets.split if self.doc_buckets is not None else None
         if sp is not None and any(int(b["error"].item()) for b in sp.batches):
             raise RuntimeError("split-document E-step: a cross-workgroup barrier timed out "
                                "(segments of one document were not co-resident)")

@@ -34,6 +34,9 @@ class LDASettings:
     em_max_iter: int = 100
     em_converged: float = 1e-4
     estimate_alpha: bool = True
+    # Engine schedule (not a settings.txt line): 0 = lda-c's per-word Gauss-Seidel;
+    # U > 0 = block Gauss-Seidel with at most U gamma refreshes per sweep (lda_ref.cpp).
+    gs_updates: int = 0
 
     def __post_init__(self):
         # lda-c keeps these as float32

@@ -506,3 +506,128 @@ def bin_columns(values, cuts):
         return out
     lib().bin_columns(vp, cp, [int(c.numel()) for c in cuts], int(n), out.data_ptr(), _stream())
     return out
+
+
+# ------------------------------------------------------- fp64 block Gauss-Seidel ---
+# lda-c-faithful E-step (csrc/hip/lda_gs64.hip): double everywhere, gamma refreshed after every
+# chunk of ceil(n / gs_updates) words (documents of <= gs_updates words: lda-c's per-word schedule).
+GS_TINY, GS_TEAM1, GS_TEAM4, GS_TEAM16 = range(4)
+
+
+def gs_umax() -> int:
+    return int(lib().gs_umax())
+
+
+def gs_tiny_max(KS: int) -> int:
+    return int(lib().gs_tiny_max(int(KS)))
+
+
+def gs_estep(doc_ptr, word_idx, counts, order, beta, K, gs_updates, params, gamma, cphi, lik, alpha_ss, iters, variant):
+    """One launch of the fp64 block Gauss-Seidel E-step over the documents in ``order``.
+    ``params``: the device parameter block {alpha, lgamma constant, VAR_MAX_ITER, VAR_CONVERGED, done}."""
+    D = doc_ptr.numel() - 1
+    nnz = word_idx.numel()
+    V, KS = beta.shape
+    if KS not in compiled_ks():
+        raise ValueError(f"beta row stride {KS} has no compiled kernel")
+    if not (0 < K <= KS):
+        raise ValueError("K out of range")
+    if not (1 <= int(gs_updates) <= gs_umax()):
+        raise ValueError(f"gs_updates must be in [1, {gs_umax()}]")
+    if variant not in (GS_TINY, GS_TEAM1, GS_TEAM4, GS_TEAM16):
+        raise ValueError(f"unknown gs variant {variant}")
+    dev = beta.device
+    args = [
+        _chk(doc_ptr, torch.int32, "doc_ptr", (D + 1,), dev),
+        _chk(word_idx, torch.int32, "word_idx", (nnz,), dev),
+        _chk(counts, torch.float32, "counts", (nnz,), dev),
+        _chk(order, torch.int32, "order", None, dev), order.numel(),
+        _chk(beta, torch.float64, "beta", (V, KS), dev), int(K), int(KS), int(gs_updates),
+        _params_ptr(params, dev) or _bad("params"),
+        _chk(gamma, torch.float64, "gamma", (D, KS), dev),
+        _chk(cphi, torch.float64, "cphi", (nnz, KS), dev),
+        _chk(lik, torch.float64, "lik", (D,), dev),
+        _chk(alpha_ss, torch.float64, "alpha_ss", (D,), dev),
+        _chk(iters, torch.int32, "iters", (D,), dev),
+        int(variant), _stream(),
+    ]
+    if order.numel() == 0:
+        return
+    lib().gs_estep(*args)
+
+
+def gs_suff64(word_ptr, csc_ent, plan: "SuffPlan", cphi, cw, part, gate=None, scalars=None):
+    """class_word[w] = sum of the cphi rows of w's corpus entries (CSC order, fp64, no atomics) + per-workgroup
+    partial rows part[b] = {lik slice, alpha_ss slice, column sums} for ``colsum_partials``."""
+    V, KS = cw.shape
+    nnz = csc_ent.numel()
+    dev = cw.device
+    if plan.covers_all and plan.order.numel() != V:
+        raise ValueError("suff plan does not cover the vocabulary")
+    if plan.order.numel() == 0:
+        return
+    if part.dim() != 2 or part.shape[1] != KS + 2 or part.shape[0] < max(plan.n_blocks, 1):
+        raise ValueError(f"part: shape {tuple(part.shape)}, expected [>= {plan.n_blocks}, {KS + 2}]")
+    if scalars is None:
+        lik = ass = 0
+        lo = hi = 0
+    else:
+        D = scalars[0].numel()
+        lik, ass, lo, hi = _scalar_slice(scalars, D, dev)
+    lib().gs_suff64(
+        _chk(word_ptr, torch.int32, "word_ptr", (V + 1,), dev), _chk(csc_ent, torch.int32, "csc_ent", (nnz,), dev),
+        _chk(plan.order, torch.int32, "order", (plan.order.numel(),), dev), plan.n_heavy, plan.n_medium, plan.n_light,
+        _chk(cphi, torch.float64, "cphi", (nnz, KS), dev), _chk(cw, torch.float64, "cw", (V, KS), dev),
+        _chk(part, torch.float64, "part", None, dev), lik, ass, lo, hi, int(KS), _gate_ptr(gate, dev), _stream())
+
+
+def gs_mstep_control(cw, class_total, beta, K, scalars, params, ctl, hist, done_count, rows=None, newton=None):
+    """fp64 M-step (beta = cw / class_total, exp(-100) floor) + alpha Newton + device EM control step."""
+    V, KS = cw.shape
+    dev = cw.device
+    slots = hist.numel() // HIST_COLS
+    n_rows = 0 if rows is None else int(rows.numel())
+    rows_ptr = 0 if rows is None else _chk(rows, torch.int32, "rows", (n_rows,), dev)
+    lib().gs_mstep_control(
+        _chk(cw, torch.float64, "cw", (V, KS), dev), _chk(class_total, torch.float64, "class_total", (KS,), dev),
+        _chk(beta, torch.float64, "beta", (V, KS), dev), int(V), int(K), int(KS),
+        _chk(scalars, torch.float64, "scalars", (2,), dev), _chk(params, torch.float64, "params", (PARAM_COUNT,), dev),
+        _chk(ctl, torch.float64, "ctl", (8,), dev), _chk(hist, torch.float64, "hist", (slots * HIST_COLS,), dev),
+        int(slots), _chk(done_count, torch.int32, "done_count", (1,), dev), _stream(), rows_ptr, n_rows,
+        0 if newton is None else 1, 0 if newton is None else int(bool(newton[0])),
+        0.0 if newton is None else float(newton[1]),
+        0 if newton is None else _chk(newton[2], torch.float64, "alpha_out", (1,), dev))
+
+
+def gs_mstep(cw, class_total, beta, K, gate=None):
+    V, KS = cw.shape
+    dev = cw.device
+    lib().gs_mstep(_chk(cw, torch.float64, "cw", (V, KS), dev),
+                   _chk(class_total, torch.float64, "class_total", (KS,), dev),
+                   _chk(beta, torch.float64, "beta", (V, KS), dev), int(V), int(K), int(KS), _gate_ptr(gate, dev),
+                   _stream())
+
+
+class GSPlan:
+    """Length buckets of the fp64 block Gauss-Seidel E-step: (variant, int32 doc order) per launch.
+
+    tiny (TG lanes per document, literal schedule) for n <= min(gs_tiny_max(KS), U); one wave per
+    document up to 256 words; a 4-wave workgroup up to 2048; a 16-wave workgroup beyond."""
+    EDGES = ((GS_TEAM16, 2048, None), (GS_TEAM4, 256, 2048), (GS_TEAM1, None, 256))
+
+    def __init__(self, lengths, KS: int, gs_updates: int, device):
+        import numpy as np
+        L = np.asarray(lengths, dtype=np.int64)
+        order = np.argsort(-L, kind="stable").astype(np.int32)
+        Ls = L[order]
+        tiny = min(gs_tiny_max(KS), int(gs_updates))
+        self.plan = []
+        for var, lo, hi in self.EDGES:
+            lo_ = tiny if lo is None else lo
+            m = (Ls > lo_) if hi is None else ((Ls > lo_) & (Ls <= hi))
+            if m.any():
+                self.plan.append((var, torch.from_numpy(order[m].copy()).to(device)))
+        m = Ls <= tiny
+        if m.any():
+            self.plan.append((GS_TINY, torch.from_numpy(order[m].copy()).to(device)))
+        self.tiny_max = tiny
