@@ -9,12 +9,23 @@ sufficient statistics, RCCL all-reduce of class_word when N > 1, M-step and
 the alpha Newton step.  value = documents processed per second summed over
 all ranks (docs x timed EM iterations / max-over-ranks wall time).
 
-Scaling is weak: rank r featurizes its own synthetic netflow day (1M events,
-seed r) through the real pipeline (CSV -> C++ ingest -> GPU featurization ->
-corpus), the ranks agree on the union vocabulary, and the N days are trained
-as one N-day corpus with documents sharded by rank.  Weights are random-init
-(lda-c "random" start).  Extras: time to EM convergence from a fresh random
-init, and (N = 1) the wall-clock of the whole ml_ops flow pipeline on the day.
+Engine: the fp64 block Gauss-Seidel engine (--precision fp64, the default: lda-c's double
+arithmetic and its per-word schedule up to blocks of ceil(n/32) words, csrc/hip/lda_gs64.hip);
+--precision fp32 runs the fp32 Jacobi engine.
+
+value = LDA docs/s TO CONVERGENCE: a fresh random-init run trained until lda-c's EM loop test
+stops it (device-side test, every iteration in full), docs x EM iterations / wall time, summed
+over ranks.  The timed K-step window (``ms_per_step``: W untimed warm-up iterations, then exactly
+K EM iterations bracketed by barrier + synchronize, max over ranks) is reported beside it as
+``window_docs_per_sec``.
+
+--scaling weak (default): rank r featurizes its own synthetic netflow day (1M events, seed r)
+through the real pipeline (CSV -> C++ ingest -> GPU featurization -> corpus), the ranks agree on
+the union vocabulary, and the N days are trained as one N-day corpus with documents sharded by
+rank.  --scaling strong: every rank builds the SAME day and the engine shards its documents
+nnz-balanced over the N ranks, as oni-lda-c splits one model.dat over its MPI ranks
+(ml_ops.sh:22-23,80).  Weights are random-init (lda-c "random" start).  Extra (N = 1): the
+wall-clock of the whole ml_ops flow pipeline on the day, with a TOL that flags >= 10^4 events.
 
   python bench.py --gpus N --steps K --warmup W
   (N > 1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...)
@@ -48,7 +59,7 @@ def _baseline():
 
 
 def build_corpus(args, rank, ctx, dev):
-    seed = args.seed + 1000 * rank
+    seed = args.seed + (1000 * rank if args.scaling == "weak" else 0)
     if args.corpus == "planted":
         from oni_ml_amd.synth.corpus import planted_corpus
         c = planted_corpus(num_docs=args.docs, num_terms=args.vocab, num_topics=24, mean_tokens=25, tail=1.1,
@@ -61,7 +72,7 @@ def build_corpus(args, rank, ctx, dev):
     else:
         from oni_ml_amd.pipeline.flow import synthetic_flow_corpus
         c, info, names = synthetic_flow_corpus(events=args.events, seed=seed, device=dev, return_names=True)
-    if ctx.world_size > 1:
+    if ctx.world_size > 1 and args.scaling == "weak":
         from oni_ml_amd.pipeline.flow import unify_vocabulary
         c, _ = unify_vocabulary(ctx, c, names)
     return c, info
@@ -79,7 +90,7 @@ def _e2e(args, dev):
         t0 = time.perf_counter()
         generate_flow_day(os.path.join(tmp, "in/"), events=args.events, seed=args.seed + 7)
         t_gen = time.perf_counter() - t0
-        cfg = CFG.resolve("20160122", "flow", tol=1e-20, conf_path=None, environ={}, lpath=os.path.join(tmp, "ml"),
+        cfg = CFG.resolve("20160122", "flow", tol=args.e2e_tol, conf_path=None, environ={}, lpath=os.path.join(tmp, "ml"),
                           flow_path=os.path.join(tmp, "in"), backend=args.backend, topics=args.topics, verbose=False)
         _sync(dev)
         t0 = time.perf_counter()
@@ -116,6 +127,11 @@ def main():
     ap.add_argument("--converge", type=int, default=1, help="also time a full random-init run to convergence")
     ap.add_argument("--e2e", type=int, default=1, help="N=1: also time the whole ml_ops flow pipeline on the day")
     ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"], help="cpu: gloo/torch rehearsal")
+    ap.add_argument("--precision", default="fp64", choices=["fp64", "fp32"],
+                    help="fp64: lda-c arithmetic, block Gauss-Seidel (default); fp32: the Jacobi fast mode")
+    ap.add_argument("--scaling", default="weak", choices=["weak", "strong"],
+                    help="weak: one day per GPU; strong: one day sharded over the GPUs")
+    ap.add_argument("--e2e-tol", type=float, default=1e-3, help="suspicion threshold of the timed e2e pipeline")
     args = ap.parse_args()
     args.backend = "hip" if args.device == "cuda" else "torch"
     if args.events is None:
@@ -134,10 +150,11 @@ def main():
     t_corpus = time.perf_counter() - t0
     dist = ctx if world > 1 else None
     # weak scaling: each rank's corpus is its own document shard of the N-day corpus
+    local = args.scaling == "weak"
     eng = LDAEngine(corpus, args.topics, LDASettings(), backend=args.backend, device=dev, dist=dist, seed=args.seed,
-                    local_shard=True, streams=args.streams)
+                    local_shard=local, streams=args.streams, precision=args.precision)
     eng.init_random()
-    docs_global = ctx.allreduce_int(corpus.num_docs)
+    docs_global = eng.global_docs
 
     def run_iters(n):
         # EM iterations exactly as LDAEngine.run() issues them without LAG saves: batches of --batch
@@ -160,13 +177,13 @@ def main():
     dt = time.perf_counter() - t1
     dt = ctx.allreduce_max(dt)
     ms = dt / args.steps * 1e3
-    value = docs_global * args.steps / dt
+    window_value = docs_global * args.steps / dt
     it = eng.iters.cpu().numpy()
 
     extra = dict(var_iter_mean=round(float(it.mean()), 3), var_iter_max=int(it.max()), var_max_iter=eng.var_max_iter)
     # variational iterations of the last E-step by document length (the long documents' share
     # of the E-step is words x iterations)
-    lens = corpus.lengths()
+    lens = eng.corpus.lengths()
     by_len = {}
     for lo, hi in ((0, 16), (16, 64), (64, 256), (256, 1024), (1024, 4096), (4096, 1 << 40)):
         m = (lens > lo) & (lens <= hi)
@@ -174,18 +191,21 @@ def main():
             by_len[f"{lo + 1}-{hi if hi < 1 << 40 else 'inf'}"] = [int(m.sum()), round(float(it[m].mean()), 2),
                                                                   int(it[m].max())]
     extra["var_iter_by_len"] = by_len
+    value = window_value
     if args.converge:
+        # to convergence: fresh engine and random init (seed + 1), lda-c's EM loop test on the device
         eng2 = LDAEngine(corpus, args.topics, LDASettings(), backend=args.backend, device=dev, dist=dist,
-                         seed=args.seed + 1, local_shard=True)
+                         seed=args.seed + 1, local_shard=local, precision=args.precision)
         ctx.barrier()
         _sync(dev)
         t2 = time.perf_counter()
         res = eng2.run()
         _sync(dev)
         tc = ctx.allreduce_max(time.perf_counter() - t2)
+        value = docs_global * res.em_iterations / tc
         extra.update(converge_seconds=round(tc, 4), converge_em_iters=res.em_iterations,
-                     converge_docs_per_sec=round(docs_global * res.em_iterations / tc, 1),
-                     final_likelihood=res.likelihoods[-1][0])
+                     converge_docs_per_sec=round(value, 1), final_likelihood=res.likelihoods[-1][0],
+                     final_alpha=res.alpha)
     if args.e2e and world == 1 and args.corpus == "flow" and args.events <= 2_000_000:
         extra.update(_e2e(args, dev))
     # the measured baseline is the 1-day netflow, K=20 corpus: other configs report no ratio
@@ -194,31 +214,35 @@ def main():
         out = {
             "metric": METRIC if args.corpus != "dns" else "LDA docs/sec to convergence, 1-day DNS",
             "value": round(value, 1),
+            "value_source": ("to convergence: fresh random init, lda-c EM loop test (converge_* fields)"
+                             if args.converge else "timed K-step window (no --converge run)"),
+            "window_docs_per_sec": round(window_value, 1),
             "unit": "docs/s (docs x EM iterations / s, all ranks)",
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(ms, 4),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": args.scaling,
             "vs_baseline": (round(value / base, 2) if base else None),
-            "dtype": "fp32 E-step / fp64 likelihood, alpha, sufficient-statistic totals (reference lda-c: fp64)",
-            # trained to convergence vs an fp64 engine with the same update schedule: likelihood within
-            # 2.6e-7 every EM iteration, alpha 2e-5, suspicious-entry ranking Spearman 1.000
-            "precision_evidence": "profiles/r1_precision_parity.md",
+            "dtype": ("fp64" if args.precision == "fp64" or args.backend != "hip" else
+                      "fp32 E-step / fp64 likelihood, alpha, sufficient-statistic totals (reference lda-c: fp64)"),
+            "schedule": eng.schedule,
+            "precision_evidence": "profiles/r2_precision_parity.md",
             "data": (f"synthetic (1-day {'DNS' if args.corpus == 'dns' else 'netflow'} per GPU through the real "
                      "featurizer, random-init topics)" if args.corpus != "planted" else "synthetic planted-topic corpus"),
             "config": {
                 "model": f"oni-lda-c variational EM LDA, K={args.topics}",
                 "global_batch": docs_global,
                 "seq_len": int(round(corpus.nnz / max(1, corpus.num_docs))),
+                "precision": args.precision,
                 "parallelism": f"dp{world}",
                 "class_word_reduction": eng.exchange_mode,
                 "corpus": args.corpus,
                 "events_per_gpu": args.events if args.corpus in ("flow", "dns") else None,
-                "docs_per_gpu": corpus.num_docs,
+                "docs_per_gpu": eng.D,
                 "vocab": corpus.num_terms,
-                "nnz_per_gpu": corpus.nnz,
+                "nnz_per_gpu": eng.corpus.nnz,
                 "max_doc_len": int(corpus.lengths().max()),
                 "device": args.device,
             },

@@ -149,11 +149,11 @@ PYBIND11_MODULE(_onihip, m) {
   m.def("gs_umax", []() { return oni::kGsUMax; });
   m.def("gs_tiny_max", [](int KS) { return oni::gs_tiny_max(KS); });
   m.def("gs_estep", [](u doc_ptr, u word_idx, u counts, u order, int n_items, u beta, int K, int KS, int gs_updates,
-                       u params, u gamma, u cphi, u lik, u alpha_ss, u iters, int variant, u stream) {
+                       u params, u gamma, u cphi, u lik, u alpha_ss, u iters, int variant, u stream, u dbg) {
     oni::GSArgs a{P<const int>(doc_ptr), P<const int>(word_idx), P<const float>(counts), P<const int>(order),
                   n_items,               P<const double>(beta),  K,                      gs_updates,
                   P<const double>(params), P<double>(gamma),     P<double>(cphi),        P<double>(lik),
-                  P<double>(alpha_ss),   P<int>(iters)};
+                  P<double>(alpha_ss),   P<int>(iters),         P<long long>(dbg)};
     oni::launch_gs_estep(a, variant, KS, S(stream));
   });
   m.def("gs_suff64", [](u word_ptr, u csc_ent, u order, int n_heavy, int n_medium, int n_light, u cphi, u cw, u part,

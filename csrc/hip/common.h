@@ -265,6 +265,16 @@ __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// Workgroup barrier ordering LDS only: s_waitcnt lgkmcnt(0) + s_barrier, WITHOUT the
+// vmcnt(0) wait of __syncthreads()' global release fence, so global loads issued before
+// the barrier (prefetches of the next chunk's rows) stay in flight across it.  Only for
+// kernels whose threads exchange data through LDS, never through global memory.
+__device__ __forceinline__ void lds_barrier() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
 // Multi-value all-reduce: the total of value i over the G lanes of a group in
 // EVERY lane's v[i] (N independent DPP chains: good ILP, no LDS traffic).
 template <int G, int N>

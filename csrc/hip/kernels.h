@@ -190,7 +190,7 @@ enum GsVariant : int {
   kGsTiny = 0,     // TG lanes per document, literal schedule, n <= gs_tiny_max(KS)
   kGsTeam1 = 1,    // one wave per document
   kGsTeam4 = 2,    // one 4-wave workgroup per document
-  kGsTeam16 = 3,   // one 16-wave workgroup per document
+  kGsTeam8 = 3,    // one 8-wave workgroup per document (8 prefetched words per slot and chunk)
 };
 struct GSArgs {
   const int* doc_ptr;     // [D+1]
@@ -207,6 +207,10 @@ struct GSArgs {
   double* lik;            // [D]
   double* alpha_ss;       // [D]
   int* iters;             // [D]
+  // optional phase timer (scripts/bench_gs64.py --phases): workgroup 0, thread 0 of the team kernels
+  // accumulates clock64() cycles into dbg[0..7]: word phase, slot reduction, barrier 1, topic phase,
+  // barrier 2, sweep likelihood, final pass, chunks
+  long long* dbg = nullptr;
 };
 void launch_gs_estep(const GSArgs& a, int variant, int KS, hipStream_t s);
 int gs_tiny_max(int KS);   // longest document of the kGsTiny kernel

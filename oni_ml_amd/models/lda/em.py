@@ -267,6 +267,16 @@ class LDAEngine:
             self._suff_part = torch.zeros(nb, 2 + self.KS, dtype=torch.float64, device=self.device)
             self._graph_a = self._graph_b = None
 
+    @property
+    def schedule(self) -> str:
+        """Variational update schedule of this engine (bench / metrics records)."""
+        if self.backend == "hip" and self.fp64:
+            return f"block Gauss-Seidel, fp64, {self._U} gamma refreshes per sweep (lda-c per-word up to {self._U} words)"
+        if self.backend == "cpu":
+            u = int(self.settings.gs_updates)
+            return "lda-c per-word Gauss-Seidel, fp64" if u == 0 else f"block Gauss-Seidel, fp64, {u} refreshes per sweep"
+        return "Jacobi, " + ("fp32 E-step" if self.backend == "hip" else "fp64")
+
     # ------------------------------------------------- fp64 block Gauss-Seidel
     def gs_updates(self) -> int:
         """U: gamma refreshes per sweep of the fp64 engine (settings.gs_updates, 0 = the default 32)."""

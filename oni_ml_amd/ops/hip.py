@@ -511,7 +511,7 @@ def bin_columns(values, cuts):
 # ------------------------------------------------------- fp64 block Gauss-Seidel ---
 # lda-c-faithful E-step (csrc/hip/lda_gs64.hip): double everywhere, gamma refreshed after every
 # chunk of ceil(n / gs_updates) words (documents of <= gs_updates words: lda-c's per-word schedule).
-GS_TINY, GS_TEAM1, GS_TEAM4, GS_TEAM16 = range(4)
+GS_TINY, GS_TEAM1, GS_TEAM4, GS_TEAM8 = range(4)
 
 
 def gs_umax() -> int:
@@ -522,7 +522,8 @@ def gs_tiny_max(KS: int) -> int:
     return int(lib().gs_tiny_max(int(KS)))
 
 
-def gs_estep(doc_ptr, word_idx, counts, order, beta, K, gs_updates, params, gamma, cphi, lik, alpha_ss, iters, variant):
+def gs_estep(doc_ptr, word_idx, counts, order, beta, K, gs_updates, params, gamma, cphi, lik, alpha_ss, iters, variant,
+             dbg=None):
     """One launch of the fp64 block Gauss-Seidel E-step over the documents in ``order``.
     ``params``: the device parameter block {alpha, lgamma constant, VAR_MAX_ITER, VAR_CONVERGED, done}."""
     D = doc_ptr.numel() - 1
@@ -534,7 +535,7 @@ def gs_estep(doc_ptr, word_idx, counts, order, beta, K, gs_updates, params, gamm
         raise ValueError("K out of range")
     if not (1 <= int(gs_updates) <= gs_umax()):
         raise ValueError(f"gs_updates must be in [1, {gs_umax()}]")
-    if variant not in (GS_TINY, GS_TEAM1, GS_TEAM4, GS_TEAM16):
+    if variant not in (GS_TINY, GS_TEAM1, GS_TEAM4, GS_TEAM8):
         raise ValueError(f"unknown gs variant {variant}")
     dev = beta.device
     args = [
@@ -549,7 +550,7 @@ def gs_estep(doc_ptr, word_idx, counts, order, beta, K, gs_updates, params, gamm
         _chk(lik, torch.float64, "lik", (D,), dev),
         _chk(alpha_ss, torch.float64, "alpha_ss", (D,), dev),
         _chk(iters, torch.int32, "iters", (D,), dev),
-        int(variant), _stream(),
+        int(variant), _stream(), 0 if dbg is None else _chk(dbg, torch.int64, "dbg", (8,), dev),
     ]
     if order.numel() == 0:
         return
@@ -612,8 +613,8 @@ class GSPlan:
     """Length buckets of the fp64 block Gauss-Seidel E-step: (variant, int32 doc order) per launch.
 
     tiny (TG lanes per document, literal schedule) for n <= min(gs_tiny_max(KS), U); one wave per
-    document up to 256 words; a 4-wave workgroup up to 2048; a 16-wave workgroup beyond."""
-    EDGES = ((GS_TEAM16, 2048, None), (GS_TEAM4, 256, 2048), (GS_TEAM1, None, 256))
+    document up to 256 words; a 4-wave workgroup up to 2048; an 8-wave workgroup beyond."""
+    EDGES = ((GS_TEAM8, 2048, None), (GS_TEAM4, 256, 2048), (GS_TEAM1, None, 256))
 
     def __init__(self, lengths, KS: int, gs_updates: int, device):
         import numpy as np

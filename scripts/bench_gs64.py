@@ -1,0 +1,95 @@
+#!/usr/bin/env python
+"""Per-bucket timing of the fp64 block Gauss-Seidel E-step (csrc/hip/lda_gs64.hip).
+
+Trains a few EM iterations on the synthetic 1-day netflow corpus (bench.py's headline corpus),
+then launches each length bucket alone (HIP events, median of repeats) and reports documents,
+lengths, sweeps and kernel time; plus suff-stats and the M-step.  ``--only VARIANT`` loops one
+bucket (for rocprofv3 --pmc runs of a single kernel).
+
+  python scripts/bench_gs64.py [--events N] [--topics K] [--gs-updates U] [--only tiny|team1|team4|team8]
+"""
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def timed(fn, reps=5):
+    ts = []
+    for _ in range(reps):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        fn()
+        b.record()
+        b.synchronize()
+        ts.append(a.elapsed_time(b))
+    return float(np.median(ts))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--events", type=int, default=1_000_000)
+    ap.add_argument("--topics", type=int, default=20)
+    ap.add_argument("--gs-updates", type=int, default=0)
+    ap.add_argument("--warm-em", type=int, default=4)
+    ap.add_argument("--only", default=None)
+    ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--phases", action="store_true", help="phase timer of the longest document of each team bucket")
+    a = ap.parse_args()
+    from oni_ml_amd.models.lda.em import LDAEngine
+    from oni_ml_amd.models.lda.settings import LDASettings
+    from oni_ml_amd.ops import hip as H
+    from oni_ml_amd.pipeline.flow import synthetic_flow_corpus
+    c, _ = synthetic_flow_corpus(events=a.events, seed=0, device="cuda")
+    st = LDASettings()
+    st.gs_updates = a.gs_updates
+    eng = LDAEngine(c, a.topics, st, backend="hip", seed=0, precision="fp64")
+    eng.init_random()
+    eng.em_iterations(a.warm_em, True, c.num_docs, stop=False)
+    torch.cuda.synchronize()
+    dc = eng.dc
+    lens = c.lengths()
+    its = eng.iters.cpu().numpy()
+    names = {H.GS_TINY: "tiny", H.GS_TEAM1: "team1", H.GS_TEAM4: "team4", H.GS_TEAM8: "team8"}
+    out = dict(docs=c.num_docs, nnz=c.nnz, U=eng._U, buckets=[])
+
+    def launch(var, order):
+        H.gs_estep(dc.doc_ptr, dc.word_idx, dc.counts, order, eng.beta, eng.K, eng._U, eng._params, eng.gamma,
+                   eng.cphi, eng.lik, eng.ass, eng.iters, var)
+
+    for var, order in eng.gs_plan.plan:
+        if a.only and names[var] != a.only:
+            continue
+        o = order.cpu().numpy()
+        L = lens[o]
+        ms = timed(lambda: launch(var, order), a.reps)
+        it = its[o]
+        out["buckets"].append(dict(kernel=names[var], docs=int(o.size), len_min=int(L.min()), len_max=int(L.max()),
+                                   entries=int(L.sum()), sweeps_mean=round(float(it.mean()), 2),
+                                   sweeps_max=int(it.max()), ms=round(ms, 4),
+                                   word_sweeps=int((L * it).sum())))
+        if a.phases and var != H.GS_TINY:
+            dbg = torch.zeros(8, dtype=torch.int64, device="cuda")
+            H.gs_estep(dc.doc_ptr, dc.word_idx, dc.counts, order, eng.beta, eng.K, eng._U, eng._params, eng.gamma,
+                       eng.cphi, eng.lik, eng.ass, eng.iters, var, dbg=dbg)
+            v = dbg.cpu().tolist()
+            ch = max(v[7], 1)
+            out["buckets"][-1]["phase_cycles_per_chunk"] = dict(
+                word=round(v[0] / ch), reduce=round(v[1] / ch), barrier1=round(v[2] / ch), topic=round(v[3] / ch),
+                barrier2=round(v[4] / ch), sweep_tail_total=v[5], chunks=v[7], doc_len=int(L.max()))
+        print(json.dumps(out["buckets"][-1]), flush=True)
+    if not a.only:
+        sp = eng.suff_plan
+        out["suff_ms"] = round(timed(lambda: H.gs_suff64(dc.word_ptr, dc.csc_ent, sp, eng.cphi, eng.cw,
+                                                         eng._suff_part, scalars=(eng.lik, eng.ass, 0, eng.D))), 4)
+        out["estep_graph_ms"] = round(timed(lambda: eng._launch_estep()), 4)
+        print(json.dumps({k: v for k, v in out.items() if k != "buckets"}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
