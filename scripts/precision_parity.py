@@ -1,15 +1,17 @@
 #!/usr/bin/env python
-"""Precision parity of the fp32 HIP E-step against fp64 engines on the headline bench corpus.
+"""Precision and schedule parity of the GPU engines against lda-c on the headline bench corpus.
 
-The reference core (oni-lda-c) computes in double.  The HIP engine
-keeps phi / gamma / E rows in fp32 and the likelihood, alpha_ss, class totals and the alpha
-Newton step in fp64.  This script trains the SAME corpus (bench.py's 1-day synthetic netflow,
-seed 0) from the SAME random init with three engines and compares what the pipeline consumes:
+The reference core (oni-lda-c) computes in double with a per-word
+Gauss-Seidel schedule.  This script trains the SAME corpus (bench.py's 1-day synthetic netflow,
+seed 0) from the SAME random init with several engines and compares what the pipeline consumes:
 
-  hip    fp32 Jacobi E-step (HIP kernels, the bench path)
+  hip    fp64 block Gauss-Seidel (HIP kernels, csrc/hip/lda_gs64.hip; the bench path): gamma
+         refreshed every ceil(n/32) words, lda-c's per-word schedule for documents <= 32 words
+  hip32  fp32 Jacobi E-step (HIP kernels, the opt-in fast mode)
   torch  fp64 Jacobi E-step (PyTorch on the host CPU, ops/reference.py)
   cpu    fp64 Gauss-Seidel E-step, a literal transcription of lda-c's lda_inference
          (csrc/native/lda_ref.cpp; the engine BASELINE.json's docs/s was measured with)
+  cpuU   the C++ engine with the GPU engine's block schedule (U = 32): the GPU engine's oracle
 
 Compared: per-EM-iteration likelihood, EM iterations to convergence, final alpha, the
 exported doc topics theta = gamma / sum(gamma) and word topics phi = softmax(log beta) rows
@@ -36,17 +38,21 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
-def _train(corpus, K, backend, dev, seed, var_max_iter=None):
+def _train(corpus, K, name, dev, seed, var_max_iter=None):
     from oni_ml_amd.models.lda.em import LDAEngine
     from oni_ml_amd.models.lda.settings import LDASettings
     st = LDASettings()
     if var_max_iter is not None:
         st.var_max_iter = var_max_iter
-    eng = LDAEngine(corpus, K, st, backend=backend, device=dev, seed=seed)
+    backend, precision = {"hip": ("hip", "fp64"), "hip32": ("hip", "fp32"), "torch": ("torch", "fp64"),
+                          "cpu": ("cpu", "fp64"), "cpuU": ("cpu", "fp64")}[name]
+    if name == "cpuU":
+        st.gs_updates = 32
+    eng = LDAEngine(corpus, K, st, backend=backend, device=dev, seed=seed, precision=precision)
     if dev.type == "cuda":
         torch.cuda.synchronize()
     t0 = time.perf_counter()
-    res = eng.run(start="random", on_iteration=lambda e, i, L, c: print(f"  {backend} it {i} L={L:.6f}", flush=True))
+    res = eng.run(start="random", on_iteration=lambda e, i, L, c: print(f"  {name} it {i} L={L:.6f}", flush=True))
     if dev.type == "cuda":
         torch.cuda.synchronize()
     sec = time.perf_counter() - t0
@@ -88,7 +94,7 @@ def main():
     ap.add_argument("--events", type=int, default=1_000_000)
     ap.add_argument("--topics", type=int, default=20)
     ap.add_argument("--seed", type=int, default=0)
-    ap.add_argument("--engines", default="hip,torch,cpu,cpu@1")
+    ap.add_argument("--engines", default="hip,cpu,cpuU,cpu@1,hip32")
     ap.add_argument("--var-max-iter", type=int, default=None, help="override settings.txt var max iter (20)")
     ap.add_argument("--json", default=None)
     ap.add_argument("--md", default=None)
@@ -101,10 +107,10 @@ def main():
 
     runs = {}
     for name in args.engines.split(","):
-        backend, _, seed = name.partition("@")        # "cpu@1": the cpu engine from another random init
+        eng_name, _, seed = name.partition("@")       # "cpu@1": the cpu engine from another random init
         # the fp64 PyTorch Jacobi engine runs on the host: its per-bucket launches make it slower on the GPU
-        d = dev if backend == "hip" else torch.device("cpu")
-        res, sec = _train(corpus, args.topics, backend, d, int(seed) if seed else args.seed, args.var_max_iter)
+        d = dev if eng_name.startswith("hip") else torch.device("cpu")
+        res, sec = _train(corpus, args.topics, eng_name, d, int(seed) if seed else args.seed, args.var_max_iter)
         runs[name] = dict(res=res, sec=sec)
         print(f"{name}: {res.em_iterations} EM iterations, {sec:.2f} s, L={res.likelihoods[-1][0]:.6f}, "
               f"alpha={res.alpha:.8f}", flush=True)
@@ -148,7 +154,7 @@ def main():
         ecols = ["seconds", "em_iterations", "final_likelihood", "alpha"]
         pcols = list(next(iter(out["pairs"].values())).keys()) if out["pairs"] else []
         fmt = lambda v: f"{v:.6g}" if isinstance(v, float) else str(v)
-        lines = ["# Precision parity: fp32 HIP E-step vs fp64 engines", "",
+        lines = ["# Precision / schedule parity: GPU engines vs lda-c (literal per-word Gauss-Seidel, fp64)", "",
                  f"Corpus: bench.py's 1-day synthetic netflow ({args.events} events, seed {args.seed}): "
                  f"{corpus.num_docs} docs, {corpus.num_terms} words, {len(corpus.word_idx)} entries; "
                  f"K = {args.topics}, lda-c default settings, same random init (seed {args.seed}). "

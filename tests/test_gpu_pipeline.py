@@ -31,7 +31,7 @@ def test_flow_words_kernel_bitwise(hip):
         assert torch.equal(g[k].cpu(), r[k]), k
 
 
-def _flow(tmp_path, backend, device, events=20000, topics=20):
+def _flow(tmp_path, backend, device, events=20000, topics=20, gs_updates=0):
     from oni_ml_amd.pipeline import run
     from oni_ml_amd.synth.flow import generate_flow_day
     if not (tmp_path / "in").exists():
@@ -40,17 +40,20 @@ def _flow(tmp_path, backend, device, events=20000, topics=20):
     cfg = CFG.resolve("20160122", "flow", tol=1e-4, conf_path=None, environ={}, lpath=str(lp),
                       flow_path=str(tmp_path / "in"), backend=backend, threads=4, verbose=False, topics=topics)
     cfg.settings = LDASettings(em_max_iter=6)
+    cfg.settings.gs_updates = gs_updates
     return run(cfg, device=device, log=lambda *a, **k: None), lp
 
 
 def test_flow_pipeline_gpu_matches_cpu_path(tmp_path):
+    """The whole flow pipeline on the GPU (fp64 block Gauss-Seidel engine) against the CPU path with
+    the C++ engine on the same schedule: identical corpus files, the same likelihood trajectory."""
     s_gpu, lg = _flow(tmp_path, "hip", "cuda")
-    s_cpu, lc = _flow(tmp_path, "torch", "cpu")
+    s_cpu, lc = _flow(tmp_path, "cpu", "cpu", gs_updates=32)
     for f in ("doc.dat", "words.dat", "model.dat"):   # featurization + corpus identical on both devices
         assert (lg / f).read_text() == (lc / f).read_text(), f
     Lg = [float(l.split()[0]) for l in (lg / "likelihood.dat").read_text().splitlines()]
     Lc = [float(l.split()[0]) for l in (lc / "likelihood.dat").read_text().splitlines()]
-    assert len(Lg) == len(Lc) and np.allclose(Lg, Lc, rtol=1e-3)
+    assert len(Lg) == len(Lc) and np.allclose(Lg, Lc, rtol=1e-9)
     fg = [l.split(",")[:27] for l in (lg / "flow_results.csv").read_text().splitlines()]
     fc = [l.split(",")[:27] for l in (lc / "flow_results.csv").read_text().splitlines()]
     sg, sc = set(map(tuple, fg)), set(map(tuple, fc))

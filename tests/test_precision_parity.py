@@ -2,8 +2,9 @@
 
 CPU: the two fp64 engines (PyTorch Jacobi, literal lda-c Gauss-Seidel) on a small synthetic day; the
 harness must report the pairwise metrics in range and write both outputs.
-GPU: the fp32 HIP engine against the fp64 Jacobi engine (same update schedule), which must agree to
-the tolerances the README quotes for the headline corpus (loosened for the small corpus)."""
+GPU: the fp64 HIP engine against the C++ engine with the same block schedule, and the fp32 HIP engine
+against the fp64 Jacobi engine (same update schedule), to the tolerances the README quotes for the
+headline corpus (loosened for the small corpus)."""
 import json
 import os
 import subprocess
@@ -33,12 +34,31 @@ def test_parity_harness_fp64_engines(tmp_path):
     assert 0.0 <= p["lowest_0p1pct_overlap"] <= 1.0
     for v in e.values():
         assert v["final_likelihood"] < 0 and v["alpha"] > 0 and len(v["likelihood_trajectory"]) == v["em_iterations"]
-    assert (tmp_path / "parity.md").read_text().startswith("# Precision parity")
+    assert (tmp_path / "parity.md").read_text().startswith("# Precision / schedule parity")
+
+
+def test_parity_harness_block_schedule_cpu(tmp_path):
+    """The C++ engine with the GPU engine's block schedule (cpuU) against literal lda-c (cpu): the
+    block schedule is the GPU engine's oracle, so its distance to lda-c is the GPU engine's."""
+    p = _run(tmp_path, "cpuU,cpu", 8000)["pairs"]["cpuU vs cpu"]
+    assert p["final_likelihood_rel_diff"] < 1e-3
+    assert p["alpha_rel_diff"] < 0.05
+
+
+@pytest.mark.gpu
+def test_fp64_hip_engine_tracks_block_oracle(tmp_path):
+    """fp64 GPU engine vs the C++ engine with the same block schedule: the same model, trained to
+    convergence (float64 on both sides)."""
+    p = _run(tmp_path, "hip,cpuU", 50000)["pairs"]["hip vs cpuU"]
+    assert p["likelihood_rel_diff_max"] < 1e-8
+    assert p["alpha_rel_diff"] < 1e-7
+    assert p["theta_doc_argmax_agree"] > 0.999
+    assert p["lowest_0p1pct_overlap"] > 0.99
 
 
 @pytest.mark.gpu
 def test_fp32_hip_engine_tracks_fp64_jacobi(tmp_path):
-    p = _run(tmp_path, "hip,torch", 50000)["pairs"]["hip vs torch"]
+    p = _run(tmp_path, "hip32,torch", 50000)["pairs"]["hip32 vs torch"]
     assert p["likelihood_rel_diff_max"] < 1e-5
     assert p["alpha_rel_diff"] < 1e-3
     assert p["theta_doc_argmax_agree"] > 0.99
