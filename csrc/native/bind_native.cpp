@@ -72,6 +72,14 @@ static std::vector<OutCol> build_cols(const py::list& spec, ColHolder& h, int64_
         c.width = (int)a.shape(1);
         if (a.shape(0) < n_rows_needed) throw std::invalid_argument("row column too short");
         c.text = t.size() > 2 ? t[2].cast<std::string>() : std::string(" ");
+        if (t.size() > 3 && !t[3].is_none()) {
+          // optional read-back target: a writable float64 array of the same shape
+          auto o = t[3].cast<py::array_t<double, py::array::c_style>>();
+          if (o.ndim() != 2 || o.shape(0) != a.shape(0) || o.shape(1) != a.shape(1))
+            throw std::invalid_argument("read-back array shape differs from the row column");
+          h.keep.push_back(o);
+          c.parsed = o.mutable_data();
+        }
       }
     } else if (kind == "int") {
       auto a = py::array_t<int64_t, py::array::c_style | py::array::forcecast>::ensure(t[1]);

@@ -1,6 +1,7 @@
 #include "table.h"
 
 #include <algorithm>
+#include <charconv>
 #include <cstdio>
 #include <cstring>
 #include <fstream>
@@ -251,10 +252,13 @@ static void format_row(std::string& out, int64_t r, const std::vector<OutCol>& c
       case OutCol::kPy2Row:
       case OutCol::kFixedRow: {
         const double* row = k.f64 + (size_t)r * k.width;
+        double* back = k.parsed ? k.parsed + (size_t)r * k.width : nullptr;
         for (int j = 0; j < k.width; ++j) {
           if (j) out += k.text;
+          const size_t at = out.size();
           if (k.kind == OutCol::kPy2Row) append_py2_float(out, row[j]);
           else append_fixed10(out, row[j]);
+          if (back) std::from_chars(out.data() + at, out.data() + out.size(), back[j]);
         }
         break;
       }

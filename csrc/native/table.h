@@ -94,6 +94,9 @@ struct OutCol {
   const std::vector<std::string>* names = nullptr;
   std::string text;                     // kConst, or the separator inside a row for kPy2Row/kFixedRow
   int width = 0;                        // kPy2Row / kFixedRow
+  double* parsed = nullptr;             // kPy2Row / kFixedRow, optional [n][width]: each printed value read
+                                        // back (strtod of its own text), so a reader's view of the file
+                                        // comes with the write instead of a second format pass
 };
 
 // Writes one line per entry of `order` (row indices), columns joined by sep.

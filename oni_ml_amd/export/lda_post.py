@@ -59,32 +59,42 @@ def check_strict_k(K: int, strict: bool):
         raise ValueError("compat=strict reproduces lda_post.py's hard-coded 20 topics; use compat=fixed for K != 20")
 
 
-def write_doc_results(path: str, doc_names: Sequence[str], theta: np.ndarray, threads: int = 8) -> int:
-    n = len(doc_names)
-    if theta.shape[0] != n:
-        raise ValueError("doc names / theta rows differ")
-    return native.lib().write_rows(path, None, [("dict", list(doc_names), np.arange(n, dtype=np.int32)),
-                                                ("py2row", np.ascontiguousarray(theta, np.float64), " ")],
-                                   threads=threads, n=n)
+def _write_table(path, names, values, threads, read_back):
+    n = len(names)
+    if values.shape[0] != n:
+        raise ValueError("names / value rows differ")
+    vals = np.ascontiguousarray(values, np.float64)
+    back = np.empty_like(vals) if read_back else None
+    kw = {"threads": threads} if threads > 0 else {}     # 0: the writer's default (hardware, <= 16)
+    native.lib().write_rows(path, None, [("dict", list(names), np.arange(n, dtype=np.int32)),
+                                         ("py2row", vals, " ", back)], n=n, **kw)
+    return back
 
 
-def write_word_results(path: str, word_names: Sequence[str], phi: np.ndarray, threads: int = 8) -> int:
-    n = len(word_names)
-    if phi.shape[0] != n:
-        raise ValueError("word names / phi rows differ")
-    return native.lib().write_rows(path, None, [("dict", list(word_names), np.arange(n, dtype=np.int32)),
-                                                ("py2row", np.ascontiguousarray(phi, np.float64), " ")],
-                                   threads=threads, n=n)
+def write_doc_results(path: str, doc_names: Sequence[str], theta: np.ndarray, threads: int = 0,
+                      read_back: bool = False):
+    """``read_back``: also return the values as a reader parses them from the file (the Python-2 str
+    text read back with strtod) -- the scorers' view, produced by the same formatting pass."""
+    return _write_table(path, doc_names, theta, threads, read_back)
 
 
-def export(doc_names, gamma, word_names, log_beta, doc_path, word_path, strict=True) -> Tuple[np.ndarray, np.ndarray, list]:
-    """Write both files; returns (θ, φ, word keys as written) as the scorers will read them back."""
+def write_word_results(path: str, word_names: Sequence[str], phi: np.ndarray, threads: int = 0,
+                       read_back: bool = False):
+    return _write_table(path, word_names, phi, threads, read_back)
+
+
+def export(doc_names, gamma, word_names, log_beta, doc_path, word_path, strict=True,
+           read_back: bool = False) -> Tuple[np.ndarray, np.ndarray, list]:
+    """Write both files; returns (θ, φ, word keys as written).  ``read_back``: θ / φ as the scorers
+    parse them from the files (each value's own text read back, same pass as the write)."""
     check_strict_k(gamma.shape[1], strict)
     theta = doc_topics(gamma, strict)
     phi = word_topics(log_beta, strict)
     wnames = truncate_s20(word_names) if strict else list(word_names)
-    write_doc_results(doc_path, doc_names, theta)
-    write_word_results(word_path, wnames, phi)
+    th_b = write_doc_results(doc_path, doc_names, theta, read_back=read_back)
+    ph_b = write_word_results(word_path, wnames, phi, read_back=read_back)
+    if read_back:
+        return th_b, ph_b, wnames
     return theta, phi, wnames
 
 

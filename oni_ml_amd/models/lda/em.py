@@ -131,10 +131,15 @@ class LDAEngine:
     def __init__(self, corpus: Corpus, num_topics: int, settings: Optional[LDASettings] = None,
                  alpha_init: float = 2.5, backend: str = "auto", device=None, dist=None, seed: int = 0,
                  streams: int = 4, local_shard: bool = False, split_docs: bool = True,
-                 split_min: Optional[int] = 4096, use_graph: bool = True, precision: str = "fp64"):
+                 split_min: Optional[int] = 4096, use_graph: bool = True, precision: str = "fp64",
+                 emulate_shards: int = 0):
         """precision (hip backend): "fp64" = lda-c arithmetic with the block Gauss-Seidel schedule
-        (lda_gs64.hip, the default); "fp32" = the fp32 Jacobi engine (opt-in fast mode)."""
+        (lda_gs64.hip, the default); "fp32" = the fp32 Jacobi engine (opt-in fast mode).
+        emulate_shards (torch backend, one process): reduce the sufficient statistics as N
+        nnz-balanced document shards summed in shard order -- bitwise the N-rank run under
+        ONI_DIST_DETERMINISTIC=1 (parallel/dist.py)."""
         self.settings = settings or LDASettings()
+        self.emulate_shards = int(emulate_shards)
         if precision not in ("fp64", "fp32"):
             raise ValueError(f"precision must be fp64 or fp32, got {precision!r}")
         self.precision = precision
@@ -385,7 +390,8 @@ class LDAEngine:
         if d is None or d.world_size <= 1 or self.backend == "cpu":
             return None
         mode = os.environ.get("ONI_DIST_EXCHANGE", "auto")
-        if mode == "dense":
+        if mode == "dense" or getattr(d, "deterministic", False):
+            # deterministic mode: one ordered reduction of the whole matrix (parallel/dist.py)
             return None
         from ...parallel.dist import VocabExchange
         words = np.unique(corpus.word_idx) if corpus.nnz else np.zeros(0, np.int64)
@@ -488,6 +494,8 @@ class LDAEngine:
             self.gamma = out["gamma"]
             self.iters = out["iters"]
             self.lik = out["lik"]
+            if self.emulate_shards > 1:
+                return self._emulated_shard_stats(out)
             self.cw = R.suffstats(self.t_doc_ptr, self.t_word, out["e"], out["r"], self.beta, self.V, self.K)
             return torch.stack([out["lik"].sum(), out["alpha_ss"].sum()])
         # cpu: lda-c Gauss-Seidel reference (C++)
@@ -501,6 +509,23 @@ class LDAEngine:
         self.lik = torch.from_numpy(res["doc_likelihood"])
         self.cw = torch.from_numpy(np.ascontiguousarray(res["class_word"].T))
         return torch.tensor([res["likelihood"], res["alpha_ss"]], dtype=torch.float64)
+
+    def _emulated_shard_stats(self, out):
+        """class_word and [likelihood, alpha_ss] as N ranks would produce them (each shard's own
+        statistics on freshly allocated tensors, then 0 + s_0 + s_1 + ... in shard order)."""
+        from ...ops import reference as R
+        from ...parallel.dist import shard_bounds
+        ptr = self.corpus.doc_ptr
+        cw = torch.zeros(self.V, self.K, dtype=torch.float64, device=self.device)
+        sc = torch.zeros(2, dtype=torch.float64, device=self.device)
+        for d0, d1 in shard_bounds(ptr, self.emulate_shards):
+            e0, e1 = int(ptr[d0]), int(ptr[d1])
+            lp = (self.t_doc_ptr[d0:d1 + 1] - self.t_doc_ptr[d0]).clone()
+            cw += R.suffstats(lp, self.t_word[e0:e1].clone(), out["e"][d0:d1].clone(), out["r"][e0:e1].clone(),
+                              self.beta, self.V, self.K)
+            sc += torch.stack([out["lik"][d0:d1].clone().sum(), out["alpha_ss"][d0:d1].clone().sum()])
+        self.cw = cw
+        return sc
 
     def _e_step_hip(self):
         """One E-step on the GPU.  The launch sequence (all buckets on their streams, suff-stats,

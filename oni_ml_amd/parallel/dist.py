@@ -32,6 +32,11 @@ class DistContext:
     local_rank: int = 0
     device: torch.device = torch.device("cpu")
     backend: str = "none"
+    # ONI_DIST_DETERMINISTIC=1: sufficient statistics are reduced by all-gather + a sum in rank order
+    # (0 + s_0 + s_1 + ...), the order a single process emulating the same shards uses
+    # (LDAEngine(emulate_shards=N)), so an N-rank run is bitwise equal to that single-process run.
+    # The default ring all-reduce is bitwise identical on every rank but its association differs.
+    deterministic: bool = False
 
     @property
     def initialized(self) -> bool:
@@ -47,10 +52,53 @@ class DistContext:
             return scalars
         import torch.distributed as td
 
+        if self.deterministic:
+            self.ordered_allreduce(scalars)
+            self.ordered_allreduce(cw)
+            return scalars
         work = td.all_reduce(scalars, async_op=True)
         td.all_reduce(cw)
         work.wait()
         return scalars
+
+    def ordered_allreduce(self, t: torch.Tensor) -> torch.Tensor:
+        """In place: t <- 0 + t_0 + t_1 + ... + t_{N-1} (rank order) on every rank."""
+        import torch.distributed as td
+
+        parts = [torch.empty_like(t) for _ in range(self.world_size)]
+        td.all_gather(parts, t.contiguous())
+        acc = torch.zeros_like(t)
+        for p in parts:
+            acc += p
+        t.copy_(acc)
+        return t
+
+    def self_check(self):
+        """Start-up check of the collective path (RCCL on GPUs): an all-reduce, a device-scoped barrier
+        and an all_to_all_single with known answers.  Raises with the backend and device named, instead
+        of letting the first EM iteration hang or return garbage."""
+        if not self.initialized:
+            return
+        import torch.distributed as td
+
+        dev = self._coll_device()
+        N, r = self.world_size, self.rank
+        try:
+            x = torch.full((4,), float(r + 1), dtype=torch.float64, device=dev)
+            td.all_reduce(x)
+            want = N * (N + 1) / 2
+            if not bool((x == want).all()):
+                raise RuntimeError(f"all_reduce returned {x.tolist()}, expected {want}")
+            self.barrier()
+            send = torch.arange(N, dtype=torch.float64, device=dev) + 100.0 * r
+            recv = torch.empty_like(send)
+            td.all_to_all_single(recv, send)
+            exp = torch.arange(N, dtype=torch.float64, device=dev) * 100.0 + r
+            if not torch.equal(recv, exp):
+                raise RuntimeError(f"all_to_all_single returned {recv.tolist()}, expected {exp.tolist()}")
+        except Exception as e:
+            raise RuntimeError(f"collective self-check failed on rank {r}/{N} (backend {self.backend}, "
+                               f"device {dev}): {e}") from e
 
     def allreduce_int(self, v: int) -> int:
         if not self.initialized:
@@ -318,7 +366,8 @@ def init_from_env(expected_world: int = None, backend: str = None, timeout_s: fl
         dev = torch.device("cuda", local % max(1, torch.cuda.device_count()))
     else:
         dev = torch.device("cpu")
-    ctx = DistContext(rank=rank, world_size=world, local_rank=local, device=dev, backend=backend)
+    ctx = DistContext(rank=rank, world_size=world, local_rank=local, device=dev, backend=backend,
+                      deterministic=os.environ.get("ONI_DIST_DETERMINISTIC", "0") == "1")
     if world > 1:
         import torch.distributed as td
 
@@ -328,4 +377,6 @@ def init_from_env(expected_world: int = None, backend: str = None, timeout_s: fl
         if backend == "nccl":
             kw["device_id"] = dev
         td.init_process_group(**kw)
+        if os.environ.get("ONI_DIST_SELFCHECK", "1") != "0":
+            ctx.self_check()
     return ctx

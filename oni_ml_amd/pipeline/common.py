@@ -57,10 +57,12 @@ def run_lda(cfg, corpus: Corpus, dist=None, device=None, log=print):
                     defer_files=dist is None or dist.world_size <= 1)
 
 
-def run_export(cfg, doc_names, gamma, word_names, log_beta) -> ModelTables:
+def run_export(cfg, doc_names, gamma, word_names, log_beta, read_back: bool = False) -> ModelTables:
+    """``read_back``: the tables as the scorers parse the files (what ``strict_tables`` computes, but
+    from the writer's own formatting pass instead of a second one)."""
     th, ph, wn = lda_post.export(doc_names, gamma, word_names, log_beta,
                                  os.path.join(cfg.lpath, "doc_results.csv"),
-                                 os.path.join(cfg.lpath, "word_results.csv"), strict=cfg.strict)
+                                 os.path.join(cfg.lpath, "word_results.csv"), strict=cfg.strict, read_back=read_back)
     return ModelTables(list(doc_names), th, wn, ph)
 
 

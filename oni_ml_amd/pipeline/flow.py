@@ -106,7 +106,7 @@ def run(cfg, dist=None, device=None, log=print) -> dict:
                 from ..models.lda.estimate import load_final
                 gamma, log_beta = load_final(cfg.lpath)
             with R.stage("lda_post") as res:
-                tables = C.strict_tables(C.run_export(cfg, doc_names, gamma, word_names, log_beta), cfg.strict)
+                tables = C.run_export(cfg, doc_names, gamma, word_names, log_beta, read_back=True)
         else:
             R.skip("lda_post")
             tables = C.load_model_tables(cfg.lpath)

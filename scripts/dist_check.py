@@ -38,7 +38,7 @@ def main():
     c = shifted_vocab(planted_corpus(num_docs=3000, num_terms=2000, num_topics=8, mean_tokens=40, tail=1.0,
                                      max_tokens=20_000, seed=4))
     eng = LDAEngine(c, K, LDASettings(em_max_iter=6), backend="hip", dist=ctx if ctx.world_size > 1 else None,
-                    seed=3)
+                    seed=3, precision=os.environ.get("DIST_CHECK_PRECISION", "fp64"))
     res = eng.run()
     lb = eng.log_beta()
     g = eng.gather_gamma()
@@ -47,7 +47,8 @@ def main():
                               rows=None if eng._xchg is None else eng._xchg.rows,
                               likelihoods=[x[0] for x in res.likelihoods], alpha=eng.alpha,
                               beta_sum=float(np.exp(lb).sum()), beta_checksum=float((lb * np.arange(lb.shape[1])).sum()),
-                              gamma_sum=float(g.sum()), gamma_shape=list(g.shape))), flush=True)
+                              gamma_sum=float(g.sum()), gamma_shape=list(g.shape), precision=eng.precision)),
+              flush=True)
     ctx.shutdown()
 
 

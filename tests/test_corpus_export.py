@@ -112,3 +112,24 @@ def test_strict_requires_20_topics():
     with pytest.raises(ValueError):
         lda_post.check_strict_k(10, True)
     lda_post.check_strict_k(10, False)
+
+
+def test_export_read_back_equals_text_roundtrip(tmp_path):
+    """lda_post export with read_back: the values handed to the scorers equal the files parsed back
+    (Python-2 str text -> strtod), bit for bit, and the files are unchanged by the option."""
+    from oni_ml_amd.export import lda_post
+    from oni_ml_amd.ops import native
+    rng = np.random.default_rng(3)
+    g = rng.random((300, 20)) * 50
+    lb = np.log(rng.random((20, 700)) / 700)
+    dn = [f"10.0.{i // 256}.{i % 256}" for i in range(300)]
+    wn = [f"{i}_80_1_2_3" for i in range(700)]
+    th, ph, _ = lda_post.export(dn, g, wn, lb, str(tmp_path / "d.csv"), str(tmp_path / "w.csv"), read_back=True)
+    d1, w1 = (tmp_path / "d.csv").read_text(), (tmp_path / "w.csv").read_text()
+    th0, ph0, _ = lda_post.export(dn, g, wn, lb, str(tmp_path / "d.csv"), str(tmp_path / "w.csv"))
+    assert (tmp_path / "d.csv").read_text() == d1 and (tmp_path / "w.csv").read_text() == w1
+    N = native.lib()
+    assert np.array_equal(th, N.roundtrip_py2(np.ascontiguousarray(th0)))
+    assert np.array_equal(ph, N.roundtrip_py2(np.ascontiguousarray(ph0)))
+    _, tv = lda_post.read_results(str(tmp_path / "d.csv"))
+    assert np.array_equal(tv, th)

@@ -21,8 +21,9 @@ def _port():
     return p
 
 
-def _run(world, exchange, overlap="1"):
-    env = dict(os.environ, ONI_DIST_EXCHANGE=exchange, ONI_DIST_BACKEND="gloo", ONI_DIST_OVERLAP=overlap)
+def _run(world, exchange, overlap="1", precision="fp64"):
+    env = dict(os.environ, ONI_DIST_EXCHANGE=exchange, ONI_DIST_BACKEND="gloo", ONI_DIST_OVERLAP=overlap,
+               DIST_CHECK_PRECISION=precision)
     if world == 1:
         cmd = [sys.executable, "scripts/dist_check.py"]
     else:
@@ -49,6 +50,26 @@ def test_two_rank_hip_exchanges_match_single_rank():
         assert o["gamma_shape"] == one["gamma_shape"]
         assert abs(o["gamma_sum"] - one["gamma_sum"]) / one["gamma_sum"] < 1e-5
         assert abs(o["beta_checksum"] - one["beta_checksum"]) / abs(one["beta_checksum"]) < 1e-5
+
+
+@pytest.mark.parametrize("exchange", ["dense", "sparse"])
+def test_four_rank_fp64_engine_matches_single_rank(exchange):
+    """The fp64 block Gauss-Seidel engine on 4 ranks (one GPU, gloo): per-document E-steps are
+    shard-independent, so only the order of the cross-rank sums differs from one rank."""
+    one = _run(1, "auto")
+    four = _run(4, exchange)
+    assert four["world"] == 4 and four["precision"] == "fp64"
+    assert len(four["likelihoods"]) == len(one["likelihoods"])
+    assert np.allclose(four["likelihoods"], one["likelihoods"], rtol=1e-10, atol=0)
+    assert abs(four["alpha"] - one["alpha"]) / one["alpha"] < 1e-9
+    assert abs(four["gamma_sum"] - one["gamma_sum"]) / one["gamma_sum"] < 1e-10
+    assert abs(four["beta_checksum"] - one["beta_checksum"]) / abs(one["beta_checksum"]) < 1e-10
+
+
+def test_two_rank_fp32_engine_matches_single_rank():
+    one = _run(1, "auto", precision="fp32")
+    two = _run(2, "sparse", precision="fp32")
+    assert np.allclose(two["likelihoods"], one["likelihoods"], rtol=2e-6)
 
 
 def test_rows_accumulate_kernel_matches_rank_order_sum():
