@@ -60,6 +60,7 @@ PYBIND11_MODULE(_onihip, m) {
 
   m.def("split_segment_words", [](int KS) { return oni::split_segment_words(KS); });
   m.def("split_max_blocks", []() { return oni::kSplitMaxBlocks; });
+  m.def("split_capacity", [](int KS, bool wide) { return wide ? oni::wsplit_capacity(KS) : oni::split_capacity(KS); });
   m.def("block_words", [](int KS, int waves) { return oni::block_words(KS, waves); });
   m.def("wide_words", [](int KS, int lanes) { return oni::wide_words(KS, lanes); });
   m.def("wide_slots", [](int KS, int lanes) { return oni::wide_slots(KS, lanes); });

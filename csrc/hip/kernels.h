@@ -97,6 +97,11 @@ void launch_lda_estep_wsplit(const EStepArgs& a, const SplitArgs& s, int KS, hip
 int wide_words(int KS, int lanes);  // register-cached words of a wide kernel with `lanes` lanes per doc
 int wide_slots(int KS, int lanes);  // word slots (lanes / topic-group width) of a wide kernel
 int split_segment_words(int KS);   // words one split workgroup keeps in registers
+// Co-resident capacity of the split kernels on this device: occupancy-API workgroups per CU x CUs.
+// The host sizes split launches to min(kSplitMaxBlocks, 3/4 of it) (ops/hip.py SplitPlan): the
+// per-iteration cross-workgroup exchange needs every segment of a launch resident at once.
+int split_capacity(int KS);
+int wsplit_capacity(int KS);
 int block_words(int KS, int waves); // register-cached words of a 4- or 8-wave document workgroup
 
 // ------------------------------------------------------------ suff stats ---

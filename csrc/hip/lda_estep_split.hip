@@ -296,6 +296,30 @@ static void split_ks(const EStepArgs& a, const SplitArgs& s, hipStream_t st) {
 }
 
 int split_segment_words(int KS) { return kNT * rows_per_lane_8w(KS); }
+
+// Workgroups of the split kernel the device can hold at once (occupancy API x CU count).
+template <int KS>
+static int split_capacity_ks() {
+  int dev = 0, per_cu = 0;
+  hipDeviceProp_t p;
+  ONI_HIP_CHECK(hipGetDevice(&dev));
+  ONI_HIP_CHECK(hipGetDeviceProperties(&p, dev));
+  ONI_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(
+      &per_cu, reinterpret_cast<const void*>(&lda_estep_split<KS, rows_per_lane_8w(KS)>), kNT, 0));
+  return per_cu * p.multiProcessorCount;
+}
+
+int split_capacity(int KS) {
+  switch (KS) {
+#define ONI_KS(X) \
+  case X:         \
+    return split_capacity_ks<X>();
+    ONI_FOR_EACH_KS(ONI_KS)
+#undef ONI_KS
+    default:
+      throw std::runtime_error("split_capacity: unsupported KS " + std::to_string(KS));
+  }
+}
 int block_words(int KS, int waves) { return waves * 64 * (waves == 8 ? rows_per_lane_8w(KS) : rows_per_lane_4w(KS)); }
 
 void launch_lda_estep_split(const EStepArgs& a, const SplitArgs& s, int KS, hipStream_t st) {

@@ -694,6 +694,29 @@ void wsplit_ks(const EStepArgs& a, const SplitArgs& sp, hipStream_t st) {
 }  // namespace
 
 int wide_words(int KS, int lanes) { return (lanes / wide_tg(KS)) * wide_cw(KS); }
+
+template <int KS>
+static int wsplit_capacity_ks() {
+  int dev = 0, per_cu = 0;
+  hipDeviceProp_t p;
+  ONI_HIP_CHECK(hipGetDevice(&dev));
+  ONI_HIP_CHECK(hipGetDeviceProperties(&p, dev));
+  ONI_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(
+      &per_cu, reinterpret_cast<const void*>(&lda_estep_wsplit<KS, wide_tg(KS), kLongCW, kLongUNR>), kWNT, 0));
+  return per_cu * p.multiProcessorCount;
+}
+
+int wsplit_capacity(int KS) {
+  switch (KS) {
+#define ONI_KS(X) \
+  case X:         \
+    return wsplit_capacity_ks<X>();
+    ONI_FOR_EACH_WIDE_KS(ONI_KS)
+#undef ONI_KS
+    default:
+      throw std::runtime_error("wsplit_capacity: unsupported KS " + std::to_string(KS));
+  }
+}
 int wide_slots(int KS, int lanes) { return lanes / wide_tg(KS); }
 
 void launch_lda_estep_wide(const EStepArgs& a, int variant, int KS, hipStream_t s) {

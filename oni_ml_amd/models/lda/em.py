@@ -272,6 +272,64 @@ class LDAEngine:
             self._suff_part = torch.zeros(nb, 2 + self.KS, dtype=torch.float64, device=self.device)
             self._graph_a = self._graph_b = None
 
+    # ------------------------------------------------------------ metrics
+    def _comm_begin(self):
+        if self.device.type == "cuda":
+            ev = torch.cuda.Event(enable_timing=True)
+            ev.record()
+            return ("cuda", ev)
+        return ("host", time.perf_counter())
+
+    def _comm_end(self, tok):
+        if not hasattr(self, "_comm_events"):
+            self._comm_events, self._comm_host_s, self._comm_iters = [], 0.0, 0
+        self._comm_iters += 1
+        if tok[0] == "cuda":
+            ev = torch.cuda.Event(enable_timing=True)
+            ev.record()
+            self._comm_events.append((tok[1], ev))
+        else:
+            self._comm_host_s += time.perf_counter() - tok[1]
+
+    def comm_seconds(self) -> float:
+        """Time of the cross-rank reductions so far (stream time from issue to the compute stream's
+        wait on them; host time for CPU collectives)."""
+        if not hasattr(self, "_comm_events"):
+            return 0.0
+        t = self._comm_host_s
+        if self._comm_events:
+            torch.cuda.synchronize(self.device)
+            t += sum(a.elapsed_time(b) for a, b in self._comm_events) / 1e3
+        return t
+
+    def exchange_bytes_per_iteration(self) -> int:
+        """Payload this rank hands to the collectives every EM iteration (class_word rows + scalars)."""
+        if self.dist is None or self.dist.world_size <= 1:
+            return 0
+        el = self.cw.element_size()
+        scal = (2 + self.KS) * 8
+        if self._xchg is not None:
+            return int(self._xchg.rows * self._xchg.width * el + scal)
+        return int(self.cw.numel() * el + scal)
+
+    def metrics(self, seconds: Optional[float] = None, em_iterations: Optional[int] = None) -> dict:
+        """Run metrics for metrics.jsonl / lda_stats.json: peak HBM, exchange payload and
+        time per EM iteration, the variational-iteration histogram of the last E-step, docs/s."""
+        it = self.iters.cpu().numpy() if isinstance(self.iters, torch.Tensor) else np.asarray(self.iters)
+        hist = np.bincount(it.astype(np.int64)).tolist() if it.size else []
+        out = dict(schedule=self.schedule, exchange=self.exchange_mode,
+                   exchange_bytes_per_iter=self.exchange_bytes_per_iteration(),
+                   var_iter_hist=hist, var_iter_mean=float(it.mean()) if it.size else 0.0,
+                   var_iter_max=int(it.max()) if it.size else 0)
+        n = getattr(self, "_comm_iters", 0)
+        out["exchange_seconds_per_iter"] = self.comm_seconds() / n if n else 0.0
+        if self.device.type == "cuda":
+            out["peak_hbm_bytes"] = int(torch.cuda.max_memory_allocated(self.device))
+            out["hbm_total_bytes"] = int(torch.cuda.get_device_properties(self.device).total_memory)
+        if seconds and em_iterations:
+            out["docs_per_sec"] = self.global_docs * em_iterations / seconds
+        return out
+
     @property
     def schedule(self) -> str:
         """Variational update schedule of this engine (bench / metrics records)."""
@@ -663,6 +721,7 @@ class LDAEngine:
             if self._xchg is not None:
                 import torch.distributed as td
                 red = torch.cat([sc.to(torch.float64), self.cw.sum(0, dtype=torch.float64)])
+                tok = self._comm_begin()
                 work = td.all_reduce(red, async_op=True)
                 local = self.cw
                 self._xchg.pack(local)
@@ -670,6 +729,7 @@ class LDAEngine:
                 self.cw = torch.zeros_like(local)     # rows of other ranks' words stay 0 (global_rows masks)
                 self._xchg.accumulate(self.cw, local)
                 work.wait()
+                self._comm_end(tok)
                 host = red[:2].cpu().tolist()
                 self.class_total = red[2:].clone()
                 self._mstep_beta()
@@ -677,7 +737,9 @@ class LDAEngine:
                     self.alpha = special.opt_alpha(float(host[1]), num_docs, self.K)
                 return float(host[0]), float(host[1])
             if self.dist is not None and self.dist.world_size > 1:
+                tok = self._comm_begin()
                 sc = self.dist.allreduce_suffstats(self.cw, sc)
+                self._comm_end(tok)
             host = sc.cpu().tolist()
             self.m_step(estimate_alpha, float(host[1]), num_docs)
             return float(host[0]), float(host[1])
@@ -780,6 +842,7 @@ class LDAEngine:
                     self._fgraph.replay()
             elif self._overlap:
                 self._run_phase("A")
+                tok = self._comm_begin()
                 work = self._xchg.exchange(async_op=True)      # shared rows in flight ...
                 self._run_phase("B")                           # ... while the private rows are computed
                 import torch.distributed as td
@@ -787,6 +850,7 @@ class LDAEngine:
                 if work is not None:
                     work.wait()
                 w2.wait()
+                self._comm_end(tok)
                 if not self.use_graph:
                     self._launch_mstep(*key)
                 elif self._mgraph_key != key:
@@ -801,7 +865,9 @@ class LDAEngine:
                     self._graph.replay()
                 else:
                     self._launch_estep()
+                tok = self._comm_begin()
                 self._reduce_stats()
+                self._comm_end(tok)
                 if not self.use_graph:
                     self._launch_mstep(*key)
                 elif self._mgraph_key != key:
@@ -827,6 +893,9 @@ class LDAEngine:
         recs = [(r[0], r[1], r[2], int(r[3]), r[4]) for r in rows]
         if any(r[0] != r[0] for r in recs):
             self._check_split_error()
+            bad = next(i for i, r in enumerate(recs) if r[0] != r[0])
+            raise RuntimeError(f"EM iteration {bad + 1} of the batch produced a NaN likelihood "
+                               f"(schedule: {self.schedule})")
         if recs:
             self.alpha, self.var_max_iter = recs[-1][2], recs[-1][3]
         self._pushed = (self.alpha, self.var_max_iter)

@@ -202,6 +202,7 @@ def estimate(corpus: Corpus, num_topics: int, alpha_init: float, settings: LDASe
         with open(os.path.join(outdir, "lda_stats.json"), "w") as f:
             json.dump(dict(em_iterations=res.em_iterations, seconds=res.seconds, alpha=res.alpha,
                            backend=eng.backend, docs=corpus.num_docs, terms=corpus.num_terms, nnz=corpus.nnz,
+                           metrics=eng.metrics(res.seconds, res.em_iterations),
                            per_iter=[s.__dict__ for s in res.stats]), f)
     res.engine = eng
     return res

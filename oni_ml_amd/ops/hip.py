@@ -122,6 +122,18 @@ def lda_estep(doc_ptr, word_idx, counts, order, beta, K, alpha, lik_const, var_m
     lib().lda_estep(*args)
 
 
+def split_launch_cap(KS: int, wide: bool) -> int:
+    """Workgroups per split launch: min(kSplitMaxBlocks, 3/4 of the device's co-resident capacity from
+    the occupancy API), so the segments of a launch are resident together with room for the other
+    streams' buckets; ONI_SPLIT_MAX_BLOCKS lowers it (tests, shared / partitioned GPUs)."""
+    L = lib()
+    cap = min(int(L.split_max_blocks()), max(1, int(L.split_capacity(int(KS), bool(wide))) * 3 // 4))
+    env = os.environ.get("ONI_SPLIT_MAX_BLOCKS")
+    if env:
+        cap = max(1, min(cap, int(env)))
+    return cap
+
+
 class SplitPlan:
     """Launch batches for the split-document E-step (huge documents over several workgroups).
 
@@ -130,8 +142,8 @@ class SplitPlan:
 
     def __init__(self, doc_ids, doc_ptr_host, KS: int, device, wide: bool = False, seg_words: int = None):
         L = lib()
-        self.max_blocks = int(L.split_max_blocks())
         self.wide = bool(wide)
+        self.max_blocks = split_launch_cap(KS, self.wide)
         # narrow kernel: a segment is exactly its register cache; wide kernel: any size
         # (the first wide_words(KS, 512) words in registers, the rest streamed)
         self.seg_words = int(L.split_segment_words(KS))

@@ -73,6 +73,10 @@ def run(cfg, dist=None, device=None, log=print) -> dict:
             lres = C.run_lda(cfg, corpus, dist=dist, device=device, log=log)
             res["_defer"] = lres.close_files   # LAG / final model files: written while later stages run
             res.update(em_iterations=lres.em_iterations, alpha=lres.alpha)
+            m = lres.engine.metrics(lres.seconds, lres.em_iterations)
+            res.update({k: v for k, v in m.items() if not isinstance(v, list)})
+            R.emit(dict(stage="lda_detail", var_iter_hist=m["var_iter_hist"], **{k: v for k, v in m.items()
+                                                                                   if not isinstance(v, list)}))
             summary["lda"] = dict(em_iterations=lres.em_iterations, seconds=lres.seconds, alpha=lres.alpha,
                                   likelihood=lres.likelihoods[-1][0] if lres.likelihoods else None)
         gamma, log_beta = lres.gamma, lres.log_beta

@@ -11,7 +11,8 @@ import pytest
 import torch
 import torch.multiprocessing as mp
 
-from test_dist import _free_port, _run
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from test_dist import _free_port, _run  # noqa: E402
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
@@ -30,6 +31,9 @@ def test_world_n_em_matches_single_rank(tmp_path, world, exchange):
     gn = np.loadtxt(tmp_path / f"w{world}" / "final.gamma")
     assert g1.shape == gn.shape and np.allclose(g1, gn, rtol=1e-6)
     assert np.allclose(one[0][5], many[0][5], rtol=1e-9, atol=1e-12)
+    m = json.load(open(tmp_path / f"w{world}" / "lda_stats.json"))["metrics"]
+    assert m["exchange_bytes_per_iter"] > 0 and m["exchange_seconds_per_iter"] > 0
+    assert m["exchange"] == ("dense-allreduce" if exchange == "dense" else "sparse-alltoall")
     parts = np.concatenate([np.atleast_2d(np.loadtxt(tmp_path / f"w{world}" / f"{r}.gamma"))
                             for r in range(world) if (tmp_path / f"w{world}" / f"{r}.gamma").stat().st_size])
     assert np.allclose(parts, gn, atol=1e-9)

@@ -338,3 +338,27 @@ def test_alpha_newton_device_matches_host(K):
         a = float(out.item())
         assert a == pytest.approx(host, rel=1e-9), (astar, a, host)
         assert float(params[1].item()) == pytest.approx(special.lik_const(a, K), rel=1e-9, abs=1e-9)
+
+
+def test_split_launch_cap_from_occupancy(hip, monkeypatch):
+    """Split launches are sized from the occupancy API (co-residency of every segment of a launch);
+    a forced small cap (ONI_SPLIT_MAX_BLOCKS) re-batches the huge documents and gives the same E-step."""
+    cap = hip.split_launch_cap(20, False)
+    assert 0 < cap <= hip.lib().split_max_blocks()
+    assert hip.lib().split_capacity(20, False) >= cap and hip.lib().split_capacity(100, True) > 0
+    c = planted_corpus(num_docs=300, num_terms=20000, num_topics=6, mean_tokens=400, tail=0.7,
+                       max_tokens=2_000_000, seed=8)
+    st = LDASettings(var_max_iter=10, var_converged=-1e30)
+    outs = []
+    for env in (None, "6"):
+        if env:
+            monkeypatch.setenv("ONI_SPLIT_MAX_BLOCKS", env)
+        eng = LDAEngine(c, 20, st, backend="hip", seed=1, precision="fp32")
+        sp = eng.doc_buckets.split
+        if env:
+            assert sp.max_blocks == 6 and all(b["n_blocks"] <= 6 for b in sp.batches)
+        eng.init_random()
+        eng.e_step()
+        torch.cuda.synchronize()
+        outs.append(eng.gamma[:, :20].double().cpu())
+    assert torch.allclose(outs[0], outs[1], rtol=2e-3, atol=1e-4)

@@ -53,6 +53,14 @@ def test_flow_pipeline_file_contract(tmp_path):
     phi = np.array([[float(x) for x in r.split(",")[1].split(" ")] for r in wres])
     assert np.allclose(phi.sum(0), 1.0, atol=1e-8)
     assert all(len(r.split(",")[0]) <= 20 for r in wres)   # strict: S20 truncation
+    # metrics.jsonl: stage seconds, the LDA engine's run metrics and the
+    # variational-iteration histogram of the last E-step
+    recs = [json.loads(l) for l in (tmp_path / "ml" / "metrics.jsonl").read_text().splitlines()]
+    lda = [r for r in recs if r.get("stage") == "lda"][-1]
+    assert lda["docs_per_sec"] > 0 and lda["var_iter_mean"] >= 1 and lda["exchange"] == "none"
+    assert lda["exchange_bytes_per_iter"] == 0 and "schedule" in lda
+    det = [r for r in recs if r.get("stage") == "lda_detail"][-1]
+    assert sum(det["var_iter_hist"]) == len(docs) and det["var_iter_hist"][0] == 0
 
 
 def test_flow_pipeline_fixed_mode_and_resume(tmp_path):
