@@ -32,6 +32,7 @@
 //             reduction of S is a row DPP reduction; cross-wave sums go through LDS in
 //             wave order (bitwise reproducible).  Topic owners (one thread per topic)
 //             run the refresh and broadcast E through LDS.
+#include <cstdlib>
 #include <stdexcept>
 #include <string>
 
@@ -757,11 +758,10 @@ __device__ __forceinline__ void load_row_full(const double* __restrict__ beta, i
   }
 }
 
-template <int KS, int NW>
+template <int KS, int NW, int RMAX>
 __global__ __launch_bounds__(wteam_threads(NW)) void gs_wteam(GSArgs a) {
   static_assert(KS <= 32 && KS % 2 == 0, "word team: KS <= 32");
   constexpr int DPB = wteam_dpb(NW), NTD = NW * 64, NS = NTD;
-  constexpr int RMAX = NW >= 8 ? 2 : 1;
   __shared__ double sC[DPB][kGsUMax][KS];
   __shared__ double sEt[DPB][kGsUMax][KS];
   __shared__ double sE[DPB][KS];
@@ -1135,13 +1135,21 @@ static void gs_estep_ks(const GSArgs& a, int variant, hipStream_t s) {
     }
     case kGsTeam4:
       if constexpr (KS <= 32)
-        hipLaunchKernelGGL((gs::gs_wteam<KS, 4>), dim3(a.n_items), dim3(256), 0, s, a);
+        hipLaunchKernelGGL((gs::gs_wteam<KS, 4, 1>), dim3(a.n_items), dim3(256), 0, s, a);
       else
         hipLaunchKernelGGL((gs::gs_team<KS, 4>), dim3(a.n_items), dim3(256), 0, s, a);
       break;
     case kGsTeam8:
-      if constexpr (KS <= 32)
-        hipLaunchKernelGGL((gs::gs_wteam<KS, 8>), dim3(a.n_items), dim3(512), 0, s, a);
+      if constexpr (KS <= 32) {
+        // longest documents: 8 waves x 2 prefetched words per lane; ONI_GS_BIG_NW=4 selects 4 waves x 4
+        // (measured on the headline corpus: 2.70 vs 2.96 ms, the 4-wave team has no second wave per
+        // SIMD to cover the fp64 dependency chains of the word phase)
+        static const bool nw4 = std::getenv("ONI_GS_BIG_NW") && std::atoi(std::getenv("ONI_GS_BIG_NW")) == 4;
+        if (nw4)
+          hipLaunchKernelGGL((gs::gs_wteam<KS, 4, 4>), dim3(a.n_items), dim3(256), 0, s, a);
+        else
+          hipLaunchKernelGGL((gs::gs_wteam<KS, 8, 2>), dim3(a.n_items), dim3(512), 0, s, a);
+      }
       else
         hipLaunchKernelGGL((gs::gs_team<KS, 8>), dim3(a.n_items), dim3(512), 0, s, a);
       break;
