@@ -126,6 +126,9 @@ PYBIND11_MODULE(_oninative, m) {
            py::arg("numeric_cols"), py::arg("dict_groups"))
       .def("load_files", &TextTable::load_files, py::arg("paths"), py::arg("drop_header") = true,
            py::arg("threads") = default_threads(), py::call_guard<py::gil_scoped_release>())
+      .def("load_range", &TextTable::load_range, py::arg("path"), py::arg("begin"), py::arg("end"),
+           py::arg("header"), py::arg("drop_header") = true, py::arg("threads") = default_threads(),
+           py::call_guard<py::gil_scoped_release>())
       .def("append_text", &TextTable::append_text, py::arg("text"), py::arg("weight") = 1,
            py::arg("threads") = default_threads(), py::call_guard<py::gil_scoped_release>())
       .def_property_readonly("num_rows", [](const TextTable& t) { return (int64_t)t.rows.size(); })

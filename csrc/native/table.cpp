@@ -113,6 +113,54 @@ void TextTable::load_files(const std::vector<std::string>& paths, bool drop_hdr,
   }
 }
 
+void TextTable::load_range(const std::string& path, int64_t begin, int64_t end, const std::string& hdr,
+                           bool drop_hdr, int threads) {
+  drop_header = drop_hdr;
+  header = hdr;
+  if (!header.empty() && header.back() == '\r') header.pop_back();
+  std::ifstream f(path, std::ios::binary);
+  if (!f) throw std::runtime_error("cannot open " + path);
+  f.seekg(0, std::ios::end);
+  const int64_t size = (int64_t)f.tellg();
+  begin = std::max<int64_t>(0, std::min(begin, size));
+  end = std::max(begin, std::min(end, size));
+  // first line starting at or after `begin`
+  int64_t b = begin;
+  if (b > 0) {
+    f.seekg(b - 1);
+    char c = 0;
+    f.get(c);
+    if (c != '\n') {
+      std::string rest;
+      std::getline(f, rest);                 // the line begun before `begin` belongs to the previous range
+      b = (int64_t)f.tellg();
+      if (b < 0) b = size;                   // no newline after it: nothing of ours in the file
+    }
+  }
+  // first line starting at or after `end` (our last line runs up to it)
+  int64_t e = end;
+  if (e < size && e > 0) {
+    f.clear();
+    f.seekg(e - 1);
+    char c = 0;
+    f.get(c);
+    if (c != '\n') {
+      std::string rest;
+      std::getline(f, rest);
+      e = (int64_t)f.tellg();
+      if (e < 0) e = size;
+    }
+  }
+  if (b >= e) return;
+  f.clear();
+  f.seekg(b);
+  std::string s((size_t)(e - b), '\0');
+  f.read(s.data(), (std::streamsize)s.size());
+  if (!s.empty() && s.back() != '\n') s.push_back('\n');
+  chunks.push_back(std::move(s));
+  ingest_chunk((uint32_t)(chunks.size() - 1), 1, threads);
+}
+
 void TextTable::append_text(std::string text, int32_t w, int threads) {
   if (!text.empty() && text.back() != '\n') text.push_back('\n');
   chunks.push_back(std::move(text));

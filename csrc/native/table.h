@@ -70,6 +70,11 @@ class TextTable {
 
   TextTable(int ncols, std::vector<int> numeric_cols, std::vector<std::vector<int>> dict_groups);
   void load_files(const std::vector<std::string>& paths, bool drop_header, int threads);
+  // Row-sharded ingest: the lines of `path` whose first byte lies in [begin, end) (a line belongs to the
+  // range holding its first byte, so N ranges of one file partition its lines exactly).  `hdr` is the
+  // header line of the job's first file (the reference's filter(_ != header) rule, applied to every line).
+  void load_range(const std::string& path, int64_t begin, int64_t end, const std::string& hdr, bool drop_header,
+                  int threads);
   void append_text(std::string text, int32_t w, int threads);  // newline-separated lines
   std::string_view row_text(size_t i) const {
     const RowSpan& r = rows[i];

@@ -36,6 +36,16 @@ def ecdf_cuts(values: torch.Tensor, quantiles: Sequence[float], weights: Optiona
     else:
         from ..corpus.builder import segment_sums
         uniq, counts = segment_sums(v, weights.to(device=v.device, dtype=torch.int64).reshape(-1))
+    return ecdf_cuts_from_hist(uniq, counts, quantiles)
+
+
+def ecdf_cuts_from_hist(uniq: torch.Tensor, counts: torch.Tensor, quantiles: Sequence[float]) -> torch.Tensor:
+    """The cut rule on a weighted histogram (sorted distinct values, integer weights): the form the
+    row-sharded featurization merges per-rank histograms into (features/flow_dist.py)."""
+    q = torch.tensor(list(quantiles), dtype=torch.float64, device=uniq.device)
+    if uniq.numel() == 0:
+        return torch.zeros_like(q)
+    counts = counts.to(torch.int64)
     cum = torch.cumsum(counts, 0)
     F = cum.to(torch.float64) / cum[-1].to(torch.float64)
     # largest index with F < q  (F is non-decreasing)

@@ -41,7 +41,33 @@ def run(cfg, dist=None, device=None, log=print) -> dict:
 
     # ------------------------------------------------------------------ pre
     need_pre = not (R.done("lda_pre") and R.done("flow_pre"))
-    if rank == 0 and (need_pre or not R.done("flow_post")):
+    # several ranks: row-sharded ingest + featurization (features/flow_dist.py), identical corpus on
+    # every rank; ONI_DIST_FEATURIZE=0 falls back to rank 0 featurizing and broadcasting
+    sharded = (dist is not None and dist.world_size > 1 and need_pre
+               and os.environ.get("ONI_DIST_FEATURIZE", "1") != "0")
+    if sharded:
+        from ..features import flow_dist as FD
+        with R.stage("load") as res:
+            ft_local = FD.load_flow_sharded(dist, cfg.flow_path, cfg.feedback_path(), cfg.dupfactor, cfg.threads)
+            res.update(rank_rows=ft_local.n)
+        with R.stage("flow_pre") as res:
+            dwc, gnames, ws, cuts = FD.featurize_sharded(dist, ft_local, device, strict=cfg.strict,
+                                                         cuts=cfg.fixed_cuts())
+            if rank == 0:
+                C.save_json(os.path.join(cfg.lpath, "flow_cuts.json"),
+                            dict(cuts={k: v.tolist() for k, v in cuts.items()}, ports=ws.ports.tolist()))
+            res["pairs"] = dwc.n
+        with R.stage("lda_pre") as res:
+            built = lda_pre(dwc)
+            doc_names = [gnames[i] for i in built.doc_keys.tolist()]
+            word_names = _word_names(ws, built.word_keys)
+            if rank == 0:
+                C.write_corpus_files(cfg.lpath, built, doc_names, word_names)
+            res.update(docs=built.corpus.num_docs, terms=built.corpus.num_terms, nnz=built.corpus.nnz)
+            summary["corpus"] = dict(docs=built.corpus.num_docs, terms=built.corpus.num_terms, nnz=built.corpus.nnz)
+        del ft_local
+        need_pre = False
+    if rank == 0 and (need_pre or not R.done("flow_post")) and not sharded:
         with R.stage("load") as res:
             ft = FF.load_flow(cfg.flow_path, cfg.feedback_path(), cfg.dupfactor, cfg.threads)
             res.update(ft.stats())
@@ -71,7 +97,7 @@ def run(cfg, dist=None, device=None, log=print) -> dict:
                 C.write_corpus_files(cfg.lpath, built, doc_names, word_names)
                 res.update(docs=built.corpus.num_docs, terms=built.corpus.num_terms, nnz=built.corpus.nnz)
                 summary["corpus"] = dict(docs=built.corpus.num_docs, terms=built.corpus.num_terms, nnz=built.corpus.nnz)
-    else:
+    elif not sharded:
         R.skip("flow_pre")
         R.skip("lda_pre")
 
@@ -80,7 +106,7 @@ def run(cfg, dist=None, device=None, log=print) -> dict:
     if not R.done("lda"):
         if corpus is None and rank == 0:
             corpus, doc_names, word_names = C.load_corpus_files(cfg.lpath)
-        if dist is not None and dist.world_size > 1:
+        if dist is not None and dist.world_size > 1 and not sharded:
             corpus = dist.broadcast_corpus(corpus)
         with R.stage("lda") as res:
             lres = C.run_lda(cfg, corpus, dist=dist, device=device, log=log)
@@ -117,6 +143,9 @@ def run(cfg, dist=None, device=None, log=print) -> dict:
 
         # ------------------------------------------------------------ flow_post
         if not R.done("flow_post"):
+            if ft is None:
+                # row-sharded pre stages: rank 0 reads the whole day for the scoring pass
+                ft = FF.load_flow(cfg.flow_path, cfg.feedback_path(), cfg.dupfactor, cfg.threads)
             with R.stage("flow_post") as res:
                 res.update(score_flow(cfg, ft, tables, device, log))
                 summary["scored"] = res.get("flagged")
