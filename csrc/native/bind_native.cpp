@@ -248,9 +248,8 @@ PYBIND11_MODULE(_oninative, m) {
         std::string s;
         for (int64_t i = n * t / threads; i < n * (t + 1) / threads; ++i) {
           s.clear();
-          if (mode == 0) append_fixed10(s, src[i]);
-          else append_py2_float(s, src[i]);
-          std::from_chars(s.data(), s.data() + s.size(), dst[i]);
+          if (mode == 0) append_fixed10(s, src[i], dst + i);
+          else append_py2_float(s, src[i], dst + i);
         }
       };
       std::vector<std::thread> th;
@@ -260,6 +259,29 @@ PYBIND11_MODULE(_oninative, m) {
     }
     return out;
   };
+  // Fast shortest-digit formatting (fmt.h) against the exact printf-equivalent conversions:
+  // (text mismatches, read-back mismatches, first bad index or -1).
+  m.def("fmt_selfcheck", [](py::array_t<double, py::array::c_style | py::array::forcecast> a, int mode) {
+    const double* src = a.data();
+    int64_t bad_text = 0, bad_value = 0, first = -1;
+    {
+      py::gil_scoped_release rel;
+      std::string f, x;
+      for (py::ssize_t i = 0; i < a.size(); ++i) {
+        f.clear();
+        x.clear();
+        double back = 0, ref = 0;
+        if (mode == 0) { append_fixed10(f, src[i], &back); append_fixed10_exact(x, src[i]); }
+        else { append_py2_float(f, src[i], &back); append_py2_float_exact(x, src[i]); }
+        std::from_chars(x.data() + (x[0] == ' ' ? x.find_first_not_of(' ') : 0), x.data() + x.size(), ref);
+        const bool tb = f != x, vb = !(back == ref || (back != back && ref != ref));
+        bad_text += tb;
+        bad_value += vb;
+        if ((tb || vb) && first < 0) first = i;
+      }
+    }
+    return py::make_tuple(bad_text, bad_value, first);
+  });
   m.def("roundtrip_fixed10", [roundtrip](py::array_t<double, py::array::c_style | py::array::forcecast> a, int threads) {
     return roundtrip(a, 0, threads);
   }, py::arg("a"), py::arg("threads") = 0);

@@ -3,8 +3,14 @@
 #include <algorithm>
 #include <charconv>
 #include <cstdio>
+#include <atomic>
+#include <chrono>
+#include <cerrno>
+#include <cstdlib>
 #include <cstring>
+#include <fcntl.h>
 #include <fstream>
+#include <unistd.h>
 #include <stdexcept>
 #include <thread>
 
@@ -14,25 +20,12 @@ namespace onin {
 
 namespace {
 
-struct LocalDict {
-  std::vector<std::string_view> names;
-  std::unordered_map<std::string_view, int32_t> index;
-  int32_t get_or_add(std::string_view s) {
-    auto it = index.find(s);
-    if (it != index.end()) return it->second;
-    int32_t id = (int32_t)names.size();
-    names.push_back(s);
-    index.emplace(s, id);
-    return id;
-  }
-};
-
-struct LocalOut {
+struct alignas(64) LocalOut {
   std::vector<uint64_t> off;
   std::vector<uint32_t> len;
   std::vector<std::vector<double>> num;
   std::vector<std::vector<int32_t>> ids;
-  std::vector<LocalDict> dicts;
+  std::vector<LocalNames> dicts;
   int64_t bad_fields = 0, bad_numeric = 0, header = 0;
 };
 
@@ -49,7 +42,8 @@ inline int java_split_count(const char* b, const char* e) {
   return n;
 }
 
-std::vector<size_t> split_points(const std::string& s, int parts) {
+template <class Text>
+std::vector<size_t> split_points(const Text& s, int parts) {
   std::vector<size_t> pts{0};
   const size_t n = s.size();
   for (int i = 1; i < parts; ++i) {
@@ -62,7 +56,169 @@ std::vector<size_t> split_points(const std::string& s, int parts) {
   return pts;
 }
 
+template <class F>
+void run_parallel(int n, int threads, F&& f) {
+  threads = std::max(1, std::min(threads, n));
+  if (threads == 1) {
+    for (int i = 0; i < n; ++i) f(i);
+    return;
+  }
+  std::atomic<int> next{0};
+  std::vector<std::thread> th;
+  for (int t = 0; t < threads; ++t)
+    th.emplace_back([&] {
+      for (int i; (i = next.fetch_add(1)) < n;) f(i);
+    });
+  for (auto& x : th) x.join();
+}
+
+// [off, off + n) of `path` into out, `threads` preads in parallel
+void read_bytes(const std::string& path, int64_t off, int64_t n, char* out, int threads) {
+  const int fd = ::open(path.c_str(), O_RDONLY);
+  if (fd < 0) throw std::runtime_error("cannot open " + path);
+  const int64_t piece = std::max<int64_t>(int64_t(8) << 20, (n + threads - 1) / std::max(1, threads));
+  const int np = (int)((n + piece - 1) / piece);
+  std::atomic<bool> bad{false};
+  run_parallel(np, threads, [&](int i) {
+    int64_t at = i * piece, left = std::min(piece, n - at);
+    while (left > 0) {
+      const ssize_t r = ::pread(fd, out + at, (size_t)left, off + at);
+      if (r <= 0) { bad = true; return; }
+      at += r;
+      left -= r;
+    }
+  });
+  ::close(fd);
+  if (bad) throw std::runtime_error("read failed: " + path);
+}
+
 }  // namespace
+
+// ------------------------------------------------------------------ dictionary --
+
+uint64_t hash_bytes(const char* p, size_t n) {
+  uint64_t h = 0x9E3779B97F4A7C15ull ^ (n * 0xff51afd7ed558ccdull);
+  while (n >= 8) {
+    uint64_t v;
+    std::memcpy(&v, p, 8);
+    h = (h ^ v) * 0xbf58476d1ce4e5b9ull;
+    h ^= h >> 31;
+    p += 8;
+    n -= 8;
+  }
+  if (n) {
+    uint64_t v = 0;
+    std::memcpy(&v, p, n);
+    h = (h ^ v) * 0x94d049bb133111ebull;
+    h ^= h >> 29;
+  }
+  h *= 0xbf58476d1ce4e5b9ull;
+  return h ^ (h >> 32);
+}
+
+StringDict::StringDict() : shards_(kShards) {}
+
+std::string_view StringDict::Shard::store(std::string_view s) {
+  if (s.size() > arena_left) {
+    const size_t cap = std::max<size_t>(size_t(1) << 20, s.size());
+    arena.emplace_back(new char[cap]);
+    arena_at = arena.back().get();
+    arena_left = cap;
+  }
+  std::memcpy(arena_at, s.data(), s.size());
+  std::string_view v(arena_at, s.size());
+  arena_at += s.size();
+  arena_left -= s.size();
+  return v;
+}
+
+int32_t StringDict::find(std::string_view s) const {
+  const uint64_t h = hash_bytes(s.data(), s.size());
+  const Shard& sh = shards_[shard_of(h)];
+  const int64_t k = sh.index.find(h, s, [&](size_t i) { return sh.keys[i]; });
+  return k < 0 ? -1 : (int32_t)sh.val[k];
+}
+
+int32_t StringDict::get_or_add(std::string_view s) {
+  const uint64_t h = hash_bytes(s.data(), s.size());
+  Shard& sh = shards_[shard_of(h)];
+  const int64_t k = sh.index.find(h, s, [&](size_t i) { return sh.keys[i]; });
+  if (k >= 0) return (int32_t)sh.val[k];
+  const int32_t id = (int32_t)names.size();
+  names.emplace_back(s);
+  sh.keys.push_back(sh.store(s));
+  sh.val.push_back(id);
+  sh.index.insert(h);
+  return id;
+}
+
+void StringDict::merge(const std::vector<const LocalNames*>& parts, std::vector<std::vector<int32_t>>& remap,
+                       int threads) {
+  const int T = (int)parts.size();
+  remap.assign(T, {});
+  // shard buckets of each part, in local (first-appearance) order
+  std::vector<std::vector<std::vector<int32_t>>> bkt(T, std::vector<std::vector<int32_t>>(kShards));
+  std::vector<std::vector<int64_t>> res(T);
+  std::vector<std::vector<uint8_t>> first(T);
+  run_parallel(T, threads, [&](int t) {
+    const auto& L = *parts[t];
+    res[t].resize(L.names.size());
+    first[t].assign(L.names.size(), 0);
+    remap[t].resize(L.names.size());
+    for (size_t j = 0; j < L.names.size(); ++j) bkt[t][shard_of(L.index.hash[j])].push_back((int32_t)j);
+  });
+  // shard-parallel lookup / insert: parts visited in order, so the first part (and first local
+  // index) that sees a new name owns it
+  std::vector<std::vector<int64_t>> pending(kShards);
+  run_parallel(kShards, threads, [&](int s) {
+    Shard& sh = shards_[s];
+    for (int t = 0; t < T; ++t) {
+      const auto& L = *parts[t];
+      for (int32_t j : bkt[t][s]) {
+        const std::string_view name = L.names[j];
+        const uint64_t h = L.index.hash[j];
+        int64_t k = sh.index.find(h, name, [&](size_t i) { return sh.keys[i]; });
+        if (k < 0) {
+          k = (int64_t)sh.keys.size();
+          sh.keys.push_back(sh.store(name));
+          sh.val.push_back(~((int64_t)t << 32 | j));
+          sh.index.insert(h);
+          pending[s].push_back(k);
+          first[t][j] = 1;
+        }
+        res[t][j] = sh.val[k];
+      }
+    }
+  });
+  // new ids in (part, local index) order
+  std::vector<int64_t> base(T + 1, (int64_t)names.size());
+  for (int t = 0; t < T; ++t) {
+    int64_t c = 0;
+    for (uint8_t f : first[t]) c += f;
+    base[t + 1] = base[t] + c;
+  }
+  if (base[T] > INT32_MAX) throw std::runtime_error("dictionary exceeds 2^31 entries");
+  names.resize((size_t)base[T]);
+  run_parallel(T, threads, [&](int t) {
+    int64_t id = base[t];
+    for (size_t j = 0; j < first[t].size(); ++j)
+      if (first[t][j]) {
+        remap[t][j] = (int32_t)id;
+        names[(size_t)id++] = std::string(parts[t]->names[j]);
+      }
+  });
+  auto decode = [&](int64_t v) {
+    const int64_t c = ~v;
+    return remap[(int)(c >> 32)][(size_t)(c & 0xffffffff)];
+  };
+  run_parallel(T, threads, [&](int t) {
+    for (size_t j = 0; j < res[t].size(); ++j)
+      if (!first[t][j]) remap[t][j] = res[t][j] >= 0 ? (int32_t)res[t][j] : decode(res[t][j]);
+  });
+  run_parallel(kShards, threads, [&](int s) {
+    for (int64_t k : pending[s]) shards_[s].val[k] = decode(shards_[s].val[k]);
+  });
+}
 
 TextTable::TextTable(int ncols_, std::vector<int> numeric_cols_, std::vector<std::vector<int>> dict_groups_)
     : ncols(ncols_), numeric_cols(std::move(numeric_cols_)), dict_groups(std::move(dict_groups_)) {
@@ -93,24 +249,38 @@ int TextTable::dict_slot(int col) const {
 
 void TextTable::load_files(const std::vector<std::string>& paths, bool drop_hdr, int threads) {
   drop_header = drop_hdr;
-  bool first = true;
+  std::vector<int64_t> sizes;
+  int64_t total = 0;
   for (const auto& p : paths) {
-    std::ifstream f(p, std::ios::binary);
+    std::ifstream f(p, std::ios::binary | std::ios::ate);
     if (!f) throw std::runtime_error("cannot open " + p);
-    f.seekg(0, std::ios::end);
-    std::string s((size_t)f.tellg(), '\0');
-    f.seekg(0);
-    f.read(s.data(), (std::streamsize)s.size());
-    if (first && drop_header) {
-      size_t e = s.find('\n');
-      header = s.substr(0, e == std::string::npos ? s.size() : e);
+    sizes.push_back((int64_t)f.tellg());
+    total += sizes.back();
+  }
+  int64_t left = total;
+  for (size_t i = 0; i < paths.size(); ++i) {
+    const std::string& p = paths[i];
+    TextChunk s((size_t)sizes[i]);
+    read_bytes(p, 0, sizes[i], s.data(), threads);
+    if (i == 0 && drop_header) {
+      const char* e = (const char*)std::memchr(s.data(), '\n', s.size());
+      header.assign(s.data(), e ? (size_t)(e - s.data()) : s.size());
       if (!header.empty() && header.back() == '\r') header.pop_back();
     }
-    first = false;
-    if (!s.empty() && s.back() != '\n') s.push_back('\n');
+    s.ensure_newline();
     chunks.push_back(std::move(s));
     ingest_chunk((uint32_t)(chunks.size() - 1), 1, threads);
+    left -= sizes[i];
+    // after the first file: room for the remaining files' rows at the observed bytes per row
+    if (i == 0 && left > 0 && !rows.empty()) reserve_rows(rows.size() + (size_t)((double)left / bytes_in * rows.size() * 1.02));
   }
+}
+
+void TextTable::reserve_rows(size_t n) {
+  rows.reserve(n);
+  weight.reserve(n);
+  for (auto& v : num) v.reserve(n);
+  for (auto& v : ids) v.reserve(n);
 }
 
 void TextTable::load_range(const std::string& path, int64_t begin, int64_t end, const std::string& hdr,
@@ -152,27 +322,30 @@ void TextTable::load_range(const std::string& path, int64_t begin, int64_t end, 
     }
   }
   if (b >= e) return;
-  f.clear();
-  f.seekg(b);
-  std::string s((size_t)(e - b), '\0');
-  f.read(s.data(), (std::streamsize)s.size());
-  if (!s.empty() && s.back() != '\n') s.push_back('\n');
+  f.close();
+  TextChunk s((size_t)(e - b));
+  read_bytes(path, b, e - b, s.data(), threads);
+  s.ensure_newline();
   chunks.push_back(std::move(s));
   ingest_chunk((uint32_t)(chunks.size() - 1), 1, threads);
 }
 
 void TextTable::append_text(std::string text, int32_t w, int threads) {
-  if (!text.empty() && text.back() != '\n') text.push_back('\n');
-  chunks.push_back(std::move(text));
+  TextChunk s(text.size());
+  std::memcpy(s.data(), text.data(), text.size());
+  s.ensure_newline();
+  chunks.push_back(std::move(s));
   ingest_chunk((uint32_t)(chunks.size() - 1), w, threads);
 }
 
 void TextTable::ingest_chunk(uint32_t cid, int32_t w, int threads) {
-  const std::string& s = chunks[cid];
+  const TextChunk& s = chunks[cid];
   if (threads < 1) threads = 1;
   if (s.size() < (1u << 20)) threads = 1;
   auto pts = split_points(s, threads);
   const int T = (int)pts.size() - 1;
+  const double bytes_per_row = rows.empty() ? 64.0 : (double)bytes_in / rows.size();
+  bytes_in += (int64_t)s.size();
   std::vector<LocalOut> outs(T);
   const int NN = (int)numeric_cols.size(), ND = (int)dict_col_index.size();
   // column -> (numeric slot, dict slot)
@@ -185,6 +358,11 @@ void TextTable::ingest_chunk(uint32_t cid, int32_t w, int threads) {
     o.num.resize(NN);
     o.ids.resize(ND);
     o.dicts.resize(dicts.size());
+    const size_t guess = (size_t)((pts[t + 1] - pts[t]) / bytes_per_row * 1.05) + 16;
+    o.off.reserve(guess);
+    o.len.reserve(guess);
+    for (auto& v : o.num) v.reserve(guess);
+    for (auto& v : o.ids) v.reserve(guess);
     std::vector<const char*> fb(ncols), fe(ncols);
     std::vector<double> vals(NN);
     std::vector<std::string_view> svals(ND);
@@ -234,32 +412,45 @@ void TextTable::ingest_chunk(uint32_t cid, int32_t w, int threads) {
       }
     }
   };
-  if (T == 1) {
-    work(0);
-  } else {
-    std::vector<std::thread> th;
-    for (int t = 0; t < T; ++t) th.emplace_back(work, t);
-    for (auto& x : th) x.join();
+  const auto tp0 = std::chrono::steady_clock::now();
+  run_parallel(T, T, work);
+  const auto tp1 = std::chrono::steady_clock::now();
+  // ordered merge: dictionaries (shard-parallel), then every thread's rows copied to its offset
+  std::vector<std::vector<std::vector<int32_t>>> remap(dicts.size());
+  for (size_t g = 0; g < dicts.size(); ++g) {
+    std::vector<const LocalNames*> parts(T);
+    for (int t = 0; t < T; ++t) parts[t] = &outs[t].dicts[g];
+    dicts[g].merge(parts, remap[g], threads);
   }
-  // ordered merge
+  const auto tp2 = std::chrono::steady_clock::now();
+  std::vector<size_t> at(T + 1, rows.size());
   for (int t = 0; t < T; ++t) {
+    n_bad_fields += outs[t].bad_fields;
+    n_bad_numeric += outs[t].bad_numeric;
+    n_header += outs[t].header;
+    at[t + 1] = at[t] + outs[t].off.size();
+  }
+  rows.resize(at[T]);
+  weight.resize(at[T], w);
+  for (int i = 0; i < NN; ++i) num[i].resize(at[T]);
+  for (int i = 0; i < ND; ++i) ids[i].resize(at[T]);
+  run_parallel(T, threads, [&](int t) {
     LocalOut& o = outs[t];
-    n_bad_fields += o.bad_fields;
-    n_bad_numeric += o.bad_numeric;
-    n_header += o.header;
-    std::vector<std::vector<int32_t>> remap(dicts.size());
-    for (size_t g = 0; g < dicts.size(); ++g) {
-      remap[g].resize(o.dicts[g].names.size());
-      for (size_t j = 0; j < o.dicts[g].names.size(); ++j) remap[g][j] = dicts[g].get_or_add(o.dicts[g].names[j]);
-    }
-    const size_t n = o.off.size();
-    for (size_t r = 0; r < n; ++r) rows.push_back(RowSpan{cid, o.len[r], o.off[r]});
-    weight.insert(weight.end(), n, w);
-    for (int i = 0; i < NN; ++i) num[i].insert(num[i].end(), o.num[i].begin(), o.num[i].end());
+    const size_t n = o.off.size(), a = at[t];
+    for (size_t r = 0; r < n; ++r) rows[a + r] = RowSpan{cid, o.len[r], o.off[r]};
+    for (int i = 0; i < NN; ++i) std::copy(o.num[i].begin(), o.num[i].end(), num[i].begin() + a);
     for (int i = 0; i < ND; ++i) {
-      auto& rm = remap[dict_col_group[i]];
-      for (int32_t v : o.ids[i]) ids[i].push_back(rm[v]);
+      const auto& rm = remap[dict_col_group[i]][t];
+      int32_t* dst = ids[i].data() + a;
+      for (size_t r = 0; r < n; ++r) dst[r] = rm[o.ids[i][r]];
     }
+    std::vector<std::vector<double>>().swap(o.num);
+  });
+  if (std::getenv("ONI_TABLE_PROFILE")) {
+    const auto tp3 = std::chrono::steady_clock::now();
+    auto ms = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
+    std::fprintf(stderr, "ingest chunk %u: %zu bytes parse %.1f ms dict %.1f ms rows %.1f ms\n", cid, s.size(),
+                 ms(tp0, tp1), ms(tp1, tp2), ms(tp2, tp3));
   }
 }
 
@@ -303,10 +494,8 @@ static void format_row(std::string& out, int64_t r, const std::vector<OutCol>& c
         double* back = k.parsed ? k.parsed + (size_t)r * k.width : nullptr;
         for (int j = 0; j < k.width; ++j) {
           if (j) out += k.text;
-          const size_t at = out.size();
-          if (k.kind == OutCol::kPy2Row) append_py2_float(out, row[j]);
-          else append_fixed10(out, row[j]);
-          if (back) std::from_chars(out.data() + at, out.data() + out.size(), back[j]);
+          if (k.kind == OutCol::kPy2Row) append_py2_float(out, row[j], back ? back + j : nullptr);
+          else append_fixed10(out, row[j], back ? back + j : nullptr);
         }
         break;
       }
@@ -318,37 +507,58 @@ static void format_row(std::string& out, int64_t r, const std::vector<OutCol>& c
 int64_t write_rows(const std::string& path, const int64_t* order, int64_t n, const std::vector<OutCol>& cols,
                    const std::string& sep, bool append, int threads) {
   FILE* f = std::fopen(path.c_str(), append ? "ab" : "wb");
-  if (!f) throw std::runtime_error("cannot open for writing: " + path);
+  if (!f) throw std::runtime_error("cannot open for writing: " + path + ": " + std::strerror(errno));
   if (threads < 1) threads = 1;
-  // Rows per thread block: ~2^16 cells of work per block, so wide rows (a K x V
+  // Rows per thread block: ~2^18 cells of work per block, so wide rows (a K x V
   // .beta file has K rows of V values) still spread over every thread.
   int64_t cells = 0;
   for (const OutCol& c : cols) cells += (c.kind == OutCol::kPy2Row || c.kind == OutCol::kFixedRow) ? c.width : 1;
-  const int64_t block = std::max<int64_t>(1, (int64_t(1) << 16) / std::max<int64_t>(1, cells));
+  const int64_t block = std::max<int64_t>(1, (int64_t(1) << 18) / std::max<int64_t>(1, cells));
+  // Two buffer sets: one writer thread writes batch b while the others format batch b + 1 (writes
+  // to one file serialise in the kernel anyway -- parallel pwrite measured slower).
   int64_t written = 0;
-  std::vector<std::string> bufs(threads);
-  for (int64_t b0 = 0; b0 < n; b0 += block * threads) {
-    auto work = [&](int t) {
-      std::string& s = bufs[t];
+  std::vector<std::string> bufs[2] = {std::vector<std::string>(threads), std::vector<std::string>(threads)};
+  std::thread writer;
+  int werr = 0;
+  auto flush = [&](int set) {
+    for (auto& s : bufs[set]) {
+      if (werr) return;
+      if (!s.empty() && std::fwrite(s.data(), 1, s.size(), f) != s.size()) werr = errno ? errno : EIO;
+      written += (int64_t)s.size();
+    }
+  };
+  int set = 0;
+  double t_fmt = 0, t_wait = 0;
+  const auto t_all = std::chrono::steady_clock::now();
+  auto since = [](std::chrono::steady_clock::time_point a) {
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - a).count();
+  };
+  for (int64_t b0 = 0; b0 < n; b0 += block * threads, set ^= 1) {
+    const auto tb = std::chrono::steady_clock::now();
+    std::vector<std::string>& cur = bufs[set];
+    const int nt = (int)std::min<int64_t>(threads, (n - b0 + block - 1) / block);
+    run_parallel(threads, nt, [&](int t) {
+      std::string s;                    // a local, not cur[t]: adjacent string headers would share
+      s.swap(cur[t]);                   // cache lines and every append would bounce them
       s.clear();
       const int64_t lo = b0 + t * block, hi = std::min(n, lo + block);
       for (int64_t i = lo; i < hi; ++i) format_row(s, order ? order[i] : i, cols, sep);
-    };
-    if (threads == 1 || n - b0 <= block) {
-      work(0);
-      for (int t = 1; t < threads; ++t) bufs[t].clear();
-    } else {
-      std::vector<std::thread> th;
-      for (int t = 0; t < threads; ++t) th.emplace_back(work, t);
-      for (auto& x : th) x.join();
-    }
-    for (auto& s : bufs) {
-      if (!s.empty() && std::fwrite(s.data(), 1, s.size(), f) != s.size()) {
-        std::fclose(f);
-        throw std::runtime_error("short write: " + path);
-      }
-      written += (int64_t)s.size();
-    }
+      s.swap(cur[t]);
+    });
+    t_fmt += since(tb);
+    const auto tw = std::chrono::steady_clock::now();
+    if (writer.joinable()) writer.join();
+    t_wait += since(tw);
+    if (werr) break;
+    writer = std::thread(flush, set);
+  }
+  if (writer.joinable()) writer.join();
+  if (std::getenv("ONI_TABLE_PROFILE"))
+    std::fprintf(stderr, "write_rows %s: %lld rows, %d threads, format %.1f ms, writer wait %.1f ms, total %.1f ms\n",
+                 path.c_str(), (long long)n, threads, t_fmt, t_wait, since(t_all));
+  if (werr) {
+    std::fclose(f);
+    throw std::runtime_error("short write: " + path + ": " + std::strerror(werr));
   }
   if (std::fclose(f) != 0) throw std::runtime_error("close failed: " + path);
   return written;

@@ -18,6 +18,7 @@
 // order), computed per thread and merged in input order, so the result does
 // not depend on the thread count.
 #pragma once
+#include <algorithm>
 #include <cstdint>
 #include <memory>
 #include <string>
@@ -33,22 +34,97 @@ struct RowSpan {
   uint64_t off;
 };
 
+// 64-bit hash of a byte string (8-byte multiply-xorshift rounds).
+uint64_t hash_bytes(const char* p, size_t n);
+
+// Open-addressing index over an external key list: slot -> key id + 1, linear probing on the
+// precomputed hash, grown at half load.  Keys are compared through `key(id)`.
+struct FlatIndex {
+  std::vector<uint32_t> slot;
+  std::vector<uint64_t> hash;   // per key id
+  size_t mask = 0;
+  template <class Key>
+  int64_t find(uint64_t h, std::string_view s, const Key& key) const {
+    if (slot.empty()) return -1;
+    for (size_t i = h & mask;; i = (i + 1) & mask) {
+      const uint32_t v = slot[i];
+      if (v == 0) return -1;
+      if (hash[v - 1] == h && key(v - 1) == s) return v - 1;
+    }
+  }
+  void insert(uint64_t h) {      // the next key id (= hash.size()) with hash h
+    hash.push_back(h);
+    if (2 * hash.size() > slot.size()) rehash(std::max<size_t>(64, 4 * hash.size()));
+    else place(h, (uint32_t)hash.size());
+  }
+
+ private:
+  void place(uint64_t h, uint32_t v) {
+    size_t i = h & mask;
+    while (slot[i] != 0) i = (i + 1) & mask;
+    slot[i] = v;
+  }
+  void rehash(size_t n) {
+    size_t cap = 64;
+    while (cap < n) cap <<= 1;
+    slot.assign(cap, 0);
+    mask = cap - 1;
+    for (size_t k = 0; k < hash.size(); ++k) place(hash[k], (uint32_t)(k + 1));
+  }
+};
+
+// One thread's first-appearance name list (string_views into the text being ingested).
+struct LocalNames {
+  std::vector<std::string_view> names;
+  FlatIndex index;
+  int32_t get_or_add(std::string_view s) {
+    const uint64_t h = hash_bytes(s.data(), s.size());
+    const int64_t k = index.find(h, s, [this](size_t i) { return names[i]; });
+    if (k >= 0) return (int32_t)k;
+    names.push_back(s);
+    index.insert(h);
+    return (int32_t)(names.size() - 1);
+  }
+};
+
+// Global dictionary: ids in first-appearance order.  The index is split into hash shards so
+// merging T threads' first-appearance lists runs in parallel (merge(): shard-parallel lookup /
+// insert, then a prefix over threads assigns the new ids in (thread, local index) order -- the
+// order a serial pass over the rows would have produced).
 class StringDict {
  public:
   std::vector<std::string> names;
-  std::unordered_map<std::string, int32_t> index;
-  int32_t get_or_add(std::string_view s) {
-    auto it = index.find(std::string(s));
-    if (it != index.end()) return it->second;
-    int32_t id = (int32_t)names.size();
-    names.emplace_back(s);
-    index.emplace(names.back(), id);
-    return id;
-  }
-  int32_t find(std::string_view s) const {
-    auto it = index.find(std::string(s));
-    return it == index.end() ? -1 : it->second;
-  }
+  static constexpr int kShards = 64;
+  StringDict();
+  int32_t get_or_add(std::string_view s);
+  int32_t find(std::string_view s) const;
+  // remap[t][j] = global id of parts[t]->names[j]
+  void merge(const std::vector<const LocalNames*>& parts, std::vector<std::vector<int32_t>>& remap, int threads);
+
+ private:
+  struct Shard {
+    FlatIndex index;
+    std::vector<std::string_view> keys;       // into arena
+    std::vector<int64_t> val;                 // global id, or ~(t << 32 | j) while a merge is pending
+    std::vector<std::unique_ptr<char[]>> arena;
+    size_t arena_left = 0;
+    char* arena_at = nullptr;
+    std::string_view store(std::string_view s);
+  };
+  std::vector<Shard> shards_;
+  static int shard_of(uint64_t h) { return (int)((h >> 40) % kShards); }
+};
+
+// Owned input text (not zero-filled: read straight into the buffer).
+struct TextChunk {
+  std::unique_ptr<char[]> buf;
+  size_t n = 0;
+  explicit TextChunk(size_t size) : buf(new char[size + 1]), n(size) {}
+  const char* data() const { return buf.get(); }
+  char* data() { return buf.get(); }
+  size_t size() const { return n; }
+  char operator[](size_t i) const { return buf[i]; }
+  void ensure_newline() { if (n == 0 || buf[n - 1] != '\n') buf[n++] = '\n'; }   // capacity is size + 1
 };
 
 class TextTable {
@@ -56,7 +132,8 @@ class TextTable {
   int ncols = 0;
   std::vector<int> numeric_cols;                 // columns parsed as double
   std::vector<std::vector<int>> dict_groups;     // columns sharing one dictionary
-  std::vector<std::string> chunks;               // owned text
+  std::vector<TextChunk> chunks;                 // owned text
+  int64_t bytes_in = 0;                          // text ingested so far (row-count estimates)
   std::vector<RowSpan> rows;
   std::vector<int32_t> weight;                   // per-row multiplicity (feedback rows: DUPFACTOR)
   std::vector<std::vector<double>> num;          // [numeric_cols.size()][rows]
@@ -76,6 +153,7 @@ class TextTable {
   void load_range(const std::string& path, int64_t begin, int64_t end, const std::string& hdr, bool drop_header,
                   int threads);
   void append_text(std::string text, int32_t w, int threads);  // newline-separated lines
+  void reserve_rows(size_t n);
   std::string_view row_text(size_t i) const {
     const RowSpan& r = rows[i];
     return std::string_view(chunks[r.chunk].data() + r.off, r.len);

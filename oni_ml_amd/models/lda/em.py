@@ -1018,8 +1018,8 @@ class LDAEngine:
             on_iteration: Optional[Callable] = None, on_save: Optional[Callable] = None,
             start_iteration: int = 0, likelihood_old: float = 0.0, verbose: bool = False) -> LDAResult:
         """Run EM to convergence. `on_save(tag, engine)` fires for '000', every LAG and 'final'."""
-        from .settings import LAG
         st = self.settings
+        lag = st.lag
         t0 = time.perf_counter()
         if start == "random":
             self.init_random()
@@ -1061,8 +1061,8 @@ class LDAEngine:
             # One batch = the iterations up to the next LAG save (the saved state must be that
             # iteration's), at most max_batch; the device stops the batch itself on convergence.
             n = 1 if per_iter_stats else self.max_batch
-            if on_save is not None:
-                n = min(n, LAG - (i % LAG))
+            if on_save is not None and lag > 0:
+                n = min(n, lag - (i % lag))
             n = max(1, min(n, st.em_max_iter - i + 1))
             ti = time.perf_counter()
             range_push(f"em_iters_{i + 1}_{i + n}")
@@ -1089,7 +1089,7 @@ class LDAEngine:
                     on_iteration(self, i, lik, conv)
             if not recs:
                 break
-            if on_save is not None and (i % LAG) == 0:
+            if on_save is not None and lag > 0 and (i % lag) == 0:
                 on_save(f"{i:03d}", self)
         if on_save is not None:
             on_save("final", self)

@@ -37,6 +37,10 @@ class LDASettings:
     # Engine schedule (not a settings.txt line): 0 = lda-c's per-word Gauss-Seidel;
     # U > 0 = block Gauss-Seidel with at most U gamma refreshes per sweep (lda_ref.cpp).
     gs_updates: int = 0
+    # Period of the %03d.{beta,gamma,other} files and checkpoint (lda-c's compile-time LAG); 0 = only
+    # 000 and final.  Not a settings.txt line: large runs (BASELINE config 5's ~8 GB gamma per save)
+    # turn it down from the caller.
+    lag: int = LAG
 
     def __post_init__(self):
         # lda-c keeps these as float32

@@ -40,12 +40,30 @@ def _ip_names(n_int: int, n_ext: int, rng) -> list:
     return names
 
 
-def generate_flow_day(path: str, events: int = 1_000_000, seed: int = 0, date=(2016, 1, 22), n_internal: int = 40_000,
-                      n_external: int = 120_000, files: int = 1, threads: int = 8) -> dict:
+def ip_population(events: int):
+    """(internal, external) address pool sizes: 40k / 120k up to 1M events (the bench day), then
+    growing as events^0.8, so a 100M-event month holds a few million documents (BASELINE config 5)."""
+    if events <= 1_000_000:
+        return 40_000, 120_000
+    f = (events / 1_000_000) ** 0.8
+    return int(40_000 * f), int(120_000 * f)
+
+
+def generate_flow_day(path: str, events: int = 1_000_000, seed: int = 0, date=(2016, 1, 22),
+                      n_internal: Optional[int] = None, n_external: Optional[int] = None, files: int = 1,
+                      threads: int = 8, chunk_events: int = 0) -> dict:
     """Write `files` CSV part files (each with the header line) under `path` (a directory) or to `path`.
 
+    The address pool scales with `events` (ip_population) unless given.  chunk_events > 0: generate
+    and write part file by part file (files = ceil(events / chunk_events)), each from its own random
+    stream, so a 100M-event month never holds more than one chunk's columns in memory.
     Returns dict(paths=[...], events=n, ips=#distinct names).
     """
+    di, de = ip_population(events)
+    n_internal = di if n_internal is None else n_internal
+    n_external = de if n_external is None else n_external
+    if chunk_events and events > chunk_events:
+        return _generate_chunked(path, events, seed, date, n_internal, n_external, threads, chunk_events)
     rng = np.random.default_rng(seed)
     N = native.lib()
     ips = _ip_names(n_internal, n_external, rng)
@@ -54,6 +72,31 @@ def generate_flow_day(path: str, events: int = 1_000_000, seed: int = 0, date=(2
     pop = 1.0 / np.arange(1, nip + 1) ** 1.05
     pop /= pop.sum()
     perm = rng.permutation(nip)
+    return _write_events(path, events, rng, ips, pop, perm, date, files, threads, N)
+
+
+def _generate_chunked(path, events, seed, date, n_internal, n_external, threads, chunk):
+    rng0 = np.random.default_rng(seed)
+    N = native.lib()
+    ips = _ip_names(n_internal, n_external, rng0)
+    nip = len(ips)
+    pop = 1.0 / np.arange(1, nip + 1) ** 1.05
+    pop /= pop.sum()
+    perm = rng0.permutation(nip)
+    os.makedirs(path, exist_ok=True)
+    nfiles = -(-events // chunk)
+    paths = []
+    for i in range(nfiles):
+        n = min(chunk, events - i * chunk)
+        rng = np.random.default_rng([seed, i + 1])
+        p = os.path.join(path, f"part-{i:05d}.csv")
+        _write_events(p, n, rng, ips, pop, perm, date, 1, threads, N)
+        paths.append(p)
+    return dict(paths=paths, events=events, ips=nip)
+
+
+def _write_events(path, events, rng, ips, pop, perm, date, files, threads, N) -> dict:
+    nip = len(ips)
     sip = perm[rng.choice(nip, size=events, p=pop)].astype(np.int32)
     dip = perm[rng.choice(nip, size=events, p=pop)].astype(np.int32)
     same = sip == dip

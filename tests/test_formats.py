@@ -202,3 +202,28 @@ def test_ldac_corpus_text_native(tmp_path):
     q.write_text("3 0:1 3:2\n")
     with pytest.raises(RuntimeError, match="declares 3 entries"):
         ldac.read_model_dat(str(q))
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+def test_fast_formatting_matches_exact(mode):
+    """fmt.h's shortest-digit fast paths ("%5.10f" and py2 "%.12g") against the exact printf-equivalent
+    conversions: text and read-back value, over magnitudes, ties at both grids, subnormals and raw bits."""
+    N = native.lib()
+    rng = np.random.default_rng(11 + mode)
+    n = 300_000
+    sets = [
+        np.exp(rng.uniform(-700, 700, n)) * rng.choice([-1, 1], n),
+        rng.random(n),
+        np.log(rng.random(n)) * rng.uniform(0, 50, n),
+        rng.integers(-10**13, 10**13, n) / 10.0 ** rng.integers(0, 16, n),
+        (rng.integers(0, 10**9, n) * 2 + 1) / 2e10,                                # %.10f midpoints
+        (rng.integers(10**11, 10**12, n) * 10 + 5) / 10.0 ** rng.integers(5, 20, n),  # %.12g midpoints
+        rng.integers(0, 2**63, n, dtype=np.uint64).view(np.float64),
+        rng.random(n) * 1e-8,
+        np.array([0.0, -0.0, 1.0, -1.0, 1e-9, -1e-9, 99999.99999999995, 1e5, 9.99999999999995e-10, 5e-324,
+                  2.2250738585072014e-308, 2.225073858507201e-308, 1e300, 123456789012.5, 999999999999.5,
+                  1e12, 1e-5, 1e-4, 0.5e-10, 1.5e-10]),
+    ]
+    for a in sets:
+        a = a[np.isfinite(a)]
+        assert N.fmt_selfcheck(a, mode) == (0, 0, -1)
