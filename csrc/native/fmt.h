@@ -69,67 +69,69 @@ inline std::string java_double(double d) {
   return s;
 }
 
-// ---- fast paths from the shortest round-trip digits ---------------------------------------
+// ---- exact fast paths without a decimal conversion library ---------------------------------
 //
-// Let S be the shortest round-trip decimal of x (Ryu: fewest digits, then closest to x) and T a
-// rounding midpoint of a P-digit grid.  T cannot lie strictly between x and S: T would then be in
-// x's round-trip interval with fewer digits than S (or as many and closer to x), so Ryu would
-// have picked it.  Hence rounding S to P digits gives the same result as rounding x, except when
-// S itself IS a midpoint (its digit P is the last one and equals 5) -- those values take the
-// exact (printf-equivalent) path.  ~4x faster than to_chars(general / fixed, precision).
+// "%.10f" and "%.12g" both print N = round-half-even(|x| * 10^k) for one k (10, or 11 - the
+// decimal exponent).  With 10^k exact (0 <= k <= 22) that rounding is decided exactly from the
+// error-free product x * 10^k = p + err.  No Ryu / printf on this path (2-5x cheaper); values
+// outside it (|x| >= 1e11 for %.12g, >= 9e5 for %.10f, tiny or non-finite) take the exact
+// library conversion.
 
-// |a| finite, nonzero: dig[0..nd) with a = d0.d1d2... x 10^e; no trailing zeros.
-inline int shortest_digits(double a, char* dig, int* e10) {
-  char buf[40];
-  auto r = std::to_chars(buf, buf + sizeof(buf), a, std::chars_format::scientific);
-  int nd = 0;
-  const char* p = buf;
-  for (; p < r.ptr && *p != 'e'; ++p)
-    if (*p != '.') dig[nd++] = *p;
-  ++p;
-  const bool neg = *p == '-';
-  if (*p == '+' || *p == '-') ++p;
-  int e = 0;
-  for (; p < r.ptr; ++p) e = e * 10 + (*p - '0');
-  *e10 = neg ? -e : e;
-  while (nd > 1 && dig[nd - 1] == '0') --nd;
-  return nd;
+inline const double* pow10_table() {
+  static const double p10[] = {1e0,  1e1,  1e2,  1e3,  1e4,  1e5,  1e6,  1e7,  1e8,  1e9,  1e10, 1e11,
+                               1e12, 1e13, 1e14, 1e15, 1e16, 1e17, 1e18, 1e19, 1e20, 1e21, 1e22};
+  return p10;
 }
 
-// Round dig to P significant digits (round half up is never needed: see above).  False on a
-// midpoint (the caller takes the exact path).
-inline bool round_digits(char* dig, int& nd, int& e, int P) {
-  if (nd <= P) return true;
-  if (P < 1) return false;
-  const char c = dig[P];
-  if (c == '5' && nd == P + 1) return false;
-  nd = P;
-  if (c >= '5') {
-    int i = P - 1;
-    while (i >= 0 && dig[i] == '9') dig[i--] = '0';
-    if (i < 0) {
-      dig[0] = '1';
-      ++e;
-    } else {
-      ++dig[i];
-    }
+// 12 decimal digits of 0 <= n < 10^12, two at a time
+inline void put_digits12(char* dig, int64_t n) {
+  static const char pairs[] =
+      "00010203040506070809101112131415161718192021222324252627282930313233343536373839"
+      "40414243444546474849505152535455565758596061626364656667686970717273747576777879"
+      "8081828384858687888990919293949596979899";
+  uint32_t hi = (uint32_t)(n / 1000000), lo = (uint32_t)(n % 1000000);
+  for (int i = 4; i >= 0; i -= 2) {
+    std::memcpy(dig + 6 + i, pairs + 2 * (lo % 100), 2);
+    std::memcpy(dig + i, pairs + 2 * (hi % 100), 2);
+    lo /= 100;
+    hi /= 100;
   }
-  while (nd > 1 && dig[nd - 1] == '0') --nd;
-  return true;
+}
+
+// Dekker's exact product a * b = p + e (no FMA instruction needed: the host build targets x86-64-v2)
+inline void two_prod(double a, double b, double* p, double* e) {
+  const double sp = 134217729.0;                // 2^27 + 1
+  double t = sp * a, ah = t - (t - a), al = a - ah;
+  t = sp * b;
+  const double bh = t - (t - b), bl = b - bh;
+  *p = a * b;
+  *e = ((ah * bh - *p) + ah * bl + al * bh) + al * bl;
+}
+
+// round-half-even(a * 10^k) for a >= 0, 0 <= k <= 22, a * 10^k < 2^52
+inline int64_t scaled_round(double a, int k) {
+  double p, err;                                // a * 10^k = p + err exactly
+  two_prod(a, pow10_table()[k], &p, &err);
+  const double q = std::floor(p);
+  const double f = p - q;                       // exact
+  int64_t n = (int64_t)q;
+  if (f < 0.25) return n;                       // |err| <= half an ulp of p
+  if (f > 0.75) return n + 1;
+  const double d = f - 0.5;                     // exact (Sterbenz); compare d + err with 0
+  if (d > -err || (d == -err && (n & 1))) ++n;
+  return n;
 }
 
 // digits -> double (Clinger's fast path: an integer mantissa < 2^53 times / over an exact power of
-// ten is one correctly rounded operation); false outside it
+// ten is one correctly rounded operation, i.e. what strtod returns); false outside it
 inline bool digits_value(const char* dig, int nd, int e, bool neg, double* out) {
-  static const double p10[] = {1e0,  1e1,  1e2,  1e3,  1e4,  1e5,  1e6,  1e7,  1e8,  1e9,  1e10, 1e11,
-                               1e12, 1e13, 1e14, 1e15, 1e16, 1e17, 1e18, 1e19, 1e20, 1e21, 1e22};
   if (nd > 15) return false;
   int64_t m = 0;
   for (int i = 0; i < nd; ++i) m = m * 10 + (dig[i] - '0');
   const int k = e - nd + 1;
   double v;
-  if (k >= 0 && k <= 22) v = (double)m * p10[k];
-  else if (k < 0 && k >= -22) v = (double)m / p10[-k];
+  if (k >= 0 && k <= 22) v = (double)m * pow10_table()[k];
+  else if (k < 0 && k >= -22) v = (double)m / pow10_table()[-k];
   else return false;
   *out = neg ? -v : v;
   return true;
@@ -138,39 +140,65 @@ inline bool digits_value(const char* dig, int nd, int e, bool neg, double* out) 
 // Python 2 str(float): "%.12g" plus ".0" on integral-looking output.  `back` (optional) receives
 // the value a reader parses from the text.
 inline void append_py2_float(std::string& out, double d, double* back = nullptr) {
-  if (std::isnan(d)) { out += "nan"; if (back) *back = d; return; }
-  if (std::isinf(d)) { out += d > 0 ? "inf" : "-inf"; if (back) *back = d; return; }
-  char dig[32];
-  int e = 0, nd = 0;
   const size_t at = out.size();
-  if (std::fabs(d) >= 2.2250738585072014e-308) {      // normal: 53 bits > 12 digits (see above)
-    nd = shortest_digits(std::fabs(d), dig, &e);
-    if (round_digits(dig, nd, e, 12)) {
-      if (d < 0) out += '-';
-      if (e < -4 || e >= 12) {
-        out += dig[0];
-        if (nd > 1) { out += '.'; out.append(dig + 1, nd - 1); }
-        out += 'e';
-        out += e < 0 ? '-' : '+';
-        const int ae = e < 0 ? -e : e;
-        if (ae < 10) out += '0';
-        char eb[8];
-        auto r = std::to_chars(eb, eb + sizeof(eb), ae);
-        out.append(eb, r.ptr - eb);
-      } else if (e >= 0) {
-        for (int i = 0; i <= e; ++i) out += i < nd ? dig[i] : '0';
-        if (nd > e + 1) { out += '.'; out.append(dig + e + 1, nd - e - 1); }
-        else out += ".0";
-      } else {
-        out += "0.";
-        out.append((size_t)(-e - 1), '0');
-        out.append(dig, nd);
+  const double a = std::fabs(d);
+  if (a >= 1e-11 && a < 1e11) {                 // 0 <= 11 - E <= 22: an exact power of ten
+    uint64_t bits;
+    std::memcpy(&bits, &a, 8);
+    const int e2 = (int)((bits >> 52) & 0x7ff) - 1022;          // a in [2^(e2-1), 2^e2)
+    int E = (int)std::floor((e2 - 1) * 0.30102999566398120);   // E or E - 1
+    int64_t N = 0;
+    bool ok = false;
+    for (int tries = 0; tries < 3; ++tries) {
+      const int k = 11 - E;
+      if (k < 0 || k > 22) break;
+      N = scaled_round(a, k);
+      if (N < 100000000000LL) { --E; continue; }
+      if (N >= 1000000000000LL) {
+        if (N == 1000000000000LL && tries > 0) { N = 100000000000LL; ++E; ok = true; break; }  // carry
+        ++E;
+        continue;
       }
-      if (back && !digits_value(dig, nd, e, d < 0, back))
+      ok = true;
+      break;
+    }
+    if (ok) {
+      char dig[12];
+      put_digits12(dig, N);
+      int nd = 12;
+      while (nd > 1 && dig[nd - 1] == '0') --nd;
+      char buf[40];
+      char* w = buf;
+      if (d < 0) *w++ = '-';
+      if (E < -4 || E >= 12) {
+        *w++ = dig[0];
+        if (nd > 1) { *w++ = '.'; std::memcpy(w, dig + 1, nd - 1); w += nd - 1; }
+        *w++ = 'e';
+        *w++ = E < 0 ? '-' : '+';
+        const int ae = E < 0 ? -E : E;
+        if (ae >= 100) *w++ = (char)('0' + ae / 100);
+        *w++ = (char)('0' + ae / 10 % 10);
+        *w++ = (char)('0' + ae % 10);
+      } else if (E >= 0) {
+        for (int i = 0; i <= E; ++i) *w++ = i < nd ? dig[i] : '0';
+        *w++ = '.';
+        if (nd > E + 1) { std::memcpy(w, dig + E + 1, nd - E - 1); w += nd - E - 1; }
+        else *w++ = '0';
+      } else {
+        *w++ = '0';
+        *w++ = '.';
+        for (int i = 0; i < -E - 1; ++i) *w++ = '0';
+        std::memcpy(w, dig, nd);
+        w += nd;
+      }
+      out.append(buf, w - buf);
+      if (back && !digits_value(dig, nd, E, d < 0, back))
         std::from_chars(out.data() + at, out.data() + out.size(), *back);
       return;
     }
   }
+  if (std::isnan(d)) { out += "nan"; if (back) *back = d; return; }
+  if (std::isinf(d)) { out += d > 0 ? "inf" : "-inf"; if (back) *back = d; return; }
   char buf[40];
   auto r = std::to_chars(buf, buf + sizeof(buf), d, std::chars_format::general, 12);
   const int n = (int)(r.ptr - buf);
@@ -182,30 +210,30 @@ inline void append_py2_float(std::string& out, double d, double* back = nullptr)
   if (back) std::from_chars(out.data() + at, out.data() + out.size(), *back);
 }
 
-// printf("%5.10f"): finite values always exceed the 5-character field width, so the
-// conversion is the exact 10-decimal rounding (fast path for 1e-9 <= |d| < 1e5, where half an
-// ulp of d is far below the 1e-10 grid); nan / inf keep printf's padded spelling.
+// printf("%5.10f"): finite values always exceed the 5-character field width, so the conversion
+// is the exact 10-decimal rounding: N = round-half-even(|d| * 1e10) for |d| < 9e5 (N < 2^53),
+// the exact printf-equivalent path beyond; nan / inf keep printf's padded spelling.
 inline void append_fixed10(std::string& out, double d, double* back = nullptr) {
-  const size_t at = out.size();
   const double a = std::fabs(d);
-  if (a >= 1e-9 && a < 1e5) {
-    char dig[32];
-    int e = 0;
-    int nd = shortest_digits(a, dig, &e);
-    if (round_digits(dig, nd, e, e + 11)) {
-      if (d < 0) out += '-';
-      if (e >= 0) {
-        for (int i = 0; i <= e; ++i) out += i < nd ? dig[i] : '0';
-      } else {
-        out += '0';
-      }
-      out += '.';
-      for (int i = e + 1; i <= e + 10; ++i) out += (i >= 0 && i < nd) ? dig[i] : '0';
-      if (back && !digits_value(dig, nd, e, d < 0, back))
-        std::from_chars(out.data() + at, out.data() + out.size(), *back);
-      return;
+  if (a < 9e5) {
+    int64_t N = scaled_round(a, 10);
+    const int64_t ip = N / 10000000000LL, fp = N % 10000000000LL;
+    if (std::signbit(d)) out += '-';
+    char b[32];
+    auto r = std::to_chars(b, b + sizeof(b), ip);
+    out.append(b, r.ptr - b);
+    out += '.';
+    char f[10];
+    int64_t v = fp;
+    for (int i = 9; i >= 0; --i) { f[i] = (char)('0' + v % 10); v /= 10; }
+    out.append(f, 10);
+    if (back) {
+      const double x = (double)N / 1e10;
+      *back = std::signbit(d) ? -x : x;
     }
+    return;
   }
+  const size_t at = out.size();
   char buf[352];
   if (!std::isfinite(d)) {
     int n = std::snprintf(buf, sizeof(buf), "%5.10f", d);

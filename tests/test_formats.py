@@ -206,8 +206,9 @@ def test_ldac_corpus_text_native(tmp_path):
 
 @pytest.mark.parametrize("mode", [0, 1])
 def test_fast_formatting_matches_exact(mode):
-    """fmt.h's shortest-digit fast paths ("%5.10f" and py2 "%.12g") against the exact printf-equivalent
-    conversions: text and read-back value, over magnitudes, ties at both grids, subnormals and raw bits."""
+    """fmt.h's error-free-product fast paths ("%5.10f" and py2 "%.12g") against the exact
+    printf-equivalent conversions: text and read-back value, over magnitudes, ties at both grids,
+    carries, powers of ten, subnormals and raw bits."""
     N = native.lib()
     rng = np.random.default_rng(11 + mode)
     n = 300_000
@@ -220,6 +221,9 @@ def test_fast_formatting_matches_exact(mode):
         (rng.integers(10**11, 10**12, n) * 10 + 5) / 10.0 ** rng.integers(5, 20, n),  # %.12g midpoints
         rng.integers(0, 2**63, n, dtype=np.uint64).view(np.float64),
         rng.random(n) * 1e-8,
+        np.ldexp(1.0, rng.integers(-60, 60, n)) * rng.integers(1, 2**20, n),            # dyadic: exact ties
+        10.0 ** rng.integers(-12, 12, n) * (1 + rng.integers(-3, 4, n) * 2.0**-52),    # around powers of 10
+        (10.0 ** rng.integers(1, 13, n) - 1) / 10.0 ** rng.integers(0, 14, n),          # 9...9 carries
         np.array([0.0, -0.0, 1.0, -1.0, 1e-9, -1e-9, 99999.99999999995, 1e5, 9.99999999999995e-10, 5e-324,
                   2.2250738585072014e-308, 2.225073858507201e-308, 1e300, 123456789012.5, 999999999999.5,
                   1e12, 1e-5, 1e-4, 0.5e-10, 1.5e-10]),
