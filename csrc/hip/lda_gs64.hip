@@ -46,6 +46,10 @@ namespace gs {
 
 constexpr double kExpM100 = 3.720075976020836e-44;   // exp(-100), lda-c's log-probability floor
 
+// c*phi rows are written once per E-step and read once by the suff-stats pass: nontemporal
+// stores keep them from evicting the beta rows every document re-gathers each sweep
+typedef double dvec2 __attribute__((ext_vector_type(2)));
+
 constexpr int ilog2(int x) { return x <= 1 ? 0 : 1 + ilog2(x / 2); }
 constexpr int tg_of(int KS) { return KS <= 32 ? 4 : (KS <= 64 ? 8 : 16); }
 constexpr int kpl_of(int KS) { return (KS + tg_of(KS) - 1) / tg_of(KS); }
@@ -333,7 +337,7 @@ __global__ __launch_bounds__(256) void gs_tiny(GSArgs a) {
       double* row = a.cphi + (size_t)(s0 + j) * KS;
 #pragma unroll
       for (int i = 0; i < KPL; ++i)
-        if (q + TG * i < KS) row[q + TG * i] = C[j][i];
+        if (q + TG * i < KS) __builtin_nontemporal_store(C[j][i], &row[q + TG * i]);
     }
   }
   if (q == 0) {
@@ -466,12 +470,15 @@ __global__ __launch_bounds__(team_threads(KS, NW)) void gs_team(GSArgs a) {
     for (int r = 0; r < RMAX; ++r) {
       const int p = n0 + slot + r * NS;
       v |= (active && p < n1) ? (1u << r) : 0u;
-      const int pc = min(p, n - 1);
+      // rounds past the chunk end re-read the chunk's last word: the same address as a valid
+      // lane, so no extra row is gathered (clamping to the document end fetched the next chunk's rows)
+      const int pc = min(p, n1 - 1);
       w[r] = wrow[pc];
       c[r] = crow[pc];
     }
   };
   auto load_rows = [&](const int (&w)[RMAX]) {
+    if (!active) return;   // wave-uniform: waves without words of a chunk gather no rows
 #pragma unroll
     for (int r = 0; r < RMAX; ++r) {
       const double* brow = a.beta + (size_t)w[r] * KS;
@@ -655,7 +662,7 @@ __global__ __launch_bounds__(team_threads(KS, NW)) void gs_team(GSArgs a) {
       double* row = a.cphi + (size_t)(s0 + p) * KS;
 #pragma unroll
       for (int i = 0; i < KPL; ++i)
-        if (q + TG * i < KS) row[q + TG * i] = E[i] * b[i] * r;
+        if (q + TG * i < KS) __builtin_nontemporal_store(E[i] * b[i] * r, &row[q + TG * i]);
     }
   }
 }
@@ -772,12 +779,13 @@ __global__ __launch_bounds__(wteam_threads(NW)) void gs_wteam(GSArgs a) {
   const int t = threadIdx.x % NTD, ds = threadIdx.x / NTD;
   const int item = blockIdx.x * DPB + ds;
   if (item >= a.n_items) return;
+  const int d = a.order[item];
+  if (d < 0) return;   // placement gap (GSPlan.isolate_longest)
   const double alpha = a.params[0], lik_const = a.params[1];
   const int vmi = (int)a.params[2];
   const double vconv = params_vconv(a.params);
   const int K = a.K;
   const int lane = t & 63, wv = t >> 6;
-  const int d = a.order[item];
   const int s0 = a.doc_ptr[d], n = a.doc_ptr[d + 1] - s0;
   const int U = a.gs_updates;
   const int W = n > 0 ? (n + U - 1) / U : 1;
@@ -816,18 +824,30 @@ __global__ __launch_bounds__(wteam_threads(NW)) void gs_wteam(GSArgs a) {
     for (int r = 0; r < RMAX; ++r) {
       const int p = n0 + t + r * NS;
       v |= (active && p < n1) ? (1u << r) : 0u;
-      const int pc = min(p, n - 1);
+      // rounds past the chunk end re-read the chunk's last word: the same address as a valid
+      // lane, so no extra row is gathered (clamping to the document end fetched the next chunk's rows)
+      const int pc = min(p, n1 - 1);
       w[r] = wrow[pc];
       c[r] = crow[pc];
     }
   };
-  auto load_rows = [&](const int (&w)[RMAX]) {
+  // rounds without a word (past the chunk end) load nothing: exec-masked lanes return no data, and
+  // the row return path (64 B/clk per CU) is what a chunk's word phase waits on
+  auto load_rows = [&](const int (&w)[RMAX], unsigned v) {
+    if (!active) return;   // wave-uniform
 #pragma unroll
-    for (int r = 0; r < RMAX; ++r) load_row_full<KS>(a.beta, w[r], bc[r]);
+    for (int r = 0; r < RMAX; ++r) {
+      if ((v >> r) & 1u) {
+        load_row_full<KS>(a.beta, w[r], bc[r]);
+      } else {
+#pragma unroll
+        for (int k = 0; k < KS; ++k) bc[r][k] = 0.0;
+      }
+    }
   };
   if (nch > 0) {
     load_ids(0, wc, cc, vc);
-    load_rows(wc);
+    load_rows(wc, vc);
     load_ids(nch > 1 ? 1 : 0, wn, cn, vn);
   }
   team_sync<NW>();
@@ -878,7 +898,7 @@ __global__ __launch_bounds__(wteam_threads(NW)) void gs_wteam(GSArgs a) {
           cc[r] = cn[r];
         }
         vc = vn;
-        load_rows(wc);
+        load_rows(wc, vc);
         load_ids(j2, wn, cn, vn);
         tick(0);
         wave_topic_sums<KS>(acc, lane, sRed[ds][wv]);
@@ -963,9 +983,290 @@ __global__ __launch_bounds__(wteam_threads(NW)) void gs_wteam(GSArgs a) {
         if (kk + 3 < KS) p3 = fma(E[kk + 3], b[kk + 3], p3);
       }
       const double r = (double)crow[p] * drcp((p0 + p1) + (p2 + p3));
-      double2* row = reinterpret_cast<double2*>(a.cphi + (size_t)(s0 + p) * KS);
+      dvec2* row = reinterpret_cast<dvec2*>(a.cphi + (size_t)(s0 + p) * KS);
 #pragma unroll
-      for (int kk = 0; kk < KS / 2; ++kk) row[kk] = make_double2(E[2 * kk] * b[2 * kk] * r, E[2 * kk + 1] * b[2 * kk + 1] * r);
+      for (int kk = 0; kk < KS / 2; ++kk) {
+        const dvec2 v = {E[2 * kk] * b[2 * kk] * r, E[2 * kk + 1] * b[2 * kk + 1] * r};
+        __builtin_nontemporal_store(v, &row[kk]);
+      }
+    }
+  }
+}
+
+// ------------------------------------------------- word team, topic wave ----
+// The longest documents (gs_wteam measured: ~8.7k cycles per chunk, the critical path of the
+// E-step).  NW word waves own the words; one extra TOPIC WAVE owns the K topics and runs the
+// refresh.  The two roles run separate loops with the same barrier sequence, so:
+//  - the word waves' registers (E, accumulators, the next chunk's prefetched rows) are not live
+//    in the refresh code, which therefore needs no spills; in gs_wteam the refresh ran in wave 0
+//    beside 256 live VGPRs and its spill reloads waited (vmcnt is in order) behind the next
+//    chunk's row prefetch;
+//  - the topic wave issues no global loads, so nothing queues in front of its LDS traffic;
+//  - the word waves take log P of their words (only the sweep likelihood needs it) while the
+//    topic wave refreshes, off the chunk's critical path.
+// Arithmetic per word and per topic is that of gs_wteam (the likelihood's lw partial sums are
+// grouped by wave, so the two kernels agree to rounding, not bitwise).
+template <int KS, int NW, int RMAX>
+__global__ __launch_bounds__((NW + 1) * 64) void gs_wsteam(GSArgs a) {
+  static_assert(KS <= 32 && KS % 2 == 0, "word team: KS <= 32");
+  constexpr int NTD = (NW + 1) * 64, NS = NW * 64;
+  __shared__ double C[kGsUMax][KS];     // chunk contributions (previous sweep)
+  __shared__ double Et[kGsUMax][KS];    // E each chunk used (final pass)
+  __shared__ double E_[KS];             // current E, broadcast
+  __shared__ double sRed[NW][KS];       // per-wave topic sums of a chunk
+  __shared__ double Cs[kGsUMax];        // chunk count sums
+  __shared__ double sScal[NW + 1][4];   // sweep partials: lw per word wave; gamma sums (topic wave)
+  __shared__ int arrive;                // word-wave arrivals (chunks x active waves), monotone
+  if (a.params[kParamDone] != 0.0) return;
+  const int t = threadIdx.x;
+  const int d = a.order[blockIdx.x];
+  if (d < 0) return;                    // placement gap (GSPlan.isolate_longest): whole workgroup
+  const double alpha = a.params[0], lik_const = a.params[1];
+  const int vmi = (int)a.params[2];
+  const double vconv = params_vconv(a.params);
+  const int K = a.K;
+  const int lane = t & 63, wv = t >> 6;
+  const bool topic_wave = wv == NW;
+  const int s0 = a.doc_ptr[d], n = a.doc_ptr[d + 1] - s0;
+  const int U = a.gs_updates;
+  const int W = n > 0 ? (n + U - 1) / U : 1;
+  const int nch = (n + W - 1) / W;
+  const int nact = min(NW, (W + 63) / 64);
+  const bool active = wv < nact;        // word waves holding words of a chunk (never the topic wave)
+  const int* __restrict__ wrow = a.word_idx + s0;
+  const float* __restrict__ crow = a.counts + s0;
+  for (int j = t; j < nch; j += NTD) Cs[j] = 0.0;
+  if (t == 0) arrive = 0;
+  lds_barrier();
+  for (int p = t; p < n; p += NTD) atomicAdd(&Cs[p / W], (double)crow[p]);   // integer counts: exact
+  lds_barrier();
+  double total = 0.0;
+  for (int j = 0; j < nch; ++j) total += Cs[j];
+  const double g0 = alpha + total / K;
+  const double m = psi_only(g0);
+  const bool timer = a.dbg != nullptr && blockIdx.x == 0 && t == 0;
+  long long ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  long long tc = timer ? clock64() : 0;
+  auto tick = [&](int i) {
+    if (timer) {
+      const long long x = clock64();
+      ph[i] += x - tc;
+      tc = x;
+    }
+  };
+  double L = 0.0, L_old = 0.0, conv = 1.0, GS = 0.0;
+  int it = 0;
+  // sweep likelihood from the partials every wave left in sScal (same order in every thread)
+  auto sweep_end = [&]() {
+    lds_barrier();
+    double LW = 0.0;
+#pragma unroll
+    for (int v = 0; v < NW; ++v) LW += sScal[v][0];
+    GS = sScal[NW][1];
+    L = lik_const - lgamma_pos(GS) + sScal[NW][2] + fma(m, total, LW) - sScal[NW][3];
+    conv = (L_old - L) / L_old;
+    L_old = L;
+    lds_barrier();
+  };
+  if (topic_wave) {
+    // ------------------------------------------------------------ topic wave
+    __builtin_amdgcn_s_setprio(3);   // its chain is the critical path; the word waves wait on it
+    const int k = lane;
+    int want = 0;
+    double gam = k < K ? g0 : 0.0, psi = m, lps = 0.0;
+    if (k < KS) {
+      E_[k] = k < K ? 1.0 : 0.0;
+      for (int j = 0; j < nch; ++j) C[j][k] = k < K ? Cs[j] / K : 0.0;
+    }
+    lds_barrier();   // (1) E_ and C ready; word waves' first rows in flight
+    while (var_continue(conv, vconv, it, vmi)) {
+      ++it;
+      lps = 0.0;
+      for (int j = 0; j < nch; ++j) {
+        // (A) the nact word waves' topic sums of chunk j are in sRed
+        want += nact;
+        while (__hip_atomic_load(&arrive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < want)
+          __builtin_amdgcn_s_sleep(1);
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+        if (k < KS) {
+          double S = 0.0;
+#pragma unroll
+          for (int v = 0; v < NW; ++v) S += v < nact ? sRed[v][k] : 0.0;
+          const double Eo = E_[k];
+          const double nw = Eo * S;
+          double En = 0.0;
+          if (k < K) {
+            lps = fma(psi, nw, lps);
+            gam += nw - C[j][k];
+            psi_exp(gam, m, psi, En);
+          }
+          C[j][k] = nw;
+          Et[j][k] = Eo;
+          E_[k] = En;
+        }
+        lds_barrier();   // (B) E of chunk j + 1 published
+      }
+      const bool own = k < K;
+      const double w1 = group_sum<64>(own ? gam : 0.0), w2 = group_sum<64>(own ? lgamma_pos(gam) : 0.0);
+      const double w3 = group_sum<64>(own ? lps : 0.0);
+      if (lane == 0) {
+        sScal[NW][1] = w1;
+        sScal[NW][2] = w2;
+        sScal[NW][3] = w3;
+      }
+      sweep_end();
+    }
+    const double ps = group_sum<64>(k < K ? psi : 0.0);
+    if (k < KS) a.gamma[(size_t)d * KS + k] = gam;
+    if (lane == 0) {
+      a.lik[d] = L;
+      a.alpha_ss[d] = ps - K * psi_only(GS);
+      a.iters[d] = it;
+    }
+    return;
+  }
+  // -------------------------------------------------------------- word waves
+  int wc[RMAX], wn[RMAX];
+  float cc[RMAX], cn[RMAX];
+  unsigned vc = 0, vn = 0;
+  double bc[RMAX][KS];
+  auto load_ids = [&](int j, int (&w)[RMAX], float (&c)[RMAX], unsigned& v) {
+    const int n0 = j * W, n1 = min(n, n0 + W);
+    v = 0;
+#pragma unroll
+    for (int r = 0; r < RMAX; ++r) {
+      const int p = n0 + t + r * NS;
+      v |= (active && p < n1) ? (1u << r) : 0u;
+      const int pc = min(p, n1 - 1);
+      w[r] = wrow[pc];
+      c[r] = crow[pc];
+    }
+  };
+  auto load_rows = [&](const int (&w)[RMAX], unsigned v) {
+    if (!active) return;   // wave-uniform
+#pragma unroll
+    for (int r = 0; r < RMAX; ++r) {
+      if ((v >> r) & 1u) {   // rounds past the chunk end gather nothing
+        load_row_full<KS>(a.beta, w[r], bc[r]);
+      } else {
+#pragma unroll
+        for (int kk = 0; kk < KS; ++kk) bc[r][kk] = 0.0;
+      }
+    }
+  };
+  if (nch > 0) {
+    load_ids(0, wc, cc, vc);
+    load_rows(wc, vc);
+    load_ids(nch > 1 ? 1 : 0, wn, cn, vn);
+  }
+  lds_barrier();   // (1)
+  while (var_continue(conv, vconv, it, vmi)) {
+    ++it;
+    double lw = 0.0;
+    for (int j = 0; j < nch; ++j) {
+      ph[7] += timer ? 1 : 0;
+      double P[RMAX], cr[RMAX];
+      if (active) {
+        const int n0 = j * W, n1 = min(n, n0 + W);
+        double E[KS], acc[KS];
+#pragma unroll
+        for (int kk = 0; kk < KS; ++kk) {
+          E[kk] = E_[kk];
+          acc[kk] = 0.0;
+        }
+#pragma unroll
+        for (int r = 0; r < RMAX; ++r) cr[r] = ((vc >> r) & 1u) ? (double)cc[r] : 0.0;
+        // dot, reciprocal and axpy now; log P after barrier A (beside the refresh)
+#pragma unroll
+        for (int u = 0; u < RMAX; ++u) {
+          double p0 = 0.0, p1 = 0.0, p2 = 0.0, p3 = 0.0;
+#pragma unroll
+          for (int kk = 0; kk < KS; kk += 4) {
+            p0 = fma(E[kk], bc[u][kk], p0);
+            if (kk + 1 < KS) p1 = fma(E[kk + 1], bc[u][kk + 1], p1);
+            if (kk + 2 < KS) p2 = fma(E[kk + 2], bc[u][kk + 2], p2);
+            if (kk + 3 < KS) p3 = fma(E[kk + 3], bc[u][kk + 3], p3);
+          }
+          P[u] = cr[u] > 0.0 ? (p0 + p1) + (p2 + p3) : 1.0;
+        }
+        if (timer) {   // split of the word phase: E read + dot | reciprocal + axpy + prefetch issue
+          __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0) only... values consumed below anyway
+          const long long x = clock64();
+          ph[6] += x - tc;
+          tc = x;
+        }
+#pragma unroll
+        for (int u = 0; u < RMAX; ++u) {
+          const double r = cr[u] * drcp(P[u]);
+#pragma unroll
+          for (int kk = 0; kk < KS; ++kk) acc[kk] = fma(r, bc[u][kk], acc[kk]);
+        }
+        for (int p = n0 + t + RMAX * NS; p < n1; p += NS) {   // beyond the prefetched rounds
+          double b[1][KS];
+          load_row_full<KS>(a.beta, wrow[p], b[0]);
+          const double cp = (double)crow[p];
+          wword_steps<KS, 1>(E, b, &cp, acc, lw);
+        }
+        tick(0);
+        wave_topic_sums<KS>(acc, lane, sRed[wv]);
+        // (A) arrival: this wave's topic sums are in sRed.  A counter instead of a workgroup barrier,
+        // so the refresh starts while the word waves are still issuing the next chunk's row loads
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");   // LDS only: no vmcnt wait
+        if (lane == 0) __hip_atomic_fetch_add(&arrive, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        tick(1);
+        // prefetch of the next chunk's rows: a chunk's ~700 row gathers keep the CU's address unit busy
+        // for ~2k cycles (64 B/clk) and the issuing wave blocks until they are queued -- now beside the
+        // refresh instead of before it
+        const int j1 = j + 1 < nch ? j + 1 : 0;
+        const int j2 = j1 + 1 < nch ? j1 + 1 : 0;
+#pragma unroll
+        for (int r = 0; r < RMAX; ++r) {
+          wc[r] = wn[r];
+          cc[r] = cn[r];
+        }
+        vc = vn;
+        load_rows(wc, vc);
+        load_ids(j2, wn, cn, vn);
+        tick(2);
+#pragma unroll
+        for (int u = 0; u < RMAX; ++u) lw = fma(cr[u], flog(P[u]), lw);
+      }
+      tick(3);
+      lds_barrier();   // (B)
+      tick(4);
+    }
+    const double w0 = group_sum<64>(lw);
+    if (lane == 0) sScal[wv][0] = w0;
+    sweep_end();
+    tick(5);
+  }
+  if (timer)
+    for (int i = 0; i < 8; ++i) a.dbg[i] = ph[i];
+  // final pass: c_n phi_nk = E_jk b_nk r_n with the final sweep's chunk E (same P as the sweep)
+  if (!active) return;
+  for (int j = 0; j < nch; ++j) {
+    const int n0 = j * W, n1 = min(n, n0 + W);
+    double E[KS];
+#pragma unroll
+    for (int kk = 0; kk < KS; ++kk) E[kk] = Et[j][kk];
+    for (int p = n0 + t; p < n1; p += NS) {
+      double b[KS];
+      load_row_full<KS>(a.beta, wrow[p], b);
+      double p0 = 0.0, p1 = 0.0, p2 = 0.0, p3 = 0.0;
+#pragma unroll
+      for (int kk = 0; kk < KS; kk += 4) {
+        p0 = fma(E[kk], b[kk], p0);
+        if (kk + 1 < KS) p1 = fma(E[kk + 1], b[kk + 1], p1);
+        if (kk + 2 < KS) p2 = fma(E[kk + 2], b[kk + 2], p2);
+        if (kk + 3 < KS) p3 = fma(E[kk + 3], b[kk + 3], p3);
+      }
+      const double r = (double)crow[p] * drcp((p0 + p1) + (p2 + p3));
+      dvec2* row = reinterpret_cast<dvec2*>(a.cphi + (size_t)(s0 + p) * KS);
+#pragma unroll
+      for (int kk = 0; kk < KS / 2; ++kk) {
+        const dvec2 v = {E[2 * kk] * b[2 * kk] * r, E[2 * kk + 1] * b[2 * kk + 1] * r};
+        __builtin_nontemporal_store(v, &row[kk]);
+      }
     }
   }
 }
@@ -1144,9 +1445,17 @@ static void gs_estep_ks(const GSArgs& a, int variant, hipStream_t s) {
         // longest documents: 8 waves x 2 prefetched words per lane; ONI_GS_BIG_NW=4 selects 4 waves x 4
         // (measured on the headline corpus: 2.70 vs 2.96 ms, the 4-wave team has no second wave per
         // SIMD to cover the fp64 dependency chains of the word phase)
-        static const bool nw4 = std::getenv("ONI_GS_BIG_NW") && std::atoi(std::getenv("ONI_GS_BIG_NW")) == 4;
-        if (nw4)
+        static const int bnw = std::getenv("ONI_GS_BIG_NW") ? std::atoi(std::getenv("ONI_GS_BIG_NW")) : 7;
+        if (bnw == 7)
+          hipLaunchKernelGGL((gs::gs_wsteam<KS, 7, 2>), dim3(a.n_items), dim3(512), 0, s, a);
+        else if (bnw == 3)
+          hipLaunchKernelGGL((gs::gs_wsteam<KS, 3, 4>), dim3(a.n_items), dim3(256), 0, s, a);
+        else if (bnw == 5)
+          hipLaunchKernelGGL((gs::gs_wsteam<KS, 5, 3>), dim3(a.n_items), dim3(384), 0, s, a);
+        else if (bnw == 4)
           hipLaunchKernelGGL((gs::gs_wteam<KS, 4, 4>), dim3(a.n_items), dim3(256), 0, s, a);
+        else if (bnw == 16)
+          hipLaunchKernelGGL((gs::gs_wteam<KS, 16, 1>), dim3(a.n_items), dim3(1024), 0, s, a);
         else
           hipLaunchKernelGGL((gs::gs_wteam<KS, 8, 2>), dim3(a.n_items), dim3(512), 0, s, a);
       }

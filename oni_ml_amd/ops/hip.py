@@ -635,12 +635,36 @@ class GSPlan:
         Ls = L[order]
         tiny = min(gs_tiny_max(KS), int(gs_updates))
         self.plan = []
+        iso = int(os.environ.get("ONI_GS_XCD", "1")) if KS <= 32 else 0
         for var, lo, hi in self.EDGES:
             lo_ = tiny if lo is None else lo
             m = (Ls > lo_) if hi is None else ((Ls > lo_) & (Ls <= hi))
             if m.any():
-                self.plan.append((var, torch.from_numpy(order[m].copy()).to(device)))
+                o = order[m].copy()
+                if var == GS_TEAM8 and iso > 0:
+                    o = self.isolate_longest(o, min(iso, 8))
+                self.plan.append((var, torch.from_numpy(o).to(device)))
         m = Ls <= tiny
         if m.any():
             self.plan.append((GS_TINY, torch.from_numpy(order[m].copy()).to(device)))
         self.tiny_max = tiny
+
+    @staticmethod
+    def isolate_longest(o, m: int, xcds: int = 8):
+        """Workgroup order of the team8 launch giving each of its m longest documents an XCD of its own:
+        workgroup b runs on XCD b mod 8 under round-robin dispatch (a speed hint only), so slots b = x mod 8,
+        x < m, stay empty (-1) after the first round.  The longest document's packed rows then have the XCD's
+        L2 to themselves."""
+        import numpy as np
+        head, rest = list(o[:m]), list(o[m:])
+        out = []
+        b = 0
+        while head or rest:
+            if b % xcds < m:
+                out.append(head.pop(0) if head else -1)
+            else:
+                out.append(rest.pop(0) if rest else -1)
+            b += 1
+        while out and out[-1] == -1:
+            out.pop()
+        return np.asarray(out, dtype=np.int32)

@@ -40,6 +40,7 @@ def main():
     ap.add_argument("--only", default=None)
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--phases", action="store_true", help="phase timer of the longest document of each team bucket")
+    ap.add_argument("--prefixes", default="", help="also time the team8 bucket on its N longest documents, e.g. 1,2,8")
     a = ap.parse_args()
     from oni_ml_amd.models.lda.em import LDAEngine
     from oni_ml_amd.models.lda.settings import LDASettings
@@ -58,14 +59,15 @@ def main():
     names = {H.GS_TINY: "tiny", H.GS_TEAM1: "team1", H.GS_TEAM4: "team4", H.GS_TEAM8: "team8"}
     out = dict(docs=c.num_docs, nnz=c.nnz, U=eng._U, buckets=[])
 
-    def launch(var, order):
+    def launch(var, order, dbg=None):
         H.gs_estep(dc.doc_ptr, dc.word_idx, dc.counts, order, eng.beta, eng.K, eng._U, eng._params, eng.gamma,
-                   eng.cphi, eng.lik, eng.ass, eng.iters, var)
+                   eng.cphi, eng.lik, eng.ass, eng.iters, var, dbg=dbg)
 
     for var, order in eng.gs_plan.plan:
         if a.only and names[var] != a.only:
             continue
         o = order.cpu().numpy()
+        o = o[o >= 0]   # XCD placement gaps
         L = lens[o]
         ms = timed(lambda: launch(var, order), a.reps)
         it = its[o]
@@ -75,14 +77,19 @@ def main():
                                    word_sweeps=int((L * it).sum())))
         if a.phases and var != H.GS_TINY:
             dbg = torch.zeros(8, dtype=torch.int64, device="cuda")
-            H.gs_estep(dc.doc_ptr, dc.word_idx, dc.counts, order, eng.beta, eng.K, eng._U, eng._params, eng.gamma,
-                       eng.cphi, eng.lik, eng.ass, eng.iters, var, dbg=dbg)
+            launch(var, order, dbg)
             v = dbg.cpu().tolist()
             ch = max(v[7], 1)
             out["buckets"][-1]["phase_cycles_per_chunk"] = dict(
-                word=round(v[0] / ch), reduce=round(v[1] / ch), barrier1=round(v[2] / ch), topic=round(v[3] / ch),
+                word=round(v[0] / ch), word_dot=round(v[6] / ch), reduce=round(v[1] / ch), barrier1=round(v[2] / ch), topic=round(v[3] / ch),
                 barrier2=round(v[4] / ch), sweep_tail_total=v[5], chunks=v[7], doc_len=int(L.max()))
         print(json.dumps(out["buckets"][-1]), flush=True)
+        if a.prefixes and var == H.GS_TEAM8:
+            # the longest documents alone: separates the per-CU gather rate from L2 sharing between documents
+            for npre in [int(x) for x in a.prefixes.split(",")]:
+                sub = torch.from_numpy(o[:npre].copy()).to(order.device)
+                print(json.dumps(dict(kernel="team8", prefix_docs=npre, len_max=int(L.max()),
+                                      ms=round(timed(lambda: launch(var, sub), a.reps), 4))), flush=True)
     if not a.only:
         sp = eng.suff_plan
         out["suff_ms"] = round(timed(lambda: H.gs_suff64(dc.word_ptr, dc.csc_ent, sp, eng.cphi, eng.cw,
