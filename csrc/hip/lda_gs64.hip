@@ -32,6 +32,7 @@
 //             reduction of S is a row DPP reduction; cross-wave sums go through LDS in
 //             wave order (bitwise reproducible).  Topic owners (one thread per topic)
 //             run the refresh and broadcast E through LDS.
+#include <algorithm>
 #include <cstdlib>
 #include <stdexcept>
 #include <string>
@@ -344,6 +345,158 @@ __global__ __launch_bounds__(256) void gs_tiny(GSArgs a) {
     a.lik[d] = L;
     a.alpha_ss[d] = ps - K * psi_only(GS);
     a.iters[d] = it;
+  }
+}
+
+// ----------------------------------------------------------------- small ----
+// Short documents (the tiny kernel's limit < n <= kGsSmallMax words): 16 lanes per document, four
+// documents per wave, everything in registers except the per-chunk tables.  A word's P is a 16-lane
+// DPP sum (every lane holds the bitwise same value), the refresh runs in the same lanes right after
+// the chunk's last word -- no LDS, no barrier between the word and the refresh, which is what a
+// per-word schedule (n <= U: every word is a chunk) pays for in the one-wave team kernel.  The chunk
+// contributions C[j] and the E each chunk used (final pass) are per-lane private arrays (scratch).
+constexpr int kGsSmallMax = 64;
+constexpr int small_kpl(int KS) { return (KS + 15) / 16; }
+
+template <int KS>
+__global__ __launch_bounds__(256) void gs_small(GSArgs a) {
+  static_assert(KS <= 32, "small kernel: KS <= 32");
+  constexpr int TG = 16, KPL = small_kpl(KS);
+  if (a.params[kParamDone] != 0.0) return;
+  const int t = threadIdx.x, q = t & (TG - 1);
+  const int item = blockIdx.x * (256 / TG) + t / TG;
+  if (item >= a.n_items) return;   // whole 16-lane groups leave together
+  const double alpha = a.params[0], lik_const = a.params[1];
+  const int vmi = (int)a.params[2];
+  const double vconv = params_vconv(a.params);
+  const int K = a.K;
+  const int d = a.order[item];
+  const int s0 = a.doc_ptr[d], n = a.doc_ptr[d + 1] - s0;
+  const int U = a.gs_updates;
+  const int W = n > 0 ? (n + U - 1) / U : 1;
+  const int nch = (n + W - 1) / W;
+  const int* __restrict__ wrow = a.word_idx + s0;
+  const float* __restrict__ crow = a.counts + s0;
+  double C[kGsUMax][KPL], Et[kGsUMax][KPL];
+  // counts: each lane sums a stride of the document, a 16-lane sum gives the total; chunk sums serially
+  double total = 0.0;
+  for (int p = q; p < n; p += TG) total += (double)crow[p];
+  total = bits_sum<0, 4, false>(total);
+  const double g0 = alpha + total / K;
+  const double m = psi_only(g0);
+  double gam[KPL], psi[KPL], E[KPL], lps[KPL];
+  bool real[KPL];
+#pragma unroll
+  for (int i = 0; i < KPL; ++i) {
+    real[i] = q + TG * i < K;
+    gam[i] = real[i] ? g0 : 0.0;
+    psi[i] = m;
+    E[i] = real[i] ? 1.0 : 0.0;
+  }
+  for (int j = 0; j < nch; ++j) {
+    const int n0 = j * W, n1 = min(n, n0 + W);
+    double cs = 0.0;
+    for (int p = n0; p < n1; ++p) cs += (double)crow[p];   // integer counts: exact in any order
+#pragma unroll
+    for (int i = 0; i < KPL; ++i) C[j][i] = real[i] ? cs / K : 0.0;
+  }
+  // one-word-ahead prefetch of (row, count); the word order wraps into the next sweep
+  auto load_row = [&](int p, double (&b)[KPL]) {
+    const double* brow = a.beta + (size_t)wrow[p] * KS;
+#pragma unroll
+    for (int i = 0; i < KPL; ++i) b[i] = (q + TG * i < KS) ? brow[q + TG * i] : 0.0;
+  };
+  double bn[KPL];
+  double cn = 0.0;
+  if (n > 0) {
+    load_row(0, bn);
+    cn = (double)crow[0];
+  }
+  double L = 0.0, L_old = 0.0, conv = 1.0, GS = 0.0;
+  int it = 0;
+  while (var_continue(conv, vconv, it, vmi)) {
+    ++it;
+    double lw = 0.0;
+#pragma unroll
+    for (int i = 0; i < KPL; ++i) lps[i] = 0.0;
+    for (int j = 0; j < nch; ++j) {
+      const int n0 = j * W, n1 = min(n, n0 + W);
+      double acc[KPL];
+#pragma unroll
+      for (int i = 0; i < KPL; ++i) acc[i] = 0.0;
+      for (int p = n0; p < n1; ++p) {
+        double b[KPL];
+#pragma unroll
+        for (int i = 0; i < KPL; ++i) b[i] = bn[i];
+        const double c = cn;
+        const int pn = p + 1 < n ? p + 1 : 0;
+        load_row(pn, bn);
+        cn = (double)crow[pn];
+        double pp = 0.0;
+#pragma unroll
+        for (int i = 0; i < KPL; ++i) pp = fma(E[i], b[i], pp);
+        const double P = bits_sum<0, 4, false>(pp);
+        const double r = c * drcp(P);
+        lw = fma(c, flog(P), lw);
+#pragma unroll
+        for (int i = 0; i < KPL; ++i) acc[i] = fma(r, b[i], acc[i]);
+      }
+#pragma unroll
+      for (int i = 0; i < KPL; ++i) {
+        const double nw = E[i] * acc[i];
+        Et[j][i] = E[i];
+        if (real[i]) {
+          lps[i] = fma(psi[i], nw, lps[i]);
+          gam[i] += nw - C[j][i];
+          psi_exp(gam[i], m, psi[i], E[i]);
+        }
+        C[j][i] = nw;
+      }
+    }
+    double gs = 0.0, lg = 0.0, lp = 0.0;
+#pragma unroll
+    for (int i = 0; i < KPL; ++i) {
+      if (real[i]) {
+        gs += gam[i];
+        lg += lgamma_pos(gam[i]);
+        lp += lps[i];
+      }
+    }
+    GS = bits_sum<0, 4, false>(gs);
+    lg = bits_sum<0, 4, false>(lg);
+    lp = bits_sum<0, 4, false>(lp);
+    L = lik_const - lgamma_pos(GS) + lg + fma(m, total, lw) - lp;
+    conv = (L_old - L) / L_old;
+    L_old = L;
+  }
+  double ps = 0.0;
+#pragma unroll
+  for (int i = 0; i < KPL; ++i) {
+    const int k = q + TG * i;
+    if (real[i]) ps += psi[i];
+    if (k < KS) a.gamma[(size_t)d * KS + k] = gam[i];
+  }
+  ps = bits_sum<0, 4, false>(ps);
+  if (q == 0) {
+    a.lik[d] = L;
+    a.alpha_ss[d] = ps - K * psi_only(GS);
+    a.iters[d] = it;
+  }
+  // final pass: c_n phi_nk = E_jk b_nk r_n with the final sweep's chunk E
+  for (int j = 0; j < nch; ++j) {
+    const int n0 = j * W, n1 = min(n, n0 + W);
+    for (int p = n0; p < n1; ++p) {
+      double b[KPL];
+      load_row(p, b);
+      double pp = 0.0;
+#pragma unroll
+      for (int i = 0; i < KPL; ++i) pp = fma(Et[j][i], b[i], pp);
+      const double r = (double)crow[p] * drcp(bits_sum<0, 4, false>(pp));
+      double* row = a.cphi + (size_t)(s0 + p) * KS;
+#pragma unroll
+      for (int i = 0; i < KPL; ++i)
+        if (q + TG * i < KS) __builtin_nontemporal_store(Et[j][i] * b[i] * r, &row[q + TG * i]);
+    }
   }
 }
 
@@ -1427,6 +1580,14 @@ static void gs_estep_ks(const GSArgs& a, int variant, hipStream_t s) {
       hipLaunchKernelGGL((gs::gs_tiny<KS>), dim3((a.n_items + per - 1) / per), dim3(256), 0, s, a);
       break;
     }
+    case kGsSmall: {
+      if constexpr (KS <= 32) {
+        hipLaunchKernelGGL((gs::gs_small<KS>), dim3((a.n_items + 15) / 16), dim3(256), 0, s, a);
+        break;
+      } else {
+        throw std::runtime_error("gs_estep: the small-document kernel needs KS <= 32");
+      }
+    }
     case kGsTeam1: {
       // one wave per document (<= 256 words, chunks of <= 8 words): the topic-group layout keeps
       // more lanes busy than one word per lane (measured 0.90 vs 1.13 ms on the headline corpus)
@@ -1435,8 +1596,13 @@ static void gs_estep_ks(const GSArgs& a, int variant, hipStream_t s) {
       break;
     }
     case kGsTeam4:
-      if constexpr (KS <= 32)
-        hipLaunchKernelGGL((gs::gs_wteam<KS, 4, 1>), dim3(a.n_items), dim3(256), 0, s, a);
+      if constexpr (KS <= 32) {
+        static const int mnw = std::getenv("ONI_GS_MID_NW") ? std::atoi(std::getenv("ONI_GS_MID_NW")) : 3;
+        if (mnw == 3)   // 3 word waves + the topic wave
+          hipLaunchKernelGGL((gs::gs_wsteam<KS, 3, 1>), dim3(a.n_items), dim3(256), 0, s, a);
+        else
+          hipLaunchKernelGGL((gs::gs_wteam<KS, 4, 1>), dim3(a.n_items), dim3(256), 0, s, a);
+      }
       else
         hipLaunchKernelGGL((gs::gs_team<KS, 4>), dim3(a.n_items), dim3(256), 0, s, a);
       break;

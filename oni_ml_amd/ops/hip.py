@@ -523,7 +523,8 @@ def bin_columns(values, cuts):
 # ------------------------------------------------------- fp64 block Gauss-Seidel ---
 # lda-c-faithful E-step (csrc/hip/lda_gs64.hip): double everywhere, gamma refreshed after every
 # chunk of ceil(n / gs_updates) words (documents of <= gs_updates words: lda-c's per-word schedule).
-GS_TINY, GS_TEAM1, GS_TEAM4, GS_TEAM8 = range(4)
+GS_TINY, GS_TEAM1, GS_TEAM4, GS_TEAM8, GS_SMALL = range(5)
+GS_SMALL_MAX = 64   # csrc/hip/lda_gs64.hip kGsSmallMax
 
 
 def gs_umax() -> int:
@@ -547,7 +548,7 @@ def gs_estep(doc_ptr, word_idx, counts, order, beta, K, gs_updates, params, gamm
         raise ValueError("K out of range")
     if not (1 <= int(gs_updates) <= gs_umax()):
         raise ValueError(f"gs_updates must be in [1, {gs_umax()}]")
-    if variant not in (GS_TINY, GS_TEAM1, GS_TEAM4, GS_TEAM8):
+    if variant not in (GS_TINY, GS_TEAM1, GS_TEAM4, GS_TEAM8, GS_SMALL):
         raise ValueError(f"unknown gs variant {variant}")
     dev = beta.device
     args = [
@@ -627,6 +628,9 @@ class GSPlan:
     tiny (TG lanes per document, literal schedule) for n <= min(gs_tiny_max(KS), U); one wave per
     document up to 256 words; a 4-wave workgroup up to 2048; an 8-wave workgroup beyond."""
     EDGES = ((GS_TEAM8, 2048, None), (GS_TEAM4, 256, 2048), (GS_TEAM1, None, 256))
+    # KS <= 32: documents up to GS_SMALL_MAX words go to the 16-lanes-per-document kernel
+    EDGES_NARROW = ((GS_TEAM8, 2048, None), (GS_TEAM4, 256, 2048), (GS_TEAM1, GS_SMALL_MAX, 256),
+                    (GS_SMALL, None, GS_SMALL_MAX))
 
     def __init__(self, lengths, KS: int, gs_updates: int, device):
         import numpy as np
@@ -636,14 +640,16 @@ class GSPlan:
         tiny = min(gs_tiny_max(KS), int(gs_updates))
         self.plan = []
         iso = int(os.environ.get("ONI_GS_XCD", "1")) if KS <= 32 else 0
-        for var, lo, hi in self.EDGES:
+        edges = self.EDGES_NARROW if KS <= 32 and os.environ.get("ONI_GS_SMALL", "1") != "0" else self.EDGES
+        for var, lo, hi in edges:
             lo_ = tiny if lo is None else lo
             m = (Ls > lo_) if hi is None else ((Ls > lo_) & (Ls <= hi))
-            if m.any():
-                o = order[m].copy()
-                if var == GS_TEAM8 and iso > 0:
-                    o = self.isolate_longest(o, min(iso, 8))
-                self.plan.append((var, torch.from_numpy(o).to(device)))
+            if not m.any():
+                continue
+            o = order[m].copy()
+            if var == GS_TEAM8 and iso > 0:
+                o = self.isolate_longest(o, min(iso, 8))
+            self.plan.append((var, torch.from_numpy(o).to(device)))
         m = Ls <= tiny
         if m.any():
             self.plan.append((GS_TINY, torch.from_numpy(order[m].copy()).to(device)))

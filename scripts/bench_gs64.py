@@ -56,7 +56,7 @@ def main():
     dc = eng.dc
     lens = c.lengths()
     its = eng.iters.cpu().numpy()
-    names = {H.GS_TINY: "tiny", H.GS_TEAM1: "team1", H.GS_TEAM4: "team4", H.GS_TEAM8: "team8"}
+    names = {H.GS_TINY: "tiny", H.GS_TEAM1: "team1", H.GS_TEAM4: "team4", H.GS_TEAM8: "team8", H.GS_SMALL: "small"}
     out = dict(docs=c.num_docs, nnz=c.nnz, U=eng._U, buckets=[])
 
     def launch(var, order, dbg=None):
@@ -75,7 +75,7 @@ def main():
                                    entries=int(L.sum()), sweeps_mean=round(float(it.mean()), 2),
                                    sweeps_max=int(it.max()), ms=round(ms, 4),
                                    word_sweeps=int((L * it).sum())))
-        if a.phases and var != H.GS_TINY:
+        if a.phases and var not in (H.GS_TINY, H.GS_SMALL):
             dbg = torch.zeros(8, dtype=torch.int64, device="cuda")
             launch(var, order, dbg)
             v = dbg.cpu().tolist()
