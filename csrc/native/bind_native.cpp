@@ -294,7 +294,7 @@ PYBIND11_MODULE(_oninative, m) {
       "write_ldac_corpus",
       [](const std::string& path, py::array_t<int64_t, py::array::c_style | py::array::forcecast> ptr,
          py::array_t<int32_t, py::array::c_style | py::array::forcecast> words,
-         py::array_t<int64_t, py::array::c_style | py::array::forcecast> counts, int threads) {
+         py::array_t<int64_t, py::array::c_style | py::array::forcecast> counts, int threads, bool assignments) {
         const int64_t D = (int64_t)ptr.size() - 1;
         if (D < 0) throw std::invalid_argument("doc_ptr must have D+1 entries");
         const int64_t* p = ptr.data();
@@ -304,9 +304,13 @@ PYBIND11_MODULE(_oninative, m) {
           if (p[d] > p[d + 1]) throw std::invalid_argument("non-monotone doc_ptr");
         if (threads <= 0) threads = default_threads();
         py::gil_scoped_release rel;
-        return write_corpus_text(path, p, D, words.data(), counts.data(), threads);
+        if (assignments)
+          for (int64_t i = 0; i < (int64_t)counts.size(); ++i)
+            if (counts.data()[i] < 0 || words.data()[i] < 0) throw std::invalid_argument("negative word or topic");
+        return write_corpus_text(path, p, D, words.data(), counts.data(), threads, assignments);
       },
-      py::arg("path"), py::arg("doc_ptr"), py::arg("words"), py::arg("counts"), py::arg("threads") = 0);
+      py::arg("path"), py::arg("doc_ptr"), py::arg("words"), py::arg("counts"), py::arg("threads") = 0,
+      py::arg("assignments") = false);
   m.def(
       "read_ldac_corpus",
       [](const std::string& path, int threads) {

@@ -17,6 +17,14 @@ inline void put_int(std::string& s, int64_t v) {
   s.append(b, r.ptr - b);
 }
 
+// printf "%0<W>d" for v >= 0
+inline void put_int_pad(std::string& s, int64_t v, int width) {
+  char b[24];
+  auto r = std::to_chars(b, b + sizeof(b), v);
+  for (int64_t k = r.ptr - b; k < width; ++k) s += '0';
+  s.append(b, r.ptr - b);
+}
+
 template <typename F>
 void parallel_for(int threads, F&& f) {
   if (threads <= 1) { f(0); return; }
@@ -29,7 +37,7 @@ void parallel_for(int threads, F&& f) {
 }  // namespace
 
 int64_t write_corpus_text(const std::string& path, const int64_t* ptr, int64_t D, const int32_t* w,
-                          const int64_t* c, int threads) {
+                          const int64_t* c, int threads, bool assignments) {
   FILE* f = std::fopen(path.c_str(), "wb");
   if (!f) throw std::runtime_error("cannot open for writing: " + path);
   threads = std::max(1, threads);
@@ -52,12 +60,22 @@ int64_t write_corpus_text(const std::string& path, const int64_t* ptr, int64_t D
       std::string& s = bufs[t];
       s.clear();
       for (int64_t d = cuts[b0 + t]; d < cuts[b0 + t + 1]; ++d) {
-        put_int(s, ptr[d + 1] - ptr[d]);
-        for (int64_t i = ptr[d]; i < ptr[d + 1]; ++i) {
-          s += ' ';
-          put_int(s, w[i]);
-          s += ':';
-          put_int(s, c[i]);
+        if (assignments) {
+          put_int_pad(s, ptr[d + 1] - ptr[d], 3);
+          for (int64_t i = ptr[d]; i < ptr[d + 1]; ++i) {
+            s += ' ';
+            put_int_pad(s, w[i], 4);
+            s += ':';
+            put_int_pad(s, c[i], 2);
+          }
+        } else {
+          put_int(s, ptr[d + 1] - ptr[d]);
+          for (int64_t i = ptr[d]; i < ptr[d + 1]; ++i) {
+            s += ' ';
+            put_int(s, w[i]);
+            s += ':';
+            put_int(s, c[i]);
+          }
         }
         s += '\n';
       }

@@ -13,9 +13,11 @@ struct TextCorpus {
   std::vector<int64_t> counts;
 };
 
-// Writes D lines; returns the number of bytes written.
+// Writes D lines; returns the number of bytes written.  assignments = false: model.dat
+// ("%d" length, " %d:%d" word:count); true: lda-c's word-assignments.dat ("%03d" length,
+// " %04d:%02d" word:topic, write_word_assignment).
 int64_t write_corpus_text(const std::string& path, const int64_t* doc_ptr, int64_t D, const int32_t* words,
-                          const int64_t* counts, int threads);
+                          const int64_t* counts, int threads, bool assignments = false);
 
 // Parses a model.dat file.  Blank lines are skipped; a line whose declared
 // entry count differs from its w:c pairs throws std::runtime_error.

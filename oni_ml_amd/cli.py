@@ -66,8 +66,11 @@ def cmd_ml_ops(argv):
     ap.add_argument("--start", default="random")
     ap.add_argument("--resume", action="store_true")
     ap.add_argument("--keep-doc-wc", action="store_true", help="keep doc_wc.dat (the reference deletes it)")
-    ap.add_argument("--word-assignments", action="store_true")
-    ap.add_argument("--rank-gamma", action="store_true", help="also write <rank>.gamma per GPU")
+    ap.add_argument("--word-assignments", dest="word_assignments", action="store_true", default=True,
+                    help="write word-assignments.dat (default, as lda-c does on every run)")
+    ap.add_argument("--no-word-assignments", dest="word_assignments", action="store_false")
+    ap.add_argument("--rank-gamma", action="store_true", default=None,
+                    help="write <rank>.gamma / <rank>.beta per GPU (default: on when running on several GPUs)")
     ap.add_argument("--threads", type=int, default=8)
     ap.add_argument("--deliver", action="store_true", help="scp -r LPATH UINODE:RPATH (ml_ops.sh:121)")
     ap.add_argument("--cuts", help="fixed flow cuts: a flow_qtiles file or its text (the reference's CUT)")
@@ -135,7 +138,8 @@ def cmd_lda(argv):
         for n in ("alpha", "k", "settings", "nproc", "data", "start", "directory"):
             ap.add_argument(n)
         ap.add_argument("--resume", action="store_true")
-        ap.add_argument("--word-assignments", action="store_true", default=True)
+        ap.add_argument("--word-assignments", dest="word_assignments", action="store_true", default=True)
+        ap.add_argument("--no-word-assignments", dest="word_assignments", action="store_false")
         _common_lda_args(ap)
         a = ap.parse_args(argv[1:])
         from .models.lda.estimate import estimate

@@ -94,8 +94,8 @@ class RunConfig:
     resume: bool = False
     threads: int = 8
     write_doc_wc: bool = True
-    word_assignments: bool = False
-    rank_gamma: bool = False
+    word_assignments: bool = True          # lda-c writes word-assignments.dat on every `lda est`
+    rank_gamma: Optional[bool] = None      # <rank>.gamma / <rank>.beta; None: on for multi-rank runs
     verbose: bool = True
     cuts: str = ""                        # fixed flow cuts in flow_qtiles form ("ibyt,ipkt,time"; the
                                           # reference's commented-out CUT consumer, flow_pre_lda.scala:95-98)

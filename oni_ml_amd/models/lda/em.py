@@ -723,7 +723,7 @@ class LDAEngine:
                 red = torch.cat([sc.to(torch.float64), self.cw.sum(0, dtype=torch.float64)])
                 tok = self._comm_begin()
                 work = td.all_reduce(red, async_op=True)
-                local = self.cw
+                local = self._cw_local = self.cw
                 self._xchg.pack(local)
                 self._xchg.exchange()
                 self.cw = torch.zeros_like(local)     # rows of other ranks' words stay 0 (global_rows masks)
@@ -737,6 +737,7 @@ class LDAEngine:
                     self.alpha = special.opt_alpha(float(host[1]), num_docs, self.K)
                 return float(host[0]), float(host[1])
             if self.dist is not None and self.dist.world_size > 1:
+                self._cw_local = self.cw.clone()     # this rank's own rows (<rank>.beta)
                 tok = self._comm_begin()
                 sc = self.dist.allreduce_suffstats(self.cw, sc)
                 self._comm_end(tok)
@@ -1001,6 +1002,15 @@ class LDAEngine:
         sparse exchange unless ``cw`` (a ``global_cw()`` result) is given."""
         cw = (self.global_cw() if cw is None else cw)[:, :self.K].double()
         ct = self.class_total[:self.K]
+        lb = torch.where(cw > 0, torch.log(cw) - torch.log(ct), torch.full_like(cw, LOG_FLOOR))
+        return lb.T.contiguous().cpu().numpy()
+
+    def local_log_beta(self) -> np.ndarray:
+        """[K, V] log of this rank's own class_word rows over the GLOBAL class totals (-100 floor):
+        the per-worker ``<rank>.beta`` (README.md:121), final.beta = log(sum over ranks of exp)."""
+        local = getattr(self, "_cw_local", None)
+        cw = (self.cw if local is None else local)[:, :self.K].double()
+        ct = self.class_total[:self.K].to(cw.device)
         lb = torch.where(cw > 0, torch.log(cw) - torch.log(ct), torch.full_like(cw, LOG_FLOOR))
         return lb.T.contiguous().cpu().numpy()
 

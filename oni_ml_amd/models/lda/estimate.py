@@ -7,8 +7,10 @@ Reference call site: ``mpiexec -n 20 -f machinefile ./lda est 2.5 20 settings.tx
   %03d.beta/.other/.gamma   every LAG=5 iterations
   final.beta/.other/.gamma  at convergence
   likelihood.dat            "%10.10f\\t%5.5e" per EM iteration
-  word-assignments.dat      (optional) per-word argmax topic under the final model
-  <rank>.gamma              (optional) each rank's contiguous gamma block
+  word-assignments.dat      per-word argmax topic under the final model (lda-c writes it on every run)
+  <rank>.gamma / <rank>.beta  (multi-rank runs; opt-in on one) each rank's gamma block and the log of
+                            its local class_word rows over the global class totals, so
+                            final.beta = log(sum_r exp(<r>.beta)) (README.md:121 "<worker index>.beta")
 
 plus ``checkpoint.npz`` every LAG iterations (log beta, alpha, iteration,
 likelihood history, VAR_MAX_ITER, RNG-free) for exact ``--resume``.
@@ -168,6 +170,7 @@ def estimate(corpus: Corpus, num_topics: int, alpha_init: float, settings: LDASe
         if write_rank_gamma and tag == "final":
             r = 0 if dist is None else dist.rank
             writer.submit(ldac.save_gamma, os.path.join(outdir, f"{r}.gamma"), e.local_gamma())
+            writer.submit(ldac.save_beta, os.path.join(outdir, f"{r}.beta"), e.local_log_beta())
         if not rank0:
             return
         writer.submit(ldac.save_model, os.path.join(outdir, tag), lb, e.alpha)
@@ -197,7 +200,13 @@ def estimate(corpus: Corpus, num_topics: int, alpha_init: float, settings: LDASe
     res.log_beta = eng.log_beta()
     res.gamma = eng.gather_gamma()
     if write_word_assignments and rank0:
-        write_assignments(os.path.join(outdir, "word-assignments.dat"), corpus, res.log_beta, res.gamma)
+        # argmax on the device now; the text formatting joins the deferred model files when allowed
+        z = word_topics(corpus, res.log_beta, res.gamma, device=eng.cw.device)
+        wa = os.path.join(outdir, "word-assignments.dat")
+        if ok and defer_files:
+            writer.submit(_write_assignment_file, wa, corpus, z)
+        else:
+            _write_assignment_file(wa, corpus, z)
     if rank0:
         with open(os.path.join(outdir, "lda_stats.json"), "w") as f:
             json.dump(dict(em_iterations=res.em_iterations, seconds=res.seconds, alpha=res.alpha,
@@ -208,12 +217,41 @@ def estimate(corpus: Corpus, num_topics: int, alpha_init: float, settings: LDASe
     return res
 
 
-def write_assignments(path: str, corpus: Corpus, log_beta: np.ndarray, gamma: np.ndarray):
-    """word-assignments.dat: per doc ``%03d`` length then `` %04d:%02d`` word:argmax-topic.
+def word_topics(corpus: Corpus, log_beta: np.ndarray, gamma: np.ndarray, device=None,
+                chunk: int = 1 << 22) -> np.ndarray:
+    """Per corpus entry argmax_k (psi(gamma_dk) + log beta_{k,w}) as int64 [nnz] (first maximum on ties).
 
-    The argmax of φ_nk ∝ exp(ψ(γ_k)) β_{k,w} is argmax_k (ψ(γ_k) + log β_{k,w}) (lda-c write_word_assignment)."""
+    The argmax of phi_nk ~ exp(psi(gamma_k)) beta_{k,w} (lda-c write_word_assignment); evaluated on
+    the engine's device in chunks of ``chunk`` entries ([chunk, K] doubles at a time)."""
     from .special import digamma
-    psi = digamma(gamma)                                  # [D, K]
+    dev = torch.device(device) if device is not None else torch.device("cpu")
+    psi = digamma(torch.from_numpy(np.ascontiguousarray(gamma, np.float64)).to(dev))       # [D, K]
+    lbt = torch.from_numpy(np.ascontiguousarray(log_beta.T, np.float64)).to(dev)           # [V, K]
+    lens = torch.from_numpy(corpus.lengths().astype(np.int64)).to(dev)
+    doc_of = torch.repeat_interleave(torch.arange(corpus.num_docs, device=dev), lens)
+    w = torch.from_numpy(corpus.word_idx.astype(np.int64)).to(dev)
+    z = torch.empty(corpus.nnz, dtype=torch.int64, device=dev)
+    for a in range(0, corpus.nnz, chunk):
+        b = min(corpus.nnz, a + chunk)
+        z[a:b] = torch.argmax(psi[doc_of[a:b]] + lbt[w[a:b]], dim=1)
+    return z.cpu().numpy()
+
+
+def write_assignments(path: str, corpus: Corpus, log_beta: np.ndarray, gamma: np.ndarray, device=None):
+    """word-assignments.dat: per doc ``%03d`` length then `` %04d:%02d`` word:argmax-topic
+    (lda-c write_word_assignment), formatted by the multithreaded native corpus writer."""
+    _write_assignment_file(path, corpus, word_topics(corpus, log_beta, gamma, device))
+
+
+def _write_assignment_file(path: str, corpus: Corpus, z: np.ndarray):
+    from ...ops import native
+    native.lib().write_ldac_corpus(path, corpus.doc_ptr, corpus.word_idx, z, assignments=True)
+
+
+def write_assignments_reference(path: str, corpus: Corpus, log_beta: np.ndarray, gamma: np.ndarray):
+    """Literal per-document loop (test oracle for write_assignments)."""
+    from .special import digamma
+    psi = digamma(gamma)
     with open(path, "w") as f:
         for d in range(corpus.num_docs):
             a, b = corpus.doc_ptr[d], corpus.doc_ptr[d + 1]

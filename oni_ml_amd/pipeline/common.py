@@ -52,7 +52,9 @@ def run_lda(cfg, corpus: Corpus, dist=None, device=None, log=print):
         ldac.write_settings(settings_path, cfg.settings)
     return estimate(corpus, cfg.topics, cfg.alpha, cfg.settings, cfg.start, outdir, backend=cfg.backend,
                     device=device, dist=dist, seed=cfg.seed, resume=cfg.resume,
-                    write_word_assignments=cfg.word_assignments, write_rank_gamma=cfg.rank_gamma,
+                    write_word_assignments=cfg.word_assignments,
+                    write_rank_gamma=(cfg.rank_gamma if cfg.rank_gamma is not None
+                                      else dist is not None and dist.world_size > 1),
                     verbose=cfg.verbose, fault_at_iteration=cfg.extra.get("fault_at_iteration"),
                     defer_files=dist is None or dist.world_size <= 1)
 

@@ -96,6 +96,17 @@ def test_two_rank_em_matches_single_rank(tmp_path, exchange):
     # per-rank gamma blocks concatenate to final.gamma (README.md:121)
     parts = np.concatenate([np.atleast_2d(np.loadtxt(tmp_path / "w2" / f"{r}.gamma")) for r in range(2)])
     assert np.allclose(parts, g2, atol=1e-9)
+    # per-rank <rank>.beta: log of the rank's own class_word over the global totals, so the ranks'
+    # probabilities sum to final.beta's
+    from oni_ml_amd.io import ldac
+    fb = ldac.load_beta(str(tmp_path / "w2" / "final.beta"))
+    rb = [ldac.load_beta(str(tmp_path / "w2" / f"{r}.beta")) for r in range(2)]
+    assert all(b.shape == fb.shape for b in rb)
+    comb = np.log(np.exp(rb[0]) + np.exp(rb[1]))
+    live = fb > -99
+    assert live.any() and np.allclose(comb[live], fb[live], atol=1e-8)
+    if exchange == "sparse":   # disjoint-ish vocabularies: each rank misses words the other has
+        assert (rb[0] == -100).sum() > 0 and (rb[1] == -100).sum() > 0
 
 
 def test_bench_two_rank_cpu_rehearsal():

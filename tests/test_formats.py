@@ -231,3 +231,23 @@ def test_fast_formatting_matches_exact(mode):
     for a in sets:
         a = a[np.isfinite(a)]
         assert N.fmt_selfcheck(a, mode) == (0, 0, -1)
+
+
+def test_word_assignments_native_matches_loop(tmp_path):
+    """word-assignments.dat (lda-c write_word_assignment: "%03d" then " %04d:%02d") from the device
+    argmax + native writer equals the literal per-document loop, incl. words >= 10^4 and docs >= 10^3."""
+    from oni_ml_amd.corpus.csr import Corpus
+    from oni_ml_amd.models.lda.estimate import write_assignments, write_assignments_reference
+    rng = np.random.default_rng(3)
+    V, K = 12_000, 7
+    lens = np.r_[rng.integers(1, 30, 200), [1500]]
+    ptr = np.concatenate([[0], np.cumsum(lens)])
+    words = np.concatenate([np.sort(rng.choice(V, n, replace=False)) for n in lens]).astype(np.int32)
+    c = Corpus(ptr, words, np.ones(len(words), np.int64), V)
+    log_beta = np.log(rng.dirichlet(np.ones(V), K))
+    gamma = rng.gamma(2.0, 3.0, (len(lens), K))
+    write_assignments(str(tmp_path / "a.dat"), c, log_beta, gamma)
+    write_assignments_reference(str(tmp_path / "b.dat"), c, log_beta, gamma)
+    a, b = (tmp_path / "a.dat").read_text(), (tmp_path / "b.dat").read_text()
+    assert a == b
+    assert a.splitlines()[-1].startswith("1500 ") and " 11" in a
