@@ -220,6 +220,12 @@ struct GSArgs {
 };
 void launch_gs_estep(const GSArgs& a, int variant, int KS, hipStream_t s);
 int gs_tiny_max(int KS);   // longest document of the kGsTiny kernel
+// One long document over s.seg_count[b] workgroups (8 waves each): every chunk is cut into
+// that many word ranges whose partials are exchanged as tagged granules (2 per double,
+// s.xchg = [2][n_blocks][2 (KS + 1)]); s.seg_words is unused.  Every segment of a launch
+// must be co-resident: n_blocks <= gs_split_capacity(KS) (the host keeps a margin).
+void launch_gs_split(const GSArgs& a, const SplitArgs& s, int KS, hipStream_t st);
+int gs_split_capacity(int KS);
 
 // class_word[w] = sum over w's CSC entries of cphi rows (fixed order, no atomics); part
 // [nb][2 + KS] per-workgroup {lik slice, alpha_ss slice, column sums} for colsum_partials.

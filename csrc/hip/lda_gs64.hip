@@ -40,6 +40,7 @@
 #include "alpha_newton.h"
 #include "common.h"
 #include "em_control.h"
+#include "estep_common.h"
 #include "kernels.h"
 
 namespace oni {
@@ -551,13 +552,44 @@ __device__ __forceinline__ void word_steps(const double (&E)[KPL], const double 
   }
 }
 
+// RMAX streamed words of one slot (p0, p0 + NS, ...; past `end` counts 0 and re-reads a valid row):
+// ids, then rows, then the word steps, so a batch costs about one gather latency
+template <int RMAX, int KS, int KPL, int TG, int LSW>
+__device__ __forceinline__ void stream_batch(const double* __restrict__ beta, const int* __restrict__ wrow,
+                                             const float* __restrict__ crow, int p0, int end, int NS, int q,
+                                             const double (&E)[KPL], double (&b)[RMAX][KPL], double (&acc)[KPL],
+                                             double& lw) {
+  int w[RMAX];
+  double c[RMAX];
+#pragma unroll
+  for (int r = 0; r < RMAX; ++r) {
+    const int p = p0 + r * NS;
+    const int pc = min(p, end - 1);
+    w[r] = wrow[pc];
+    c[r] = p < end ? (double)crow[pc] : 0.0;
+  }
+#pragma unroll
+  for (int r = 0; r < RMAX; ++r) {
+    const double* brow = beta + (size_t)w[r] * KS;
+#pragma unroll
+    for (int i = 0; i < KPL; ++i) b[r][i] = brow[min(q + TG * i, KS - 1)];
+  }
+  word_steps<RMAX, KPL, LSW>(E, b, c, acc, lw);
+}
+
 template <int KS, int NW>
 __global__ __launch_bounds__(team_threads(KS, NW)) void gs_team(GSArgs a) {
   using T = TeamShape<KS, NW>;
   constexpr int DPB = T::DPB, NTD = T::NTD, TG = T::TG, KPL = T::KPL, NSW = T::NSW, LSW = T::LSW, NS = T::NS,
                 TO = T::TO, RMAX = T::RMAX;
-  __shared__ double sC[DPB][kGsUMax][KS];    // chunk contributions (previous sweep)
-  __shared__ double sEt[DPB][kGsUMax][KS];   // E each chunk used (final pass)
+  // GM (one-wave documents, KS > 32): the chunk tables live in the document's own c*phi rows
+  // instead of LDS (2 x 32 x KS doubles of LDS held one wave per CU to ~3 waves): C_j in row
+  // j W, the E chunk j used in row j W + 1 (chunks of >= 2 words).  A one-word chunk's C_j IS
+  // that word's c*phi (E_j r b), so documents of <= U words need no final pass at all.
+  constexpr bool GM = (NW == 1 && KS > 32);
+  constexpr int UT = GM ? 1 : kGsUMax;
+  __shared__ double sC[DPB][UT][KS];         // chunk contributions (previous sweep)
+  __shared__ double sEt[DPB][UT][KS];        // E each chunk used (final pass)
   __shared__ double sE[DPB][KS];             // current E, broadcast
   __shared__ double sRed[DPB][NW][KS];       // per-wave slot sums
   __shared__ double sCs[DPB][kGsUMax];       // chunk count sums
@@ -604,7 +636,20 @@ __global__ __launch_bounds__(team_threads(KS, NW)) void gs_team(GSArgs a) {
     lps[o] = 0.0;
     if (k < KS) {
       E_[k] = k < K ? 1.0 : 0.0;
-      for (int j = 0; j < nch; ++j) C[j][k] = k < K ? Cs[j] / K : 0.0;
+      if constexpr (GM) {
+        for (int j = 0; j < nch; ++j) a.cphi[(size_t)(s0 + j * W) * KS + k] = k < K ? Cs[j] / K : 0.0;
+      } else {
+        for (int j = 0; j < nch; ++j) C[j][k] = k < K ? Cs[j] / K : 0.0;
+      }
+    }
+  }
+  // GM: C of the next chunk, loaded one chunk ahead (this thread wrote it: same-address order)
+  double Cn[TO];
+  if constexpr (GM) {
+#pragma unroll
+    for (int o = 0; o < TO; ++o) {
+      const int k = t + NTD * o;
+      Cn[o] = (k < KS && nch > 0) ? a.cphi[(size_t)s0 * KS + k] : 0.0;
     }
   }
   // chunk-ahead prefetch: the word ids of chunk j + 2 and the beta rows of chunk j + 1 are in
@@ -684,15 +729,11 @@ __global__ __launch_bounds__(team_threads(KS, NW)) void gs_team(GSArgs a) {
         } else {
           word_steps<2, KPL, LSW>(E, bc, cr, acc, lw);
         }
-        // words beyond the prefetched rounds (documents longer than RMAX * NS * U): streamed
-        for (int p = n0 + slot + RMAX * NS; p < n1; p += NS) {
-          const double* brow = a.beta + (size_t)wrow[p] * KS;
-          double b[1][KPL];
-#pragma unroll
-          for (int i = 0; i < KPL; ++i) b[0][i] = brow[min(q + TG * i, KS - 1)];
-          const double cp = (double)crow[p];
-          word_steps<1, KPL, LSW>(E, b, &cp, acc, lw);
-        }
+        // words beyond the prefetched rounds (documents longer than RMAX * NS * U): streamed in
+        // batches of RMAX rows per slot with a batch's loads in flight together (bc is free until
+        // the next chunk's prefetch below); one row at a time left the word phase latency-bound
+        for (int pb = n0 + slot + RMAX * NS; pb < n1; pb += RMAX * NS)
+          stream_batch<RMAX, KS, KPL, TG, LSW>(a.beta, wrow, crow, pb, n1, NS, q, E, bc, acc, lw);
         // next chunk's rows (ids already here), then the ids after it
         const int j1 = j + 1 < nch ? j + 1 : 0;
         const int j2 = j1 + 1 < nch ? j1 + 1 : 0;
@@ -727,13 +768,26 @@ __global__ __launch_bounds__(team_threads(KS, NW)) void gs_team(GSArgs a) {
           const double Eo = E_[k];
           const double nw = Eo * S;
           double En = 0.0;
-          if (k < K) {
-            lps[o] = fma(psi[o], nw, lps[o]);
-            gam[o] += nw - C[j][k];
-            psi_exp(gam[o], m, psi[o], En);
+          if constexpr (GM) {
+            if (k < K) {
+              lps[o] = fma(psi[o], nw, lps[o]);
+              gam[o] += nw - Cn[o];
+              psi_exp(gam[o], m, psi[o], En);
+            }
+            double* crw = a.cphi + (size_t)(s0 + j * W) * KS;
+            crw[k] = nw;
+            if (min(n, (j + 1) * W) - j * W >= 2) crw[KS + k] = Eo;
+            const int j1 = j + 1 < nch ? j + 1 : 0;
+            Cn[o] = a.cphi[(size_t)(s0 + j1 * W) * KS + k];
+          } else {
+            if (k < K) {
+              lps[o] = fma(psi[o], nw, lps[o]);
+              gam[o] += nw - C[j][k];
+              psi_exp(gam[o], m, psi[o], En);
+            }
+            C[j][k] = nw;
+            Et[j][k] = Eo;
           }
-          C[j][k] = nw;
-          Et[j][k] = Eo;
           E_[k] = En;
         }
       }
@@ -800,8 +854,17 @@ __global__ __launch_bounds__(team_threads(KS, NW)) void gs_team(GSArgs a) {
   for (int j = 0; j < nch; ++j) {
     const int n0 = j * W, n1 = min(n, n0 + W);
     double E[KPL];
+    if constexpr (GM) {
+      // one-word chunk: its c*phi row already holds C_j; else E_j from row n0 + 1, read by the
+      // whole wave before any lane overwrites the chunk's rows (the stores depend on the loads)
+      if (n1 - n0 < 2) continue;
+      const double* er = a.cphi + (size_t)(s0 + n0 + 1) * KS;
 #pragma unroll
-    for (int i = 0; i < KPL; ++i) E[i] = (q + TG * i < KS) ? Et[j][q + TG * i] : 0.0;
+      for (int i = 0; i < KPL; ++i) E[i] = (q + TG * i < KS) ? er[q + TG * i] : 0.0;
+    } else {
+#pragma unroll
+      for (int i = 0; i < KPL; ++i) E[i] = (q + TG * i < KS) ? Et[j][q + TG * i] : 0.0;
+    }
     for (int p = n0 + slot; p < n1; p += NS) {
       const double* brow = a.beta + (size_t)wrow[p] * KS;
       const double c = (double)crow[p];
@@ -816,6 +879,337 @@ __global__ __launch_bounds__(team_threads(KS, NW)) void gs_team(GSArgs a) {
 #pragma unroll
       for (int i = 0; i < KPL; ++i)
         if (q + TG * i < KS) __builtin_nontemporal_store(E[i] * b[i] * r, &row[q + TG * i]);
+    }
+  }
+}
+
+// ----------------------------------------------------------------- split ----
+// One long document over G workgroups (the fp64 block Gauss-Seidel analogue of
+// lda_estep_split.hip).  Chunk j of a sweep (W = ceil(n / U) words) is
+// cut into G contiguous ranges of ceil(W / G) words; workgroup g gathers and reduces its
+// range's S_k = sum_n r_n b_nk and sum_n c_n log P_n, publishes them, and reads all G
+// partials back in segment order (the same bits in every workgroup), so the G replicas of
+// (gamma, psi, E, C) run the identical refresh and the identical lda-c convergence test:
+// one exchange per chunk and no second barrier.  A double travels as two tagged 8-byte
+// granules {uint32 half, uint32 tag} (relaxed agent-scope 64-bit stores / loads are
+// single-copy atomic); tag = (launch epoch, chunk sequence number) and the parity
+// double-buffer are as in the fp32 split kernel (estep_common.h): a workgroup reuses buffer
+// (seq & 1) at seq + 2 only after every segment has published seq + 1, i.e. after every
+// segment has finished reading seq.  The host caps a launch at the co-resident capacity
+// (gs_split_capacity), so the exchange cannot deadlock; a bounded wait sets `error`.
+__device__ __forceinline__ void put_tagged_bits(unsigned long long* p, unsigned v, unsigned tag) {
+  __hip_atomic_store(p, ((unsigned long long)tag << 32) | (unsigned long long)v, __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// sum_{q < n} of the double at granules (x[q * stride], x[q * stride + 1]) = (lo, hi) bits,
+// in order q = 0, 1, ...; 4 segments (8 granules) in flight per round trip.  False on a timeout.
+__device__ __forceinline__ bool tagged_sum_f64(const unsigned long long* x, int n, int stride, unsigned tag,
+                                               double& out) {
+  double s = 0.0;
+  long spins = 0;
+  for (int q0 = 0; q0 < n; q0 += 4) {
+    unsigned long long v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      v[u] = __hip_atomic_load(x + (size_t)min(q0 + u / 2, n - 1) * stride + (u & 1), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      if (q0 + u / 2 >= n) continue;
+      while ((unsigned)(v[u] >> 32) != tag) {
+        if (++spins > kSplitSpinLimit) {
+          out = __builtin_nan("");
+          return false;
+        }
+        __builtin_amdgcn_s_sleep(1);
+        v[u] = __hip_atomic_load(x + (size_t)(q0 + u / 2) * stride + (u & 1), __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 8; u += 2)
+      if (q0 + u / 2 < n)
+        s += __longlong_as_double((long long)(((v[u + 1] & 0xffffffffull) << 32) | (v[u] & 0xffffffffull)));
+  }
+  out = s;
+  return true;
+}
+
+template <int KS>
+__global__ __launch_bounds__(512) void gs_split(GSArgs a, SplitArgs sp) {
+  using T = TeamShape<KS, 8>;
+  constexpr int NW = 8, NTD = T::NTD, TG = T::TG, KPL = T::KPL, NSW = T::NSW, LSW = T::LSW, NS = T::NS,
+                TO = T::TO, RMAX = T::RMAX;
+  constexpr int NC = KS + 1;                 // exchanged columns: KS topic sums + the log-sum
+  constexpr int GR = 2 * NC;                 // granules per segment row
+  // NP gatherer threads per column, each summing a fixed contiguous range of the segments (one
+  // polling round trip for G <= 4 NP instead of one per 4 segments); the column's owner adds the
+  // NP partials in order, so every workgroup still gets the same bits
+  constexpr int NP = (NTD / NC) < 8 ? (NTD / NC) : 8;
+  static_assert(NP >= 1, "one exchange thread per topic plus one for the log-sum");
+  __shared__ double sC[kGsUMax][KS];
+  __shared__ double sEt[kGsUMax][KS];
+  __shared__ double sE[KS];
+  __shared__ double sRed[NW][KS];
+  __shared__ double sRedL[NW];
+  __shared__ double sCs[kGsUMax];
+  __shared__ double sScal[NW][4];
+  __shared__ double sPart[NP][NC];
+  __shared__ double sLW;
+  __shared__ int sFail;
+  if (a.params[kParamDone] != 0.0) return;
+  const int t = threadIdx.x, b = blockIdx.x;
+  const int d = sp.seg_doc[b], g = sp.seg_index[b], G = sp.seg_count[b], base = sp.seg_base[b];
+  int* counter = sp.counter + sp.doc_slot[b];
+  const int epoch = __hip_atomic_load(counter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const double alpha = a.params[0], lik_const = a.params[1];
+  const int vmi = (int)a.params[2];
+  const double vconv = params_vconv(a.params);
+  const int K = a.K;
+  const int lane = t & 63, wv = t >> 6;
+  const int q = lane >> LSW, sl = lane & (NSW - 1);
+  const int slot = wv * NSW + sl;
+  const int s0 = a.doc_ptr[d], n = a.doc_ptr[d + 1] - s0;   // n > 0 (host)
+  const int U = a.gs_updates;
+  const int W = (n + U - 1) / U;
+  const int nch = (n + W - 1) / W;
+  const int WG = (W + G - 1) / G;             // words of a chunk per segment
+  const int nact = min(NW, (WG + NSW - 1) / NSW);
+  const bool active = wv < nact;
+  const int* __restrict__ wrow = a.word_idx + s0;
+  const float* __restrict__ crow = a.counts + s0;
+  auto range = [&](int j, int& m0, int& m1) {
+    const int n1 = min(n, (j + 1) * W);
+    m0 = min(n1, j * W + g * WG);
+    m1 = min(n1, m0 + WG);
+  };
+  for (int j = t; j < nch; j += NTD) sCs[j] = 0.0;
+  if (t == 0) {
+    sFail = 0;
+    sLW = 0.0;
+  }
+  lds_barrier();
+  for (int p = t; p < n; p += NTD) atomicAdd(&sCs[p / W], (double)crow[p]);   // integer counts: exact
+  lds_barrier();
+  double total = 0.0;
+  for (int j = 0; j < nch; ++j) total += sCs[j];
+  const double g0 = alpha + total / K;
+  const double m = psi_only(g0);
+  double gam[TO], psi[TO], lps[TO];
+#pragma unroll
+  for (int o = 0; o < TO; ++o) {
+    const int k = t + NTD * o;
+    gam[o] = k < K ? g0 : 0.0;
+    psi[o] = m;
+    lps[o] = 0.0;
+    if (k < KS) {
+      sE[k] = k < K ? 1.0 : 0.0;
+      for (int j = 0; j < nch; ++j) sC[j][k] = k < K ? sCs[j] / K : 0.0;
+    }
+  }
+  int wc[RMAX], wn[RMAX];
+  float cc[RMAX], cn[RMAX];
+  unsigned vc = 0, vn = 0;
+  double bc[RMAX][KPL];
+  auto load_ids = [&](int j, int (&w)[RMAX], float (&c)[RMAX], unsigned& v) {
+    int m0, m1;
+    range(j, m0, m1);
+    v = 0;
+#pragma unroll
+    for (int r = 0; r < RMAX; ++r) {
+      const int p = m0 + slot + r * NS;
+      v |= (active && p < m1) ? (1u << r) : 0u;
+      const int pc = max(0, min(p, m1 - 1));
+      w[r] = wrow[pc];
+      c[r] = crow[pc];
+    }
+  };
+  auto load_rows = [&](const int (&w)[RMAX]) {
+    if (!active) return;
+#pragma unroll
+    for (int r = 0; r < RMAX; ++r) {
+      const double* brow = a.beta + (size_t)w[r] * KS;
+#pragma unroll
+      for (int i = 0; i < KPL; ++i) bc[r][i] = brow[min(q + TG * i, KS - 1)];
+    }
+  };
+  load_ids(0, wc, cc, vc);
+  load_rows(wc);
+  load_ids(nch > 1 ? 1 : 0, wn, cn, vn);
+  lds_barrier();
+  double L = 0.0, L_old = 0.0, conv = 1.0, GS = 0.0, LWs = 0.0;
+  int it = 0;
+  bool failed = false;
+  while (!failed && var_continue(conv, vconv, it, vmi)) {
+    ++it;
+#pragma unroll
+    for (int o = 0; o < TO; ++o) lps[o] = 0.0;
+    for (int j = 0; j < nch; ++j) {
+      if (active) {
+        int m0, m1;
+        range(j, m0, m1);
+        double E[KPL], acc[KPL], lw = 0.0;
+#pragma unroll
+        for (int i = 0; i < KPL; ++i) {
+          E[i] = (q + TG * i < KS) ? sE[q + TG * i] : 0.0;
+          acc[i] = 0.0;
+        }
+        double cr[RMAX];
+#pragma unroll
+        for (int r = 0; r < RMAX; ++r) cr[r] = ((vc >> r) & 1u) ? (double)cc[r] : 0.0;
+        word_steps<RMAX, KPL, LSW>(E, bc, cr, acc, lw);
+        for (int pb = m0 + slot + RMAX * NS; pb < m1; pb += RMAX * NS)   // beyond the prefetched rounds
+          stream_batch<RMAX, KS, KPL, TG, LSW>(a.beta, wrow, crow, pb, m1, NS, q, E, bc, acc, lw);
+        const int j1 = j + 1 < nch ? j + 1 : 0;
+        const int j2 = j1 + 1 < nch ? j1 + 1 : 0;
+#pragma unroll
+        for (int r = 0; r < RMAX; ++r) {
+          wc[r] = wn[r];
+          cc[r] = cn[r];
+        }
+        vc = vn;
+        load_rows(wc);
+        load_ids(j2, wn, cn, vn);
+#pragma unroll
+        for (int i = 0; i < KPL; ++i) acc[i] = bits_sum<0, LSW, false>(acc[i]);
+        lw = group_sum<64>(q == 0 ? lw : 0.0);
+        if (sl == 0) {
+#pragma unroll
+          for (int i = 0; i < KPL; ++i)
+            if (q + TG * i < KS) sRed[wv][q + TG * i] = acc[i];
+        }
+        if (lane == 0) sRedL[wv] = lw;
+      }
+      lds_barrier();
+      // exchange: thread k < KS owns topic k, thread KS the log-sum
+      const int seq = (it - 1) * nch + j + 1;
+      const unsigned tag = split_tag(epoch, seq);
+      unsigned long long* xb = sp.xchg + (size_t)(seq & 1) * sp.n_blocks * GR;
+      if (t < NC) {
+        double part = 0.0;
+#pragma unroll
+        for (int v = 0; v < NW; ++v)
+          part += v < nact ? (t < KS ? sRed[v][t] : sRedL[v]) : 0.0;
+        const unsigned long long bits = (unsigned long long)__double_as_longlong(part);
+        unsigned long long* row = xb + (size_t)b * GR + 2 * t;
+        put_tagged_bits(row, (unsigned)(bits & 0xffffffffull), tag);
+        put_tagged_bits(row + 1, (unsigned)(bits >> 32), tag);
+      }
+      if (t < NP * NC) {
+        const int col = t % NC, pi = t / NC;
+        const int q0 = pi * G / NP, q1 = (pi + 1) * G / NP;
+        double ps;
+        if (!tagged_sum_f64(xb + (size_t)(base + q0) * GR + 2 * col, q1 - q0, GR, tag, ps)) {
+          sFail = 1;
+          __hip_atomic_store(sp.error, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        sPart[pi][col] = ps;
+      }
+      lds_barrier();
+      if (t < NC) {
+        double tot = 0.0;
+#pragma unroll
+        for (int pi = 0; pi < NP; ++pi) tot += sPart[pi][t];
+        if (t < KS) {
+          const int k = t;
+          const double Eo = sE[k];
+          const double nw = Eo * tot;
+          double En = 0.0;
+          if (k < K) {
+            lps[0] = fma(psi[0], nw, lps[0]);
+            gam[0] += nw - sC[j][k];
+            psi_exp(gam[0], m, psi[0], En);
+          }
+          sC[j][k] = nw;
+          sEt[j][k] = Eo;
+          sE[k] = En;
+        } else {
+          LWs += tot;
+        }
+      }
+      lds_barrier();
+      if (sFail) {
+        failed = true;
+        break;
+      }
+    }
+    if (failed) break;
+    // sweep likelihood (every workgroup of the document computes the same bits)
+    double gs = 0.0, lg = 0.0, lp = 0.0;
+#pragma unroll
+    for (int o = 0; o < TO; ++o) {
+      if (t + NTD * o < K) {
+        gs += gam[o];
+        lg += lgamma_pos(gam[o]);
+        lp += lps[o];
+      }
+    }
+    const double w1 = group_sum<64>(gs), w2 = group_sum<64>(lg), w3 = group_sum<64>(lp);
+    if (lane == 0) {
+      sScal[wv][1] = w1;
+      sScal[wv][2] = w2;
+      sScal[wv][3] = w3;
+    }
+    if (t == KS) {
+      sLW = LWs;
+      LWs = 0.0;
+    }
+    lds_barrier();
+    double LG = 0.0, LP = 0.0;
+    GS = 0.0;
+#pragma unroll
+    for (int v = 0; v < NW; ++v) {
+      GS += sScal[v][1];
+      LG += sScal[v][2];
+      LP += sScal[v][3];
+    }
+    L = lik_const - lgamma_pos(GS) + LG + fma(m, total, sLW) - LP;
+    conv = (L_old - L) / L_old;
+    L_old = L;
+    lds_barrier();
+  }
+  // every thread of this workgroup is past its last exchange (the loops end on a barrier)
+  split_exit(counter, sp.n_docs, G);
+  double ps = 0.0;
+#pragma unroll
+  for (int o = 0; o < TO; ++o) {
+    const int k = t + NTD * o;
+    if (k < K) ps += psi[o];
+    if (g == 0 && k < KS) a.gamma[(size_t)d * KS + k] = gam[o];
+  }
+  ps = group_sum<64>(ps);
+  if (lane == 0) sScal[wv][0] = ps;
+  lds_barrier();
+  if (g == 0 && t == 0) {
+    double PS = 0.0;
+    for (int v = 0; v < NW; ++v) PS += sScal[v][0];
+    a.lik[d] = failed ? __builtin_nan("") : L;   // a timed-out exchange surfaces as a NaN likelihood
+    a.alpha_ss[d] = PS - K * psi_only(GS);
+    a.iters[d] = it;
+  }
+  // final pass over this segment's ranges: c_n phi_nk = E_jk b_nk r_n with the final sweep's chunk E
+  if (!active) return;
+  for (int j = 0; j < nch; ++j) {
+    int m0, m1;
+    range(j, m0, m1);
+    double E[KPL];
+#pragma unroll
+    for (int i = 0; i < KPL; ++i) E[i] = (q + TG * i < KS) ? sEt[j][q + TG * i] : 0.0;
+    for (int p = m0 + slot; p < m1; p += NS) {
+      const double* brow = a.beta + (size_t)wrow[p] * KS;
+      const double c = (double)crow[p];
+      double bv[KPL];
+#pragma unroll
+      for (int i = 0; i < KPL; ++i) bv[i] = (q + TG * i < KS) ? brow[q + TG * i] : 0.0;
+      double pp = 0.0;
+#pragma unroll
+      for (int i = 0; i < KPL; ++i) pp = fma(E[i], bv[i], pp);
+      const double r = c * drcp(bits_sum<LSW, 6>(pp));
+      double* row = a.cphi + (size_t)(s0 + p) * KS;
+#pragma unroll
+      for (int i = 0; i < KPL; ++i)
+        if (q + TG * i < KS) __builtin_nontemporal_store(E[i] * bv[i] * r, &row[q + TG * i]);
     }
   }
 }
@@ -1660,6 +2054,47 @@ int gs_tiny_max(int KS) {
     default:
       throw std::runtime_error("gs_tiny_max: unsupported KS " + std::to_string(KS));
   }
+}
+
+template <int KS>
+static int gs_split_capacity_ks() {
+  int dev = 0, per_cu = 0;
+  hipDeviceProp_t p;
+  ONI_HIP_CHECK(hipGetDevice(&dev));
+  ONI_HIP_CHECK(hipGetDeviceProperties(&p, dev));
+  ONI_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(&gs::gs_split<KS>),
+                                                             512, 0));
+  return per_cu * p.multiProcessorCount;
+}
+
+int gs_split_capacity(int KS) {
+  switch (KS) {
+#define ONI_KS(X) \
+  case X:         \
+    return gs_split_capacity_ks<X>();
+    ONI_FOR_EACH_KS(ONI_KS)
+#undef ONI_KS
+    default:
+      throw std::runtime_error("gs_split_capacity: unsupported KS " + std::to_string(KS));
+  }
+}
+
+void launch_gs_split(const GSArgs& a, const SplitArgs& s, int KS, hipStream_t st) {
+  if (s.n_blocks <= 0) return;
+  if (a.gs_updates < 1 || a.gs_updates > kGsUMax)
+    throw std::runtime_error("gs_split: gs_updates must be in [1, " + std::to_string(kGsUMax) + "]");
+  if (!a.params) throw std::runtime_error("gs_split: params block required");
+  switch (KS) {
+#define ONI_KS(X)                                                                       \
+  case X:                                                                               \
+    hipLaunchKernelGGL((gs::gs_split<X>), dim3(s.n_blocks), dim3(512), 0, st, a, s);    \
+    break;
+    ONI_FOR_EACH_KS(ONI_KS)
+#undef ONI_KS
+    default:
+      throw std::runtime_error("gs_split: unsupported KS " + std::to_string(KS));
+  }
+  ONI_HIP_CHECK(hipGetLastError());
 }
 
 void launch_gs_suff64(const int* word_ptr, const int* csc_ent, const int* order, int n_heavy, int n_medium,

@@ -408,16 +408,24 @@ class LDAEngine:
         streams = [main] + self._streams
         self._ev_fork.record(main)
         used = []
-        # side streams: the long-document buckets (critical path) are dispatched first
+        # side streams: the long-document buckets (critical path) are dispatched first, the split
+        # documents' batches (back to back on one stream) before everything
         work = list(self.gs_plan.plan)
+        if self.gs_plan.split is not None:
+            work.insert(0, ("split", self.gs_plan.split.batches))
         for si, (var, order) in zip(range(len(work)), work):
             s = streams[(si + 1) % len(streams)] if si < len(work) - 1 else main
-            if s is not main:
+            if s is not main and s not in used:
                 s.wait_event(self._ev_fork)
                 used.append(s)
             with torch.cuda.stream(s):
-                H.gs_estep(dc.doc_ptr, dc.word_idx, dc.counts, order, self.beta, self.K, self._U, prm, self.gamma,
-                           self.cphi, self.lik, self.ass, self.iters, var)
+                if var == "split":
+                    for batch in order:
+                        H.gs_split(dc.doc_ptr, dc.word_idx, dc.counts, self.beta, self.K, self._U, prm, self.gamma,
+                                   self.cphi, self.lik, self.ass, self.iters, batch)
+                else:
+                    H.gs_estep(dc.doc_ptr, dc.word_idx, dc.counts, order, self.beta, self.K, self._U, prm,
+                               self.gamma, self.cphi, self.lik, self.ass, self.iters, var)
         for j, s in enumerate(used):
             self._ev_join[j].record(s)
             main.wait_event(self._ev_join[j])
@@ -916,7 +924,9 @@ class LDAEngine:
         """A NaN likelihood: if a split-document barrier timed out, fail loudly (the kernel
         flags it instead of hanging the GPU)."""
         sp = self.doc_buckets.split if self.doc_buckets is not None else None
-        if sp is not None and any(int(b["error"].item()) for b in sp.batches):
+        gp = getattr(self, "gs_plan", None)
+        gp = gp.split if gp is not None else None
+        if any(int(b["error"].item()) for x in (sp, gp) if x is not None for b in x.batches):
             raise RuntimeError("split-document E-step: a cross-workgroup barrier timed out "
                                "(segments of one document were not co-resident)")
 

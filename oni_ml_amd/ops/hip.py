@@ -13,6 +13,7 @@ from __future__ import annotations
 import importlib
 import os
 import sys
+from typing import Optional
 
 import torch
 
@@ -622,6 +623,100 @@ def gs_mstep(cw, class_total, beta, K, gate=None):
                    _stream())
 
 
+def gs_split_launch_cap(KS: int) -> int:
+    """Workgroups per gs_split launch: 3/4 of the co-resident capacity (occupancy API x CUs), so a
+    launch's segments are resident together with room for the other streams' buckets;
+    ONI_SPLIT_MAX_BLOCKS lowers it (tests, shared / partitioned GPUs)."""
+    cap = max(1, int(lib().gs_split_capacity(int(KS))) * 3 // 4)
+    env = os.environ.get("ONI_SPLIT_MAX_BLOCKS")
+    if env:
+        cap = max(1, min(cap, int(env)))
+    return cap
+
+
+def gs_team8_words(KS: int) -> int:
+    """Words of a chunk one 8-wave fp64 workgroup holds in its prefetched rounds (TeamShape<KS, 8>:
+    slots x RMAX); the split kernel sizes segments to this."""
+    tg = 4 if KS <= 32 else (8 if KS <= 64 else 16)
+    kpl = -(-KS // tg)
+    return 8 * (64 // tg) * (8 if kpl <= 5 else 4)
+
+
+class GSSplitPlan:
+    """Launch batches of the fp64 split-document kernel (gs_split): document d of n words gets
+    G = clamp(ceil(ceil(n / U) / seg_words), 2, max_seg) workgroups, each taking 1/G of every chunk;
+    a batch holds <= gs_split_launch_cap(KS) workgroups (co-resident, so the per-chunk exchange
+    cannot deadlock).  Documents longer first; batches run back to back on one stream."""
+
+    def __init__(self, doc_ids, lengths, KS: int, gs_updates: int, device, seg_words: int = 0,
+                 max_seg: int = 0):
+        import numpy as np
+        self.KS = int(KS)
+        self.max_blocks = gs_split_launch_cap(KS)
+        self.seg_words = int(seg_words) or gs_team8_words(KS)
+        max_seg = min(int(max_seg) or int(os.environ.get("ONI_GS_SPLIT_G", "16")), self.max_blocks)
+        U = int(gs_updates)
+        self.segments = {}
+        self.batches = []
+        cur, used = [], 0
+        for d in doc_ids:
+            n = int(lengths[d])
+            W = -(-n // U)
+            G = max(2, min(max_seg, -(-W // self.seg_words)))
+            G = min(G, max(1, W))
+            self.segments[int(d)] = G
+            if used + G > self.max_blocks:
+                self.batches.append(self._make(cur, device))
+                cur, used = [], 0
+            cur.append((int(d), G))
+            used += G
+        if cur:
+            self.batches.append(self._make(cur, device))
+        self.n_docs = len(self.segments)
+
+    def _make(self, docs, device):
+        import numpy as np
+        sd, si, sc, sb, slot = [], [], [], [], []
+        for j, (d, G) in enumerate(docs):
+            base = len(sd)
+            for q in range(G):
+                sd.append(d), si.append(q), sc.append(G), sb.append(base), slot.append(j)
+        t = lambda a: torch.tensor(np.asarray(a, np.int32), device=device)
+        nb = len(sd)
+        return dict(seg_doc=t(sd), seg_index=t(si), seg_count=t(sc), seg_base=t(sb), doc_slot=t(slot), n_blocks=nb,
+                    # tagged granules {uint32 half of a double, uint32 tag}: [2][n_blocks][2 (KS + 1)]
+                    xchg=torch.zeros(2 * nb * 2 * (self.KS + 1), dtype=torch.int64, device=device),
+                    counter=torch.zeros(2 * len(docs), dtype=torch.int32, device=device),
+                    error=torch.zeros(1, dtype=torch.int32, device=device), docs=len(docs))
+
+
+def gs_split(doc_ptr, word_idx, counts, beta, K, gs_updates, params, gamma, cphi, lik, alpha_ss, iters, batch):
+    """One launch of the fp64 split-document E-step over one GSSplitPlan batch."""
+    D = doc_ptr.numel() - 1
+    nnz = word_idx.numel()
+    V, KS = beta.shape
+    dev = beta.device
+    nb = batch["n_blocks"]
+    if KS not in compiled_ks():
+        raise ValueError(f"beta row stride {KS} has no compiled kernel")
+    if not (0 < K <= KS) or not (1 <= int(gs_updates) <= gs_umax()):
+        raise ValueError("K or gs_updates out of range")
+    for k in ("seg_doc", "seg_index", "seg_count", "seg_base", "doc_slot"):
+        _chk(batch[k], torch.int32, k, (nb,), dev)
+    lib().gs_split(
+        _chk(doc_ptr, torch.int32, "doc_ptr", (D + 1,), dev), _chk(word_idx, torch.int32, "word_idx", (nnz,), dev),
+        _chk(counts, torch.float32, "counts", (nnz,), dev), _chk(beta, torch.float64, "beta", (V, KS), dev),
+        int(K), int(KS), int(gs_updates), _params_ptr(params, dev) or _bad("params"),
+        _chk(gamma, torch.float64, "gamma", (D, KS), dev), _chk(cphi, torch.float64, "cphi", (nnz, KS), dev),
+        _chk(lik, torch.float64, "lik", (D,), dev), _chk(alpha_ss, torch.float64, "alpha_ss", (D,), dev),
+        _chk(iters, torch.int32, "iters", (D,), dev),
+        batch["seg_doc"].data_ptr(), batch["seg_index"].data_ptr(), batch["seg_count"].data_ptr(),
+        batch["seg_base"].data_ptr(), batch["doc_slot"].data_ptr(), int(nb),
+        _chk(batch["xchg"], torch.int64, "xchg", (2 * nb * 2 * (KS + 1),), dev),
+        _chk(batch["counter"], torch.int32, "counter", (2 * batch["docs"],), dev), int(batch["docs"]),
+        _chk(batch["error"], torch.int32, "error", (1,), dev), _stream())
+
+
 class GSPlan:
     """Length buckets of the fp64 block Gauss-Seidel E-step: (variant, int32 doc order) per launch.
 
@@ -632,10 +727,20 @@ class GSPlan:
     EDGES_NARROW = ((GS_TEAM8, 2048, None), (GS_TEAM4, 256, 2048), (GS_TEAM1, GS_SMALL_MAX, 256),
                     (GS_SMALL, None, GS_SMALL_MAX))
 
-    def __init__(self, lengths, KS: int, gs_updates: int, device):
+    def __init__(self, lengths, KS: int, gs_updates: int, device, split_min: Optional[int] = None):
         import numpy as np
         L = np.asarray(lengths, dtype=np.int64)
         order = np.argsort(-L, kind="stable").astype(np.int32)
+        # documents longer than split_min words: one document over several workgroups (gs_split);
+        # default on for KS > 32 (the topic-group team kernels' chunk of a long document is bound
+        # by one CU's row gathers), ONI_GS_SPLIT_MIN overrides (0: off)
+        if split_min is None:
+            split_min = int(os.environ.get("ONI_GS_SPLIT_MIN", "16384" if KS > 32 else "0"))
+        self.split = None
+        if split_min > 0 and (L > split_min).any():
+            m = L[order] > split_min
+            self.split = GSSplitPlan(order[m], L, KS, gs_updates, device)
+            order = order[~m]
         Ls = L[order]
         tiny = min(gs_tiny_max(KS), int(gs_updates))
         self.plan = []

@@ -6,7 +6,7 @@ then launches each length bucket alone (HIP events, median of repeats) and repor
 lengths, sweeps and kernel time; plus suff-stats and the M-step.  ``--only VARIANT`` loops one
 bucket (for rocprofv3 --pmc runs of a single kernel).
 
-  python scripts/bench_gs64.py [--events N] [--topics K] [--gs-updates U] [--only tiny|team1|team4|team8]
+  python scripts/bench_gs64.py [--events N] [--topics K] [--gs-updates U] [--only split|tiny|team1|team4|team8]
 """
 import argparse
 import json
@@ -63,6 +63,21 @@ def main():
         H.gs_estep(dc.doc_ptr, dc.word_idx, dc.counts, order, eng.beta, eng.K, eng._U, eng._params, eng.gamma,
                    eng.cphi, eng.lik, eng.ass, eng.iters, var, dbg=dbg)
 
+    spl = eng.gs_plan.split
+    if spl is not None and (not a.only or a.only == "split"):
+        def launch_split():
+            for b in spl.batches:
+                H.gs_split(dc.doc_ptr, dc.word_idx, dc.counts, eng.beta, eng.K, eng._U, eng._params, eng.gamma,
+                           eng.cphi, eng.lik, eng.ass, eng.iters, b)
+        o = np.asarray(sorted(spl.segments), dtype=np.int64)
+        L, it = lens[o], its[o]
+        out["buckets"].append(dict(kernel="split", docs=int(o.size), len_min=int(L.min()), len_max=int(L.max()),
+                                   entries=int(L.sum()), sweeps_mean=round(float(it.mean()), 2),
+                                   sweeps_max=int(it.max()), ms=round(timed(launch_split, a.reps), 4),
+                                   word_sweeps=int((L * it).sum()), batches=len(spl.batches),
+                                   workgroups=int(sum(spl.segments.values())),
+                                   max_segments=int(max(spl.segments.values()))))
+        print(json.dumps(out["buckets"][-1]), flush=True)
     for var, order in eng.gs_plan.plan:
         if a.only and names[var] != a.only:
             continue

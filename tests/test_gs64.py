@@ -180,3 +180,47 @@ def test_longest_documents_match_oracle(head):
     assert _rel(eng.lik.cpu().numpy(), ref["doc_likelihood"], 1.0) < 1e-10
     cw = eng._cw_local[:, :K].cpu().numpy()
     assert _rel(cw, np.ascontiguousarray(ref["class_word"].T), 1e-30) < 1e-10
+
+
+@pytest.mark.parametrize("K,env", [
+    (100, {}),                                                          # default split for KS > 32
+    (100, {"ONI_SPLIT_MAX_BLOCKS": "9", "ONI_GS_SPLIT_G": "3"}),        # several batches, uneven ranges
+    (20, {"ONI_GS_SPLIT_MIN": "3000", "ONI_GS_SPLIT_G": "5"}),          # forced on a narrow KS
+    (52, {"ONI_GS_SPLIT_MIN": "2500"}),
+])
+def test_split_documents_match_oracle(K, env, monkeypatch):
+    """gs_split (one document over G workgroups exchanging tagged per-chunk partials) against the
+    oracle: every replica runs the same refresh, so gamma / likelihood / class_word match at 1e-10."""
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    rng = np.random.default_rng(K)
+    V, D = 40000, 260
+    lens = np.minimum(rng.zipf(1.5, D), 200)
+    lens[:7] = [30000, 20000, 12000, 9100, 5000, 3100, 2600]
+    lens[9] = 0
+    ptr = np.concatenate([[0], np.cumsum(lens)])
+    words = np.concatenate([rng.choice(V, n, replace=False) for n in lens]).astype(np.int32)
+    counts = rng.integers(1, 4, words.size)
+    c = Corpus(ptr.astype(np.int64), words, counts.astype(np.int64), V)
+    U = 32
+    lb = _log_beta(V, K, seed=5)
+    st = LDASettings(var_max_iter=5, var_converged=-1e30)
+    ref = _oracle(c, lb, 0.33, st, U)
+    eng, sc = _gpu_estep(c, K, lb, 0.33, LDASettings(var_max_iter=5, var_converged=-1e30), U)
+    sp = eng.gs_plan.split
+    assert sp is not None and sp.n_docs >= 4 and max(sp.segments.values()) >= 2
+    if "ONI_SPLIT_MAX_BLOCKS" in env:
+        assert len(sp.batches) >= 2
+    assert int(sum(b["error"].item() for b in sp.batches)) == 0
+    full = lens > 0      # the empty document's 0/0 convergence test may stop a sweep apart (see above)
+    assert np.array_equal(eng.iters.cpu().numpy()[full], ref["iters"][full])
+    assert _rel(eng.gamma[:, :K].cpu().numpy(), ref["gamma"], 1e-12) < 1e-10
+    assert _rel(eng.lik.cpu().numpy(), ref["doc_likelihood"], 1.0) < 1e-10
+    cw = eng._cw_local[:, :K].cpu().numpy()
+    assert _rel(cw, np.ascontiguousarray(ref["class_word"].T), 1e-30) < 1e-10
+    assert abs(sc[0] - ref["likelihood"]) / abs(ref["likelihood"]) < 1e-11
+    # graph replay: the launch epoch moves on, the tags of the previous launch never match
+    g1 = eng.gamma.clone()
+    eng.e_step()
+    torch.cuda.synchronize()
+    assert torch.equal(g1, eng.gamma)
