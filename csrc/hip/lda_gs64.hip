@@ -577,6 +577,21 @@ __device__ __forceinline__ void stream_batch(const double* __restrict__ beta, co
   word_steps<RMAX, KPL, LSW>(E, b, c, acc, lw);
 }
 
+// the streamed tail of one slot: full batches while >= 2 rounds remain, the last round alone (a
+// lone word in a full batch paid RMAX rows and word steps; measured on the split kernel)
+template <int RMAX, int KS, int KPL, int TG, int LSW>
+__device__ __forceinline__ void stream_tail(const double* __restrict__ beta, const int* __restrict__ wrow,
+                                            const float* __restrict__ crow, int p0, int end, int NS, int q,
+                                            const double (&E)[KPL], double (&b)[RMAX][KPL], double (&acc)[KPL],
+                                            double& lw) {
+  int p = p0;
+  for (; p + NS < end; p += RMAX * NS) stream_batch<RMAX, KS, KPL, TG, LSW>(beta, wrow, crow, p, end, NS, q, E, b, acc, lw);
+  if (p < end) {
+    double b1[1][KPL];
+    stream_batch<1, KS, KPL, TG, LSW>(beta, wrow, crow, p, end, NS, q, E, b1, acc, lw);
+  }
+}
+
 template <int KS, int NW>
 __global__ __launch_bounds__(team_threads(KS, NW)) void gs_team(GSArgs a) {
   using T = TeamShape<KS, NW>;
@@ -732,8 +747,7 @@ __global__ __launch_bounds__(team_threads(KS, NW)) void gs_team(GSArgs a) {
         // words beyond the prefetched rounds (documents longer than RMAX * NS * U): streamed in
         // batches of RMAX rows per slot with a batch's loads in flight together (bc is free until
         // the next chunk's prefetch below); one row at a time left the word phase latency-bound
-        for (int pb = n0 + slot + RMAX * NS; pb < n1; pb += RMAX * NS)
-          stream_batch<RMAX, KS, KPL, TG, LSW>(a.beta, wrow, crow, pb, n1, NS, q, E, bc, acc, lw);
+        stream_tail<RMAX, KS, KPL, TG, LSW>(a.beta, wrow, crow, n0 + slot + RMAX * NS, n1, NS, q, E, bc, acc, lw);
         // next chunk's rows (ids already here), then the ids after it
         const int j1 = j + 1 < nch ? j + 1 : 0;
         const int j2 = j1 + 1 < nch ? j1 + 1 : 0;
@@ -1059,8 +1073,8 @@ __global__ __launch_bounds__(512) void gs_split(GSArgs a, SplitArgs sp) {
 #pragma unroll
         for (int r = 0; r < RMAX; ++r) cr[r] = ((vc >> r) & 1u) ? (double)cc[r] : 0.0;
         word_steps<RMAX, KPL, LSW>(E, bc, cr, acc, lw);
-        for (int pb = m0 + slot + RMAX * NS; pb < m1; pb += RMAX * NS)   // beyond the prefetched rounds
-          stream_batch<RMAX, KS, KPL, TG, LSW>(a.beta, wrow, crow, pb, m1, NS, q, E, bc, acc, lw);
+        // beyond the prefetched rounds
+        stream_tail<RMAX, KS, KPL, TG, LSW>(a.beta, wrow, crow, m0 + slot + RMAX * NS, m1, NS, q, E, bc, acc, lw);
         const int j1 = j + 1 < nch ? j + 1 : 0;
         const int j2 = j1 + 1 < nch ? j1 + 1 : 0;
 #pragma unroll
