@@ -592,8 +592,10 @@ __device__ __forceinline__ void stream_tail(const double* __restrict__ beta, con
   }
 }
 
-template <int KS, int NW>
-__global__ __launch_bounds__(team_threads(KS, NW)) void gs_team(GSArgs a) {
+// MINW: minimum waves per SIMD requested from the register allocator (the LDS-free one-wave team
+// at K > 32 is latency-bound on its per-word refresh chains; ONI_TEAM1_WAVES selects 1 / 3 / 4)
+template <int KS, int NW, int MINW = 1>
+__global__ __launch_bounds__(team_threads(KS, NW), MINW) void gs_team(GSArgs a) {
   using T = TeamShape<KS, NW>;
   constexpr int DPB = T::DPB, NTD = T::NTD, TG = T::TG, KPL = T::KPL, NSW = T::NSW, LSW = T::LSW, NS = T::NS,
                 TO = T::TO, RMAX = T::RMAX;
@@ -2000,7 +2002,18 @@ static void gs_estep_ks(const GSArgs& a, int variant, hipStream_t s) {
       // one wave per document (<= 256 words, chunks of <= 8 words): the topic-group layout keeps
       // more lanes busy than one word per lane (measured 0.90 vs 1.13 ms on the headline corpus)
       constexpr int dpb = gs::TeamShape<KS, 1>::DPB;
-      hipLaunchKernelGGL((gs::gs_team<KS, 1>), dim3((a.n_items + dpb - 1) / dpb), dim3(dpb * 64), 0, s, a);
+      const dim3 grid((a.n_items + dpb - 1) / dpb), blk(dpb * 64);
+      if constexpr (KS > 32) {
+        static const int tw = std::getenv("ONI_TEAM1_WAVES") ? std::atoi(std::getenv("ONI_TEAM1_WAVES")) : 1;
+        if (tw == 3)
+          hipLaunchKernelGGL((gs::gs_team<KS, 1, 3>), grid, blk, 0, s, a);
+        else if (tw == 4)
+          hipLaunchKernelGGL((gs::gs_team<KS, 1, 4>), grid, blk, 0, s, a);
+        else
+          hipLaunchKernelGGL((gs::gs_team<KS, 1>), grid, blk, 0, s, a);
+      } else {
+        hipLaunchKernelGGL((gs::gs_team<KS, 1>), grid, blk, 0, s, a);
+      }
       break;
     }
     case kGsTeam4:
