@@ -2004,7 +2004,9 @@ static void gs_estep_ks(const GSArgs& a, int variant, hipStream_t s) {
       constexpr int dpb = gs::TeamShape<KS, 1>::DPB;
       const dim3 grid((a.n_items + dpb - 1) / dpb), blk(dpb * 64);
       if constexpr (KS > 32) {
-        static const int tw = std::getenv("ONI_TEAM1_WAVES") ? std::atoi(std::getenv("ONI_TEAM1_WAVES")) : 1;
+        // 3 waves per SIMD (168 VGPRs, 12 B spilled): K = 100 shard team1 13.2 -> 11.7 ms; 4 (128 VGPRs,
+        // 100 B spilled) 19.5 ms (profiles/r2_k100_split.md)
+        static const int tw = std::getenv("ONI_TEAM1_WAVES") ? std::atoi(std::getenv("ONI_TEAM1_WAVES")) : 3;
         if (tw == 3)
           hipLaunchKernelGGL((gs::gs_team<KS, 1, 3>), grid, blk, 0, s, a);
         else if (tw == 4)

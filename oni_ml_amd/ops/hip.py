@@ -646,28 +646,35 @@ class GSSplitPlan:
     """Launch batches of the fp64 split-document kernel (gs_split): document d of n words gets
     G = clamp(ceil(ceil(n / U) / seg_words), 2, max_seg) workgroups, each taking 1/G of every chunk;
     a batch holds <= gs_split_launch_cap(KS) workgroups (co-resident, so the per-chunk exchange
-    cannot deadlock).  Documents longer first; batches run back to back on one stream."""
+    cannot deadlock).  Documents are taken longest first into at most `max_batches` batches (batches
+    run back to back on one stream, so a second batch lengthens the critical path); documents that
+    do not fit stay with the one-workgroup team (``leftover``)."""
 
     def __init__(self, doc_ids, lengths, KS: int, gs_updates: int, device, seg_words: int = 0,
-                 max_seg: int = 0):
+                 max_seg: int = 0, max_batches: int = 0):
         import numpy as np
         self.KS = int(KS)
         self.max_blocks = gs_split_launch_cap(KS)
-        self.seg_words = int(seg_words) or gs_team8_words(KS)
+        self.seg_words = int(seg_words) or int(os.environ.get("ONI_GS_SPLIT_WORDS", "0")) or min(128, gs_team8_words(KS))
         max_seg = min(int(max_seg) or int(os.environ.get("ONI_GS_SPLIT_G", "16")), self.max_blocks)
+        max_batches = int(max_batches) or int(os.environ.get("ONI_GS_SPLIT_BATCHES", "1"))
         U = int(gs_updates)
         self.segments = {}
         self.batches = []
+        self.leftover = []
         cur, used = [], 0
         for d in doc_ids:
             n = int(lengths[d])
             W = -(-n // U)
             G = max(2, min(max_seg, -(-W // self.seg_words)))
             G = min(G, max(1, W))
-            self.segments[int(d)] = G
             if used + G > self.max_blocks:
+                if len(self.batches) + 1 >= max_batches:
+                    self.leftover.append(int(d))
+                    continue
                 self.batches.append(self._make(cur, device))
                 cur, used = [], 0
+            self.segments[int(d)] = G
             cur.append((int(d), G))
             used += G
         if cur:
@@ -735,12 +742,16 @@ class GSPlan:
         # default on for KS > 32 (the topic-group team kernels' chunk of a long document is bound
         # by one CU's row gathers), ONI_GS_SPLIT_MIN overrides (0: off)
         if split_min is None:
-            split_min = int(os.environ.get("ONI_GS_SPLIT_MIN", "16384" if KS > 32 else "0"))
+            split_min = int(os.environ.get("ONI_GS_SPLIT_MIN", "4096" if KS > 32 else "0"))
         self.split = None
         if split_min > 0 and (L > split_min).any():
             m = L[order] > split_min
-            self.split = GSSplitPlan(order[m], L, KS, gs_updates, device)
-            order = order[~m]
+            sp = GSSplitPlan(order[m], L, KS, gs_updates, device)
+            if sp.n_docs:
+                self.split = sp
+                keep = np.ones(len(order), bool)
+                keep[np.flatnonzero(m)] = ~np.isin(order[m], np.asarray(sorted(sp.segments), np.int64))
+                order = order[keep]
         Ls = L[order]
         tiny = min(gs_tiny_max(KS), int(gs_updates))
         self.plan = []

@@ -185,7 +185,7 @@ def test_longest_documents_match_oracle(head):
 @pytest.mark.parametrize("K,env", [
     (100, {}),                                                          # default split for KS > 32
     (100, {"ONI_GS_SPLIT_MIN": "4000"}),
-    (100, {"ONI_GS_SPLIT_MIN": "4000", "ONI_SPLIT_MAX_BLOCKS": "9", "ONI_GS_SPLIT_G": "3"}),  # several batches
+    (100, {"ONI_GS_SPLIT_MIN": "4000", "ONI_SPLIT_MAX_BLOCKS": "9", "ONI_GS_SPLIT_G": "3", "ONI_GS_SPLIT_BATCHES": "8"}),
     (20, {"ONI_GS_SPLIT_MIN": "3000", "ONI_GS_SPLIT_G": "5"}),          # forced on a narrow KS
     (52, {"ONI_GS_SPLIT_MIN": "2500"}),
 ])
