@@ -20,3 +20,29 @@ def test_isolate_longest_gives_each_head_document_its_own_xcd():
 def test_isolate_longest_short_lists():
     assert GSPlan.isolate_longest(np.array([5, 6, 7], dtype=np.int32), 1).tolist() == [5, 6, 7]
     assert GSPlan.isolate_longest(np.array([5], dtype=np.int32), 2).tolist() == [5]
+
+
+def test_split_plan_one_batch_longest_first(monkeypatch):
+    """GSSplitPlan: G = clamp(ceil(ceil(n / U) / seg_words), 2, max_seg); longest documents first into
+    one co-resident batch, the rest left to the one-workgroup team; batch arrays consistent."""
+    from oni_ml_amd.ops import hip as H
+    monkeypatch.setattr(H, "gs_split_launch_cap", lambda KS: 20)
+    lens = np.array([82418, 5000, 30000, 4200, 9100, 100, 12000], dtype=np.int64)
+    order = np.argsort(-lens, kind="stable")
+    cand = order[lens[order] > 4096]
+    sp = H.GSSplitPlan(cand, lens, 100, 32, "cpu", seg_words=128, max_seg=16)
+    # 82418 -> W 2576 -> 16 segments; 30000 -> 938 -> 8 does not fit (16 + 8 > 20); 12000 -> 375 -> 3;
+    # 9100 -> 285 -> 3 does not fit (19 + 3); 5000 -> 157 -> 2 does not fit
+    assert sp.segments == {0: 16, 6: 3}
+    assert sorted(sp.leftover) == [1, 2, 3, 4]      # 4200 -> 132 -> 2 does not fit either
+    assert len(sp.batches) == 1
+    b = sp.batches[0]
+    assert b["n_blocks"] == 19 and b["docs"] == 2
+    assert b["seg_doc"].tolist() == [0] * 16 + [6] * 3
+    assert b["seg_index"].tolist() == list(range(16)) + [0, 1, 2]
+    assert b["seg_base"].tolist() == [0] * 16 + [16] * 3
+    assert b["xchg"].numel() == 2 * 19 * 2 * 101
+    # several batches when allowed
+    sp2 = H.GSSplitPlan(cand, lens, 100, 32, "cpu", seg_words=128, max_seg=16, max_batches=8)
+    assert sp2.leftover == [] and len(sp2.batches) >= 2
+    assert all(bb["n_blocks"] <= 20 for bb in sp2.batches)
