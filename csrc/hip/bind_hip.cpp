@@ -171,10 +171,11 @@ PYBIND11_MODULE(_onihip, m) {
     oni::launch_gs_split(a, s, KS, S(stream));
   });
   m.def("gs_suff64", [](u word_ptr, u csc_ent, u order, int n_heavy, int n_medium, int n_light, u cphi, u cw, u part,
-                        u lik, u ass, int lo, int hi, int KS, u gate, u stream) {
+                        u lik, u ass, int lo, int hi, int KS, u gate, u stream, u cw_base) {
     oni::launch_gs_suff64(P<const int>(word_ptr), P<const int>(csc_ent), P<const int>(order), n_heavy, n_medium,
                           n_light, P<const double>(cphi), P<double>(cw), P<double>(part), P<const double>(lik),
-                          P<const double>(ass), lo, hi, KS, P<const double>(gate), S(stream));
+                          P<const double>(ass), lo, hi, KS, P<const double>(gate), S(stream),
+                          P<const double>(cw_base));
   });
   m.def("gs_mstep_control", [](u cw, u class_total, u beta, int V, int K, int KS, u scalars, u params, u ctl,
                                u hist, int hist_slots, u done_count, u stream, u rows, int n_rows, int newton,

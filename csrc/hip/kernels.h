@@ -231,7 +231,8 @@ int gs_split_capacity(int KS);
 // [nb][2 + KS] per-workgroup {lik slice, alpha_ss slice, column sums} for colsum_partials.
 void launch_gs_suff64(const int* word_ptr, const int* csc_ent, const int* order, int n_heavy, int n_medium,
                       int n_light, const double* cphi, double* cw, double* part, const double* lik,
-                      const double* ass, int lo, int hi, int KS, const double* gate, hipStream_t s);
+                      const double* ass, int lo, int hi, int KS, const double* gate, hipStream_t s,
+                      const double* cw_base = nullptr);   // cw[w] = cw_base[w] + sum (nullable)
 // fp64 M-step + alpha Newton + EM control (as launch_lda_mstep_control)
 void launch_gs_mstep_control(const double* cw, const double* class_total, double* beta, int V, int K, int KS,
                              const int* rows, int n_rows, const EMControlArgs& c, const NewtonArgs& nw,

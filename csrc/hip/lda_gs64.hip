@@ -1843,7 +1843,8 @@ __global__ __launch_bounds__(256) void gs_suff64(const int* __restrict__ word_pt
                                                  int n_light, const double* __restrict__ cphi,
                                                  double* __restrict__ cw, double* __restrict__ part,
                                                  const double* __restrict__ lik, const double* __restrict__ ass,
-                                                 int lo, int hi, const double* gate) {
+                                                 int lo, int hi, const double* gate,
+                                                 const double* __restrict__ cw_base) {
   constexpr int TG = tg_of(KS), KPL = kpl_of(KS), NSLOT = 256 / TG;
   __shared__ double sAcc[NSLOT][KS];
   __shared__ double sRow[16][KS];
@@ -1916,9 +1917,12 @@ __global__ __launch_bounds__(256) void gs_suff64(const int* __restrict__ word_pt
   for (int idx = t; idx < ngroups * KS; idx += 256) {
     const int g = idx / KS, k = idx % KS;
     const int it = (G == 256 ? item : item - gi + g);
-    double v = 0.0;
+    // cw_base (nullable): rows summed earlier from the other entries of each word (the early /
+    // late split of the suff-stats, em.py), added first so the order is fixed
+    const size_t row = it < nitems ? (size_t)order[base + it] * KS : 0;
+    double v = (cw_base != nullptr && it < nitems) ? cw_base[row + k] : 0.0;
     for (int u = 0; u < S; ++u) v += sAcc[g * S + u][k];
-    if (it < nitems) cw[(size_t)order[base + it] * KS + k] = v;
+    if (it < nitems) cw[row + k] = v;
     else v = 0.0;
     sRow[g][k] = v;
   }
@@ -2128,14 +2132,15 @@ void launch_gs_split(const GSArgs& a, const SplitArgs& s, int KS, hipStream_t st
 
 void launch_gs_suff64(const int* word_ptr, const int* csc_ent, const int* order, int n_heavy, int n_medium,
                       int n_light, const double* cphi, double* cw, double* part, const double* lik,
-                      const double* ass, int lo, int hi, int KS, const double* gate, hipStream_t s) {
+                      const double* ass, int lo, int hi, int KS, const double* gate, hipStream_t s,
+                      const double* cw_base) {
   const int nb = suff_fused_blocks(n_heavy, n_medium, n_light);
   if (nb <= 0) return;
   switch (KS) {
 #define ONI_KS(X)                                                                                        \
   case X:                                                                                                \
     hipLaunchKernelGGL((gs::gs_suff64<X>), dim3(nb), dim3(256), 0, s, word_ptr, csc_ent, order, n_heavy, \
-                       n_medium, n_light, cphi, cw, part, lik, ass, lo, hi, gate);                       \
+                       n_medium, n_light, cphi, cw, part, lik, ass, lo, hi, gate, cw_base);              \
     break;
     ONI_FOR_EACH_KS(ONI_KS)
 #undef ONI_KS

@@ -391,6 +391,36 @@ class LDAEngine:
         self._out_host = torch.zeros(self._ctlhist.numel(), dtype=f64).pin_memory()
         self._pushed = None
         self.doc_buckets = None
+        self._suff_split = self._build_suff_split() if os.environ.get("ONI_SUFF_SPLIT", "1") != "0" else None
+
+    def _build_suff_split(self):
+        """Early / late sufficient statistics: class_word[w] = (sum over w's entries in documents of the
+        other buckets, computed while the longest-document bucket still runs) + (sum over its entries in
+        the longest-document bucket, after it).  Two CSC subsets of the corpus; the late pass adds the
+        early rows first (``gs_suff64(base=...)``), so the order is fixed.  None when there is nothing
+        to overlap (one bucket, or the late bucket holds most of the entries)."""
+        from ...ops import hip as H
+        gp, dc, dev = self.gs_plan, self.dc, self.device
+        if len(gp.plan) + (gp.split is not None) < 2:
+            return None
+        if gp.split is not None:
+            late = np.asarray(sorted(gp.split.segments), np.int64)
+        else:
+            o = gp.plan[0][1].cpu().numpy()
+            late = o[o >= 0].astype(np.int64)
+        force = os.environ.get("ONI_SUFF_SPLIT") == "force"
+        if late.size == 0 or (not force and dc.doc_len[late].sum() > 0.6 * max(1, int(dc.doc_len.sum()))):
+            return None
+        mask = torch.zeros(self.D, dtype=torch.bool, device=dev)
+        mask[torch.from_numpy(late).to(dev)] = True
+        wpE, ceE, lenE = H.csc_subset(dc.word_ptr, dc.csc_ent, dc.csc_doc, ~mask)
+        wpL, ceL, lenL = H.csc_subset(dc.word_ptr, dc.csc_ent, dc.csc_doc, mask)
+        planE, planL = H.SuffPlan(lenE, dev), H.SuffPlan(lenL, dev)
+        need = max(planE.n_blocks, planL.n_blocks, 1)
+        if self._suff_part.shape[0] < need:
+            self._suff_part = torch.zeros(need, self._suff_part.shape[1], dtype=torch.float64, device=dev)
+        return dict(wpE=wpE, ceE=ceE, planE=planE, wpL=wpL, ceL=ceL, planL=planL,
+                    cw_early=torch.zeros_like(self.cw), late_docs=int(late.size))
 
     def _launch_estep64(self, newton_key=None, phase: str = "all"):
         """fp64 E-step: length buckets on 4 streams (longest first), one join, then the CSC
@@ -426,10 +456,23 @@ class LDAEngine:
                 else:
                     H.gs_estep(dc.doc_ptr, dc.word_idx, dc.counts, order, self.beta, self.K, self._U, prm,
                                self.gamma, self.cphi, self.lik, self.ass, self.iters, var)
+        # early / late suff-stats (phase "all"): work[0], the longest-document bucket, runs on
+        # streams[1]; every other bucket is joined first and the early pass overlaps it
+        ss = self._suff_split if (phase == "all" and len(work) >= 2) else None
+        late_s = streams[1] if ss is not None else None
         for j, s in enumerate(used):
             self._ev_join[j].record(s)
-            main.wait_event(self._ev_join[j])
+            if s is not late_s:
+                main.wait_event(self._ev_join[j])
         scal = (self.lik, self.ass, 0, self.lik.numel())
+        if late_s is not None:
+            H.gs_suff64(ss["wpE"], ss["ceE"], ss["planE"], self.cphi, ss["cw_early"], self._suff_part, gate=gate)
+            main.wait_event(self._ev_join[used.index(late_s)])
+            H.gs_suff64(ss["wpL"], ss["ceL"], ss["planL"], self.cphi, self._cw_local, self._suff_part, gate=gate,
+                        scalars=scal, base=ss["cw_early"])
+            H.colsum_partials(self._suff_part, ss["planL"].n_blocks, self._red_local, gate=gate)
+            self._finish_suff64(newton_key)
+            return
         if phase == "A":
             H.gs_suff64(dc.word_ptr, dc.csc_ent, self._plan_a, self.cphi, self._cw_local,
                         self._suff_part[:max(self._plan_a.n_blocks, 1)], gate=gate, scalars=scal)
@@ -439,6 +482,9 @@ class LDAEngine:
         H.gs_suff64(dc.word_ptr, dc.csc_ent, sp, self.cphi, self._cw_local, self._suff_part[:max(sp.n_blocks, 1)],
                     gate=gate, scalars=scal)
         H.colsum_partials(self._suff_part, sp.n_blocks, self._red_local, gate=gate)
+        self._finish_suff64(newton_key)
+
+    def _finish_suff64(self, newton_key):
         if self._distributed:
             if self._xchg is not None:
                 self._xchg.pack(self._cw_local)

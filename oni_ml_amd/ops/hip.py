@@ -571,9 +571,10 @@ def gs_estep(doc_ptr, word_idx, counts, order, beta, K, gs_updates, params, gamm
     lib().gs_estep(*args)
 
 
-def gs_suff64(word_ptr, csc_ent, plan: "SuffPlan", cphi, cw, part, gate=None, scalars=None):
+def gs_suff64(word_ptr, csc_ent, plan: "SuffPlan", cphi, cw, part, gate=None, scalars=None, base=None):
     """class_word[w] = sum of the cphi rows of w's corpus entries (CSC order, fp64, no atomics) + per-workgroup
-    partial rows part[b] = {lik slice, alpha_ss slice, column sums} for ``colsum_partials``."""
+    partial rows part[b] = {lik slice, alpha_ss slice, column sums} for ``colsum_partials``.
+    ``base`` [V, KS] (optional): added to each written row first (cw[w] = base[w] + sum)."""
     V, KS = cw.shape
     nnz = csc_ent.numel()
     dev = cw.device
@@ -593,7 +594,21 @@ def gs_suff64(word_ptr, csc_ent, plan: "SuffPlan", cphi, cw, part, gate=None, sc
         _chk(word_ptr, torch.int32, "word_ptr", (V + 1,), dev), _chk(csc_ent, torch.int32, "csc_ent", (nnz,), dev),
         _chk(plan.order, torch.int32, "order", (plan.order.numel(),), dev), plan.n_heavy, plan.n_medium, plan.n_light,
         _chk(cphi, torch.float64, "cphi", (nnz, KS), dev), _chk(cw, torch.float64, "cw", (V, KS), dev),
-        _chk(part, torch.float64, "part", None, dev), lik, ass, lo, hi, int(KS), _gate_ptr(gate, dev), _stream())
+        _chk(part, torch.float64, "part", None, dev), lik, ass, lo, hi, int(KS), _gate_ptr(gate, dev), _stream(),
+        0 if base is None else _chk(base, torch.float64, "base", (V, KS), dev))
+
+
+def csc_subset(word_ptr, csc_ent, csc_doc, doc_mask):
+    """(word_ptr, csc_ent) of the CSC slots whose document is in ``doc_mask`` (bool [D], device), slot
+    order kept; plus the per-word entry counts on the host (for a SuffPlan)."""
+    V = word_ptr.numel() - 1
+    keep = doc_mask[csc_doc.long()]
+    wlen = (word_ptr[1:] - word_ptr[:-1]).long()
+    word_of = torch.repeat_interleave(torch.arange(V, device=word_ptr.device), wlen)
+    cnt = torch.bincount(word_of[keep], minlength=V)
+    ptr = torch.zeros(V + 1, dtype=torch.int64, device=word_ptr.device)
+    ptr[1:] = torch.cumsum(cnt, 0)
+    return ptr.to(torch.int32), csc_ent[keep].contiguous(), cnt.cpu().numpy()
 
 
 def gs_mstep_control(cw, class_total, beta, K, scalars, params, ctl, hist, done_count, rows=None, newton=None):

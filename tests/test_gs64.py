@@ -226,3 +226,25 @@ def test_split_documents_match_oracle(K, env, monkeypatch):
     eng.e_step()
     torch.cuda.synchronize()
     assert torch.equal(g1, eng.gamma)
+
+
+@pytest.mark.parametrize("K", [20, 100])
+def test_suff_split_matches_single_pass(K, monkeypatch):
+    """Early / late sufficient statistics (the early pass overlaps the longest-document bucket, the late
+    pass adds its rows first) against the single CSC pass: class_word, class totals and likelihood."""
+    c = _edge_corpus(seed=3, max_len=5000)
+    lb = _log_beta(c.num_terms, K, seed=6)
+    out = []
+    for mode in ("0", "force"):
+        monkeypatch.setenv("ONI_SUFF_SPLIT", mode)
+        eng, sc = _gpu_estep(c, K, lb, 0.45, LDASettings(var_max_iter=4), 32)
+        assert (eng._suff_split is None) == (mode == "0")
+        eng.e_step()                                   # graph replay of the same launch sequence
+        torch.cuda.synchronize()
+        out.append((eng._cw_local[:, :K].cpu().numpy(), eng.class_total[:K].cpu().numpy(), sc,
+                    eng.gamma.cpu().numpy()))
+    (cw0, ct0, sc0, g0), (cw1, ct1, sc1, g1) = out
+    assert np.array_equal(g0, g1)
+    assert _rel(cw1, cw0, 1e-30) < 1e-13
+    assert _rel(ct1, ct0, 1e-30) < 1e-13
+    assert abs(sc1[0] - sc0[0]) <= 1e-13 * abs(sc0[0])
