@@ -576,12 +576,14 @@ def gs_suff64(word_ptr, csc_ent, plan: "SuffPlan", cphi, cw, part, gate=None, sc
     partial rows part[b] = {lik slice, alpha_ss slice, column sums} for ``colsum_partials``.
     ``base`` [V, KS] (optional): added to each written row first (cw[w] = base[w] + sum)."""
     V, KS = cw.shape
-    nnz = csc_ent.numel()
+    nnz = cphi.shape[0]            # csc_ent may be a subset of the corpus entries (csc_subset)
     dev = cw.device
     if plan.covers_all and plan.order.numel() != V:
         raise ValueError("suff plan does not cover the vocabulary")
     if plan.order.numel() == 0:
         return
+    if csc_ent.numel() > nnz:
+        raise ValueError("csc_ent longer than the corpus")
     if part.dim() != 2 or part.shape[1] != KS + 2 or part.shape[0] < max(plan.n_blocks, 1):
         raise ValueError(f"part: shape {tuple(part.shape)}, expected [>= {plan.n_blocks}, {KS + 2}]")
     if scalars is None:
@@ -591,7 +593,7 @@ def gs_suff64(word_ptr, csc_ent, plan: "SuffPlan", cphi, cw, part, gate=None, sc
         D = scalars[0].numel()
         lik, ass, lo, hi = _scalar_slice(scalars, D, dev)
     lib().gs_suff64(
-        _chk(word_ptr, torch.int32, "word_ptr", (V + 1,), dev), _chk(csc_ent, torch.int32, "csc_ent", (nnz,), dev),
+        _chk(word_ptr, torch.int32, "word_ptr", (V + 1,), dev), _chk(csc_ent, torch.int32, "csc_ent", None, dev),
         _chk(plan.order, torch.int32, "order", (plan.order.numel(),), dev), plan.n_heavy, plan.n_medium, plan.n_light,
         _chk(cphi, torch.float64, "cphi", (nnz, KS), dev), _chk(cw, torch.float64, "cw", (V, KS), dev),
         _chk(part, torch.float64, "part", None, dev), lik, ass, lo, hi, int(KS), _gate_ptr(gate, dev), _stream(),
