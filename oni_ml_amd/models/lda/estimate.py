@@ -200,13 +200,17 @@ def estimate(corpus: Corpus, num_topics: int, alpha_init: float, settings: LDASe
     res.log_beta = eng.log_beta()
     res.gamma = eng.gather_gamma()
     if write_word_assignments and rank0:
-        # argmax on the device now; the text formatting joins the deferred model files when allowed
-        z = word_topics(corpus, res.log_beta, res.gamma, device=eng.cw.device)
-        wa = os.path.join(outdir, "word-assignments.dat")
+        # device argmax + native formatting; on the background writer with the deferred model files
+        # when allowed (the caller's next stages do not wait for it)
+        wa, lb, g, dev = os.path.join(outdir, "word-assignments.dat"), res.log_beta, res.gamma, eng.cw.device
+
+        def _assign():
+            _write_assignment_file(wa, corpus, word_topics(corpus, lb, g, device=dev))
+
         if ok and defer_files:
-            writer.submit(_write_assignment_file, wa, corpus, z)
+            writer.submit(_assign)
         else:
-            _write_assignment_file(wa, corpus, z)
+            _assign()
     if rank0:
         with open(os.path.join(outdir, "lda_stats.json"), "w") as f:
             json.dump(dict(em_iterations=res.em_iterations, seconds=res.seconds, alpha=res.alpha,
