@@ -97,8 +97,9 @@ __device__ __forceinline__ void put_tagged(unsigned long long* p, float v, unsig
 }
 
 // sum_{q < n} value(x[q * stride]) in order q = 0, 1, ..., in double, each granule
-// awaited until it carries `tag`; 8 loads in flight per round trip.  Returns false
-// on a timeout.
+// awaited until it carries `tag`; 8 loads in flight per round trip, and the granules still
+// missing their tag are re-polled together (one round trip per poll, not one per stale
+// granule).  Returns false on a timeout.
 __device__ __forceinline__ bool tagged_sum(const unsigned long long* x, int n, int stride, unsigned tag, double& out) {
   double s = 0.0;
   long spins = 0;
@@ -107,19 +108,24 @@ __device__ __forceinline__ bool tagged_sum(const unsigned long long* x, int n, i
 #pragma unroll
     for (int u = 0; u < 8; ++u)
       v[u] = __hip_atomic_load(x + (size_t)min(q0 + u, n - 1) * stride, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (;;) {
+      unsigned pending = 0;
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      if (q0 + u >= n) continue;
-      while ((unsigned)(v[u] >> 32) != tag) {
-        if (++spins > kSplitSpinLimit) {
-          out = __builtin_nan("");
-          return false;
-        }
-        __builtin_amdgcn_s_sleep(1);
-        v[u] = __hip_atomic_load(x + (size_t)(q0 + u) * stride, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      for (int u = 0; u < 8; ++u) pending |= (q0 + u < n && (unsigned)(v[u] >> 32) != tag) ? (1u << u) : 0u;
+      if (pending == 0) break;
+      if (++spins > kSplitSpinLimit) {
+        out = __builtin_nan("");
+        return false;
       }
-      s += (double)__uint_as_float((unsigned)(v[u] & 0xffffffffu));
+      __builtin_amdgcn_s_sleep(1);
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if ((pending >> u) & 1u)
+          v[u] = __hip_atomic_load(x + (size_t)(q0 + u) * stride, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+      if (q0 + u < n) s += (double)__uint_as_float((unsigned)(v[u] & 0xffffffffu));
   }
   out = s;
   return true;

@@ -919,7 +919,9 @@ __device__ __forceinline__ void put_tagged_bits(unsigned long long* p, unsigned 
 }
 
 // sum_{q < n} of the double at granules (x[q * stride], x[q * stride + 1]) = (lo, hi) bits,
-// in order q = 0, 1, ...; 4 segments (8 granules) in flight per round trip.  False on a timeout.
+// in order q = 0, 1, ...; 4 segments (8 granules) in flight per round trip.  Granules that do not
+// carry `tag` yet are re-polled TOGETHER (one round trip per poll, not one per stale granule).
+// False on a timeout.
 __device__ __forceinline__ bool tagged_sum_f64(const unsigned long long* x, int n, int stride, unsigned tag,
                                                double& out) {
   double s = 0.0;
@@ -930,18 +932,22 @@ __device__ __forceinline__ bool tagged_sum_f64(const unsigned long long* x, int 
     for (int u = 0; u < 8; ++u)
       v[u] = __hip_atomic_load(x + (size_t)min(q0 + u / 2, n - 1) * stride + (u & 1), __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_AGENT);
+    for (;;) {
+      unsigned pending = 0;
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      if (q0 + u / 2 >= n) continue;
-      while ((unsigned)(v[u] >> 32) != tag) {
-        if (++spins > kSplitSpinLimit) {
-          out = __builtin_nan("");
-          return false;
-        }
-        __builtin_amdgcn_s_sleep(1);
-        v[u] = __hip_atomic_load(x + (size_t)(q0 + u / 2) * stride + (u & 1), __ATOMIC_RELAXED,
-                                 __HIP_MEMORY_SCOPE_AGENT);
+      for (int u = 0; u < 8; ++u)
+        pending |= (q0 + u / 2 < n && (unsigned)(v[u] >> 32) != tag) ? (1u << u) : 0u;
+      if (pending == 0) break;
+      if (++spins > kSplitSpinLimit) {
+        out = __builtin_nan("");
+        return false;
       }
+      __builtin_amdgcn_s_sleep(1);
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if ((pending >> u) & 1u)
+          v[u] = __hip_atomic_load(x + (size_t)(q0 + u / 2) * stride + (u & 1), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
     }
 #pragma unroll
     for (int u = 0; u < 8; u += 2)
