@@ -1047,17 +1047,18 @@ __global__ __launch_bounds__(512) void gs_split(GSArgs a, SplitArgs sp) {
       c[r] = crow[pc];
     }
   };
-  auto load_rows = [&](const int (&w)[RMAX]) {
+  auto load_rows = [&](const int (&w)[RMAX], unsigned v) {
     if (!active) return;
 #pragma unroll
     for (int r = 0; r < RMAX; ++r) {
+      // rounds past this segment's range gather nothing (a segment is often one or two rounds)
       const double* brow = a.beta + (size_t)w[r] * KS;
 #pragma unroll
-      for (int i = 0; i < KPL; ++i) bc[r][i] = brow[min(q + TG * i, KS - 1)];
+      for (int i = 0; i < KPL; ++i) bc[r][i] = ((v >> r) & 1u) ? brow[min(q + TG * i, KS - 1)] : 0.0;
     }
   };
   load_ids(0, wc, cc, vc);
-  load_rows(wc);
+  load_rows(wc, vc);
   load_ids(nch > 1 ? 1 : 0, wn, cn, vn);
   lds_barrier();
   double L = 0.0, L_old = 0.0, conv = 1.0, GS = 0.0, LWs = 0.0;
@@ -1080,7 +1081,17 @@ __global__ __launch_bounds__(512) void gs_split(GSArgs a, SplitArgs sp) {
         double cr[RMAX];
 #pragma unroll
         for (int r = 0; r < RMAX; ++r) cr[r] = ((vc >> r) & 1u) ? (double)cc[r] : 0.0;
-        word_steps<RMAX, KPL, LSW>(E, bc, cr, acc, lw);
+        // only the rounds this segment's range fills (workgroup-uniform)
+        const int R = (m1 - m0 + NS - 1) / NS;
+        if (R <= 1) {
+          word_steps<1, KPL, LSW>(E, bc, cr, acc, lw);
+        } else if (R <= 2 || RMAX <= 2) {
+          word_steps<(RMAX < 2 ? RMAX : 2), KPL, LSW>(E, bc, cr, acc, lw);
+        } else if (R <= 4 || RMAX <= 4) {
+          word_steps<(RMAX < 4 ? RMAX : 4), KPL, LSW>(E, bc, cr, acc, lw);
+        } else {
+          word_steps<RMAX, KPL, LSW>(E, bc, cr, acc, lw);
+        }
         // beyond the prefetched rounds
         stream_tail<RMAX, KS, KPL, TG, LSW>(a.beta, wrow, crow, m0 + slot + RMAX * NS, m1, NS, q, E, bc, acc, lw);
         const int j1 = j + 1 < nch ? j + 1 : 0;
@@ -1091,7 +1102,7 @@ __global__ __launch_bounds__(512) void gs_split(GSArgs a, SplitArgs sp) {
           cc[r] = cn[r];
         }
         vc = vn;
-        load_rows(wc);
+        load_rows(wc, vc);
         load_ids(j2, wn, cn, vn);
 #pragma unroll
         for (int i = 0; i < KPL; ++i) acc[i] = bits_sum<0, LSW, false>(acc[i]);
