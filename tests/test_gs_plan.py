@@ -46,3 +46,24 @@ def test_split_plan_one_batch_longest_first(monkeypatch):
     sp2 = H.GSSplitPlan(cand, lens, 100, 32, "cpu", seg_words=128, max_seg=16, max_batches=8)
     assert sp2.leftover == [] and len(sp2.batches) >= 2
     assert all(bb["n_blocks"] <= 20 for bb in sp2.batches)
+
+
+def test_csc_subset_partitions_each_word_in_order():
+    """csc_subset (early / late suff-stats): the two subsets partition every word's CSC slots by
+    document, each keeping the original slot order."""
+    import torch
+    from oni_ml_amd.corpus.csr import DeviceCorpus
+    from oni_ml_amd.ops.hip import csc_subset
+    from oni_ml_amd.synth.corpus import planted_corpus
+    c = planted_corpus(num_docs=300, num_terms=120, num_topics=4, seed=2)
+    dc = DeviceCorpus.build(c, "cpu")
+    late = torch.zeros(c.num_docs, dtype=torch.bool)
+    late[torch.tensor([0, 5, 17, 100, 299])] = True
+    pe, ee, le = csc_subset(dc.word_ptr, dc.csc_ent, dc.csc_doc, ~late)
+    pl, el, ll = csc_subset(dc.word_ptr, dc.csc_ent, dc.csc_doc, late)
+    wp, ce, cd = dc.word_ptr.tolist(), dc.csc_ent.tolist(), dc.csc_doc.tolist()
+    assert int(pe[-1]) + int(pl[-1]) == len(ce) and (le + ll).tolist() == np.diff(wp).tolist()
+    for w in range(c.num_terms):
+        slots = range(wp[w], wp[w + 1])
+        assert ee[int(pe[w]):int(pe[w + 1])].tolist() == [ce[s] for s in slots if not late[cd[s]]]
+        assert el[int(pl[w]):int(pl[w + 1])].tolist() == [ce[s] for s in slots if late[cd[s]]]
