@@ -247,6 +247,7 @@ __global__ __launch_bounds__(256) void gs_tiny(GSArgs a) {
   const double vconv = params_vconv(a.params);
   const int K = a.K;
   const int d = a.order[item];
+  if (d < 0) return;   // XCD placement gap (GSPlan.xcd_gaps): this document slot only
   const int s0 = a.doc_ptr[d];
   const int n = min(a.doc_ptr[d + 1] - s0, NMAX);
   const int* __restrict__ wrow = a.word_idx + s0;
@@ -372,6 +373,7 @@ __global__ __launch_bounds__(256) void gs_small(GSArgs a) {
   const double vconv = params_vconv(a.params);
   const int K = a.K;
   const int d = a.order[item];
+  if (d < 0) return;   // XCD placement gap (GSPlan.xcd_gaps): this document slot only
   const int s0 = a.doc_ptr[d], n = a.doc_ptr[d + 1] - s0;
   const int U = a.gs_updates;
   const int W = n > 0 ? (n + U - 1) / U : 1;
@@ -623,6 +625,7 @@ __global__ __launch_bounds__(team_threads(KS, NW), MINW) void gs_team(GSArgs a) 
   const int q = lane >> LSW, sl = lane & (NSW - 1);
   const int slot = wv * NSW + sl;
   const int d = a.order[item];
+  if (d < 0) return;   // XCD placement gap (GSPlan.xcd_gaps): this document slot only
   const int s0 = a.doc_ptr[d], n = a.doc_ptr[d + 1] - s0;
   const int U = a.gs_updates;
   const int W = n > 0 ? (n + U - 1) / U : 1;

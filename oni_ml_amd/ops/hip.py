@@ -787,6 +787,36 @@ class GSPlan:
         if m.any():
             self.plan.append((GS_TINY, torch.from_numpy(order[m].copy()).to(device)))
         self.tiny_max = tiny
+        # ONI_GS_XCD_SKIP=1: the other buckets leave XCD 0 (the longest document's, isolate_longest)
+        # to team8 -- their workgroups b = 0 mod 8 get empty document slots.  Measured on the headline
+        # day: 2.20 / 2.27 vs 2.18 / 2.18 ms per EM iteration (off by default; profiles/r2_tuning_log.md)
+        self.xcd_skip = bool(iso > 0 and os.environ.get("ONI_GS_XCD_SKIP", "0") != "0"
+                             and any(v == GS_TEAM8 for v, _ in self.plan))
+        if self.xcd_skip:
+            dpb = {GS_TINY: 256 // (8 if KS <= 32 else 16), GS_SMALL: 16, GS_TEAM1: 4 if KS <= 32 else 1,
+                   GS_TEAM4: 1}
+            self.plan = [(v, o if v == GS_TEAM8 else
+                          torch.from_numpy(self.xcd_gaps(o.cpu().numpy(), dpb[v])).to(device))
+                         for v, o in self.plan]
+
+    @staticmethod
+    def xcd_gaps(o, dpb: int, xcds: int = 8):
+        """Document order with the slots of every workgroup b = 0 mod xcds empty (-1): a launch of
+        dpb documents per workgroup then leaves XCD 0 alone under round-robin dispatch."""
+        import numpy as np
+        o = np.asarray(o, np.int32)
+        nb = -(-o.size // dpb)
+        out = []
+        b = 0
+        i = 0
+        while i < nb:
+            if b % xcds == 0:
+                out.append(np.full(dpb, -1, np.int32))
+            else:
+                out.append(o[i * dpb:(i + 1) * dpb])
+                i += 1
+            b += 1
+        return np.concatenate(out) if out else o
 
     @staticmethod
     def isolate_longest(o, m: int, xcds: int = 8):

@@ -67,3 +67,13 @@ def test_csc_subset_partitions_each_word_in_order():
         slots = range(wp[w], wp[w + 1])
         assert ee[int(pe[w]):int(pe[w + 1])].tolist() == [ce[s] for s in slots if not late[cd[s]]]
         assert el[int(pl[w]):int(pl[w + 1])].tolist() == [ce[s] for s in slots if late[cd[s]]]
+
+
+def test_xcd_gaps_leave_block_zero_mod_8_empty():
+    o = np.arange(1, 101, dtype=np.int32)
+    for dpb in (1, 4, 16, 32):
+        g = GSPlan.xcd_gaps(o, dpb)
+        blocks = [g[i:i + dpb] for i in range(0, g.size, dpb)]
+        assert all((blk == -1).all() for b, blk in enumerate(blocks) if b % 8 == 0)
+        assert g[g >= 0].tolist() == o.tolist()
+        assert all((blk >= 0).all() for b, blk in enumerate(blocks[:-1]) if b % 8)
