@@ -157,6 +157,9 @@ PYBIND11_MODULE(_onihip, m) {
                   P<double>(alpha_ss),   P<int>(iters),         P<long long>(dbg)};
     oni::launch_gs_estep(a, variant, KS, S(stream));
   });
+  m.def("init_random_ss", [](u cw, int V, int K, int KS, unsigned long long seed, u stream) {
+    oni::launch_init_random_ss(P<double>(cw), V, K, KS, seed, S(stream));
+  });
   m.def("gs_split_capacity", [](int KS) { return oni::gs_split_capacity(KS); });
   m.def("gs_split", [](u doc_ptr, u word_idx, u counts, u beta, int K, int KS, int gs_updates, u params, u gamma,
                        u cphi, u lik, u alpha_ss, u iters, u seg_doc, u seg_index, u seg_count, u seg_base,

@@ -237,6 +237,9 @@ void launch_gs_suff64(const int* word_ptr, const int* csc_ent, const int* order,
 void launch_gs_mstep_control(const double* cw, const double* class_total, double* beta, int V, int K, int KS,
                              const int* rows, int n_rows, const EMControlArgs& c, const NewtonArgs& nw,
                              hipStream_t s);
+// lda-c random start on the device: cw[w][k] = 1/V + u(seed, k V + w) (k < K), 0 for padding;
+// the same values as csrc/native random_ss (counter-based splitmix64).
+void launch_init_random_ss(double* cw, int V, int K, int KS, unsigned long long seed, hipStream_t s);
 void launch_gs_mstep(const double* cw, const double* class_total, double* beta, int V, int K, int KS,
                      const double* gate, hipStream_t s);
 

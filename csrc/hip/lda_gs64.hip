@@ -1954,6 +1954,34 @@ __global__ __launch_bounds__(256) void gs_suff64(const int* __restrict__ word_pt
   }
 }
 
+// ------------------------------------------------------------ random init ---
+// lda-c "random" start (random_initialize_ss): class_word[k][w] = 1/V + u, u ~ U[0, 1) from a
+// counter-based generator, so the host (csrc/native, CPU backends) and the device produce the same
+// bits without a host-side stream: u = splitmix64(splitmix64(seed) ^ (k V + w)) >> 11, x 2^-53.
+__device__ __forceinline__ unsigned long long smix64(unsigned long long x) {
+  x += 0x9E3779B97F4A7C15ull;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+  return x ^ (x >> 31);
+}
+
+__global__ __launch_bounds__(256) void init_random_ss_kernel(double* __restrict__ cw, int V, int K, int KS,
+                                                             unsigned long long seed) {
+  const unsigned long long s = smix64(seed);
+  const double inv = 1.0 / (double)V;
+  const long long total = (long long)V * KS;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int w = (int)(i / KS), k = (int)(i % KS);
+    double v = 0.0;
+    if (k < K) {
+      const unsigned long long h = smix64(s ^ ((unsigned long long)k * (unsigned long long)V + (unsigned long long)w));
+      v = inv + (double)(h >> 11) * 0x1.0p-53;
+    }
+    cw[i] = v;
+  }
+}
+
 // ----------------------------------------------------------------- M-step ---
 __device__ __forceinline__ double mle(double c, double ct) { return c > 0.0 ? c / ct : kExpM100; }
 
@@ -2179,6 +2207,15 @@ void launch_gs_mstep_control(const double* cw, const double* class_total, double
   if (blocks < 1) blocks = 1;
   hipLaunchKernelGGL(gs::gs_mstep_control_kernel, dim3((unsigned)blocks), dim3(256), 0, s, cw, class_total, beta, V,
                      K, KS, rows, n_rows, c, nw);
+  ONI_HIP_CHECK(hipGetLastError());
+}
+
+void launch_init_random_ss(double* cw, int V, int K, int KS, unsigned long long seed, hipStream_t s) {
+  const long long total = (long long)V * KS;
+  if (total <= 0) return;
+  long long blocks = (total + 255) / 256;
+  if (blocks > 8192) blocks = 8192;
+  hipLaunchKernelGGL(gs::init_random_ss_kernel, dim3((unsigned)blocks), dim3(256), 0, s, cw, V, K, KS, seed);
   ONI_HIP_CHECK(hipGetLastError());
 }
 

@@ -324,6 +324,39 @@ PYBIND11_MODULE(_oninative, m) {
       },
       py::arg("path"), py::arg("threads") = 0);
 
+  // lda-c "random" start: [K, V] class_word = 1/V + u, the counter-based generator of the HIP
+  // init_random_ss kernel (csrc/hip/lda_gs64.hip), so every backend starts from the same bits
+  m.def(
+      "random_ss",
+      [](int K, int V, unsigned long long seed, int threads) {
+        if (K < 0 || V < 0) throw std::invalid_argument("K, V must be >= 0");
+        py::array_t<double> out({(py::ssize_t)K, (py::ssize_t)V});
+        double* o = out.mutable_data();
+        if (threads <= 0) threads = default_threads();
+        {
+          py::gil_scoped_release rel;
+          auto mix = [](unsigned long long x) {
+            x += 0x9E3779B97F4A7C15ull;
+            x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+            x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+            return x ^ (x >> 31);
+          };
+          const unsigned long long s = mix(seed);
+          const double inv = 1.0 / (double)V;
+          const long long total = (long long)K * V;
+          auto work = [&](int t) {
+            for (long long i = total * t / threads; i < total * (t + 1) / threads; ++i)
+              o[i] = inv + (double)(mix(s ^ (unsigned long long)i) >> 11) * 0x1.0p-53;
+          };
+          std::vector<std::thread> th;
+          for (int t = 1; t < threads; ++t) th.emplace_back(work, t);
+          work(0);
+          for (auto& x : th) x.join();
+        }
+        return out;
+      },
+      py::arg("K"), py::arg("V"), py::arg("seed"), py::arg("threads") = 0);
+
   // ---------------------------------------------------------------- lda-c --
   m.def("digamma", &ldac_digamma);
   m.def("trigamma", &ldac_trigamma);

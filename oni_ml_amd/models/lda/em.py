@@ -525,10 +525,19 @@ class LDAEngine:
 
     # ------------------------------------------------------------------ init
     def init_random(self, seed: Optional[int] = None):
-        """random_initialize_ss + lda_mle(..., 0): cw[k][w] = 1/V + U(0,1)."""
-        rng = np.random.default_rng(self.seed if seed is None else seed)
-        cw = 1.0 / self.V + rng.random((self.K, self.V))
-        self._set_ss_host(cw)
+        """random_initialize_ss + lda_mle(..., 0): cw[k][w] = 1/V + U(0,1).  U comes from a counter-based
+        generator (splitmix64 of (seed, k V + w)): the fp64 HIP engine fills class_word on the device
+        (no host stream, no 8-byte-per-entry upload), every other backend gets the same bits from the
+        native ``random_ss``."""
+        s = self.seed if seed is None else seed
+        if self.backend == "hip" and self.fp64:
+            from ...ops import hip as H
+            H.init_random_ss(self.cw, self.K, s)
+            H.colsum_partials(self.cw, self.V, self.class_total)
+            self._mstep_beta()
+        else:
+            from ...ops import native
+            self._set_ss_host(native.lib().random_ss(self.K, self.V, int(s) & 0xFFFFFFFFFFFFFFFF))
         self.alpha = self.alpha_init
 
     def init_seeded(self, corpus_global: Corpus, seed: Optional[int] = None):

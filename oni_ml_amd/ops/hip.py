@@ -363,6 +363,13 @@ def rows_accumulate(rows, ptr, src, own, recv, out):
                           int(n), int(W), _stream())
 
 
+def init_random_ss(cw, K, seed):
+    """cw [V, KS] float64 <- lda-c random start 1/V + u(seed, k V + w) (native ``random_ss`` bits)."""
+    V, KS = cw.shape
+    lib().init_random_ss(_chk(cw, torch.float64, "cw", (V, KS), cw.device), int(V), int(K), int(KS),
+                         int(seed) & 0xFFFFFFFFFFFFFFFF, _stream())
+
+
 def colsum_partials(part, n_blocks, out, gate=None):
     """out[k] = sum_b part[b, k] for b < n_blocks (deterministic order)."""
     dev = part.device

@@ -160,5 +160,11 @@ def test_two_rank_ml_ops_pipeline_matches_one_rank(tmp_path, exchange):
     s1 = json.load(open(tmp_path / "one" / "run_summary.json"))
     s2 = json.load(open(tmp_path / "two" / "run_summary.json"))
     assert s1["scored"] == s2["scored"] > 0
-    assert (tmp_path / "one" / "flow_results.csv").read_text().splitlines()[:20] == \
-        (tmp_path / "two" / "flow_results.csv").read_text().splitlines()[:20]
+    # the same events flagged, in the same order; the two scores agree up to the all-reduce order
+    f1 = (tmp_path / "one" / "flow_results.csv").read_text().splitlines()[:20]
+    f2 = (tmp_path / "two" / "flow_results.csv").read_text().splitlines()[:20]
+    assert len(f1) == len(f2)
+    for a, b in zip(f1, f2):
+        ra, rb = a.split(","), b.split(",")
+        assert ra[:-2] == rb[:-2]
+        assert np.allclose([float(x) for x in ra[-2:]], [float(x) for x in rb[-2:]], rtol=1e-9)

@@ -248,3 +248,16 @@ def test_suff_split_matches_single_pass(K, monkeypatch):
     assert _rel(cw1, cw0, 1e-30) < 1e-13
     assert _rel(ct1, ct0, 1e-30) < 1e-13
     assert abs(sc1[0] - sc0[0]) <= 1e-13 * abs(sc0[0])
+
+
+def test_device_random_init_matches_native():
+    """The fp64 engine's on-device lda-c random start equals the native counter-based generator the CPU
+    backends use (same bits), and class_total is its column sum."""
+    c = planted_corpus(num_docs=200, num_terms=300, num_topics=4, seed=1)
+    eng = LDAEngine(c, 20, LDASettings(), backend="hip", seed=11, precision="fp64")
+    eng.init_random()
+    torch.cuda.synchronize()
+    ref = native.lib().random_ss(20, c.num_terms, 11)
+    assert np.array_equal(eng.cw[:, :20].cpu().numpy(), ref.T)
+    assert eng.cw[:, 20:].abs().max().item() == 0 if eng.KS > 20 else True
+    assert _rel(eng.class_total[:20].cpu().numpy(), ref.sum(1), 1e-30) < 1e-14

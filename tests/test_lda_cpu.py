@@ -177,3 +177,15 @@ def test_settings_roundtrip(tmp_path):
     s2 = LDASettings.load(str(p))
     assert (s2.var_max_iter, s2.em_max_iter, s2.estimate_alpha) == (30, 50, False)
     assert s2.var_converged == s.var_converged
+
+
+def test_random_ss_counter_generator():
+    """lda-c random start from the counter-based generator: deterministic per seed, thread-count
+    invariant, 1/V + U[0, 1), distinct seeds differ."""
+    N = native.lib()
+    a = N.random_ss(5, 1000, 7, threads=1)
+    b = N.random_ss(5, 1000, 7, threads=8)
+    assert a.shape == (5, 1000) and np.array_equal(a, b)
+    assert not np.array_equal(a, N.random_ss(5, 1000, 8))
+    u = a - 1.0 / 1000
+    assert u.min() >= 0.0 and u.max() < 1.0 and abs(u.mean() - 0.5) < 0.02
