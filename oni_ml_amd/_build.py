@@ -32,6 +32,14 @@ HIPCC = str(ROCM / "bin" / "hipcc")
 ARCH = os.environ.get("ONI_OFFLOAD_ARCH", "gfx950")
 
 _lock = threading.Lock()
+# what the last build_all() did, per artefact: {"artefact", "action": compiled | up-to-date, "seconds"}
+RECORD: list = []
+
+
+def _note(out: Path, compiled: bool, t0: float):
+    import time
+    RECORD.append(dict(artefact=str(Path(out).relative_to(ROOT)), action="compiled" if compiled else "up-to-date",
+                       seconds=round(time.perf_counter() - t0, 3)))
 
 
 def _ext_suffix() -> str:
@@ -78,13 +86,29 @@ def _stamp(out: Path, digest: str):
 
 
 def _compile(src: Path, out: Path, cmd_prefix, flags, deps, verbose):
+    import time
+    t0 = time.perf_counter()
     digest = _hash([src] + list(deps), cmd_prefix + flags)
     if not _stale(out, digest):
+        _note(out, False, t0)
         return out
     out.parent.mkdir(parents=True, exist_ok=True)
     _run(cmd_prefix + flags + ["-c", str(src), "-o", str(out)], verbose)
     _stamp(out, digest)
+    _note(out, True, t0)
     return out
+
+
+def _link(out: Path, objs, cmd, verbose):
+    import time
+    t0 = time.perf_counter()
+    digest = _hash(objs, cmd)
+    stale = _stale(out, digest)
+    if stale:
+        out.parent.mkdir(parents=True, exist_ok=True)
+        _run(cmd, verbose)
+        _stamp(out, digest)
+    _note(out, stale, t0)
 
 
 def hip_flags():
@@ -118,11 +142,7 @@ def build_hip(verbose=False, jobs=8) -> Path:
     with ThreadPoolExecutor(max_workers=jobs) as ex:
         objs = list(ex.map(one, srcs + [bind]))
     link = [HIPCC, "-shared", f"--offload-arch={ARCH}", "-fPIC", "-o", str(out)] + [str(o) for o in objs]
-    digest = _hash(objs, link)
-    if _stale(out, digest):
-        LIB.mkdir(parents=True, exist_ok=True)
-        _run(link, verbose)
-        _stamp(out, digest)
+    _link(out, objs, link, verbose)
     return out
 
 
@@ -146,11 +166,7 @@ def build_native(verbose=False, jobs=8) -> Path:
     with ThreadPoolExecutor(max_workers=jobs) as ex:
         objs = list(ex.map(one, lib_srcs + [bind]))
     link = [cxx, "-shared", "-fPIC", "-pthread", "-o", str(out)] + [str(o) for o in objs]
-    digest = _hash(objs, link)
-    if _stale(out, digest):
-        LIB.mkdir(parents=True, exist_ok=True)
-        _run(link, verbose)
-        _stamp(out, digest)
+    _link(out, objs, link, verbose)
     # standalone lda-c compatible executable
     main = CSRC / "native" / "lda_main.cpp"
     if main.exists():
@@ -158,10 +174,7 @@ def build_native(verbose=False, jobs=8) -> Path:
         exe = LIB / "lda"
         lib_objs = [o for o in objs if o.stem != "bind_native"]
         cmd = [cxx, "-pthread", "-o", str(exe), str(mo)] + [str(o) for o in lib_objs]
-        digest = _hash([mo] + lib_objs, cmd)
-        if _stale(exe, digest):
-            _run(cmd, verbose)
-            _stamp(exe, digest)
+        _link(exe, [mo] + lib_objs, cmd, verbose)
     return out
 
 
@@ -187,6 +200,7 @@ def build_sanitized(kind: str = "thread", verbose=False) -> Path:
 
 def build_all(verbose=False, hip=True, native=True):
     with _lock:
+        RECORD.clear()
         outs = []
         if native:
             o = build_native(verbose)

@@ -443,8 +443,16 @@ class LDAEngine:
         work = list(self.gs_plan.plan)
         if self.gs_plan.split is not None:
             work.insert(0, ("split", self.gs_plan.split.batches))
+        # early / late suff-stats (phase "all"): work[0], the longest-document bucket, runs alone on
+        # streams[1] (late_s); the early pass joins every other stream, so no other bucket may share
+        # late_s (with 6 work items the round robin would put item 4 there and the early pass would
+        # read its cphi rows before they are written)
+        ss = self._suff_split if (phase == "all" and len(work) >= 2) else None
+        late_s = streams[1] if ss is not None else None
         for si, (var, order) in zip(range(len(work)), work):
             s = streams[(si + 1) % len(streams)] if si < len(work) - 1 else main
+            if si > 0 and s is late_s:
+                s = streams[2]
             if s is not main and s not in used:
                 s.wait_event(self._ev_fork)
                 used.append(s)
@@ -456,10 +464,7 @@ class LDAEngine:
                 else:
                     H.gs_estep(dc.doc_ptr, dc.word_idx, dc.counts, order, self.beta, self.K, self._U, prm,
                                self.gamma, self.cphi, self.lik, self.ass, self.iters, var)
-        # early / late suff-stats (phase "all"): work[0], the longest-document bucket, runs on
-        # streams[1]; every other bucket is joined first and the early pass overlaps it
-        ss = self._suff_split if (phase == "all" and len(work) >= 2) else None
-        late_s = streams[1] if ss is not None else None
+        # every bucket but work[0] is joined first and the early pass overlaps work[0]
         for j, s in enumerate(used):
             self._ev_join[j].record(s)
             if s is not late_s:

@@ -5,17 +5,18 @@
 #   config 4  DNS 1-day (2M queries), K=20
 #   config 5  flow 30-day / 8 = 12.5M events per GPU, K=100
 set -o pipefail
-mkdir -p gpurun_out/cfg
+D=${OUTDIR:-gpurun_out}/cfg
+mkdir -p $D
 export TMPDIR=/tmp
 run() {
   local name=$1; shift
-  timeout -k 10 400 python -u bench.py --steps 20 --warmup 3 "$@" > gpurun_out/cfg/$name.log 2>&1 || { echo "$name failed rc=$?"; tail -20 gpurun_out/cfg/$name.log; return 1; }
-  grep '^{' gpurun_out/cfg/$name.log | tail -1 > gpurun_out/cfg/$name.json
-  python - "$name" <<'PY'
+  timeout -k 10 400 python -u bench.py --steps 20 --warmup 3 "$@" > $D/$name.log 2>&1 || { echo "$name failed rc=$?"; tail -20 $D/$name.log; return 1; }
+  grep '^{' $D/$name.log | tail -1 > $D/$name.json
+  python - "$D/$name.json" "$name" <<'PY'
 import json, sys
-d = json.load(open(f"gpurun_out/cfg/{sys.argv[1]}.json"))
+d = json.load(open(sys.argv[1]))
 c = d["config"]
-print(f"{sys.argv[1]:10s} K={c['model'][-3:]} docs={c['docs_per_gpu']} V={c['vocab']} nnz={c['nnz_per_gpu']} "
+print(f"{sys.argv[2]:10s} K={c['model'][-3:]} docs={c['docs_per_gpu']} V={c['vocab']} nnz={c['nnz_per_gpu']} "
       f"ms/iter={d['ms_per_step']} docs/s={d['value']:.3e} var_iter_mean={d.get('var_iter_mean')} "
       f"converge={d.get('converge_seconds')}s/{d.get('converge_em_iters')}it corpus_build={d.get('corpus_build_s')}s")
 PY

@@ -228,17 +228,24 @@ def test_split_documents_match_oracle(K, env, monkeypatch):
     assert torch.equal(g1, eng.gamma)
 
 
-@pytest.mark.parametrize("K", [20, 100])
-def test_suff_split_matches_single_pass(K, monkeypatch):
+@pytest.mark.parametrize("K,split_min", [(20, None), (100, None), (20, "3000")])
+def test_suff_split_matches_single_pass(K, split_min, monkeypatch):
     """Early / late sufficient statistics (the early pass overlaps the longest-document bucket, the late
-    pass adds its rows first) against the single CSC pass: class_word, class totals and likelihood."""
-    c = _edge_corpus(seed=3, max_len=5000)
+    pass adds its rows first) against the single CSC pass: class_word, class totals and likelihood.
+    split_min: split documents plus all five length buckets = 6 work items, more than the 4 streams
+    (the case where a round-robin stream choice would put a bucket beside the late pass's stream)."""
+    if split_min:
+        monkeypatch.setenv("ONI_GS_SPLIT_MIN", split_min)
+    c = _edge_corpus(seed=3, max_len=9000 if split_min else 5000)
     lb = _log_beta(c.num_terms, K, seed=6)
     out = []
     for mode in ("0", "force"):
         monkeypatch.setenv("ONI_SUFF_SPLIT", mode)
         eng, sc = _gpu_estep(c, K, lb, 0.45, LDASettings(var_max_iter=4), 32)
         assert (eng._suff_split is None) == (mode == "0")
+        if split_min:
+            assert eng.gs_plan.split is not None and len(eng.gs_plan.plan) + 1 >= 6, \
+                [v for v, _ in eng.gs_plan.plan]
         eng.e_step()                                   # graph replay of the same launch sequence
         torch.cuda.synchronize()
         out.append((eng._cw_local[:, :K].cpu().numpy(), eng.class_total[:K].cpu().numpy(), sc,
