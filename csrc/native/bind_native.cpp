@@ -27,6 +27,23 @@ static py::array_t<T> to_np(const std::vector<T>& v) {
   return a;
 }
 
+// Consecutive text chunks -> one numpy uint8 array (the row-sharded writers hand it to os.pwrite or
+// to a byte all-to-all).
+static py::array_t<uint8_t> join_chunks(const std::vector<std::string>& chunks) {
+  int64_t total = 0;
+  for (const auto& c : chunks) total += (int64_t)c.size();
+  py::array_t<uint8_t> out(total);
+  uint8_t* dst = out.mutable_data();
+  {
+    py::gil_scoped_release rel;
+    for (const auto& c : chunks) {
+      std::memcpy(dst, c.data(), c.size());
+      dst += c.size();
+    }
+  }
+  return out;
+}
+
 static int default_threads() {
   unsigned n = std::thread::hardware_concurrency();
   return n ? (int)std::min(n, 16u) : 4;
@@ -150,6 +167,20 @@ PYBIND11_MODULE(_oninative, m) {
         if (group < 0 || group >= (int)t.dicts.size()) throw std::invalid_argument("bad group");
         return t.dicts[group].names;
       })
+      .def("dict_bytes", [](const TextTable& t, int group) {
+        // the group's names as (concatenated UTF-8 bytes, int64 offsets [n + 1]): the row-sharded
+        // dictionary merge packs them into fixed-width integer rows without a Python loop
+        if (group < 0 || group >= (int)t.dicts.size()) throw std::invalid_argument("bad group");
+        const auto& names = t.dicts[group].names;
+        py::array_t<int64_t> off(names.size() + 1);
+        int64_t* o = off.mutable_data();
+        o[0] = 0;
+        for (size_t i = 0; i < names.size(); ++i) o[i + 1] = o[i] + (int64_t)names[i].size();
+        py::array_t<uint8_t> data(o[names.size()]);
+        uint8_t* d = data.mutable_data();
+        for (size_t i = 0; i < names.size(); ++i) std::memcpy(d + o[i], names[i].data(), names[i].size());
+        return py::make_tuple(data, off);
+      })
       .def("weights", [](const TextTable& t) { return to_np(t.weight); })
       .def("row_text", [](const TextTable& t, int64_t i) {
         if (i < 0 || i >= (int64_t)t.rows.size()) throw std::out_of_range("row");
@@ -184,6 +215,41 @@ PYBIND11_MODULE(_oninative, m) {
       py::arg("threads") = default_threads(), py::arg("n") = -1);
 
   m.def(
+      "format_rows",
+      [](py::object order, py::list spec, const std::string& sep, int threads, int64_t n, bool row_ends) {
+        ColHolder h;
+        const int64_t* ord = nullptr;
+        py::array_t<int64_t, py::array::c_style | py::array::forcecast> oa;
+        int64_t max_row = n - 1;
+        if (!order.is_none()) {
+          oa = py::array_t<int64_t, py::array::c_style | py::array::forcecast>::ensure(order);
+          ord = oa.data();
+          n = oa.size();
+          max_row = -1;
+          for (int64_t i = 0; i < n; ++i) {
+            if (ord[i] < 0) throw std::invalid_argument("negative row index");
+            max_row = std::max(max_row, ord[i]);
+          }
+        }
+        if (n < 0) throw std::invalid_argument("format_rows needs n or order");
+        auto cols = build_cols(spec, h, max_row + 1);
+        for (auto& c : cols)
+          if (c.kind == OutCol::kTable && !c.rowmap && max_row >= (int64_t)c.table->rows.size())
+            throw std::invalid_argument("row index beyond table");
+        std::vector<int64_t> ends;
+        std::vector<std::string> chunks;
+        {
+          py::gil_scoped_release rel;
+          chunks = format_rows(ord, n, cols, sep, threads <= 0 ? default_threads() : threads, row_ends ? &ends : nullptr);
+        }
+        py::array_t<uint8_t> text = join_chunks(chunks);
+        if (!row_ends) return py::object(text);
+        return py::object(py::make_tuple(text, to_np(ends)));
+      },
+      py::arg("order"), py::arg("cols"), py::arg("sep") = ",", py::arg("threads") = 0, py::arg("n") = -1,
+      py::arg("row_ends") = false);
+
+  m.def(
       "dns_features",
       [](py::buffer data, py::array_t<int64_t, py::array::c_style | py::array::forcecast> offsets,
          std::vector<std::string> cc, std::vector<std::string> top, std::string special, int threads) {
@@ -212,6 +278,36 @@ PYBIND11_MODULE(_oninative, m) {
       },
       py::arg("data"), py::arg("offsets"), py::arg("country_codes"), py::arg("top_domains"),
       py::arg("special") = "intel", py::arg("threads") = default_threads());
+
+  // Concatenate byte spans of one buffer in the given order (the result-file merge: rows received
+  // from every rank, put in global sort order).
+  m.def(
+      "concat_spans",
+      [](py::array_t<uint8_t, py::array::c_style> src, py::array_t<int64_t, py::array::c_style | py::array::forcecast> starts,
+         py::array_t<int64_t, py::array::c_style | py::array::forcecast> lens) {
+        const int64_t n = starts.size();
+        if (lens.size() != n) throw std::invalid_argument("starts / lens differ in length");
+        const int64_t* s = starts.data();
+        const int64_t* l = lens.data();
+        const int64_t cap = src.size();
+        int64_t total = 0;
+        for (int64_t i = 0; i < n; ++i) {
+          if (s[i] < 0 || l[i] < 0 || s[i] + l[i] > cap) throw std::invalid_argument("span out of range");
+          total += l[i];
+        }
+        py::array_t<uint8_t> out(total);
+        uint8_t* d = out.mutable_data();
+        const uint8_t* b = src.data();
+        {
+          py::gil_scoped_release rel;
+          for (int64_t i = 0; i < n; ++i) {
+            std::memcpy(d, b + s[i], l[i]);
+            d += l[i];
+          }
+        }
+        return out;
+      },
+      py::arg("src"), py::arg("starts"), py::arg("lens"));
 
   m.def("scala_entropy", [](const std::string& s) { return scala_entropy(s); });
   m.def("java_double", [](double d) { return java_double(d); });
@@ -310,6 +406,28 @@ PYBIND11_MODULE(_oninative, m) {
         return write_corpus_text(path, p, D, words.data(), counts.data(), threads, assignments);
       },
       py::arg("path"), py::arg("doc_ptr"), py::arg("words"), py::arg("counts"), py::arg("threads") = 0,
+      py::arg("assignments") = false);
+  m.def(
+      "format_ldac_corpus",
+      [](py::array_t<int64_t, py::array::c_style | py::array::forcecast> ptr,
+         py::array_t<int32_t, py::array::c_style | py::array::forcecast> words,
+         py::array_t<int64_t, py::array::c_style | py::array::forcecast> counts, int threads, bool assignments) {
+        const int64_t D = (int64_t)ptr.size() - 1;
+        if (D < 0) throw std::invalid_argument("doc_ptr must have D+1 entries");
+        const int64_t* p = ptr.data();
+        if (p[0] != 0 || p[D] != (int64_t)words.size() || words.size() != counts.size())
+          throw std::invalid_argument("inconsistent corpus arrays");
+        for (int64_t d = 0; d < D; ++d)
+          if (p[d] > p[d + 1]) throw std::invalid_argument("non-monotone doc_ptr");
+        if (threads <= 0) threads = default_threads();
+        std::vector<std::string> chunks;
+        {
+          py::gil_scoped_release rel;
+          chunks = format_corpus_text(p, D, words.data(), counts.data(), threads, assignments);
+        }
+        return join_chunks(chunks);
+      },
+      py::arg("doc_ptr"), py::arg("words"), py::arg("counts"), py::arg("threads") = 0,
       py::arg("assignments") = false);
   m.def(
       "read_ldac_corpus",

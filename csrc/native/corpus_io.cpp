@@ -36,12 +36,10 @@ void parallel_for(int threads, F&& f) {
 
 }  // namespace
 
-int64_t write_corpus_text(const std::string& path, const int64_t* ptr, int64_t D, const int32_t* w,
-                          const int64_t* c, int threads, bool assignments) {
-  FILE* f = std::fopen(path.c_str(), "wb");
-  if (!f) throw std::runtime_error("cannot open for writing: " + path);
-  threads = std::max(1, threads);
-  // blocks of ~2^18 entries so heavy-tailed document lengths still balance
+namespace {
+
+// blocks of ~2^18 entries so heavy-tailed document lengths still balance
+std::vector<int64_t> corpus_blocks(const int64_t* ptr, int64_t D) {
   const int64_t nnz = ptr[D];
   const int64_t per = std::max<int64_t>(1, nnz / std::max<int64_t>(1, (nnz >> 18)));
   std::vector<int64_t> cuts{0};
@@ -52,6 +50,41 @@ int64_t write_corpus_text(const std::string& path, const int64_t* ptr, int64_t D
     cuts.push_back(e);
     d = e;
   }
+  return cuts;
+}
+
+void format_docs(std::string& s, const int64_t* ptr, int64_t d0, int64_t d1, const int32_t* w, const int64_t* c,
+                 bool assignments) {
+  for (int64_t d = d0; d < d1; ++d) {
+    if (assignments) {
+      put_int_pad(s, ptr[d + 1] - ptr[d], 3);
+      for (int64_t i = ptr[d]; i < ptr[d + 1]; ++i) {
+        s += ' ';
+        put_int_pad(s, w[i], 4);
+        s += ':';
+        put_int_pad(s, c[i], 2);
+      }
+    } else {
+      put_int(s, ptr[d + 1] - ptr[d]);
+      for (int64_t i = ptr[d]; i < ptr[d + 1]; ++i) {
+        s += ' ';
+        put_int(s, w[i]);
+        s += ':';
+        put_int(s, c[i]);
+      }
+    }
+    s += '\n';
+  }
+}
+
+}  // namespace
+
+int64_t write_corpus_text(const std::string& path, const int64_t* ptr, int64_t D, const int32_t* w,
+                          const int64_t* c, int threads, bool assignments) {
+  FILE* f = std::fopen(path.c_str(), "wb");
+  if (!f) throw std::runtime_error("cannot open for writing: " + path);
+  threads = std::max(1, threads);
+  const std::vector<int64_t> cuts = corpus_blocks(ptr, D);
   const int64_t nb = (int64_t)cuts.size() - 1;
   int64_t written = 0;
   std::vector<std::string> bufs(threads);
@@ -59,26 +92,7 @@ int64_t write_corpus_text(const std::string& path, const int64_t* ptr, int64_t D
     parallel_for(std::min<int64_t>(threads, nb - b0), [&](int t) {
       std::string& s = bufs[t];
       s.clear();
-      for (int64_t d = cuts[b0 + t]; d < cuts[b0 + t + 1]; ++d) {
-        if (assignments) {
-          put_int_pad(s, ptr[d + 1] - ptr[d], 3);
-          for (int64_t i = ptr[d]; i < ptr[d + 1]; ++i) {
-            s += ' ';
-            put_int_pad(s, w[i], 4);
-            s += ':';
-            put_int_pad(s, c[i], 2);
-          }
-        } else {
-          put_int(s, ptr[d + 1] - ptr[d]);
-          for (int64_t i = ptr[d]; i < ptr[d + 1]; ++i) {
-            s += ' ';
-            put_int(s, w[i]);
-            s += ':';
-            put_int(s, c[i]);
-          }
-        }
-        s += '\n';
-      }
+      format_docs(s, ptr, cuts[b0 + t], cuts[b0 + t + 1], w, c, assignments);
     });
     for (int64_t t = 0; t < std::min<int64_t>(threads, nb - b0); ++t) {
       const std::string& s = bufs[t];
@@ -91,6 +105,18 @@ int64_t write_corpus_text(const std::string& path, const int64_t* ptr, int64_t D
   }
   if (std::fclose(f) != 0) throw std::runtime_error("close failed: " + path);
   return written;
+}
+
+std::vector<std::string> format_corpus_text(const int64_t* ptr, int64_t D, const int32_t* w, const int64_t* c,
+                                            int threads, bool assignments) {
+  threads = std::max(1, threads);
+  const std::vector<int64_t> cuts = corpus_blocks(ptr, D);
+  const int64_t nb = (int64_t)cuts.size() - 1;
+  std::vector<std::string> out(std::max<int64_t>(nb, 0));
+  for (int64_t b0 = 0; b0 < nb; b0 += threads)
+    parallel_for(std::min<int64_t>(threads, nb - b0),
+                 [&](int t) { format_docs(out[b0 + t], ptr, cuts[b0 + t], cuts[b0 + t + 1], w, c, assignments); });
+  return out;
 }
 
 TextCorpus read_corpus_text(const std::string& path, int threads) {

@@ -19,6 +19,10 @@ struct TextCorpus {
 int64_t write_corpus_text(const std::string& path, const int64_t* doc_ptr, int64_t D, const int32_t* words,
                           const int64_t* counts, int threads, bool assignments = false);
 
+// The same text in memory (the row-sharded writers), as consecutive chunks.
+std::vector<std::string> format_corpus_text(const int64_t* doc_ptr, int64_t D, const int32_t* words,
+                                            const int64_t* counts, int threads, bool assignments = false);
+
 // Parses a model.dat file.  Blank lines are skipped; a line whose declared
 // entry count differs from its w:c pairs throws std::runtime_error.
 TextCorpus read_corpus_text(const std::string& path, int threads);

@@ -564,4 +564,34 @@ int64_t write_rows(const std::string& path, const int64_t* order, int64_t n, con
   return written;
 }
 
+std::vector<std::string> format_rows(const int64_t* order, int64_t n, const std::vector<OutCol>& cols,
+                                     const std::string& sep, int threads, std::vector<int64_t>* row_ends) {
+  if (threads < 1) threads = 1;
+  int64_t cells = 0;
+  for (const OutCol& c : cols) cells += (c.kind == OutCol::kPy2Row || c.kind == OutCol::kFixedRow) ? c.width : 1;
+  const int64_t block = std::max<int64_t>(1, (int64_t(1) << 16) / std::max<int64_t>(1, cells));
+  const int64_t nb = (n + block - 1) / block;
+  std::vector<std::string> out(nb);
+  if (row_ends) row_ends->assign(n, 0);
+  if (nb > INT32_MAX) throw std::invalid_argument("format_rows: too many rows");
+  run_parallel((int)nb, threads, [&](int b) {
+    std::string s;
+    const int64_t lo = b * block, hi = std::min(n, lo + block);
+    for (int64_t i = lo; i < hi; ++i) {
+      format_row(s, order ? order[i] : i, cols, sep);
+      if (row_ends) (*row_ends)[i] = (int64_t)s.size();        // block-local for now
+    }
+    out[b].swap(s);
+  });
+  if (row_ends) {
+    int64_t base = 0;
+    for (int64_t b = 0; b < nb; ++b) {
+      const int64_t lo = b * block, hi = std::min(n, lo + block);
+      for (int64_t i = lo; i < hi; ++i) (*row_ends)[i] += base;
+      base += (int64_t)out[b].size();
+    }
+  }
+  return out;
+}
+
 }  // namespace onin

@@ -188,4 +188,10 @@ struct OutCol {
 int64_t write_rows(const std::string& path, const int64_t* order, int64_t n, const std::vector<OutCol>& cols,
                    const std::string& sep, bool append, int threads);
 
+// In-memory variant (the row-sharded writers: every rank formats its own rows, then writes them at
+// its byte offset of the shared file): the text of the rows in `order` as consecutive chunks, and
+// optionally the end offset (over the concatenated chunks) of every row.
+std::vector<std::string> format_rows(const int64_t* order, int64_t n, const std::vector<OutCol>& cols,
+                                     const std::string& sep, int threads, std::vector<int64_t>* row_ends);
+
 }  // namespace onin

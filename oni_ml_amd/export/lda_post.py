@@ -98,6 +98,55 @@ def export(doc_names, gamma, word_names, log_beta, doc_path, word_path, strict=T
     return theta, phi, wnames
 
 
+def _format_table(names, values, read_back):
+    n = len(names)
+    vals = np.ascontiguousarray(values, np.float64)
+    back = np.empty_like(vals) if read_back else None
+    text = native.lib().format_rows(None, [("dict", list(names), np.arange(n, dtype=np.int32)),
+                                           ("py2row", vals, " ", back)], n=n)
+    return text, back
+
+
+def export_sharded(ctx, doc_names, gamma, word_names, log_beta, doc_path, word_path, strict=True,
+                   read_back: bool = False, gather: bool = True):
+    """``export`` with every rank writing its own rows of both files (the row-sharded lda_post stage).
+
+    ``doc_names`` / ``gamma``: this rank's documents (its contiguous block of doc.dat, in rank order);
+    ``word_names`` / ``log_beta``: the whole vocabulary, on every rank.  doc_results.csv takes the
+    ranks' document blocks in rank order; word_results.csv is split by vocabulary slice
+    [V r / N, V (r + 1) / N).  lda_post.py normalises each topic by Python's sequential sum over all V
+    words (lda_post.py:88-96): here rank r continues the running sums of ranks < r
+    (``shardio.chain``), so the totals -- and every byte of both files -- equal the one-process
+    export.  ``gather``: also return the whole θ / φ read-back tables on every rank (the scorers'
+    broadcast model, flow_post_lda.scala:112-123)."""
+    from ..parallel import shardio as SIO
+    N, r = SIO.world(ctx), SIO.rank(ctx)
+    check_strict_k(log_beta.shape[0], strict)
+    theta = doc_topics(gamma, strict)
+    text, th_b = _format_table(doc_names, theta, read_back)
+    SIO.write_segments(ctx, doc_path, [text])
+    V = log_beta.shape[1]
+    v0, v1 = V * r // N, V * (r + 1) // N
+    lb = np.ascontiguousarray(np.asarray(log_beta, np.float64)[:, v0:v1])
+    if strict:
+        lb = native.lib().roundtrip_fixed10(lb)
+    raw = np.exp(lb)
+    K = raw.shape[0]
+    total = SIO.chain(ctx, lambda carry: np.cumsum(np.concatenate([carry[:, None], raw], 1), 1)[:, -1],
+                      np.zeros(K, np.float64))
+    phi = np.ascontiguousarray((raw / total[:, None]).T)
+    wn = list(word_names[v0:v1])
+    wnames = truncate_s20(wn) if strict else wn
+    text, ph_b = _format_table(wnames, phi, read_back)
+    SIO.write_segments(ctx, word_path, [text])
+    th, ph = (th_b, ph_b) if read_back else (theta, phi)
+    if gather:
+        th = np.concatenate(SIO.allgather_array(ctx, np.ascontiguousarray(th)))
+        ph = np.concatenate(SIO.allgather_array(ctx, np.ascontiguousarray(ph)))
+    all_names = truncate_s20(word_names) if strict else list(word_names)
+    return th, ph, all_names
+
+
 def read_results(path: str):
     """doc_results.csv / word_results.csv -> (keys, values [n, K]) as the Scala scorers parse them
     (key = field 0, values = field 1 with quotes removed, split on ' ', toDouble;

@@ -3,16 +3,18 @@
 
 Every rank ingests only its byte range of the input (a line belongs to the range holding its first
 byte, so the N ranges partition the rows exactly and in file order), and the ranks meet only where
-the single-process pipeline looks at all rows at once:
+the single-process pipeline looks at all rows at once -- always through tensor collectives
+(parallel/shardio.py), never pickled objects:
 
-* IP dictionary -- ids in global first-appearance order: the per-rank dictionaries (each in local
-  first-appearance order) are all-gathered and merged in rank order;
+* IP dictionary -- ids in global first-appearance order: every rank's dictionary (local
+  first-appearance order) packed into fixed-width integer rows, all-gathered, merged with one
+  ``torch.unique(dim=0)`` (``shardio.first_appearance``);
 * ECDF cuts -- each rank's weighted value histogram (distinct values, summed integer weights) is
   all-gathered and merged; the cut rule runs on the merged histogram, which is exactly the weighted
   multiset the single-process ecdf_cuts sees;
 * word space -- the union of the ranks' distinct word_port values;
-* (ip, word) counts -- each rank counts its own rows (reduceByKey), the partial counts are
-  all-gathered and merged by the same sort-based group-by (integer sums: order-free).
+* (ip, word) counts -- each rank counts its own rows (reduceByKey); the partial counts are NOT
+  replicated: corpus/sharded.py routes them to the rank owning each document's id range.
 
 The result (cuts, word space, doc_wc and hence doc.dat / words.dat / model.dat) is identical to
 one process featurizing all rows (tests/test_flow_dist.py).  Analyst-feedback rows come last in the
@@ -26,8 +28,9 @@ from typing import List, Tuple
 import numpy as np
 import torch
 
-from ..corpus.builder import DocWordCounts, concat, count_pairs, segment_sums
+from ..corpus.builder import DocWordCounts, count_pairs, segment_sums
 from ..ops import native
+from ..parallel import shardio as SIO
 from . import flow as FF
 from .quantiles import DECILES, QUINTILES, ecdf_cuts_from_hist
 
@@ -69,63 +72,58 @@ def load_flow_sharded(ctx, flow_path: str, feedback_path=None, dupfactor: int = 
     return FF.FlowTable(t, n_raw, t.num_rows - n_raw, int(dupfactor))
 
 
-def _gather(ctx, obj):
-    import torch.distributed as td
-    out = [None] * ctx.world_size
-    td.all_gather_object(out, obj)
-    return out
+def global_ip_dictionary(ctx, ft: FF.FlowTable):
+    """(global names table in first-appearance order, local id -> global id)."""
+    data, off = ft.table.dict_bytes(0)
+    return SIO.first_appearance(ctx, data, off)
 
 
-def global_ip_dictionary(ctx, ft: FF.FlowTable) -> Tuple[List[str], np.ndarray]:
-    """(global names in first-appearance order, local id -> global id)."""
-    names = ft.ip_names
-    gd, gl = {}, []
-    for part in _gather(ctx, names):
-        for n in part:
-            if n not in gd:
-                gd[n] = len(gl)
-                gl.append(n)
-    return gl, np.fromiter((gd[n] for n in names), dtype=np.int64, count=len(names))
-
-
-def _hist(values: torch.Tensor, w: torch.Tensor):
+def merged_hist(ctx, values: torch.Tensor, w: torch.Tensor):
+    """Global weighted histogram (sorted distinct values, summed weights) of every rank's values."""
     u, c = segment_sums(values.to(torch.float64).reshape(-1), w.to(torch.int64).reshape(-1))
-    return u.cpu().numpy(), c.cpu().numpy()
+    us = SIO.allgather_array(ctx, u.cpu().numpy())
+    cs = SIO.allgather_array(ctx, c.cpu().numpy())
+    dev = values.device
+    return segment_sums(torch.from_numpy(np.concatenate(us)).to(dev), torch.from_numpy(np.concatenate(cs)).to(dev))
 
 
 def global_cuts(ctx, cols: dict, w: torch.Tensor, device) -> dict:
     time = (cols["hour"] + cols["minute"] / 60) + cols["second"] / 3600
-    local = {name: _hist(v, w) for name, v in (("time", time), ("ibyt", cols["ibyt"]), ("ipkt", cols["ipkt"]))}
-    parts = _gather(ctx, local)
     qs = dict(time=DECILES, ibyt=DECILES, ipkt=QUINTILES)
     out = {}
-    for name in ("time", "ibyt", "ipkt"):
-        u = torch.from_numpy(np.concatenate([p[name][0] for p in parts])).to(device)
-        c = torch.from_numpy(np.concatenate([p[name][1] for p in parts])).to(device)
-        mu, mc = segment_sums(u, c)
+    for name, v in (("time", time), ("ibyt", cols["ibyt"]), ("ipkt", cols["ipkt"])):
+        mu, mc = merged_hist(ctx, v, w)
         out[name] = ecdf_cuts_from_hist(mu, mc, qs[name])
     return out
 
 
-def featurize_sharded(ctx, ft: FF.FlowTable, device, strict: bool = True, cuts=None):
-    """Distributed pre-LDA featurization.  Returns (doc_wc [all ranks' pairs, merged], global IP names,
-    word space, cuts) -- identical on every rank and to the single-process pipeline.  ``cuts``: fixed
-    cuts (the CUT setting) instead of the global ECDF ones."""
-    device = torch.device(device)
+def table_columns(ft: FF.FlowTable, n: int, device) -> Tuple[dict, torch.Tensor]:
     t = ft.table
-    n = ft.n
 
     def col(c):
         return torch.from_numpy(t.numeric(c)[:n]).to(device)
     cols = dict(hour=col(FF.C_HOUR), minute=col(FF.C_MIN), second=col(FF.C_SEC), a=col(FF.C_A), b=col(FF.C_B),
                 ipkt=col(FF.C_IPKT), ibyt=col(FF.C_IBYT))
-    w = torch.from_numpy(t.weights()[:n].astype(np.int64)).to(device)
+    return cols, torch.from_numpy(t.weights()[:n].astype(np.int64)).to(device)
+
+
+def featurize_sharded(ctx, ft: FF.FlowTable, device, cuts=None):
+    """Distributed pre-LDA featurization of this rank's rows.
+
+    Returns (sections, names, ip_map, ws, cuts): the source- and destination-side (ip, word) counts
+    of this rank's rows (global ip ids, sorted by (ip, word)); the global IP dictionary; this rank's
+    local -> global ip ids; the word space and the cuts (identical on every rank and to the
+    single-process pipeline).  ``cuts``: fixed cuts (the CUT setting) instead of the global ECDF."""
+    device = torch.device(device)
+    t = ft.table
+    n = ft.n
+    cols, w = table_columns(ft, n, device)
     if cuts is None:
         cuts = global_cuts(ctx, cols, w, device)
     else:
         cuts = {k: torch.as_tensor(np.asarray(v, np.float64), device=device) for k, v in cuts.items()}
     out = FF._flow_words(cols, cuts, device)
-    ports = np.unique(np.concatenate(_gather(ctx, torch.unique(out["word_port"]).cpu().numpy())))
+    ports = np.unique(np.concatenate(SIO.allgather_array(ctx, torch.unique(out["word_port"]).cpu().numpy())))
     ws = FF.FlowWordSpace(ports, len(cuts["time"]) + 1, len(cuts["ibyt"]) + 1, len(cuts["ipkt"]) + 1)
     names, gmap = global_ip_dictionary(ctx, ft)
     gm = torch.from_numpy(gmap).to(device)
@@ -136,11 +134,5 @@ def featurize_sharded(ctx, ft: FF.FlowTable, device, strict: bool = True, cuts=N
                            dst_prefix=out["dst_prefix"], sip=sip, dip=dip, weight=w,
                            cuts={k: v.cpu().numpy() for k, v in cuts.items()}, rows=np.arange(n, dtype=np.int64))
     src, dst = FF.word_keys(feat, ws)
-    sections = []
-    for doc, key in ((sip, src), (dip, dst)):
-        loc = count_pairs(doc, key, w)
-        parts = _gather(ctx, (loc.doc.cpu().numpy(), loc.word.cpu().numpy(), loc.count.cpu().numpy()))
-        cat = [torch.from_numpy(np.concatenate([p[i] for p in parts])).to(device) for i in range(3)]
-        sections.append(count_pairs(cat[0], cat[1], cat[2]))
-    dwc = concat(sections, merge=not strict)
-    return dwc, names, ws, feat.cuts
+    sections = [count_pairs(sip, src, w), count_pairs(dip, dst, w)]
+    return sections, names, gmap, ws, feat.cuts

@@ -132,12 +132,14 @@ class LDAEngine:
                  alpha_init: float = 2.5, backend: str = "auto", device=None, dist=None, seed: int = 0,
                  streams: int = 4, local_shard: bool = False, split_docs: bool = True,
                  split_min: Optional[int] = 4096, use_graph: bool = True, precision: str = "fp64",
-                 emulate_shards: int = 0):
+                 emulate_shards: int = 0, doc_offset: int = 0):
         """precision (hip backend): "fp64" = lda-c arithmetic with the block Gauss-Seidel schedule
         (lda_gs64.hip, the default); "fp32" = the fp32 Jacobi engine (opt-in fast mode).
         emulate_shards (torch backend, one process): reduce the sufficient statistics as N
         nnz-balanced document shards summed in shard order -- bitwise the N-rank run under
-        ONI_DIST_DETERMINISTIC=1 (parallel/dist.py)."""
+        ONI_DIST_DETERMINISTIC=1 (parallel/dist.py).
+        local_shard: ``corpus`` is already this rank's shard; ``doc_offset`` its first global document
+        (the row-sharded pipeline, corpus/sharded.py)."""
         self.settings = settings or LDASettings()
         self.emulate_shards = int(emulate_shards)
         if precision not in ("fp64", "fp32"):
@@ -163,6 +165,10 @@ class LDAEngine:
             else:
                 backend = "torch"
         self.backend = backend
+        # ONI_DIST_DETERMINISTIC=chain (torch backend): sufficient statistics and the likelihood /
+        # alpha_ss sums continue one sequential fold over the documents in corpus order, rank after
+        # rank (parallel/shardio.chain): the model is bitwise the same for any number of ranks
+        self._chain = backend == "torch" and os.environ.get("ONI_DIST_DETERMINISTIC", "0") == "chain"
         if device is None:
             device = torch.device("cuda", torch.cuda.current_device()) if (
                 backend == "hip" or torch.cuda.is_available()) and torch.cuda.is_available() else torch.device("cpu")
@@ -170,8 +176,8 @@ class LDAEngine:
         # shard (data parallel over documents)
         self.global_docs = corpus.num_docs
         if local_shard:
-            # caller already hands this rank its own shard (weak-scaling bench)
-            self.doc_range = (0, corpus.num_docs)
+            # caller already hands this rank its own shard (weak-scaling bench, sharded pipeline)
+            self.doc_range = (int(doc_offset), int(doc_offset) + corpus.num_docs)
             if dist is not None:
                 self.global_docs = dist.allreduce_int(corpus.num_docs)
         elif dist is not None and dist.world_size > 1:
@@ -504,7 +510,7 @@ class LDAEngine:
         overlap little; ONI_DIST_EXCHANGE = auto (default) | sparse | dense.  Collective: every rank
         builds it (or none does)."""
         d = self.dist
-        if d is None or d.world_size <= 1 or self.backend == "cpu":
+        if d is None or d.world_size <= 1 or self.backend == "cpu" or self._chain:
             return None
         mode = os.environ.get("ONI_DIST_EXCHANGE", "auto")
         if mode == "dense" or getattr(d, "deterministic", False):
@@ -545,16 +551,29 @@ class LDAEngine:
             self._set_ss_host(native.lib().random_ss(self.K, self.V, int(s) & 0xFFFFFFFFFFFFFFFF))
         self.alpha = self.alpha_init
 
-    def init_seeded(self, corpus_global: Corpus, seed: Optional[int] = None):
-        """corpus_initialize_ss: NUM_INIT random docs per topic + 1 smoothing."""
+    def init_seeded(self, corpus_global: Optional[Corpus] = None, seed: Optional[int] = None):
+        """corpus_initialize_ss: NUM_INIT random docs per topic + 1 smoothing.  Every rank draws the
+        same global document ids; a rank adds the words of the chosen documents it holds, and the
+        integer counts are summed over the ranks (exact in any order).  ``corpus_global``: the whole
+        corpus when every rank has it (then no reduction is needed)."""
         rng = np.random.default_rng(self.seed if seed is None else seed)
+        local = corpus_global is None
+        c = self.corpus if local else corpus_global
+        d0 = self.doc_range[0] if local else 0
+        D = self.global_docs if local else corpus_global.num_docs
         cw = np.zeros((self.K, self.V))
         for k in range(self.K):
             for _ in range(NUM_INIT):
-                d = int(math.floor(rng.random() * corpus_global.num_docs))
-                a, b = corpus_global.doc_ptr[d], corpus_global.doc_ptr[d + 1]
-                np.add.at(cw[k], corpus_global.word_idx[a:b], corpus_global.counts[a:b])
-            cw[k] += 1.0
+                d = int(math.floor(rng.random() * D)) - d0
+                if 0 <= d < c.num_docs:
+                    a, b = c.doc_ptr[d], c.doc_ptr[d + 1]
+                    np.add.at(cw[k], c.word_idx[a:b], c.counts[a:b])
+        if local and self.dist is not None and self.dist.world_size > 1:
+            import torch.distributed as td
+            t = torch.from_numpy(cw).to(self.dist._coll_device())
+            td.all_reduce(t)
+            cw = t.cpu().numpy()
+        cw += 1.0
         self._set_ss_host(cw)
         self.alpha = self.alpha_init
 
@@ -620,6 +639,8 @@ class LDAEngine:
             self.gamma = out["gamma"]
             self.iters = out["iters"]
             self.lik = out["lik"]
+            if self._chain:
+                return self._chain_stats(out)
             if self.emulate_shards > 1:
                 return self._emulated_shard_stats(out)
             self.cw = R.suffstats(self.t_doc_ptr, self.t_word, out["e"], out["r"], self.beta, self.V, self.K)
@@ -635,6 +656,30 @@ class LDAEngine:
         self.lik = torch.from_numpy(res["doc_likelihood"])
         self.cw = torch.from_numpy(np.ascontiguousarray(res["class_word"].T))
         return torch.tensor([res["likelihood"], res["alpha_ss"]], dtype=torch.float64)
+
+    def _chain_stats(self, out):
+        """class_word and [likelihood, alpha_ss] as one sequential fold over the corpus in document
+        order: this rank continues the fold of the ranks before it (parallel/shardio.chain)."""
+        from ...parallel import shardio as SIO
+        V, K = self.V, self.K
+        lens = (self.t_doc_ptr[1:] - self.t_doc_ptr[:-1]).to(torch.int64)
+        doc_of = torch.repeat_interleave(torch.arange(self.D, device=self.device), lens)
+        contrib = (out["e"][doc_of][:, :K] * out["r"].unsqueeze(1)).cpu()
+        widx = self.t_word.cpu()
+        lik = out["lik"].double().cpu().numpy()
+        ass = out["alpha_ss"].double().cpu().numpy()
+
+        def fold(carry):
+            s = torch.from_numpy(carry[:V * K].reshape(V, K).copy()).index_add_(0, widx, contrib)
+            l = np.cumsum(np.concatenate([carry[V * K:V * K + 1], lik]))[-1]
+            a = np.cumsum(np.concatenate([carry[V * K + 1:], ass]))[-1]
+            return np.concatenate([s.numpy().reshape(-1), [l, a]])
+
+        tot = SIO.chain(self.dist, fold, np.zeros(V * K + 2))
+        s = torch.from_numpy(tot[:V * K].reshape(V, K).copy()).to(self.device)
+        self.cw = self.beta[:, :K].to(s.dtype) * s
+        self._chained = True
+        return torch.tensor(tot[V * K:], dtype=torch.float64, device=self.device)
 
     def _emulated_shard_stats(self, out):
         """class_word and [likelihood, alpha_ss] as N ranks would produce them (each shard's own
@@ -804,7 +849,7 @@ class LDAEngine:
                 if estimate_alpha:
                     self.alpha = special.opt_alpha(float(host[1]), num_docs, self.K)
                 return float(host[0]), float(host[1])
-            if self.dist is not None and self.dist.world_size > 1:
+            if self.dist is not None and self.dist.world_size > 1 and not self._chain:
                 self._cw_local = self.cw.clone()     # this rank's own rows (<rank>.beta)
                 tok = self._comm_begin()
                 sc = self.dist.allreduce_suffstats(self.cw, sc)
@@ -1121,7 +1166,7 @@ class LDAEngine:
         if start == "random":
             self.init_random()
         elif start == "seeded":
-            self.init_seeded(corpus_global if corpus_global is not None else self.corpus)
+            self.init_seeded(corpus_global)
         elif start == "resume":
             pass  # state restored by caller (checkpoint.restore)
         else:

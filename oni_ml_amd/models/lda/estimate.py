@@ -93,11 +93,15 @@ def _write_checkpoint(outdir: str, arrays: dict):
 
 
 def load_final(outdir: str):
-    """(gamma, log_beta) of a finished run: the binary copy when present, else the lda-c text files."""
+    """(gamma, log_beta) of a finished run: the binary copy when present (a multi-rank run stores only
+    log beta there), else the lda-c text files."""
     p = os.path.join(outdir, "final_model.npz")
     if os.path.exists(p):
         with np.load(p, allow_pickle=False) as z:
-            return z["gamma"], z["log_beta"]
+            if "gamma" in z.files:
+                return z["gamma"], z["log_beta"]
+            lb = z["log_beta"]
+        return ldac.load_gamma(os.path.join(outdir, "final.gamma")), lb
     lb, _ = ldac.load_model(os.path.join(outdir, "final"))
     return ldac.load_gamma(os.path.join(outdir, "final.gamma")), lb
 
@@ -113,18 +117,29 @@ def load_checkpoint(outdir: str) -> Optional[dict]:
 def estimate(corpus: Corpus, num_topics: int, alpha_init: float, settings: LDASettings, start: str, outdir: str,
              backend: str = "auto", device=None, dist=None, seed: int = 0, resume: bool = False,
              write_word_assignments: bool = False, write_rank_gamma: bool = False, verbose: bool = False,
-             fault_at_iteration: Optional[int] = None, defer_files: bool = False) -> LDAResult:
+             fault_at_iteration: Optional[int] = None, defer_files: bool = False, local_shard: bool = False,
+             doc_offset: int = 0) -> LDAResult:
     """Run EM and write lda-c files.  `start`: random | seeded | <model prefix>.
 
     `fault_at_iteration` raises after that EM iteration (fault-injection hook for the resume tests).
     `defer_files`: return while the background writer is still formatting the LAG / final model
-    files; the caller must call ``res.close_files()`` (which re-raises a write error).  Without it
-    the files are complete when this returns."""
+    files; the caller must call ``res.close_files()`` (which re-raises a write error, and with several
+    ranks is a collective).  Without it the files are complete when this returns.
+    `local_shard`: ``corpus`` is this rank's document shard starting at global document ``doc_offset``
+    (the row-sharded pipeline).
+
+    Several ranks: gamma is never gathered.  Each rank formats its own rows (``res.gamma`` = this
+    rank's block) into a part file, and the parts are concatenated in rank order into
+    ``<tag>.gamma`` / ``word-assignments.dat`` when the files are closed -- oni-lda-c's per-worker
+    ``<rank>.gamma`` blocks "combined to form final.gamma" (README.md:121)."""
     rank0 = dist is None or dist.rank == 0
+    multi = dist is not None and dist.world_size > 1
+    r = 0 if dist is None else dist.rank
     if rank0:
         os.makedirs(outdir, exist_ok=True)
     eng = LDAEngine(corpus, num_topics, settings, alpha_init=alpha_init, backend=backend, device=device, dist=dist,
-                    seed=seed)
+                    seed=seed, local_shard=local_shard, doc_offset=doc_offset)
+    parts = []          # (final file, this rank's part file): concatenated at close
     start_it, L_old, hist = 0, 0.0, []
     ck = load_checkpoint(outdir) if resume else None
     if ck is not None:
@@ -163,18 +178,23 @@ def estimate(corpus: Corpus, num_topics: int, alpha_init: float, settings: LDASe
     writer = AsyncWriter()
 
     def on_save(tag, e):
-        # collectives first, on every rank: global class_word (sparse exchange) and the gamma gather
+        # collectives first, on every rank: global class_word (sparse exchange)
         st = e.state_arrays()
         lb = e.log_beta(torch.from_numpy(st["cw"]).to(e.cw.device))
-        g = e.gather_gamma() if tag != "000" else None
+        g = None
+        if tag != "000":
+            g = e.local_gamma()
+            if multi:
+                part = os.path.join(outdir, f".{tag}.gamma.part{r}")
+                parts.append((os.path.join(outdir, f"{tag}.gamma"), part))
+                writer.submit(ldac.save_gamma, part, g)
         if write_rank_gamma and tag == "final":
-            r = 0 if dist is None else dist.rank
             writer.submit(ldac.save_gamma, os.path.join(outdir, f"{r}.gamma"), e.local_gamma())
             writer.submit(ldac.save_beta, os.path.join(outdir, f"{r}.beta"), e.local_log_beta())
         if not rank0:
             return
         writer.submit(ldac.save_model, os.path.join(outdir, tag), lb, e.alpha)
-        if g is not None:
+        if g is not None and not multi:
             writer.submit(ldac.save_gamma, os.path.join(outdir, f"{tag}.gamma"), g)
         if tag not in ("000", "final"):
             # engine state is read now (host copies); only the file write is deferred
@@ -184,38 +204,60 @@ def estimate(corpus: Corpus, num_topics: int, alpha_init: float, settings: LDASe
                       **st)
             writer.submit(_write_checkpoint, outdir, ck)
         if tag == "final":  # exact binary copy of what final.* hold as text (stage resume reloads this)
-            writer.submit(np.savez, os.path.join(outdir, "final_model.npz"), log_beta=lb, gamma=g,
-                          alpha=np.float64(e.alpha))
+            extra = {} if multi else dict(gamma=g)
+            writer.submit(np.savez, os.path.join(outdir, "final_model.npz"), log_beta=lb,
+                          alpha=np.float64(e.alpha), **extra)
+
+    def concat_parts():
+        if multi:
+            from ...parallel import shardio as SIO
+            for path, part in parts:
+                SIO.concat_part_files(dist, path, part)
+        parts.clear()
+
+    def close_files():
+        writer.close()
+        concat_parts()
 
     ok = False
     try:
-        res = eng.run(start=mode, corpus_global=corpus, on_iteration=on_iteration, on_save=on_save,
-                      start_iteration=start_it, likelihood_old=L_old, verbose=verbose and rank0)
+        # corpus_global: only when every rank holds the whole corpus (seeded init draws from it)
+        res = eng.run(start=mode, corpus_global=None if local_shard else corpus, on_iteration=on_iteration,
+                      on_save=on_save, start_iteration=start_it, likelihood_old=L_old, verbose=verbose and rank0)
         ok = True
     finally:
         if not (ok and defer_files):
             writer.close()
-    res.close_files = writer.close if defer_files else (lambda: None)
     res.likelihoods = history
     res.log_beta = eng.log_beta()
-    res.gamma = eng.gather_gamma()
-    if write_word_assignments and rank0:
+    res.gamma = eng.local_gamma()          # this rank's documents (all of them with one rank)
+    res.doc_range = eng.doc_range
+    if write_word_assignments:
         # device argmax + native formatting; on the background writer with the deferred model files
         # when allowed (the caller's next stages do not wait for it)
-        wa, lb, g, dev = os.path.join(outdir, "word-assignments.dat"), res.log_beta, res.gamma, eng.cw.device
+        wa, lb, g, dev, shard = os.path.join(outdir, "word-assignments.dat"), res.log_beta, res.gamma, \
+            eng.cw.device, eng.corpus
+        if multi:
+            part = os.path.join(outdir, f".word-assignments.dat.part{r}")
+            parts.append((wa, part))
+            wa = part
 
         def _assign():
-            _write_assignment_file(wa, corpus, word_topics(corpus, lb, g, device=dev))
+            _write_assignment_file(wa, shard, word_topics(shard, lb, g, device=dev))
 
-        if ok and defer_files:
+        if defer_files:
             writer.submit(_assign)
         else:
             _assign()
+    if not defer_files:
+        concat_parts()
+    res.close_files = close_files if defer_files else (lambda: None)
+    nnz = dist.allreduce_int(eng.corpus.nnz) if multi else eng.corpus.nnz
     if rank0:
         with open(os.path.join(outdir, "lda_stats.json"), "w") as f:
             json.dump(dict(em_iterations=res.em_iterations, seconds=res.seconds, alpha=res.alpha,
-                           backend=eng.backend, docs=corpus.num_docs, terms=corpus.num_terms, nnz=corpus.nnz,
-                           metrics=eng.metrics(res.seconds, res.em_iterations),
+                           backend=eng.backend, docs=eng.global_docs, terms=eng.V, nnz=nnz, ranks=dist.world_size
+                           if multi else 1, metrics=eng.metrics(res.seconds, res.em_iterations),
                            per_iter=[s.__dict__ for s in res.stats]), f)
     res.engine = eng
     return res

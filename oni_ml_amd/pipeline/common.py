@@ -45,7 +45,7 @@ def load_corpus_files(lpath: str):
     return c, docs, words
 
 
-def run_lda(cfg, corpus: Corpus, dist=None, device=None, log=print):
+def run_lda(cfg, corpus: Corpus, dist=None, device=None, log=print, local_shard: bool = False, doc_offset: int = 0):
     outdir = cfg.lpath
     settings_path = os.path.join(outdir, "settings.txt")
     if dist is None or dist.rank == 0:
@@ -56,7 +56,7 @@ def run_lda(cfg, corpus: Corpus, dist=None, device=None, log=print):
                     write_rank_gamma=(cfg.rank_gamma if cfg.rank_gamma is not None
                                       else dist is not None and dist.world_size > 1),
                     verbose=cfg.verbose, fault_at_iteration=cfg.extra.get("fault_at_iteration"),
-                    defer_files=dist is None or dist.world_size <= 1)
+                    defer_files=True, local_shard=local_shard, doc_offset=doc_offset)
 
 
 def run_export(cfg, doc_names, gamma, word_names, log_beta, read_back: bool = False) -> ModelTables:

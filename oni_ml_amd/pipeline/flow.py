@@ -31,6 +31,9 @@ def _word_names(ws: FF.FlowWordSpace, keys: np.ndarray):
 
 
 def run(cfg, dist=None, device=None, log=print) -> dict:
+    if dist is not None and dist.world_size > 1 and os.environ.get("ONI_DIST_FEATURIZE", "1") != "0":
+        from .sharded import run_flow
+        return run_flow(cfg, dist, device, log)
     rank = 0 if dist is None else dist.rank
     device = torch.device(device or ("cuda" if torch.cuda.is_available() else "cpu"))
     R = StageRunner(cfg.lpath, resume=cfg.resume, rank=rank, log=log,
@@ -41,32 +44,7 @@ def run(cfg, dist=None, device=None, log=print) -> dict:
 
     # ------------------------------------------------------------------ pre
     need_pre = not (R.done("lda_pre") and R.done("flow_pre"))
-    # several ranks: row-sharded ingest + featurization (features/flow_dist.py), identical corpus on
-    # every rank; ONI_DIST_FEATURIZE=0 falls back to rank 0 featurizing and broadcasting
-    sharded = (dist is not None and dist.world_size > 1 and need_pre
-               and os.environ.get("ONI_DIST_FEATURIZE", "1") != "0")
-    if sharded:
-        from ..features import flow_dist as FD
-        with R.stage("load") as res:
-            ft_local = FD.load_flow_sharded(dist, cfg.flow_path, cfg.feedback_path(), cfg.dupfactor, cfg.threads)
-            res.update(rank_rows=ft_local.n)
-        with R.stage("flow_pre") as res:
-            dwc, gnames, ws, cuts = FD.featurize_sharded(dist, ft_local, device, strict=cfg.strict,
-                                                         cuts=cfg.fixed_cuts())
-            if rank == 0:
-                C.save_json(os.path.join(cfg.lpath, "flow_cuts.json"),
-                            dict(cuts={k: v.tolist() for k, v in cuts.items()}, ports=ws.ports.tolist()))
-            res["pairs"] = dwc.n
-        with R.stage("lda_pre") as res:
-            built = lda_pre(dwc)
-            doc_names = [gnames[i] for i in built.doc_keys.tolist()]
-            word_names = _word_names(ws, built.word_keys)
-            if rank == 0:
-                C.write_corpus_files(cfg.lpath, built, doc_names, word_names)
-            res.update(docs=built.corpus.num_docs, terms=built.corpus.num_terms, nnz=built.corpus.nnz)
-            summary["corpus"] = dict(docs=built.corpus.num_docs, terms=built.corpus.num_terms, nnz=built.corpus.nnz)
-        del ft_local
-        need_pre = False
+    sharded = False     # several ranks: pipeline/sharded.py (ONI_DIST_FEATURIZE=0: rank 0 featurizes)
     if rank == 0 and (need_pre or not R.done("flow_post")) and not sharded:
         with R.stage("load") as res:
             ft = FF.load_flow(cfg.flow_path, cfg.feedback_path(), cfg.dupfactor, cfg.threads)
@@ -159,12 +137,24 @@ def run(cfg, dist=None, device=None, log=print) -> dict:
     return summary
 
 
-def score_flow(cfg, ft: FF.FlowTable, tables: C.ModelTables, device, log=print) -> dict:
-    """flow_post_lda.scala: features of raw rows, θ·φ per side, min, < TOL, ascending, 37-column rows."""
+def score_flow(cfg, ft: FF.FlowTable, tables: C.ModelTables, device, log=print, ctx=None, ip_rows=None) -> dict:
+    """flow_post_lda.scala: features of raw rows, θ·φ per side, min, < TOL, ascending, 37-column rows.
+
+    ``ctx`` (several ranks): ``ft`` holds this rank's rows; the cuts come from every rank's raw rows,
+    and the survivors of all ranks are merged into one ascending file (``shardio.merge_sorted_rows``,
+    the sortByKey shuffle).  ``ip_rows``: doc row of every ip dictionary id of ``ft`` (-1: not a
+    document) -- replaces the name lookup through ``tables.doc_index()``."""
+    from ..parallel import shardio as SIO
+    multi = SIO.world(ctx) > 1
     cuts = cfg.fixed_cuts()          # fixed CUT cuts apply to both stages (flow_pre_lda.scala:95-98)
     if cuts is None and not cfg.strict:
         saved = C.load_json(os.path.join(cfg.lpath, "flow_cuts.json"))
         cuts = {k: np.asarray(v, np.float64) for k, v in saved["cuts"].items()}
+    if cuts is None and multi:
+        # flow_post_lda.scala:143-150: the cuts of the raw rows (no feedback) of the whole day
+        from ..features import flow_dist as FDS
+        cols, w = FDS.table_columns(ft, ft.n_raw, torch.device(device))
+        cuts = {k: v.cpu().numpy() for k, v in FDS.global_cuts(ctx, cols, w, device).items()}
     feat = FF.featurize(ft, device, cuts=cuts, raw_only=True)
     ws = FF.word_space_for(feat)
     src, dst = FF.word_keys(feat, ws)
@@ -176,7 +166,10 @@ def score_flow(cfg, ft: FF.FlowTable, tables: C.ModelTables, device, log=print) 
     widx = C.map_names(unames, tables.word_index(), device)[inv]
     w_src, w_dst = widx[: src.numel()], widx[src.numel():]
     ipn = ft.ip_names
-    didx = C.map_names(ipn, tables.doc_index(), device)
+    if ip_rows is not None:
+        didx = torch.from_numpy(np.asarray(ip_rows, np.int64)).to(device)
+    else:
+        didx = C.map_names(ipn, tables.doc_index(), device)
     K = tables.theta.shape[1]
     if cfg.strict and K != 20:
         raise ValueError("compat=strict scores over exactly 20 topics (flow_post_lda.scala:232)")
@@ -204,10 +197,14 @@ def score_flow(cfg, ft: FF.FlowTable, tables: C.ModelTables, device, log=print) 
         ("java", sel(sb)),
     ]
     from ..ops import native
+    if multi:
+        text, ends = native.lib().format_rows(None, cols, n=n, row_ends=True, threads=cfg.threads)
+        total = SIO.merge_sorted_rows(ctx, sel(key).astype(np.float64), text, ends, out)
+        log(f"flow_post: {total} events with score < {cfg.tol} written to {out} ({n} from rank {ctx.rank})")
+        return dict(flagged=total, rank_flagged=n, events=ctx.allreduce_int(int(feat.time.numel())))
     native.lib().write_rows(out, None, cols, threads=cfg.threads, n=n)
     log(f"flow_post: {n} events with score < {cfg.tol} written to {out}")
     return dict(flagged=n, events=int(feat.time.numel()))
-
 
 
 def synthetic_flow_corpus(events: int = 1_000_000, seed: int = 0, workdir: Optional[str] = None, device=None,

@@ -76,7 +76,9 @@ class StageRunner:
         self.resume = resume
         self.rank = rank
         self.mdir = os.path.join(workdir, ".stages")
-        self.metrics = os.path.join(workdir, metrics_name)
+        # rank 0: metrics.jsonl; rank r > 0: metrics.rank<r>.jsonl (per-rank stage times of a sharded run)
+        base, ext = os.path.splitext(metrics_name)
+        self.metrics = os.path.join(workdir, metrics_name if rank == 0 else f"{base}.rank{rank}{ext}")
         self.log = log
         self.sync = sync
         self.times = {}
@@ -100,9 +102,8 @@ class StageRunner:
                 os.unlink(os.path.join(self.mdir, f))
 
     def emit(self, rec: dict):
-        if self.rank == 0:
-            with open(self.metrics, "a") as f:
-                f.write(json.dumps(rec) + "\n")
+        with open(self.metrics, "a") as f:
+            f.write(json.dumps(dict(rec, rank=self.rank)) + "\n")
 
     @contextmanager
     def stage(self, name: str, **meta):

@@ -1,0 +1,191 @@
+"""Row-sharded ``ml_ops`` pipeline: every stage runs on every rank (one process per GPU).
+
+The reference runs featurization and scoring on ``SPK_EXEC`` Spark executors (ml_ops.sh:57,108),
+LDA on 20 MPI ranks (:80) and lda_pre / lda_post serially.  Here each stage is split over the N ranks
+and the ranks exchange only what the single-process pipeline would look at globally
+(parallel/shardio.py):
+
+  load       rank r ingests byte range r of FLOW_PATH (+ the feedback rows on the last rank)
+  flow_pre   global cuts from merged histograms, global IP dictionary, local (ip, word) counts
+  lda_pre    counts routed to the rank owning each document's id range; global word / document ids;
+             entries moved to the nnz-balanced engine shards (corpus/sharded.py); words.dat,
+             doc.dat, model.dat and doc_wc.dat written by all ranks at their byte offsets
+  lda        the engine on this rank's shard; final.gamma = the ranks' blocks in rank order
+  lda_post   doc_results.csv by document shard, word_results.csv by vocabulary slice
+  flow_post  every rank scores its own rows; the survivors are merged into one ascending file
+
+Every output file is byte-identical to the one-process pipeline's when the LDA model is
+(ONI_DIST_DETERMINISTIC=chain, tests/test_sharded_pipeline.py).  Resumed runs (``--resume``) read
+the finished stages' files on every rank.
+"""
+from __future__ import annotations
+
+import os
+
+import numpy as np
+import torch
+
+from ..parallel import shardio as SIO
+from . import common as C
+from .runner import StageRunner
+
+
+def _runner(cfg, ctx, device, log):
+    return StageRunner(cfg.lpath, resume=cfg.resume, rank=ctx.rank, log=log,
+                       sync=(torch.cuda.synchronize if device.type == "cuda" else None))
+
+
+def write_corpus_files_sharded(ctx, lpath, sc, doc_names, word_names_of, threads=0):
+    """words.dat (vocabulary slices), doc.dat and model.dat (document shards) from every rank."""
+    from ..ops import native
+    N, r = SIO.world(ctx), SIO.rank(ctx)
+    L = native.lib()
+    V = sc.word_keys.size
+    v0, v1 = V * r // N, V * (r + 1) // N
+    wn = word_names_of(sc.word_keys[v0:v1])
+    t = L.format_rows(None, [("int", np.arange(v0, v1, dtype=np.int64)),
+                             ("dict", wn, np.arange(v1 - v0, dtype=np.int32))], n=v1 - v0, threads=threads)
+    SIO.write_segments(ctx, os.path.join(lpath, "words.dat"), [t])
+    d0, d1 = sc.doc_range
+    t = L.format_rows(None, [("int", np.arange(d0 + 1, d1 + 1, dtype=np.int64)),
+                             ("dict", doc_names, np.arange(d1 - d0, dtype=np.int32))], n=d1 - d0, threads=threads)
+    SIO.write_segments(ctx, os.path.join(lpath, "doc.dat"), [t])
+    c = sc.corpus
+    SIO.write_segments(ctx, os.path.join(lpath, "model.dat"),
+                       [L.format_ldac_corpus(c.doc_ptr, c.word_idx, c.counts, threads=threads)])
+
+
+def write_doc_wc_sharded(ctx, path, sc, ip_names, word_names_of, threads=0):
+    """doc_wc.dat: this rank's block of every section, sections one after another."""
+    from ..ops import native
+    segs = []
+    for sec in sc.lines:
+        doc = sec.doc.cpu().numpy()
+        ud, dinv = np.unique(doc, return_inverse=True)
+        uw, winv = np.unique(sec.word.cpu().numpy(), return_inverse=True)
+        segs.append(native.lib().format_rows(None, [("dict", ip_names.take(ud), dinv.astype(np.int32)),
+                                                    ("dict", word_names_of(uw), winv.astype(np.int32)),
+                                                    ("int", sec.count.cpu().numpy().astype(np.int64))],
+                                             n=sec.n, threads=threads))
+    SIO.write_segments(ctx, path, segs)
+
+
+def _lda_stage(R, cfg, ctx, corpus, device, log, summary, local_shard, doc_offset=0):
+    with R.stage("lda") as res:
+        lres = C.run_lda(cfg, corpus, dist=ctx, device=device, log=log, local_shard=local_shard,
+                         doc_offset=doc_offset)
+        res["_defer"] = lres.close_files   # LAG / final model files: written while later stages run
+        res.update(em_iterations=lres.em_iterations, likelihood=lres.likelihoods[-1][0] if lres.likelihoods else 0.0,
+                   alpha=lres.alpha)
+        m = lres.engine.metrics(lres.seconds, lres.em_iterations)
+        res.update({k: v for k, v in m.items() if not isinstance(v, list)})
+        R.emit(dict(stage="lda_detail", var_iter_hist=m["var_iter_hist"],
+                    **{k: v for k, v in m.items() if not isinstance(v, list)}))
+        summary["lda"] = dict(em_iterations=lres.em_iterations, seconds=lres.seconds, alpha=lres.alpha,
+                              likelihood=lres.likelihoods[-1][0] if lres.likelihoods else None)
+    return lres
+
+
+def _files_state(cfg, ctx):
+    """Resume: the corpus files on every rank, this rank's shard of them."""
+    from ..parallel.dist import shard_bounds
+    corpus, doc_names, word_names = C.load_corpus_files(cfg.lpath)
+    d0, d1 = shard_bounds(corpus.doc_ptr, ctx.world_size)[ctx.rank]
+    return corpus, doc_names, word_names, (d0, d1)
+
+
+def run_flow(cfg, ctx, device=None, log=print) -> dict:
+    from ..corpus.sharded import build_sharded
+    from ..export import lda_post
+    from ..features import flow as FF
+    from ..features import flow_dist as FD
+    from .flow import score_flow
+    device = torch.device(device or ("cuda" if torch.cuda.is_available() else "cpu"))
+    R = _runner(cfg, ctx, device, log)
+    summary = {}
+    rank0 = ctx.rank == 0
+    ft = sc = names = gmap = ws = None
+    lres = None
+    need_pre = not (R.done("lda_pre") and R.done("flow_pre"))
+    if need_pre or not R.done("flow_post"):
+        with R.stage("load") as res:
+            ft = FD.load_flow_sharded(ctx, cfg.flow_path, cfg.feedback_path(), cfg.dupfactor, cfg.threads)
+            res.update(rank_rows=ft.n)
+            summary["input"] = dict(rows=ctx.allreduce_int(ft.n), feedback_rows=ctx.allreduce_int(ft.n_feedback))
+    if need_pre:
+        with R.stage("flow_pre") as res:
+            sections, names, gmap, ws, cuts = FD.featurize_sharded(ctx, ft, device, cuts=cfg.fixed_cuts())
+            if rank0:
+                C.save_json(os.path.join(cfg.lpath, "flow_cuts.json"),
+                            dict(cuts={k: v.tolist() for k, v in cuts.items()}, ports=ws.ports.tolist()))
+            res["rank_pairs"] = sum(s.n for s in sections)
+        with R.stage("lda_pre") as res:
+            sc = build_sharded(ctx, sections, len(names), merge=not cfg.strict, device=device)
+            del sections
+            doc_names = names.take(sc.doc_keys)
+            write_corpus_files_sharded(ctx, cfg.lpath, sc, doc_names, ws.decode, cfg.threads)
+            if cfg.write_doc_wc:
+                write_doc_wc_sharded(ctx, os.path.join(cfg.lpath, "doc_wc.dat"), sc, names, ws.decode, cfg.threads)
+            res.update(docs=sc.num_docs, terms=int(sc.word_keys.size), nnz=sc.nnz, rank_docs=sc.corpus.num_docs,
+                       rank_nnz=sc.corpus.nnz)
+            summary["corpus"] = dict(docs=sc.num_docs, terms=int(sc.word_keys.size), nnz=sc.nnz)
+    else:
+        R.skip("flow_pre")
+        R.skip("lda_pre")
+    try:
+        # ------------------------------------------------------------------ lda
+        word_names = None
+        if not R.done("lda"):
+            if sc is not None:
+                lres = _lda_stage(R, cfg, ctx, sc.corpus, device, log, summary, True, sc.doc_range[0])
+            else:
+                corpus, all_docs, word_names, (d0, d1) = _files_state(cfg, ctx)
+                doc_names = all_docs[d0:d1]
+                lres = _lda_stage(R, cfg, ctx, corpus, device, log, summary, False)
+            gamma, log_beta = lres.gamma, lres.log_beta
+        else:
+            R.skip("lda")
+            gamma = log_beta = None
+        # ------------------------------------------------------------- lda_post
+        ip_rows = None
+        if not R.done("lda_post"):
+            if word_names is None:
+                word_names = ws.decode(sc.word_keys) if sc is not None else C.load_corpus_files(cfg.lpath)[2]
+            if gamma is None:
+                from ..models.lda.estimate import load_final
+                corpus, all_docs, _, (d0, d1) = _files_state(cfg, ctx)
+                doc_names = all_docs[d0:d1]
+                g_all, log_beta = load_final(cfg.lpath)
+                gamma = g_all[d0:d1]
+            with R.stage("lda_post") as res:
+                th, ph, wn = lda_post.export_sharded(ctx, doc_names, gamma, word_names, log_beta,
+                                                     os.path.join(cfg.lpath, "doc_results.csv"),
+                                                     os.path.join(cfg.lpath, "word_results.csv"),
+                                                     strict=cfg.strict, read_back=True)
+                if sc is not None:
+                    # doc row of every ip id: the scorers' name lookup without a name dictionary
+                    keys = np.concatenate(SIO.allgather_array(ctx, sc.doc_keys))
+                    g2d = np.full(len(names), -1, np.int64)
+                    g2d[keys] = np.arange(keys.size)
+                    ip_rows = g2d[gmap]
+                    all_docs = None
+                else:
+                    all_docs = C.load_corpus_files(cfg.lpath)[1]
+                tables = C.ModelTables(all_docs, th, wn, ph)
+        else:
+            R.skip("lda_post")
+            tables = C.load_model_tables(cfg.lpath)
+        # ------------------------------------------------------------ flow_post
+        if not R.done("flow_post"):
+            with R.stage("flow_post") as res:
+                res.update(score_flow(cfg, ft, tables, device, log if rank0 else (lambda *a, **k: None),
+                                      ctx=ctx, ip_rows=ip_rows))
+                summary["scored"] = res.get("flagged")
+        else:
+            R.skip("flow_post")
+    except BaseException:
+        R.finish_deferred(suppress=True)
+        raise
+    R.finish_deferred()
+    summary["stage_seconds"] = dict(R.times)
+    return summary

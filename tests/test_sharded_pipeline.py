@@ -1,0 +1,104 @@
+"""Row-sharded ml_ops pipeline (pipeline/sharded.py) over 2 and 4 gloo ranks == one process, byte for
+byte: every file of the run (corpus files, doc_wc.dat, the lda-c model files, doc_results.csv,
+word_results.csv and the scored results).
+
+ONI_DIST_DETERMINISTIC=chain makes the LDA model itself independent of the number of ranks (the
+sufficient statistics and likelihood sums are one sequential fold over the documents in corpus
+order, continued rank after rank), so any difference in the files is a sharding error of the
+featurization, corpus builder, export or scoring stages."""
+import os
+import sys
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from test_dist import _free_port  # noqa: E402
+
+FLOW_FILES = ["words.dat", "doc.dat", "model.dat", "doc_wc.dat", "final.beta", "final.gamma", "final.other",
+              "likelihood.dat", "005.gamma", "word-assignments.dat", "doc_results.csv", "word_results.csv",
+              "flow_results.csv", "flow_cuts.json"]
+DNS_FILES = ["words.dat", "doc.dat", "model.dat", "doc_wc.dat", "final.beta", "final.gamma", "likelihood.dat",
+             "doc_results.csv", "word_results.csv", "dns_results.csv"]
+
+
+def _cfg(kind, indir, lpath, extra):
+    from oni_ml_amd import config as CFG
+    from oni_ml_amd.models.lda.settings import LDASettings
+    kw = dict(flow_path=indir) if kind == "flow" else dict(dns_path=extra["dns_path"], top1m=extra["top1m"])
+    cfg = CFG.resolve("20160122", kind, tol=extra["tol"], conf_path=None, environ={}, lpath=lpath, backend="torch",
+                      threads=2, verbose=False, **kw)
+    cfg.settings = LDASettings(em_max_iter=6)
+    if extra.get("compat"):
+        cfg.compat = extra["compat"]
+    return cfg
+
+
+def _worker(rank, world, port, kind, indir, lpath, extra, q):
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank), MASTER_ADDR="127.0.0.1",
+                      MASTER_PORT=str(port), ONI_DIST_DETERMINISTIC="chain")
+    torch.set_num_threads(1)
+    try:
+        from oni_ml_amd.parallel import dist as D
+        from oni_ml_amd.pipeline import run
+        ctx = D.init_from_env(backend="gloo")
+        s = run(_cfg(kind, indir, lpath, extra), dist=ctx if world > 1 else None, device="cpu",
+                log=lambda *a, **k: None)
+        q.put((rank, s.get("scored")))
+        ctx.shutdown()
+    except Exception:  # pragma: no cover
+        import traceback
+        q.put((rank, traceback.format_exc()))
+
+
+def _run(world, kind, indir, lpath, extra):
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    ps = [ctx.Process(target=_worker, args=(r, world, port, kind, indir, lpath, extra, q)) for r in range(world)]
+    for p in ps:
+        p.start()
+    out = sorted([q.get(timeout=600) for _ in ps], key=lambda x: x[0])
+    for p in ps:
+        p.join(timeout=60)
+    for r, o in out:
+        assert not isinstance(o, str), o
+    return out
+
+
+@pytest.fixture(scope="module")
+def flow_day(tmp_path_factory):
+    from oni_ml_amd.synth.flow import generate_flow_day, generate_flow_feedback
+    d = tmp_path_factory.mktemp("shflow")
+    generate_flow_day(str(d / "in") + "/", events=5000, seed=3, n_internal=300, n_external=700, files=3)
+    rows = (d / "in" / "part-00000.csv").read_text().splitlines()[1:300]
+    generate_flow_feedback(str(d / "fb.csv"), rows, seed=2, n=12)
+    return d
+
+
+@pytest.mark.parametrize("compat", ["strict", "fixed"])
+def test_sharded_flow_pipeline_bytes_equal_one_process(flow_day, compat, tmp_path):
+    extra = dict(tol=1e-3, compat=compat)
+    one = tmp_path / "w1"
+    one.mkdir()
+    os.link(flow_day / "fb.csv", one / "flow_scores.csv")
+    r1 = _run(1, "flow", str(flow_day / "in"), str(one), extra)
+    assert r1[0][1] > 0
+    for world in (2, 4):
+        lp = tmp_path / f"w{world}"
+        lp.mkdir()
+        os.link(flow_day / "fb.csv", lp / "flow_scores.csv")
+        rn = _run(world, "flow", str(flow_day / "in"), str(lp), extra)
+        assert all(o == r1[0][1] for _, o in rn)
+        for f in FLOW_FILES:
+            a, b = (one / f).read_bytes(), (lp / f).read_bytes()
+            assert a == b, (world, f, len(a), len(b))
+        # no part files left behind
+        assert not [p for p in os.listdir(lp) if ".part" in p]
+        # every rank ran every stage (per-rank stage times in metrics.rank<r>.jsonl)
+        import json
+        for r in range(1, world):
+            recs = [json.loads(l) for l in (lp / f"metrics.rank{r}.jsonl").read_text().splitlines()]
+            ran = {x["stage"] for x in recs if x.get("status") == "ok"}
+            assert {"load", "flow_pre", "lda_pre", "lda", "lda_post", "flow_post"} <= ran, ran
