@@ -135,12 +135,52 @@ def load_dns(dns_path: str, feedback_path: Optional[str] = None, dupfactor: int 
     for p in select_paths(dns_path, strict):
         if not p:
             continue
-        t = pq.read_table(p, columns=COLUMNS)
-        t = t.filter(pc.and_(pc.is_valid(t["frame_len"]), pc.is_valid(t["unix_tstamp"])))
-        tables.append(t)
+        tables.append(pq.read_table(p, columns=COLUMNS))
     if not tables:
         raise FileNotFoundError(f"no DNS input in {dns_path!r}")
-    t = pa.concat_tables(tables, promote_options="permissive") if len(tables) > 1 else tables[0]
+    fb = read_dns_feedback(feedback_path) if feedback_path else []
+    return table_from_arrow(tables, fb, dupfactor)
+
+
+def _parquet_files(p: str) -> List[str]:
+    """The files pq.read_table reads for ``p`` (a file, or a directory dataset), in its order."""
+    if os.path.isdir(p):
+        import pyarrow.dataset as ds
+        return list(ds.dataset(p, format="parquet").files)
+    return [p]
+
+
+def load_dns_rows(dns_path: str, lo: int, hi: int, strict: bool = True):
+    """Rows [lo, hi) of the selected parquet inputs taken as one table (before the null filter): only
+    the row groups holding them are read (the row-sharded DNS ingest, pipeline/sharded.py)."""
+    pa, pc, pq = _pa()
+    out, off = [], 0
+    for p in [f for q in select_paths(dns_path, strict) if q for f in _parquet_files(q)]:
+        f = pq.ParquetFile(p)
+        for g in range(f.metadata.num_row_groups):
+            n = f.metadata.row_group(g).num_rows
+            a, b = max(lo, off), min(hi, off + n)
+            if a < b:
+                t = f.read_row_group(g, columns=COLUMNS)
+                out.append(t.slice(a - off, b - a))
+            off += n
+    return out
+
+
+def dns_total_rows(dns_path: str, strict: bool = True) -> int:
+    _, _, pq = _pa()
+    return sum(pq.ParquetFile(f).metadata.num_rows for p in select_paths(dns_path, strict) if p
+               for f in _parquet_files(p))
+
+
+def table_from_arrow(tables, fb, dupfactor: int = 1000) -> DnsTable:
+    """The reference's row rules on the read tables (in order) + the feedback rows (weight DUPFACTOR)."""
+    pa, pc, pq = _pa()
+    tables = [t.filter(pc.and_(pc.is_valid(t["frame_len"]), pc.is_valid(t["unix_tstamp"]))) for t in tables]
+    if not tables:
+        t = pa.table({c: pa.array([], pa.string()) for c in COLUMNS})
+    else:
+        t = pa.concat_tables(tables, promote_options="permissive") if len(tables) > 1 else tables[0]
     strs = {c: _arrow_strings(pa, pc, t[c]).combine_chunks() for c in COLUMNS}
     # Row.mkString(",").split(",") must give back 8 fields: no comma anywhere; trailing empty fields vanish
     bad = None
@@ -151,10 +191,12 @@ def load_dns(dns_path: str, feedback_path: Optional[str] = None, dupfactor: int 
     keep = pc.invert(bad)
     n_before = len(t)
     strs = {c: pc.filter(v, keep) for c, v in strs.items()}
-    flen = pc.filter(t["frame_len"], keep).to_numpy(zero_copy_only=False).astype(np.float64)
-    tst = pc.filter(t["unix_tstamp"], keep).to_numpy(zero_copy_only=False).astype(np.float64)
+    if len(t):
+        flen = pc.filter(t["frame_len"], keep).to_numpy(zero_copy_only=False).astype(np.float64)
+        tst = pc.filter(t["unix_tstamp"], keep).to_numpy(zero_copy_only=False).astype(np.float64)
+    else:
+        flen = tst = np.zeros(0, np.float64)
     n_raw = len(flen)
-    fb = read_dns_feedback(feedback_path) if feedback_path else []
     fb_ok = []
     for r in fb:
         if any("," in x for x in r) or r[-1] == "":

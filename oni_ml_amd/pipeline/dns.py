@@ -21,6 +21,9 @@ from .runner import StageRunner
 
 
 def run(cfg, dist=None, device=None, log=print) -> dict:
+    if dist is not None and dist.world_size > 1:
+        from .sharded import run_dns
+        return run_dns(cfg, dist, device, log)
     rank = 0 if dist is None else dist.rank
     device = torch.device(device or ("cuda" if torch.cuda.is_available() else "cpu"))
     R = StageRunner(cfg.lpath, resume=cfg.resume, rank=rank, log=log,
@@ -114,16 +117,28 @@ def run(cfg, dist=None, device=None, log=print) -> dict:
     return summary
 
 
-def score_dns(cfg, tab: FD.DnsTable, top, tables: C.ModelTables, device, log=print) -> dict:
+def score_dns(cfg, tab: FD.DnsTable, top, tables: C.ModelTables, device, log=print, ctx=None, ip_map=None) -> dict:
+    """dns_post_lda.scala:108-331.  ``ctx`` (several ranks): ``tab`` holds this rank's rows; cuts over
+    every rank's raw rows; the survivors of all ranks merged into one ascending file.  ``ip_map``:
+    doc row of every ip_dst id of the pre-LDA dictionary of ``tab`` (its raw rows' ids are a prefix)."""
+    from ..parallel import shardio as SIO
+    multi = SIO.world(ctx) > 1
     cuts = None
     if not cfg.strict:
         cuts = {k: np.asarray(v, np.float64) for k, v in C.load_json(os.path.join(cfg.lpath, "dns_cuts.json"))["cuts"].items()}
+    elif multi:
+        from ..features import dns_dist as FDD
+        cuts = FDD.global_cuts(ctx, tab, top, device, raw_only=True, threads=cfg.threads)
     feat = FD.featurize(tab, device, top, cuts=cuts, raw_only=True, threads=cfg.threads)
     wsp = FD.DnsWordSpace(feat.cuts, feat.qpairs)
     uk, inv = torch.unique(feat.word_key, return_inverse=True)
     unames = wsp.decode(uk.cpu().numpy())
     widx = C.map_names(unames, tables.word_index(), device)[inv]
-    didx = C.map_names(feat.ip_names, tables.doc_index(), device)[feat.ip]
+    if ip_map is not None:
+        m = np.asarray(ip_map, np.int64)[:len(feat.ip_names)]
+        didx = torch.from_numpy(m).to(device)[feat.ip]
+    else:
+        didx = C.map_names(feat.ip_names, tables.doc_index(), device)[feat.ip]
     K = tables.theta.shape[1]
     if cfg.strict and K != 20:
         raise ValueError("compat=strict scores over exactly 20 topics (dns_post_lda.scala:316)")
@@ -137,6 +152,7 @@ def score_dns(cfg, tab: FD.DnsTable, top, tables: C.ModelTables, device, log=pri
         ids, names = FD.dictionary_encode(tab.take(c, order))
         cols.append(("dict", names, ids))
     H = feat.host
+    o_t = torch.from_numpy(order).to(sc.device)
     cols += [
         ("dict", H["domains"], H["domain_id"][order]),
         ("dict", H["subdomains"], H["subdomain_id"][order]),
@@ -145,9 +161,14 @@ def score_dns(cfg, tab: FD.DnsTable, top, tables: C.ModelTables, device, log=pri
         ("java", H["entropy"][order]),
         ("int", H["top_domain"][order].astype(np.int64)),
         ("dict", unames, inv[torch.from_numpy(order).to(inv.device)].cpu().numpy().astype(np.int32)),
-        ("java", sc[torch.from_numpy(order).to(sc.device)].cpu().numpy()),
+        ("java", sc[o_t].cpu().numpy()),
     ]
     from ..ops import native
+    if multi:
+        text, ends = native.lib().format_rows(None, cols, n=n, row_ends=True, threads=cfg.threads)
+        total = SIO.merge_sorted_rows(ctx, key[o_t].cpu().numpy().astype(np.float64), text, ends, out)
+        log(f"dns_post: {total} queries with score < {cfg.tol} written to {out} ({n} from rank {ctx.rank})")
+        return dict(flagged=total, rank_flagged=n, events=ctx.allreduce_int(int(feat.word_key.numel())))
     native.lib().write_rows(out, None, cols, threads=cfg.threads, n=n)
     log(f"dns_post: {n} queries with score < {cfg.tol} written to {out}")
     return dict(flagged=n, events=int(feat.word_key.numel()))

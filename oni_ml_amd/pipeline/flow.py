@@ -31,7 +31,7 @@ def _word_names(ws: FF.FlowWordSpace, keys: np.ndarray):
 
 
 def run(cfg, dist=None, device=None, log=print) -> dict:
-    if dist is not None and dist.world_size > 1 and os.environ.get("ONI_DIST_FEATURIZE", "1") != "0":
+    if dist is not None and dist.world_size > 1:
         from .sharded import run_flow
         return run_flow(cfg, dist, device, log)
     rank = 0 if dist is None else dist.rank
@@ -44,7 +44,7 @@ def run(cfg, dist=None, device=None, log=print) -> dict:
 
     # ------------------------------------------------------------------ pre
     need_pre = not (R.done("lda_pre") and R.done("flow_pre"))
-    sharded = False     # several ranks: pipeline/sharded.py (ONI_DIST_FEATURIZE=0: rank 0 featurizes)
+    sharded = False     # several ranks: pipeline/sharded.py
     if rank == 0 and (need_pre or not R.done("flow_post")) and not sharded:
         with R.stage("load") as res:
             ft = FF.load_flow(cfg.flow_path, cfg.feedback_path(), cfg.dupfactor, cfg.threads)

@@ -133,48 +133,8 @@ def run_flow(cfg, ctx, device=None, log=print) -> dict:
         R.skip("flow_pre")
         R.skip("lda_pre")
     try:
-        # ------------------------------------------------------------------ lda
-        word_names = None
-        if not R.done("lda"):
-            if sc is not None:
-                lres = _lda_stage(R, cfg, ctx, sc.corpus, device, log, summary, True, sc.doc_range[0])
-            else:
-                corpus, all_docs, word_names, (d0, d1) = _files_state(cfg, ctx)
-                doc_names = all_docs[d0:d1]
-                lres = _lda_stage(R, cfg, ctx, corpus, device, log, summary, False)
-            gamma, log_beta = lres.gamma, lres.log_beta
-        else:
-            R.skip("lda")
-            gamma = log_beta = None
-        # ------------------------------------------------------------- lda_post
-        ip_rows = None
-        if not R.done("lda_post"):
-            if word_names is None:
-                word_names = ws.decode(sc.word_keys) if sc is not None else C.load_corpus_files(cfg.lpath)[2]
-            if gamma is None:
-                from ..models.lda.estimate import load_final
-                corpus, all_docs, _, (d0, d1) = _files_state(cfg, ctx)
-                doc_names = all_docs[d0:d1]
-                g_all, log_beta = load_final(cfg.lpath)
-                gamma = g_all[d0:d1]
-            with R.stage("lda_post") as res:
-                th, ph, wn = lda_post.export_sharded(ctx, doc_names, gamma, word_names, log_beta,
-                                                     os.path.join(cfg.lpath, "doc_results.csv"),
-                                                     os.path.join(cfg.lpath, "word_results.csv"),
-                                                     strict=cfg.strict, read_back=True)
-                if sc is not None:
-                    # doc row of every ip id: the scorers' name lookup without a name dictionary
-                    keys = np.concatenate(SIO.allgather_array(ctx, sc.doc_keys))
-                    g2d = np.full(len(names), -1, np.int64)
-                    g2d[keys] = np.arange(keys.size)
-                    ip_rows = g2d[gmap]
-                    all_docs = None
-                else:
-                    all_docs = C.load_corpus_files(cfg.lpath)[1]
-                tables = C.ModelTables(all_docs, th, wn, ph)
-        else:
-            R.skip("lda_post")
-            tables = C.load_model_tables(cfg.lpath)
+        tables, ip_rows = _lda_and_export(R, cfg, ctx, sc, names, gmap,
+                                          (lambda k: ws.decode(k)) if ws is not None else None, device, log, summary)
         # ------------------------------------------------------------ flow_post
         if not R.done("flow_post"):
             with R.stage("flow_post") as res:
@@ -189,3 +149,110 @@ def run_flow(cfg, ctx, device=None, log=print) -> dict:
     R.finish_deferred()
     summary["stage_seconds"] = dict(R.times)
     return summary
+
+
+def run_dns(cfg, ctx, device=None, log=print) -> dict:
+    from ..corpus.sharded import build_sharded
+    from ..export import lda_post
+    from ..features import dns as FD
+    from ..features import dns_dist as FDD
+    from .dns import score_dns
+    device = torch.device(device or ("cuda" if torch.cuda.is_available() else "cpu"))
+    R = _runner(cfg, ctx, device, log)
+    summary = {}
+    rank0 = ctx.rank == 0
+    tab = sc = names = gmap = wsp = top = None
+    need_pre = not (R.done("lda_pre") and R.done("dns_pre"))
+    if need_pre or not R.done("dns_post"):
+        with R.stage("load") as res:
+            tab = FDD.load_dns_sharded(ctx, cfg.dns_path, cfg.feedback_path(), cfg.dupfactor, strict=cfg.strict)
+            top = FD.load_top_domains(cfg.top1m)
+            if not top and rank0:
+                log(f"warning: top-1m list {cfg.top1m!r} not found; every domain gets top_domain 0/2")
+            res.update(rank_rows=tab.n, top_domains=len(top))
+            summary["input"] = dict(rows=ctx.allreduce_int(tab.n), feedback_rows=ctx.allreduce_int(tab.n_feedback),
+                                    dropped=ctx.allreduce_int(tab.dropped))
+    if need_pre:
+        with R.stage("dns_pre") as res:
+            sections, names, gmap, wsp, cuts = FDD.featurize_sharded(ctx, tab, device, top, threads=cfg.threads)
+            if rank0:
+                C.save_json(os.path.join(cfg.lpath, "dns_cuts.json"), dict(cuts={k: v.tolist() for k, v in cuts.items()}))
+            res["rank_pairs"] = sum(s.n for s in sections)
+        with R.stage("lda_pre") as res:
+            sc = build_sharded(ctx, sections, len(names), device=device)
+            del sections
+            doc_names = names.take(sc.doc_keys)
+            write_corpus_files_sharded(ctx, cfg.lpath, sc, doc_names, wsp.decode, cfg.threads)
+            if cfg.write_doc_wc:
+                write_doc_wc_sharded(ctx, os.path.join(cfg.lpath, "doc_wc.dat"), sc, names, wsp.decode, cfg.threads)
+            res.update(docs=sc.num_docs, terms=int(sc.word_keys.size), nnz=sc.nnz, rank_docs=sc.corpus.num_docs,
+                       rank_nnz=sc.corpus.nnz)
+            summary["corpus"] = dict(docs=sc.num_docs, terms=int(sc.word_keys.size), nnz=sc.nnz)
+    else:
+        R.skip("dns_pre")
+        R.skip("lda_pre")
+    try:
+        tables, ip_rows = _lda_and_export(R, cfg, ctx, sc, names, gmap,
+                                          (lambda k: wsp.decode(k)) if wsp is not None else None, device, log, summary)
+        if not R.done("dns_post"):
+            with R.stage("dns_post") as res:
+                res.update(score_dns(cfg, tab, top, tables, device, log if rank0 else (lambda *a, **k: None),
+                                     ctx=ctx, ip_map=ip_rows))
+                summary["scored"] = res.get("flagged")
+        else:
+            R.skip("dns_post")
+    except BaseException:
+        R.finish_deferred(suppress=True)
+        raise
+    R.finish_deferred()
+    summary["stage_seconds"] = dict(R.times)
+    return summary
+
+
+def _lda_and_export(R, cfg, ctx, sc, names, gmap, decode, device, log, summary):
+    """lda + lda_post of the sharded pipeline (in memory after a fresh pre stage, from the files on
+    resume).  Returns (scoring tables, doc row of every local ip id or None)."""
+    from ..export import lda_post
+    word_names = doc_names = None
+    if sc is not None:
+        doc_names = names.take(sc.doc_keys)
+    gamma = log_beta = None
+    if not R.done("lda"):
+        if sc is not None:
+            lres = _lda_stage(R, cfg, ctx, sc.corpus, device, log, summary, True, sc.doc_range[0])
+        else:
+            corpus, all_docs, word_names, (d0, d1) = _files_state(cfg, ctx)
+            doc_names = all_docs[d0:d1]
+            lres = _lda_stage(R, cfg, ctx, corpus, device, log, summary, False)
+        gamma, log_beta = lres.gamma, lres.log_beta
+    else:
+        R.skip("lda")
+    ip_rows = None
+    if not R.done("lda_post"):
+        if word_names is None:
+            word_names = decode(sc.word_keys) if sc is not None else C.load_corpus_files(cfg.lpath)[2]
+        if gamma is None:
+            from ..models.lda.estimate import load_final
+            corpus, all_docs, _, (d0, d1) = _files_state(cfg, ctx)
+            doc_names = all_docs[d0:d1]
+            g_all, log_beta = load_final(cfg.lpath)
+            gamma = g_all[d0:d1]
+        with R.stage("lda_post"):
+            th, ph, wn = lda_post.export_sharded(ctx, doc_names, gamma, word_names, log_beta,
+                                                 os.path.join(cfg.lpath, "doc_results.csv"),
+                                                 os.path.join(cfg.lpath, "word_results.csv"),
+                                                 strict=cfg.strict, read_back=True)
+            all_docs = None
+            if sc is not None:
+                # doc row of every ip id: the scorers' name lookup without a name dictionary
+                keys = np.concatenate(SIO.allgather_array(ctx, sc.doc_keys))
+                g2d = np.full(len(names), -1, np.int64)
+                g2d[keys] = np.arange(keys.size)
+                ip_rows = g2d[gmap]
+            else:
+                all_docs = C.load_corpus_files(cfg.lpath)[1]
+            tables = C.ModelTables(all_docs, th, wn, ph)
+    else:
+        R.skip("lda_post")
+        tables = C.load_model_tables(cfg.lpath)
+    return tables, ip_rows

@@ -33,17 +33,18 @@ def _worker(rank, world, port, indir, fb, q):
                       MASTER_PORT=str(port))
     torch.set_num_threads(1)
     try:
-        from oni_ml_amd.corpus.builder import lda_pre
+        from oni_ml_amd.corpus.sharded import build_sharded
         from oni_ml_amd.features import flow_dist as FD
         from oni_ml_amd.parallel import dist as D
         ctx = D.init_from_env(backend="gloo")
         ft = FD.load_flow_sharded(ctx, indir, fb, 1000, threads=2)
-        dwc, names, ws, cuts = FD.featurize_sharded(ctx, ft, "cpu")
-        b = lda_pre(dwc)
+        sections, names, gmap, ws, cuts = FD.featurize_sharded(ctx, ft, "cpu")
+        sc = build_sharded(ctx, sections, len(names))
+        c = sc.corpus
         q.put((rank, dict(cuts={k: v.tolist() for k, v in cuts.items()}, ports=ws.ports.tolist(),
-                          docs=[names[i] for i in b.doc_keys.tolist()], words=ws.decode(b.word_keys),
-                          ptr=b.corpus.doc_ptr.tolist(), widx=b.corpus.word_idx.tolist(),
-                          cnt=b.corpus.counts.tolist(), rows=ft.n)))
+                          docs=names.take(sc.doc_keys), words=ws.decode(sc.word_keys),
+                          ptr=c.doc_ptr.tolist(), widx=c.word_idx.tolist(), cnt=c.counts.tolist(), rows=ft.n,
+                          doc_range=sc.doc_range, bounds=sc.bounds, D=sc.num_docs, nnz=sc.nnz)))
         ctx.shutdown()
     except Exception:  # pragma: no cover
         import traceback
@@ -76,9 +77,20 @@ def test_sharded_featurization_equals_single_process(flow_input, world):
     for r, o in out:
         assert isinstance(o, dict), o
     assert sum(o["rows"] for _, o in out) == ref["rows"]          # the byte ranges partition the rows
+    from oni_ml_amd.parallel.dist import shard_bounds
+    rptr = np.asarray(ref["ptr"])
+    want_bounds = [b[0] for b in shard_bounds(rptr, world)] + [len(rptr) - 1]
     for r, o in out:
-        for k in ("cuts", "ports", "docs", "words", "ptr", "widx", "cnt"):
+        for k in ("cuts", "ports", "words"):
             assert o[k] == ref[k], (r, k)
+        # each rank holds exactly its nnz-balanced shard of the one-process corpus
+        assert o["bounds"] == want_bounds and o["D"] == len(rptr) - 1 and o["nnz"] == rptr[-1]
+        d0, d1 = o["doc_range"]
+        assert (d0, d1) == (want_bounds[r], want_bounds[r + 1])
+        assert o["docs"] == ref["docs"][d0:d1]
+        a, b = rptr[d0], rptr[d1]
+        assert o["ptr"] == (rptr[d0:d1 + 1] - a).tolist()
+        assert o["widx"] == ref["widx"][a:b] and o["cnt"] == ref["cnt"][a:b]
 
 
 def test_byte_ranges_partition_lines(tmp_path):

@@ -102,3 +102,39 @@ def test_sharded_flow_pipeline_bytes_equal_one_process(flow_day, compat, tmp_pat
             recs = [json.loads(l) for l in (lp / f"metrics.rank{r}.jsonl").read_text().splitlines()]
             ran = {x["stage"] for x in recs if x.get("status") == "ok"}
             assert {"load", "flow_pre", "lda_pre", "lda", "lda_post", "flow_post"} <= ran, ran
+
+
+def _dns_feedback(path, dns_path, n=10):
+    """dns_scores.csv (24 columns, dns_pre_lda.scala:84-117) with severity 3 on n queries of the day."""
+    import pyarrow.parquet as pq
+    t = pq.read_table(dns_path.split(",")[0]).to_pylist()[:3 * n]
+    lines = [",".join(f"c{i}" for i in range(24))]
+    for i, r in enumerate(t):
+        f = ["x"] * 24
+        f[0], f[23], f[1], f[2], f[3] = str(r["frame_time"]), str(r["unix_tstamp"]), str(r["frame_len"]), \
+            str(r["ip_dst"]), str(r["dns_qry_name"])
+        f[4], f[5], f[6] = str(r["dns_qry_class"]), str(r["dns_qry_type"]), str(r["dns_qry_rcode"])
+        f[18] = "3" if i % 3 else "1"
+        if "," not in ",".join(f[:4]) and f[3] != "None":
+            lines.append(",".join(f))
+    with open(path, "w") as fh:
+        fh.write("\n".join(lines) + "\n")
+
+
+@pytest.mark.parametrize("compat", ["strict", "fixed"])
+def test_sharded_dns_pipeline_bytes_equal_one_process(compat, tmp_path):
+    from oni_ml_amd.synth.dns import generate_dns_day
+    g = generate_dns_day(str(tmp_path / "in"), events=6000, seed=4, files=4, n_names=700, n_clients=250)
+    extra = dict(tol=1e-2, compat=compat, dns_path=g["dns_path"], top1m=g["top1m"])
+    outs = {}
+    for world in (1, 2, 4):
+        lp = tmp_path / f"w{world}"
+        lp.mkdir()
+        _dns_feedback(str(lp / "dns_scores.csv"), g["dns_path"])
+        outs[world] = _run(world, "dns", None, str(lp), extra)
+    assert outs[1][0][1] > 0
+    for world in (2, 4):
+        assert all(o == outs[1][0][1] for _, o in outs[world])
+        for f in DNS_FILES:
+            a, b = (tmp_path / "w1" / f).read_bytes(), (tmp_path / f"w{world}" / f).read_bytes()
+            assert a == b, (world, f, len(a), len(b))
