@@ -11,7 +11,8 @@ all ranks (docs x timed EM iterations / max-over-ranks wall time).
 
 Engine: the fp64 block Gauss-Seidel engine (--precision fp64, the default: lda-c's double
 arithmetic and its per-word schedule up to blocks of ceil(n/32) words, csrc/hip/lda_gs64.hip);
---precision fp32 runs the fp32 Jacobi engine.
+--precision fp32 runs the experimental fp32 Jacobi engine (a known model bias against lda-c,
+profiles/r2_precision_parity.md; its tests run only with ONI_EXPERIMENTAL=1).
 
 value = LDA docs/s TO CONVERGENCE: a fresh random-init run trained until lda-c's EM loop test
 stops it (device-side test, every iteration in full), docs x EM iterations / wall time, summed
@@ -128,7 +129,7 @@ def main():
     ap.add_argument("--e2e", type=int, default=1, help="N=1: also time the whole ml_ops flow pipeline on the day")
     ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"], help="cpu: gloo/torch rehearsal")
     ap.add_argument("--precision", default="fp64", choices=["fp64", "fp32"],
-                    help="fp64: lda-c arithmetic, block Gauss-Seidel (default); fp32: the Jacobi fast mode")
+                    help="fp64: lda-c arithmetic, block Gauss-Seidel (default); fp32: the experimental Jacobi mode")
     ap.add_argument("--scaling", default="weak", choices=["weak", "strong"],
                     help="weak: one day per GPU; strong: one day sharded over the GPUs")
     ap.add_argument("--e2e-tol", type=float, default=1e-5,
@@ -194,19 +195,24 @@ def main():
     extra["var_iter_by_len"] = by_len
     value = window_value
     if args.converge:
-        # to convergence: fresh engine and random init (seed + 1), lda-c's EM loop test on the device
-        eng2 = LDAEngine(corpus, args.topics, LDASettings(), backend=args.backend, device=dev, dist=dist,
-                         seed=args.seed + 1, local_shard=local, precision=args.precision)
+        # to convergence: fresh engine and random init (seed + 1), lda-c's EM loop test on the device;
+        # the clock includes the engine's construction (device CSR / CSC, length plans, buffers)
         ctx.barrier()
         _sync(dev)
         t2 = time.perf_counter()
+        eng2 = LDAEngine(corpus, args.topics, LDASettings(), backend=args.backend, device=dev, dist=dist,
+                         seed=args.seed + 1, local_shard=local, precision=args.precision)
+        _sync(dev)
+        t_setup = time.perf_counter() - t2
         res = eng2.run()
         _sync(dev)
         tc = ctx.allreduce_max(time.perf_counter() - t2)
+        t_setup = ctx.allreduce_max(t_setup)
         value = docs_global * res.em_iterations / tc
-        extra.update(converge_seconds=round(tc, 4), converge_em_iters=res.em_iterations,
-                     converge_docs_per_sec=round(value, 1), final_likelihood=res.likelihoods[-1][0],
-                     final_alpha=res.alpha)
+        extra.update(converge_seconds=round(tc, 4), converge_setup_seconds=round(t_setup, 4),
+                     converge_em_iters=res.em_iterations, converge_docs_per_sec=round(value, 1),
+                     converge_em_only_docs_per_sec=round(docs_global * res.em_iterations / max(tc - t_setup, 1e-9), 1),
+                     final_likelihood=res.likelihoods[-1][0], final_alpha=res.alpha)
     if args.e2e and world == 1 and args.corpus == "flow" and args.events <= 2_000_000:
         extra.update(_e2e(args, dev))
     # the measured baseline is the 1-day netflow, K=20 corpus: other configs report no ratio
@@ -215,7 +221,8 @@ def main():
         out = {
             "metric": METRIC if args.corpus != "dns" else "LDA docs/sec to convergence, 1-day DNS",
             "value": round(value, 1),
-            "value_source": ("to convergence: fresh random init, lda-c EM loop test (converge_* fields)"
+            "value_source": ("to convergence incl. engine setup: fresh engine + random init, lda-c EM loop test "
+                             "(converge_* fields)"
                              if args.converge else "timed K-step window (no --converge run)"),
             "window_docs_per_sec": round(window_value, 1),
             "unit": "docs/s (docs x EM iterations / s, all ranks)",

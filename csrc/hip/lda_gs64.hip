@@ -1067,11 +1067,24 @@ __global__ __launch_bounds__(512) void gs_split(GSArgs a, SplitArgs sp) {
   double L = 0.0, L_old = 0.0, conv = 1.0, GS = 0.0, LWs = 0.0;
   int it = 0;
   bool failed = false;
+  // phase timer (thread 0 of workgroup 0, a.dbg): word phase, barrier 1, publish + gather, barrier 2,
+  // refresh, barrier 3, sweep end, chunks
+  const bool timer = a.dbg != nullptr && b == 0 && t == 0;
+  long long ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  long long tc = timer ? clock64() : 0;
+  auto tick = [&](int i) {
+    if (timer) {
+      const long long x = clock64();
+      ph[i] += x - tc;
+      tc = x;
+    }
+  };
   while (!failed && var_continue(conv, vconv, it, vmi)) {
     ++it;
 #pragma unroll
     for (int o = 0; o < TO; ++o) lps[o] = 0.0;
     for (int j = 0; j < nch; ++j) {
+      ph[7] += timer ? 1 : 0;
       if (active) {
         int m0, m1;
         range(j, m0, m1);
@@ -1117,7 +1130,9 @@ __global__ __launch_bounds__(512) void gs_split(GSArgs a, SplitArgs sp) {
         }
         if (lane == 0) sRedL[wv] = lw;
       }
+      tick(0);
       lds_barrier();
+      tick(1);
       // exchange: thread k < KS owns topic k, thread KS the log-sum
       const int seq = (it - 1) * nch + j + 1;
       const unsigned tag = split_tag(epoch, seq);
@@ -1142,7 +1157,9 @@ __global__ __launch_bounds__(512) void gs_split(GSArgs a, SplitArgs sp) {
         }
         sPart[pi][col] = ps;
       }
+      tick(2);
       lds_barrier();
+      tick(3);
       if (t < NC) {
         double tot = 0.0;
 #pragma unroll
@@ -1164,7 +1181,9 @@ __global__ __launch_bounds__(512) void gs_split(GSArgs a, SplitArgs sp) {
           LWs += tot;
         }
       }
+      tick(4);
       lds_barrier();
+      tick(5);
       if (sFail) {
         failed = true;
         break;
@@ -1204,7 +1223,10 @@ __global__ __launch_bounds__(512) void gs_split(GSArgs a, SplitArgs sp) {
     conv = (L_old - L) / L_old;
     L_old = L;
     lds_barrier();
+    tick(6);
   }
+  if (timer)
+    for (int i = 0; i < 8; ++i) a.dbg[i] = ph[i];
   // every thread of this workgroup is past its last exchange (the loops end on a barrier)
   split_exit(counter, sp.n_docs, G);
   double ps = 0.0;
@@ -2087,7 +2109,18 @@ static void gs_estep_ks(const GSArgs& a, int variant, hipStream_t s) {
         // (measured on the headline corpus: 2.70 vs 2.96 ms, the 4-wave team has no second wave per
         // SIMD to cover the fp64 dependency chains of the word phase)
         static const int bnw = std::getenv("ONI_GS_BIG_NW") ? std::atoi(std::getenv("ONI_GS_BIG_NW")) : 7;
-        if (bnw == 7)
+        // ONI_GS_TEAM8_LDS=<bytes>: dynamic LDS requested on top of the kernel's own, so no workgroup of
+        // another bucket (all of them use LDS) is co-resident on a longest-document CU
+        static const int pad = std::getenv("ONI_GS_TEAM8_LDS") ? std::atoi(std::getenv("ONI_GS_TEAM8_LDS")) : 0;
+        if (bnw == 7 && pad > 0) {
+          static bool attr = false;
+          if (!attr) {
+            ONI_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&gs::gs_wsteam<KS, 7, 2>),
+                                              hipFuncAttributeMaxDynamicSharedMemorySize, pad));
+            attr = true;
+          }
+          hipLaunchKernelGGL((gs::gs_wsteam<KS, 7, 2>), dim3(a.n_items), dim3(512), pad, s, a);
+        } else if (bnw == 7)
           hipLaunchKernelGGL((gs::gs_wsteam<KS, 7, 2>), dim3(a.n_items), dim3(512), 0, s, a);
         else if (bnw == 3)
           hipLaunchKernelGGL((gs::gs_wsteam<KS, 3, 4>), dim3(a.n_items), dim3(256), 0, s, a);

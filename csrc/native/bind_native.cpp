@@ -481,6 +481,31 @@ PYBIND11_MODULE(_oninative, m) {
   m.def("log_sum", &ldac_log_sum);
   m.def("opt_alpha", &ldac_opt_alpha, py::arg("ss"), py::arg("D"), py::arg("K"));
   m.def(
+      "lda_assign_ldac",
+      [](py::array_t<int64_t, py::array::c_style | py::array::forcecast> doc_ptr,
+         py::array_t<int32_t, py::array::c_style | py::array::forcecast> words,
+         py::array_t<double, py::array::c_style | py::array::forcecast> counts,
+         py::array_t<double, py::array::c_style | py::array::forcecast> log_beta, double alpha, int var_max_iter,
+         double var_conv, int threads, int gs_updates) {
+        const int D = (int)doc_ptr.size() - 1;
+        if (log_beta.ndim() != 2) throw std::invalid_argument("log_beta must be [K, V]");
+        const int K = (int)log_beta.shape(0), V = (int)log_beta.shape(1);
+        if (words.size() != counts.size() || doc_ptr.data()[D] != words.size())
+          throw std::invalid_argument("inconsistent corpus arrays");
+        for (py::ssize_t i = 0; i < words.size(); ++i)
+          if (words.data()[i] < 0 || words.data()[i] >= V) throw std::invalid_argument("word id out of range");
+        if (threads <= 0) threads = default_threads();
+        std::vector<int32_t> z;
+        {
+          py::gil_scoped_release rel;
+          z = ldac_word_assignments(doc_ptr.data(), words.data(), counts.data(), D, V, K, log_beta.data(), alpha,
+                                    var_max_iter, (float)var_conv, gs_updates, threads);
+        }
+        return to_np(z);
+      },
+      py::arg("doc_ptr"), py::arg("words"), py::arg("counts"), py::arg("log_beta"), py::arg("alpha"),
+      py::arg("var_max_iter"), py::arg("var_conv"), py::arg("threads") = 0, py::arg("gs_updates") = 0);
+  m.def(
       "lda_estep_ldac",
       [](py::array_t<int64_t, py::array::c_style | py::array::forcecast> doc_ptr,
          py::array_t<int32_t, py::array::c_style | py::array::forcecast> words,

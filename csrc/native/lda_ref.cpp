@@ -477,26 +477,45 @@ int ldac_estimate(const LdacCorpus& c, int K, double alpha_init, const LdacSetti
   std::fclose(lf);
   save_model(dir + "/final", lb, K, V, alpha);
   save_gamma(dir + "/final.gamma", r.gamma, D, K);
-  // word assignments under the final model
+  // word assignments under the final model (a fresh lda_inference per document, run_em's final pass)
+  const std::vector<int32_t> z = ldac_word_assignments(c.doc_ptr.data(), c.words.data(), cnt.data(), D, V, K, lb.data(),
+                                                       alpha, st.var_max_iter, st.var_converged, st.gs_updates, threads);
   FILE* wf = std::fopen((dir + "/word-assignments.dat").c_str(), "w");
-  Workspace ws;
-  std::vector<double> gam(K);
   for (int d = 0; d < D; d++) {
-    DocView dv{c.words.data() + c.doc_ptr[d], cnt.data() + c.doc_ptr[d], (int)(c.doc_ptr[d + 1] - c.doc_ptr[d]), 0};
-    for (int n = 0; n < dv.n; n++) dv.total += dv.c[n];
-    lda_inference(dv, lb.data(), V, K, alpha, st.var_max_iter, st.var_converged, gam.data(), ws, nullptr,
-                  st.gs_updates);
-    std::fprintf(wf, "%03d", dv.n);
-    for (int n = 0; n < dv.n; n++) {
-      int best = 0;
-      for (int k = 1; k < K; k++)
-        if (ws.phi[(size_t)n * K + k] > ws.phi[(size_t)n * K + best]) best = k;
-      std::fprintf(wf, " %04d:%02d", dv.w[n], best);
-    }
+    std::fprintf(wf, "%03d", (int)(c.doc_ptr[d + 1] - c.doc_ptr[d]));
+    for (int64_t e = c.doc_ptr[d]; e < c.doc_ptr[d + 1]; e++) std::fprintf(wf, " %04d:%02d", c.words[e], z[e]);
     std::fprintf(wf, "\n");
   }
   std::fclose(wf);
   return i;
+}
+
+std::vector<int32_t> ldac_word_assignments(const int64_t* doc_ptr, const int32_t* words, const double* counts, int D,
+                                           int V, int K, const double* log_beta, double alpha, int var_max_iter,
+                                           float var_converged, int gs_updates, int threads) {
+  std::vector<int32_t> z(doc_ptr[D], 0);
+  threads = std::max(1, threads);
+  std::atomic<int> next{0};
+  auto work = [&]() {
+    Workspace ws;
+    std::vector<double> gam(K);
+    for (int d; (d = next.fetch_add(1)) < D;) {
+      DocView dv{words + doc_ptr[d], counts + doc_ptr[d], (int)(doc_ptr[d + 1] - doc_ptr[d]), 0};
+      for (int n = 0; n < dv.n; n++) dv.total += dv.c[n];
+      lda_inference(dv, log_beta, V, K, alpha, var_max_iter, var_converged, gam.data(), ws, nullptr, gs_updates);
+      for (int n = 0; n < dv.n; n++) {
+        int best = 0;   // write_word_assignment: the first maximum
+        for (int k = 1; k < K; k++)
+          if (ws.phi[(size_t)n * K + k] > ws.phi[(size_t)n * K + best]) best = k;
+        z[doc_ptr[d] + n] = best;
+      }
+    }
+  };
+  std::vector<std::thread> th;
+  for (int t = 1; t < threads; ++t) th.emplace_back(work);
+  work();
+  for (auto& x : th) x.join();
+  return z;
 }
 
 int ldac_infer(const LdacCorpus& c, const std::string& model_prefix, const LdacSettings& st,

@@ -51,6 +51,12 @@ EStepOut ldac_estep(const int64_t* doc_ptr, const int32_t* words, const double* 
                     const double* log_beta, double alpha, int var_max_iter, float var_converged, int nshards,
                     int threads, int gs_updates = 0);
 
+// run_em's final pass: a fresh lda_inference of every document under the final model, and for every
+// corpus entry the topic of its largest phi (the first maximum; write_word_assignment).
+std::vector<int32_t> ldac_word_assignments(const int64_t* doc_ptr, const int32_t* words, const double* counts, int D,
+                                           int V, int K, const double* log_beta, double alpha, int var_max_iter,
+                                           float var_converged, int gs_updates, int threads);
+
 LdacCorpus read_ldac_corpus(const std::string& path);
 LdacSettings read_ldac_settings(const std::string& path);
 

@@ -109,7 +109,7 @@ def cmd_ml_ops(argv):
         lock = RunLock(os.path.join(cfg.lpath, ".lock")).__enter__()
     ctx.barrier()
     try:
-        summary = run(cfg, dist=ctx if ctx.world_size > 1 else None, device=ctx.device, log=log)
+        summary = run(cfg, dist=ctx if ctx.active else None, device=ctx.device, log=log)
     finally:
         if lock is not None:
             lock.__exit__(None, None, None)
@@ -148,7 +148,7 @@ def cmd_lda(argv):
         corpus = ldac.read_model_dat(a.data)
         st = LDASettings.load(a.settings)
         res = estimate(corpus, int(a.k), float(a.alpha), st, a.start, a.directory, backend=a.backend,
-                       device=ctx.device, dist=ctx if ctx.world_size > 1 else None, seed=a.seed, resume=a.resume,
+                       device=ctx.device, dist=ctx if ctx.active else None, seed=a.seed, resume=a.resume,
                        write_word_assignments=a.word_assignments, verbose=True)
         if ctx.rank == 0:
             print(f"em iterations: {res.em_iterations}  seconds: {res.seconds:.3f}")

@@ -97,6 +97,8 @@ class DeviceCorpus:
     def build(c: Corpus, device) -> "DeviceCorpus":
         if c.nnz >= 2**31 - 1:
             raise ValueError("nnz exceeds int32 offsets; shard the corpus")
+        if torch.device(device).type == "cuda":
+            return DeviceCorpus._build_device(c, torch.device(device))
         D, V = c.num_docs, c.num_terms
         lens = c.lengths()
         doc_of = np.repeat(np.arange(D, dtype=np.int32), lens)
@@ -115,4 +117,25 @@ class DeviceCorpus:
             csc_doc=t(doc_of[perm], torch.int32),
             num_docs=D, num_terms=V, nnz=c.nnz,
             doc_len=lens.astype(np.int64), word_len=wlen,
+        )
+
+    @staticmethod
+    def _build_device(c: Corpus, dev) -> "DeviceCorpus":
+        """The CSC permutation on the GPU: one stable radix sort of the word ids (nnz entries), the
+        column pointer from a searchsorted -- instead of a host argsort of nnz entries (the engine's
+        setup cost, seconds at the 30-day scale)."""
+        D, V = c.num_docs, c.num_terms
+        lens = c.lengths()
+        ptr = torch.from_numpy(c.doc_ptr).to(dev)
+        w = torch.from_numpy(c.word_idx).to(dev)
+        cnt = torch.from_numpy(c.counts).to(dev).to(torch.float32)
+        ws, perm = torch.sort(w, stable=True)
+        wptr = torch.searchsorted(ws, torch.arange(V + 1, device=dev, dtype=ws.dtype))
+        doc_of = torch.repeat_interleave(torch.arange(D, device=dev, dtype=torch.int32),
+                                         (ptr[1:] - ptr[:-1]), output_size=c.nnz)
+        wlen = torch.diff(wptr).cpu().numpy().astype(np.int64)
+        return DeviceCorpus(
+            doc_ptr=ptr.to(torch.int32), word_idx=w.to(torch.int32), counts=cnt,
+            word_ptr=wptr.to(torch.int32), csc_ent=perm.to(torch.int32), csc_doc=doc_of[perm],
+            num_docs=D, num_terms=V, nnz=c.nnz, doc_len=lens.astype(np.int64), word_len=wlen,
         )

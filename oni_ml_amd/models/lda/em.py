@@ -180,7 +180,7 @@ class LDAEngine:
             self.doc_range = (int(doc_offset), int(doc_offset) + corpus.num_docs)
             if dist is not None:
                 self.global_docs = dist.allreduce_int(corpus.num_docs)
-        elif dist is not None and dist.world_size > 1:
+        elif dist is not None and dist.active:
             d0, d1 = dist.shard_range(corpus)
             self.doc_range = (d0, d1)
             corpus = corpus.slice_docs(d0, d1)
@@ -214,7 +214,7 @@ class LDAEngine:
             self.class_total = self._red[2:]
             # Several ranks: the E-step writes rank-local statistics, the all-reduce works on copies
             # (re-reducing unchanged locals after the device loop has converged is then a no-op).
-            self._distributed = dist is not None and dist.world_size > 1
+            self._distributed = dist is not None and dist.active
             self._cw_local = torch.zeros_like(self.cw) if self._distributed else self.cw
             self._red_local = torch.zeros_like(self._red) if self._distributed else self._red
             self.suff_plan = H.SuffPlan(self.dc.word_len, dev, wide=_use_wide(self.KS))
@@ -310,7 +310,7 @@ class LDAEngine:
 
     def exchange_bytes_per_iteration(self) -> int:
         """Payload this rank hands to the collectives every EM iteration (class_word rows + scalars)."""
-        if self.dist is None or self.dist.world_size <= 1:
+        if self.dist is None or not self.dist.active:
             return 0
         el = self.cw.element_size()
         scal = (2 + self.KS) * 8
@@ -376,7 +376,7 @@ class LDAEngine:
         self._red = torch.zeros(2 + KS, dtype=f64, device=dev)
         self._scalars = self._red[:2]
         self.class_total = self._red[2:]
-        self._distributed = self.dist is not None and self.dist.world_size > 1
+        self._distributed = self.dist is not None and self.dist.active
         self._cw_local = torch.zeros_like(self.cw) if self._distributed else self.cw
         self._red_local = torch.zeros_like(self._red) if self._distributed else self._red
         self.suff_plan = H.SuffPlan(self.dc.word_len, dev)
@@ -436,8 +436,11 @@ class LDAEngine:
         main = torch.cuda.current_stream(self.device)
         if phase == "B":
             pa, pb = self._plan_a, self._plan_b
+            # the likelihood / alpha_ss slices ride on phase A's launch unless it has no workgroups
+            # (a rank that shares no word with any other)
             H.gs_suff64(dc.word_ptr, dc.csc_ent, pb, self.cphi, self._cw_local,
-                        self._suff_part[pa.n_blocks:pa.n_blocks + pb.n_blocks], gate=gate)
+                        self._suff_part[pa.n_blocks:pa.n_blocks + pb.n_blocks], gate=gate,
+                        scalars=None if pa.n_blocks else (self.lik, self.ass, 0, self.lik.numel()))
             H.colsum_partials(self._suff_part, pa.n_blocks + pb.n_blocks, self._red_local, gate=gate)
             self._red.copy_(self._red_local)
             return
@@ -475,6 +478,8 @@ class LDAEngine:
             self._ev_join[j].record(s)
             if s is not late_s:
                 main.wait_event(self._ev_join[j])
+        if phase == "estep":             # the document kernels only (final inference pass)
+            return
         scal = (self.lik, self.ass, 0, self.lik.numel())
         if late_s is not None:
             H.gs_suff64(ss["wpE"], ss["ceE"], ss["planE"], self.cphi, ss["cw_early"], self._suff_part, gate=gate)
@@ -510,7 +515,7 @@ class LDAEngine:
         overlap little; ONI_DIST_EXCHANGE = auto (default) | sparse | dense.  Collective: every rank
         builds it (or none does)."""
         d = self.dist
-        if d is None or d.world_size <= 1 or self.backend == "cpu" or self._chain:
+        if d is None or not d.active or self.backend == "cpu" or self._chain:
             return None
         mode = os.environ.get("ONI_DIST_EXCHANGE", "auto")
         if mode == "dense" or getattr(d, "deterministic", False):
@@ -523,7 +528,7 @@ class LDAEngine:
 
     @property
     def exchange_mode(self) -> str:
-        if self.dist is None or self.dist.world_size <= 1:
+        if self.dist is None or not self.dist.active:
             return "none"
         return "sparse-alltoall" if self._xchg is not None else "dense-allreduce"
 
@@ -568,7 +573,7 @@ class LDAEngine:
                 if 0 <= d < c.num_docs:
                     a, b = c.doc_ptr[d], c.doc_ptr[d + 1]
                     np.add.at(cw[k], c.word_idx[a:b], c.counts[a:b])
-        if local and self.dist is not None and self.dist.world_size > 1:
+        if local and self.dist is not None and self.dist.active:
             import torch.distributed as td
             t = torch.from_numpy(cw).to(self.dist._coll_device())
             td.all_reduce(t)
@@ -733,7 +738,8 @@ class LDAEngine:
             # totals of both launches and the all-reduce input
             pa, pb = self._plan_a, self._plan_b
             H.lda_suffstats_fused(dc.word_ptr, dc.csc_ent, dc.csc_doc, pb, self.e, self.r, self.beta,
-                                  self._cw_local, self._suff_part[pa.n_blocks:pa.n_blocks + pb.n_blocks], gate=gate)
+                                  self._cw_local, self._suff_part[pa.n_blocks:pa.n_blocks + pb.n_blocks], gate=gate,
+                                  scalars=None if pa.n_blocks else (self.lik, self.ass, 0, self.lik.numel()))
             H.colsum_partials(self._suff_part, pa.n_blocks + pb.n_blocks, self._red_local, gate=gate)
             self._red.copy_(self._red_local)
             return
@@ -849,7 +855,7 @@ class LDAEngine:
                 if estimate_alpha:
                     self.alpha = special.opt_alpha(float(host[1]), num_docs, self.K)
                 return float(host[0]), float(host[1])
-            if self.dist is not None and self.dist.world_size > 1 and not self._chain:
+            if self.dist is not None and self.dist.active and not self._chain:
                 self._cw_local = self.cw.clone()     # this rank's own rows (<rank>.beta)
                 tok = self._comm_begin()
                 sc = self.dist.allreduce_suffstats(self.cw, sc)
@@ -1132,26 +1138,57 @@ class LDAEngine:
     def log_beta(self, cw: Optional[torch.Tensor] = None) -> np.ndarray:
         """[K, V] float64 log p(w|z) as lda-c would save it (-100 floor).  Collective under the
         sparse exchange unless ``cw`` (a ``global_cw()`` result) is given."""
-        cw = (self.global_cw() if cw is None else cw)[:, :self.K].double()
-        ct = self.class_total[:self.K]
-        lb = torch.where(cw > 0, torch.log(cw) - torch.log(ct), torch.full_like(cw, LOG_FLOOR))
-        return lb.T.contiguous().cpu().numpy()
+        cw = (self.global_cw() if cw is None else cw)[:, :self.K]
+        return _log_beta_host(cw, self.class_total[:self.K])
 
     def local_log_beta(self) -> np.ndarray:
         """[K, V] log of this rank's own class_word rows over the GLOBAL class totals (-100 floor):
         the per-worker ``<rank>.beta`` (README.md:121), final.beta = log(sum over ranks of exp)."""
         local = getattr(self, "_cw_local", None)
-        cw = (self.cw if local is None else local)[:, :self.K].double()
-        ct = self.class_total[:self.K].to(cw.device)
-        lb = torch.where(cw > 0, torch.log(cw) - torch.log(ct), torch.full_like(cw, LOG_FLOOR))
-        return lb.T.contiguous().cpu().numpy()
+        cw = (self.cw if local is None else local)[:, :self.K]
+        return _log_beta_host(cw, self.class_total[:self.K].to(cw.device))
+
+    def word_assignments(self) -> np.ndarray:
+        """run_em's final pass: a fresh E-step of every document under the current
+        (final) model, then for every corpus entry of this rank the topic of its largest phi, the first
+        maximum (lda-c write_word_assignment).  Overwrites gamma and the per-document state: read the
+        model and gamma first.  Returns int64 [nnz] in corpus entry order.
+
+        fp64 HIP engine: the document kernels alone (no sufficient statistics), whose final pass leaves
+        c_n phi_nk = E_jk b_nk c_n / P_n -- phi of each word under its chunk's gamma, as lda-c's
+        sequential pass leaves phi[n] -- in the c.phi rows; torch backend: Jacobi phi = E_k b_kn / P_n;
+        cpu backend: psi(gamma) + log beta with the fresh gamma."""
+        K = self.K
+        if self.backend == "hip" and self.fp64:
+            self._push_params()
+            self._launch_estep64(phase="estep")
+            z = torch.empty(self.corpus.nnz, dtype=torch.int64, device=self.device)
+            step = 1 << 22
+            for a in range(0, self.corpus.nnz, step):
+                b = min(self.corpus.nnz, a + step)
+                z[a:b] = torch.argmax(self.cphi[a:b, :K], dim=1)
+            return z.cpu().numpy()
+        if self.backend == "torch":
+            from ...ops import reference as R
+            out = R.estep_jacobi(self.t_doc_ptr, self.t_word, self.t_cnt, self.beta, K, self.alpha,
+                                 self.var_max_iter, self.settings.var_converged)
+            lens = (self.t_doc_ptr[1:] - self.t_doc_ptr[:-1]).to(torch.int64)
+            doc_of = torch.repeat_interleave(torch.arange(self.D, device=self.device), lens)
+            return torch.argmax(out["e"][doc_of][:, :K] * self.beta[self.t_word, :K], dim=1).cpu().numpy()
+        if self.backend == "cpu":
+            lb = torch.where(self.beta > 0, torch.log(self.beta), torch.full_like(self.beta, LOG_FLOOR))
+            return self._native.lda_assign_ldac(self.corpus.doc_ptr, self.corpus.word_idx,
+                                                self.corpus.counts.astype(np.float64), np.ascontiguousarray(lb.T.numpy()),
+                                                self.alpha, self.var_max_iter, self.settings.var_converged,
+                                                gs_updates=self.settings.gs_updates).astype(np.int64)
+        raise NotImplementedError(f"word assignments for backend {self.backend} / {self.precision}")
 
     def local_gamma(self) -> np.ndarray:
         return self.gamma[:, :self.K].to("cpu", torch.float64, copy=True).numpy()
 
     def gather_gamma(self) -> np.ndarray:
         g = self.local_gamma()
-        if self.dist is not None and self.dist.world_size > 1:
+        if self.dist is not None and self.dist.active:
             return self.dist.gather_rows(g, self.global_docs)
         return g
 
@@ -1238,6 +1275,21 @@ class LDAEngine:
         res = LDAResult(log_beta=None, gamma=None, alpha=self.alpha, num_topics=self.K, num_terms=self.V,
                         likelihoods=hist, stats=stats, em_iterations=i, seconds=time.perf_counter() - t0)
         return res
+
+
+def _log_beta_host(cw: torch.Tensor, ct: torch.Tensor, rows: int = 1 << 20) -> np.ndarray:
+    """[K, V] float64 host array of log(cw) - log(ct) (-100 floor where cw == 0), computed in blocks of
+    ``rows`` words: the device transient stays ~rows x K doubles instead of five V x K temporaries
+    (11-14 GB at the 30-day scale, K = 100)."""
+    V, K = cw.shape
+    out = np.empty((K, V), np.float64)
+    lct = torch.log(ct.to(torch.float64))
+    for a in range(0, V, rows):
+        b = min(V, a + rows)
+        c = cw[a:b].to(torch.float64)
+        lb = torch.where(c > 0, torch.log(c) - lct, torch.full_like(c, LOG_FLOOR))
+        out[:, a:b] = lb.T.cpu().numpy()
+    return out
 
 
 def _conv(L_old: float, lik: float) -> float:

@@ -133,7 +133,7 @@ def estimate(corpus: Corpus, num_topics: int, alpha_init: float, settings: LDASe
     ``<tag>.gamma`` / ``word-assignments.dat`` when the files are closed -- oni-lda-c's per-worker
     ``<rank>.gamma`` blocks "combined to form final.gamma" (README.md:121)."""
     rank0 = dist is None or dist.rank == 0
-    multi = dist is not None and dist.world_size > 1
+    multi = dist is not None and dist.active
     r = 0 if dist is None else dist.rank
     if rank0:
         os.makedirs(outdir, exist_ok=True)
@@ -233,17 +233,18 @@ def estimate(corpus: Corpus, num_topics: int, alpha_init: float, settings: LDASe
     res.gamma = eng.local_gamma()          # this rank's documents (all of them with one rank)
     res.doc_range = eng.doc_range
     if write_word_assignments:
-        # device argmax + native formatting; on the background writer with the deferred model files
-        # when allowed (the caller's next stages do not wait for it)
-        wa, lb, g, dev, shard = os.path.join(outdir, "word-assignments.dat"), res.log_beta, res.gamma, \
-            eng.cw.device, eng.corpus
+        # run_em's final pass: a fresh E-step under the final model (after gamma and beta were read),
+        # the argmax of each word's phi; native formatting on the background writer with the deferred
+        # model files when allowed (the caller's next stages do not wait for it)
+        wa, shard = os.path.join(outdir, "word-assignments.dat"), eng.corpus
+        z = eng.word_assignments()
         if multi:
             part = os.path.join(outdir, f".word-assignments.dat.part{r}")
             parts.append((wa, part))
             wa = part
 
         def _assign():
-            _write_assignment_file(wa, shard, word_topics(shard, lb, g, device=dev))
+            _write_assignment_file(wa, shard, z)
 
         if defer_files:
             writer.submit(_assign)

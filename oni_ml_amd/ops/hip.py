@@ -721,8 +721,11 @@ class GSSplitPlan:
                     error=torch.zeros(1, dtype=torch.int32, device=device), docs=len(docs))
 
 
-def gs_split(doc_ptr, word_idx, counts, beta, K, gs_updates, params, gamma, cphi, lik, alpha_ss, iters, batch):
-    """One launch of the fp64 split-document E-step over one GSSplitPlan batch."""
+def gs_split(doc_ptr, word_idx, counts, beta, K, gs_updates, params, gamma, cphi, lik, alpha_ss, iters, batch,
+             dbg=None):
+    """One launch of the fp64 split-document E-step over one GSSplitPlan batch.  dbg: optional int64[8]
+    phase timer of workgroup 0 (word phase, barrier 1, publish + gather, barrier 2, refresh, barrier 3,
+    sweep end, chunks)."""
     D = doc_ptr.numel() - 1
     nnz = word_idx.numel()
     V, KS = beta.shape
@@ -745,7 +748,8 @@ def gs_split(doc_ptr, word_idx, counts, beta, K, gs_updates, params, gamma, cphi
         batch["seg_base"].data_ptr(), batch["doc_slot"].data_ptr(), int(nb),
         _chk(batch["xchg"], torch.int64, "xchg", (2 * nb * 2 * (KS + 1),), dev),
         _chk(batch["counter"], torch.int32, "counter", (2 * batch["docs"],), dev), int(batch["docs"]),
-        _chk(batch["error"], torch.int32, "error", (1,), dev), _stream())
+        _chk(batch["error"], torch.int32, "error", (1,), dev), _stream(),
+        0 if dbg is None else _chk(dbg, torch.int64, "dbg", (8,), dev))
 
 
 class GSPlan:

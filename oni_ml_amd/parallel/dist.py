@@ -37,10 +37,18 @@ class DistContext:
     # (LDAEngine(emulate_shards=N)), so an N-rank run is bitwise equal to that single-process run.
     # The default ring all-reduce is bitwise identical on every rank but its association differs.
     deterministic: bool = False
+    # ONI_DIST_FORCE_GROUP=1: a process group even for one rank -- every distributed code path (the
+    # collectives, the sharded pipeline) then runs, e.g. one-rank RCCL on a one-GPU box
+    forced: bool = False
 
     @property
     def initialized(self) -> bool:
-        return self.world_size > 1 and torch.distributed.is_initialized()
+        return (self.world_size > 1 or self.forced) and torch.distributed.is_initialized()
+
+    @property
+    def active(self) -> bool:
+        """The multi-rank code paths apply: several ranks, or a forced one-rank group."""
+        return self.world_size > 1 or self.forced
 
     # -------------------------------------------------------------- sharding
     def shard_range(self, corpus):
@@ -366,9 +374,11 @@ def init_from_env(expected_world: int = None, backend: str = None, timeout_s: fl
         dev = torch.device("cuda", local % max(1, torch.cuda.device_count()))
     else:
         dev = torch.device("cpu")
+    forced = os.environ.get("ONI_DIST_FORCE_GROUP", "0") == "1"
     ctx = DistContext(rank=rank, world_size=world, local_rank=local, device=dev, backend=backend,
-                      deterministic=os.environ.get("ONI_DIST_DETERMINISTIC", "0") == "1")
-    if world > 1:
+                      deterministic=os.environ.get("ONI_DIST_DETERMINISTIC", "0") == "1", forced=forced)
+    if world > 1 or forced:
+        os.environ.setdefault("MASTER_PORT", "29533")
         import torch.distributed as td
 
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")

@@ -54,7 +54,7 @@ def run_lda(cfg, corpus: Corpus, dist=None, device=None, log=print, local_shard:
                     device=device, dist=dist, seed=cfg.seed, resume=cfg.resume,
                     write_word_assignments=cfg.word_assignments,
                     write_rank_gamma=(cfg.rank_gamma if cfg.rank_gamma is not None
-                                      else dist is not None and dist.world_size > 1),
+                                      else dist is not None and dist.active),
                     verbose=cfg.verbose, fault_at_iteration=cfg.extra.get("fault_at_iteration"),
                     defer_files=True, local_shard=local_shard, doc_offset=doc_offset)
 

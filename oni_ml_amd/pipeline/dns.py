@@ -21,7 +21,7 @@ from .runner import StageRunner
 
 
 def run(cfg, dist=None, device=None, log=print) -> dict:
-    if dist is not None and dist.world_size > 1:
+    if dist is not None and dist.active:
         from .sharded import run_dns
         return run_dns(cfg, dist, device, log)
     rank = 0 if dist is None else dist.rank
@@ -122,7 +122,7 @@ def score_dns(cfg, tab: FD.DnsTable, top, tables: C.ModelTables, device, log=pri
     every rank's raw rows; the survivors of all ranks merged into one ascending file.  ``ip_map``:
     doc row of every ip_dst id of the pre-LDA dictionary of ``tab`` (its raw rows' ids are a prefix)."""
     from ..parallel import shardio as SIO
-    multi = SIO.world(ctx) > 1
+    multi = ctx is not None and ctx.active
     cuts = None
     if not cfg.strict:
         cuts = {k: np.asarray(v, np.float64) for k, v in C.load_json(os.path.join(cfg.lpath, "dns_cuts.json"))["cuts"].items()}

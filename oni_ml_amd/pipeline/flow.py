@@ -31,7 +31,7 @@ def _word_names(ws: FF.FlowWordSpace, keys: np.ndarray):
 
 
 def run(cfg, dist=None, device=None, log=print) -> dict:
-    if dist is not None and dist.world_size > 1:
+    if dist is not None and dist.active:
         from .sharded import run_flow
         return run_flow(cfg, dist, device, log)
     rank = 0 if dist is None else dist.rank
@@ -145,7 +145,7 @@ def score_flow(cfg, ft: FF.FlowTable, tables: C.ModelTables, device, log=print, 
     the sortByKey shuffle).  ``ip_rows``: doc row of every ip dictionary id of ``ft`` (-1: not a
     document) -- replaces the name lookup through ``tables.doc_index()``."""
     from ..parallel import shardio as SIO
-    multi = SIO.world(ctx) > 1
+    multi = ctx is not None and ctx.active
     cuts = cfg.fixed_cuts()          # fixed CUT cuts apply to both stages (flow_pre_lda.scala:95-98)
     if cuts is None and not cfg.strict:
         saved = C.load_json(os.path.join(cfg.lpath, "flow_cuts.json"))

@@ -77,6 +77,19 @@ def main():
                                    word_sweeps=int((L * it).sum()), batches=len(spl.batches),
                                    workgroups=int(sum(spl.segments.values())),
                                    max_segments=int(max(spl.segments.values()))))
+        if a.phases:
+            dbg = torch.zeros(8, dtype=torch.int64, device="cuda")
+            b0 = spl.batches[0]
+            H.gs_split(dc.doc_ptr, dc.word_idx, dc.counts, eng.beta, eng.K, eng._U, eng._params, eng.gamma,
+                       eng.cphi, eng.lik, eng.ass, eng.iters, b0, dbg=dbg)
+            v = dbg.cpu().tolist()
+            ch = max(v[7], 1)
+            d0 = int(b0["seg_doc"][0].item())
+            out["buckets"][-1]["phase_cycles_per_chunk"] = dict(
+                word=round(v[0] / ch), barrier1=round(v[1] / ch), exchange=round(v[2] / ch),
+                barrier2=round(v[3] / ch), refresh=round(v[4] / ch), barrier3=round(v[5] / ch),
+                sweep_end_total=v[6], chunks=v[7], doc_len=int(lens[d0]),
+                segments=int(b0["seg_count"][0].item()))
         print(json.dumps(out["buckets"][-1]), flush=True)
     for var, order in eng.gs_plan.plan:
         if a.only and names[var] != a.only:

@@ -37,7 +37,7 @@ def main():
     ctx = D.init_from_env()
     c = shifted_vocab(planted_corpus(num_docs=3000, num_terms=2000, num_topics=8, mean_tokens=40, tail=1.0,
                                      max_tokens=20_000, seed=4))
-    eng = LDAEngine(c, K, LDASettings(em_max_iter=6), backend="hip", dist=ctx if ctx.world_size > 1 else None,
+    eng = LDAEngine(c, K, LDASettings(em_max_iter=6), backend="hip", dist=ctx if ctx.active else None,
                     seed=3, precision=os.environ.get("DIST_CHECK_PRECISION", "fp64"))
     res = eng.run()
     lb = eng.log_beta()

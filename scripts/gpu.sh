@@ -8,13 +8,15 @@
 #   smoke     __graft_entry__.smoke()
 #   bench     python bench.py $BENCH_ARGS                       -> $OUT/bench.json
 #   prof      rocprofv3 --kernel-trace --stats of a short bench -> $OUT/prof_summary.md, timeline.txt
-#   phases    scripts/bench_gs64.py --phases (per-bucket E-step times)
+#   phases    scripts/bench_gs64.py --phases $PHASES_ARGS (per-bucket E-step times, phase cycles per chunk)
 #   configs   scripts/bench_configs.sh (every BASELINE config on one GPU)
 #   strong    scripts/strong_emulated.py (per-shard EM times for N = 2/4/8)
 #   parity    scripts/precision_parity.py $PARITY_ARGS
 #   micro     build + run scripts/micro/*.hip (fp64 latency / throughput probes)
 #   pmc       one rocprofv3 --pmc pass ($PMC = counter list) over a short bench
 #   nccl      the one-rank RCCL test (tests/test_gpu_dist.py -k nccl)
+#   ab        scripts/ab_env.sh $AB_ROUNDS $AB_VARIANTS (space-separated env settings, one per variant)
+#   ranks     scripts/pipeline_ranks.py $RANKS_ARGS (per-rank stage seconds of the sharded ml_ops pipeline)
 # env: TAG (output dir gpurun_out/$TAG, default s), BENCH_ARGS, PROF_ARGS, PARITY_ARGS, PMC, KEEP_GOING=1
 # (a failing pytest with exit status 1 -- assertion failures, not a crash -- does not stop the session)
 set -u -o pipefail
@@ -49,7 +51,7 @@ for s in "$@"; do
       python scripts/timeline.py "$db" --last-ms ${TIMELINE_MS:-6} > "$OUT/timeline.txt"
       rm -f "$db"; head -14 "$OUT/prof_summary.md" ;;
     phases)
-      timeout -k 10 300 python -u scripts/bench_gs64.py --phases > "$OUT/phases.log" 2>&1 || { tail -20 "$OUT/phases.log"; stop phases 1; }
+      timeout -k 10 300 python -u scripts/bench_gs64.py --phases ${PHASES_ARGS:-} > "$OUT/phases.log" 2>&1 || { tail -20 "$OUT/phases.log"; stop phases 1; }
       grep '^{' "$OUT/phases.log" | cut -c1-300 ;;
     configs)
       OUTDIR="$OUT" timeout -k 10 1000 bash scripts/bench_configs.sh || stop configs $? ;;
@@ -75,6 +77,14 @@ for s in "$@"; do
       db=$(find "$OUT/pmc" -name "*.db" | head -1)
       python scripts/pmc_summary.py "$db" ${PMC_MATCH:+--match "$PMC_MATCH"} --md "$OUT/pmc_summary.md" > /dev/null
       rm -f "$db"; head -30 "$OUT/pmc_summary.md" ;;
+    ab)
+      timeout -k 10 1000 bash scripts/ab_env.sh ${AB_ROUNDS:-3} ${AB_VARIANTS:?set AB_VARIANTS} -- ${AB_ARGS:---steps 20 --warmup 5} \
+        > "$OUT/ab.log" 2>&1 || { tail -20 "$OUT/ab.log"; stop ab 1; }
+      cat "$OUT/ab.log" ;;
+    ranks)
+      timeout -k 10 1100 python -u scripts/pipeline_ranks.py ${RANKS_ARGS:-} --json "$OUT/ranks.json" \
+        --md "$OUT/ranks.md" > "$OUT/ranks.log" 2>&1 || { tail -30 "$OUT/ranks.log"; stop ranks 1; }
+      cat "$OUT/ranks.md" ;;
     nccl)
       timeout -k 10 300 python -u -m pytest tests/test_gpu_dist.py -m gpu -v -k nccl --timeout 120 \
         --timeout-method thread > "$OUT/nccl.log" 2>&1 || { tail -30 "$OUT/nccl.log"; stop nccl 1; }

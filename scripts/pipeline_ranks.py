@@ -1,0 +1,122 @@
+#!/usr/bin/env python
+"""Per-rank stage times of the row-sharded ``ml_ops`` pipeline (pipeline/sharded.py).
+
+Generates one synthetic day, then runs ``oni_ml_amd.cli ml_ops YYYYMMDD <flow|dns> TOL`` with
+N = 1, 2, 4 ... ranks (torchrun; several ranks on one GPU rehearse over gloo -- ONI_DIST_BACKEND
+=gloo -- exactly as the 8-GPU RCCL run splits the work) and reads every rank's metrics file
+(metrics.jsonl / metrics.rank<r>.jsonl).  Reports, per N, the pipeline wall, each stage's seconds
+on every rank, and rank 0's serial share: the seconds rank 0 spends in stages beyond the slowest
+other rank, over the wall.
+
+  python scripts/pipeline_ranks.py --events 1000000 --ranks 1,4 --md out.md --json out.json
+"""
+import argparse
+import json
+import os
+import shutil
+import socket
+import subprocess
+import sys
+import tempfile
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+STAGES = {"flow": ["load", "flow_pre", "lda_pre", "lda", "lda_post", "flow_post"],
+          "dns": ["load", "dns_pre", "lda_pre", "lda", "lda_post", "dns_post"]}
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--source", default="flow", choices=["flow", "dns"])
+    ap.add_argument("--events", type=int, default=1_000_000)
+    ap.add_argument("--ranks", default="1,4")
+    ap.add_argument("--tol", default=None)
+    ap.add_argument("--backend", default="gloo", help="collective backend of the ranks (gloo: many ranks per GPU)")
+    ap.add_argument("--lda-backend", default="auto")
+    ap.add_argument("--md")
+    ap.add_argument("--json")
+    ap.add_argument("--timeout", type=int, default=900)
+    a = ap.parse_args()
+    tol = a.tol or ("1e-5" if a.source == "flow" else "1e-4")
+    tmp = tempfile.mkdtemp(prefix="oni_ranks_")
+    out = dict(source=a.source, events=a.events, backend=a.backend, runs=[])
+    try:
+        if a.source == "flow":
+            from oni_ml_amd.synth.flow import generate_flow_day
+            generate_flow_day(os.path.join(tmp, "in/"), events=a.events, seed=7)
+            inp = ["--flow-path", os.path.join(tmp, "in")]
+        else:
+            from oni_ml_amd.synth.dns import generate_dns_day
+            g = generate_dns_day(os.path.join(tmp, "in"), events=a.events, seed=7, files=4,
+                                 n_names=max(20_000, a.events // 10), n_clients=max(5_000, a.events // 40),
+                                 with_edge_rows=False)
+            inp = ["--dns-path", g["dns_path"], "--top1m", g["top1m"]]
+        for n in [int(x) for x in a.ranks.split(",")]:
+            lp = os.path.join(tmp, f"ml{n}")
+            cli = ["-m", "oni_ml_amd.cli", "ml_ops", "20160122", a.source, tol, "--lpath", lp, "--gpus", str(n),
+                   "--conf", "/nonexistent", "--quiet", "--backend", a.lda_backend] + inp
+            cmd = [sys.executable] + (cli if n == 1 else
+                                      ["-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n),
+                                       "--master-addr", "127.0.0.1", "--master-port", str(_port())] + cli)
+            env = dict(os.environ, ONI_DIST_BACKEND=a.backend)
+            t0 = time.perf_counter()
+            r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=a.timeout)
+            wall = time.perf_counter() - t0
+            if r.returncode != 0:
+                print(r.stdout[-3000:], r.stderr[-6000:], file=sys.stderr)
+                raise SystemExit(f"N={n} failed rc={r.returncode}")
+            summ = json.load(open(os.path.join(lp, "run_summary.json")))
+            per_rank = []
+            for k in range(n):
+                f = os.path.join(lp, "metrics.jsonl" if k == 0 else f"metrics.rank{k}.jsonl")
+                st = {}
+                for line in open(f):
+                    rec = json.loads(line)
+                    if rec.get("status") == "ok" and rec.get("stage") in STAGES[a.source]:
+                        st[rec["stage"]] = st.get(rec["stage"], 0.0) + rec["seconds"]
+                per_rank.append(st)
+            pw = summ["wall_seconds"]
+            serial = 0.0
+            for s in STAGES[a.source]:
+                others = [p.get(s, 0.0) for p in per_rank[1:]]
+                serial += max(0.0, per_rank[0].get(s, 0.0) - (max(others) if others else 0.0))
+            run = dict(ranks=n, process_wall_s=round(wall, 3), pipeline_wall_s=round(pw, 3),
+                       flagged=summ.get("scored"), corpus=summ.get("corpus"),
+                       em_iterations=summ.get("lda", {}).get("em_iterations"),
+                       stage_s=[{k: round(v, 3) for k, v in p.items()} for p in per_rank],
+                       rank0_serial_s=round(serial, 3) if n > 1 else None,
+                       rank0_serial_share=round(serial / pw, 4) if n > 1 else None)
+            out["runs"].append(run)
+            print(json.dumps(run), flush=True)
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
+    if a.json:
+        json.dump(out, open(a.json, "w"), indent=1)
+    if a.md:
+        lines = [f"# Per-rank stage seconds, {a.source} day of {a.events} events (collectives: {a.backend})", ""]
+        for run in out["runs"]:
+            lines.append(f"## N = {run['ranks']}: pipeline wall {run['pipeline_wall_s']} s, flagged {run['flagged']}, "
+                         f"EM iterations {run['em_iterations']}"
+                         + (f", rank 0 serial {run['rank0_serial_s']} s = {100 * run['rank0_serial_share']:.1f} % of the wall"
+                            if run["ranks"] > 1 else ""))
+            lines.append("")
+            lines.append("| rank | " + " | ".join(STAGES[a.source]) + " |")
+            lines.append("|---" * (len(STAGES[a.source]) + 1) + "|")
+            for k, p in enumerate(run["stage_s"]):
+                lines.append(f"| {k} | " + " | ".join(f"{p.get(s, 0):.3f}" for s in STAGES[a.source]) + " |")
+            lines.append("")
+        open(a.md, "w").write("\n".join(lines) + "\n")
+
+
+if __name__ == "__main__":
+    main()

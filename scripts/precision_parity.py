@@ -22,6 +22,13 @@ A fourth run, `cpu@1`, is lda-c's own run-to-run spread: the same fp64 engine fr
 random init (oni-lda-c seeds its MT19937 from the clock, so no two reference runs agree).
 
   python scripts/precision_parity.py [--events 1000000] [--topics 20] [--engines hip,torch,cpu,cpu@1]
+  python scripts/precision_parity.py --corpus dns --events 2000000 --engines cpu,cpuU,cpu@1      (config 4)
+  python scripts/precision_parity.py --events 12500000 --topics 100 --sub-nnz 1500000 --engines cpu,cpuU,cpu@1
+
+``cpuU`` is the GPU engine's arithmetic and schedule (tests/test_gs64.py pins the HIP kernels to it at
+1e-10), so a CPU-only run (cpu, cpuU, cpu@1) measures the GPU engine's parity with lda-c.
+``--sub-nnz``: keep the longest documents (they carry the block schedule's largest chunks) plus a
+seeded random sample of the others up to about that many corpus entries.
 """
 from __future__ import annotations
 
@@ -47,7 +54,7 @@ def _train(corpus, K, name, dev, seed, var_max_iter=None):
     backend, precision = {"hip": ("hip", "fp64"), "hip32": ("hip", "fp32"), "torch": ("torch", "fp64"),
                           "cpu": ("cpu", "fp64"), "cpuU": ("cpu", "fp64")}[name]
     if name == "cpuU":
-        st.gs_updates = 32
+        st.gs_updates = GS_U
     eng = LDAEngine(corpus, K, st, backend=backend, device=dev, seed=seed, precision=precision)
     if dev.type == "cuda":
         torch.cuda.synchronize()
@@ -59,6 +66,32 @@ def _train(corpus, K, name, dev, seed, var_max_iter=None):
     res.gamma = np.asarray(eng.gather_gamma(), dtype=np.float64)
     res.log_beta = np.asarray(eng.log_beta(), dtype=np.float64)
     return res, sec
+
+
+GS_U = 32
+
+
+def _subsample(c, nnz, keep, seed):
+    """The `keep` longest documents plus random others (corpus order kept) up to ~nnz entries; the
+    vocabulary is re-indexed to the words that remain."""
+    from oni_ml_amd.corpus.csr import Corpus
+    lens = c.lengths()
+    order = np.argsort(-lens, kind="stable")
+    chosen = set(order[:keep].tolist())
+    budget = nnz - int(lens[order[:keep]].sum())
+    rng = np.random.default_rng(seed + 17)
+    for d in rng.permutation(c.num_docs):
+        if budget <= 0:
+            break
+        if d not in chosen:
+            chosen.add(int(d))
+            budget -= int(lens[d])
+    docs = np.array(sorted(chosen), np.int64)
+    ptr = np.concatenate([[0], np.cumsum(lens[docs])])
+    idx = np.concatenate([np.arange(c.doc_ptr[d], c.doc_ptr[d + 1]) for d in docs])
+    w = c.word_idx[idx]
+    uw, inv = np.unique(w, return_inverse=True)
+    return Corpus(ptr, inv.astype(np.int32), c.counts[idx], int(uw.size))
 
 
 def _theta(gamma):
@@ -96,13 +129,25 @@ def main():
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--engines", default="hip,cpu,cpuU,cpu@1,hip32")
     ap.add_argument("--var-max-iter", type=int, default=None, help="override settings.txt var max iter (20)")
+    ap.add_argument("--corpus", default="flow", choices=["flow", "dns"])
+    ap.add_argument("--sub-nnz", type=int, default=0, help="sub-sample to ~this many entries, longest documents kept")
+    ap.add_argument("--keep-longest", type=int, default=20)
+    ap.add_argument("--gs-updates", type=int, default=32, help="U of the cpuU engine (the GPU schedule)")
     ap.add_argument("--json", default=None)
     ap.add_argument("--md", default=None)
     args = ap.parse_args()
 
-    from oni_ml_amd.pipeline.flow import synthetic_flow_corpus
     dev = torch.device("cuda", 0) if torch.cuda.is_available() else torch.device("cpu")
-    corpus, _ = synthetic_flow_corpus(events=args.events, seed=args.seed, device=dev)
+    if args.corpus == "dns":
+        from oni_ml_amd.pipeline.dns import synthetic_dns_corpus
+        corpus, _ = synthetic_dns_corpus(events=args.events, seed=args.seed, device=dev)
+    else:
+        from oni_ml_amd.pipeline.flow import synthetic_flow_corpus
+        corpus, _ = synthetic_flow_corpus(events=args.events, seed=args.seed, device=dev)
+    if args.sub_nnz and corpus.nnz > args.sub_nnz:
+        corpus = _subsample(corpus, args.sub_nnz, args.keep_longest, args.seed)
+    global GS_U
+    GS_U = args.gs_updates
     print(f"corpus: {corpus.num_docs} docs, {corpus.num_terms} words, {len(corpus.word_idx)} entries", flush=True)
 
     runs = {}
@@ -154,8 +199,12 @@ def main():
         ecols = ["seconds", "em_iterations", "final_likelihood", "alpha"]
         pcols = list(next(iter(out["pairs"].values())).keys()) if out["pairs"] else []
         fmt = lambda v: f"{v:.6g}" if isinstance(v, float) else str(v)
+        src = "DNS" if args.corpus == "dns" else "netflow"
+        sub = f", sub-sampled to the {args.keep_longest} longest + random documents" if args.sub_nnz else ""
         lines = ["# Precision / schedule parity: GPU engines vs lda-c (literal per-word Gauss-Seidel, fp64)", "",
-                 f"Corpus: bench.py's 1-day synthetic netflow ({args.events} events, seed {args.seed}): "
+                 f"Corpus: synthetic 1-day {src} ({args.events} events, seed {args.seed}{sub}), longest document "
+                 f"{int(corpus.lengths().max())} words (block schedule chunk {-(-int(corpus.lengths().max()) // GS_U)} "
+                 f"words at U = {GS_U}): "
                  f"{corpus.num_docs} docs, {corpus.num_terms} words, {len(corpus.word_idx)} entries; "
                  f"K = {args.topics}, lda-c default settings, same random init (seed {args.seed}). "
                  f"Scores = theta_d . phi_w over every corpus entry; overlap = shared fraction of the "

@@ -1,0 +1,146 @@
+#!/usr/bin/env python
+"""Strong-scaling ceiling of document data parallelism, measured on one GPU.
+
+oni-lda-c splits one model.dat over its MPI ranks (ml_ops.sh:22-23,80); the engine shards the
+documents contiguously and nnz-balanced (parallel/dist.py shard_bounds).  An N-GPU EM iteration
+takes max over ranks r of (rank r's E-step + M-step on its shard) + the class_word reduction.  This
+script measures the first term exactly, one shard at a time on one GPU, and models the second:
+
+  1. train the whole corpus a few EM iterations (the global model of a real run);
+  2. for N = 1, 2, 4, 8 and every rank r: an engine on shard r alone (global vocabulary), started
+     from that global model, times one EM iteration (median of --reps, the model reloaded before
+     each) -- the work rank r does per iteration of the N-GPU run;
+  3. the longest document alone: the chain floor no document sharding can go below;
+  4. the dense class_word all-reduce (K V 8 bytes): a ring over the xGMI links (2 (N-1)/N bytes per
+     153 GB/s link) and the fully connected mesh's direct all-to-all form (2 bytes / (N 153 GB/s)),
+     each + 10 us per step of latency.
+
+  python scripts/strong_emulated.py --configs headline,k50,dns,c5shard --json out.json --md out.md
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+CONFIGS = {
+    "headline": dict(kind="flow", events=1_000_000, K=20, label="config 2: flow 1-day, K=20"),
+    "k50": dict(kind="flow", events=1_000_000, K=50, label="config 3: flow 1-day, K=50"),
+    "dns": dict(kind="dns", events=2_000_000, K=20, label="config 4: DNS 1-day, K=20"),
+    "c5shard": dict(kind="flow", events=12_500_000, K=100, label="config 5 shard: flow 12.5M events, K=100"),
+}
+LINK_BPS = 153e9
+STEP_LAT = 10e-6
+
+
+def _corpus(cfg):
+    if cfg["kind"] == "dns":
+        from oni_ml_amd.pipeline.dns import synthetic_dns_corpus
+        c, _ = synthetic_dns_corpus(events=cfg["events"], seed=0, device="cuda")
+    else:
+        from oni_ml_amd.pipeline.flow import synthetic_flow_corpus
+        c, _ = synthetic_flow_corpus(events=cfg["events"], seed=0, device="cuda")
+    return c
+
+
+def _time_iteration(eng, lb, alpha, vmi, D, reps):
+    ts = []
+    for _ in range(reps):
+        eng.init_from_model(lb, alpha)
+        eng.var_max_iter = vmi
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        eng.em_iterations(1, True, D, stop=False)
+        torch.cuda.synchronize()
+        ts.append(time.perf_counter() - t0)
+    return float(np.median(ts))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--configs", default="headline,k50,dns,c5shard")
+    ap.add_argument("--ranks", default="1,2,4,8")
+    ap.add_argument("--warm-em", type=int, default=6)
+    ap.add_argument("--reps", type=int, default=7)
+    ap.add_argument("--json")
+    ap.add_argument("--md")
+    a = ap.parse_args()
+    from oni_ml_amd.corpus.csr import Corpus
+    from oni_ml_amd.models.lda.em import LDAEngine
+    from oni_ml_amd.models.lda.settings import LDASettings
+    from oni_ml_amd.parallel.dist import shard_bounds
+    out = {}
+    for name in a.configs.split(","):
+        cfg = CONFIGS[name]
+        c = _corpus(cfg)
+        K, D = cfg["K"], c.num_docs
+        full = LDAEngine(c, K, LDASettings(), backend="hip", seed=0, precision="fp64")
+        full.init_random()
+        full.em_iterations(a.warm_em, True, D, stop=False)
+        torch.cuda.synchronize()
+        lb, alpha, vmi = full.log_beta(), full.alpha, full.var_max_iter
+        t_full = _time_iteration(full, lb, alpha, vmi, D, a.reps)
+        del full
+        torch.cuda.empty_cache()
+        lens = c.lengths()
+        dl = int(np.argmax(lens))
+        one = c.slice_docs(dl, dl + 1)
+        e1 = LDAEngine(Corpus(one.doc_ptr, one.word_idx, one.counts, c.num_terms), K, LDASettings(), backend="hip",
+                       seed=0, precision="fp64", local_shard=True)
+        t_chain = _time_iteration(e1, lb, alpha, vmi, D, a.reps)
+        del e1
+        rec = dict(label=cfg["label"], docs=D, nnz=c.nnz, vocab=c.num_terms, K=K, longest_doc=int(lens[dl]),
+                   full_ms=round(t_full * 1e3, 4), chain_floor_ms=round(t_chain * 1e3, 4), ranks={})
+        bytes_ = K * c.num_terms * 8
+        for n in [int(x) for x in a.ranks.split(",")]:
+            if n == 1:
+                per = [t_full]
+            else:
+                per = []
+                for d0, d1 in shard_bounds(c.doc_ptr, n):
+                    sh = c.slice_docs(d0, d1)
+                    e = LDAEngine(Corpus(sh.doc_ptr, sh.word_idx, sh.counts, c.num_terms), K, LDASettings(),
+                                  backend="hip", seed=0, precision="fp64", local_shard=True)
+                    per.append(_time_iteration(e, lb, alpha, vmi, D, a.reps))
+                    del e
+                    torch.cuda.empty_cache()
+            ring = 0.0 if n == 1 else 2 * (n - 1) / n * bytes_ / LINK_BPS + 2 * (n - 1) * STEP_LAT
+            mesh = 0.0 if n == 1 else 2 * bytes_ / (n * LINK_BPS) + 2 * STEP_LAT
+            mx = max(per)
+            rec["ranks"][n] = dict(per_rank_ms=[round(x * 1e3, 4) for x in per], max_ms=round(mx * 1e3, 4),
+                                   allreduce_ring_ms=round(ring * 1e3, 4), allreduce_mesh_ms=round(mesh * 1e3, 4),
+                                   iter_ms_ring=round((mx + ring) * 1e3, 4), iter_ms_mesh=round((mx + mesh) * 1e3, 4),
+                                   speedup_ring=round(t_full / (mx + ring), 3), speedup_mesh=round(t_full / (mx + mesh), 3),
+                                   chain_bound_speedup=round(t_full / max(t_chain, 1e-12), 3))
+            print(json.dumps(dict(config=name, n=n, **rec["ranks"][n])), flush=True)
+        out[name] = rec
+        del c
+        torch.cuda.empty_cache()
+    if a.json:
+        json.dump(out, open(a.json, "w"), indent=1)
+    if a.md:
+        L = ["# Strong scaling emulated on one MI355X (per-shard EM iteration, max over ranks + modelled all-reduce)", ""]
+        for name, rec in out.items():
+            L.append(f"## {rec['label']}")
+            L.append(f"docs {rec['docs']}, nnz {rec['nnz']}, V {rec['vocab']}; longest document {rec['longest_doc']} "
+                     f"words; one GPU {rec['full_ms']} ms / EM iteration; **chain floor** (longest document alone) "
+                     f"{rec['chain_floor_ms']} ms = at most {rec['full_ms'] / max(rec['chain_floor_ms'], 1e-9):.2f}x")
+            L.append("")
+            L.append("| N | max shard ms | per-rank ms | all-reduce ring / mesh ms | iteration ms (ring / mesh) | speedup (ring / mesh) |")
+            L.append("|---|---|---|---|---|---|")
+            for n, r in rec["ranks"].items():
+                L.append(f"| {n} | {r['max_ms']} | {' '.join(str(x) for x in r['per_rank_ms'])} | "
+                         f"{r['allreduce_ring_ms']} / {r['allreduce_mesh_ms']} | {r['iter_ms_ring']} / {r['iter_ms_mesh']} | "
+                         f"{r['speedup_ring']} / {r['speedup_mesh']} |")
+            L.append("")
+        open(a.md, "w").write("\n".join(L) + "\n")
+
+
+if __name__ == "__main__":
+    main()

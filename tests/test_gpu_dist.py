@@ -66,6 +66,7 @@ def test_four_rank_fp64_engine_matches_single_rank(exchange):
     assert abs(four["beta_checksum"] - one["beta_checksum"]) / abs(one["beta_checksum"]) < 1e-10
 
 
+@pytest.mark.experimental
 def test_two_rank_fp32_engine_matches_single_rank():
     one = _run(1, "auto", precision="fp32")
     two = _run(2, "sparse", precision="fp32")
@@ -117,3 +118,54 @@ def test_rows_accumulate_kernel_matches_rank_order_sum():
                       recv.to(d), out)
     torch.cuda.synchronize()
     assert torch.equal(out.cpu(), ref)
+
+
+def _nccl_env(**kw):
+    env = dict(os.environ, ONI_DIST_FORCE_GROUP="1", ONI_DIST_BACKEND="nccl", WORLD_SIZE="1", RANK="0",
+               LOCAL_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_port()))
+    env.update(kw)
+    return env
+
+
+@pytest.mark.parametrize("exchange,overlap", [("dense", "1"), ("sparse", "1"), ("sparse", "0")])
+def test_nccl_one_rank_engine_matches_plain_run(exchange, overlap):
+    """A one-rank RCCL process group (ONI_DIST_FORCE_GROUP=1) drives the engine's distributed path on
+    the one-GPU box: init_process_group(device_id), the start-up self-check (all_reduce,
+    barrier(device_ids), all_to_all_single), the E-step graph -> fp64 all-reduce of
+    [likelihood, alpha_ss, class_total] -> (dense class_word all-reduce | sparse VocabExchange
+    all-to-all, async when overlapped) -> M-step graph.  A sum over one rank is the identity, so the
+    trajectory equals the plain single-process run."""
+    one = _run(1, "auto")
+    r = subprocess.run([sys.executable, "scripts/dist_check.py"], cwd=ROOT, capture_output=True, text=True,
+                       timeout=300, env=_nccl_env(ONI_DIST_EXCHANGE=exchange, ONI_DIST_OVERLAP=overlap))
+    assert r.returncode == 0, r.stderr[-4000:]
+    o = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    assert o["world"] == 1
+    assert o["exchange"] == ("dense-allreduce" if exchange == "dense" else "sparse-alltoall")
+    assert o["likelihoods"] == one["likelihoods"]
+    assert o["alpha"] == one["alpha"] and o["beta_checksum"] == one["beta_checksum"]
+    assert o["gamma_sum"] == one["gamma_sum"]
+
+
+def test_nccl_one_rank_sharded_pipeline_bytes_equal_single_process(tmp_path):
+    """The row-sharded ml_ops pipeline (pipeline/sharded.py) over a one-rank RCCL group -- every
+    shardio collective (all_gather, all_to_all_single, broadcast, barriers) on device buffers --
+    writes byte for byte the files of the single-process pipeline."""
+    from oni_ml_amd.synth.flow import generate_flow_day
+    generate_flow_day(str(tmp_path / "in") + "/", events=200_000, seed=5)
+    files = ["words.dat", "doc.dat", "model.dat", "final.beta", "final.gamma", "likelihood.dat", "doc_results.csv",
+             "word_results.csv", "flow_results.csv", "word-assignments.dat"]
+    outs = {}
+    for mode in ("plain", "rccl"):
+        lp = tmp_path / mode
+        cmd = [sys.executable, "-m", "oni_ml_amd.cli", "ml_ops", "20160122", "flow", "1e-5", "--lpath", str(lp),
+               "--flow-path", str(tmp_path / "in"), "--conf", "/nonexistent", "--quiet"]
+        env = _nccl_env() if mode == "rccl" else dict(os.environ)
+        r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=300, env=env)
+        assert r.returncode == 0, r.stderr[-4000:]
+        outs[mode] = json.load(open(lp / "run_summary.json"))
+    assert outs["plain"]["scored"] == outs["rccl"]["scored"] > 0
+    recs = [json.loads(l) for l in (tmp_path / "rccl" / "metrics.jsonl").read_text().splitlines()]
+    assert any(x.get("stage") == "lda" and x.get("exchange") == "dense-allreduce" for x in recs)
+    for f in files:
+        assert (tmp_path / "plain" / f).read_bytes() == (tmp_path / "rccl" / f).read_bytes(), f

@@ -96,30 +96,45 @@ def test_bench_smoke():
 
 
 def test_lda_inf_hip_matches_references():
-    """`lda inf` (held-out documents under a fixed model) on the GPU engine: equal to the fp64 Jacobi
-    engine run for the same number of variational iterations, and to the literal lda-c Gauss-Seidel
-    engine (C++) up to the different sweep order, at the corpus-likelihood level."""
+    """`lda inf` (held-out documents under a fixed model) on the GPU engine: the fp64 engine against the
+    C++ engine with the same schedule (32 refreshes per sweep), and against literal lda-c at the
+    corpus-likelihood level."""
     from oni_ml_amd.models.lda.inference import infer
     from oni_ml_amd.models.lda.settings import LDASettings
-    from oni_ml_amd.synth.corpus import planted_corpus
-    c = planted_corpus(num_docs=400, num_terms=300, num_topics=6, mean_tokens=40, seed=11)
-    rng = np.random.default_rng(2)
-    b = rng.random((12, 300)) ** 3 + 1e-3
-    lb = np.log(b / b.sum(1, keepdims=True))
-    fixed = LDASettings(var_max_iter=30, var_converged=-1e30)       # exactly 30 Jacobi sweeps
-    g_hip, l_hip = infer(c, lb, 0.8, fixed, backend="hip", device="cuda", precision="fp32")
-    g_ref, l_ref = infer(c, lb, 0.8, fixed, backend="torch", device="cpu")
-    assert g_hip.shape == g_ref.shape == (400, 12)
-    assert np.allclose(g_hip, g_ref, rtol=2e-3, atol=1e-4), np.abs(g_hip - g_ref).max()
-    assert np.allclose(l_hip, l_ref, rtol=1e-5)
+    c, lb = _inf_case()
     ldac = LDASettings()                                             # lda-c defaults: 20 sweeps, 1e-6
-    _, l_gpu = infer(c, lb, 0.8, ldac, backend="hip", device="cuda", precision="fp32")
-    _, l_cpu = infer(c, lb, 0.8, ldac, backend="cpu")
-    assert abs(l_gpu.sum() - l_cpu.sum()) / abs(l_cpu.sum()) < 1e-4
-    # the fp64 engine against the C++ engine with the same schedule (32 refreshes per sweep)
     g64, l64 = infer(c, lb, 0.8, ldac, backend="hip", device="cuda")
     ldac32 = LDASettings()
     ldac32.gs_updates = 32
     g32, l32 = infer(c, lb, 0.8, ldac32, backend="cpu")
     assert np.allclose(l64, l32, rtol=1e-10, atol=1e-9)
     assert np.allclose(g64, g32, rtol=1e-10, atol=1e-12)
+    _, l_cpu = infer(c, lb, 0.8, ldac, backend="cpu")
+    assert abs(l64.sum() - l_cpu.sum()) / abs(l_cpu.sum()) < 1e-4
+
+
+def _inf_case():
+    from oni_ml_amd.synth.corpus import planted_corpus
+    c = planted_corpus(num_docs=400, num_terms=300, num_topics=6, mean_tokens=40, seed=11)
+    rng = np.random.default_rng(2)
+    b = rng.random((12, 300)) ** 3 + 1e-3
+    return c, np.log(b / b.sum(1, keepdims=True))
+
+
+@pytest.mark.experimental
+def test_lda_inf_fp32_engine_matches_references():
+    """`lda inf` on the experimental fp32 Jacobi engine: the fp64 Jacobi engine run for the same number
+    of variational iterations, and literal lda-c at the corpus-likelihood level."""
+    from oni_ml_amd.models.lda.inference import infer
+    from oni_ml_amd.models.lda.settings import LDASettings
+    c, lb = _inf_case()
+    fixed = LDASettings(var_max_iter=30, var_converged=-1e30)       # exactly 30 Jacobi sweeps
+    g_hip, l_hip = infer(c, lb, 0.8, fixed, backend="hip", device="cuda", precision="fp32")
+    g_ref, l_ref = infer(c, lb, 0.8, fixed, backend="torch", device="cpu")
+    assert g_hip.shape == g_ref.shape == (400, 12)
+    assert np.allclose(g_hip, g_ref, rtol=2e-3, atol=1e-4), np.abs(g_hip - g_ref).max()
+    assert np.allclose(l_hip, l_ref, rtol=1e-5)
+    ldac = LDASettings()
+    _, l_gpu = infer(c, lb, 0.8, ldac, backend="hip", device="cuda", precision="fp32")
+    _, l_cpu = infer(c, lb, 0.8, ldac, backend="cpu")
+    assert abs(l_gpu.sum() - l_cpu.sum()) / abs(l_cpu.sum()) < 1e-4

@@ -268,3 +268,25 @@ def test_device_random_init_matches_native():
     assert np.array_equal(eng.cw[:, :20].cpu().numpy(), ref.T)
     assert eng.cw[:, 20:].abs().max().item() == 0 if eng.KS > 20 else True
     assert _rel(eng.class_total[:20].cpu().numpy(), ref.sum(1), 1e-30) < 1e-14
+
+
+@pytest.mark.parametrize("vconv", [-1e30, 1e-6])
+def test_final_pass_word_assignments_match_oracle(vconv):
+    """word-assignments.dat: run_em's final pass -- a fresh E-step under the final model, then the first
+    argmax of each word's phi -- on the GPU (c.phi rows of the document kernels alone) against the C++
+    oracle's lda_inference + write_word_assignment with the same schedule."""
+    c = _edge_corpus(seed=13, max_len=3000)
+    K, U, alpha = 20, 32, 0.6
+    lb = _log_beta(c.num_terms, K, seed=7)
+    st = LDASettings(var_max_iter=8, var_converged=vconv)
+    st.gs_updates = U
+    eng = LDAEngine(c, K, st, backend="hip", seed=0, precision="fp64")
+    eng.init_from_model(lb, alpha)
+    z = eng.word_assignments()
+    ref = native.lib().lda_assign_ldac(c.doc_ptr, c.word_idx, c.counts.astype(np.float64), np.ascontiguousarray(lb),
+                                       alpha, st.var_max_iter, st.var_converged, gs_updates=U)
+    if vconv < 0:
+        assert np.array_equal(z, ref)
+    else:
+        # documents whose convergence test sits within rounding of 1e-6 may stop a sweep apart
+        assert (z == ref).mean() > 0.999

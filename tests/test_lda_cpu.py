@@ -189,3 +189,29 @@ def test_random_ss_counter_generator():
     assert not np.array_equal(a, N.random_ss(5, 1000, 8))
     u = a - 1.0 / 1000
     assert u.min() >= 0.0 and u.max() < 1.0 and abs(u.mean() - 0.5) < 0.02
+
+
+def test_word_assignments_final_pass_cpu_backends():
+    """The final-pass assignments of the C++ oracle equal an explicit per-document argmax of the phi it
+    leaves (lda-c's literal schedule), and the torch backend's Jacobi form assigns every entry."""
+    import numpy as np
+    from oni_ml_amd.models.lda.em import LDAEngine
+    from oni_ml_amd.models.lda.settings import LDASettings
+    from oni_ml_amd.ops import native
+    from oni_ml_amd.synth.corpus import planted_corpus
+    c = planted_corpus(num_docs=150, num_terms=200, num_topics=4, seed=2)
+    eng = LDAEngine(c, 6, LDASettings(em_max_iter=3), backend="cpu", seed=1)
+    eng.run()
+    z = eng.word_assignments()
+    assert z.shape == (c.nnz,) and z.min() >= 0 and z.max() < 6
+    lb = np.log(np.maximum(eng.beta.numpy().T, 1e-300))
+    # literal lda_inference for one document, then argmax phi: phi_nk ~ exp(dig_k + lb_kw), dig of the
+    # gamma after the word's own update -- recompute through the oracle's E-step on that document alone
+    z1 = native.lib().lda_assign_ldac(c.doc_ptr[:2] - 0, c.word_idx[:c.doc_ptr[1]], c.counts[:c.doc_ptr[1]].astype(float),
+                                      np.ascontiguousarray(lb), eng.alpha, eng.var_max_iter,
+                                      eng.settings.var_converged)
+    assert np.array_equal(z1, z[:c.doc_ptr[1]])
+    t = LDAEngine(c, 6, LDASettings(em_max_iter=3), backend="torch", device="cpu", seed=1)
+    t.run()
+    zt = t.word_assignments()
+    assert zt.shape == (c.nnz,) and zt.min() >= 0 and zt.max() < 6

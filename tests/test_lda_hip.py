@@ -1,4 +1,9 @@
-"""Numerics of the gfx950 LDA kernels against the float64 PyTorch reference."""
+"""Numerics of the gfx950 LDA kernels against the float64 PyTorch reference.
+
+Most tests here cover the fp32 Jacobi engine (``--precision fp32``, lda_estep*.hip), an opt-in fast
+mode with a documented model bias against lda-c (profiles/r2_precision_parity.md): they are marked
+``experimental`` and run only with ONI_EXPERIMENTAL=1.  The kernels the fp64 product path shares
+(scoring, the alpha Newton, the device EM loop control) are tested unconditionally."""
 import math
 
 import numpy as np
@@ -33,6 +38,7 @@ def _random_beta(V, K, KS, seed=0, dev="cuda"):
 @pytest.mark.parametrize("K,vconv,wide", [(20, -1e30, None), (7, -1e30, None), (50, -1e30, None), (100, -1e30, None),
                                           (20, 1e-6, None), (30, -1e30, "1"), (30, -1e30, "0"), (64, -1e30, None),
                                           (128, -1e30, None), (100, 1e-6, None), (50, -1e30, "0")])
+@pytest.mark.experimental
 def test_estep_matches_reference(hip, K, vconv, wide, monkeypatch):
     """Every length bucket of the narrow (K <= 32) and wide-topic (K > 32, lda_estep_wide.hip)
     E-step kernels against the fp64 Jacobi oracle; ``wide`` forces a layout (ONI_ESTEP_WIDE)."""
@@ -87,6 +93,7 @@ def test_estep_matches_reference(hip, K, vconv, wide, monkeypatch):
         assert rrel < 2e-3, rrel
 
 
+@pytest.mark.experimental
 def test_suffstats_and_mstep(hip):
     c = _corpus_with_long_docs(seed=5)
     K = 20
@@ -124,6 +131,7 @@ def test_suffstats_and_mstep(hip):
         assert b2[:, K:].abs().max().item() == 0
 
 
+@pytest.mark.experimental
 @pytest.mark.parametrize("K,wide", [(20, False), (30, True), (50, True), (100, True), (128, True)])
 def test_suffstats_fused_and_partial_colsums(hip, K, wide):
     """Single-launch suff-stats (heavy / medium / light words, empty words included) against the
@@ -213,6 +221,7 @@ def test_device_convergence_matches_host_loop():
     assert not (L1[-1][1] > 2e-4 or L1[-1][1] < 0)
 
 
+@pytest.mark.experimental
 def test_em_hip_tracks_torch_reference():
     c = planted_corpus(num_docs=2000, num_terms=600, num_topics=8, seed=11)
     st = LDASettings(em_max_iter=8)
@@ -246,6 +255,7 @@ def test_score_kernel_bitwise(hip):
         assert torch.equal(a.cpu(), b), "scores must match the sequential f64 reference bit for bit"
 
 
+@pytest.mark.experimental
 @pytest.mark.parametrize("K", [20, 50, 100])
 def test_split_documents_match_single_workgroup(hip, K):  # K = 50, 100: wide-topic split kernel
     """Huge documents split across workgroups (per-iteration cross-workgroup reduction) give the
@@ -276,6 +286,7 @@ def test_split_documents_match_single_workgroup(hip, K):  # K = 50, 100: wide-to
     assert ((g1 - ref["gamma"]).abs() / ref["gamma"].abs().clamp_min(1e-3)).max().item() < 2e-3
 
 
+@pytest.mark.experimental
 @pytest.mark.parametrize("K", [3, 13, 24, 33, 77, 128])
 def test_estep_random_corpora_edge_cases(hip, K):
     """Randomised corpora with the shapes real featurization produces: empty documents, duplicate
@@ -340,6 +351,7 @@ def test_alpha_newton_device_matches_host(K):
         assert float(params[1].item()) == pytest.approx(special.lik_const(a, K), rel=1e-9, abs=1e-9)
 
 
+@pytest.mark.experimental
 def test_split_launch_cap_from_occupancy(hip, monkeypatch):
     """Split launches are sized from the occupancy API (co-residency of every segment of a launch);
     a forced small cap (ONI_SPLIT_MAX_BLOCKS) re-batches the huge documents and gives the same E-step."""

@@ -57,6 +57,7 @@ def test_fp64_hip_engine_tracks_block_oracle(tmp_path):
 
 
 @pytest.mark.gpu
+@pytest.mark.experimental
 def test_fp32_hip_engine_tracks_fp64_jacobi(tmp_path):
     p = _run(tmp_path, "hip32,torch", 50000)["pairs"]["hip32 vs torch"]
     assert p["likelihood_rel_diff_max"] < 1e-5
