@@ -1272,6 +1272,340 @@ __global__ __launch_bounds__(512) void gs_split(GSArgs a, SplitArgs sp) {
   }
 }
 
+// ------------------------------------------------------------ split, v2 ----
+// gs_split with the exchange in a dedicated topic wave (7 word waves + 1 topic wave): the word
+// waves leave their chunk partials in LDS, signal an LDS arrival counter and issue the NEXT chunk's
+// row prefetch at once; the topic wave sums the waves, publishes the segment's tagged granules,
+// sweeps the document's G segments and runs the refresh.  Its poll loads never queue behind row
+// prefetches (vmcnt is in order per wave, and the hand-off price sits in the consumer's memory
+// queue -- MI355X_MICROARCH handoff-1to1 / gather-pass), and a chunk costs one workgroup barrier
+// instead of three.  Same exchange buffer, tags, epoch and co-residency rules as gs_split.
+template <int KS>
+__global__ __launch_bounds__(512) void gs_splitw(GSArgs a, SplitArgs sp) {
+  using T = TeamShape<KS, 8>;   // word-slot geometry and prefetch depth of the 8-wave team
+  constexpr int NW = 7, NTD = (NW + 1) * 64, TG = T::TG, KPL = T::KPL, NSW = T::NSW, LSW = T::LSW, NS = NW * NSW,
+                RMAX = T::RMAX;
+  constexpr int NC = KS + 1;                 // exchanged columns: KS topic sums + the log-sum
+  constexpr int GR = 2 * NC;                 // granules per segment row
+  constexpr int TC = (NC + 63) / 64;         // columns per topic-wave lane
+  __shared__ double sC[kGsUMax][KS];
+  __shared__ double sEt[kGsUMax][KS];
+  __shared__ double sE[KS];
+  __shared__ double sRed[NW][KS];
+  __shared__ double sRedL[NW];
+  __shared__ double sCs[kGsUMax];
+  __shared__ double sScal[4];
+  __shared__ int arrive;
+  __shared__ int sFail;
+  if (a.params[kParamDone] != 0.0) return;
+  const int t = threadIdx.x, b = blockIdx.x;
+  const int d = sp.seg_doc[b], g = sp.seg_index[b], G = sp.seg_count[b], base = sp.seg_base[b];
+  int* counter = sp.counter + sp.doc_slot[b];
+  const int epoch = __hip_atomic_load(counter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const double alpha = a.params[0], lik_const = a.params[1];
+  const int vmi = (int)a.params[2];
+  const double vconv = params_vconv(a.params);
+  const int K = a.K;
+  const int lane = t & 63, wv = t >> 6;
+  const bool topic_wave = wv == NW;
+  const int q = lane >> LSW, sl = lane & (NSW - 1);
+  const int slot = wv * NSW + sl;
+  const int s0 = a.doc_ptr[d], n = a.doc_ptr[d + 1] - s0;   // n > 0 (host)
+  const int U = a.gs_updates;
+  const int W = (n + U - 1) / U;
+  const int nch = (n + W - 1) / W;
+  const int WG = (W + G - 1) / G;             // words of a chunk per segment
+  const int nact = min(NW, (WG + NSW - 1) / NSW);
+  const bool active = wv < nact;              // never the topic wave
+  const int* __restrict__ wrow = a.word_idx + s0;
+  const float* __restrict__ crow = a.counts + s0;
+  auto range = [&](int j, int& m0, int& m1) {
+    const int n1 = min(n, (j + 1) * W);
+    m0 = min(n1, j * W + g * WG);
+    m1 = min(n1, m0 + WG);
+  };
+  for (int j = t; j < nch; j += NTD) sCs[j] = 0.0;
+  if (t == 0) {
+    sFail = 0;
+    arrive = 0;
+  }
+  lds_barrier();
+  for (int p = t; p < n; p += NTD) atomicAdd(&sCs[p / W], (double)crow[p]);   // integer counts: exact
+  lds_barrier();
+  double total = 0.0;
+  for (int j = 0; j < nch; ++j) total += sCs[j];
+  const double g0 = alpha + total / K;
+  const double m = psi_only(g0);
+  const bool twt = a.dbg != nullptr && b == 0 && t == NW * 64;   // topic-wave timer lane
+  const bool wwt = a.dbg != nullptr && b == 0 && t == 0;         // word-wave timer lane
+  long long ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  long long tc = (twt || wwt) ? clock64() : 0;
+  auto tick = [&](int i) {
+    if (twt || wwt) {
+      const long long x = clock64();
+      ph[i] += x - tc;
+      tc = x;
+    }
+  };
+  double L = 0.0, L_old = 0.0, conv = 1.0, GS = 0.0;
+  int it = 0;
+  bool failed = false;
+  auto sweep_end = [&]() {
+    lds_barrier();
+    GS = sScal[1];
+    L = lik_const - lgamma_pos(GS) + sScal[2] + fma(m, total, sScal[0]) - sScal[3];
+    conv = (L_old - L) / L_old;
+    L_old = L;
+    lds_barrier();
+  };
+  if (topic_wave) {
+    // ------------------------------------------------------------ topic wave
+    __builtin_amdgcn_s_setprio(3);   // its chain is the critical path; the word waves wait on it
+    double gam[TC], psi[TC], lps[TC];
+#pragma unroll
+    for (int o = 0; o < TC; ++o) {
+      const int k = lane + 64 * o;
+      gam[o] = k < K ? g0 : 0.0;
+      psi[o] = m;
+      lps[o] = 0.0;
+      if (k < KS) {
+        sE[k] = k < K ? 1.0 : 0.0;
+        for (int j = 0; j < nch; ++j) sC[j][k] = k < K ? sCs[j] / K : 0.0;
+      }
+    }
+    double LWs = 0.0;
+    int want = 0;
+    lds_barrier();   // (1)
+    while (!failed && var_continue(conv, vconv, it, vmi)) {
+      ++it;
+#pragma unroll
+      for (int o = 0; o < TC; ++o) lps[o] = 0.0;
+      for (int j = 0; j < nch; ++j) {
+        ph[7] += twt ? 1 : 0;
+        want += nact;
+        while (__hip_atomic_load(&arrive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < want)
+          __builtin_amdgcn_s_sleep(1);
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+        tick(3);
+        const int seq = (it - 1) * nch + j + 1;
+        const unsigned tag = split_tag(epoch, seq);
+        unsigned long long* xb = sp.xchg + (size_t)(seq & 1) * sp.n_blocks * GR;
+        // publish this segment's column sums (waves in order), then sweep the G segments
+#pragma unroll
+        for (int o = 0; o < TC; ++o) {
+          const int c = lane + 64 * o;
+          if (c < NC) {
+            double part = 0.0;
+#pragma unroll
+            for (int v = 0; v < NW; ++v) part += v < nact ? (c < KS ? sRed[v][c] : sRedL[v]) : 0.0;
+            const unsigned long long bits = (unsigned long long)__double_as_longlong(part);
+            unsigned long long* row = xb + (size_t)b * GR + 2 * c;
+            put_tagged_bits(row, (unsigned)(bits & 0xffffffffull), tag);
+            put_tagged_bits(row + 1, (unsigned)(bits >> 32), tag);
+          }
+        }
+        double tot[TC];
+        bool ok = true;
+#pragma unroll
+        for (int o = 0; o < TC; ++o) {
+          const int c = lane + 64 * o;
+          tot[o] = 0.0;
+          if (c < NC) ok &= tagged_sum_f64(xb + (size_t)base * GR + 2 * c, G, GR, tag, tot[o]);
+        }
+        tick(4);
+        if (!ok) {
+          sFail = 1;
+          __hip_atomic_store(sp.error, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+#pragma unroll
+        for (int o = 0; o < TC; ++o) {
+          const int k = lane + 64 * o;
+          if (k < KS) {
+            const double Eo = sE[k];
+            const double nw = Eo * tot[o];
+            double En = 0.0;
+            if (k < K) {
+              lps[o] = fma(psi[o], nw, lps[o]);
+              gam[o] += nw - sC[j][k];
+              psi_exp(gam[o], m, psi[o], En);
+            }
+            sC[j][k] = nw;
+            sEt[j][k] = Eo;
+            sE[k] = En;
+          } else if (k == KS) {
+            LWs += tot[o];
+          }
+        }
+        tick(5);
+        lds_barrier();   // (B) E of chunk j + 1 published
+        if (sFail) {
+          failed = true;
+          break;
+        }
+      }
+      if (failed) break;
+      double gs = 0.0, lg = 0.0, lp = 0.0, lw = 0.0;
+#pragma unroll
+      for (int o = 0; o < TC; ++o) {
+        const int k = lane + 64 * o;
+        if (k < K) {
+          gs += gam[o];
+          lg += lgamma_pos(gam[o]);
+          lp += lps[o];
+        }
+        if (k == KS) lw = LWs;
+      }
+      LWs = 0.0;
+      const double w1 = group_sum<64>(gs), w2 = group_sum<64>(lg), w3 = group_sum<64>(lp), w0 = group_sum<64>(lw);
+      if (lane == 0) {
+        sScal[0] = w0;
+        sScal[1] = w1;
+        sScal[2] = w2;
+        sScal[3] = w3;
+      }
+      sweep_end();
+      tick(6);
+    }
+    if (twt)
+      for (int i = 3; i < 8; ++i) a.dbg[i] = ph[i];
+    split_exit(counter, sp.n_docs, G);   // thread 0 only: a no-op here (kept beside the word waves' call)
+    double ps = 0.0;
+#pragma unroll
+    for (int o = 0; o < TC; ++o) {
+      const int k = lane + 64 * o;
+      if (k < K) ps += psi[o];
+      if (g == 0 && k < KS) a.gamma[(size_t)d * KS + k] = gam[o];
+    }
+    ps = group_sum<64>(ps);
+    if (g == 0 && lane == 0) {
+      a.lik[d] = failed ? __builtin_nan("") : L;   // a timed-out exchange surfaces as a NaN likelihood
+      a.alpha_ss[d] = ps - K * psi_only(GS);
+      a.iters[d] = it;
+    }
+    return;
+  }
+  // -------------------------------------------------------------- word waves
+  int wc[RMAX], wn[RMAX];
+  float cc[RMAX], cn[RMAX];
+  unsigned vc = 0, vn = 0;
+  double bc[RMAX][KPL];
+  auto load_ids = [&](int j, int (&w)[RMAX], float (&c)[RMAX], unsigned& v) {
+    int m0, m1;
+    range(j, m0, m1);
+    v = 0;
+#pragma unroll
+    for (int r = 0; r < RMAX; ++r) {
+      const int p = m0 + slot + r * NS;
+      v |= (active && p < m1) ? (1u << r) : 0u;
+      const int pc = max(0, min(p, m1 - 1));
+      w[r] = wrow[pc];
+      c[r] = crow[pc];
+    }
+  };
+  auto load_rows = [&](const int (&w)[RMAX], unsigned v) {
+    if (!active) return;
+#pragma unroll
+    for (int r = 0; r < RMAX; ++r) {
+      const double* brow = a.beta + (size_t)w[r] * KS;
+#pragma unroll
+      for (int i = 0; i < KPL; ++i) bc[r][i] = ((v >> r) & 1u) ? brow[min(q + TG * i, KS - 1)] : 0.0;
+    }
+  };
+  load_ids(0, wc, cc, vc);
+  load_rows(wc, vc);
+  load_ids(nch > 1 ? 1 : 0, wn, cn, vn);
+  lds_barrier();   // (1)
+  while (!failed && var_continue(conv, vconv, it, vmi)) {
+    ++it;
+    for (int j = 0; j < nch; ++j) {
+      if (active) {
+        int m0, m1;
+        range(j, m0, m1);
+        double E[KPL], acc[KPL], lw = 0.0;
+#pragma unroll
+        for (int i = 0; i < KPL; ++i) {
+          E[i] = (q + TG * i < KS) ? sE[q + TG * i] : 0.0;
+          acc[i] = 0.0;
+        }
+        double cr[RMAX];
+#pragma unroll
+        for (int r = 0; r < RMAX; ++r) cr[r] = ((vc >> r) & 1u) ? (double)cc[r] : 0.0;
+        const int R = (m1 - m0 + NS - 1) / NS;
+        if (R <= 1) {
+          word_steps<1, KPL, LSW>(E, bc, cr, acc, lw);
+        } else if (R <= 2 || RMAX <= 2) {
+          word_steps<(RMAX < 2 ? RMAX : 2), KPL, LSW>(E, bc, cr, acc, lw);
+        } else if (R <= 4 || RMAX <= 4) {
+          word_steps<(RMAX < 4 ? RMAX : 4), KPL, LSW>(E, bc, cr, acc, lw);
+        } else {
+          word_steps<RMAX, KPL, LSW>(E, bc, cr, acc, lw);
+        }
+        stream_tail<RMAX, KS, KPL, TG, LSW>(a.beta, wrow, crow, m0 + slot + RMAX * NS, m1, NS, q, E, bc, acc, lw);
+#pragma unroll
+        for (int i = 0; i < KPL; ++i) acc[i] = bits_sum<0, LSW, false>(acc[i]);
+        lw = group_sum<64>(q == 0 ? lw : 0.0);
+        if (sl == 0) {
+#pragma unroll
+          for (int i = 0; i < KPL; ++i)
+            if (q + TG * i < KS) sRed[wv][q + TG * i] = acc[i];
+        }
+        if (lane == 0) sRedL[wv] = lw;
+        // arrival (LDS only: no vmcnt wait), then the next chunk's rows -- beside the exchange
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+        if (lane == 0) __hip_atomic_fetch_add(&arrive, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        tick(0);
+        const int j1 = j + 1 < nch ? j + 1 : 0;
+        const int j2 = j1 + 1 < nch ? j1 + 1 : 0;
+#pragma unroll
+        for (int r = 0; r < RMAX; ++r) {
+          wc[r] = wn[r];
+          cc[r] = cn[r];
+        }
+        vc = vn;
+        load_rows(wc, vc);
+        load_ids(j2, wn, cn, vn);
+        tick(1);
+      }
+      lds_barrier();   // (B)
+      tick(2);
+      if (sFail) {
+        failed = true;
+        break;
+      }
+    }
+    if (failed) break;
+    sweep_end();
+  }
+  if (wwt)
+    for (int i = 0; i < 3; ++i) a.dbg[i] = ph[i];
+  // every thread of this workgroup is past its last exchange (the loops end on a barrier)
+  split_exit(counter, sp.n_docs, G);
+  // final pass over this segment's ranges: c_n phi_nk = E_jk b_nk r_n with the final sweep's chunk E
+  if (!active) return;
+  for (int j = 0; j < nch; ++j) {
+    int m0, m1;
+    range(j, m0, m1);
+    double E[KPL];
+#pragma unroll
+    for (int i = 0; i < KPL; ++i) E[i] = (q + TG * i < KS) ? sEt[j][q + TG * i] : 0.0;
+    for (int p = m0 + slot; p < m1; p += NS) {
+      const double* brow = a.beta + (size_t)wrow[p] * KS;
+      const double c = (double)crow[p];
+      double bv[KPL];
+#pragma unroll
+      for (int i = 0; i < KPL; ++i) bv[i] = (q + TG * i < KS) ? brow[q + TG * i] : 0.0;
+      double pp = 0.0;
+#pragma unroll
+      for (int i = 0; i < KPL; ++i) pp = fma(E[i], bv[i], pp);
+      const double r = c * drcp(bits_sum<LSW, 6>(pp));
+      double* row = a.cphi + (size_t)(s0 + p) * KS;
+#pragma unroll
+      for (int i = 0; i < KPL; ++i)
+        if (q + TG * i < KS) __builtin_nontemporal_store(E[i] * bv[i] * r, &row[q + TG * i]);
+    }
+  }
+}
+
 // ------------------------------------------------------------- word team ----
 // Word-per-lane team kernel for KS <= 32: every lane owns whole words (all KS topics in
 // registers), so a word costs 2 KS FMAs, one reciprocal and one log per LANE instead of per
@@ -2170,14 +2504,24 @@ int gs_tiny_max(int KS) {
   }
 }
 
+// gs_split variant: 2 = gs_splitw (exchange in a topic wave, the default), 1 = gs_split (ONI_GS_SPLIT_V)
+static int gs_split_variant() {
+  static const int v = std::getenv("ONI_GS_SPLIT_V") ? std::atoi(std::getenv("ONI_GS_SPLIT_V")) : 2;
+  return v;
+}
+
 template <int KS>
 static int gs_split_capacity_ks() {
   int dev = 0, per_cu = 0;
   hipDeviceProp_t p;
   ONI_HIP_CHECK(hipGetDevice(&dev));
   ONI_HIP_CHECK(hipGetDeviceProperties(&p, dev));
-  ONI_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(&gs::gs_split<KS>),
-                                                             512, 0));
+  if (gs_split_variant() == 2)
+    ONI_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(
+        &per_cu, reinterpret_cast<const void*>(&gs::gs_splitw<KS>), 512, 0));
+  else
+    ONI_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(
+        &per_cu, reinterpret_cast<const void*>(&gs::gs_split<KS>), 512, 0));
   return per_cu * p.multiProcessorCount;
 }
 
@@ -2199,9 +2543,12 @@ void launch_gs_split(const GSArgs& a, const SplitArgs& s, int KS, hipStream_t st
     throw std::runtime_error("gs_split: gs_updates must be in [1, " + std::to_string(kGsUMax) + "]");
   if (!a.params) throw std::runtime_error("gs_split: params block required");
   switch (KS) {
-#define ONI_KS(X)                                                                       \
-  case X:                                                                               \
-    hipLaunchKernelGGL((gs::gs_split<X>), dim3(s.n_blocks), dim3(512), 0, st, a, s);    \
+#define ONI_KS(X)                                                                         \
+  case X:                                                                                 \
+    if (gs_split_variant() == 2)                                                          \
+      hipLaunchKernelGGL((gs::gs_splitw<X>), dim3(s.n_blocks), dim3(512), 0, st, a, s);   \
+    else                                                                                  \
+      hipLaunchKernelGGL((gs::gs_split<X>), dim3(s.n_blocks), dim3(512), 0, st, a, s);    \
     break;
     ONI_FOR_EACH_KS(ONI_KS)
 #undef ONI_KS

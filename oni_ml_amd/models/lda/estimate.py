@@ -137,8 +137,16 @@ def estimate(corpus: Corpus, num_topics: int, alpha_init: float, settings: LDASe
     r = 0 if dist is None else dist.rank
     if rank0:
         os.makedirs(outdir, exist_ok=True)
+
+    def _now():
+        if torch.cuda.is_available() and device is not None and torch.device(device).type == "cuda":
+            torch.cuda.synchronize()
+        return time.perf_counter()
+
+    t_start = _now()
     eng = LDAEngine(corpus, num_topics, settings, alpha_init=alpha_init, backend=backend, device=device, dist=dist,
                     seed=seed, local_shard=local_shard, doc_offset=doc_offset)
+    timing = dict(setup_s=round(_now() - t_start, 4))
     parts = []          # (final file, this rank's part file): concatenated at close
     start_it, L_old, hist = 0, 0.0, []
     ck = load_checkpoint(outdir) if resume else None
@@ -228,16 +236,21 @@ def estimate(corpus: Corpus, num_topics: int, alpha_init: float, settings: LDASe
     finally:
         if not (ok and defer_files):
             writer.close()
+    timing["em_s"] = round(res.seconds, 4)
+    t_out = _now()
     res.likelihoods = history
     res.log_beta = eng.log_beta()
     res.gamma = eng.local_gamma()          # this rank's documents (all of them with one rank)
     res.doc_range = eng.doc_range
+    timing["model_copies_s"] = round(_now() - t_out, 4)
     if write_word_assignments:
         # run_em's final pass: a fresh E-step under the final model (after gamma and beta were read),
         # the argmax of each word's phi; native formatting on the background writer with the deferred
         # model files when allowed (the caller's next stages do not wait for it)
         wa, shard = os.path.join(outdir, "word-assignments.dat"), eng.corpus
+        t_wa = _now()
         z = eng.word_assignments()
+        timing["final_pass_s"] = round(_now() - t_wa, 4)
         if multi:
             part = os.path.join(outdir, f".word-assignments.dat.part{r}")
             parts.append((wa, part))
@@ -253,12 +266,14 @@ def estimate(corpus: Corpus, num_topics: int, alpha_init: float, settings: LDASe
     if not defer_files:
         concat_parts()
     res.close_files = close_files if defer_files else (lambda: None)
+    timing["total_s"] = round(_now() - t_start, 4)
+    res.timing = timing
     nnz = dist.allreduce_int(eng.corpus.nnz) if multi else eng.corpus.nnz
     if rank0:
         with open(os.path.join(outdir, "lda_stats.json"), "w") as f:
             json.dump(dict(em_iterations=res.em_iterations, seconds=res.seconds, alpha=res.alpha,
                            backend=eng.backend, docs=eng.global_docs, terms=eng.V, nnz=nnz, ranks=dist.world_size
-                           if multi else 1, metrics=eng.metrics(res.seconds, res.em_iterations),
+                           if multi else 1, timing=timing, metrics=eng.metrics(res.seconds, res.em_iterations),
                            per_iter=[s.__dict__ for s in res.stats]), f)
     res.engine = eng
     return res

@@ -75,6 +75,7 @@ def run(cfg, dist=None, device=None, log=print) -> dict:
         with R.stage("lda") as res:
             lres = C.run_lda(cfg, corpus, dist=dist, device=device, log=log)
             res["_defer"] = lres.close_files   # LAG / final model files: written while later stages run
+            res.update(getattr(lres, "timing", {}))
             res.update(em_iterations=lres.em_iterations, alpha=lres.alpha)
             m = lres.engine.metrics(lres.seconds, lres.em_iterations)
             res.update({k: v for k, v in m.items() if not isinstance(v, list)})

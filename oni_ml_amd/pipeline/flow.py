@@ -89,6 +89,7 @@ def run(cfg, dist=None, device=None, log=print) -> dict:
         with R.stage("lda") as res:
             lres = C.run_lda(cfg, corpus, dist=dist, device=device, log=log)
             res["_defer"] = lres.close_files   # LAG / final model files: written while later stages run
+            res.update(getattr(lres, "timing", {}))
             res.update(em_iterations=lres.em_iterations, likelihood=lres.likelihoods[-1][0] if lres.likelihoods else 0.0,
                        alpha=lres.alpha)
             m = lres.engine.metrics(lres.seconds, lres.em_iterations)

@@ -75,6 +75,7 @@ def _lda_stage(R, cfg, ctx, corpus, device, log, summary, local_shard, doc_offse
         lres = C.run_lda(cfg, corpus, dist=ctx, device=device, log=log, local_shard=local_shard,
                          doc_offset=doc_offset)
         res["_defer"] = lres.close_files   # LAG / final model files: written while later stages run
+        res.update(getattr(lres, "timing", {}))
         res.update(em_iterations=lres.em_iterations, likelihood=lres.likelihoods[-1][0] if lres.likelihoods else 0.0,
                    alpha=lres.alpha)
         m = lres.engine.metrics(lres.seconds, lres.em_iterations)
