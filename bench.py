@@ -100,7 +100,7 @@ def _e2e(args, dev):
         wall = time.perf_counter() - t0
         return dict(e2e_wall_s=round(wall, 3), e2e_synth_input_s=round(t_gen, 3),
                     e2e_stage_s={k: round(v, 3) for k, v in s["stage_seconds"].items()},
-                    e2e_em_iters=s["lda"]["em_iterations"], e2e_flagged=s.get("scored"), e2e_corpus=s.get("corpus"))
+                    e2e_em_iters=s["lda"]["em_iterations"], e2e_lda_timing=s["lda"].get("timing"), e2e_flagged=s.get("scored"), e2e_corpus=s.get("corpus"))
     finally:
         shutil.rmtree(tmp, ignore_errors=True)
 

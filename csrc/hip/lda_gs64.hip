@@ -961,6 +961,46 @@ __device__ __forceinline__ bool tagged_sum_f64(const unsigned long long* x, int 
   return true;
 }
 
+// tagged_sum_f64 with every granule of up to 16 segments in flight at once: one polling round trip
+// for G <= 16 (tagged_sum_f64 waits for each group of 4 segments before issuing the next group's
+// loads -- ceil(G / 4) dependent fabric round trips per chunk)
+__device__ __forceinline__ bool tagged_sum_f64_wide(const unsigned long long* x, int n, int stride, unsigned tag,
+                                                    double& out) {
+  constexpr int B = 16;
+  double s = 0.0;
+  long spins = 0;
+  for (int q0 = 0; q0 < n; q0 += B) {
+    unsigned long long v[2 * B];
+#pragma unroll
+    for (int u = 0; u < 2 * B; ++u)
+      v[u] = (q0 + u / 2 < n) ? __hip_atomic_load(x + (size_t)(q0 + u / 2) * stride + (u & 1), __ATOMIC_RELAXED,
+                                                  __HIP_MEMORY_SCOPE_AGENT)
+                              : ((unsigned long long)tag << 32);
+    for (;;) {
+      unsigned pending = 0;
+#pragma unroll
+      for (int u = 0; u < 2 * B; ++u) pending |= ((unsigned)(v[u] >> 32) != tag) ? (1u << u) : 0u;
+      if (pending == 0) break;
+      if (++spins > kSplitSpinLimit) {
+        out = __builtin_nan("");
+        return false;
+      }
+      __builtin_amdgcn_s_sleep(1);
+#pragma unroll
+      for (int u = 0; u < 2 * B; ++u)
+        if ((pending >> u) & 1u)
+          v[u] = __hip_atomic_load(x + (size_t)(q0 + u / 2) * stride + (u & 1), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+    }
+#pragma unroll
+    for (int u = 0; u < 2 * B; u += 2)
+      if (q0 + u / 2 < n)
+        s += __longlong_as_double((long long)(((v[u + 1] & 0xffffffffull) << 32) | (v[u] & 0xffffffffull)));
+  }
+  out = s;
+  return true;
+}
+
 template <int KS>
 __global__ __launch_bounds__(512) void gs_split(GSArgs a, SplitArgs sp) {
   using T = TeamShape<KS, 8>;
@@ -1410,7 +1450,7 @@ __global__ __launch_bounds__(512) void gs_splitw(GSArgs a, SplitArgs sp) {
         for (int o = 0; o < TC; ++o) {
           const int c = lane + 64 * o;
           tot[o] = 0.0;
-          if (c < NC) ok &= tagged_sum_f64(xb + (size_t)base * GR + 2 * c, G, GR, tag, tot[o]);
+          if (c < NC) ok &= tagged_sum_f64_wide(xb + (size_t)base * GR + 2 * c, G, GR, tag, tot[o]);
         }
         tick(4);
         if (!ok) {
@@ -2217,10 +2257,10 @@ template <int KS>
 __global__ __launch_bounds__(256) void gs_suff64(const int* __restrict__ word_ptr, const int* __restrict__ csc_ent,
                                                  const int* __restrict__ order, int n_heavy, int n_medium,
                                                  int n_light, const double* __restrict__ cphi,
-                                                 double* __restrict__ cw, double* __restrict__ part,
+                                                 double* cw, double* __restrict__ part,
                                                  const double* __restrict__ lik, const double* __restrict__ ass,
                                                  int lo, int hi, const double* gate,
-                                                 const double* __restrict__ cw_base) {
+                                                 const double* cw_base) {
   constexpr int TG = tg_of(KS), KPL = kpl_of(KS), NSLOT = 256 / TG;
   __shared__ double sAcc[NSLOT][KS];
   __shared__ double sRow[16][KS];
@@ -2294,7 +2334,8 @@ __global__ __launch_bounds__(256) void gs_suff64(const int* __restrict__ word_pt
     const int g = idx / KS, k = idx % KS;
     const int it = (G == 256 ? item : item - gi + g);
     // cw_base (nullable): rows summed earlier from the other entries of each word (the early /
-    // late split of the suff-stats, em.py), added first so the order is fixed
+    // late split of the suff-stats and the c.phi windows, em.py), added first so the order is
+    // fixed; cw_base == cw (in place) is allowed: each element is read, then written, by one thread
     const size_t row = it < nitems ? (size_t)order[base + it] * KS : 0;
     double v = (cw_base != nullptr && it < nitems) ? cw_base[row + k] : 0.0;
     for (int u = 0; u < S; ++u) v += sAcc[g * S + u][k];

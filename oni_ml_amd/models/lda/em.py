@@ -18,9 +18,8 @@ MI355X design:
 """
 from __future__ import annotations
 
-import os
-
 import math
+import os
 import time
 from dataclasses import dataclass, field
 from typing import Callable, List, Optional
@@ -127,21 +126,56 @@ class _Buckets:
         self.plan = plan
 
 
+
+def cphi_window_bounds(doc_ptr, budget_rows: int):
+    """Contiguous nnz-balanced document windows of <= budget_rows corpus entries each (a document
+    longer than the budget gets a window of its own): [{d0, d1, e0, e1}] covering every document."""
+    from ...parallel.dist import shard_bounds
+    ptr = np.asarray(doc_ptr, np.int64)
+    nnz = int(ptr[-1])
+    n0 = max(1, -(-nnz // max(1, int(budget_rows))))
+    for B in range(n0, 4 * n0 + 1):
+        cuts = [(a, b) for a, b in shard_bounds(ptr, B) if b > a]
+        if max(int(ptr[b] - ptr[a]) for a, b in cuts) <= budget_rows:
+            break
+    else:
+        # nnz-balanced cuts cannot isolate the over-long documents: greedy, one document at a time
+        cuts, a = [], 0
+        while a < len(ptr) - 1:
+            b = a + 1
+            while b < len(ptr) - 1 and ptr[b + 1] - ptr[a] <= budget_rows:
+                b += 1
+            cuts.append((a, b))
+            a = b
+    return [dict(d0=int(a), d1=int(b), e0=int(ptr[a]), e1=int(ptr[b])) for a, b in cuts]
+
+
+def _cpu_threads() -> int:
+    """Threads of the C++ lda-c engine (its result does not depend on the count)."""
+    return int(os.environ.get("ONI_CPU_THREADS", min(8, os.cpu_count() or 1)))
+
 class LDAEngine:
     def __init__(self, corpus: Corpus, num_topics: int, settings: Optional[LDASettings] = None,
                  alpha_init: float = 2.5, backend: str = "auto", device=None, dist=None, seed: int = 0,
                  streams: int = 4, local_shard: bool = False, split_docs: bool = True,
                  split_min: Optional[int] = 4096, use_graph: bool = True, precision: str = "fp64",
-                 emulate_shards: int = 0, doc_offset: int = 0):
+                 emulate_shards: int = 0, doc_offset: int = 0, cphi_gb: Optional[float] = None):
         """precision (hip backend): "fp64" = lda-c arithmetic with the block Gauss-Seidel schedule
         (lda_gs64.hip, the default); "fp32" = the fp32 Jacobi engine (opt-in fast mode).
         emulate_shards (torch backend, one process): reduce the sufficient statistics as N
         nnz-balanced document shards summed in shard order -- bitwise the N-rank run under
         ONI_DIST_DETERMINISTIC=1 (parallel/dist.py).
         local_shard: ``corpus`` is already this rank's shard; ``doc_offset`` its first global document
-        (the row-sharded pipeline, corpus/sharded.py)."""
+        (the row-sharded pipeline, corpus/sharded.py).
+        cphi_gb (fp64 hip engine): HBM budget of the per-entry c.phi rows (nnz x KS x 8 bytes); a
+        corpus whose rows exceed it runs its E-step in contiguous document windows, each followed by
+        its share of the sufficient statistics (``_cphi_windows``).  None: ONI_CPHI_GB, else windows
+        only when the rows would take more than 35 % of the GPU's memory."""
+        self.cphi_gb = cphi_gb
         self.settings = settings or LDASettings()
         self.emulate_shards = int(emulate_shards)
+        # cpu backend: lda-c's MPI ranks (document shards reduced in shard order; 1 = one process)
+        self.cpu_shards = 1
         if precision not in ("fp64", "fp32"):
             raise ValueError(f"precision must be fp64 or fp32, got {precision!r}")
         self.precision = precision
@@ -263,7 +297,7 @@ class LDAEngine:
         # sparse exchange on the GPU: suff-stats of the shared words first, so their all-to-all runs
         # while the suff-stats of the rank's private words (the bulk) are computed
         self._overlap = self._xchg is not None and backend == "hip" and \
-            os.environ.get("ONI_DIST_OVERLAP", "1") != "0"
+            os.environ.get("ONI_DIST_OVERLAP", "1") != "0" and getattr(self, "_cwin", None) is None
         if self._overlap:
             from ...ops import hip as H
             # only this rank's words: rows of other words stay zero in cw_local and are never read
@@ -363,12 +397,20 @@ class LDAEngine:
         self.dc = DeviceCorpus.build(corpus, self.device)
         dev, D, V, nnz = self.device, self.D, self.V, corpus.nnz
         self._U = self.gs_updates()
-        self.gs_plan = H.GSPlan(self.dc.doc_len, KS, self._U, dev)
         f64 = torch.float64
+        self._cwin = self._cphi_windows(corpus, KS)
+        if self._cwin is None:
+            self.gs_plan = H.GSPlan(self.dc.doc_len, KS, self._U, dev)
+            rows = nnz
+        else:
+            self.gs_plan = None
+            for w in self._cwin:
+                w["gp"] = H.GSPlan(self.dc.doc_len, KS, self._U, dev, doc_range=(w["d0"], w["d1"]))
+            rows = max(w["e1"] - w["e0"] for w in self._cwin)
         self.beta = torch.zeros(V, KS, dtype=f64, device=dev)
         self.cw = torch.zeros(V, KS, dtype=f64, device=dev)
         self.gamma = torch.zeros(D, KS, dtype=f64, device=dev)
-        self.cphi = torch.zeros(max(nnz, 1), KS, dtype=f64, device=dev)[:nnz]
+        self.cphi = torch.zeros(max(rows, 1), KS, dtype=f64, device=dev)[:rows]
         self.lik = torch.zeros(D, dtype=f64, device=dev)
         self.ass = torch.zeros(D, dtype=f64, device=dev)
         self.iters = torch.zeros(D, dtype=torch.int32, device=dev)
@@ -397,7 +439,50 @@ class LDAEngine:
         self._out_host = torch.zeros(self._ctlhist.numel(), dtype=f64).pin_memory()
         self._pushed = None
         self.doc_buckets = None
-        self._suff_split = self._build_suff_split() if os.environ.get("ONI_SUFF_SPLIT", "1") != "0" else None
+        self._suff_split = None
+        if self._cwin is not None:
+            self._build_window_suff()
+        elif os.environ.get("ONI_SUFF_SPLIT", "1") != "0":
+            self._suff_split = self._build_suff_split()
+
+    def _cphi_windows(self, corpus: Corpus, KS: int):
+        """Contiguous document windows [d0, d1) of <= the c.phi budget's rows each (nnz-balanced, a
+        document longer than the budget alone in its window), or None when the whole corpus fits.
+
+        The E-step of a window writes its c.phi rows into one shared buffer, the window's slice of the
+        sufficient statistics (a CSC subset) adds them to class_word (in place, window order), then the
+        next window runs: peak HBM drops from nnz x KS x 8 bytes to the largest window's rows, for one
+        more suff-stats pass per window.  class_word[w] is summed window by window, so it differs from
+        the one-buffer engine in the last bits (sums in another order); fixed for a given budget."""
+        nnz = corpus.nnz
+        row_bytes = KS * 8
+        gb = self.cphi_gb
+        if gb is None and os.environ.get("ONI_CPHI_GB"):
+            gb = float(os.environ["ONI_CPHI_GB"])
+        if gb is None:
+            total = torch.cuda.get_device_properties(self.device).total_memory if self.device.type == "cuda" else 0
+            if not total or nnz * row_bytes <= 0.35 * total:
+                return None
+            gb = 0.25 * total / 2**30
+        budget = max(1, int(gb * 2**30) // row_bytes)
+        if gb <= 0 or budget >= nnz:
+            return None
+        return cphi_window_bounds(corpus.doc_ptr, budget)
+
+    def _build_window_suff(self):
+        """Per window: its CSC subset (entry ids relative to the window's first entry) and suff plan."""
+        from ...ops import hip as H
+        dc, dev = self.dc, self.device
+        doc_ids = torch.arange(self.D, device=dev)
+        need = 1
+        for w in self._cwin:
+            mask = (doc_ids >= w["d0"]) & (doc_ids < w["d1"])
+            wp, ce, wl = H.csc_subset(dc.word_ptr, dc.csc_ent, dc.csc_doc, mask)
+            w["wp"], w["ce"] = wp, (ce - w["e0"]).contiguous()
+            w["sp"] = H.SuffPlan(wl, dev)
+            need = max(need, w["sp"].n_blocks)
+        if self._suff_part.shape[0] < need:
+            self._suff_part = torch.zeros(need, self._suff_part.shape[1], dtype=torch.float64, device=dev)
 
     def _build_suff_split(self):
         """Early / late sufficient statistics: class_word[w] = (sum over w's entries in documents of the
@@ -444,40 +529,14 @@ class LDAEngine:
             H.colsum_partials(self._suff_part, pa.n_blocks + pb.n_blocks, self._red_local, gate=gate)
             self._red.copy_(self._red_local)
             return
-        streams = [main] + self._streams
-        self._ev_fork.record(main)
-        used = []
-        # side streams: the long-document buckets (critical path) are dispatched first, the split
-        # documents' batches (back to back on one stream) before everything
-        work = list(self.gs_plan.plan)
-        if self.gs_plan.split is not None:
-            work.insert(0, ("split", self.gs_plan.split.batches))
+        if self._cwin is not None:
+            self._launch_windows(newton_key, phase)
+            return
+        gp = self.gs_plan
         # early / late suff-stats (phase "all"): work[0], the longest-document bucket, runs alone on
-        # streams[1] (late_s); the early pass joins every other stream, so no other bucket may share
-        # late_s (with 6 work items the round robin would put item 4 there and the early pass would
-        # read its cphi rows before they are written)
-        ss = self._suff_split if (phase == "all" and len(work) >= 2) else None
-        late_s = streams[1] if ss is not None else None
-        for si, (var, order) in zip(range(len(work)), work):
-            s = streams[(si + 1) % len(streams)] if si < len(work) - 1 else main
-            if si > 0 and s is late_s:
-                s = streams[2]
-            if s is not main and s not in used:
-                s.wait_event(self._ev_fork)
-                used.append(s)
-            with torch.cuda.stream(s):
-                if var == "split":
-                    for batch in order:
-                        H.gs_split(dc.doc_ptr, dc.word_idx, dc.counts, self.beta, self.K, self._U, prm, self.gamma,
-                                   self.cphi, self.lik, self.ass, self.iters, batch)
-                else:
-                    H.gs_estep(dc.doc_ptr, dc.word_idx, dc.counts, order, self.beta, self.K, self._U, prm,
-                               self.gamma, self.cphi, self.lik, self.ass, self.iters, var)
-        # every bucket but work[0] is joined first and the early pass overlaps work[0]
-        for j, s in enumerate(used):
-            self._ev_join[j].record(s)
-            if s is not late_s:
-                main.wait_event(self._ev_join[j])
+        # streams[1] (late_s); the early pass joins every other stream
+        ss = self._suff_split if (phase == "all" and len(gp.plan) + (gp.split is not None) >= 2) else None
+        used, late_s = self._launch_buckets(gp, ss is not None)
         if phase == "estep":             # the document kernels only (final inference pass)
             return
         scal = (self.lik, self.ass, 0, self.lik.numel())
@@ -498,6 +557,63 @@ class LDAEngine:
         H.gs_suff64(dc.word_ptr, dc.csc_ent, sp, self.cphi, self._cw_local, self._suff_part[:max(sp.n_blocks, 1)],
                     gate=gate, scalars=scal)
         H.colsum_partials(self._suff_part, sp.n_blocks, self._red_local, gate=gate)
+        self._finish_suff64(newton_key)
+
+    def _launch_buckets(self, gp, late: bool = False, ent_base=None):
+        """The document kernels of GSPlan ``gp`` on 4 streams, joined back into the current stream.
+        late: work[0] (the longest-document bucket) stays un-joined on streams[1], returned as late_s,
+        for the early / late suff-stats; ent_base: the c.phi buffer is a window (``_cphi_windows``)."""
+        from ...ops import hip as H
+        dc, prm = self.dc, self._params
+        main = torch.cuda.current_stream(self.device)
+        streams = [main] + self._streams
+        self._ev_fork.record(main)
+        used = []
+        # side streams: the long-document buckets (critical path) are dispatched first, the split
+        # documents' batches (back to back on one stream) before everything
+        work = list(gp.plan)
+        if gp.split is not None:
+            work.insert(0, ("split", gp.split.batches))
+        # no other bucket may share late_s (with 6 work items the round robin would put item 4 there
+        # and the early pass would read its cphi rows before they are written)
+        late_s = streams[1] if late else None
+        for si, (var, order) in zip(range(len(work)), work):
+            s = streams[(si + 1) % len(streams)] if si < len(work) - 1 else main
+            if si > 0 and s is late_s:
+                s = streams[2]
+            if s is not main and s not in used:
+                s.wait_event(self._ev_fork)
+                used.append(s)
+            with torch.cuda.stream(s):
+                if var == "split":
+                    for batch in order:
+                        H.gs_split(dc.doc_ptr, dc.word_idx, dc.counts, self.beta, self.K, self._U, prm, self.gamma,
+                                   self.cphi, self.lik, self.ass, self.iters, batch, ent_base=ent_base)
+                else:
+                    H.gs_estep(dc.doc_ptr, dc.word_idx, dc.counts, order, self.beta, self.K, self._U, prm,
+                               self.gamma, self.cphi, self.lik, self.ass, self.iters, var, ent_base=ent_base)
+        # every bucket but work[0] is joined first and the early pass overlaps work[0]
+        for j, s in enumerate(used):
+            self._ev_join[j].record(s)
+            if s is not late_s:
+                main.wait_event(self._ev_join[j])
+        return used, late_s
+
+    def _launch_windows(self, newton_key, phase: str):
+        """E-step in c.phi windows: per window its document kernels, then its CSC subset's rows added
+        to class_word in place (window 0 writes, later windows add); the likelihood / alpha_ss slices
+        and the class totals ride on the last window's pass."""
+        from ...ops import hip as H
+        if phase not in ("all",):
+            raise NotImplementedError(f"c.phi windows: E-step phase {phase!r}")
+        gate = self._gate
+        scal = (self.lik, self.ass, 0, self.lik.numel())
+        last = len(self._cwin) - 1
+        for b, w in enumerate(self._cwin):
+            self._launch_buckets(w["gp"], ent_base=w["e0"])
+            H.gs_suff64(w["wp"], w["ce"], w["sp"], self.cphi, self._cw_local, self._suff_part, gate=gate,
+                        scalars=scal if b == last else None, base=None if b == 0 else self._cw_local)
+        H.colsum_partials(self._suff_part, self._cwin[last]["sp"].n_blocks, self._red_local, gate=gate)
         self._finish_suff64(newton_key)
 
     def _finish_suff64(self, newton_key):
@@ -654,8 +770,8 @@ class LDAEngine:
         lb = torch.where(self.beta > 0, torch.log(self.beta), torch.full_like(self.beta, LOG_FLOOR))
         res = self._native.lda_estep_ldac(
             self.corpus.doc_ptr, self.corpus.word_idx, self.corpus.counts,
-            np.ascontiguousarray(lb.T.numpy()), self.alpha, self.var_max_iter, self.settings.var_converged, 0,
-            gs_updates=self.settings.gs_updates)
+            np.ascontiguousarray(lb.T.numpy()), self.alpha, self.var_max_iter, self.settings.var_converged,
+            nshards=self.cpu_shards, threads=_cpu_threads(), gs_updates=self.settings.gs_updates)
         self.gamma = torch.from_numpy(res["gamma"])
         self.iters = torch.from_numpy(res["iters"])
         self.lik = torch.from_numpy(res["doc_likelihood"])
@@ -1034,10 +1150,11 @@ class LDAEngine:
     def _check_split_error(self):
         """A NaN likelihood: if a split-document barrier timed out, fail loudly (the kernel
         flags it instead of hanging the GPU)."""
-        sp = self.doc_buckets.split if self.doc_buckets is not None else None
+        plans = [self.doc_buckets.split if self.doc_buckets is not None else None]
         gp = getattr(self, "gs_plan", None)
-        gp = gp.split if gp is not None else None
-        if any(int(b["error"].item()) for x in (sp, gp) if x is not None for b in x.batches):
+        plans.append(gp.split if gp is not None else None)
+        plans += [w["gp"].split for w in (getattr(self, "_cwin", None) or [])]
+        if any(int(b["error"].item()) for x in plans if x is not None for b in x.batches):
             raise RuntimeError("split-document E-step: a cross-workgroup barrier timed out "
                                "(segments of one document were not co-resident)")
 
@@ -1161,12 +1278,17 @@ class LDAEngine:
         K = self.K
         if self.backend == "hip" and self.fp64:
             self._push_params()
-            self._launch_estep64(phase="estep")
             z = torch.empty(self.corpus.nnz, dtype=torch.int64, device=self.device)
             step = 1 << 22
-            for a in range(0, self.corpus.nnz, step):
-                b = min(self.corpus.nnz, a + step)
-                z[a:b] = torch.argmax(self.cphi[a:b, :K], dim=1)
+            wins = self._cwin or [dict(gp=None, e0=0, e1=self.corpus.nnz)]
+            for w in wins:
+                if w["gp"] is None:
+                    self._launch_estep64(phase="estep")
+                else:
+                    self._launch_buckets(w["gp"], ent_base=w["e0"])
+                for a in range(w["e0"], w["e1"], step):
+                    b = min(w["e1"], a + step)
+                    z[a:b] = torch.argmax(self.cphi[a - w["e0"]:b - w["e0"], :K], dim=1)
             return z.cpu().numpy()
         if self.backend == "torch":
             from ...ops import reference as R

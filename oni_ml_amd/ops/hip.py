@@ -543,10 +543,24 @@ def gs_tiny_max(KS: int) -> int:
     return int(lib().gs_tiny_max(int(KS)))
 
 
+def _cphi_ptr(cphi, nnz, KS, dev, ent_base):
+    """Device address of c.phi row 0 of the corpus: the whole [nnz, KS] buffer, or (``ent_base`` given)
+    a window [rows, KS] holding corpus entries [ent_base, ent_base + rows) -- the kernels index rows by
+    corpus entry, so the address is shifted back by ent_base rows.  The caller guarantees that every
+    document of the launch has its entries inside the window (GSPlan(doc_range=...))."""
+    if ent_base is None:
+        return _chk(cphi, torch.float64, "cphi", (nnz, KS), dev)
+    ptr = _chk(cphi, torch.float64, "cphi", None, dev)
+    if cphi.dim() != 2 or cphi.shape[1] != KS or not (0 <= int(ent_base) and int(ent_base) + cphi.shape[0] <= nnz):
+        raise ValueError(f"cphi window {tuple(cphi.shape)} at entry {ent_base} does not fit [{nnz}, {KS}]")
+    return ptr - int(ent_base) * KS * 8
+
+
 def gs_estep(doc_ptr, word_idx, counts, order, beta, K, gs_updates, params, gamma, cphi, lik, alpha_ss, iters, variant,
-             dbg=None):
+             dbg=None, ent_base=None):
     """One launch of the fp64 block Gauss-Seidel E-step over the documents in ``order``.
-    ``params``: the device parameter block {alpha, lgamma constant, VAR_MAX_ITER, VAR_CONVERGED, done}."""
+    ``params``: the device parameter block {alpha, lgamma constant, VAR_MAX_ITER, VAR_CONVERGED, done}.
+    ``ent_base``: ``cphi`` is a window starting at that corpus entry (_cphi_ptr)."""
     D = doc_ptr.numel() - 1
     nnz = word_idx.numel()
     V, KS = beta.shape
@@ -567,7 +581,7 @@ def gs_estep(doc_ptr, word_idx, counts, order, beta, K, gs_updates, params, gamm
         _chk(beta, torch.float64, "beta", (V, KS), dev), int(K), int(KS), int(gs_updates),
         _params_ptr(params, dev) or _bad("params"),
         _chk(gamma, torch.float64, "gamma", (D, KS), dev),
-        _chk(cphi, torch.float64, "cphi", (nnz, KS), dev),
+        _cphi_ptr(cphi, nnz, KS, dev, ent_base),
         _chk(lik, torch.float64, "lik", (D,), dev),
         _chk(alpha_ss, torch.float64, "alpha_ss", (D,), dev),
         _chk(iters, torch.int32, "iters", (D,), dev),
@@ -722,7 +736,7 @@ class GSSplitPlan:
 
 
 def gs_split(doc_ptr, word_idx, counts, beta, K, gs_updates, params, gamma, cphi, lik, alpha_ss, iters, batch,
-             dbg=None):
+             dbg=None, ent_base=None):
     """One launch of the fp64 split-document E-step over one GSSplitPlan batch.  dbg: optional int64[8]
     phase timer of workgroup 0 (word phase, barrier 1, publish + gather, barrier 2, refresh, barrier 3,
     sweep end, chunks)."""
@@ -741,7 +755,7 @@ def gs_split(doc_ptr, word_idx, counts, beta, K, gs_updates, params, gamma, cphi
         _chk(doc_ptr, torch.int32, "doc_ptr", (D + 1,), dev), _chk(word_idx, torch.int32, "word_idx", (nnz,), dev),
         _chk(counts, torch.float32, "counts", (nnz,), dev), _chk(beta, torch.float64, "beta", (V, KS), dev),
         int(K), int(KS), int(gs_updates), _params_ptr(params, dev) or _bad("params"),
-        _chk(gamma, torch.float64, "gamma", (D, KS), dev), _chk(cphi, torch.float64, "cphi", (nnz, KS), dev),
+        _chk(gamma, torch.float64, "gamma", (D, KS), dev), _cphi_ptr(cphi, nnz, KS, dev, ent_base),
         _chk(lik, torch.float64, "lik", (D,), dev), _chk(alpha_ss, torch.float64, "alpha_ss", (D,), dev),
         _chk(iters, torch.int32, "iters", (D,), dev),
         batch["seg_doc"].data_ptr(), batch["seg_index"].data_ptr(), batch["seg_count"].data_ptr(),
@@ -762,10 +776,15 @@ class GSPlan:
     EDGES_NARROW = ((GS_TEAM8, 2048, None), (GS_TEAM4, 256, 2048), (GS_TEAM1, GS_SMALL_MAX, 256),
                     (GS_SMALL, None, GS_SMALL_MAX))
 
-    def __init__(self, lengths, KS: int, gs_updates: int, device, split_min: Optional[int] = None):
+    def __init__(self, lengths, KS: int, gs_updates: int, device, split_min: Optional[int] = None,
+                 doc_range=None):
         import numpy as np
         L = np.asarray(lengths, dtype=np.int64)
         order = np.argsort(-L, kind="stable").astype(np.int32)
+        # doc_range (d0, d1): only documents d0 <= d < d1 (one c.phi window of the engine)
+        self.doc_range = None if doc_range is None else (int(doc_range[0]), int(doc_range[1]))
+        if self.doc_range is not None:
+            order = order[(order >= self.doc_range[0]) & (order < self.doc_range[1])]
         # documents longer than split_min words: one document over several workgroups (gs_split);
         # default on for KS > 32 (the topic-group team kernels' chunk of a long document is bound
         # by one CU's row gathers), ONI_GS_SPLIT_MIN overrides (0: off)

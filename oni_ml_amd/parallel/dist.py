@@ -70,15 +70,26 @@ class DistContext:
         return scalars
 
     def ordered_allreduce(self, t: torch.Tensor) -> torch.Tensor:
-        """In place: t <- 0 + t_0 + t_1 + ... + t_{N-1} (rank order) on every rank."""
+        """In place: t <- 0 + t_0 + t_1 + ... + t_{N-1} (rank order) on every rank.
+
+        Gathered in slices of <= ONI_ORDERED_CHUNK_MB (default 256) MiB per rank, so the extra memory is
+        N x the slice, not N full copies (a config-5 class_word is 3.8 GB per copy)."""
         import torch.distributed as td
 
-        parts = [torch.empty_like(t) for _ in range(self.world_size)]
-        td.all_gather(parts, t.contiguous())
-        acc = torch.zeros_like(t)
-        for p in parts:
-            acc += p
-        t.copy_(acc)
+        flat = t.view(-1) if t.is_contiguous() else t.contiguous().view(-1)
+        step = max(1, int(float(os.environ.get("ONI_ORDERED_CHUNK_MB", "256")) * 2**20) // max(1, t.element_size()))
+        step = min(step, max(1, flat.numel()))
+        parts = [torch.empty(step, dtype=t.dtype, device=t.device) for _ in range(self.world_size)]
+        for a in range(0, flat.numel(), step):
+            b = min(flat.numel(), a + step)
+            views = [p[:b - a] for p in parts]
+            td.all_gather(views, flat[a:b].contiguous())
+            acc = torch.zeros(b - a, dtype=t.dtype, device=t.device)
+            for v in views:
+                acc += v
+            flat[a:b] = acc
+        if flat.data_ptr() != t.data_ptr():
+            t.copy_(flat.view_as(t))
         return t
 
     def self_check(self):

@@ -96,7 +96,7 @@ def run(cfg, dist=None, device=None, log=print) -> dict:
             res.update({k: v for k, v in m.items() if not isinstance(v, list)})
             R.emit(dict(stage="lda_detail", var_iter_hist=m["var_iter_hist"], **{k: v for k, v in m.items()
                                                                                    if not isinstance(v, list)}))
-            summary["lda"] = dict(em_iterations=lres.em_iterations, seconds=lres.seconds, alpha=lres.alpha,
+            summary["lda"] = dict(em_iterations=lres.em_iterations, timing=getattr(lres, "timing", {}), seconds=lres.seconds, alpha=lres.alpha,
                                   likelihood=lres.likelihoods[-1][0] if lres.likelihoods else None)
         gamma, log_beta = lres.gamma, lres.log_beta
     else:

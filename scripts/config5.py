@@ -40,7 +40,11 @@ def main():
     ap.add_argument("--workdir", default=os.path.join(os.environ.get("TMPDIR", "/tmp"), "oni_config5"))
     ap.add_argument("--out", default="gpurun_out/config5.json")
     ap.add_argument("--keep", action="store_true")
+    ap.add_argument("--cphi-gb", type=float, default=None,
+                    help="HBM budget of the engine's c.phi rows (ONI_CPHI_GB): E-step in document windows")
     a = ap.parse_args()
+    if a.cphi_gb is not None:
+        os.environ["ONI_CPHI_GB"] = str(a.cphi_gb)
 
     import torch
     from oni_ml_amd.config import RunConfig
@@ -85,13 +89,13 @@ def main():
                events=a.events, part_files=len(gen["paths"]), input_gb=round(in_bytes / 1e9, 3), addresses=gen["ips"],
                generate_s=round(gen_s, 2), corpus=summary.get("corpus"), stage_seconds=stages,
                pipeline_wall_s=round(wall, 2), em_iterations=em_it,
-               lda_seconds=summary.get("lda", {}).get("seconds"),
+               lda_seconds=summary.get("lda", {}).get("seconds"), lda_timing=summary.get("lda", {}).get("timing"),
                ms_per_em_iteration=(round(1e3 * summary["lda"]["seconds"] / em_it, 2) if em_it else None),
                ingest_mb_per_s=round(in_bytes / 1e6 / stages["load"], 1) if stages.get("load") else None,
                flagged=summary.get("scored"), lda_metrics={k: v for k, v in m.items() if not isinstance(v, list)},
                peak_hbm_gb=(round(torch.cuda.max_memory_allocated() / 2**30, 2) if dev.type == "cuda" else None),
                device=(torch.cuda.get_device_name(0) if dev.type == "cuda" else "cpu"), backend=a.backend,
-               threads=a.threads, lag=a.lag, output_gb=round(_du(lpath) / 1e9, 3), data="synthetic (synth/flow.py, scaled address pool)")
+               threads=a.threads, lag=a.lag, cphi_gb=a.cphi_gb, output_gb=round(_du(lpath) / 1e9, 3), data="synthetic (synth/flow.py, scaled address pool)")
     os.makedirs(os.path.dirname(os.path.abspath(a.out)), exist_ok=True)
     with open(a.out, "w") as f:
         json.dump(rec, f, indent=1, default=str)

@@ -18,6 +18,8 @@ exported doc topics theta = gamma / sum(gamma) and word topics phi = softmax(log
 (lda_post.py semantics), and the scorer's ranking of (doc, word) entries by
 theta_d . phi_w (flow_post_lda.scala:227-239: the lowest scores are the flagged events).
 
+`cpu#20` is lda-c with its statistics reduced as 20 MPI ranks (the reference's process_count):
+the reference's own floating-point spread from nothing but summation order.
 A fourth run, `cpu@1`, is lda-c's own run-to-run spread: the same fp64 engine from another
 random init (oni-lda-c seeds its MT19937 from the clock, so no two reference runs agree).
 
@@ -51,11 +53,14 @@ def _train(corpus, K, name, dev, seed, var_max_iter=None):
     st = LDASettings()
     if var_max_iter is not None:
         st.var_max_iter = var_max_iter
+    name, _, shards = name.partition("#")       # "cpu#20": lda-c reduced as 20 MPI ranks
     backend, precision = {"hip": ("hip", "fp64"), "hip32": ("hip", "fp32"), "torch": ("torch", "fp64"),
                           "cpu": ("cpu", "fp64"), "cpuU": ("cpu", "fp64")}[name]
     if name == "cpuU":
         st.gs_updates = GS_U
     eng = LDAEngine(corpus, K, st, backend=backend, device=dev, seed=seed, precision=precision)
+    if shards:
+        eng.cpu_shards = int(shards)
     if dev.type == "cuda":
         torch.cuda.synchronize()
     t0 = time.perf_counter()

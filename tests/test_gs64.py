@@ -290,3 +290,54 @@ def test_final_pass_word_assignments_match_oracle(vconv):
     else:
         # documents whose convergence test sits within rounding of 1e-6 may stop a sweep apart
         assert (z == ref).mean() > 0.999
+
+
+@pytest.mark.parametrize("K,split_min", [(20, None), (100, None), (20, "3000")])
+def test_cphi_windows_match_one_buffer(K, split_min, monkeypatch):
+    """c.phi windows (the E-step in contiguous document windows sharing one small c.phi buffer, each
+    window's suff-stats added in place) against the one-buffer engine: gamma bitwise (the document
+    kernels do not change), class_word / class totals / likelihood to summation order, an EM run's
+    trajectory, and the final pass's word assignments."""
+    if split_min:
+        monkeypatch.setenv("ONI_GS_SPLIT_MIN", split_min)
+    c = _edge_corpus(seed=5, max_len=9000)
+    lb = _log_beta(c.num_terms, K, seed=9)
+    KS = 24 if K == 20 else 104
+    budget_gb = (c.nnz // 3) * KS * 8 / 2**30          # ~3-4 windows
+    out = []
+    for gb in (None, budget_gb):
+        st = LDASettings(var_max_iter=5)
+        st.gs_updates = 32
+        eng = LDAEngine(c, K, st, backend="hip", seed=0, precision="fp64", cphi_gb=gb)
+        assert (eng._cwin is None) == (gb is None)
+        if gb is not None:
+            assert len(eng._cwin) >= 3 and eng.cphi.shape[0] < c.nnz
+        eng.init_from_model(lb, 0.45)
+        sc = eng.e_step().cpu().numpy()
+        eng.e_step()                                   # graph replay
+        torch.cuda.synchronize()
+        z = eng.word_assignments()
+        out.append((eng.gamma.cpu().numpy(), eng._cw_local[:, :K].cpu().numpy(), eng.class_total[:K].cpu().numpy(),
+                    sc, z))
+    (g0, cw0, ct0, sc0, z0), (g1, cw1, ct1, sc1, z1) = out
+    assert np.array_equal(g0, g1)
+    assert _rel(cw1, cw0, 1e-30) < 1e-13
+    assert _rel(ct1, ct0, 1e-30) < 1e-13
+    assert abs(sc1[0] - sc0[0]) <= 1e-13 * abs(sc0[0]) and abs(sc1[1] - sc0[1]) <= 1e-13 * abs(sc0[1])
+    assert np.array_equal(z0, z1)
+
+
+def test_cphi_windows_em_run():
+    """A whole EM run in c.phi windows tracks the one-buffer run (same iterations, likelihoods to 1e-12)."""
+    c = planted_corpus(num_docs=1500, num_terms=900, num_topics=6, mean_tokens=60, tail=1.0, max_tokens=9000,
+                       seed=4)
+    runs = []
+    for gb in (None, (c.nnz // 4) * 24 * 8 / 2**30):
+        st = LDASettings(em_max_iter=8)
+        eng = LDAEngine(c, 20, st, backend="hip", seed=3, precision="fp64", cphi_gb=gb)
+        r = eng.run()
+        runs.append((np.array([x[0] for x in r.likelihoods]), eng.alpha))
+    (L0, a0), (L1, a1) = runs
+    assert L0.shape == L1.shape
+    assert np.max(np.abs(L1 - L0) / np.abs(L0)) < 1e-12
+    assert abs(a1 - a0) <= 1e-12 * a0

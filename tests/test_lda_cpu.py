@@ -215,3 +215,21 @@ def test_word_assignments_final_pass_cpu_backends():
     t.run()
     zt = t.word_assignments()
     assert zt.shape == (c.nnz,) and zt.min() >= 0 and zt.max() < 6
+
+
+def test_cphi_window_bounds_cover_corpus_within_budget():
+    """c.phi windows of the fp64 engine: contiguous, covering every document, each within the row
+    budget unless it is one document longer than the budget."""
+    from oni_ml_amd.models.lda.em import cphi_window_bounds
+    rng = np.random.default_rng(0)
+    L = rng.integers(0, 50, size=2000)
+    L[700], L[701] = 5000, 3000
+    ptr = np.concatenate([[0], np.cumsum(L)])
+    for budget in (60, 2500, 5000, 9000, int(ptr[-1])):
+        w = cphi_window_bounds(ptr, budget)
+        assert w[0]["d0"] == 0 and w[-1]["d1"] == len(L)
+        assert all(a["d1"] == b["d0"] for a, b in zip(w, w[1:]))
+        for x in w:
+            assert x["e0"] == ptr[x["d0"]] and x["e1"] == ptr[x["d1"]]
+            assert x["e1"] - x["e0"] <= budget or x["d1"] - x["d0"] == 1
+    assert len(cphi_window_bounds(ptr, int(ptr[-1]))) == 1
