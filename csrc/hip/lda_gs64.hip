@@ -961,46 +961,6 @@ __device__ __forceinline__ bool tagged_sum_f64(const unsigned long long* x, int 
   return true;
 }
 
-// tagged_sum_f64 with every granule of up to 16 segments in flight at once: one polling round trip
-// for G <= 16 (tagged_sum_f64 waits for each group of 4 segments before issuing the next group's
-// loads -- ceil(G / 4) dependent fabric round trips per chunk)
-__device__ __forceinline__ bool tagged_sum_f64_wide(const unsigned long long* x, int n, int stride, unsigned tag,
-                                                    double& out) {
-  constexpr int B = 16;
-  double s = 0.0;
-  long spins = 0;
-  for (int q0 = 0; q0 < n; q0 += B) {
-    unsigned long long v[2 * B];
-#pragma unroll
-    for (int u = 0; u < 2 * B; ++u)
-      v[u] = (q0 + u / 2 < n) ? __hip_atomic_load(x + (size_t)(q0 + u / 2) * stride + (u & 1), __ATOMIC_RELAXED,
-                                                  __HIP_MEMORY_SCOPE_AGENT)
-                              : ((unsigned long long)tag << 32);
-    for (;;) {
-      unsigned pending = 0;
-#pragma unroll
-      for (int u = 0; u < 2 * B; ++u) pending |= ((unsigned)(v[u] >> 32) != tag) ? (1u << u) : 0u;
-      if (pending == 0) break;
-      if (++spins > kSplitSpinLimit) {
-        out = __builtin_nan("");
-        return false;
-      }
-      __builtin_amdgcn_s_sleep(1);
-#pragma unroll
-      for (int u = 0; u < 2 * B; ++u)
-        if ((pending >> u) & 1u)
-          v[u] = __hip_atomic_load(x + (size_t)(q0 + u / 2) * stride + (u & 1), __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
-    }
-#pragma unroll
-    for (int u = 0; u < 2 * B; u += 2)
-      if (q0 + u / 2 < n)
-        s += __longlong_as_double((long long)(((v[u + 1] & 0xffffffffull) << 32) | (v[u] & 0xffffffffull)));
-  }
-  out = s;
-  return true;
-}
-
 template <int KS>
 __global__ __launch_bounds__(512) void gs_split(GSArgs a, SplitArgs sp) {
   using T = TeamShape<KS, 8>;
@@ -1450,7 +1410,7 @@ __global__ __launch_bounds__(512) void gs_splitw(GSArgs a, SplitArgs sp) {
         for (int o = 0; o < TC; ++o) {
           const int c = lane + 64 * o;
           tot[o] = 0.0;
-          if (c < NC) ok &= tagged_sum_f64_wide(xb + (size_t)base * GR + 2 * c, G, GR, tag, tot[o]);
+          if (c < NC) ok &= tagged_sum_f64(xb + (size_t)base * GR + 2 * c, G, GR, tag, tot[o]);
         }
         tick(4);
         if (!ok) {
@@ -2484,18 +2444,9 @@ static void gs_estep_ks(const GSArgs& a, int variant, hipStream_t s) {
         // (measured on the headline corpus: 2.70 vs 2.96 ms, the 4-wave team has no second wave per
         // SIMD to cover the fp64 dependency chains of the word phase)
         static const int bnw = std::getenv("ONI_GS_BIG_NW") ? std::atoi(std::getenv("ONI_GS_BIG_NW")) : 7;
-        // ONI_GS_TEAM8_LDS=<bytes>: dynamic LDS requested on top of the kernel's own, so no workgroup of
-        // another bucket (all of them use LDS) is co-resident on a longest-document CU
-        static const int pad = std::getenv("ONI_GS_TEAM8_LDS") ? std::atoi(std::getenv("ONI_GS_TEAM8_LDS")) : 0;
-        if (bnw == 7 && pad > 0) {
-          static bool attr = false;
-          if (!attr) {
-            ONI_HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&gs::gs_wsteam<KS, 7, 2>),
-                                              hipFuncAttributeMaxDynamicSharedMemorySize, pad));
-            attr = true;
-          }
-          hipLaunchKernelGGL((gs::gs_wsteam<KS, 7, 2>), dim3(a.n_items), dim3(512), pad, s, a);
-        } else if (bnw == 7)
+        // (a dynamic-LDS pad keeping other buckets off the longest-document CUs measured no change:
+        // 2.175 vs 2.175 ms per EM iteration, profiles/r3_tuning_log.md)
+        if (bnw == 7)
           hipLaunchKernelGGL((gs::gs_wsteam<KS, 7, 2>), dim3(a.n_items), dim3(512), 0, s, a);
         else if (bnw == 3)
           hipLaunchKernelGGL((gs::gs_wsteam<KS, 3, 4>), dim3(a.n_items), dim3(256), 0, s, a);

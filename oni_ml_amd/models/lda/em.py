@@ -470,17 +470,30 @@ class LDAEngine:
         return cphi_window_bounds(corpus.doc_ptr, budget)
 
     def _build_window_suff(self):
-        """Per window: its CSC subset (entry ids relative to the window's first entry) and suff plan."""
+        """Per window: its CSC subset (entry ids relative to the window's first entry) and a suff plan
+        over only the words it holds (the other rows of class_word are not touched by its pass); plus
+        the closing pass over the whole vocabulary with no entries, which yields the class totals and
+        the likelihood / alpha_ss slices (``_launch_windows``)."""
         from ...ops import hip as H
-        dc, dev = self.dc, self.device
-        doc_ids = torch.arange(self.D, device=dev)
+        dc, dev, V = self.dc, self.device, self.V
+        wlen = (dc.word_ptr[1:] - dc.word_ptr[:-1]).long()
+        word_of = torch.repeat_interleave(torch.arange(V, device=dev), wlen)      # once for all windows
         need = 1
         for w in self._cwin:
-            mask = (doc_ids >= w["d0"]) & (doc_ids < w["d1"])
-            wp, ce, wl = H.csc_subset(dc.word_ptr, dc.csc_ent, dc.csc_doc, mask)
-            w["wp"], w["ce"] = wp, (ce - w["e0"]).contiguous()
-            w["sp"] = H.SuffPlan(wl, dev)
+            keep = (dc.csc_doc >= w["d0"]) & (dc.csc_doc < w["d1"])
+            cnt = torch.bincount(word_of[keep], minlength=V)
+            ptr = torch.zeros(V + 1, dtype=torch.int64, device=dev)
+            ptr[1:] = torch.cumsum(cnt, 0)
+            w["wp"] = ptr.to(torch.int32)
+            w["ce"] = (dc.csc_ent[keep] - w["e0"]).contiguous()
+            wl = cnt.cpu().numpy()
+            w["sp"] = H.SuffPlan(wl, dev, words=np.flatnonzero(wl))
             need = max(need, w["sp"].n_blocks)
+        del word_of
+        self._win_total = dict(wp=torch.zeros(V + 1, dtype=torch.int32, device=dev),
+                               ce=torch.zeros(1, dtype=torch.int32, device=dev),
+                               sp=H.SuffPlan(np.zeros(V, np.int64), dev))
+        need = max(need, self._win_total["sp"].n_blocks)
         if self._suff_part.shape[0] < need:
             self._suff_part = torch.zeros(need, self._suff_part.shape[1], dtype=torch.float64, device=dev)
 
@@ -559,10 +572,11 @@ class LDAEngine:
         H.colsum_partials(self._suff_part, sp.n_blocks, self._red_local, gate=gate)
         self._finish_suff64(newton_key)
 
-    def _launch_buckets(self, gp, late: bool = False, ent_base=None):
+    def _launch_buckets(self, gp, late: bool = False, win=None):
         """The document kernels of GSPlan ``gp`` on 4 streams, joined back into the current stream.
         late: work[0] (the longest-document bucket) stays un-joined on streams[1], returned as late_s,
-        for the early / late suff-stats; ent_base: the c.phi buffer is a window (``_cphi_windows``)."""
+        for the early / late suff-stats; win: one of the c.phi windows (``_cphi_windows``) -- the document
+        kernels write its entries into the first rows of the shared buffer."""
         from ...ops import hip as H
         dc, prm = self.dc, self._params
         main = torch.cuda.current_stream(self.device)
@@ -577,6 +591,9 @@ class LDAEngine:
         # no other bucket may share late_s (with 6 work items the round robin would put item 4 there
         # and the early pass would read its cphi rows before they are written)
         late_s = streams[1] if late else None
+        # a c.phi window: the buffer's first e1 - e0 rows hold the window's entries
+        cphi = self.cphi if win is None else self.cphi[:win["e1"] - win["e0"]]
+        ent_base = None if win is None else win["e0"]
         for si, (var, order) in zip(range(len(work)), work):
             s = streams[(si + 1) % len(streams)] if si < len(work) - 1 else main
             if si > 0 and s is late_s:
@@ -588,10 +605,10 @@ class LDAEngine:
                 if var == "split":
                     for batch in order:
                         H.gs_split(dc.doc_ptr, dc.word_idx, dc.counts, self.beta, self.K, self._U, prm, self.gamma,
-                                   self.cphi, self.lik, self.ass, self.iters, batch, ent_base=ent_base)
+                                   cphi, self.lik, self.ass, self.iters, batch, ent_base=ent_base)
                 else:
                     H.gs_estep(dc.doc_ptr, dc.word_idx, dc.counts, order, self.beta, self.K, self._U, prm,
-                               self.gamma, self.cphi, self.lik, self.ass, self.iters, var, ent_base=ent_base)
+                               self.gamma, cphi, self.lik, self.ass, self.iters, var, ent_base=ent_base)
         # every bucket but work[0] is joined first and the early pass overlaps work[0]
         for j, s in enumerate(used):
             self._ev_join[j].record(s)
@@ -608,12 +625,18 @@ class LDAEngine:
             raise NotImplementedError(f"c.phi windows: E-step phase {phase!r}")
         gate = self._gate
         scal = (self.lik, self.ass, 0, self.lik.numel())
-        last = len(self._cwin) - 1
-        for b, w in enumerate(self._cwin):
-            self._launch_buckets(w["gp"], ent_base=w["e0"])
-            H.gs_suff64(w["wp"], w["ce"], w["sp"], self.cphi, self._cw_local, self._suff_part, gate=gate,
-                        scalars=scal if b == last else None, base=None if b == 0 else self._cw_local)
-        H.colsum_partials(self._suff_part, self._cwin[last]["sp"].n_blocks, self._red_local, gate=gate)
+        cw = self._cw_local
+        cw.zero_()
+        for w in self._cwin:
+            self._launch_buckets(w["gp"], win=w)
+            # only the window's words: their rows += the window's entries (in place)
+            H.gs_suff64(w["wp"], w["ce"], w["sp"], self.cphi[:w["e1"] - w["e0"]], cw, self._suff_part, gate=gate,
+                        base=cw)
+        # closing pass, every word and no entries: rows unchanged, column sums + likelihood slices
+        tp = self._win_total
+        H.gs_suff64(tp["wp"], tp["ce"], tp["sp"], self.cphi[:1], cw, self._suff_part, gate=gate, scalars=scal,
+                    base=cw)
+        H.colsum_partials(self._suff_part, tp["sp"].n_blocks, self._red_local, gate=gate)
         self._finish_suff64(newton_key)
 
     def _finish_suff64(self, newton_key):
@@ -1258,6 +1281,39 @@ class LDAEngine:
         cw = (self.global_cw() if cw is None else cw)[:, :self.K]
         return _log_beta_host(cw, self.class_total[:self.K])
 
+    # outputs up to this size are copied behind the device work (pinned buffer + event) by the
+    # *_deferred variants; larger ones take the blocking, chunked path
+    DEFER_BYTES = 256 << 20
+
+    def log_beta_deferred(self, cw: Optional[torch.Tensor] = None):
+        """(host [K, V] array, event or None): ``log_beta`` whose device-to-host copy is queued on the
+        current stream into a pinned buffer; the array is valid once ``event`` completed.  The LAG saves
+        hand both to the file writer, so an EM run with saves does not wait for each copy."""
+        full = self.global_cw() if cw is None else cw
+        c = full[:, :self.K]
+        V, K = c.shape
+        if self.device.type != "cuda" or K * V * 8 > self.DEFER_BYTES:
+            return _log_beta_host(c, self.class_total[:K]), None
+        cT = c.T.to(torch.float64).contiguous()
+        lct = torch.log(self.class_total[:K].to(torch.float64))
+        lb = torch.where(cT > 0, torch.log(cT) - lct[:, None], torch.full_like(cT, LOG_FLOOR))
+        host = torch.empty((K, V), dtype=torch.float64, pin_memory=True)
+        host.copy_(lb, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        return host.numpy(), ev
+
+    def local_gamma_deferred(self):
+        """(host [D_local, K] gamma, event or None): ``local_gamma`` with a queued pinned copy."""
+        g = self.gamma[:, :self.K]
+        if self.device.type != "cuda" or g.numel() * 8 > self.DEFER_BYTES:
+            return self.local_gamma(), None
+        host = torch.empty(tuple(g.shape), dtype=torch.float64, pin_memory=True)
+        host.copy_(g if g.is_contiguous() else g.contiguous(), non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        return host.numpy(), ev
+
     def local_log_beta(self) -> np.ndarray:
         """[K, V] log of this rank's own class_word rows over the GLOBAL class totals (-100 floor):
         the per-worker ``<rank>.beta`` (README.md:121), final.beta = log(sum over ranks of exp)."""
@@ -1285,7 +1341,7 @@ class LDAEngine:
                 if w["gp"] is None:
                     self._launch_estep64(phase="estep")
                 else:
-                    self._launch_buckets(w["gp"], ent_base=w["e0"])
+                    self._launch_buckets(w["gp"], win=w)
                 for a in range(w["e0"], w["e1"], step):
                     b = min(w["e1"], a + step)
                     z[a:b] = torch.argmax(self.cphi[a - w["e0"]:b - w["e0"], :K], dim=1)
@@ -1306,7 +1362,9 @@ class LDAEngine:
         raise NotImplementedError(f"word assignments for backend {self.backend} / {self.precision}")
 
     def local_gamma(self) -> np.ndarray:
-        return self.gamma[:, :self.K].to("cpu", torch.float64, copy=True).numpy()
+        g = self.gamma[:, :self.K]
+        # padded topics (KS > K): made contiguous on the device, so the D2H copy is one block
+        return (g if g.is_contiguous() else g.contiguous()).to("cpu", torch.float64, copy=True).numpy()
 
     def gather_gamma(self) -> np.ndarray:
         g = self.local_gamma()
@@ -1399,18 +1457,23 @@ class LDAEngine:
         return res
 
 
-def _log_beta_host(cw: torch.Tensor, ct: torch.Tensor, rows: int = 1 << 20) -> np.ndarray:
+def _log_beta_host(cw: torch.Tensor, ct: torch.Tensor, elems: int = 1 << 25) -> np.ndarray:
     """[K, V] float64 host array of log(cw) - log(ct) (-100 floor where cw == 0), computed in blocks of
-    ``rows`` words: the device transient stays ~rows x K doubles instead of five V x K temporaries
-    (11-14 GB at the 30-day scale, K = 100)."""
+    topics: each block is transposed on the device into [k, V] rows, so it lands in its contiguous rows
+    of the host array with one copy (a block of words lands in K strided pieces), and the device
+    transient stays ~``elems`` doubles instead of V x K temporaries (3.6 GB each at config 5)."""
     V, K = cw.shape
     out = np.empty((K, V), np.float64)
+    if V == 0 or K == 0:
+        return out
     lct = torch.log(ct.to(torch.float64))
-    for a in range(0, V, rows):
-        b = min(V, a + rows)
-        c = cw[a:b].to(torch.float64)
-        lb = torch.where(c > 0, torch.log(c) - lct, torch.full_like(c, LOG_FLOOR))
-        out[:, a:b] = lb.T.cpu().numpy()
+    host = torch.from_numpy(out)
+    kb = max(1, min(K, elems // max(V, 1)))
+    for k0 in range(0, K, kb):
+        k1 = min(K, k0 + kb)
+        c = cw[:, k0:k1].T.to(torch.float64).contiguous()          # [k, V], transposed on the device
+        lb = torch.where(c > 0, torch.log(c) - lct[k0:k1, None], torch.full_like(c, LOG_FLOOR))
+        host[k0:k1].copy_(lb)                                       # one contiguous D2H copy
     return out
 
 

@@ -74,6 +74,17 @@ class AsyncWriter:
             raise self._err
 
 
+def _after(event, fn):
+    """fn, run once ``event`` (a queued device-to-host copy of its inputs, or None) has completed."""
+    if event is None:
+        return fn
+
+    def run(*args, **kw):
+        event.synchronize()
+        return fn(*args, **kw)
+    return run
+
+
 def save_checkpoint(outdir: str, eng: LDAEngine, iteration: int, L_old: float, history):
     """Collective under the sparse class_word exchange: every rank calls it (rank 0 writes)."""
     st = eng.state_arrays()
@@ -185,32 +196,42 @@ def estimate(corpus: Corpus, num_topics: int, alpha_init: float, settings: LDASe
 
     writer = AsyncWriter()
 
+    saved = {}          # the final save's host copies, reused for the result
+
     def on_save(tag, e):
         # collectives first, on every rank: global class_word (sparse exchange)
-        st = e.state_arrays()
-        lb = e.log_beta(torch.from_numpy(st["cw"]).to(e.cw.device))
-        g = None
-        if tag != "000":
-            g = e.local_gamma()
-            if multi:
-                part = os.path.join(outdir, f".{tag}.gamma.part{r}")
-                parts.append((os.path.join(outdir, f"{tag}.gamma"), part))
-                writer.submit(ldac.save_gamma, part, g)
+        ckpt = tag not in ("000", "final")
+        cwg = e.global_cw()
+        st = dict(cw=cwg.to("cpu", copy=True).numpy(),
+                  class_total=e.class_total.to("cpu", copy=True).numpy()) if ckpt else None
+        # host copies queued behind the device work; the writer waits for their events
+        lb, ev_lb = e.log_beta_deferred(cwg)
+        g, ev_g = e.local_gamma_deferred() if tag != "000" else (None, None)
+        if tag == "final":
+            for ev in (ev_lb, ev_g):
+                if ev is not None:
+                    ev.synchronize()
+            ev_lb = ev_g = None
+            saved.update(log_beta=lb, gamma=g)
+        if g is not None and multi:
+            part = os.path.join(outdir, f".{tag}.gamma.part{r}")
+            parts.append((os.path.join(outdir, f"{tag}.gamma"), part))
+            writer.submit(_after(ev_g, ldac.save_gamma), part, g)
         if write_rank_gamma and tag == "final":
-            writer.submit(ldac.save_gamma, os.path.join(outdir, f"{r}.gamma"), e.local_gamma())
+            writer.submit(ldac.save_gamma, os.path.join(outdir, f"{r}.gamma"), g)
             writer.submit(ldac.save_beta, os.path.join(outdir, f"{r}.beta"), e.local_log_beta())
         if not rank0:
             return
-        writer.submit(ldac.save_model, os.path.join(outdir, tag), lb, e.alpha)
+        writer.submit(_after(ev_lb, ldac.save_model), os.path.join(outdir, tag), lb, e.alpha)
         if g is not None and not multi:
-            writer.submit(ldac.save_gamma, os.path.join(outdir, f"{tag}.gamma"), g)
+            writer.submit(_after(ev_g, ldac.save_gamma), os.path.join(outdir, f"{tag}.gamma"), g)
         if tag not in ("000", "final"):
             # engine state is read now (host copies); only the file write is deferred
             ck = dict(log_beta=lb, alpha=np.float64(e.alpha), iteration=np.int64(int(tag)),
                       likelihood_old=np.float64(history[-1][0] if history else 0.0),
                       var_max_iter=np.int64(e.var_max_iter), history=np.asarray(history, np.float64).reshape(-1, 2),
                       **st)
-            writer.submit(_write_checkpoint, outdir, ck)
+            writer.submit(_after(ev_lb, _write_checkpoint), outdir, ck)
         if tag == "final":  # exact binary copy of what final.* hold as text (stage resume reloads this)
             extra = {} if multi else dict(gamma=g)
             writer.submit(np.savez, os.path.join(outdir, "final_model.npz"), log_beta=lb,
@@ -239,8 +260,9 @@ def estimate(corpus: Corpus, num_topics: int, alpha_init: float, settings: LDASe
     timing["em_s"] = round(res.seconds, 4)
     t_out = _now()
     res.likelihoods = history
-    res.log_beta = eng.log_beta()
-    res.gamma = eng.local_gamma()          # this rank's documents (all of them with one rank)
+    # this rank's documents (all of them with one rank); the final save already copied both
+    res.log_beta = saved["log_beta"] if "log_beta" in saved else eng.log_beta()
+    res.gamma = saved["gamma"] if saved.get("gamma") is not None else eng.local_gamma()
     res.doc_range = eng.doc_range
     timing["model_copies_s"] = round(_now() - t_out, 4)
     if write_word_assignments:

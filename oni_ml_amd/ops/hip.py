@@ -780,11 +780,14 @@ class GSPlan:
                  doc_range=None):
         import numpy as np
         L = np.asarray(lengths, dtype=np.int64)
-        order = np.argsort(-L, kind="stable").astype(np.int32)
-        # doc_range (d0, d1): only documents d0 <= d < d1 (one c.phi window of the engine)
+        # doc_range (d0, d1): only documents d0 <= d < d1 (one c.phi window of the engine); the stable
+        # sort of the range equals the range's documents in the stable sort of all of them
         self.doc_range = None if doc_range is None else (int(doc_range[0]), int(doc_range[1]))
-        if self.doc_range is not None:
-            order = order[(order >= self.doc_range[0]) & (order < self.doc_range[1])]
+        if self.doc_range is None:
+            order = np.argsort(-L, kind="stable").astype(np.int32)
+        else:
+            d0, d1 = self.doc_range
+            order = (d0 + np.argsort(-L[d0:d1], kind="stable")).astype(np.int32)
         # documents longer than split_min words: one document over several workgroups (gs_split);
         # default on for KS > 32 (the topic-group team kernels' chunk of a long document is bound
         # by one CU's row gathers), ONI_GS_SPLIT_MIN overrides (0: off)
