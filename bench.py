@@ -79,6 +79,13 @@ def build_corpus(args, rank, ctx, dev):
     return c, info
 
 
+def _settings(args):
+    from oni_ml_amd.models.lda.settings import LDASettings
+    st = LDASettings()
+    st.gs_updates = int(args.gs_updates)
+    return st
+
+
 def _e2e(args, dev):
     """Wall-clock of the full pipeline (ml_ops.sh YYYYMMDD flow TOL equivalent) on a synthetic day."""
     import shutil
@@ -116,6 +123,8 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--topics", type=int, default=20)
+    ap.add_argument("--gs-updates", type=int, default=0,
+                    help="U, gamma refreshes per sweep of the fp64 engine (0: 32; > 32 needs K > 32)")
     ap.add_argument("--events", type=int, default=None, help="events per GPU (default: flow 1M, dns 2M)")
     ap.add_argument("--corpus", choices=["flow", "dns", "planted"], default="flow",
                     help="flow: BASELINE headline (1-day netflow); dns: BASELINE config 4 (1-day DNS)")
@@ -153,7 +162,7 @@ def main():
     dist = ctx if world > 1 else None
     # weak scaling: each rank's corpus is its own document shard of the N-day corpus
     local = args.scaling == "weak"
-    eng = LDAEngine(corpus, args.topics, LDASettings(), backend=args.backend, device=dev, dist=dist, seed=args.seed,
+    eng = LDAEngine(corpus, args.topics, _settings(args), backend=args.backend, device=dev, dist=dist, seed=args.seed,
                     local_shard=local, streams=args.streams, precision=args.precision)
     eng.init_random()
     docs_global = eng.global_docs
@@ -200,7 +209,7 @@ def main():
         ctx.barrier()
         _sync(dev)
         t2 = time.perf_counter()
-        eng2 = LDAEngine(corpus, args.topics, LDASettings(), backend=args.backend, device=dev, dist=dist,
+        eng2 = LDAEngine(corpus, args.topics, _settings(args), backend=args.backend, device=dev, dist=dist,
                          seed=args.seed + 1, local_shard=local, precision=args.precision)
         _sync(dev)
         t_setup = time.perf_counter() - t2

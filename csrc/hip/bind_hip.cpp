@@ -147,7 +147,7 @@ PYBIND11_MODULE(_onihip, m) {
 
 
   // ---------------------------------------------- fp64 block Gauss-Seidel ---
-  m.def("gs_umax", []() { return oni::kGsUMax; });
+  m.def("gs_umax", [](int KS) { return KS > 0 ? oni::gs_umax(KS) : oni::kGsUMax; }, py::arg("KS") = 0);
   m.def("gs_tiny_max", [](int KS) { return oni::gs_tiny_max(KS); });
   m.def("gs_estep", [](u doc_ptr, u word_idx, u counts, u order, int n_items, u beta, int K, int KS, int gs_updates,
                        u params, u gamma, u cphi, u lik, u alpha_ss, u iters, int variant, u stream, u dbg) {

@@ -190,7 +190,8 @@ void launch_lda_mstep_control(const float* cw, const double* class_total, float*
 // after every chunk of W = ceil(n / U) words (U = gs_updates refreshes per sweep; a
 // document of n <= U words is lda-c's literal per-word schedule).  The CPU oracle is
 // csrc/native/lda_ref.cpp lda_inference(..., gs_updates).
-constexpr int kGsUMax = 32;          // largest U (chunk tables live in LDS)
+constexpr int kGsUMax = 32;          // largest U with the chunk tables in LDS
+constexpr int kGsUMaxWide = 4096;    // largest U at KS > 32 (chunk tables in the c*phi rows, gs_team GM)
 enum GsVariant : int {
   kGsTiny = 0,     // TG lanes per document, literal schedule, n <= gs_tiny_max(KS)
   kGsTeam1 = 1,    // one wave per document
@@ -206,7 +207,7 @@ struct GSArgs {
   int n_items;
   const double* beta;     // [V][KS] p(w|z) = exp(log_prob_w), word-major; 0 for padding topics
   int K;
-  int gs_updates;         // U, 1 <= U <= kGsUMax
+  int gs_updates;         // U, 1 <= U <= gs_umax(KS)
   const double* params;   // {alpha, lgamma(K a) - K lgamma(a), VAR_MAX_ITER, VAR_CONVERGED, done, ...}
   double* gamma;          // [D][KS]
   double* cphi;           // [nnz][KS] c_n * phi_nk of the final sweep (sufficient-statistic input)
@@ -220,6 +221,7 @@ struct GSArgs {
 };
 void launch_gs_estep(const GSArgs& a, int variant, int KS, hipStream_t s);
 int gs_tiny_max(int KS);   // longest document of the kGsTiny kernel
+int gs_umax(int KS);       // largest gs_updates the E-step accepts at row stride KS (split: kGsUMax)
 // One long document over s.seg_count[b] workgroups (8 waves each): every chunk is cut into
 // that many word ranges whose partials are exchanged as tagged granules (2 per double,
 // s.xchg = [2][n_blocks][2 (KS + 1)]); s.seg_words is unused.  Every segment of a launch

@@ -596,22 +596,24 @@ __device__ __forceinline__ void stream_tail(const double* __restrict__ beta, con
 
 // MINW: minimum waves per SIMD requested from the register allocator (the LDS-free one-wave team
 // at K > 32 is latency-bound on its per-word refresh chains; ONI_TEAM1_WAVES selects 1 / 3 / 4)
-template <int KS, int NW, int MINW = 1>
+template <int KS, int NW, int MINW = 1, bool GMT = false>
 __global__ __launch_bounds__(team_threads(KS, NW), MINW) void gs_team(GSArgs a) {
   using T = TeamShape<KS, NW>;
   constexpr int DPB = T::DPB, NTD = T::NTD, TG = T::TG, KPL = T::KPL, NSW = T::NSW, LSW = T::LSW, NS = T::NS,
                 TO = T::TO, RMAX = T::RMAX;
-  // GM (one-wave documents, KS > 32): the chunk tables live in the document's own c*phi rows
-  // instead of LDS (2 x 32 x KS doubles of LDS held one wave per CU to ~3 waves): C_j in row
-  // j W, the E chunk j used in row j W + 1 (chunks of >= 2 words).  A one-word chunk's C_j IS
+  // GM (one-wave documents at KS > 32, and every team size when GMT: U > kGsUMax refreshes per
+  // sweep): the chunk tables live in the document's own c*phi rows instead of LDS (2 x 32 x KS
+  // doubles of LDS held one wave per CU to ~3 waves; U chunks of them do not fit at all): C_j in
+  // row j W, the E chunk j used in row j W + 1 (chunks of >= 2 words).  A one-word chunk's C_j IS
   // that word's c*phi (E_j r b), so documents of <= U words need no final pass at all.
-  constexpr bool GM = (NW == 1 && KS > 32);
+  constexpr bool GM = GMT || (NW == 1 && KS > 32);
+  static_assert(!GMT || KS > 32, "U > kGsUMax: KS > 32 team kernels only");
   constexpr int UT = GM ? 1 : kGsUMax;
   __shared__ double sC[DPB][UT][KS];         // chunk contributions (previous sweep)
   __shared__ double sEt[DPB][UT][KS];        // E each chunk used (final pass)
   __shared__ double sE[DPB][KS];             // current E, broadcast
   __shared__ double sRed[DPB][NW][KS];       // per-wave slot sums
-  __shared__ double sCs[DPB][kGsUMax];       // chunk count sums
+  __shared__ double sCs[DPB][UT];            // chunk count sums (GM: straight into the C_j rows)
   __shared__ double sScal[DPB][NW][4];       // per-wave sweep partials
   if (a.params[kParamDone] != 0.0) return;
   const int t = threadIdx.x % NTD, ds = threadIdx.x / NTD;
@@ -629,7 +631,7 @@ __global__ __launch_bounds__(team_threads(KS, NW), MINW) void gs_team(GSArgs a) 
   const int s0 = a.doc_ptr[d], n = a.doc_ptr[d + 1] - s0;
   const int U = a.gs_updates;
   const int W = n > 0 ? (n + U - 1) / U : 1;
-  const int nch = (n + W - 1) / W;           // <= U <= kGsUMax (host-checked)
+  const int nch = (n + W - 1) / W;           // <= U (host-checked: <= kGsUMax unless GM)
   const int nact = min(NW, (W + NSW - 1) / NSW);   // waves holding words of a chunk
   const bool active = wv < nact;
   const int* __restrict__ wrow = a.word_idx + s0;
@@ -637,14 +639,38 @@ __global__ __launch_bounds__(team_threads(KS, NW), MINW) void gs_team(GSArgs a) 
   double(*C)[KS] = sC[ds];
   double(*Et)[KS] = sEt[ds];
   double* E_ = sE[ds];
-  double* Cs = sCs[ds];
-  for (int j = t; j < nch; j += NTD) Cs[j] = 0.0;
-  team_sync<NW>();
-  // integer counts: the LDS double atomics are exact in any order
-  for (int p = t; p < n; p += NTD) atomicAdd(&Cs[p / W], (double)crow[p]);
-  team_sync<NW>();
   double total = 0.0;
-  for (int j = 0; j < nch; ++j) total += Cs[j];
+  if constexpr (GM) {
+    // a thread per chunk: its count sum Cs_j, and C_j = Cs_j / K straight into row j W (any number
+    // of chunks); the document total from the per-thread sums (integer counts: exact in any order)
+    double part = 0.0;
+    for (int j = t; j < nch; j += NTD) {
+      const int n0 = j * W, n1 = min(n, n0 + W);
+      double cs = 0.0;
+      for (int p = n0; p < n1; ++p) cs += (double)crow[p];
+      part += cs;
+      double* row = a.cphi + (size_t)(s0 + n0) * KS;
+      for (int k = 0; k < KS; ++k) row[k] = k < K ? cs / K : 0.0;
+    }
+    part = group_sum<64>(part);
+    if constexpr (NW == 1) {
+      total = part;
+    } else {
+      if (lane == 0) sScal[ds][wv][0] = part;
+      __syncthreads();   // also orders the C_j row stores before the topic owners read them
+#pragma unroll
+      for (int v = 0; v < NW; ++v) total += sScal[ds][v][0];
+      __syncthreads();
+    }
+  } else {
+    double* Cs = sCs[ds];
+    for (int j = t; j < nch; j += NTD) Cs[j] = 0.0;
+    team_sync<NW>();
+    // integer counts: the LDS double atomics are exact in any order
+    for (int p = t; p < n; p += NTD) atomicAdd(&Cs[p / W], (double)crow[p]);
+    team_sync<NW>();
+    for (int j = 0; j < nch; ++j) total += Cs[j];
+  }
   const double g0 = alpha + total / K;
   const double m = psi_only(g0);
   double gam[TO], psi[TO], lps[TO];
@@ -656,14 +682,13 @@ __global__ __launch_bounds__(team_threads(KS, NW), MINW) void gs_team(GSArgs a) 
     lps[o] = 0.0;
     if (k < KS) {
       E_[k] = k < K ? 1.0 : 0.0;
-      if constexpr (GM) {
-        for (int j = 0; j < nch; ++j) a.cphi[(size_t)(s0 + j * W) * KS + k] = k < K ? Cs[j] / K : 0.0;
-      } else {
-        for (int j = 0; j < nch; ++j) C[j][k] = k < K ? Cs[j] / K : 0.0;
+      if constexpr (!GM) {
+        for (int j = 0; j < nch; ++j) C[j][k] = k < K ? sCs[ds][j] / K : 0.0;
       }
     }
   }
-  // GM: C of the next chunk, loaded one chunk ahead (this thread wrote it: same-address order)
+  // GM: C of the next chunk, loaded one chunk ahead (NW == 1: this wave wrote it, same-address
+  // order; NW > 1: behind the __syncthreads above)
   double Cn[TO];
   if constexpr (GM) {
 #pragma unroll
@@ -869,6 +894,38 @@ __global__ __launch_bounds__(team_threads(KS, NW), MINW) void gs_team(GSArgs a) 
     a.iters[d] = it;
   }
   // final pass: c_n phi_nk = E_jk b_nk r_n with the final sweep's chunk E (same P as the sweep)
+  if constexpr (GM && NW > 1) {
+    // every wave reads E_j from row n0 + 1 before any wave overwrites the chunk's rows: one
+    // workgroup barrier per chunk, so the waves without words stay in the loop
+    __syncthreads();   // the last sweep's C_j / E_j row stores (topic owners) before the reads
+    for (int j = 0; j < nch; ++j) {
+      const int n0 = j * W, n1 = min(n, n0 + W);
+      if (n1 - n0 < 2) continue;           // team-uniform: a one-word chunk's row is its c*phi
+      const double* er = a.cphi + (size_t)(s0 + n0 + 1) * KS;
+      double E[KPL];
+#pragma unroll
+      for (int i = 0; i < KPL; ++i) E[i] = (q + TG * i < KS) ? er[q + TG * i] : 0.0;
+      __syncthreads();
+      if (active) {
+        for (int p = n0 + slot; p < n1; p += NS) {
+          const double* brow = a.beta + (size_t)wrow[p] * KS;
+          const double c = (double)crow[p];
+          double b[KPL];
+#pragma unroll
+          for (int i = 0; i < KPL; ++i) b[i] = (q + TG * i < KS) ? brow[q + TG * i] : 0.0;
+          double pp = 0.0;
+#pragma unroll
+          for (int i = 0; i < KPL; ++i) pp = fma(E[i], b[i], pp);
+          const double r = c * drcp(bits_sum<LSW, 6>(pp));
+          double* row = a.cphi + (size_t)(s0 + p) * KS;
+#pragma unroll
+          for (int i = 0; i < KPL; ++i)
+            if (q + TG * i < KS) __builtin_nontemporal_store(E[i] * b[i] * r, &row[q + TG * i]);
+        }
+      }
+    }
+    return;
+  }
   if (!active) return;
   for (int j = 0; j < nch; ++j) {
     const int n0 = j * W, n1 = min(n, n0 + W);
@@ -1945,7 +2002,10 @@ __global__ __launch_bounds__(wteam_threads(NW)) void gs_wteam(GSArgs a) {
 //    topic wave refreshes, off the chunk's critical path.
 // Arithmetic per word and per topic is that of gs_wteam (the likelihood's lw partial sums are
 // grouped by wave, so the two kernels agree to rounding, not bitwise).
-template <int KS, int NW, int RMAX>
+// EP (early prefetch, ONI_GS_EARLY_PREFETCH=EP): rounds u < EP of the next chunk's rows are gathered
+// into bc[u] as soon as the axpy of round u has consumed them -- before the topic sums and the
+// arrival -- so the address unit works beside the reduction; the other rounds after the arrival.
+template <int KS, int NW, int RMAX, int EP = 0>
 __global__ __launch_bounds__((NW + 1) * 64) void gs_wsteam(GSArgs a) {
   static_assert(KS <= 32 && KS % 2 == 0, "word team: KS <= 32");
   constexpr int NTD = (NW + 1) * 64, NS = NW * 64;
@@ -2139,6 +2199,15 @@ __global__ __launch_bounds__((NW + 1) * 64) void gs_wsteam(GSArgs a) {
           const double r = cr[u] * drcp(P[u]);
 #pragma unroll
           for (int kk = 0; kk < KS; ++kk) acc[kk] = fma(r, bc[u][kk], acc[kk]);
+          if (u < EP) {   // bc[u] is free: the next chunk's round u (ids already here)
+            __builtin_amdgcn_sched_barrier(0);   // keep the gather below the axpy (no second row set)
+            if ((vn >> u) & 1u) {
+              load_row_full<KS>(a.beta, wn[u], bc[u]);
+            } else {
+#pragma unroll
+              for (int kk = 0; kk < KS; ++kk) bc[u][kk] = 0.0;
+            }
+          }
         }
         for (int p = n0 + t + RMAX * NS; p < n1; p += NS) {   // beyond the prefetched rounds
           double b[1][KS];
@@ -2164,7 +2233,19 @@ __global__ __launch_bounds__((NW + 1) * 64) void gs_wsteam(GSArgs a) {
           cc[r] = cn[r];
         }
         vc = vn;
-        load_rows(wc, vc);
+        if constexpr (EP == 0) {
+          load_rows(wc, vc);
+        } else if (active) {
+#pragma unroll
+          for (int r = EP; r < RMAX; ++r) {
+            if ((vc >> r) & 1u) {
+              load_row_full<KS>(a.beta, wc[r], bc[r]);
+            } else {
+#pragma unroll
+              for (int kk = 0; kk < KS; ++kk) bc[r][kk] = 0.0;
+            }
+          }
+        }
         load_ids(j2, wn, cn, vn);
         tick(2);
 #pragma unroll
@@ -2435,6 +2516,8 @@ static void gs_estep_ks(const GSArgs& a, int variant, hipStream_t s) {
         else
           hipLaunchKernelGGL((gs::gs_wteam<KS, 4, 1>), dim3(a.n_items), dim3(256), 0, s, a);
       }
+      else if (a.gs_updates > kGsUMax)
+        hipLaunchKernelGGL((gs::gs_team<KS, 4, 1, true>), dim3(a.n_items), dim3(256), 0, s, a);
       else
         hipLaunchKernelGGL((gs::gs_team<KS, 4>), dim3(a.n_items), dim3(256), 0, s, a);
       break;
@@ -2446,7 +2529,14 @@ static void gs_estep_ks(const GSArgs& a, int variant, hipStream_t s) {
         static const int bnw = std::getenv("ONI_GS_BIG_NW") ? std::atoi(std::getenv("ONI_GS_BIG_NW")) : 7;
         // (a dynamic-LDS pad keeping other buckets off the longest-document CUs measured no change:
         // 2.175 vs 2.175 ms per EM iteration, profiles/r3_tuning_log.md)
-        if (bnw == 7)
+        // ONI_GS_EARLY_PREFETCH: next-chunk rounds gathered before the arrival (1, the default: 2.13-2.14
+        // vs 2.17-2.18 ms per EM iteration, 3 A/B rounds; 2 spills 192 B: 3.27 ms; 0 = after it)
+        static const int ep = std::getenv("ONI_GS_EARLY_PREFETCH") ? std::atoi(std::getenv("ONI_GS_EARLY_PREFETCH")) : 1;
+        if (bnw == 7 && ep == 1)
+          hipLaunchKernelGGL((gs::gs_wsteam<KS, 7, 2, 1>), dim3(a.n_items), dim3(512), 0, s, a);
+        else if (bnw == 7 && ep >= 2)
+          hipLaunchKernelGGL((gs::gs_wsteam<KS, 7, 2, 2>), dim3(a.n_items), dim3(512), 0, s, a);
+        else if (bnw == 7)
           hipLaunchKernelGGL((gs::gs_wsteam<KS, 7, 2>), dim3(a.n_items), dim3(512), 0, s, a);
         else if (bnw == 3)
           hipLaunchKernelGGL((gs::gs_wsteam<KS, 3, 4>), dim3(a.n_items), dim3(256), 0, s, a);
@@ -2459,6 +2549,8 @@ static void gs_estep_ks(const GSArgs& a, int variant, hipStream_t s) {
         else
           hipLaunchKernelGGL((gs::gs_wteam<KS, 8, 2>), dim3(a.n_items), dim3(512), 0, s, a);
       }
+      else if (a.gs_updates > kGsUMax)
+        hipLaunchKernelGGL((gs::gs_team<KS, 8, 1, true>), dim3(a.n_items), dim3(512), 0, s, a);
       else
         hipLaunchKernelGGL((gs::gs_team<KS, 8>), dim3(a.n_items), dim3(512), 0, s, a);
       break;
@@ -2468,9 +2560,12 @@ static void gs_estep_ks(const GSArgs& a, int variant, hipStream_t s) {
   ONI_HIP_CHECK(hipGetLastError());
 }
 
+int gs_umax(int KS) { return KS > 32 ? kGsUMaxWide : kGsUMax; }
+
 void launch_gs_estep(const GSArgs& a, int variant, int KS, hipStream_t s) {
-  if (a.gs_updates < 1 || a.gs_updates > kGsUMax)
-    throw std::runtime_error("gs_estep: gs_updates must be in [1, " + std::to_string(kGsUMax) + "]");
+  if (a.gs_updates < 1 || a.gs_updates > gs_umax(KS))
+    throw std::runtime_error("gs_estep: gs_updates must be in [1, " + std::to_string(gs_umax(KS)) + "] at KS " +
+                             std::to_string(KS));
   if (!a.params) throw std::runtime_error("gs_estep: params block required");
   switch (KS) {
 #define ONI_KS(X)                       \

@@ -37,6 +37,25 @@ def _common_lda_args(ap):
     ap.add_argument("--backend", default="auto", choices=["auto", "hip", "torch", "cpu"])
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--verbose", action="store_true")
+    ap.add_argument("--gs-updates", type=int, default=None,
+                    help="U, gamma refreshes per document sweep of the fp64 GPU engine (default 32; up to 4096 "
+                         "at K > 32; lda-c's per-word schedule is U >= document length -- "
+                         "profiles/r3_precision_parity.md gives the U per K that matches lda-c)")
+    ap.add_argument("--lag", type=int, default=None, help="period of the %%03d model files (lda-c: 5; 0: only 000 "
+                                                          "and final)")
+    ap.add_argument("--cphi-gb", type=float, default=None,
+                    help="HBM budget of the per-entry c.phi rows: larger corpora run the E-step in document windows")
+
+
+def _apply_lda_args(a, st):
+    """--gs-updates / --lag / --cphi-gb onto an LDASettings (and the engine's environment)."""
+    if a.gs_updates is not None:
+        st.gs_updates = int(a.gs_updates)
+    if a.lag is not None:
+        st.lag = int(a.lag)
+    if a.cphi_gb is not None:
+        os.environ["ONI_CPHI_GB"] = str(a.cphi_gb)
+    return st
 
 
 def clean_workdir(lpath: str):
@@ -96,6 +115,7 @@ def cmd_ml_ops(argv):
                       cuts=a.cuts, hdfs=a.hdfs or None, hadoop=a.hadoop)
     if a.settings:
         cfg.settings = LDASettings.load(a.settings)
+    _apply_lda_args(a, cfg.settings)
     cfg.validate()
     from .pipeline import run
     from .pipeline.runner import RunLock
@@ -146,7 +166,7 @@ def cmd_lda(argv):
         from .parallel import dist as D
         ctx = D.init_from_env()
         corpus = ldac.read_model_dat(a.data)
-        st = LDASettings.load(a.settings)
+        st = _apply_lda_args(a, LDASettings.load(a.settings))
         res = estimate(corpus, int(a.k), float(a.alpha), st, a.start, a.directory, backend=a.backend,
                        device=ctx.device, dist=ctx if ctx.active else None, seed=a.seed, resume=a.resume,
                        write_word_assignments=a.word_assignments, verbose=True)

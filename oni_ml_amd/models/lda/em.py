@@ -384,9 +384,11 @@ class LDAEngine:
     def gs_updates(self) -> int:
         """U: gamma refreshes per sweep of the fp64 engine (settings.gs_updates, 0 = the default 32)."""
         from ...ops import hip as H
-        u = int(self.settings.gs_updates) or min(32, H.gs_umax())
-        if not 1 <= u <= H.gs_umax():
-            raise ValueError(f"gs_updates={u}: the GPU engine supports 1..{H.gs_umax()}")
+        KS = H.padded_topics(self.K)
+        u = int(self.settings.gs_updates) or min(32, H.gs_umax(KS))
+        if not 1 <= u <= H.gs_umax(KS):
+            raise ValueError(f"gs_updates={u}: the GPU engine supports 1..{H.gs_umax(KS)} at K={self.K} "
+                             f"(more than {H.gs_umax()} needs K > 32)")
         return u
 
     def _init_gs64(self, corpus: Corpus):

@@ -535,8 +535,10 @@ GS_TINY, GS_TEAM1, GS_TEAM4, GS_TEAM8, GS_SMALL = range(5)
 GS_SMALL_MAX = 64   # csrc/hip/lda_gs64.hip kGsSmallMax
 
 
-def gs_umax() -> int:
-    return int(lib().gs_umax())
+def gs_umax(KS: int = 0) -> int:
+    """Largest U (gamma refreshes per sweep) of the fp64 engine: 32 with the chunk tables in LDS
+    (KS <= 32, and the split-document kernel), more at KS > 32 (tables in the c.phi rows)."""
+    return int(lib().gs_umax(int(KS)))
 
 
 def gs_tiny_max(KS: int) -> int:
@@ -568,8 +570,8 @@ def gs_estep(doc_ptr, word_idx, counts, order, beta, K, gs_updates, params, gamm
         raise ValueError(f"beta row stride {KS} has no compiled kernel")
     if not (0 < K <= KS):
         raise ValueError("K out of range")
-    if not (1 <= int(gs_updates) <= gs_umax()):
-        raise ValueError(f"gs_updates must be in [1, {gs_umax()}]")
+    if not (1 <= int(gs_updates) <= gs_umax(KS)):
+        raise ValueError(f"gs_updates must be in [1, {gs_umax(KS)}] at KS {KS}")
     if variant not in (GS_TINY, GS_TEAM1, GS_TEAM4, GS_TEAM8, GS_SMALL):
         raise ValueError(f"unknown gs variant {variant}")
     dev = beta.device
@@ -793,6 +795,8 @@ class GSPlan:
         # by one CU's row gathers), ONI_GS_SPLIT_MIN overrides (0: off)
         if split_min is None:
             split_min = int(os.environ.get("ONI_GS_SPLIT_MIN", "4096" if KS > 32 else "0"))
+        if int(gs_updates) > gs_umax():
+            split_min = 0       # the split kernel keeps its chunk tables in LDS: U <= 32 only
         self.split = None
         if split_min > 0 and (L > split_min).any():
             m = L[order] > split_min

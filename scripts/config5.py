@@ -40,6 +40,7 @@ def main():
     ap.add_argument("--workdir", default=os.path.join(os.environ.get("TMPDIR", "/tmp"), "oni_config5"))
     ap.add_argument("--out", default="gpurun_out/config5.json")
     ap.add_argument("--keep", action="store_true")
+    ap.add_argument("--gs-updates", type=int, default=0, help="U of the fp64 engine (0: 32)")
     ap.add_argument("--cphi-gb", type=float, default=None,
                     help="HBM budget of the engine's c.phi rows (ONI_CPHI_GB): E-step in document windows")
     a = ap.parse_args()
@@ -66,6 +67,7 @@ def main():
         f" in {gen_s:.1f}s")
 
     st = LDASettings(em_max_iter=a.em_iters)
+    st.gs_updates = a.gs_updates
     st.lag = a.lag          # each %03d save of a 6M-document gamma is ~8 GB of text
     cfg = RunConfig(fdate="20160122", dsource="flow", lpath=lpath, flow_path=inp, topics=a.topics, backend=a.backend,
                     threads=a.threads, write_doc_wc=False, verbose=True, settings=st,
@@ -95,7 +97,7 @@ def main():
                flagged=summary.get("scored"), lda_metrics={k: v for k, v in m.items() if not isinstance(v, list)},
                peak_hbm_gb=(round(torch.cuda.max_memory_allocated() / 2**30, 2) if dev.type == "cuda" else None),
                device=(torch.cuda.get_device_name(0) if dev.type == "cuda" else "cpu"), backend=a.backend,
-               threads=a.threads, lag=a.lag, cphi_gb=a.cphi_gb, output_gb=round(_du(lpath) / 1e9, 3), data="synthetic (synth/flow.py, scaled address pool)")
+               threads=a.threads, lag=a.lag, cphi_gb=a.cphi_gb, gs_updates=a.gs_updates, output_gb=round(_du(lpath) / 1e9, 3), data="synthetic (synth/flow.py, scaled address pool)")
     os.makedirs(os.path.dirname(os.path.abspath(a.out)), exist_ok=True)
     with open(a.out, "w") as f:
         json.dump(rec, f, indent=1, default=str)

@@ -61,7 +61,9 @@ def _rel(a, b, floor):
 
 
 @pytest.mark.parametrize("K,U,vconv", [(20, 32, -1e30), (20, 8, -1e30), (3, 32, -1e30), (24, 32, -1e30),
-                                       (50, 32, -1e30), (100, 16, -1e30), (128, 32, -1e30), (20, 32, 1e-6)])
+                                       (50, 32, -1e30), (100, 16, -1e30), (128, 32, -1e30), (20, 32, 1e-6),
+                                       # U > 32 at K > 32: chunk tables in the c.phi rows, no split kernel
+                                       (50, 64, -1e30), (100, 256, -1e30), (64, 1024, -1e30), (50, 128, 1e-6)])
 def test_estep_matches_oracle(K, U, vconv):
     c = _edge_corpus(seed=K + U)
     lb = _log_beta(c.num_terms, K, seed=K)
@@ -341,3 +343,30 @@ def test_cphi_windows_em_run():
     assert L0.shape == L1.shape
     assert np.max(np.abs(L1 - L0) / np.abs(L0)) < 1e-12
     assert abs(a1 - a0) <= 1e-12 * a0
+
+
+@pytest.mark.parametrize("K,U", [(50, 128), (100, 64)])
+def test_final_pass_word_assignments_large_u(K, U):
+    """The final pass with U > 32 (chunk tables in the c.phi rows, 4- and 8-wave teams read E_j from
+    row n0 + 1 before the chunk's rows are overwritten) against the oracle."""
+    c = _edge_corpus(seed=17, max_len=6000)
+    alpha = 0.6
+    lb = _log_beta(c.num_terms, K, seed=3)
+    st = LDASettings(var_max_iter=6, var_converged=-1e30)
+    st.gs_updates = U
+    eng = LDAEngine(c, K, st, backend="hip", seed=0, precision="fp64")
+    assert eng.gs_plan.split is None
+    eng.init_from_model(lb, alpha)
+    z = eng.word_assignments()
+    ref = native.lib().lda_assign_ldac(c.doc_ptr, c.word_idx, c.counts.astype(np.float64), np.ascontiguousarray(lb),
+                                       alpha, st.var_max_iter, st.var_converged, gs_updates=U)
+    assert np.array_equal(z, ref)
+
+
+def test_large_u_needs_wide_topics():
+    """U > 32 at K <= 32 is refused (those kernels keep the chunk tables in LDS)."""
+    c = planted_corpus(num_docs=50, num_terms=60, num_topics=3, seed=2)
+    st = LDASettings()
+    st.gs_updates = 64
+    with pytest.raises(ValueError, match="needs K > 32"):
+        LDAEngine(c, 20, st, backend="hip", seed=0, precision="fp64")
