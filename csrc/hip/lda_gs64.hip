@@ -2510,9 +2510,14 @@ static void gs_estep_ks(const GSArgs& a, int variant, hipStream_t s) {
     }
     case kGsTeam4:
       if constexpr (KS <= 32) {
-        static const int mnw = std::getenv("ONI_GS_MID_NW") ? std::atoi(std::getenv("ONI_GS_MID_NW")) : 3;
+        // 1 (default): one wave per document, a word per lane, in-wave refresh -- 2.128 / 2.129 / 2.143 vs
+        // 2.136 / 2.141 / 2.144 ms per EM iteration for 3 (3 word waves + a topic wave), 3 A/B rounds:
+        // a quarter of the waves for the same chains leaves the CUs to the other buckets
+        static const int mnw = std::getenv("ONI_GS_MID_NW") ? std::atoi(std::getenv("ONI_GS_MID_NW")) : 1;
         if (mnw == 3)   // 3 word waves + the topic wave
           hipLaunchKernelGGL((gs::gs_wsteam<KS, 3, 1>), dim3(a.n_items), dim3(256), 0, s, a);
+        else if (mnw == 1)   // one wave per document, a word per lane, in-wave refresh
+          hipLaunchKernelGGL((gs::gs_wteam<KS, 1, 1>), dim3(a.n_items), dim3(64), 0, s, a);
         else
           hipLaunchKernelGGL((gs::gs_wteam<KS, 4, 1>), dim3(a.n_items), dim3(256), 0, s, a);
       }

@@ -1305,6 +1305,17 @@ class LDAEngine:
         ev.record()
         return host.numpy(), ev
 
+    def host_copy_deferred(self, t: torch.Tensor):
+        """(host array, event or None): a copy of device tensor ``t`` queued on the current stream into a
+        pinned buffer (valid once ``event`` completed); blocking for host tensors or above DEFER_BYTES."""
+        if t.device.type != "cuda" or t.numel() * t.element_size() > self.DEFER_BYTES:
+            return t.to("cpu", copy=True).numpy(), None
+        host = torch.empty(tuple(t.shape), dtype=t.dtype, pin_memory=True)
+        host.copy_(t if t.is_contiguous() else t.contiguous(), non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record()
+        return host.numpy(), ev
+
     def local_gamma_deferred(self):
         """(host [D_local, K] gamma, event or None): ``local_gamma`` with a queued pinned copy."""
         g = self.gamma[:, :self.K]

@@ -202,8 +202,12 @@ def estimate(corpus: Corpus, num_topics: int, alpha_init: float, settings: LDASe
         # collectives first, on every rank: global class_word (sparse exchange)
         ckpt = tag not in ("000", "final")
         cwg = e.global_cw()
-        st = dict(cw=cwg.to("cpu", copy=True).numpy(),
-                  class_total=e.class_total.to("cpu", copy=True).numpy()) if ckpt else None
+        ev_st = None
+        st = None
+        if ckpt:   # the checkpoint's exact statistics, copied behind the device work like the model
+            cw_h, _ = e.host_copy_deferred(cwg)
+            ct_h, ev_st = e.host_copy_deferred(e.class_total)     # queued after cw: its event covers both
+            st = dict(cw=cw_h, class_total=ct_h)
         # host copies queued behind the device work; the writer waits for their events
         lb, ev_lb = e.log_beta_deferred(cwg)
         g, ev_g = e.local_gamma_deferred() if tag != "000" else (None, None)
@@ -231,7 +235,7 @@ def estimate(corpus: Corpus, num_topics: int, alpha_init: float, settings: LDASe
                       likelihood_old=np.float64(history[-1][0] if history else 0.0),
                       var_max_iter=np.int64(e.var_max_iter), history=np.asarray(history, np.float64).reshape(-1, 2),
                       **st)
-            writer.submit(_after(ev_lb, _write_checkpoint), outdir, ck)
+            writer.submit(_after(ev_st, _after(ev_lb, _write_checkpoint)), outdir, ck)
         if tag == "final":  # exact binary copy of what final.* hold as text (stage resume reloads this)
             extra = {} if multi else dict(gamma=g)
             writer.submit(np.savez, os.path.join(outdir, "final_model.npz"), log_beta=lb,
