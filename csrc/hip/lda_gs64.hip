@@ -2072,6 +2072,18 @@ __global__ __launch_bounds__((NW + 1) * 64) void gs_wsteam(GSArgs a) {
     __builtin_amdgcn_s_setprio(3);   // its chain is the critical path; the word waves wait on it
     const int k = lane;
     int want = 0;
+    // dbg[8..11] (the int64[16] timer of gs_estep): this wave's cycles waiting for the arrivals,
+    // summing + refreshing, and at barrier B, summed over chunks
+    const bool ttimer = a.dbg != nullptr && blockIdx.x == 0 && lane == 0;
+    long long tph[4] = {0, 0, 0, 0};
+    long long ttc = ttimer ? clock64() : 0;
+    auto ttick = [&](int i) {
+      if (ttimer) {
+        const long long x = clock64();
+        tph[i] += x - ttc;
+        ttc = x;
+      }
+    };
     double gam = k < K ? g0 : 0.0, psi = m, lps = 0.0;
     if (k < KS) {
       E_[k] = k < K ? 1.0 : 0.0;
@@ -2084,9 +2096,11 @@ __global__ __launch_bounds__((NW + 1) * 64) void gs_wsteam(GSArgs a) {
       for (int j = 0; j < nch; ++j) {
         // (A) the nact word waves' topic sums of chunk j are in sRed
         want += nact;
+        ttick(3);
         while (__hip_atomic_load(&arrive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < want)
           __builtin_amdgcn_s_sleep(1);
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+        ttick(0);
         if (k < KS) {
           double S = 0.0;
 #pragma unroll
@@ -2103,7 +2117,9 @@ __global__ __launch_bounds__((NW + 1) * 64) void gs_wsteam(GSArgs a) {
           Et[j][k] = Eo;
           E_[k] = En;
         }
+        ttick(1);
         lds_barrier();   // (B) E of chunk j + 1 published
+        ttick(2);
       }
       const bool own = k < K;
       const double w1 = group_sum<64>(own ? gam : 0.0), w2 = group_sum<64>(own ? lgamma_pos(gam) : 0.0);
@@ -2115,6 +2131,8 @@ __global__ __launch_bounds__((NW + 1) * 64) void gs_wsteam(GSArgs a) {
       }
       sweep_end();
     }
+    if (ttimer)
+      for (int i = 0; i < 4; ++i) a.dbg[8 + i] = tph[i];
     const double ps = group_sum<64>(k < K ? psi : 0.0);
     if (k < KS) a.gamma[(size_t)d * KS + k] = gam;
     if (lane == 0) {

@@ -587,7 +587,7 @@ def gs_estep(doc_ptr, word_idx, counts, order, beta, K, gs_updates, params, gamm
         _chk(lik, torch.float64, "lik", (D,), dev),
         _chk(alpha_ss, torch.float64, "alpha_ss", (D,), dev),
         _chk(iters, torch.int32, "iters", (D,), dev),
-        int(variant), _stream(), 0 if dbg is None else _chk(dbg, torch.int64, "dbg", (8,), dev),
+        int(variant), _stream(), 0 if dbg is None else _chk(dbg, torch.int64, "dbg", (16,), dev),
     ]
     if order.numel() == 0:
         return
@@ -793,8 +793,12 @@ class GSPlan:
         # documents longer than split_min words: one document over several workgroups (gs_split);
         # default on for KS > 32 (the topic-group team kernels' chunk of a long document is bound
         # by one CU's row gathers), ONI_GS_SPLIT_MIN overrides (0: off)
+        # K > 32: 2048 (the whole team8 range) -- at 4096 the 2-4 k-word documents' 512-thread
+        # workgroups were dispatched behind the short-document floods in some iterations (a bimodal
+        # 2.75 / 4.5 ms team8 bucket); one co-resident split launch holds them all: K = 50 4.53 / 4.73
+        # -> 3.36 / 3.34 ms per EM iteration (profiles/r3_tuning_log.md)
         if split_min is None:
-            split_min = int(os.environ.get("ONI_GS_SPLIT_MIN", "4096" if KS > 32 else "0"))
+            split_min = int(os.environ.get("ONI_GS_SPLIT_MIN", "2048" if KS > 32 else "0"))
         if int(gs_updates) > gs_umax():
             split_min = 0       # the split kernel keeps its chunk tables in LDS: U <= 32 only
         self.split = None

@@ -104,13 +104,17 @@ def main():
                                    sweeps_max=int(it.max()), ms=round(ms, 4),
                                    word_sweeps=int((L * it).sum())))
         if a.phases and var not in (H.GS_TINY, H.GS_SMALL):
-            dbg = torch.zeros(8, dtype=torch.int64, device="cuda")
+            dbg = torch.zeros(16, dtype=torch.int64, device="cuda")
             launch(var, order, dbg)
             v = dbg.cpu().tolist()
             ch = max(v[7], 1)
             out["buckets"][-1]["phase_cycles_per_chunk"] = dict(
                 word=round(v[0] / ch), word_dot=round(v[6] / ch), reduce=round(v[1] / ch), barrier1=round(v[2] / ch), topic=round(v[3] / ch),
                 barrier2=round(v[4] / ch), sweep_tail_total=v[5], chunks=v[7], doc_len=int(L.max()))
+            if any(v[8:12]):   # gs_wsteam's topic wave
+                out["buckets"][-1]["topic_wave_cycles_per_chunk"] = dict(
+                    wait_arrivals=round(v[8] / ch), sum_refresh=round(v[9] / ch), barrier_b=round(v[10] / ch),
+                    after_barrier=round(v[11] / ch))
         print(json.dumps(out["buckets"][-1]), flush=True)
         if a.prefixes and var == H.GS_TEAM8:
             # the longest documents alone: separates the per-CU gather rate from L2 sharing between documents

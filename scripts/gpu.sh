@@ -17,7 +17,8 @@
 #   nccl      the one-rank RCCL test (tests/test_gpu_dist.py -k nccl)
 #   ab        scripts/ab_env.sh $AB_ROUNDS $AB_VARIANTS (space-separated env settings, one per variant)
 #   ranks     scripts/pipeline_ranks.py $RANKS_ARGS (per-rank stage seconds of the sharded ml_ops pipeline)
-# env: TAG (output dir gpurun_out/$TAG, default s), BENCH_ARGS, PROF_ARGS, PARITY_ARGS, PMC, KEEP_GOING=1
+# env: TAG (output dir gpurun_out/$TAG, default s), BENCH_ARGS, PROF_ARGS, PARITY_ARGS, PMC, PMC_ARGS, KEEP_GOING=1
+# (this script replaces the per-experiment gpu_*.sh drivers of rounds 1-2; their records name them)
 # (a failing pytest with exit status 1 -- assertion failures, not a crash -- does not stop the session)
 set -u -o pipefail
 cd /tmp && export TMPDIR=/tmp
@@ -73,7 +74,7 @@ for s in "$@"; do
     pmc)
       rm -rf "$OUT/pmc"; mkdir -p "$OUT/pmc"
       timeout -s KILL 120 rocprofv3 --pmc ${PMC:?set PMC} -d "$OUT/pmc" -o pmc -- python3 bench.py \
-        --steps 3 --warmup 1 --converge 0 --e2e 0 > "$OUT/pmc/log.txt" 2>&1 || stop pmc $?
+        ${PMC_ARGS:---steps 3 --warmup 1 --converge 0 --e2e 0} > "$OUT/pmc/log.txt" 2>&1 || stop pmc $?
       db=$(find "$OUT/pmc" -name "*.db" | head -1)
       python scripts/pmc_summary.py "$db" ${PMC_MATCH:+--match "$PMC_MATCH"} --md "$OUT/pmc_summary.md" > /dev/null
       rm -f "$db"; head -30 "$OUT/pmc_summary.md" ;;
