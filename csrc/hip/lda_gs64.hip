@@ -2085,8 +2085,11 @@ __global__ __launch_bounds__((NW + 1) * 64) void gs_wsteam(GSArgs a) {
       }
     };
     double gam = k < K ? g0 : 0.0, psi = m, lps = 0.0;
+    // this lane's E_k stays in a register (the wave is E_'s only writer), and C_jk is read before
+    // the arrival wait: after the last arrival only the sRed loads precede the refresh chain
+    double Ecur = k < K ? 1.0 : 0.0;
     if (k < KS) {
-      E_[k] = k < K ? 1.0 : 0.0;
+      E_[k] = Ecur;
       for (int j = 0; j < nch; ++j) C[j][k] = k < K ? Cs[j] / K : 0.0;
     }
     lds_barrier();   // (1) E_ and C ready; word waves' first rows in flight
@@ -2097,6 +2100,7 @@ __global__ __launch_bounds__((NW + 1) * 64) void gs_wsteam(GSArgs a) {
         // (A) the nact word waves' topic sums of chunk j are in sRed
         want += nact;
         ttick(3);
+        const double Cj = k < KS ? C[j][k] : 0.0;
         while (__hip_atomic_load(&arrive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < want)
           __builtin_amdgcn_s_sleep(1);
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
@@ -2105,17 +2109,18 @@ __global__ __launch_bounds__((NW + 1) * 64) void gs_wsteam(GSArgs a) {
           double S = 0.0;
 #pragma unroll
           for (int v = 0; v < NW; ++v) S += v < nact ? sRed[v][k] : 0.0;
-          const double Eo = E_[k];
+          const double Eo = Ecur;
           const double nw = Eo * S;
           double En = 0.0;
           if (k < K) {
             lps = fma(psi, nw, lps);
-            gam += nw - C[j][k];
+            gam += nw - Cj;
             psi_exp(gam, m, psi, En);
           }
+          E_[k] = En;
           C[j][k] = nw;
           Et[j][k] = Eo;
-          E_[k] = En;
+          Ecur = En;
         }
         ttick(1);
         lds_barrier();   // (B) E of chunk j + 1 published
