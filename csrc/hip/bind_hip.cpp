@@ -150,12 +150,18 @@ PYBIND11_MODULE(_onihip, m) {
   m.def("gs_umax", [](int KS) { return KS > 0 ? oni::gs_umax(KS) : oni::kGsUMax; }, py::arg("KS") = 0);
   m.def("gs_tiny_max", [](int KS) { return oni::gs_tiny_max(KS); });
   m.def("gs_estep", [](u doc_ptr, u word_idx, u counts, u order, int n_items, u beta, int K, int KS, int gs_updates,
-                       u params, u gamma, u cphi, u lik, u alpha_ss, u iters, int variant, u stream, u dbg) {
+                       u params, u gamma, u cphi, u lik, u alpha_ss, u iters, int variant, u stream, u dbg,
+                       u stage, u stage_off) {
     oni::GSArgs a{P<const int>(doc_ptr), P<const int>(word_idx), P<const float>(counts), P<const int>(order),
                   n_items,               P<const double>(beta),  K,                      gs_updates,
                   P<const double>(params), P<double>(gamma),     P<double>(cphi),        P<double>(lik),
-                  P<double>(alpha_ss),   P<int>(iters),         P<long long>(dbg)};
+                  P<double>(alpha_ss),   P<int>(iters),         P<long long>(dbg),      P<const double>(stage),
+                  P<const long long>(stage_off)};
     oni::launch_gs_estep(a, variant, KS, S(stream));
+  });
+  m.def("gs_stage", [](u beta, u word_idx, u tile_ent, u tile_cnt, int n_tiles, u stage, int KS, u stream) {
+    oni::launch_gs_stage(P<const double>(beta), P<const int>(word_idx), P<const int>(tile_ent),
+                         P<const int>(tile_cnt), n_tiles, P<double>(stage), KS, S(stream));
   });
   m.def("init_random_ss", [](u cw, int V, int K, int KS, unsigned long long seed, u stream) {
     oni::launch_init_random_ss(P<double>(cw), V, K, KS, seed, S(stream));

@@ -218,8 +218,17 @@ struct GSArgs {
   // accumulates clock64() cycles into dbg[0..7]: word phase, slot reduction, barrier 1, topic phase,
   // barrier 2, sweep likelihood, final pass, chunks
   long long* dbg = nullptr;
+  // optional staged rows (kGsTeam8 at KS <= 32, launch_gs_stage): item i's document has its beta rows
+  // copied in document order to stage + stage_off[i] (double2 units), tiled [n/64][KS/2][64] so that a
+  // wave's 64 consecutive words are 16-byte-contiguous per topic pair; stage_off[i] < 0: not staged
+  const double* stage = nullptr;
+  const long long* stage_off = nullptr;
 };
 void launch_gs_estep(const GSArgs& a, int variant, int KS, hipStream_t s);
+// stage[(t KS/2 + k) 64 + l] (double2) = beta row pair k of the word at corpus entry tile_ent[t] + l
+// (l < tile_cnt[t], else 0): the staged rows of launch_gs_estep, filled after every M-step
+void launch_gs_stage(const double* beta, const int* word_idx, const int* tile_ent, const int* tile_cnt, int n_tiles,
+                     double* stage, int KS, hipStream_t s);
 int gs_tiny_max(int KS);   // longest document of the kGsTiny kernel
 int gs_umax(int KS);       // largest gs_updates the E-step accepts at row stride KS (split: kGsUMax)
 // One long document over s.seg_count[b] workgroups (8 waves each): every chunk is cut into

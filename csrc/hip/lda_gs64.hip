@@ -1750,6 +1750,20 @@ __device__ __forceinline__ void wave_topic_sums(const double (&acc)[KS], int lan
   if (i < H2 && (!hi4 || H2 + i < H1) && base + i < KS) out[base + i] = v;
 }
 
+// the row of word position p from a staged document copy ([n/64][KS/2][64] double2 tiles,
+// launch_gs_stage): 64 consecutive positions are 16-byte-contiguous per topic pair, so a wave's
+// gather of 64 words touches ~9 cache lines per instruction instead of 64 rows' worth
+template <int KS>
+__device__ __forceinline__ void load_row_staged(const dvec2* __restrict__ s, int p, double (&b)[KS]) {
+  const dvec2* q = s + (size_t)(p >> 6) * (KS / 2) * 64 + (p & 63);
+#pragma unroll
+  for (int k = 0; k < KS / 2; ++k) {
+    const dvec2 v = q[k * 64];
+    b[2 * k] = v.x;
+    b[2 * k + 1] = v.y;
+  }
+}
+
 template <int KS>
 __device__ __forceinline__ void load_row_full(const double* __restrict__ beta, int w, double (&b)[KS]) {
   const double2* p = reinterpret_cast<const double2*>(beta + (size_t)w * KS);
@@ -2005,7 +2019,7 @@ __global__ __launch_bounds__(wteam_threads(NW)) void gs_wteam(GSArgs a) {
 // EP (early prefetch, ONI_GS_EARLY_PREFETCH=EP): rounds u < EP of the next chunk's rows are gathered
 // into bc[u] as soon as the axpy of round u has consumed them -- before the topic sums and the
 // arrival -- so the address unit works beside the reduction; the other rounds after the arrival.
-template <int KS, int NW, int RMAX, int EP = 0>
+template <int KS, int NW, int RMAX, int EP = 0, bool STG = false>
 __global__ __launch_bounds__((NW + 1) * 64) void gs_wsteam(GSArgs a) {
   static_assert(KS <= 32 && KS % 2 == 0, "word team: KS <= 32");
   constexpr int NTD = (NW + 1) * 64, NS = NW * 64;
@@ -2148,6 +2162,17 @@ __global__ __launch_bounds__((NW + 1) * 64) void gs_wsteam(GSArgs a) {
     return;
   }
   // -------------------------------------------------------------- word waves
+  // STG: rows come from the document's staged copy (launch_gs_stage) indexed by word position, so
+  // the ids below are positions; otherwise they are vocabulary ids into beta
+  const dvec2* stg = nullptr;
+  if constexpr (STG) stg = reinterpret_cast<const dvec2*>(a.stage) + a.stage_off[blockIdx.x];
+  auto row_of = [&](int p) { return STG ? p : wrow[p]; };
+  auto load_row = [&](int id, double(&b)[KS]) {
+    if constexpr (STG)
+      load_row_staged<KS>(stg, id, b);
+    else
+      load_row_full<KS>(a.beta, id, b);
+  };
   int wc[RMAX], wn[RMAX];
   float cc[RMAX], cn[RMAX];
   unsigned vc = 0, vn = 0;
@@ -2160,7 +2185,7 @@ __global__ __launch_bounds__((NW + 1) * 64) void gs_wsteam(GSArgs a) {
       const int p = n0 + t + r * NS;
       v |= (active && p < n1) ? (1u << r) : 0u;
       const int pc = min(p, n1 - 1);
-      w[r] = wrow[pc];
+      w[r] = row_of(pc);
       c[r] = crow[pc];
     }
   };
@@ -2169,7 +2194,7 @@ __global__ __launch_bounds__((NW + 1) * 64) void gs_wsteam(GSArgs a) {
 #pragma unroll
     for (int r = 0; r < RMAX; ++r) {
       if ((v >> r) & 1u) {   // rounds past the chunk end gather nothing
-        load_row_full<KS>(a.beta, w[r], bc[r]);
+        load_row(w[r], bc[r]);
       } else {
 #pragma unroll
         for (int kk = 0; kk < KS; ++kk) bc[r][kk] = 0.0;
@@ -2225,7 +2250,7 @@ __global__ __launch_bounds__((NW + 1) * 64) void gs_wsteam(GSArgs a) {
           if (u < EP) {   // bc[u] is free: the next chunk's round u (ids already here)
             __builtin_amdgcn_sched_barrier(0);   // keep the gather below the axpy (no second row set)
             if ((vn >> u) & 1u) {
-              load_row_full<KS>(a.beta, wn[u], bc[u]);
+              load_row(wn[u], bc[u]);
             } else {
 #pragma unroll
               for (int kk = 0; kk < KS; ++kk) bc[u][kk] = 0.0;
@@ -2234,7 +2259,7 @@ __global__ __launch_bounds__((NW + 1) * 64) void gs_wsteam(GSArgs a) {
         }
         for (int p = n0 + t + RMAX * NS; p < n1; p += NS) {   // beyond the prefetched rounds
           double b[1][KS];
-          load_row_full<KS>(a.beta, wrow[p], b[0]);
+          load_row(row_of(p), b[0]);
           const double cp = (double)crow[p];
           wword_steps<KS, 1>(E, b, &cp, acc, lw);
         }
@@ -2262,7 +2287,7 @@ __global__ __launch_bounds__((NW + 1) * 64) void gs_wsteam(GSArgs a) {
 #pragma unroll
           for (int r = EP; r < RMAX; ++r) {
             if ((vc >> r) & 1u) {
-              load_row_full<KS>(a.beta, wc[r], bc[r]);
+              load_row(wc[r], bc[r]);
             } else {
 #pragma unroll
               for (int kk = 0; kk < KS; ++kk) bc[r][kk] = 0.0;
@@ -2294,7 +2319,7 @@ __global__ __launch_bounds__((NW + 1) * 64) void gs_wsteam(GSArgs a) {
     for (int kk = 0; kk < KS; ++kk) E[kk] = Et[j][kk];
     for (int p = n0 + t; p < n1; p += NS) {
       double b[KS];
-      load_row_full<KS>(a.beta, wrow[p], b);
+      load_row(row_of(p), b);
       double p0 = 0.0, p1 = 0.0, p2 = 0.0, p3 = 0.0;
 #pragma unroll
       for (int kk = 0; kk < KS; kk += 4) {
@@ -2491,6 +2516,35 @@ __global__ __launch_bounds__(256) void gs_mstep_kernel(const double* __restrict_
   }
 }
 
+// Staged rows of the longest documents (GSArgs::stage): one thread per double2 of the tiled copy,
+// coalesced stores and 16-byte gathers from beta (the gathers are spread over the whole GPU here,
+// instead of through the one CU that walks the document 20 times per E-step)
+template <int KS>
+__global__ __launch_bounds__(256) void gs_stage_kernel(const double* __restrict__ beta,
+                                                       const int* __restrict__ word_idx,
+                                                       const int* __restrict__ tile_ent,
+                                                       const int* __restrict__ tile_cnt, int n_tiles,
+                                                       dvec2* __restrict__ out) {
+  // one thread per (tile, lane): its word's whole row in KS / 2 independent 16-byte loads, stored
+  // as one 16-byte element per topic pair (a wave's stores are 1 KB-contiguous per pair)
+  const long long total = (long long)n_tiles * 64;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
+    const int t = (int)(i >> 6), l = (int)(i & 63);
+    dvec2 v[KS / 2];
+    if (l < tile_cnt[t]) {
+      const dvec2* row = reinterpret_cast<const dvec2*>(beta + (size_t)word_idx[tile_ent[t] + l] * KS);
+#pragma unroll
+      for (int k = 0; k < KS / 2; ++k) v[k] = row[k];
+    } else {
+#pragma unroll
+      for (int k = 0; k < KS / 2; ++k) v[k] = dvec2{0.0, 0.0};
+    }
+    dvec2* o = out + (size_t)t * (KS / 2) * 64 + l;
+#pragma unroll
+    for (int k = 0; k < KS / 2; ++k) o[k * 64] = v[k];
+  }
+}
+
 }  // namespace gs
 
 // ------------------------------------------------------------------ launch ---
@@ -2560,7 +2614,13 @@ static void gs_estep_ks(const GSArgs& a, int variant, hipStream_t s) {
         // ONI_GS_EARLY_PREFETCH: next-chunk rounds gathered before the arrival (1, the default: 2.13-2.14
         // vs 2.17-2.18 ms per EM iteration, 3 A/B rounds; 2 spills 192 B: 3.27 ms; 0 = after it)
         static const int ep = std::getenv("ONI_GS_EARLY_PREFETCH") ? std::atoi(std::getenv("ONI_GS_EARLY_PREFETCH")) : 1;
-        if (bnw == 7 && ep == 1)
+        if (a.stage != nullptr) {   // staged rows (launch_gs_stage): the default shape only
+          if (bnw != 7 || ep > 1) throw std::runtime_error("gs_estep: staged rows need the 7-wave team8 kernel");
+          if (ep == 1)
+            hipLaunchKernelGGL((gs::gs_wsteam<KS, 7, 2, 1, true>), dim3(a.n_items), dim3(512), 0, s, a);
+          else
+            hipLaunchKernelGGL((gs::gs_wsteam<KS, 7, 2, 0, true>), dim3(a.n_items), dim3(512), 0, s, a);
+        } else if (bnw == 7 && ep == 1)
           hipLaunchKernelGGL((gs::gs_wsteam<KS, 7, 2, 1>), dim3(a.n_items), dim3(512), 0, s, a);
         else if (bnw == 7 && ep >= 2)
           hipLaunchKernelGGL((gs::gs_wsteam<KS, 7, 2, 2>), dim3(a.n_items), dim3(512), 0, s, a);
@@ -2589,6 +2649,27 @@ static void gs_estep_ks(const GSArgs& a, int variant, hipStream_t s) {
 }
 
 int gs_umax(int KS) { return KS > 32 ? kGsUMaxWide : kGsUMax; }
+
+void launch_gs_stage(const double* beta, const int* word_idx, const int* tile_ent, const int* tile_cnt, int n_tiles,
+                     double* stage, int KS, hipStream_t s) {
+  if (n_tiles <= 0) return;
+  if (KS > 32 || KS % 2) throw std::runtime_error("gs_stage: staged rows need an even KS <= 32");
+  const long long total = (long long)n_tiles * 64;
+  const unsigned blocks = (unsigned)std::min<long long>((total + 255) / 256, 16384);
+  switch (KS) {
+#define ONI_KS(X)                                                                                           \
+  case X:                                                                                                   \
+    if constexpr (X <= 32 && X % 2 == 0)                                                                    \
+      hipLaunchKernelGGL((gs::gs_stage_kernel<X>), dim3(blocks), dim3(256), 0, s, beta, word_idx, tile_ent, \
+                         tile_cnt, n_tiles, reinterpret_cast<gs::dvec2*>(stage));                           \
+    break;
+    ONI_FOR_EACH_KS(ONI_KS)
+#undef ONI_KS
+    default:
+      throw std::runtime_error("gs_stage: unsupported KS " + std::to_string(KS));
+  }
+  ONI_HIP_CHECK(hipGetLastError());
+}
 
 void launch_gs_estep(const GSArgs& a, int variant, int KS, hipStream_t s) {
   if (a.gs_updates < 1 || a.gs_updates > gs_umax(KS))

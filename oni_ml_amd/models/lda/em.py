@@ -410,6 +410,7 @@ class LDAEngine:
                 w["gp"] = H.GSPlan(self.dc.doc_len, KS, self._U, dev, doc_range=(w["d0"], w["d1"]))
             rows = max(w["e1"] - w["e0"] for w in self._cwin)
         self.beta = torch.zeros(V, KS, dtype=f64, device=dev)
+        self._stages = self._build_stages(corpus, KS)
         self.cw = torch.zeros(V, KS, dtype=f64, device=dev)
         self.gamma = torch.zeros(D, KS, dtype=f64, device=dev)
         self.cphi = torch.zeros(max(rows, 1), KS, dtype=f64, device=dev)[:rows]
@@ -448,6 +449,29 @@ class LDAEngine:
             self._build_window_suff()
         elif os.environ.get("ONI_SUFF_SPLIT", "1") != "0":
             self._suff_split = self._build_suff_split()
+
+    def _build_stages(self, corpus: Corpus, KS: int) -> dict:
+        """Staged beta rows (ops/hip.py GSStage) of every kGsTeam8 launch at KS <= 32, keyed by the id of
+        the launch's order tensor.  ONI_GS_STAGE=0 turns them off; a plan whose copies would exceed
+        ONI_GS_STAGE_GB (default 4) is left unstaged."""
+        from ...ops import hip as H
+        if KS > 32 or os.environ.get("ONI_GS_STAGE", "1") == "0":
+            return {}
+        cap = float(os.environ.get("ONI_GS_STAGE_GB", "4")) * 2**30
+        plans = [self.gs_plan] if self._cwin is None else [w["gp"] for w in self._cwin]
+        out = {}
+        for gp in plans:
+            for var, order in gp.plan:
+                if var != H.GS_TEAM8:
+                    continue
+                o = order.cpu().numpy()
+                o = o[o >= 0]
+                need = int(corpus.doc_ptr[o + 1].sum() - corpus.doc_ptr[o].sum()) * KS * 8
+                if need > cap:
+                    continue
+                cap -= need
+                out[id(order)] = H.GSStage(order, corpus.doc_ptr, KS, self.device)
+        return out
 
     def _cphi_windows(self, corpus: Corpus, KS: int):
         """Contiguous document windows [d0, d1) of <= the c.phi budget's rows each (nnz-balanced, a
@@ -585,6 +609,14 @@ class LDAEngine:
         dc, prm = self.dc, self._params
         main = torch.cuda.current_stream(self.device)
         streams = [main] + self._streams
+        # staged rows refilled before the fork (ONI_GS_STAGE_AT=main, default): the team8 launch is then
+        # the first dispatched, instead of queueing behind the other buckets' workgroups for whole CUs
+        stage_main = os.environ.get("ONI_GS_STAGE_AT", "main") == "main"
+        if stage_main:
+            for var, order in gp.plan:
+                st = self._stages.get(id(order))
+                if st is not None:
+                    H.gs_stage(self.beta, dc.word_idx, st)
         self._ev_fork.record(main)
         used = []
         # side streams: the long-document buckets (critical path) are dispatched first, the split
@@ -611,8 +643,11 @@ class LDAEngine:
                         H.gs_split(dc.doc_ptr, dc.word_idx, dc.counts, self.beta, self.K, self._U, prm, self.gamma,
                                    cphi, self.lik, self.ass, self.iters, batch, ent_base=ent_base)
                 else:
+                    st = self._stages.get(id(order))
+                    if st is not None and not stage_main:   # refill on the bucket's own stream
+                        H.gs_stage(self.beta, dc.word_idx, st)
                     H.gs_estep(dc.doc_ptr, dc.word_idx, dc.counts, order, self.beta, self.K, self._U, prm,
-                               self.gamma, cphi, self.lik, self.ass, self.iters, var, ent_base=ent_base)
+                               self.gamma, cphi, self.lik, self.ass, self.iters, var, ent_base=ent_base, stage=st)
         # every bucket but work[0] is joined first and the early pass overlaps work[0]
         for j, s in enumerate(used):
             self._ev_join[j].record(s)

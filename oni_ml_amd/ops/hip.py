@@ -558,11 +558,64 @@ def _cphi_ptr(cphi, nnz, KS, dev, ent_base):
     return ptr - int(ent_base) * KS * 8
 
 
+class GSStage:
+    """Staged beta rows of one kGsTeam8 launch (KS <= 32): every document of ``order`` gets its rows
+    copied in document order into one buffer, tiled [ceil(n / 64)][KS / 2][64] double2, refilled by
+    ``gs_stage`` after each M-step.  The longest document's kernel then gathers 64 consecutive words
+    as 16-byte-contiguous runs (one CU walks those rows U x 20 times per E-step) instead of 64
+    scattered 8 KS-byte rows; the copy itself is spread over the whole GPU.  Costs n x KS x 8 bytes."""
+
+    def __init__(self, order, doc_ptr_host, KS: int, device):
+        import numpy as np
+        if KS > 32 or KS % 2:
+            raise ValueError("staged rows need an even KS <= 32")
+        o = np.asarray(order.cpu().numpy() if torch.is_tensor(order) else order, np.int64)
+        dp = np.asarray(doc_ptr_host, np.int64)
+        per = (KS // 2) * 64
+        off = np.zeros(o.size, np.int64)
+        ents, cnts = [], []
+        nt = 0
+        for i, d in enumerate(o):
+            if d < 0:
+                continue
+            s0, n = int(dp[d]), int(dp[d + 1] - dp[d])
+            T = -(-n // 64)
+            off[i] = nt * per
+            ents.append(s0 + 64 * np.arange(T, dtype=np.int64))
+            cnts.append(np.minimum(64, n - 64 * np.arange(T, dtype=np.int64)))
+            nt += T
+        self.KS, self.n_tiles = int(KS), nt
+        cat = lambda xs: np.concatenate(xs) if xs else np.zeros(0, np.int64)
+        self.tile_ent = torch.from_numpy(cat(ents).astype(np.int32)).to(device)
+        self.tile_cnt = torch.from_numpy(cat(cnts).astype(np.int32)).to(device)
+        self.stage_off = torch.from_numpy(off).to(device)
+        self.buf = torch.zeros(max(nt, 1) * per * 2, dtype=torch.float64, device=device)
+
+    @property
+    def nbytes(self) -> int:
+        return self.n_tiles * (self.KS // 2) * 64 * 16
+
+
+def gs_stage(beta, word_idx, st: "GSStage"):
+    """Refill the staged rows of ``st`` from ``beta`` (after every M-step, before the team8 launch)."""
+    V, KS = beta.shape
+    dev = beta.device
+    if KS != st.KS:
+        raise ValueError(f"staged rows of KS {st.KS}, beta has {KS}")
+    if st.n_tiles == 0:
+        return
+    lib().gs_stage(_chk(beta, torch.float64, "beta", (V, KS), dev), _chk(word_idx, torch.int32, "word_idx", None, dev),
+                   _chk(st.tile_ent, torch.int32, "tile_ent", (st.n_tiles,), dev),
+                   _chk(st.tile_cnt, torch.int32, "tile_cnt", (st.n_tiles,), dev), st.n_tiles,
+                   _chk(st.buf, torch.float64, "stage", None, dev), int(KS), _stream())
+
+
 def gs_estep(doc_ptr, word_idx, counts, order, beta, K, gs_updates, params, gamma, cphi, lik, alpha_ss, iters, variant,
-             dbg=None, ent_base=None):
+             dbg=None, ent_base=None, stage: Optional["GSStage"] = None):
     """One launch of the fp64 block Gauss-Seidel E-step over the documents in ``order``.
     ``params``: the device parameter block {alpha, lgamma constant, VAR_MAX_ITER, VAR_CONVERGED, done}.
-    ``ent_base``: ``cphi`` is a window starting at that corpus entry (_cphi_ptr)."""
+    ``ent_base``: ``cphi`` is a window starting at that corpus entry (_cphi_ptr).
+    ``stage``: the GSStage of this (kGsTeam8) launch, filled by ``gs_stage`` from the current beta."""
     D = doc_ptr.numel() - 1
     nnz = word_idx.numel()
     V, KS = beta.shape
@@ -588,7 +641,11 @@ def gs_estep(doc_ptr, word_idx, counts, order, beta, K, gs_updates, params, gamm
         _chk(alpha_ss, torch.float64, "alpha_ss", (D,), dev),
         _chk(iters, torch.int32, "iters", (D,), dev),
         int(variant), _stream(), 0 if dbg is None else _chk(dbg, torch.int64, "dbg", (16,), dev),
+        0 if stage is None else _chk(stage.buf, torch.float64, "stage", None, dev),
+        0 if stage is None else _chk(stage.stage_off, torch.int64, "stage_off", (order.numel(),), dev),
     ]
+    if stage is not None and (variant != GS_TEAM8 or KS != stage.KS):
+        raise ValueError("staged rows: kGsTeam8 launches of the stage's KS only")
     if order.numel() == 0:
         return
     lib().gs_estep(*args)

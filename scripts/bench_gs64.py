@@ -60,8 +60,11 @@ def main():
     out = dict(docs=c.num_docs, nnz=c.nnz, U=eng._U, buckets=[])
 
     def launch(var, order, dbg=None):
+        st = eng._stages.get(id(order))   # team8's staged rows (ops/hip.py GSStage): refill + launch
+        if st is not None:
+            H.gs_stage(eng.beta, dc.word_idx, st)
         H.gs_estep(dc.doc_ptr, dc.word_idx, dc.counts, order, eng.beta, eng.K, eng._U, eng._params, eng.gamma,
-                   eng.cphi, eng.lik, eng.ass, eng.iters, var, dbg=dbg)
+                   eng.cphi, eng.lik, eng.ass, eng.iters, var, dbg=dbg, stage=st)
 
     spl = eng.gs_plan.split
     if spl is not None and (not a.only or a.only == "split"):
@@ -115,6 +118,10 @@ def main():
                 out["buckets"][-1]["topic_wave_cycles_per_chunk"] = dict(
                     wait_arrivals=round(v[8] / ch), sum_refresh=round(v[9] / ch), barrier_b=round(v[10] / ch),
                     after_barrier=round(v[11] / ch))
+        st = eng._stages.get(id(order))
+        if st is not None:
+            out["buckets"][-1]["stage_ms"] = round(timed(lambda: H.gs_stage(eng.beta, dc.word_idx, st), a.reps), 4)
+            out["buckets"][-1]["stage_mb"] = round(st.nbytes / 2**20, 1)
         print(json.dumps(out["buckets"][-1]), flush=True)
         if a.prefixes and var == H.GS_TEAM8:
             # the longest documents alone: separates the per-CU gather rate from L2 sharing between documents

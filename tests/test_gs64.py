@@ -152,16 +152,19 @@ def test_gs64_graph_replay_and_gate():
     assert eng.gamma.abs().max().item() == 0
 
 
+@pytest.mark.parametrize("stage", ["1", "0"])
 @pytest.mark.parametrize("head", [
     # longest chunk 938 words: past the two prefetched rounds (7 waves x 64 lanes x 2), streamed remainder
     [30000, 20000, 15000, 9000, 6000, 5000, 4000, 3500, 3000, 2500, 2200, 2100],
     [24000, 20000, 15000, 9000, 6000, 5000, 4000, 3500, 3000, 2500, 2200, 2100],
 ])
-def test_longest_documents_match_oracle(head):
+def test_longest_documents_match_oracle(head, stage, monkeypatch):
     """The longest-document kernel (gs_wsteam: word waves + a topic wave) against the oracle, on chunks
     that need both prefetched rounds, with more than 8 team8 documents so the XCD-aware workgroup order
-    holds empty slots (GSPlan.isolate_longest)."""
+    holds empty slots (GSPlan.isolate_longest); with the staged row copies (GSStage, default) and
+    gathering from beta."""
     from oni_ml_amd.ops import hip as H
+    monkeypatch.setenv("ONI_GS_STAGE", stage)
     rng = np.random.default_rng(11)
     V, D = 40000, 300
     lens = np.minimum(rng.zipf(1.5, D), 200)
@@ -177,11 +180,44 @@ def test_longest_documents_match_oracle(head):
     eng, sc = _gpu_estep(c, K, lb, 0.41, LDASettings(var_max_iter=4, var_converged=-1e30), U)
     launches = {v: o.cpu().numpy() for v, o in eng.gs_plan.plan}
     assert (launches[H.GS_TEAM8] < 0).any() and launches[H.GS_TEAM8][0] == 0   # placement gaps
+    assert len(eng._stages) == (1 if stage == "1" else 0)
     assert np.array_equal(eng.iters.cpu().numpy(), ref["iters"])
     assert _rel(eng.gamma[:, :K].cpu().numpy(), ref["gamma"], 1e-12) < 1e-10
     assert _rel(eng.lik.cpu().numpy(), ref["doc_likelihood"], 1.0) < 1e-10
     cw = eng._cw_local[:, :K].cpu().numpy()
     assert _rel(cw, np.ascontiguousarray(ref["class_word"].T), 1e-30) < 1e-10
+
+
+def test_staged_rows_bitwise_equal_beta_rows(monkeypatch):
+    """Staged rows change where the team8 kernel reads beta, not what it reads: the E-step outputs are
+    bitwise those of the gather from beta, and the staged copy holds exactly each position's row."""
+    from oni_ml_amd.ops import hip as H
+    rng = np.random.default_rng(3)
+    V, D = 20000, 120
+    lens = np.minimum(rng.zipf(1.5, D), 150)
+    lens[:5] = [12000, 7000, 4100, 3000, 2100]
+    ptr = np.concatenate([[0], np.cumsum(lens)])
+    words = np.concatenate([rng.choice(V, n, replace=False) for n in lens]).astype(np.int32)
+    c = Corpus(ptr.astype(np.int64), words, rng.integers(1, 4, words.size).astype(np.int64), V)
+    K = 20
+    lb = _log_beta(V, K, seed=8)
+    out = {}
+    for stage in ("1", "0"):
+        monkeypatch.setenv("ONI_GS_STAGE", stage)
+        eng, sc = _gpu_estep(c, K, lb, 0.3, LDASettings(var_max_iter=6, var_converged=-1e30), 32)
+        out[stage] = (eng.gamma.cpu().numpy(), eng.cphi.cpu().numpy(), eng.lik.cpu().numpy(), sc)
+        if stage == "1":
+            (st,) = eng._stages.values()
+            buf = st.buf.view(-1, K // 2, 64, 2).cpu().numpy()          # [tile][pair][lane][2]
+            beta = eng.beta.cpu().numpy()
+            ent, cnt = st.tile_ent.cpu().numpy(), st.tile_cnt.cpu().numpy()
+            for t in (0, 1, len(ent) - 1):
+                rows = beta[words[ent[t]:ent[t] + cnt[t]]]              # [cnt][KS]
+                got = buf[t].transpose(1, 0, 2).reshape(64, K)[:cnt[t]]
+                assert np.array_equal(got, rows)
+                assert not buf[t].transpose(1, 0, 2).reshape(64, K)[cnt[t]:].any()
+    for a, b in zip(out["1"], out["0"]):
+        assert np.array_equal(a, b)
 
 
 @pytest.mark.parametrize("K,env", [

@@ -77,3 +77,19 @@ def test_xcd_gaps_leave_block_zero_mod_8_empty():
         assert all((blk == -1).all() for b, blk in enumerate(blocks) if b % 8 == 0)
         assert g[g >= 0].tolist() == o.tolist()
         assert all((blk >= 0).all() for b, blk in enumerate(blocks[:-1]) if b % 8)
+
+
+def test_stage_tiles_cover_each_document_in_order():
+    """GSStage: per launch item, the document's positions in 64-word tiles (entry of position 0, valid
+    count), the item's offset at its first tile; placement gaps (-1) take no tiles."""
+    import torch
+
+    from oni_ml_amd.ops.hip import GSStage
+    dp = np.array([0, 130, 130, 200, 264], dtype=np.int64)       # lengths 130, 0, 70, 64
+    st = GSStage(np.array([0, -1, 2, 3], np.int32), dp, 20, torch.device("cpu"))
+    per = 10 * 64
+    assert st.n_tiles == 3 + 2 + 1
+    assert st.tile_ent.tolist() == [0, 64, 128, 130, 194, 200]
+    assert st.tile_cnt.tolist() == [64, 64, 2, 64, 6, 64]
+    assert st.stage_off.tolist() == [0, 0, 3 * per, 5 * per]
+    assert st.buf.numel() == 6 * per * 2 and st.nbytes == 6 * per * 16
