@@ -2029,7 +2029,7 @@ __global__ __launch_bounds__((NW + 1) * 64) void gs_wsteam(GSArgs a) {
   __shared__ double sRed[NW][KS];       // per-wave topic sums of a chunk
   __shared__ double Cs[kGsUMax];        // chunk count sums
   __shared__ double sScal[NW + 1][4];   // sweep partials: lw per word wave; gamma sums (topic wave)
-  __shared__ int arrive;                // word-wave arrivals (chunks x active waves), monotone
+  __shared__ int arrive[NW];            // per word wave: chunks whose topic sums it has left in sRed
   if (a.params[kParamDone] != 0.0) return;
   const int t = threadIdx.x;
   const int d = a.order[blockIdx.x];
@@ -2049,7 +2049,7 @@ __global__ __launch_bounds__((NW + 1) * 64) void gs_wsteam(GSArgs a) {
   const int* __restrict__ wrow = a.word_idx + s0;
   const float* __restrict__ crow = a.counts + s0;
   for (int j = t; j < nch; j += NTD) Cs[j] = 0.0;
-  if (t == 0) arrive = 0;
+  if (t < NW) arrive[t] = 0;
   lds_barrier();
   for (int p = t; p < n; p += NTD) atomicAdd(&Cs[p / W], (double)crow[p]);   // integer counts: exact
   lds_barrier();
@@ -2111,24 +2111,29 @@ __global__ __launch_bounds__((NW + 1) * 64) void gs_wsteam(GSArgs a) {
       ++it;
       lps = 0.0;
       for (int j = 0; j < nch; ++j) {
-        // (A) the nact word waves' topic sums of chunk j are in sRed
-        want += nact;
+        // (A) the nact word waves' topic sums of chunk j are in sRed: summed in wave order as each
+        // wave arrives, so after the last arrival one add remains (not nact dependent adds)
+        ++want;
         ttick(3);
-        const double Cj = k < KS ? C[j][k] : 0.0;
-        while (__hip_atomic_load(&arrive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < want)
-          __builtin_amdgcn_s_sleep(1);
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+        const double gC = k < KS ? gam - C[j][k] : 0.0;
+        double S = 0.0;
+#pragma unroll
+        for (int v = 0; v < NW; ++v) {
+          if (v < nact) {
+            while (__hip_atomic_load(&arrive[v], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < want)
+              __builtin_amdgcn_s_sleep(1);
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+            S += k < KS ? sRed[v][k] : 0.0;
+          }
+        }
         ttick(0);
         if (k < KS) {
-          double S = 0.0;
-#pragma unroll
-          for (int v = 0; v < NW; ++v) S += v < nact ? sRed[v][k] : 0.0;
           const double Eo = Ecur;
           const double nw = Eo * S;
           double En = 0.0;
           if (k < K) {
             lps = fma(psi, nw, lps);
-            gam += nw - Cj;
+            gam = fma(Eo, S, gC);   // gamma_k + (new_jk - C_jk) in one rounding, off the nw product
             psi_exp(gam, m, psi, En);
           }
           E_[k] = En;
@@ -2268,7 +2273,7 @@ __global__ __launch_bounds__((NW + 1) * 64) void gs_wsteam(GSArgs a) {
         // (A) arrival: this wave's topic sums are in sRed.  A counter instead of a workgroup barrier,
         // so the refresh starts while the word waves are still issuing the next chunk's row loads
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");   // LDS only: no vmcnt wait
-        if (lane == 0) __hip_atomic_fetch_add(&arrive, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (lane == 0) __hip_atomic_fetch_add(&arrive[wv], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         tick(1);
         // prefetch of the next chunk's rows: a chunk's ~700 row gathers keep the CU's address unit busy
         // for ~2k cycles (64 B/clk) and the issuing wave blocks until they are queued -- now beside the
