@@ -1352,7 +1352,7 @@ __global__ __launch_bounds__(512) void gs_splitw(GSArgs a, SplitArgs sp) {
   __shared__ double sRedL[NW];
   __shared__ double sCs[kGsUMax];
   __shared__ double sScal[4];
-  __shared__ int arrive;
+  __shared__ int arrive[NW];   // per word wave: chunks whose partial sums it has left in sRed / sRedL
   __shared__ int sFail;
   if (a.params[kParamDone] != 0.0) return;
   const int t = threadIdx.x, b = blockIdx.x;
@@ -1382,10 +1382,8 @@ __global__ __launch_bounds__(512) void gs_splitw(GSArgs a, SplitArgs sp) {
     m1 = min(n1, m0 + WG);
   };
   for (int j = t; j < nch; j += NTD) sCs[j] = 0.0;
-  if (t == 0) {
-    sFail = 0;
-    arrive = 0;
-  }
+  if (t == 0) sFail = 0;
+  if (t < NW) arrive[t] = 0;
   lds_barrier();
   for (int p = t; p < n; p += NTD) atomicAdd(&sCs[p / W], (double)crow[p]);   // integer counts: exact
   lds_barrier();
@@ -1439,23 +1437,42 @@ __global__ __launch_bounds__(512) void gs_splitw(GSArgs a, SplitArgs sp) {
       for (int o = 0; o < TC; ++o) lps[o] = 0.0;
       for (int j = 0; j < nch; ++j) {
         ph[7] += twt ? 1 : 0;
-        want += nact;
-        while (__hip_atomic_load(&arrive, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < want)
-          __builtin_amdgcn_s_sleep(1);
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+        ++want;
+        // this chunk's C_jk and E_k before the waits (the LDS reads are off the chain)
+        double gC[TC], Eo[TC];
+#pragma unroll
+        for (int o = 0; o < TC; ++o) {
+          const int k = lane + 64 * o;
+          gC[o] = k < KS ? gam[o] - sC[j][k] : 0.0;
+          Eo[o] = k < KS ? sE[k] : 0.0;
+        }
+        // the segment's column sums, in wave order as the waves arrive (one add after the last)
+        double part[TC];
+#pragma unroll
+        for (int o = 0; o < TC; ++o) part[o] = 0.0;
+#pragma unroll
+        for (int v = 0; v < NW; ++v) {
+          if (v < nact) {
+            while (__hip_atomic_load(&arrive[v], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < want)
+              __builtin_amdgcn_s_sleep(1);
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+#pragma unroll
+            for (int o = 0; o < TC; ++o) {
+              const int c = lane + 64 * o;
+              part[o] += c < KS ? sRed[v][c] : (c == KS ? sRedL[v] : 0.0);
+            }
+          }
+        }
         tick(3);
         const int seq = (it - 1) * nch + j + 1;
         const unsigned tag = split_tag(epoch, seq);
         unsigned long long* xb = sp.xchg + (size_t)(seq & 1) * sp.n_blocks * GR;
-        // publish this segment's column sums (waves in order), then sweep the G segments
+        // publish this segment's column sums, then sweep the G segments
 #pragma unroll
         for (int o = 0; o < TC; ++o) {
           const int c = lane + 64 * o;
           if (c < NC) {
-            double part = 0.0;
-#pragma unroll
-            for (int v = 0; v < NW; ++v) part += v < nact ? (c < KS ? sRed[v][c] : sRedL[v]) : 0.0;
-            const unsigned long long bits = (unsigned long long)__double_as_longlong(part);
+            const unsigned long long bits = (unsigned long long)__double_as_longlong(part[o]);
             unsigned long long* row = xb + (size_t)b * GR + 2 * c;
             put_tagged_bits(row, (unsigned)(bits & 0xffffffffull), tag);
             put_tagged_bits(row + 1, (unsigned)(bits >> 32), tag);
@@ -1478,16 +1495,15 @@ __global__ __launch_bounds__(512) void gs_splitw(GSArgs a, SplitArgs sp) {
         for (int o = 0; o < TC; ++o) {
           const int k = lane + 64 * o;
           if (k < KS) {
-            const double Eo = sE[k];
-            const double nw = Eo * tot[o];
+            const double nw = Eo[o] * tot[o];
             double En = 0.0;
             if (k < K) {
               lps[o] = fma(psi[o], nw, lps[o]);
-              gam[o] += nw - sC[j][k];
+              gam[o] = fma(Eo[o], tot[o], gC[o]);   // gamma_k + (new_jk - C_jk) in one rounding
               psi_exp(gam[o], m, psi[o], En);
             }
             sC[j][k] = nw;
-            sEt[j][k] = Eo;
+            sEt[j][k] = Eo[o];
             sE[k] = En;
           } else if (k == KS) {
             LWs += tot[o];
@@ -1609,7 +1625,7 @@ __global__ __launch_bounds__(512) void gs_splitw(GSArgs a, SplitArgs sp) {
         if (lane == 0) sRedL[wv] = lw;
         // arrival (LDS only: no vmcnt wait), then the next chunk's rows -- beside the exchange
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
-        if (lane == 0) __hip_atomic_fetch_add(&arrive, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (lane == 0) __hip_atomic_fetch_add(&arrive[wv], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         tick(0);
         const int j1 = j + 1 < nch ? j + 1 : 0;
         const int j2 = j1 + 1 < nch ? j1 + 1 : 0;
@@ -2089,7 +2105,7 @@ __global__ __launch_bounds__((NW + 1) * 64) void gs_wsteam(GSArgs a) {
     // dbg[8..11] (the int64[16] timer of gs_estep): this wave's cycles waiting for the arrivals,
     // summing + refreshing, and at barrier B, summed over chunks
     const bool ttimer = a.dbg != nullptr && blockIdx.x == 0 && lane == 0;
-    long long tph[4] = {0, 0, 0, 0};
+    long long tph[8] = {0, 0, 0, 0, 0, 0, 0, 0};   // [4 + i]: chunk start -> wave v_i's arrival seen
     long long ttc = ttimer ? clock64() : 0;
     auto ttick = [&](int i) {
       if (ttimer) {
@@ -2123,6 +2139,8 @@ __global__ __launch_bounds__((NW + 1) * 64) void gs_wsteam(GSArgs a) {
             while (__hip_atomic_load(&arrive[v], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < want)
               __builtin_amdgcn_s_sleep(1);
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+            if (ttimer && (v == 0 || v == 3 || v == 4 || v == nact - 1))
+              tph[v == 0 ? 4 : v == 3 ? 5 : v == 4 ? 6 : 7] += clock64() - ttc;
             S += k < KS ? sRed[v][k] : 0.0;
           }
         }
@@ -2156,7 +2174,7 @@ __global__ __launch_bounds__((NW + 1) * 64) void gs_wsteam(GSArgs a) {
       sweep_end();
     }
     if (ttimer)
-      for (int i = 0; i < 4; ++i) a.dbg[8 + i] = tph[i];
+      for (int i = 0; i < 8; ++i) a.dbg[8 + i] = tph[i];
     const double ps = group_sum<64>(k < K ? psi : 0.0);
     if (k < KS) a.gamma[(size_t)d * KS + k] = gam;
     if (lane == 0) {

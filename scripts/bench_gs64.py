@@ -117,7 +117,8 @@ def main():
             if any(v[8:12]):   # gs_wsteam's topic wave
                 out["buckets"][-1]["topic_wave_cycles_per_chunk"] = dict(
                     wait_arrivals=round(v[8] / ch), sum_refresh=round(v[9] / ch), barrier_b=round(v[10] / ch),
-                    after_barrier=round(v[11] / ch))
+                    after_barrier=round(v[11] / ch), seen_wave0=round(v[12] / ch), seen_wave3=round(v[13] / ch),
+                    seen_wave4=round(v[14] / ch), seen_last=round(v[15] / ch))
         st = eng._stages.get(id(order))
         if st is not None:
             out["buckets"][-1]["stage_ms"] = round(timed(lambda: H.gs_stage(eng.beta, dc.word_idx, st), a.reps), 4)
