@@ -269,7 +269,7 @@ class LDAEngine:
             self.use_graph = use_graph
             self._graph = None
             self._mgraph, self._mgraph_key = None, None
-            self._fgraph, self._fgraph_key = None, None
+            self._fgraphs, self._fgraph_key = {}, None
             self._out_host = torch.zeros(self._ctlhist.numel(), dtype=torch.float64).pin_memory()
             self._pushed = None
             self._build_schedule()
@@ -440,7 +440,7 @@ class LDAEngine:
         self._ev_join = [torch.cuda.Event() for _ in range(4)]
         self._graph = None
         self._mgraph, self._mgraph_key = None, None
-        self._fgraph, self._fgraph_key = None, None
+        self._fgraphs, self._fgraph_key = {}, None
         self._out_host = torch.zeros(self._ctlhist.numel(), dtype=f64).pin_memory()
         self._pushed = None
         self.doc_buckets = None
@@ -1129,15 +1129,26 @@ class LDAEngine:
             self._ctl.copy_(torch.tensor([likelihood_old, emc, 0.0, float(iteration), float(emx),
                                           1.0 if stop else 0.0, 0.0, 0.0], dtype=torch.float64))
         key = (bool(estimate_alpha), int(num_docs))
-        for _ in range(n):
-            if not self._distributed:
-                if not self.use_graph:
-                    self._launch_estep(newton_key=key)
-                elif self._fgraph_key != key:
-                    self._fgraph = self._capture(lambda: self._launch_estep(newton_key=key))
-                    self._fgraph_key = key
+        if not self._distributed and self.use_graph:
+            # one rank: the batch's n iterations as ONE graph replay (cached per (key, n)): the ~12 us
+            # between back-to-back graph launches stays off all but the first iteration of the batch;
+            # ONI_GRAPH_ITERS=m caps the iterations per graph (1 = a graph per iteration)
+            if self._fgraph_key != key:
+                self._fgraphs, self._fgraph_key = {}, key
+            cap = int(os.environ.get("ONI_GRAPH_ITERS", "0")) or n
+            left = n
+            while left > 0:
+                m = min(cap, left)
+                g = self._fgraphs.get(m)
+                if g is None:
+                    self._fgraphs[m] = self._capture(
+                        lambda: [self._launch_estep(newton_key=key) for _ in range(m)])
                 else:
-                    self._fgraph.replay()
+                    g.replay()
+                left -= m
+        for _ in range(0 if (not self._distributed and self.use_graph) else n):
+            if not self._distributed:
+                self._launch_estep(newton_key=key)
             elif self._overlap:
                 self._run_phase("A")
                 tok = self._comm_begin()
