@@ -1130,9 +1130,9 @@ class LDAEngine:
                                           1.0 if stop else 0.0, 0.0, 0.0], dtype=torch.float64))
         key = (bool(estimate_alpha), int(num_docs))
         if not self._distributed and self.use_graph:
-            # one rank: the batch's n iterations as ONE graph replay (cached per (key, n)): the ~12 us
-            # between back-to-back graph launches stays off all but the first iteration of the batch;
-            # ONI_GRAPH_ITERS=m caps the iterations per graph (1 = a graph per iteration)
+            # one rank: the batch's n iterations as ONE graph replay (cached per (key, n)), one host call
+            # per batch; per EM iteration it measured the same as a replay per iteration (1.82-1.83 ms,
+            # profiles/r3_tuning_log.md).  ONI_GRAPH_ITERS=m caps the iterations per graph
             if self._fgraph_key != key:
                 self._fgraphs, self._fgraph_key = {}, key
             cap = int(os.environ.get("ONI_GRAPH_ITERS", "0")) or n
