@@ -1130,12 +1130,13 @@ class LDAEngine:
                                           1.0 if stop else 0.0, 0.0, 0.0], dtype=torch.float64))
         key = (bool(estimate_alpha), int(num_docs))
         if not self._distributed and self.use_graph:
-            # one rank: the batch's n iterations as ONE graph replay (cached per (key, n)), one host call
-            # per batch; per EM iteration it measured the same as a replay per iteration (1.82-1.83 ms,
-            # profiles/r3_tuning_log.md).  ONI_GRAPH_ITERS=m caps the iterations per graph
+            # one rank: graphs of m = ONI_GRAPH_ITERS EM iterations (default 1), cached per m.  A batch
+            # graph (m = the batch) measured the same per iteration (1.82-1.83 ms) but captures a new
+            # graph for every new batch size -- inside bench.py's timed window when the warm-up batch
+            # differs (2.00 vs 1.82 ms), so the default stays one graph per iteration
             if self._fgraph_key != key:
                 self._fgraphs, self._fgraph_key = {}, key
-            cap = int(os.environ.get("ONI_GRAPH_ITERS", "0")) or n
+            cap = max(1, int(os.environ.get("ONI_GRAPH_ITERS", "1")))
             left = n
             while left > 0:
                 m = min(cap, left)
