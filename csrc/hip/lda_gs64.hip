@@ -2637,12 +2637,21 @@ static void gs_estep_ks(const GSArgs& a, int variant, hipStream_t s) {
         // ONI_GS_EARLY_PREFETCH: next-chunk rounds gathered before the arrival (1, the default: 2.13-2.14
         // vs 2.17-2.18 ms per EM iteration, 3 A/B rounds; 2 spills 192 B: 3.27 ms; 0 = after it)
         static const int ep = std::getenv("ONI_GS_EARLY_PREFETCH") ? std::atoi(std::getenv("ONI_GS_EARLY_PREFETCH")) : 1;
-        if (a.stage != nullptr) {   // staged rows (launch_gs_stage): the default shape only
-          if (bnw != 7 || ep > 1) throw std::runtime_error("gs_estep: staged rows need the 7-wave team8 kernel");
-          if (ep == 1)
+        if (a.stage != nullptr) {
+          // staged rows (launch_gs_stage): every next-chunk round gathered after the arrival is the
+          // default here (ONI_GS_EARLY_PREFETCH unset: 1.726-1.740 vs 1.824-1.833 ms per EM iteration
+          // for the early round-0 gather, 3 A/B rounds -- the contiguous loads no longer need the head start)
+          static const int eps = std::getenv("ONI_GS_EARLY_PREFETCH") ? std::atoi(std::getenv("ONI_GS_EARLY_PREFETCH")) : 0;
+          if (bnw == 7 && eps == 1)
             hipLaunchKernelGGL((gs::gs_wsteam<KS, 7, 2, 1, true>), dim3(a.n_items), dim3(512), 0, s, a);
-          else
+          else if (bnw == 7 && eps == 0)
             hipLaunchKernelGGL((gs::gs_wsteam<KS, 7, 2, 0, true>), dim3(a.n_items), dim3(512), 0, s, a);
+          else if (bnw == 5 && eps == 0)
+            hipLaunchKernelGGL((gs::gs_wsteam<KS, 5, 3, 0, true>), dim3(a.n_items), dim3(384), 0, s, a);
+          else if (bnw == 3 && eps == 0)
+            hipLaunchKernelGGL((gs::gs_wsteam<KS, 3, 4, 0, true>), dim3(a.n_items), dim3(256), 0, s, a);
+          else
+            throw std::runtime_error("gs_estep: staged rows: ONI_GS_BIG_NW 7 (EP 0/1), 5 or 3 (EP 0)");
         } else if (bnw == 7 && ep == 1)
           hipLaunchKernelGGL((gs::gs_wsteam<KS, 7, 2, 1>), dim3(a.n_items), dim3(512), 0, s, a);
         else if (bnw == 7 && ep >= 2)

@@ -86,6 +86,37 @@ def strict_tables(mt: ModelTables, strict: bool = True) -> ModelTables:
                        n.roundtrip_py2(np.ascontiguousarray(mt.phi)))
 
 
+def background(fn, name: str = "oni-writer"):
+    """Run ``fn`` on a thread (the native writers release the GIL); returns the join callable a stage
+    puts in ``result["_defer"]``, which re-raises the thread's exception."""
+    import threading
+    box = {}
+
+    def body():
+        try:
+            fn()
+        except BaseException as e:  # noqa: BLE001 -- handed to the joiner
+            box["err"] = e
+
+    t = threading.Thread(target=body, name=name, daemon=True)
+    t.start()
+
+    def join():
+        t.join()
+        if "err" in box:
+            raise box["err"]
+    return join
+
+
+def doc_rows_of(doc_keys, n_keys: int) -> np.ndarray:
+    """Doc row of every dictionary id (-1: not a document): the in-memory equivalent of looking the
+    names up in doc_results.csv, when the documents are ``doc_keys`` in row order."""
+    rows = np.full(int(n_keys), -1, np.int64)
+    dk = np.asarray(doc_keys, np.int64)
+    rows[dk] = np.arange(dk.size, dtype=np.int64)
+    return rows
+
+
 def map_names(names: List[str], index: dict, device) -> torch.Tensor:
     """Name list -> row ids through a {name: row} map (-1 when absent), as a device int64 tensor."""
     ids = np.fromiter((index.get(n, -1) for n in names), dtype=np.int64, count=len(names))

@@ -30,6 +30,19 @@ def _word_names(ws: FF.FlowWordSpace, keys: np.ndarray):
     return ws.decode(keys)
 
 
+def _vocab_lookup(word_keys, word_names):
+    """keys -> (names, index) through the built vocabulary (every doc_wc key is in it): a vectorized
+    search instead of decoding the unique keys again -- the writer thread then holds the GIL only
+    briefly while the lda stage drives the GPU."""
+    wk = np.asarray(word_keys)
+    srt = np.argsort(wk, kind="stable")
+    sk = wk[srt]
+
+    def lookup(keys):
+        return word_names, srt[np.searchsorted(sk, np.asarray(keys))]
+    return lookup
+
+
 def run(cfg, dist=None, device=None, log=print) -> dict:
     if dist is not None and dist.active:
         from .sharded import run_flow
@@ -68,11 +81,16 @@ def run(cfg, dist=None, device=None, log=print) -> dict:
                 ipn = ft.ip_names
                 doc_names = [ipn[i] for i in built.doc_keys.tolist()]
                 word_names = _word_names(ws, built.word_keys)
-                if cfg.write_doc_wc:
-                    from ..corpus.builder import write_doc_wc
-                    write_doc_wc(os.path.join(cfg.lpath, "doc_wc.dat"), dwc, ipn,
-                                 lambda keys: (lambda u: (_word_names(ws, u[0]), u[1]))(np.unique(keys, return_inverse=True)))
-                C.write_corpus_files(cfg.lpath, built, doc_names, word_names)
+                lp, b_, dn_, wn_ = cfg.lpath, built, doc_names, word_names
+
+                def write_files():
+                    if cfg.write_doc_wc:
+                        from ..corpus.builder import write_doc_wc
+                        write_doc_wc(os.path.join(lp, "doc_wc.dat"), dwc, ipn, _vocab_lookup(b_.word_keys, wn_))
+                    C.write_corpus_files(lp, b_, dn_, wn_)
+                # the text files are the stage contract, not an input of the in-memory lda stage: written
+                # on a thread while the GPU runs EM; the lda_pre marker waits for them (finish_deferred)
+                res["_defer"] = C.background(write_files, "oni-lda-pre-writer")
                 res.update(docs=built.corpus.num_docs, terms=built.corpus.num_terms, nnz=built.corpus.nnz)
                 summary["corpus"] = dict(docs=built.corpus.num_docs, terms=built.corpus.num_terms, nnz=built.corpus.nnz)
     elif not sharded:
@@ -125,8 +143,10 @@ def run(cfg, dist=None, device=None, log=print) -> dict:
             if ft is None:
                 # row-sharded pre stages: rank 0 reads the whole day for the scoring pass
                 ft = FF.load_flow(cfg.flow_path, cfg.feedback_path(), cfg.dupfactor, cfg.threads)
+            # documents built in this process: ip dictionary id -> doc row without the name lookup
+            ip_rows = C.doc_rows_of(built.doc_keys, len(ft.ip_names)) if built is not None else None
             with R.stage("flow_post") as res:
-                res.update(score_flow(cfg, ft, tables, device, log))
+                res.update(score_flow(cfg, ft, tables, device, log, ip_rows=ip_rows))
                 summary["scored"] = res.get("flagged")
         else:
             R.skip("flow_post")
