@@ -90,7 +90,10 @@ def run(cfg, dist=None, device=None, log=print) -> dict:
                     C.write_corpus_files(lp, b_, dn_, wn_)
                 # the text files are the stage contract, not an input of the in-memory lda stage: written
                 # on a thread while the GPU runs EM; the lda_pre marker waits for them (finish_deferred)
-                res["_defer"] = C.background(write_files, "oni-lda-pre-writer")
+                if os.environ.get("ONI_DEFER_PRE", "1") != "0":
+                    res["_defer"] = C.background(write_files, "oni-lda-pre-writer")
+                else:
+                    write_files()
                 res.update(docs=built.corpus.num_docs, terms=built.corpus.num_terms, nnz=built.corpus.nnz)
                 summary["corpus"] = dict(docs=built.corpus.num_docs, terms=built.corpus.num_terms, nnz=built.corpus.nnz)
     elif not sharded:
