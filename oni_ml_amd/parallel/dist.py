@@ -52,7 +52,10 @@ class DistContext:
 
     # -------------------------------------------------------------- sharding
     def shard_range(self, corpus):
-        return shard_bounds(corpus.doc_ptr, self.world_size)[self.rank]
+        """This rank's documents of a corpus every rank holds whole (strong scaling): nnz-balanced, or
+        chain-aware with ONI_SHARD_CHAIN=1 (``chain_bounds``)."""
+        chain = os.environ.get("ONI_SHARD_CHAIN", "0") != "0"
+        return shard_bounds(corpus.doc_ptr, self.world_size, chain=chain)[self.rank]
 
     # ----------------------------------------------------------- collectives
     def allreduce_suffstats(self, cw: torch.Tensor, scalars: torch.Tensor) -> torch.Tensor:
@@ -352,8 +355,50 @@ class VocabExchange:
         return gc.to(cw.device)
 
 
-def shard_bounds(doc_ptr: np.ndarray, world: int):
-    """Contiguous [d0, d1) ranges with ~equal nnz (ties broken toward equal doc counts)."""
+CHAIN_KAPPA = 88.0   # chain cost of one word of the longest document / throughput cost of one entry:
+                     # headline day, K = 20: 1.64 ms for 22,721 words vs ~1.1 ms for the other 1.34 M entries
+
+
+def chain_bounds(doc_ptr: np.ndarray, world: int, kappa: float = CHAIN_KAPPA):
+    """Chain-aware contiguous shards: the rank that holds the longest document gets that document
+    alone, and the documents left and right of it are nnz-balanced over the other world - 1 ranks
+    (each side gets ranks in proportion to its entries).  Its block Gauss-Seidel sweeps are a serial
+    chain that no sharding shortens (profiles/r3_strong_emulated.md), so every other document on its
+    GPU only slows it.  Falls back to ``shard_bounds`` when the chain does not bound the shards
+    (kappa x longest <= nnz / world) or with fewer than 3 ranks."""
+    D = len(doc_ptr) - 1
+    nnz = int(doc_ptr[-1])
+    if world < 3 or D < world:
+        return shard_bounds(doc_ptr, world)
+    lens = np.diff(np.asarray(doc_ptr, np.int64))
+    p = int(np.argmax(lens))
+    if kappa * lens[p] <= nnz / world:
+        return shard_bounds(doc_ptr, world)
+    nl, nr = int(doc_ptr[p]), nnz - int(doc_ptr[p + 1])
+    rest = world - 1
+    kl = int(round(rest * nl / max(1, nl + nr)))
+    kl = min(max(kl, 1 if (nl > 0 and p > 0) else 0), rest - (1 if (nr > 0 and p < D - 1) else 0))
+    kr = rest - kl
+    out = []
+    if kl:
+        out += shard_bounds(np.asarray(doc_ptr[:p + 1], np.int64), kl)
+    elif p > 0:
+        return shard_bounds(doc_ptr, world)
+    out.append((p, p + 1))
+    if kr:
+        sub = np.asarray(doc_ptr[p + 1:], np.int64) - int(doc_ptr[p + 1])
+        out += [(p + 1 + a, p + 1 + b) for a, b in shard_bounds(sub, kr)]
+    elif p < D - 1:
+        return shard_bounds(doc_ptr, world)
+    return out
+
+
+def shard_bounds(doc_ptr: np.ndarray, world: int, chain: bool = False):
+    """Contiguous [d0, d1) ranges with ~equal nnz (ties broken toward equal doc counts).
+    ``chain``: ``chain_bounds`` instead (the engine's own sharding under ONI_SHARD_CHAIN=1; the
+    row-sharded pipeline keeps the nnz cut, which its corpus builder computes collectively)."""
+    if chain:
+        return chain_bounds(doc_ptr, world)
     D = len(doc_ptr) - 1
     nnz = int(doc_ptr[-1])
     if world <= 1 or D == 0:

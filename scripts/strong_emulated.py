@@ -99,21 +99,28 @@ def main():
                    full_ms=round(t_full * 1e3, 4), chain_floor_ms=round(t_chain * 1e3, 4), ranks={})
         bytes_ = K * c.num_terms * 8
         for n in [int(x) for x in a.ranks.split(",")]:
-            if n == 1:
-                per = [t_full]
-            else:
+            def shard_times(bounds):
                 per = []
-                for d0, d1 in shard_bounds(c.doc_ptr, n):
+                for d0, d1 in bounds:
                     sh = c.slice_docs(d0, d1)
                     e = LDAEngine(Corpus(sh.doc_ptr, sh.word_idx, sh.counts, c.num_terms), K, LDASettings(),
                                   backend="hip", seed=0, precision="fp64", local_shard=True)
                     per.append(_time_iteration(e, lb, alpha, vmi, D, a.reps))
                     del e
                     torch.cuda.empty_cache()
+                return per
+            per = [t_full] if n == 1 else shard_times(shard_bounds(c.doc_ptr, n))
+            # chain-aware shards (parallel/dist.py chain_bounds, ONI_SHARD_CHAIN=1): the longest document alone
+            cb = shard_bounds(c.doc_ptr, n, chain=True) if n > 1 else None
+            per_chain = shard_times(cb) if cb is not None and cb != shard_bounds(c.doc_ptr, n) else None
             ring = 0.0 if n == 1 else 2 * (n - 1) / n * bytes_ / LINK_BPS + 2 * (n - 1) * STEP_LAT
             mesh = 0.0 if n == 1 else 2 * bytes_ / (n * LINK_BPS) + 2 * STEP_LAT
             mx = max(per)
+            mc = max(per_chain) if per_chain else None
             rec["ranks"][n] = dict(per_rank_ms=[round(x * 1e3, 4) for x in per], max_ms=round(mx * 1e3, 4),
+                                   chain_aware_per_rank_ms=None if per_chain is None else [round(x * 1e3, 4) for x in per_chain],
+                                   chain_aware_max_ms=None if mc is None else round(mc * 1e3, 4),
+                                   chain_aware_speedup_mesh=None if mc is None else round(t_full / (mc + mesh), 3),
                                    allreduce_ring_ms=round(ring * 1e3, 4), allreduce_mesh_ms=round(mesh * 1e3, 4),
                                    iter_ms_ring=round((mx + ring) * 1e3, 4), iter_ms_mesh=round((mx + mesh) * 1e3, 4),
                                    speedup_ring=round(t_full / (mx + ring), 3), speedup_mesh=round(t_full / (mx + mesh), 3),
@@ -132,12 +139,15 @@ def main():
                      f"words; one GPU {rec['full_ms']} ms / EM iteration; **chain floor** (longest document alone) "
                      f"{rec['chain_floor_ms']} ms = at most {rec['full_ms'] / max(rec['chain_floor_ms'], 1e-9):.2f}x")
             L.append("")
-            L.append("| N | max shard ms | per-rank ms | all-reduce ring / mesh ms | iteration ms (ring / mesh) | speedup (ring / mesh) |")
-            L.append("|---|---|---|---|---|---|")
+            L.append("| N | max shard ms | per-rank ms | all-reduce ring / mesh ms | iteration ms (ring / mesh) | speedup (ring / mesh) | chain-aware: max shard ms, per-rank ms, speedup (mesh) |")
+            L.append("|---|---|---|---|---|---|---|")
             for n, r in rec["ranks"].items():
+                ca = "—" if not r.get("chain_aware_max_ms") else (
+                    f"{r['chain_aware_max_ms']}; {' '.join(str(x) for x in r['chain_aware_per_rank_ms'])}; "
+                    f"{r['chain_aware_speedup_mesh']}")
                 L.append(f"| {n} | {r['max_ms']} | {' '.join(str(x) for x in r['per_rank_ms'])} | "
                          f"{r['allreduce_ring_ms']} / {r['allreduce_mesh_ms']} | {r['iter_ms_ring']} / {r['iter_ms_mesh']} | "
-                         f"{r['speedup_ring']} / {r['speedup_mesh']} |")
+                         f"{r['speedup_ring']} / {r['speedup_mesh']} | {ca} |")
             L.append("")
         open(a.md, "w").write("\n".join(L) + "\n")
 

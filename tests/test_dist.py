@@ -168,3 +168,25 @@ def test_two_rank_ml_ops_pipeline_matches_one_rank(tmp_path, exchange):
         ra, rb = a.split(","), b.split(",")
         assert ra[:-2] == rb[:-2]
         assert np.allclose([float(x) for x in ra[-2:]], [float(x) for x in rb[-2:]], rtol=1e-9)
+
+
+def test_chain_bounds_isolate_the_longest_document():
+    """Chain-aware shards: contiguous, cover every document once, the longest document alone on its
+    rank, the rest nnz-balanced on both sides; nnz balance when no chain dominates."""
+    from oni_ml_amd.parallel.dist import chain_bounds
+    rng = np.random.default_rng(4)
+    lens = rng.integers(1, 12, 5000)
+    lens[3100] = 4000                                   # 4000 x 88 >> nnz / 8
+    ptr = np.concatenate([[0], np.cumsum(lens)])
+    for world in (3, 4, 8):
+        b = chain_bounds(ptr, world)
+        assert len(b) == world and b[0][0] == 0 and b[-1][1] == 5000
+        assert all(b[i][1] == b[i + 1][0] for i in range(world - 1))
+        assert (3100, 3101) in b
+        others = [int(ptr[e] - ptr[s]) for s, e in b if (s, e) != (3100, 3101)]
+        assert max(others) < 1.3 * (ptr[-1] - 4000) / (world - 1)
+    flat = np.concatenate([[0], np.cumsum(np.full(1000, 5))])
+    assert chain_bounds(flat, 4) == shard_bounds(flat, 4)
+    edge = np.concatenate([[0], np.cumsum(np.r_[9000, np.full(999, 5)])])   # longest first
+    b = chain_bounds(edge, 4)
+    assert b[0] == (0, 1) and b[-1][1] == 1000 and len(b) == 4
