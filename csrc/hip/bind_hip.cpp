@@ -167,6 +167,7 @@ PYBIND11_MODULE(_onihip, m) {
     oni::launch_init_random_ss(P<double>(cw), V, K, KS, seed, S(stream));
   });
   m.def("gs_split_capacity", [](int KS) { return oni::gs_split_capacity(KS); });
+  m.def("gs_split_umax", [](int KS) { return oni::gs_split_umax(KS); });
   m.def("gs_split", [](u doc_ptr, u word_idx, u counts, u beta, int K, int KS, int gs_updates, u params, u gamma,
                        u cphi, u lik, u alpha_ss, u iters, u seg_doc, u seg_index, u seg_count, u seg_base,
                        u doc_slot, int n_blocks, u xchg, u counter, int n_docs, u error, u stream, u dbg) {

@@ -230,7 +230,8 @@ void launch_gs_estep(const GSArgs& a, int variant, int KS, hipStream_t s);
 void launch_gs_stage(const double* beta, const int* word_idx, const int* tile_ent, const int* tile_cnt, int n_tiles,
                      double* stage, int KS, hipStream_t s);
 int gs_tiny_max(int KS);   // longest document of the kGsTiny kernel
-int gs_umax(int KS);       // largest gs_updates the E-step accepts at row stride KS (split: kGsUMax)
+int gs_umax(int KS);       // largest gs_updates the E-step accepts at row stride KS
+int gs_split_umax(int KS); // largest gs_updates of the split kernel (64 at KS <= 52, else kGsUMax)
 // One long document over s.seg_count[b] workgroups (8 waves each): every chunk is cut into
 // that many word ranges whose partials are exchanged as tagged granules (2 per double,
 // s.xchg = [2][n_blocks][2 (KS + 1)]); s.seg_words is unused.  Every segment of a launch

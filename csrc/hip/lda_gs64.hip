@@ -1337,7 +1337,10 @@ __global__ __launch_bounds__(512) void gs_split(GSArgs a, SplitArgs sp) {
 // prefetches (vmcnt is in order per wave, and the hand-off price sits in the consumer's memory
 // queue -- MI355X_MICROARCH handoff-1to1 / gather-pass), and a chunk costs one workgroup barrier
 // instead of three.  Same exchange buffer, tags, epoch and co-residency rules as gs_split.
-template <int KS>
+// UM: chunk-table rows in LDS (U <= UM): 32, or 64 where 2 x 64 x KS doubles still fit the 64 KB of
+// static LDS (KS <= 52: K = 50 at U = 64, the schedule that meets lda-c parity there,
+// profiles/r3_precision_parity.md)
+template <int KS, int UM = kGsUMax>
 __global__ __launch_bounds__(512) void gs_splitw(GSArgs a, SplitArgs sp) {
   using T = TeamShape<KS, 8>;   // word-slot geometry and prefetch depth of the 8-wave team
   constexpr int NW = 7, NTD = (NW + 1) * 64, TG = T::TG, KPL = T::KPL, NSW = T::NSW, LSW = T::LSW, NS = NW * NSW,
@@ -1345,12 +1348,12 @@ __global__ __launch_bounds__(512) void gs_splitw(GSArgs a, SplitArgs sp) {
   constexpr int NC = KS + 1;                 // exchanged columns: KS topic sums + the log-sum
   constexpr int GR = 2 * NC;                 // granules per segment row
   constexpr int TC = (NC + 63) / 64;         // columns per topic-wave lane
-  __shared__ double sC[kGsUMax][KS];
-  __shared__ double sEt[kGsUMax][KS];
+  __shared__ double sC[UM][KS];
+  __shared__ double sEt[UM][KS];
   __shared__ double sE[KS];
   __shared__ double sRed[NW][KS];
   __shared__ double sRedL[NW];
-  __shared__ double sCs[kGsUMax];
+  __shared__ double sCs[UM];
   __shared__ double sScal[4];
   __shared__ int arrive[NW];   // per word wave: chunks whose partial sums it has left in sRed / sRedL
   __shared__ int sFail;
@@ -2739,12 +2742,31 @@ static int gs_split_variant() {
 }
 
 template <int KS>
+constexpr int split_umax_ks() { return KS <= 52 ? 64 : kGsUMax; }
+
+int gs_split_umax(int KS) {
+  switch (KS) {
+#define ONI_KS(X) \
+  case X:         \
+    return split_umax_ks<X>();
+    ONI_FOR_EACH_KS(ONI_KS)
+#undef ONI_KS
+    default:
+      return kGsUMax;
+  }
+}
+
+template <int KS>
 static int gs_split_capacity_ks() {
   int dev = 0, per_cu = 0;
   hipDeviceProp_t p;
   ONI_HIP_CHECK(hipGetDevice(&dev));
   ONI_HIP_CHECK(hipGetDeviceProperties(&p, dev));
-  if (gs_split_variant() == 2)
+  if (gs_split_variant() == 2 && split_umax_ks<KS>() > kGsUMax) {
+    // the U <= 64 instantiation holds the larger LDS tables: its residency bounds both
+    ONI_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(
+        &per_cu, reinterpret_cast<const void*>(&gs::gs_splitw<KS, split_umax_ks<KS>()>), 512, 0));
+  } else if (gs_split_variant() == 2)
     ONI_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(
         &per_cu, reinterpret_cast<const void*>(&gs::gs_splitw<KS>), 512, 0));
   else
@@ -2767,16 +2789,21 @@ int gs_split_capacity(int KS) {
 
 void launch_gs_split(const GSArgs& a, const SplitArgs& s, int KS, hipStream_t st) {
   if (s.n_blocks <= 0) return;
-  if (a.gs_updates < 1 || a.gs_updates > kGsUMax)
-    throw std::runtime_error("gs_split: gs_updates must be in [1, " + std::to_string(kGsUMax) + "]");
+  const int um = gs_split_variant() == 2 ? gs_split_umax(KS) : kGsUMax;
+  if (a.gs_updates < 1 || a.gs_updates > um)
+    throw std::runtime_error("gs_split: gs_updates must be in [1, " + std::to_string(um) + "] at KS " +
+                             std::to_string(KS));
   if (!a.params) throw std::runtime_error("gs_split: params block required");
   switch (KS) {
-#define ONI_KS(X)                                                                         \
-  case X:                                                                                 \
-    if (gs_split_variant() == 2)                                                          \
-      hipLaunchKernelGGL((gs::gs_splitw<X>), dim3(s.n_blocks), dim3(512), 0, st, a, s);   \
-    else                                                                                  \
-      hipLaunchKernelGGL((gs::gs_split<X>), dim3(s.n_blocks), dim3(512), 0, st, a, s);    \
+#define ONI_KS(X)                                                                                          \
+  case X:                                                                                                  \
+    if (gs_split_variant() == 2 && a.gs_updates > kGsUMax) {                                               \
+      if constexpr (split_umax_ks<X>() > kGsUMax)                                                          \
+        hipLaunchKernelGGL((gs::gs_splitw<X, split_umax_ks<X>()>), dim3(s.n_blocks), dim3(512), 0, st, a, s); \
+    } else if (gs_split_variant() == 2)                                                                    \
+      hipLaunchKernelGGL((gs::gs_splitw<X>), dim3(s.n_blocks), dim3(512), 0, st, a, s);                    \
+    else                                                                                                   \
+      hipLaunchKernelGGL((gs::gs_split<X>), dim3(s.n_blocks), dim3(512), 0, st, a, s);                     \
     break;
     ONI_FOR_EACH_KS(ONI_KS)
 #undef ONI_KS

@@ -541,6 +541,13 @@ def gs_umax(KS: int = 0) -> int:
     return int(lib().gs_umax(int(KS)))
 
 
+def gs_split_umax(KS: int) -> int:
+    """Largest U of the split-document kernel: its chunk tables live in LDS (64 at KS <= 52, else 32)."""
+    if os.environ.get("ONI_GS_SPLIT_V", "2") != "2":
+        return gs_umax()
+    return int(lib().gs_split_umax(int(KS)))
+
+
 def gs_tiny_max(KS: int) -> int:
     return int(lib().gs_tiny_max(int(KS)))
 
@@ -806,7 +813,7 @@ def gs_split(doc_ptr, word_idx, counts, beta, K, gs_updates, params, gamma, cphi
     nb = batch["n_blocks"]
     if KS not in compiled_ks():
         raise ValueError(f"beta row stride {KS} has no compiled kernel")
-    if not (0 < K <= KS) or not (1 <= int(gs_updates) <= gs_umax()):
+    if not (0 < K <= KS) or not (1 <= int(gs_updates) <= gs_split_umax(KS)):
         raise ValueError("K or gs_updates out of range")
     for k in ("seg_doc", "seg_index", "seg_count", "seg_base", "doc_slot"):
         _chk(batch[k], torch.int32, k, (nb,), dev)
@@ -856,8 +863,8 @@ class GSPlan:
         # -> 3.36 / 3.34 ms per EM iteration (profiles/r3_tuning_log.md)
         if split_min is None:
             split_min = int(os.environ.get("ONI_GS_SPLIT_MIN", "2048" if KS > 32 else "0"))
-        if int(gs_updates) > gs_umax():
-            split_min = 0       # the split kernel keeps its chunk tables in LDS: U <= 32 only
+        if int(gs_updates) > gs_split_umax(KS):
+            split_min = 0       # the split kernel keeps its chunk tables in LDS: U <= 64 at KS <= 52, else 32
         self.split = None
         if split_min > 0 and (L > split_min).any():
             m = L[order] > split_min

@@ -220,14 +220,16 @@ def test_staged_rows_bitwise_equal_beta_rows(monkeypatch):
         assert np.array_equal(a, b)
 
 
-@pytest.mark.parametrize("K,env", [
-    (100, {}),                                                          # default split for KS > 32
-    (100, {"ONI_GS_SPLIT_MIN": "4000"}),
-    (100, {"ONI_GS_SPLIT_MIN": "4000", "ONI_SPLIT_MAX_BLOCKS": "9", "ONI_GS_SPLIT_G": "3", "ONI_GS_SPLIT_BATCHES": "8"}),
-    (20, {"ONI_GS_SPLIT_MIN": "3000", "ONI_GS_SPLIT_G": "5"}),          # forced on a narrow KS
-    (52, {"ONI_GS_SPLIT_MIN": "2500"}),
+@pytest.mark.parametrize("K,env,U", [
+    (100, {}, 32),                                                      # default split for KS > 32
+    (100, {"ONI_GS_SPLIT_MIN": "4000"}, 32),
+    (100, {"ONI_GS_SPLIT_MIN": "4000", "ONI_SPLIT_MAX_BLOCKS": "9", "ONI_GS_SPLIT_G": "3", "ONI_GS_SPLIT_BATCHES": "8"}, 32),
+    (20, {"ONI_GS_SPLIT_MIN": "3000", "ONI_GS_SPLIT_G": "5"}, 32),      # forced on a narrow KS
+    (52, {"ONI_GS_SPLIT_MIN": "2500"}, 32),
+    (50, {}, 64),                                                       # 64-row LDS tables (KS 52, U = 64)
+    (50, {"ONI_GS_SPLIT_MIN": "2500", "ONI_GS_SPLIT_G": "3"}, 48),
 ])
-def test_split_documents_match_oracle(K, env, monkeypatch):
+def test_split_documents_match_oracle(K, env, U, monkeypatch):
     """gs_split (one document over G workgroups exchanging tagged per-chunk partials) against the
     oracle: every replica runs the same refresh, so gamma / likelihood / class_word match at 1e-10."""
     for k, v in env.items():
@@ -241,7 +243,6 @@ def test_split_documents_match_oracle(K, env, monkeypatch):
     words = np.concatenate([rng.choice(V, n, replace=False) for n in lens]).astype(np.int32)
     counts = rng.integers(1, 4, words.size)
     c = Corpus(ptr.astype(np.int64), words, counts.astype(np.int64), V)
-    U = 32
     lb = _log_beta(V, K, seed=5)
     st = LDASettings(var_max_iter=5, var_converged=-1e30)
     ref = _oracle(c, lb, 0.33, st, U)
