@@ -159,9 +159,9 @@ PYBIND11_MODULE(_onihip, m) {
                   P<const long long>(stage_off)};
     oni::launch_gs_estep(a, variant, KS, S(stream));
   });
-  m.def("gs_stage", [](u beta, u word_idx, u tile_ent, u tile_cnt, int n_tiles, u stage, int KS, u stream) {
+  m.def("gs_stage", [](u beta, u word_idx, u tile_ent, u tile_cnt, int n_tiles, u stage, int KS, u gate, u stream) {
     oni::launch_gs_stage(P<const double>(beta), P<const int>(word_idx), P<const int>(tile_ent),
-                         P<const int>(tile_cnt), n_tiles, P<double>(stage), KS, S(stream));
+                         P<const int>(tile_cnt), n_tiles, P<double>(stage), KS, P<const double>(gate), S(stream));
   });
   m.def("init_random_ss", [](u cw, int V, int K, int KS, unsigned long long seed, u stream) {
     oni::launch_init_random_ss(P<double>(cw), V, K, KS, seed, S(stream));

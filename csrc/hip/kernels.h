@@ -228,7 +228,7 @@ void launch_gs_estep(const GSArgs& a, int variant, int KS, hipStream_t s);
 // stage[(t KS/2 + k) 64 + l] (double2) = beta row pair k of the word at corpus entry tile_ent[t] + l
 // (l < tile_cnt[t], else 0): the staged rows of launch_gs_estep, filled after every M-step
 void launch_gs_stage(const double* beta, const int* word_idx, const int* tile_ent, const int* tile_cnt, int n_tiles,
-                     double* stage, int KS, hipStream_t s);
+                     double* stage, int KS, const double* gate, hipStream_t s);   // gate: as gs_mstep
 int gs_tiny_max(int KS);   // longest document of the kGsTiny kernel
 int gs_umax(int KS);       // largest gs_updates the E-step accepts at row stride KS
 int gs_split_umax(int KS); // largest gs_updates of the split kernel (64 at KS <= 52, else kGsUMax)

@@ -2550,7 +2550,8 @@ __global__ __launch_bounds__(256) void gs_stage_kernel(const double* __restrict_
                                                        const int* __restrict__ word_idx,
                                                        const int* __restrict__ tile_ent,
                                                        const int* __restrict__ tile_cnt, int n_tiles,
-                                                       dvec2* __restrict__ out) {
+                                                       dvec2* __restrict__ out, const double* gate) {
+  if (gate != nullptr && *gate != 0.0) return;   // converged EM loop: the queued iterations are no-ops
   // one thread per (tile, lane): its word's whole row in KS / 2 independent 16-byte loads, stored
   // as one 16-byte element per topic pair (a wave's stores are 1 KB-contiguous per pair)
   const long long total = (long long)n_tiles * 64;
@@ -2686,7 +2687,7 @@ static void gs_estep_ks(const GSArgs& a, int variant, hipStream_t s) {
 int gs_umax(int KS) { return KS > 32 ? kGsUMaxWide : kGsUMax; }
 
 void launch_gs_stage(const double* beta, const int* word_idx, const int* tile_ent, const int* tile_cnt, int n_tiles,
-                     double* stage, int KS, hipStream_t s) {
+                     double* stage, int KS, const double* gate, hipStream_t s) {
   if (n_tiles <= 0) return;
   if (KS > 32 || KS % 2) throw std::runtime_error("gs_stage: staged rows need an even KS <= 32");
   const long long total = (long long)n_tiles * 64;
@@ -2696,7 +2697,7 @@ void launch_gs_stage(const double* beta, const int* word_idx, const int* tile_en
   case X:                                                                                                   \
     if constexpr (X <= 32 && X % 2 == 0)                                                                    \
       hipLaunchKernelGGL((gs::gs_stage_kernel<X>), dim3(blocks), dim3(256), 0, s, beta, word_idx, tile_ent, \
-                         tile_cnt, n_tiles, reinterpret_cast<gs::dvec2*>(stage));                           \
+                         tile_cnt, n_tiles, reinterpret_cast<gs::dvec2*>(stage), gate);                     \
     break;
     ONI_FOR_EACH_KS(ONI_KS)
 #undef ONI_KS

@@ -616,7 +616,7 @@ class LDAEngine:
             for var, order in gp.plan:
                 st = self._stages.get(id(order))
                 if st is not None:
-                    H.gs_stage(self.beta, dc.word_idx, st)
+                    H.gs_stage(self.beta, dc.word_idx, st, gate=self._gate)
         self._ev_fork.record(main)
         used = []
         # side streams: the long-document buckets (critical path) are dispatched first, the split
@@ -645,7 +645,7 @@ class LDAEngine:
                 else:
                     st = self._stages.get(id(order))
                     if st is not None and not stage_main:   # refill on the bucket's own stream
-                        H.gs_stage(self.beta, dc.word_idx, st)
+                        H.gs_stage(self.beta, dc.word_idx, st, gate=self._gate)
                     H.gs_estep(dc.doc_ptr, dc.word_idx, dc.counts, order, self.beta, self.K, self._U, prm,
                                self.gamma, cphi, self.lik, self.ass, self.iters, var, ent_base=ent_base, stage=st)
         # every bucket but work[0] is joined first and the early pass overlaps work[0]

@@ -603,8 +603,9 @@ class GSStage:
         return self.n_tiles * (self.KS // 2) * 64 * 16
 
 
-def gs_stage(beta, word_idx, st: "GSStage"):
-    """Refill the staged rows of ``st`` from ``beta`` (after every M-step, before the team8 launch)."""
+def gs_stage(beta, word_idx, st: "GSStage", gate=None):
+    """Refill the staged rows of ``st`` from ``beta`` (after every M-step, before the team8 launch);
+    ``gate``: the EM loop's done flag (a converged loop's queued iterations skip the copy)."""
     V, KS = beta.shape
     dev = beta.device
     if KS != st.KS:
@@ -614,7 +615,7 @@ def gs_stage(beta, word_idx, st: "GSStage"):
     lib().gs_stage(_chk(beta, torch.float64, "beta", (V, KS), dev), _chk(word_idx, torch.int32, "word_idx", None, dev),
                    _chk(st.tile_ent, torch.int32, "tile_ent", (st.n_tiles,), dev),
                    _chk(st.tile_cnt, torch.int32, "tile_cnt", (st.n_tiles,), dev), st.n_tiles,
-                   _chk(st.buf, torch.float64, "stage", None, dev), int(KS), _stream())
+                   _chk(st.buf, torch.float64, "stage", None, dev), int(KS), _gate_ptr(gate, dev), _stream())
 
 
 def gs_estep(doc_ptr, word_idx, counts, order, beta, K, gs_updates, params, gamma, cphi, lik, alpha_ss, iters, variant,

@@ -275,3 +275,17 @@ def test_stage_runner_deferred_markers(tmp_path):
         res["_defer"] = boom
     R.finish_deferred(suppress=True)           # another error already propagating
     assert not R.done("d")
+
+
+def test_background_writer_join_reraises():
+    """pipeline/common.py background(): the join callable a stage defers re-raises the thread's error."""
+    from oni_ml_amd.pipeline import common as C
+    out = []
+    C.background(lambda: out.append(1))()
+    assert out == [1]
+
+    def boom():
+        raise OSError("disk full")
+    join = C.background(boom)
+    with pytest.raises(OSError, match="disk full"):
+        join()
