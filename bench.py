@@ -124,7 +124,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--topics", type=int, default=20)
     ap.add_argument("--gs-updates", type=int, default=0,
-                    help="U, gamma refreshes per sweep of the fp64 engine (0: 32; > 32 needs K > 32)")
+                    help="U, gamma refreshes per sweep of the fp64 engine (0: 32; > 32 needs K > 32; -1: the U "
+                         "per K that meets lda-c parity, em.parity_gs_updates)")
     ap.add_argument("--events", type=int, default=None, help="events per GPU (default: flow 1M, dns 2M)")
     ap.add_argument("--corpus", choices=["flow", "dns", "planted"], default="flow",
                     help="flow: BASELINE headline (1-day netflow); dns: BASELINE config 4 (1-day DNS)")

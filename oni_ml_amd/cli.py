@@ -39,8 +39,8 @@ def _common_lda_args(ap):
     ap.add_argument("--verbose", action="store_true")
     ap.add_argument("--gs-updates", type=int, default=None,
                     help="U, gamma refreshes per document sweep of the fp64 GPU engine (default 32; up to 4096 "
-                         "at K > 32; lda-c's per-word schedule is U >= document length -- "
-                         "profiles/r3_precision_parity.md gives the U per K that matches lda-c)")
+                         "at K > 32; lda-c's per-word schedule is U >= document length; -1: the U per K that "
+                         "meets lda-c parity, profiles/r3_precision_parity.md)")
     ap.add_argument("--lag", type=int, default=None, help="period of the %%03d model files (lda-c: 5; 0: only 000 "
                                                           "and final)")
     ap.add_argument("--cphi-gb", type=float, default=None,

@@ -376,16 +376,20 @@ class LDAEngine:
         if self.backend == "hip" and self.fp64:
             return f"block Gauss-Seidel, fp64, {self._U} gamma refreshes per sweep (lda-c per-word up to {self._U} words)"
         if self.backend == "cpu":
-            u = int(self.settings.gs_updates)
+            u = resolved_gs_updates(self.settings, self.K)
             return "lda-c per-word Gauss-Seidel, fp64" if u == 0 else f"block Gauss-Seidel, fp64, {u} refreshes per sweep"
         return "Jacobi, " + ("fp32 E-step" if self.backend == "hip" else "fp64")
 
     # ------------------------------------------------- fp64 block Gauss-Seidel
     def gs_updates(self) -> int:
-        """U: gamma refreshes per sweep of the fp64 engine (settings.gs_updates, 0 = the default 32)."""
+        """U: gamma refreshes per sweep of the fp64 engine (settings.gs_updates, 0 = the default 32,
+        -1 = ``parity_gs_updates(K)``)."""
         from ...ops import hip as H
         KS = H.padded_topics(self.K)
-        u = int(self.settings.gs_updates) or min(32, H.gs_umax(KS))
+        u = int(self.settings.gs_updates)
+        if u < 0:
+            u = parity_gs_updates(self.K)
+        u = u or min(32, H.gs_umax(KS))
         if not 1 <= u <= H.gs_umax(KS):
             raise ValueError(f"gs_updates={u}: the GPU engine supports 1..{H.gs_umax(KS)} at K={self.K} "
                              f"(more than {H.gs_umax()} needs K > 32)")
@@ -833,7 +837,7 @@ class LDAEngine:
         res = self._native.lda_estep_ldac(
             self.corpus.doc_ptr, self.corpus.word_idx, self.corpus.counts,
             np.ascontiguousarray(lb.T.numpy()), self.alpha, self.var_max_iter, self.settings.var_converged,
-            nshards=self.cpu_shards, threads=_cpu_threads(), gs_updates=self.settings.gs_updates)
+            nshards=self.cpu_shards, threads=_cpu_threads(), gs_updates=resolved_gs_updates(self.settings, self.K))
         self.gamma = torch.from_numpy(res["gamma"])
         self.iters = torch.from_numpy(res["iters"])
         self.lik = torch.from_numpy(res["doc_likelihood"])
@@ -1420,7 +1424,7 @@ class LDAEngine:
             return self._native.lda_assign_ldac(self.corpus.doc_ptr, self.corpus.word_idx,
                                                 self.corpus.counts.astype(np.float64), np.ascontiguousarray(lb.T.numpy()),
                                                 self.alpha, self.var_max_iter, self.settings.var_converged,
-                                                gs_updates=self.settings.gs_updates).astype(np.int64)
+                                                gs_updates=resolved_gs_updates(self.settings, self.K)).astype(np.int64)
         raise NotImplementedError(f"word assignments for backend {self.backend} / {self.precision}")
 
     def local_gamma(self) -> np.ndarray:
@@ -1517,6 +1521,24 @@ class LDAEngine:
         res = LDAResult(log_beta=None, gamma=None, alpha=self.alpha, num_topics=self.K, num_terms=self.V,
                         likelihoods=hist, stats=stats, em_iterations=i, seconds=time.perf_counter() - t0)
         return res
+
+
+def resolved_gs_updates(settings, K: int) -> int:
+    """settings.gs_updates with -1 (the parity mode) resolved for K; 0 stays 0 (the CPU engine's
+    literal per-word schedule, the GPU engine's default 32)."""
+    u = int(settings.gs_updates)
+    return parity_gs_updates(K) if u < 0 else u
+
+
+def parity_gs_updates(K: int) -> int:
+    """The U per K that meets lda-c parity on the BASELINE configs (profiles/r3_precision_parity.md:
+    >= 85 % overlap of the 0.1 % most suspicious entries, alpha <= 1 %, final likelihood <= 1e-4;
+    K = 100 reaches 82-84 % overlap from U = 1024 on, with alpha and the likelihood within 1e-5)."""
+    if K <= 32:
+        return 32
+    if K <= 52:
+        return 64          # K = 50: 94.5 % overlap; the split kernel keeps 64-row tables (5.6 ms / EM iteration)
+    return 1024
 
 
 def _log_beta_host(cw: torch.Tensor, ct: torch.Tensor, elems: int = 1 << 25) -> np.ndarray:

@@ -9,7 +9,7 @@ import numpy as np
 import torch
 
 from ...io import ldac
-from .em import LDAEngine
+from .em import LDAEngine, resolved_gs_updates
 from .settings import LDASettings
 
 
@@ -27,7 +27,7 @@ def infer(corpus, log_beta: np.ndarray, alpha: float, settings: LDASettings, bac
         lb = np.ascontiguousarray(log_beta)
         r = eng._native.lda_estep_ldac(corpus.doc_ptr, corpus.word_idx, corpus.counts, lb, alpha,
                                        settings.var_max_iter, settings.var_converged, 1, 0,
-                                       gs_updates=settings.gs_updates)
+                                       gs_updates=resolved_gs_updates(settings, K))
         lik = np.asarray(r["doc_likelihood"])
         return r["gamma"], lik
     eng.e_step()

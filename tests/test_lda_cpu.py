@@ -233,3 +233,13 @@ def test_cphi_window_bounds_cover_corpus_within_budget():
             assert x["e0"] == ptr[x["d0"]] and x["e1"] == ptr[x["d1"]]
             assert x["e1"] - x["e0"] <= budget or x["d1"] - x["d0"] == 1
     assert len(cphi_window_bounds(ptr, int(ptr[-1]))) == 1
+
+
+def test_parity_gs_updates_mode():
+    """gs_updates = -1: the U per K of profiles/r3_precision_parity.md, resolved for every engine."""
+    from oni_ml_amd.models.lda.em import parity_gs_updates, resolved_gs_updates
+    from oni_ml_amd.models.lda.settings import LDASettings
+    assert [parity_gs_updates(k) for k in (20, 32, 50, 52, 100)] == [32, 32, 64, 64, 1024]
+    assert resolved_gs_updates(LDASettings(gs_updates=-1), 50) == 64
+    assert resolved_gs_updates(LDASettings(gs_updates=0), 50) == 0
+    assert resolved_gs_updates(LDASettings(gs_updates=16), 100) == 16
