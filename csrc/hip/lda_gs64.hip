@@ -2503,6 +2503,9 @@ __global__ __launch_bounds__(256) void gs_mstep_control_kernel(const double* __r
                                                                const int* __restrict__ rows, int n_rows,
                                                                EMControlArgs c, NewtonArgs nw) {
   if (c.params[kParamDone] != 0.0) return;
+  // with the alpha Newton (a serial chain of ~10-20 digamma / trigamma / exp / log steps on two lanes),
+  // block 0 runs only the Newton and the other blocks compute beta beside it
+  const bool newton = nw.enabled && gridDim.x > 1;
   if (nw.enabled && blockIdx.x == 0 && threadIdx.x < 64) {
     if (threadIdx.x < 2)
       alpha_newton_lanes(c.scalars, nw.num_docs, K, nw.estimate, c.params, nw.alpha_out, threadIdx.x);
@@ -2512,7 +2515,8 @@ __global__ __launch_bounds__(256) void gs_mstep_control_kernel(const double* __r
   const int total2 = (rows ? n_rows : V) * hq;
   const double2* cw2 = reinterpret_cast<const double2*>(cw);
   double2* beta2 = reinterpret_cast<double2*>(beta);
-  for (int g = blockIdx.x * blockDim.x + threadIdx.x; g < total2; g += gridDim.x * blockDim.x) {
+  const int bx = newton ? (int)blockIdx.x - 1 : (int)blockIdx.x, nbx = newton ? (int)gridDim.x - 1 : (int)gridDim.x;
+  for (int g = bx * blockDim.x + threadIdx.x; bx >= 0 && g < total2; g += nbx * blockDim.x) {
     const int k0 = (g % hq) * 2;
     const int i = rows ? rows[g / hq] * hq + g % hq : g;
     const double2 v = cw2[i];
@@ -2841,6 +2845,7 @@ void launch_gs_mstep_control(const double* cw, const double* class_total, double
   int64_t blocks = (total / 2 + 255) / 256;
   if (blocks > 512) blocks = 512;
   if (blocks < 1) blocks = 1;
+  if (nw.enabled) blocks += 1;   // block 0: the alpha Newton alone
   hipLaunchKernelGGL(gs::gs_mstep_control_kernel, dim3((unsigned)blocks), dim3(256), 0, s, cw, class_total, beta, V,
                      K, KS, rows, n_rows, c, nw);
   ONI_HIP_CHECK(hipGetLastError());
