@@ -17,6 +17,7 @@
 #   nccl      the one-rank RCCL test (tests/test_gpu_dist.py -k nccl)
 #   ab        scripts/ab_env.sh $AB_ROUNDS $AB_VARIANTS (space-separated env settings, one per variant)
 #   ranks     scripts/pipeline_ranks.py $RANKS_ARGS (per-rank stage seconds of the sharded ml_ops pipeline)
+#   e2e       scripts/ab_e2e.sh $E2E_ROUNDS $E2E_VARIANTS (bench's ml_ops e2e wall under env variants)
 # env: TAG (output dir gpurun_out/$TAG, default s), BENCH_ARGS, PROF_ARGS, PARITY_ARGS, PMC, PMC_ARGS, KEEP_GOING=1
 # (this script replaces the per-experiment gpu_*.sh drivers of rounds 1-2; their records name them)
 # (a failing pytest with exit status 1 -- assertion failures, not a crash -- does not stop the session)
@@ -86,6 +87,10 @@ for s in "$@"; do
       timeout -k 10 1100 python -u scripts/pipeline_ranks.py ${RANKS_ARGS:-} --json "$OUT/ranks.json" \
         --md "$OUT/ranks.md" > "$OUT/ranks.log" 2>&1 || { tail -30 "$OUT/ranks.log"; stop ranks 1; }
       cat "$OUT/ranks.md" ;;
+    e2e)
+      timeout -k 10 1000 bash scripts/ab_e2e.sh ${E2E_ROUNDS:-2} ${E2E_VARIANTS:-ONI_DEFER_PRE=1} > "$OUT/ab_e2e.log" 2>&1 \
+        || { tail -20 "$OUT/ab_e2e.log"; stop e2e 1; }
+      cat "$OUT/ab_e2e.log" ;;
     nccl)
       timeout -k 10 300 python -u -m pytest tests/test_gpu_dist.py -m gpu -v -k nccl --timeout 120 \
         --timeout-method thread > "$OUT/nccl.log" 2>&1 || { tail -30 "$OUT/nccl.log"; stop nccl 1; }
