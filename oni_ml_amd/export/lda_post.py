@@ -98,6 +98,27 @@ def export(doc_names, gamma, word_names, log_beta, doc_path, word_path, strict=T
     return theta, phi, wnames
 
 
+def export_deferred(doc_names, gamma, word_names, log_beta, doc_path, word_path, strict=True):
+    """``export(read_back=True)`` whose two files are written on a thread: returns (θ, φ as the scorers
+    parse them, word keys as written, join).  The read-back tables come from ``roundtrip_py2`` (the
+    same Python-2 str -> strtod text round trip the writer's read-back performs, value by value), so
+    the scoring stage starts while the files are still being formatted."""
+    from ..pipeline.common import background
+    check_strict_k(gamma.shape[1], strict)
+    theta = doc_topics(gamma, strict)
+    phi = word_topics(log_beta, strict)
+    wnames = truncate_s20(word_names) if strict else list(word_names)
+    n = native.lib()
+    th_b = n.roundtrip_py2(np.ascontiguousarray(theta))
+    ph_b = n.roundtrip_py2(np.ascontiguousarray(phi))
+    dn = list(doc_names)
+
+    def write():
+        write_doc_results(doc_path, dn, theta)
+        write_word_results(word_path, wnames, phi)
+    return th_b, ph_b, wnames, background(write, "oni-lda-post-writer")
+
+
 def _format_table(names, values, read_back):
     n = len(names)
     vals = np.ascontiguousarray(values, np.float64)

@@ -136,7 +136,18 @@ def run(cfg, dist=None, device=None, log=print) -> dict:
                 from ..models.lda.estimate import load_final
                 gamma, log_beta = load_final(cfg.lpath)
             with R.stage("lda_post") as res:
-                tables = C.run_export(cfg, doc_names, gamma, word_names, log_beta, read_back=True)
+                if os.environ.get("ONI_DEFER_POST", "1") != "0":
+                    # the result files are written on a thread while flow_post scores (its tables
+                    # are the text round trip of the same values); the lda_post marker waits for them
+                    from ..export import lda_post as LP
+                    th, ph, wn, join = LP.export_deferred(doc_names, gamma, word_names, log_beta,
+                                                          os.path.join(cfg.lpath, "doc_results.csv"),
+                                                          os.path.join(cfg.lpath, "word_results.csv"),
+                                                          strict=cfg.strict)
+                    tables = C.ModelTables(list(doc_names), th, wn, ph)
+                    res["_defer"] = join
+                else:
+                    tables = C.run_export(cfg, doc_names, gamma, word_names, log_beta, read_back=True)
         else:
             R.skip("lda_post")
             tables = C.load_model_tables(cfg.lpath)

@@ -133,3 +133,28 @@ def test_export_read_back_equals_text_roundtrip(tmp_path):
     assert np.array_equal(ph, N.roundtrip_py2(np.ascontiguousarray(ph0)))
     _, tv = lda_post.read_results(str(tmp_path / "d.csv"))
     assert np.array_equal(tv, th)
+
+
+def test_export_deferred_matches_read_back_export(tmp_path):
+    """export_deferred: the same files, and the round-trip tables bitwise equal to the writer's read-back."""
+    import numpy as np
+    from oni_ml_amd.export import lda_post
+    rng = np.random.default_rng(5)
+    D, V, K = 300, 200, 20
+    gamma = rng.gamma(0.3, 2.0, (D, K)) + 1e-3
+    gamma[3] = 0.0
+    lb = np.log(rng.dirichlet(np.full(V, 0.1), K))
+    docs = [f"10.0.{i // 256}.{i % 256}" for i in range(D)]
+    words = [f"{i}_80_tcp_{'x' * (i % 30)}" for i in range(V)]
+    for strict in (True, False):
+        a = tmp_path / f"a{strict}"
+        b = tmp_path / f"b{strict}"
+        a.mkdir(), b.mkdir()
+        th, ph, wn = lda_post.export(docs, gamma, words, lb, str(a / "d.csv"), str(a / "w.csv"), strict=strict,
+                                     read_back=True)
+        th2, ph2, wn2, join = lda_post.export_deferred(docs, gamma, words, lb, str(b / "d.csv"), str(b / "w.csv"),
+                                                       strict=strict)
+        join()
+        assert np.array_equal(th, th2) and np.array_equal(ph, ph2) and wn == wn2
+        for f in ("d.csv", "w.csv"):
+            assert (a / f).read_bytes() == (b / f).read_bytes()
