@@ -136,7 +136,7 @@ def run(cfg, dist=None, device=None, log=print) -> dict:
                 from ..models.lda.estimate import load_final
                 gamma, log_beta = load_final(cfg.lpath)
             with R.stage("lda_post") as res:
-                if os.environ.get("ONI_DEFER_POST", "1") != "0":
+                if os.environ.get("ONI_DEFER_POST", "0") != "0":   # measured: no e2e gain (tuning log)
                     # the result files are written on a thread while flow_post scores (its tables
                     # are the text round trip of the same values); the lda_post marker waits for them
                     from ..export import lda_post as LP
