@@ -790,8 +790,12 @@ __global__ __launch_bounds__(team_threads(KS, NW), MINW) void gs_team(GSArgs a) 
         load_rows(wc);
         load_ids(j2, wn, cn, vn);
         tick(0);
+        // whole active waves; a one-word chunk (lda-c's per-word schedule: every chunk of a document of
+        // <= U words) has its word in slot 0 and exact zeros in the other slots, so the sum is slot 0's
+        if (n1 - n0 > 1) {
 #pragma unroll
-        for (int i = 0; i < KPL; ++i) acc[i] = bits_sum<0, LSW, false>(acc[i]);   // whole active waves
+          for (int i = 0; i < KPL; ++i) acc[i] = bits_sum<0, LSW, false>(acc[i]);
+        }
         if (sl == 0) {
 #pragma unroll
           for (int i = 0; i < KPL; ++i)
