@@ -108,6 +108,19 @@ def background(fn, name: str = "oni-writer"):
     return join
 
 
+def vocab_lookup(word_keys, word_names):
+    """keys -> (names, index) through the built vocabulary (every doc_wc key is in it): a vectorized
+    search instead of decoding the unique keys again -- a writer thread then holds the GIL only
+    briefly while the lda stage drives the GPU."""
+    wk = np.asarray(word_keys)
+    srt = np.argsort(wk, kind="stable")
+    sk = wk[srt]
+
+    def lookup(keys):
+        return word_names, srt[np.searchsorted(sk, np.asarray(keys))]
+    return lookup
+
+
 def doc_rows_of(doc_keys, n_keys: int) -> np.ndarray:
     """Doc row of every dictionary id (-1: not a document): the in-memory equivalent of looking the
     names up in doc_results.csv, when the documents are ``doc_keys`` in row order."""

@@ -55,11 +55,18 @@ def run(cfg, dist=None, device=None, log=print) -> dict:
                 built = lda_pre(dwc)
                 doc_names = [feat.ip_names[i] for i in built.doc_keys.tolist()]
                 word_names = wsp.decode(built.word_keys)
-                if cfg.write_doc_wc:
-                    from ..corpus.builder import write_doc_wc
-                    write_doc_wc(os.path.join(cfg.lpath, "doc_wc.dat"), dwc, feat.ip_names,
-                                 lambda keys: (lambda u: (wsp.decode(u[0]), u[1]))(np.unique(keys, return_inverse=True)))
-                C.write_corpus_files(cfg.lpath, built, doc_names, word_names)
+                lp, b_, dn_, wn_, ipn = cfg.lpath, built, doc_names, word_names, feat.ip_names
+
+                def write_files():
+                    if cfg.write_doc_wc:
+                        from ..corpus.builder import write_doc_wc
+                        write_doc_wc(os.path.join(lp, "doc_wc.dat"), dwc, ipn, C.vocab_lookup(b_.word_keys, wn_))
+                    C.write_corpus_files(lp, b_, dn_, wn_)
+                # as in the flow pipeline: the text files on a thread during EM, the marker waits for them
+                if os.environ.get("ONI_DEFER_PRE", "1") != "0":
+                    res["_defer"] = C.background(write_files, "oni-lda-pre-writer")
+                else:
+                    write_files()
                 res.update(docs=built.corpus.num_docs, terms=built.corpus.num_terms, nnz=built.corpus.nnz)
                 summary["corpus"] = dict(docs=built.corpus.num_docs, terms=built.corpus.num_terms, nnz=built.corpus.nnz)
     else:

@@ -30,19 +30,6 @@ def _word_names(ws: FF.FlowWordSpace, keys: np.ndarray):
     return ws.decode(keys)
 
 
-def _vocab_lookup(word_keys, word_names):
-    """keys -> (names, index) through the built vocabulary (every doc_wc key is in it): a vectorized
-    search instead of decoding the unique keys again -- the writer thread then holds the GIL only
-    briefly while the lda stage drives the GPU."""
-    wk = np.asarray(word_keys)
-    srt = np.argsort(wk, kind="stable")
-    sk = wk[srt]
-
-    def lookup(keys):
-        return word_names, srt[np.searchsorted(sk, np.asarray(keys))]
-    return lookup
-
-
 def run(cfg, dist=None, device=None, log=print) -> dict:
     if dist is not None and dist.active:
         from .sharded import run_flow
@@ -86,7 +73,7 @@ def run(cfg, dist=None, device=None, log=print) -> dict:
                 def write_files():
                     if cfg.write_doc_wc:
                         from ..corpus.builder import write_doc_wc
-                        write_doc_wc(os.path.join(lp, "doc_wc.dat"), dwc, ipn, _vocab_lookup(b_.word_keys, wn_))
+                        write_doc_wc(os.path.join(lp, "doc_wc.dat"), dwc, ipn, C.vocab_lookup(b_.word_keys, wn_))
                     C.write_corpus_files(lp, b_, dn_, wn_)
                 # the text files are the stage contract, not an input of the in-memory lda stage: written
                 # on a thread while the GPU runs EM; the lda_pre marker waits for them (finish_deferred)
