@@ -465,10 +465,8 @@ class LDAEngine:
         plans = [self.gs_plan] if self._cwin is None else [w["gp"] for w in self._cwin]
         out = {}
         for gp in plans:
-            for i, (var, order) in enumerate(gp.plan):
-                # the first team8 launch only (with ONI_GS_HEAD: the head of the longest documents; the
-                # rest gather from beta -- they are not on the critical path)
-                if var != H.GS_TEAM8 or any(v == H.GS_TEAM8 for v, _ in gp.plan[:i]):
+            for var, order in gp.plan:
+                if var != H.GS_TEAM8:
                     continue
                 o = order.cpu().numpy()
                 o = o[o >= 0]

@@ -880,26 +880,12 @@ class GSPlan:
         self.plan = []
         iso = int(os.environ.get("ONI_GS_XCD", "1")) if KS <= 32 else 0
         edges = self.EDGES_NARROW if KS <= 32 and os.environ.get("ONI_GS_SMALL", "1") != "0" else self.EDGES
-        # ONI_GS_HEAD (K <= 32, default on): the team8 documents of >= 1/4 of the longest one's words are
-        # a launch of their own (the head: work[0], the late suff-stats and the staged rows cover only
-        # them); the shorter team8 documents run in a second launch on another stream
-        head = KS <= 32 and os.environ.get("ONI_GS_HEAD", "1") != "0"
         for var, lo, hi in edges:
             lo_ = tiny if lo is None else lo
             m = (Ls > lo_) if hi is None else ((Ls > lo_) & (Ls <= hi))
             if not m.any():
                 continue
             o = order[m].copy()
-            if var == GS_TEAM8 and head:
-                h = L[o] * 4 >= L[o[0]]
-                rest = o[~h]
-                o = o[h]
-                if iso > 0:
-                    o = self.isolate_longest(o, min(iso, 8))
-                self.plan.append((var, torch.from_numpy(o).to(device)))
-                if rest.size:
-                    self.plan.append((var, torch.from_numpy(rest.copy()).to(device)))
-                continue
             if var == GS_TEAM8 and iso > 0:
                 o = self.isolate_longest(o, min(iso, 8))
             self.plan.append((var, torch.from_numpy(o).to(device)))
