@@ -284,6 +284,24 @@ def lda_suffstats(word_ptr, csc_ent, csc_doc, order, e, r, beta, cw, variant, ga
     lib().lda_suffstats(*args)
 
 
+def argsort_desc_stable(keys):
+    """np.argsort(-keys, kind="stable") for non-negative integer keys, as numpy's O(n) radix sort on
+    16-bit digits (one pass below 2^16, two below 2^32): the length plans are inside the engine
+    setup, which bench.py's to-convergence clock includes (4x faster on 124 k document lengths)."""
+    import numpy as np
+    k = np.asarray(keys, np.int64)
+    if k.size == 0:
+        return np.zeros(0, np.int64)
+    m = int(k.max())
+    if int(k.min()) < 0 or m >= 1 << 32:
+        return np.argsort(-k, kind="stable")
+    r = m - k
+    if m < 1 << 16:
+        return np.argsort(r.astype(np.uint16), kind="stable")
+    o = np.argsort((r & 0xFFFF).astype(np.uint16), kind="stable")
+    return o[np.argsort((r[o] >> 16).astype(np.uint16), kind="stable")]
+
+
 class SuffPlan:
     """Word order for the single-launch suff-stats kernel: [heavy | medium | light] (heavy first).
 
@@ -299,7 +317,7 @@ class SuffPlan:
         if ids.size and (ids.min() < 0 or ids.max() >= wl.size):
             raise ValueError("suff sub-plan word ids out of range")
         self.covers_all = words is None
-        order = ids[np.argsort(-wl[ids], kind="stable")].astype(np.int32)
+        order = ids[argsort_desc_stable(wl[ids])].astype(np.int32)
         L = wl[order]
         self.n_heavy = int((L > self.HEAVY).sum())
         self.n_medium = int(((L > self.LIGHT) & (L <= self.HEAVY)).sum())
@@ -851,10 +869,10 @@ class GSPlan:
         # sort of the range equals the range's documents in the stable sort of all of them
         self.doc_range = None if doc_range is None else (int(doc_range[0]), int(doc_range[1]))
         if self.doc_range is None:
-            order = np.argsort(-L, kind="stable").astype(np.int32)
+            order = argsort_desc_stable(L).astype(np.int32)
         else:
             d0, d1 = self.doc_range
-            order = (d0 + np.argsort(-L[d0:d1], kind="stable")).astype(np.int32)
+            order = (d0 + argsort_desc_stable(L[d0:d1])).astype(np.int32)
         # documents longer than split_min words: one document over several workgroups (gs_split);
         # default on for KS > 32 (the topic-group team kernels' chunk of a long document is bound
         # by one CU's row gathers), ONI_GS_SPLIT_MIN overrides (0: off)

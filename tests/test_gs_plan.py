@@ -93,3 +93,13 @@ def test_stage_tiles_cover_each_document_in_order():
     assert st.tile_cnt.tolist() == [64, 64, 2, 64, 6, 64]
     assert st.stage_off.tolist() == [0, 0, 3 * per, 5 * per]
     assert st.buf.numel() == 6 * per * 2 and st.nbytes == 6 * per * 16
+
+
+def test_argsort_desc_stable_matches_numpy():
+    from oni_ml_amd.ops.hip import argsort_desc_stable
+    rng = np.random.default_rng(2)
+    for hi in (5, 300, 65535, 65536, 82418, 3_000_000):
+        k = rng.integers(0, hi + 1, 20000)
+        k[:50] = hi
+        assert np.array_equal(argsort_desc_stable(k), np.argsort(-k, kind="stable"))
+    assert argsort_desc_stable(np.zeros(0, np.int64)).size == 0
