@@ -204,6 +204,10 @@ def main():
                                                                   int(it[m].max())]
     extra["var_iter_by_len"] = by_len
     value = window_value
+    # the window's engine is done: its buffers go back to the allocator cache before the
+    # to-convergence engine is built (one engine per process, as in a production run)
+    eng_schedule, eng_xmode, eng_D, eng_nnz = eng.schedule, eng.exchange_mode, eng.D, eng.corpus.nnz
+    del eng
     if args.converge:
         # to convergence: fresh engine and random init (seed + 1), lda-c's EM loop test on the device;
         # the clock includes the engine's construction (device CSR / CSC, length plans, buffers)
@@ -245,7 +249,7 @@ def main():
             "vs_baseline": (round(value / base, 2) if base else None),
             "dtype": ("fp64" if args.precision == "fp64" or args.backend != "hip" else
                       "fp32 E-step / fp64 likelihood, alpha, sufficient-statistic totals (reference lda-c: fp64)"),
-            "schedule": eng.schedule,
+            "schedule": eng_schedule,
             "precision_evidence": "profiles/r2_precision_parity.md",
             "data": (f"synthetic (1-day {'DNS' if args.corpus == 'dns' else 'netflow'} per GPU through the real "
                      "featurizer, random-init topics)" if args.corpus != "planted" else "synthetic planted-topic corpus"),
@@ -255,12 +259,12 @@ def main():
                 "seq_len": int(round(corpus.nnz / max(1, corpus.num_docs))),
                 "precision": args.precision,
                 "parallelism": f"dp{world}",
-                "class_word_reduction": eng.exchange_mode,
+                "class_word_reduction": eng_xmode,
                 "corpus": args.corpus,
                 "events_per_gpu": args.events if args.corpus in ("flow", "dns") else None,
-                "docs_per_gpu": eng.D,
+                "docs_per_gpu": eng_D,
                 "vocab": corpus.num_terms,
-                "nnz_per_gpu": eng.corpus.nnz,
+                "nnz_per_gpu": eng_nnz,
                 "max_doc_len": int(corpus.lengths().max()),
                 "device": args.device,
             },
