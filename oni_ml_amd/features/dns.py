@@ -344,7 +344,9 @@ class DnsWordSpace:
             k = k // r
         top = k
         parts = parts[::-1]
-        out = []
-        for i in range(len(top)):
-            out.append("_".join([str(int(top[i]))] + [str(int(p[i])) for p in parts] + [self.qpairs[int(q[i])]]))
-        return out
+        # column-wise str conversion, then one join per word (the per-element int() / indexing of a
+        # row-wise loop cost ~1 us per word on the DNS day's 42 k words)
+        cols = [list(map(str, top.tolist()))] + [list(map(str, p.tolist())) for p in parts]
+        qp = self.qpairs
+        cols.append([qp[i] for i in q.tolist()])
+        return ["_".join(t) for t in zip(*cols)]
