@@ -23,7 +23,9 @@ def main():
         # host enqueue time of 5 iterations (no read-back): replay / launch calls only
         t0 = time.perf_counter()
         if graph:
-            eng._fgraphs[5].replay()          # the batch's 5 iterations are one graph
+            (m, g), = eng._fgraphs.items()    # graphs of m = ONI_GRAPH_ITERS iterations (default 1)
+            for _ in range(5 // m):
+                g.replay()
         else:
             for _ in range(5):
                 eng._launch_estep(newton_key=(True, c.num_docs))
