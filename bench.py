@@ -1,32 +1,33 @@
 #!/usr/bin/env python
-"""Headline benchmark: LDA variational-EM throughput on a synthetic 1-day netflow corpus.
+"""Headline benchmark: LDA variational-EM throughput + the ml_ops wall-clock on a synthetic 1-day netflow.
 
 Metric (BASELINE.json): "LDA docs/sec to convergence + ml_ops.sh wall-clock, 1-day netflow".
 
-One step = one full EM iteration of the oni-lda-c algorithm: the length-bucketed
-fused E-step run to per-document convergence (hipGraph replay), deterministic
-sufficient statistics, RCCL all-reduce of class_word when N > 1, M-step and
-the alpha Newton step.  value = documents processed per second summed over
-all ranks (docs x timed EM iterations / max-over-ranks wall time).
+One step = one full EM iteration of the oni-lda-c algorithm (reference call site ml_ops.sh:80):
+the length-bucketed fp64 block Gauss-Seidel E-step run to per-document convergence (hipGraph
+replay), deterministic sufficient statistics, the class_word reduction over RCCL when N > 1, the
+M-step and the alpha Newton (csrc/hip/lda_gs64.hip; lda-c's double arithmetic).
 
-Engine: the fp64 block Gauss-Seidel engine (--precision fp64, the default: lda-c's double
-arithmetic and its per-word schedule up to blocks of ceil(n/32) words, csrc/hip/lda_gs64.hip);
---precision fp32 runs the experimental fp32 Jacobi engine (a known model bias against lda-c,
-profiles/r2_precision_parity.md; its tests run only with ONI_EXPERIMENTAL=1).
+What is measured, at every N (one process per GPU, `torchrun --nproc-per-node N`):
 
-value = LDA docs/s TO CONVERGENCE: a fresh random-init run trained until lda-c's EM loop test
-stops it (device-side test, every iteration in full), docs x EM iterations / wall time, summed
-over ranks.  The timed K-step window (``ms_per_step``: W untimed warm-up iterations, then exactly
-K EM iterations bracketed by barrier + synchronize, max over ranks) is reported beside it as
-``window_docs_per_sec``.
-
---scaling weak (default): rank r featurizes its own synthetic netflow day (1M events, seed r)
-through the real pipeline (CSV -> C++ ingest -> GPU featurization -> corpus), the ranks agree on
-the union vocabulary, and the N days are trained as one N-day corpus with documents sharded by
-rank.  --scaling strong: every rank builds the SAME day and the engine shards its documents
-nnz-balanced over the N ranks, as oni-lda-c splits one model.dat over its MPI ranks
-(ml_ops.sh:22-23,80).  Weights are random-init (lda-c "random" start).  Extra (N = 1): the
-wall-clock of the whole ml_ops flow pipeline on the day, with a TOL that flags >= 10^4 events.
+* ``value`` -- LDA docs/s TO CONVERGENCE on the BASELINE config: ONE 1-day corpus (1M events, seed
+  0, built by every rank through the real featurizer) whose documents the engine shards over the N
+  ranks (chain-aware contiguous shards, parallel/dist.py engine_bounds), exactly as oni-lda-c splits
+  one model.dat over its MPI ranks (ml_ops.sh:22-23,80): strong scaling.  A fresh random-init engine
+  is trained until lda-c's EM loop test stops it (device-side test, every iteration in full);
+  docs x EM iterations / wall time, the clock includes the engine's construction.
+* ``ms_per_step`` -- W untimed warm-up EM iterations, then exactly K EM iterations bracketed by
+  barrier + synchronize, max over ranks (``window_docs_per_sec``).
+* ``weak_docs_per_sec`` -- secondary: rank r featurizes its own day (seed 1000 r), the ranks agree on
+  the union vocabulary and train the N-day corpus to convergence, one day per GPU (at N = 1 the same
+  run as ``value``).
+* ``e2e_wall_s`` -- the whole ml_ops flow pipeline (load, flow_pre, lda_pre, lda, lda_post,
+  flow_post) on a fresh synthetic day, in this process (warm: interpreter, torch, HIP and the
+  kernels already loaded); row-sharded over the N ranks at N > 1 (pipeline/sharded.py).
+* ``e2e_cold_wall_s`` -- the same run as fresh child processes (`python -m oni_ml_amd ml_ops
+  20160122 flow TOL ...`, one per rank, their own process group), timed from spawn to exit:
+  interpreter start-up, imports, HIP init, code-object loads and the pipeline -- what the
+  reference's `time` prefixes measure (ml_ops.sh:57,67,80,84,108).  This is the ml_ops wall-clock.
 
   python bench.py --gpus N --steps K --warmup W
   (N > 1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N ...)
@@ -37,7 +38,11 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import shutil
+import socket
+import subprocess
 import sys
+import tempfile
 import time
 
 import numpy as np
@@ -59,24 +64,34 @@ def _baseline():
         return None
 
 
-def build_corpus(args, rank, ctx, dev):
-    seed = args.seed + (1000 * rank if args.scaling == "weak" else 0)
+_T0 = time.perf_counter()
+
+
+def _log(msg):
+    """Progress on stderr (the JSON line is the only stdout output)."""
+    print(f"[bench {time.perf_counter() - _T0:7.1f}s rank {os.environ.get('RANK', '0')}] {msg}", file=sys.stderr,
+          flush=True)
+
+
+def _sync(dev):
+    if torch.device(dev).type == "cuda":
+        torch.cuda.synchronize()
+
+
+def build_corpus(args, seed, dev):
+    """One synthetic day through the real featurizer (CSV -> C++ ingest -> GPU featurization -> corpus)."""
     if args.corpus == "planted":
         from oni_ml_amd.synth.corpus import planted_corpus
         c = planted_corpus(num_docs=args.docs, num_terms=args.vocab, num_topics=24, mean_tokens=25, tail=1.1,
                            max_tokens=300_000, seed=seed)
-        names = [str(i) for i in range(c.num_terms)]
-        info = {}
-    elif args.corpus == "dns":
+        return c, {}, [str(i) for i in range(c.num_terms)]
+    if args.corpus == "dns":
         from oni_ml_amd.pipeline.dns import synthetic_dns_corpus
         c, info, names = synthetic_dns_corpus(events=args.events, seed=seed, device=dev, return_names=True)
     else:
         from oni_ml_amd.pipeline.flow import synthetic_flow_corpus
         c, info, names = synthetic_flow_corpus(events=args.events, seed=seed, device=dev, return_names=True)
-    if ctx.world_size > 1 and args.scaling == "weak":
-        from oni_ml_amd.pipeline.flow import unify_vocabulary
-        c, _ = unify_vocabulary(ctx, c, names)
-    return c, info
+    return c, info, names
 
 
 def _settings(args):
@@ -86,35 +101,123 @@ def _settings(args):
     return st
 
 
-def _e2e(args, dev):
-    """Wall-clock of the full pipeline (ml_ops.sh YYYYMMDD flow TOL equivalent) on a synthetic day."""
-    import shutil
-    import tempfile
+def _engine(args, corpus, ctx, dev, seed, local):
+    from oni_ml_amd.models.lda.em import LDAEngine
+    return LDAEngine(corpus, args.topics, _settings(args), backend=args.backend, device=dev,
+                     dist=ctx if ctx.active else None, seed=seed, local_shard=local, streams=args.streams)
+
+
+def _to_convergence(args, corpus, ctx, dev, seed, local):
+    """Fresh engine + random init trained until lda-c's EM loop test stops it; the clock includes the
+    engine's construction (device CSR / CSC, length plans, buffers).  Returns (docs/s, record)."""
+    ctx.barrier()
+    _sync(dev)
+    t0 = time.perf_counter()
+    eng = _engine(args, corpus, ctx, dev, seed, local)
+    _sync(dev)
+    t_setup = time.perf_counter() - t0
+    res = eng.run()
+    _sync(dev)
+    tc = ctx.allreduce_max(time.perf_counter() - t0)
+    t_setup = ctx.allreduce_max(t_setup)
+    docs = eng.global_docs
+    v = docs * res.em_iterations / tc
+    rec = dict(seconds=round(tc, 4), setup_seconds=round(t_setup, 4), em_iters=res.em_iterations,
+               docs=docs, docs_per_sec=round(v, 1),
+               em_only_docs_per_sec=round(docs * res.em_iterations / max(tc - t_setup, 1e-9), 1),
+               final_likelihood=res.likelihoods[-1][0], final_alpha=res.alpha, exchange=eng.exchange_mode,
+               doc_range=list(eng.doc_range), docs_this_rank=eng.D, nnz_this_rank=eng.corpus.nnz)
+    del eng
+    return v, rec
+
+
+def _shared_tmpdir(ctx, prefix):
+    """One scratch directory every rank of this node sees (rank 0 creates it)."""
+    path = tempfile.mkdtemp(prefix=prefix) if ctx.rank == 0 else None
+    return ctx.broadcast_object(path)
+
+
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _e2e_input(args, ctx, tmp):
+    from oni_ml_amd.synth.flow import generate_flow_day
+    t0 = time.perf_counter()
+    if ctx.rank == 0:
+        generate_flow_day(os.path.join(tmp, "in/"), events=args.events, seed=args.seed + 7)
+    ctx.barrier()
+    return time.perf_counter() - t0
+
+
+def _e2e_warm(args, ctx, dev, tmp):
+    """The whole ml_ops flow pipeline in this process (row-sharded over the ranks at N > 1)."""
     from oni_ml_amd import config as CFG
     from oni_ml_amd.pipeline import run
-    from oni_ml_amd.synth.flow import generate_flow_day
-    tmp = tempfile.mkdtemp(prefix="oni_e2e_")
-    try:
-        t0 = time.perf_counter()
-        generate_flow_day(os.path.join(tmp, "in/"), events=args.events, seed=args.seed + 7)
-        t_gen = time.perf_counter() - t0
-        cfg = CFG.resolve("20160122", "flow", tol=args.e2e_tol, conf_path=None, environ={}, lpath=os.path.join(tmp, "ml"),
-                          flow_path=os.path.join(tmp, "in"), backend=args.backend, topics=args.topics, verbose=False)
-        _sync(dev)
-        t0 = time.perf_counter()
-        s = run(cfg, device=dev, log=lambda *a, **k: None)
-        _sync(dev)
-        wall = time.perf_counter() - t0
-        return dict(e2e_wall_s=round(wall, 3), e2e_synth_input_s=round(t_gen, 3),
-                    e2e_stage_s={k: round(v, 3) for k, v in s["stage_seconds"].items()},
-                    e2e_em_iters=s["lda"]["em_iterations"], e2e_lda_timing=s["lda"].get("timing"), e2e_flagged=s.get("scored"), e2e_corpus=s.get("corpus"))
-    finally:
-        shutil.rmtree(tmp, ignore_errors=True)
+    lpath = os.path.join(tmp, "ml_warm")
+    cfg = CFG.resolve("20160122", "flow", tol=args.e2e_tol, conf_path=None, environ={}, lpath=lpath,
+                      flow_path=os.path.join(tmp, "in"), backend=args.backend, topics=args.topics, verbose=False,
+                      gpus=ctx.world_size)
+    if ctx.rank == 0:
+        os.makedirs(lpath, exist_ok=True)
+    ctx.barrier()
+    _sync(dev)
+    t0 = time.perf_counter()
+    s = run(cfg, dist=ctx if ctx.active else None, device=dev, log=lambda *a, **k: None)
+    _sync(dev)
+    ctx.barrier()
+    wall = ctx.allreduce_max(time.perf_counter() - t0)
+    out = dict(e2e_wall_s=round(wall, 3), e2e_stage_s={k: round(v, 3) for k, v in s.get("stage_seconds", {}).items()},
+               e2e_em_iters=s.get("lda", {}).get("em_iterations"), e2e_flagged=s.get("scored"),
+               e2e_corpus=s.get("corpus"))
+    return out
 
 
-def _sync(dev):
-    if torch.device(dev).type == "cuda":
-        torch.cuda.synchronize()
+def _e2e_cold(args, ctx, tmp):
+    """`python -m oni_ml_amd ml_ops 20160122 flow TOL` as fresh child processes (one per rank, a process
+    group of their own on a new port), timed from spawn to exit; max over ranks."""
+    lpath = os.path.join(tmp, "ml_cold")
+    port = ctx.broadcast_object(_free_port() if ctx.rank == 0 else None)
+    env = dict(os.environ)
+    for k in ("FLOW_PATH", "DNS_PATH", "LPATH", "TOL", "HPATH"):   # duxbay keys: the flags below decide
+        env.pop(k, None)
+    # torchrun's agent-store variables would make the children wait for a store server nobody starts
+    # (TORCHELASTIC_USE_AGENT_STORE): their rank 0 creates its own store on the new port
+    for k in [k for k in env if k.startswith("TORCHELASTIC_")]:
+        env.pop(k)
+    env.update(RANK=str(ctx.rank), LOCAL_RANK=str(ctx.local_rank), WORLD_SIZE=str(ctx.world_size),
+               MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), PYTHONPATH=ROOT + os.pathsep + env.get("PYTHONPATH", ""))
+    if args.device == "cpu":
+        env["ONI_DIST_BACKEND"] = "gloo"
+    cmd = [sys.executable, "-m", "oni_ml_amd", "ml_ops", "20160122", "flow", repr(float(args.e2e_tol)),
+           "--lpath", lpath, "--flow-path", os.path.join(tmp, "in"), "--conf", os.path.join(tmp, "no-duxbay.conf"),
+           "--gpus", str(ctx.world_size), "--topics", str(args.topics), "--backend", args.backend, "--quiet"]
+    if args.device == "cuda":
+        torch.cuda.empty_cache()     # this process's cached blocks back to the device for the child
+    ctx.barrier()
+    t0 = time.perf_counter()
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=args.e2e_timeout)
+    wall = time.perf_counter() - t0
+    if r.returncode != 0:
+        raise RuntimeError(f"cold ml_ops child (rank {ctx.rank}) exited {r.returncode}:\n{r.stderr[-3000:]}")
+    ctx.barrier()
+    wall = ctx.allreduce_max(wall)
+    out = dict(e2e_cold_wall_s=round(wall, 3), e2e_cold_cmd=" ".join(cmd[1:6]))
+    if ctx.rank == 0:
+        try:
+            with open(os.path.join(lpath, "run_summary.json")) as f:
+                sm = json.load(f)
+            out["e2e_cold_stage_s"] = {k: round(v, 3) for k, v in sm.get("stage_seconds", {}).items()}
+            out["e2e_cold_inprocess_wall_s"] = round(float(sm.get("wall_seconds", 0.0)), 3)
+            out["e2e_cold_startup_s"] = round(wall - float(sm.get("wall_seconds", 0.0)), 3)
+            out["e2e_cold_flagged"] = sm.get("scored")
+        except (OSError, ValueError):
+            pass
+    return out
 
 
 def main():
@@ -126,7 +229,7 @@ def main():
     ap.add_argument("--gs-updates", type=int, default=0,
                     help="U, gamma refreshes per sweep of the fp64 engine (0: 32; > 32 needs K > 32; -1: the U "
                          "per K that meets lda-c parity, em.parity_gs_updates)")
-    ap.add_argument("--events", type=int, default=None, help="events per GPU (default: flow 1M, dns 2M)")
+    ap.add_argument("--events", type=int, default=None, help="events of the day (default: flow 1M, dns 2M)")
     ap.add_argument("--corpus", choices=["flow", "dns", "planted"], default="flow",
                     help="flow: BASELINE headline (1-day netflow); dns: BASELINE config 4 (1-day DNS)")
     ap.add_argument("--docs", type=int, default=80_000)
@@ -134,16 +237,18 @@ def main():
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--streams", type=int, default=4, help="HIP streams for the E-step buckets")
     ap.add_argument("--batch", type=int, default=5,
-                    help="EM iterations per host read-back (LDAEngine.run() batches LAG=5 when saving, 8 otherwise)")
-    ap.add_argument("--converge", type=int, default=1, help="also time a full random-init run to convergence")
-    ap.add_argument("--e2e", type=int, default=1, help="N=1: also time the whole ml_ops flow pipeline on the day")
+                    help="EM iterations per host read-back in the timed window (LDAEngine.run() batches 8)")
+    ap.add_argument("--converge", type=int, default=1, help="time a full random-init run to convergence (value)")
+    ap.add_argument("--weak", type=int, default=1, help="N > 1: also the one-day-per-GPU weak-scaling run")
+    ap.add_argument("--e2e", type=int, default=1, help="time the whole ml_ops flow pipeline in-process (warm)")
+    ap.add_argument("--e2e-cold", type=int, default=1, help="time ml_ops as fresh child processes (cold)")
+    ap.add_argument("--e2e-timeout", type=float, default=900.0)
     ap.add_argument("--device", default="cuda", choices=["cuda", "cpu"], help="cpu: gloo/torch rehearsal")
-    ap.add_argument("--precision", default="fp64", choices=["fp64", "fp32"],
-                    help="fp64: lda-c arithmetic, block Gauss-Seidel (default); fp32: the experimental Jacobi mode")
-    ap.add_argument("--scaling", default="weak", choices=["weak", "strong"],
-                    help="weak: one day per GPU; strong: one day sharded over the GPUs")
+    ap.add_argument("--scaling", default="strong", choices=["weak", "strong"],
+                    help="which run is `value`: strong (the BASELINE 1-day corpus sharded over the GPUs, default) "
+                         "or weak (one day per GPU)")
     ap.add_argument("--e2e-tol", type=float, default=1e-5,
-                    help="suspicion threshold of the timed e2e pipeline (1e-5 flags ~5 %% of the synthetic day)")
+                    help="suspicion threshold of the timed ml_ops runs (1e-5 flags ~5 %% of the synthetic day)")
     args = ap.parse_args()
     args.backend = "hip" if args.device == "cuda" else "torch"
     if args.events is None:
@@ -154,31 +259,25 @@ def main():
     rank, world = ctx.rank, ctx.world_size
     dev = ctx.device if args.device == "cuda" else torch.device("cpu")
 
-    from oni_ml_amd.models.lda.em import LDAEngine
-    from oni_ml_amd.models.lda.settings import LDASettings
-
+    # ---------------------------------------------------------------- strong: the BASELINE 1-day corpus
+    _log(f"world {world}, device {dev}: building the 1-day corpus")
     t0 = time.perf_counter()
-    corpus, info = build_corpus(args, rank, ctx, dev)
+    corpus, info, names = build_corpus(args, args.seed, dev)
     t_corpus = time.perf_counter() - t0
-    dist = ctx if world > 1 else None
-    # weak scaling: each rank's corpus is its own document shard of the N-day corpus
-    local = args.scaling == "weak"
-    eng = LDAEngine(corpus, args.topics, _settings(args), backend=args.backend, device=dev, dist=dist, seed=args.seed,
-                    local_shard=local, streams=args.streams, precision=args.precision)
+    eng = _engine(args, corpus, ctx, dev, args.seed, local=False)
     eng.init_random()
     docs_global = eng.global_docs
 
     def run_iters(n):
         # EM iterations exactly as LDAEngine.run() issues them without LAG saves: batches of --batch
         # iterations (one hipGraph replay each on one rank; E-step graph -> RCCL collectives -> M-step
-        # graph on several), one batch always queued ahead of the host's read-back of the previous
-        # batch's (likelihood, conv, alpha) history, the lda-c convergence test evaluated on the
-        # device.  stop=False: every one of the n iterations runs in full (none is skipped by a
-        # converged loop).
+        # graph on several), one batch queued ahead of the host's read-back of the previous batch's
+        # (likelihood, conv, alpha) history.  stop=False: all n iterations run in full.
         batches = [min(args.batch, n - b) for b in range(0, n, args.batch)]
         recs = eng.em_iterations_pipelined(batches, True, docs_global, stop=False)
         assert len(recs) == n, (len(recs), n)
 
+    _log("timed window")
     run_iters(args.warmup)
     ctx.barrier()
     _sync(dev)
@@ -186,15 +285,11 @@ def main():
     run_iters(args.steps)
     _sync(dev)
     ctx.barrier()
-    dt = time.perf_counter() - t1
-    dt = ctx.allreduce_max(dt)
+    dt = ctx.allreduce_max(time.perf_counter() - t1)
     ms = dt / args.steps * 1e3
     window_value = docs_global * args.steps / dt
     it = eng.iters.cpu().numpy()
-
     extra = dict(var_iter_mean=round(float(it.mean()), 3), var_iter_max=int(it.max()), var_max_iter=eng.var_max_iter)
-    # variational iterations of the last E-step by document length (the long documents' share
-    # of the E-step is words x iterations)
     lens = eng.corpus.lengths()
     by_len = {}
     for lo, hi in ((0, 16), (16, 64), (64, 256), (256, 1024), (1024, 4096), (4096, 1 << 40)):
@@ -202,42 +297,63 @@ def main():
         if m.any():
             by_len[f"{lo + 1}-{hi if hi < 1 << 40 else 'inf'}"] = [int(m.sum()), round(float(it[m].mean()), 2),
                                                                   int(it[m].max())]
-    extra["var_iter_by_len"] = by_len
-    value = window_value
-    # the window's engine is done: its buffers go back to the allocator cache before the
-    # to-convergence engine is built (one engine per process, as in a production run)
-    eng_schedule, eng_xmode, eng_D, eng_nnz = eng.schedule, eng.exchange_mode, eng.D, eng.corpus.nnz
+    extra["var_iter_by_len_rank0"] = by_len
+    extra["window_exchange"] = eng.exchange_mode
+    shard = dict(doc_range=list(eng.doc_range), docs=eng.D, nnz=eng.corpus.nnz,
+                 max_doc_len=int(lens.max()) if lens.size else 0)
+    from oni_ml_amd.parallel import shardio as SIO
+    all_shards = SIO.allgather_array(ctx, np.asarray([shard["doc_range"][0], shard["doc_range"][1], shard["docs"],
+                                                       shard["nnz"], shard["max_doc_len"]], np.int64)[None, :])
+    extra["shards"] = [dict(doc_range=[int(a[0, 0]), int(a[0, 1])], nnz=int(a[0, 3]), max_doc_len=int(a[0, 4]))
+                       for a in all_shards]
+    eng_schedule = eng.schedule
     del eng
+    value_strong = window_value
     if args.converge:
-        # to convergence: fresh engine and random init (seed + 1), lda-c's EM loop test on the device;
-        # the clock includes the engine's construction (device CSR / CSC, length plans, buffers)
-        ctx.barrier()
-        _sync(dev)
-        t2 = time.perf_counter()
-        eng2 = LDAEngine(corpus, args.topics, _settings(args), backend=args.backend, device=dev, dist=dist,
-                         seed=args.seed + 1, local_shard=local, precision=args.precision)
-        _sync(dev)
-        t_setup = time.perf_counter() - t2
-        res = eng2.run()
-        _sync(dev)
-        tc = ctx.allreduce_max(time.perf_counter() - t2)
-        t_setup = ctx.allreduce_max(t_setup)
-        value = docs_global * res.em_iterations / tc
-        extra.update(converge_seconds=round(tc, 4), converge_setup_seconds=round(t_setup, 4),
-                     converge_em_iters=res.em_iterations, converge_docs_per_sec=round(value, 1),
-                     converge_em_only_docs_per_sec=round(docs_global * res.em_iterations / max(tc - t_setup, 1e-9), 1),
-                     final_likelihood=res.likelihoods[-1][0], final_alpha=res.alpha)
-    if args.e2e and world == 1 and args.corpus == "flow" and args.events <= 2_000_000:
-        extra.update(_e2e(args, dev))
-    # the measured baseline is the 1-day netflow, K=20 corpus: other configs report no ratio
+        _log("strong scaling to convergence")
+        value_strong, rec = _to_convergence(args, corpus, ctx, dev, args.seed + 1, local=False)
+        extra.update({f"converge_{k}": v for k, v in rec.items() if k not in ("doc_range", "docs_this_rank",
+                                                                               "nnz_this_rank")})
+
+    # ---------------------------------------------------------------- weak: one day per GPU
+    value_weak = value_strong
+    if world > 1 and args.weak and args.converge:
+        _log("weak scaling: one day per rank")
+        cw, _, wnames = build_corpus(args, args.seed + 1000 * rank, dev)
+        from oni_ml_amd.pipeline.flow import unify_vocabulary
+        cw, _ = unify_vocabulary(ctx, cw, wnames)
+        value_weak, wrec = _to_convergence(args, cw, ctx, dev, args.seed + 1, local=True)
+        extra.update(weak_em_iters=wrec["em_iters"], weak_seconds=wrec["seconds"], weak_docs=wrec["docs"],
+                     weak_exchange=wrec["exchange"])
+        del cw
+    extra["weak_docs_per_sec"] = round(value_weak, 1)
+
+    # ---------------------------------------------------------------- ml_ops wall-clock (warm, cold)
+    if args.corpus == "flow" and (args.e2e or args.e2e_cold):
+        tmp = _shared_tmpdir(ctx, "oni_e2e_")
+        try:
+            extra["e2e_synth_input_s"] = round(_e2e_input(args, ctx, tmp), 3)
+            if args.e2e:
+                _log("ml_ops pipeline, in-process (warm)")
+                extra.update(_e2e_warm(args, ctx, dev, tmp))
+            if args.e2e_cold:
+                _log("ml_ops pipeline, fresh child processes (cold)")
+                extra.update(_e2e_cold(args, ctx, tmp))
+        finally:
+            ctx.barrier()
+            if rank == 0:
+                shutil.rmtree(tmp, ignore_errors=True)
+
+    value = value_strong if args.scaling == "strong" else value_weak
+    # the measured baseline is the 1-day netflow, K = 20 corpus: other configs report no ratio
     base = _baseline() if (args.corpus == "flow" and args.topics == 20 and args.events == 1_000_000) else None
     if rank == 0:
         out = {
             "metric": METRIC if args.corpus != "dns" else "LDA docs/sec to convergence, 1-day DNS",
             "value": round(value, 1),
-            "value_source": ("to convergence incl. engine setup: fresh engine + random init, lda-c EM loop test "
-                             "(converge_* fields)"
-                             if args.converge else "timed K-step window (no --converge run)"),
+            "value_source": (f"{args.scaling} scaling, to convergence incl. engine setup: fresh engine + random init, "
+                             "lda-c EM loop test (converge_* fields)" if args.converge
+                             else "timed K-step window (no --converge run)"),
             "window_docs_per_sec": round(window_value, 1),
             "unit": "docs/s (docs x EM iterations / s, all ranks)",
             "n_gpus": world,
@@ -247,24 +363,22 @@ def main():
             "higher_is_better": True,
             "scaling": args.scaling,
             "vs_baseline": (round(value / base, 2) if base else None),
-            "dtype": ("fp64" if args.precision == "fp64" or args.backend != "hip" else
-                      "fp32 E-step / fp64 likelihood, alpha, sufficient-statistic totals (reference lda-c: fp64)"),
+            "dtype": "fp64",
             "schedule": eng_schedule,
-            "precision_evidence": "profiles/r2_precision_parity.md",
-            "data": (f"synthetic (1-day {'DNS' if args.corpus == 'dns' else 'netflow'} per GPU through the real "
+            "precision_evidence": "profiles/r3_precision_parity.md",
+            "data": (f"synthetic (one 1-day {'DNS' if args.corpus == 'dns' else 'netflow'} corpus through the real "
                      "featurizer, random-init topics)" if args.corpus != "planted" else "synthetic planted-topic corpus"),
             "config": {
                 "model": f"oni-lda-c variational EM LDA, K={args.topics}",
                 "global_batch": docs_global,
                 "seq_len": int(round(corpus.nnz / max(1, corpus.num_docs))),
-                "precision": args.precision,
                 "parallelism": f"dp{world}",
-                "class_word_reduction": eng_xmode,
+                "shards": "chain-aware contiguous document shards (parallel/dist.py engine_bounds)" if world > 1 else None,
                 "corpus": args.corpus,
-                "events_per_gpu": args.events if args.corpus in ("flow", "dns") else None,
-                "docs_per_gpu": eng_D,
+                "events": args.events if args.corpus in ("flow", "dns") else None,
+                "docs": corpus.num_docs,
                 "vocab": corpus.num_terms,
-                "nnz_per_gpu": eng_nnz,
+                "nnz": corpus.nnz,
                 "max_doc_len": int(corpus.lengths().max()),
                 "device": args.device,
             },

@@ -1,5 +1,5 @@
-// lda-c opt_alpha on the device, shared by the fp32 (lda_suffstats.hip)
-// and fp64 (lda_gs64.hip) M-step launches.
+// lda-c opt_alpha on the device, shared by the fused M-step launch
+// (lda_gs64.hip) and the stand-alone kernel (em_control.hip).
 #pragma once
 #include "common.h"
 #include "kernels.h"

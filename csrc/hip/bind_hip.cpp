@@ -43,90 +43,13 @@ PYBIND11_MODULE(_onihip, m) {
     return std::string(p.gcnArchName);
   });
 
-  m.def(
-      "lda_estep",
-      [](u doc_ptr, u word_idx, u counts, u order, int n_items, u beta, int K, int KS, float alpha,
-         double lik_const, int var_max_iter, float var_conv, u gamma, u e_out, u r_out, u lik, u alpha_ss,
-         u iters, int variant, u params, u stream, u dbg) {
-        oni::EStepArgs a{P<const int>(doc_ptr), P<const int>(word_idx), P<const float>(counts),
-                         P<const int>(order),   n_items,              P<const float>(beta),
-                         K,                     alpha,                lik_const,
-                         var_max_iter,          var_conv,             P<float>(gamma),
-                         P<float>(e_out),       P<float>(r_out),      P<double>(lik),
-                         P<double>(alpha_ss),   P<int>(iters),        P<const double>(params),
-                         P<long long>(dbg)};
-        oni::launch_lda_estep(a, variant, KS, S(stream));
-      });
-
-  m.def("split_segment_words", [](int KS) { return oni::split_segment_words(KS); });
-  m.def("split_max_blocks", []() { return oni::kSplitMaxBlocks; });
-  m.def("split_capacity", [](int KS, bool wide) { return wide ? oni::wsplit_capacity(KS) : oni::split_capacity(KS); });
-  m.def("block_words", [](int KS, int waves) { return oni::block_words(KS, waves); });
-  m.def("wide_words", [](int KS, int lanes) { return oni::wide_words(KS, lanes); });
-  m.def("wide_slots", [](int KS, int lanes) { return oni::wide_slots(KS, lanes); });
-  m.def(
-      "lda_estep_split",
-      [](bool wide, u doc_ptr, u word_idx, u counts, u beta, int K, int KS, float alpha, double lik_const, int var_max_iter,
-         float var_conv, u gamma, u e_out, u r_out, u lik, u alpha_ss, u iters, u seg_doc, u seg_index, u seg_count,
-         u seg_base, u doc_slot, int n_blocks, int seg_words, u xchg, u counter, int n_docs, u error, u params, u stream,
-         u dbg) {
-        oni::EStepArgs a{P<const int>(doc_ptr), P<const int>(word_idx), P<const float>(counts),
-                         nullptr,               n_blocks,             P<const float>(beta),
-                         K,                     alpha,                lik_const,
-                         var_max_iter,          var_conv,             P<float>(gamma),
-                         P<float>(e_out),       P<float>(r_out),      P<double>(lik),
-                         P<double>(alpha_ss),   P<int>(iters),        P<const double>(params),
-                         P<long long>(dbg)};
-        oni::SplitArgs s{P<const int>(seg_doc), P<const int>(seg_index), P<const int>(seg_count),
-                         P<const int>(seg_base), P<const int>(doc_slot), n_blocks, seg_words,
-                         P<unsigned long long>(xchg), P<int>(counter), n_docs, P<int>(error)};
-        if (wide)
-          oni::launch_lda_estep_wsplit(a, s, KS, S(stream));
-        else
-          oni::launch_lda_estep_split(a, s, KS, S(stream));
-      });
-
-  m.def("lda_suffstats", [](u word_ptr, u csc_ent, u csc_doc, u order, int n_items, u e, u r, u beta, u cw,
-                            int KS, int variant, u gate, u stream) {
-    oni::SuffArgs a{P<const int>(word_ptr), P<const int>(csc_ent), P<const int>(csc_doc),
-                    P<const int>(order),    n_items,               P<const float>(e),
-                    P<const float>(r),      P<const float>(beta),  P<float>(cw),
-                    P<const double>(gate)};
-    oni::launch_lda_suffstats(a, variant, KS, S(stream));
-  });
-
   m.def("suff_fused_blocks", [](int h, int m_, int l) { return oni::suff_fused_blocks(h, m_, l); });
-  m.def("lda_suffstats_fused", [](u word_ptr, u csc_ent, u csc_doc, u order, int n_heavy, int n_medium, int n_light,
-                                  u e, u r, u beta, u cw, u part, int KS, u gate, u stream, bool wide, int pstride,
-                                  u lik, u ass, int lo, int hi) {
-    oni::SuffArgs a{P<const int>(word_ptr), P<const int>(csc_ent),  P<const int>(csc_doc),
-                    P<const int>(order),    n_heavy + n_medium + n_light, P<const float>(e),
-                    P<const float>(r),      P<const float>(beta),   P<float>(cw),
-                    P<const double>(gate)};
-    const oni::SuffPartLayout lay{pstride, pstride == KS ? 0 : 2, P<const double>(lik), P<const double>(ass), lo, hi};
-    oni::launch_lda_suffstats_fused(a, n_heavy, n_medium, n_light, P<double>(part), KS, wide, lay, S(stream));
-  });
   m.def("rows_accumulate", [](u rows, u ptr, u src, u own, u recv, u out, int n_rows, int width, u stream) {
-    oni::launch_rows_accumulate(P<const int>(rows), P<const int>(ptr), P<const int>(src), P<const float>(own),
-                                P<const float>(recv), P<float>(out), n_rows, width, S(stream));
+    oni::launch_rows_accumulate(P<const int>(rows), P<const int>(ptr), P<const int>(src), P<const double>(own),
+                                P<const double>(recv), P<double>(out), n_rows, width, S(stream));
   });
   m.def("colsum_partials", [](u part, int nb, int cols, u out, u gate, u stream) {
     oni::launch_colsum_partials(P<const double>(part), nb, cols, P<double>(out), P<const double>(gate), S(stream));
-  });
-  m.def("lda_mstep_control", [](u cw, u class_total, u beta, int V, int K, int KS, u scalars, u params, u ctl,
-                                u hist, int hist_slots, u done_count, u stream, u rows, int n_rows, int newton,
-                                int estimate, double num_docs, u alpha_out) {
-    oni::EMControlArgs c{P<const double>(scalars), P<double>(params), P<double>(ctl), P<double>(hist), hist_slots,
-                         P<int>(done_count)};
-    const oni::NewtonArgs nw{newton, estimate, num_docs, P<double>(alpha_out)};
-    if (newton && !alpha_out) throw std::runtime_error("lda_mstep_control: alpha_out required with newton");
-    oni::launch_lda_mstep_control(P<const float>(cw), P<const double>(class_total), P<float>(beta), V, K, KS,
-                                  P<const int>(rows), n_rows, c, nw, S(stream));
-  });
-  m.def("reduce_scratch_doubles", [](int cols) { return oni::reduce_scratch_doubles(cols); });
-  m.def("colsum", [](u mat, int rows, int cols, u out, u scratch, u gate, u stream) {
-    oni::launch_colsum(P<const float>(mat), rows, cols, P<double>(out), P<double>(scratch), P<const double>(gate),
-                       S(stream));
   });
   m.def("em_control", [](u scalars, u params, u ctl, u hist, int hist_slots, u stream) {
     oni::launch_em_control(P<const double>(scalars), P<double>(params), P<double>(ctl), P<double>(hist), hist_slots,
@@ -138,11 +61,6 @@ PYBIND11_MODULE(_onihip, m) {
   m.def("alpha_newton", [](u scalars, double num_docs, int K, bool estimate, u params, u alpha_out, u stream) {
     oni::launch_alpha_newton(P<const double>(scalars), num_docs, K, estimate, P<double>(params), P<double>(alpha_out),
                              S(stream));
-  });
-
-  m.def("lda_mstep", [](u cw, u class_total, u beta, int V, int K, int KS, u gate, u stream) {
-    oni::launch_lda_mstep(P<const float>(cw), P<const double>(class_total), P<float>(beta), V, K, KS,
-                          P<const double>(gate), S(stream));
   });
 
 

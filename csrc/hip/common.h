@@ -24,78 +24,12 @@
 
 namespace oni {
 
-// exp(-100): the value lda-c's M-step floor (log_prob_w = -100) contributes in
-// the E-step.  It is an f32 subnormal; hipcc keeps f32 denormals by default.  The
-// literal rounds to the nearest subnormal, 27 * 2^-149 = 3.7835e-44 (1.7 % above
-// exp(-100) = 3.7201e-44): the fp32 engine's floor.  The fp64 engine (lda_gs64.hip)
-// keeps exp(-100) exactly.
-constexpr float kExpMinus100 = 3.7200759760208e-44f;
-
-// lda-c digamma (utils.c): x+6 shift, 4-term asymptotic series, then the six
-// recurrence corrections.
-// Reciprocals use v_rcp_f32 (1 ulp) instead of IEEE division (a 10-instruction
-// div_scale/fmas/fixup sequence each): the E-step's per-topic phase is
-// dominated by these.
-__device__ __forceinline__ float frcp(float x) { return __builtin_amdgcn_rcpf(x); }
-
 // Device-side EM loop control (em_control.hip): once the convergence test has
 // fired, every kernel of the iterations still queued behind it returns at once.
 __device__ __forceinline__ bool gated(const double* gate) { return gate != nullptr && *gate != 0.0; }
 
-__device__ __forceinline__ float digammaf_ldac(float x) {
-  float p;
-  x = x + 6.0f;
-  const float ix = frcp(x);
-  p = ix * ix;
-  p = (((0.004166666666667f * p - 0.003968253986254f) * p + 0.008333333333333f) * p -
-       0.083333333333333f) * p;
-  p = p + __logf(x) - 0.5f * ix - frcp(x - 1.0f) - frcp(x - 2.0f) - frcp(x - 3.0f) - frcp(x - 4.0f) -
-      frcp(x - 5.0f) - frcp(x - 6.0f);
-  return p;
-}
-
-// log Gamma(x), x > 0: Stirling series at x + 6 and the recurrence (the form of
-// lda-c's utils.c log_gamma), float with fast reciprocal / log.  About 1e-7
-// relative, the precision of the float lgammaf it replaces, at a fraction of
-// its cost.
-__device__ __forceinline__ float lgammaf_fast(float x) {
-  const float xs = x + 6.0f;
-  const float ix = frcp(xs);
-  const float z = ix * ix;
-  const float ser = (((-0.000595238095238f * z + 0.000793650793651f) * z - 0.002777777777778f) * z +
-                     0.083333333333333f) * ix;
-  const float p = x * (x + 1.0f) * (x + 2.0f);
-  const float q = (x + 3.0f) * (x + 4.0f) * (x + 5.0f);
-  return (xs - 0.5f) * __logf(xs) - xs + 0.918938533204673f + ser - __logf(p) - __logf(q);
-}
-
-// psi(x) and lnGamma(x) together, x > 0, in the shift-by-6 forms above.  The
-// six reciprocals 1/(x+i), i < 6, collapse into two: sum_{i<3} 1/(x+i) = A'/A
-// with A = x(x+1)(x+2) (likewise B over x+3..x+5), and log A, log B, log(x+6),
-// 1/(x+6) are shared with lnGamma: 3 v_rcp + 3 v_log instead of 8 + 4.
-// A, B stay finite for x < 6e12 (gamma values are bounded by document counts).
-// Natural log of a positive NORMAL float: v_log_f32 (log2, ~1 ulp) x ln 2, without the
-// denormal scaling and extended-precision ln 2 of the library logf (a shorter chain).
-__device__ __forceinline__ float log_normal(float x) { return __builtin_amdgcn_logf(x) * 0.693147180559945f; }
-
-__device__ __forceinline__ void digamma_lgamma(float x, float& psi, float& lg) {
-  const float xs = x + 6.0f;
-  const float ix = frcp(xs);
-  const float z = ix * ix;
-  const float x1 = x + 1.0f, x2 = x + 2.0f, x3 = x + 3.0f, x4 = x + 4.0f, x5 = x + 5.0f;
-  const float A = x * x1 * x2, dA = fmaf(x, x1 + x2, x1 * x2);
-  const float B = x3 * x4 * x5, dB = fmaf(x3, x4 + x5, x4 * x5);
-  // v_log_f32 (log2) x ln 2: xs >= 6 and A, B > 0 are normal floats, so the denormal
-  // scaling and extended-precision ln 2 of the library logf only lengthen the chain
-  const float lxs = log_normal(xs), lA = log_normal(A), lB = log_normal(B);
-  const float pser = (((0.004166666666667f * z - 0.003968253986254f) * z + 0.008333333333333f) * z -
-                      0.083333333333333f) * z;
-  psi = pser + lxs - 0.5f * ix - dA * frcp(A) - dB * frcp(B);
-  const float lser = (((-0.000595238095238f * z + 0.000793650793651f) * z - 0.002777777777778f) * z +
-                      0.083333333333333f) * ix;
-  lg = (xs - 0.5f) * lxs - xs + 0.918938533204673f + lser - lA - lB;
-}
-
+// lda-c digamma (utils.c): x+6 shift, 4-term asymptotic series, then the six
+// recurrence corrections.
 __device__ __forceinline__ double digamma_ldac(double x) {
   double p;
   x = x + 6.0;
@@ -250,12 +184,6 @@ __device__ __forceinline__ T wave_sum_last(T x) {
   return x;   // lane 63: the total
 }
 
-template <int N>
-__device__ __forceinline__ void wave_sum_last_vec(float (&v)[N]) {
-#pragma unroll
-  for (int i = 0; i < N; ++i) v[i] = wave_sum_last(v[i]);
-}
-
 // Wave-level LDS hand-off between lanes of ONE wavefront: orders the
 // ds_writes before the ds_reads (same wave, so no s_barrier is needed and
 // divergent groups never deadlock).
@@ -277,12 +205,6 @@ __device__ __forceinline__ void lds_barrier() {
 
 // Multi-value all-reduce: the total of value i over the G lanes of a group in
 // EVERY lane's v[i] (N independent DPP chains: good ILP, no LDS traffic).
-template <int G, int N>
-__device__ __forceinline__ void group_sum_vec(float (&v)[N]) {
-#pragma unroll
-  for (int i = 0; i < N; ++i) v[i] = group_sum<G>(v[i]);
-}
-
 // Bijective XCD-aware remap of a 1-D grid (cdna_hip_programming.md §5 T1):
 // consecutive logical blocks land on the same XCD (L2) for locality.
 __device__ __forceinline__ int xcd_remap(int bid, int nwg) {

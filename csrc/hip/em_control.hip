@@ -15,6 +15,7 @@
 #include "common.h"
 #include "kernels.h"
 #include "em_control.h"
+#include "alpha_newton.h"
 
 namespace oni {
 
@@ -27,6 +28,20 @@ __global__ void em_control_kernel(const double* __restrict__ scalars, double* __
 void launch_em_control(const double* scalars, double* params, double* ctl, double* hist, int hist_slots,
                        hipStream_t s) {
   hipLaunchKernelGGL(em_control_kernel, dim3(1), dim3(64), 0, s, scalars, params, ctl, hist, hist_slots);
+  ONI_HIP_CHECK(hipGetLastError());
+}
+
+__global__ void alpha_newton_kernel(const double* __restrict__ scalars, double num_docs, int K, int estimate,
+                                    double* __restrict__ params, double* __restrict__ alpha_out) {
+  const int lane = threadIdx.x;
+  if (blockIdx.x != 0 || lane >= 2 || params[kParamDone] != 0.0) return;
+  alpha_newton_lanes(scalars, num_docs, K, estimate, params, alpha_out, lane);
+}
+
+void launch_alpha_newton(const double* scalars, double num_docs, int K, bool estimate, double* params,
+                         double* alpha_out, hipStream_t s) {
+  hipLaunchKernelGGL(alpha_newton_kernel, dim3(1), dim3(64), 0, s, scalars, num_docs, K, estimate ? 1 : 0, params,
+                     alpha_out);
   ONI_HIP_CHECK(hipGetLastError());
 }
 

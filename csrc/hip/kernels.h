@@ -16,37 +16,11 @@ constexpr int kParamCount = 8;
 constexpr int kHistCols = 6;
 
 #define ONI_FOR_EACH_KS(X) X(8) X(12) X(16) X(20) X(24) X(32) X(52) X(64) X(100) X(128)
-// Padded topic counts with wide-topic E-step kernels (lda_estep_wide.hip): a word's
-// topics split over 4 lanes; the host uses them for K > 32.
-#define ONI_FOR_EACH_WIDE_KS(X) X(32) X(52) X(64) X(100) X(128)
 
-// ---------------------------------------------------------------- E-step ---
-enum EStepVariant : int {
-  kEStepG16 = 0,   // 16 lanes/doc, 16 docs per 256-thread block
-  kEStepG32 = 1,   // 32 lanes/doc
-  kEStepG64 = 2,   // one wave per doc
-  kEStepG64C = 3,  // one wave per doc, several beta rows cached per lane
-  kEStepB4 = 4,    // one doc per 4-wave workgroup
-  kEStepB8 = 5,    // one doc per 8-wave workgroup (longest docs)
-  kEStepT1 = 6,    // one thread per document (tiny documents, KS <= 32)
-  // wide-topic layout (lda_estep_wide.hip): 4 lanes share a word's topics
-  kEStepW16 = 7,   // 16 lanes (4 word slots) per doc
-  kEStepW32 = 8,   // 32 lanes (8 slots) per doc
-  kEStepW64 = 9,   // one wave (16 slots) per doc
-  kEStepWB4 = 10,  // one doc per 4-wave workgroup (64 slots)
-  kEStepWB8 = 11,  // one doc per 8-wave workgroup (128 slots)
-};
-
-// Huge documents (the long-context analogue): one document is
-// split into `nseg` contiguous word segments, one workgroup each; every
-// variational iteration the segments exchange their partial
-// (sum_n c_n beta_n / P_n, sum_n c_n log P_n) through global memory as
-// iteration-tagged 8-byte granules {float value, uint32 tag} -- a reader polls
-// the granules themselves, so a hand-off costs one write and the polling reads
-// (no arrival counter, no store-completion wait) -- and each workgroup then runs
-// the identical (deterministic) topic update.  All workgroups of one launch must
-// be co-resident: the host caps a launch at kSplitMaxBlocks workgroups.
-constexpr int kSplitMaxBlocks = 192;   // 8-wave workgroups, ~1 per CU: keep a margin below 256 CUs
+// Huge documents (the long-context analogue): one document over
+// several workgroups that exchange their per-chunk partials through global memory
+// as tagged granules (launch_gs_split).  All workgroups of one launch must be
+// co-resident: the host caps a launch below gs_split_capacity(KS).
 struct SplitArgs {
   const int* seg_doc;     // [n_blocks] document of each workgroup
   const int* seg_index;   // [n_blocks] segment number within its document
@@ -54,94 +28,17 @@ struct SplitArgs {
   const int* seg_base;    // [n_blocks] block id of the document's segment 0
   const int* doc_slot;    // [n_blocks] counter slot of the document
   int n_blocks;
-  int seg_words;          // words per segment
-  unsigned long long* xchg;  // [2][n_blocks][KS + 2] tagged granules (parity double-buffer): KS topic
-                             // partials, then sum_n c_n log P_n as a float pair (hi, lo)
+  int seg_words;          // unused by the fp64 kernels
+  unsigned long long* xchg;  // tagged granules (parity double-buffer), layout per kernel
   int* counter;           // [2][n_docs] per document: launch epoch (tags of different launches never
                           // match), exit count (the last segment out bumps the epoch, resets the count)
   int n_docs;             // documents in this launch
   int* error;             // set to 1 if a wait times out (never hangs the GPU)
 };
 
-struct EStepArgs {
-  const int* doc_ptr;     // [D+1] CSR offsets
-  const int* word_idx;    // [nnz]
-  const float* counts;    // [nnz]
-  const int* order;       // [n_items] doc ids of this bucket
-  int n_items;
-  const float* beta;      // [V][KS]  exp(log p(w|z)), word-major
-  int K;                  // real topic count
-  float alpha;
-  double lik_const;       // lgamma(K*alpha) - K*lgamma(alpha)
-  int var_max_iter;       // -1 = unbounded
-  float var_conv;
-  float* gamma;           // [D][KS]
-  float* e_out;           // [D][KS]
-  float* r_out;           // [nnz]
-  double* lik;            // [D]
-  double* alpha_ss;       // [D]
-  int* iters;             // [D]
-  // Optional device parameter block (kParamCount doubles): when set, its
-  // {alpha, lik_const, var_max_iter, var_conv} override those four fields, so a
-  // captured hipGraph of the E-step can be replayed every EM iteration while alpha
-  // / VAR_MAX_ITER change, and params[kParamDone] != 0 skips the launch.
-  const double* params = nullptr;
-  // Optional phase timer (diagnostics, scripts/bench_estep.py --phases): block 0, thread 0 of the
-  // block kernels accumulate clock64() cycles per phase of the variational loop into dbg[0..7].
-  long long* dbg = nullptr;
-};
-void launch_lda_estep(const EStepArgs& a, int variant, int KS, hipStream_t s);
-void launch_lda_estep_split(const EStepArgs& a, const SplitArgs& s, int KS, hipStream_t st);
-void launch_lda_estep_wide(const EStepArgs& a, int variant, int KS, hipStream_t s);
-void launch_lda_estep_wsplit(const EStepArgs& a, const SplitArgs& s, int KS, hipStream_t st);
-int wide_words(int KS, int lanes);  // register-cached words of a wide kernel with `lanes` lanes per doc
-int wide_slots(int KS, int lanes);  // word slots (lanes / topic-group width) of a wide kernel
-int split_segment_words(int KS);   // words one split workgroup keeps in registers
-// Co-resident capacity of the split kernels on this device: occupancy-API workgroups per CU x CUs.
-// The host sizes split launches to min(kSplitMaxBlocks, 3/4 of it) (ops/hip.py SplitPlan): the
-// per-iteration cross-workgroup exchange needs every segment of a launch resident at once.
-int split_capacity(int KS);
-int wsplit_capacity(int KS);
-int block_words(int KS, int waves); // register-cached words of a 4- or 8-wave document workgroup
-
-// ------------------------------------------------------------ suff stats ---
-enum SuffVariant : int { kSuffG16 = 0, kSuffG64 = 1, kSuffB8 = 2 };
-
-struct SuffArgs {
-  const int* word_ptr;    // [V+1] CSC offsets (entries of each word)
-  const int* csc_ent;     // [nnz] CSR entry index of each CSC slot
-  const int* csc_doc;     // [nnz] document of each CSC slot
-  const int* order;       // [n_items] word ids of this bucket
-  int n_items;
-  const float* e;         // [D][KS]
-  const float* r;         // [nnz]
-  const float* beta;      // [V][KS]
-  float* cw;              // [V][KS] class_word (word-major), written for listed words
-  const double* gate;     // nullable: skip when *gate != 0 (converged EM loop)
-};
-void launch_lda_suffstats(const SuffArgs& a, int variant, int KS, hipStream_t s);
-// All words in one launch: a.order = [heavy | medium | light] word ids (heavy first);
-// part receives suff_fused_blocks(...) x KS per-workgroup column sums (double).
+// Sufficient-statistic launches: workgroups for [heavy | medium | light] word lists
+// (a heavy word per workgroup, 4 medium or 16 light words per workgroup).
 int suff_fused_blocks(int n_heavy, int n_medium, int n_light);
-// wide: the wide-topic layout (KS >= 32; lda_suff_wide), used with the wide E-step.
-// Partial-row layout of the fused suff-stats launch: row stride `stride` doubles, topic
-// column sums at [off, off + KS); with off == 2 columns 0 / 1 receive this workgroup's
-// slice sums of lik[] / alpha_ss[] over documents [lo, hi) (zeros when lik == nullptr), so
-// one colsum_partials pass yields {likelihood, alpha_ss, class_total[KS]}.
-struct SuffPartLayout {
-  int stride;
-  int off;
-  const double* lik;
-  const double* ass;
-  int lo, hi;
-};
-void launch_lda_suffstats_fused(const SuffArgs& a, int n_heavy, int n_medium, int n_light, double* part, int KS,
-                                bool wide, const SuffPartLayout& lay, hipStream_t s);
-
-// ----------------------------------------------------------------- M-step ---
-// beta[w][k] = cw/ct_k if cw > 0 else exp(-100) (k < K); 0 for padding topics.
-void launch_lda_mstep(const float* cw, const double* class_total, float* beta, int V, int K, int KS,
-                      const double* gate, hipStream_t s);
 
 // alpha Newton on the device: reads scalars[1] (alpha_ss), writes params[0..1]
 // (alpha, lgamma(K alpha) - K lgamma(alpha)) and alpha_out[0].
@@ -162,9 +59,9 @@ void launch_alpha_newton(const double* scalars, double num_docs, int K, bool est
 void launch_em_control(const double* scalars, double* params, double* ctl, double* hist, int hist_slots,
                        hipStream_t s);
 
-// M-step fused with the EM control step: the last workgroup to finish (every
-// other one has read the gate) runs em_control_step.  done_count: one int,
-// zero before the first launch, left zero by the kernel.
+// M-step fused with the EM control step (launch_gs_mstep_control): the last workgroup to finish
+// (every other one has read the gate) runs em_control_step.  done_count: one int, zero before the
+// first launch, left zero by the kernel.
 struct EMControlArgs {
   const double* scalars;
   double* params;
@@ -181,10 +78,6 @@ struct NewtonArgs {
   double num_docs;
   double* alpha_out;      // [1]
 };
-void launch_lda_mstep_control(const float* cw, const double* class_total, float* beta, int V, int K, int KS,
-                              const int* rows, int n_rows, const EMControlArgs& c, const NewtonArgs& nw,
-                              hipStream_t s);
-
 // ------------------------------------------------- fp64 block Gauss-Seidel ---
 // lda-c-faithful E-step (lda_gs64.hip): everything in double, gamma / digamma refreshed
 // after every chunk of W = ceil(n / U) words (U = gs_updates refreshes per sweep; a
@@ -245,7 +138,7 @@ void launch_gs_suff64(const int* word_ptr, const int* csc_ent, const int* order,
                       int n_light, const double* cphi, double* cw, double* part, const double* lik,
                       const double* ass, int lo, int hi, int KS, const double* gate, hipStream_t s,
                       const double* cw_base = nullptr);   // cw[w] = cw_base[w] + sum (nullable)
-// fp64 M-step + alpha Newton + EM control (as launch_lda_mstep_control)
+// fp64 M-step + alpha Newton (workgroup 0) + EM control (last workgroup)
 void launch_gs_mstep_control(const double* cw, const double* class_total, double* beta, int V, int K, int KS,
                              const int* rows, int n_rows, const EMControlArgs& c, const NewtonArgs& nw,
                              hipStream_t s);
@@ -256,18 +149,13 @@ void launch_gs_mstep(const double* cw, const double* class_total, double* beta, 
                      const double* gate, hipStream_t s);
 
 // ------------------------------------------------------------- reductions ---
-// Deterministic two-pass reductions (reduce.hip).  scratch holds
-// reduce_scratch_doubles(cols) doubles.
-int reduce_scratch_doubles(int cols);
-// gate (nullable): skip when *gate != 0.
-void launch_colsum(const float* m, int rows, int cols, double* out, double* scratch, const double* gate,
-                   hipStream_t s);
+// Deterministic reductions (reduce.hip).  gate (nullable): skip when *gate != 0.
 // out[k] = sum_b part[b][k] (b in order), the second pass of the fused suff-stats.
 void launch_colsum_partials(const double* part, int nb, int cols, double* out, const double* gate, hipStream_t s);
 // Sparse class_word exchange: out[rows[i]] = 0 + src_0 + src_1 + ... over row i's sources
-// (CSR ptr/src; src >= 0: recv row, src < 0: the rank's own row own[rows[i]]), float4 granules.
-void launch_rows_accumulate(const int* rows, const int* ptr, const int* src, const float* own, const float* recv,
-                            float* out, int n_rows, int width, hipStream_t s);
+// (CSR ptr/src; src >= 0: recv row, src < 0: the rank's own row own[rows[i]]), fp64, double2 granules.
+void launch_rows_accumulate(const int* rows, const int* ptr, const int* src, const double* own, const double* recv,
+                            double* out, int n_rows, int width, hipStream_t s);
 
 // ---------------------------------------------------------------- scoring ---
 struct ScoreArgs {

@@ -2822,6 +2822,10 @@ void launch_gs_split(const GSArgs& a, const SplitArgs& s, int KS, hipStream_t st
   ONI_HIP_CHECK(hipGetLastError());
 }
 
+int suff_fused_blocks(int n_heavy, int n_medium, int n_light) {
+  return n_heavy + (n_medium + 3) / 4 + (n_light + 15) / 16;
+}
+
 void launch_gs_suff64(const int* word_ptr, const int* csc_ent, const int* order, int n_heavy, int n_medium,
                       int n_light, const double* cphi, double* cw, double* part, const double* lik,
                       const double* ass, int lo, int hi, int KS, const double* gate, hipStream_t s,

@@ -12,9 +12,9 @@ Steps (all tensor collectives, parallel/shardio.py):
    minima all-gathered and merged (V rows, not nnz);
 4. doc ids (doc.dat, 1-based): a document's first line decides its place, and the blocks are in
    (section, rank) order, so a document's id is its block's offset plus its rank inside the block;
-5. the nnz-balanced engine shards (``parallel.dist.shard_bounds`` of the global doc_ptr) are found
-   from per-block nnz totals and an all-reduce of N - 1 boundary candidates; the entries move to the
-   rank owning their document (``all_to_all``), where they become this rank's CSR shard.
+5. the engine shards (``parallel.dist.engine_bounds`` of the global doc_ptr: chain-aware by default)
+   from every document's length, gathered as (id, length) pairs; the entries move to the rank owning
+   their document (``all_to_all``), where they become this rank's CSR shard.
 
 The result -- shard bounds, every entry's word id, every document's id and entries in line order --
 is identical to ``corpus.builder.lda_pre`` of the whole doc_wc (tests/test_sharded_pipeline.py).
@@ -129,21 +129,20 @@ def build_sharded(ctx, sections: Sequence[DocWordCounts], n_ids: int, merge: boo
     cum_in_sorted = torch.cumsum(len_sorted, 0) - len_sorted               # exclusive, over my sorted docs
     cum_sec_start = torch.from_numpy(np.concatenate([[0], np.cumsum(B)])[:-1].copy())
     start_sorted = torch.from_numpy(blk_nnz_off[:, r].copy())[fs_sorted] + (cum_in_sorted - cum_sec_start[fs_sorted])
-    # ---- engine shard bounds: shard_bounds(doc_ptr, N) (first d with doc_ptr[d] >= nnz k / N)
-    bounds = [0]
+    # ---- engine shard bounds (parallel.dist.engine_bounds of the global doc_ptr): every rank's
+    # (document id, length) pairs gathered, so every rank builds the same global doc_ptr (D lengths,
+    # 16 bytes per document) and applies the engine's own rule -- chain-aware by default
+    bounds = [0, D]
     if N > 1:
-        cand = np.full(N - 1, D, np.int64)
-        st = start_sorted.numpy()
-        ix = idx_sorted.numpy()
-        for j in range(1, N):
-            target = nnz * j / N
-            m = st >= target
-            if m.any():
-                cand[j - 1] = int(ix[m].min())
-        cand = _allreduce_min(ctx, cand)
-        for j in range(1, N):
-            bounds.append(int(min(max(int(cand[j - 1]), bounds[-1]), D)))
-    bounds.append(D)
+        from ..parallel.dist import engine_bounds
+        pairs = np.stack([idx_sorted.numpy(), len_sorted.numpy()], 1) if idx_sorted.numel() else \
+            np.zeros((0, 2), np.int64)
+        allp = np.concatenate(SIO.allgather_array(ctx, pairs))
+        glen = np.zeros(D, np.int64)
+        glen[allp[:, 0]] = allp[:, 1]
+        gptr = np.concatenate([[0], np.cumsum(glen)])
+        cut = engine_bounds(gptr, N)
+        bounds = [0] + [int(b1) for _, b1 in cut]
     # ---- entries to the shard owners: (doc index, word id, count, ip id), line order kept per doc
     line_doc = doc_index[dinv]
     order = torch.sort(line_doc, stable=True).indices
@@ -164,12 +163,3 @@ def build_sharded(ctx, sections: Sequence[DocWordCounts], n_ids: int, merge: boo
     corpus = Corpus(ptr, allent[:, 1].astype(np.int32), allent[:, 2], int(word_keys.size))
     return ShardedCorpus(corpus=corpus, doc_range=(d0, d1), doc_keys=doc_keys, num_docs=D, nnz=nnz,
                          word_keys=word_keys, bounds=bounds, lines=owned)
-
-
-def _allreduce_min(ctx, a: np.ndarray) -> np.ndarray:
-    if SIO.world(ctx) == 1:
-        return a
-    import torch.distributed as td
-    t = torch.from_numpy(np.ascontiguousarray(a, np.int64)).to(ctx._coll_device())
-    td.all_reduce(t, op=td.ReduceOp.MIN)
-    return t.cpu().numpy()

@@ -58,75 +58,6 @@ class LDAResult:
     seconds: float = 0.0
 
 
-def _use_wide(ks: int) -> bool:
-    """Wide-topic E-step kernels for K > 32 (ONI_ESTEP_WIDE=0 / 1 forces narrow / wide)."""
-    from ...ops import hip as H
-    env = os.environ.get("ONI_ESTEP_WIDE")
-    if ks not in H.WIDE_KS:
-        return False
-    if env is not None:
-        return env == "1"
-    return ks > 32
-
-
-class _Buckets:
-    """Length-bucket plan: (variant, int32 order tensor) launched per E-step."""
-
-    def __init__(self, lengths: np.ndarray, ks: int, device, kind: str, doc_ptr: Optional[np.ndarray] = None,
-                 split: bool = True, split_min: Optional[int] = None):
-        from ...ops import hip as H
-        order = np.argsort(-lengths, kind="stable").astype(np.int32)
-        L = lengths[order]
-        plan = []
-        self.split = None
-        if kind == "doc" and _use_wide(ks):
-            # wide-topic kernels (K > 32): 4 lanes per word; WB8 and split segments stream the
-            # words beyond their register cache, so the split threshold is a tuning knob only
-            wb8 = H.lib().wide_words(ks, 512)
-            if split and doc_ptr is not None:
-                huge = order[L > max(wb8, split_min or 0)]
-                if huge.size:
-                    self.split = H.SplitPlan(huge, doc_ptr, ks, device, wide=True, seg_words=2 * wb8)
-                    rest = np.asarray(self.split.leftover, np.int32)
-                    keep = ~np.isin(order, huge) | np.isin(order, rest)
-                    order, L = order[keep], L[keep]
-            edges = [(H.ESTEP_WB8, 256, None), (H.ESTEP_WB4, 64, 256), (H.ESTEP_W64, 32, 64),
-                     (H.ESTEP_W32, 16, 32), (H.ESTEP_W16, 0, 16)]
-            L = np.where(L == 0, 1, L)
-        elif kind == "doc":
-            cws = 4 if ks <= 32 else (2 if ks <= 64 else 1)
-            b4_words = H.lib().block_words(ks, 4)       # 4-wave workgroup, all words in registers
-            b8_words = H.lib().block_words(ks, 8)       # 8-wave workgroup, all words in registers
-            if split and doc_ptr is not None:
-                # documents beyond one workgroup's register cache: split over several workgroups
-                huge = order[L > max(b8_words, split_min or 0)]
-                if huge.size:
-                    self.split = H.SplitPlan(huge, doc_ptr, ks, device)
-                    rest = np.asarray(self.split.leftover, np.int32)
-                    keep = ~np.isin(order, huge) | np.isin(order, rest)
-                    order, L = order[keep], L[keep]
-            # tiny documents: one thread each while the topic state fits the registers (KS <= 24) and
-            # the document fits the thread's row cache (t1_max words); longer tiny documents would
-            # re-stream their rows every variational iteration from one thread, so they take 16 lanes
-            t1_max = int(os.environ.get("ONI_T1_MAX", "16"))
-            if ks <= 24:
-                tiny = [(H.ESTEP_G16, t1_max, 16), (H.ESTEP_T1, 0, min(t1_max, 16))]
-            else:
-                tiny = [(H.ESTEP_G16, 0, 16)]
-            edges = [(H.ESTEP_B8, b4_words, None), (H.ESTEP_B4, 64 * cws, b4_words),
-                     (H.ESTEP_G64C, 64, 64 * cws), (H.ESTEP_G64, 32, 64), (H.ESTEP_G32, 16, 32)] + tiny
-            L = np.where(L == 0, 1, L)
-        else:
-            # every word gets a row (empty words write zeros), so class_word needs no clearing
-            edges = [(H.SUFF_B8, 1024, None), (H.SUFF_G64, 64, 1024), (H.SUFF_G16, -1, 64)]
-        for var, lo, hi in edges:
-            m = (L > lo) if hi is None else ((L > lo) & (L <= hi))
-            if m.any():
-                plan.append((var, torch.from_numpy(order[m].copy()).to(device)))
-        self.plan = plan
-
-
-
 def cphi_window_bounds(doc_ptr, budget_rows: int):
     """Contiguous nnz-balanced document windows of <= budget_rows corpus entries each (a document
     longer than the budget gets a window of its own): [{d0, d1, e0, e1}] covering every document."""
@@ -160,10 +91,10 @@ class LDAEngine:
                  streams: int = 4, local_shard: bool = False, split_docs: bool = True,
                  split_min: Optional[int] = 4096, use_graph: bool = True, precision: str = "fp64",
                  emulate_shards: int = 0, doc_offset: int = 0, cphi_gb: Optional[float] = None):
-        """precision (hip backend): "fp64" = lda-c arithmetic with the block Gauss-Seidel schedule
-        (lda_gs64.hip, the default); "fp32" = the fp32 Jacobi engine (opt-in fast mode).
-        emulate_shards (torch backend, one process): reduce the sufficient statistics as N
-        nnz-balanced document shards summed in shard order -- bitwise the N-rank run under
+        """precision: "fp64" (the only engine: lda-c's double arithmetic; the hip backend runs the block
+        Gauss-Seidel schedule of lda_gs64.hip).
+        emulate_shards (torch backend, one process): reduce the sufficient statistics as the N
+        document shards of ``dist.engine_bounds`` summed in shard order -- bitwise the N-rank run under
         ONI_DIST_DETERMINISTIC=1 (parallel/dist.py).
         local_shard: ``corpus`` is already this rank's shard; ``doc_offset`` its first global document
         (the row-sharded pipeline, corpus/sharded.py).
@@ -176,8 +107,8 @@ class LDAEngine:
         self.emulate_shards = int(emulate_shards)
         # cpu backend: lda-c's MPI ranks (document shards reduced in shard order; 1 = one process)
         self.cpu_shards = 1
-        if precision not in ("fp64", "fp32"):
-            raise ValueError(f"precision must be fp64 or fp32, got {precision!r}")
+        if precision != "fp64":
+            raise ValueError(f"precision must be fp64 (lda-c's arithmetic), got {precision!r}")
         self.precision = precision
         self.K = int(num_topics)
         self.V = corpus.num_terms
@@ -222,57 +153,10 @@ class LDAEngine:
             self.doc_range = (0, corpus.num_docs)
         self.corpus = corpus
         self.D = corpus.num_docs
-        self.fp64 = backend == "hip" and precision == "fp64"
+        self.fp64 = backend == "hip"
         self.use_graph = use_graph
         if self.fp64:
             self._init_gs64(corpus)
-        elif backend == "hip":
-            from ...ops import hip as H
-            self.KS = H.padded_topics(self.K)
-            self.dc = DeviceCorpus.build(corpus, self.device)
-            self.doc_buckets = _Buckets(self.dc.doc_len, self.KS, self.device, "doc",
-                                        doc_ptr=corpus.doc_ptr, split=split_docs, split_min=split_min)
-            dev, D, V, KS, nnz = self.device, self.D, self.V, self.KS, corpus.nnz
-            self.beta = torch.zeros(V, KS, dtype=torch.float32, device=dev)
-            self.cw = torch.zeros(V, KS, dtype=torch.float32, device=dev)
-            self.gamma = torch.zeros(D, KS, dtype=torch.float32, device=dev)
-            self.e = torch.zeros(D, KS, dtype=torch.float32, device=dev)
-            self.r = torch.zeros(max(nnz, 1), dtype=torch.float32, device=dev)[:nnz]
-            self.lik = torch.zeros(D, dtype=torch.float64, device=dev)
-            self.ass = torch.zeros(D, dtype=torch.float64, device=dev)
-            self.iters = torch.zeros(D, dtype=torch.int32, device=dev)
-            self._streams = [torch.cuda.Stream(device=dev) for _ in range(max(0, streams - 1))]
-            # [likelihood, alpha_ss, class_total[0..KS)]: the doubles one EM iteration reduces
-            self._red = torch.zeros(2 + KS, dtype=torch.float64, device=dev)
-            self._scalars = self._red[:2]
-            self.class_total = self._red[2:]
-            # Several ranks: the E-step writes rank-local statistics, the all-reduce works on copies
-            # (re-reducing unchanged locals after the device loop has converged is then a no-op).
-            self._distributed = dist is not None and dist.active
-            self._cw_local = torch.zeros_like(self.cw) if self._distributed else self.cw
-            self._red_local = torch.zeros_like(self._red) if self._distributed else self._red
-            self.suff_plan = H.SuffPlan(self.dc.word_len, dev, wide=_use_wide(self.KS))
-            # per-workgroup partial rows {lik, alpha_ss, class_total[KS]} -> one colsum pass -> _red
-            self._suff_part = torch.zeros(max(self.suff_plan.n_blocks, 1), 2 + KS, dtype=torch.float64, device=dev)
-            self._done_count = torch.zeros(1, dtype=torch.int32, device=dev)
-            self._alpha_dummy = torch.zeros(1, dtype=torch.float64, device=dev)
-            self._red_scratch = torch.zeros(H.lib().reduce_scratch_doubles(KS), dtype=torch.float64, device=dev)
-            self._ct_fresh = False
-            self._params = torch.zeros(H.PARAM_COUNT, dtype=torch.float64, device=dev)
-            self._gate = self._params[H.PARAM_DONE:H.PARAM_DONE + 1]
-            # device EM loop control block + per-iteration history (em_control.hip)
-            self._hist_cap = 64
-            self._ctlhist = torch.zeros(8 + H.HIST_COLS * self._hist_cap, dtype=torch.float64, device=dev)
-            self._ctl, self._hist = self._ctlhist[:8], self._ctlhist[8:]
-            self._ev_fork = torch.cuda.Event()
-            self._ev_join = [torch.cuda.Event() for _ in range(1 + len(self._streams))]
-            self.use_graph = use_graph
-            self._graph = None
-            self._mgraph, self._mgraph_key = None, None
-            self._fgraphs, self._fgraph_key = {}, None
-            self._out_host = torch.zeros(self._ctlhist.numel(), dtype=torch.float64).pin_memory()
-            self._pushed = None
-            self._build_schedule()
         elif backend == "torch":
             dev = self.device
             self.KS = self.K
@@ -305,9 +189,8 @@ class LDAEngine:
             shared = np.unique(self._xchg.send_idx.cpu().numpy())
             local = self._xchg.local_ids.cpu().numpy()
             private = np.setdiff1d(local, shared, assume_unique=True)
-            wide = _use_wide(self.KS) and not self.fp64
-            self._plan_a = H.SuffPlan(self.dc.word_len, self.device, wide=wide, words=shared)
-            self._plan_b = H.SuffPlan(self.dc.word_len, self.device, wide=wide, words=private)
+            self._plan_a = H.SuffPlan(self.dc.word_len, self.device, words=shared)
+            self._plan_b = H.SuffPlan(self.dc.word_len, self.device, words=private)
             nb = max(self._plan_a.n_blocks + self._plan_b.n_blocks, self.suff_plan.n_blocks, 1)
             self._suff_part = torch.zeros(nb, 2 + self.KS, dtype=torch.float64, device=self.device)
             self._graph_a = self._graph_b = None
@@ -378,7 +261,7 @@ class LDAEngine:
         if self.backend == "cpu":
             u = resolved_gs_updates(self.settings, self.K)
             return "lda-c per-word Gauss-Seidel, fp64" if u == 0 else f"block Gauss-Seidel, fp64, {u} refreshes per sweep"
-        return "Jacobi, " + ("fp32 E-step" if self.backend == "hip" else "fp64")
+        return "Jacobi, fp64"
 
     # ------------------------------------------------- fp64 block Gauss-Seidel
     def gs_updates(self) -> int:
@@ -447,7 +330,6 @@ class LDAEngine:
         self._fgraphs, self._fgraph_key = {}, None
         self._out_host = torch.zeros(self._ctlhist.numel(), dtype=f64).pin_memory()
         self._pushed = None
-        self.doc_buckets = None
         self._suff_split = None
         if self._cwin is not None:
             self._build_window_suff()
@@ -470,7 +352,8 @@ class LDAEngine:
                     continue
                 o = order.cpu().numpy()
                 o = o[o >= 0]
-                need = int(corpus.doc_ptr[o + 1].sum() - corpus.doc_ptr[o].sum()) * KS * 8
+                # GSStage pads every document to whole 64-row tiles
+                need = int((-(-(corpus.doc_ptr[o + 1] - corpus.doc_ptr[o]) // 64)).sum()) * 64 * KS * 8
                 if need > cap:
                     continue
                 cap -= need
@@ -807,10 +690,7 @@ class LDAEngine:
     def _mstep_beta(self):
         if self.backend == "hip":
             from ...ops import hip as H
-            if self.fp64:
-                H.gs_mstep(self.cw, self.class_total, self.beta, self.K)
-            else:
-                H.lda_mstep(self.cw, self.class_total, self.beta, self.K)
+            H.gs_mstep(self.cw, self.class_total, self.beta, self.K)
         else:
             from ...ops import reference as R
             self.beta.copy_(R.mstep(self.cw, self.class_total, self.K))
@@ -872,11 +752,11 @@ class LDAEngine:
         """class_word and [likelihood, alpha_ss] as N ranks would produce them (each shard's own
         statistics on freshly allocated tensors, then 0 + s_0 + s_1 + ... in shard order)."""
         from ...ops import reference as R
-        from ...parallel.dist import shard_bounds
+        from ...parallel.dist import engine_bounds
         ptr = self.corpus.doc_ptr
         cw = torch.zeros(self.V, self.K, dtype=torch.float64, device=self.device)
         sc = torch.zeros(2, dtype=torch.float64, device=self.device)
-        for d0, d1 in shard_bounds(ptr, self.emulate_shards):
+        for d0, d1 in engine_bounds(ptr, self.emulate_shards):
             e0, e1 = int(ptr[d0]), int(ptr[d1])
             lp = (self.t_doc_ptr[d0:d1 + 1] - self.t_doc_ptr[d0]).clone()
             cw += R.suffstats(lp, self.t_word[e0:e1].clone(), out["e"][d0:d1].clone(), out["r"][e0:e1].clone(),
@@ -901,100 +781,21 @@ class LDAEngine:
         return self._scalars
 
     def _launch_estep(self, newton_key=None, phase: str = "all"):
-        """Enqueue one E-step: document buckets on their streams, one join, then (main stream) the
-        suff-stats launch, which also sums slices of the per-document likelihood / alpha_ss, and one
-        column pass giving {likelihood, alpha_ss, class_total}.  With ``newton_key`` =
+        """Enqueue one E-step (``_launch_estep64``): document buckets on their streams, one join, then
+        (main stream) the suff-stats launch, which also sums slices of the per-document likelihood /
+        alpha_ss, and one column pass giving {likelihood, alpha_ss, class_total}.  With ``newton_key`` =
         (estimate_alpha, num_docs) the M-step follows in the same launch sequence (single-rank fused
         EM iteration): beta, the alpha Newton (workgroup 0) and the EM convergence test in one launch.
         Every kernel is gated on params[DONE] (device-side convergence)."""
-        if self.fp64:
-            return self._launch_estep64(newton_key, phase)
-        from ...ops import hip as H
-        dc = self.dc
-        prm = self._params
-        gate = self._gate
-        a = self.alpha
-        main = torch.cuda.current_stream(self.device)
-        if phase == "B":
-            # overlap mode, after the shared rows left: the private words' suff-stats, then the class
-            # totals of both launches and the all-reduce input
-            pa, pb = self._plan_a, self._plan_b
-            H.lda_suffstats_fused(dc.word_ptr, dc.csc_ent, dc.csc_doc, pb, self.e, self.r, self.beta,
-                                  self._cw_local, self._suff_part[pa.n_blocks:pa.n_blocks + pb.n_blocks], gate=gate,
-                                  scalars=None if pa.n_blocks else (self.lik, self.ass, 0, self.lik.numel()))
-            H.colsum_partials(self._suff_part, pa.n_blocks + pb.n_blocks, self._red_local, gate=gate)
-            self._red.copy_(self._red_local)
-            return
-        streams = [main] + self._streams
-        self._ev_fork.record(main)
-        used = set()
-        # side streams first: the long-document kernels (the critical path) are dispatched before the
-        # short-document bulk floods the CUs
-        order = list(range(1, len(self._schedule))) + [0]
-        for si in order:
-            work = self._schedule[si]
-            if not work:
-                continue
-            s = streams[si % len(streams)]
-            used.add(si % len(streams))
-            if s is not main:
-                s.wait_event(self._ev_fork)
-            with torch.cuda.stream(s):
-                for kind, item in work:
-                    if kind == "split":
-                        sp = self.doc_buckets.split
-                        H.lda_estep_split(dc.doc_ptr, dc.word_idx, dc.counts, self.beta, self.K, a, 0.0, 0, 0.0,
-                                          self.gamma, self.e, self.r, self.lik, self.ass, self.iters, item,
-                                          sp.seg_words, params=prm, wide=sp.wide)
-                    else:
-                        var, order = item
-                        H.lda_estep(dc.doc_ptr, dc.word_idx, dc.counts, order, self.beta, self.K, a, 0.0, 0, 0.0,
-                                    self.gamma, self.e, self.r, self.lik, self.ass, self.iters, var, params=prm)
-        for si in sorted(used):
-            s = streams[si]
-            if s is main:
-                continue
-            self._ev_join[si].record(s)
-            main.wait_event(self._ev_join[si])
-        # sufficient statistics: one deterministic CSC gather-reduce launch over every word (empty
-        # words included, so cw needs no clearing); each workgroup also sums a slice of the
-        # documents' likelihood / alpha_ss, so one column pass over the partial rows gives
-        # {likelihood, alpha_ss, class_total} (no side-stream reduction, no stream join)
-        scal = (self.lik, self.ass, 0, self.lik.numel())
-        if phase == "A":
-            # overlap mode: the shared words' rows first, packed for the all-to-all
-            H.lda_suffstats_fused(dc.word_ptr, dc.csc_ent, dc.csc_doc, self._plan_a, self.e, self.r, self.beta,
-                                  self._cw_local, self._suff_part[:max(self._plan_a.n_blocks, 1)], gate=gate,
-                                  scalars=scal)
-            self._xchg.pack(self._cw_local)
-            return
-        sp = self.suff_plan
-        H.lda_suffstats_fused(dc.word_ptr, dc.csc_ent, dc.csc_doc, sp, self.e, self.r, self.beta, self._cw_local,
-                              self._suff_part[:max(sp.n_blocks, 1)], gate=gate, scalars=scal)
-        H.colsum_partials(self._suff_part, sp.n_blocks, self._red_local, gate=gate)
-        if self._distributed:
-            # collective inputs (see __init__): the dense all-reduce runs on self.cw / self._red;
-            # the sparse exchange packs the shared rows here and accumulates in the M graph
-            if self._xchg is not None:
-                self._xchg.pack(self._cw_local)
-            else:
-                self.cw.copy_(self._cw_local)
-            self._red.copy_(self._red_local)
-        if newton_key is not None:
-            self._launch_beta_control(newton_key)
+        return self._launch_estep64(newton_key, phase)
 
     def _launch_beta_control(self, newton_key):
         """beta, the alpha Newton (workgroup 0 of the same launch) and the EM convergence step."""
         from ...ops import hip as H
         rows = self._xchg.local_rows32 if self._xchg is not None else None
-        if self.fp64:
-            H.gs_mstep_control(self.cw, self.class_total, self.beta, self.K, self._scalars, self._params, self._ctl,
-                               self._hist, self._done_count, rows=rows,
-                               newton=(newton_key[0], newton_key[1], self._alpha_dummy))
-            return
-        H.lda_mstep_control(self.cw, self.class_total, self.beta, self.K, self._scalars, self._params, self._ctl,
-                            self._hist, self._done_count, rows=rows,
-                            newton=(newton_key[0], newton_key[1], self._alpha_dummy))
+        H.gs_mstep_control(self.cw, self.class_total, self.beta, self.K, self._scalars, self._params, self._ctl,
+                           self._hist, self._done_count, rows=rows,
+                           newton=(newton_key[0], newton_key[1], self._alpha_dummy))
 
     def _reduce_stats(self):
         """Cross-rank reduction of one EM iteration's statistics (outside the graphs): the packed
@@ -1228,9 +1029,8 @@ class LDAEngine:
     def _check_split_error(self):
         """A NaN likelihood: if a split-document barrier timed out, fail loudly (the kernel
         flags it instead of hanging the GPU)."""
-        plans = [self.doc_buckets.split if self.doc_buckets is not None else None]
         gp = getattr(self, "gs_plan", None)
-        plans.append(gp.split if gp is not None else None)
+        plans = [gp.split if gp is not None else None]
         plans += [w["gp"].split for w in (getattr(self, "_cwin", None) or [])]
         if any(int(b["error"].item()) for x in plans if x is not None for b in x.batches):
             raise RuntimeError("split-document E-step: a cross-workgroup barrier timed out "
@@ -1278,53 +1078,9 @@ class LDAEngine:
         self._graph = self._capture(self._launch_estep)
 
 
-    def _build_schedule(self):
-        """Assign E-step work to streams (critical path first): [side 1: split batches],
-        [side 2: B8 + B4], [side 3: G64C/G64/G32], [main: thread-per-document bulk]."""
-        from ...ops import hip as H
-        nstreams = 1 + len(self._streams)
-        long_vars = (H.ESTEP_B8, H.ESTEP_B4, H.ESTEP_WB8, H.ESTEP_WB4)
-        tiny_vars = (H.ESTEP_T1, H.ESTEP_G16, H.ESTEP_W16)
-        sched = [[] for _ in range(max(nstreams, 1))]
-        sp = self.doc_buckets.split
-        split_work = [("split", b) for b in sp.batches] if sp is not None else []
-        plan = self.doc_buckets.plan
-        long_work = [("bucket", (v, o)) for v, o in plan if v in long_vars]
-        mid_work = [("bucket", (v, o)) for v, o in plan if v not in long_vars and v not in tiny_vars]
-        tiny_work = [("bucket", (v, o)) for v, o in plan if v in tiny_vars]
-        b8_work = [w for w in long_work if w[1][0] in (H.ESTEP_B8, H.ESTEP_WB8)]
-        b4_work = [w for w in long_work if w[1][0] not in (H.ESTEP_B8, H.ESTEP_WB8)]
-        spec = os.environ.get("ONI_ESTEP_SCHED")
-        if spec and nstreams >= 4:
-            # experiment hook: "split+B4|B8|G64C+G64+G32|T1" = side streams 1..3 | main
-            names = {"split": None, "B8": (H.ESTEP_B8, H.ESTEP_WB8), "B4": (H.ESTEP_B4, H.ESTEP_WB4),
-                     "G64C": (H.ESTEP_G64C,), "G64": (H.ESTEP_G64, H.ESTEP_W64), "G32": (H.ESTEP_G32, H.ESTEP_W32),
-                     "T1": tiny_vars}
-            lanes = spec.split("|")
-            for si, lane in zip([1, 2, 3, 0], lanes):
-                for tok in lane.split("+"):
-                    if tok == "split":
-                        sched[si] += split_work
-                    else:
-                        sched[si] += [("bucket", (v, o)) for v, o in plan if v in names[tok]]
-        elif nstreams >= 4:
-            # B4 queues behind the split batches: B8 alone is about as long as split + B4 (measured
-            # against moving B4 behind B8 and the short-document buckets behind split: 3-7 % slower)
-            sched[1], sched[2], sched[3], sched[0] = split_work + b4_work, b8_work, mid_work, tiny_work
-        elif nstreams == 3:
-            sched[1], sched[2], sched[0] = split_work, long_work, mid_work + tiny_work
-        elif nstreams == 2:
-            sched[1], sched[0] = split_work + long_work, mid_work + tiny_work
-        else:
-            sched[0] = split_work + long_work + mid_work + tiny_work
-        self._schedule = sched
-
     def m_step(self, estimate_alpha: bool, alpha_ss: float, num_docs: int):
-        if self.backend == "hip":
-            from ...ops import hip as H
-            H.colsum(self.cw, self.class_total, self._red_scratch)
-        else:
-            self.class_total = self.cw.sum(0, dtype=torch.float64)
+        """Host M-step of the torch / cpu backends (the hip engine's runs inside its launch sequence)."""
+        self.class_total = self.cw.sum(0, dtype=torch.float64)
         self._mstep_beta()
         if estimate_alpha:
             self.alpha = special.opt_alpha(alpha_ss, num_docs, self.K)

@@ -252,6 +252,10 @@ def estimate(corpus: Corpus, num_topics: int, alpha_init: float, settings: LDASe
         writer.close()
         concat_parts()
 
+    # error path (StageRunner.finish_deferred(suppress=True)): only the failing rank may get there, so
+    # drain this rank's writer and leave the collective part-file concatenation out
+    close_files.abort = writer.close
+
     ok = False
     try:
         # corpus_global: only when every rank holds the whole corpus (seeded init draws from it)

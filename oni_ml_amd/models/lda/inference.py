@@ -13,15 +13,14 @@ from .em import LDAEngine, resolved_gs_updates
 from .settings import LDASettings
 
 
-def infer(corpus, log_beta: np.ndarray, alpha: float, settings: LDASettings, backend: str = "auto", device=None,
-          precision: str = "fp64"):
-    """Returns (gamma [D, K] f64, per-document likelihood [D] f64).  ``precision``: GPU engine (fp64 block
-    Gauss-Seidel, or the fp32 Jacobi engine); the cpu backend is lda-c's schedule (settings.gs_updates)."""
+def infer(corpus, log_beta: np.ndarray, alpha: float, settings: LDASettings, backend: str = "auto", device=None):
+    """Returns (gamma [D, K] f64, per-document likelihood [D] f64).  The GPU engine runs the fp64 block
+    Gauss-Seidel schedule; the cpu backend is lda-c's schedule (settings.gs_updates)."""
     K, V = log_beta.shape
     if corpus.num_terms > V:
         raise ValueError("corpus word id beyond the model vocabulary")
     corpus.num_terms = V
-    eng = LDAEngine(corpus, K, settings, alpha_init=alpha, backend=backend, device=device, precision=precision)
+    eng = LDAEngine(corpus, K, settings, alpha_init=alpha, backend=backend, device=device)
     eng.init_from_model(log_beta, alpha)
     if eng.backend == "cpu":
         lb = np.ascontiguousarray(log_beta)

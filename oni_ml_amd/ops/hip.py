@@ -20,13 +20,6 @@ import torch
 _LIB = None
 _ERR = None
 
-# estep / suffstats variant ids (csrc/hip/kernels.h)
-ESTEP_G16, ESTEP_G32, ESTEP_G64, ESTEP_G64C, ESTEP_B4, ESTEP_B8, ESTEP_T1 = range(7)
-# wide-topic variants (lda_estep_wide.hip): 4 lanes share one word's topics
-ESTEP_W16, ESTEP_W32, ESTEP_W64, ESTEP_WB4, ESTEP_WB8 = range(7, 12)
-WIDE_KS = (32, 52, 64, 100, 128)   # kernels.h ONI_FOR_EACH_WIDE_KS
-SUFF_G16, SUFF_G64, SUFF_B8 = range(3)
-
 
 def _import():
     global _LIB, _ERR
@@ -89,165 +82,6 @@ def _chk(t: torch.Tensor, dtype, name, shape=None, device=None):
     return t.data_ptr()
 
 
-def lda_estep(doc_ptr, word_idx, counts, order, beta, K, alpha, lik_const, var_max_iter, var_conv,
-              gamma, e_out, r_out, lik, alpha_ss, iters, variant, params=None, dbg=None):
-    """`params`: optional device f64[4] {alpha, lik_const, var_max_iter, var_conv} overriding the scalars
-    (graph-replayed E-steps)."""
-    D = doc_ptr.numel() - 1
-    nnz = word_idx.numel()
-    V, KS = beta.shape
-    if KS not in compiled_ks():
-        raise ValueError(f"beta row stride {KS} has no compiled kernel")
-    if not (0 < K <= KS):
-        raise ValueError("K out of range")
-    dev = beta.device
-    args = [
-        _chk(doc_ptr, torch.int32, "doc_ptr", (D + 1,), dev),
-        _chk(word_idx, torch.int32, "word_idx", (nnz,), dev),
-        _chk(counts, torch.float32, "counts", (nnz,), dev),
-        _chk(order, torch.int32, "order", None, dev),
-        order.numel(),
-        _chk(beta, torch.float32, "beta", (V, KS), dev),
-        int(K), int(KS), float(alpha), float(lik_const), int(var_max_iter), float(var_conv),
-        _chk(gamma, torch.float32, "gamma", (D, KS), dev),
-        _chk(e_out, torch.float32, "e_out", (D, KS), dev),
-        _chk(r_out, torch.float32, "r_out", (nnz,), dev),
-        _chk(lik, torch.float64, "lik", (D,), dev),
-        _chk(alpha_ss, torch.float64, "alpha_ss", (D,), dev),
-        _chk(iters, torch.int32, "iters", (D,), dev),
-        int(variant), _params_ptr(params, dev), _stream(),
-        0 if dbg is None else _chk(dbg, torch.int64, "dbg", (8,), dev),
-    ]
-    if order.numel() == 0:
-        return
-    lib().lda_estep(*args)
-
-
-def split_launch_cap(KS: int, wide: bool) -> int:
-    """Workgroups per split launch: min(kSplitMaxBlocks, 3/4 of the device's co-resident capacity from
-    the occupancy API), so the segments of a launch are resident together with room for the other
-    streams' buckets; ONI_SPLIT_MAX_BLOCKS lowers it (tests, shared / partitioned GPUs)."""
-    L = lib()
-    cap = min(int(L.split_max_blocks()), max(1, int(L.split_capacity(int(KS), bool(wide))) * 3 // 4))
-    env = os.environ.get("ONI_SPLIT_MAX_BLOCKS")
-    if env:
-        cap = max(1, min(cap, int(env)))
-    return cap
-
-
-class SplitPlan:
-    """Launch batches for the split-document E-step (huge documents over several workgroups).
-
-    Each batch holds <= split_max_blocks() workgroups so every segment of a batch is
-    co-resident (the per-iteration cross-workgroup barrier cannot deadlock)."""
-
-    def __init__(self, doc_ids, doc_ptr_host, KS: int, device, wide: bool = False, seg_words: int = None):
-        L = lib()
-        self.wide = bool(wide)
-        self.max_blocks = split_launch_cap(KS, self.wide)
-        # narrow kernel: a segment is exactly its register cache; wide kernel: any size
-        # (the first wide_words(KS, 512) words in registers, the rest streamed)
-        self.seg_words = int(L.split_segment_words(KS))
-        if wide:
-            # wide kernel segments stream their words, so the size is free: pick it to minimise
-            # the split path's critical path, sum over launches of (longest segment + barrier)
-            lens = [int(doc_ptr_host[d + 1] - doc_ptr_host[d]) for d in doc_ids]
-            self.seg_words = self.plan_segments(lens, int(L.wide_slots(KS, 512)), self.max_blocks,
-                                                int(seg_words or 0))
-
-        self.batches = []
-        self.leftover = []          # docs needing more segments than a batch holds
-        cur = []
-        used = 0
-        for d in doc_ids:
-            n = int(doc_ptr_host[d + 1] - doc_ptr_host[d])
-            nseg = (n + self.seg_words - 1) // self.seg_words
-            if nseg > self.max_blocks:
-                self.leftover.append(int(d))
-                continue
-            if used + nseg > self.max_blocks:
-                self.batches.append(self._make(cur, doc_ptr_host, KS, device))
-                cur, used = [], 0
-            cur.append((int(d), nseg))
-            used += nseg
-        if cur:
-            self.batches.append(self._make(cur, doc_ptr_host, KS, device))
-
-    @staticmethod
-    def plan_segments(lens, unit: int, max_blocks: int, min_words: int = 0, barrier_words: int = 2500) -> int:
-        """Segment size (a multiple of `unit`) minimising sum_batches(max segment words + barrier_words):
-        per variational iteration a launch costs its longest segment's streaming time plus one
-        cross-workgroup barrier (~10 us ~ 2.5k words of K = 100 rows at one CU's L2 bandwidth)."""
-        if not lens:
-            return max(unit, min_words)
-        mx = max(lens)
-        lo = max(unit, min_words, -(-mx // max_blocks))
-        best = None
-        seg = -(-lo // unit) * unit
-        cands = set()
-        while seg < mx:
-            cands.add(seg)
-            seg = -(-int(seg * 1.25) // unit) * unit
-        cands.add(-(-mx // unit) * unit)
-        for seg in sorted(cands):
-            cost, used, cur = 0, 0, 0
-            for n in lens:
-                k = -(-n // seg)
-                if used + k > max_blocks:
-                    cost += cur + barrier_words
-                    used, cur = 0, 0
-                used += k
-                cur = max(cur, min(n, seg))
-            cost += cur + barrier_words
-            if best is None or cost < best[0]:
-                best = (cost, seg)
-        return best[1]
-
-    def _make(self, docs, doc_ptr_host, KS, device):
-        import numpy as np
-        sd, si, sc, sb, slot = [], [], [], [], []
-        for j, (d, nseg) in enumerate(docs):
-            base = len(sd)
-            for q in range(nseg):
-                sd.append(d), si.append(q), sc.append(nseg), sb.append(base), slot.append(j)
-        t = lambda a: torch.tensor(np.asarray(a, np.int32), device=device)
-        nb = len(sd)
-        return dict(seg_doc=t(sd), seg_index=t(si), seg_count=t(sc), seg_base=t(sb), doc_slot=t(slot), n_blocks=nb,
-                    # tagged hand-off granules {float, uint32 tag}: [2][n_blocks][KS + 2]
-                    xchg=torch.zeros(2 * nb * (KS + 2), dtype=torch.int64, device=device),
-                    # per document: launch epoch, exit count (the kernel keeps both consistent)
-                    counter=torch.zeros(2 * len(docs), dtype=torch.int32, device=device),
-                    error=torch.zeros(1, dtype=torch.int32, device=device), docs=len(docs))
-
-
-def lda_estep_split(doc_ptr, word_idx, counts, beta, K, alpha, lik_const, var_max_iter, var_conv, gamma, e_out, r_out,
-                    lik, alpha_ss, iters, batch, seg_words, params=None, wide=False, dbg=None):
-    """dbg: optional int64[8] phase timer of workgroup 0 (narrow kernel): cycles in word pass, reductions,
-    publish, gather wait, topic phase, loop barrier; iterations; segments of its document."""
-    D = doc_ptr.numel() - 1
-    nnz = word_idx.numel()
-    V, KS = beta.shape
-    dev = beta.device
-    nb = batch["n_blocks"]
-    for k in ("seg_doc", "seg_index", "seg_count", "seg_base", "doc_slot"):
-        _chk(batch[k], torch.int32, k, (nb,), dev)
-    if wide and KS not in WIDE_KS:
-        raise ValueError(f"no wide split kernel for KS={KS}")
-    lib().lda_estep_split(
-        bool(wide), _chk(doc_ptr, torch.int32, "doc_ptr", (D + 1,), dev), _chk(word_idx, torch.int32, "word_idx", (nnz,), dev),
-        _chk(counts, torch.float32, "counts", (nnz,), dev), _chk(beta, torch.float32, "beta", (V, KS), dev),
-        int(K), int(KS), float(alpha), float(lik_const), int(var_max_iter), float(var_conv),
-        _chk(gamma, torch.float32, "gamma", (D, KS), dev), _chk(e_out, torch.float32, "e_out", (D, KS), dev),
-        _chk(r_out, torch.float32, "r_out", (nnz,), dev), _chk(lik, torch.float64, "lik", (D,), dev),
-        _chk(alpha_ss, torch.float64, "alpha_ss", (D,), dev), _chk(iters, torch.int32, "iters", (D,), dev),
-        batch["seg_doc"].data_ptr(), batch["seg_index"].data_ptr(), batch["seg_count"].data_ptr(),
-        batch["seg_base"].data_ptr(), batch["doc_slot"].data_ptr(), int(nb), int(seg_words),
-        _chk(batch["xchg"], torch.int64, "xchg", (2 * nb * (KS + 2),), dev),
-        _chk(batch["counter"], torch.int32, "counter", (2 * batch["docs"],), dev), int(batch["docs"]),
-        _chk(batch["error"], torch.int32, "error", (1,), dev),
-        _params_ptr(params, dev), _stream(), 0 if dbg is None else _chk(dbg, torch.int64, "dbg", (8,), dev))
-
-
 PARAM_COUNT = 8      # device parameter block (csrc/hip/kernels.h kParamCount)
 PARAM_DONE = 4       # params[PARAM_DONE] != 0: the EM loop converged, kernels skip
 HIST_COLS = 6        # em_control history row: likelihood, conv, alpha, VAR_MAX_ITER, alpha_ss, -
@@ -260,28 +94,6 @@ def _params_ptr(params, dev) -> int:
 def _gate_ptr(gate, dev) -> int:
     """Pointer to a float64 flag (e.g. params[PARAM_DONE:PARAM_DONE+1]) or 0."""
     return 0 if gate is None else _chk(gate, torch.float64, "gate", (1,), dev)
-
-
-def lda_suffstats(word_ptr, csc_ent, csc_doc, order, e, r, beta, cw, variant, gate=None):
-    V, KS = beta.shape
-    nnz = csc_ent.numel()
-    D = e.shape[0]
-    dev = beta.device
-    args = [
-        _chk(word_ptr, torch.int32, "word_ptr", (V + 1,), dev),
-        _chk(csc_ent, torch.int32, "csc_ent", (nnz,), dev),
-        _chk(csc_doc, torch.int32, "csc_doc", (nnz,), dev),
-        _chk(order, torch.int32, "order", None, dev),
-        order.numel(),
-        _chk(e, torch.float32, "e", (D, KS), dev),
-        _chk(r, torch.float32, "r", (nnz,), dev),
-        _chk(beta, torch.float32, "beta", (V, KS), dev),
-        _chk(cw, torch.float32, "cw", (V, KS), dev),
-        int(KS), int(variant), _gate_ptr(gate, dev), _stream(),
-    ]
-    if order.numel() == 0:
-        return
-    lib().lda_suffstats(*args)
 
 
 def argsort_desc_stable(keys):
@@ -303,15 +115,14 @@ def argsort_desc_stable(keys):
 
 
 class SuffPlan:
-    """Word order for the single-launch suff-stats kernel: [heavy | medium | light] (heavy first).
+    """Word order for the single-launch suff-stats kernel (gs_suff64): [heavy | medium | light] (heavy first).
 
     ``words``: restrict the plan to these word ids (a sub-plan; several sub-plans must together
     cover the vocabulary, since every word's class_word row is written by exactly one launch)."""
     HEAVY, LIGHT = 1024, 64
 
-    def __init__(self, word_len, device, wide: bool = False, words=None):
+    def __init__(self, word_len, device, words=None):
         import numpy as np
-        self.wide = bool(wide)      # wide-topic kernel (lda_suff_wide), KS >= 32
         wl = np.asarray(word_len)
         ids = np.arange(wl.size, dtype=np.int64) if words is None else np.asarray(words, np.int64)
         if ids.size and (ids.min() < 0 or ids.max() >= wl.size):
@@ -326,36 +137,6 @@ class SuffPlan:
         self.n_blocks = int(lib().suff_fused_blocks(self.n_heavy, self.n_medium, self.n_light))
 
 
-def lda_suffstats_fused(word_ptr, csc_ent, csc_doc, plan: "SuffPlan", e, r, beta, cw, part, gate=None, scalars=None):
-    """class_word for every word (one launch) + per-workgroup column sums into part.
-
-    part [n_blocks, KS]: topic sums only.  part [n_blocks, 2 + KS]: columns 0 / 1 hold the
-    workgroup's slice sums of ``scalars`` = (lik, alpha_ss, lo, hi) over documents [lo, hi)
-    (zeros without ``scalars``), topics follow -- colsum_partials then yields
-    {likelihood, alpha_ss, class_total} in one pass."""
-    V, KS = beta.shape
-    nnz = csc_ent.numel()
-    D = e.shape[0]
-    dev = beta.device
-    if plan.covers_all and plan.order.numel() != V:
-        raise ValueError("suff plan does not cover the vocabulary")
-    if plan.order.numel() == 0:
-        return
-    if plan.wide and KS < 32:
-        raise ValueError(f"wide suff-stats layout needs KS >= 32 (got {KS})")
-    if part.dim() != 2 or part.shape[1] not in (KS, KS + 2) or part.shape[0] < max(plan.n_blocks, 1):
-        raise ValueError(f"part: shape {tuple(part.shape)}, expected [>= {plan.n_blocks}, {KS} or {KS + 2}]")
-    lib().lda_suffstats_fused(
-        _chk(word_ptr, torch.int32, "word_ptr", (V + 1,), dev), _chk(csc_ent, torch.int32, "csc_ent", (nnz,), dev),
-        _chk(csc_doc, torch.int32, "csc_doc", (nnz,), dev),
-        _chk(plan.order, torch.int32, "order", (plan.order.numel(),), dev),
-        plan.n_heavy, plan.n_medium, plan.n_light,
-        _chk(e, torch.float32, "e", (D, KS), dev), _chk(r, torch.float32, "r", (nnz,), dev),
-        _chk(beta, torch.float32, "beta", (V, KS), dev), _chk(cw, torch.float32, "cw", (V, KS), dev),
-        _chk(part, torch.float64, "part", None, dev), int(KS), _gate_ptr(gate, dev), _stream(),
-        bool(plan.wide), int(part.shape[1]), *_scalar_slice(scalars, D, dev))
-
-
 def _scalar_slice(scalars, D, dev):
     if scalars is None:
         return 0, 0, 0, 0
@@ -368,7 +149,7 @@ def _scalar_slice(scalars, D, dev):
 
 def rows_accumulate(rows, ptr, src, own, recv, out):
     """out[rows[i]] = 0 + sum over j in [ptr[i], ptr[i+1]) of (own[rows[i]] if src[j] < 0 else recv[src[j]]),
-    fp32, in j order (parallel/dist.py VocabExchange.accumulate)."""
+    fp64, in j order (parallel/dist.py VocabExchange.accumulate)."""
     dev = out.device
     V, W = out.shape
     n = rows.numel()
@@ -376,8 +157,8 @@ def rows_accumulate(rows, ptr, src, own, recv, out):
         return
     # ptr / src are built and bounds-checked once on the host (VocabExchange.__init__)
     lib().rows_accumulate(_chk(rows, torch.int32, "rows", (n,), dev), _chk(ptr, torch.int32, "ptr", (n + 1,), dev),
-                          _chk(src, torch.int32, "src", None, dev), _chk(own, torch.float32, "own", (V, W), dev),
-                          _chk(recv, torch.float32, "recv", None, dev), _chk(out, torch.float32, "out", (V, W), dev),
+                          _chk(src, torch.int32, "src", None, dev), _chk(own, torch.float64, "own", (V, W), dev),
+                          _chk(recv, torch.float64, "recv", None, dev), _chk(out, torch.float64, "out", (V, W), dev),
                           int(n), int(W), _stream())
 
 
@@ -396,27 +177,6 @@ def colsum_partials(part, n_blocks, out, gate=None):
         raise ValueError("n_blocks exceeds partial rows")
     lib().colsum_partials(_chk(part, torch.float64, "part", None, dev), int(n_blocks), int(cols),
                           _chk(out, torch.float64, "out", (cols,), dev), _gate_ptr(gate, dev), _stream())
-
-
-def lda_mstep_control(cw, class_total, beta, K, scalars, params, ctl, hist, done_count, rows=None, newton=None):
-    """M-step (beta = cw / class_total) + the device EM convergence step in the last workgroup.
-    ``rows``: int32 word ids, restrict the M-step to them (validated host-side once by the caller).
-    ``newton`` = (estimate_alpha, num_docs, alpha_out): the lda-c alpha Newton runs in workgroup 0 of
-    the same launch (params[0:2] <- alpha, lgamma constant) beside the beta rows."""
-    V, KS = cw.shape
-    dev = cw.device
-    slots = hist.numel() // HIST_COLS
-    n_rows = 0 if rows is None else int(rows.numel())
-    rows_ptr = 0 if rows is None else _chk(rows, torch.int32, "rows", (n_rows,), dev)
-    lib().lda_mstep_control(
-        _chk(cw, torch.float32, "cw", (V, KS), dev), _chk(class_total, torch.float64, "class_total", (KS,), dev),
-        _chk(beta, torch.float32, "beta", (V, KS), dev), int(V), int(K), int(KS),
-        _chk(scalars, torch.float64, "scalars", (2,), dev), _chk(params, torch.float64, "params", (PARAM_COUNT,), dev),
-        _chk(ctl, torch.float64, "ctl", (8,), dev), _chk(hist, torch.float64, "hist", (slots * HIST_COLS,), dev),
-        int(slots), _chk(done_count, torch.int32, "done_count", (1,), dev), _stream(), rows_ptr, n_rows,
-        0 if newton is None else 1, 0 if newton is None else int(bool(newton[0])),
-        0.0 if newton is None else float(newton[1]),
-        0 if newton is None else _chk(newton[2], torch.float64, "alpha_out", (1,), dev))
 
 
 def alpha_newton(scalars, num_docs, K, estimate, params, alpha_out):
@@ -438,30 +198,8 @@ def em_control(scalars, params, ctl, hist):
                      int(slots), _stream())
 
 
-def colsum(mat, out, scratch, gate=None):
-    """out[k] = sum_r mat[r, k] (f32 -> f64, deterministic)."""
-    rows, cols = mat.shape
-    dev = mat.device
-    need = lib().reduce_scratch_doubles(cols)
-    lib().colsum(_chk(mat, torch.float32, "mat", None, dev), int(rows), int(cols),
-                 _chk(out, torch.float64, "out", (cols,), dev),
-                 _chk(scratch, torch.float64, "scratch", None, dev) if scratch.numel() >= need else _bad("scratch"),
-                 _gate_ptr(gate, dev), _stream())
-
-
 def _bad(name):
     raise ValueError(f"{name}: buffer too small")
-
-
-def lda_mstep(cw, class_total, beta, K, gate=None):
-    V, KS = cw.shape
-    dev = cw.device
-    lib().lda_mstep(
-        _chk(cw, torch.float32, "cw", (V, KS), dev),
-        _chk(class_total, torch.float64, "class_total", (KS,), dev),
-        _chk(beta, torch.float32, "beta", (V, KS), dev),
-        int(V), int(K), int(KS), _gate_ptr(gate, dev), _stream(),
-    )
 
 
 def score_events(theta, phi, K, dflt, doc_a, word_a, doc_b, word_b, tol):

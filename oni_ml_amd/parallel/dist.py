@@ -8,7 +8,7 @@ ml_ops.sh:80):
   per-worker <rank>.gamma files combined into final.gamma (README.md:121);
 * per EM iteration the collectives are the class_word reduction and one small
   f64 all-reduce ([likelihood, alpha ss, class_total]).  class_word is reduced
-  either densely (ring all-reduce of [V x KS] f32, K*V*4 bytes) or -- when the
+  either densely (ring all-reduce of [V x KS] f64, K*V*8 bytes) or -- when the
   ranks' vocabularies overlap little, as IP/port "words" of different days do --
   by `VocabExchange`: an all-to-all of only the rows two ranks share.  On the
   fully connected xGMI mesh an all-to-all uses every link at once, while a ring
@@ -52,10 +52,9 @@ class DistContext:
 
     # -------------------------------------------------------------- sharding
     def shard_range(self, corpus):
-        """This rank's documents of a corpus every rank holds whole (strong scaling): nnz-balanced, or
-        chain-aware with ONI_SHARD_CHAIN=1 (``chain_bounds``)."""
-        chain = os.environ.get("ONI_SHARD_CHAIN", "0") != "0"
-        return shard_bounds(corpus.doc_ptr, self.world_size, chain=chain)[self.rank]
+        """This rank's documents of a corpus every rank holds whole (strong scaling): ``engine_bounds``,
+        the one shard rule every consumer of a rank's document range uses."""
+        return engine_bounds(corpus.doc_ptr, self.world_size)[self.rank]
 
     # ----------------------------------------------------------- collectives
     def allreduce_suffstats(self, cw: torch.Tensor, scalars: torch.Tensor) -> torch.Tensor:
@@ -331,7 +330,8 @@ class VocabExchange:
     def accumulate(self, cw_out: torch.Tensor, cw_local: torch.Tensor):
         """cw_out[w] = 0 + c_0[w] + c_1[w] + ... for this rank's words w (rank order); rows of other
         words are not touched (never read on this rank).  Cost ~ local rows, not the union vocabulary."""
-        if cw_out.is_cuda and cw_out.dtype == torch.float32 and self.width % 4 == 0:
+        if cw_out.is_cuda and cw_out.dtype == torch.float64 and self.width % 2 == 0:
+            # one HIP launch (csrc/hip/reduce.hip rows_accumulate_kernel), the same bits as the loop below
             from ..ops import hip as H
             H.rows_accumulate(self.local_rows32, self.acc_ptr, self.acc_src, cw_local, self.recv, cw_out)
             return
@@ -393,10 +393,22 @@ def chain_bounds(doc_ptr: np.ndarray, world: int, kappa: float = CHAIN_KAPPA):
     return out
 
 
+def chain_default() -> bool:
+    """Chain-aware document shards are the default (ONI_SHARD_CHAIN=0: plain nnz-balanced cuts)."""
+    return os.environ.get("ONI_SHARD_CHAIN", "1") != "0"
+
+
+def engine_bounds(doc_ptr: np.ndarray, world: int):
+    """The engine's document shards of a corpus split over ``world`` ranks: chain-aware
+    (``chain_bounds``) unless ONI_SHARD_CHAIN=0.  The strong-scaling engine (``shard_range``), the
+    row-sharded pipeline's corpus builder (corpus/sharded.py) and its resume path all use this rule, so
+    a rank's gamma rows and its document names always cover the same documents."""
+    return shard_bounds(doc_ptr, world, chain=chain_default())
+
+
 def shard_bounds(doc_ptr: np.ndarray, world: int, chain: bool = False):
     """Contiguous [d0, d1) ranges with ~equal nnz (ties broken toward equal doc counts).
-    ``chain``: ``chain_bounds`` instead (the engine's own sharding under ONI_SHARD_CHAIN=1; the
-    row-sharded pipeline keeps the nnz cut, which its corpus builder computes collectively)."""
+    ``chain``: ``chain_bounds`` instead (``engine_bounds``, the default rule of the engine's shards)."""
     if chain:
         return chain_bounds(doc_ptr, world)
     D = len(doc_ptr) - 1

@@ -150,11 +150,20 @@ class StageRunner:
 
     def finish_deferred(self, suppress: bool = False):
         """Wait for background output writers; a stage is marked complete only once its files are.
-        ``suppress``: another error is already propagating -- drain the writers, raise nothing."""
+        ``suppress``: another error is already propagating -- drain the writers, raise nothing.  That
+        path may run on one rank only, so a join with an ``abort`` attribute (a writer whose completion
+        is collective, e.g. the LDA part files' concatenation) runs ``abort`` instead: local work only,
+        and no stage is marked complete."""
         pending, self._pending = self._pending, []
         err = None
         for name, rec, join in pending:
             t0 = time.perf_counter()
+            if suppress and hasattr(join, "abort"):
+                try:
+                    join.abort()
+                except Exception:  # noqa: BLE001 -- an error is already propagating
+                    pass
+                continue
             try:
                 join()
             except Exception as e:  # noqa: BLE001 -- re-raised after the other writers finished

@@ -88,10 +88,11 @@ def _lda_stage(R, cfg, ctx, corpus, device, log, summary, local_shard, doc_offse
 
 
 def _files_state(cfg, ctx):
-    """Resume: the corpus files on every rank, this rank's shard of them."""
-    from ..parallel.dist import shard_bounds
+    """Resume: the corpus files on every rank, this rank's shard of them (the engine's own rule,
+    ``dist.engine_bounds``: the engine that re-runs the lda stage splits the documents the same way)."""
+    from ..parallel.dist import engine_bounds
     corpus, doc_names, word_names = C.load_corpus_files(cfg.lpath)
-    d0, d1 = shard_bounds(corpus.doc_ptr, ctx.world_size)[ctx.rank]
+    d0, d1 = engine_bounds(corpus.doc_ptr, ctx.world_size)[ctx.rank]
     return corpus, doc_names, word_names, (d0, d1)
 
 

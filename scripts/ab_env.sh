@@ -10,7 +10,7 @@ while [ $# -gt 0 ] && [ "$1" != "--" ]; do variants+=("$1"); shift; done
 args=("$@")
 for r in $(seq 1 "$rounds"); do
   for v in "${variants[@]}"; do
-    out=$(env $v timeout -k 10 300 python -u bench.py --converge 0 --e2e 0 "${args[@]}" 2>/dev/null | grep '^{') || { echo "variant $v failed"; exit 1; }
+    out=$(env $v timeout -k 10 300 python -u bench.py --converge 0 --e2e 0 --e2e-cold 0 "${args[@]}" 2>/dev/null | grep '^{') || { echo "variant $v failed"; exit 1; }
     ms=$(echo "$out" | python -c "import json,sys; print(json.loads(sys.stdin.read())['ms_per_step'])")
     echo "round $r  $v  ms_per_step=$ms"
   done

@@ -22,6 +22,6 @@ print(f"{sys.argv[2]:10s} K={c['model'][-3:]} docs={c['docs_per_gpu']} V={c['voc
 PY
 }
 run headline "$@" && \
-run flow_k50 --topics 50 --e2e 0 "$@" && \
-run dns_k20 --corpus dns --e2e 0 "$@" && \
-run flow30d_k100 --topics 100 --events 12500000 --e2e 0 "$@"
+run flow_k50 --topics 50 --e2e 0 --e2e-cold 0 "$@" && \
+run dns_k20 --corpus dns --e2e 0 --e2e-cold 0 "$@" && \
+run flow30d_k100 --topics 100 --events 12500000 --e2e 0 --e2e-cold 0 "$@"

@@ -47,7 +47,7 @@ for s in "$@"; do
     prof)
       rm -rf "$OUT/prof"; mkdir -p "$OUT/prof"
       timeout -k 10 500 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run -- python3 bench.py \
-        ${PROF_ARGS:---steps 10 --warmup 3 --converge 0 --e2e 0} > "$OUT/prof/bench.log" 2>&1 || { tail -20 "$OUT/prof/bench.log"; stop prof 1; }
+        ${PROF_ARGS:---steps 10 --warmup 3 --converge 0 --e2e 0 --e2e-cold 0} > "$OUT/prof/bench.log" 2>&1 || { tail -20 "$OUT/prof/bench.log"; stop prof 1; }
       db=$(find "$OUT/prof" -name "*.db" | head -1)
       python scripts/prof_summary.py "$db" --top 30 --md "$OUT/prof_summary.md" > /dev/null
       python scripts/timeline.py "$db" --last-ms ${TIMELINE_MS:-6} > "$OUT/timeline.txt"
@@ -75,7 +75,7 @@ for s in "$@"; do
     pmc)
       rm -rf "$OUT/pmc"; mkdir -p "$OUT/pmc"
       timeout -s KILL 120 rocprofv3 --pmc ${PMC:?set PMC} -d "$OUT/pmc" -o pmc -- python3 bench.py \
-        ${PMC_ARGS:---steps 3 --warmup 1 --converge 0 --e2e 0} > "$OUT/pmc/log.txt" 2>&1 || stop pmc $?
+        ${PMC_ARGS:---steps 3 --warmup 1 --converge 0 --e2e 0 --e2e-cold 0} > "$OUT/pmc/log.txt" 2>&1 || stop pmc $?
       db=$(find "$OUT/pmc" -name "*.db" | head -1)
       python scripts/pmc_summary.py "$db" ${PMC_MATCH:+--match "$PMC_MATCH"} --md "$OUT/pmc_summary.md" > /dev/null
       rm -f "$db"; head -30 "$OUT/pmc_summary.md" ;;

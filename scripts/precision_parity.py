@@ -7,7 +7,6 @@ seed 0) from the SAME random init with several engines and compares what the pip
 
   hip    fp64 block Gauss-Seidel (HIP kernels, csrc/hip/lda_gs64.hip; the bench path): gamma
          refreshed every ceil(n/32) words, lda-c's per-word schedule for documents <= 32 words
-  hip32  fp32 Jacobi E-step (HIP kernels, the opt-in fast mode)
   torch  fp64 Jacobi E-step (PyTorch on the host CPU, ops/reference.py)
   cpu    fp64 Gauss-Seidel E-step, a literal transcription of lda-c's lda_inference
          (csrc/native/lda_ref.cpp; the engine BASELINE.json's docs/s was measured with)
@@ -54,11 +53,10 @@ def _train(corpus, K, name, dev, seed, var_max_iter=None):
     if var_max_iter is not None:
         st.var_max_iter = var_max_iter
     name, _, shards = name.partition("#")       # "cpu#20": lda-c reduced as 20 MPI ranks
-    backend, precision = {"hip": ("hip", "fp64"), "hip32": ("hip", "fp32"), "torch": ("torch", "fp64"),
-                          "cpu": ("cpu", "fp64"), "cpuU": ("cpu", "fp64")}[name]
+    backend = {"hip": "hip", "torch": "torch", "cpu": "cpu", "cpuU": "cpu"}[name]
     if name == "cpuU":
         st.gs_updates = GS_U
-    eng = LDAEngine(corpus, K, st, backend=backend, device=dev, seed=seed, precision=precision)
+    eng = LDAEngine(corpus, K, st, backend=backend, device=dev, seed=seed)
     if shards:
         eng.cpu_shards = int(shards)
     if dev.type == "cuda":
@@ -132,7 +130,7 @@ def main():
     ap.add_argument("--events", type=int, default=1_000_000)
     ap.add_argument("--topics", type=int, default=20)
     ap.add_argument("--seed", type=int, default=0)
-    ap.add_argument("--engines", default="hip,cpu,cpuU,cpu@1,hip32")
+    ap.add_argument("--engines", default="hip,cpu,cpuU,cpu@1")
     ap.add_argument("--var-max-iter", type=int, default=None, help="override settings.txt var max iter (20)")
     ap.add_argument("--corpus", default="flow", choices=["flow", "dns"])
     ap.add_argument("--sub-nnz", type=int, default=0, help="sub-sample to ~this many entries, longest documents kept")

@@ -23,18 +23,11 @@ def pytest_configure(config):
     _ensure_built()
     config.addinivalue_line("markers", "gpu: needs an MI355X (gfx950) GPU and the built HIP extension")
     config.addinivalue_line("markers", "slow: long-running test")
-    config.addinivalue_line("markers", "experimental: the opt-in fp32 Jacobi engine (--precision fp32); "
-                                       "skipped unless ONI_EXPERIMENTAL=1")
 
 
 def pytest_collection_modifyitems(config, items):
     import torch
 
-    if os.environ.get("ONI_EXPERIMENTAL", "0") != "1":
-        exp = pytest.mark.skip(reason="experimental fp32 engine (set ONI_EXPERIMENTAL=1)")
-        for it in items:
-            if "experimental" in it.keywords:
-                it.add_marker(exp)
     if torch.cuda.is_available():
         return
     skip = pytest.mark.skip(reason="no GPU in this environment")

@@ -110,18 +110,31 @@ def test_two_rank_em_matches_single_rank(tmp_path, exchange):
 
 
 def test_bench_two_rank_cpu_rehearsal():
-    """bench.py's multi-rank path (vocabulary union, sharded EM, max-over-ranks timing) on gloo."""
+    """bench.py at N = 2 on gloo: every field of the BENCH line -- the strong-scaling 1-day value (one
+    corpus sharded over the ranks), the weak-scaling secondary, the row-sharded ml_ops pipeline in-process
+    (warm) and as fresh child processes (cold)."""
     import json
     import subprocess
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
                         "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "bench.py", "--gpus", "2",
-                        "--steps", "1", "--warmup", "1", "--events", "5000", "--device", "cpu", "--converge", "0"],
-                       cwd=root, capture_output=True, text=True, timeout=600)
+                        "--steps", "1", "--warmup", "1", "--events", "5000", "--device", "cpu"],
+                       cwd=root, capture_output=True, text=True, timeout=900)
     assert r.returncode == 0, r.stderr[-3000:]
     out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
     assert out["n_gpus"] == 2 and out["config"]["parallelism"] == "dp2" and out["value"] > 0
+    assert out["scaling"] == "strong" and out["config"]["docs"] == out["config"]["global_batch"]
+    # the strong run splits ONE corpus: the shards partition its documents
+    sh = out["shards"]
+    assert sh[0]["doc_range"][0] == 0 and sh[0]["doc_range"][1] == sh[1]["doc_range"][0]
+    assert sh[1]["doc_range"][1] == out["config"]["docs"]
+    assert sum(s["nnz"] for s in sh) == out["config"]["nnz"]
+    assert out["weak_docs_per_sec"] > 0 and out["weak_docs"] > out["config"]["docs"]
+    for k in ("e2e_wall_s", "e2e_cold_wall_s"):
+        assert out[k] > 0, k
+    assert out["e2e_cold_wall_s"] >= out["e2e_cold_inprocess_wall_s"] > 0
+    assert set(out["e2e_stage_s"]) >= {"load", "flow_pre", "lda_pre", "lda", "lda_post", "flow_post"}
 
 
 @pytest.mark.parametrize("exchange", ["dense", "sparse"])

@@ -95,12 +95,12 @@ def test_deterministic_world4_bitwise_equals_emulated_shards(tmp_path):
 
 @pytest.mark.parametrize("world", [4, 8])
 def test_bench_strong_scaling_cpu_rehearsal(world):
-    """bench.py --scaling strong: one day, documents nnz-balanced over the ranks (oni-lda-c's one
-    model.dat over MPI ranks), value aggregated over all ranks."""
+    """bench.py --scaling strong: one day, its documents sharded over the ranks (chain-aware,
+    dist.engine_bounds: oni-lda-c's one model.dat over MPI ranks), value aggregated over all ranks."""
     r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(world),
                         "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "bench.py", "--gpus",
                         str(world), "--steps", "1", "--warmup", "1", "--events", "3000", "--device", "cpu",
-                        "--scaling", "strong", "--converge", "0", "--e2e", "0"],
+                        "--scaling", "strong", "--converge", "0", "--e2e", "0", "--e2e-cold", "0"],
                        cwd=ROOT, capture_output=True, text=True, timeout=900,
                        env=dict(os.environ, OMP_NUM_THREADS="1"))
     assert r.returncode == 0, r.stderr[-3000:]

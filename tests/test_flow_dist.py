@@ -77,13 +77,13 @@ def test_sharded_featurization_equals_single_process(flow_input, world):
     for r, o in out:
         assert isinstance(o, dict), o
     assert sum(o["rows"] for _, o in out) == ref["rows"]          # the byte ranges partition the rows
-    from oni_ml_amd.parallel.dist import shard_bounds
+    from oni_ml_amd.parallel.dist import engine_bounds
     rptr = np.asarray(ref["ptr"])
-    want_bounds = [b[0] for b in shard_bounds(rptr, world)] + [len(rptr) - 1]
+    want_bounds = [b[0] for b in engine_bounds(rptr, world)] + [len(rptr) - 1]
     for r, o in out:
         for k in ("cuts", "ports", "words"):
             assert o[k] == ref[k], (r, k)
-        # each rank holds exactly its nnz-balanced shard of the one-process corpus
+        # each rank holds exactly its engine shard (engine_bounds) of the one-process corpus
         assert o["bounds"] == want_bounds and o["D"] == len(rptr) - 1 and o["nnz"] == rptr[-1]
         d0, d1 = o["doc_range"]
         assert (d0, d1) == (want_bounds[r], want_bounds[r + 1])

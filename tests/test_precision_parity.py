@@ -2,9 +2,7 @@
 
 CPU: the two fp64 engines (PyTorch Jacobi, literal lda-c Gauss-Seidel) on a small synthetic day; the
 harness must report the pairwise metrics in range and write both outputs.
-GPU: the fp64 HIP engine against the C++ engine with the same block schedule, and the fp32 HIP engine
-against the fp64 Jacobi engine (same update schedule), to the tolerances the README quotes for the
-headline corpus (loosened for the small corpus)."""
+GPU: the fp64 HIP engine against the C++ engine with the same block schedule."""
 import json
 import os
 import subprocess
@@ -57,13 +55,3 @@ def test_fp64_hip_engine_tracks_block_oracle(tmp_path):
     assert p["alpha_rel_diff"] < 1e-7
     assert p["theta_doc_argmax_agree"] > 0.999
     assert p["lowest_0p1pct_overlap"] > 0.99
-
-
-@pytest.mark.gpu
-@pytest.mark.experimental
-def test_fp32_hip_engine_tracks_fp64_jacobi(tmp_path):
-    p = _run(tmp_path, "hip32,torch", 50000)["pairs"]["hip32 vs torch"]
-    assert p["likelihood_rel_diff_max"] < 1e-5
-    assert p["alpha_rel_diff"] < 1e-3
-    assert p["theta_doc_argmax_agree"] > 0.99
-    assert p["score_spearman"] > 0.999
