@@ -200,6 +200,7 @@ def _e2e_cold(args, ctx, tmp):
         torch.cuda.empty_cache()     # this process's cached blocks back to the device for the child
     ctx.barrier()
     t0 = time.perf_counter()
+    env["ONI_T_SPAWN"] = repr(time.time())
     r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=args.e2e_timeout)
     wall = time.perf_counter() - t0
     if r.returncode != 0:
@@ -215,6 +216,7 @@ def _e2e_cold(args, ctx, tmp):
             out["e2e_cold_inprocess_wall_s"] = round(float(sm.get("wall_seconds", 0.0)), 3)
             out["e2e_cold_startup_s"] = round(wall - float(sm.get("wall_seconds", 0.0)), 3)
             out["e2e_cold_flagged"] = sm.get("scored")
+            out["e2e_cold_startup_marks"] = sm.get("startup_marks")
         except (OSError, ValueError):
             pass
     return out

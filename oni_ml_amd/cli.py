@@ -25,6 +25,18 @@ import subprocess
 import sys
 import time
 
+# wall-clock marks (time.time()) of the process's start-up: `python -m oni_ml_amd` records "main" before its
+# first import; ml_ops adds the rest.  ONI_T_SPAWN (set by a parent that launches this process, e.g. bench.py's
+# cold run) is the spawn time, so interpreter start-up is measured too (startup_marks in run_summary.json).
+MARKS = {}
+
+
+def startup_marks() -> dict:
+    """Seconds from the spawn (ONI_T_SPAWN, else "main") to each recorded mark."""
+    t0 = float(os.environ.get("ONI_T_SPAWN", MARKS.get("main", 0.0)) or 0.0)
+    return {k: round(v - t0, 4) for k, v in sorted(MARKS.items(), key=lambda kv: kv[1])} if t0 else {}
+
+
 SYNTAX = """ml_ops.sh syntax error
 Please run ml_ops.sh again with the correct syntax:
 ./ml_ops.sh YYYYMMDD TYPE [TOL]
@@ -102,11 +114,18 @@ def cmd_ml_ops(argv):
     if len(a.fdate) != 8 or not a.dsource:
         print(SYNTAX)
         return 1
+    import torch  # noqa: F401  (first: its import time is a start-up mark of its own)
+    MARKS["torch_imported"] = time.time()
     from . import config as CFG
     from .models.lda.settings import LDASettings
     from .parallel import dist as D
+    MARKS["package_imported"] = time.time()
 
     ctx = D.init_from_env(expected_world=a.gpus if a.gpus > 1 else None)
+    if ctx.device.type == "cuda":
+        import torch
+        torch.zeros(1, device=ctx.device)     # HIP runtime + context (the first device call)
+    MARKS["device_ready"] = time.time()
     cfg = CFG.resolve(a.fdate, a.dsource, tol=float(a.tol) if a.tol is not None else None, conf_path=a.conf,
                       lpath=a.lpath, flow_path=a.flow_path, dns_path=a.dns_path, top1m=a.top1m, topics=a.topics,
                       alpha=a.alpha, dupfactor=a.dupfactor, gpus=ctx.world_size, backend=a.backend, compat=a.compat,
@@ -128,13 +147,16 @@ def cmd_ml_ops(argv):
             clean_workdir(cfg.lpath)
         lock = RunLock(os.path.join(cfg.lpath, ".lock")).__enter__()
     ctx.barrier()
+    MARKS["pipeline_start"] = time.time()
     try:
         summary = run(cfg, dist=ctx if ctx.active else None, device=ctx.device, log=log)
     finally:
         if lock is not None:
             lock.__exit__(None, None, None)
+    MARKS["pipeline_end"] = time.time()
     if ctx.rank == 0:
         summary["wall_seconds"] = time.perf_counter() - t0
+        summary["startup_marks"] = startup_marks()
         with open(os.path.join(cfg.lpath, "run_summary.json"), "w") as f:
             json.dump(summary, f, indent=1, default=str)
         log(json.dumps(summary, default=str))
@@ -318,6 +340,15 @@ def main(argv=None):
     if not argv or argv[0] not in COMMANDS:
         print(__doc__)
         return 1
+    prof = os.environ.get("ONI_CPROFILE")
+    if prof:
+        # host profile of a whole command (cold-start analysis, scripts/cold_start.py)
+        import cProfile
+        pr = cProfile.Profile()
+        try:
+            return pr.runcall(COMMANDS[argv[0]], argv[1:])
+        finally:
+            pr.dump_stats(prof)
     return COMMANDS[argv[0]](argv[1:])
 
 

@@ -40,6 +40,8 @@ def main():
     ap.add_argument("--only", default=None)
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--phases", action="store_true", help="phase timer of the longest document of each team bucket")
+    ap.add_argument("--first", type=int, default=0,
+                    help="team buckets: only their FIRST longest documents (e.g. 1: the longest document alone)")
     ap.add_argument("--prefixes", default="", help="also time the team8 bucket on its N longest documents, e.g. 1,2,8")
     a = ap.parse_args()
     from oni_ml_amd.models.lda.em import LDAEngine
@@ -99,6 +101,12 @@ def main():
             continue
         o = order.cpu().numpy()
         o = o[o >= 0]   # XCD placement gaps
+        if a.first and var in (H.GS_TEAM1, H.GS_TEAM4, H.GS_TEAM8):
+            o = o[:a.first]
+            keep = eng._stages.pop(id(order), None)
+            order = torch.from_numpy(o.astype(np.int32)).to(order.device)
+            if keep is not None:
+                eng._stages[id(order)] = H.GSStage(order, c.doc_ptr, eng.KS, order.device)
         L = lens[o]
         ms = timed(lambda: launch(var, order), a.reps)
         it = its[o]

@@ -1,0 +1,116 @@
+#!/usr/bin/env python
+"""Where a cold `ml_ops` process spends its time (verdict r3 item 2: the cold ml_ops wall-clock).
+
+Runs `python -m oni_ml_amd ml_ops 20160122 flow TOL` as fresh child processes on a synthetic day, as
+bench.py's cold leg does (ml_ops.sh times each stage as a fresh process: ml_ops.sh:57,67,80,84,108):
+
+  1. REPS plain runs: spawn -> exit wall, the start-up marks (interpreter, `import torch`, package,
+     HIP context, pipeline start / end; cli.startup_marks) and the stage seconds;
+  2. one run under `-X importtime`: the slowest imports (cumulative);
+  3. one run under cProfile (ONI_CPROFILE): the host functions with the most cumulative time.
+
+  python scripts/cold_start.py [--events 1000000] [--reps 3] [--md out.md] [--json out.json]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import pstats
+import shutil
+import subprocess
+import sys
+import tempfile
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def _child(tmp, tag, tol, extra_env=None, pyflags=()):
+    lpath = os.path.join(tmp, tag)
+    env = dict(os.environ, PYTHONPATH=ROOT, **(extra_env or {}))
+    for k in ("FLOW_PATH", "LPATH", "TOL"):
+        env.pop(k, None)
+    cmd = [sys.executable, *pyflags, "-m", "oni_ml_amd", "ml_ops", "20160122", "flow", repr(tol), "--lpath", lpath,
+           "--flow-path", os.path.join(tmp, "in"), "--conf", os.path.join(tmp, "none.conf"), "--quiet"]
+    env["ONI_T_SPAWN"] = repr(time.time())
+    t0 = time.perf_counter()
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
+    wall = time.perf_counter() - t0
+    if r.returncode != 0:
+        raise RuntimeError(f"{tag}: rc {r.returncode}\n{r.stderr[-3000:]}")
+    with open(os.path.join(lpath, "run_summary.json")) as f:
+        sm = json.load(f)
+    return wall, sm, r.stderr
+
+
+def _importtime(stderr, top):
+    rows = []
+    for line in stderr.splitlines():
+        if not line.startswith("import time:") or "|" not in line:
+            continue
+        parts = line[len("import time:"):].split("|")
+        try:
+            rows.append((int(parts[1]), int(parts[0]), parts[2].rstrip()))
+        except ValueError:
+            continue
+    rows.sort(reverse=True)
+    # top-level packages only (the cumulative time of nested ones is inside their parent's)
+    out = [(c, s, n) for c, s, n in rows if not n.startswith("    ")][:top]
+    return [dict(module=n.strip(), cumulative_ms=round(c / 1e3, 1), self_ms=round(s / 1e3, 1)) for c, s, n in out]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--events", type=int, default=1_000_000)
+    ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--tol", type=float, default=1e-5)
+    ap.add_argument("--md")
+    ap.add_argument("--json")
+    a = ap.parse_args()
+    from oni_ml_amd.synth.flow import generate_flow_day
+    tmp = tempfile.mkdtemp(prefix="oni_cold_")
+    try:
+        generate_flow_day(os.path.join(tmp, "in/"), events=a.events, seed=7)
+        runs = []
+        for i in range(a.reps):
+            wall, sm, _ = _child(tmp, f"plain{i}", a.tol)
+            runs.append(dict(wall_s=round(wall, 3), inprocess_s=round(sm["wall_seconds"], 3),
+                             marks=sm.get("startup_marks"), stages={k: round(v, 3) for k, v in sm["stage_seconds"].items()},
+                             flagged=sm.get("scored")))
+            print(json.dumps(runs[-1]), flush=True)
+        _, _, err = _child(tmp, "importtime", a.tol, pyflags=("-X", "importtime"))
+        imports = _importtime(err, 15)
+        prof = os.path.join(tmp, "cold.prof")
+        _child(tmp, "cprofile", a.tol, extra_env=dict(ONI_CPROFILE=prof))
+        st = pstats.Stats(prof)
+        st.sort_stats("cumulative")
+        fn = []
+        for (f, line, name), (cc, nc, tt, ct, callers) in sorted(st.stats.items(), key=lambda kv: -kv[1][3])[:40]:
+            fn.append(dict(function=f"{os.path.relpath(f, ROOT) if f.startswith(ROOT) else os.path.basename(f)}:{line}({name})",
+                           cumulative_s=round(ct, 4), self_s=round(tt, 4), calls=nc))
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
+    rec = dict(events=a.events, runs=runs, imports=imports, cprofile=fn)
+    if a.json:
+        with open(a.json, "w") as f:
+            json.dump(rec, f, indent=1)
+    if a.md:
+        L = [f"# Cold `ml_ops` process, 1-day flow ({a.events} events)", "",
+             "| run | spawn -> exit s | in-process s | start-up marks (s after spawn) | stages s | flagged |",
+             "|---|---|---|---|---|---|"]
+        for i, r in enumerate(runs):
+            L.append(f"| {i} | {r['wall_s']} | {r['inprocess_s']} | {r['marks']} | {r['stages']} | {r['flagged']} |")
+        L += ["", "## Slowest imports (-X importtime, cumulative)", "", "| module | cumulative ms | self ms |",
+              "|---|---|---|"]
+        L += [f"| `{m['module']}` | {m['cumulative_ms']} | {m['self_ms']} |" for m in imports]
+        L += ["", "## Host profile of the whole command (cProfile, cumulative)", "",
+              "| function | cumulative s | self s | calls |", "|---|---|---|---|"]
+        L += [f"| `{x['function']}` | {x['cumulative_s']} | {x['self_s']} | {x['calls']} |" for x in fn]
+        with open(a.md, "w") as f:
+            f.write("\n".join(L) + "\n")
+
+
+if __name__ == "__main__":
+    main()

@@ -13,7 +13,8 @@
 #   strong    scripts/strong_emulated.py (per-shard EM times for N = 2/4/8)
 #   parity    scripts/precision_parity.py $PARITY_ARGS
 #   micro     build + run scripts/micro/*.hip (fp64 latency / throughput probes)
-#   pmc       one rocprofv3 --pmc pass ($PMC = counter list) over a short bench
+#   pmc       rocprofv3 --pmc passes ($PMC = counter groups separated by ';', PMC_CMD = program, default a short bench)
+#   cold      scripts/cold_start.py: where a cold ml_ops process spends its time
 #   nccl      the one-rank RCCL test (tests/test_gpu_dist.py -k nccl)
 #   ab        scripts/ab_env.sh $AB_ROUNDS $AB_VARIANTS (space-separated env settings, one per variant)
 #   ranks     scripts/pipeline_ranks.py $RANKS_ARGS (per-rank stage seconds of the sharded ml_ops pipeline)
@@ -54,7 +55,7 @@ for s in "$@"; do
       rm -f "$db"; head -14 "$OUT/prof_summary.md" ;;
     phases)
       timeout -k 10 300 python -u scripts/bench_gs64.py --phases ${PHASES_ARGS:-} > "$OUT/phases.log" 2>&1 || { tail -20 "$OUT/phases.log"; stop phases 1; }
-      grep '^{' "$OUT/phases.log" | cut -c1-300 ;;
+      grep '^{' "$OUT/phases.log" | cut -c1-600 ;;
     configs)
       OUTDIR="$OUT" timeout -k 10 1000 bash scripts/bench_configs.sh || stop configs $? ;;
     strong)
@@ -73,12 +74,21 @@ for s in "$@"; do
         cat "$OUT/$(basename "$f" .hip).txt"
       done ;;
     pmc)
-      rm -rf "$OUT/pmc"; mkdir -p "$OUT/pmc"
-      timeout -s KILL 120 rocprofv3 --pmc ${PMC:?set PMC} -d "$OUT/pmc" -o pmc -- python3 bench.py \
-        ${PMC_ARGS:---steps 3 --warmup 1 --converge 0 --e2e 0 --e2e-cold 0} > "$OUT/pmc/log.txt" 2>&1 || stop pmc $?
-      db=$(find "$OUT/pmc" -name "*.db" | head -1)
-      python scripts/pmc_summary.py "$db" ${PMC_MATCH:+--match "$PMC_MATCH"} --md "$OUT/pmc_summary.md" > /dev/null
-      rm -f "$db"; head -30 "$OUT/pmc_summary.md" ;;
+      # PMC: counter groups separated by ';' (one rocprofv3 pass each); PMC_CMD: the profiled program
+      i=0
+      IFS=';' read -ra groups <<< "${PMC:?set PMC}"
+      for g in "${groups[@]}"; do
+        i=$((i + 1)); rm -rf "$OUT/pmc$i"; mkdir -p "$OUT/pmc$i"
+        timeout -s KILL 120 rocprofv3 --pmc $g -d "$OUT/pmc$i" -o pmc -- python3 ${PMC_CMD:-bench.py ${PMC_ARGS:---steps 3 --warmup 1 --converge 0 --e2e 0 --e2e-cold 0}} \
+          > "$OUT/pmc$i/log.txt" 2>&1 || stop pmc $?
+        db=$(find "$OUT/pmc$i" -name "*.db" | head -1)
+        python scripts/pmc_summary.py "$db" ${PMC_MATCH:+--match "$PMC_MATCH"} --md "$OUT/pmc_summary$i.md" > /dev/null
+        rm -f "$db"; head -12 "$OUT/pmc_summary$i.md"
+      done ;;
+    cold)
+      timeout -k 10 600 python -u scripts/cold_start.py ${COLD_ARGS:-} --md "$OUT/cold.md" --json "$OUT/cold.json" \
+        > "$OUT/cold.log" 2>&1 || { tail -30 "$OUT/cold.log"; stop cold 1; }
+      head -12 "$OUT/cold.md" ;;
     ab)
       timeout -k 10 1000 bash scripts/ab_env.sh ${AB_ROUNDS:-3} ${AB_VARIANTS:?set AB_VARIANTS} -- ${AB_ARGS:---steps 20 --warmup 5} \
         > "$OUT/ab.log" 2>&1 || { tail -20 "$OUT/ab.log"; stop ab 1; }

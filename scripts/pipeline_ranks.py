@@ -9,6 +9,8 @@ on every rank, and rank 0's serial share: the seconds rank 0 spends in stages be
 other rank, over the wall.
 
   python scripts/pipeline_ranks.py --events 1000000 --ranks 1,4 --md out.md --json out.json
+  BASELINE config 5 (a month, K = 100) on 8 ranks sharing one GPU, a TOL that flags events:
+  python scripts/pipeline_ranks.py --events 100000000 --days 30 --topics 100 --compat fixed --tol 1e-9 --ranks 8
 """
 import argparse
 import json
@@ -46,6 +48,12 @@ def main():
     ap.add_argument("--md")
     ap.add_argument("--json")
     ap.add_argument("--timeout", type=int, default=900)
+    ap.add_argument("--days", type=int, default=1, help="flow: part files (one per day) of the generated input")
+    ap.add_argument("--topics", type=int, default=20)
+    ap.add_argument("--compat", default=None, help="strict | fixed (default: strict at K = 20, else fixed)")
+    ap.add_argument("--threads", type=int, default=8, help="native threads per rank")
+    ap.add_argument("--cphi-gb", default=None, help="per-rank HBM budget of the c.phi rows")
+    ap.add_argument("--no-word-assignments", action="store_true")
     a = ap.parse_args()
     tol = a.tol or ("1e-5" if a.source == "flow" else "1e-4")
     tmp = tempfile.mkdtemp(prefix="oni_ranks_")
@@ -53,7 +61,11 @@ def main():
     try:
         if a.source == "flow":
             from oni_ml_amd.synth.flow import generate_flow_day
-            generate_flow_day(os.path.join(tmp, "in/"), events=a.events, seed=7)
+            tg = time.perf_counter()
+            generate_flow_day(os.path.join(tmp, "in/"), events=a.events, seed=7,
+                              chunk_events=-(-a.events // a.days) if a.days > 1 else 0, threads=16)
+            out["generate_s"] = round(time.perf_counter() - tg, 2)
+            print(json.dumps(dict(generated=a.events, seconds=out["generate_s"])), flush=True)
             inp = ["--flow-path", os.path.join(tmp, "in")]
         else:
             from oni_ml_amd.synth.dns import generate_dns_day
@@ -63,8 +75,14 @@ def main():
             inp = ["--dns-path", g["dns_path"], "--top1m", g["top1m"]]
         for n in [int(x) for x in a.ranks.split(",")]:
             lp = os.path.join(tmp, f"ml{n}")
+            compat = a.compat or ("strict" if a.topics == 20 else "fixed")
             cli = ["-m", "oni_ml_amd.cli", "ml_ops", "20160122", a.source, tol, "--lpath", lp, "--gpus", str(n),
-                   "--conf", "/nonexistent", "--quiet", "--backend", a.lda_backend] + inp
+                   "--conf", "/nonexistent", "--quiet", "--backend", a.lda_backend, "--topics", str(a.topics),
+                   "--compat", compat, "--threads", str(a.threads)] + inp
+            if a.cphi_gb:
+                cli += ["--cphi-gb", str(a.cphi_gb)]
+            if a.no_word_assignments:
+                cli += ["--no-word-assignments"]
             cmd = [sys.executable] + (cli if n == 1 else
                                       ["-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n),
                                        "--master-addr", "127.0.0.1", "--master-port", str(_port())] + cli)
@@ -90,6 +108,7 @@ def main():
             for s in STAGES[a.source]:
                 others = [p.get(s, 0.0) for p in per_rank[1:]]
                 serial += max(0.0, per_rank[0].get(s, 0.0) - (max(others) if others else 0.0))
+            shutil.rmtree(lp, ignore_errors=True)       # (config 5 writes ~50 GB of text per run)
             run = dict(ranks=n, process_wall_s=round(wall, 3), pipeline_wall_s=round(pw, 3),
                        flagged=summ.get("scored"), corpus=summ.get("corpus"),
                        em_iterations=summ.get("lda", {}).get("em_iterations"),
