@@ -129,7 +129,7 @@ def _format_table(names, values, read_back):
 
 
 def export_sharded(ctx, doc_names, gamma, word_names, log_beta, doc_path, word_path, strict=True,
-                   read_back: bool = False, gather: bool = True):
+                   read_back: bool = False, gather: bool = True, num_words: int = None):
     """``export`` with every rank writing its own rows of both files (the row-sharded lda_post stage).
 
     ``doc_names`` / ``gamma``: this rank's documents (its contiguous block of doc.dat, in rank order);
@@ -138,8 +138,10 @@ def export_sharded(ctx, doc_names, gamma, word_names, log_beta, doc_path, word_p
     [V r / N, V (r + 1) / N).  lda_post.py normalises each topic by Python's sequential sum over all V
     words (lda_post.py:88-96): here rank r continues the running sums of ranks < r
     (``shardio.chain``), so the totals -- and every byte of both files -- equal the one-process
-    export.  ``gather``: also return the whole θ / φ read-back tables on every rank (the scorers'
-    broadcast model, flow_post_lda.scala:112-123)."""
+    export.  ``gather``: return the whole θ / φ read-back tables on every rank (the scorers' broadcast
+    model, flow_post_lda.scala:112-123; the resume path); otherwise this rank's rows and the names of
+    its vocabulary slice.  ``word_names``: every word, or (``gather=False``) only the slice
+    [V r / N, V (r + 1) / N) with ``num_words`` = V."""
     from ..parallel import shardio as SIO
     N, r = SIO.world(ctx), SIO.rank(ctx)
     check_strict_k(log_beta.shape[0], strict)
@@ -156,14 +158,19 @@ def export_sharded(ctx, doc_names, gamma, word_names, log_beta, doc_path, word_p
     total = SIO.chain(ctx, lambda carry: np.cumsum(np.concatenate([carry[:, None], raw], 1), 1)[:, -1],
                       np.zeros(K, np.float64))
     phi = np.ascontiguousarray((raw / total[:, None]).T)
-    wn = list(word_names[v0:v1])
+    wn = list(word_names[v0:v1]) if num_words is None else list(word_names)
+    if len(wn) != v1 - v0:
+        raise ValueError(f"word names: {len(wn)} for the vocabulary slice [{v0}, {v1})")
     wnames = truncate_s20(wn) if strict else wn
     text, ph_b = _format_table(wnames, phi, read_back)
     SIO.write_segments(ctx, word_path, [text])
     th, ph = (th_b, ph_b) if read_back else (theta, phi)
-    if gather:
-        th = np.concatenate(SIO.allgather_array(ctx, np.ascontiguousarray(th)))
-        ph = np.concatenate(SIO.allgather_array(ctx, np.ascontiguousarray(ph)))
+    if not gather:
+        # this rank's rows only: its documents' θ, its vocabulary slice's φ and the slice's names as
+        # written (pipeline/common.py ShardedTables fetches the rows a scorer needs from their ranks)
+        return th, ph, wnames
+    th = np.concatenate(SIO.allgather_array(ctx, np.ascontiguousarray(th)))
+    ph = np.concatenate(SIO.allgather_array(ctx, np.ascontiguousarray(ph)))
     all_names = truncate_s20(word_names) if strict else list(word_names)
     return th, ph, all_names
 

@@ -6,8 +6,10 @@ on the GPU box, host tensors under gloo) -- no pickled objects:
 
 * ``allgather_array`` / ``alltoallv``: variable-length arrays of any dtype (as raw bytes);
 * ``first_appearance``: a global string dictionary in first-appearance order (rank order, then each
-  rank's local order), merged as fixed-width integer rows with ``torch.unique(dim=0)`` -- no
-  Python loop over names (the Spark job's collect + driver-side dict, flow_pre_lda.scala);
+  rank's local order), hash-partitioned over the ranks as fixed-width integer rows (the Spark job's
+  distinct + zipWithIndex, flow_pre_lda.scala) and kept in id-range slices (``DistNameTable``);
+* ``fetch_rows`` / ``range_put``: rows of a table held in contiguous row ranges, fetched by the ranks
+  that need them (the scorers' model rows, the doc row of an ip) instead of replicated;
 * ``write_segments``: every rank writes its own formatted rows at its byte offset of the shared
   output file (the reference's ``part-*`` files concatenated by ``cat`` in part order,
   ml_ops.sh:59-62,110-115);
@@ -207,32 +209,237 @@ def names_to_bytes(names: Sequence[str]):
     return np.frombuffer(b"".join(enc), np.uint8), off
 
 
-def first_appearance(ctx, data: np.ndarray, off: np.ndarray) -> Tuple[NameTable, np.ndarray]:
-    """Global dictionary of every rank's local dictionary (each in local first-appearance order):
-    ids in order of first appearance over the ranks' rows in rank order -- the single-process
-    dictionary of the concatenated input.  Returns (global names, local id -> global id)."""
-    lens = np.diff(np.asarray(off, np.int64))
-    w = allreduce_max_int(ctx, int(lens.max()) if lens.size else 0)
+def range_starts(total: int, n: int) -> List[int]:
+    """Range partition of ids [0, total) over n ranks: rank s owns [starts[s], starts[s + 1])."""
+    return [int(total) * s // n for s in range(n + 1)]
+
+
+def fetch_rows(ctx, local: np.ndarray, starts: Sequence[int], query) -> np.ndarray:
+    """Rows of a table held in contiguous row ranges (rank s keeps global rows [starts[s], starts[s + 1])
+    as ``local``), for the global ids ``query`` (any order, repeats allowed; -1: a zero row).  Collective:
+    every rank asks only for the rows it needs (two ``alltoallv``), nothing is replicated."""
+    local = np.ascontiguousarray(local)
+    q = np.asarray(query, np.int64).reshape(-1)
+    valid = q >= 0
+    uq, inv = np.unique(q[valid], return_inverse=True)
+    N, r = world(ctx), rank(ctx)
+    st = np.asarray(starts, np.int64)
+    if not _active(ctx):
+        got = local[uq - st[0]]
+    else:
+        owner = np.searchsorted(st, uq, side="right") - 1
+        cuts = np.searchsorted(owner, np.arange(N + 1), side="left")
+        req = alltoallv(ctx, [uq[cuts[d]:cuts[d + 1]] for d in range(N)])
+        if any(x.size and (x.min() < st[r] or x.max() >= st[r + 1]) for x in req):
+            raise IndexError("fetch_rows: a request outside this rank's rows")
+        resp = alltoallv(ctx, [local[x - st[r]] for x in req])
+        got = np.concatenate(resp) if resp else local[:0]
+    out = np.zeros((q.size,) + local.shape[1:], local.dtype)
+    if uq.size:
+        out[valid] = got[inv]
+    return out
+
+
+def range_put(ctx, ids, rows: np.ndarray, total: int, fill=0) -> np.ndarray:
+    """(id, row) pairs of every rank -> the rank owning each id's range (``range_starts(total, N)``);
+    returns this rank's slice [starts[r], starts[r + 1]) (ids never sent keep ``fill``)."""
+    ids = np.asarray(ids, np.int64).reshape(-1)
+    rows = np.ascontiguousarray(rows)
+    N, r = world(ctx), rank(ctx)
+    st = range_starts(total, N)
+    o = np.argsort(ids, kind="stable")
+    ids_s, rows_s = ids[o], rows[o]
+    cuts = np.searchsorted(ids_s, np.asarray(st, np.int64), side="left")
+    if _active(ctx):
+        rid = np.concatenate(alltoallv(ctx, [ids_s[cuts[d]:cuts[d + 1]] for d in range(N)]))
+        rrow = np.concatenate(alltoallv(ctx, [rows_s[cuts[d]:cuts[d + 1]] for d in range(N)]))
+    else:
+        rid, rrow = ids_s, rows_s
+    lo, hi = st[r], st[r + 1]
+    out = np.full((hi - lo,) + rows.shape[1:], fill, rows.dtype)
+    if rid.size:
+        out[rid - lo] = rrow
+    return out
+
+
+class DistNameTable:
+    """A global dictionary (ids 0 .. total - 1) held in range slices: rank r keeps the names of ids
+    [total r / N, total (r + 1) / N) as fixed-width byte rows.  ``take`` is collective (``fetch_rows``):
+    a rank receives only the names it asks for."""
+
+    def __init__(self, ctx, mat: np.ndarray, lens: np.ndarray, total: int):
+        self.ctx, self.total = ctx, int(total)
+        self.mat = np.ascontiguousarray(mat, np.uint8)
+        self.lens = np.ascontiguousarray(lens, np.int64)
+        self.starts = range_starts(self.total, world(ctx))
+
+    def __len__(self):
+        return self.total
+
+    def all(self) -> List[str]:
+        """Every name on every rank (collective; for small dictionaries, e.g. DNS query types)."""
+        return self.take(np.arange(self.total, dtype=np.int64))
+
+    def take(self, ids) -> List[str]:
+        ids = np.asarray(ids, np.int64).reshape(-1)
+        rows = fetch_rows(self.ctx, np.concatenate([self.mat.view(np.int64).reshape(self.mat.shape[0], -1),
+                                                    self.lens[:, None]], 1), self.starts, ids)
+        W = self.mat.shape[1]
+        m = np.ascontiguousarray(rows[:, :W // 8]).view(np.uint8).reshape(ids.size, W)
+        ln = rows[:, W // 8]
+        out = []
+        for i in range(ids.size):
+            out.append(bytes(m[i, :ln[i]]).decode("utf-8", errors="surrogateescape"))
+        return out
+
+
+class DistDict:
+    """name -> int64 value over the ranks, hash-partitioned by name: rank hash(name) mod N keeps the
+    entries of its names.  Where several entries share a name the largest value wins -- the map the
+    Scala scorers build with ``collectAsMap`` over word_results.csv rows (later rows win,
+    flow_post_lda.scala:107-123).  Construction and ``lookup`` are collective; nothing is replicated."""
+
+    def __init__(self, ctx, names: Sequence[str], values):
+        self.ctx = ctx
+        N = world(ctx)
+        data, off = names_to_bytes(names)
+        lens = np.diff(off)
+        self.W = max(8, -(-allreduce_max_int(ctx, int(lens.max()) if lens.size else 0) // 8) * 8)
+        key = self._key(data, off)
+        vals = np.asarray(values, np.int64).reshape(-1, 1)
+        owner = self._owner(key)
+        o = np.argsort(owner, kind="stable")
+        cuts = np.searchsorted(owner[o], np.arange(N + 1), side="left")
+        send = np.concatenate([key, vals], 1)[o]
+        recv = alltoallv(ctx, [send[cuts[d]:cuts[d + 1]] for d in range(N)]) if N > 1 else [send]
+        allr = np.concatenate(recv) if recv else send[:0]
+        if allr.shape[0]:
+            u, inv = torch.unique(torch.from_numpy(np.ascontiguousarray(allr[:, :-1])), dim=0, return_inverse=True)
+            v = torch.full((u.shape[0],), -1, dtype=torch.int64).scatter_reduce_(
+                0, inv, torch.from_numpy(np.ascontiguousarray(allr[:, -1])), reduce="amax")
+            self.keys, self.vals = u.numpy(), v.numpy()
+        else:
+            self.keys, self.vals = allr[:, :-1], np.zeros(0, np.int64)
+
+    def _key(self, data, off) -> np.ndarray:
+        off = np.asarray(off, np.int64)
+        lens = np.diff(off)
+        mat = pack_names(data, off, self.W)
+        return np.concatenate([mat.view(np.int64).reshape(lens.size, self.W // 8), lens[:, None]], 1)
+
+    def _owner(self, key) -> np.ndarray:
+        N = world(self.ctx)
+        return (_row_hash(key) % np.uint64(N)).astype(np.int64) if N > 1 else np.zeros(key.shape[0], np.int64)
+
+    def lookup(self, names: Sequence[str]) -> np.ndarray:
+        """Value of every name (-1: absent).  Collective."""
+        N = world(self.ctx)
+        data, off = names_to_bytes(names)
+        lens = np.diff(off)
+        fits = lens <= self.W                    # longer names cannot be keys
+        idx = np.flatnonzero(fits)
+        sub_off = np.concatenate([[0], np.cumsum(lens[idx])]).astype(np.int64)
+        raw = np.frombuffer(memoryview(data), np.uint8) if len(data) else np.zeros(0, np.uint8)
+        sub = raw if fits.all() else raw[np.repeat(fits, lens)]
+        key = self._key(sub, sub_off)
+        owner = self._owner(key)
+        o = np.argsort(owner, kind="stable")
+        cuts = np.searchsorted(owner[o], np.arange(N + 1), side="left")
+        q = key[o]
+        recv = alltoallv(self.ctx, [q[cuts[d]:cuts[d + 1]] for d in range(N)]) if N > 1 else [q]
+        rsz = [x.shape[0] for x in recv]
+        allq = np.concatenate(recv) if recv else q[:0]
+        ans = np.full(allq.shape[0], -1, np.int64)
+        if allq.shape[0] and self.keys.shape[0]:
+            both = torch.from_numpy(np.ascontiguousarray(np.concatenate([self.keys, allq])))
+            _, inv = torch.unique(both, dim=0, return_inverse=True)
+            inv = inv.numpy()
+            val_u = np.full(int(inv.max()) + 1, -1, np.int64)
+            val_u[inv[:self.keys.shape[0]]] = self.vals
+            ans = val_u[inv[self.keys.shape[0]:]]
+        rc = np.concatenate([[0], np.cumsum(rsz)])
+        back = alltoallv(self.ctx, [ans[rc[d]:rc[d + 1]] for d in range(N)]) if N > 1 else [ans]
+        got = np.empty(idx.size, np.int64)
+        got[o] = np.concatenate(back) if back else np.zeros(0, np.int64)
+        out = np.full(lens.size, -1, np.int64)
+        out[idx] = got
+        return out
+
+
+def _row_hash(rows64: np.ndarray) -> np.ndarray:
+    """A 64-bit mix of each int64 row (the owner of a name in the hash-partitioned dictionary)."""
+    h = np.zeros(rows64.shape[0], np.uint64)
+    with np.errstate(over="ignore"):
+        for j in range(rows64.shape[1]):
+            h = (h ^ rows64[:, j].view(np.uint64)) * np.uint64(0x9E3779B97F4A7C15)
+            h ^= h >> np.uint64(29)
+    return h
+
+
+def first_appearance(ctx, data: np.ndarray, off: np.ndarray) -> Tuple[DistNameTable, np.ndarray]:
+    """Global dictionary of every rank's local dictionary (each in local first-appearance order): ids in
+    order of first appearance over the ranks' rows in rank order -- the single-process dictionary of
+    the concatenated input.  Returns (global names, local id -> global id).
+
+    Hash-partitioned, nothing replicated (the Spark job's distinct + zipWithIndex, not a driver-side
+    collect): every name goes, with its global position (lower ranks' names first, then local order), to
+    the rank owning hash(name); owners merge duplicates keeping the minimum position; each first
+    position goes to the rank whose position range holds it, where a prefix count over the ranks gives
+    its global id; the ids travel back to the owners and on to every sender; the names land in range
+    slices by id (``DistNameTable``).  Rows carry the name length, so names that differ only by
+    trailing NUL bytes stay distinct."""
+    N, r = world(ctx), rank(ctx)
+    off = np.asarray(off, np.int64)
+    lens = np.diff(off)
+    n = lens.size
+    w = allreduce_max_int(ctx, int(lens.max()) if n else 0)
     W = max(8, -(-w // 8) * 8)
     mat = pack_names(data, off, W)
-    parts = allgather_array(ctx, mat)
-    sizes = [p.shape[0] for p in parts]
-    allm = np.concatenate(parts) if len(parts) > 1 else parts[0]
-    n_all = allm.shape[0]
-    if n_all == 0:
-        return NameTable(np.zeros((0, W), np.uint8)), np.zeros(0, np.int64)
-    rows = torch.from_numpy(allm.view(np.int64).reshape(n_all, W // 8))
-    uniq, inv = torch.unique(rows, dim=0, return_inverse=True)
-    first = torch.full((uniq.shape[0],), n_all, dtype=torch.int64).scatter_reduce_(
-        0, inv, torch.arange(n_all, dtype=torch.int64), reduce="amin")
-    order = torch.argsort(first)                       # unique rows by first appearance
-    gid = torch.empty_like(order)
-    gid[order] = torch.arange(order.numel())
-    r = rank(ctx)
-    lo = sum(sizes[:r])
-    local = gid[inv[lo:lo + sizes[r]]].numpy().astype(np.int64)
-    gm = allm[first[order].numpy()]
-    return NameTable(gm), local
+    sizes = allgather_sizes(ctx, n)
+    base = sum(sizes[:r])
+    key = np.concatenate([mat.view(np.int64).reshape(n, W // 8), lens[:, None]], 1)     # [n, W/8 + 1]
+    pos = base + np.arange(n, dtype=np.int64)
+    owner = (_row_hash(key) % np.uint64(N)).astype(np.int64) if N > 1 else np.zeros(n, np.int64)
+    o = np.argsort(owner, kind="stable")
+    cuts = np.searchsorted(owner[o], np.arange(N + 1), side="left")
+    send = np.concatenate([key, pos[:, None]], 1)[o]
+    recv = alltoallv(ctx, [send[cuts[d]:cuts[d + 1]] for d in range(N)]) if N > 1 else [send]
+    rsz = [x.shape[0] for x in recv]
+    allr = np.concatenate(recv) if recv else send[:0]
+    # ---- owner: distinct names, minimum position
+    if allr.shape[0]:
+        uniq, inv = torch.unique(torch.from_numpy(np.ascontiguousarray(allr[:, :-1])), dim=0, return_inverse=True)
+        minpos = torch.full((uniq.shape[0],), np.iinfo(np.int64).max, dtype=torch.int64).scatter_reduce_(
+            0, inv, torch.from_numpy(np.ascontiguousarray(allr[:, -1])), reduce="amin").numpy()
+        uniq, inv = uniq.numpy(), inv.numpy()
+    else:
+        uniq, inv, minpos = allr[:, :-1], np.zeros(0, np.int64), np.zeros(0, np.int64)
+    # ---- global ids: first positions counted in position order, across the ranks' position ranges
+    pstarts = np.concatenate([[0], np.cumsum(sizes)]).astype(np.int64)
+    powner = np.searchsorted(pstarts, minpos, side="right") - 1
+    po = np.argsort(powner, kind="stable")
+    pcuts = np.searchsorted(powner[po], np.arange(N + 1), side="left")
+    firsts = alltoallv(ctx, [minpos[po][pcuts[d]:pcuts[d + 1]] for d in range(N)]) if N > 1 else [minpos]
+    fl = np.concatenate(firsts) if firsts else minpos
+    cnt = allgather_sizes(ctx, fl.size)
+    total = int(sum(cnt))
+    rank_in = np.empty(fl.size, np.int64)
+    rank_in[np.argsort(fl, kind="stable")] = np.arange(fl.size, dtype=np.int64)
+    gid_fl = sum(cnt[:r]) + rank_in
+    fcuts = np.concatenate([[0], np.cumsum([x.size for x in firsts])])
+    back = alltoallv(ctx, [gid_fl[fcuts[d]:fcuts[d + 1]] for d in range(N)]) if N > 1 else [gid_fl]
+    gid_u = np.empty(minpos.size, np.int64)
+    gid_u[po] = np.concatenate(back) if back else np.zeros(0, np.int64)
+    # ---- every sender's names get their ids (same order as sent)
+    gid_rows = gid_u[inv] if inv.size else np.zeros(0, np.int64)
+    rcuts = np.concatenate([[0], np.cumsum(rsz)])
+    mine = alltoallv(ctx, [gid_rows[rcuts[d]:rcuts[d + 1]] for d in range(N)]) if N > 1 else [gid_rows]
+    lmap = np.empty(n, np.int64)
+    lmap[o] = np.concatenate(mine) if mine else np.zeros(0, np.int64)
+    # ---- the names by id range
+    rows = range_put(ctx, gid_u, np.ascontiguousarray(uniq), total) if total else uniq[:0]
+    tab = np.ascontiguousarray(rows[:, :W // 8]).view(np.uint8).reshape(rows.shape[0], W)
+    return DistNameTable(ctx, tab, rows[:, W // 8], total), lmap
 
 
 # ------------------------------------------------------------------------------------ file output

@@ -30,6 +30,58 @@ class ModelTables:
     def word_index(self) -> dict:
         return {n: i for i, n in enumerate(self.word_names)}
 
+    @property
+    def K(self) -> int:
+        return int(self.theta.shape[1])
+
+    def word_rows(self, names: List[str]) -> np.ndarray:
+        """φ row of every word name (-1: not in word_results)."""
+        idx = self.word_index()
+        return np.fromiter((idx.get(n, -1) for n in names), dtype=np.int64, count=len(names))
+
+    def compact(self, doc_rows: np.ndarray, word_rows: np.ndarray):
+        """(θ, φ, doc rows, word rows) the score kernel indexes: the whole tables, rows unchanged."""
+        return self.theta, self.phi, np.asarray(doc_rows, np.int64), np.asarray(word_rows, np.int64)
+
+
+@dataclass
+class ShardedTables:
+    """The scorers' model in the row-sharded pipeline, nothing replicated: θ rows stay with the rank of
+    their documents (global rows [doc_starts[r], doc_starts[r + 1])), φ rows with the rank of their
+    vocabulary slice; the word name -> φ row map is hash-partitioned (``shardio.DistDict``, later rows
+    win as in ``collectAsMap``).  A rank fetches only the θ / φ rows its own events reference
+    (``shardio.fetch_rows``) -- the reference broadcasts the whole model to every executor
+    (flow_post_lda.scala:112-123).  ``word_rows`` and ``compact`` are collective."""
+    ctx: object
+    theta: np.ndarray          # this rank's θ rows
+    doc_starts: List[int]
+    phi: np.ndarray            # this rank's φ rows (vocabulary slice)
+    word_starts: List[int]
+    words: object              # shardio.DistDict: word name as written -> global φ row
+
+    @property
+    def K(self) -> int:
+        return int(self.theta.shape[1])
+
+    def word_rows(self, names: List[str]) -> np.ndarray:
+        return self.words.lookup(names)
+
+    def compact(self, doc_rows: np.ndarray, word_rows: np.ndarray):
+        """(θ rows, φ rows, local doc rows, local word rows): the distinct rows the given global rows
+        reference, fetched from their owners, and the given rows renumbered into them (-1 kept)."""
+        from ..parallel import shardio as SIO
+        out = []
+        for rows, tab, starts in ((doc_rows, self.theta, self.doc_starts), (word_rows, self.phi, self.word_starts)):
+            rows = np.asarray(rows, np.int64)
+            ok = rows >= 0
+            u, inv = np.unique(rows[ok], return_inverse=True)
+            got = SIO.fetch_rows(self.ctx, tab, starts, u)
+            loc = np.full(rows.size, -1, np.int64)
+            loc[ok] = inv
+            out.append((got, loc))
+        (th, dl), (ph, wl) = out
+        return th, ph, dl, wl
+
 
 def write_corpus_files(lpath: str, built: BuiltCorpus, doc_names: List[str], word_names: List[str]):
     ldac.write_words_dat(os.path.join(lpath, "words.dat"), word_names)
@@ -128,12 +180,6 @@ def doc_rows_of(doc_keys, n_keys: int) -> np.ndarray:
     dk = np.asarray(doc_keys, np.int64)
     rows[dk] = np.arange(dk.size, dtype=np.int64)
     return rows
-
-
-def map_names(names: List[str], index: dict, device) -> torch.Tensor:
-    """Name list -> row ids through a {name: row} map (-1 when absent), as a device int64 tensor."""
-    ids = np.fromiter((index.get(n, -1) for n in names), dtype=np.int64, count=len(names))
-    return torch.from_numpy(ids).to(device)
 
 
 def save_json(path: str, obj):

@@ -141,16 +141,19 @@ def score_dns(cfg, tab: FD.DnsTable, top, tables: C.ModelTables, device, log=pri
     wsp = FD.DnsWordSpace(feat.cuts, feat.qpairs)
     uk, inv = torch.unique(feat.word_key, return_inverse=True)
     unames = wsp.decode(uk.cpu().numpy())
-    widx = C.map_names(unames, tables.word_index(), device)[inv]
     if ip_map is not None:
         m = np.asarray(ip_map, np.int64)[:len(feat.ip_names)]
-        didx = torch.from_numpy(m).to(device)[feat.ip]
     else:
-        didx = C.map_names(feat.ip_names, tables.doc_index(), device)[feat.ip]
-    K = tables.theta.shape[1]
+        di = tables.doc_index()
+        m = np.fromiter((di.get(n, -1) for n in feat.ip_names), dtype=np.int64, count=len(feat.ip_names))
+    # the rows these queries reference: the whole tables (one process) or fetched from their ranks
+    th, ph, drow, wrow = tables.compact(m, tables.word_rows(unames))
+    widx = torch.from_numpy(wrow).to(device)[inv]
+    didx = torch.from_numpy(drow).to(device)[feat.ip]
+    K = tables.K
     if cfg.strict and K != 20:
         raise ValueError("compat=strict scores over exactly 20 topics (dns_post_lda.scala:316)")
-    model = S.TopicModel.build(tables.theta, tables.phi, S.default_value("dns", K, cfg.strict), device)
+    model = S.TopicModel.build(th, ph, S.default_value("dns", K, cfg.strict), device)
     sc, _, key, flag = S.score(model, didx, widx, None, None, cfg.tol)
     order = S.rank_flagged(key, flag)
     n = int(order.size)

@@ -185,17 +185,18 @@ def score_flow(cfg, ft: FF.FlowTable, tables: C.ModelTables, device, log=print, 
     uk, inv = torch.unique(both, return_inverse=True)
     uk_np = uk.cpu().numpy()
     unames = ws.decode(uk_np)
-    widx = C.map_names(unames, tables.word_index(), device)[inv]
-    w_src, w_dst = widx[: src.numel()], widx[src.numel():]
     ipn = ft.ip_names
-    if ip_rows is not None:
-        didx = torch.from_numpy(np.asarray(ip_rows, np.int64)).to(device)
-    else:
-        didx = C.map_names(ipn, tables.doc_index(), device)
-    K = tables.theta.shape[1]
+    if ip_rows is None:
+        ip_rows = np.fromiter((tables.doc_index().get(n, -1) for n in ipn), dtype=np.int64, count=len(ipn))
+    # the rows these events reference: the whole tables (one process) or fetched from their ranks
+    th, ph, drow, wrow = tables.compact(ip_rows, tables.word_rows(unames))
+    widx = torch.from_numpy(wrow).to(device)[inv]
+    w_src, w_dst = widx[: src.numel()], widx[src.numel():]
+    didx = torch.from_numpy(drow).to(device)
+    K = tables.K
     if cfg.strict and K != 20:
         raise ValueError("compat=strict scores over exactly 20 topics (flow_post_lda.scala:232)")
-    model = S.TopicModel.build(tables.theta, tables.phi, S.default_value("flow", K, cfg.strict), device)
+    model = S.TopicModel.build(th, ph, S.default_value("flow", K, cfg.strict), device)
     sa, sb, key, flag = S.score(model, didx[feat.sip.long()], w_src, didx[feat.dip.long()], w_dst, cfg.tol)
     order = S.rank_flagged(key, flag)
     n = int(order.size)

@@ -124,7 +124,7 @@ def run_flow(cfg, ctx, device=None, log=print) -> dict:
         with R.stage("lda_pre") as res:
             sc = build_sharded(ctx, sections, len(names), merge=not cfg.strict, device=device)
             del sections
-            doc_names = names.take(sc.doc_keys)
+            doc_names = sc.doc_names = names.take(sc.doc_keys)
             write_corpus_files_sharded(ctx, cfg.lpath, sc, doc_names, ws.decode, cfg.threads)
             if cfg.write_doc_wc:
                 write_doc_wc_sharded(ctx, os.path.join(cfg.lpath, "doc_wc.dat"), sc, names, ws.decode, cfg.threads)
@@ -183,7 +183,7 @@ def run_dns(cfg, ctx, device=None, log=print) -> dict:
         with R.stage("lda_pre") as res:
             sc = build_sharded(ctx, sections, len(names), device=device)
             del sections
-            doc_names = names.take(sc.doc_keys)
+            doc_names = sc.doc_names = names.take(sc.doc_keys)
             write_corpus_files_sharded(ctx, cfg.lpath, sc, doc_names, wsp.decode, cfg.threads)
             if cfg.write_doc_wc:
                 write_doc_wc_sharded(ctx, os.path.join(cfg.lpath, "doc_wc.dat"), sc, names, wsp.decode, cfg.threads)
@@ -217,7 +217,9 @@ def _lda_and_export(R, cfg, ctx, sc, names, gmap, decode, device, log, summary):
     from ..export import lda_post
     word_names = doc_names = None
     if sc is not None:
-        doc_names = names.take(sc.doc_keys)
+        doc_names = getattr(sc, "doc_names", None)
+        if doc_names is None:
+            doc_names = names.take(sc.doc_keys)
     gamma = log_beta = None
     if not R.done("lda"):
         if sc is not None:
@@ -231,8 +233,6 @@ def _lda_and_export(R, cfg, ctx, sc, names, gmap, decode, device, log, summary):
         R.skip("lda")
     ip_rows = None
     if not R.done("lda_post"):
-        if word_names is None:
-            word_names = decode(sc.word_keys) if sc is not None else C.load_corpus_files(cfg.lpath)[2]
         if gamma is None:
             from ..models.lda.estimate import load_final
             corpus, all_docs, _, (d0, d1) = _files_state(cfg, ctx)
@@ -240,20 +240,33 @@ def _lda_and_export(R, cfg, ctx, sc, names, gmap, decode, device, log, summary):
             g_all, log_beta = load_final(cfg.lpath)
             gamma = g_all[d0:d1]
         with R.stage("lda_post"):
-            th, ph, wn = lda_post.export_sharded(ctx, doc_names, gamma, word_names, log_beta,
-                                                 os.path.join(cfg.lpath, "doc_results.csv"),
-                                                 os.path.join(cfg.lpath, "word_results.csv"),
-                                                 strict=cfg.strict, read_back=True)
-            all_docs = None
             if sc is not None:
-                # doc row of every ip id: the scorers' name lookup without a name dictionary
-                keys = np.concatenate(SIO.allgather_array(ctx, sc.doc_keys))
-                g2d = np.full(len(names), -1, np.int64)
-                g2d[keys] = np.arange(keys.size)
-                ip_rows = g2d[gmap]
+                # nothing replicated: this rank's θ rows and vocabulary slice, the word map hash-partitioned,
+                # the doc row of an ip id in id-range slices (shardio.range_put / fetch_rows)
+                V = int(log_beta.shape[1])
+                N, r = SIO.world(ctx), SIO.rank(ctx)
+                v0, v1 = V * r // N, V * (r + 1) // N
+                if word_names is None:
+                    word_names = decode(sc.word_keys[v0:v1])
+                elif len(word_names) == V:
+                    word_names = word_names[v0:v1]
+                th, ph, wn = lda_post.export_sharded(ctx, doc_names, gamma, word_names, log_beta,
+                                                     os.path.join(cfg.lpath, "doc_results.csv"),
+                                                     os.path.join(cfg.lpath, "word_results.csv"),
+                                                     strict=cfg.strict, read_back=True, gather=False, num_words=V)
+                ws = SIO.range_starts(V, N)
+                tables = C.ShardedTables(ctx, th, list(sc.bounds), ph, ws, SIO.DistDict(ctx, wn, np.arange(v0, v1)))
+                d0, d1 = sc.doc_range
+                ip_doc = SIO.range_put(ctx, sc.doc_keys, np.arange(d0, d1, dtype=np.int64), len(names), fill=-1)
+                ip_rows = SIO.fetch_rows(ctx, ip_doc, SIO.range_starts(len(names), N), gmap)
             else:
-                all_docs = C.load_corpus_files(cfg.lpath)[1]
-            tables = C.ModelTables(all_docs, th, wn, ph)
+                if word_names is None:
+                    word_names = C.load_corpus_files(cfg.lpath)[2]
+                th, ph, wn = lda_post.export_sharded(ctx, doc_names, gamma, word_names, log_beta,
+                                                     os.path.join(cfg.lpath, "doc_results.csv"),
+                                                     os.path.join(cfg.lpath, "word_results.csv"),
+                                                     strict=cfg.strict, read_back=True)
+                tables = C.ModelTables(C.load_corpus_files(cfg.lpath)[1], th, wn, ph)
     else:
         R.skip("lda_post")
         tables = C.load_model_tables(cfg.lpath)
