@@ -84,11 +84,39 @@ inline const double* pow10_table() {
 }
 
 // 12 decimal digits of 0 <= n < 10^12, two at a time
-inline void put_digits12(char* dig, int64_t n) {
+inline void put_digits12(char* dig, int64_t n);
+
+// the exact product a * b = p + e: one fused multiply-add (x86-64-v3 hosts), else Dekker's split
+inline void two_prod(double a, double b, double* p, double* e) {
+  *p = a * b;
+#if defined(__FMA__)
+  *e = __builtin_fma(a, b, -*p);
+#else
+  const double sp = 134217729.0;                // 2^27 + 1
+  double t = sp * a, ah = t - (t - a), al = a - ah;
+  t = sp * b;
+  const double bh = t - (t - b), bl = b - bh;
+  *e = ((ah * bh - *p) + ah * bl + al * bh) + al * bl;
+#endif
+}
+
+// 10^i as the nearest double, i in [-12, 12] (decade of a value: a >= ten_pow(E + 1) -> E + 1)
+inline double ten_pow(int i) {
+  static const double t[25] = {1e-12, 1e-11, 1e-10, 1e-9, 1e-8, 1e-7, 1e-6, 1e-5, 1e-4, 1e-3, 1e-2, 1e-1, 1e0,
+                               1e1,   1e2,   1e3,   1e4,  1e5,  1e6,  1e7,  1e8,  1e9,  1e10, 1e11, 1e12};
+  return t[i + 12];
+}
+
+inline const char* digit_pairs() {
   static const char pairs[] =
       "00010203040506070809101112131415161718192021222324252627282930313233343536373839"
       "40414243444546474849505152535455565758596061626364656667686970717273747576777879"
       "8081828384858687888990919293949596979899";
+  return pairs;
+}
+
+inline void put_digits12(char* dig, int64_t n) {
+  const char* pairs = digit_pairs();
   uint32_t hi = (uint32_t)(n / 1000000), lo = (uint32_t)(n % 1000000);
   for (int i = 4; i >= 0; i -= 2) {
     std::memcpy(dig + 6 + i, pairs + 2 * (lo % 100), 2);
@@ -98,28 +126,18 @@ inline void put_digits12(char* dig, int64_t n) {
   }
 }
 
-// Dekker's exact product a * b = p + e (no FMA instruction needed: the host build targets x86-64-v2)
-inline void two_prod(double a, double b, double* p, double* e) {
-  const double sp = 134217729.0;                // 2^27 + 1
-  double t = sp * a, ah = t - (t - a), al = a - ah;
-  t = sp * b;
-  const double bh = t - (t - b), bl = b - bh;
-  *p = a * b;
-  *e = ((ah * bh - *p) + ah * bl + al * bh) + al * bl;
-}
-
 // round-half-even(a * 10^k) for a >= 0, 0 <= k <= 22, a * 10^k < 2^52
 inline int64_t scaled_round(double a, int k) {
   double p, err;                                // a * 10^k = p + err exactly
   two_prod(a, pow10_table()[k], &p, &err);
   const double q = std::floor(p);
   const double f = p - q;                       // exact
-  int64_t n = (int64_t)q;
-  if (f < 0.25) return n;                       // |err| <= half an ulp of p
-  if (f > 0.75) return n + 1;
-  const double d = f - 0.5;                     // exact (Sterbenz); compare d + err with 0
-  if (d > -err || (d == -err && (n & 1))) ++n;
-  return n;
+  const int64_t n = (int64_t)q;
+  // round up iff f + err > 1/2, ties to even; d = f - 1/2 is exact (Sterbenz for f in [1/4, 1], exact
+  // below) and |err| <= half an ulp of p < 1/4, so one branch-free comparison decides every case (the
+  // fraction is random in the formatted tables: a three-way branch mispredicted half the time)
+  const double d = f - 0.5;
+  return n + (int64_t)((d > -err) | ((d == -err) & (int)(n & 1)));
 }
 
 // digits -> double (Clinger's fast path: an integer mantissa < 2^53 times / over an exact power of
@@ -137,16 +155,17 @@ inline bool digits_value(const char* dig, int nd, int e, bool neg, double* out) 
   return true;
 }
 
-// Python 2 str(float): "%.12g" plus ".0" on integral-looking output.  `back` (optional) receives
-// the value a reader parses from the text.
-inline void append_py2_float(std::string& out, double d, double* back = nullptr) {
-  const size_t at = out.size();
+// Python 2 str(float): "%.12g" plus ".0" on integral-looking output, written at w (at most 32 bytes);
+// returns the end.  `back` (optional) receives the value a reader parses from the text.
+inline char* put_py2_float(char* w, double d, double* back = nullptr) {
+  char* const start = w;
   const double a = std::fabs(d);
   if (a >= 1e-11 && a < 1e11) {                 // 0 <= 11 - E <= 22: an exact power of ten
     uint64_t bits;
     std::memcpy(&bits, &a, 8);
     const int e2 = (int)((bits >> 52) & 0x7ff) - 1022;          // a in [2^(e2-1), 2^e2)
     int E = (int)std::floor((e2 - 1) * 0.30102999566398120);   // E or E - 1
+    if (a >= ten_pow(E + 1)) ++E;               // almost always the decade now (the loop repairs the rest)
     int64_t N = 0;
     bool ok = false;
     for (int tries = 0; tries < 3; ++tries) {
@@ -155,7 +174,7 @@ inline void append_py2_float(std::string& out, double d, double* back = nullptr)
       N = scaled_round(a, k);
       if (N < 100000000000LL) { --E; continue; }
       if (N >= 1000000000000LL) {
-        if (N == 1000000000000LL && tries > 0) { N = 100000000000LL; ++E; ok = true; break; }  // carry
+        if (N == 1000000000000LL) { N = 100000000000LL; ++E; ok = true; break; }  // rounded up to 10^12
         ++E;
         continue;
       }
@@ -167,8 +186,6 @@ inline void append_py2_float(std::string& out, double d, double* back = nullptr)
       put_digits12(dig, N);
       int nd = 12;
       while (nd > 1 && dig[nd - 1] == '0') --nd;
-      char buf[40];
-      char* w = buf;
       if (d < 0) *w++ = '-';
       if (E < -4 || E >= 12) {
         *w++ = dig[0];
@@ -191,46 +208,64 @@ inline void append_py2_float(std::string& out, double d, double* back = nullptr)
         std::memcpy(w, dig, nd);
         w += nd;
       }
-      out.append(buf, w - buf);
-      if (back && !digits_value(dig, nd, E, d < 0, back))
-        std::from_chars(out.data() + at, out.data() + out.size(), *back);
-      return;
+      if (back && !digits_value(dig, nd, E, d < 0, back)) std::from_chars(start, w, *back);
+      return w;
     }
   }
-  if (std::isnan(d)) { out += "nan"; if (back) *back = d; return; }
-  if (std::isinf(d)) { out += d > 0 ? "inf" : "-inf"; if (back) *back = d; return; }
-  char buf[40];
-  auto r = std::to_chars(buf, buf + sizeof(buf), d, std::chars_format::general, 12);
-  const int n = (int)(r.ptr - buf);
-  out.append(buf, n);
+  if (std::isnan(d)) { std::memcpy(w, "nan", 3); if (back) *back = d; return w + 3; }
+  if (std::isinf(d)) {
+    const char* t = d > 0 ? "inf" : "-inf";
+    const size_t n = std::strlen(t);
+    std::memcpy(w, t, n);
+    if (back) *back = d;
+    return w + n;
+  }
+  auto r = std::to_chars(w, w + 32, d, std::chars_format::general, 12);
   bool has = false;
-  for (int i = 0; i < n; ++i)
-    if (buf[i] == '.' || buf[i] == 'e') { has = true; break; }
-  if (!has) out += ".0";
-  if (back) std::from_chars(out.data() + at, out.data() + out.size(), *back);
+  for (char* q = w; q < r.ptr; ++q)
+    if (*q == '.' || *q == 'e') { has = true; break; }
+  w = r.ptr;
+  if (!has) { *w++ = '.'; *w++ = '0'; }
+  if (back) std::from_chars(start, w, *back);
+  return w;
+}
+
+inline void append_py2_float(std::string& out, double d, double* back = nullptr) {
+  char buf[40];
+  out.append(buf, put_py2_float(buf, d, back) - buf);
 }
 
 // printf("%5.10f"): finite values always exceed the 5-character field width, so the conversion
-// is the exact 10-decimal rounding: N = round-half-even(|d| * 1e10) for |d| < 9e5 (N < 2^53),
+// is the exact 10-decimal rounding: N = round-half-even(|d| * 1e10) for |d| < 4.5e5 (N < 2^52),
 // the exact printf-equivalent path beyond; nan / inf keep printf's padded spelling.
-inline void append_fixed10(std::string& out, double d, double* back = nullptr) {
+inline char* put_fixed10(char* w, double d, double* back = nullptr) {
   const double a = std::fabs(d);
-  if (a < 9e5) {
+  if (a < 4.5e5) {                              // |d| 1e10 < 2^52: the rounding error term is <= 1/4
     int64_t N = scaled_round(a, 10);
     const int64_t ip = N / 10000000000LL, fp = N % 10000000000LL;
-    if (std::signbit(d)) out += '-';
-    char b[32];
-    auto r = std::to_chars(b, b + sizeof(b), ip);
-    out.append(b, r.ptr - b);
-    out += '.';
-    char f[10];
-    int64_t v = fp;
-    for (int i = 9; i >= 0; --i) { f[i] = (char)('0' + v % 10); v /= 10; }
-    out.append(f, 10);
+    if (std::signbit(d)) *w++ = '-';
+    w = std::to_chars(w, w + 24, ip).ptr;
+    *w++ = '.';
+    const char* pr = digit_pairs();
+    uint64_t v = (uint64_t)fp;
+    for (int i = 8; i >= 0; i -= 2) {
+      std::memcpy(w + i, pr + 2 * (v % 100), 2);
+      v /= 100;
+    }
+    w += 10;
     if (back) {
       const double x = (double)N / 1e10;
       *back = std::signbit(d) ? -x : x;
     }
+    return w;
+  }
+  return nullptr;                               // caller takes the exact path (append_fixed10)
+}
+
+inline void append_fixed10(std::string& out, double d, double* back = nullptr) {
+  char b[48];
+  if (char* e = put_fixed10(b, d, back)) {
+    out.append(b, e - b);
     return;
   }
   const size_t at = out.size();
