@@ -101,7 +101,7 @@ def cmd_ml_ops(argv):
                     help="write word-assignments.dat (default, as lda-c does on every run)")
     ap.add_argument("--no-word-assignments", dest="word_assignments", action="store_false")
     ap.add_argument("--rank-gamma", action="store_true", default=None,
-                    help="write <rank>.gamma / <rank>.beta per GPU (default: on when running on several GPUs)")
+                    help="write <rank>.gamma / <rank>.beta per GPU (default: on when running on several GPUs and K x V <= 2^26)")
     ap.add_argument("--threads", type=int, default=8)
     ap.add_argument("--deliver", action="store_true", help="scp -r LPATH UINODE:RPATH (ml_ops.sh:121)")
     ap.add_argument("--cuts", help="fixed flow cuts: a flow_qtiles file or its text (the reference's CUT)")

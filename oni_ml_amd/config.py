@@ -95,7 +95,7 @@ class RunConfig:
     threads: int = 8
     write_doc_wc: bool = True
     word_assignments: bool = True          # lda-c writes word-assignments.dat on every `lda est`
-    rank_gamma: Optional[bool] = None      # <rank>.gamma / <rank>.beta; None: on for multi-rank runs
+    rank_gamma: Optional[bool] = None      # <rank>.gamma / <rank>.beta; None: multi-rank runs of K x V <= 2^26
     verbose: bool = True
     cuts: str = ""                        # fixed flow cuts in flow_qtiles form ("ibyt,ipkt,time"; the
                                           # reference's commented-out CUT consumer, flow_pre_lda.scala:95-98)

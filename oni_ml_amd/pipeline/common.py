@@ -97,16 +97,24 @@ def load_corpus_files(lpath: str):
     return c, docs, words
 
 
+RANK_FILES_MAX_VALUES = 1 << 26
+
+
 def run_lda(cfg, corpus: Corpus, dist=None, device=None, log=print, local_shard: bool = False, doc_offset: int = 0):
     outdir = cfg.lpath
     settings_path = os.path.join(outdir, "settings.txt")
     if dist is None or dist.rank == 0:
         ldac.write_settings(settings_path, cfg.settings)
+    rank_files = cfg.rank_gamma
+    if rank_files is None:
+        # oni-lda-c's per-worker <rank>.beta / <rank>.gamma temporaries (README.md:121): on for multi-rank
+        # runs while a worker's K x V beta text stays small (<= RANK_FILES_MAX_VALUES values; BASELINE
+        # config 5's would be ~7 GB per rank); --rank-gamma forces them
+        rank_files = dist is not None and dist.active and cfg.topics * corpus.num_terms <= RANK_FILES_MAX_VALUES
     return estimate(corpus, cfg.topics, cfg.alpha, cfg.settings, cfg.start, outdir, backend=cfg.backend,
                     device=device, dist=dist, seed=cfg.seed, resume=cfg.resume,
                     write_word_assignments=cfg.word_assignments,
-                    write_rank_gamma=(cfg.rank_gamma if cfg.rank_gamma is not None
-                                      else dist is not None and dist.active),
+                    write_rank_gamma=rank_files,
                     verbose=cfg.verbose, fault_at_iteration=cfg.extra.get("fault_at_iteration"),
                     defer_files=True, local_shard=local_shard, doc_offset=doc_offset)
 

@@ -198,6 +198,7 @@ def score_flow(cfg, ft: FF.FlowTable, tables: C.ModelTables, device, log=print, 
         raise ValueError("compat=strict scores over exactly 20 topics (flow_post_lda.scala:232)")
     model = S.TopicModel.build(th, ph, S.default_value("flow", K, cfg.strict), device)
     sa, sb, key, flag = S.score(model, didx[feat.sip.long()], w_src, didx[feat.dip.long()], w_dst, cfg.tol)
+    qs = S.key_quantiles(key)
     order = S.rank_flagged(key, flag)
     n = int(order.size)
     out = os.path.join(cfg.lpath, "flow_results.csv")
@@ -224,10 +225,10 @@ def score_flow(cfg, ft: FF.FlowTable, tables: C.ModelTables, device, log=print, 
         text, ends = native.lib().format_rows(None, cols, n=n, row_ends=True, threads=cfg.threads)
         total = SIO.merge_sorted_rows(ctx, sel(key).astype(np.float64), text, ends, out)
         log(f"flow_post: {total} events with score < {cfg.tol} written to {out} ({n} from rank {ctx.rank})")
-        return dict(flagged=total, rank_flagged=n, events=ctx.allreduce_int(int(feat.time.numel())))
+        return dict(flagged=total, rank_flagged=n, events=ctx.allreduce_int(int(feat.time.numel())), **qs)
     native.lib().write_rows(out, None, cols, threads=cfg.threads, n=n)
     log(f"flow_post: {n} events with score < {cfg.tol} written to {out}")
-    return dict(flagged=n, events=int(feat.time.numel()))
+    return dict(flagged=n, events=int(feat.time.numel()), **qs)
 
 
 def synthetic_flow_corpus(events: int = 1_000_000, seed: int = 0, workdir: Optional[str] = None, device=None,

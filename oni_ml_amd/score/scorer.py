@@ -55,6 +55,17 @@ def score(model: TopicModel, doc_a, word_a, doc_b=None, word_b=None, tol: float 
     return ref(model.theta, model.phi, model.K, model.default, doc_a, word_a, doc_b, word_b, tol)
 
 
+def key_quantiles(key: torch.Tensor, qs=(1e-4, 1e-3, 1e-2, 0.1, 0.5), sample: int = 1 << 20) -> dict:
+    """Quantiles of the events' scores (a strided sample of at most ``sample``), for choosing TOL: the
+    fraction q of events scoring below key_q<q> would be flagged.  Metrics only."""
+    n = key.numel()
+    if n == 0:
+        return {}
+    k = key[:: max(1, n // sample)].to(torch.float64)
+    v = torch.quantile(k, torch.tensor(qs, dtype=torch.float64, device=k.device)).cpu().tolist()
+    return {f"key_q{q:g}": float(x) for q, x in zip(qs, v)}
+
+
 def rank_flagged(key: torch.Tensor, flag: torch.Tensor) -> torch.Tensor:
     """Indices of flagged rows in ascending key order (stable) as an int64 host array."""
     sel = torch.nonzero(flag.to(torch.bool), as_tuple=False).reshape(-1)

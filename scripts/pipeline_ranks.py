@@ -54,6 +54,7 @@ def main():
     ap.add_argument("--threads", type=int, default=8, help="native threads per rank")
     ap.add_argument("--cphi-gb", default=None, help="per-rank HBM budget of the c.phi rows")
     ap.add_argument("--no-word-assignments", action="store_true")
+    ap.add_argument("--lag", default=None, help="LAG save period (lda-c: 5; 0: only 000 and final)")
     a = ap.parse_args()
     tol = a.tol or ("1e-5" if a.source == "flow" else "1e-4")
     tmp = tempfile.mkdtemp(prefix="oni_ranks_")
@@ -83,6 +84,8 @@ def main():
                 cli += ["--cphi-gb", str(a.cphi_gb)]
             if a.no_word_assignments:
                 cli += ["--no-word-assignments"]
+            if a.lag is not None:
+                cli += ["--lag", str(a.lag)]
             cmd = [sys.executable] + (cli if n == 1 else
                                       ["-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n),
                                        "--master-addr", "127.0.0.1", "--master-port", str(_port())] + cli)
@@ -108,13 +111,18 @@ def main():
             for s in STAGES[a.source]:
                 others = [p.get(s, 0.0) for p in per_rank[1:]]
                 serial += max(0.0, per_rank[0].get(s, 0.0) - (max(others) if others else 0.0))
+            fp = [json.loads(l) for l in open(os.path.join(lp, "metrics.jsonl"))] if os.path.exists(
+                os.path.join(lp, "metrics.jsonl")) else []
+            keyq = {k: v for rec in fp if rec.get("stage") in ("flow_post", "dns_post")
+                    for k, v in rec.items() if k.startswith("key_q")}
+            out_gb = sum(os.path.getsize(os.path.join(d, f)) for d, _, fs in os.walk(lp) for f in fs) / 1e9
             shutil.rmtree(lp, ignore_errors=True)       # (config 5 writes ~50 GB of text per run)
             run = dict(ranks=n, process_wall_s=round(wall, 3), pipeline_wall_s=round(pw, 3),
-                       flagged=summ.get("scored"), corpus=summ.get("corpus"),
+                       flagged=summ.get("scored"), rank0_key_quantiles=keyq, startup_marks=summ.get("startup_marks"), corpus=summ.get("corpus"),
                        em_iterations=summ.get("lda", {}).get("em_iterations"),
                        stage_s=[{k: round(v, 3) for k, v in p.items()} for p in per_rank],
                        rank0_serial_s=round(serial, 3) if n > 1 else None,
-                       rank0_serial_share=round(serial / pw, 4) if n > 1 else None)
+                       rank0_serial_share=round(serial / pw, 4) if n > 1 else None, output_gb=round(out_gb, 3))
             out["runs"].append(run)
             print(json.dumps(run), flush=True)
     finally:
