@@ -2369,6 +2369,393 @@ __global__ __launch_bounds__((NW + 1) * 64) void gs_wsteam(GSArgs a) {
   }
 }
 
+// ------------------------------------------------- word team, LDS ring -------
+// gs_ring: the longest documents (kGsTeam8 with staged rows, KS <= 32) as gs_wsteam computes them,
+// with the rows streamed into an LDS ring by a dedicated LOADER WAVE (LDS-DMA: one
+// global_load_lds_dwordx4 moves one 1 KB topic-pair row of a 64-word staged tile).
+//
+// Why: one CU walks the longest document's rows 20 x U times per E-step, and in gs_wsteam every word
+// wave gathers the next chunk's rows into registers only after its own arrival -- the CU's load path
+// idles while the word waves compute and again while the topic wave refreshes, and the registers hold
+// exactly one chunk ahead.  Here the loader keeps up to DEPTH tiles in flight at all times, into
+// NSLOT ring slots (~140 KB of LDS, more than a chunk of the headline document), and recycles a slot
+// as soon as its tile is consumed: the load path streams through the refresh and the barriers.
+//
+// Synchronisation is by LDS flags only (no s_barrier after the set-up, so the loader never waits on
+// the compute waves' phases):
+//   full[s]  = q + 1 once item q (the q-th tile of the document stream: sweep, chunk, tile) landed
+//            in slot s = q mod NSLOT (the loader's counted vmcnt wait, then the flag);
+//   freed[s] = q + 1 once the word wave owning item q has read it;
+//   arrive[v] = chunks whose topic sums word wave v left in sRed; eready = chunks whose E the topic
+//            wave published; sarr[v] / sweep_seq = the same for the sweep-end likelihood; stop = 1 when
+//            the sweeps end (the loader drains its loads and leaves).
+// Tile i of a chunk (tiles 64-aligned in the document: the chunk's first and last tiles may be shared
+// with the neighbours and are streamed once per chunk) belongs to word wave own(i), spread so every
+// SIMD gets the same number of tiles.  Arithmetic per word and per topic is gs_wsteam's; the topic
+// sums add the word waves in wave order (the grouping differs from gs_wsteam: agreement to rounding).
+constexpr int kRingSpinLimit = 1 << 22;     // polls of one flag (~0.1 s) before the workgroup aborts
+
+template <int KS>
+struct RingGeom {
+  static constexpr int PAIRS = KS / 2;
+  static constexpr int ROWB = PAIRS * 1024;                    // [PAIRS][64] double2 of a tile
+  static constexpr int SLOTB = ROWB + 256;                     // + the tile's 64 float counts
+  static constexpr int LDS_OTHER = 16 * 1024;                  // the kernel's other LDS (tables, flags)
+  static constexpr int NSLOT_RAW = (160 * 1024 - LDS_OTHER) / SLOTB;
+  static constexpr int NSLOT = NSLOT_RAW > 16 ? 16 : NSLOT_RAW;
+  static constexpr int IPT = PAIRS + 1;                        // DMA instructions per tile
+  static constexpr int DEPTH_RAW = 63 / IPT;                   // vmcnt is 6 bits
+  static constexpr int DEPTH = DEPTH_RAW > 5 ? 5 : DEPTH_RAW;  // tiles in flight past a counted wait
+};
+
+// The loader's LDS-DMA is inline asm: hipcc's wait-count pass treats a pending
+// __builtin_amdgcn_global_load_lds as an LDS write and drains it (vmcnt(0)) at every LDS fence or flag
+// store, which would serialise the ring; invisible to it, the loads stay in flight and the loader
+// counts them itself (wait_vmcnt).  M0 (the destination base) is compiler-reserved: saved and restored
+// in the same statement (cdna_hip_programming.md, inline asm rules).
+__device__ __forceinline__ unsigned lds_offset(const void* p) {
+  return (unsigned)(size_t)((const __attribute__((address_space(3))) char*)p);
+}
+
+__device__ __forceinline__ void glds16(const void* src, unsigned lds_dst) {
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(src), "s"(lds_dst) : "memory");
+}
+
+__device__ __forceinline__ void glds4(const void* src, unsigned lds_dst) {
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(src), "s"(lds_dst) : "memory");
+}
+
+// s_waitcnt vmcnt(N): the loader's own count of its LDS-DMA (invisible to the compiler)
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  static_assert(N >= 0 && N < 64, "vmcnt is 6 bits");
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// the word wave owning tile i of a chunk: tiles round-robin over the SIMDs (wave v runs on SIMD v mod 4),
+// and over the word waves of a SIMD
+template <int NW>
+__device__ __forceinline__ int ring_owner(int i) {
+  const int s = i & 3, k = i >> 2;
+  const int per = (NW - s + 3) / 4;        // word waves on SIMD s: s, s + 4, ...
+  return s + 4 * (k % per);
+}
+
+template <int KS, int NW>
+__global__ __launch_bounds__((NW + 2) * 64) void gs_ring(GSArgs a) {
+  static_assert(KS <= 32 && KS % 2 == 0, "ring: KS <= 32");
+  static_assert(NW >= 4, "ring: every SIMD owns tiles");
+  using G = RingGeom<KS>;
+  constexpr int NS = NW * 64;
+  constexpr int MAXI = 2;                  // tiles per wave per chunk whose log P waits for the arrival
+  __shared__ __attribute__((aligned(16))) char ring[G::NSLOT * G::SLOTB];
+  __shared__ double C[kGsUMax][KS];        // chunk contributions (previous sweep)
+  __shared__ double Et[kGsUMax][KS];       // E each chunk used (final pass)
+  __shared__ double E_[KS];                // current E
+  __shared__ double sRed[NW][KS];          // per-wave topic sums of a chunk
+  __shared__ double Cs[kGsUMax];           // chunk count sums
+  __shared__ double sLw[NW];               // per-wave sweep sums of c log P
+  __shared__ double sLc[2];                // likelihood, conv of the last sweep
+  __shared__ int qbase[kGsUMax + 1];       // items of the chunks before chunk j (one sweep)
+  __shared__ int full[G::NSLOT], freed[G::NSLOT];
+  __shared__ int arrive[NW], sarr[NW];
+  __shared__ int eready, sweep_seq, stop;
+  __shared__ int abort_;                   // a wait ran past kRingSpinLimit: every wave leaves, lik = NaN
+  if (a.params[kParamDone] != 0.0) return;
+  const int t = threadIdx.x;
+  const int d = a.order[blockIdx.x];
+  if (d < 0) return;                       // placement gap (GSPlan.isolate_longest): whole workgroup
+  const double alpha = a.params[0], lik_const = a.params[1];
+  const int vmi = (int)a.params[2];
+  const double vconv = params_vconv(a.params);
+  const int K = a.K;
+  const int lane = t & 63, wv = __builtin_amdgcn_readfirstlane(t >> 6);   // wave-uniform (SGPR)
+  const int s0 = a.doc_ptr[d], n = a.doc_ptr[d + 1] - s0;
+  const int U = a.gs_updates;
+  const int W = n > 0 ? (n + U - 1) / U : 1;
+  const int nch = (n + W - 1) / W;
+  const float* __restrict__ crow = a.counts + s0;
+  for (int j = t; j < nch; j += (NW + 2) * 64) Cs[j] = 0.0;
+  if (t < G::NSLOT) full[t] = freed[t] = 0;
+  if (t < NW) arrive[t] = sarr[t] = 0;
+  if (t == 0) {
+    eready = 0;
+    sweep_seq = 0;
+    stop = 0;
+    abort_ = 0;
+    int q = 0;
+    for (int j = 0; j < nch; ++j) {
+      qbase[j] = q;
+      const int n0 = j * W, n1 = min(n, n0 + W);
+      q += ((n1 - 1) >> 6) - (n0 >> 6) + 1;
+    }
+    qbase[nch] = q;
+  }
+  lds_barrier();
+  for (int p = t; p < n; p += (NW + 2) * 64) atomicAdd(&Cs[p / W], (double)crow[p]);   // integer counts: exact
+  lds_barrier();                           // the last barrier: from here on flags only
+  double total = 0.0;
+  for (int j = 0; j < nch; ++j) total += Cs[j];
+  const double g0 = alpha + total / K;
+  const double m = psi_only(g0);
+  const int ips = qbase[nch];              // items per sweep
+  const dvec2* __restrict__ stg = reinterpret_cast<const dvec2*>(a.stage) + a.stage_off[blockIdx.x];
+  // bounded wait on an LDS flag: false when the workgroup aborted (a protocol fault never hangs the GPU)
+  auto wait_for = [&](const int* flag, int want, int sleep) -> bool {
+    int spins = 0;
+    while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < want) {
+      if (__hip_atomic_load(&abort_, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) return false;
+      if (++spins > kRingSpinLimit) {
+        __hip_atomic_store(&abort_, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        return false;
+      }
+      if (sleep) __builtin_amdgcn_s_sleep(1);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+    return true;
+  };
+
+  if (wv == NW + 1) {
+    // ---------------------------------------------------------------- loader wave
+    int q = 0, pub = 0, j = 0, i = 0;
+    int n0 = 0, nt = nch > 0 ? qbase[1] : 0;
+    auto publish_to = [&](int upto) {      // items [pub, upto) have landed (the caller's vmcnt wait)
+      for (; pub < upto; ++pub)
+        if (lane == 0) __hip_atomic_store(&full[pub % G::NSLOT], pub + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    };
+    while (nch > 0) {
+      if (__hip_atomic_load(&stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) ||
+          __hip_atomic_load(&abort_, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP))
+        break;
+      const int slot = q % G::NSLOT;
+      if (q >= G::NSLOT &&
+          __hip_atomic_load(&freed[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < q - G::NSLOT + 1) {
+        // the slot's previous tile is still being read: land and publish everything in flight first
+        // (a word wave may be waiting for exactly those), then wait for the slot
+        wait_vmcnt<0>();
+        publish_to(q);
+        bool quit = false;
+        int spins = 0;
+        while (__hip_atomic_load(&freed[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < q - G::NSLOT + 1) {
+          if (__hip_atomic_load(&stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) ||
+              __hip_atomic_load(&abort_, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) { quit = true; break; }
+          if (++spins > kRingSpinLimit) {
+            __hip_atomic_store(&abort_, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            quit = true;
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+        }
+        if (quit) break;
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+      }
+      const int tile = (n0 >> 6) + i;
+      const unsigned dst = __builtin_amdgcn_readfirstlane(lds_offset(ring) + (unsigned)(slot * G::SLOTB));
+      const dvec2* src = stg + (size_t)tile * G::PAIRS * 64 + lane;
+#pragma unroll
+      for (int k = 0; k < G::PAIRS; ++k) glds16(src + k * 64, dst + (unsigned)(k * 1024));
+      const int pc = min(tile * 64 + lane, n - 1);     // the last tile's lanes past the document end
+      glds4(crow + pc, dst + (unsigned)G::ROWB);
+      ++q;
+      if (++i == nt) {                     // next chunk (and sweep)
+        i = 0;
+        if (++j == nch) j = 0;
+        n0 = j * W;
+        nt = qbase[j + 1] - qbase[j];
+      }
+      if (q - pub > G::DEPTH) {
+        wait_vmcnt<G::DEPTH * G::IPT>();   // all but the last DEPTH tiles have landed
+        publish_to(q - G::DEPTH);
+      }
+    }
+    wait_vmcnt<0>();                       // no LDS-DMA may land after the workgroup's waves are gone
+    return;
+  }
+
+  double L = 0.0, L_old = 0.0, conv = 1.0, GS = 0.0;
+  int it = 0;
+  if (wv == NW) {
+    // ---------------------------------------------------------------- topic wave
+    __builtin_amdgcn_s_setprio(3);
+    const int k = lane;
+    double gam = k < K ? g0 : 0.0, psi = m, lps = 0.0;
+    double Ecur = k < K ? 1.0 : 0.0;
+    if (k < KS) {
+      E_[k] = Ecur;
+      for (int j = 0; j < nch; ++j) C[j][k] = k < K ? Cs[j] / K : 0.0;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    if (lane == 0) __hip_atomic_store(&eready, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    int gch = 0;                           // chunks refreshed so far
+    bool ok = true;
+    while (ok && var_continue(conv, vconv, it, vmi)) {
+      ++it;
+      lps = 0.0;
+      for (int j = 0; j < nch; ++j, ++gch) {
+        const double gC = k < KS ? gam - C[j][k] : 0.0;
+        double S = 0.0;
+#pragma unroll
+        for (int v = 0; v < NW; ++v) {
+          ok = ok && wait_for(&arrive[v], gch + 1, 1);
+          S += k < KS ? sRed[v][k] : 0.0;
+        }
+        if (!ok) break;
+        if (k < KS) {
+          const double Eo = Ecur;
+          const double nw = Eo * S;
+          double En = 0.0;
+          if (k < K) {
+            lps = fma(psi, nw, lps);
+            gam = fma(Eo, S, gC);
+            psi_exp(gam, m, psi, En);
+          }
+          E_[k] = En;
+          C[j][k] = nw;
+          Et[j][k] = Eo;
+          Ecur = En;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+        if (lane == 0) __hip_atomic_store(&eready, gch + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+      const bool own = k < K;
+      const double w1 = group_sum<64>(own ? gam : 0.0), w2 = group_sum<64>(own ? lgamma_pos(gam) : 0.0);
+      const double w3 = group_sum<64>(own ? lps : 0.0);
+      double LW = 0.0;
+#pragma unroll
+      for (int v = 0; v < NW; ++v) {
+        ok = ok && wait_for(&sarr[v], it, 1);
+        LW += sLw[v];
+      }
+      if (!ok) break;
+      GS = w1;
+      L = lik_const - lgamma_pos(GS) + w2 + fma(m, total, LW) - w3;
+      conv = (L_old - L) / L_old;
+      L_old = L;
+      if (lane == 0) {
+        sLc[0] = L;
+        sLc[1] = conv;
+        if (!var_continue(conv, vconv, it, vmi)) stop = 1;
+      }
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+      if (lane == 0) __hip_atomic_store(&sweep_seq, it, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+    if (lane == 0) stop = 1;
+    if (!ok) L = __builtin_nan("");        // surfaces as a RuntimeError on the host (NaN likelihood)
+    const double ps = group_sum<64>(k < K ? psi : 0.0);
+    if (k < KS) a.gamma[(size_t)d * KS + k] = gam;
+    if (lane == 0) {
+      a.lik[d] = L;
+      a.alpha_ss[d] = ps - K * psi_only(GS);
+      a.iters[d] = it;
+    }
+    return;
+  }
+
+  // ------------------------------------------------------------------ word waves
+  int gch = 0;
+  bool ok = true;
+  while (ok && var_continue(conv, vconv, it, vmi)) {
+    ++it;
+    double lw = 0.0;
+    const int qs = (it - 1) * ips;
+    for (int j = 0; j < nch && ok; ++j, ++gch) {
+      if (!(ok = wait_for(&eready, gch + 1, 0))) break;
+      double E[KS], acc[KS];
+#pragma unroll
+      for (int kk = 0; kk < KS; ++kk) {
+        E[kk] = E_[kk];
+        acc[kk] = 0.0;
+      }
+      const int n0 = j * W, n1 = min(n, n0 + W);
+      const int nt = qbase[j + 1] - qbase[j];
+      double Pq[MAXI], cq[MAXI];
+      int nq = 0;
+      for (int i = 0; i < nt; ++i) {
+        if (ring_owner<NW>(i) != wv) continue;
+        const int q = qs + qbase[j] + i;
+        const int slot = q % G::NSLOT;
+        if (!(ok = wait_for(&full[slot], q + 1, 0))) break;
+        const char* sb = ring + slot * G::SLOTB;
+        const int p = ((n0 >> 6) + i) * 64 + lane;
+        const float cf = reinterpret_cast<const float*>(sb + G::ROWB)[lane];
+        const double c = (p >= n0 && p < n1) ? (double)cf : 0.0;
+        double b[KS];
+#pragma unroll
+        for (int k2 = 0; k2 < G::PAIRS; ++k2) {
+          const dvec2 v = reinterpret_cast<const dvec2*>(sb)[k2 * 64 + lane];
+          b[2 * k2] = v.x;
+          b[2 * k2 + 1] = v.y;
+        }
+        double p0 = 0.0, p1 = 0.0, p2 = 0.0, p3 = 0.0;
+#pragma unroll
+        for (int kk = 0; kk < KS; kk += 4) {
+          p0 = fma(E[kk], b[kk], p0);
+          if (kk + 1 < KS) p1 = fma(E[kk + 1], b[kk + 1], p1);
+          if (kk + 2 < KS) p2 = fma(E[kk + 2], b[kk + 2], p2);
+          if (kk + 3 < KS) p3 = fma(E[kk + 3], b[kk + 3], p3);
+        }
+        const double P = c > 0.0 ? (p0 + p1) + (p2 + p3) : 1.0;
+        // the slot's bytes are in registers (b and cf were consumed above): hand it back to the loader
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+        if (lane == 0) __hip_atomic_store(&freed[slot], q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        const double r = c * drcp(P);
+#pragma unroll
+        for (int kk = 0; kk < KS; ++kk) acc[kk] = fma(r, b[kk], acc[kk]);
+        if (nq < MAXI) {
+          Pq[nq] = P;
+          cq[nq] = c;
+          ++nq;
+        } else {
+          lw = fma(c, flog(P), lw);
+        }
+      }
+      wave_topic_sums<KS>(acc, lane, sRed[wv]);
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+      if (lane == 0) __hip_atomic_store(&arrive[wv], gch + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      for (int u = 0; u < nq; ++u) lw = fma(cq[u], flog(Pq[u]), lw);   // beside the refresh
+    }
+    if (!ok) break;
+    const double w0 = group_sum<64>(lw);
+    if (lane == 0) sLw[wv] = w0;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    if (lane == 0) __hip_atomic_store(&sarr[wv], it, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    if (!(ok = wait_for(&sweep_seq, it, 1))) break;
+    L = sLc[0];
+    conv = sLc[1];
+  }
+  if (!ok) return;                         // aborted: the topic wave reports NaN
+  // final pass: c_n phi_nk = E_jk b_nk r_n with the final sweep's chunk E, rows from the staged copy
+  for (int j = 0; j < nch; ++j) {
+    const int n0 = j * W, n1 = min(n, n0 + W);
+    double E[KS];
+#pragma unroll
+    for (int kk = 0; kk < KS; ++kk) E[kk] = Et[j][kk];
+    for (int p = n0 + t; p < n1; p += NS) {
+      double b[KS];
+      load_row_staged<KS>(stg, p, b);
+      double p0 = 0.0, p1 = 0.0, p2 = 0.0, p3 = 0.0;
+#pragma unroll
+      for (int kk = 0; kk < KS; kk += 4) {
+        p0 = fma(E[kk], b[kk], p0);
+        if (kk + 1 < KS) p1 = fma(E[kk + 1], b[kk + 1], p1);
+        if (kk + 2 < KS) p2 = fma(E[kk + 2], b[kk + 2], p2);
+        if (kk + 3 < KS) p3 = fma(E[kk + 3], b[kk + 3], p3);
+      }
+      const double r = (double)crow[p] * drcp((p0 + p1) + (p2 + p3));
+      dvec2* row = reinterpret_cast<dvec2*>(a.cphi + (size_t)(s0 + p) * KS);
+#pragma unroll
+      for (int kk = 0; kk < KS / 2; ++kk) {
+        const dvec2 v = {E[2 * kk] * b[2 * kk] * r, E[2 * kk + 1] * b[2 * kk + 1] * r};
+        __builtin_nontemporal_store(v, &row[kk]);
+      }
+    }
+  }
+}
+
 // ------------------------------------------------------------ suff stats ----
 // One word per workgroup (heavy) / wave (medium) / 16 lanes (light); a CSC entry's
 // row is read by TG lanes (KPL topics each), S = G / TG entries in flight per group.
@@ -2649,7 +3036,16 @@ static void gs_estep_ks(const GSArgs& a, int variant, hipStream_t s) {
         // ONI_GS_EARLY_PREFETCH: next-chunk rounds gathered before the arrival (1, the default: 2.13-2.14
         // vs 2.17-2.18 ms per EM iteration, 3 A/B rounds; 2 spills 192 B: 3.27 ms; 0 = after it)
         static const int ep = std::getenv("ONI_GS_EARLY_PREFETCH") ? std::atoi(std::getenv("ONI_GS_EARLY_PREFETCH")) : 1;
-        if (a.stage != nullptr) {
+        // ONI_GS_RING=1: the LDS-ring kernel (loader wave + LDS-DMA) for the staged longest documents
+        // (read per launch, not cached: tests switch it within one process)
+        const char* ring_env = std::getenv("ONI_GS_RING");
+        const int ring = ring_env ? std::atoi(ring_env) : 0;
+        if (a.stage != nullptr && ring) {
+          if constexpr (KS % 2 == 0)
+            hipLaunchKernelGGL((gs::gs_ring<KS, 7>), dim3(a.n_items), dim3(576), 0, s, a);
+          else
+            throw std::runtime_error("gs_estep: ring needs an even KS");
+        } else if (a.stage != nullptr) {
           // staged rows (launch_gs_stage): every next-chunk round gathered after the arrival is the
           // default here (ONI_GS_EARLY_PREFETCH unset: 1.726-1.740 vs 1.824-1.833 ms per EM iteration
           // for the early round-0 gather, 3 A/B rounds -- the contiguous loads no longer need the head start)

@@ -220,6 +220,41 @@ def test_staged_rows_bitwise_equal_beta_rows(monkeypatch):
         assert np.array_equal(a, b)
 
 
+@pytest.mark.parametrize("K,vconv", [(20, -1e30), (20, 1e-6), (24, -1e30), (8, -1e30), (32, -1e30)])
+def test_ring_kernel_matches_oracle(monkeypatch, K, vconv):
+    """gs_ring (ONI_GS_RING=1: the staged longest documents streamed through an LDS ring by a loader
+    wave, flags instead of barriers) against the CPU oracle of the same schedule: gamma, likelihoods,
+    sweeps and the sufficient statistics of its c.phi rows at 1e-10; and against gs_wsteam to rounding."""
+    rng = np.random.default_rng(11 + K)
+    V, D = 20000, 150
+    lens = np.minimum(rng.zipf(1.5, D), 150)
+    lens[:6] = [13000, 7000, 4100, 3000, 2100, 2049]
+    ptr = np.concatenate([[0], np.cumsum(lens)])
+    words = np.concatenate([rng.choice(V, n, replace=False) for n in lens]).astype(np.int32)
+    c = Corpus(ptr.astype(np.int64), words, rng.integers(1, 4, words.size).astype(np.int64), V)
+    lb = _log_beta(V, K, seed=K)
+    alpha = 0.41
+    ref = _oracle(c, lb, alpha, LDASettings(var_max_iter=7, var_converged=vconv), 32)
+    out = {}
+    for ring in ("1", "0"):
+        monkeypatch.setenv("ONI_GS_RING", ring)
+        eng, sc = _gpu_estep(c, K, lb, alpha, LDASettings(var_max_iter=7, var_converged=vconv), 32)
+        assert eng._stages, "the team8 bucket must be staged for the ring kernel"
+        out[ring] = (eng.gamma[:, :K].cpu().numpy(), eng.lik.cpu().numpy(), eng.iters.cpu().numpy(),
+                     eng._cw_local[:, :K].cpu().numpy(), sc)
+    g, lik, it, cw, sc = out["1"]
+    same = it == ref["iters"]
+    assert same[:6].all() and same.mean() > 0.99
+    assert _rel(g[same], ref["gamma"][same], 1e-12) < 1e-10
+    assert _rel(lik[same], ref["doc_likelihood"][same], 1.0) < 1e-10
+    if vconv < 0:
+        assert _rel(cw, np.ascontiguousarray(ref["class_word"].T), 1e-30) < 1e-10
+        assert abs(sc[0] - ref["likelihood"]) / abs(ref["likelihood"]) < 1e-11
+    g0, lik0, it0, cw0, _ = out["0"]
+    assert np.array_equal(it, it0)
+    assert _rel(g, g0, 1e-12) < 1e-12 and _rel(cw, cw0, 1e-30) < 1e-12
+
+
 @pytest.mark.parametrize("K,env,U", [
     (100, {}, 32),                                                      # default split for KS > 32
     (100, {"ONI_GS_SPLIT_MIN": "4000"}, 32),
