@@ -232,8 +232,9 @@ def score_flow(cfg, ft: FF.FlowTable, tables: C.ModelTables, device, log=print, 
 
 
 def synthetic_flow_corpus(events: int = 1_000_000, seed: int = 0, workdir: Optional[str] = None, device=None,
-                          strict: bool = True, threads: int = 8, return_names: bool = False):
+                          strict: bool = True, threads: int = 8, return_names: bool = False, chunk_events: int = 0):
     """Synthetic netflow day -> featurized -> lda-c corpus (the bench / test input path).
+    ``chunk_events``: generate part file by part file (a month: one file per day, synth/flow.py).
 
     Returns (Corpus, info dict with stage timings[, word names])."""
     import tempfile
@@ -242,7 +243,8 @@ def synthetic_flow_corpus(events: int = 1_000_000, seed: int = 0, workdir: Optio
     device = torch.device(device or ("cuda" if torch.cuda.is_available() else "cpu"))
     tmp = tempfile.mkdtemp(prefix="oni_flow_") if workdir is None else workdir
     t0 = time.perf_counter()
-    gen = generate_flow_day(os.path.join(tmp, "in/"), events=events, seed=seed, threads=threads)
+    gen = generate_flow_day(os.path.join(tmp, "in/"), events=events, seed=seed, threads=threads,
+                            chunk_events=chunk_events)
     t1 = time.perf_counter()
     ft = FF.load_flow(os.path.join(tmp, "in"), None, 1000, threads)
     t2 = time.perf_counter()

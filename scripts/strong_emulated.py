@@ -34,6 +34,9 @@ CONFIGS = {
     "k50": dict(kind="flow", events=1_000_000, K=50, label="config 3: flow 1-day, K=50"),
     "dns": dict(kind="dns", events=2_000_000, K=20, label="config 4: DNS 1-day, K=20"),
     "c5shard": dict(kind="flow", events=12_500_000, K=100, label="config 5 shard: flow 12.5M events, K=100"),
+    # BASELINE config 5 itself: the month's real corpus, cut into the N ranks' shards
+    "c5": dict(kind="flow", events=100_000_000, days=30, K=100, warm_em=3, reps=3,
+               label="config 5: flow 30-day month (100M events), K=100"),
 }
 LINK_BPS = 153e9
 STEP_LAT = 10e-6
@@ -45,8 +48,28 @@ def _corpus(cfg):
         c, _ = synthetic_dns_corpus(events=cfg["events"], seed=0, device="cuda")
     else:
         from oni_ml_amd.pipeline.flow import synthetic_flow_corpus
-        c, _ = synthetic_flow_corpus(events=cfg["events"], seed=0, device="cuda")
+        days = cfg.get("days", 1)
+        c, _ = synthetic_flow_corpus(events=cfg["events"], seed=0, device="cuda", threads=16,
+                                     chunk_events=-(-cfg["events"] // days) if days > 1 else 0)
     return c
+
+
+def _exchange_model(c, bounds, K):
+    """The engine's sparse class_word exchange (parallel/dist.py VocabExchange) for these shards: rows
+    rank r sends = sum over s != r of |words(r) & words(s)|; an all_to_all over the fully connected
+    mesh moves a rank's rows over its N - 1 links at once.  Returns (max rows sent, ms, dense ms)."""
+    from oni_ml_amd.ops import hip as H
+    KS = H.padded_topics(K)
+    sets = [np.unique(c.word_idx[c.doc_ptr[d0]:c.doc_ptr[d1]]) for d0, d1 in bounds]
+    N = len(bounds)
+    cnt = np.zeros(c.num_terms, np.int32)
+    for w in sets:
+        cnt[w] += 1
+    rows = [int((cnt[w] - 1).sum()) for w in sets]     # each local word shared with cnt - 1 other ranks
+    mx = max(rows)
+    t = mx * KS * 8 / ((N - 1) * LINK_BPS) + STEP_LAT
+    dense = 2 * KS * 8 * c.num_terms / (N * LINK_BPS) + 2 * STEP_LAT
+    return mx, t, dense
 
 
 def _time_iteration(eng, lb, alpha, vmi, D, reps):
@@ -82,10 +105,11 @@ def main():
         K, D = cfg["K"], c.num_docs
         full = LDAEngine(c, K, LDASettings(), backend="hip", seed=0, precision="fp64")
         full.init_random()
-        full.em_iterations(a.warm_em, True, D, stop=False)
+        full.em_iterations(cfg.get("warm_em", a.warm_em), True, D, stop=False)
         torch.cuda.synchronize()
         lb, alpha, vmi = full.log_beta(), full.alpha, full.var_max_iter
-        t_full = _time_iteration(full, lb, alpha, vmi, D, a.reps)
+        reps = cfg.get("reps", a.reps)
+        t_full = _time_iteration(full, lb, alpha, vmi, D, reps)
         del full
         torch.cuda.empty_cache()
         lens = c.lengths()
@@ -93,7 +117,7 @@ def main():
         one = c.slice_docs(dl, dl + 1)
         e1 = LDAEngine(Corpus(one.doc_ptr, one.word_idx, one.counts, c.num_terms), K, LDASettings(), backend="hip",
                        seed=0, precision="fp64", local_shard=True)
-        t_chain = _time_iteration(e1, lb, alpha, vmi, D, a.reps)
+        t_chain = _time_iteration(e1, lb, alpha, vmi, D, reps)
         del e1
         rec = dict(label=cfg["label"], docs=D, nnz=c.nnz, vocab=c.num_terms, K=K, longest_doc=int(lens[dl]),
                    full_ms=round(t_full * 1e3, 4), chain_floor_ms=round(t_chain * 1e3, 4), ranks={})
@@ -105,7 +129,7 @@ def main():
                     sh = c.slice_docs(d0, d1)
                     e = LDAEngine(Corpus(sh.doc_ptr, sh.word_idx, sh.counts, c.num_terms), K, LDASettings(),
                                   backend="hip", seed=0, precision="fp64", local_shard=True)
-                    per.append(_time_iteration(e, lb, alpha, vmi, D, a.reps))
+                    per.append(_time_iteration(e, lb, alpha, vmi, D, reps))
                     del e
                     torch.cuda.empty_cache()
                 return per
@@ -117,6 +141,11 @@ def main():
             mesh = 0.0 if n == 1 else 2 * bytes_ / (n * LINK_BPS) + 2 * STEP_LAT
             mx = max(per)
             mc = max(per_chain) if per_chain else None
+            if n > 1:
+                xb = cb if cb is not None else shard_bounds(c.doc_ptr, n)
+                xrows, xms, _ = _exchange_model(c, xb, K)
+            else:
+                xrows, xms = 0, 0.0
             rec["ranks"][n] = dict(per_rank_ms=[round(x * 1e3, 4) for x in per], max_ms=round(mx * 1e3, 4),
                                    chain_aware_per_rank_ms=None if per_chain is None else [round(x * 1e3, 4) for x in per_chain],
                                    chain_aware_max_ms=None if mc is None else round(mc * 1e3, 4),
@@ -124,7 +153,10 @@ def main():
                                    allreduce_ring_ms=round(ring * 1e3, 4), allreduce_mesh_ms=round(mesh * 1e3, 4),
                                    iter_ms_ring=round((mx + ring) * 1e3, 4), iter_ms_mesh=round((mx + mesh) * 1e3, 4),
                                    speedup_ring=round(t_full / (mx + ring), 3), speedup_mesh=round(t_full / (mx + mesh), 3),
-                                   chain_bound_speedup=round(t_full / max(t_chain, 1e-12), 3))
+                                   chain_bound_speedup=round(t_full / max(t_chain, 1e-12), 3),
+                                   sparse_exchange_rows=xrows, sparse_exchange_ms=round(xms * 1e3, 4),
+                                   iter_ms_sparse=round(((mc if mc is not None else mx) + xms) * 1e3, 4),
+                                   speedup_sparse=round(t_full / ((mc if mc is not None else mx) + xms), 3))
             print(json.dumps(dict(config=name, n=n, **rec["ranks"][n])), flush=True)
         out[name] = rec
         del c
@@ -139,15 +171,16 @@ def main():
                      f"words; one GPU {rec['full_ms']} ms / EM iteration; **chain floor** (longest document alone) "
                      f"{rec['chain_floor_ms']} ms = at most {rec['full_ms'] / max(rec['chain_floor_ms'], 1e-9):.2f}x")
             L.append("")
-            L.append("| N | max shard ms | per-rank ms | all-reduce ring / mesh ms | iteration ms (ring / mesh) | speedup (ring / mesh) | chain-aware: max shard ms, per-rank ms, speedup (mesh) |")
-            L.append("|---|---|---|---|---|---|---|")
+            L.append("| N | max shard ms | per-rank ms | all-reduce ring / mesh ms | iteration ms (ring / mesh) | speedup (ring / mesh) | chain-aware: max shard ms, per-rank ms, speedup (mesh) | sparse exchange: rows, ms, iteration ms, speedup |")
+            L.append("|---|---|---|---|---|---|---|---|")
             for n, r in rec["ranks"].items():
                 ca = "—" if not r.get("chain_aware_max_ms") else (
                     f"{r['chain_aware_max_ms']}; {' '.join(str(x) for x in r['chain_aware_per_rank_ms'])}; "
                     f"{r['chain_aware_speedup_mesh']}")
                 L.append(f"| {n} | {r['max_ms']} | {' '.join(str(x) for x in r['per_rank_ms'])} | "
                          f"{r['allreduce_ring_ms']} / {r['allreduce_mesh_ms']} | {r['iter_ms_ring']} / {r['iter_ms_mesh']} | "
-                         f"{r['speedup_ring']} / {r['speedup_mesh']} | {ca} |")
+                         f"{r['speedup_ring']} / {r['speedup_mesh']} | {ca} | {r.get('sparse_exchange_rows')}, "
+                         f"{r.get('sparse_exchange_ms')}, {r.get('iter_ms_sparse')}, {r.get('speedup_sparse')} |")
             L.append("")
         open(a.md, "w").write("\n".join(L) + "\n")
 
