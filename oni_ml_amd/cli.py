@@ -114,6 +114,8 @@ def cmd_ml_ops(argv):
     if len(a.fdate) != 8 or not a.dsource:
         print(SYNTAX)
         return 1
+    from .utils import warmup
+    warmup.early_hip_init(int(os.environ.get("LOCAL_RANK", "0")))   # HIP context while torch imports
     import torch  # noqa: F401  (first: its import time is a start-up mark of its own)
     MARKS["torch_imported"] = time.time()
     from . import config as CFG
@@ -126,6 +128,7 @@ def cmd_ml_ops(argv):
         import torch
         torch.zeros(1, device=ctx.device)     # HIP runtime + context (the first device call)
     MARKS["device_ready"] = time.time()
+    warm = warmup.start(ctx.device)           # first-stage kernels load while the inputs parse
     cfg = CFG.resolve(a.fdate, a.dsource, tol=float(a.tol) if a.tol is not None else None, conf_path=a.conf,
                       lpath=a.lpath, flow_path=a.flow_path, dns_path=a.dns_path, top1m=a.top1m, topics=a.topics,
                       alpha=a.alpha, dupfactor=a.dupfactor, gpus=ctx.world_size, backend=a.backend, compat=a.compat,
@@ -164,6 +167,8 @@ def cmd_ml_ops(argv):
             ui, rp = cfg.extra.get("UINODE"), cfg.extra.get("RPATH")
             if ui and rp:
                 subprocess.run(["scp", "-r", cfg.lpath, f"{ui}:{rp}"], check=True)
+    if warm is not None:
+        warm.join()
     ctx.shutdown()
     return 0
 

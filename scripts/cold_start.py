@@ -4,7 +4,7 @@
 Runs `python -m oni_ml_amd ml_ops 20160122 flow TOL` as fresh child processes on a synthetic day, as
 bench.py's cold leg does (ml_ops.sh times each stage as a fresh process: ml_ops.sh:57,67,80,84,108):
 
-  1. REPS plain runs: spawn -> exit wall, the start-up marks (interpreter, `import torch`, package,
+  1. REPS runs with the start-up overlaps of utils/warmup.py and REPS without (alternating): spawn -> exit wall, the start-up marks (interpreter, `import torch`, package,
      HIP context, pipeline start / end; cli.startup_marks) and the stage seconds;
   2. one run under `-X importtime`: the slowest imports (cumulative);
   3. one run under cProfile (ONI_CPROFILE): the host functions with the most cumulative time.
@@ -74,12 +74,15 @@ def main():
     try:
         generate_flow_day(os.path.join(tmp, "in/"), events=a.events, seed=7)
         runs = []
+        # alternate the start-up overlaps (utils/warmup.py) on and off, so the A/B sees the same box state
         for i in range(a.reps):
-            wall, sm, _ = _child(tmp, f"plain{i}", a.tol)
-            runs.append(dict(wall_s=round(wall, 3), inprocess_s=round(sm["wall_seconds"], 3),
-                             marks=sm.get("startup_marks"), stages={k: round(v, 3) for k, v in sm["stage_seconds"].items()},
-                             flagged=sm.get("scored")))
-            print(json.dumps(runs[-1]), flush=True)
+            for tag, env in (("overlap", {}), ("no-overlap", dict(ONI_WARMUP="0", ONI_EARLY_HIP="0"))):
+                wall, sm, _ = _child(tmp, f"{tag}{i}", a.tol, extra_env=env)
+                runs.append(dict(variant=tag, wall_s=round(wall, 3), inprocess_s=round(sm["wall_seconds"], 3),
+                                 marks=sm.get("startup_marks"),
+                                 stages={k: round(v, 3) for k, v in sm["stage_seconds"].items()},
+                                 flagged=sm.get("scored")))
+                print(json.dumps(runs[-1]), flush=True)
         _, _, err = _child(tmp, "importtime", a.tol, pyflags=("-X", "importtime"))
         imports = _importtime(err, 15)
         prof = os.path.join(tmp, "cold.prof")
@@ -98,10 +101,14 @@ def main():
             json.dump(rec, f, indent=1)
     if a.md:
         L = [f"# Cold `ml_ops` process, 1-day flow ({a.events} events)", "",
-             "| run | spawn -> exit s | in-process s | start-up marks (s after spawn) | stages s | flagged |",
-             "|---|---|---|---|---|---|"]
+             "| run | variant | spawn -> exit s | in-process s | start-up marks (s after spawn) | stages s | flagged |",
+             "|---|---|---|---|---|---|---|"]
         for i, r in enumerate(runs):
-            L.append(f"| {i} | {r['wall_s']} | {r['inprocess_s']} | {r['marks']} | {r['stages']} | {r['flagged']} |")
+            L.append(f"| {i} | {r['variant']} | {r['wall_s']} | {r['inprocess_s']} | {r['marks']} | {r['stages']} | "
+                     f"{r['flagged']} |")
+        for v in ("overlap", "no-overlap"):
+            w = sorted(r["wall_s"] for r in runs if r["variant"] == v)
+            L.append(f"\nmedian spawn -> exit, {v}: {w[len(w) // 2]} s")
         L += ["", "## Slowest imports (-X importtime, cumulative)", "", "| module | cumulative ms | self ms |",
               "|---|---|---|"]
         L += [f"| `{m['module']}` | {m['cumulative_ms']} | {m['self_ms']} |" for m in imports]
