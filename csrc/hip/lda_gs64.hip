@@ -2371,7 +2371,7 @@ __global__ __launch_bounds__((NW + 1) * 64) void gs_wsteam(GSArgs a) {
 
 // ------------------------------------------------- word team, LDS ring -------
 // gs_ring: the longest documents (kGsTeam8 with staged rows, KS <= 32) as gs_wsteam computes them,
-// with the rows streamed into an LDS ring by a dedicated LOADER WAVE (LDS-DMA: one
+// with the rows streamed into an LDS ring by NL dedicated LOADER WAVES (LDS-DMA: one
 // global_load_lds_dwordx4 moves one 1 KB topic-pair row of a 64-word staged tile).
 //
 // Why: one CU walks the longest document's rows 20 x U times per E-step, and in gs_wsteam every word
@@ -2436,6 +2436,19 @@ __device__ __forceinline__ void wait_vmcnt() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
+// wait until at most `left` tiles (IPT DMA instructions each) are in flight; left <= DEPTH
+template <int IPT, int DEPTH>
+__device__ __forceinline__ void ring_wait_tiles(int left) {
+  switch (left) {
+    case 0: wait_vmcnt<0>(); break;
+    case 1: wait_vmcnt<(DEPTH >= 1 ? IPT : 0)>(); break;
+    case 2: wait_vmcnt<(DEPTH >= 2 ? 2 * IPT : 0)>(); break;
+    case 3: wait_vmcnt<(DEPTH >= 3 ? 3 * IPT : 0)>(); break;
+    case 4: wait_vmcnt<(DEPTH >= 4 ? 4 * IPT : 0)>(); break;
+    default: wait_vmcnt<(DEPTH >= 5 ? 5 * IPT : 0)>(); break;
+  }
+}
+
 // the word wave owning tile i of a chunk: tiles round-robin over the SIMDs (wave v runs on SIMD v mod 4),
 // and over the word waves of a SIMD
 template <int NW>
@@ -2445,8 +2458,8 @@ __device__ __forceinline__ int ring_owner(int i) {
   return s + 4 * (k % per);
 }
 
-template <int KS, int NW>
-__global__ __launch_bounds__((NW + 2) * 64) void gs_ring(GSArgs a) {
+template <int KS, int NW, int NL>
+__global__ __launch_bounds__((NW + 1 + NL) * 64) void gs_ring(GSArgs a) {
   static_assert(KS <= 32 && KS % 2 == 0, "ring: KS <= 32");
   static_assert(NW >= 4, "ring: every SIMD owns tiles");
   using G = RingGeom<KS>;
@@ -2479,7 +2492,7 @@ __global__ __launch_bounds__((NW + 2) * 64) void gs_ring(GSArgs a) {
   const int W = n > 0 ? (n + U - 1) / U : 1;
   const int nch = (n + W - 1) / W;
   const float* __restrict__ crow = a.counts + s0;
-  for (int j = t; j < nch; j += (NW + 2) * 64) Cs[j] = 0.0;
+  for (int j = t; j < nch; j += (NW + 1 + NL) * 64) Cs[j] = 0.0;
   if (t < G::NSLOT) full[t] = freed[t] = 0;
   if (t < NW) arrive[t] = sarr[t] = 0;
   if (t == 0) {
@@ -2496,7 +2509,7 @@ __global__ __launch_bounds__((NW + 2) * 64) void gs_ring(GSArgs a) {
     qbase[nch] = q;
   }
   lds_barrier();
-  for (int p = t; p < n; p += (NW + 2) * 64) atomicAdd(&Cs[p / W], (double)crow[p]);   // integer counts: exact
+  for (int p = t; p < n; p += (NW + 1 + NL) * 64) atomicAdd(&Cs[p / W], (double)crow[p]);   // integer counts: exact
   lds_barrier();                           // the last barrier: from here on flags only
   double total = 0.0;
   for (int j = 0; j < nch; ++j) total += Cs[j];
@@ -2519,28 +2532,48 @@ __global__ __launch_bounds__((NW + 2) * 64) void gs_ring(GSArgs a) {
     return true;
   };
 
-  if (wv == NW + 1) {
-    // ---------------------------------------------------------------- loader wave
-    int q = 0, pub = 0, j = 0, i = 0;
+  if (wv > NW) {
+    // --------------------------------------------------------------- loader waves
+    // loader l streams items l, l + NL, l + 2 NL, ...: c_ tiles issued, cp tiles published
+    __builtin_amdgcn_s_setprio(2);         // issue as soon as a slot frees (below the topic wave)
+    const int l = wv - (NW + 1);
+    int c_ = 0, cp = 0, j = 0, i = 0;
     int n0 = 0, nt = nch > 0 ? qbase[1] : 0;
-    auto publish_to = [&](int upto) {      // items [pub, upto) have landed (the caller's vmcnt wait)
-      for (; pub < upto; ++pub)
-        if (lane == 0) __hip_atomic_store(&full[pub % G::NSLOT], pub + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    auto advance = [&]() {                 // (j, i) <- the stream's next tile (chunks, then sweeps, cyclic)
+      if (++i == nt) {
+        i = 0;
+        if (++j == nch) j = 0;
+        n0 = j * W;
+        nt = qbase[j + 1] - qbase[j];
+      }
     };
+    auto item = [&](int cc) { return l + NL * cc; };
+    auto publish_to = [&](int upto) {      // own tiles [cp, upto) have landed (the caller's vmcnt wait)
+      for (; cp < upto; ++cp)
+        if (lane == 0)
+          __hip_atomic_store(&full[item(cp) % G::NSLOT], item(cp) + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    };
+    if (nch > 0)
+      for (int u = 0; u < l; ++u) advance();
     while (nch > 0) {
       if (__hip_atomic_load(&stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) ||
           __hip_atomic_load(&abort_, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP))
         break;
+      const int q = item(c_);
       const int slot = q % G::NSLOT;
       if (q >= G::NSLOT &&
           __hip_atomic_load(&freed[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < q - G::NSLOT + 1) {
-        // the slot's previous tile is still being read: land and publish everything in flight first
-        // (a word wave may be waiting for exactly those), then wait for the slot
-        wait_vmcnt<0>();
-        publish_to(q);
+        // the slot's previous tile is still being read: while waiting, land and publish the own tiles in
+        // flight one at a time, oldest first (a word wave may be waiting for exactly those) -- never a
+        // full drain, so the load pipe stays as deep as the free slots allow
         bool quit = false;
         int spins = 0;
         while (__hip_atomic_load(&freed[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < q - G::NSLOT + 1) {
+          if (cp < c_) {
+            ring_wait_tiles<G::IPT, G::DEPTH>(c_ - cp - 1);
+            publish_to(cp + 1);
+            continue;
+          }
           if (__hip_atomic_load(&stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) ||
               __hip_atomic_load(&abort_, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) { quit = true; break; }
           if (++spins > kRingSpinLimit) {
@@ -2560,16 +2593,11 @@ __global__ __launch_bounds__((NW + 2) * 64) void gs_ring(GSArgs a) {
       for (int k = 0; k < G::PAIRS; ++k) glds16(src + k * 64, dst + (unsigned)(k * 1024));
       const int pc = min(tile * 64 + lane, n - 1);     // the last tile's lanes past the document end
       glds4(crow + pc, dst + (unsigned)G::ROWB);
-      ++q;
-      if (++i == nt) {                     // next chunk (and sweep)
-        i = 0;
-        if (++j == nch) j = 0;
-        n0 = j * W;
-        nt = qbase[j + 1] - qbase[j];
-      }
-      if (q - pub > G::DEPTH) {
-        wait_vmcnt<G::DEPTH * G::IPT>();   // all but the last DEPTH tiles have landed
-        publish_to(q - G::DEPTH);
+      ++c_;
+      for (int u = 0; u < NL; ++u) advance();
+      if (c_ - cp > G::DEPTH) {
+        wait_vmcnt<G::DEPTH * G::IPT>();   // all but the last DEPTH own tiles have landed
+        publish_to(c_ - G::DEPTH);
       }
     }
     wait_vmcnt<0>();                       // no LDS-DMA may land after the workgroup's waves are gone
@@ -3041,8 +3069,12 @@ static void gs_estep_ks(const GSArgs& a, int variant, hipStream_t s) {
         const char* ring_env = std::getenv("ONI_GS_RING");
         const int ring = ring_env ? std::atoi(ring_env) : 0;
         if (a.stage != nullptr && ring) {
-          if constexpr (KS % 2 == 0)
-            hipLaunchKernelGGL((gs::gs_ring<KS, 7>), dim3(a.n_items), dim3(576), 0, s, a);
+          if constexpr (KS % 2 == 0) {
+            if (ring >= 2)   // ONI_GS_RING=2: two loader waves (twice the LDS-DMA in flight)
+              hipLaunchKernelGGL((gs::gs_ring<KS, 7, 2>), dim3(a.n_items), dim3(640), 0, s, a);
+            else
+              hipLaunchKernelGGL((gs::gs_ring<KS, 7, 1>), dim3(a.n_items), dim3(576), 0, s, a);
+          }
           else
             throw std::runtime_error("gs_estep: ring needs an even KS");
         } else if (a.stage != nullptr) {

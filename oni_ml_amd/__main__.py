@@ -7,4 +7,13 @@ from . import cli  # noqa: E402
 
 cli.MARKS["main"] = _T_MAIN
 cli.MARKS["cli_imported"] = time.time()
-sys.exit(cli.main())
+rc = cli.main()
+if cli.FAST_EXIT:
+    # ml_ops finished: every output file is closed and the process group is gone.  Leave without the
+    # interpreter's and the HIP runtime's teardown (~0.5 s of a cold run's wall, profiles/r4_cold_start.md);
+    # ONI_FAST_EXIT=0 keeps the full teardown
+    import os
+    sys.stdout.flush()
+    sys.stderr.flush()
+    os._exit(rc or 0)
+sys.exit(rc)

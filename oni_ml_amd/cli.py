@@ -29,6 +29,8 @@ import time
 # first import; ml_ops adds the rest.  ONI_T_SPAWN (set by a parent that launches this process, e.g. bench.py's
 # cold run) is the spawn time, so interpreter start-up is measured too (startup_marks in run_summary.json).
 MARKS = {}
+# set by a completed ml_ops when ONI_FAST_EXIT (default 1) allows `python -m oni_ml_amd` to skip teardown
+FAST_EXIT = False
 
 
 def startup_marks() -> dict:
@@ -170,6 +172,8 @@ def cmd_ml_ops(argv):
     if warm is not None:
         warm.join()
     ctx.shutdown()
+    global FAST_EXIT
+    FAST_EXIT = os.environ.get("ONI_FAST_EXIT", "1") != "0"
     return 0
 
 

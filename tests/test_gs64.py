@@ -220,10 +220,11 @@ def test_staged_rows_bitwise_equal_beta_rows(monkeypatch):
         assert np.array_equal(a, b)
 
 
+@pytest.mark.parametrize("loaders", ["1", "2"])
 @pytest.mark.parametrize("K,vconv", [(20, -1e30), (20, 1e-6), (24, -1e30), (8, -1e30), (32, -1e30)])
-def test_ring_kernel_matches_oracle(monkeypatch, K, vconv):
-    """gs_ring (ONI_GS_RING=1: the staged longest documents streamed through an LDS ring by a loader
-    wave, flags instead of barriers) against the CPU oracle of the same schedule: gamma, likelihoods,
+def test_ring_kernel_matches_oracle(monkeypatch, K, vconv, loaders):
+    """gs_ring (ONI_GS_RING=1 / 2: the staged longest documents streamed through an LDS ring by one / two
+    loader waves, flags instead of barriers) against the CPU oracle of the same schedule: gamma, likelihoods,
     sweeps and the sufficient statistics of its c.phi rows at 1e-10; and against gs_wsteam to rounding."""
     rng = np.random.default_rng(11 + K)
     V, D = 20000, 150
@@ -236,13 +237,13 @@ def test_ring_kernel_matches_oracle(monkeypatch, K, vconv):
     alpha = 0.41
     ref = _oracle(c, lb, alpha, LDASettings(var_max_iter=7, var_converged=vconv), 32)
     out = {}
-    for ring in ("1", "0"):
+    for ring in (loaders, "0"):
         monkeypatch.setenv("ONI_GS_RING", ring)
         eng, sc = _gpu_estep(c, K, lb, alpha, LDASettings(var_max_iter=7, var_converged=vconv), 32)
         assert eng._stages, "the team8 bucket must be staged for the ring kernel"
         out[ring] = (eng.gamma[:, :K].cpu().numpy(), eng.lik.cpu().numpy(), eng.iters.cpu().numpy(),
                      eng._cw_local[:, :K].cpu().numpy(), sc)
-    g, lik, it, cw, sc = out["1"]
+    g, lik, it, cw, sc = out[loaders]
     same = it == ref["iters"]
     assert same[:6].all() and same.mean() > 0.99
     assert _rel(g[same], ref["gamma"][same], 1e-12) < 1e-10
