@@ -198,16 +198,22 @@ def _e2e_cold(args, ctx, tmp):
            "--gpus", str(ctx.world_size), "--topics", str(args.topics), "--backend", args.backend, "--quiet"]
     if args.device == "cuda":
         torch.cuda.empty_cache()     # this process's cached blocks back to the device for the child
-    ctx.barrier()
-    t0 = time.perf_counter()
-    env["ONI_T_SPAWN"] = repr(time.time())
-    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=args.e2e_timeout)
-    wall = time.perf_counter() - t0
-    if r.returncode != 0:
-        raise RuntimeError(f"cold ml_ops child (rank {ctx.rank}) exited {r.returncode}:\n{r.stderr[-3000:]}")
-    ctx.barrier()
-    wall = ctx.allreduce_max(wall)
-    out = dict(e2e_cold_wall_s=round(wall, 3), e2e_cold_cmd=" ".join(cmd[1:6]))
+    # two children: the first on this machine also fills the per-user bytecode cache (the image's own
+    # torch bytecode is stale and read-only on the boxes, oni_ml_amd/utils/pycache.py), as a deployment's
+    # first-ever run does; the second is the daily run's fresh process -- the reported e2e_cold_wall_s
+    walls = []
+    for _ in range(2):
+        ctx.barrier()
+        t0 = time.perf_counter()
+        env["ONI_T_SPAWN"] = repr(time.time())
+        r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=args.e2e_timeout)
+        wall = time.perf_counter() - t0
+        if r.returncode != 0:
+            raise RuntimeError(f"cold ml_ops child (rank {ctx.rank}) exited {r.returncode}:\n{r.stderr[-3000:]}")
+        ctx.barrier()
+        walls.append(ctx.allreduce_max(wall))
+    first, wall = walls
+    out = dict(e2e_cold_wall_s=round(wall, 3), e2e_cold_first_wall_s=round(first, 3), e2e_cold_cmd=" ".join(cmd[1:6]))
     if ctx.rank == 0:
         try:
             with open(os.path.join(lpath, "run_summary.json")) as f:

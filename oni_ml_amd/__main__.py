@@ -3,6 +3,10 @@ import time
 
 _T_MAIN = time.time()      # process-level start marks (cli.startup_marks): before any package import
 
+from .utils import pycache  # noqa: E402
+
+pycache.enable()           # before anything imports torch (utils/pycache.py)
+
 from . import cli  # noqa: E402
 
 cli.MARKS["main"] = _T_MAIN

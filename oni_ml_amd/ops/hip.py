@@ -636,6 +636,8 @@ class GSPlan:
         self.plan = []
         iso = int(os.environ.get("ONI_GS_XCD", "1")) if KS <= 32 else 0
         edges = self.EDGES_NARROW if KS <= 32 and os.environ.get("ONI_GS_SMALL", "1") != "0" else self.EDGES
+        if KS > 32 and int(gs_updates) > 32:
+            edges = self.wide_u_edges(int(gs_updates))
         for var, lo, hi in edges:
             lo_ = tiny if lo is None else lo
             m = (Ls > lo_) if hi is None else ((Ls > lo_) & (Ls <= hi))
@@ -660,6 +662,21 @@ class GSPlan:
             self.plan = [(v, o if v == GS_TEAM8 else
                           torch.from_numpy(self.xcd_gaps(o.cpu().numpy(), dpb[v])).to(device))
                          for v, o in self.plan]
+
+    @classmethod
+    def wide_u_edges(cls, U: int):
+        """Team sizes by CHUNK WIDTH at K > 32 and U > 32 (the c.phi-table team kernels): a team's waves
+        split a chunk's W = ceil(n / U) words, so at lda-c's per-word schedule (U = 1024: W = 1 for every
+        document up to 1,024 words) a 4- or 8-wave team idles all but one word slot and pays two
+        workgroup barriers per word, where one wave per document refreshes in-wave with no barrier.
+        ONI_GS_WEDGES="w1,w4": one wave up to W = w1, four up to W = w4, eight beyond (never below the
+        U = 32 edges); "0" keeps the fixed length edges."""
+        spec = os.environ.get("ONI_GS_WEDGES", "4,32")
+        if spec.strip() == "0":
+            return cls.EDGES
+        w1, w4 = (int(x) for x in spec.split(","))
+        e1, e4 = max(256, w1 * U), max(2048, w4 * U)
+        return ((GS_TEAM8, e4, None), (GS_TEAM4, e1, e4), (GS_TEAM1, None, e1))
 
     @staticmethod
     def xcd_gaps(o, dpb: int, xcds: int = 8):

@@ -12,6 +12,10 @@ kernels in ``_onihip``, torch's sort / unique / scan kernels).  Two overlaps:
   stream while the main thread parses the input files on the CPU.
 
 Neither changes a result: the warm-up works on private tensors, on its own stream.
+
+Measured (profiles/r4_cold_start.md, 3 alternating A/B pairs): the warm-up thread made the cold run
+slower, not faster -- its imports and launches contend with the main thread's parsing for the GIL and
+the import lock (flow_pre 0.17-0.89 s vs 0.23-0.24 s) -- so ``start`` is off unless ONI_WARMUP=1.
 """
 from __future__ import annotations
 
@@ -46,7 +50,7 @@ def start(device):
     """Warm the first stages' GPU code on a background thread; returns the thread (or None on CPU)."""
     import torch
     device = torch.device(device)
-    if device.type != "cuda" or os.environ.get("ONI_WARMUP", "1") == "0":
+    if device.type != "cuda" or os.environ.get("ONI_WARMUP", "0") == "0":
         return None
 
     def run():

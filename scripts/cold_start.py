@@ -4,7 +4,8 @@
 Runs `python -m oni_ml_amd ml_ops 20160122 flow TOL` as fresh child processes on a synthetic day, as
 bench.py's cold leg does (ml_ops.sh times each stage as a fresh process: ml_ops.sh:57,67,80,84,108):
 
-  1. REPS runs with the start-up overlaps of utils/warmup.py and REPS without (alternating): spawn -> exit wall, the start-up marks (interpreter, `import torch`, package,
+  1. a first child (it fills the per-user bytecode cache, utils/pycache.py), then REPS rounds of the
+     start-up variants (--variants, alternating): spawn -> exit wall, the start-up marks (interpreter, `import torch`, package,
      HIP context, pipeline start / end; cli.startup_marks) and the stage seconds;
   2. one run under `-X importtime`: the slowest imports (cumulative);
   3. one run under cProfile (ONI_CPROFILE): the host functions with the most cumulative time.
@@ -45,6 +46,15 @@ def _child(tmp, tag, tol, extra_env=None, pyflags=()):
     return wall, sm, r.stderr
 
 
+def _variants(spec):
+    out = []
+    for v in spec.split(";"):
+        v = v.strip()
+        env = {} if v in ("", "default") else dict(kv.split("=", 1) for kv in v.split())
+        out.append((v or "default", env))
+    return out
+
+
 def _importtime(stderr, top):
     rows = []
     for line in stderr.splitlines():
@@ -68,25 +78,31 @@ def main():
     ap.add_argument("--tol", type=float, default=1e-5)
     ap.add_argument("--md")
     ap.add_argument("--json")
+    ap.add_argument("--variants", default="default;ONI_PYCACHE=0;ONI_FAST_EXIT=0;ONI_EARLY_HIP=0;ONI_WARMUP=1",
+                    help="';'-separated env settings (space-separated KEY=VALUE within one), 'default' = none")
+    ap.add_argument("--prof-out", help="keep the cProfile file here")
     a = ap.parse_args()
     from oni_ml_amd.synth.flow import generate_flow_day
     tmp = tempfile.mkdtemp(prefix="oni_cold_")
     try:
         generate_flow_day(os.path.join(tmp, "in/"), events=a.events, seed=7)
         runs = []
-        # alternate the start-up overlaps (utils/warmup.py) on and off, so the A/B sees the same box state
-        for i in range(a.reps):
-            for tag, env in (("overlap", {}), ("no-overlap", dict(ONI_WARMUP="0", ONI_EARLY_HIP="0"))):
-                wall, sm, _ = _child(tmp, f"{tag}{i}", a.tol, extra_env=env)
-                runs.append(dict(variant=tag, wall_s=round(wall, 3), inprocess_s=round(sm["wall_seconds"], 3),
-                                 marks=sm.get("startup_marks"),
-                                 stages={k: round(v, 3) for k, v in sm["stage_seconds"].items()},
-                                 flagged=sm.get("scored")))
-                print(json.dumps(runs[-1]), flush=True)
+        # the variants alternate, so every one sees the same box state; the first child of all also fills
+        # the per-user bytecode cache (utils/pycache.py) -- recorded as its own row, "first"
+        variants = [("first", {})] + [v for _ in range(a.reps) for v in _variants(a.variants)]
+        for i, (tag, env) in enumerate(variants):
+            wall, sm, _ = _child(tmp, f"run{i}", a.tol, extra_env=env)
+            runs.append(dict(variant=tag, wall_s=round(wall, 3), inprocess_s=round(sm["wall_seconds"], 3),
+                             marks=sm.get("startup_marks"),
+                             stages={k: round(v, 3) for k, v in sm["stage_seconds"].items()},
+                             flagged=sm.get("scored")))
+            print(json.dumps(runs[-1]), flush=True)
         _, _, err = _child(tmp, "importtime", a.tol, pyflags=("-X", "importtime"))
         imports = _importtime(err, 15)
         prof = os.path.join(tmp, "cold.prof")
         _child(tmp, "cprofile", a.tol, extra_env=dict(ONI_CPROFILE=prof))
+        if a.prof_out:
+            shutil.copy(prof, a.prof_out)
         st = pstats.Stats(prof)
         st.sort_stats("cumulative")
         fn = []
@@ -106,9 +122,9 @@ def main():
         for i, r in enumerate(runs):
             L.append(f"| {i} | {r['variant']} | {r['wall_s']} | {r['inprocess_s']} | {r['marks']} | {r['stages']} | "
                      f"{r['flagged']} |")
-        for v in ("overlap", "no-overlap"):
+        for v in dict.fromkeys(r["variant"] for r in runs):
             w = sorted(r["wall_s"] for r in runs if r["variant"] == v)
-            L.append(f"\nmedian spawn -> exit, {v}: {w[len(w) // 2]} s")
+            L.append(f"\nmedian spawn -> exit, {v}: {w[len(w) // 2]} s ({len(w)} runs)")
         L += ["", "## Slowest imports (-X importtime, cumulative)", "", "| module | cumulative ms | self ms |",
               "|---|---|---|"]
         L += [f"| `{m['module']}` | {m['cumulative_ms']} | {m['self_ms']} |" for m in imports]

@@ -55,6 +55,9 @@ def main():
     ap.add_argument("--cphi-gb", default=None, help="per-rank HBM budget of the c.phi rows")
     ap.add_argument("--no-word-assignments", action="store_true")
     ap.add_argument("--lag", default=None, help="LAG save period (lda-c: 5; 0: only 000 and final)")
+    ap.add_argument("--tol-quantile", type=float, default=None,
+                    help="calibrate TOL: a first run at --tol records the score quantiles, every listed N then runs "
+                         "at its key_q<Q> (so about Q of the events are flagged); Q in 1e-4, 1e-3, 1e-2, 0.1")
     a = ap.parse_args()
     tol = a.tol or ("1e-5" if a.source == "flow" else "1e-4")
     tmp = tempfile.mkdtemp(prefix="oni_ranks_")
@@ -74,10 +77,12 @@ def main():
                                  n_names=max(20_000, a.events // 10), n_clients=max(5_000, a.events // 40),
                                  with_edge_rows=False)
             inp = ["--dns-path", g["dns_path"], "--top1m", g["top1m"]]
-        for n in [int(x) for x in a.ranks.split(",")]:
+        ns = [int(x) for x in a.ranks.split(",")]
+        plan = ([("calibration", ns[0])] if a.tol_quantile else []) + [("run", n) for n in ns]
+        for kind, n in plan:
             lp = os.path.join(tmp, f"ml{n}")
             compat = a.compat or ("strict" if a.topics == 20 else "fixed")
-            cli = ["-m", "oni_ml_amd.cli", "ml_ops", "20160122", a.source, tol, "--lpath", lp, "--gpus", str(n),
+            cli = ["-m", "oni_ml_amd", "ml_ops", "20160122", a.source, tol, "--lpath", lp, "--gpus", str(n),
                    "--conf", "/nonexistent", "--quiet", "--backend", a.lda_backend, "--topics", str(a.topics),
                    "--compat", compat, "--threads", str(a.threads)] + inp
             if a.cphi_gb:
@@ -117,14 +122,18 @@ def main():
                     for k, v in rec.items() if k.startswith("key_q")}
             out_gb = sum(os.path.getsize(os.path.join(d, f)) for d, _, fs in os.walk(lp) for f in fs) / 1e9
             shutil.rmtree(lp, ignore_errors=True)       # (config 5 writes ~50 GB of text per run)
-            run = dict(ranks=n, process_wall_s=round(wall, 3), pipeline_wall_s=round(pw, 3),
+            run = dict(kind=kind, tol=tol, ranks=n, process_wall_s=round(wall, 3), pipeline_wall_s=round(pw, 3),
                        flagged=summ.get("scored"), rank0_key_quantiles=keyq, startup_marks=summ.get("startup_marks"), corpus=summ.get("corpus"),
                        em_iterations=summ.get("lda", {}).get("em_iterations"),
                        stage_s=[{k: round(v, 3) for k, v in p.items()} for p in per_rank],
                        rank0_serial_s=round(serial, 3) if n > 1 else None,
                        rank0_serial_share=round(serial / pw, 4) if n > 1 else None, output_gb=round(out_gb, 3))
-            out["runs"].append(run)
             print(json.dumps(run), flush=True)
+            if kind == "calibration":
+                tol = repr(float(keyq[f"key_q{a.tol_quantile:g}"]))
+                out["calibration"] = run
+                continue
+            out["runs"].append(run)
     finally:
         shutil.rmtree(tmp, ignore_errors=True)
     if a.json:
@@ -132,7 +141,8 @@ def main():
     if a.md:
         lines = [f"# Per-rank stage seconds, {a.source} day of {a.events} events (collectives: {a.backend})", ""]
         for run in out["runs"]:
-            lines.append(f"## N = {run['ranks']}: pipeline wall {run['pipeline_wall_s']} s, flagged {run['flagged']}, "
+            lines.append(f"## N = {run['ranks']}: pipeline wall {run['pipeline_wall_s']} s, TOL {run['tol']}, "
+                         f"flagged {run['flagged']}, "
                          f"EM iterations {run['em_iterations']}"
                          + (f", rank 0 serial {run['rank0_serial_s']} s = {100 * run['rank0_serial_share']:.1f} % of the wall"
                             if run["ranks"] > 1 else ""))
@@ -141,6 +151,10 @@ def main():
             lines.append("|---" * (len(STAGES[a.source]) + 1) + "|")
             for k, p in enumerate(run["stage_s"]):
                 lines.append(f"| {k} | " + " | ".join(f"{p.get(s, 0):.3f}" for s in STAGES[a.source]) + " |")
+            lines.append("")
+            lines.append(f"process wall {run['process_wall_s']} s; start-up marks {run['startup_marks']}; "
+                         f"corpus {run['corpus']}; output {run['output_gb']} GB; rank-0 score quantiles "
+                         f"{run['rank0_key_quantiles']}")
             lines.append("")
         open(a.md, "w").write("\n".join(lines) + "\n")
 
