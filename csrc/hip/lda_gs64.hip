@@ -3070,7 +3070,11 @@ static void gs_estep_ks(const GSArgs& a, int variant, hipStream_t s) {
         const int ring = ring_env ? std::atoi(ring_env) : 0;
         if (a.stage != nullptr && ring) {
           if constexpr (KS % 2 == 0) {
-            if (ring >= 2)   // ONI_GS_RING=2: two loader waves (twice the LDS-DMA in flight)
+            if (ring >= 4)   // ONI_GS_RING=N: N loader waves (N times the LDS-DMA in flight)
+              hipLaunchKernelGGL((gs::gs_ring<KS, 7, 4>), dim3(a.n_items), dim3(768), 0, s, a);
+            else if (ring == 3)
+              hipLaunchKernelGGL((gs::gs_ring<KS, 7, 3>), dim3(a.n_items), dim3(704), 0, s, a);
+            else if (ring == 2)
               hipLaunchKernelGGL((gs::gs_ring<KS, 7, 2>), dim3(a.n_items), dim3(640), 0, s, a);
             else
               hipLaunchKernelGGL((gs::gs_ring<KS, 7, 1>), dim3(a.n_items), dim3(576), 0, s, a);

@@ -74,7 +74,8 @@ def _apply_lda_args(a, st):
 
 def clean_workdir(lpath: str):
     """ml_ops.sh:53-54: remove stale *.dat,*.beta,*.gamma,*.other,*.pkl; keep *.csv (analyst feedback)."""
-    for pat in ("*.dat", "*.beta", "*.gamma", "*.other", "*.pkl", "checkpoint.npz", "final_model.npz"):
+    for pat in ("*.dat", "*.beta", "*.gamma", "*.other", "*.pkl", "checkpoint.npz", "final_model.npz",
+                "final_gamma.rank*.npz"):
         for f in glob.glob(os.path.join(lpath, pat)):
             os.unlink(f)
     shutil.rmtree(os.path.join(lpath, ".stages"), ignore_errors=True)

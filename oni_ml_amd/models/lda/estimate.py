@@ -117,6 +117,36 @@ def load_final(outdir: str):
     return ldac.load_gamma(os.path.join(outdir, "final.gamma")), lb
 
 
+def load_final_rows(outdir: str, d0: int, d1: int):
+    """(gamma rows [d0, d1), log_beta) of a finished run, exact: from the binary copies (final_model.npz;
+    a multi-rank run's per-rank final_gamma.rank<r>.npz blocks, any world size), else final.gamma's text."""
+    import glob
+    blocks = []
+    for f in glob.glob(os.path.join(outdir, "final_gamma.rank*.npz")):
+        with np.load(f, allow_pickle=False) as z:
+            a, b = (int(x) for x in z["doc_range"])
+            if a < d1 and b > d0:
+                blocks.append((a, b, z["gamma"]))
+    p = os.path.join(outdir, "final_model.npz")
+    if blocks and os.path.exists(p):
+        blocks.sort(key=lambda x: x[0])
+        covered, rows = d0, []
+        for a, b, g in blocks:
+            if a > covered:
+                break
+            rows.append(g[max(0, covered - a):min(b, d1) - a])
+            covered = min(b, d1)
+            if covered >= d1:
+                break
+        if covered >= d1:
+            with np.load(p, allow_pickle=False) as z:
+                lb = z["log_beta"]
+            K = rows[0].shape[1] if rows else lb.shape[0]
+            return (np.concatenate(rows) if rows else np.zeros((0, K))), lb
+    g, lb = load_final(outdir)
+    return g[d0:d1], lb
+
+
 def load_checkpoint(outdir: str) -> Optional[dict]:
     p = os.path.join(outdir, CKPT)
     if not os.path.exists(p):
@@ -221,6 +251,12 @@ def estimate(corpus: Corpus, num_topics: int, alpha_init: float, settings: LDASe
             part = os.path.join(outdir, f".{tag}.gamma.part{r}")
             parts.append((os.path.join(outdir, f"{tag}.gamma"), part))
             writer.submit(_after(ev_g, ldac.save_gamma), part, g)
+        if multi and tag == "final":
+            # exact binary gamma rows of this rank's documents (a resumed lda_post reads them instead of the
+            # %5.10f text of final.gamma, load_final_rows)
+            d0, d1 = e.doc_range
+            writer.submit(np.savez, os.path.join(outdir, f"final_gamma.rank{r}.npz"), gamma=g,
+                          doc_range=np.asarray([d0, d1], np.int64))
         if write_rank_gamma and tag == "final":
             writer.submit(ldac.save_gamma, os.path.join(outdir, f"{r}.gamma"), g)
             writer.submit(ldac.save_beta, os.path.join(outdir, f"{r}.beta"), e.local_log_beta())

@@ -234,11 +234,10 @@ def _lda_and_export(R, cfg, ctx, sc, names, gmap, decode, device, log, summary):
     ip_rows = None
     if not R.done("lda_post"):
         if gamma is None:
-            from ..models.lda.estimate import load_final
+            from ..models.lda.estimate import load_final_rows
             corpus, all_docs, _, (d0, d1) = _files_state(cfg, ctx)
             doc_names = all_docs[d0:d1]
-            g_all, log_beta = load_final(cfg.lpath)
-            gamma = g_all[d0:d1]
+            gamma, log_beta = load_final_rows(cfg.lpath, d0, d1)
         with R.stage("lda_post"):
             if sc is not None:
                 # nothing replicated: this rank's θ rows and vocabulary slice, the word map hash-partitioned,

@@ -20,6 +20,7 @@ import socket
 import subprocess
 import sys
 import tempfile
+import threading
 import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -52,6 +53,7 @@ def main():
     ap.add_argument("--topics", type=int, default=20)
     ap.add_argument("--compat", default=None, help="strict | fixed (default: strict at K = 20, else fixed)")
     ap.add_argument("--threads", type=int, default=8, help="native threads per rank")
+    ap.add_argument("--split-threads", action="store_true", help="--threads is the box's share: N ranks get threads / N each")
     ap.add_argument("--cphi-gb", default=None, help="per-rank HBM budget of the c.phi rows")
     ap.add_argument("--no-word-assignments", action="store_true")
     ap.add_argument("--lag", default=None, help="LAG save period (lda-c: 5; 0: only 000 and final)")
@@ -59,6 +61,13 @@ def main():
                     help="calibrate TOL: a first run at --tol records the score quantiles, every listed N then runs "
                          "at its key_q<Q> (so about Q of the events are flagged); Q in 1e-4, 1e-3, 1e-2, 0.1")
     a = ap.parse_args()
+    t_start = time.perf_counter()
+
+    def heartbeat():     # a long generation / config-5 run prints nothing for minutes otherwise
+        while True:
+            time.sleep(60)
+            print(json.dumps(dict(heartbeat_s=round(time.perf_counter() - t_start))), flush=True)
+    threading.Thread(target=heartbeat, daemon=True).start()
     tol = a.tol or ("1e-5" if a.source == "flow" else "1e-4")
     tmp = tempfile.mkdtemp(prefix="oni_ranks_")
     out = dict(source=a.source, events=a.events, backend=a.backend, runs=[])
@@ -84,7 +93,7 @@ def main():
             compat = a.compat or ("strict" if a.topics == 20 else "fixed")
             cli = ["-m", "oni_ml_amd", "ml_ops", "20160122", a.source, tol, "--lpath", lp, "--gpus", str(n),
                    "--conf", "/nonexistent", "--quiet", "--backend", a.lda_backend, "--topics", str(a.topics),
-                   "--compat", compat, "--threads", str(a.threads)] + inp
+                   "--compat", compat, "--threads", str(max(1, a.threads // n) if a.split_threads else a.threads)] + inp
             if a.cphi_gb:
                 cli += ["--cphi-gb", str(a.cphi_gb)]
             if a.no_word_assignments:

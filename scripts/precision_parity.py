@@ -119,6 +119,16 @@ def _topk_overlap(a, b, k):
     return len(ia & ib) / k
 
 
+def _tie_closed_overlap(a, b, k):
+    """Overlap of the lowest-k sets with every entry TIED (exactly equal score, same run) with the k-th
+    one included on both sides: |A* & B*| / min(|A*|, |B*|).  Entries of identical documents and words
+    score identically, so a cut through a tie group picks an arbitrary (entry-id) part of it; when two
+    runs order two near-equal groups differently, the plain overlap drops by a whole group."""
+    ta, tb = np.sort(a, kind="stable")[k - 1], np.sort(b, kind="stable")[k - 1]
+    ia, ib = np.flatnonzero(a <= ta), np.flatnonzero(b <= tb)
+    return float(np.intersect1d(ia, ib).size / max(1, min(ia.size, ib.size))), int(ia.size), int(ib.size)
+
+
 def _spearman(a, b):
     ra = np.empty(len(a)); ra[np.argsort(a, kind="stable")] = np.arange(len(a))
     rb = np.empty(len(b)); rb[np.argsort(b, kind="stable")] = np.arange(len(b))
@@ -138,6 +148,7 @@ def main():
     ap.add_argument("--gs-updates", type=int, default=32, help="U of the cpuU engine (the GPU schedule)")
     ap.add_argument("--json", default=None)
     ap.add_argument("--md", default=None)
+    ap.add_argument("--save-scores", default=None, help="npz of every engine's entry scores (re-derive metrics later)")
     args = ap.parse_args()
 
     dev = torch.device("cuda", 0) if torch.cuda.is_available() else torch.device("cpu")
@@ -171,6 +182,8 @@ def main():
         derived[name] = dict(theta=th, phi=ph, score=_entry_scores(corpus, th, ph),
                              L=np.array([x[0] for x in r["res"].likelihoods]))
     k_top = max(1, len(corpus.word_idx) // 1000)
+    if args.save_scores:
+        np.savez(args.save_scores, **{n.replace("@", "_at_").replace("#", "_x"): d["score"] for n, d in derived.items()})
     out = dict(corpus=dict(docs=corpus.num_docs, words=corpus.num_terms, entries=int(len(corpus.word_idx)),
                            events=args.events, seed=args.seed), topics=args.topics, engines={}, pairs={})
     for name, r in runs.items():
@@ -192,7 +205,13 @@ def main():
                 phi_max_abs_diff=float(np.abs(A["phi"] - B["phi"]).max()),
                 score_spearman=_spearman(A["score"], B["score"]),
                 lowest_0p1pct_overlap=_topk_overlap(A["score"], B["score"], k_top),
+                lowest_0p5pct_overlap=_topk_overlap(A["score"], B["score"], 5 * k_top),
+                lowest_1pct_overlap=_topk_overlap(A["score"], B["score"], 10 * k_top),
             )
+            tc, na, nb = _tie_closed_overlap(A["score"], B["score"], k_top)
+            out["pairs"][f"{a} vs {b}"].update(lowest_0p1pct_tie_closed_overlap=tc, tie_closed_set_sizes=f"{na}/{nb}",
+                                               distinct_scores_in_lowest_0p1pct=int(np.unique(
+                                                   np.sort(A["score"], kind="stable")[:k_top]).size))
     print(json.dumps(dict(engines={k: {kk: vv for kk, vv in v.items() if kk != "likelihood_trajectory"}
                                    for k, v in out["engines"].items()}, pairs=out["pairs"]), indent=1), flush=True)
     if args.json:

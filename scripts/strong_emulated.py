@@ -21,6 +21,7 @@ import argparse
 import json
 import os
 import sys
+import threading
 import time
 
 import numpy as np
@@ -94,6 +95,13 @@ def main():
     ap.add_argument("--json")
     ap.add_argument("--md")
     a = ap.parse_args()
+    t_start = time.perf_counter()
+
+    def heartbeat():     # config 5's corpus build prints nothing for minutes otherwise
+        while True:
+            time.sleep(60)
+            print(json.dumps(dict(heartbeat_s=round(time.perf_counter() - t_start))), flush=True)
+    threading.Thread(target=heartbeat, daemon=True).start()
     from oni_ml_amd.corpus.csr import Corpus
     from oni_ml_amd.models.lda.em import LDAEngine
     from oni_ml_amd.models.lda.settings import LDASettings

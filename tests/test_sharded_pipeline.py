@@ -32,6 +32,7 @@ def _cfg(kind, indir, lpath, extra):
     cfg.settings = LDASettings(em_max_iter=6)
     if extra.get("compat"):
         cfg.compat = extra["compat"]
+    cfg.resume = bool(extra.get("resume"))
     return cfg
 
 
@@ -102,6 +103,34 @@ def test_sharded_flow_pipeline_bytes_equal_one_process(flow_day, compat, tmp_pat
             recs = [json.loads(l) for l in (lp / f"metrics.rank{r}.jsonl").read_text().splitlines()]
             ran = {x["stage"] for x in recs if x.get("status") == "ok"}
             assert {"load", "flow_pre", "lda_pre", "lda", "lda_post", "flow_post"} <= ran, ran
+
+
+@pytest.mark.parametrize("world,after", [(2, "lda_pre"), (3, "lda_pre"), (3, "lda")])
+def test_sharded_flow_resume_bytes_equal_one_process(flow_day, world, after, tmp_path):
+    """A sharded run resumed after lda_pre (the lda stage reloads the corpus files on every rank, the
+    engine shards them by its own rule) or after lda (gamma sliced from final.gamma, the scorers index
+    the document rows through doc_results.csv) writes the files of an uninterrupted one-process run."""
+    extra = dict(tol=1e-3, compat="fixed")
+    one = tmp_path / "w1"
+    one.mkdir()
+    os.link(flow_day / "fb.csv", one / "flow_scores.csv")
+    r1 = _run(1, "flow", str(flow_day / "in"), str(one), extra)
+    lp = tmp_path / f"w{world}"
+    lp.mkdir()
+    os.link(flow_day / "fb.csv", lp / "flow_scores.csv")
+    _run(world, "flow", str(flow_day / "in"), str(lp), extra)
+    later = ["lda", "lda_post", "flow_post"][(1 if after == "lda" else 0):]
+    outputs = {"lda": ["final.beta", "final.gamma", "final.other", "likelihood.dat", "word-assignments.dat"],
+               "lda_post": ["doc_results.csv", "word_results.csv"], "flow_post": ["flow_results.csv"]}
+    for st in later:
+        os.unlink(lp / ".stages" / f"{st}.done")
+        for f in outputs[st]:
+            os.unlink(lp / f)
+    rn = _run(world, "flow", str(flow_day / "in"), str(lp), dict(extra, resume=True))
+    assert all(o == r1[0][1] for _, o in rn)
+    for f in FLOW_FILES:
+        a, b = (one / f).read_bytes(), (lp / f).read_bytes()
+        assert a == b, (world, after, f, len(a), len(b))
 
 
 def _dns_feedback(path, dns_path, n=10):
