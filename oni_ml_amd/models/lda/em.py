@@ -85,6 +85,12 @@ def _cpu_threads() -> int:
     """Threads of the C++ lda-c engine (its result does not depend on the count)."""
     return int(os.environ.get("ONI_CPU_THREADS", min(8, os.cpu_count() or 1)))
 
+def _hbm_total(device) -> int:
+    """The device's HBM bytes from hipMemGetInfo.  (torch.cuda.get_device_properties first counts the
+    devices through amd-smi: 0.11 s of a cold ml_ops process, profiles/r4_cold_start.md.)"""
+    return int(torch.cuda.mem_get_info(device)[1])
+
+
 class LDAEngine:
     def __init__(self, corpus: Corpus, num_topics: int, settings: Optional[LDASettings] = None,
                  alpha_init: float = 2.5, backend: str = "auto", device=None, dist=None, seed: int = 0,
@@ -248,7 +254,7 @@ class LDAEngine:
         out["exchange_seconds_per_iter"] = self.comm_seconds() / n if n else 0.0
         if self.device.type == "cuda":
             out["peak_hbm_bytes"] = int(torch.cuda.max_memory_allocated(self.device))
-            out["hbm_total_bytes"] = int(torch.cuda.get_device_properties(self.device).total_memory)
+            out["hbm_total_bytes"] = _hbm_total(self.device)
         if seconds and em_iterations:
             out["docs_per_sec"] = self.global_docs * em_iterations / seconds
         return out
@@ -375,7 +381,7 @@ class LDAEngine:
         if gb is None and os.environ.get("ONI_CPHI_GB"):
             gb = float(os.environ["ONI_CPHI_GB"])
         if gb is None:
-            total = torch.cuda.get_device_properties(self.device).total_memory if self.device.type == "cuda" else 0
+            total = _hbm_total(self.device) if self.device.type == "cuda" else 0
             if not total or nnz * row_bytes <= 0.35 * total:
                 return None
             gb = 0.25 * total / 2**30

@@ -670,8 +670,9 @@ class GSPlan:
         document up to 1,024 words) a 4- or 8-wave team idles all but one word slot and pays two
         workgroup barriers per word, where one wave per document refreshes in-wave with no barrier.
         ONI_GS_WEDGES="w1,w4": one wave up to W = w1, four up to W = w4, eight beyond (never below the
-        U = 32 edges); "0" keeps the fixed length edges."""
-        spec = os.environ.get("ONI_GS_WEDGES", "4,32")
+        U = 32 edges); "0" keeps the fixed length edges.  K = 100 shard at U = 1024 (profiles/r4_tuning_log.md):
+        fixed edges 172.4 ms per EM iteration, "8,64" 133.2, "4,32" 107.3, "2,16" 106.7 (the default)."""
+        spec = os.environ.get("ONI_GS_WEDGES", "2,16")
         if spec.strip() == "0":
             return cls.EDGES
         w1, w4 = (int(x) for x in spec.split(","))
