@@ -697,14 +697,16 @@ __global__ __launch_bounds__(team_threads(KS, NW), MINW) void gs_team(GSArgs a) 
       Cn[o] = (k < KS && nch > 0) ? a.cphi[(size_t)s0 * KS + k] : 0.0;
     }
   }
-  // chunk-ahead prefetch: the word ids of chunk j + 2 and the beta rows of chunk j + 1 are in
-  // flight while chunk j reduces and refreshes (chunks wrap into the next sweep).  Loads are
-  // unconditional (clamped indices) and their values are first used a chunk later: vmcnt is
-  // in-order, so consuming a load early would also wait for every prefetch issued before it.
-  // A round without a word has count 0 (its row is a real but unused one).
-  int wc[RMAX], wn[RMAX];
-  float cc[RMAX], cn[RMAX];
-  unsigned vc = 0, vn = 0;                    // valid-round masks
+  // chunk-ahead prefetch: the beta rows of chunk j + 1 are in flight while chunk j reduces and
+  // refreshes (chunks wrap into the next sweep); chunk j + 1's word ids are loaded at the START of
+  // chunk j (after its counts left the registers) and land during its word phase.  (Ids loaded two
+  // chunks ahead just before the barrier had to be rotated into the loop-carried registers at the
+  // loop latch, and that copy made the compiler wait for every outstanding load -- the row prefetch
+  // included -- before barrier 1, putting the row latency in front of the refresh.)  Loads are
+  // unconditional (clamped indices); a round without a word has count 0 (its row is real but unused).
+  int wc[RMAX];
+  float cc[RMAX];
+  unsigned vc = 0;                            // valid-round mask
   double bc[RMAX][KPL];
   auto load_ids = [&](int j, int (&w)[RMAX], float (&c)[RMAX], unsigned& v) {
     const int n0 = j * W, n1 = min(n, n0 + W);
@@ -732,7 +734,6 @@ __global__ __launch_bounds__(team_threads(KS, NW), MINW) void gs_team(GSArgs a) 
   if (nch > 0) {
     load_ids(0, wc, cc, vc);
     load_rows(wc);
-    load_ids(nch > 1 ? 1 : 0, wn, cn, vn);
   }
   team_sync<NW>();
   double L = 0.0, L_old = 0.0, conv = 1.0, GS = 0.0;
@@ -756,6 +757,11 @@ __global__ __launch_bounds__(team_threads(KS, NW), MINW) void gs_team(GSArgs a) 
       ph[7] += timer ? 1 : 0;
       if (active) {
         const int n0 = j * W, n1 = min(n, n0 + W);
+        // this chunk's counts out of the id registers, then the next chunk's ids into them
+        double cr[RMAX];
+#pragma unroll
+        for (int r = 0; r < RMAX; ++r) cr[r] = ((vc >> r) & 1u) ? (double)cc[r] : 0.0;
+        load_ids(j + 1 < nch ? j + 1 : 0, wc, cc, vc);
         double E[KPL], acc[KPL];
 #pragma unroll
         for (int i = 0; i < KPL; ++i) {
@@ -764,9 +770,6 @@ __global__ __launch_bounds__(team_threads(KS, NW), MINW) void gs_team(GSArgs a) 
         }
         // rounds of this chunk (team-uniform): pairs of words in flight per slot
         const int R = (n1 - n0 + NS - 1) / NS;
-        double cr[RMAX];
-#pragma unroll
-        for (int r = 0; r < RMAX; ++r) cr[r] = ((vc >> r) & 1u) ? (double)cc[r] : 0.0;
         if constexpr (RMAX == 1) {
           word_steps<1, KPL, LSW>(E, bc, cr, acc, lw);
         } else if (R > 2) {
@@ -778,17 +781,8 @@ __global__ __launch_bounds__(team_threads(KS, NW), MINW) void gs_team(GSArgs a) 
         // batches of RMAX rows per slot with a batch's loads in flight together (bc is free until
         // the next chunk's prefetch below); one row at a time left the word phase latency-bound
         stream_tail<RMAX, KS, KPL, TG, LSW>(a.beta, wrow, crow, n0 + slot + RMAX * NS, n1, NS, q, E, bc, acc, lw);
-        // next chunk's rows (ids already here), then the ids after it
-        const int j1 = j + 1 < nch ? j + 1 : 0;
-        const int j2 = j1 + 1 < nch ? j1 + 1 : 0;
-#pragma unroll
-        for (int r = 0; r < RMAX; ++r) {
-          wc[r] = wn[r];
-          cc[r] = cn[r];
-        }
-        vc = vn;
+        // next chunk's rows (its ids landed during the word phase)
         load_rows(wc);
-        load_ids(j2, wn, cn, vn);
         tick(0);
         // whole active waves; a one-word chunk (lda-c's per-word schedule: every chunk of a document of
         // <= U words) has its word in slot 0 and exact zeros in the other slots, so the sum is slot 0's
@@ -2231,10 +2225,15 @@ __global__ __launch_bounds__((NW + 1) * 64) void gs_wsteam(GSArgs a) {
       }
     }
   };
+  // EP == 0: chunk j + 1's ids / counts are loaded at the START of chunk j (after its counts left the
+  // registers) and land during the word phase, so the loop carries registers loaded a whole word phase
+  // before the latch.  (Loaded two chunks ahead right after the row prefetch, they were rotated into the
+  // loop-carried registers at the latch, and that copy made the compiler wait there for every outstanding
+  // load -- the row prefetch included -- before barrier B.)  EP > 0 keeps the two-ahead ids it needs.
   if (nch > 0) {
     load_ids(0, wc, cc, vc);
     load_rows(wc, vc);
-    load_ids(nch > 1 ? 1 : 0, wn, cn, vn);
+    if constexpr (EP > 0) load_ids(nch > 1 ? 1 : 0, wn, cn, vn);
   }
   lds_barrier();   // (1)
   while (var_continue(conv, vconv, it, vmi)) {
@@ -2253,6 +2252,7 @@ __global__ __launch_bounds__((NW + 1) * 64) void gs_wsteam(GSArgs a) {
         }
 #pragma unroll
         for (int r = 0; r < RMAX; ++r) cr[r] = ((vc >> r) & 1u) ? (double)cc[r] : 0.0;
+        if constexpr (EP == 0) load_ids(j + 1 < nch ? j + 1 : 0, wc, cc, vc);
         // dot, reciprocal and axpy now; log P after barrier A (beside the refresh)
 #pragma unroll
         for (int u = 0; u < RMAX; ++u) {
@@ -2303,28 +2303,30 @@ __global__ __launch_bounds__((NW + 1) * 64) void gs_wsteam(GSArgs a) {
         // prefetch of the next chunk's rows: a chunk's ~700 row gathers keep the CU's address unit busy
         // for ~2k cycles (64 B/clk) and the issuing wave blocks until they are queued -- now beside the
         // refresh instead of before it
-        const int j1 = j + 1 < nch ? j + 1 : 0;
-        const int j2 = j1 + 1 < nch ? j1 + 1 : 0;
-#pragma unroll
-        for (int r = 0; r < RMAX; ++r) {
-          wc[r] = wn[r];
-          cc[r] = cn[r];
-        }
-        vc = vn;
         if constexpr (EP == 0) {
           load_rows(wc, vc);
-        } else if (active) {
+        } else {
+          const int j1 = j + 1 < nch ? j + 1 : 0;
+          const int j2 = j1 + 1 < nch ? j1 + 1 : 0;
 #pragma unroll
-          for (int r = EP; r < RMAX; ++r) {
-            if ((vc >> r) & 1u) {
-              load_row(wc[r], bc[r]);
-            } else {
+          for (int r = 0; r < RMAX; ++r) {
+            wc[r] = wn[r];
+            cc[r] = cn[r];
+          }
+          vc = vn;
+          if (active) {
 #pragma unroll
-              for (int kk = 0; kk < KS; ++kk) bc[r][kk] = 0.0;
+            for (int r = EP; r < RMAX; ++r) {
+              if ((vc >> r) & 1u) {
+                load_row(wc[r], bc[r]);
+              } else {
+#pragma unroll
+                for (int kk = 0; kk < KS; ++kk) bc[r][kk] = 0.0;
+              }
             }
           }
+          load_ids(j2, wn, cn, vn);
         }
-        load_ids(j2, wn, cn, vn);
         tick(2);
 #pragma unroll
         for (int u = 0; u < RMAX; ++u) lw = fma(cr[u], flog(P[u]), lw);

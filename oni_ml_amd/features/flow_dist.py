@@ -7,8 +7,8 @@ the single-process pipeline looks at all rows at once -- always through tensor c
 (parallel/shardio.py), never pickled objects:
 
 * IP dictionary -- ids in global first-appearance order: every rank's dictionary (local
-  first-appearance order) packed into fixed-width integer rows, all-gathered, merged with one
-  ``torch.unique(dim=0)`` (``shardio.first_appearance``);
+  first-appearance order) packed into fixed-width integer rows, hash-partitioned over the ranks and
+  merged by each owner with ``shardio.unique_rows`` (``shardio.first_appearance``);
 * ECDF cuts -- each rank's weighted value histogram (distinct values, summed integer weights) is
   all-gathered and merged; the cut rule runs on the merged histogram, which is exactly the weighted
   multiset the single-process ecdf_cuts sees;

@@ -314,10 +314,10 @@ class DistDict:
         recv = alltoallv(ctx, [send[cuts[d]:cuts[d + 1]] for d in range(N)]) if N > 1 else [send]
         allr = np.concatenate(recv) if recv else send[:0]
         if allr.shape[0]:
-            u, inv = torch.unique(torch.from_numpy(np.ascontiguousarray(allr[:, :-1])), dim=0, return_inverse=True)
-            v = torch.full((u.shape[0],), -1, dtype=torch.int64).scatter_reduce_(
-                0, inv, torch.from_numpy(np.ascontiguousarray(allr[:, -1])), reduce="amax")
-            self.keys, self.vals = u.numpy(), v.numpy()
+            u, inv = unique_rows(np.ascontiguousarray(allr[:, :-1]))
+            v = np.full(u.shape[0], -1, np.int64)
+            np.maximum.at(v, inv, allr[:, -1])
+            self.keys, self.vals = u, v
         else:
             self.keys, self.vals = allr[:, :-1], np.zeros(0, np.int64)
 
@@ -351,9 +351,7 @@ class DistDict:
         allq = np.concatenate(recv) if recv else q[:0]
         ans = np.full(allq.shape[0], -1, np.int64)
         if allq.shape[0] and self.keys.shape[0]:
-            both = torch.from_numpy(np.ascontiguousarray(np.concatenate([self.keys, allq])))
-            _, inv = torch.unique(both, dim=0, return_inverse=True)
-            inv = inv.numpy()
+            _, inv = unique_rows(np.ascontiguousarray(np.concatenate([self.keys, allq])))
             val_u = np.full(int(inv.max()) + 1, -1, np.int64)
             val_u[inv[:self.keys.shape[0]]] = self.vals
             ans = val_u[inv[self.keys.shape[0]:]]
@@ -374,6 +372,31 @@ def _row_hash(rows64: np.ndarray) -> np.ndarray:
             h = (h ^ rows64[:, j].view(np.uint64)) * np.uint64(0x9E3779B97F4A7C15)
             h ^= h >> np.uint64(29)
     return h
+
+
+def unique_rows(rows64: np.ndarray) -> Tuple[np.ndarray, np.ndarray]:
+    """(distinct rows, inverse) of an int64 [n, c] array, rows grouped by a 64-bit hash (one argsort of
+    n keys) and checked for equality within each hash run; a run that mixes rows (a hash collision)
+    falls back to a lexicographic sort.  (torch.unique(dim=0) on the host took 13.8 s for 3 M rows of
+    3 columns here, this 0.5 s: the 8-rank config-5 flow_pre spent minutes in it, profiles/r4_config5.md.)"""
+    n = rows64.shape[0]
+    h = _row_hash(rows64)
+    o = np.argsort(h, kind="stable")
+    hs, ks = h[o], rows64[o]
+    new_h = np.empty(n, bool)
+    new_h[0] = True
+    np.not_equal(hs[1:], hs[:-1], out=new_h[1:])
+    new_r = np.empty(n, bool)
+    new_r[0] = True
+    np.any(ks[1:] != ks[:-1], axis=1, out=new_r[1:])
+    if np.any(new_r & ~new_h):          # equal hashes, different rows: sort the rows themselves
+        o = np.lexsort(rows64.T[::-1])
+        ks = rows64[o]
+        new_r[1:] = np.any(ks[1:] != ks[:-1], axis=1)
+    gid = np.cumsum(new_r) - 1
+    inv = np.empty(n, np.int64)
+    inv[o] = gid
+    return ks[new_r], inv
 
 
 def first_appearance(ctx, data: np.ndarray, off: np.ndarray) -> Tuple[DistNameTable, np.ndarray]:
@@ -408,10 +431,9 @@ def first_appearance(ctx, data: np.ndarray, off: np.ndarray) -> Tuple[DistNameTa
     allr = np.concatenate(recv) if recv else send[:0]
     # ---- owner: distinct names, minimum position
     if allr.shape[0]:
-        uniq, inv = torch.unique(torch.from_numpy(np.ascontiguousarray(allr[:, :-1])), dim=0, return_inverse=True)
-        minpos = torch.full((uniq.shape[0],), np.iinfo(np.int64).max, dtype=torch.int64).scatter_reduce_(
-            0, inv, torch.from_numpy(np.ascontiguousarray(allr[:, -1])), reduce="amin").numpy()
-        uniq, inv = uniq.numpy(), inv.numpy()
+        uniq, inv = unique_rows(np.ascontiguousarray(allr[:, :-1]))
+        minpos = np.full(uniq.shape[0], np.iinfo(np.int64).max, np.int64)
+        np.minimum.at(minpos, inv, allr[:, -1])
     else:
         uniq, inv, minpos = allr[:, :-1], np.zeros(0, np.int64), np.zeros(0, np.int64)
     # ---- global ids: first positions counted in position order, across the ranks' position ranges
