@@ -343,6 +343,7 @@ PYBIND11_MODULE(_oninative, m) {
       auto work = [&](int t) {
         std::string s;
         for (int64_t i = n * t / threads; i < n * (t + 1) / threads; ++i) {
+          if (mode == 1 && py2_value(src[i], dst + i)) continue;     // no text needed
           s.clear();
           if (mode == 0) append_fixed10(s, src[i], dst + i);
           else append_py2_float(s, src[i], dst + i);

@@ -230,6 +230,36 @@ inline char* put_py2_float(char* w, double d, double* back = nullptr) {
   return w;
 }
 
+// The value a reader parses from Python 2 str(d), without the text: the 12 significant digits N and
+// decade E exactly as put_py2_float computes them, then N / 10^(11 - E) -- one correctly rounded
+// division of exact operands, the same double strtod returns for the digits (Clinger; trailing zeros
+// do not change the real number).  False outside 1e-11 <= |d| < 1e11 (the caller formats and parses).
+inline bool py2_value(double d, double* out) {
+  const double a = std::fabs(d);
+  if (!(a >= 1e-11 && a < 1e11)) return false;
+  uint64_t bits;
+  std::memcpy(&bits, &a, 8);
+  const int e2 = (int)((bits >> 52) & 0x7ff) - 1022;
+  int E = (int)std::floor((e2 - 1) * 0.30102999566398120);
+  if (a >= ten_pow(E + 1)) ++E;
+  for (int tries = 0; tries < 3; ++tries) {
+    const int k = 11 - E;
+    if (k < 0 || k > 22) return false;
+    int64_t N = scaled_round(a, k);
+    if (N < 100000000000LL) { --E; continue; }
+    if (N >= 1000000000000LL) {
+      if (N == 1000000000000LL) { N = 100000000000LL; ++E; }
+      else { ++E; continue; }
+    }
+    const int kk = 11 - E;
+    if (kk < 0 || kk > 22) return false;
+    const double v = (double)N / pow10_table()[kk];
+    *out = d < 0 ? -v : v;
+    return true;
+  }
+  return false;
+}
+
 inline void append_py2_float(std::string& out, double d, double* back = nullptr) {
   char buf[40];
   out.append(buf, put_py2_float(buf, d, back) - buf);

@@ -14,6 +14,7 @@ bytes (the ``dtype="S20"`` array, lda_post.py:78-84) and K must be 20
 """
 from __future__ import annotations
 
+import os
 from typing import Sequence, Tuple
 
 import numpy as np
@@ -21,28 +22,66 @@ import numpy as np
 from ..ops import native
 
 
+def _host_threads() -> int:
+    return max(1, int(os.environ.get("ONI_HOST_THREADS", min(16, os.cpu_count() or 1))))
+
+
+def _par(fn, n: int, min_block: int = 1 << 15):
+    """fn(lo, hi) over [0, n) in blocks on a thread pool (numpy ufuncs release the GIL).  Every
+    operation split this way is elementwise or per row, so the results are bitwise those of one call:
+    config 5's θ / φ (5.7 M x 100 and 100 x 4.5 M) took ~10 s of numpy on one core."""
+    t = min(_host_threads(), max(1, n // min_block))
+    if t <= 1:
+        fn(0, n)
+        return
+    from concurrent.futures import ThreadPoolExecutor
+    cuts = [n * i // t for i in range(t + 1)]
+    with ThreadPoolExecutor(t) as ex:
+        list(ex.map(lambda i: fn(cuts[i], cuts[i + 1]), range(t)))
+
+
 def doc_topics(gamma: np.ndarray, strict: bool = True) -> np.ndarray:
-    """θ [D, K] float64 from γ [D, K]."""
+    """θ [D, K] float64 from γ [D, K] (each row over its sequential sum, lda_post.py:42-53)."""
     g = np.asarray(gamma, np.float64)
     if strict:
         g = native.lib().roundtrip_fixed10(np.ascontiguousarray(g))
     if g.size == 0:
         return g.copy()
-    total = np.cumsum(g, axis=1)[:, -1]
     theta = np.zeros_like(g)
-    pos = total > 0
-    theta[pos] = g[pos] / total[pos, None]
+
+    def rows(lo, hi):
+        gb = g[lo:hi]
+        total = np.cumsum(gb, axis=1)[:, -1]
+        pos = total > 0
+        tb = theta[lo:hi]
+        tb[pos] = gb[pos] / total[pos, None]
+    _par(rows, g.shape[0])
     return theta
 
 
 def word_topics(log_beta: np.ndarray, strict: bool = True) -> np.ndarray:
-    """p(w|z) [V, K] float64 from log β [K, V]."""
+    """p(w|z) [V, K] float64 from log β [K, V] (each topic over its sequential sum, lda_post.py:88-96)."""
     lb = np.asarray(log_beta, np.float64)
     if strict:
         lb = native.lib().roundtrip_fixed10(np.ascontiguousarray(lb))
-    raw = np.exp(lb)
-    total = np.cumsum(raw, axis=1)[:, -1:]
-    return np.ascontiguousarray((raw / total).T)
+    K, V = lb.shape
+    raw = np.empty_like(lb)
+
+    def ex(lo, hi):
+        np.exp(lb[:, lo:hi], out=raw[:, lo:hi])
+    _par(ex, V)
+    total = np.empty((K, 1), np.float64)
+
+    def sums(lo, hi):
+        if hi > lo:
+            total[lo:hi, 0] = np.cumsum(raw[lo:hi], axis=1)[:, -1] if V else 0.0
+    _par(sums, K, min_block=1)
+    out = np.empty((V, K), np.float64)
+
+    def tr(lo, hi):
+        out[lo:hi] = (raw[:, lo:hi] / total).T
+    _par(tr, V)
+    return out
 
 
 def truncate_s20(names: Sequence[str]) -> list:
