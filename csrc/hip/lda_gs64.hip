@@ -2225,15 +2225,10 @@ __global__ __launch_bounds__((NW + 1) * 64) void gs_wsteam(GSArgs a) {
       }
     }
   };
-  // EP == 0: chunk j + 1's ids / counts are loaded at the START of chunk j (after its counts left the
-  // registers) and land during the word phase, so the loop carries registers loaded a whole word phase
-  // before the latch.  (Loaded two chunks ahead right after the row prefetch, they were rotated into the
-  // loop-carried registers at the latch, and that copy made the compiler wait there for every outstanding
-  // load -- the row prefetch included -- before barrier B.)  EP > 0 keeps the two-ahead ids it needs.
   if (nch > 0) {
     load_ids(0, wc, cc, vc);
     load_rows(wc, vc);
-    if constexpr (EP > 0) load_ids(nch > 1 ? 1 : 0, wn, cn, vn);
+    load_ids(nch > 1 ? 1 : 0, wn, cn, vn);
   }
   lds_barrier();   // (1)
   while (var_continue(conv, vconv, it, vmi)) {
@@ -2252,7 +2247,6 @@ __global__ __launch_bounds__((NW + 1) * 64) void gs_wsteam(GSArgs a) {
         }
 #pragma unroll
         for (int r = 0; r < RMAX; ++r) cr[r] = ((vc >> r) & 1u) ? (double)cc[r] : 0.0;
-        if constexpr (EP == 0) load_ids(j + 1 < nch ? j + 1 : 0, wc, cc, vc);
         // dot, reciprocal and axpy now; log P after barrier A (beside the refresh)
 #pragma unroll
         for (int u = 0; u < RMAX; ++u) {
@@ -2303,30 +2297,28 @@ __global__ __launch_bounds__((NW + 1) * 64) void gs_wsteam(GSArgs a) {
         // prefetch of the next chunk's rows: a chunk's ~700 row gathers keep the CU's address unit busy
         // for ~2k cycles (64 B/clk) and the issuing wave blocks until they are queued -- now beside the
         // refresh instead of before it
+        const int j1 = j + 1 < nch ? j + 1 : 0;
+        const int j2 = j1 + 1 < nch ? j1 + 1 : 0;
+#pragma unroll
+        for (int r = 0; r < RMAX; ++r) {
+          wc[r] = wn[r];
+          cc[r] = cn[r];
+        }
+        vc = vn;
         if constexpr (EP == 0) {
           load_rows(wc, vc);
-        } else {
-          const int j1 = j + 1 < nch ? j + 1 : 0;
-          const int j2 = j1 + 1 < nch ? j1 + 1 : 0;
+        } else if (active) {
 #pragma unroll
-          for (int r = 0; r < RMAX; ++r) {
-            wc[r] = wn[r];
-            cc[r] = cn[r];
-          }
-          vc = vn;
-          if (active) {
+          for (int r = EP; r < RMAX; ++r) {
+            if ((vc >> r) & 1u) {
+              load_row(wc[r], bc[r]);
+            } else {
 #pragma unroll
-            for (int r = EP; r < RMAX; ++r) {
-              if ((vc >> r) & 1u) {
-                load_row(wc[r], bc[r]);
-              } else {
-#pragma unroll
-                for (int kk = 0; kk < KS; ++kk) bc[r][kk] = 0.0;
-              }
+              for (int kk = 0; kk < KS; ++kk) bc[r][kk] = 0.0;
             }
           }
-          load_ids(j2, wn, cn, vn);
         }
+        load_ids(j2, wn, cn, vn);
         tick(2);
 #pragma unroll
         for (int u = 0; u < RMAX; ++u) lw = fma(cr[u], flog(P[u]), lw);
