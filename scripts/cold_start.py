@@ -28,13 +28,16 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
-def _child(tmp, tag, tol, extra_env=None, pyflags=()):
+INPUT = []     # the source's input flags (main)
+
+
+def _child(tmp, tag, tol, extra_env=None, pyflags=(), source="flow"):
     lpath = os.path.join(tmp, tag)
     env = dict(os.environ, PYTHONPATH=ROOT, **(extra_env or {}))
-    for k in ("FLOW_PATH", "LPATH", "TOL"):
+    for k in ("FLOW_PATH", "DNS_PATH", "LPATH", "TOL"):
         env.pop(k, None)
-    cmd = [sys.executable, *pyflags, "-m", "oni_ml_amd", "ml_ops", "20160122", "flow", repr(tol), "--lpath", lpath,
-           "--flow-path", os.path.join(tmp, "in"), "--conf", os.path.join(tmp, "none.conf"), "--quiet"]
+    cmd = [sys.executable, *pyflags, "-m", "oni_ml_amd", "ml_ops", "20160122", source, repr(tol), "--lpath", lpath,
+           "--conf", os.path.join(tmp, "none.conf"), "--quiet"] + INPUT
     env["ONI_T_SPAWN"] = repr(time.time())
     t0 = time.perf_counter()
     r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
@@ -75,7 +78,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--events", type=int, default=1_000_000)
     ap.add_argument("--reps", type=int, default=3)
-    ap.add_argument("--tol", type=float, default=1e-5)
+    ap.add_argument("--tol", type=float, default=None, help="default 1e-5 (flow), 1e-4 (dns)")
+    ap.add_argument("--source", default="flow", choices=["flow", "dns"])
     ap.add_argument("--md")
     ap.add_argument("--json")
     ap.add_argument("--variants", default="default;ONI_PYCACHE=0;ONI_FAST_EXIT=0;ONI_EARLY_HIP=0;ONI_WARMUP=1",
@@ -85,22 +89,31 @@ def main():
     from oni_ml_amd.synth.flow import generate_flow_day
     tmp = tempfile.mkdtemp(prefix="oni_cold_")
     try:
-        generate_flow_day(os.path.join(tmp, "in/"), events=a.events, seed=7)
+        if a.source == "flow":
+            generate_flow_day(os.path.join(tmp, "in/"), events=a.events, seed=7)
+            INPUT[:] = ["--flow-path", os.path.join(tmp, "in")]
+        else:
+            from oni_ml_amd.synth.dns import generate_dns_day
+            g = generate_dns_day(os.path.join(tmp, "in"), events=a.events, seed=7, files=4,
+                                 n_names=max(20_000, a.events // 10), n_clients=max(5_000, a.events // 40),
+                                 with_edge_rows=False)
+            INPUT[:] = ["--dns-path", g["dns_path"], "--top1m", g["top1m"]]
+        a.tol = a.tol if a.tol is not None else (1e-5 if a.source == "flow" else 1e-4)
         runs = []
         # the variants alternate, so every one sees the same box state; the first child of all also fills
         # the per-user bytecode cache (utils/pycache.py) -- recorded as its own row, "first"
         variants = [("first", {})] + [v for _ in range(a.reps) for v in _variants(a.variants)]
         for i, (tag, env) in enumerate(variants):
-            wall, sm, _ = _child(tmp, f"run{i}", a.tol, extra_env=env)
+            wall, sm, _ = _child(tmp, f"run{i}", a.tol, extra_env=env, source=a.source)
             runs.append(dict(variant=tag, wall_s=round(wall, 3), inprocess_s=round(sm["wall_seconds"], 3),
                              marks=sm.get("startup_marks"),
                              stages={k: round(v, 3) for k, v in sm["stage_seconds"].items()},
                              flagged=sm.get("scored")))
             print(json.dumps(runs[-1]), flush=True)
-        _, _, err = _child(tmp, "importtime", a.tol, pyflags=("-X", "importtime"))
+        _, _, err = _child(tmp, "importtime", a.tol, pyflags=("-X", "importtime"), source=a.source)
         imports = _importtime(err, 15)
         prof = os.path.join(tmp, "cold.prof")
-        _child(tmp, "cprofile", a.tol, extra_env=dict(ONI_CPROFILE=prof))
+        _child(tmp, "cprofile", a.tol, extra_env=dict(ONI_CPROFILE=prof), source=a.source)
         if a.prof_out:
             shutil.copy(prof, a.prof_out)
         st = pstats.Stats(prof)
@@ -116,7 +129,7 @@ def main():
         with open(a.json, "w") as f:
             json.dump(rec, f, indent=1)
     if a.md:
-        L = [f"# Cold `ml_ops` process, 1-day flow ({a.events} events)", "",
+        L = [f"# Cold `ml_ops` process, 1-day {a.source} ({a.events} events)", "",
              "| run | variant | spawn -> exit s | in-process s | start-up marks (s after spawn) | stages s | flagged |",
              "|---|---|---|---|---|---|---|"]
         for i, r in enumerate(runs):
