@@ -23,6 +23,11 @@ class ModelTables:
     theta: np.ndarray          # [D, K]
     word_names: List[str]      # keys as written (strict: truncated to 20 bytes)
     phi: np.ndarray            # [V, K]
+    # set when the tables were built in this process from its own vocabulary (compat=fixed): the word
+    # key of every φ row and the key space that encodes them -- the flow scorer then maps event keys
+    # to rows without decoding or hashing millions of word names
+    word_keys: Optional[np.ndarray] = None
+    key_space: Optional[object] = None
 
     def doc_index(self) -> dict:
         return {n: i for i, n in enumerate(self.doc_names)}      # later duplicates win (collectAsMap)

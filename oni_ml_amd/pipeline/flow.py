@@ -123,7 +123,10 @@ def run(cfg, dist=None, device=None, log=print) -> dict:
                 from ..models.lda.estimate import load_final
                 gamma, log_beta = load_final(cfg.lpath)
             with R.stage("lda_post") as res:
-                if os.environ.get("ONI_DEFER_POST", "0") != "0":   # measured: no e2e gain (tuning log)
+                # deferred text (ONI_DEFER_POST): measured no e2e gain on the 1-day tables (tuning log);
+                # on by default from 2^26 values, where formatting ~1 G values (config 5) overlaps scoring
+                big = (len(doc_names) + len(word_names)) * int(gamma.shape[1]) >= C.RANK_FILES_MAX_VALUES
+                if os.environ.get("ONI_DEFER_POST", "1" if big else "0") != "0":
                     # the result files are written on a thread while flow_post scores (its tables
                     # are the text round trip of the same values); the lda_post marker waits for them
                     from ..export import lda_post as LP
@@ -135,6 +138,8 @@ def run(cfg, dist=None, device=None, log=print) -> dict:
                     res["_defer"] = join
                 else:
                     tables = C.run_export(cfg, doc_names, gamma, word_names, log_beta, read_back=True)
+                if built is not None and ws is not None and not cfg.strict:
+                    tables.word_keys, tables.key_space = np.asarray(built.word_keys), ws
         else:
             R.skip("lda_post")
             tables = C.load_model_tables(cfg.lpath)
@@ -178,18 +183,31 @@ def score_flow(cfg, ft: FF.FlowTable, tables: C.ModelTables, device, log=print, 
         cols, w = FDS.table_columns(ft, ft.n_raw, torch.device(device))
         cuts = {k: v.cpu().numpy() for k, v in FDS.global_cuts(ctx, cols, w, device).items()}
     feat = FF.featurize(ft, device, cuts=cuts, raw_only=True)
-    ws = FF.word_space_for(feat)
+    # keys straight to φ rows when the tables carry this process's vocabulary (compat=fixed: names are
+    # untruncated and unique, so key -> name -> row is key -> row; the cuts are the pre stage's, so the
+    # pre stage's key space encodes these events too); otherwise through the names as written (strict:
+    # 20-byte keys never match long words, later duplicate rows win)
+    fast = (not multi and not cfg.strict and getattr(tables, "word_keys", None) is not None
+            and getattr(tables, "key_space", None) is not None)
+    ws = tables.key_space if fast else FF.word_space_for(feat)
     src, dst = FF.word_keys(feat, ws)
-    # word keys -> names -> word_results rows (names as written; strict: 20-byte keys never match long words)
     both = torch.cat([src, dst])
     uk, inv = torch.unique(both, return_inverse=True)
     uk_np = uk.cpu().numpy()
-    unames = ws.decode(uk_np)
+    if fast:
+        wk = np.asarray(tables.word_keys, np.int64)
+        o = np.argsort(wk, kind="stable")
+        pos = np.minimum(np.searchsorted(wk[o], uk_np), max(wk.size - 1, 0))
+        word_rows = np.where(wk[o][pos] == uk_np, o[pos], -1) if wk.size else np.full(uk_np.size, -1, np.int64)
+        unames = None
+    else:
+        unames = ws.decode(uk_np)
+        word_rows = tables.word_rows(unames)
     ipn = ft.ip_names
     if ip_rows is None:
         ip_rows = np.fromiter((tables.doc_index().get(n, -1) for n in ipn), dtype=np.int64, count=len(ipn))
     # the rows these events reference: the whole tables (one process) or fetched from their ranks
-    th, ph, drow, wrow = tables.compact(ip_rows, tables.word_rows(unames))
+    th, ph, drow, wrow = tables.compact(ip_rows, word_rows)
     widx = torch.from_numpy(wrow).to(device)[inv]
     w_src, w_dst = widx[: src.numel()], widx[src.numel():]
     didx = torch.from_numpy(drow).to(device)
@@ -206,6 +224,11 @@ def score_flow(cfg, ft: FF.FlowTable, tables: C.ModelTables, device, log=print, 
     o_t = torch.from_numpy(order).to(device)
     inv_src = inv[: src.numel()][o_t].cpu().numpy().astype(np.int32)
     inv_dst = inv[src.numel():][o_t].cpu().numpy().astype(np.int32)
+    if unames is None:      # names only for the words of the flagged rows
+        need = np.unique(np.concatenate([inv_src, inv_dst]))
+        unames = ws.decode(uk_np[need])
+        inv_src = np.searchsorted(need, inv_src).astype(np.int32)
+        inv_dst = np.searchsorted(need, inv_dst).astype(np.int32)
     sel = lambda t: t[o_t].cpu().numpy()
     cols = [
         ("table", ft.table, order),

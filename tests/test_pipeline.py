@@ -289,3 +289,29 @@ def test_background_writer_join_reraises():
     join = C.background(boom)
     with pytest.raises(OSError, match="disk full"):
         join()
+
+
+@pytest.mark.parametrize("compat", ["strict", "fixed"])
+def test_flow_post_paths_byte_identical(tmp_path, monkeypatch, compat):
+    """The big-table paths of the one-process flow pipeline write the bytes of the plain ones: the
+    deferred lda_post text (ONI_DEFER_POST=1, the default from 2^26 values) and, in fixed mode, the
+    scorer's key -> φ row map instead of the word-name dictionary (checked against a resumed run,
+    which scores through the names as written)."""
+    outs = {}
+    for tag, env in (("plain", "0"), ("deferred", "1")):
+        monkeypatch.setenv("ONI_DEFER_POST", env)
+        d = tmp_path / tag
+        d.mkdir()
+        cfg = _flow_cfg(d, compat=compat)
+        s = run(cfg, device="cpu", log=lambda *a, **k: None)
+        assert s["scored"] > 0
+        outs[tag] = {f: (d / "ml" / f).read_bytes() for f in FLOW_FILES}
+    assert outs["plain"] == outs["deferred"]
+    # a resumed flow_post (tables from the result files, no vocabulary keys): the same flow_results.csv
+    d = tmp_path / "deferred"
+    os.unlink(d / "ml" / ".stages" / "flow_post.done")
+    os.unlink(d / "ml" / "flow_results.csv")
+    cfg = _flow_cfg(d, compat=compat)
+    cfg.resume = True
+    run(cfg, device="cpu", log=lambda *a, **k: None)
+    assert (d / "ml" / "flow_results.csv").read_bytes() == outs["plain"]["flow_results.csv"]
