@@ -2036,7 +2036,7 @@ __global__ __launch_bounds__(wteam_threads(NW)) void gs_wteam(GSArgs a) {
 // EP (early prefetch, ONI_GS_EARLY_PREFETCH=EP): rounds u < EP of the next chunk's rows are gathered
 // into bc[u] as soon as the axpy of round u has consumed them -- before the topic sums and the
 // arrival -- so the address unit works beside the reduction; the other rounds after the arrival.
-template <int KS, int NW, int RMAX, int EP = 0, bool STG = false>
+template <int KS, int NW, int RMAX, int EP = 0, bool STG = false, bool TR = false>
 __global__ __launch_bounds__((NW + 1) * 64) void gs_wsteam(GSArgs a) {
   static_assert(KS <= 32 && KS % 2 == 0, "word team: KS <= 32");
   constexpr int NTD = (NW + 1) * 64, NS = NW * 64;
@@ -2047,6 +2047,13 @@ __global__ __launch_bounds__((NW + 1) * 64) void gs_wsteam(GSArgs a) {
   __shared__ double Cs[kGsUMax];        // chunk count sums
   __shared__ double sScal[NW + 1][4];   // sweep partials: lw per word wave; gamma sums (topic wave)
   __shared__ int arrive[NW];            // per word wave: chunks whose topic sums it has left in sRed
+  // TR (topic-wave reduction): a word wave leaves its 64 lanes' KS partial sums in LDS instead of
+  // reducing them across lanes (wave_topic_sums: ~1 k cycles of the word waves' SIMD time per chunk,
+  // two word waves per SIMD); the topic wave, idle while it waits for the arrivals, sums each wave's
+  // block as that wave arrives (lane = topic + KS x part, TRP parts of TRL lanes each, then the parts
+  // combined).  Rows [wave][topic][65]: the pad keeps both the writes and the reads conflict-free.
+  constexpr int TRP = TR ? (64 / KS < 4 ? 64 / KS : 4) : 1, TRL = (64 + TRP - 1) / TRP;
+  __shared__ double sAcc[TR ? NW * KS * 65 : 1];
   if (a.params[kParamDone] != 0.0) return;
   const int t = threadIdx.x;
   const int d = a.order[blockIdx.x];
@@ -2134,6 +2141,8 @@ __global__ __launch_bounds__((NW + 1) * 64) void gs_wsteam(GSArgs a) {
         ttick(3);
         const double gC = k < KS ? gam - C[j][k] : 0.0;
         double S = 0.0;
+        double s4[4] = {0.0, 0.0, 0.0, 0.0};
+        const int tk = lane % KS, tp = lane / KS;   // TR: this lane's topic and part
 #pragma unroll
         for (int v = 0; v < NW; ++v) {
           if (v < nact) {
@@ -2142,7 +2151,26 @@ __global__ __launch_bounds__((NW + 1) * 64) void gs_wsteam(GSArgs a) {
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
             if (ttimer && (v == 0 || v == 3 || v == 4 || v == nact - 1))
               tph[v == 0 ? 4 : v == 3 ? 5 : v == 4 ? 6 : 7] += clock64() - ttc;
-            S += k < KS ? sRed[v][k] : 0.0;
+            if constexpr (TR) {
+              if (tp < TRP) {
+                const double* blk = sAcc + (v * KS + tk) * 65 + tp * TRL;
+#pragma unroll
+                for (int i = 0; i < TRL; ++i)
+                  if (tp * TRL + i < 64) s4[i & 3] += blk[i];
+              }
+            } else {
+              S += k < KS ? sRed[v][k] : 0.0;
+            }
+          }
+        }
+        if constexpr (TR) {
+          // part sums of topic tk sit in lanes tk + KS p: gathered into lane tk in part order
+          const double part = (s4[0] + s4[1]) + (s4[2] + s4[3]);
+          S = part;
+#pragma unroll
+          for (int pp = 1; pp < TRP; ++pp) {
+            const int src = min(lane + KS * pp, 63);
+            S += __shfl(part, src, 64);
           }
         }
         ttick(0);
@@ -2288,7 +2316,12 @@ __global__ __launch_bounds__((NW + 1) * 64) void gs_wsteam(GSArgs a) {
           wword_steps<KS, 1>(E, b, &cp, acc, lw);
         }
         tick(0);
-        wave_topic_sums<KS>(acc, lane, sRed[wv]);
+        if constexpr (TR) {
+#pragma unroll
+          for (int kk = 0; kk < KS; ++kk) sAcc[(wv * KS + kk) * 65 + lane] = acc[kk];
+        } else {
+          wave_topic_sums<KS>(acc, lane, sRed[wv]);
+        }
         // (A) arrival: this wave's topic sums are in sRed.  A counter instead of a workgroup barrier,
         // so the refresh starts while the word waves are still issuing the next chunk's row loads
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");   // LDS only: no vmcnt wait
@@ -3080,8 +3113,14 @@ static void gs_estep_ks(const GSArgs& a, int variant, hipStream_t s) {
           // default here (ONI_GS_EARLY_PREFETCH unset: 1.726-1.740 vs 1.824-1.833 ms per EM iteration
           // for the early round-0 gather, 3 A/B rounds -- the contiguous loads no longer need the head start)
           static const int eps = std::getenv("ONI_GS_EARLY_PREFETCH") ? std::atoi(std::getenv("ONI_GS_EARLY_PREFETCH")) : 0;
+          // ONI_GS_TOPIC_REDUCE=1: the topic wave sums the word waves' lane partials (gs_wsteam TR)
+          // (read per launch: tests switch it within one process)
+          const char* tr_env = std::getenv("ONI_GS_TOPIC_REDUCE");
+          const bool tr = tr_env && std::atoi(tr_env) != 0;
           if (bnw == 7 && eps == 1)
             hipLaunchKernelGGL((gs::gs_wsteam<KS, 7, 2, 1, true>), dim3(a.n_items), dim3(512), 0, s, a);
+          else if (bnw == 7 && eps == 0 && tr)
+            hipLaunchKernelGGL((gs::gs_wsteam<KS, 7, 2, 0, true, true>), dim3(a.n_items), dim3(512), 0, s, a);
           else if (bnw == 7 && eps == 0)
             hipLaunchKernelGGL((gs::gs_wsteam<KS, 7, 2, 0, true>), dim3(a.n_items), dim3(512), 0, s, a);
           else if (bnw == 5 && eps == 0)

@@ -106,7 +106,14 @@ def _link(out: Path, objs, cmd, verbose):
     stale = _stale(out, digest)
     if stale:
         out.parent.mkdir(parents=True, exist_ok=True)
+        # link to a temporary name, then rename: a reader (a running import, a tree snapshot) sees the
+        # old library or the new one, never a half-written file
+        tmp = out.with_name(out.name + ".tmp")
+        cmd = list(cmd)
+        i = cmd.index("-o")
+        cmd[i + 1] = str(tmp)
         _run(cmd, verbose)
+        os.replace(tmp, out)
         _stamp(out, digest)
     _note(out, stale, t0)
 

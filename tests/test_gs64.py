@@ -152,19 +152,21 @@ def test_gs64_graph_replay_and_gate():
     assert eng.gamma.abs().max().item() == 0
 
 
-@pytest.mark.parametrize("stage", ["1", "0"])
+@pytest.mark.parametrize("stage,tr", [("1", "0"), ("0", "0"), ("1", "1")])
 @pytest.mark.parametrize("head", [
     # longest chunk 938 words: past the two prefetched rounds (7 waves x 64 lanes x 2), streamed remainder
     [30000, 20000, 15000, 9000, 6000, 5000, 4000, 3500, 3000, 2500, 2200, 2100],
     [24000, 20000, 15000, 9000, 6000, 5000, 4000, 3500, 3000, 2500, 2200, 2100],
 ])
-def test_longest_documents_match_oracle(head, stage, monkeypatch):
+def test_longest_documents_match_oracle(head, stage, tr, monkeypatch):
     """The longest-document kernel (gs_wsteam: word waves + a topic wave) against the oracle, on chunks
     that need both prefetched rounds, with more than 8 team8 documents so the XCD-aware workgroup order
     holds empty slots (GSPlan.isolate_longest); with the staged row copies (GSStage, default) and
-    gathering from beta."""
+    gathering from beta; and with the topic wave summing the word waves' lane partials
+    (ONI_GS_TOPIC_REDUCE=1, staged)."""
     from oni_ml_amd.ops import hip as H
     monkeypatch.setenv("ONI_GS_STAGE", stage)
+    monkeypatch.setenv("ONI_GS_TOPIC_REDUCE", tr)
     rng = np.random.default_rng(11)
     V, D = 40000, 300
     lens = np.minimum(rng.zipf(1.5, D), 200)
