@@ -41,47 +41,31 @@ def _par(fn, n: int, min_block: int = 1 << 15):
 
 
 def doc_topics(gamma: np.ndarray, strict: bool = True) -> np.ndarray:
-    """θ [D, K] float64 from γ [D, K] (each row over its sequential sum, lda_post.py:42-53)."""
-    g = np.asarray(gamma, np.float64)
+    """θ [D, K] float64 from γ [D, K]: each row over its sequential sum (lda_post.py:42-53; zeros where
+    the sum is not positive).  Native, row-parallel, bitwise numpy's cumsum-and-divide."""
+    g = np.ascontiguousarray(np.asarray(gamma, np.float64))
     if strict:
-        g = native.lib().roundtrip_fixed10(np.ascontiguousarray(g))
+        g = native.lib().roundtrip_fixed10(g)
     if g.size == 0:
         return g.copy()
-    theta = np.zeros_like(g)
-
-    def rows(lo, hi):
-        gb = g[lo:hi]
-        total = np.cumsum(gb, axis=1)[:, -1]
-        pos = total > 0
-        tb = theta[lo:hi]
-        tb[pos] = gb[pos] / total[pos, None]
-    _par(rows, g.shape[0])
-    return theta
+    return native.lib().doc_topics(g, _host_threads())
 
 
 def word_topics(log_beta: np.ndarray, strict: bool = True) -> np.ndarray:
-    """p(w|z) [V, K] float64 from log β [K, V] (each topic over its sequential sum, lda_post.py:88-96)."""
+    """p(w|z) [V, K] float64 from log β [K, V]: numpy's exp (blocks on a thread pool), then each topic
+    over its sequential sum, transposed (native; lda_post.py:88-96)."""
     lb = np.asarray(log_beta, np.float64)
     if strict:
         lb = native.lib().roundtrip_fixed10(np.ascontiguousarray(lb))
     K, V = lb.shape
-    raw = np.empty_like(lb)
+    raw = np.empty((K, V), np.float64)
 
     def ex(lo, hi):
         np.exp(lb[:, lo:hi], out=raw[:, lo:hi])
     _par(ex, V)
-    total = np.empty((K, 1), np.float64)
-
-    def sums(lo, hi):
-        if hi > lo:
-            total[lo:hi, 0] = np.cumsum(raw[lo:hi], axis=1)[:, -1] if V else 0.0
-    _par(sums, K, min_block=1)
-    out = np.empty((V, K), np.float64)
-
-    def tr(lo, hi):
-        out[lo:hi] = (raw[:, lo:hi] / total).T
-    _par(tr, V)
-    return out
+    if raw.size == 0:
+        return np.zeros((V, K), np.float64)
+    return native.lib().topic_normalize_t(raw, _host_threads())
 
 
 def truncate_s20(names: Sequence[str]) -> list:
