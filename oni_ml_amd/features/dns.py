@@ -117,6 +117,18 @@ class DnsTable:
         pa, pc, _ = _pa()
         return pc.take(self.arrays[name], pa.array(np.asarray(rows, np.int64))).to_pylist()
 
+    def take_encoded(self, name: str, rows):
+        """(first-appearance ids int32, distinct names) of column ``name`` at ``rows`` -- what
+        ``dictionary_encode(take(...))`` returns, from Arrow's dictionary encoding (indices in order of
+        first occurrence): only the distinct names become Python strings (a cold DNS day flags 505 k
+        queries x 8 columns: 1.6 s of Python lists and dict probes before)."""
+        pa, pc, _ = _pa()
+        t = pc.take(self.arrays[name], pa.array(np.asarray(rows, np.int64)))
+        if isinstance(t, pa.ChunkedArray):
+            t = t.combine_chunks()
+        d = pc.dictionary_encode(t)
+        return np.asarray(d.indices.to_numpy(zero_copy_only=False), np.int32), d.dictionary.to_pylist()
+
     @property
     def cols(self) -> Dict[str, list]:
         """All columns as Python lists (tests / small tables only)."""

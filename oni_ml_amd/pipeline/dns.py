@@ -160,7 +160,7 @@ def score_dns(cfg, tab: FD.DnsTable, top, tables: C.ModelTables, device, log=pri
     out = os.path.join(cfg.lpath, "dns_results.csv")
     cols = []
     for c in FD.COLUMNS:
-        ids, names = FD.dictionary_encode(tab.take(c, order))
+        ids, names = tab.take_encoded(c, order)
         cols.append(("dict", names, ids))
     H = feat.host
     o_t = torch.from_numpy(order).to(sc.device)
