@@ -360,37 +360,48 @@ CHAIN_KAPPA = 88.0   # chain cost of one word of the longest document / throughp
 
 
 def chain_bounds(doc_ptr: np.ndarray, world: int, kappa: float = CHAIN_KAPPA):
-    """Chain-aware contiguous shards: the rank that holds the longest document gets that document
-    alone, and the documents left and right of it are nnz-balanced over the other world - 1 ranks
-    (each side gets ranks in proportion to its entries).  Its block Gauss-Seidel sweeps are a serial
-    chain that no sharding shortens (profiles/r3_strong_emulated.md), so every other document on its
-    GPU only slows it.  Falls back to ``shard_bounds`` when the chain does not bound the shards
-    (kappa x longest <= nnz / world) or with fewer than 3 ranks."""
+    """Chain-aware contiguous shards.  The longest document's block Gauss-Seidel sweeps are a serial
+    chain that no sharding shortens (profiles/r3_strong_emulated.md), and every other document on its
+    GPU lengthens it: modelled, a rank costs its entries, and the rank holding the longest document
+    costs kappa x its length plus its other entries.  Candidates: the plain nnz-balanced cut, and every
+    split of the other world - 1 ranks between the documents left and right of the longest one (a side
+    given no rank shares the longest document's rank); the cheapest wins (largest rank, then the largest
+    of the other ranks).  Config 5 (a 443 k-word document, 90 M entries) at 8 ranks: the side-proportional
+    rule gave its 3 % left side a rank of its own, 69 ms vs 57 ms for plain cuts (r4_strong_emulated.md).
+    Plain cuts when the chain does not bound the shards (kappa x longest <= nnz / world)."""
     D = len(doc_ptr) - 1
     nnz = int(doc_ptr[-1])
-    if world < 3 or D < world:
+    if world < 2 or D < world:
         return shard_bounds(doc_ptr, world)
-    lens = np.diff(np.asarray(doc_ptr, np.int64))
+    ptr = np.asarray(doc_ptr, np.int64)
+    lens = np.diff(ptr)
     p = int(np.argmax(lens))
-    if kappa * lens[p] <= nnz / world:
+    L = int(lens[p])
+    if kappa * L <= nnz / world:
         return shard_bounds(doc_ptr, world)
-    nl, nr = int(doc_ptr[p]), nnz - int(doc_ptr[p + 1])
-    rest = world - 1
-    kl = int(round(rest * nl / max(1, nl + nr)))
-    kl = min(max(kl, 1 if (nl > 0 and p > 0) else 0), rest - (1 if (nr > 0 and p < D - 1) else 0))
-    kr = rest - kl
-    out = []
-    if kl:
-        out += shard_bounds(np.asarray(doc_ptr[:p + 1], np.int64), kl)
-    elif p > 0:
-        return shard_bounds(doc_ptr, world)
-    out.append((p, p + 1))
-    if kr:
-        sub = np.asarray(doc_ptr[p + 1:], np.int64) - int(doc_ptr[p + 1])
-        out += [(p + 1 + a, p + 1 + b) for a, b in shard_bounds(sub, kr)]
-    elif p < D - 1:
-        return shard_bounds(doc_ptr, world)
-    return out
+
+    def cost(bounds):
+        worst, other = 0.0, 0.0
+        for a, b in bounds:
+            e = float(ptr[b] - ptr[a])
+            if a <= p < b:
+                worst = max(worst, kappa * L + e - L)
+            else:
+                worst, other = max(worst, e), max(other, e)
+        return worst, other
+
+    cands = [shard_bounds(doc_ptr, world)]
+    for kl in range(world):
+        kr = world - 1 - kl
+        if (kl and p == 0) or (kr and p == D - 1) or kl > p or kr > D - 1 - p:
+            continue                    # a rank for a side without (enough) documents
+        out = list(shard_bounds(ptr[:p + 1], kl)) if kl else []
+        out.append((0 if not kl else p, D if not kr else p + 1))
+        if kr:
+            sub = ptr[p + 1:] - ptr[p + 1]
+            out += [(p + 1 + a, p + 1 + b) for a, b in shard_bounds(sub, kr)]
+        cands.append(out)
+    return min(cands, key=cost)
 
 
 def chain_default() -> bool:
