@@ -66,7 +66,7 @@ def _route(ctx, sec: DocWordCounts, n_ids: int, device) -> DocWordCounts:
 
 
 def build_sharded(ctx, sections: Sequence[DocWordCounts], n_ids: int, merge: bool = False,
-                  device="cpu") -> ShardedCorpus:
+                  device="cpu", K: int = None) -> ShardedCorpus:
     """``sections``: this rank's (global ip id, word key, count) lines per doc_wc section, each sorted by
     (ip, word) with counts merged (``count_pairs``); ``n_ids``: size of the global ip dictionary;
     ``merge``: sum a (doc, word) pair's counts across sections (compat=fixed, ``concat(merge=True)``)."""
@@ -141,7 +141,7 @@ def build_sharded(ctx, sections: Sequence[DocWordCounts], n_ids: int, merge: boo
         glen = np.zeros(D, np.int64)
         glen[allp[:, 0]] = allp[:, 1]
         gptr = np.concatenate([[0], np.cumsum(glen)])
-        cut = engine_bounds(gptr, N)
+        cut = engine_bounds(gptr, N, K)
         bounds = [0] + [int(b1) for _, b1 in cut]
     # ---- entries to the shard owners: (doc index, word id, count, ip id), line order kept per doc
     line_doc = doc_index[dinv]

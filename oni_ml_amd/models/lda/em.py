@@ -152,7 +152,7 @@ class LDAEngine:
             if dist is not None:
                 self.global_docs = dist.allreduce_int(corpus.num_docs)
         elif dist is not None and dist.active:
-            d0, d1 = dist.shard_range(corpus)
+            d0, d1 = dist.shard_range(corpus, self.K)
             self.doc_range = (d0, d1)
             corpus = corpus.slice_docs(d0, d1)
         else:
@@ -762,7 +762,7 @@ class LDAEngine:
         ptr = self.corpus.doc_ptr
         cw = torch.zeros(self.V, self.K, dtype=torch.float64, device=self.device)
         sc = torch.zeros(2, dtype=torch.float64, device=self.device)
-        for d0, d1 in engine_bounds(ptr, self.emulate_shards):
+        for d0, d1 in engine_bounds(ptr, self.emulate_shards, self.K):
             e0, e1 = int(ptr[d0]), int(ptr[d1])
             lp = (self.t_doc_ptr[d0:d1 + 1] - self.t_doc_ptr[d0]).clone()
             cw += R.suffstats(lp, self.t_word[e0:e1].clone(), out["e"][d0:d1].clone(), out["r"][e0:e1].clone(),

@@ -51,10 +51,10 @@ class DistContext:
         return self.world_size > 1 or self.forced
 
     # -------------------------------------------------------------- sharding
-    def shard_range(self, corpus):
+    def shard_range(self, corpus, K: int = None):
         """This rank's documents of a corpus every rank holds whole (strong scaling): ``engine_bounds``,
         the one shard rule every consumer of a rank's document range uses."""
-        return engine_bounds(corpus.doc_ptr, self.world_size)[self.rank]
+        return engine_bounds(corpus.doc_ptr, self.world_size, K)[self.rank]
 
     # ----------------------------------------------------------- collectives
     def allreduce_suffstats(self, cw: torch.Tensor, scalars: torch.Tensor) -> torch.Tensor:
@@ -359,7 +359,17 @@ CHAIN_KAPPA = 88.0   # chain cost of one word of the longest document / throughp
                      # headline day, K = 20: 1.64 ms for 22,721 words vs ~1.1 ms for the other 1.34 M entries
 
 
-def chain_bounds(doc_ptr: np.ndarray, world: int, kappa: float = CHAIN_KAPPA):
+def chain_kappa(K: int = None) -> float:
+    """CHAIN_KAPPA at K topics.  The chain costs ~72-76 ns per word at K = 20 and K = 100 alike (a chunk's
+    refresh, not its K-wide rows, sets the pace), while an entry's throughput cost grows with K: 0.82 ns
+    at K = 20, 2.7 ns at K = 100 (config 5: 245 ms for 90.3 M entries, its 443 k-word chain 33.6 ms,
+    r4_strong_emulated.md) -- kappa ~ 88 (20 / K)^0.74.  Unknown K: the K = 20 value."""
+    if not K:
+        return CHAIN_KAPPA
+    return CHAIN_KAPPA * (20.0 / float(K)) ** 0.74
+
+
+def chain_bounds(doc_ptr: np.ndarray, world: int, kappa: float = None, K: int = None):
     """Chain-aware contiguous shards.  The longest document's block Gauss-Seidel sweeps are a serial
     chain that no sharding shortens (profiles/r3_strong_emulated.md), and every other document on its
     GPU lengthens it: modelled, a rank costs its entries, and the rank holding the longest document
@@ -368,7 +378,10 @@ def chain_bounds(doc_ptr: np.ndarray, world: int, kappa: float = CHAIN_KAPPA):
     given no rank shares the longest document's rank); the cheapest wins (largest rank, then the largest
     of the other ranks).  Config 5 (a 443 k-word document, 90 M entries) at 8 ranks: the side-proportional
     rule gave its 3 % left side a rank of its own, 69 ms vs 57 ms for plain cuts (r4_strong_emulated.md).
-    Plain cuts when the chain does not bound the shards (kappa x longest <= nnz / world)."""
+    Plain cuts when the chain does not bound the shards (kappa x longest <= nnz / world).  ``kappa``
+    defaults to ``chain_kappa(K)``."""
+    if kappa is None:
+        kappa = chain_kappa(K)
     D = len(doc_ptr) - 1
     nnz = int(doc_ptr[-1])
     if world < 2 or D < world:
@@ -409,19 +422,20 @@ def chain_default() -> bool:
     return os.environ.get("ONI_SHARD_CHAIN", "1") != "0"
 
 
-def engine_bounds(doc_ptr: np.ndarray, world: int):
+def engine_bounds(doc_ptr: np.ndarray, world: int, K: int = None):
     """The engine's document shards of a corpus split over ``world`` ranks: chain-aware
     (``chain_bounds``) unless ONI_SHARD_CHAIN=0.  The strong-scaling engine (``shard_range``), the
     row-sharded pipeline's corpus builder (corpus/sharded.py) and its resume path all use this rule, so
-    a rank's gamma rows and its document names always cover the same documents."""
-    return shard_bounds(doc_ptr, world, chain=chain_default())
+    a rank's gamma rows and its document names always cover the same documents (``K``: the model's
+    topics, which set the chain's relative cost; every caller of one run passes the same K)."""
+    return shard_bounds(doc_ptr, world, chain=chain_default(), K=K)
 
 
-def shard_bounds(doc_ptr: np.ndarray, world: int, chain: bool = False):
+def shard_bounds(doc_ptr: np.ndarray, world: int, chain: bool = False, K: int = None):
     """Contiguous [d0, d1) ranges with ~equal nnz (ties broken toward equal doc counts).
     ``chain``: ``chain_bounds`` instead (``engine_bounds``, the default rule of the engine's shards)."""
     if chain:
-        return chain_bounds(doc_ptr, world)
+        return chain_bounds(doc_ptr, world, K=K)
     D = len(doc_ptr) - 1
     nnz = int(doc_ptr[-1])
     if world <= 1 or D == 0:

@@ -92,7 +92,7 @@ def _files_state(cfg, ctx):
     ``dist.engine_bounds``: the engine that re-runs the lda stage splits the documents the same way)."""
     from ..parallel.dist import engine_bounds
     corpus, doc_names, word_names = C.load_corpus_files(cfg.lpath)
-    d0, d1 = engine_bounds(corpus.doc_ptr, ctx.world_size)[ctx.rank]
+    d0, d1 = engine_bounds(corpus.doc_ptr, ctx.world_size, cfg.topics)[ctx.rank]
     return corpus, doc_names, word_names, (d0, d1)
 
 
@@ -122,7 +122,7 @@ def run_flow(cfg, ctx, device=None, log=print) -> dict:
                             dict(cuts={k: v.tolist() for k, v in cuts.items()}, ports=ws.ports.tolist()))
             res["rank_pairs"] = sum(s.n for s in sections)
         with R.stage("lda_pre") as res:
-            sc = build_sharded(ctx, sections, len(names), merge=not cfg.strict, device=device)
+            sc = build_sharded(ctx, sections, len(names), merge=not cfg.strict, device=device, K=cfg.topics)
             del sections
             doc_names = sc.doc_names = names.take(sc.doc_keys)
             write_corpus_files_sharded(ctx, cfg.lpath, sc, doc_names, ws.decode, cfg.threads)
@@ -181,7 +181,7 @@ def run_dns(cfg, ctx, device=None, log=print) -> dict:
                 C.save_json(os.path.join(cfg.lpath, "dns_cuts.json"), dict(cuts={k: v.tolist() for k, v in cuts.items()}))
             res["rank_pairs"] = sum(s.n for s in sections)
         with R.stage("lda_pre") as res:
-            sc = build_sharded(ctx, sections, len(names), device=device)
+            sc = build_sharded(ctx, sections, len(names), device=device, K=cfg.topics)
             del sections
             doc_names = sc.doc_names = names.take(sc.doc_keys)
             write_corpus_files_sharded(ctx, cfg.lpath, sc, doc_names, wsp.decode, cfg.threads)

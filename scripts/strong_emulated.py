@@ -143,7 +143,7 @@ def main():
                 return per
             per = [t_full] if n == 1 else shard_times(shard_bounds(c.doc_ptr, n))
             # chain-aware shards (parallel/dist.py chain_bounds, ONI_SHARD_CHAIN=1): the longest document alone
-            cb = shard_bounds(c.doc_ptr, n, chain=True) if n > 1 else None
+            cb = shard_bounds(c.doc_ptr, n, chain=True, K=K) if n > 1 else None
             per_chain = shard_times(cb) if cb is not None and cb != shard_bounds(c.doc_ptr, n) else None
             ring = 0.0 if n == 1 else 2 * (n - 1) / n * bytes_ / LINK_BPS + 2 * (n - 1) * STEP_LAT
             mesh = 0.0 if n == 1 else 2 * bytes_ / (n * LINK_BPS) + 2 * STEP_LAT
