@@ -189,7 +189,7 @@ inline char* put_py2_float(char* w, double d, double* back = nullptr) {
       if (d < 0) *w++ = '-';
       if (E < -4 || E >= 12) {
         *w++ = dig[0];
-        if (nd > 1) { *w++ = '.'; std::memcpy(w, dig + 1, nd - 1); w += nd - 1; }
+        if (nd > 1) { *w++ = '.'; std::memcpy(w, dig + 1, 11); w += nd - 1; }   // fixed-size copy
         *w++ = 'e';
         *w++ = E < 0 ? '-' : '+';
         const int ae = E < 0 ? -E : E;
@@ -202,10 +202,11 @@ inline char* put_py2_float(char* w, double d, double* back = nullptr) {
         if (nd > E + 1) { std::memcpy(w, dig + E + 1, nd - E - 1); w += nd - E - 1; }
         else *w++ = '0';
       } else {
-        *w++ = '0';
-        *w++ = '.';
-        for (int i = 0; i < -E - 1; ++i) *w++ = '0';
-        std::memcpy(w, dig, nd);
+        // -4 <= E <= -1: "0." and 0-3 zeros from one fixed copy, then the digits from another (both
+        // fixed-size: the lengths vary value to value, and variable copies / loops mispredicted)
+        std::memcpy(w, "0.000", 5);
+        w += 1 - E;
+        std::memcpy(w, dig, 12);
         w += nd;
       }
       if (back && !digits_value(dig, nd, E, d < 0, back)) std::from_chars(start, w, *back);
@@ -273,15 +274,26 @@ inline char* put_fixed10(char* w, double d, double* back = nullptr) {
   if (a < 4.5e5) {                              // |d| 1e10 < 2^52: the rounding error term is <= 1/4
     int64_t N = scaled_round(a, 10);
     const int64_t ip = N / 10000000000LL, fp = N % 10000000000LL;
-    if (std::signbit(d)) *w++ = '-';
-    w = std::to_chars(w, w + 24, ip).ptr;
-    *w++ = '.';
+    *w = '-';
+    w += std::signbit(d) ? 1 : 0;               // branch-free sign (log beta: always '-'; gamma: never)
     const char* pr = digit_pairs();
-    uint64_t v = (uint64_t)fp;
-    for (int i = 8; i >= 0; i -= 2) {
-      std::memcpy(w + i, pr + 2 * (v % 100), 2);
-      v /= 100;
+    if (ip < 100) {                             // 1 or 2 integer digits without a data-dependent branch
+      const int one = ip < 10;
+      std::memcpy(w, pr + 2 * ip + one, 2);
+      w += 2 - one;
+    } else {
+      w = std::to_chars(w, w + 24, ip).ptr;
     }
+    *w++ = '.';
+    // ten fraction digits as two independent five-digit halves (shorter dependency chains)
+    const uint32_t hi = (uint32_t)(fp / 100000), lo = (uint32_t)(fp % 100000);
+    w[0] = (char)('0' + hi / 10000);
+    w[5] = (char)('0' + lo / 10000);
+    const uint32_t h4 = hi % 10000, l4 = lo % 10000;
+    std::memcpy(w + 1, pr + 2 * (h4 / 100), 2);
+    std::memcpy(w + 3, pr + 2 * (h4 % 100), 2);
+    std::memcpy(w + 6, pr + 2 * (l4 / 100), 2);
+    std::memcpy(w + 8, pr + 2 * (l4 % 100), 2);
     w += 10;
     if (back) {
       const double x = (double)N / 1e10;
