@@ -521,11 +521,85 @@ static void format_row(std::string& out, int64_t r, const std::vector<OutCol>& c
   out += '\n';
 }
 
+// values [j0, j1) of row r of a row column (kPy2Row / kFixedRow), each after its in-row separator
+// (none before value 0) -- format_row's text for that range
+static void format_row_values(std::string& out, const OutCol& k, int64_t r, int64_t j0, int64_t j1) {
+  const double* row = k.f64 + (size_t)r * k.width;
+  double* back = k.parsed ? k.parsed + (size_t)r * k.width : nullptr;
+  char b[64];
+  for (int64_t j = j0; j < j1; ++j) {
+    if (j) out += k.text;
+    double* bj = back ? back + j : nullptr;
+    if (k.kind == OutCol::kPy2Row) {
+      out.append(b, put_py2_float(b, row[j], bj) - b);
+    } else if (char* e = put_fixed10(b, row[j], bj)) {
+      out.append(b, e - b);
+    } else {
+      append_fixed10(out, row[j], bj);
+    }
+  }
+}
+
+// Few very wide rows (a K x V .beta file: 100 rows of 4.5 M values at config 5): one row per thread
+// left most threads idle in the last batches; here each row's values are cut into one segment per
+// thread, and the row is written as its scalar columns, then the segments in order.
+static int64_t write_wide_rows(FILE* f, const int64_t* order, int64_t n, const std::vector<OutCol>& cols,
+                               const std::string& sep, int threads, int& werr) {
+  const OutCol& k = cols.back();
+  std::vector<OutCol> head(cols.begin(), cols.end() - 1);
+  std::vector<std::string> seg((size_t)threads);
+  int64_t written = 0;
+  for (int64_t i = 0; i < n && !werr; ++i) {
+    const int64_t r = order ? order[i] : i;
+    std::string pre;
+    if (!head.empty()) {
+      format_row(pre, r, head, sep);
+      pre.pop_back();                          // format_row's newline
+      pre += sep;
+    }
+    const int64_t W = k.width;
+    run_parallel(threads, threads, [&](int t) {
+      std::string s;
+      s.swap(seg[(size_t)t]);
+      s.clear();
+      const int64_t j0 = W * t / threads, j1 = W * (t + 1) / threads;
+      s.reserve((size_t)(j1 - j0) * 18);
+      format_row_values(s, k, r, j0, j1);
+      s.swap(seg[(size_t)t]);
+    });
+    seg.back() += '\n';
+    if (!pre.empty() && std::fwrite(pre.data(), 1, pre.size(), f) != pre.size()) werr = errno ? errno : EIO;
+    written += (int64_t)pre.size();
+    for (auto& x : seg) {
+      if (werr) break;
+      if (!x.empty() && std::fwrite(x.data(), 1, x.size(), f) != x.size()) werr = errno ? errno : EIO;
+      written += (int64_t)x.size();
+    }
+  }
+  return written;
+}
+
 int64_t write_rows(const std::string& path, const int64_t* order, int64_t n, const std::vector<OutCol>& cols,
                    const std::string& sep, bool append, int threads) {
   FILE* f = std::fopen(path.c_str(), append ? "ab" : "wb");
   if (!f) throw std::runtime_error("cannot open for writing: " + path + ": " + std::strerror(errno));
   if (threads < 1) threads = 1;
+  if (!cols.empty() && (cols.back().kind == OutCol::kPy2Row || cols.back().kind == OutCol::kFixedRow) &&
+      cols.back().width >= (1 << 16) && n < 2 * (int64_t)threads && threads > 1) {
+    bool scalar_head = true;
+    for (size_t c = 0; c + 1 < cols.size(); ++c)
+      scalar_head = scalar_head && cols[c].kind != OutCol::kPy2Row && cols[c].kind != OutCol::kFixedRow;
+    if (scalar_head) {
+      int werr = 0;
+      const int64_t written = write_wide_rows(f, order, n, cols, sep, threads, werr);
+      if (werr) {
+        std::fclose(f);
+        throw std::runtime_error("short write: " + path + ": " + std::strerror(werr));
+      }
+      if (std::fclose(f) != 0) throw std::runtime_error("close failed: " + path);
+      return written;
+    }
+  }
   // Rows per thread block: ~2^18 cells of work per block, so wide rows (a K x V
   // .beta file has K rows of V values) still spread over every thread.
   int64_t cells = 0;
