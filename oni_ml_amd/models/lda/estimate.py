@@ -38,22 +38,27 @@ CKPT = "checkpoint.npz"
 
 
 class AsyncWriter:
-    """One background thread for the LAG-period model files.
+    """Background threads for the LAG-period and final model files.
 
     lda-c writes %03d.beta/.gamma every LAG iterations inside its EM loop; here
-    the host copies are handed to this thread (the C++ writers release the GIL)
-    so the device keeps iterating while text is formatted.  Jobs run in
-    submission order; `close()` drains the queue and re-raises the first error."""
+    the host copies are handed to these threads (the C++ writers release the GIL)
+    so the device keeps iterating while text is formatted.  Jobs start in
+    submission order on ``workers`` threads (every job writes its own file: a text
+    job's formatting overlaps another's disk write, e.g. the 3.6 GB final_model.npz
+    of config 5); `close()` drains the queue and re-raises the first error."""
 
-    def __init__(self):
-        self._q: "queue.Queue" = queue.Queue()
+    def __init__(self, workers: int = 2):
+        self._qs = [queue.Queue() for _ in range(workers)]
         self._err: Optional[BaseException] = None
-        self._t = threading.Thread(target=self._loop, name="oni-lda-writer", daemon=True)
-        self._t.start()
+        self._next = 0
+        self._ts = [threading.Thread(target=self._loop, args=(q,), name=f"oni-lda-writer{i}", daemon=True)
+                    for i, q in enumerate(self._qs)]
+        for t in self._ts:
+            t.start()
 
-    def _loop(self):
+    def _loop(self, q):
         while True:
-            job = self._q.get()
+            job = q.get()
             if job is None:
                 return
             if self._err is None:
@@ -62,14 +67,23 @@ class AsyncWriter:
                 except BaseException as e:  # surfaced by close()
                     self._err = e
 
-    def submit(self, fn, *args, **kw):
+    def submit(self, fn, *args, key: Optional[str] = None, **kw):
+        """``key``: jobs with the same key run on one thread in submission order (one file rewritten
+        several times, e.g. checkpoint.npz); other jobs go round-robin."""
         if self._err is not None:
             raise self._err
-        self._q.put(lambda: fn(*args, **kw))
+        if key is not None:
+            i = sum(key.encode()) % len(self._qs)
+        else:
+            i = self._next
+            self._next = (self._next + 1) % len(self._qs)
+        self._qs[i].put(lambda: fn(*args, **kw))
 
     def close(self):
-        self._q.put(None)
-        self._t.join()
+        for q in self._qs:
+            q.put(None)
+        for t in self._ts:
+            t.join()
         if self._err is not None:
             raise self._err
 
@@ -271,7 +285,7 @@ def estimate(corpus: Corpus, num_topics: int, alpha_init: float, settings: LDASe
                       likelihood_old=np.float64(history[-1][0] if history else 0.0),
                       var_max_iter=np.int64(e.var_max_iter), history=np.asarray(history, np.float64).reshape(-1, 2),
                       **st)
-            writer.submit(_after(ev_st, _after(ev_lb, _write_checkpoint)), outdir, ck)
+            writer.submit(_after(ev_st, _after(ev_lb, _write_checkpoint)), outdir, ck, key="checkpoint")
         if tag == "final":  # exact binary copy of what final.* hold as text (stage resume reloads this)
             extra = {} if multi else dict(gamma=g)
             writer.submit(np.savez, os.path.join(outdir, "final_model.npz"), log_beta=lb,
