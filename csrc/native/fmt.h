@@ -366,6 +366,33 @@ inline bool java_parse_double(const char* b, const char* e, double* out) {
   const size_t n = e - s;
   if (n == 3 && std::memcmp(s, "NaN", 3) == 0) { *out = NAN; return true; }
   if (n == 8 && std::memcmp(s, "Infinity", 8) == 0) { *out = neg ? -INFINITY : INFINITY; return true; }
+  // fast path: at most 15 digits and at most one '.': N (the digits) is an exact integer and so is
+  // 10^f (f fraction digits <= 15), so N / 10^f is the correctly rounded value Java returns
+  if (n <= 16) {
+    uint64_t N = 0;
+    int nd = 0, f = -1;
+    const char* q = s;
+    for (; q < e; ++q) {
+      const unsigned d = (unsigned)(unsigned char)*q - '0';
+      if (d < 10) {
+        N = N * 10 + d;
+        ++nd;
+        f += f >= 0;
+      } else if (*q == '.' && f < 0) {
+        f = 0;
+      } else {
+        break;
+      }
+    }
+    if (q == e && nd > 0 && nd <= 15) {
+      static constexpr double p10[16] = {1e0, 1e1, 1e2, 1e3, 1e4, 1e5, 1e6, 1e7,
+                                         1e8, 1e9, 1e10, 1e11, 1e12, 1e13, 1e14, 1e15};
+      double v = (double)N;
+      if (f > 0) v /= p10[f];
+      *out = neg ? -v : v;
+      return true;
+    }
+  }
   // from_chars does not accept a leading '+'
   double v;
   auto r = std::from_chars(s, e, v, std::chars_format::general);

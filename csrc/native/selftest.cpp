@@ -51,8 +51,8 @@ int main(int argc, char** argv) {
       if (i % 50021 == 0) f << "h0,h1,h2,h3\n";
     }
   }
-  std::vector<std::vector<double>> nums;
-  std::vector<std::vector<int32_t>> ids;
+  std::vector<ColVec<double>> nums;
+  std::vector<ColVec<int32_t>> ids;
   std::vector<std::vector<std::string>> names;
   for (int th : {1, 3, 8}) {
     TextTable t(4, {0, 3}, {{1, 2}});

@@ -1,5 +1,9 @@
 #include "table.h"
 
+#include <future>
+
+#include <immintrin.h>
+
 #include <algorithm>
 #include <charconv>
 #include <cstdio>
@@ -165,7 +169,7 @@ void StringDict::merge(const std::vector<const LocalNames*>& parts, std::vector<
     res[t].resize(L.names.size());
     first[t].assign(L.names.size(), 0);
     remap[t].resize(L.names.size());
-    for (size_t j = 0; j < L.names.size(); ++j) bkt[t][shard_of(L.index.hash[j])].push_back((int32_t)j);
+    for (size_t j = 0; j < L.names.size(); ++j) bkt[t][shard_of(L.hash[j])].push_back((int32_t)j);
   });
   // shard-parallel lookup / insert: parts visited in order, so the first part (and first local
   // index) that sees a new name owns it
@@ -176,7 +180,7 @@ void StringDict::merge(const std::vector<const LocalNames*>& parts, std::vector<
       const auto& L = *parts[t];
       for (int32_t j : bkt[t][s]) {
         const std::string_view name = L.names[j];
-        const uint64_t h = L.index.hash[j];
+        const uint64_t h = L.hash[j];
         int64_t k = sh.index.find(h, name, [&](size_t i) { return sh.keys[i]; });
         if (k < 0) {
           k = (int64_t)sh.keys.size();
@@ -258,10 +262,17 @@ void TextTable::load_files(const std::vector<std::string>& paths, bool drop_hdr,
     total += sizes.back();
   }
   int64_t left = total;
-  for (size_t i = 0; i < paths.size(); ++i) {
-    const std::string& p = paths[i];
+  // file i + 1 is read on a thread (a quarter of the threads) while file i is parsed
+  auto read_file = [&](size_t i, int th) {
     TextChunk s((size_t)sizes[i]);
-    read_bytes(p, 0, sizes[i], s.data(), threads);
+    read_bytes(paths[i], 0, sizes[i], s.data(), th);
+    return s;
+  };
+  std::future<TextChunk> next;
+  for (size_t i = 0; i < paths.size(); ++i) {
+    TextChunk s = next.valid() ? next.get() : read_file(i, threads);
+    if (i + 1 < paths.size())
+      next = std::async(std::launch::async, read_file, i + 1, std::max(1, threads / 4));
     if (i == 0 && drop_header) {
       const char* e = (const char*)std::memchr(s.data(), '\n', s.size());
       header.assign(s.data(), e ? (size_t)(e - s.data()) : s.size());
@@ -365,38 +376,79 @@ void TextTable::ingest_chunk(uint32_t cid, int32_t w, int threads) {
     for (auto& v : o.ids) v.reserve(guess);
     std::vector<const char*> fb(ncols), fe(ncols);
     std::vector<double> vals(NN);
-    std::vector<std::string_view> svals(ND);
+    std::vector<uint64_t> dh(ND);
     const char* base = s.data();
     size_t p = pts[t];
     const size_t end = pts[t + 1];
+    const char* const lim = base + end;
+    const __m256i vcomma = _mm256_set1_epi8(','), vnl = _mm256_set1_epi8('\n');
     while (p < end) {
       const char* lb = base + p;
-      const char* nl = (const char*)std::memchr(lb, '\n', end - p);
-      const char* le = nl ? nl : base + end;
+      // one pass over the line, 32 bytes at a time: its end and its first ncols - 1 commas
+      int f = 0;
+      auto commas = [&](uint32_t m, const char* at) {
+        for (; m; m &= m - 1) {
+          const char* c = at + __builtin_ctz(m);
+          if (f + 1 < ncols) {
+            fe[f] = c;
+            fb[f + 1] = c + 1;
+          }
+          ++f;
+        }
+      };
+      fb[0] = lb;
+      const char* q = lb;
+      for (;;) {
+        if (q + 32 <= lim) {
+          const __m256i v = _mm256_loadu_si256((const __m256i*)q);
+          const uint32_t mc = (uint32_t)_mm256_movemask_epi8(_mm256_cmpeq_epi8(v, vcomma));
+          const uint32_t mn = (uint32_t)_mm256_movemask_epi8(_mm256_cmpeq_epi8(v, vnl));
+          if (mn) {
+            const int stop = __builtin_ctz(mn);
+            commas(mc & ((1u << stop) - 1u), q);
+            q += stop;
+            break;
+          }
+          commas(mc, q);
+          q += 32;
+        } else {
+          for (; q < lim && *q != '\n'; ++q)
+            if (*q == ',') commas(1u, q);
+          break;
+        }
+      }
+      const char* le = q;
       p = (le - base) + 1;
       if (le > lb && le[-1] == '\r') --le;
       if (drop_header && (size_t)(le - lb) == header.size() && std::memcmp(lb, header.data(), header.size()) == 0) {
         ++o.header;
         continue;
       }
-      if (java_split_count(lb, le) != ncols) { ++o.bad_fields; continue; }
       const char* tb = lb;
       const char* te = le;
-      while (tb < te && is_ws(*tb)) ++tb;
-      while (te > tb && is_ws(te[-1])) --te;
-      while (te > tb && te[-1] == ',') --te;  // trailing empty fields vanish in split + mkString
-      if (java_split_count(tb, te) != ncols) { ++o.bad_fields; continue; }
-      // field boundaries
-      int f = 0;
-      const char* q = tb;
-      fb[0] = tb;
-      for (; q < te; ++q) {
-        if (*q == ',') {
-          fe[f] = q;
-          fb[++f] = q + 1;
+      if (!(f == ncols - 1 && le > lb && !is_ws(*lb) && !is_ws(le[-1]) && le[-1] != ',')) {
+        // not the plain form (ncols fields, nothing to trim, no trailing empty field): the reference's
+        // split / trim / split rules in full
+        if (java_split_count(lb, le) != ncols) { ++o.bad_fields; continue; }
+        while (tb < te && is_ws(*tb)) ++tb;
+        while (te > tb && is_ws(te[-1])) --te;
+        while (te > tb && te[-1] == ',') --te;  // trailing empty fields vanish in split + mkString
+        if (java_split_count(tb, te) != ncols) { ++o.bad_fields; continue; }
+        f = 0;
+        fb[0] = tb;
+        for (const char* r = tb; r < te; ++r) {
+          if (*r == ',') {
+            fe[f] = r;
+            fb[++f] = r + 1;
+          }
         }
       }
       fe[f] = te;
+      for (int i = 0; i < ND; ++i) {
+        const int c = dict_col_index[i];
+        dh[i] = hash_bytes(fb[c], fe[c] - fb[c]);
+        o.dicts[dict_col_group[i]].prefetch(dh[i]);
+      }
       bool ok = true;
       for (int i = 0; i < NN && ok; ++i) {
         const int c = numeric_cols[i];
@@ -408,7 +460,7 @@ void TextTable::ingest_chunk(uint32_t cid, int32_t w, int threads) {
       for (int i = 0; i < NN; ++i) o.num[i].push_back(vals[i]);
       for (int i = 0; i < ND; ++i) {
         const int c = dict_col_index[i];
-        o.ids[i].push_back(o.dicts[dict_col_group[i]].get_or_add(std::string_view(fb[c], fe[c] - fb[c])));
+        o.ids[i].push_back(o.dicts[dict_col_group[i]].get_or_add(std::string_view(fb[c], fe[c] - fb[c]), dh[i]));
       }
     }
   };
@@ -430,14 +482,15 @@ void TextTable::ingest_chunk(uint32_t cid, int32_t w, int threads) {
     n_header += outs[t].header;
     at[t + 1] = at[t] + outs[t].off.size();
   }
-  rows.resize(at[T]);
-  weight.resize(at[T], w);
+  rows.resize(at[T]);      // ColVec: no fill here; every element is written below, thread-parallel
+  weight.resize(at[T]);
   for (int i = 0; i < NN; ++i) num[i].resize(at[T]);
   for (int i = 0; i < ND; ++i) ids[i].resize(at[T]);
   run_parallel(T, threads, [&](int t) {
     LocalOut& o = outs[t];
     const size_t n = o.off.size(), a = at[t];
     for (size_t r = 0; r < n; ++r) rows[a + r] = RowSpan{cid, o.len[r], o.off[r]};
+    std::fill(weight.begin() + a, weight.begin() + a + n, w);
     for (int i = 0; i < NN; ++i) std::copy(o.num[i].begin(), o.num[i].end(), num[i].begin() + a);
     for (int i = 0; i < ND; ++i) {
       const auto& rm = remap[dict_col_group[i]][t];

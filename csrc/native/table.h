@@ -20,13 +20,34 @@
 #pragma once
 #include <algorithm>
 #include <cstdint>
+#include <cstring>
 #include <memory>
 #include <string>
 #include <string_view>
+#include <type_traits>
 #include <unordered_map>
+#include <utility>
 #include <vector>
 
 namespace onin {
+
+// std::allocator whose value-initialising construct() default-initialises instead: resize() of a
+// column leaves the new elements untouched, so the rows of an ingested chunk are first written (and
+// their pages first touched) by the threads that copy them in, not by a serial zero fill
+template <class T>
+struct DefaultInit : std::allocator<T> {
+  template <class U>
+  struct rebind { using other = DefaultInit<U>; };
+  DefaultInit() = default;
+  template <class U>
+  DefaultInit(const DefaultInit<U>&) noexcept {}
+  template <class U>
+  void construct(U* p) noexcept(std::is_nothrow_default_constructible<U>::value) { ::new ((void*)p) U; }
+  template <class U, class... A>
+  void construct(U* p, A&&... a) { ::new ((void*)p) U(std::forward<A>(a)...); }
+};
+template <class T>
+using ColVec = std::vector<T, DefaultInit<T>>;
 
 struct RowSpan {
   uint32_t chunk;
@@ -73,17 +94,61 @@ struct FlatIndex {
   }
 };
 
-// One thread's first-appearance name list (string_views into the text being ingested).
+// One thread's first-appearance name list (string_views into the text being ingested).  The index
+// holds keys of up to 16 bytes (every IPv4 address) inline in its slots, so a lookup touches one slot
+// line instead of slot -> hash -> name -> text (the ingest's hottest path: two lookups per flow row);
+// a longer key's slot holds its hash and is compared through `names`.
 struct LocalNames {
   std::vector<std::string_view> names;
-  FlatIndex index;
-  int32_t get_or_add(std::string_view s) {
-    const uint64_t h = hash_bytes(s.data(), s.size());
-    const int64_t k = index.find(h, s, [this](size_t i) { return names[i]; });
-    if (k >= 0) return (int32_t)k;
-    names.push_back(s);
-    index.insert(h);
-    return (int32_t)(names.size() - 1);
+  std::vector<uint64_t> hash;    // per id (the merge's shard key)
+  struct Slot {
+    uint64_t k0, k1;             // key bytes (<= 16) zero-padded, or (hash, 0) for a longer key
+    uint32_t id1;                // id + 1; 0 = empty
+    uint32_t len;
+  };
+  std::vector<Slot> slot;
+  size_t mask = 0;
+
+  int32_t get_or_add(std::string_view s) { return get_or_add(s, hash_bytes(s.data(), s.size())); }
+  // the slot line of hash h into cache ahead of get_or_add(s, h) (the ingest issues it before parsing
+  // the row's numbers)
+  void prefetch(uint64_t h) const {
+    if (!slot.empty()) __builtin_prefetch(&slot[h & mask]);
+  }
+  int32_t get_or_add(std::string_view s, uint64_t h) {
+    const size_t n = s.size();
+    uint64_t k0 = 0, k1 = 0;
+    if (n <= 16) {
+      std::memcpy(&k0, s.data(), n < 8 ? n : 8);
+      if (n > 8) std::memcpy(&k1, s.data() + 8, n - 8);
+    } else {
+      k0 = h;
+    }
+    if (2 * (names.size() + 1) > slot.size()) grow();
+    for (size_t i = h & mask;; i = (i + 1) & mask) {
+      Slot& x = slot[i];
+      if (x.id1 == 0) {
+        x = Slot{k0, k1, (uint32_t)names.size() + 1, (uint32_t)n};
+        names.push_back(s);
+        hash.push_back(h);
+        return (int32_t)(names.size() - 1);
+      }
+      if (x.len == n && x.k0 == k0 && x.k1 == k1 && (n <= 16 || names[x.id1 - 1] == s)) return (int32_t)(x.id1 - 1);
+    }
+  }
+
+ private:
+  void grow() {
+    std::vector<Slot> old;
+    old.swap(slot);
+    slot.assign(std::max<size_t>(64, 2 * old.size()), Slot{0, 0, 0, 0});
+    mask = slot.size() - 1;
+    for (const Slot& x : old)
+      if (x.id1) {
+        size_t i = hash[x.id1 - 1] & mask;
+        while (slot[i].id1) i = (i + 1) & mask;
+        slot[i] = x;
+      }
   }
 };
 
@@ -134,10 +199,10 @@ class TextTable {
   std::vector<std::vector<int>> dict_groups;     // columns sharing one dictionary
   std::vector<TextChunk> chunks;                 // owned text
   int64_t bytes_in = 0;                          // text ingested so far (row-count estimates)
-  std::vector<RowSpan> rows;
-  std::vector<int32_t> weight;                   // per-row multiplicity (feedback rows: DUPFACTOR)
-  std::vector<std::vector<double>> num;          // [numeric_cols.size()][rows]
-  std::vector<std::vector<int32_t>> ids;         // per dict column (flattened over groups) [rows]
+  ColVec<RowSpan> rows;
+  ColVec<int32_t> weight;                        // per-row multiplicity (feedback rows: DUPFACTOR)
+  std::vector<ColVec<double>> num;               // [numeric_cols.size()][rows]
+  std::vector<ColVec<int32_t>> ids;              // per dict column (flattened over groups) [rows]
   std::vector<int> dict_col_group;               // dict column slot -> group
   std::vector<int> dict_col_index;               // dict column slot -> column index
   std::vector<StringDict> dicts;                 // one per group

@@ -199,7 +199,7 @@ def build_sanitized(kind: str = "thread", verbose=False) -> Path:
     outdir.mkdir(parents=True, exist_ok=True)
     srcs = [CSRC / "native" / f for f in ("table.cpp", "dns.cpp", "lda_ref.cpp", "selftest.cpp")]
     exe = outdir / "native_selftest"
-    flags = ["-O1", "-g", "-fno-omit-frame-pointer", "-std=c++17", "-pthread", f"-I{CSRC / 'native'}"] + san
+    flags = ["-O1", "-g", "-fno-omit-frame-pointer", "-std=c++17", "-march=x86-64-v3", "-pthread", f"-I{CSRC / 'native'}"] + san
     digest = _hash(srcs + sorted((CSRC / "native").glob("*.h")), flags)
     if _stale(exe, digest):
         _run([cxx] + flags + [str(s) for s in srcs] + ["-o", str(exe)], verbose)

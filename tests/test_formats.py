@@ -105,6 +105,41 @@ def test_table_ingest_thread_invariance(tmp_path):
     assert outs[0] == outs[1]
 
 
+def test_table_numbers_and_long_names(tmp_path):
+    """Numeric fields through the exact short-number path (<= 15 digits, one '.') and the general
+    parse agree with a correctly rounded parse; names longer than the inline 16 key bytes (sharing a
+    16-byte prefix) stay distinct; lines of every length around the 32-byte scan blocks."""
+    rng = np.random.default_rng(5)
+    vals, lines = [], ["h,n,s"]
+    for i in range(4000):
+        nd = int(rng.integers(1, 19))
+        digits = "".join(str(d) for d in rng.integers(0, 10, nd))
+        dot = int(rng.integers(0, nd + 1))
+        txt = digits[:dot] + "." + digits[dot:] if rng.random() < 0.7 else digits
+        txt = ("-" if rng.random() < 0.2 else "") + txt
+        if txt in (".", "-."):
+            txt = "0"
+        vals.append(float(txt))
+        pad = "x" * int(rng.integers(1, 40))
+        name = "prefix-sixteen-b" + str(i % 97) if i % 3 == 0 else f"10.{i % 5}.{i % 7}.{pad[:3]}"
+        lines.append(f"{txt},{name},{pad}")
+    for txt in ["5.", ".5", "-0", "1e5", "2.5E-3", "7d", "+3", "0.1000000000000000055511151231257827"]:
+        vals.append(float(txt.rstrip("d")))
+        lines.append(f"{txt},z,q")
+    p = tmp_path / "nums.csv"
+    p.write_text("\n".join(lines) + "\n")
+    for th in (1, 5):
+        t = N.TextTable(3, [0], [[1]])
+        t.load_files([str(p)], drop_header=True, threads=th)
+        got = t.numeric(0)
+        assert t.num_rows == len(vals)
+        assert got.tolist() == vals
+        assert np.array_equal(np.signbit(got), np.signbit(np.array(vals)))
+        names = t.dict_names(0)
+        ids = t.dict_ids(1)
+        assert [names[j] for j in ids.tolist()] == [ln.split(",")[1] for ln in lines[1:]]
+
+
 def test_writer_kinds(tmp_path):
     t = N.TextTable(2, [0], [[1]])
     p = tmp_path / "t.csv"
