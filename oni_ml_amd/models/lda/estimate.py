@@ -57,6 +57,8 @@ class AsyncWriter:
             t.start()
 
     def _loop(self, q):
+        from ...utils.sched import background_priority
+        background_priority()
         while True:
             job = q.get()
             if job is None:

@@ -158,6 +158,8 @@ def background(fn, name: str = "oni-writer"):
     box = {}
 
     def body():
+        from ..utils.sched import background_priority
+        background_priority()
         try:
             fn()
         except BaseException as e:  # noqa: BLE001 -- handed to the joiner

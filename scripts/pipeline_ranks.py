@@ -137,6 +137,7 @@ def main():
             run = dict(kind=kind, tol=tol, ranks=n, process_wall_s=round(wall, 3), pipeline_wall_s=round(pw, 3),
                        flagged=summ.get("scored"), rank0_key_quantiles=keyq, startup_marks=summ.get("startup_marks"), corpus=summ.get("corpus"),
                        em_iterations=summ.get("lda", {}).get("em_iterations"),
+                       lda_seconds=summ.get("lda", {}).get("seconds"), lda_timing=summ.get("lda", {}).get("timing"),
                        stage_s=[{k: round(v, 3) for k, v in p.items()} for p in per_rank],
                        rank0_serial_s=round(serial, 3) if n > 1 else None,
                        rank0_serial_share=round(serial / pw, 4) if n > 1 else None, output_gb=round(out_gb, 3))
