@@ -119,9 +119,27 @@ def cmd_ml_ops(argv):
         return 1
     from .utils import warmup
     warmup.early_hip_init(int(os.environ.get("LOCAL_RANK", "0")))   # HIP context while torch imports
-    import torch  # noqa: F401  (first: its import time is a start-up mark of its own)
-    MARKS["torch_imported"] = time.time()
     from . import config as CFG
+
+    def resolve(world):
+        return CFG.resolve(a.fdate, a.dsource, tol=float(a.tol) if a.tol is not None else None, conf_path=a.conf,
+                           lpath=a.lpath, flow_path=a.flow_path, dns_path=a.dns_path, top1m=a.top1m,
+                           topics=a.topics, alpha=a.alpha, dupfactor=a.dupfactor, gpus=world, backend=a.backend,
+                           compat=a.compat, seed=a.seed, start=a.start, resume=a.resume, threads=a.threads,
+                           write_doc_wc=a.keep_doc_wc, word_assignments=a.word_assignments,
+                           rank_gamma=a.rank_gamma, verbose=not a.quiet, cuts=a.cuts, hdfs=a.hdfs or None,
+                           hadoop=a.hadoop)
+    # one process, fresh run: the day's inputs are read on a thread while torch imports
+    # (pipeline/prefetch.py); the load stage takes the result
+    if (os.environ.get("ONI_PREFETCH", "1") != "0" and a.gpus <= 1 and int(os.environ.get("WORLD_SIZE", "1")) == 1
+            and not a.resume and not a.hdfs):
+        try:
+            from .pipeline import prefetch
+            prefetch.start_for(resolve(1))
+        except Exception:  # noqa: BLE001 -- a bad configuration is reported by the resolve below
+            pass
+    import torch  # noqa: F401  (its import time is a start-up mark of its own)
+    MARKS["torch_imported"] = time.time()
     from .models.lda.settings import LDASettings
     from .parallel import dist as D
     MARKS["package_imported"] = time.time()
@@ -132,12 +150,7 @@ def cmd_ml_ops(argv):
         torch.zeros(1, device=ctx.device)     # HIP runtime + context (the first device call)
     MARKS["device_ready"] = time.time()
     warm = warmup.start(ctx.device)           # first-stage kernels load while the inputs parse
-    cfg = CFG.resolve(a.fdate, a.dsource, tol=float(a.tol) if a.tol is not None else None, conf_path=a.conf,
-                      lpath=a.lpath, flow_path=a.flow_path, dns_path=a.dns_path, top1m=a.top1m, topics=a.topics,
-                      alpha=a.alpha, dupfactor=a.dupfactor, gpus=ctx.world_size, backend=a.backend, compat=a.compat,
-                      seed=a.seed, start=a.start, resume=a.resume, threads=a.threads, write_doc_wc=a.keep_doc_wc,
-                      word_assignments=a.word_assignments, rank_gamma=a.rank_gamma, verbose=not a.quiet,
-                      cuts=a.cuts, hdfs=a.hdfs or None, hadoop=a.hadoop)
+    cfg = resolve(ctx.world_size)
     if a.settings:
         cfg.settings = LDASettings.load(a.settings)
     _apply_lda_args(a, cfg.settings)

@@ -17,6 +17,7 @@ from ..corpus.builder import count_pairs, lda_pre
 from ..features import dns as FD
 from ..score import scorer as S
 from . import common as C
+from . import prefetch
 from .runner import StageRunner
 
 
@@ -35,8 +36,13 @@ def run(cfg, dist=None, device=None, log=print) -> dict:
     need_pre = not (R.done("lda_pre") and R.done("dns_pre"))
     if rank == 0 and (need_pre or not R.done("dns_post")):
         with R.stage("load") as res:
-            tab = FD.load_dns(cfg.dns_path, cfg.feedback_path(), cfg.dupfactor, strict=cfg.strict)
-            top = FD.load_top_domains(cfg.top1m)
+            got = prefetch.take(prefetch.dns_key(cfg))
+            res["prefetched"] = got is not None
+            if got is not None:
+                tab, top = got
+            else:
+                tab = FD.load_dns(cfg.dns_path, cfg.feedback_path(), cfg.dupfactor, strict=cfg.strict)
+                top = FD.load_top_domains(cfg.top1m)
             if not top:
                 log(f"warning: top-1m list {cfg.top1m!r} not found; every domain gets top_domain 0/2")
             res.update(rows=tab.n, raw_rows=tab.n_raw, feedback_rows=tab.n_feedback, dropped=tab.dropped,

@@ -23,6 +23,7 @@ from ..corpus.builder import concat, count_pairs, lda_pre
 from ..features import flow as FF
 from ..score import scorer as S
 from . import common as C
+from . import prefetch
 from .runner import StageRunner
 
 
@@ -47,7 +48,10 @@ def run(cfg, dist=None, device=None, log=print) -> dict:
     sharded = False     # several ranks: pipeline/sharded.py
     if rank == 0 and (need_pre or not R.done("flow_post")) and not sharded:
         with R.stage("load") as res:
-            ft = FF.load_flow(cfg.flow_path, cfg.feedback_path(), cfg.dupfactor, cfg.threads)
+            ft = prefetch.take(prefetch.flow_key(cfg))
+            res["prefetched"] = ft is not None
+            if ft is None:
+                ft = FF.load_flow(cfg.flow_path, cfg.feedback_path(), cfg.dupfactor, cfg.threads)
             res.update(ft.stats())
             summary["input"] = ft.stats()
     if need_pre:
@@ -148,7 +152,8 @@ def run(cfg, dist=None, device=None, log=print) -> dict:
         if not R.done("flow_post"):
             if ft is None:
                 # row-sharded pre stages: rank 0 reads the whole day for the scoring pass
-                ft = FF.load_flow(cfg.flow_path, cfg.feedback_path(), cfg.dupfactor, cfg.threads)
+                ft = prefetch.take(prefetch.flow_key(cfg)) or FF.load_flow(cfg.flow_path, cfg.feedback_path(),
+                                                                          cfg.dupfactor, cfg.threads)
             # documents built in this process: ip dictionary id -> doc row without the name lookup
             ip_rows = C.doc_rows_of(built.doc_keys, len(ft.ip_names)) if built is not None else None
             with R.stage("flow_post") as res:

@@ -47,3 +47,32 @@ def test_fast_exit_keeps_outputs(tmp_path):
         outs[v] = {f: (lp / f).read_bytes() for f in ("flow_results.csv", "doc_results.csv", "word_results.csv",
                                                       "final.gamma", "final.beta", "word-assignments.dat")}
     assert outs["1"] == outs["0"]
+
+
+def test_input_prefetch_keeps_outputs(tmp_path):
+    """The day's inputs read on a thread while torch imports (pipeline/prefetch.py, ONI_PREFETCH=1, the
+    default) give the same files as the load stage reading them itself; the load record says which."""
+    import json
+    from oni_ml_amd.synth.dns import generate_dns_day
+    env = dict(os.environ, PYTHONPATH=ROOT)
+    inp = tmp_path / "in"
+    subprocess.run([sys.executable, "-m", "oni_ml_amd", "synth", "flow", "--out", str(inp) + "/", "--events", "3000"],
+                   cwd=ROOT, env=env, check=True, capture_output=True)
+    g = generate_dns_day(str(tmp_path / "dns"), events=4000, seed=3, files=3)
+    (tmp_path / "none.conf").write_text("")
+    files = {"flow": ("flow_results.csv", "doc_results.csv", "word_results.csv", "final.gamma"),
+             "dns": ("dns_results.csv", "doc_results.csv", "word_results.csv", "final.gamma")}
+    for src, tol, extra in (("flow", "1e-3", ["--flow-path", str(inp)]),
+                            ("dns", "1e-2", ["--dns-path", g["dns_path"], "--top1m", g["top1m"]])):
+        outs = {}
+        for v in ("1", "0"):
+            lp = tmp_path / f"{src}{v}"
+            r = subprocess.run([sys.executable, "-m", "oni_ml_amd", "ml_ops", "20160122", src, tol, "--lpath", str(lp),
+                                "--conf", str(tmp_path / "none.conf"), "--quiet", "--backend", "cpu"] + extra,
+                               cwd=ROOT, env=dict(env, ONI_PREFETCH=v), capture_output=True, text=True, timeout=600)
+            assert r.returncode == 0, r.stderr[-2000:]
+            recs = [json.loads(x) for x in open(lp / "metrics.jsonl")]
+            load = [x for x in recs if x.get("stage") == "load" and x.get("status") == "ok"]
+            assert load and load[0]["prefetched"] is (v == "1")
+            outs[v] = {f: (lp / f).read_bytes() for f in files[src]}
+        assert outs["1"] == outs["0"], src
