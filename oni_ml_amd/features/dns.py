@@ -87,11 +87,19 @@ def dictionary_encode(values: List[str]):
 
 
 def featurize(tab: DnsTable, device, top_domains: Sequence[str], cuts: Optional[Dict[str, np.ndarray]] = None,
-              raw_only: bool = False, threads: int = 8) -> DnsFeatures:
+              raw_only: bool = False, threads: int = 8, host: Optional[dict] = None) -> DnsFeatures:
+    """``host``: the name features ``featurize`` already returned for a prefix-compatible row set of
+    the same table (dns_pre's, over every row, reused by dns_post over the raw rows): the per-row
+    arrays are cut to this call's rows; the domain / subdomain dictionaries are first-appearance over
+    the rows, so a prefix keeps its ids."""
     device = torch.device(device)
     n = tab.n_raw if raw_only else tab.n
-    data, off = _offsets(tab.column("dns_qry_name", n))
-    F = native.lib().dns_features(data, off, list(COUNTRY_CODES), list(top_domains), SPECIAL_DOMAIN, threads)
+    if host is not None and len(host["entropy"]) >= n:
+        m = len(host["entropy"])
+        F = {k: (v[:n] if isinstance(v, np.ndarray) and v.ndim == 1 and len(v) == m else v) for k, v in host.items()}
+    else:
+        data, off = _offsets(tab.column("dns_qry_name", n))
+        F = native.lib().dns_features(data, off, list(COUNTRY_CODES), list(top_domains), SPECIAL_DOMAIN, threads)
     w = torch.from_numpy(tab.weight[:n]).to(device)
     vals = dict(
         frame_len=torch.from_numpy(tab.frame_len[:n]).to(device),
@@ -110,9 +118,10 @@ def featurize(tab: DnsTable, device, top_domains: Sequence[str], cuts: Optional[
     else:
         cuts_t = {k: torch.as_tensor(np.asarray(v, np.float64), device=device) for k, v in cuts.items()}
     bins = {k: (vals[k].unsqueeze(-1) > cuts_t[k].unsqueeze(0)).sum(-1) for k in vals}
-    _, pc, _ = _pa()
-    qid, qnames = arrow_dictionary_encode(
-        pc.binary_join_element_wise(tab.column("dns_qry_type", n), tab.column("dns_qry_rcode", n), "_"))
+    pa, pc, _ = _pa()
+    qt, qr = tab.column("dns_qry_type", n), tab.column("dns_qry_rcode", n)
+    # the separator must have the columns' type (large_string once feedback rows are appended)
+    qid, qnames = arrow_dictionary_encode(pc.binary_join_element_wise(qt, qr, pa.scalar("_", qt.type)))
     top = torch.from_numpy(F["top_domain"].astype(np.int64)).to(device)
     key = top
     radix = dict(frame_len=len(cuts_t["frame_len"]) + 1, unix_tstamp=len(cuts_t["unix_tstamp"]) + 1,

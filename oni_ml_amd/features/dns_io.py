@@ -18,10 +18,24 @@ FEEDBACK_IDX = dict(frame_time=0, unix_tstamp=23, frame_len=1, ip_dst=2, dns_qry
                     dns_qry_type=5, dns_qry_rcode=6, dns_sev=18)
 
 
+_ARROW_THREADS = False
+
+
 def _pa():
+    global _ARROW_THREADS
     import pyarrow as pa
     import pyarrow.compute as pc
     import pyarrow.parquet as pq
+    if not _ARROW_THREADS:
+        # Arrow sizes its pool by the machine's cores (hundreds on a GPU host, of which a job gets 16):
+        # cap it at this process's share so a parquet read beside the torch import does not swamp it
+        _ARROW_THREADS = True
+        try:
+            n = int(os.environ.get("OMP_NUM_THREADS") or 0) or min(os.cpu_count() or 8, 16)
+            if pa.cpu_count() > n:
+                pa.set_cpu_count(n)
+        except (ValueError, AttributeError):
+            pass
     return pa, pc, pq
 
 

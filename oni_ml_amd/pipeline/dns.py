@@ -33,6 +33,7 @@ def run(cfg, dist=None, device=None, log=print) -> dict:
     tab = built = None
     doc_names = word_names = None
     top = None
+    pre_host = None      # dns_pre's name features: dns_post takes its raw rows' slice
     need_pre = not (R.done("lda_pre") and R.done("dns_pre"))
     if rank == 0 and (need_pre or not R.done("dns_post")):
         with R.stage("load") as res:
@@ -52,6 +53,7 @@ def run(cfg, dist=None, device=None, log=print) -> dict:
         if rank == 0:
             with R.stage("dns_pre") as res:
                 feat = FD.featurize(tab, device, top, threads=cfg.threads)
+                pre_host = feat.host
                 wsp = FD.DnsWordSpace(feat.cuts, feat.qpairs)
                 dwc = count_pairs(feat.ip, feat.word_key, feat.weight)
                 C.save_json(os.path.join(cfg.lpath, "dns_cuts.json"), dict(cuts={k: v.tolist() for k, v in feat.cuts.items()}))
@@ -119,7 +121,7 @@ def run(cfg, dist=None, device=None, log=print) -> dict:
 
         if not R.done("dns_post"):
             with R.stage("dns_post") as res:
-                res.update(score_dns(cfg, tab, top, tables, device, log))
+                res.update(score_dns(cfg, tab, top, tables, device, log, host=pre_host))
                 summary["scored"] = res.get("flagged")
         else:
             R.skip("dns_post")
@@ -131,7 +133,8 @@ def run(cfg, dist=None, device=None, log=print) -> dict:
     return summary
 
 
-def score_dns(cfg, tab: FD.DnsTable, top, tables: C.ModelTables, device, log=print, ctx=None, ip_map=None) -> dict:
+def score_dns(cfg, tab: FD.DnsTable, top, tables: C.ModelTables, device, log=print, ctx=None, ip_map=None,
+              host=None) -> dict:
     """dns_post_lda.scala:108-331.  ``ctx`` (several ranks): ``tab`` holds this rank's rows; cuts over
     every rank's raw rows; the survivors of all ranks merged into one ascending file.  ``ip_map``:
     doc row of every ip_dst id of the pre-LDA dictionary of ``tab`` (its raw rows' ids are a prefix)."""
@@ -143,7 +146,7 @@ def score_dns(cfg, tab: FD.DnsTable, top, tables: C.ModelTables, device, log=pri
     elif multi:
         from ..features import dns_dist as FDD
         cuts = FDD.global_cuts(ctx, tab, top, device, raw_only=True, threads=cfg.threads)
-    feat = FD.featurize(tab, device, top, cuts=cuts, raw_only=True, threads=cfg.threads)
+    feat = FD.featurize(tab, device, top, cuts=cuts, raw_only=True, threads=cfg.threads, host=host)
     wsp = FD.DnsWordSpace(feat.cuts, feat.qpairs)
     uk, inv = torch.unique(feat.word_key, return_inverse=True)
     unames = wsp.decode(uk.cpu().numpy())
@@ -164,10 +167,12 @@ def score_dns(cfg, tab: FD.DnsTable, top, tables: C.ModelTables, device, log=pri
     order = S.rank_flagged(key, flag)
     n = int(order.size)
     out = os.path.join(cfg.lpath, "dns_results.csv")
-    cols = []
-    for c in FD.COLUMNS:
-        ids, names = tab.take_encoded(c, order)
-        cols.append(("dict", names, ids))
+    # the flagged rows' 8 input columns, dictionary-encoded by Arrow on a thread each (its kernels
+    # release the GIL)
+    from concurrent.futures import ThreadPoolExecutor
+    with ThreadPoolExecutor(len(FD.COLUMNS)) as ex:
+        enc = list(ex.map(lambda c: tab.take_encoded(c, order), FD.COLUMNS))
+    cols = [("dict", names, ids) for ids, names in enc]
     H = feat.host
     o_t = torch.from_numpy(order).to(sc.device)
     cols += [

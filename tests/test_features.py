@@ -171,3 +171,30 @@ def test_arrow_dictionary_encode_first_appearance():
     arrl = pa.array(vals, pa.large_string())
     d3, o3 = _offsets(arrl)
     assert bytes(d3)[o3[7]:o3[8]].decode() == vals[7]
+
+
+def test_dns_post_features_reuse_pre_host(tmp_path):
+    """dns_post's featurization over the raw rows, with the name features dns_pre computed over every
+    row (feedback rows last) cut to the raw prefix, equals featurizing the raw rows from scratch."""
+    import torch
+    from oni_ml_amd.features import dns as FD
+    from oni_ml_amd.synth.dns import generate_dns_day
+    g = generate_dns_day(str(tmp_path / "d"), events=3000, seed=4, files=2)
+    tab = FD.load_dns(g["dns_path"], None, 1000, strict=True)
+    fb = [["2016-01-22 00:00:01", "1453420801", "120", "10.0.0.5", "new.feedback-only.example", "1", "1", "0"],
+          ["2016-01-22 00:00:02", "1453420802", "99", "10.0.0.6", "www.google.com", "1", "28", "3"]]
+    import pyarrow as pa
+    tables = [pa.table({c: tab.arrays[c][:tab.n_raw] for c in FD.COLUMNS})]
+    # rebuild with the feedback rows appended (frame_len / tstamp columns as the reader sees them)
+    full = FD.table_from_arrow([t.set_column(1, "unix_tstamp", pa.array(tab.unix_tstamp[:tab.n_raw]))
+                                 .set_column(2, "frame_len", pa.array(tab.frame_len[:tab.n_raw])) for t in tables], fb)
+    assert full.n_feedback == 2
+    top = FD.load_top_domains(g["top1m"])
+    pre = FD.featurize(full, "cpu", top, threads=2)
+    a = FD.featurize(full, "cpu", top, raw_only=True, threads=2)
+    b = FD.featurize(full, "cpu", top, raw_only=True, threads=2, host=pre.host)
+    assert torch.equal(a.word_key, b.word_key) and a.qpairs == b.qpairs and a.ip_names == b.ip_names
+    for k in ("domain_id", "subdomain_id", "subdomain_length", "num_periods", "entropy", "top_domain"):
+        assert np.array_equal(np.asarray(a.host[k]), np.asarray(b.host[k])), k
+    assert list(a.host["domains"]) == list(b.host["domains"])[:len(a.host["domains"])]
+    assert list(a.host["subdomains"]) == list(b.host["subdomains"])[:len(a.host["subdomains"])]
