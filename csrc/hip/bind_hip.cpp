@@ -9,6 +9,7 @@
 #include <pybind11/stl.h>
 
 #include <stdexcept>
+#include <tuple>
 #include <string>
 #include <vector>
 
@@ -107,14 +108,29 @@ PYBIND11_MODULE(_onihip, m) {
   });
   m.def("gs_mstep_control", [](u cw, u class_total, u beta, int V, int K, int KS, u scalars, u params, u ctl,
                                u hist, int hist_slots, u done_count, u stream, u rows, int n_rows, int newton,
-                               int estimate, double num_docs, u alpha_out) {
+                               int estimate, double num_docs, u alpha_out, u st_word_idx,
+                               std::vector<std::tuple<u, u, u, int>> st_sets) {
     oni::EMControlArgs c{P<const double>(scalars), P<double>(params), P<double>(ctl), P<double>(hist), hist_slots,
                          P<int>(done_count)};
     const oni::NewtonArgs nw{newton, estimate, num_docs, P<double>(alpha_out)};
     if (newton && !alpha_out) throw std::runtime_error("gs_mstep_control: alpha_out required with newton");
+    oni::StageFuseArgs sf;
+    if (st_sets.size() > 2) throw std::runtime_error("gs_mstep_control: at most 2 staged sets");
+    sf.word_idx = P<const int>(st_word_idx);
+    for (const auto& [ent, cnt, out, n] : st_sets) {
+      sf.tile_ent[sf.n_sets] = P<const int>(ent);
+      sf.tile_cnt[sf.n_sets] = P<const int>(cnt);
+      sf.out[sf.n_sets] = P<double>(out);
+      sf.n_tiles[sf.n_sets] = n;
+      ++sf.n_sets;
+    }
     oni::launch_gs_mstep_control(P<const double>(cw), P<const double>(class_total), P<double>(beta), V, K, KS,
-                                 P<const int>(rows), n_rows, c, nw, S(stream));
-  });
+                                 P<const int>(rows), n_rows, c, nw, S(stream), sf);
+  }, py::arg("cw"), py::arg("class_total"), py::arg("beta"), py::arg("V"), py::arg("K"), py::arg("KS"),
+     py::arg("scalars"), py::arg("params"), py::arg("ctl"), py::arg("hist"), py::arg("hist_slots"),
+     py::arg("done_count"), py::arg("stream"), py::arg("rows"), py::arg("n_rows"), py::arg("newton"),
+     py::arg("estimate"), py::arg("num_docs"), py::arg("alpha_out"), py::arg("st_word_idx") = 0,
+     py::arg("st_sets") = std::vector<std::tuple<u, u, u, int>>());
   m.def("gs_mstep", [](u cw, u class_total, u beta, int V, int K, int KS, u gate, u stream) {
     oni::launch_gs_mstep(P<const double>(cw), P<const double>(class_total), P<double>(beta), V, K, KS,
                          P<const double>(gate), S(stream));

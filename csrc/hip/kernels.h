@@ -138,10 +138,23 @@ void launch_gs_suff64(const int* word_ptr, const int* csc_ent, const int* order,
                       int n_light, const double* cphi, double* cw, double* part, const double* lik,
                       const double* ass, int lo, int hi, int KS, const double* gate, hipStream_t s,
                       const double* cw_base = nullptr);   // cw[w] = cw_base[w] + sum (nullable)
-// fp64 M-step + alpha Newton (workgroup 0) + EM control (last workgroup)
+// Staged rows refilled by the M-step launch itself (trailing workgroups): the next E-step's staged
+// copies of the longest documents' beta rows (launch_gs_stage's layout) computed straight from cw and
+// class_total, so no separate stage launch (and its inter-kernel gap) sits between the M-step and the
+// longest-document kernel.  n_sets = 0: none.
+struct StageFuseArgs {
+  const int* word_idx = nullptr;
+  const int* tile_ent[2] = {nullptr, nullptr};
+  const int* tile_cnt[2] = {nullptr, nullptr};
+  double* out[2] = {nullptr, nullptr};
+  int n_tiles[2] = {0, 0};
+  int n_sets = 0;
+  int blocks = 0;     // set by the launcher
+};
+// fp64 M-step + alpha Newton (workgroup 0) + EM control (last workgroup) [+ staged rows]
 void launch_gs_mstep_control(const double* cw, const double* class_total, double* beta, int V, int K, int KS,
                              const int* rows, int n_rows, const EMControlArgs& c, const NewtonArgs& nw,
-                             hipStream_t s);
+                             hipStream_t s, StageFuseArgs sf = StageFuseArgs());
 // lda-c random start on the device: cw[w][k] = 1/V + u(seed, k V + w) (k < K), 0 for padding;
 // the same values as csrc/native random_ss (counter-based splitmix64).
 void launch_init_random_ss(double* cw, int V, int K, int KS, unsigned long long seed, hipStream_t s);

@@ -2943,11 +2943,14 @@ __global__ __launch_bounds__(256) void init_random_ss_kernel(double* __restrict_
 // ----------------------------------------------------------------- M-step ---
 __device__ __forceinline__ double mle(double c, double ct) { return c > 0.0 ? c / ct : kExpM100; }
 
+// SKS > 0: the trailing sf.blocks workgroups refill staged rows at KS = SKS (one thread per staged
+// position: its word's row in SKS / 2 independent 16-byte loads, as gs_stage_kernel)
+template <int SKS>
 __global__ __launch_bounds__(256) void gs_mstep_control_kernel(const double* __restrict__ cw,
                                                                const double* __restrict__ ct,
                                                                double* __restrict__ beta, int V, int K, int KS,
                                                                const int* __restrict__ rows, int n_rows,
-                                                               EMControlArgs c, NewtonArgs nw) {
+                                                               EMControlArgs c, NewtonArgs nw, StageFuseArgs sf) {
   if (c.params[kParamDone] != 0.0) return;
   // with the alpha Newton (a serial chain of ~10-20 digamma / trigamma / exp / log steps on two lanes),
   // block 0 runs only the Newton and the other blocks compute beta beside it
@@ -2961,15 +2964,49 @@ __global__ __launch_bounds__(256) void gs_mstep_control_kernel(const double* __r
   const int total2 = (rows ? n_rows : V) * hq;
   const double2* cw2 = reinterpret_cast<const double2*>(cw);
   double2* beta2 = reinterpret_cast<double2*>(beta);
-  const int bx = newton ? (int)blockIdx.x - 1 : (int)blockIdx.x, nbx = newton ? (int)gridDim.x - 1 : (int)gridDim.x;
-  for (int g = bx * blockDim.x + threadIdx.x; bx >= 0 && g < total2; g += nbx * blockDim.x) {
-    const int k0 = (g % hq) * 2;
-    const int i = rows ? rows[g / hq] * hq + g % hq : g;
-    const double2 v = cw2[i];
-    double2 o;
-    o.x = k0 < K ? mle(v.x, ct[k0]) : 0.0;
-    o.y = k0 + 1 < K ? mle(v.y, ct[k0 + 1]) : 0.0;
-    beta2[i] = o;
+  const int sb0 = (int)gridDim.x - sf.blocks;   // the trailing sf.blocks workgroups refill staged rows
+  if constexpr (SKS > 0) {
+    if ((int)blockIdx.x >= sb0) {
+      // one thread per (tile, lane): the row's SKS / 2 pairs loaded together, mle(cw, ct) -- bit for bit
+      // the beta entries -- stored one 16-byte element per pair in [tile][pair][64 lanes]
+      constexpr int HQ = SKS / 2;
+      const int n0 = sf.n_tiles[0] * 64, n1 = sf.n_sets > 1 ? sf.n_tiles[1] * 64 : 0;
+      for (int e = ((int)blockIdx.x - sb0) * (int)blockDim.x + (int)threadIdx.x; e < n0 + n1;
+           e += sf.blocks * (int)blockDim.x) {
+        const int set = e < n0 ? 0 : 1;
+        const int el = set ? e - n0 : e;
+        const int t = el >> 6, l = el & 63;
+        double2 v[HQ];
+        if (l < sf.tile_cnt[set][t]) {
+          const double2* row = cw2 + (size_t)sf.word_idx[sf.tile_ent[set][t] + l] * HQ;
+#pragma unroll
+          for (int k = 0; k < HQ; ++k) v[k] = row[k];
+#pragma unroll
+          for (int k = 0; k < HQ; ++k) {
+            v[k].x = 2 * k < K ? mle(v[k].x, ct[2 * k]) : 0.0;
+            v[k].y = 2 * k + 1 < K ? mle(v[k].y, ct[2 * k + 1]) : 0.0;
+          }
+        } else {
+#pragma unroll
+          for (int k = 0; k < HQ; ++k) v[k] = double2{0.0, 0.0};
+        }
+        double2* o = reinterpret_cast<double2*>(sf.out[set]) + (size_t)t * HQ * 64 + l;
+#pragma unroll
+        for (int k = 0; k < HQ; ++k) o[k * 64] = v[k];
+      }
+    }
+  }
+  if ((int)blockIdx.x < sb0) {
+    const int bx = newton ? (int)blockIdx.x - 1 : (int)blockIdx.x, nbx = newton ? sb0 - 1 : sb0;
+    for (int g = bx * blockDim.x + threadIdx.x; bx >= 0 && g < total2; g += nbx * blockDim.x) {
+      const int k0 = (g % hq) * 2;
+      const int i = rows ? rows[g / hq] * hq + g % hq : g;
+      const double2 v = cw2[i];
+      double2 o;
+      o.x = k0 < K ? mle(v.x, ct[k0]) : 0.0;
+      o.y = k0 + 1 < K ? mle(v.y, ct[k0 + 1]) : 0.0;
+      beta2[i] = o;
+    }
   }
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -3313,14 +3350,43 @@ void launch_gs_suff64(const int* word_ptr, const int* csc_ent, const int* order,
 
 void launch_gs_mstep_control(const double* cw, const double* class_total, double* beta, int V, int K, int KS,
                              const int* rows, int n_rows, const EMControlArgs& c, const NewtonArgs& nw,
-                             hipStream_t s) {
+                             hipStream_t s, StageFuseArgs sf) {
   const int64_t total = (int64_t)(rows ? n_rows : V) * KS;
   int64_t blocks = (total / 2 + 255) / 256;
   if (blocks > 512) blocks = 512;
   if (blocks < 1) blocks = 1;
   if (nw.enabled) blocks += 1;   // block 0: the alpha Newton alone
-  hipLaunchKernelGGL(gs::gs_mstep_control_kernel, dim3((unsigned)blocks), dim3(256), 0, s, cw, class_total, beta, V,
-                     K, KS, rows, n_rows, c, nw);
+  sf.blocks = 0;
+  if (sf.n_sets > 0) {
+    if (sf.n_sets > 2 || KS > 32 || KS % 2 || !sf.word_idx)
+      throw std::runtime_error("gs_mstep_control: staged rows need 1-2 sets, an even KS <= 32 and word_idx");
+    long long pos = 0;
+    for (int i = 0; i < sf.n_sets; ++i) {
+      if (sf.n_tiles[i] > 0 && (!sf.tile_ent[i] || !sf.tile_cnt[i] || !sf.out[i]))
+        throw std::runtime_error("gs_mstep_control: staged set without its tables");
+      pos += (long long)std::max(sf.n_tiles[i], 0) * 64;
+    }
+    if (pos > INT32_MAX) throw std::runtime_error("gs_mstep_control: too many staged positions");
+    sf.blocks = (int)std::min<long long>((pos + 255) / 256, 1024);   // one thread per staged position
+    blocks += sf.blocks;
+  }
+  if (sf.blocks == 0) {
+    hipLaunchKernelGGL(gs::gs_mstep_control_kernel<0>, dim3((unsigned)blocks), dim3(256), 0, s, cw, class_total,
+                       beta, V, K, KS, rows, n_rows, c, nw, sf);
+  } else {
+    switch (KS) {
+#define ONI_KS(X)                                                                                          \
+  case X:                                                                                                  \
+    if constexpr (X <= 32 && X % 2 == 0)                                                                   \
+      hipLaunchKernelGGL((gs::gs_mstep_control_kernel<X>), dim3((unsigned)blocks), dim3(256), 0, s, cw,    \
+                         class_total, beta, V, K, KS, rows, n_rows, c, nw, sf);                            \
+    break;
+      ONI_FOR_EACH_KS(ONI_KS)
+#undef ONI_KS
+      default:
+        throw std::runtime_error("gs_mstep_control: staged rows at unsupported KS " + std::to_string(KS));
+    }
+  }
   ONI_HIP_CHECK(hipGetLastError());
 }
 

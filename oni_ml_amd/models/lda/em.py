@@ -470,7 +470,10 @@ class LDAEngine:
         # early / late suff-stats (phase "all"): work[0], the longest-document bucket, runs alone on
         # streams[1] (late_s); the early pass joins every other stream
         ss = self._suff_split if (phase == "all" and len(gp.plan) + (gp.split is not None) >= 2) else None
-        used, late_s = self._launch_buckets(gp, ss is not None)
+        # one rank, fused EM iteration: this launch's M-step refills the staged rows for the next E-step,
+        # and this E-step uses the rows the previous M-step (or the batch's opening refill) left
+        fused = newton_key is not None and phase == "all" and bool(self._fused_stages(gp))
+        used, late_s = self._launch_buckets(gp, ss is not None, fused_stage=fused)
         if phase == "estep":             # the document kernels only (final inference pass)
             return
         scal = (self.lik, self.ass, 0, self.lik.numel())
@@ -480,7 +483,7 @@ class LDAEngine:
             H.gs_suff64(ss["wpL"], ss["ceL"], ss["planL"], self.cphi, self._cw_local, self._suff_part, gate=gate,
                         scalars=scal, base=ss["cw_early"])
             H.colsum_partials(self._suff_part, ss["planL"].n_blocks, self._red_local, gate=gate)
-            self._finish_suff64(newton_key)
+            self._finish_suff64(newton_key, stages=self._fused_stages(gp) if fused else ())
             return
         if phase == "A":
             H.gs_suff64(dc.word_ptr, dc.csc_ent, self._plan_a, self.cphi, self._cw_local,
@@ -491,9 +494,26 @@ class LDAEngine:
         H.gs_suff64(dc.word_ptr, dc.csc_ent, sp, self.cphi, self._cw_local, self._suff_part[:max(sp.n_blocks, 1)],
                     gate=gate, scalars=scal)
         H.colsum_partials(self._suff_part, sp.n_blocks, self._red_local, gate=gate)
-        self._finish_suff64(newton_key)
+        self._finish_suff64(newton_key, stages=self._fused_stages(gp) if fused else ())
 
-    def _launch_buckets(self, gp, late: bool = False, win=None):
+    def _fused_stages(self, gp) -> list:
+        """The staged-row sets of plan ``gp`` that the fused M-step launch refills (one rank, staged rows
+        refilled on the main stream, at most 2 sets; ``ONI_GS_STAGE_FUSE=0``: none, a gs_stage launch
+        before every E-step as before)."""
+        if (self._distributed or self._cwin is not None or os.environ.get("ONI_GS_STAGE_FUSE", "1") == "0"
+                or os.environ.get("ONI_GS_STAGE_AT", "main") != "main"):
+            return []
+        sts = [self._stages[id(order)] for _, order in gp.plan if id(order) in self._stages]
+        return sts if len(sts) <= 2 else []
+
+    def _refill_stages(self):
+        """gs_stage for every staged set of the plan (before a batch of fused EM iterations: beta may
+        have been set by the host since the last fused M-step)."""
+        from ...ops import hip as H
+        for st in self._fused_stages(self.gs_plan):
+            H.gs_stage(self.beta, self.dc.word_idx, st, gate=self._gate)
+
+    def _launch_buckets(self, gp, late: bool = False, win=None, fused_stage: bool = False):
         """The document kernels of GSPlan ``gp`` on 4 streams, joined back into the current stream.
         late: work[0] (the longest-document bucket) stays un-joined on streams[1], returned as late_s,
         for the early / late suff-stats; win: one of the c.phi windows (``_cphi_windows``) -- the document
@@ -505,7 +525,7 @@ class LDAEngine:
         # staged rows refilled before the fork (ONI_GS_STAGE_AT=main, default): the team8 launch is then
         # the first dispatched, instead of queueing behind the other buckets' workgroups for whole CUs
         stage_main = os.environ.get("ONI_GS_STAGE_AT", "main") == "main"
-        if stage_main:
+        if stage_main and not fused_stage:      # fused: the previous M-step launch refilled them
             for var, order in gp.plan:
                 st = self._stages.get(id(order))
                 if st is not None:
@@ -571,7 +591,7 @@ class LDAEngine:
         H.colsum_partials(self._suff_part, tp["sp"].n_blocks, self._red_local, gate=gate)
         self._finish_suff64(newton_key)
 
-    def _finish_suff64(self, newton_key):
+    def _finish_suff64(self, newton_key, stages=()):
         if self._distributed:
             if self._xchg is not None:
                 self._xchg.pack(self._cw_local)
@@ -579,7 +599,7 @@ class LDAEngine:
                 self.cw.copy_(self._cw_local)
             self._red.copy_(self._red_local)
         if newton_key is not None:
-            self._launch_beta_control(newton_key)
+            self._launch_beta_control(newton_key, stages)
 
     def _make_exchange(self, corpus: Corpus):
         """Sparse class_word exchange (parallel/dist.py VocabExchange) when the ranks' vocabularies
@@ -795,13 +815,15 @@ class LDAEngine:
         Every kernel is gated on params[DONE] (device-side convergence)."""
         return self._launch_estep64(newton_key, phase)
 
-    def _launch_beta_control(self, newton_key):
-        """beta, the alpha Newton (workgroup 0 of the same launch) and the EM convergence step."""
+    def _launch_beta_control(self, newton_key, stages=()):
+        """beta, the alpha Newton (workgroup 0 of the same launch) and the EM convergence step [and the
+        next E-step's staged rows, trailing workgroups]."""
         from ...ops import hip as H
         rows = self._xchg.local_rows32 if self._xchg is not None else None
         H.gs_mstep_control(self.cw, self.class_total, self.beta, self.K, self._scalars, self._params, self._ctl,
                            self._hist, self._done_count, rows=rows,
-                           newton=(newton_key[0], newton_key[1], self._alpha_dummy))
+                           newton=(newton_key[0], newton_key[1], self._alpha_dummy),
+                           stages=stages, word_idx=self.dc.word_idx)
 
     def _reduce_stats(self):
         """Cross-rank reduction of one EM iteration's statistics (outside the graphs): the packed
@@ -940,6 +962,8 @@ class LDAEngine:
             self._ctl.copy_(torch.tensor([likelihood_old, emc, 0.0, float(iteration), float(emx),
                                           1.0 if stop else 0.0, 0.0, 0.0], dtype=torch.float64))
         key = (bool(estimate_alpha), int(num_docs))
+        if not self._distributed:
+            self._refill_stages()       # the fused iterations below use staged rows of the current beta
         if not self._distributed and self.use_graph:
             # one rank: graphs of m = ONI_GRAPH_ITERS EM iterations (default 1), cached per m.  A batch
             # graph (m = the batch) measured the same per iteration (1.82-1.83 ms) but captures a new

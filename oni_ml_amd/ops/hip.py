@@ -457,10 +457,24 @@ def csc_subset(word_ptr, csc_ent, csc_doc, doc_mask):
     return ptr.to(torch.int32), csc_ent[keep].contiguous(), cnt.cpu().numpy()
 
 
-def gs_mstep_control(cw, class_total, beta, K, scalars, params, ctl, hist, done_count, rows=None, newton=None):
-    """fp64 M-step (beta = cw / class_total, exp(-100) floor) + alpha Newton + device EM control step."""
+def gs_mstep_control(cw, class_total, beta, K, scalars, params, ctl, hist, done_count, rows=None, newton=None,
+                     stages=(), word_idx=None):
+    """fp64 M-step (beta = cw / class_total, exp(-100) floor) + alpha Newton + device EM control step.
+    ``stages`` (at most 2 GSStage, with the corpus ``word_idx``): their staged rows refilled by trailing
+    workgroups of the same launch, from cw / class_total (bit-equal to gs_stage from the new beta)."""
     V, KS = cw.shape
     dev = cw.device
+    sets = []
+    for st in stages:
+        if st.KS != KS:
+            raise ValueError(f"staged rows of KS {st.KS}, cw has {KS}")
+        if st.n_tiles:
+            sets.append((_chk(st.tile_ent, torch.int32, "tile_ent", (st.n_tiles,), dev),
+                         _chk(st.tile_cnt, torch.int32, "tile_cnt", (st.n_tiles,), dev),
+                         _chk(st.buf, torch.float64, "stage", None, dev), int(st.n_tiles)))
+    if len(sets) > 2:
+        raise ValueError("gs_mstep_control: at most 2 staged sets")
+    wi = _chk(word_idx, torch.int32, "word_idx", None, dev) if sets else 0
     slots = hist.numel() // HIST_COLS
     n_rows = 0 if rows is None else int(rows.numel())
     rows_ptr = 0 if rows is None else _chk(rows, torch.int32, "rows", (n_rows,), dev)
@@ -472,7 +486,7 @@ def gs_mstep_control(cw, class_total, beta, K, scalars, params, ctl, hist, done_
         int(slots), _chk(done_count, torch.int32, "done_count", (1,), dev), _stream(), rows_ptr, n_rows,
         0 if newton is None else 1, 0 if newton is None else int(bool(newton[0])),
         0.0 if newton is None else float(newton[1]),
-        0 if newton is None else _chk(newton[2], torch.float64, "alpha_out", (1,), dev))
+        0 if newton is None else _chk(newton[2], torch.float64, "alpha_out", (1,), dev), wi, sets)
 
 
 def gs_mstep(cw, class_total, beta, K, gate=None):

@@ -134,6 +134,39 @@ def test_em_run_matches_cpu_engine():
     assert np.max(np.abs(b1 - b2)) < 1e-6
 
 
+@pytest.mark.gpu
+def test_mstep_refills_staged_rows_bitwise(monkeypatch):
+    """The M-step launch refilling the next E-step's staged rows (ONI_GS_STAGE_FUSE=1, default) gives
+    whole EM runs bitwise equal to a gs_stage launch before every E-step, and leaves each staged
+    position holding its word's final beta row."""
+    rng = np.random.default_rng(5)
+    V, D = 6000, 400
+    lens = np.minimum(rng.zipf(1.6, D), 120)
+    lens[:4] = [5000, 3000, 2500, 2100]
+    ptr = np.concatenate([[0], np.cumsum(lens)])
+    words = np.concatenate([rng.choice(V, n, replace=False) for n in lens]).astype(np.int32)
+    c = Corpus(ptr.astype(np.int64), words, rng.integers(1, 4, words.size).astype(np.int64), V)
+    runs = {}
+    for fuse in ("1", "0"):
+        monkeypatch.setenv("ONI_GS_STAGE_FUSE", fuse)
+        st = LDASettings(em_max_iter=7)
+        eng = LDAEngine(c, 20, st, backend="hip", seed=9, precision="fp64")
+        assert eng._stages and bool(eng._fused_stages(eng.gs_plan)) == (fuse == "1")
+        r = eng.run()
+        runs[fuse] = (np.array([x[0] for x in r.likelihoods]), eng.alpha, eng.gather_gamma(), eng.log_beta())
+        if fuse == "1":
+            beta = eng.beta.cpu().numpy()
+            for stg in eng._stages.values():
+                buf = stg.buf.view(-1, 10, 64, 2).cpu().numpy()
+                ent, cnt = stg.tile_ent.cpu().numpy(), stg.tile_cnt.cpu().numpy()
+                for t in range(len(ent)):
+                    got = buf[t].transpose(1, 0, 2).reshape(64, 20)[:cnt[t]]
+                    assert np.array_equal(got, beta[words[ent[t]:ent[t] + cnt[t]]])
+    (L1, a1, g1, b1), (L0, a0, g0, b0) = runs["1"], runs["0"]
+    assert len(L1) >= 3 and np.array_equal(L1, L0) and a1 == a0
+    assert np.array_equal(g1, g0) and np.array_equal(b1, b0)
+
+
 def test_gs64_graph_replay_and_gate():
     """The captured E-step graph replays bit-identically; a set done flag skips every launch."""
     c = _edge_corpus(seed=7, max_len=3000)
