@@ -600,35 +600,48 @@ static int64_t write_wide_rows(FILE* f, const int64_t* order, int64_t n, const s
                                const std::string& sep, int threads, int& werr) {
   const OutCol& k = cols.back();
   std::vector<OutCol> head(cols.begin(), cols.end() - 1);
-  std::vector<std::string> seg((size_t)threads);
+  // two buffer sets: a writer thread writes row i while the threads format row i + 1
+  std::vector<std::string> seg[2] = {std::vector<std::string>((size_t)threads),
+                                     std::vector<std::string>((size_t)threads)};
+  std::string pre[2];
   int64_t written = 0;
-  for (int64_t i = 0; i < n && !werr; ++i) {
+  std::thread writer;
+  auto flush = [&](int set) {
+    if (!pre[set].empty() && std::fwrite(pre[set].data(), 1, pre[set].size(), f) != pre[set].size())
+      werr = errno ? errno : EIO;
+    written += (int64_t)pre[set].size();
+    for (auto& x : seg[set]) {
+      if (werr) return;
+      if (!x.empty() && std::fwrite(x.data(), 1, x.size(), f) != x.size()) werr = errno ? errno : EIO;
+      written += (int64_t)x.size();
+    }
+  };
+  int set = 0;
+  for (int64_t i = 0; i < n; ++i, set ^= 1) {
     const int64_t r = order ? order[i] : i;
-    std::string pre;
+    pre[set].clear();
     if (!head.empty()) {
-      format_row(pre, r, head, sep);
-      pre.pop_back();                          // format_row's newline
-      pre += sep;
+      format_row(pre[set], r, head, sep);
+      pre[set].pop_back();                     // format_row's newline
+      pre[set] += sep;
     }
     const int64_t W = k.width;
+    std::vector<std::string>& cur = seg[set];
     run_parallel(threads, threads, [&](int t) {
       std::string s;
-      s.swap(seg[(size_t)t]);
+      s.swap(cur[(size_t)t]);
       s.clear();
       const int64_t j0 = W * t / threads, j1 = W * (t + 1) / threads;
       s.reserve((size_t)(j1 - j0) * 18);
       format_row_values(s, k, r, j0, j1);
-      s.swap(seg[(size_t)t]);
+      s.swap(cur[(size_t)t]);
     });
-    seg.back() += '\n';
-    if (!pre.empty() && std::fwrite(pre.data(), 1, pre.size(), f) != pre.size()) werr = errno ? errno : EIO;
-    written += (int64_t)pre.size();
-    for (auto& x : seg) {
-      if (werr) break;
-      if (!x.empty() && std::fwrite(x.data(), 1, x.size(), f) != x.size()) werr = errno ? errno : EIO;
-      written += (int64_t)x.size();
-    }
+    cur.back() += '\n';
+    if (writer.joinable()) writer.join();
+    if (werr) break;
+    writer = std::thread(flush, set);
   }
+  if (writer.joinable()) writer.join();
   return written;
 }
 

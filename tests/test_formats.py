@@ -203,7 +203,7 @@ def test_fixed10_and_py2_match_printf(tmp_path):
 
 def test_wide_rows_thread_invariant(tmp_path):
     """A K x V .beta file (few, very wide rows) is split over threads; output is identical to 1 thread."""
-    lb = np.random.default_rng(0).uniform(-100, 0, (7, 50_001))
+    lb = np.random.default_rng(0).uniform(-100, 0, (7, 70_001))   # >= 2^16 wide: the per-row segment path
     a, b = tmp_path / "a.beta", tmp_path / "b.beta"
     native.lib().write_rows(str(a), None, [("const", ""), ("fixedrow", lb, " ")], sep=" ", n=7, threads=1)
     native.lib().write_rows(str(b), None, [("const", ""), ("fixedrow", lb, " ")], sep=" ", n=7, threads=8)
