@@ -6,7 +6,13 @@ device context, and the lazy load of every code object at its first launch (the 
 kernels in ``_onihip``, torch's sort / unique / scan kernels).  Two overlaps:
 
 * ``early_hip_init``: the HIP runtime + primary context of this rank's device on a thread, before
-  ``import torch`` -- the ctypes call releases the GIL, so it runs while the interpreter imports torch;
+  ``import torch`` -- the ctypes call releases the GIL, so it runs while the interpreter imports torch.
+  OFF by default (``ONI_EARLY_HIP=1`` enables it): with the runtime initialised from that thread
+  while torch imported, the config-5 EM ran 25 iterations in 9.25-9.29 s in the five runs whose torch
+  import was quick and 5.89-5.93 s in the two whose import took 11 s (the thread long finished), and
+  6.00-6.09 s in all three runs without it (profiles/r4_config5.md) -- the side streams of the E-step
+  lose their overlap when the runtime comes up racing torch's first HIP calls.  Its start-up gain
+  was ~0.05 s;
 * ``start``: after the imports, a thread issues tiny versions of the first stages' GPU work (the torch
   ops featurization and the corpus builder use, one launch of each engine kernel family) on its own
   stream while the main thread parses the input files on the CPU.
@@ -26,7 +32,7 @@ import threading
 def early_hip_init(local_rank: int = 0):
     """Start HIP runtime + context creation for ``local_rank`` on a daemon thread (no torch needed).
     Returns the thread (or None when there is no HIP runtime)."""
-    if os.environ.get("ONI_EARLY_HIP", "1") == "0":
+    if os.environ.get("ONI_EARLY_HIP", "0") == "0":
         return None
 
     def run():

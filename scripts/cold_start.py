@@ -82,7 +82,7 @@ def main():
     ap.add_argument("--source", default="flow", choices=["flow", "dns"])
     ap.add_argument("--md")
     ap.add_argument("--json")
-    ap.add_argument("--variants", default="default;ONI_PYCACHE=0;ONI_FAST_EXIT=0;ONI_EARLY_HIP=0;ONI_WARMUP=1",
+    ap.add_argument("--variants", default="default;ONI_PYCACHE=0;ONI_FAST_EXIT=0;ONI_EARLY_HIP=1;ONI_WARMUP=1",
                     help="';'-separated env settings (space-separated KEY=VALUE within one), 'default' = none")
     ap.add_argument("--prof-out", help="keep the cProfile file here")
     a = ap.parse_args()
