@@ -10,9 +10,8 @@ kernels in ``_onihip``, torch's sort / unique / scan kernels).  Two overlaps:
   OFF by default (``ONI_EARLY_HIP=1`` enables it): with the runtime initialised from that thread
   while torch imported, the config-5 EM ran 25 iterations in 9.25-9.29 s in the five runs whose torch
   import was quick and 5.89-5.93 s in the two whose import took 11 s (the thread long finished), and
-  6.00-6.09 s in all three runs without it (profiles/r4_config5.md) -- the side streams of the E-step
-  lose their overlap when the runtime comes up racing torch's first HIP calls.  Its start-up gain
-  was ~0.05 s;
+  6.00-6.09 s in all three runs without it (profiles/r4_config5.md): the E-step is 1.55x slower when
+  the runtime comes up racing torch's first HIP calls.  Its start-up gain was ~0.05 s;
 * ``start``: after the imports, a thread issues tiny versions of the first stages' GPU work (the torch
   ops featurization and the corpus builder use, one launch of each engine kernel family) on its own
   stream while the main thread parses the input files on the CPU.
