@@ -16,7 +16,8 @@ run() {
 import json, sys
 d = json.load(open(sys.argv[1]))
 c = d["config"]
-print(f"{sys.argv[2]:10s} K={c['model'][-3:]} docs={c['docs_per_gpu']} V={c['vocab']} nnz={c['nnz_per_gpu']} "
+print(f"{sys.argv[2]:10s} K={c['model'][-3:]} docs={c.get('docs', c.get('docs_per_gpu'))} V={c['vocab']} "
+      f"nnz={c.get('nnz', c.get('nnz_per_gpu'))} "
       f"ms/iter={d['ms_per_step']} docs/s={d['value']:.3e} var_iter_mean={d.get('var_iter_mean')} "
       f"converge={d.get('converge_seconds')}s/{d.get('converge_em_iters')}it corpus_build={d.get('corpus_build_s')}s")
 PY
