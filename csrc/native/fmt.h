@@ -130,7 +130,8 @@ inline void put_digits12(char* dig, int64_t n) {
 inline int64_t scaled_round(double a, int k) {
   double p, err;                                // a * 10^k = p + err exactly
   two_prod(a, pow10_table()[k], &p, &err);
-  const double q = std::floor(p);
+  // floor(p) for 0 <= p < 2^53 (every caller): the truncating conversion, not a libm floor() call
+  const double q = (double)(int64_t)p;
   const double f = p - q;                       // exact
   const int64_t n = (int64_t)q;
   // round up iff f + err > 1/2, ties to even; d = f - 1/2 is exact (Sterbenz for f in [1/4, 1], exact
@@ -164,7 +165,7 @@ inline char* put_py2_float(char* w, double d, double* back = nullptr) {
     uint64_t bits;
     std::memcpy(&bits, &a, 8);
     const int e2 = (int)((bits >> 52) & 0x7ff) - 1022;          // a in [2^(e2-1), 2^e2)
-    int E = (int)std::floor((e2 - 1) * 0.30102999566398120);   // E or E - 1
+    int E = ((e2 - 1) * 78913) >> 18;          // floor((e2 - 1) log10 2) for |e2| < 1100: E or E - 1
     if (a >= ten_pow(E + 1)) ++E;               // almost always the decade now (the loop repairs the rest)
     int64_t N = 0;
     bool ok = false;
@@ -241,8 +242,22 @@ inline bool py2_value(double d, double* out) {
   uint64_t bits;
   std::memcpy(&bits, &a, 8);
   const int e2 = (int)((bits >> 52) & 0x7ff) - 1022;
-  int E = (int)std::floor((e2 - 1) * 0.30102999566398120);
-  if (a >= ten_pow(E + 1)) ++E;
+  int E = ((e2 - 1) * 78913) >> 18;            // floor((e2 - 1) log10 2), as put_py2_float
+  E += a >= ten_pow(E + 1) ? 1 : 0;             // (a select, not a data-dependent branch)
+  {
+    // the common case without branches on the data: E right, N in [10^11, 10^12], where N = 10^12 is
+    // a round-up into the next decade (12 digits "100000000000" one decade up: the same value)
+    int k = 11 - E;                             // 1 <= k <= 22 for 1e-11 <= a < 1e11
+    int64_t N = scaled_round(a, k);
+    if (__builtin_expect(N >= 100000000000LL && N <= 1000000000000LL, 1)) {
+      const int up = N == 1000000000000LL ? 1 : 0;
+      N = up ? 100000000000LL : N;
+      k -= up;
+      const double v = (double)N / pow10_table()[k];
+      *out = std::copysign(v, d);
+      return true;
+    }
+  }
   for (int tries = 0; tries < 3; ++tries) {
     const int k = 11 - E;
     if (k < 0 || k > 22) return false;

@@ -60,6 +60,7 @@ def main():
     ap.add_argument("--tol-quantile", type=float, default=None,
                     help="calibrate TOL: a first run at --tol records the score quantiles, every listed N then runs "
                          "at its key_q<Q> (so about Q of the events are flagged); Q in 1e-4, 1e-3, 1e-2, 0.1")
+    ap.add_argument("--cprofile", default=None, help="one-process runs under cProfile, stats written here")
     a = ap.parse_args()
     t_start = time.perf_counter()
 
@@ -100,10 +101,14 @@ def main():
                 cli += ["--no-word-assignments"]
             if a.lag is not None:
                 cli += ["--lag", str(a.lag)]
+            if a.cprofile and n == 1:    # the whole one-process run under cProfile (no fast exit: it writes at exit)
+                cli = ["-m", "cProfile", "-o", a.cprofile] + cli
             cmd = [sys.executable] + (cli if n == 1 else
                                       ["-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n),
                                        "--master-addr", "127.0.0.1", "--master-port", str(_port())] + cli)
             env = dict(os.environ, ONI_DIST_BACKEND=a.backend)
+            if a.cprofile:
+                env["ONI_FAST_EXIT"] = "0"
             t0 = time.perf_counter()
             r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=a.timeout)
             if a.json:      # the children's stderr (e.g. ONI_TABLE_PROFILE writer timings) next to the record
