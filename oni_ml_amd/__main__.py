@@ -1,4 +1,3 @@
-import os
 import sys
 import time
 
@@ -12,14 +11,12 @@ from . import cli  # noqa: E402
 
 cli.MARKS["main"] = _T_MAIN
 cli.MARKS["cli_imported"] = time.time()
-# the process leaves through os._exit after a completed ml_ops: the pipeline may keep its large
-# objects alive until then (pipeline/common.py HOLD_FOR_EXIT)
-cli.HOLD_FOR_EXIT = os.environ.get("ONI_FAST_EXIT", "1") != "0"
 rc = cli.main()
 if cli.FAST_EXIT:
     # ml_ops finished: every output file is closed and the process group is gone.  Leave without the
     # interpreter's and the HIP runtime's teardown (~0.5 s of a cold run's wall, profiles/r4_cold_start.md);
     # ONI_FAST_EXIT=0 keeps the full teardown
+    import os
     sys.stdout.flush()
     sys.stderr.flush()
     os._exit(rc or 0)

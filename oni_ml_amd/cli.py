@@ -31,8 +31,6 @@ import time
 MARKS = {}
 # set by a completed ml_ops when ONI_FAST_EXIT (default 1) allows `python -m oni_ml_amd` to skip teardown
 FAST_EXIT = False
-# set by `python -m oni_ml_amd` (it will os._exit after ml_ops): the pipeline keeps its large objects
-HOLD_FOR_EXIT = False
 
 
 def startup_marks() -> dict:
@@ -158,9 +156,7 @@ def cmd_ml_ops(argv):
     _apply_lda_args(a, cfg.settings)
     cfg.validate()
     from .pipeline import run
-    from .pipeline import common as PC
     from .pipeline.runner import RunLock
-    PC.HOLD_FOR_EXIT = HOLD_FOR_EXIT
     log = (lambda *x, **k: None) if (a.quiet or ctx.rank != 0) else print
     t0 = time.perf_counter()
     lock = None

@@ -151,20 +151,6 @@ def strict_tables(mt: ModelTables, strict: bool = True) -> ModelTables:
                        n.roundtrip_py2(np.ascontiguousarray(mt.phi)))
 
 
-# Set by `python -m oni_ml_amd` when the process will leave through os._exit after ml_ops: the
-# pipelines then keep their large host objects (the day's text table, name lists of millions of
-# strings, θ / φ tables) referenced until exit instead of freeing them object by object when run()
-# returns -- config 5 spent 3.6 s of its pipeline wall in that teardown (profiles/r4_config5.md); the
-# kernel reclaims the address space at exit in one pass.
-HOLD_FOR_EXIT = False
-_HELD = []
-
-
-def hold_for_exit(ns: dict) -> None:
-    if HOLD_FOR_EXIT:
-        _HELD.append(ns)
-
-
 def background(fn, name: str = "oni-writer"):
     """Run ``fn`` on a thread (the native writers release the GIL); returns the join callable a stage
     puts in ``result["_defer"]``, which re-raises the thread's exception."""

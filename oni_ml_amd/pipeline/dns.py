@@ -104,7 +104,6 @@ def run(cfg, dist=None, device=None, log=print) -> dict:
         gamma = log_beta = None
     if rank != 0:
         R.finish_deferred()
-        C.hold_for_exit(locals())
         return summary
     try:
 
@@ -131,7 +130,6 @@ def run(cfg, dist=None, device=None, log=print) -> dict:
         raise
     R.finish_deferred()
     summary["stage_seconds"] = dict(R.times)
-    C.hold_for_exit(locals())
     return summary
 
 
