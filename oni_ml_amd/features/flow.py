@@ -57,20 +57,21 @@ class FlowWordSpace:
         return torch.where(ok, i, torch.full_like(i, -1))
 
     def decode(self, keys: np.ndarray) -> List[str]:
+        """Word strings of ``keys``: one concatenation per word of a head ("[-1_]<port>_", one per
+        (port, side)) and a tail ("<time>_<ibyt>_<ipkt>", one per bin triple), both built once."""
         k = np.asarray(keys, np.int64)
         prefix = k % 2
         k = k // 2
-        pb = k % self.NP
-        k = k // self.NP
-        bb = k % self.NB
-        k = k // self.NB
-        tb = k % self.NT
-        port = k // self.NT
+        nt = self.NT * self.NB * self.NP
+        tail = k % nt                     # (tb * NB + bb) * NP + pb
+        port = k // nt
         from ..ops import native
         pstr = native.lib().java_double_array(np.asarray(self.ports, np.float64))
         bstr = [java_double(float(i)) for i in range(max(self.NT, self.NB, self.NP))]
-        return [("-1_" if pr else "") + f"{pstr[po]}_{bstr[t]}_{bstr[b]}_{bstr[p]}"
-                for pr, po, t, b, p in zip(prefix.tolist(), port.tolist(), tb.tolist(), bb.tolist(), pb.tolist())]
+        heads = [h for ps in pstr for h in (f"{ps}_", f"-1_{ps}_")]
+        tails = [f"{bstr[t]}_{bstr[b]}_{bstr[p]}" for t in range(self.NT) for b in range(self.NB)
+                 for p in range(self.NP)]
+        return [heads[h] + tails[t] for h, t in zip((port * 2 + prefix).tolist(), tail.tolist())]
 
 
 @dataclass

@@ -83,7 +83,12 @@ class FlowTable:
 
     @property
     def ip_names(self) -> List[str]:
-        return self.table.dict_names(0)
+        """The IP dictionary's names (built once: config 5's is millions of strings, read by lda_pre,
+        the post stage's row map and the scorer)."""
+        names = self.__dict__.get("_ip_names")
+        if names is None:
+            names = self.__dict__["_ip_names"] = self.table.dict_names(0)
+        return names
 
     def stats(self) -> dict:
         t = self.table
