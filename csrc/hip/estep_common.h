@@ -1,4 +1,4 @@
-// Device helpers of the split-document E-step (lda_gs64.hip gs_split / gs_splitw).
+// Device helpers of the split-document E-step kernels (lda_gs64.hip gs_splitw).
 #pragma once
 #include "common.h"
 #include "kernels.h"

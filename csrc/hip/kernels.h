@@ -132,6 +132,30 @@ int gs_split_umax(int KS); // largest gs_updates of the split kernel (64 at KS <
 void launch_gs_split(const GSArgs& a, const SplitArgs& s, int KS, hipStream_t st);
 int gs_split_capacity(int KS);
 
+// One long document over the CUs of one XCD (K <= 32, lda_xsplit.hip): G one-wave workgroups
+// (blocks b = x + 8 m of a launch of 8 x groups blocks share XCD x under the round-robin dispatch),
+// each holding its share of every chunk's beta rows in LDS for the whole E-step, exchange their
+// per-chunk partial topic sums as 16-byte self-tagged granules.  proto 1: L2-resident stores, used
+// only after the members have checked (one write-through round per launch) that they share an XCD;
+// otherwise (and proto 0) write-through stores.  All members of a launch must be co-resident.
+struct XSplitArgs {
+  const int* seg_doc;     // [n_blocks] document of each block, -1: none (the block leaves at once)
+  const int* seg_index;   // [n_blocks] member number within its document
+  const int* seg_count;   // [n_blocks] members of that document
+  const int* seg_base;    // [n_blocks] exchange row of the document's member 0
+  const int* doc_slot;    // [n_blocks] counter slot of the document
+  int n_blocks;           // grid
+  int n_rows;             // exchange rows (members over all documents of the launch)
+  unsigned* xchg;         // [2][n_rows][KS + 1] granules {lo, tag, hi, tag}
+  int* counter;           // [2][n_docs] launch epoch, exit count (as SplitArgs)
+  int n_docs;
+  int* error;             // set to 1 if a wait times out (never hangs the GPU)
+  int proto;              // 0: write-through stores; 1: L2-resident stores after the placement check
+  int* placed;            // [n_docs] written by member 0: 1 = members on one XCD (and proto 1 used)
+};
+void launch_gs_xsplit(const GSArgs& a, const XSplitArgs& s, int KS, hipStream_t st);
+int gs_xsplit_rows(int KS);   // LDS row capacity of one member (its words over all chunks of a sweep)
+
 // class_word[w] = sum over w's CSC entries of cphi rows (fixed order, no atomics); part
 // [nb][2 + KS] per-workgroup {lik slice, alpha_ss slice, column sums} for colsum_partials.
 void launch_gs_suff64(const int* word_ptr, const int* csc_ent, const int* order, int n_heavy, int n_medium,

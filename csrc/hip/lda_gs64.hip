@@ -41,6 +41,7 @@
 #include "common.h"
 #include "em_control.h"
 #include "estep_common.h"
+#include "gs_math.h"
 #include "kernels.h"
 
 namespace oni {
@@ -48,11 +49,6 @@ namespace gs {
 
 constexpr double kExpM100 = 3.720075976020836e-44;   // exp(-100), lda-c's log-probability floor
 
-// c*phi rows are written once per E-step and read once by the suff-stats pass: nontemporal
-// stores keep them from evicting the beta rows every document re-gathers each sweep
-typedef double dvec2 __attribute__((ext_vector_type(2)));
-
-constexpr int ilog2(int x) { return x <= 1 ? 0 : 1 + ilog2(x / 2); }
 constexpr int tg_of(int KS) { return KS <= 32 ? 4 : (KS <= 64 ? 8 : 16); }
 constexpr int kpl_of(int KS) { return (KS + tg_of(KS) - 1) / tg_of(KS); }
 // tiny kernel: wider topic groups than the team kernels (fewer topics, hence fewer
@@ -60,144 +56,6 @@ constexpr int kpl_of(int KS) { return (KS + tg_of(KS) - 1) / tg_of(KS); }
 constexpr int tiny_tg(int KS) { return KS <= 32 ? 8 : 16; }
 constexpr int tiny_kpl(int KS) { return (KS + tiny_tg(KS) - 1) / tiny_tg(KS); }
 constexpr int tiny_max(int KS) { return tiny_kpl(KS) <= 4 ? 8 : 4; }
-
-// 1/x for a positive normal double: v_rcp_f64 and two Newton steps (~1 ulp).
-__device__ __forceinline__ double drcp(double x) {
-  double r = __builtin_amdgcn_rcp(x);
-  double e = fma(-x, r, 1.0);
-  r = fma(r, e, r);
-  e = fma(-x, r, 1.0);
-  return fma(r, e, r);
-}
-
-// fp64 VALU results have a ~30-cycle dependent latency on gfx950 (scripts/micro/fp64_latency.hip:
-// a dependent v_fma_f64 chain runs at ~1/8 of the issue rate), so the transcendentals below are
-// written for a short dependency chain: Estrin-scheme polynomials (depth log2(degree) + 1 instead
-// of the degree) and one reciprocal where lda-c's digamma has seven.
-
-// Natural log of a positive normal double: y = 2^e m, m in [sqrt(1/2), sqrt(2)),
-// log m = 2 atanh(f) = 2f + f s P(s), f = (m - 1) / (m + 1), s = f^2 <= 0.0295, P through
-// s^10 (truncation < 1e-17), ln 2 split hi / lo.  ~2 ulp; ~15 dependent steps (OCML's log: ~100
-// instructions, ~490 cycles dependent).
-__device__ __forceinline__ double flog(double y) {
-  int e = __builtin_amdgcn_frexp_exp(y);
-  double mt = __builtin_amdgcn_frexp_mant(y);            // [0.5, 1)
-  const bool lo = mt < 0.70710678118654752;
-  mt = lo ? mt + mt : mt;
-  e = lo ? e - 1 : e;
-  const double f = (mt - 1.0) * drcp(mt + 1.0);
-  const double s = f * f, s2 = s * s, s4 = s2 * s2, s8 = s4 * s4;
-  // c_i = 2 / (2 i + 3), i = 0..10
-  const double a0 = fma(0.4, s, 0.66666666666666667), a1 = fma(0.22222222222222222, s, 0.28571428571428571);
-  const double a2 = fma(0.15384615384615385, s, 0.18181818181818182);
-  const double a3 = fma(0.11764705882352941, s, 0.13333333333333333);
-  const double a4 = fma(0.095238095238095238, s, 0.10526315789473684);
-  const double b0 = fma(a1, s2, a0), b1 = fma(a3, s2, a2), b2 = fma(0.086956521739130435, s2, a4);
-  const double P = fma(b2, s8, fma(b1, s4, b0));
-  const double de = (double)e;
-  return fma(de, 6.93147180369123816490e-01, fma(de, 1.90821492927058770002e-10, fma(f * s, P, f + f)));
-}
-
-// exp(x) for |x| < 700: x = k ln 2 + r, |r| <= ln2 / 2, degree-12 Taylor polynomial in Estrin
-// form (truncation < 2e-16 relative), 2^k by ldexp.
-__device__ __forceinline__ double fexp(double x) {
-  const double k = __builtin_rint(x * 1.44269504088896340736);
-  const double r = fma(-k, 1.90821492927058770002e-10, fma(-k, 6.93147180369123816490e-01, x));
-  const double r2 = r * r, r4 = r2 * r2, r8 = r4 * r4;
-  const double a0 = 1.0 + r, a1 = fma(1.66666666666666667e-01, r, 0.5);
-  const double a2 = fma(8.33333333333333333e-03, r, 4.16666666666666667e-02);
-  const double a3 = fma(1.98412698412698413e-04, r, 1.38888888888888889e-03);
-  const double a4 = fma(2.75573192239858907e-06, r, 2.48015873015873016e-05);
-  const double a5 = fma(2.50521083854417188e-08, r, 2.75573192239858907e-07);
-  const double b0 = fma(a1, r2, a0), b1 = fma(a3, r2, a2), b2 = fma(a5, r2, a4);
-  const double c0 = fma(b1, r4, b0), c1 = fma(2.08767569878680990e-09, r4, b2);
-  return __builtin_amdgcn_ldexp(fma(c1, r8, c0), (int)k);
-}
-
-// lda-c digamma (x + 6 shift, 4-term series, six recurrence terms) and
-// E = exp(psi - m).  The six reciprocals 1/(x+i) are (dA B + dB A) / (A B) with
-// A = x(x+1)(x+2), B = (x+3)(x+4)(x+5) (one reciprocal; A B < 1e54 for x < 1e9);
-// E = (x+6) exp(rest - m) does not wait on the log.
-__device__ __forceinline__ void psi_exp(double x, double m, double& psi, double& e) {
-  const double y = x + 6.0;
-  const double iy = drcp(y);
-  const double z = iy * iy;
-  const double x1 = x + 1.0, x2 = x + 2.0, x3 = x + 3.0, x4 = x + 4.0, x5 = x + 5.0;
-  const double A = x * x1 * x2, dA = fma(x, x1 + x2, x1 * x2);
-  const double B = x3 * x4 * x5, dB = fma(x3, x4 + x5, x4 * x5);
-  const double ser = fma(fma(0.004166666666667, z, -0.003968253986254), z * z,
-                         fma(0.008333333333333, z, -0.083333333333333)) * z;
-  const double rest = fma(-0.5, iy, ser) - fma(dA, B, dB * A) * drcp(A * B);
-  psi = flog(y) + rest;
-  e = y * fexp(rest - m);
-}
-
-// ln Gamma(x), x > 0: Stirling series at y = x + 6 (terms through 1/y^13, truncation
-// < 1e-13 absolute) and the recurrence lnG(x) = lnG(x + 6) - ln(x (x+1) ... (x+5)).
-// Same accuracy class as the libm lgamma lda-c calls, at a fraction of OCML's cost.
-__device__ __forceinline__ double lgamma_pos(double x) {
-  const double y = x + 6.0;
-  const double iy = drcp(y);
-  const double z = iy * iy;
-  const double ser = ((((((0.0064102564102564103 * z - 0.0019175269175269175) * z + 0.00084175084175084175) * z -
-                         0.00059523809523809524) * z + 0.00079365079365079365) * z - 0.0027777777777777778) * z +
-                      0.083333333333333333) * iy;
-  const double p = x * (x + 1.0) * (x + 2.0) * ((x + 3.0) * (x + 4.0) * (x + 5.0));
-  return (y - 0.5) * flog(y) - y + 0.91893853320467274 + ser - flog(p);
-}
-
-__device__ __forceinline__ double psi_only(double x) {
-  double p, e;
-  psi_exp(x, 0.0, p, e);
-  return p;
-}
-
-// ---- symmetric lane reductions (every participating lane ends with the same bits) ----
-// DIRECT: every exchange reads the partner lane itself (safe when only some lane groups are
-// active); otherwise xor 4 may route through the lanes of a neighbouring group (two DPP moves,
-// no LDS crossbar), which needs the whole 8-lane half-row active.
-template <int MASK, bool DIRECT = true>
-__device__ __forceinline__ double xsum(double x) {
-  using namespace detail;
-  if constexpr (MASK == 1) {
-    return x + xchg<kQuadXor1>(x);
-  } else if constexpr (MASK == 2) {
-    return x + xchg<kQuadXor2>(x);
-  } else if constexpr (MASK == 4 && !DIRECT) {
-    // xor 4 = row_half_mirror (l -> 7 - l within 8) then quad_perm [3,2,1,0]
-    return x + xchg<0x1B>(xchg<kRowHalfMirror>(x));
-  } else if constexpr (MASK == 4) {
-    const long long b = __double_as_longlong(x);
-    const int lo = __builtin_amdgcn_ds_swizzle((int)(b & 0xffffffffLL), 0x101F);
-    const int hi = __builtin_amdgcn_ds_swizzle((int)(b >> 32), 0x101F);
-    return x + __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
-  } else if constexpr (MASK == 8) {
-    return x + xchg<0x128>(x);   // row_ror:8 == xor 8 inside a 16-lane row
-  } else if constexpr (MASK == 16) {
-    return swap_combine<false>(x, add<double>);
-  } else {
-    static_assert(MASK == 32, "lane mask");
-    return swap_combine<true>(x, add<double>);
-  }
-}
-
-// sum over lane bits [LO, HI)
-template <int LO, int HI, bool DIRECT = true>
-__device__ __forceinline__ double bits_sum(double x) {
-  if constexpr (LO >= HI) {
-    return x;
-  } else {
-    return bits_sum<LO + 1, HI, DIRECT>(xsum<(1 << LO), DIRECT>(x));
-  }
-}
-
-__device__ __forceinline__ double params_vconv(const double* p) { return (double)(float)p[3]; }
-
-// lda-c: converged = (L_old - L) / L_old; the loop runs while converged > VAR_CONVERGED
-// and (var_iter < VAR_MAX_ITER or VAR_MAX_ITER == -1).
-__device__ __forceinline__ bool var_continue(double conv, double vconv, int it, int vmi) {
-  return conv > vconv && (it < vmi || vmi == -1);
-}
 
 // ------------------------------------------------------------------ tiny ----
 // C[j][.] (the current contribution of word j) is a register queue: word j always
@@ -595,7 +453,8 @@ __device__ __forceinline__ void stream_tail(const double* __restrict__ beta, con
 }
 
 // MINW: minimum waves per SIMD requested from the register allocator (the LDS-free one-wave team
-// at K > 32 is latency-bound on its per-word refresh chains; ONI_TEAM1_WAVES selects 1 / 3 / 4)
+// at K > 32 is latency-bound on its per-word refresh chains: 3 waves per SIMD, 13.2 -> 11.7 ms on the
+// K = 100 shard; 4 spilled, 19.5 ms -- profiles/r2_k100_split.md)
 template <int KS, int NW, int MINW = 1, bool GMT = false>
 __global__ __launch_bounds__(team_threads(KS, NW), MINW) void gs_team(GSArgs a) {
   using T = TeamShape<KS, NW>;
@@ -958,19 +817,17 @@ __global__ __launch_bounds__(team_threads(KS, NW), MINW) void gs_team(GSArgs a) 
 }
 
 // ----------------------------------------------------------------- split ----
-// One long document over G workgroups (the fp64 block Gauss-Seidel analogue of
-// lda_estep_split.hip).  Chunk j of a sweep (W = ceil(n / U) words) is
-// cut into G contiguous ranges of ceil(W / G) words; workgroup g gathers and reduces its
-// range's S_k = sum_n r_n b_nk and sum_n c_n log P_n, publishes them, and reads all G
-// partials back in segment order (the same bits in every workgroup), so the G replicas of
-// (gamma, psi, E, C) run the identical refresh and the identical lda-c convergence test:
-// one exchange per chunk and no second barrier.  A double travels as two tagged 8-byte
-// granules {uint32 half, uint32 tag} (relaxed agent-scope 64-bit stores / loads are
-// single-copy atomic); tag = (launch epoch, chunk sequence number) and the parity
-// double-buffer are as in the fp32 split kernel (estep_common.h): a workgroup reuses buffer
-// (seq & 1) at seq + 2 only after every segment has published seq + 1, i.e. after every
-// segment has finished reading seq.  The host caps a launch at the co-resident capacity
-// (gs_split_capacity), so the exchange cannot deadlock; a bounded wait sets `error`.
+// One long document over G workgroups (K > 32).  Chunk j of a sweep
+// (W = ceil(n / U) words) is cut into G contiguous ranges of ceil(W / G) words; workgroup g gathers
+// and reduces its range's S_k = sum_n r_n b_nk and sum_n c_n log P_n, publishes them, and reads all
+// G partials back in segment order (the same bits in every workgroup), so the G replicas of
+// (gamma, psi, E, C) run the identical refresh and the identical lda-c convergence test: one
+// exchange per chunk.  A double travels as two tagged 8-byte granules {uint32 half, uint32 tag}
+// (relaxed agent-scope 64-bit stores / loads are single-copy atomic); tag = (launch epoch, chunk
+// sequence number) (estep_common.h) and a parity double buffer: a workgroup reuses buffer (seq & 1)
+// at seq + 2 only after every segment has published seq + 1, i.e. after every segment has finished
+// reading seq.  The host caps a launch below the co-resident capacity (gs_split_capacity), so the
+// exchange cannot deadlock; a bounded wait sets `error`.
 __device__ __forceinline__ void put_tagged_bits(unsigned long long* p, unsigned v, unsigned tag) {
   __hip_atomic_store(p, ((unsigned long long)tag << 32) | (unsigned long long)v, __ATOMIC_RELAXED,
                      __HIP_MEMORY_SCOPE_AGENT);
@@ -1016,325 +873,14 @@ __device__ __forceinline__ bool tagged_sum_f64(const unsigned long long* x, int 
   return true;
 }
 
-template <int KS>
-__global__ __launch_bounds__(512) void gs_split(GSArgs a, SplitArgs sp) {
-  using T = TeamShape<KS, 8>;
-  constexpr int NW = 8, NTD = T::NTD, TG = T::TG, KPL = T::KPL, NSW = T::NSW, LSW = T::LSW, NS = T::NS,
-                TO = T::TO, RMAX = T::RMAX;
-  constexpr int NC = KS + 1;                 // exchanged columns: KS topic sums + the log-sum
-  constexpr int GR = 2 * NC;                 // granules per segment row
-  // NP gatherer threads per column, each summing a fixed contiguous range of the segments (one
-  // polling round trip for G <= 4 NP instead of one per 4 segments); the column's owner adds the
-  // NP partials in order, so every workgroup still gets the same bits
-  constexpr int NP = (NTD / NC) < 8 ? (NTD / NC) : 8;
-  static_assert(NP >= 1, "one exchange thread per topic plus one for the log-sum");
-  __shared__ double sC[kGsUMax][KS];
-  __shared__ double sEt[kGsUMax][KS];
-  __shared__ double sE[KS];
-  __shared__ double sRed[NW][KS];
-  __shared__ double sRedL[NW];
-  __shared__ double sCs[kGsUMax];
-  __shared__ double sScal[NW][4];
-  __shared__ double sPart[NP][NC];
-  __shared__ double sLW;
-  __shared__ int sFail;
-  if (a.params[kParamDone] != 0.0) return;
-  const int t = threadIdx.x, b = blockIdx.x;
-  const int d = sp.seg_doc[b], g = sp.seg_index[b], G = sp.seg_count[b], base = sp.seg_base[b];
-  int* counter = sp.counter + sp.doc_slot[b];
-  const int epoch = __hip_atomic_load(counter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  const double alpha = a.params[0], lik_const = a.params[1];
-  const int vmi = (int)a.params[2];
-  const double vconv = params_vconv(a.params);
-  const int K = a.K;
-  const int lane = t & 63, wv = t >> 6;
-  const int q = lane >> LSW, sl = lane & (NSW - 1);
-  const int slot = wv * NSW + sl;
-  const int s0 = a.doc_ptr[d], n = a.doc_ptr[d + 1] - s0;   // n > 0 (host)
-  const int U = a.gs_updates;
-  const int W = (n + U - 1) / U;
-  const int nch = (n + W - 1) / W;
-  const int WG = (W + G - 1) / G;             // words of a chunk per segment
-  const int nact = min(NW, (WG + NSW - 1) / NSW);
-  const bool active = wv < nact;
-  const int* __restrict__ wrow = a.word_idx + s0;
-  const float* __restrict__ crow = a.counts + s0;
-  auto range = [&](int j, int& m0, int& m1) {
-    const int n1 = min(n, (j + 1) * W);
-    m0 = min(n1, j * W + g * WG);
-    m1 = min(n1, m0 + WG);
-  };
-  for (int j = t; j < nch; j += NTD) sCs[j] = 0.0;
-  if (t == 0) {
-    sFail = 0;
-    sLW = 0.0;
-  }
-  lds_barrier();
-  for (int p = t; p < n; p += NTD) atomicAdd(&sCs[p / W], (double)crow[p]);   // integer counts: exact
-  lds_barrier();
-  double total = 0.0;
-  for (int j = 0; j < nch; ++j) total += sCs[j];
-  const double g0 = alpha + total / K;
-  const double m = psi_only(g0);
-  double gam[TO], psi[TO], lps[TO];
-#pragma unroll
-  for (int o = 0; o < TO; ++o) {
-    const int k = t + NTD * o;
-    gam[o] = k < K ? g0 : 0.0;
-    psi[o] = m;
-    lps[o] = 0.0;
-    if (k < KS) {
-      sE[k] = k < K ? 1.0 : 0.0;
-      for (int j = 0; j < nch; ++j) sC[j][k] = k < K ? sCs[j] / K : 0.0;
-    }
-  }
-  int wc[RMAX], wn[RMAX];
-  float cc[RMAX], cn[RMAX];
-  unsigned vc = 0, vn = 0;
-  double bc[RMAX][KPL];
-  auto load_ids = [&](int j, int (&w)[RMAX], float (&c)[RMAX], unsigned& v) {
-    int m0, m1;
-    range(j, m0, m1);
-    v = 0;
-#pragma unroll
-    for (int r = 0; r < RMAX; ++r) {
-      const int p = m0 + slot + r * NS;
-      v |= (active && p < m1) ? (1u << r) : 0u;
-      const int pc = max(0, min(p, m1 - 1));
-      w[r] = wrow[pc];
-      c[r] = crow[pc];
-    }
-  };
-  auto load_rows = [&](const int (&w)[RMAX], unsigned v) {
-    if (!active) return;
-#pragma unroll
-    for (int r = 0; r < RMAX; ++r) {
-      // rounds past this segment's range gather nothing (a segment is often one or two rounds)
-      const double* brow = a.beta + (size_t)w[r] * KS;
-#pragma unroll
-      for (int i = 0; i < KPL; ++i) bc[r][i] = ((v >> r) & 1u) ? brow[min(q + TG * i, KS - 1)] : 0.0;
-    }
-  };
-  load_ids(0, wc, cc, vc);
-  load_rows(wc, vc);
-  load_ids(nch > 1 ? 1 : 0, wn, cn, vn);
-  lds_barrier();
-  double L = 0.0, L_old = 0.0, conv = 1.0, GS = 0.0, LWs = 0.0;
-  int it = 0;
-  bool failed = false;
-  // phase timer (thread 0 of workgroup 0, a.dbg): word phase, barrier 1, publish + gather, barrier 2,
-  // refresh, barrier 3, sweep end, chunks
-  const bool timer = a.dbg != nullptr && b == 0 && t == 0;
-  long long ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  long long tc = timer ? clock64() : 0;
-  auto tick = [&](int i) {
-    if (timer) {
-      const long long x = clock64();
-      ph[i] += x - tc;
-      tc = x;
-    }
-  };
-  while (!failed && var_continue(conv, vconv, it, vmi)) {
-    ++it;
-#pragma unroll
-    for (int o = 0; o < TO; ++o) lps[o] = 0.0;
-    for (int j = 0; j < nch; ++j) {
-      ph[7] += timer ? 1 : 0;
-      if (active) {
-        int m0, m1;
-        range(j, m0, m1);
-        double E[KPL], acc[KPL], lw = 0.0;
-#pragma unroll
-        for (int i = 0; i < KPL; ++i) {
-          E[i] = (q + TG * i < KS) ? sE[q + TG * i] : 0.0;
-          acc[i] = 0.0;
-        }
-        double cr[RMAX];
-#pragma unroll
-        for (int r = 0; r < RMAX; ++r) cr[r] = ((vc >> r) & 1u) ? (double)cc[r] : 0.0;
-        // only the rounds this segment's range fills (workgroup-uniform)
-        const int R = (m1 - m0 + NS - 1) / NS;
-        if (R <= 1) {
-          word_steps<1, KPL, LSW>(E, bc, cr, acc, lw);
-        } else if (R <= 2 || RMAX <= 2) {
-          word_steps<(RMAX < 2 ? RMAX : 2), KPL, LSW>(E, bc, cr, acc, lw);
-        } else if (R <= 4 || RMAX <= 4) {
-          word_steps<(RMAX < 4 ? RMAX : 4), KPL, LSW>(E, bc, cr, acc, lw);
-        } else {
-          word_steps<RMAX, KPL, LSW>(E, bc, cr, acc, lw);
-        }
-        // beyond the prefetched rounds
-        stream_tail<RMAX, KS, KPL, TG, LSW>(a.beta, wrow, crow, m0 + slot + RMAX * NS, m1, NS, q, E, bc, acc, lw);
-        const int j1 = j + 1 < nch ? j + 1 : 0;
-        const int j2 = j1 + 1 < nch ? j1 + 1 : 0;
-#pragma unroll
-        for (int r = 0; r < RMAX; ++r) {
-          wc[r] = wn[r];
-          cc[r] = cn[r];
-        }
-        vc = vn;
-        load_rows(wc, vc);
-        load_ids(j2, wn, cn, vn);
-#pragma unroll
-        for (int i = 0; i < KPL; ++i) acc[i] = bits_sum<0, LSW, false>(acc[i]);
-        lw = group_sum<64>(q == 0 ? lw : 0.0);
-        if (sl == 0) {
-#pragma unroll
-          for (int i = 0; i < KPL; ++i)
-            if (q + TG * i < KS) sRed[wv][q + TG * i] = acc[i];
-        }
-        if (lane == 0) sRedL[wv] = lw;
-      }
-      tick(0);
-      lds_barrier();
-      tick(1);
-      // exchange: thread k < KS owns topic k, thread KS the log-sum
-      const int seq = (it - 1) * nch + j + 1;
-      const unsigned tag = split_tag(epoch, seq);
-      unsigned long long* xb = sp.xchg + (size_t)(seq & 1) * sp.n_blocks * GR;
-      if (t < NC) {
-        double part = 0.0;
-#pragma unroll
-        for (int v = 0; v < NW; ++v)
-          part += v < nact ? (t < KS ? sRed[v][t] : sRedL[v]) : 0.0;
-        const unsigned long long bits = (unsigned long long)__double_as_longlong(part);
-        unsigned long long* row = xb + (size_t)b * GR + 2 * t;
-        put_tagged_bits(row, (unsigned)(bits & 0xffffffffull), tag);
-        put_tagged_bits(row + 1, (unsigned)(bits >> 32), tag);
-      }
-      if (t < NP * NC) {
-        const int col = t % NC, pi = t / NC;
-        const int q0 = pi * G / NP, q1 = (pi + 1) * G / NP;
-        double ps;
-        if (!tagged_sum_f64(xb + (size_t)(base + q0) * GR + 2 * col, q1 - q0, GR, tag, ps)) {
-          sFail = 1;
-          __hip_atomic_store(sp.error, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        sPart[pi][col] = ps;
-      }
-      tick(2);
-      lds_barrier();
-      tick(3);
-      if (t < NC) {
-        double tot = 0.0;
-#pragma unroll
-        for (int pi = 0; pi < NP; ++pi) tot += sPart[pi][t];
-        if (t < KS) {
-          const int k = t;
-          const double Eo = sE[k];
-          const double nw = Eo * tot;
-          double En = 0.0;
-          if (k < K) {
-            lps[0] = fma(psi[0], nw, lps[0]);
-            gam[0] += nw - sC[j][k];
-            psi_exp(gam[0], m, psi[0], En);
-          }
-          sC[j][k] = nw;
-          sEt[j][k] = Eo;
-          sE[k] = En;
-        } else {
-          LWs += tot;
-        }
-      }
-      tick(4);
-      lds_barrier();
-      tick(5);
-      if (sFail) {
-        failed = true;
-        break;
-      }
-    }
-    if (failed) break;
-    // sweep likelihood (every workgroup of the document computes the same bits)
-    double gs = 0.0, lg = 0.0, lp = 0.0;
-#pragma unroll
-    for (int o = 0; o < TO; ++o) {
-      if (t + NTD * o < K) {
-        gs += gam[o];
-        lg += lgamma_pos(gam[o]);
-        lp += lps[o];
-      }
-    }
-    const double w1 = group_sum<64>(gs), w2 = group_sum<64>(lg), w3 = group_sum<64>(lp);
-    if (lane == 0) {
-      sScal[wv][1] = w1;
-      sScal[wv][2] = w2;
-      sScal[wv][3] = w3;
-    }
-    if (t == KS) {
-      sLW = LWs;
-      LWs = 0.0;
-    }
-    lds_barrier();
-    double LG = 0.0, LP = 0.0;
-    GS = 0.0;
-#pragma unroll
-    for (int v = 0; v < NW; ++v) {
-      GS += sScal[v][1];
-      LG += sScal[v][2];
-      LP += sScal[v][3];
-    }
-    L = lik_const - lgamma_pos(GS) + LG + fma(m, total, sLW) - LP;
-    conv = (L_old - L) / L_old;
-    L_old = L;
-    lds_barrier();
-    tick(6);
-  }
-  if (timer)
-    for (int i = 0; i < 8; ++i) a.dbg[i] = ph[i];
-  // every thread of this workgroup is past its last exchange (the loops end on a barrier)
-  split_exit(counter, sp.n_docs, G);
-  double ps = 0.0;
-#pragma unroll
-  for (int o = 0; o < TO; ++o) {
-    const int k = t + NTD * o;
-    if (k < K) ps += psi[o];
-    if (g == 0 && k < KS) a.gamma[(size_t)d * KS + k] = gam[o];
-  }
-  ps = group_sum<64>(ps);
-  if (lane == 0) sScal[wv][0] = ps;
-  lds_barrier();
-  if (g == 0 && t == 0) {
-    double PS = 0.0;
-    for (int v = 0; v < NW; ++v) PS += sScal[v][0];
-    a.lik[d] = failed ? __builtin_nan("") : L;   // a timed-out exchange surfaces as a NaN likelihood
-    a.alpha_ss[d] = PS - K * psi_only(GS);
-    a.iters[d] = it;
-  }
-  // final pass over this segment's ranges: c_n phi_nk = E_jk b_nk r_n with the final sweep's chunk E
-  if (!active) return;
-  for (int j = 0; j < nch; ++j) {
-    int m0, m1;
-    range(j, m0, m1);
-    double E[KPL];
-#pragma unroll
-    for (int i = 0; i < KPL; ++i) E[i] = (q + TG * i < KS) ? sEt[j][q + TG * i] : 0.0;
-    for (int p = m0 + slot; p < m1; p += NS) {
-      const double* brow = a.beta + (size_t)wrow[p] * KS;
-      const double c = (double)crow[p];
-      double bv[KPL];
-#pragma unroll
-      for (int i = 0; i < KPL; ++i) bv[i] = (q + TG * i < KS) ? brow[q + TG * i] : 0.0;
-      double pp = 0.0;
-#pragma unroll
-      for (int i = 0; i < KPL; ++i) pp = fma(E[i], bv[i], pp);
-      const double r = c * drcp(bits_sum<LSW, 6>(pp));
-      double* row = a.cphi + (size_t)(s0 + p) * KS;
-#pragma unroll
-      for (int i = 0; i < KPL; ++i)
-        if (q + TG * i < KS) __builtin_nontemporal_store(E[i] * bv[i] * r, &row[q + TG * i]);
-    }
-  }
-}
-
-// ------------------------------------------------------------ split, v2 ----
-// gs_split with the exchange in a dedicated topic wave (7 word waves + 1 topic wave): the word
-// waves leave their chunk partials in LDS, signal an LDS arrival counter and issue the NEXT chunk's
-// row prefetch at once; the topic wave sums the waves, publishes the segment's tagged granules,
-// sweeps the document's G segments and runs the refresh.  Its poll loads never queue behind row
-// prefetches (vmcnt is in order per wave, and the hand-off price sits in the consumer's memory
-// queue -- MI355X_MICROARCH handoff-1to1 / gather-pass), and a chunk costs one workgroup barrier
-// instead of three.  Same exchange buffer, tags, epoch and co-residency rules as gs_split.
+// ------------------------------------------------------------ split kernel ----
+// 7 word waves + 1 topic wave: the word waves leave their chunk partials in LDS, signal an LDS arrival
+// counter and issue the NEXT chunk's row prefetch at once; the topic wave sums the waves, publishes the
+// segment's tagged granules, sweeps the document's G segments and runs the refresh.  Its poll loads
+// never queue behind row prefetches (vmcnt is in order per wave, and the hand-off price sits in the
+// consumer's memory queue -- MI355X_MICROARCH handoff-1to1 / gather-pass), and a chunk costs one
+// workgroup barrier.  (The round-2 form with all three roles in the same eight waves and three barriers
+// per chunk was 3.82 vs 3.17 ms on the K = 50 split bucket and is gone; profiles/r3_tuning_log.md.)
 // UM: chunk-table rows in LDS (U <= UM): 32, or 64 where 2 x 64 x KS doubles still fit the 64 KB of
 // static LDS (KS <= 52: K = 50 at U = 64, the schedule that meets lda-c parity there,
 // profiles/r3_precision_parity.md)
@@ -1716,57 +1262,6 @@ __device__ __forceinline__ void wword_steps(const double (&E)[KS], const double 
   }
 }
 
-// Sum KS per-lane values over the 64 lanes of a wave and store topic totals into out[k]:
-// a reduce-scatter in registers, no LDS.  v_permlane32_swap (xor 32) and v_permlane16_swap
-// (xor 16) each combine a PAIR of values with one swap per dword (lanes of one half keep the
-// first value's sum, the other half the second's), leaving ceil(ceil(KS/2)/2) values per lane;
-// these are summed over the 16 lanes of each row by DPP (quad xor 1 / 2, half-mirror + quad
-// reverse = xor 4, row_ror 8 = xor 8).  Row rho = lane bits 5..4 then holds topics
-// (bit5 ? H1 : 0) + (bit4 ? H2 : 0) + i, i < H2.  Needs all 64 lanes active.
-__device__ __forceinline__ double swap_sum32(double first, double second) {
-  // permlane32_swap(vdst = first, vsrc = second) exchanges vdst's upper half with vsrc's lower
-  // half: vdst' = [first_lo, second_lo], vsrc' = [first_hi, second_hi], so the sum leaves lanes
-  // 0-31 with first's total and lanes 32-63 with second's
-  const unsigned long long f = (unsigned long long)__double_as_longlong(first);
-  const unsigned long long g = (unsigned long long)__double_as_longlong(second);
-  const auto lo = __builtin_amdgcn_permlane32_swap((unsigned)f, (unsigned)g, false, false);
-  const auto hi = __builtin_amdgcn_permlane32_swap((unsigned)(f >> 32), (unsigned)(g >> 32), false, false);
-  const double x = __longlong_as_double((long long)(((unsigned long long)hi[0] << 32) | lo[0]));
-  const double y = __longlong_as_double((long long)(((unsigned long long)hi[1] << 32) | lo[1]));
-  return x + y;
-}
-__device__ __forceinline__ double swap_sum16(double first, double second) {
-  // permlane16_swap(vdst = first, vsrc = second) exchanges vdst's odd rows with vsrc's even rows:
-  // the sum leaves rows 0 / 2 with first's total, rows 1 / 3 with second's
-  const unsigned long long f = (unsigned long long)__double_as_longlong(first);
-  const unsigned long long g = (unsigned long long)__double_as_longlong(second);
-  const auto lo = __builtin_amdgcn_permlane16_swap((unsigned)f, (unsigned)g, false, false);
-  const auto hi = __builtin_amdgcn_permlane16_swap((unsigned)(f >> 32), (unsigned)(g >> 32), false, false);
-  const double x = __longlong_as_double((long long)(((unsigned long long)hi[0] << 32) | lo[0]));
-  const double y = __longlong_as_double((long long)(((unsigned long long)hi[1] << 32) | lo[1]));
-  return x + y;
-}
-
-template <int KS>
-__device__ __forceinline__ void wave_topic_sums(const double (&acc)[KS], int lane, double* out) {
-  constexpr int H1 = (KS + 1) / 2, H2 = (H1 + 1) / 2;
-  double a1[H1];
-#pragma unroll
-  for (int i = 0; i < H1; ++i) a1[i] = swap_sum32(acc[i], i + H1 < KS ? acc[i + H1] : 0.0);
-  double a2[H2];
-#pragma unroll
-  for (int i = 0; i < H2; ++i) a2[i] = swap_sum16(a1[i], i + H2 < H1 ? a1[i + H2] : 0.0);
-#pragma unroll
-  for (int i = 0; i < H2; ++i) a2[i] = bits_sum<0, 4, false>(a2[i]);
-  const int base = ((lane >> 5) & 1) * H1 + ((lane >> 4) & 1) * H2;
-  const int i = lane & 15;
-  double v = 0.0;
-#pragma unroll
-  for (int ii = 0; ii < H2; ++ii) v = i == ii ? a2[ii] : v;
-  const bool hi4 = (lane >> 4) & 1;
-  if (i < H2 && (!hi4 || H2 + i < H1) && base + i < KS) out[base + i] = v;
-}
-
 // the row of word position p from a staged document copy ([n/64][KS/2][64] double2 tiles,
 // launch_gs_stage): 64 consecutive positions are 16-byte-contiguous per topic pair, so a wave's
 // gather of 64 words touches ~9 cache lines per instruction instead of 64 rows' worth
@@ -2033,10 +1528,12 @@ __global__ __launch_bounds__(wteam_threads(NW)) void gs_wteam(GSArgs a) {
 //    topic wave refreshes, off the chunk's critical path.
 // Arithmetic per word and per topic is that of gs_wteam (the likelihood's lw partial sums are
 // grouped by wave, so the two kernels agree to rounding, not bitwise).
-// EP (early prefetch, ONI_GS_EARLY_PREFETCH=EP): rounds u < EP of the next chunk's rows are gathered
+// EP (early prefetch): rounds u < EP of the next chunk's rows are gathered
 // into bc[u] as soon as the axpy of round u has consumed them -- before the topic sums and the
 // arrival -- so the address unit works beside the reduction; the other rounds after the arrival.
-template <int KS, int NW, int RMAX, int EP = 0, bool STG = false, bool TR = false>
+// (Measured slower and removed in round 5, records in profiles/r4_tuning_log.md: the topic wave summing
+// the word waves' lane partials, 5 or 3 word waves, two early rounds, the LDS-ring loader variant.)
+template <int KS, int NW, int RMAX, int EP = 0, bool STG = false>
 __global__ __launch_bounds__((NW + 1) * 64) void gs_wsteam(GSArgs a) {
   static_assert(KS <= 32 && KS % 2 == 0, "word team: KS <= 32");
   constexpr int NTD = (NW + 1) * 64, NS = NW * 64;
@@ -2047,13 +1544,6 @@ __global__ __launch_bounds__((NW + 1) * 64) void gs_wsteam(GSArgs a) {
   __shared__ double Cs[kGsUMax];        // chunk count sums
   __shared__ double sScal[NW + 1][4];   // sweep partials: lw per word wave; gamma sums (topic wave)
   __shared__ int arrive[NW];            // per word wave: chunks whose topic sums it has left in sRed
-  // TR (topic-wave reduction): a word wave leaves its 64 lanes' KS partial sums in LDS instead of
-  // reducing them across lanes (wave_topic_sums: ~1 k cycles of the word waves' SIMD time per chunk,
-  // two word waves per SIMD); the topic wave, idle while it waits for the arrivals, sums each wave's
-  // block as that wave arrives (lane = topic + KS x part, TRP parts of TRL lanes each, then the parts
-  // combined).  Rows [wave][topic][65]: the pad keeps both the writes and the reads conflict-free.
-  constexpr int TRP = TR ? (64 / KS < 4 ? 64 / KS : 4) : 1, TRL = (64 + TRP - 1) / TRP;
-  __shared__ double sAcc[TR ? NW * KS * 65 : 1];
   if (a.params[kParamDone] != 0.0) return;
   const int t = threadIdx.x;
   const int d = a.order[blockIdx.x];
@@ -2141,8 +1631,6 @@ __global__ __launch_bounds__((NW + 1) * 64) void gs_wsteam(GSArgs a) {
         ttick(3);
         const double gC = k < KS ? gam - C[j][k] : 0.0;
         double S = 0.0;
-        double s4[4] = {0.0, 0.0, 0.0, 0.0};
-        const int tk = lane % KS, tp = lane / KS;   // TR: this lane's topic and part
 #pragma unroll
         for (int v = 0; v < NW; ++v) {
           if (v < nact) {
@@ -2151,26 +1639,7 @@ __global__ __launch_bounds__((NW + 1) * 64) void gs_wsteam(GSArgs a) {
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
             if (ttimer && (v == 0 || v == 3 || v == 4 || v == nact - 1))
               tph[v == 0 ? 4 : v == 3 ? 5 : v == 4 ? 6 : 7] += clock64() - ttc;
-            if constexpr (TR) {
-              if (tp < TRP) {
-                const double* blk = sAcc + (v * KS + tk) * 65 + tp * TRL;
-#pragma unroll
-                for (int i = 0; i < TRL; ++i)
-                  if (tp * TRL + i < 64) s4[i & 3] += blk[i];
-              }
-            } else {
-              S += k < KS ? sRed[v][k] : 0.0;
-            }
-          }
-        }
-        if constexpr (TR) {
-          // part sums of topic tk sit in lanes tk + KS p: gathered into lane tk in part order
-          const double part = (s4[0] + s4[1]) + (s4[2] + s4[3]);
-          S = part;
-#pragma unroll
-          for (int pp = 1; pp < TRP; ++pp) {
-            const int src = min(lane + KS * pp, 63);
-            S += __shfl(part, src, 64);
+            S += k < KS ? sRed[v][k] : 0.0;
           }
         }
         ttick(0);
@@ -2316,12 +1785,7 @@ __global__ __launch_bounds__((NW + 1) * 64) void gs_wsteam(GSArgs a) {
           wword_steps<KS, 1>(E, b, &cp, acc, lw);
         }
         tick(0);
-        if constexpr (TR) {
-#pragma unroll
-          for (int kk = 0; kk < KS; ++kk) sAcc[(wv * KS + kk) * 65 + lane] = acc[kk];
-        } else {
-          wave_topic_sums<KS>(acc, lane, sRed[wv]);
-        }
+        wave_topic_sums<KS>(acc, lane, sRed[wv]);
         // (A) arrival: this wave's topic sums are in sRed.  A counter instead of a workgroup barrier,
         // so the refresh starts while the word waves are still issuing the next chunk's row loads
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");   // LDS only: no vmcnt wait
@@ -2377,421 +1841,6 @@ __global__ __launch_bounds__((NW + 1) * 64) void gs_wsteam(GSArgs a) {
     for (int p = n0 + t; p < n1; p += NS) {
       double b[KS];
       load_row(row_of(p), b);
-      double p0 = 0.0, p1 = 0.0, p2 = 0.0, p3 = 0.0;
-#pragma unroll
-      for (int kk = 0; kk < KS; kk += 4) {
-        p0 = fma(E[kk], b[kk], p0);
-        if (kk + 1 < KS) p1 = fma(E[kk + 1], b[kk + 1], p1);
-        if (kk + 2 < KS) p2 = fma(E[kk + 2], b[kk + 2], p2);
-        if (kk + 3 < KS) p3 = fma(E[kk + 3], b[kk + 3], p3);
-      }
-      const double r = (double)crow[p] * drcp((p0 + p1) + (p2 + p3));
-      dvec2* row = reinterpret_cast<dvec2*>(a.cphi + (size_t)(s0 + p) * KS);
-#pragma unroll
-      for (int kk = 0; kk < KS / 2; ++kk) {
-        const dvec2 v = {E[2 * kk] * b[2 * kk] * r, E[2 * kk + 1] * b[2 * kk + 1] * r};
-        __builtin_nontemporal_store(v, &row[kk]);
-      }
-    }
-  }
-}
-
-// ------------------------------------------------- word team, LDS ring -------
-// gs_ring: the longest documents (kGsTeam8 with staged rows, KS <= 32) as gs_wsteam computes them,
-// with the rows streamed into an LDS ring by NL dedicated LOADER WAVES (LDS-DMA: one
-// global_load_lds_dwordx4 moves one 1 KB topic-pair row of a 64-word staged tile).
-//
-// Why: one CU walks the longest document's rows 20 x U times per E-step, and in gs_wsteam every word
-// wave gathers the next chunk's rows into registers only after its own arrival -- the CU's load path
-// idles while the word waves compute and again while the topic wave refreshes, and the registers hold
-// exactly one chunk ahead.  Here the loader keeps up to DEPTH tiles in flight at all times, into
-// NSLOT ring slots (~140 KB of LDS, more than a chunk of the headline document), and recycles a slot
-// as soon as its tile is consumed: the load path streams through the refresh and the barriers.
-//
-// Synchronisation is by LDS flags only (no s_barrier after the set-up, so the loader never waits on
-// the compute waves' phases):
-//   full[s]  = q + 1 once item q (the q-th tile of the document stream: sweep, chunk, tile) landed
-//            in slot s = q mod NSLOT (the loader's counted vmcnt wait, then the flag);
-//   freed[s] = q + 1 once the word wave owning item q has read it;
-//   arrive[v] = chunks whose topic sums word wave v left in sRed; eready = chunks whose E the topic
-//            wave published; sarr[v] / sweep_seq = the same for the sweep-end likelihood; stop = 1 when
-//            the sweeps end (the loader drains its loads and leaves).
-// Tile i of a chunk (tiles 64-aligned in the document: the chunk's first and last tiles may be shared
-// with the neighbours and are streamed once per chunk) belongs to word wave own(i), spread so every
-// SIMD gets the same number of tiles.  Arithmetic per word and per topic is gs_wsteam's; the topic
-// sums add the word waves in wave order (the grouping differs from gs_wsteam: agreement to rounding).
-constexpr int kRingSpinLimit = 1 << 22;     // polls of one flag (~0.1 s) before the workgroup aborts
-
-template <int KS>
-struct RingGeom {
-  static constexpr int PAIRS = KS / 2;
-  static constexpr int ROWB = PAIRS * 1024;                    // [PAIRS][64] double2 of a tile
-  static constexpr int SLOTB = ROWB + 256;                     // + the tile's 64 float counts
-  static constexpr int LDS_OTHER = 16 * 1024;                  // the kernel's other LDS (tables, flags)
-  static constexpr int NSLOT_RAW = (160 * 1024 - LDS_OTHER) / SLOTB;
-  static constexpr int NSLOT = NSLOT_RAW > 16 ? 16 : NSLOT_RAW;
-  static constexpr int IPT = PAIRS + 1;                        // DMA instructions per tile
-  static constexpr int DEPTH_RAW = 63 / IPT;                   // vmcnt is 6 bits
-  static constexpr int DEPTH = DEPTH_RAW > 5 ? 5 : DEPTH_RAW;  // tiles in flight past a counted wait
-};
-
-// The loader's LDS-DMA is inline asm: hipcc's wait-count pass treats a pending
-// __builtin_amdgcn_global_load_lds as an LDS write and drains it (vmcnt(0)) at every LDS fence or flag
-// store, which would serialise the ring; invisible to it, the loads stay in flight and the loader
-// counts them itself (wait_vmcnt).  M0 (the destination base) is compiler-reserved: saved and restored
-// in the same statement (cdna_hip_programming.md, inline asm rules).
-__device__ __forceinline__ unsigned lds_offset(const void* p) {
-  return (unsigned)(size_t)((const __attribute__((address_space(3))) char*)p);
-}
-
-__device__ __forceinline__ void glds16(const void* src, unsigned lds_dst) {
-  unsigned keep;
-  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-               : "=&s"(keep) : "v"(src), "s"(lds_dst) : "memory");
-}
-
-__device__ __forceinline__ void glds4(const void* src, unsigned lds_dst) {
-  unsigned keep;
-  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dword %1, off\n\ts_mov_b32 m0, %0"
-               : "=&s"(keep) : "v"(src), "s"(lds_dst) : "memory");
-}
-
-// s_waitcnt vmcnt(N): the loader's own count of its LDS-DMA (invisible to the compiler)
-template <int N>
-__device__ __forceinline__ void wait_vmcnt() {
-  static_assert(N >= 0 && N < 64, "vmcnt is 6 bits");
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-}
-
-// wait until at most `left` tiles (IPT DMA instructions each) are in flight; left <= DEPTH
-template <int IPT, int DEPTH>
-__device__ __forceinline__ void ring_wait_tiles(int left) {
-  switch (left) {
-    case 0: wait_vmcnt<0>(); break;
-    case 1: wait_vmcnt<(DEPTH >= 1 ? IPT : 0)>(); break;
-    case 2: wait_vmcnt<(DEPTH >= 2 ? 2 * IPT : 0)>(); break;
-    case 3: wait_vmcnt<(DEPTH >= 3 ? 3 * IPT : 0)>(); break;
-    case 4: wait_vmcnt<(DEPTH >= 4 ? 4 * IPT : 0)>(); break;
-    default: wait_vmcnt<(DEPTH >= 5 ? 5 * IPT : 0)>(); break;
-  }
-}
-
-// the word wave owning tile i of a chunk: tiles round-robin over the SIMDs (wave v runs on SIMD v mod 4),
-// and over the word waves of a SIMD
-template <int NW>
-__device__ __forceinline__ int ring_owner(int i) {
-  const int s = i & 3, k = i >> 2;
-  const int per = (NW - s + 3) / 4;        // word waves on SIMD s: s, s + 4, ...
-  return s + 4 * (k % per);
-}
-
-template <int KS, int NW, int NL>
-__global__ __launch_bounds__((NW + 1 + NL) * 64) void gs_ring(GSArgs a) {
-  static_assert(KS <= 32 && KS % 2 == 0, "ring: KS <= 32");
-  static_assert(NW >= 4, "ring: every SIMD owns tiles");
-  using G = RingGeom<KS>;
-  constexpr int NS = NW * 64;
-  constexpr int MAXI = 2;                  // tiles per wave per chunk whose log P waits for the arrival
-  __shared__ __attribute__((aligned(16))) char ring[G::NSLOT * G::SLOTB];
-  __shared__ double C[kGsUMax][KS];        // chunk contributions (previous sweep)
-  __shared__ double Et[kGsUMax][KS];       // E each chunk used (final pass)
-  __shared__ double E_[KS];                // current E
-  __shared__ double sRed[NW][KS];          // per-wave topic sums of a chunk
-  __shared__ double Cs[kGsUMax];           // chunk count sums
-  __shared__ double sLw[NW];               // per-wave sweep sums of c log P
-  __shared__ double sLc[2];                // likelihood, conv of the last sweep
-  __shared__ int qbase[kGsUMax + 1];       // items of the chunks before chunk j (one sweep)
-  __shared__ int full[G::NSLOT], freed[G::NSLOT];
-  __shared__ int arrive[NW], sarr[NW];
-  __shared__ int eready, sweep_seq, stop;
-  __shared__ int abort_;                   // a wait ran past kRingSpinLimit: every wave leaves, lik = NaN
-  if (a.params[kParamDone] != 0.0) return;
-  const int t = threadIdx.x;
-  const int d = a.order[blockIdx.x];
-  if (d < 0) return;                       // placement gap (GSPlan.isolate_longest): whole workgroup
-  const double alpha = a.params[0], lik_const = a.params[1];
-  const int vmi = (int)a.params[2];
-  const double vconv = params_vconv(a.params);
-  const int K = a.K;
-  const int lane = t & 63, wv = __builtin_amdgcn_readfirstlane(t >> 6);   // wave-uniform (SGPR)
-  const int s0 = a.doc_ptr[d], n = a.doc_ptr[d + 1] - s0;
-  const int U = a.gs_updates;
-  const int W = n > 0 ? (n + U - 1) / U : 1;
-  const int nch = (n + W - 1) / W;
-  const float* __restrict__ crow = a.counts + s0;
-  for (int j = t; j < nch; j += (NW + 1 + NL) * 64) Cs[j] = 0.0;
-  if (t < G::NSLOT) full[t] = freed[t] = 0;
-  if (t < NW) arrive[t] = sarr[t] = 0;
-  if (t == 0) {
-    eready = 0;
-    sweep_seq = 0;
-    stop = 0;
-    abort_ = 0;
-    int q = 0;
-    for (int j = 0; j < nch; ++j) {
-      qbase[j] = q;
-      const int n0 = j * W, n1 = min(n, n0 + W);
-      q += ((n1 - 1) >> 6) - (n0 >> 6) + 1;
-    }
-    qbase[nch] = q;
-  }
-  lds_barrier();
-  for (int p = t; p < n; p += (NW + 1 + NL) * 64) atomicAdd(&Cs[p / W], (double)crow[p]);   // integer counts: exact
-  lds_barrier();                           // the last barrier: from here on flags only
-  double total = 0.0;
-  for (int j = 0; j < nch; ++j) total += Cs[j];
-  const double g0 = alpha + total / K;
-  const double m = psi_only(g0);
-  const int ips = qbase[nch];              // items per sweep
-  const dvec2* __restrict__ stg = reinterpret_cast<const dvec2*>(a.stage) + a.stage_off[blockIdx.x];
-  // bounded wait on an LDS flag: false when the workgroup aborted (a protocol fault never hangs the GPU)
-  auto wait_for = [&](const int* flag, int want, int sleep) -> bool {
-    int spins = 0;
-    while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < want) {
-      if (__hip_atomic_load(&abort_, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) return false;
-      if (++spins > kRingSpinLimit) {
-        __hip_atomic_store(&abort_, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        return false;
-      }
-      if (sleep) __builtin_amdgcn_s_sleep(1);
-    }
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
-    return true;
-  };
-
-  if (wv > NW) {
-    // --------------------------------------------------------------- loader waves
-    // loader l streams items l, l + NL, l + 2 NL, ...: c_ tiles issued, cp tiles published
-    __builtin_amdgcn_s_setprio(2);         // issue as soon as a slot frees (below the topic wave)
-    const int l = wv - (NW + 1);
-    int c_ = 0, cp = 0, j = 0, i = 0;
-    int n0 = 0, nt = nch > 0 ? qbase[1] : 0;
-    auto advance = [&]() {                 // (j, i) <- the stream's next tile (chunks, then sweeps, cyclic)
-      if (++i == nt) {
-        i = 0;
-        if (++j == nch) j = 0;
-        n0 = j * W;
-        nt = qbase[j + 1] - qbase[j];
-      }
-    };
-    auto item = [&](int cc) { return l + NL * cc; };
-    auto publish_to = [&](int upto) {      // own tiles [cp, upto) have landed (the caller's vmcnt wait)
-      for (; cp < upto; ++cp)
-        if (lane == 0)
-          __hip_atomic_store(&full[item(cp) % G::NSLOT], item(cp) + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    };
-    if (nch > 0)
-      for (int u = 0; u < l; ++u) advance();
-    while (nch > 0) {
-      if (__hip_atomic_load(&stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) ||
-          __hip_atomic_load(&abort_, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP))
-        break;
-      const int q = item(c_);
-      const int slot = q % G::NSLOT;
-      if (q >= G::NSLOT &&
-          __hip_atomic_load(&freed[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < q - G::NSLOT + 1) {
-        // the slot's previous tile is still being read: while waiting, land and publish the own tiles in
-        // flight one at a time, oldest first (a word wave may be waiting for exactly those) -- never a
-        // full drain, so the load pipe stays as deep as the free slots allow
-        bool quit = false;
-        int spins = 0;
-        while (__hip_atomic_load(&freed[slot], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < q - G::NSLOT + 1) {
-          if (cp < c_) {
-            ring_wait_tiles<G::IPT, G::DEPTH>(c_ - cp - 1);
-            publish_to(cp + 1);
-            continue;
-          }
-          if (__hip_atomic_load(&stop, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) ||
-              __hip_atomic_load(&abort_, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) { quit = true; break; }
-          if (++spins > kRingSpinLimit) {
-            __hip_atomic_store(&abort_, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            quit = true;
-            break;
-          }
-          __builtin_amdgcn_s_sleep(1);
-        }
-        if (quit) break;
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
-      }
-      const int tile = (n0 >> 6) + i;
-      const unsigned dst = __builtin_amdgcn_readfirstlane(lds_offset(ring) + (unsigned)(slot * G::SLOTB));
-      const dvec2* src = stg + (size_t)tile * G::PAIRS * 64 + lane;
-#pragma unroll
-      for (int k = 0; k < G::PAIRS; ++k) glds16(src + k * 64, dst + (unsigned)(k * 1024));
-      const int pc = min(tile * 64 + lane, n - 1);     // the last tile's lanes past the document end
-      glds4(crow + pc, dst + (unsigned)G::ROWB);
-      ++c_;
-      for (int u = 0; u < NL; ++u) advance();
-      if (c_ - cp > G::DEPTH) {
-        wait_vmcnt<G::DEPTH * G::IPT>();   // all but the last DEPTH own tiles have landed
-        publish_to(c_ - G::DEPTH);
-      }
-    }
-    wait_vmcnt<0>();                       // no LDS-DMA may land after the workgroup's waves are gone
-    return;
-  }
-
-  double L = 0.0, L_old = 0.0, conv = 1.0, GS = 0.0;
-  int it = 0;
-  if (wv == NW) {
-    // ---------------------------------------------------------------- topic wave
-    __builtin_amdgcn_s_setprio(3);
-    const int k = lane;
-    double gam = k < K ? g0 : 0.0, psi = m, lps = 0.0;
-    double Ecur = k < K ? 1.0 : 0.0;
-    if (k < KS) {
-      E_[k] = Ecur;
-      for (int j = 0; j < nch; ++j) C[j][k] = k < K ? Cs[j] / K : 0.0;
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
-    if (lane == 0) __hip_atomic_store(&eready, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    int gch = 0;                           // chunks refreshed so far
-    bool ok = true;
-    while (ok && var_continue(conv, vconv, it, vmi)) {
-      ++it;
-      lps = 0.0;
-      for (int j = 0; j < nch; ++j, ++gch) {
-        const double gC = k < KS ? gam - C[j][k] : 0.0;
-        double S = 0.0;
-#pragma unroll
-        for (int v = 0; v < NW; ++v) {
-          ok = ok && wait_for(&arrive[v], gch + 1, 1);
-          S += k < KS ? sRed[v][k] : 0.0;
-        }
-        if (!ok) break;
-        if (k < KS) {
-          const double Eo = Ecur;
-          const double nw = Eo * S;
-          double En = 0.0;
-          if (k < K) {
-            lps = fma(psi, nw, lps);
-            gam = fma(Eo, S, gC);
-            psi_exp(gam, m, psi, En);
-          }
-          E_[k] = En;
-          C[j][k] = nw;
-          Et[j][k] = Eo;
-          Ecur = En;
-        }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
-        if (lane == 0) __hip_atomic_store(&eready, gch + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      }
-      const bool own = k < K;
-      const double w1 = group_sum<64>(own ? gam : 0.0), w2 = group_sum<64>(own ? lgamma_pos(gam) : 0.0);
-      const double w3 = group_sum<64>(own ? lps : 0.0);
-      double LW = 0.0;
-#pragma unroll
-      for (int v = 0; v < NW; ++v) {
-        ok = ok && wait_for(&sarr[v], it, 1);
-        LW += sLw[v];
-      }
-      if (!ok) break;
-      GS = w1;
-      L = lik_const - lgamma_pos(GS) + w2 + fma(m, total, LW) - w3;
-      conv = (L_old - L) / L_old;
-      L_old = L;
-      if (lane == 0) {
-        sLc[0] = L;
-        sLc[1] = conv;
-        if (!var_continue(conv, vconv, it, vmi)) stop = 1;
-      }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
-      if (lane == 0) __hip_atomic_store(&sweep_seq, it, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    }
-    if (lane == 0) stop = 1;
-    if (!ok) L = __builtin_nan("");        // surfaces as a RuntimeError on the host (NaN likelihood)
-    const double ps = group_sum<64>(k < K ? psi : 0.0);
-    if (k < KS) a.gamma[(size_t)d * KS + k] = gam;
-    if (lane == 0) {
-      a.lik[d] = L;
-      a.alpha_ss[d] = ps - K * psi_only(GS);
-      a.iters[d] = it;
-    }
-    return;
-  }
-
-  // ------------------------------------------------------------------ word waves
-  int gch = 0;
-  bool ok = true;
-  while (ok && var_continue(conv, vconv, it, vmi)) {
-    ++it;
-    double lw = 0.0;
-    const int qs = (it - 1) * ips;
-    for (int j = 0; j < nch && ok; ++j, ++gch) {
-      if (!(ok = wait_for(&eready, gch + 1, 0))) break;
-      double E[KS], acc[KS];
-#pragma unroll
-      for (int kk = 0; kk < KS; ++kk) {
-        E[kk] = E_[kk];
-        acc[kk] = 0.0;
-      }
-      const int n0 = j * W, n1 = min(n, n0 + W);
-      const int nt = qbase[j + 1] - qbase[j];
-      double Pq[MAXI], cq[MAXI];
-      int nq = 0;
-      for (int i = 0; i < nt; ++i) {
-        if (ring_owner<NW>(i) != wv) continue;
-        const int q = qs + qbase[j] + i;
-        const int slot = q % G::NSLOT;
-        if (!(ok = wait_for(&full[slot], q + 1, 0))) break;
-        const char* sb = ring + slot * G::SLOTB;
-        const int p = ((n0 >> 6) + i) * 64 + lane;
-        const float cf = reinterpret_cast<const float*>(sb + G::ROWB)[lane];
-        const double c = (p >= n0 && p < n1) ? (double)cf : 0.0;
-        double b[KS];
-#pragma unroll
-        for (int k2 = 0; k2 < G::PAIRS; ++k2) {
-          const dvec2 v = reinterpret_cast<const dvec2*>(sb)[k2 * 64 + lane];
-          b[2 * k2] = v.x;
-          b[2 * k2 + 1] = v.y;
-        }
-        double p0 = 0.0, p1 = 0.0, p2 = 0.0, p3 = 0.0;
-#pragma unroll
-        for (int kk = 0; kk < KS; kk += 4) {
-          p0 = fma(E[kk], b[kk], p0);
-          if (kk + 1 < KS) p1 = fma(E[kk + 1], b[kk + 1], p1);
-          if (kk + 2 < KS) p2 = fma(E[kk + 2], b[kk + 2], p2);
-          if (kk + 3 < KS) p3 = fma(E[kk + 3], b[kk + 3], p3);
-        }
-        const double P = c > 0.0 ? (p0 + p1) + (p2 + p3) : 1.0;
-        // the slot's bytes are in registers (b and cf were consumed above): hand it back to the loader
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
-        if (lane == 0) __hip_atomic_store(&freed[slot], q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        const double r = c * drcp(P);
-#pragma unroll
-        for (int kk = 0; kk < KS; ++kk) acc[kk] = fma(r, b[kk], acc[kk]);
-        if (nq < MAXI) {
-          Pq[nq] = P;
-          cq[nq] = c;
-          ++nq;
-        } else {
-          lw = fma(c, flog(P), lw);
-        }
-      }
-      wave_topic_sums<KS>(acc, lane, sRed[wv]);
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
-      if (lane == 0) __hip_atomic_store(&arrive[wv], gch + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      for (int u = 0; u < nq; ++u) lw = fma(cq[u], flog(Pq[u]), lw);   // beside the refresh
-    }
-    if (!ok) break;
-    const double w0 = group_sum<64>(lw);
-    if (lane == 0) sLw[wv] = w0;
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
-    if (lane == 0) __hip_atomic_store(&sarr[wv], it, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    if (!(ok = wait_for(&sweep_seq, it, 1))) break;
-    L = sLc[0];
-    conv = sLc[1];
-  }
-  if (!ok) return;                         // aborted: the topic wave reports NaN
-  // final pass: c_n phi_nk = E_jk b_nk r_n with the final sweep's chunk E, rows from the staged copy
-  for (int j = 0; j < nch; ++j) {
-    const int n0 = j * W, n1 = min(n, n0 + W);
-    double E[KS];
-#pragma unroll
-    for (int kk = 0; kk < KS; ++kk) E[kk] = Et[j][kk];
-    for (int p = n0 + t; p < n1; p += NS) {
-      double b[KS];
-      load_row_staged<KS>(stg, p, b);
       double p0 = 0.0, p1 = 0.0, p2 = 0.0, p3 = 0.0;
 #pragma unroll
       for (int kk = 0; kk < KS; kk += 4) {
@@ -3087,13 +2136,7 @@ static void gs_estep_ks(const GSArgs& a, int variant, hipStream_t s) {
       if constexpr (KS > 32) {
         // 3 waves per SIMD (168 VGPRs, 12 B spilled): K = 100 shard team1 13.2 -> 11.7 ms; 4 (128 VGPRs,
         // 100 B spilled) 19.5 ms (profiles/r2_k100_split.md)
-        static const int tw = std::getenv("ONI_TEAM1_WAVES") ? std::atoi(std::getenv("ONI_TEAM1_WAVES")) : 3;
-        if (tw == 3)
-          hipLaunchKernelGGL((gs::gs_team<KS, 1, 3>), grid, blk, 0, s, a);
-        else if (tw == 4)
-          hipLaunchKernelGGL((gs::gs_team<KS, 1, 4>), grid, blk, 0, s, a);
-        else
-          hipLaunchKernelGGL((gs::gs_team<KS, 1>), grid, blk, 0, s, a);
+        hipLaunchKernelGGL((gs::gs_team<KS, 1, 3>), grid, blk, 0, s, a);
       } else {
         hipLaunchKernelGGL((gs::gs_team<KS, 1>), grid, blk, 0, s, a);
       }
@@ -3101,16 +2144,10 @@ static void gs_estep_ks(const GSArgs& a, int variant, hipStream_t s) {
     }
     case kGsTeam4:
       if constexpr (KS <= 32) {
-        // 1 (default): one wave per document, a word per lane, in-wave refresh -- 2.128 / 2.129 / 2.143 vs
-        // 2.136 / 2.141 / 2.144 ms per EM iteration for 3 (3 word waves + a topic wave), 3 A/B rounds:
+        // one wave per document, a word per lane, in-wave refresh: 2.128 / 2.129 / 2.143 vs 2.136 / 2.141 /
+        // 2.144 ms per EM iteration for 3 word waves + a topic wave (3 A/B rounds, profiles/r3_tuning_log.md):
         // a quarter of the waves for the same chains leaves the CUs to the other buckets
-        static const int mnw = std::getenv("ONI_GS_MID_NW") ? std::atoi(std::getenv("ONI_GS_MID_NW")) : 1;
-        if (mnw == 3)   // 3 word waves + the topic wave
-          hipLaunchKernelGGL((gs::gs_wsteam<KS, 3, 1>), dim3(a.n_items), dim3(256), 0, s, a);
-        else if (mnw == 1)   // one wave per document, a word per lane, in-wave refresh
-          hipLaunchKernelGGL((gs::gs_wteam<KS, 1, 1>), dim3(a.n_items), dim3(64), 0, s, a);
-        else
-          hipLaunchKernelGGL((gs::gs_wteam<KS, 4, 1>), dim3(a.n_items), dim3(256), 0, s, a);
+        hipLaunchKernelGGL((gs::gs_wteam<KS, 1, 1>), dim3(a.n_items), dim3(64), 0, s, a);
       }
       else if (a.gs_updates > kGsUMax)
         hipLaunchKernelGGL((gs::gs_team<KS, 4, 1, true>), dim3(a.n_items), dim3(256), 0, s, a);
@@ -3119,69 +2156,15 @@ static void gs_estep_ks(const GSArgs& a, int variant, hipStream_t s) {
       break;
     case kGsTeam8:
       if constexpr (KS <= 32) {
-        // longest documents: 8 waves x 2 prefetched words per lane; ONI_GS_BIG_NW=4 selects 4 waves x 4
-        // (measured on the headline corpus: 2.70 vs 2.96 ms, the 4-wave team has no second wave per
-        // SIMD to cover the fp64 dependency chains of the word phase)
-        static const int bnw = std::getenv("ONI_GS_BIG_NW") ? std::atoi(std::getenv("ONI_GS_BIG_NW")) : 7;
-        // (a dynamic-LDS pad keeping other buckets off the longest-document CUs measured no change:
-        // 2.175 vs 2.175 ms per EM iteration, profiles/r3_tuning_log.md)
-        // ONI_GS_EARLY_PREFETCH: next-chunk rounds gathered before the arrival (1, the default: 2.13-2.14
-        // vs 2.17-2.18 ms per EM iteration, 3 A/B rounds; 2 spills 192 B: 3.27 ms; 0 = after it)
-        static const int ep = std::getenv("ONI_GS_EARLY_PREFETCH") ? std::atoi(std::getenv("ONI_GS_EARLY_PREFETCH")) : 1;
-        // ONI_GS_RING=1: the LDS-ring kernel (loader wave + LDS-DMA) for the staged longest documents
-        // (read per launch, not cached: tests switch it within one process)
-        const char* ring_env = std::getenv("ONI_GS_RING");
-        const int ring = ring_env ? std::atoi(ring_env) : 0;
-        if (a.stage != nullptr && ring) {
-          if constexpr (KS % 2 == 0) {
-            if (ring >= 4)   // ONI_GS_RING=N: N loader waves (N times the LDS-DMA in flight)
-              hipLaunchKernelGGL((gs::gs_ring<KS, 7, 4>), dim3(a.n_items), dim3(768), 0, s, a);
-            else if (ring == 3)
-              hipLaunchKernelGGL((gs::gs_ring<KS, 7, 3>), dim3(a.n_items), dim3(704), 0, s, a);
-            else if (ring == 2)
-              hipLaunchKernelGGL((gs::gs_ring<KS, 7, 2>), dim3(a.n_items), dim3(640), 0, s, a);
-            else
-              hipLaunchKernelGGL((gs::gs_ring<KS, 7, 1>), dim3(a.n_items), dim3(576), 0, s, a);
-          }
-          else
-            throw std::runtime_error("gs_estep: ring needs an even KS");
-        } else if (a.stage != nullptr) {
-          // staged rows (launch_gs_stage): every next-chunk round gathered after the arrival is the
-          // default here (ONI_GS_EARLY_PREFETCH unset: 1.726-1.740 vs 1.824-1.833 ms per EM iteration
-          // for the early round-0 gather, 3 A/B rounds -- the contiguous loads no longer need the head start)
-          static const int eps = std::getenv("ONI_GS_EARLY_PREFETCH") ? std::atoi(std::getenv("ONI_GS_EARLY_PREFETCH")) : 0;
-          // ONI_GS_TOPIC_REDUCE=1: the topic wave sums the word waves' lane partials (gs_wsteam TR)
-          // (read per launch: tests switch it within one process)
-          const char* tr_env = std::getenv("ONI_GS_TOPIC_REDUCE");
-          const bool tr = tr_env && std::atoi(tr_env) != 0;
-          if (bnw == 7 && eps == 1)
-            hipLaunchKernelGGL((gs::gs_wsteam<KS, 7, 2, 1, true>), dim3(a.n_items), dim3(512), 0, s, a);
-          else if (bnw == 7 && eps == 0 && tr)
-            hipLaunchKernelGGL((gs::gs_wsteam<KS, 7, 2, 0, true, true>), dim3(a.n_items), dim3(512), 0, s, a);
-          else if (bnw == 7 && eps == 0)
-            hipLaunchKernelGGL((gs::gs_wsteam<KS, 7, 2, 0, true>), dim3(a.n_items), dim3(512), 0, s, a);
-          else if (bnw == 5 && eps == 0)
-            hipLaunchKernelGGL((gs::gs_wsteam<KS, 5, 3, 0, true>), dim3(a.n_items), dim3(384), 0, s, a);
-          else if (bnw == 3 && eps == 0)
-            hipLaunchKernelGGL((gs::gs_wsteam<KS, 3, 4, 0, true>), dim3(a.n_items), dim3(256), 0, s, a);
-          else
-            throw std::runtime_error("gs_estep: staged rows: ONI_GS_BIG_NW 7 (EP 0/1), 5 or 3 (EP 0)");
-        } else if (bnw == 7 && ep == 1)
-          hipLaunchKernelGGL((gs::gs_wsteam<KS, 7, 2, 1>), dim3(a.n_items), dim3(512), 0, s, a);
-        else if (bnw == 7 && ep >= 2)
-          hipLaunchKernelGGL((gs::gs_wsteam<KS, 7, 2, 2>), dim3(a.n_items), dim3(512), 0, s, a);
-        else if (bnw == 7)
-          hipLaunchKernelGGL((gs::gs_wsteam<KS, 7, 2>), dim3(a.n_items), dim3(512), 0, s, a);
-        else if (bnw == 3)
-          hipLaunchKernelGGL((gs::gs_wsteam<KS, 3, 4>), dim3(a.n_items), dim3(256), 0, s, a);
-        else if (bnw == 5)
-          hipLaunchKernelGGL((gs::gs_wsteam<KS, 5, 3>), dim3(a.n_items), dim3(384), 0, s, a);
-        else if (bnw == 4)
-          hipLaunchKernelGGL((gs::gs_wteam<KS, 4, 4>), dim3(a.n_items), dim3(256), 0, s, a);
-        else if (bnw == 16)
-          hipLaunchKernelGGL((gs::gs_wteam<KS, 16, 1>), dim3(a.n_items), dim3(1024), 0, s, a);
+        // longest documents: 7 word waves x 2 prefetched words per lane + a topic wave (5 x 3: 2.64 ms, 3 x 4:
+        // 2.06 ms vs 1.74 per headline EM iteration; profiles/r4_tuning_log.md).  Staged rows (GSStage): every
+        // next-chunk round gathered after the arrival (1.726-1.740 vs 1.824-1.833 ms for an early round-0
+        // gather); rows gathered from beta (a plan past the staging budget): round 0 early (2.13-2.14 vs
+        // 2.17-2.18 ms).  The LDS-ring and topic-wave-reduction variants were slower and are gone.
+        if (a.stage != nullptr)
+          hipLaunchKernelGGL((gs::gs_wsteam<KS, 7, 2, 0, true>), dim3(a.n_items), dim3(512), 0, s, a);
         else
-          hipLaunchKernelGGL((gs::gs_wteam<KS, 8, 2>), dim3(a.n_items), dim3(512), 0, s, a);
+          hipLaunchKernelGGL((gs::gs_wsteam<KS, 7, 2, 1>), dim3(a.n_items), dim3(512), 0, s, a);
       }
       else if (a.gs_updates > kGsUMax)
         hipLaunchKernelGGL((gs::gs_team<KS, 8, 1, true>), dim3(a.n_items), dim3(512), 0, s, a);
@@ -3246,12 +2229,6 @@ int gs_tiny_max(int KS) {
   }
 }
 
-// gs_split variant: 2 = gs_splitw (exchange in a topic wave, the default), 1 = gs_split (ONI_GS_SPLIT_V)
-static int gs_split_variant() {
-  static const int v = std::getenv("ONI_GS_SPLIT_V") ? std::atoi(std::getenv("ONI_GS_SPLIT_V")) : 2;
-  return v;
-}
-
 template <int KS>
 constexpr int split_umax_ks() { return KS <= 52 ? 64 : kGsUMax; }
 
@@ -3273,16 +2250,13 @@ static int gs_split_capacity_ks() {
   hipDeviceProp_t p;
   ONI_HIP_CHECK(hipGetDevice(&dev));
   ONI_HIP_CHECK(hipGetDeviceProperties(&p, dev));
-  if (gs_split_variant() == 2 && split_umax_ks<KS>() > kGsUMax) {
-    // the U <= 64 instantiation holds the larger LDS tables: its residency bounds both
+  // the U <= 64 instantiation holds the larger LDS tables: where it exists its residency bounds both
+  if constexpr (split_umax_ks<KS>() > kGsUMax)
     ONI_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(
         &per_cu, reinterpret_cast<const void*>(&gs::gs_splitw<KS, split_umax_ks<KS>()>), 512, 0));
-  } else if (gs_split_variant() == 2)
-    ONI_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(
-        &per_cu, reinterpret_cast<const void*>(&gs::gs_splitw<KS>), 512, 0));
   else
     ONI_HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(
-        &per_cu, reinterpret_cast<const void*>(&gs::gs_split<KS>), 512, 0));
+        &per_cu, reinterpret_cast<const void*>(&gs::gs_splitw<KS>), 512, 0));
   return per_cu * p.multiProcessorCount;
 }
 
@@ -3300,7 +2274,7 @@ int gs_split_capacity(int KS) {
 
 void launch_gs_split(const GSArgs& a, const SplitArgs& s, int KS, hipStream_t st) {
   if (s.n_blocks <= 0) return;
-  const int um = gs_split_variant() == 2 ? gs_split_umax(KS) : kGsUMax;
+  const int um = gs_split_umax(KS);
   if (a.gs_updates < 1 || a.gs_updates > um)
     throw std::runtime_error("gs_split: gs_updates must be in [1, " + std::to_string(um) + "] at KS " +
                              std::to_string(KS));
@@ -3308,13 +2282,11 @@ void launch_gs_split(const GSArgs& a, const SplitArgs& s, int KS, hipStream_t st
   switch (KS) {
 #define ONI_KS(X)                                                                                          \
   case X:                                                                                                  \
-    if (gs_split_variant() == 2 && a.gs_updates > kGsUMax) {                                               \
+    if (a.gs_updates > kGsUMax) {                                                                          \
       if constexpr (split_umax_ks<X>() > kGsUMax)                                                          \
         hipLaunchKernelGGL((gs::gs_splitw<X, split_umax_ks<X>()>), dim3(s.n_blocks), dim3(512), 0, st, a, s); \
-    } else if (gs_split_variant() == 2)                                                                    \
+    } else                                                                                                 \
       hipLaunchKernelGGL((gs::gs_splitw<X>), dim3(s.n_blocks), dim3(512), 0, st, a, s);                    \
-    else                                                                                                   \
-      hipLaunchKernelGGL((gs::gs_split<X>), dim3(s.n_blocks), dim3(512), 0, st, a, s);                     \
     break;
     ONI_FOR_EACH_KS(ONI_KS)
 #undef ONI_KS

@@ -164,7 +164,16 @@ static std::vector<OutCol> build_cols(const py::list& spec, ColHolder& h, int64_
   return cols;
 }
 
+// The module is built for x86-64-v3 (table.cpp scans lines with AVX2 compares): on a host without
+// AVX2 / FMA refuse to import with a clear message instead of dying on SIGILL in the first ingest.
+__attribute__((target("arch=x86-64"))) static bool host_has_avx2_fma() {
+  __builtin_cpu_init();
+  return __builtin_cpu_supports("avx2") && __builtin_cpu_supports("fma");
+}
+
 PYBIND11_MODULE(_oninative, m) {
+  if (!host_has_avx2_fma())
+    throw py::import_error("_oninative needs an x86-64-v3 CPU (AVX2 + FMA); this host lacks them");
   m.doc() = "oni_ml_amd C++ host runtime";
 
   py::class_<TextTable>(m, "TextTable")

@@ -1,8 +1,12 @@
 // `lda` executable with oni-lda-c's command line (reference call site
 // /root/reference/ml_ops.sh:80):
 //
-//   lda est <alpha> <k> <settings> <nproc> <corpus> <random|seeded|model-prefix> <dir>
-//   lda inf <settings> <model-prefix> <corpus> <save-prefix>
+//   lda est <alpha> <k> <settings> <nproc> <corpus> <random|seeded|model-prefix> <dir> [--gs-updates U]
+//   lda inf <settings> <model-prefix> <corpus> <save-prefix> [--gs-updates U]
+//
+// --gs-updates U (an addition; default 0 = lda-c's literal per-word schedule): gamma / digamma refreshed
+// after every chunk of ceil(n / U) words -- the block Gauss-Seidel schedule of the MI355X engine
+// (csrc/hip/lda_gs64.hip), so a CPU baseline can be measured on the GPU's own schedule.
 //
 // <nproc> is the number of document shards (oni-lda-c's MPI ranks); shards run
 // on threads of this process (ONI_THREADS, default: hardware threads) instead
@@ -19,8 +23,25 @@
 
 static void usage() {
   std::fprintf(stderr,
-               "usage: lda est [initial alpha] [k] [settings] [nproc] [data] [random/seeded/*] [directory]\n"
-               "       lda inf [settings] [model] [data] [name]\n");
+               "usage: lda est [initial alpha] [k] [settings] [nproc] [data] [random/seeded/*] [directory]"
+               " [--gs-updates U]\n"
+               "       lda inf [settings] [model] [data] [name] [--gs-updates U]\n");
+}
+
+// trailing "--gs-updates U" after the positional arguments; -1: malformed
+static int gs_updates_flag(int argc, char** argv, int first) {
+  int u = 0;
+  for (int i = first; i < argc; ++i) {
+    if (std::strcmp(argv[i], "--gs-updates") == 0 && i + 1 < argc) {
+      char* end = nullptr;
+      const long v = std::strtol(argv[++i], &end, 10);
+      if (!end || *end || v < 0 || v > (1 << 20)) return -1;
+      u = (int)v;
+    } else {
+      return -1;
+    }
+  }
+  return u;
 }
 
 int main(int argc, char** argv) {
@@ -33,15 +54,26 @@ int main(int argc, char** argv) {
       double alpha = std::atof(argv[2]);
       int K = std::atoi(argv[3]);
       onin::LdacSettings st = onin::read_ldac_settings(argv[4]);
+      st.gs_updates = gs_updates_flag(argc, argv, 9);
+      if (st.gs_updates < 0) {
+        usage();
+        return 1;
+      }
       int nproc = std::atoi(argv[5]);
       onin::LdacCorpus c = onin::read_ldac_corpus(argv[6]);
       std::printf("number of docs    : %d\nnumber of terms   : %d\n", c.num_docs(), c.num_terms);
+      if (st.gs_updates > 0) std::printf("schedule          : block Gauss-Seidel, %d refreshes per sweep\n", st.gs_updates);
       int it = onin::ldac_estimate(c, K, alpha, st, argv[7], argv[8], nproc, threads, seed, true);
       std::printf("em iterations: %d\n", it);
       return 0;
     }
     if (argc >= 6 && std::strcmp(argv[1], "inf") == 0) {
       onin::LdacSettings st = onin::read_ldac_settings(argv[2]);
+      st.gs_updates = gs_updates_flag(argc, argv, 6);
+      if (st.gs_updates < 0) {
+        usage();
+        return 1;
+      }
       onin::LdacCorpus c = onin::read_ldac_corpus(argv[4]);
       onin::ldac_infer(c, argv[3], st, argv[5], 1, threads);
       return 0;

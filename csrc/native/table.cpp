@@ -24,6 +24,15 @@ namespace onin {
 
 namespace {
 
+// ONI_PROFILE contains "table": ingest and writer timings on stderr
+bool table_profile() {
+  static const bool on = [] {
+    const char* e = std::getenv("ONI_PROFILE");
+    return e && std::strstr(e, "table") != nullptr;
+  }();
+  return on;
+}
+
 struct alignas(64) LocalOut {
   std::vector<uint64_t> off;
   std::vector<uint32_t> len;
@@ -499,7 +508,7 @@ void TextTable::ingest_chunk(uint32_t cid, int32_t w, int threads) {
     }
     std::vector<std::vector<double>>().swap(o.num);
   });
-  if (std::getenv("ONI_TABLE_PROFILE")) {
+  if (table_profile()) {
     const auto tp3 = std::chrono::steady_clock::now();
     auto ms = [](auto a, auto b) { return std::chrono::duration<double, std::milli>(b - a).count(); };
     std::fprintf(stderr, "ingest chunk %u: %zu bytes parse %.1f ms dict %.1f ms rows %.1f ms\n", cid, s.size(),
@@ -596,6 +605,15 @@ static void format_row_values(std::string& out, const OutCol& k, int64_t r, int6
 // Few very wide rows (a K x V .beta file: 100 rows of 4.5 M values at config 5): one row per thread
 // left most threads idle in the last batches; here each row's values are cut into one segment per
 // thread, and the row is written as its scalar columns, then the segments in order.
+// A formatting exception (e.g. bad_alloc on a multi-GB row) must not leave a writer thread joinable:
+// the std::thread destructor would call std::terminate instead of letting the caller report the error.
+struct JoinGuard {
+  std::thread& t;
+  ~JoinGuard() {
+    if (t.joinable()) t.join();
+  }
+};
+
 static int64_t write_wide_rows(FILE* f, const int64_t* order, int64_t n, const std::vector<OutCol>& cols,
                                const std::string& sep, int threads, int& werr) {
   const OutCol& k = cols.back();
@@ -616,6 +634,7 @@ static int64_t write_wide_rows(FILE* f, const int64_t* order, int64_t n, const s
       written += (int64_t)x.size();
     }
   };
+  JoinGuard guard{writer};
   int set = 0;
   for (int64_t i = 0; i < n; ++i, set ^= 1) {
     const int64_t r = order ? order[i] : i;
@@ -657,7 +676,13 @@ int64_t write_rows(const std::string& path, const int64_t* order, int64_t n, con
       scalar_head = scalar_head && cols[c].kind != OutCol::kPy2Row && cols[c].kind != OutCol::kFixedRow;
     if (scalar_head) {
       int werr = 0;
-      const int64_t written = write_wide_rows(f, order, n, cols, sep, threads, werr);
+      int64_t written = 0;
+      try {
+        written = write_wide_rows(f, order, n, cols, sep, threads, werr);
+      } catch (...) {
+        std::fclose(f);
+        throw;
+      }
       if (werr) {
         std::fclose(f);
         throw std::runtime_error("short write: " + path + ": " + std::strerror(werr));
@@ -684,6 +709,14 @@ int64_t write_rows(const std::string& path, const int64_t* order, int64_t n, con
       written += (int64_t)s.size();
     }
   };
+  struct CloseOnThrow {   // declared before the join guard: the writer is joined first, then f closed
+    FILE* f;
+    bool armed = true;
+    ~CloseOnThrow() {
+      if (armed) std::fclose(f);
+    }
+  } closer{f};
+  JoinGuard guard{writer};
   int set = 0;
   double t_fmt = 0, t_wait = 0;
   const auto t_all = std::chrono::steady_clock::now();
@@ -711,7 +744,8 @@ int64_t write_rows(const std::string& path, const int64_t* order, int64_t n, con
     writer = std::thread(flush, set);
   }
   if (writer.joinable()) writer.join();
-  if (std::getenv("ONI_TABLE_PROFILE"))
+  closer.armed = false;
+  if (table_profile())
     std::fprintf(stderr, "write_rows %s: %lld rows, %d threads, format %.1f ms, writer wait %.1f ms, total %.1f ms\n",
                  path.c_str(), (long long)n, threads, t_fmt, t_wait, since(t_all));
   if (werr) {

@@ -11,8 +11,9 @@
   qtiles gen <FLOW_PATH> [--out DIR]           gen_qtiles.sh + qtiles.py: sample ntile cuts -> flow_qtiles
   install [--nodes a,b] [--dry-run]            install_ml.sh: rsync the framework to NODES:${LUSER}/ml
 
-Multi-GPU: launch with torchrun (one process per GPU); ranks share the LDA
-stage over RCCL, rank 0 runs featurization, export and scoring.
+Multi-GPU: launch with torchrun (one process per GPU).  Every ml_ops stage is row-sharded over the ranks
+(pipeline/sharded.py): each featurizes its byte range of the day, builds and trains its document shard and
+scores its own rows; they meet only in tensor collectives over RCCL (parallel/shardio.py, parallel/dist.py).
 """
 from __future__ import annotations
 
@@ -25,6 +26,8 @@ import subprocess
 import sys
 import time
 
+from . import knobs
+
 # wall-clock marks (time.time()) of the process's start-up: `python -m oni_ml_amd` records "main" before its
 # first import; ml_ops adds the rest.  ONI_T_SPAWN (set by a parent that launches this process, e.g. bench.py's
 # cold run) is the spawn time, so interpreter start-up is measured too (startup_marks in run_summary.json).
@@ -33,9 +36,20 @@ MARKS = {}
 FAST_EXIT = False
 
 
+def _tool_attached() -> bool:
+    """A profiler, tracer or coverage tool that writes its output at exit (python -m cProfile / coverage,
+    rocprofv3's preloaded tool library): the process then keeps the normal teardown."""
+    if sys.getprofile() is not None or sys.gettrace() is not None:
+        return True
+    if "coverage" in sys.modules or "cProfile" in sys.modules:
+        return True
+    pre = os.environ.get("LD_PRELOAD", "")
+    return "rocprof" in pre or any(k.startswith(("ROCP_", "ROCPROF")) for k in os.environ)
+
+
 def startup_marks() -> dict:
     """Seconds from the spawn (ONI_T_SPAWN, else "main") to each recorded mark."""
-    t0 = float(os.environ.get("ONI_T_SPAWN", MARKS.get("main", 0.0)) or 0.0)
+    t0 = float(knobs.get("ONI_T_SPAWN", MARKS.get("main", 0.0)) or 0.0)
     return {k: round(v - t0, 4) for k, v in sorted(MARKS.items(), key=lambda kv: kv[1])} if t0 else {}
 
 
@@ -86,7 +100,7 @@ def cmd_ml_ops(argv):
     ap.add_argument("fdate", nargs="?", default="")
     ap.add_argument("dsource", nargs="?", default="")
     ap.add_argument("tol", nargs="?", default=None)
-    ap.add_argument("--conf", default=os.environ.get("ONI_CONF", "/etc/duxbay.conf"))
+    ap.add_argument("--conf", default=knobs.get("ONI_CONF", "/etc/duxbay.conf"))
     ap.add_argument("--lpath")
     ap.add_argument("--flow-path")
     ap.add_argument("--dns-path")
@@ -117,8 +131,9 @@ def cmd_ml_ops(argv):
     if len(a.fdate) != 8 or not a.dsource:
         print(SYNTAX)
         return 1
-    from .utils import warmup
-    warmup.early_hip_init(int(os.environ.get("LOCAL_RANK", "0")))   # HIP context while torch imports
+    # (a HIP context created on a thread during `import torch`, and a warm-up thread launching the first
+    # stages' kernels while the inputs parse, were both measured slower and removed in round 5:
+    # profiles/r4_cold_start.md, profiles/r4_tuning_log.md §3)
     from . import config as CFG
 
     def resolve(world):
@@ -131,7 +146,7 @@ def cmd_ml_ops(argv):
                            hadoop=a.hadoop)
     # one process, fresh run: the day's inputs are read on a thread while torch imports
     # (pipeline/prefetch.py); the load stage takes the result
-    if (os.environ.get("ONI_PREFETCH", "1") != "0" and a.gpus <= 1 and int(os.environ.get("WORLD_SIZE", "1")) == 1
+    if (knobs.get("ONI_PREFETCH", "1") != "0" and a.gpus <= 1 and int(os.environ.get("WORLD_SIZE", "1")) == 1
             and not a.resume and not a.hdfs):
         try:
             from .pipeline import prefetch
@@ -149,7 +164,6 @@ def cmd_ml_ops(argv):
         import torch
         torch.zeros(1, device=ctx.device)     # HIP runtime + context (the first device call)
     MARKS["device_ready"] = time.time()
-    warm = warmup.start(ctx.device)           # first-stage kernels load while the inputs parse
     cfg = resolve(ctx.world_size)
     if a.settings:
         cfg.settings = LDASettings.load(a.settings)
@@ -183,11 +197,9 @@ def cmd_ml_ops(argv):
             ui, rp = cfg.extra.get("UINODE"), cfg.extra.get("RPATH")
             if ui and rp:
                 subprocess.run(["scp", "-r", cfg.lpath, f"{ui}:{rp}"], check=True)
-    if warm is not None:
-        warm.join()
     ctx.shutdown()
     global FAST_EXIT
-    FAST_EXIT = os.environ.get("ONI_FAST_EXIT", "1") != "0"
+    FAST_EXIT = knobs.get("ONI_FAST_EXIT", "1") != "0" and not _tool_attached()
     return 0
 
 
@@ -209,12 +221,32 @@ def cmd_lda(argv):
         a = ap.parse_args(argv[1:])
         from .models.lda.estimate import estimate
         from .parallel import dist as D
+        try:
+            nproc = int(a.nproc)
+        except ValueError:
+            nproc = 0
+        if nproc < 1:
+            print(f"lda est: nproc must be a positive rank count, got {a.nproc!r}", file=sys.stderr)
+            return 1
+        world = int(os.environ.get("WORLD_SIZE", "1"))
+        # oni-lda-c's nproc is its MPI rank count (ml_ops.sh:80 passes PROCESS_COUNT = 20).  Here the ranks are
+        # the torchrun processes (one per GPU): a multi-rank launch must say how many it is; one process runs
+        # every document (on the GPU, or the C++ engine with nproc document shards reduced in shard order --
+        # the MPI job's arithmetic)
+        if world > 1 and nproc != world:
+            print(f"lda est: nproc = {nproc} but {world} ranks were launched (WORLD_SIZE); pass nproc = {world}",
+                  file=sys.stderr)
+            return 1
         ctx = D.init_from_env()
         corpus = ldac.read_model_dat(a.data)
         st = _apply_lda_args(a, LDASettings.load(a.settings))
+        if world == 1 and nproc > 1 and a.backend not in ("cpu",) and ctx.device.type == "cuda":
+            print(f"lda est: nproc = {nproc}: one process runs every document on one GPU (launch nproc processes "
+                  f"with torchrun --nproc-per-node for that many GPUs)", file=sys.stderr)
         res = estimate(corpus, int(a.k), float(a.alpha), st, a.start, a.directory, backend=a.backend,
                        device=ctx.device, dist=ctx if ctx.active else None, seed=a.seed, resume=a.resume,
-                       write_word_assignments=a.word_assignments, verbose=True)
+                       write_word_assignments=a.word_assignments, verbose=True,
+                       cpu_shards=nproc if world == 1 else 1)
         if ctx.rank == 0:
             print(f"em iterations: {res.em_iterations}  seconds: {res.seconds:.3f}")
         ctx.shutdown()
@@ -331,7 +363,7 @@ def cmd_qtiles(argv):
 def cmd_install(argv):
     """install_ml.sh: rsync the framework (dot-files excluded) to every node in NODES:${LUSER}/ml."""
     ap = argparse.ArgumentParser(prog="install")
-    ap.add_argument("--conf", default=os.environ.get("ONI_CONF", "/etc/duxbay.conf"))
+    ap.add_argument("--conf", default=knobs.get("ONI_CONF", "/etc/duxbay.conf"))
     ap.add_argument("--nodes", help="comma-separated node list (default: NODES from the config)")
     ap.add_argument("--luser", help="remote base dir (default: LUSER from the config)")
     ap.add_argument("--src", default=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
@@ -363,8 +395,8 @@ def main(argv=None):
     if not argv or argv[0] not in COMMANDS:
         print(__doc__)
         return 1
-    prof = os.environ.get("ONI_CPROFILE")
-    if prof:
+    prof = knobs.profile("cprofile")
+    if isinstance(prof, str):
         # host profile of a whole command (cold-start analysis, scripts/cold_start.py)
         import cProfile
         pr = cProfile.Profile()

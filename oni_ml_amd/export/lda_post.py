@@ -23,7 +23,8 @@ from ..ops import native
 
 
 def _host_threads() -> int:
-    return max(1, int(os.environ.get("ONI_HOST_THREADS", min(16, os.cpu_count() or 1))))
+    from .. import knobs
+    return knobs.threads(16)
 
 
 def _par(fn, n: int, min_block: int = 1 << 15):

@@ -31,7 +31,7 @@ def _pa():
         # cap it at this process's share so a parquet read beside the torch import does not swamp it
         _ARROW_THREADS = True
         try:
-            n = (int(os.environ.get("ONI_ARROW_THREADS") or 0) or int(os.environ.get("OMP_NUM_THREADS") or 0)
+            n = (int(os.environ.get("ONI_THREADS") or 0) or int(os.environ.get("OMP_NUM_THREADS") or 0)
                  or min(os.cpu_count() or 8, 16))
             if pa.cpu_count() > n:
                 pa.set_cpu_count(n)

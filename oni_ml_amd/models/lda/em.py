@@ -6,15 +6,20 @@ optional alpha Newton); conv = (L_old - L)/L_old; if conv < 0: VAR_MAX_ITER *= 2
 while (conv < 0 or conv > EM_CONV or i <= 2) and i <= EM_MAX_ITER.
 
 MI355X design:
-* the corpus (CSR + CSC) and the model (word-major beta, f32) stay resident in
-  HBM for the whole run; one EM iteration = length-bucketed fused E-step
-  kernels (launched on up to 3 HIP streams so the long-document buckets overlap
-  the short ones) -> deterministic CSC sufficient statistics -> (RCCL all-reduce
-  of the flat [class_word | scalars] buffer when data-parallel) -> M-step kernel.
-  The only host sync per iteration is the 3-scalar read the convergence test
-  and alpha Newton need.
-* backends: "hip" (gfx950 kernels), "torch" (vectorised reference, any device),
-  "cpu" (lda-c semantics C++ reference, Gauss-Seidel).
+* the corpus (CSR + CSC) and the model (word-major beta, fp64 like lda-c) stay resident in
+  HBM for the whole run; one EM iteration = length-bucketed fp64 block Gauss-Seidel E-step
+  kernels (csrc/hip/lda_gs64.hip, on 4 HIP streams so the long-document buckets overlap
+  the short ones) -> deterministic CSC sufficient statistics -> (RCCL sparse row exchange
+  or all-reduce when data-parallel) -> M-step + alpha Newton + the EM convergence test, all
+  on the device and replayed as hipGraphs: the host reads the per-iteration history back once
+  per batch of iterations.
+* backends ("auto": hip on a GPU with the kernels, else cpu):
+  "hip"   the gfx950 kernels (the MI355X engine);
+  "cpu"   lda-c semantics in C++ (csrc/native/lda_ref.cpp: per-word Gauss-Seidel, or the GPU's block
+          schedule with settings.gs_updates), multithreaded -- the engine of a GPU-less host;
+  "torch" a vectorised Jacobi fixed point in torch (any device), a test rehearsal engine only: it is
+          the one whose multi-rank statistics fold bitwise like one process
+          (ONI_DIST_DETERMINISTIC=chain, tests/test_sharded_pipeline.py) and must be asked for by name.
 """
 from __future__ import annotations
 
@@ -27,6 +32,7 @@ from typing import Callable, List, Optional
 import numpy as np
 import torch
 
+from ... import knobs
 from ...corpus.csr import Corpus, DeviceCorpus
 from ...utils.trace import range_push, range_pop
 from . import special
@@ -83,7 +89,7 @@ def cphi_window_bounds(doc_ptr, budget_rows: int):
 
 def _cpu_threads() -> int:
     """Threads of the C++ lda-c engine (its result does not depend on the count)."""
-    return int(os.environ.get("ONI_CPU_THREADS", min(8, os.cpu_count() or 1)))
+    return knobs.threads(8)
 
 def _hbm_total(device) -> int:
     """The device's HBM bytes from hipMemGetInfo.  (torch.cuda.get_device_properties first counts the
@@ -96,7 +102,8 @@ class LDAEngine:
                  alpha_init: float = 2.5, backend: str = "auto", device=None, dist=None, seed: int = 0,
                  streams: int = 4, local_shard: bool = False, split_docs: bool = True,
                  split_min: Optional[int] = 4096, use_graph: bool = True, precision: str = "fp64",
-                 emulate_shards: int = 0, doc_offset: int = 0, cphi_gb: Optional[float] = None):
+                 emulate_shards: int = 0, doc_offset: int = 0, cphi_gb: Optional[float] = None,
+                 suff_split: str = "auto", xsplit: Optional[dict] = None):
         """precision: "fp64" (the only engine: lda-c's double arithmetic; the hip backend runs the block
         Gauss-Seidel schedule of lda_gs64.hip).
         emulate_shards (torch backend, one process): reduce the sufficient statistics as the N
@@ -107,8 +114,17 @@ class LDAEngine:
         cphi_gb (fp64 hip engine): HBM budget of the per-entry c.phi rows (nnz x KS x 8 bytes); a
         corpus whose rows exceed it runs its E-step in contiguous document windows, each followed by
         its share of the sufficient statistics (``_cphi_windows``).  None: ONI_CPHI_GB, else windows
-        only when the rows would take more than 35 % of the GPU's memory."""
+        only when the rows would take more than 35 % of the GPU's memory.
+        suff_split (fp64 hip engine): "auto" -- the longest-document bucket's entries reduced after it, the
+        others while it still runs (``_build_suff_split``) when that overlaps anything; "off"; "force"."""
         self.cphi_gb = cphi_gb
+        if suff_split not in ("auto", "off", "force"):
+            raise ValueError(f"suff_split must be auto | off | force, got {suff_split!r}")
+        self.suff_split = suff_split
+        self.xsplit = xsplit          # experimental XCD-split plan of the longest documents (ops/hip.py GSPlan)
+        # the fused EM iteration's M-step launch refills the next E-step's staged rows (one rank); False: a
+        # gs_stage launch before every E-step (tests/test_gs64.py pins the two bitwise equal)
+        self.stage_fuse = True
         self.settings = settings or LDASettings()
         self.emulate_shards = int(emulate_shards)
         # cpu backend: lda-c's MPI ranks (document shards reduced in shard order; 1 = one process)
@@ -134,12 +150,13 @@ class LDAEngine:
                 H.lib()
                 raise RuntimeError("HIP extension loaded but unusable on this GPU")
             else:
-                backend = "torch"
+                # a GPU-less host runs lda-c's own algorithm (C++, threads), never the Jacobi rehearsal engine
+                backend = "cpu"
         self.backend = backend
         # ONI_DIST_DETERMINISTIC=chain (torch backend): sufficient statistics and the likelihood /
         # alpha_ss sums continue one sequential fold over the documents in corpus order, rank after
         # rank (parallel/shardio.chain): the model is bitwise the same for any number of ranks
-        self._chain = backend == "torch" and os.environ.get("ONI_DIST_DETERMINISTIC", "0") == "chain"
+        self._chain = backend == "torch" and knobs.get("ONI_DIST_DETERMINISTIC", "0") == "chain"
         if device is None:
             device = torch.device("cuda", torch.cuda.current_device()) if (
                 backend == "hip" or torch.cuda.is_available()) and torch.cuda.is_available() else torch.device("cpu")
@@ -187,7 +204,7 @@ class LDAEngine:
         # sparse exchange on the GPU: suff-stats of the shared words first, so their all-to-all runs
         # while the suff-stats of the rank's private words (the bulk) are computed
         self._overlap = self._xchg is not None and backend == "hip" and \
-            os.environ.get("ONI_DIST_OVERLAP", "1") != "0" and getattr(self, "_cwin", None) is None
+            knobs.get("ONI_DIST_EXCHANGE", "auto") != "sparse-serial" and getattr(self, "_cwin", None) is None
         if self._overlap:
             from ...ops import hip as H
             # only this rank's words: rows of other words stay zero in cw_local and are never read
@@ -295,7 +312,7 @@ class LDAEngine:
         f64 = torch.float64
         self._cwin = self._cphi_windows(corpus, KS)
         if self._cwin is None:
-            self.gs_plan = H.GSPlan(self.dc.doc_len, KS, self._U, dev)
+            self.gs_plan = H.GSPlan(self.dc.doc_len, KS, self._U, dev, xsplit=self.xsplit)
             rows = nnz
         else:
             self.gs_plan = None
@@ -339,17 +356,18 @@ class LDAEngine:
         self._suff_split = None
         if self._cwin is not None:
             self._build_window_suff()
-        elif os.environ.get("ONI_SUFF_SPLIT", "1") != "0":
+        elif self.suff_split != "off":
             self._suff_split = self._build_suff_split()
 
     def _build_stages(self, corpus: Corpus, KS: int) -> dict:
         """Staged beta rows (ops/hip.py GSStage) of every kGsTeam8 launch at KS <= 32, keyed by the id of
-        the launch's order tensor.  ONI_GS_STAGE=0 turns them off; a plan whose copies would exceed
-        ONI_GS_STAGE_GB (default 4) is left unstaged."""
+        the launch's order tensor.  ONI_GS_STAGE = the budget in GB (default 4; 0 turns them off): a plan
+        whose copies would exceed it is left unstaged."""
         from ...ops import hip as H
-        if KS > 32 or os.environ.get("ONI_GS_STAGE", "1") == "0":
+        gb = float(knobs.get("ONI_GS_STAGE", "4"))
+        if KS > 32 or gb <= 0:
             return {}
-        cap = float(os.environ.get("ONI_GS_STAGE_GB", "4")) * 2**30
+        cap = gb * 2**30
         plans = [self.gs_plan] if self._cwin is None else [w["gp"] for w in self._cwin]
         out = {}
         for gp in plans:
@@ -378,8 +396,8 @@ class LDAEngine:
         nnz = corpus.nnz
         row_bytes = KS * 8
         gb = self.cphi_gb
-        if gb is None and os.environ.get("ONI_CPHI_GB"):
-            gb = float(os.environ["ONI_CPHI_GB"])
+        if gb is None and knobs.get("ONI_CPHI_GB"):
+            gb = float(knobs.get("ONI_CPHI_GB"))
         if gb is None:
             total = _hbm_total(self.device) if self.device.type == "cuda" else 0
             if not total or nnz * row_bytes <= 0.35 * total:
@@ -433,7 +451,7 @@ class LDAEngine:
         else:
             o = gp.plan[0][1].cpu().numpy()
             late = o[o >= 0].astype(np.int64)
-        force = os.environ.get("ONI_SUFF_SPLIT") == "force"
+        force = self.suff_split == "force"
         if late.size == 0 or (not force and dc.doc_len[late].sum() > 0.6 * max(1, int(dc.doc_len.sum()))):
             return None
         mask = torch.zeros(self.D, dtype=torch.bool, device=dev)
@@ -498,10 +516,9 @@ class LDAEngine:
 
     def _fused_stages(self, gp) -> list:
         """The staged-row sets of plan ``gp`` that the fused M-step launch refills (one rank, staged rows
-        refilled on the main stream, at most 2 sets; ``ONI_GS_STAGE_FUSE=0``: none, a gs_stage launch
+        refilled on the main stream, at most 2 sets; ``stage_fuse = False``: none, a gs_stage launch
         before every E-step as before)."""
-        if (self._distributed or self._cwin is not None or os.environ.get("ONI_GS_STAGE_FUSE", "1") == "0"
-                or os.environ.get("ONI_GS_STAGE_AT", "main") != "main"):
+        if self._distributed or self._cwin is not None or not self.stage_fuse:
             return []
         sts = [self._stages[id(order)] for _, order in gp.plan if id(order) in self._stages]
         return sts if len(sts) <= 2 else []
@@ -522,10 +539,10 @@ class LDAEngine:
         dc, prm = self.dc, self._params
         main = torch.cuda.current_stream(self.device)
         streams = [main] + self._streams
-        # staged rows refilled before the fork (ONI_GS_STAGE_AT=main, default): the team8 launch is then
-        # the first dispatched, instead of queueing behind the other buckets' workgroups for whole CUs
-        stage_main = os.environ.get("ONI_GS_STAGE_AT", "main") == "main"
-        if stage_main and not fused_stage:      # fused: the previous M-step launch refilled them
+        # staged rows refilled before the fork: the team8 launch is then the first dispatched, instead of
+        # queueing behind the other buckets' workgroups for whole CUs (1.861 vs 1.904-1.933 ms per EM
+        # iteration refilled on the bucket's own stream; profiles/r3_tuning_log.md)
+        if not fused_stage:                     # fused: the previous M-step launch refilled them
             for var, order in gp.plan:
                 st = self._stages.get(id(order))
                 if st is not None:
@@ -553,12 +570,11 @@ class LDAEngine:
             with torch.cuda.stream(s):
                 if var == "split":
                     for batch in order:
-                        H.gs_split(dc.doc_ptr, dc.word_idx, dc.counts, self.beta, self.K, self._U, prm, self.gamma,
-                                   cphi, self.lik, self.ass, self.iters, batch, ent_base=ent_base)
+                        launch = H.gs_xsplit if batch.get("x") else H.gs_split
+                        launch(dc.doc_ptr, dc.word_idx, dc.counts, self.beta, self.K, self._U, prm, self.gamma,
+                               cphi, self.lik, self.ass, self.iters, batch, ent_base=ent_base)
                 else:
                     st = self._stages.get(id(order))
-                    if st is not None and not stage_main:   # refill on the bucket's own stream
-                        H.gs_stage(self.beta, dc.word_idx, st, gate=self._gate)
                     H.gs_estep(dc.doc_ptr, dc.word_idx, dc.counts, order, self.beta, self.K, self._U, prm,
                                self.gamma, cphi, self.lik, self.ass, self.iters, var, ent_base=ent_base, stage=st)
         # every bucket but work[0] is joined first and the early pass overlaps work[0]
@@ -603,19 +619,19 @@ class LDAEngine:
 
     def _make_exchange(self, corpus: Corpus):
         """Sparse class_word exchange (parallel/dist.py VocabExchange) when the ranks' vocabularies
-        overlap little; ONI_DIST_EXCHANGE = auto (default) | sparse | dense.  Collective: every rank
-        builds it (or none does)."""
+        overlap little; ONI_DIST_EXCHANGE = auto (default) | sparse | sparse-serial | dense.  Collective:
+        every rank builds it (or none does)."""
         d = self.dist
         if d is None or not d.active or self.backend == "cpu" or self._chain:
             return None
-        mode = os.environ.get("ONI_DIST_EXCHANGE", "auto")
+        mode = knobs.get("ONI_DIST_EXCHANGE", "auto")
         if mode == "dense" or getattr(d, "deterministic", False):
             # deterministic mode: one ordered reduction of the whole matrix (parallel/dist.py)
             return None
         from ...parallel.dist import VocabExchange
         words = np.unique(corpus.word_idx) if corpus.nnz else np.zeros(0, np.int64)
         x = VocabExchange(d, words, self.V, self.KS, self.cw.device, self.cw.dtype)
-        return x if (mode == "sparse" or x.worthwhile()) else None
+        return x if (mode in ("sparse", "sparse-serial") or x.worthwhile()) else None
 
     @property
     def exchange_mode(self) -> str:
@@ -965,13 +981,12 @@ class LDAEngine:
         if not self._distributed:
             self._refill_stages()       # the fused iterations below use staged rows of the current beta
         if not self._distributed and self.use_graph:
-            # one rank: graphs of m = ONI_GRAPH_ITERS EM iterations (default 1), cached per m.  A batch
-            # graph (m = the batch) measured the same per iteration (1.82-1.83 ms) but captures a new
-            # graph for every new batch size -- inside bench.py's timed window when the warm-up batch
-            # differs (2.00 vs 1.82 ms), so the default stays one graph per iteration
+            # one rank: one graph per EM iteration (``graph_iters``), cached.  A batch graph (m = the batch)
+            # measured the same per iteration (1.82-1.83 ms) but captures a new graph for every new batch
+            # size -- inside bench.py's timed window when the warm-up batch differs (2.00 vs 1.82 ms)
             if self._fgraph_key != key:
                 self._fgraphs, self._fgraph_key = {}, key
-            cap = max(1, int(os.environ.get("ONI_GRAPH_ITERS", "1")))
+            cap = max(1, int(getattr(self, "graph_iters", 1)))
             left = n
             while left > 0:
                 m = min(cap, left)
@@ -1075,10 +1090,7 @@ class LDAEngine:
         on entry: those cost ~2 ms per capture and the first EM iteration captures two graphs."""
         launch()
         # the host records the graph while the GPU still runs the real launch (the capture stream waits
-        # on the current stream, so replays stay ordered after it): first EM iteration 5.1 -> 3.6 ms;
-        # ONI_CAPTURE_SYNC=1 restores a device sync before the capture
-        if os.environ.get("ONI_CAPTURE_SYNC", "0") != "0":
-            torch.cuda.synchronize(self.device)
+        # on the current stream, so replays stay ordered after it): first EM iteration 5.1 -> 3.6 ms
         g = torch.cuda.CUDAGraph()
         if getattr(self, "_capture_stream", None) is None:
             self._capture_stream = torch.cuda.Stream(device=self.device)

@@ -133,32 +133,47 @@ def load_final(outdir: str):
     return ldac.load_gamma(os.path.join(outdir, "final.gamma")), lb
 
 
+def _save_npz_atomic(path: str, **arrays):
+    """np.savez to a temp name, then rename: a crash never leaves a torn or half-written file."""
+    tmp = path + ".tmp.npz"
+    np.savez(tmp, **arrays)
+    os.replace(tmp, path)
+
+
 def load_final_rows(outdir: str, d0: int, d1: int):
     """(gamma rows [d0, d1), log_beta) of a finished run, exact: from the binary copies (final_model.npz;
-    a multi-rank run's per-rank final_gamma.rank<r>.npz blocks, any world size), else final.gamma's text."""
+    a multi-rank run's per-rank final_gamma.rank<r>.npz blocks, any world size), else final.gamma's text.
+
+    The rank blocks are used only when they come from ONE run -- the same (world size, final likelihood)
+    stamp in every file, exactly `world` files -- and tile the whole corpus without gap or overlap; a
+    leftover file of another run (a crash before the stage marker, resumed with fewer GPUs) makes the
+    set fail that check and the text of final.gamma is read instead."""
     import glob
-    blocks = []
+    runs = {}
     for f in glob.glob(os.path.join(outdir, "final_gamma.rank*.npz")):
         with np.load(f, allow_pickle=False) as z:
+            if "run" not in z.files:
+                continue
+            world, lik = int(z["run"][0]), float(z["run"][1])
             a, b = (int(x) for x in z["doc_range"])
-            if a < d1 and b > d0:
-                blocks.append((a, b, z["gamma"]))
+            runs.setdefault((world, lik), []).append((a, b, f))
     p = os.path.join(outdir, "final_model.npz")
-    if blocks and os.path.exists(p):
+    for (world, _), blocks in runs.items():
+        if len(blocks) != world or not os.path.exists(p):
+            continue
         blocks.sort(key=lambda x: x[0])
-        covered, rows = d0, []
-        for a, b, g in blocks:
-            if a > covered:
-                break
-            rows.append(g[max(0, covered - a):min(b, d1) - a])
-            covered = min(b, d1)
-            if covered >= d1:
-                break
-        if covered >= d1:
-            with np.load(p, allow_pickle=False) as z:
-                lb = z["log_beta"]
-            K = rows[0].shape[1] if rows else lb.shape[0]
-            return (np.concatenate(rows) if rows else np.zeros((0, K))), lb
+        if blocks[0][0] != 0 or any(blocks[i][1] != blocks[i + 1][0] for i in range(len(blocks) - 1)) \
+                or blocks[-1][1] < d1:
+            continue
+        rows = []
+        for a, b, f in blocks:
+            if a < d1 and b > d0:
+                with np.load(f, allow_pickle=False) as z:
+                    rows.append(z["gamma"][max(0, d0 - a):min(b, d1) - a])
+        with np.load(p, allow_pickle=False) as z:
+            lb = z["log_beta"]
+        K = rows[0].shape[1] if rows else lb.shape[0]
+        return (np.concatenate(rows) if rows else np.zeros((0, K))), lb
     g, lb = load_final(outdir)
     return g[d0:d1], lb
 
@@ -175,10 +190,12 @@ def estimate(corpus: Corpus, num_topics: int, alpha_init: float, settings: LDASe
              backend: str = "auto", device=None, dist=None, seed: int = 0, resume: bool = False,
              write_word_assignments: bool = False, write_rank_gamma: bool = False, verbose: bool = False,
              fault_at_iteration: Optional[int] = None, defer_files: bool = False, local_shard: bool = False,
-             doc_offset: int = 0) -> LDAResult:
+             doc_offset: int = 0, cpu_shards: int = 1) -> LDAResult:
     """Run EM and write lda-c files.  `start`: random | seeded | <model prefix>.
 
     `fault_at_iteration` raises after that EM iteration (fault-injection hook for the resume tests).
+    `cpu_shards` (cpu backend, one process): oni-lda-c's MPI ranks -- document shards whose statistics are
+    reduced in shard order (``lda est <nproc>``).
     `defer_files`: return while the background writer is still formatting the LAG / final model
     files; the caller must call ``res.close_files()`` (which re-raises a write error, and with several
     ranks is a collective).  Without it the files are complete when this returns.
@@ -203,6 +220,8 @@ def estimate(corpus: Corpus, num_topics: int, alpha_init: float, settings: LDASe
     t_start = _now()
     eng = LDAEngine(corpus, num_topics, settings, alpha_init=alpha_init, backend=backend, device=device, dist=dist,
                     seed=seed, local_shard=local_shard, doc_offset=doc_offset)
+    if eng.backend == "cpu":
+        eng.cpu_shards = max(1, int(cpu_shards))   # lda est <nproc>: the C++ engine's document shards
     timing = dict(setup_s=round(_now() - t_start, 4))
     parts = []          # (final file, this rank's part file): concatenated at close
     start_it, L_old, hist = 0, 0.0, []
@@ -241,6 +260,10 @@ def estimate(corpus: Corpus, num_topics: int, alpha_init: float, settings: LDASe
             raise RuntimeError(f"injected fault after EM iteration {i}")
 
     writer = AsyncWriter()
+    # this rank's exact gamma block of an earlier run (load_final_rows) is stale from here on
+    stale = os.path.join(outdir, f"final_gamma.rank{r}.npz")
+    if os.path.exists(stale):
+        os.remove(stale)
 
     saved = {}          # the final save's host copies, reused for the result
 
@@ -271,8 +294,9 @@ def estimate(corpus: Corpus, num_topics: int, alpha_init: float, settings: LDASe
             # exact binary gamma rows of this rank's documents (a resumed lda_post reads them instead of the
             # %5.10f text of final.gamma, load_final_rows)
             d0, d1 = e.doc_range
-            writer.submit(np.savez, os.path.join(outdir, f"final_gamma.rank{r}.npz"), gamma=g,
-                          doc_range=np.asarray([d0, d1], np.int64))
+            run = np.asarray([dist.world_size, history[-1][0] if history else 0.0], np.float64)
+            writer.submit(_save_npz_atomic, os.path.join(outdir, f"final_gamma.rank{r}.npz"), gamma=g,
+                          doc_range=np.asarray([d0, d1], np.int64), run=run)
         if write_rank_gamma and tag == "final":
             writer.submit(ldac.save_gamma, os.path.join(outdir, f"{r}.gamma"), g)
             writer.submit(ldac.save_beta, os.path.join(outdir, f"{r}.beta"), e.local_log_beta())

@@ -299,8 +299,6 @@ def gs_umax(KS: int = 0) -> int:
 
 def gs_split_umax(KS: int) -> int:
     """Largest U of the split-document kernel: its chunk tables live in LDS (64 at KS <= 52, else 32)."""
-    if os.environ.get("ONI_GS_SPLIT_V", "2") != "2":
-        return gs_umax()
     return int(lib().gs_split_umax(int(KS)))
 
 
@@ -498,12 +496,32 @@ def gs_mstep(cw, class_total, beta, K, gate=None):
                    _stream())
 
 
+def split_spec(KS: int) -> dict:
+    """The split-document plan of ONI_GS_SPLIT_MIN = 'N[,g=G][,batches=B][,words=W]': documents longer
+    than N words split (default 2048 at KS > 32, 0 = off at KS <= 32), at most G workgroups per document
+    (16), B launch batches (1), W words of a chunk per workgroup (0: the 8-wave team's prefetch)."""
+    from .. import knobs
+    spec = (knobs.get("ONI_GS_SPLIT_MIN") or "").strip()
+    out = dict(min=2048 if KS > 32 else 0, g=16, batches=1, words=0)
+    if spec:
+        head, *rest = [x.strip() for x in spec.split(",")]
+        if head:
+            out["min"] = int(head)
+        for kv in rest:
+            k, v = kv.split("=")
+            if k.strip() not in ("g", "batches", "words"):
+                raise ValueError(f"ONI_GS_SPLIT_MIN: unknown field {k!r} in {spec!r}")
+            out[k.strip()] = int(v)
+    return out
+
+
 def gs_split_launch_cap(KS: int) -> int:
     """Workgroups per gs_split launch: 3/4 of the co-resident capacity (occupancy API x CUs), so a
     launch's segments are resident together with room for the other streams' buckets;
     ONI_SPLIT_MAX_BLOCKS lowers it (tests, shared / partitioned GPUs)."""
+    from .. import knobs
     cap = max(1, int(lib().gs_split_capacity(int(KS))) * 3 // 4)
-    env = os.environ.get("ONI_SPLIT_MAX_BLOCKS")
+    env = knobs.get("ONI_SPLIT_MAX_BLOCKS")
     if env:
         cap = max(1, min(cap, int(env)))
     return cap
@@ -530,9 +548,10 @@ class GSSplitPlan:
         import numpy as np
         self.KS = int(KS)
         self.max_blocks = gs_split_launch_cap(KS)
-        self.seg_words = int(seg_words) or int(os.environ.get("ONI_GS_SPLIT_WORDS", "0")) or min(128, gs_team8_words(KS))
-        max_seg = min(int(max_seg) or int(os.environ.get("ONI_GS_SPLIT_G", "16")), self.max_blocks)
-        max_batches = int(max_batches) or int(os.environ.get("ONI_GS_SPLIT_BATCHES", "1"))
+        sp = split_spec(KS)
+        self.seg_words = int(seg_words) or sp["words"] or min(128, gs_team8_words(KS))
+        max_seg = min(int(max_seg) or sp["g"], self.max_blocks)
+        max_batches = int(max_batches) or sp["batches"]
         U = int(gs_updates)
         self.segments = {}
         self.batches = []
@@ -603,6 +622,108 @@ def gs_split(doc_ptr, word_idx, counts, beta, K, gs_updates, params, gamma, cphi
         0 if dbg is None else _chk(dbg, torch.int64, "dbg", (8,), dev))
 
 
+def gs_xsplit_rows(KS: int) -> int:
+    """LDS row capacity of one gs_xsplit member (its words over every chunk of a sweep), 0: no kernel."""
+    return int(lib().gs_xsplit_rows(int(KS)))
+
+
+class GSXSplitPlan:
+    """Documents split over the CUs of one XCD each (gs_xsplit, csrc/hip/lda_xsplit.hip, even KS <= 32).
+
+    The first ``limit`` documents of ``doc_ids`` (longest first) that fit are taken.  Document d of n words
+    (W = ceil(n / U) words per chunk) gets G one-wave members, each holding its
+    ceil(W / G) words of every chunk in LDS: G >= the LDS minimum, ``members`` or as
+    many as that takes, at most 32 (the CUs of an XCD).  Documents are first-fit packed into the 8 XCD
+    groups (members of group x are blocks x, x + 8, ... of a grid of 8 x max-members blocks: one XCD
+    under the observed round-robin dispatch); a document that fits no group stays with the team
+    kernels (``leftover``).  Duck-types GSSplitPlan for the engine (segments, batches, n_docs)."""
+
+    def __init__(self, doc_ids, lengths, KS: int, gs_updates: int, device, members: int = 0, groups: int = 8,
+                 proto: int = 1, limit: int = 0):
+        import numpy as np
+        self.KS, U = int(KS), int(gs_updates)
+        cap = gs_xsplit_rows(KS)
+        if cap <= 0 or not 1 <= U <= 32:
+            raise ValueError(f"gs_xsplit: no kernel for KS {KS} / U {U}")
+        members = int(members)
+        self.proto = int(proto)
+        used = [0] * 8
+        slots = [[] for _ in range(8)]          # per group: (doc, G)
+        self.segments, self.leftover = {}, []
+        for d in doc_ids:
+            if limit and len(self.segments) >= limit:
+                break
+            n = int(lengths[d])
+            W = -(-n // U)
+            nch = -(-n // W)
+            per = cap // nch                     # words of one chunk a member can hold
+            gmin = -(-W // per) if per > 0 else 10 ** 9
+            G = max(gmin, min(members, W) if members else gmin, 2)
+            x = next((x for x in range(min(groups, 8)) if used[x] + G <= 32), None)
+            if G > 32 or x is None or W < 2:
+                self.leftover.append(int(d))
+                continue
+            slots[x].append((int(d), G))
+            used[x] += G
+            self.segments[int(d)] = G
+        self.n_docs = len(self.segments)
+        gmax = max(used) if self.n_docs else 0
+        nb = 8 * gmax
+        seg_doc = np.full(nb, -1, np.int32)
+        seg_index = np.zeros(nb, np.int32)
+        seg_count = np.ones(nb, np.int32)
+        seg_base = np.zeros(nb, np.int32)
+        doc_slot = np.zeros(nb, np.int32)
+        row, slot = 0, 0
+        for x in range(8):
+            m = 0
+            for d, G in slots[x]:
+                for gi in range(G):
+                    b = x + 8 * (m + gi)
+                    seg_doc[b], seg_index[b], seg_count[b], seg_base[b], doc_slot[b] = d, gi, G, row, slot
+                m += G
+                row += G
+                slot += 1
+        t = lambda a: torch.from_numpy(a).to(device)
+        self.batches = [] if not self.n_docs else [dict(
+            x=True, seg_doc=t(seg_doc), seg_index=t(seg_index), seg_count=t(seg_count), seg_base=t(seg_base),
+            doc_slot=t(doc_slot), n_blocks=nb, n_rows=row,
+            # granules {lo, tag, hi, tag} (uint32): [2][n_rows][KS + 1][4]
+            xchg=torch.zeros(2 * row * (self.KS + 1) * 4, dtype=torch.int32, device=device),
+            counter=torch.zeros(2 * slot, dtype=torch.int32, device=device),
+            error=torch.zeros(1, dtype=torch.int32, device=device),
+            placed=torch.zeros(max(slot, 1), dtype=torch.int32, device=device), docs=slot, proto=self.proto)]
+
+
+def gs_xsplit(doc_ptr, word_idx, counts, beta, K, gs_updates, params, gamma, cphi, lik, alpha_ss, iters, batch,
+              dbg=None, ent_base=None):
+    """One launch of the XCD-split E-step over a GSXSplitPlan batch.  dbg: optional int64[8] phase timer
+    of member 0 of the first document (word phase + reduction, publish -> gathered, refresh, chunks)."""
+    D = doc_ptr.numel() - 1
+    nnz = word_idx.numel()
+    V, KS = beta.shape
+    dev = beta.device
+    nb = batch["n_blocks"]
+    if gs_xsplit_rows(KS) <= 0 or not (0 < K <= KS) or not (1 <= int(gs_updates) <= 32):
+        raise ValueError("gs_xsplit: KS, K or gs_updates out of range")
+    for k in ("seg_doc", "seg_index", "seg_count", "seg_base", "doc_slot"):
+        _chk(batch[k], torch.int32, k, (nb,), dev)
+    lib().gs_xsplit(
+        _chk(doc_ptr, torch.int32, "doc_ptr", (D + 1,), dev), _chk(word_idx, torch.int32, "word_idx", (nnz,), dev),
+        _chk(counts, torch.float32, "counts", (nnz,), dev), _chk(beta, torch.float64, "beta", (V, KS), dev),
+        int(K), int(KS), int(gs_updates), _params_ptr(params, dev) or _bad("params"),
+        _chk(gamma, torch.float64, "gamma", (D, KS), dev), _cphi_ptr(cphi, nnz, KS, dev, ent_base),
+        _chk(lik, torch.float64, "lik", (D,), dev), _chk(alpha_ss, torch.float64, "alpha_ss", (D,), dev),
+        _chk(iters, torch.int32, "iters", (D,), dev),
+        batch["seg_doc"].data_ptr(), batch["seg_index"].data_ptr(), batch["seg_count"].data_ptr(),
+        batch["seg_base"].data_ptr(), batch["doc_slot"].data_ptr(), int(nb), int(batch["n_rows"]),
+        _chk(batch["xchg"], torch.int32, "xchg", (2 * batch["n_rows"] * (KS + 1) * 4,), dev),
+        _chk(batch["counter"], torch.int32, "counter", (2 * batch["docs"],), dev), int(batch["docs"]),
+        _chk(batch["error"], torch.int32, "error", (1,), dev), int(batch["proto"]),
+        _chk(batch["placed"], torch.int32, "placed", None, dev), _stream(),
+        0 if dbg is None else _chk(dbg, torch.int64, "dbg", (8,), dev))
+
+
 class GSPlan:
     """Length buckets of the fp64 block Gauss-Seidel E-step: (variant, int32 doc order) per launch.
 
@@ -614,7 +735,7 @@ class GSPlan:
                     (GS_SMALL, None, GS_SMALL_MAX))
 
     def __init__(self, lengths, KS: int, gs_updates: int, device, split_min: Optional[int] = None,
-                 doc_range=None):
+                 doc_range=None, xsplit: Optional[dict] = None):
         import numpy as np
         L = np.asarray(lengths, dtype=np.int64)
         # doc_range (d0, d1): only documents d0 <= d < d1 (one c.phi window of the engine); the stable
@@ -627,16 +748,28 @@ class GSPlan:
             order = (d0 + argsort_desc_stable(L[d0:d1])).astype(np.int32)
         # documents longer than split_min words: one document over several workgroups (gs_split);
         # default on for KS > 32 (the topic-group team kernels' chunk of a long document is bound
-        # by one CU's row gathers), ONI_GS_SPLIT_MIN overrides (0: off)
+        # by one CU's row gathers), ONI_GS_SPLIT_MIN overrides (0: off; split_spec)
         # K > 32: 2048 (the whole team8 range) -- at 4096 the 2-4 k-word documents' 512-thread
         # workgroups were dispatched behind the short-document floods in some iterations (a bimodal
         # 2.75 / 4.5 ms team8 bucket); one co-resident split launch holds them all: K = 50 4.53 / 4.73
         # -> 3.36 / 3.34 ms per EM iteration (profiles/r3_tuning_log.md)
         if split_min is None:
-            split_min = int(os.environ.get("ONI_GS_SPLIT_MIN", "2048" if KS > 32 else "0"))
+            split_min = split_spec(KS)["min"]
         if int(gs_updates) > gs_split_umax(KS):
             split_min = 0       # the split kernel keeps its chunk tables in LDS: U <= 64 at KS <= 52, else 32
         self.split = None
+        # xsplit = {docs: N, members: G, proto: P} (even KS <= 32): the N longest documents over the CUs of
+        # one XCD each (gs_xsplit; an experiment, off by default: profiles/r5_xcd_split.md)
+        xs = dict(xsplit or {})
+        nx = int(xs.pop("docs", 0)) if KS <= 32 and KS % 2 == 0 and int(gs_updates) <= 32 else 0
+        if nx > 0 and L.size and gs_xsplit_rows(KS) > 0:
+            head = order[:nx + 16]
+            head = head[L[head] > 2 * int(gs_updates)]
+            xp = GSXSplitPlan(head, L, KS, gs_updates, device, limit=nx, **xs) if head.size else None
+            if xp is not None and xp.n_docs:
+                self.split = xp
+                order = order[~np.isin(order, np.asarray(sorted(xp.segments), np.int64))]
+                split_min = 0
         if split_min > 0 and (L > split_min).any():
             m = L[order] > split_min
             sp = GSSplitPlan(order[m], L, KS, gs_updates, device)
@@ -648,8 +781,10 @@ class GSPlan:
         Ls = L[order]
         tiny = min(gs_tiny_max(KS), int(gs_updates))
         self.plan = []
-        iso = int(os.environ.get("ONI_GS_XCD", "1")) if KS <= 32 else 0
-        edges = self.EDGES_NARROW if KS <= 32 and os.environ.get("ONI_GS_SMALL", "1") != "0" else self.EDGES
+        # team8 at KS <= 32: the longest document first in a workgroup order that gives it an XCD of its own
+        # under round-robin dispatch (isolate_longest, a speed hint)
+        iso = 1 if KS <= 32 else 0
+        edges = self.EDGES_NARROW if KS <= 32 else self.EDGES
         if KS > 32 and int(gs_updates) > 32:
             edges = self.wide_u_edges(int(gs_updates))
         for var, lo, hi in edges:
@@ -665,17 +800,9 @@ class GSPlan:
         if m.any():
             self.plan.append((GS_TINY, torch.from_numpy(order[m].copy()).to(device)))
         self.tiny_max = tiny
-        # ONI_GS_XCD_SKIP=1: the other buckets leave XCD 0 (the longest document's, isolate_longest)
-        # to team8 -- their workgroups b = 0 mod 8 get empty document slots.  Measured on the headline
-        # day: 2.20 / 2.27 vs 2.18 / 2.18 ms per EM iteration (off by default; profiles/r2_tuning_log.md)
-        self.xcd_skip = bool(iso > 0 and os.environ.get("ONI_GS_XCD_SKIP", "0") != "0"
-                             and any(v == GS_TEAM8 for v, _ in self.plan))
-        if self.xcd_skip:
-            dpb = {GS_TINY: 256 // (8 if KS <= 32 else 16), GS_SMALL: 16, GS_TEAM1: 4 if KS <= 32 else 1,
-                   GS_TEAM4: 1}
-            self.plan = [(v, o if v == GS_TEAM8 else
-                          torch.from_numpy(self.xcd_gaps(o.cpu().numpy(), dpb[v])).to(device))
-                         for v, o in self.plan]
+        # (the other buckets leaving the longest document's XCD to it measured slower twice and is gone:
+        # 2.20 / 2.27 vs 2.18 / 2.18 ms, then 1.746 / 1.742 / 1.761 vs 1.734 / 1.733 / 1.739 ms per EM
+        # iteration; profiles/r2_tuning_log.md, r3_tuning_log.md)
 
     @classmethod
     def wide_u_edges(cls, U: int):
@@ -683,34 +810,12 @@ class GSPlan:
         split a chunk's W = ceil(n / U) words, so at lda-c's per-word schedule (U = 1024: W = 1 for every
         document up to 1,024 words) a 4- or 8-wave team idles all but one word slot and pays two
         workgroup barriers per word, where one wave per document refreshes in-wave with no barrier.
-        ONI_GS_WEDGES="w1,w4": one wave up to W = w1, four up to W = w4, eight beyond (never below the
-        U = 32 edges); "0" keeps the fixed length edges.  K = 100 shard at U = 1024 (profiles/r4_tuning_log.md):
-        fixed edges 172.4 ms per EM iteration, "8,64" 133.2, "4,32" 107.3, "2,16" 106.7 (the default)."""
-        spec = os.environ.get("ONI_GS_WEDGES", "2,16")
-        if spec.strip() == "0":
-            return cls.EDGES
-        w1, w4 = (int(x) for x in spec.split(","))
+        One wave up to W = 2, four up to W = 16, eight beyond (never below the U = 32 edges).  K = 100 shard
+        at U = 1024 (profiles/r4_tuning_log.md): fixed length edges 172.4 ms per EM iteration, (8, 64) 133.2,
+        (4, 32) 107.3, (2, 16) 106.7."""
+        w1, w4 = 2, 16
         e1, e4 = max(256, w1 * U), max(2048, w4 * U)
         return ((GS_TEAM8, e4, None), (GS_TEAM4, e1, e4), (GS_TEAM1, None, e1))
-
-    @staticmethod
-    def xcd_gaps(o, dpb: int, xcds: int = 8):
-        """Document order with the slots of every workgroup b = 0 mod xcds empty (-1): a launch of
-        dpb documents per workgroup then leaves XCD 0 alone under round-robin dispatch."""
-        import numpy as np
-        o = np.asarray(o, np.int32)
-        nb = -(-o.size // dpb)
-        out = []
-        b = 0
-        i = 0
-        while i < nb:
-            if b % xcds == 0:
-                out.append(np.full(dpb, -1, np.int32))
-            else:
-                out.append(o[i * dpb:(i + 1) * dpb])
-                i += 1
-            b += 1
-        return np.concatenate(out) if out else o
 
     @staticmethod
     def isolate_longest(o, m: int, xcds: int = 8):

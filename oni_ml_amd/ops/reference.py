@@ -1,10 +1,12 @@
-"""Pure-PyTorch reference implementations of the HIP hot ops.
+"""Pure-PyTorch reference implementations of the LDA hot ops.
 
-Used (a) as the numerics oracle for the gfx950 kernels in the GPU tests and
-(b) as the portable `torch` LDA backend (CPU runs, CI without a GPU).  The
-E-step here is the same Jacobi fixed-point iteration with the same closed-form
-likelihood and lda-c convergence rule as csrc/hip/lda_estep.hip, vectorised
-across documents with per-document convergence masks.
+The `torch` LDA backend: a vectorised Jacobi fixed-point E-step (every word's phi from one digamma
+vector per variational iteration; the closed-form likelihood and lda-c's convergence rule) across
+documents with per-document convergence masks, plus the suff-stats and M-step.  It is a test rehearsal
+engine only -- the one whose multi-rank statistics can fold bitwise like one process
+(ONI_DIST_DETERMINISTIC=chain, tests/test_sharded_pipeline.py).  The MI355X engine is the fp64 block
+Gauss-Seidel of csrc/hip/lda_gs64.hip and the CPU engine the lda-c Gauss-Seidel of
+csrc/native/lda_ref.cpp; both are checked against lda_ref.cpp, not against this module.
 """
 from __future__ import annotations
 

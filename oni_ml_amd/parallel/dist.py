@@ -24,6 +24,11 @@ from dataclasses import dataclass
 import numpy as np
 import torch
 
+from .. import knobs
+
+# ordered_allreduce's slice per rank (MiB): N x the slice of extra memory, not N full copies
+ORDERED_CHUNK_MB = 256
+
 
 @dataclass
 class DistContext:
@@ -74,12 +79,12 @@ class DistContext:
     def ordered_allreduce(self, t: torch.Tensor) -> torch.Tensor:
         """In place: t <- 0 + t_0 + t_1 + ... + t_{N-1} (rank order) on every rank.
 
-        Gathered in slices of <= ONI_ORDERED_CHUNK_MB (default 256) MiB per rank, so the extra memory is
+        Gathered in slices of <= ORDERED_CHUNK_MB (256) MiB per rank, so the extra memory is
         N x the slice, not N full copies (a config-5 class_word is 3.8 GB per copy)."""
         import torch.distributed as td
 
         flat = t.view(-1) if t.is_contiguous() else t.contiguous().view(-1)
-        step = max(1, int(float(os.environ.get("ONI_ORDERED_CHUNK_MB", "256")) * 2**20) // max(1, t.element_size()))
+        step = max(1, int(ORDERED_CHUNK_MB * 2**20) // max(1, t.element_size()))
         step = min(step, max(1, flat.numel()))
         parts = [torch.empty(step, dtype=t.dtype, device=t.device) for _ in range(self.world_size)]
         for a in range(0, flat.numel(), step):
@@ -419,7 +424,7 @@ def chain_bounds(doc_ptr: np.ndarray, world: int, kappa: float = None, K: int = 
 
 def chain_default() -> bool:
     """Chain-aware document shards are the default (ONI_SHARD_CHAIN=0: plain nnz-balanced cuts)."""
-    return os.environ.get("ONI_SHARD_CHAIN", "1") != "0"
+    return knobs.get("ONI_SHARD_CHAIN", "1") != "0"
 
 
 def engine_bounds(doc_ptr: np.ndarray, world: int, K: int = None):
@@ -459,7 +464,7 @@ def init_from_env(expected_world: int = None, backend: str = None, timeout_s: fl
         raise RuntimeError(f"--gpus {expected_world} but WORLD_SIZE={world}")
     if backend is None:
         # ONI_DIST_BACKEND=gloo rehearses several ranks on one GPU (RCCL needs one GPU per rank)
-        backend = os.environ.get("ONI_DIST_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
+        backend = knobs.get("ONI_DIST_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
     if torch.cuda.is_available() and backend == "nccl":
         torch.cuda.set_device(local)
         dev = torch.device("cuda", local)
@@ -467,9 +472,9 @@ def init_from_env(expected_world: int = None, backend: str = None, timeout_s: fl
         dev = torch.device("cuda", local % max(1, torch.cuda.device_count()))
     else:
         dev = torch.device("cpu")
-    forced = os.environ.get("ONI_DIST_FORCE_GROUP", "0") == "1"
+    forced = knobs.get("ONI_DIST_FORCE_GROUP", "0") == "1"
     ctx = DistContext(rank=rank, world_size=world, local_rank=local, device=dev, backend=backend,
-                      deterministic=os.environ.get("ONI_DIST_DETERMINISTIC", "0") == "1", forced=forced)
+                      deterministic=knobs.get("ONI_DIST_DETERMINISTIC", "0") == "1", forced=forced)
     if world > 1 or forced:
         os.environ.setdefault("MASTER_PORT", "29533")
         import torch.distributed as td
@@ -480,6 +485,5 @@ def init_from_env(expected_world: int = None, backend: str = None, timeout_s: fl
         if backend == "nccl":
             kw["device_id"] = dev
         td.init_process_group(**kw)
-        if os.environ.get("ONI_DIST_SELFCHECK", "1") != "0":
-            ctx.self_check()
+        ctx.self_check()
     return ctx

@@ -103,6 +103,8 @@ def load_corpus_files(lpath: str):
 
 
 RANK_FILES_MAX_VALUES = 1 << 26
+# lda_post writes its result files on a thread while the scoring stage runs from this many doc + word values
+DEFER_POST_VALUES = 1 << 26
 
 
 def run_lda(cfg, corpus: Corpus, dist=None, device=None, log=print, local_shard: bool = False, doc_offset: int = 0):

@@ -71,7 +71,7 @@ def run(cfg, dist=None, device=None, log=print) -> dict:
                         write_doc_wc(os.path.join(lp, "doc_wc.dat"), dwc, ipn, C.vocab_lookup(b_.word_keys, wn_))
                     C.write_corpus_files(lp, b_, dn_, wn_)
                 # as in the flow pipeline: the text files on a thread during EM, the marker waits for them
-                if os.environ.get("ONI_DEFER_PRE", "1") != "0":
+                if True:   # text files on a thread beside the EM (pipeline/flow.py)
                     res["_defer"] = C.background(write_files, "oni-lda-pre-writer")
                 else:
                     write_files()

@@ -81,7 +81,7 @@ def run(cfg, dist=None, device=None, log=print) -> dict:
                     C.write_corpus_files(lp, b_, dn_, wn_)
                 # the text files are the stage contract, not an input of the in-memory lda stage: written
                 # on a thread while the GPU runs EM; the lda_pre marker waits for them (finish_deferred)
-                if os.environ.get("ONI_DEFER_PRE", "1") != "0":
+                if True:   # text files on a thread beside the EM (profiles/r3_tuning_log.md: e2e 0.66 -> 0.53 s)
                     res["_defer"] = C.background(write_files, "oni-lda-pre-writer")
                 else:
                     write_files()
@@ -127,10 +127,10 @@ def run(cfg, dist=None, device=None, log=print) -> dict:
                 from ..models.lda.estimate import load_final
                 gamma, log_beta = load_final(cfg.lpath)
             with R.stage("lda_post") as res:
-                # deferred text (ONI_DEFER_POST): measured no e2e gain on the 1-day tables (tuning log);
-                # on by default from 2^26 values, where formatting ~1 G values (config 5) overlaps scoring
-                big = (len(doc_names) + len(word_names)) * int(gamma.shape[1]) >= C.RANK_FILES_MAX_VALUES
-                if os.environ.get("ONI_DEFER_POST", "1" if big else "0") != "0":
+                # deferred text: measured no e2e gain on the 1-day tables (tuning log); on from
+                # DEFER_POST_VALUES (2^26) values, where formatting ~1 G values (config 5) overlaps scoring
+                big = (len(doc_names) + len(word_names)) * int(gamma.shape[1]) >= C.DEFER_POST_VALUES
+                if big:
                     # the result files are written on a thread while flow_post scores (its tables
                     # are the text round trip of the same values); the lda_post marker waits for them
                     from ..export import lda_post as LP

@@ -11,12 +11,14 @@ import os
 import threading
 
 
+BG_NICE = 10     # background writers' nice value: they take the cycles the stages leave
+
 def background_priority() -> None:
-    """Raise the calling thread's nice value by ``ONI_BG_NICE`` (default 10; 0 keeps it).  Linux
+    """Raise the calling thread's nice value by BG_NICE (10).  Linux
     applies PRIO_PROCESS with a thread id to that thread only; raising a nice value needs no
     privilege.  Best effort: other platforms or a refused call leave the priority as it is."""
     try:
-        n = int(os.environ.get("ONI_BG_NICE", "10"))
+        n = BG_NICE
     except ValueError:
         n = 10
     if n <= 0 or not hasattr(os, "setpriority"):

@@ -43,6 +43,8 @@ def main():
     ap.add_argument("--first", type=int, default=0,
                     help="team buckets: only their FIRST longest documents (e.g. 1: the longest document alone)")
     ap.add_argument("--prefixes", default="", help="also time the team8 bucket on its N longest documents, e.g. 1,2,8")
+    ap.add_argument("--xsplit", type=int, default=0, help="the N longest documents on the XCD-split kernel (gs_xsplit)")
+    ap.add_argument("--xsplit-g", type=int, default=0, help="gs_xsplit members per document (0: the LDS minimum)")
     a = ap.parse_args()
     from oni_ml_amd.models.lda.em import LDAEngine
     from oni_ml_amd.models.lda.settings import LDASettings
@@ -51,7 +53,8 @@ def main():
     c, _ = synthetic_flow_corpus(events=a.events, seed=0, device="cuda")
     st = LDASettings()
     st.gs_updates = a.gs_updates
-    eng = LDAEngine(c, a.topics, st, backend="hip", seed=0, precision="fp64")
+    xs = dict(docs=a.xsplit, members=a.xsplit_g) if a.xsplit else None
+    eng = LDAEngine(c, a.topics, st, backend="hip", seed=0, precision="fp64", xsplit=xs)
     eng.init_random()
     eng.em_iterations(a.warm_em, True, c.num_docs, stop=False)
     torch.cuda.synchronize()
@@ -70,10 +73,13 @@ def main():
 
     spl = eng.gs_plan.split
     if spl is not None and (not a.only or a.only == "split"):
+        def split_fn(b):
+            return H.gs_xsplit if b.get("x") else H.gs_split
+
         def launch_split():
             for b in spl.batches:
-                H.gs_split(dc.doc_ptr, dc.word_idx, dc.counts, eng.beta, eng.K, eng._U, eng._params, eng.gamma,
-                           eng.cphi, eng.lik, eng.ass, eng.iters, b)
+                split_fn(b)(dc.doc_ptr, dc.word_idx, dc.counts, eng.beta, eng.K, eng._U, eng._params, eng.gamma,
+                            eng.cphi, eng.lik, eng.ass, eng.iters, b)
         o = np.asarray(sorted(spl.segments), dtype=np.int64)
         L, it = lens[o], its[o]
         out["buckets"].append(dict(kernel="split", docs=int(o.size), len_min=int(L.min()), len_max=int(L.max()),
@@ -85,12 +91,21 @@ def main():
         if a.phases:
             dbg = torch.zeros(8, dtype=torch.int64, device="cuda")
             b0 = spl.batches[0]
-            H.gs_split(dc.doc_ptr, dc.word_idx, dc.counts, eng.beta, eng.K, eng._U, eng._params, eng.gamma,
-                       eng.cphi, eng.lik, eng.ass, eng.iters, b0, dbg=dbg)
+            split_fn(b0)(dc.doc_ptr, dc.word_idx, dc.counts, eng.beta, eng.K, eng._U, eng._params, eng.gamma,
+                         eng.cphi, eng.lik, eng.ass, eng.iters, b0, dbg=dbg)
             v = dbg.cpu().tolist()
-            ch = max(v[7], 1)
-            d0 = int(b0["seg_doc"][0].item())
-            out["buckets"][-1]["phase_cycles_per_chunk"] = dict(
+            if b0.get("x"):   # gs_xsplit: word + reduce, publish -> gathered, refresh, chunks
+                ch = max(v[3], 1)
+                d0 = int(spl.batches[0]["seg_doc"][(b0["seg_doc"] >= 0).nonzero()[0, 0]].item())
+                out["buckets"][-1]["phase_cycles_per_chunk"] = dict(
+                    word_reduce=round(v[0] / ch), exchange=round(v[1] / ch), refresh=round(v[2] / ch), chunks=v[3],
+                    doc_len=int(lens[d0]), members=int(spl.segments[d0]),
+                    placed=b0["placed"].cpu().tolist())
+            else:
+                ch = max(v[7], 1)
+                d0 = int(b0["seg_doc"][0].item())
+            if not b0.get("x"):
+                out["buckets"][-1]["phase_cycles_per_chunk"] = dict(
                 word=round(v[0] / ch), barrier1=round(v[1] / ch), exchange=round(v[2] / ch),
                 barrier2=round(v[3] / ch), refresh=round(v[4] / ch), barrier3=round(v[5] / ch),
                 sweep_end_total=v[6], chunks=v[7], doc_len=int(lens[d0]),

@@ -8,7 +8,7 @@ bench.py's cold leg does (ml_ops.sh times each stage as a fresh process: ml_ops.
      start-up variants (--variants, alternating): spawn -> exit wall, the start-up marks (interpreter, `import torch`, package,
      HIP context, pipeline start / end; cli.startup_marks) and the stage seconds;
   2. one run under `-X importtime`: the slowest imports (cumulative);
-  3. one run under cProfile (ONI_CPROFILE): the host functions with the most cumulative time.
+  3. one run under cProfile (ONI_PROFILE=cprofile:FILE): the host functions with the most cumulative time.
 
   python scripts/cold_start.py [--events 1000000] [--reps 3] [--md out.md] [--json out.json]
 """
@@ -82,7 +82,7 @@ def main():
     ap.add_argument("--source", default="flow", choices=["flow", "dns"])
     ap.add_argument("--md")
     ap.add_argument("--json")
-    ap.add_argument("--variants", default="default;ONI_PYCACHE=0;ONI_FAST_EXIT=0;ONI_EARLY_HIP=1;ONI_WARMUP=1",
+    ap.add_argument("--variants", default="default;ONI_PYCACHE=0;ONI_FAST_EXIT=0;ONI_PREFETCH=0",
                     help="';'-separated env settings (space-separated KEY=VALUE within one), 'default' = none")
     ap.add_argument("--prof-out", help="keep the cProfile file here")
     a = ap.parse_args()
@@ -113,7 +113,7 @@ def main():
         _, _, err = _child(tmp, "importtime", a.tol, pyflags=("-X", "importtime"), source=a.source)
         imports = _importtime(err, 15)
         prof = os.path.join(tmp, "cold.prof")
-        _child(tmp, "cprofile", a.tol, extra_env=dict(ONI_CPROFILE=prof), source=a.source)
+        _child(tmp, "cprofile", a.tol, extra_env=dict(ONI_PROFILE=f"cprofile:{prof}"), source=a.source)
         if a.prof_out:
             shutil.copy(prof, a.prof_out)
         st = pstats.Stats(prof)

@@ -98,7 +98,7 @@ for s in "$@"; do
         --md "$OUT/ranks.md" > "$OUT/ranks.log" 2>&1 || { tail -30 "$OUT/ranks.log"; stop ranks 1; }
       cat "$OUT/ranks.md" ;;
     e2e)
-      timeout -k 10 1000 bash scripts/ab_e2e.sh ${E2E_ROUNDS:-2} ${E2E_VARIANTS:-ONI_DEFER_PRE=1} > "$OUT/ab_e2e.log" 2>&1 \
+      timeout -k 10 1000 bash scripts/ab_e2e.sh ${E2E_ROUNDS:-2} ${E2E_VARIANTS:-ONI_PREFETCH=1} > "$OUT/ab_e2e.log" 2>&1 \
         || { tail -20 "$OUT/ab_e2e.log"; stop e2e 1; }
       cat "$OUT/ab_e2e.log" ;;
     nccl)

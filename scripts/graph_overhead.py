@@ -23,7 +23,7 @@ def main():
         # host enqueue time of 5 iterations (no read-back): replay / launch calls only
         t0 = time.perf_counter()
         if graph:
-            (m, g), = eng._fgraphs.items()    # graphs of m = ONI_GRAPH_ITERS iterations (default 1)
+            (m, g), = eng._fgraphs.items()    # graphs of m = LDAEngine.graph_iters iterations (default 1)
             for _ in range(5 // m):
                 g.replay()
         else:

@@ -111,7 +111,7 @@ def main():
                 env["ONI_FAST_EXIT"] = "0"
             t0 = time.perf_counter()
             r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=a.timeout)
-            if a.json:      # the children's stderr (e.g. ONI_TABLE_PROFILE writer timings) next to the record
+            if a.json:      # the children's stderr (e.g. ONI_PROFILE=table writer timings) next to the record
                 with open(os.path.splitext(a.json)[0] + f".{kind}.N{n}.stderr.txt", "w") as fh:
                     fh.write(r.stderr[-200000:])
             wall = time.perf_counter() - t0

@@ -1,0 +1,93 @@
+"""docs/COMPONENTS.md cites real code: every file, symbol and test named in its implementation / test
+columns exists (verdict r4: the component map had gone stale against deleted kernels and tests)."""
+import os
+import re
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SEARCH = ["", "oni_ml_amd", "csrc/hip", "csrc/native", "scripts", "tests", "docs", "oni_ml_amd/models/lda"]
+CODE_EXT = (".py", ".hip", ".cpp", ".h", ".sh")
+# columns holding this repo's code (the "reference" columns cite /root/reference and are not checked here)
+REPO_COLUMNS = {"onimx", "tests", "kernel"}
+
+
+def _resolve(path):
+    for base in SEARCH:
+        p = os.path.join(ROOT, base, path)
+        if os.path.isfile(p):
+            return p
+    # a bare file name (`scorer.py`): the one file of that name in the package or csrc
+    hits = [os.path.join(d, f) for top in ("oni_ml_amd", "csrc") for d, _, fs in os.walk(os.path.join(ROOT, top))
+            for f in fs if f == os.path.basename(path) and os.path.join(d, f).endswith(path)]
+    return hits[0] if len(hits) == 1 else None
+
+
+def _cells():
+    """(row text, column header, cell) of every table cell in a repo column of docs/COMPONENTS.md."""
+    header = None
+    for line in open(os.path.join(ROOT, "docs", "COMPONENTS.md"), encoding="utf-8"):
+        if not line.startswith("|"):
+            header = None
+            continue
+        cells = [c.strip() for c in line.strip().strip("|").split("|")]
+        if header is None:
+            header = cells
+            continue
+        if set(cells[0]) <= set("-: "):
+            continue
+        for h, c in zip(header, cells):
+            if h in REPO_COLUMNS:
+                yield line, h, c
+
+
+def _test_refs(cell):
+    """(file, test) pairs: `test_x.py::test_y` and following `::test_z` (same file)."""
+    out, cur = [], None
+    for m in re.finditer(r"(test_\w+\.py)?::(test_\w+)", cell):
+        cur = m.group(1) or cur
+        out.append((cur, m.group(2)))
+    return out
+
+
+def _code_refs(cell):
+    """(path, symbol or None) of backticked `path.ext[:symbol]` references."""
+    out = []
+    for tok in re.findall(r"`([^`]+)`", cell):
+        m = re.match(r"^([\w./-]+\.(?:py|hip|cpp|h|sh))(?::([A-Za-z_][\w/]*))?", tok)
+        if m and not m.group(1).startswith("test_"):
+            out.append((m.group(1), m.group(2)))
+    return out
+
+
+def test_component_map_cites_existing_tests():
+    missing = []
+    for line, _, cell in _cells():
+        for f, t in _test_refs(cell):
+            p = _resolve(os.path.join("tests", f)) if f else None
+            if p is None or not re.search(rf"^def {t}\(", open(p).read(), re.M):
+                missing.append(f"{f}::{t}")
+    assert not missing, missing
+
+
+def test_component_map_cites_existing_code():
+    missing = []
+    for line, _, cell in _cells():
+        for path, sym in _code_refs(cell):
+            p = _resolve(path)
+            if p is None:
+                missing.append(path)
+                continue
+            if sym:
+                text = open(p, encoding="utf-8", errors="replace").read()
+                for s in sym.split("/"):          # `module.py:a/b` cites two symbols
+                    if not re.search(rf"\b{re.escape(s)}\b", text):
+                        missing.append(f"{path}:{s}")
+    assert not missing, missing
+
+
+def test_component_map_covers_every_survey_component():
+    text = open(os.path.join(ROOT, "docs", "COMPONENTS.md"), encoding="utf-8").read()
+    ids = ["C1", "C2", "C3", "C14", "C15"] + [f"C4{x}" for x in "abcdefg"] + [f"C5{x}" for x in "abcd"] + \
+          [f"C6{x}" for x in "abcdefghi"] + [f"C7{x}" for x in "abcd"] + ["C8", "C10"] + \
+          [f"C9{x}" for x in "abcdefghijkl"] + ["C11a", "C11b", "C11c", "C12", "P1", "P2", "P3", "P4"]
+    rows = {m.group(1) for m in re.finditer(r"^\| (C\d+[a-z]?|P\d) \|", text, re.M)}
+    assert not [i for i in ids if i not in rows]

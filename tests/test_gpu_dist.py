@@ -22,8 +22,9 @@ def _port():
 
 
 def _run(world, exchange, overlap="1"):
-    env = dict(os.environ, ONI_DIST_EXCHANGE=exchange, ONI_DIST_BACKEND="gloo", ONI_DIST_OVERLAP=overlap,
-               )
+    # overlap "0": the sparse exchange not overlapped with the private words' suff-stats (sparse-serial)
+    mode = "sparse-serial" if (exchange == "sparse" and overlap == "0") else exchange
+    env = dict(os.environ, ONI_DIST_EXCHANGE=mode, ONI_DIST_BACKEND="gloo")
     if world == 1:
         cmd = [sys.executable, "scripts/dist_check.py"]
     else:
@@ -146,7 +147,8 @@ def test_nccl_one_rank_engine_matches_plain_run(exchange, overlap):
     trajectory equals the plain single-process run."""
     one = _run(1, "auto")
     r = subprocess.run([sys.executable, "scripts/dist_check.py"], cwd=ROOT, capture_output=True, text=True,
-                       timeout=300, env=_nccl_env(ONI_DIST_EXCHANGE=exchange, ONI_DIST_OVERLAP=overlap))
+                       timeout=300, env=_nccl_env(ONI_DIST_EXCHANGE="sparse-serial" if (exchange == "sparse" and
+                                                                                       overlap == "0") else exchange))
     assert r.returncode == 0, r.stderr[-4000:]
     o = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
     assert o["world"] == 1

@@ -47,9 +47,9 @@ def _oracle(c, lb, alpha, st, U):
                             st.var_max_iter, st.var_converged, 1, 0, gs_updates=U)
 
 
-def _gpu_estep(c, K, lb, alpha, st, U):
+def _gpu_estep(c, K, lb, alpha, st, U, **kw):
     st.gs_updates = U
-    eng = LDAEngine(c, K, st, backend="hip", seed=0, precision="fp64")
+    eng = LDAEngine(c, K, st, backend="hip", seed=0, precision="fp64", **kw)
     eng.init_from_model(lb, alpha)
     sc = eng.e_step()
     torch.cuda.synchronize()
@@ -136,7 +136,7 @@ def test_em_run_matches_cpu_engine():
 
 @pytest.mark.gpu
 def test_mstep_refills_staged_rows_bitwise(monkeypatch):
-    """The M-step launch refilling the next E-step's staged rows (ONI_GS_STAGE_FUSE=1, default) gives
+    """The M-step launch refilling the next E-step's staged rows (LDAEngine.stage_fuse, default) gives
     whole EM runs bitwise equal to a gs_stage launch before every E-step, and leaves each staged
     position holding its word's final beta row."""
     rng = np.random.default_rng(5)
@@ -148,9 +148,9 @@ def test_mstep_refills_staged_rows_bitwise(monkeypatch):
     c = Corpus(ptr.astype(np.int64), words, rng.integers(1, 4, words.size).astype(np.int64), V)
     runs = {}
     for fuse in ("1", "0"):
-        monkeypatch.setenv("ONI_GS_STAGE_FUSE", fuse)
         st = LDASettings(em_max_iter=7)
         eng = LDAEngine(c, 20, st, backend="hip", seed=9, precision="fp64")
+        eng.stage_fuse = fuse == "1"
         assert eng._stages and bool(eng._fused_stages(eng.gs_plan)) == (fuse == "1")
         r = eng.run()
         runs[fuse] = (np.array([x[0] for x in r.likelihoods]), eng.alpha, eng.gather_gamma(), eng.log_beta())
@@ -185,21 +185,19 @@ def test_gs64_graph_replay_and_gate():
     assert eng.gamma.abs().max().item() == 0
 
 
-@pytest.mark.parametrize("stage,tr", [("1", "0"), ("0", "0"), ("1", "1")])
+@pytest.mark.parametrize("stage", ["1", "0"])
 @pytest.mark.parametrize("head", [
     # longest chunk 938 words: past the two prefetched rounds (7 waves x 64 lanes x 2), streamed remainder
     [30000, 20000, 15000, 9000, 6000, 5000, 4000, 3500, 3000, 2500, 2200, 2100],
     [24000, 20000, 15000, 9000, 6000, 5000, 4000, 3500, 3000, 2500, 2200, 2100],
 ])
-def test_longest_documents_match_oracle(head, stage, tr, monkeypatch):
+def test_longest_documents_match_oracle(head, stage, monkeypatch):
     """The longest-document kernel (gs_wsteam: word waves + a topic wave) against the oracle, on chunks
     that need both prefetched rounds, with more than 8 team8 documents so the XCD-aware workgroup order
     holds empty slots (GSPlan.isolate_longest); with the staged row copies (GSStage, default) and
-    gathering from beta; and with the topic wave summing the word waves' lane partials
-    (ONI_GS_TOPIC_REDUCE=1, staged)."""
+    gathering from beta."""
     from oni_ml_amd.ops import hip as H
     monkeypatch.setenv("ONI_GS_STAGE", stage)
-    monkeypatch.setenv("ONI_GS_TOPIC_REDUCE", tr)
     rng = np.random.default_rng(11)
     V, D = 40000, 300
     lens = np.minimum(rng.zipf(1.5, D), 200)
@@ -255,50 +253,14 @@ def test_staged_rows_bitwise_equal_beta_rows(monkeypatch):
         assert np.array_equal(a, b)
 
 
-@pytest.mark.parametrize("loaders", ["1", "2"])
-@pytest.mark.parametrize("K,vconv", [(20, -1e30), (20, 1e-6), (24, -1e30), (8, -1e30), (32, -1e30)])
-def test_ring_kernel_matches_oracle(monkeypatch, K, vconv, loaders):
-    """gs_ring (ONI_GS_RING=1 / 2: the staged longest documents streamed through an LDS ring by one / two
-    loader waves, flags instead of barriers) against the CPU oracle of the same schedule: gamma, likelihoods,
-    sweeps and the sufficient statistics of its c.phi rows at 1e-10; and against gs_wsteam to rounding."""
-    rng = np.random.default_rng(11 + K)
-    V, D = 20000, 150
-    lens = np.minimum(rng.zipf(1.5, D), 150)
-    lens[:6] = [13000, 7000, 4100, 3000, 2100, 2049]
-    ptr = np.concatenate([[0], np.cumsum(lens)])
-    words = np.concatenate([rng.choice(V, n, replace=False) for n in lens]).astype(np.int32)
-    c = Corpus(ptr.astype(np.int64), words, rng.integers(1, 4, words.size).astype(np.int64), V)
-    lb = _log_beta(V, K, seed=K)
-    alpha = 0.41
-    ref = _oracle(c, lb, alpha, LDASettings(var_max_iter=7, var_converged=vconv), 32)
-    out = {}
-    for ring in (loaders, "0"):
-        monkeypatch.setenv("ONI_GS_RING", ring)
-        eng, sc = _gpu_estep(c, K, lb, alpha, LDASettings(var_max_iter=7, var_converged=vconv), 32)
-        assert eng._stages, "the team8 bucket must be staged for the ring kernel"
-        out[ring] = (eng.gamma[:, :K].cpu().numpy(), eng.lik.cpu().numpy(), eng.iters.cpu().numpy(),
-                     eng._cw_local[:, :K].cpu().numpy(), sc)
-    g, lik, it, cw, sc = out[loaders]
-    same = it == ref["iters"]
-    assert same[:6].all() and same.mean() > 0.99
-    assert _rel(g[same], ref["gamma"][same], 1e-12) < 1e-10
-    assert _rel(lik[same], ref["doc_likelihood"][same], 1.0) < 1e-10
-    if vconv < 0:
-        assert _rel(cw, np.ascontiguousarray(ref["class_word"].T), 1e-30) < 1e-10
-        assert abs(sc[0] - ref["likelihood"]) / abs(ref["likelihood"]) < 1e-11
-    g0, lik0, it0, cw0, _ = out["0"]
-    assert np.array_equal(it, it0)
-    assert _rel(g, g0, 1e-12) < 1e-12 and _rel(cw, cw0, 1e-30) < 1e-12
-
-
 @pytest.mark.parametrize("K,env,U", [
     (100, {}, 32),                                                      # default split for KS > 32
     (100, {"ONI_GS_SPLIT_MIN": "4000"}, 32),
-    (100, {"ONI_GS_SPLIT_MIN": "4000", "ONI_SPLIT_MAX_BLOCKS": "9", "ONI_GS_SPLIT_G": "3", "ONI_GS_SPLIT_BATCHES": "8"}, 32),
-    (20, {"ONI_GS_SPLIT_MIN": "3000", "ONI_GS_SPLIT_G": "5"}, 32),      # forced on a narrow KS
+    (100, {"ONI_GS_SPLIT_MIN": "4000,g=3,batches=8", "ONI_SPLIT_MAX_BLOCKS": "9"}, 32),
+    (20, {"ONI_GS_SPLIT_MIN": "3000,g=5"}, 32),                         # forced on a narrow KS
     (52, {"ONI_GS_SPLIT_MIN": "2500"}, 32),
     (50, {}, 64),                                                       # 64-row LDS tables (KS 52, U = 64)
-    (50, {"ONI_GS_SPLIT_MIN": "2500", "ONI_GS_SPLIT_G": "3"}, 48),
+    (50, {"ONI_GS_SPLIT_MIN": "2500,g=3"}, 48),
 ])
 def test_split_documents_match_oracle(K, env, U, monkeypatch):
     """gs_split (one document over G workgroups exchanging tagged per-chunk partials) against the
@@ -349,10 +311,9 @@ def test_suff_split_matches_single_pass(K, split_min, monkeypatch):
     c = _edge_corpus(seed=3, max_len=9000 if split_min else 5000)
     lb = _log_beta(c.num_terms, K, seed=6)
     out = []
-    for mode in ("0", "force"):
-        monkeypatch.setenv("ONI_SUFF_SPLIT", mode)
-        eng, sc = _gpu_estep(c, K, lb, 0.45, LDASettings(var_max_iter=4), 32)
-        assert (eng._suff_split is None) == (mode == "0")
+    for mode in ("off", "force"):
+        eng, sc = _gpu_estep(c, K, lb, 0.45, LDASettings(var_max_iter=4), 32, suff_split=mode)
+        assert (eng._suff_split is None) == (mode == "off")
         if split_min:
             assert eng.gs_plan.split is not None and len(eng.gs_plan.plan) + 1 >= 6, \
                 [v for v, _ in eng.gs_plan.plan]
@@ -478,3 +439,53 @@ def test_large_u_needs_wide_topics():
     st.gs_updates = 64
     with pytest.raises(ValueError, match="needs K > 32"):
         LDAEngine(c, 20, st, backend="hip", seed=0, precision="fp64")
+
+
+@pytest.mark.parametrize("K,xs", [
+    (20, dict(docs=3)),                                  # LDS-minimum members, placement-checked stores
+    (20, dict(docs=3, proto=0)),                         # write-through stores only
+    (20, dict(docs=4, members=11)),                      # more members than the LDS needs
+    (8, dict(docs=2, members=3)),                        # > 64 words of a chunk per member
+    (32, dict(docs=2)),                                  # one member part per column (KS + 1 = 33)
+])
+def test_xsplit_documents_match_oracle(K, xs):
+    """gs_xsplit (csrc/hip/lda_xsplit.hip: one document over one-wave members of one XCD, beta rows resident
+    in LDS, 16-byte self-tagged granules) against the oracle at 1e-10, every member replaying the same
+    refresh; graph replay moves the launch epoch on."""
+    rng = np.random.default_rng(K + 7)
+    V, D = 40000, 260
+    lens = np.minimum(rng.zipf(1.5, D), 200)
+    lens[:6] = [30000, 20000, 12000, 9100, 5000, 3100]
+    lens[9] = 0
+    ptr = np.concatenate([[0], np.cumsum(lens)])
+    words = np.concatenate([rng.choice(V, n, replace=False) for n in lens]).astype(np.int32)
+    counts = rng.integers(1, 4, words.size)
+    c = Corpus(ptr.astype(np.int64), words, counts.astype(np.int64), V)
+    lb = _log_beta(V, K, seed=5)
+    for vconv in (-1e30, 1e-6):
+        st = LDASettings(var_max_iter=5, var_converged=vconv)
+        ref = _oracle(c, lb, 0.33, st, 32)
+        eng, sc = _gpu_estep(c, K, lb, 0.33, LDASettings(var_max_iter=5, var_converged=vconv), 32, xsplit=xs)
+        sp = eng.gs_plan.split
+        assert sp is not None and sp.n_docs == xs["docs"]
+        (b,) = sp.batches
+        assert b.get("x") and int(b["error"].item()) == 0
+        if xs.get("proto", 1) == 1:
+            assert set(b["placed"].cpu().tolist()) <= {0, 1}
+        full = lens > 0
+        it = eng.iters.cpu().numpy()
+        same = (it == ref["iters"]) | ~full
+        if vconv < 0:
+            assert same.all()
+        else:
+            assert same.mean() > 0.99 and same[:6].all()
+        assert _rel(eng.gamma[:, :K].cpu().numpy()[same], ref["gamma"][same], 1e-12) < 1e-10
+        assert _rel(eng.lik.cpu().numpy()[same], ref["doc_likelihood"][same], 1.0) < 1e-10
+        if vconv < 0:
+            cw = eng._cw_local[:, :K].cpu().numpy()
+            assert _rel(cw, np.ascontiguousarray(ref["class_word"].T), 1e-30) < 1e-10
+            assert abs(sc[0] - ref["likelihood"]) / abs(ref["likelihood"]) < 1e-11
+            g1 = eng.gamma.clone()
+            eng.e_step()
+            torch.cuda.synchronize()
+            assert torch.equal(g1, eng.gamma)

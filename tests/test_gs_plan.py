@@ -69,16 +69,6 @@ def test_csc_subset_partitions_each_word_in_order():
         assert el[int(pl[w]):int(pl[w + 1])].tolist() == [ce[s] for s in slots if late[cd[s]]]
 
 
-def test_xcd_gaps_leave_block_zero_mod_8_empty():
-    o = np.arange(1, 101, dtype=np.int32)
-    for dpb in (1, 4, 16, 32):
-        g = GSPlan.xcd_gaps(o, dpb)
-        blocks = [g[i:i + dpb] for i in range(0, g.size, dpb)]
-        assert all((blk == -1).all() for b, blk in enumerate(blocks) if b % 8 == 0)
-        assert g[g >= 0].tolist() == o.tolist()
-        assert all((blk >= 0).all() for b, blk in enumerate(blocks[:-1]) if b % 8)
-
-
 def test_stage_tiles_cover_each_document_in_order():
     """GSStage: per launch item, the document's positions in 64-word tiles (entry of position 0, valid
     count), the item's offset at its first tile; placement gaps (-1) take no tiles."""

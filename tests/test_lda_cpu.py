@@ -2,6 +2,7 @@
 import math
 import os
 import subprocess
+import sys
 
 import numpy as np
 import pytest
@@ -243,3 +244,50 @@ def test_parity_gs_updates_mode():
     assert resolved_gs_updates(LDASettings(gs_updates=-1), 50) == 64
     assert resolved_gs_updates(LDASettings(gs_updates=0), 50) == 0
     assert resolved_gs_updates(LDASettings(gs_updates=16), 100) == 16
+
+
+def test_lda_executable_gs_updates(tmp_path):
+    """`lda est ... --gs-updates U` runs the GPU engine's block schedule in the C++ baseline: the same
+    result as the in-process C++ engine with settings.gs_updates = U; a bad flag is refused."""
+    exe = os.path.join(os.path.dirname(native.__file__), "..", "_lib", "lda")
+    c = planted_corpus(num_docs=80, num_terms=60, num_topics=3, mean_tokens=60, seed=8)
+    ldac.write_model_dat(str(tmp_path / "model.dat"), c)
+    (tmp_path / "settings.txt").write_text(LDASettings(em_max_iter=3).dumps())
+    outs = {}
+    for u in ("0", "4"):
+        out = tmp_path / f"out{u}"
+        r = subprocess.run([exe, "est", "2.5", "5", str(tmp_path / "settings.txt"), "1", str(tmp_path / "model.dat"),
+                            "random", str(out), "--gs-updates", u], capture_output=True, text=True,
+                           env=dict(os.environ, ONI_THREADS="2"))
+        assert r.returncode == 0, r.stderr
+        assert ("block Gauss-Seidel" in r.stdout) == (u != "0")
+        outs[u] = (out / "likelihood.dat").read_text()
+    assert outs["0"] != outs["4"]          # a different schedule, a different trajectory
+    r = subprocess.run([exe, "est", "2.5", "5", str(tmp_path / "settings.txt"), "1", str(tmp_path / "model.dat"),
+                        "random", str(tmp_path / "bad"), "--gs-updates", "x"], capture_output=True, text=True)
+    assert r.returncode == 1 and "usage" in r.stderr
+
+
+def test_auto_backend_without_gpu_is_ldac_engine():
+    """No GPU: backend "auto" is the C++ lda-c engine (csrc/native/lda_ref.cpp), never the Jacobi rehearsal."""
+    if torch.cuda.is_available():
+        pytest.skip("a GPU is present: auto selects the hip engine")
+    c = planted_corpus(num_docs=40, num_terms=30, num_topics=3, seed=9)
+    eng = LDAEngine(c, 4, LDASettings(em_max_iter=2), seed=1)
+    assert eng.backend == "cpu" and "Gauss-Seidel" in eng.schedule
+
+
+def test_lda_est_nproc_must_match_world_size(tmp_path):
+    """`lda est <nproc>` is oni-lda-c's rank count: a torchrun launch of another size fails loudly."""
+    c = planted_corpus(num_docs=30, num_terms=20, num_topics=3, seed=10)
+    ldac.write_model_dat(str(tmp_path / "model.dat"), c)
+    (tmp_path / "settings.txt").write_text(LDASettings(em_max_iter=2).dumps())
+    env = dict(os.environ, WORLD_SIZE="2", RANK="0")
+    r = subprocess.run([sys.executable, "-m", "oni_ml_amd", "lda", "est", "2.5", "4", str(tmp_path / "settings.txt"),
+                        "3", str(tmp_path / "model.dat"), "random", str(tmp_path / "o")],
+                       capture_output=True, text=True, env=env, cwd=os.path.dirname(os.path.dirname(__file__)))
+    assert r.returncode == 1 and "nproc = 3 but 2 ranks" in r.stderr
+    r = subprocess.run([sys.executable, "-m", "oni_ml_amd", "lda", "est", "2.5", "4", str(tmp_path / "settings.txt"),
+                        "0", str(tmp_path / "model.dat"), "random", str(tmp_path / "o")],
+                       capture_output=True, text=True, cwd=os.path.dirname(os.path.dirname(__file__)))
+    assert r.returncode == 1 and "nproc must be a positive" in r.stderr

@@ -294,12 +294,13 @@ def test_background_writer_join_reraises():
 @pytest.mark.parametrize("compat", ["strict", "fixed"])
 def test_flow_post_paths_byte_identical(tmp_path, monkeypatch, compat):
     """The big-table paths of the one-process flow pipeline write the bytes of the plain ones: the
-    deferred lda_post text (ONI_DEFER_POST=1, the default from 2^26 values) and, in fixed mode, the
+    deferred lda_post text (on from pipeline/common.py DEFER_POST_VALUES values) and, in fixed mode, the
     scorer's key -> φ row map instead of the word-name dictionary (checked against a resumed run,
     which scores through the names as written)."""
     outs = {}
-    for tag, env in (("plain", "0"), ("deferred", "1")):
-        monkeypatch.setenv("ONI_DEFER_POST", env)
+    from oni_ml_amd.pipeline import common as PC
+    for tag, limit in (("plain", 1 << 62), ("deferred", 0)):
+        monkeypatch.setattr(PC, "DEFER_POST_VALUES", limit)
         d = tmp_path / tag
         d.mkdir()
         cfg = _flow_cfg(d, compat=compat)

@@ -18,7 +18,7 @@ def _run(tmp_path, engines, events):
     out = tmp_path / "parity.json"
     # one host thread per engine: torch's OpenMP workers spin-wait, and beside other busy processes
     # (pytest -n, a parity run) an 8-thread pool on this tiny corpus ran ~60x slower than one thread
-    env = dict(os.environ, OMP_NUM_THREADS="1", ONI_CPU_THREADS="1")
+    env = dict(os.environ, OMP_NUM_THREADS="1", ONI_THREADS="1")
     r = subprocess.run([sys.executable, SCRIPT, "--events", str(events), "--engines", engines, "--json", str(out),
                         "--md", str(tmp_path / "parity.md")], capture_output=True, text=True, timeout=600, env=env)
     assert r.returncode == 0, r.stderr[-2000:]

@@ -1,4 +1,4 @@
-"""Row-sharded ml_ops pipeline (pipeline/sharded.py) over 2 and 4 gloo ranks == one process, byte for
+"""Row-sharded ml_ops pipeline (pipeline/sharded.py) over 2, 4 and 8 gloo ranks == one process, byte for
 byte: every file of the run (corpus files, doc_wc.dat, the lda-c model files, doc_results.csv,
 word_results.csv and the scored results).
 
@@ -86,7 +86,7 @@ def test_sharded_flow_pipeline_bytes_equal_one_process(flow_day, compat, tmp_pat
     os.link(flow_day / "fb.csv", one / "flow_scores.csv")
     r1 = _run(1, "flow", str(flow_day / "in"), str(one), extra)
     assert r1[0][1] > 0
-    for world in (2, 4):
+    for world in (2, 4, 8):     # 8: the ranks of one MI355X node (the reference's job: 20 MPI ranks)
         lp = tmp_path / f"w{world}"
         lp.mkdir()
         os.link(flow_day / "fb.csv", lp / "flow_scores.csv")
@@ -156,13 +156,13 @@ def test_sharded_dns_pipeline_bytes_equal_one_process(compat, tmp_path):
     g = generate_dns_day(str(tmp_path / "in"), events=6000, seed=4, files=4, n_names=700, n_clients=250)
     extra = dict(tol=1e-2, compat=compat, dns_path=g["dns_path"], top1m=g["top1m"])
     outs = {}
-    for world in (1, 2, 4):
+    for world in (1, 2, 4, 8):
         lp = tmp_path / f"w{world}"
         lp.mkdir()
         _dns_feedback(str(lp / "dns_scores.csv"), g["dns_path"])
         outs[world] = _run(world, "dns", None, str(lp), extra)
     assert outs[1][0][1] > 0
-    for world in (2, 4):
+    for world in (2, 4, 8):
         assert all(o == outs[1][0][1] for _, o in outs[world])
         for f in DNS_FILES:
             a, b = (tmp_path / "w1" / f).read_bytes(), (tmp_path / f"w{world}" / f).read_bytes()
