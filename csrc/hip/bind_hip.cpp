@@ -99,20 +99,6 @@ PYBIND11_MODULE(_onihip, m) {
                      P<unsigned long long>(xchg), P<int>(counter), n_docs, P<int>(error)};
     oni::launch_gs_split(a, s, KS, S(stream));
   });
-  m.def("gs_xsplit_rows", [](int KS) { return oni::gs_xsplit_rows(KS); });
-  m.def("gs_xsplit", [](u doc_ptr, u word_idx, u counts, u beta, int K, int KS, int gs_updates, u params, u gamma,
-                        u cphi, u lik, u alpha_ss, u iters, u seg_doc, u seg_index, u seg_count, u seg_base,
-                        u doc_slot, int n_blocks, int n_rows, u xchg, u counter, int n_docs, u error, int proto,
-                        u placed, u stream, u dbg) {
-    oni::GSArgs a{P<const int>(doc_ptr), P<const int>(word_idx), P<const float>(counts), nullptr,
-                  n_blocks,              P<const double>(beta),  K,                      gs_updates,
-                  P<const double>(params), P<double>(gamma),     P<double>(cphi),        P<double>(lik),
-                  P<double>(alpha_ss),   P<int>(iters),         P<long long>(dbg)};
-    oni::XSplitArgs s{P<const int>(seg_doc), P<const int>(seg_index), P<const int>(seg_count),
-                      P<const int>(seg_base), P<const int>(doc_slot), n_blocks, n_rows,
-                      P<unsigned>(xchg), P<int>(counter), n_docs, P<int>(error), proto, P<int>(placed)};
-    oni::launch_gs_xsplit(a, s, KS, S(stream));
-  });
   m.def("gs_suff64", [](u word_ptr, u csc_ent, u order, int n_heavy, int n_medium, int n_light, u cphi, u cw, u part,
                         u lik, u ass, int lo, int hi, int KS, u gate, u stream, u cw_base) {
     oni::launch_gs_suff64(P<const int>(word_ptr), P<const int>(csc_ent), P<const int>(order), n_heavy, n_medium,

@@ -1,5 +1,5 @@
 // fp64 math and wave-reduction helpers shared by the block Gauss-Seidel E-step kernels
-// (lda_gs64.hip: the one-workgroup document kernels; lda_xsplit.hip: one document over the CUs of
+// (lda_gs64.hip: the one-workgroup document kernels; experimental/lda_xsplit.hip: one document over the CUs of
 // an XCD).  lda-c's arithmetic in short dependency chains for gfx950.
 #pragma once
 #include "common.h"

@@ -132,7 +132,7 @@ int gs_split_umax(int KS); // largest gs_updates of the split kernel (64 at KS <
 void launch_gs_split(const GSArgs& a, const SplitArgs& s, int KS, hipStream_t st);
 int gs_split_capacity(int KS);
 
-// One long document over the CUs of one XCD (K <= 32, lda_xsplit.hip): G one-wave workgroups
+// One long document over the CUs of one XCD (K <= 32, experimental/lda_xsplit.hip): G one-wave workgroups
 // (blocks b = x + 8 m of a launch of 8 x groups blocks share XCD x under the round-robin dispatch),
 // each holding its share of every chunk's beta rows in LDS for the whole E-step, exchange their
 // per-chunk partial topic sums as 16-byte self-tagged granules.  proto 1: L2-resident stores, used

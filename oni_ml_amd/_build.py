@@ -155,6 +155,28 @@ def build_hip(verbose=False, jobs=8) -> Path:
     return out
 
 
+def build_hip_exp(verbose=False, jobs=8) -> Path:
+    """csrc/hip/experimental/ (E-step variants measured not faster, for their tests and benchmarks)
+    into _onihip_exp: a module of its own, so the production code object and ml_ops never carry them."""
+    out = LIB / ("_onihip_exp" + _ext_suffix())
+    exp = CSRC / "hip" / "experimental"
+    hdrs = sorted((CSRC / "hip").glob("*.h")) + sorted(exp.glob("*.h"))
+    srcs = sorted(exp.glob("*.hip"))
+    bind = exp / "bind_exp.cpp"
+    flags = hip_flags()
+
+    def one(src):
+        o = OBJ / "hip_exp" / (src.stem + ".o")
+        extra = [f"-I{_pybind_inc()}", f"-I{_py_inc()}"] if src == bind else []
+        return _compile(src, o, [HIPCC], flags + extra, hdrs, verbose)
+
+    with ThreadPoolExecutor(max_workers=jobs) as ex:
+        objs = list(ex.map(one, srcs + [bind]))
+    link = [HIPCC, "-shared", f"--offload-arch={ARCH}", "-fPIC", "-o", str(out)] + [str(o) for o in objs]
+    _link(out, objs, link, verbose)
+    return out
+
+
 def build_native(verbose=False, jobs=8) -> Path:
     """Compile csrc/native/*.cpp (host runtime) into _oninative + the `lda` CLI binary."""
     cxx = os.environ.get("CXX", "g++")
@@ -219,6 +241,7 @@ def build_all(verbose=False, hip=True, native=True):
             if not Path(HIPCC).exists():
                 raise RuntimeError(f"hipcc not found at {HIPCC}")
             outs.append(build_hip(verbose))
+            outs.append(build_hip_exp(verbose))
         return outs
 
 

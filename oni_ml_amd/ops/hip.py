@@ -50,6 +50,23 @@ def lib():
     return _LIB
 
 
+_EXP = None
+
+
+def exp_lib():
+    """The experimental kernels' module (`_onihip_exp`: variants measured not faster, loaded only when a
+    caller asks for one -- never by ml_ops); raises loudly if it is missing."""
+    global _EXP
+    if _EXP is None:
+        lib()
+        try:
+            _EXP = importlib.import_module("_onihip_exp")
+        except Exception as e:  # pragma: no cover - depends on build state
+            raise RuntimeError(f"oni_ml_amd experimental HIP extension (_onihip_exp) failed to load: {e!r}. "
+                               "Run `python -m oni_ml_amd._build`.") from e
+    return _EXP
+
+
 def compiled_ks():
     return list(lib().compiled_ks())
 
@@ -624,11 +641,12 @@ def gs_split(doc_ptr, word_idx, counts, beta, K, gs_updates, params, gamma, cphi
 
 def gs_xsplit_rows(KS: int) -> int:
     """LDS row capacity of one gs_xsplit member (its words over every chunk of a sweep), 0: no kernel."""
-    return int(lib().gs_xsplit_rows(int(KS)))
+    return int(exp_lib().gs_xsplit_rows(int(KS)))
 
 
 class GSXSplitPlan:
-    """Documents split over the CUs of one XCD each (gs_xsplit, csrc/hip/lda_xsplit.hip, even KS <= 32).
+    """Documents split over the CUs of one XCD each (gs_xsplit, csrc/hip/experimental/lda_xsplit.hip, even KS <= 32;
+    measured not faster than one workgroup: profiles/r5_xcd_split.md).
 
     The first ``limit`` documents of ``doc_ids`` (longest first) that fit are taken.  Document d of n words
     (W = ceil(n / U) words per chunk) gets G one-wave members, each holding its
@@ -708,7 +726,7 @@ def gs_xsplit(doc_ptr, word_idx, counts, beta, K, gs_updates, params, gamma, cph
         raise ValueError("gs_xsplit: KS, K or gs_updates out of range")
     for k in ("seg_doc", "seg_index", "seg_count", "seg_base", "doc_slot"):
         _chk(batch[k], torch.int32, k, (nb,), dev)
-    lib().gs_xsplit(
+    exp_lib().gs_xsplit(
         _chk(doc_ptr, torch.int32, "doc_ptr", (D + 1,), dev), _chk(word_idx, torch.int32, "word_idx", (nnz,), dev),
         _chk(counts, torch.float32, "counts", (nnz,), dev), _chk(beta, torch.float64, "beta", (V, KS), dev),
         int(K), int(KS), int(gs_updates), _params_ptr(params, dev) or _bad("params"),

@@ -449,7 +449,7 @@ def test_large_u_needs_wide_topics():
     (32, dict(docs=2)),                                  # one member part per column (KS + 1 = 33)
 ])
 def test_xsplit_documents_match_oracle(K, xs):
-    """gs_xsplit (csrc/hip/lda_xsplit.hip: one document over one-wave members of one XCD, beta rows resident
+    """gs_xsplit (csrc/hip/experimental/lda_xsplit.hip: one document over one-wave members of one XCD, beta rows resident
     in LDS, 16-byte self-tagged granules) against the oracle at 1e-10, every member replaying the same
     refresh; graph replay moves the launch epoch on."""
     rng = np.random.default_rng(K + 7)
