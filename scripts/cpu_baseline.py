@@ -32,15 +32,16 @@ def main():
     ap.add_argument("--topics", type=int, default=20)
     ap.add_argument("--out", default="profiles/r5_cpu_baseline.json")
     ap.add_argument("--schedules", default="0,32", help="gs_updates values (0 = lda-c's per-word schedule)")
+    ap.add_argument("--exe", default=None, help="another build of the `lda` binary (e.g. an older commit's)")
     a = ap.parse_args()
     import torch
     from oni_ml_amd.io import ldac
     from oni_ml_amd.models.lda.settings import LDASettings
     from oni_ml_amd.pipeline.flow import synthetic_flow_corpus
     c, _ = synthetic_flow_corpus(events=a.events, seed=0, device=torch.device("cpu"))
-    exe = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "oni_ml_amd", "_lib", "lda")
+    exe = a.exe or os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "oni_ml_amd", "_lib", "lda")
     threads = os.environ.get("ONI_THREADS", "8")
-    rec = dict(corpus=dict(events=a.events, docs=c.num_docs, terms=c.num_terms, nnz=c.nnz),
+    rec = dict(exe=exe, corpus=dict(events=a.events, docs=c.num_docs, terms=c.num_terms, nnz=c.nnz),
                topics=a.topics, threads=int(threads), cpu=os.cpu_count(), runs=[])
     with tempfile.TemporaryDirectory() as tmp:
         ldac.write_model_dat(os.path.join(tmp, "model.dat"), c)
