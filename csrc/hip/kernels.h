@@ -90,7 +90,8 @@ enum GsVariant : int {
   kGsTeam1 = 1,    // one wave per document
   kGsTeam4 = 2,    // one 4-wave workgroup per document
   kGsTeam8 = 3,    // one 8-wave workgroup per document (8 prefetched words per slot and chunk)
-  kGsSmall = 4,    // 16 lanes per document, tiny < n <= 64 words, KS <= 32 (register state)
+  kGsSmall = 4,    // 16 lanes per document: KS <= 32 tiny < n <= 64 words (register state); KS > 32 the
+                   // one-wave range (gs_smallw, chunk tables in the c*phi rows)
 };
 struct GSArgs {
   const int* doc_ptr;     // [D+1]

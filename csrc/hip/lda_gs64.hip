@@ -152,15 +152,20 @@ __global__ __launch_bounds__(256) void gs_tiny(GSArgs a) {
       const double P = bits_sum<0, LTG, false>(pp);
       const double r = c * drcp(P);
       lw = fma(c, flog(P), lw);
+      // branch-free refresh: the KPL digamma/exp chains interleave (a topic-guarded psi_exp is a basic block
+      // of its own and the chains ran one after another); padding topics have E = 0, so nw = 0, and keep
+      // gamma = 0, psi = m, E = 0
 #pragma unroll
       for (int i = 0; i < KPL; ++i) {
-        if (q + TG * i < K) {
-          const double nw = E[i] * b[i] * r;
-          lp = fma(psi[i], nw, lp);
-          gam[i] += nw - C[0][i];
-          C[0][i] = nw;
-          psi_exp(gam[i], m, psi[i], E[i]);
-        }
+        const bool real = q + TG * i < K;
+        const double nw = E[i] * b[i] * r;
+        lp = fma(psi[i], nw, lp);
+        gam[i] += nw - C[0][i];
+        C[0][i] = nw;
+        double pn, en;
+        psi_exp(real ? gam[i] : 1.0, m, pn, en);
+        psi[i] = real ? pn : psi[i];
+        E[i] = real ? en : 0.0;
       }
       rotl1(C);
     }
@@ -302,15 +307,17 @@ __global__ __launch_bounds__(256) void gs_small(GSArgs a) {
 #pragma unroll
         for (int i = 0; i < KPL; ++i) acc[i] = fma(r, b[i], acc[i]);
       }
+      // branch-free refresh (interleaved chains; padding topics: E = 0, nw = 0, psi stays m)
 #pragma unroll
       for (int i = 0; i < KPL; ++i) {
         const double nw = E[i] * acc[i];
         Et[j][i] = E[i];
-        if (real[i]) {
-          lps[i] = fma(psi[i], nw, lps[i]);
-          gam[i] += nw - C[j][i];
-          psi_exp(gam[i], m, psi[i], E[i]);
-        }
+        lps[i] = fma(psi[i], nw, lps[i]);
+        gam[i] += nw - C[j][i];
+        double pn, en;
+        psi_exp(real[i] ? gam[i] : 1.0, m, pn, en);
+        psi[i] = real[i] ? pn : psi[i];
+        E[i] = real[i] ? en : 0.0;
         C[j][i] = nw;
       }
     }
@@ -357,6 +364,249 @@ __global__ __launch_bounds__(256) void gs_small(GSArgs a) {
 #pragma unroll
       for (int i = 0; i < KPL; ++i)
         if (q + TG * i < KS) __builtin_nontemporal_store(Et[j][i] * b[i] * r, &row[q + TG * i]);
+    }
+  }
+}
+
+// ---------------------------------------------------------- small, K > 32 ----
+// The one-wave range at K > 32 (short documents; at lda-c's per-word schedule every document whose chunks
+// hold <= 2 words): 16 lanes per document, KPL = ceil(KS / 16) topics per lane, four documents per wave,
+// no LDS and no barrier.  The one-wave team (gs_team<KS, 1>) spreads a chunk's words over 4 word slots, then
+// pays a cross-slot reduction and an LDS round trip per chunk and refreshes 2 topics per lane with 28 of
+// 128 lane slots idle at K = 100; here the word loop runs in the document's 16 lanes and the refresh is
+// KPL independent digamma/exp chains per lane (100 of 112 lane slots busy at K = 100).  Chunk tables live in
+// the document's own c*phi rows (gs_team's GM layout): C_j in row j W, the E chunk j used in row j W + 1
+// (chunks of >= 2 words); a one-word chunk's C_j IS that word's c*phi, so documents of <= U words need no
+// final pass.  Every access to a row is by the lane that owns the topic (same-lane program order).
+// RQ: words of the NEXT chunk whose rows are gathered during this chunk (ids one chunk earlier still); the
+// rest of a chunk streams in batches of RQ.  Row loads are brow[q + 16 i] at constant offsets: lanes whose
+// topic is >= KS read into the next row (beta carries one zero pad row, LDAEngine), values that only ever
+// meet E = 0 / are never stored -- the clamped index held two address VGPRs per load.
+template <int N, int KPL>
+__device__ __forceinline__ void quad_word_steps(const double (&E)[KPL], const double (*b)[KPL], const double* c,
+                                                double (&acc)[KPL], double& lw) {
+  double P[N];
+#pragma unroll
+  for (int u = 0; u < N; ++u) {
+    double p0 = 0.0, p1 = 0.0;
+#pragma unroll
+    for (int i = 0; i < KPL; i += 2) p0 = fma(E[i], b[u][i], p0);
+#pragma unroll
+    for (int i = 1; i < KPL; i += 2) p1 = fma(E[i], b[u][i], p1);
+    P[u] = bits_sum<0, 4, false>(p0 + p1);
+  }
+#pragma unroll
+  for (int u = 0; u < N; ++u) {
+    const double Pu = c[u] > 0.0 ? P[u] : 1.0;
+    const double r = c[u] * drcp(Pu);
+    lw = fma(c[u], flog(Pu), lw);
+#pragma unroll
+    for (int i = 0; i < KPL; ++i) acc[i] = fma(r, b[u][i], acc[i]);
+  }
+}
+
+template <int KS, int RQ, int MINW = 1>
+__global__ __launch_bounds__(256, MINW) void gs_smallw(GSArgs a) {
+  static_assert(KS > 32, "gs_smallw: KS > 32 (gs_small covers KS <= 32)");
+  constexpr int TG = 16, KPL = (KS + TG - 1) / TG;
+  if (a.params[kParamDone] != 0.0) return;
+  const int t = threadIdx.x, q = t & (TG - 1);
+  const int item = blockIdx.x * (256 / TG) + t / TG;
+  if (item >= a.n_items) return;   // whole 16-lane groups leave together
+  const double alpha = a.params[0], lik_const = a.params[1];
+  const int vmi = (int)a.params[2];
+  const double vconv = params_vconv(a.params);
+  const int K = a.K;
+  const int d = a.order[item];
+  if (d < 0) return;
+  const int s0 = a.doc_ptr[d], n = a.doc_ptr[d + 1] - s0;
+  if (n <= 0) return;              // (the planner never sends an empty document)
+  const int U = a.gs_updates;
+  const int W = (n + U - 1) / U;
+  const int nch = (n + W - 1) / W;
+  const int* __restrict__ wrow = a.word_idx + s0;
+  const float* __restrict__ crow = a.counts + s0;
+  double* __restrict__ rows = a.cphi + (size_t)s0 * KS;
+  // chunk count sums: C_j = cs_j / K into row j W (integer counts: the sums are exact in any order)
+  double total = 0.0;
+  for (int j = 0; j < nch; ++j) {
+    const int n0 = j * W, n1 = min(n, n0 + W);
+    double cs;
+    if (W == 1) {
+      cs = (double)crow[n0];
+    } else {
+      cs = 0.0;
+      for (int p = n0 + q; p < n1; p += TG) cs += (double)crow[p];
+      cs = bits_sum<0, 4, false>(cs);
+    }
+    total += cs;
+#pragma unroll
+    for (int i = 0; i < KPL; ++i) {
+      const int k = q + TG * i;
+      if (k < KS) rows[(size_t)n0 * KS + k] = k < K ? cs / K : 0.0;
+    }
+  }
+  const double g0 = alpha + total / K;
+  const double m = psi_only(g0);
+  double gam[KPL], psi[KPL], E[KPL], Cn[KPL];
+#pragma unroll
+  for (int i = 0; i < KPL; ++i) {
+    const int k = q + TG * i;
+    gam[i] = k < K ? g0 : 0.0;
+    psi[i] = m;
+    E[i] = k < K ? 1.0 : 0.0;
+    Cn[i] = k < KS ? rows[k] : 0.0;   // C_0 (this lane's own stores above)
+  }
+  // head of a chunk: its first RQ words (past the chunk's end: count 0, the chunk's last row again)
+  int wn[RQ];
+  float cn[RQ];
+  double bq[RQ][KPL], cq[RQ];
+  auto head_ids = [&](int j) {
+    const int n0 = j * W, n1 = min(n, n0 + W);
+#pragma unroll
+    for (int r = 0; r < RQ; ++r) {
+      const int pc = min(n0 + r, n1 - 1);
+      wn[r] = wrow[pc];
+      cn[r] = n0 + r < n1 ? crow[pc] : 0.0f;
+    }
+  };
+  auto head_rows = [&]() {
+#pragma unroll
+    for (int r = 0; r < RQ; ++r) {
+      const double* brow = a.beta + (size_t)wn[r] * KS + q;
+      cq[r] = (double)cn[r];
+#pragma unroll
+      for (int i = 0; i < KPL; ++i) bq[r][i] = brow[TG * i];
+    }
+  };
+  head_ids(0);
+  head_rows();
+  head_ids(nch > 1 ? 1 : 0);
+  double L = 0.0, L_old = 0.0, conv = 1.0, GS = 0.0;
+  int it = 0;
+  while (var_continue(conv, vconv, it, vmi)) {
+    ++it;
+    double lw = 0.0, lp = 0.0;   // lp: sum of psi_k nw_jk over this lane's topics and the chunks
+    for (int j = 0; j < nch; ++j) {
+      const int n0 = j * W, n1 = min(n, n0 + W);
+      double acc[KPL];
+#pragma unroll
+      for (int i = 0; i < KPL; ++i) acc[i] = 0.0;
+      quad_word_steps<RQ, KPL>(E, bq, cq, acc, lw);
+      // the rest of the chunk: batches of RQ rows, a batch's loads in flight together
+      for (int p0 = n0 + RQ; p0 < n1; p0 += RQ) {
+        double c[RQ];
+#pragma unroll
+        for (int r = 0; r < RQ; ++r) {
+          const int pc = min(p0 + r, n1 - 1);
+          const double* brow = a.beta + (size_t)wrow[pc] * KS + q;
+          c[r] = p0 + r < n1 ? (double)crow[pc] : 0.0;
+#pragma unroll
+          for (int i = 0; i < KPL; ++i) bq[r][i] = brow[TG * i];
+        }
+        quad_word_steps<RQ, KPL>(E, bq, c, acc, lw);
+      }
+      // next chunk's head rows in flight during the refresh; ids of the one after
+      const int j1 = j + 1 < nch ? j + 1 : 0;
+      head_rows();
+      head_ids(j1 + 1 < nch ? j1 + 1 : 0);
+      const bool two = n1 - n0 >= 2;
+      // this chunk's C_j (and E_j) rows; lanes past KS exist only in the last topic group (static test)
+#pragma unroll
+      for (int i = 0; i < KPL; ++i) {
+        const int k = q + TG * i;
+        if (TG * (i + 1) <= KS || k < KS) {
+          rows[(size_t)n0 * KS + k] = E[i] * acc[i];
+          if (two) rows[(size_t)(n0 + 1) * KS + k] = E[i];
+        }
+      }
+      // the refresh without branches: a topic-guarded psi_exp is a basic block of its own, so the KPL
+      // chains would run one after another instead of interleaved (padding topics compute psi_exp(1) and
+      // keep psi = m, E = 0, gamma = 0: nw = 0 there)
+#pragma unroll
+      for (int i = 0; i < KPL; ++i) {
+        const bool real = q + TG * i < K;
+        const double nw = E[i] * acc[i];
+        lp = fma(psi[i], nw, lp);
+        gam[i] += nw - Cn[i];
+        double p, e;
+        psi_exp(real ? gam[i] : 1.0, m, p, e);
+        psi[i] = real ? p : psi[i];
+        E[i] = real ? e : 0.0;
+      }
+      // C of the next chunk, after this chunk's row stores (nch == 1: the same row)
+#pragma unroll
+      for (int i = 0; i < KPL; ++i) {
+        const int k = q + TG * i;
+        Cn[i] = (TG * (i + 1) <= KS || k < KS) ? rows[(size_t)j1 * W * KS + k] : 0.0;
+      }
+    }
+    double gs = 0.0, lg = 0.0;
+#pragma unroll
+    for (int i = 0; i < KPL; ++i) {
+      const bool real = q + TG * i < K;
+      const double l = lgamma_pos(real ? gam[i] : 1.0);
+      gs += real ? gam[i] : 0.0;
+      lg += real ? l : 0.0;
+    }
+    GS = bits_sum<0, 4, false>(gs);
+    lg = bits_sum<0, 4, false>(lg);
+    lp = bits_sum<0, 4, false>(lp);
+    L = lik_const - lgamma_pos(GS) + lg + fma(m, total, lw) - lp;
+    conv = (L_old - L) / L_old;
+    L_old = L;
+  }
+  double ps = 0.0;
+#pragma unroll
+  for (int i = 0; i < KPL; ++i) {
+    const int k = q + TG * i;
+    if (k < K) ps += psi[i];
+    if (k < KS) a.gamma[(size_t)d * KS + k] = gam[i];
+  }
+  ps = bits_sum<0, 4, false>(ps);
+  if (q == 0) {
+    a.lik[d] = L;
+    a.alpha_ss[d] = ps - K * psi_only(GS);
+    a.iters[d] = it;
+  }
+  // final pass over chunks of >= 2 words: c_n phi_nk = E_jk b_nk r_n with the final sweep's chunk E
+  // (read from row j W + 1 before the chunk's rows are overwritten; the same lane's addresses only)
+  if (W < 2) return;
+  for (int j = 0; j < nch; ++j) {
+    const int n0 = j * W, n1 = min(n, n0 + W);
+    if (n1 - n0 < 2) continue;
+    double Ej[KPL];
+#pragma unroll
+    for (int i = 0; i < KPL; ++i) {
+      const int k = q + TG * i;
+      Ej[i] = k < KS ? rows[(size_t)(n0 + 1) * KS + k] : 0.0;
+    }
+    for (int p0 = n0; p0 < n1; p0 += RQ) {
+      double b[RQ][KPL], c[RQ];
+#pragma unroll
+      for (int r = 0; r < RQ; ++r) {
+        const int pc = min(p0 + r, n1 - 1);
+        const double* brow = a.beta + (size_t)wrow[pc] * KS + q;
+        c[r] = (double)crow[pc];
+#pragma unroll
+        for (int i = 0; i < KPL; ++i) b[r][i] = brow[TG * i];
+      }
+#pragma unroll
+      for (int r = 0; r < RQ; ++r) {
+        if (p0 + r >= n1) break;
+        double pp0 = 0.0, pp1 = 0.0;
+#pragma unroll
+        for (int i = 0; i < KPL; i += 2) pp0 = fma(Ej[i], b[r][i], pp0);
+#pragma unroll
+        for (int i = 1; i < KPL; i += 2) pp1 = fma(Ej[i], b[r][i], pp1);
+        const double rr = c[r] * drcp(bits_sum<0, 4, false>(pp0 + pp1));
+        double* row = rows + (size_t)(p0 + r) * KS;
+#pragma unroll
+        for (int i = 0; i < KPL; ++i) {
+          const int k = q + TG * i;
+          if (k < KS) __builtin_nontemporal_store(Ej[i] * b[r][i] * rr, &row[k]);
+        }
+      }
     }
   }
 }
@@ -658,38 +908,44 @@ __global__ __launch_bounds__(team_threads(KS, NW), MINW) void gs_team(GSArgs a) 
       }
       team_sync<NW>();
       tick(2);
+      // gather, then a branch-free refresh (TO > 1: the chains of a thread interleave; a topic-guarded
+      // psi_exp is a basic block of its own), then the table stores.  Padding topics: Eo = 0, nw = 0,
+      // gamma = 0, psi = m, E = 0.
+      double nwv[TO], Eov[TO], Env[TO];
+#pragma unroll
+      for (int o = 0; o < TO; ++o) {
+        const int k = t + NTD * o;
+        const int kc = k < KS ? k : KS - 1;
+        // all NW loads issued together (a dynamic loop serialises LDS round trips)
+        double S = 0.0;
+#pragma unroll
+        for (int v = 0; v < NW; ++v) S += v < nact ? sRed[ds][v][kc] : 0.0;
+        Eov[o] = k < KS ? E_[kc] : 0.0;
+        nwv[o] = Eov[o] * S;
+        const double Cj = GM ? Cn[o] : C[j][kc];
+        const bool real = k < K;
+        lps[o] = fma(psi[o], nwv[o], lps[o]);
+        gam[o] = real ? gam[o] + (nwv[o] - Cj) : gam[o];
+        double pn, en;
+        psi_exp(real ? gam[o] : 1.0, m, pn, en);
+        psi[o] = real ? pn : psi[o];
+        Env[o] = real ? en : 0.0;
+      }
 #pragma unroll
       for (int o = 0; o < TO; ++o) {
         const int k = t + NTD * o;
         if (k < KS) {
-          // all NW loads issued together (a dynamic loop serialises LDS round trips)
-          double S = 0.0;
-#pragma unroll
-          for (int v = 0; v < NW; ++v) S += v < nact ? sRed[ds][v][k] : 0.0;
-          const double Eo = E_[k];
-          const double nw = Eo * S;
-          double En = 0.0;
           if constexpr (GM) {
-            if (k < K) {
-              lps[o] = fma(psi[o], nw, lps[o]);
-              gam[o] += nw - Cn[o];
-              psi_exp(gam[o], m, psi[o], En);
-            }
             double* crw = a.cphi + (size_t)(s0 + j * W) * KS;
-            crw[k] = nw;
-            if (min(n, (j + 1) * W) - j * W >= 2) crw[KS + k] = Eo;
+            crw[k] = nwv[o];
+            if (min(n, (j + 1) * W) - j * W >= 2) crw[KS + k] = Eov[o];
             const int j1 = j + 1 < nch ? j + 1 : 0;
             Cn[o] = a.cphi[(size_t)(s0 + j1 * W) * KS + k];
           } else {
-            if (k < K) {
-              lps[o] = fma(psi[o], nw, lps[o]);
-              gam[o] += nw - C[j][k];
-              psi_exp(gam[o], m, psi[o], En);
-            }
-            C[j][k] = nw;
-            Et[j][k] = Eo;
+            C[j][k] = nwv[o];
+            Et[j][k] = Eov[o];
           }
-          E_[k] = En;
+          E_[k] = Env[o];
         }
       }
       tick(3);
@@ -833,43 +1089,53 @@ __device__ __forceinline__ void put_tagged_bits(unsigned long long* p, unsigned 
                      __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// sum_{q < n} of the double at granules (x[q * stride], x[q * stride + 1]) = (lo, hi) bits,
-// in order q = 0, 1, ...; 4 segments (8 granules) in flight per round trip.  Granules that do not
-// carry `tag` yet are re-polled TOGETHER (one round trip per poll, not one per stale granule).
-// False on a timeout.
-__device__ __forceinline__ bool tagged_sum_f64(const unsigned long long* x, int n, int stride, unsigned tag,
-                                               double& out) {
-  double s = 0.0;
+// Segment-order sums of the tagged doubles of TC columns (column c: granules x[u * stride + 2 c] and
+// x[u * stride + 2 c + 1] = (lo, hi) bits of segment u's value, u < G <= GMX).  Every pass issues ALL
+// TC x GMX x 2 loads back to back (unconditional, clamped indices) and then checks the tags; a pass that
+// finds any stale granule is repeated whole.  Loads inside per-granule branches get a vmcnt(0) each -- one
+// round trip per granule group; the round-3 form polled 4 segments per round trip, 2 x 4 serial round
+// trips per chunk at G = 16, K = 100 (12.8 k cycles per chunk, profiles/r5f) -- and the microbenchmark
+// (scripts/micro/xcd_exchange.hip) measured batched polls at half the per-granule form.  False on a timeout.
+constexpr int kSplitMaxSeg = 16;   // GMX: segments per document (GSSplitPlan caps G)
+template <int TC, int GMX, int NC>
+__device__ __forceinline__ bool tagged_gather(const unsigned long long* x, int G, int stride, int lane, unsigned tag,
+                                              double (&out)[TC]) {
+  unsigned long long v[TC][GMX][2];
   long spins = 0;
-  for (int q0 = 0; q0 < n; q0 += 4) {
-    unsigned long long v[8];
+  for (;;) {
 #pragma unroll
-    for (int u = 0; u < 8; ++u)
-      v[u] = __hip_atomic_load(x + (size_t)min(q0 + u / 2, n - 1) * stride + (u & 1), __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
-    for (;;) {
-      unsigned pending = 0;
+    for (int o = 0; o < TC; ++o) {
+      const int c = min(lane + 64 * o, NC - 1);
 #pragma unroll
-      for (int u = 0; u < 8; ++u)
-        pending |= (q0 + u / 2 < n && (unsigned)(v[u] >> 32) != tag) ? (1u << u) : 0u;
-      if (pending == 0) break;
-      if (++spins > kSplitSpinLimit) {
-        out = __builtin_nan("");
-        return false;
+      for (int u = 0; u < GMX; ++u) {
+        const unsigned long long* p = x + (size_t)min(u, G - 1) * stride + 2 * c;
+        v[o][u][0] = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        v[o][u][1] = __hip_atomic_load(p + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
-      __builtin_amdgcn_s_sleep(1);
-#pragma unroll
-      for (int u = 0; u < 8; ++u)
-        if ((pending >> u) & 1u)
-          v[u] = __hip_atomic_load(x + (size_t)(q0 + u / 2) * stride + (u & 1), __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
     }
+    bool ok = true;
 #pragma unroll
-    for (int u = 0; u < 8; u += 2)
-      if (q0 + u / 2 < n)
-        s += __longlong_as_double((long long)(((v[u + 1] & 0xffffffffull) << 32) | (v[u] & 0xffffffffull)));
+    for (int o = 0; o < TC; ++o)
+#pragma unroll
+      for (int u = 0; u < GMX; ++u)
+        ok &= u >= G || ((unsigned)(v[o][u][0] >> 32) == tag && (unsigned)(v[o][u][1] >> 32) == tag);
+    if (ok) break;
+    if (++spins > kSplitSpinLimit) {
+#pragma unroll
+      for (int o = 0; o < TC; ++o) out[o] = __builtin_nan("");
+      return false;
+    }
+    __builtin_amdgcn_s_sleep(1);
   }
-  out = s;
+#pragma unroll
+  for (int o = 0; o < TC; ++o) {
+    double s = 0.0;
+#pragma unroll
+    for (int u = 0; u < GMX; ++u)
+      if (u < G)
+        s += __longlong_as_double((long long)(((v[o][u][1] & 0xffffffffull) << 32) | (v[o][u][0] & 0xffffffffull)));
+    out[o] = s;
+  }
   return true;
 }
 
@@ -1025,33 +1291,49 @@ __global__ __launch_bounds__(512) void gs_splitw(GSArgs a, SplitArgs sp) {
             put_tagged_bits(row + 1, (unsigned)(bits >> 32), tag);
           }
         }
+        // one batched pass over every column and segment up to 8 segments; past that a pass per column
+        // (TC x 16 x 2 granules in flight spilled at K = 100)
         double tot[TC];
+        const unsigned long long* xs = xb + (size_t)base * GR;
         bool ok = true;
+        if (G <= 4) {
+          ok = tagged_gather<TC, 4, NC>(xs, G, GR, lane, tag, tot);
+        } else if (G <= 8) {
+          ok = tagged_gather<TC, 8, NC>(xs, G, GR, lane, tag, tot);
+        } else {
 #pragma unroll
-        for (int o = 0; o < TC; ++o) {
-          const int c = lane + 64 * o;
-          tot[o] = 0.0;
-          if (c < NC) ok &= tagged_sum_f64(xb + (size_t)base * GR + 2 * c, G, GR, tag, tot[o]);
+          for (int o = 0; o < TC; ++o) {
+            double t1[1];
+            ok &= tagged_gather<1, kSplitMaxSeg, NC>(xs, G, GR, lane + 64 * o, tag, t1);
+            tot[o] = t1[0];
+          }
         }
         tick(4);
         if (!ok) {
           sFail = 1;
           __hip_atomic_store(sp.error, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
+        // branch-free refresh: the TC chains of a lane interleave (padding / log-sum columns have
+        // Eo = 0: nw = 0, and keep gamma = 0, psi = m, E = 0)
+        double En[TC];
+#pragma unroll
+        for (int o = 0; o < TC; ++o) {
+          const bool real = lane + 64 * o < K;
+          const double nw = Eo[o] * tot[o];
+          lps[o] = fma(psi[o], nw, lps[o]);
+          gam[o] = real ? fma(Eo[o], tot[o], gC[o]) : gam[o];   // gamma_k + (new_jk - C_jk) in one rounding
+          double pn, en;
+          psi_exp(real ? gam[o] : 1.0, m, pn, en);
+          psi[o] = real ? pn : psi[o];
+          En[o] = real ? en : 0.0;
+        }
 #pragma unroll
         for (int o = 0; o < TC; ++o) {
           const int k = lane + 64 * o;
           if (k < KS) {
-            const double nw = Eo[o] * tot[o];
-            double En = 0.0;
-            if (k < K) {
-              lps[o] = fma(psi[o], nw, lps[o]);
-              gam[o] = fma(Eo[o], tot[o], gC[o]);   // gamma_k + (new_jk - C_jk) in one rounding
-              psi_exp(gam[o], m, psi[o], En);
-            }
-            sC[j][k] = nw;
+            sC[j][k] = Eo[o] * tot[o];
             sEt[j][k] = Eo[o];
-            sE[k] = En;
+            sE[k] = En[o];
           } else if (k == KS) {
             LWs += tot[o];
           }
@@ -2121,12 +2403,11 @@ static void gs_estep_ks(const GSArgs& a, int variant, hipStream_t s) {
       break;
     }
     case kGsSmall: {
-      if constexpr (KS <= 32) {
+      if constexpr (KS <= 32)
         hipLaunchKernelGGL((gs::gs_small<KS>), dim3((a.n_items + 15) / 16), dim3(256), 0, s, a);
-        break;
-      } else {
-        throw std::runtime_error("gs_estep: the small-document kernel needs KS <= 32");
-      }
+      else
+        hipLaunchKernelGGL((gs::gs_smallw<KS, 2, 2>), dim3((a.n_items + 15) / 16), dim3(256), 0, s, a);
+      break;
     }
     case kGsTeam1: {
       // one wave per document (<= 256 words, chunks of <= 8 words): the topic-group layout keeps

@@ -319,7 +319,8 @@ class LDAEngine:
             for w in self._cwin:
                 w["gp"] = H.GSPlan(self.dc.doc_len, KS, self._U, dev, doc_range=(w["d0"], w["d1"]))
             rows = max(w["e1"] - w["e0"] for w in self._cwin)
-        self.beta = torch.zeros(V, KS, dtype=f64, device=dev)
+        # one zero pad row past the vocabulary: gs_smallw's constant-offset row loads may read past row V - 1
+        self.beta = torch.zeros(V + 1, KS, dtype=f64, device=dev)[:V]
         self._stages = self._build_stages(corpus, KS)
         self.cw = torch.zeros(V, KS, dtype=f64, device=dev)
         self.gamma = torch.zeros(D, KS, dtype=f64, device=dev)

@@ -423,6 +423,9 @@ def gs_estep(doc_ptr, word_idx, counts, order, beta, K, gs_updates, params, gamm
         0 if stage is None else _chk(stage.buf, torch.float64, "stage", None, dev),
         0 if stage is None else _chk(stage.stage_off, torch.int64, "stage_off", (order.numel(),), dev),
     ]
+    if variant == GS_SMALL and KS > 32 and \
+            beta.untyped_storage().nbytes() < (beta.storage_offset() + (V + 1) * KS) * 8:
+        raise ValueError("gs_smallw reads up to one row past beta: allocate a zero pad row ([V + 1, KS] storage)")
     if stage is not None and (variant != GS_TEAM8 or KS != stage.KS):
         raise ValueError("staged rows: kGsTeam8 launches of the stage's KS only")
     if order.numel() == 0:
@@ -544,6 +547,9 @@ def gs_split_launch_cap(KS: int) -> int:
     return cap
 
 
+SPLIT_MAX_SEG = 16   # csrc/hip/lda_gs64.hip kSplitMaxSeg
+
+
 def gs_team8_words(KS: int) -> int:
     """Words of a chunk one 8-wave fp64 workgroup holds in its prefetched rounds (TeamShape<KS, 8>:
     slots x RMAX); the split kernel sizes segments to this."""
@@ -567,7 +573,8 @@ class GSSplitPlan:
         self.max_blocks = gs_split_launch_cap(KS)
         sp = split_spec(KS)
         self.seg_words = int(seg_words) or sp["words"] or min(128, gs_team8_words(KS))
-        max_seg = min(int(max_seg) or sp["g"], self.max_blocks)
+        # the kernel's exchange polls at most SPLIT_MAX_SEG segments per document (lda_gs64.hip kSplitMaxSeg)
+        max_seg = min(int(max_seg) or sp["g"], self.max_blocks, SPLIT_MAX_SEG)
         max_batches = int(max_batches) or sp["batches"]
         U = int(gs_updates)
         self.segments = {}
@@ -601,6 +608,8 @@ class GSSplitPlan:
                 sd.append(d), si.append(q), sc.append(G), sb.append(base), slot.append(j)
         t = lambda a: torch.tensor(np.asarray(a, np.int32), device=device)
         nb = len(sd)
+        if sc and max(sc) > SPLIT_MAX_SEG:
+            raise ValueError(f"gs_split: {max(sc)} segments per document > {SPLIT_MAX_SEG}")
         return dict(seg_doc=t(sd), seg_index=t(si), seg_count=t(sc), seg_base=t(sb), doc_slot=t(slot), n_blocks=nb,
                     # tagged granules {uint32 half of a double, uint32 tag}: [2][n_blocks][2 (KS + 1)]
                     xchg=torch.zeros(2 * nb * 2 * (self.KS + 1), dtype=torch.int64, device=device),
@@ -745,9 +754,10 @@ def gs_xsplit(doc_ptr, word_idx, counts, beta, K, gs_updates, params, gamma, cph
 class GSPlan:
     """Length buckets of the fp64 block Gauss-Seidel E-step: (variant, int32 doc order) per launch.
 
-    tiny (TG lanes per document, literal schedule) for n <= min(gs_tiny_max(KS), U); one wave per
-    document up to 256 words; a 4-wave workgroup up to 2048; an 8-wave workgroup beyond."""
-    EDGES = ((GS_TEAM8, 2048, None), (GS_TEAM4, 256, 2048), (GS_TEAM1, None, 256))
+    tiny (TG lanes per document, literal schedule) for n <= min(gs_tiny_max(KS), U); up to 256 words
+    one wave per document at KS <= 32, 16 lanes per document at KS > 32 (gs_smallw); a 4-wave workgroup
+    up to 2048; an 8-wave workgroup beyond."""
+    EDGES = ((GS_TEAM8, 2048, None), (GS_TEAM4, 256, 2048), (GS_SMALL, None, 256))
     # KS <= 32: documents up to GS_SMALL_MAX words go to the 16-lanes-per-document kernel
     EDGES_NARROW = ((GS_TEAM8, 2048, None), (GS_TEAM4, 256, 2048), (GS_TEAM1, GS_SMALL_MAX, 256),
                     (GS_SMALL, None, GS_SMALL_MAX))
@@ -828,12 +838,15 @@ class GSPlan:
         split a chunk's W = ceil(n / U) words, so at lda-c's per-word schedule (U = 1024: W = 1 for every
         document up to 1,024 words) a 4- or 8-wave team idles all but one word slot and pays two
         workgroup barriers per word, where one wave per document refreshes in-wave with no barrier.
-        One wave up to W = 2, four up to W = 16, eight beyond (never below the U = 32 edges).  K = 100 shard
-        at U = 1024 (profiles/r4_tuning_log.md): fixed length edges 172.4 ms per EM iteration, (8, 64) 133.2,
-        (4, 32) 107.3, (2, 16) 106.7."""
+        One wave per document up to W = 2, four up to W = 16, eight beyond (never below the U = 32 edges).
+        K = 100 shard at U = 1024 (profiles/r4_tuning_log.md): fixed length edges 172.4 ms per EM iteration,
+        (8, 64) 133.2, (4, 32) 107.3, (2, 16) 106.7.  Documents of <= 256 words keep the 16-lane kernel
+        (gs_smallw: throughput); above, the one-wave range is a per-word chain of up to U refreshes per sweep,
+        where the 16-lane kernel's 7 digamma/exp chains per lane cost more latency per refresh than one wave's
+        2 (r5g: the bucket 66.4 ms on 16 lanes per document vs 43.1 ms on one wave)."""
         w1, w4 = 2, 16
         e1, e4 = max(256, w1 * U), max(2048, w4 * U)
-        return ((GS_TEAM8, e4, None), (GS_TEAM4, e1, e4), (GS_TEAM1, None, e1))
+        return ((GS_TEAM8, e4, None), (GS_TEAM4, e1, e4), (GS_TEAM1, 256, e1), (GS_SMALL, None, 256))
 
     @staticmethod
     def isolate_longest(o, m: int, xcds: int = 8):

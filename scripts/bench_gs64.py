@@ -106,8 +106,9 @@ def main():
                 d0 = int(b0["seg_doc"][0].item())
             if not b0.get("x"):
                 out["buckets"][-1]["phase_cycles_per_chunk"] = dict(
-                word=round(v[0] / ch), barrier1=round(v[1] / ch), exchange=round(v[2] / ch),
-                barrier2=round(v[3] / ch), refresh=round(v[4] / ch), barrier3=round(v[5] / ch),
+                # gs_splitw tick indices: word waves 0-2, topic wave 3-6 (lda_gs64.hip)
+                word=round(v[0] / ch), word_prefetch_issue=round(v[1] / ch), word_barrier_b=round(v[2] / ch),
+                topic_wait_arrivals=round(v[3] / ch), exchange=round(v[4] / ch), refresh=round(v[5] / ch),
                 sweep_end_total=v[6], chunks=v[7], doc_len=int(lens[d0]),
                 segments=int(b0["seg_count"][0].item()))
         print(json.dumps(out["buckets"][-1]), flush=True)

@@ -261,6 +261,9 @@ def test_staged_rows_bitwise_equal_beta_rows(monkeypatch):
     (52, {"ONI_GS_SPLIT_MIN": "2500"}, 32),
     (50, {}, 64),                                                       # 64-row LDS tables (KS 52, U = 64)
     (50, {"ONI_GS_SPLIT_MIN": "2500,g=3"}, 48),
+    # 16 / 6-8 / 2-4 segments: the exchange's per-column, 8- and 4-segment batched polls
+    (100, {"ONI_GS_SPLIT_MIN": "2500,g=16,words=16"}, 32),
+    (20, {"ONI_GS_SPLIT_MIN": "2500,g=12,words=24"}, 32),
 ])
 def test_split_documents_match_oracle(K, env, U, monkeypatch):
     """gs_split (one document over G workgroups exchanging tagged per-chunk partials) against the
@@ -283,6 +286,9 @@ def test_split_documents_match_oracle(K, env, U, monkeypatch):
     sp = eng.gs_plan.split
     assert sp is not None and sp.n_docs >= (4 if "ONI_GS_SPLIT_MIN" in env else 2)
     assert max(sp.segments.values()) >= 2
+    if "words=" in env.get("ONI_GS_SPLIT_MIN", ""):
+        G = sorted(sp.segments.values())
+        assert G[-1] > 8 and any(4 < g <= 8 for g in G), G
     if "ONI_SPLIT_MAX_BLOCKS" in env:
         assert len(sp.batches) >= 2
     assert int(sum(b["error"].item() for b in sp.batches)) == 0
