@@ -34,6 +34,7 @@ struct SplitArgs {
                           // match), exit count (the last segment out bumps the epoch, resets the count)
   int n_docs;             // documents in this launch
   int* error;             // set to 1 if a wait times out (never hangs the GPU)
+  double* tab = nullptr;  // U > the LDS table rows (KS > 32): per-segment chunk tables [n_blocks][U][2][KS]
 };
 
 // Sufficient-statistic launches: workgroups for [heavy | medium | light] word lists
@@ -125,7 +126,8 @@ void launch_gs_stage(const double* beta, const int* word_idx, const int* tile_en
                      double* stage, int KS, const double* gate, hipStream_t s);   // gate: as gs_mstep
 int gs_tiny_max(int KS);   // longest document of the kGsTiny kernel
 int gs_umax(int KS);       // largest gs_updates the E-step accepts at row stride KS
-int gs_split_umax(int KS); // largest gs_updates of the split kernel (64 at KS <= 52, else kGsUMax)
+int gs_split_umax(int KS); // largest gs_updates of the split kernel (KS > 32: kGsUMaxWide, else 32 / 64)
+int gs_split_lds_umax(int KS);   // largest gs_updates with the chunk tables in LDS (64 at KS <= 52, else 32)
 // One long document over s.seg_count[b] workgroups (8 waves each): every chunk is cut into
 // that many word ranges whose partials are exchanged as tagged granules (2 per double,
 // s.xchg = [2][n_blocks][2 (KS + 1)]); s.seg_words is unused.  Every segment of a launch

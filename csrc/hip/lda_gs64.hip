@@ -680,9 +680,9 @@ __device__ __forceinline__ void stream_batch(const double* __restrict__ beta, co
   }
 #pragma unroll
   for (int r = 0; r < RMAX; ++r) {
-    const double* brow = beta + (size_t)w[r] * KS;
+    const double* brow = beta + (size_t)w[r] * KS + q;   // constant offsets (beta's pad row: gs_smallw)
 #pragma unroll
-    for (int i = 0; i < KPL; ++i) b[r][i] = brow[min(q + TG * i, KS - 1)];
+    for (int i = 0; i < KPL; ++i) b[r][i] = brow[TG * i];
   }
   word_steps<RMAX, KPL, LSW>(E, b, c, acc, lw);
 }
@@ -835,9 +835,9 @@ __global__ __launch_bounds__(team_threads(KS, NW), MINW) void gs_team(GSArgs a) 
     if (!active) return;   // wave-uniform: waves without words of a chunk gather no rows
 #pragma unroll
     for (int r = 0; r < RMAX; ++r) {
-      const double* brow = a.beta + (size_t)w[r] * KS;
+      const double* brow = a.beta + (size_t)w[r] * KS + q;   // constant offsets (beta's pad row: gs_smallw)
 #pragma unroll
-      for (int i = 0; i < KPL; ++i) bc[r][i] = brow[min(q + TG * i, KS - 1)];
+      for (int i = 0; i < KPL; ++i) bc[r][i] = brow[TG * i];
     }
   };
   if (nch > 0) {
@@ -1149,8 +1149,10 @@ __device__ __forceinline__ bool tagged_gather(const unsigned long long* x, int G
 // per chunk was 3.82 vs 3.17 ms on the K = 50 split bucket and is gone; profiles/r3_tuning_log.md.)
 // UM: chunk-table rows in LDS (U <= UM): 32, or 64 where 2 x 64 x KS doubles still fit the 64 KB of
 // static LDS (KS <= 52: K = 50 at U = 64, the schedule that meets lda-c parity there,
-// profiles/r3_precision_parity.md)
-template <int KS, int UM = kGsUMax>
+// profiles/r3_precision_parity.md).  GM (U > UM at KS > 32, lda-c's per-word schedule): the chunk tables
+// move to the launch's per-segment scratch sp.tab ([n_blocks][U][C_j | E_j][KS]; each replica reads only
+// what it wrote itself) and C_j is loaded one chunk ahead, as gs_team's c*phi-row layout does.
+template <int KS, int UM = kGsUMax, bool GM = false>
 __global__ __launch_bounds__(512) void gs_splitw(GSArgs a, SplitArgs sp) {
   using T = TeamShape<KS, 8>;   // word-slot geometry and prefetch depth of the 8-wave team
   constexpr int NW = 7, NTD = (NW + 1) * 64, TG = T::TG, KPL = T::KPL, NSW = T::NSW, LSW = T::LSW, NS = NW * NSW,
@@ -1158,12 +1160,13 @@ __global__ __launch_bounds__(512) void gs_splitw(GSArgs a, SplitArgs sp) {
   constexpr int NC = KS + 1;                 // exchanged columns: KS topic sums + the log-sum
   constexpr int GR = 2 * NC;                 // granules per segment row
   constexpr int TC = (NC + 63) / 64;         // columns per topic-wave lane
-  __shared__ double sC[UM][KS];
-  __shared__ double sEt[UM][KS];
+  constexpr int UT = GM ? 1 : UM;             // LDS chunk-table rows
+  __shared__ double sC[UT][KS];
+  __shared__ double sEt[UT][KS];
   __shared__ double sE[KS];
   __shared__ double sRed[NW][KS];
   __shared__ double sRedL[NW];
-  __shared__ double sCs[UM];
+  __shared__ double sCs[GM ? kGsUMaxWide : UM];
   __shared__ double sScal[4];
   __shared__ int arrive[NW];   // per word wave: chunks whose partial sums it has left in sRed / sRedL
   __shared__ int sFail;
@@ -1176,6 +1179,7 @@ __global__ __launch_bounds__(512) void gs_splitw(GSArgs a, SplitArgs sp) {
   const int vmi = (int)a.params[2];
   const double vconv = params_vconv(a.params);
   const int K = a.K;
+  auto kc_ = [](int k) { return k < KS ? k : KS - 1; };   // an in-bounds LDS column for guarded reads
   const int lane = t & 63, wv = t >> 6;
   const bool topic_wave = wv == NW;
   const int q = lane >> LSW, sl = lane & (NSW - 1);
@@ -1189,6 +1193,7 @@ __global__ __launch_bounds__(512) void gs_splitw(GSArgs a, SplitArgs sp) {
   const bool active = wv < nact;              // never the topic wave
   const int* __restrict__ wrow = a.word_idx + s0;
   const float* __restrict__ crow = a.counts + s0;
+  double* __restrict__ tab = GM ? sp.tab + (size_t)b * U * 2 * KS : nullptr;   // row j: C_j, then E_j
   auto range = [&](int j, int& m0, int& m1) {
     const int n1 = min(n, (j + 1) * W);
     m0 = min(n1, j * W + g * WG);
@@ -1229,16 +1234,24 @@ __global__ __launch_bounds__(512) void gs_splitw(GSArgs a, SplitArgs sp) {
   if (topic_wave) {
     // ------------------------------------------------------------ topic wave
     __builtin_amdgcn_s_setprio(3);   // its chain is the critical path; the word waves wait on it
-    double gam[TC], psi[TC], lps[TC];
+    double gam[TC], psi[TC], lps[TC], Cn[TC];
 #pragma unroll
     for (int o = 0; o < TC; ++o) {
       const int k = lane + 64 * o;
       gam[o] = k < K ? g0 : 0.0;
       psi[o] = m;
       lps[o] = 0.0;
+      Cn[o] = 0.0;
       if (k < KS) {
         sE[k] = k < K ? 1.0 : 0.0;
-        for (int j = 0; j < nch; ++j) sC[j][k] = k < K ? sCs[j] / K : 0.0;
+        for (int j = 0; j < nch; ++j) {
+          const double c0 = k < K ? sCs[j] / K : 0.0;
+          if constexpr (GM)
+            tab[(size_t)j * 2 * KS + k] = c0;
+          else
+            sC[j][k] = c0;
+        }
+        if constexpr (GM) Cn[o] = tab[k];   // C_0 (this lane's own store)
       }
     }
     double LWs = 0.0;
@@ -1256,7 +1269,7 @@ __global__ __launch_bounds__(512) void gs_splitw(GSArgs a, SplitArgs sp) {
 #pragma unroll
         for (int o = 0; o < TC; ++o) {
           const int k = lane + 64 * o;
-          gC[o] = k < KS ? gam[o] - sC[j][k] : 0.0;
+          gC[o] = k < KS ? gam[o] - (GM ? Cn[o] : sC[j][kc_(k)]) : 0.0;
           Eo[o] = k < KS ? sE[k] : 0.0;
         }
         // the segment's column sums, in wave order as the waves arrive (one add after the last)
@@ -1331,8 +1344,14 @@ __global__ __launch_bounds__(512) void gs_splitw(GSArgs a, SplitArgs sp) {
         for (int o = 0; o < TC; ++o) {
           const int k = lane + 64 * o;
           if (k < KS) {
-            sC[j][k] = Eo[o] * tot[o];
-            sEt[j][k] = Eo[o];
+            if constexpr (GM) {
+              tab[(size_t)j * 2 * KS + k] = Eo[o] * tot[o];
+              tab[(size_t)j * 2 * KS + KS + k] = Eo[o];
+              Cn[o] = tab[(size_t)(j + 1 < nch ? j + 1 : 0) * 2 * KS + k];   // after the store (nch == 1)
+            } else {
+              sC[j][k] = Eo[o] * tot[o];
+              sEt[j][k] = Eo[o];
+            }
             sE[k] = En[o];
           } else if (k == KS) {
             LWs += tot[o];
@@ -1368,6 +1387,7 @@ __global__ __launch_bounds__(512) void gs_splitw(GSArgs a, SplitArgs sp) {
       sweep_end();
       tick(6);
     }
+    if constexpr (GM) __syncthreads();   // pairs with the word waves': the E_j table stores before their final pass
     if (twt)
       for (int i = 3; i < 8; ++i) a.dbg[i] = ph[i];
     split_exit(counter, sp.n_docs, G);   // thread 0 only: a no-op here (kept beside the word waves' call)
@@ -1408,9 +1428,11 @@ __global__ __launch_bounds__(512) void gs_splitw(GSArgs a, SplitArgs sp) {
     if (!active) return;
 #pragma unroll
     for (int r = 0; r < RMAX; ++r) {
-      const double* brow = a.beta + (size_t)w[r] * KS;
+      // unconditional, constant offsets: a round past the range re-reads a valid row of the document
+      // and carries count 0 (beta's pad row covers topic lanes past KS: gs_smallw)
+      const double* brow = a.beta + (size_t)w[r] * KS + q;
 #pragma unroll
-      for (int i = 0; i < KPL; ++i) bc[r][i] = ((v >> r) & 1u) ? brow[min(q + TG * i, KS - 1)] : 0.0;
+      for (int i = 0; i < KPL; ++i) bc[r][i] = brow[TG * i];
     }
   };
   load_ids(0, wc, cc, vc);
@@ -1478,6 +1500,7 @@ __global__ __launch_bounds__(512) void gs_splitw(GSArgs a, SplitArgs sp) {
     if (failed) break;
     sweep_end();
   }
+  if constexpr (GM) __syncthreads();     // the topic wave's E_j table stores are visible past this
   if (wwt)
     for (int i = 0; i < 3; ++i) a.dbg[i] = ph[i];
   // every thread of this workgroup is past its last exchange (the loops end on a barrier)
@@ -1489,7 +1512,10 @@ __global__ __launch_bounds__(512) void gs_splitw(GSArgs a, SplitArgs sp) {
     range(j, m0, m1);
     double E[KPL];
 #pragma unroll
-    for (int i = 0; i < KPL; ++i) E[i] = (q + TG * i < KS) ? sEt[j][q + TG * i] : 0.0;
+    for (int i = 0; i < KPL; ++i) {
+      const int k = q + TG * i;
+      E[i] = k < KS ? (GM ? tab[(size_t)j * 2 * KS + KS + k] : sEt[j][kc_(k)]) : 0.0;
+    }
     for (int p = m0 + slot; p < m1; p += NS) {
       const double* brow = a.beta + (size_t)wrow[p] * KS;
       const double c = (double)crow[p];
@@ -1834,6 +1860,7 @@ __global__ __launch_bounds__((NW + 1) * 64) void gs_wsteam(GSArgs a) {
   const int vmi = (int)a.params[2];
   const double vconv = params_vconv(a.params);
   const int K = a.K;
+  auto kc_ = [](int k) { return k < KS ? k : KS - 1; };   // an in-bounds LDS column for guarded reads
   const int lane = t & 63, wv = t >> 6;
   const bool topic_wave = wv == NW;
   const int s0 = a.doc_ptr[d], n = a.doc_ptr[d + 1] - s0;
@@ -2511,9 +2538,9 @@ int gs_tiny_max(int KS) {
 }
 
 template <int KS>
-constexpr int split_umax_ks() { return KS <= 52 ? 64 : kGsUMax; }
+constexpr int split_umax_ks() { return KS <= 52 ? 64 : kGsUMax; }   // chunk tables in LDS
 
-int gs_split_umax(int KS) {
+int gs_split_lds_umax(int KS) {
   switch (KS) {
 #define ONI_KS(X) \
   case X:         \
@@ -2524,6 +2551,9 @@ int gs_split_umax(int KS) {
       return kGsUMax;
   }
 }
+
+// past the LDS tables, KS > 32 keeps its chunk tables in the launch's scratch (gs_splitw GM)
+int gs_split_umax(int KS) { return KS > 32 ? kGsUMaxWide : gs_split_lds_umax(KS); }
 
 template <int KS>
 static int gs_split_capacity_ks() {
@@ -2563,7 +2593,12 @@ void launch_gs_split(const GSArgs& a, const SplitArgs& s, int KS, hipStream_t st
   switch (KS) {
 #define ONI_KS(X)                                                                                          \
   case X:                                                                                                  \
-    if (a.gs_updates > kGsUMax) {                                                                          \
+    if (a.gs_updates > split_umax_ks<X>()) {                                                               \
+      if constexpr (X > 32) {                                                                              \
+        if (!s.tab) throw std::runtime_error("gs_split: U past the LDS chunk tables needs the tab scratch");   \
+        hipLaunchKernelGGL((gs::gs_splitw<X, kGsUMax, true>), dim3(s.n_blocks), dim3(512), 0, st, a, s);   \
+      }                                                                                                    \
+    } else if (a.gs_updates > kGsUMax) {                                                                   \
       if constexpr (split_umax_ks<X>() > kGsUMax)                                                          \
         hipLaunchKernelGGL((gs::gs_splitw<X, split_umax_ks<X>()>), dim3(s.n_blocks), dim3(512), 0, st, a, s); \
     } else                                                                                                 \

@@ -315,8 +315,14 @@ def gs_umax(KS: int = 0) -> int:
 
 
 def gs_split_umax(KS: int) -> int:
-    """Largest U of the split-document kernel: its chunk tables live in LDS (64 at KS <= 52, else 32)."""
+    """Largest U of the split-document kernel: 4096 at KS > 32 (chunk tables past the LDS ones in a
+    per-segment scratch, GSSplitPlan ``tab``), else its LDS tables' (64 at KS <= 52, else 32)."""
     return int(lib().gs_split_umax(int(KS)))
+
+
+def gs_split_lds_umax(KS: int) -> int:
+    """Largest U with the split kernel's chunk tables in LDS (64 at KS <= 52, else 32)."""
+    return int(lib().gs_split_lds_umax(int(KS)))
 
 
 def gs_tiny_max(KS: int) -> int:
@@ -389,6 +395,14 @@ def gs_stage(beta, word_idx, st: "GSStage", gate=None):
                    _chk(st.buf, torch.float64, "stage", None, dev), int(KS), _gate_ptr(gate, dev), _stream())
 
 
+def _need_pad_row(beta):
+    """The E-step kernels load a row's topic lanes at constant offsets: lanes past KS read into the next
+    row, the last row's into one zero pad row past the vocabulary (LDAEngine allocates [V + 1, KS])."""
+    V, KS = beta.shape
+    if beta.untyped_storage().nbytes() < (beta.storage_offset() + (V + 1) * KS) * beta.element_size():
+        raise ValueError("beta needs a zero pad row past its last row ([V + 1, KS] storage, view [:V])")
+
+
 def gs_estep(doc_ptr, word_idx, counts, order, beta, K, gs_updates, params, gamma, cphi, lik, alpha_ss, iters, variant,
              dbg=None, ent_base=None, stage: Optional["GSStage"] = None):
     """One launch of the fp64 block Gauss-Seidel E-step over the documents in ``order``.
@@ -423,9 +437,7 @@ def gs_estep(doc_ptr, word_idx, counts, order, beta, K, gs_updates, params, gamm
         0 if stage is None else _chk(stage.buf, torch.float64, "stage", None, dev),
         0 if stage is None else _chk(stage.stage_off, torch.int64, "stage_off", (order.numel(),), dev),
     ]
-    if variant == GS_SMALL and KS > 32 and \
-            beta.untyped_storage().nbytes() < (beta.storage_offset() + (V + 1) * KS) * 8:
-        raise ValueError("gs_smallw reads up to one row past beta: allocate a zero pad row ([V + 1, KS] storage)")
+    _need_pad_row(beta)
     if stage is not None and (variant != GS_TEAM8 or KS != stage.KS):
         raise ValueError("staged rows: kGsTeam8 launches of the stage's KS only")
     if order.numel() == 0:
@@ -577,6 +589,9 @@ class GSSplitPlan:
         max_seg = min(int(max_seg) or sp["g"], self.max_blocks, SPLIT_MAX_SEG)
         max_batches = int(max_batches) or sp["batches"]
         U = int(gs_updates)
+        self.U = U
+        # U past the LDS chunk tables: per-segment tables in a scratch ([n_blocks][U][2][KS] doubles)
+        self.tab_rows = U if U > gs_split_lds_umax(self.KS) else 0
         self.segments = {}
         self.batches = []
         self.leftover = []
@@ -614,7 +629,9 @@ class GSSplitPlan:
                     # tagged granules {uint32 half of a double, uint32 tag}: [2][n_blocks][2 (KS + 1)]
                     xchg=torch.zeros(2 * nb * 2 * (self.KS + 1), dtype=torch.int64, device=device),
                     counter=torch.zeros(2 * len(docs), dtype=torch.int32, device=device),
-                    error=torch.zeros(1, dtype=torch.int32, device=device), docs=len(docs))
+                    error=torch.zeros(1, dtype=torch.int32, device=device), docs=len(docs),
+                    tab=(torch.empty(nb * self.tab_rows * 2 * self.KS, dtype=torch.float64, device=device)
+                         if self.tab_rows else None))
 
 
 def gs_split(doc_ptr, word_idx, counts, beta, K, gs_updates, params, gamma, cphi, lik, alpha_ss, iters, batch,
@@ -633,6 +650,7 @@ def gs_split(doc_ptr, word_idx, counts, beta, K, gs_updates, params, gamma, cphi
         raise ValueError("K or gs_updates out of range")
     for k in ("seg_doc", "seg_index", "seg_count", "seg_base", "doc_slot"):
         _chk(batch[k], torch.int32, k, (nb,), dev)
+    _need_pad_row(beta)
     lib().gs_split(
         _chk(doc_ptr, torch.int32, "doc_ptr", (D + 1,), dev), _chk(word_idx, torch.int32, "word_idx", (nnz,), dev),
         _chk(counts, torch.float32, "counts", (nnz,), dev), _chk(beta, torch.float64, "beta", (V, KS), dev),
@@ -645,7 +663,18 @@ def gs_split(doc_ptr, word_idx, counts, beta, K, gs_updates, params, gamma, cphi
         _chk(batch["xchg"], torch.int64, "xchg", (2 * nb * 2 * (KS + 1),), dev),
         _chk(batch["counter"], torch.int32, "counter", (2 * batch["docs"],), dev), int(batch["docs"]),
         _chk(batch["error"], torch.int32, "error", (1,), dev), _stream(),
-        0 if dbg is None else _chk(dbg, torch.int64, "dbg", (8,), dev))
+        0 if dbg is None else _chk(dbg, torch.int64, "dbg", (8,), dev),
+        _split_tab(batch, nb, int(gs_updates), KS, dev))
+
+
+def _split_tab(batch, nb, U, KS, dev) -> int:
+    """The split batch's chunk-table scratch (required past the LDS tables' U)."""
+    tab = batch.get("tab")
+    if U > gs_split_lds_umax(KS):
+        if tab is None or tab.numel() < nb * U * 2 * KS:
+            raise ValueError(f"gs_split: U = {U} needs a chunk-table scratch of {nb} x {U} x 2 x {KS} doubles")
+        return _chk(tab, torch.float64, "tab", None, dev)
+    return 0
 
 
 def gs_xsplit_rows(KS: int) -> int:
@@ -784,7 +813,7 @@ class GSPlan:
         if split_min is None:
             split_min = split_spec(KS)["min"]
         if int(gs_updates) > gs_split_umax(KS):
-            split_min = 0       # the split kernel keeps its chunk tables in LDS: U <= 64 at KS <= 52, else 32
+            split_min = 0       # KS <= 32: the split kernel's chunk tables live in LDS (U <= 32)
         self.split = None
         # xsplit = {docs: N, members: G, proto: P} (even KS <= 32): the N longest documents over the CUs of
         # one XCD each (gs_xsplit; an experiment, off by default: profiles/r5_xcd_split.md)

@@ -420,17 +420,22 @@ def test_cphi_windows_em_run():
     assert abs(a1 - a0) <= 1e-12 * a0
 
 
-@pytest.mark.parametrize("K,U", [(50, 128), (100, 64)])
-def test_final_pass_word_assignments_large_u(K, U):
-    """The final pass with U > 32 (chunk tables in the c.phi rows, 4- and 8-wave teams read E_j from
-    row n0 + 1 before the chunk's rows are overwritten) against the oracle."""
+@pytest.mark.parametrize("K,U,split", [(50, 128, False), (100, 64, False), (50, 128, True), (100, 1024, True)])
+def test_final_pass_word_assignments_large_u(K, U, split, monkeypatch):
+    """The final pass with U > 32 against the oracle: the team kernels keep their chunk tables in the c.phi
+    rows (4- and 8-wave teams read E_j from row n0 + 1 before the chunk's rows are overwritten); the split
+    kernel past its LDS tables keeps them in a per-segment scratch (gs_splitw GM)."""
+    monkeypatch.setenv("ONI_GS_SPLIT_MIN", "2000" if split else "0")
     c = _edge_corpus(seed=17, max_len=6000)
     alpha = 0.6
     lb = _log_beta(c.num_terms, K, seed=3)
     st = LDASettings(var_max_iter=6, var_converged=-1e30)
     st.gs_updates = U
     eng = LDAEngine(c, K, st, backend="hip", seed=0, precision="fp64")
-    assert eng.gs_plan.split is None
+    if split:
+        assert eng.gs_plan.split is not None and all(b["tab"] is not None for b in eng.gs_plan.split.batches)
+    else:
+        assert eng.gs_plan.split is None
     eng.init_from_model(lb, alpha)
     z = eng.word_assignments()
     ref = native.lib().lda_assign_ldac(c.doc_ptr, c.word_idx, c.counts.astype(np.float64), np.ascontiguousarray(lb),
