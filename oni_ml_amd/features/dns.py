@@ -33,31 +33,8 @@ from .quantiles import DECILES, QUINTILES, ecdf_cuts
 
 from .dns_io import (  # noqa: F401  (re-exported: the torch-free ingest)
     COLUMNS, FEEDBACK_IDX, _pa, select_paths, _java_split_len, read_dns_feedback, _java_double, DnsTable,
-    _arrow_strings, load_dns, _parquet_files, load_dns_rows, dns_total_rows, table_from_arrow, load_top_domains)
-
-
-def _offsets(names):
-    """(bytes buffer, int64 offsets) of a list of str or an Arrow string array (zero-copy data)."""
-    if isinstance(names, list):
-        enc = [s.encode("utf-8") for s in names]
-        off = np.zeros(len(enc) + 1, np.int64)
-        np.cumsum([len(b) for b in enc], out=off[1:])
-        return b"".join(enc), off
-    pa, _, _ = _pa()
-    a = names
-    wide = pa.types.is_large_string(a.type)
-    bufs = a.buffers()
-    off = np.frombuffer(bufs[1], dtype=np.int64 if wide else np.int32)[a.offset: a.offset + len(a) + 1]
-    data = bufs[2] if bufs[2] is not None else b""
-    return data, off.astype(np.int64)
-
-
-def arrow_dictionary_encode(arr):
-    """First-appearance ids + names of an Arrow string array (Arrow's hash memo assigns codes in
-    order of first occurrence, like ``dictionary_encode``)."""
-    _, pc, _ = _pa()
-    d = pc.dictionary_encode(arr)
-    return d.indices.to_numpy(zero_copy_only=False).astype(np.int32), d.dictionary.to_pylist()
+    _arrow_strings, load_dns, _parquet_files, load_dns_rows, dns_total_rows, table_from_arrow, load_top_domains,
+    _offsets, arrow_dictionary_encode, host_features)
 
 
 @dataclass
@@ -88,18 +65,20 @@ def dictionary_encode(values: List[str]):
 
 def featurize(tab: DnsTable, device, top_domains: Sequence[str], cuts: Optional[Dict[str, np.ndarray]] = None,
               raw_only: bool = False, threads: int = 8, host: Optional[dict] = None) -> DnsFeatures:
-    """``host``: the name features ``featurize`` already returned for a prefix-compatible row set of
-    the same table (dns_pre's, over every row, reused by dns_post over the raw rows): the per-row
-    arrays are cut to this call's rows; the domain / subdomain dictionaries are first-appearance over
-    the rows, so a prefix keeps its ids."""
+    """``host``: the host features (``host_features``, or what ``featurize`` returned) of a prefix-compatible
+    row set of the same table (the prefetch thread's or dns_pre's, over every row, reused by dns_post over
+    the raw rows): the per-row arrays are cut to this call's rows; the dictionaries are first-appearance over
+    the rows, so a prefix keeps its ids (and its names are a prefix of the names)."""
     device = torch.device(device)
     n = tab.n_raw if raw_only else tab.n
     if host is not None and len(host["entropy"]) >= n:
         m = len(host["entropy"])
         F = {k: (v[:n] if isinstance(v, np.ndarray) and v.ndim == 1 and len(v) == m else v) for k, v in host.items()}
+        if n < m:   # a prefix: its dictionaries' names are the names up to its largest id
+            for ids, names in (("_qid", "_qnames"), ("_ip_ids", "_ip_names")):
+                F[names] = F[names][:int(F[ids].max()) + 1] if n else []
     else:
-        data, off = _offsets(tab.column("dns_qry_name", n))
-        F = native.lib().dns_features(data, off, list(COUNTRY_CODES), list(top_domains), SPECIAL_DOMAIN, threads)
+        F = host_features(tab, top_domains, threads, n)
     w = torch.from_numpy(tab.weight[:n]).to(device)
     vals = dict(
         frame_len=torch.from_numpy(tab.frame_len[:n]).to(device),
@@ -118,10 +97,7 @@ def featurize(tab: DnsTable, device, top_domains: Sequence[str], cuts: Optional[
     else:
         cuts_t = {k: torch.as_tensor(np.asarray(v, np.float64), device=device) for k, v in cuts.items()}
     bins = {k: (vals[k].unsqueeze(-1) > cuts_t[k].unsqueeze(0)).sum(-1) for k in vals}
-    pa, pc, _ = _pa()
-    qt, qr = tab.column("dns_qry_type", n), tab.column("dns_qry_rcode", n)
-    # the separator must have the columns' type (large_string once feedback rows are appended)
-    qid, qnames = arrow_dictionary_encode(pc.binary_join_element_wise(qt, qr, pa.scalar("_", qt.type)))
+    qid, qnames = F["_qid"], F["_qnames"]
     top = torch.from_numpy(F["top_domain"].astype(np.int64)).to(device)
     key = top
     radix = dict(frame_len=len(cuts_t["frame_len"]) + 1, unix_tstamp=len(cuts_t["unix_tstamp"]) + 1,
@@ -130,7 +106,7 @@ def featurize(tab: DnsTable, device, top_domains: Sequence[str], cuts: Optional[
     for k in ("frame_len", "unix_tstamp", "subdomain_length", "entropy", "num_periods"):
         key = key * radix[k] + bins[k]
     key = key * max(1, len(qnames)) + torch.from_numpy(qid.astype(np.int64)).to(device)
-    ip_ids, ip_names = arrow_dictionary_encode(tab.column("ip_dst", n))
+    ip_ids, ip_names = F["_ip_ids"], F["_ip_names"]
     return DnsFeatures(rows=np.arange(n, dtype=np.int64), ip=torch.from_numpy(ip_ids.astype(np.int64)).to(device),
                        ip_names=ip_names, word_key=key, weight=w, bins=bins,
                        cuts={k: v.cpu().numpy() for k, v in cuts_t.items()}, host=F, qpairs=qnames)

@@ -240,3 +240,46 @@ def load_top_domains(path: Optional[str]) -> List[str]:
                 continue
             out.append(parts[1].split(".")[0])
     return out
+
+
+def _offsets(names):
+    """(bytes buffer, int64 offsets) of a list of str or an Arrow string array (zero-copy data)."""
+    if isinstance(names, list):
+        enc = [s.encode("utf-8") for s in names]
+        off = np.zeros(len(enc) + 1, np.int64)
+        np.cumsum([len(b) for b in enc], out=off[1:])
+        return b"".join(enc), off
+    pa, _, _ = _pa()
+    a = names
+    wide = pa.types.is_large_string(a.type)
+    bufs = a.buffers()
+    off = np.frombuffer(bufs[1], dtype=np.int64 if wide else np.int32)[a.offset: a.offset + len(a) + 1]
+    data = bufs[2] if bufs[2] is not None else b""
+    return data, off.astype(np.int64)
+
+
+def arrow_dictionary_encode(arr):
+    """First-appearance ids + names of an Arrow string array (Arrow's hash memo assigns codes in
+    order of first occurrence, like ``dictionary_encode``)."""
+    _, pc, _ = _pa()
+    d = pc.dictionary_encode(arr)
+    return d.indices.to_numpy(zero_copy_only=False).astype(np.int32), d.dictionary.to_pylist()
+
+
+def host_features(tab: DnsTable, top_domains, threads: int = 8, n: Optional[int] = None) -> dict:
+    """The torch-free part of dns_pre over every row of ``tab``: the C++ name features (domain, subdomain,
+    lengths, entropy, top-1m flag), and the first-appearance dictionaries of "qry_type_qry_rcode" and of
+    ip_dst.  `pipeline/prefetch.py` runs it on the input thread while torch imports; features/dns.py's
+    ``featurize`` takes it (``host``) for the whole table or any prefix of it (the raw rows: a prefix of a
+    first-appearance encoding is the encoding of the prefix)."""
+    from .dns_data import COUNTRY_CODES, SPECIAL_DOMAIN
+    pa, pc, _ = _pa()
+    n = tab.n if n is None else n
+    data, off = _offsets(tab.column("dns_qry_name", n))
+    F = native.lib().dns_features(data, off, list(COUNTRY_CODES), list(top_domains), SPECIAL_DOMAIN, threads)
+    qt, qr = tab.column("dns_qry_type", n), tab.column("dns_qry_rcode", n)
+    # the separator must have the columns' type (large_string once feedback rows are appended)
+    F["_qid"], F["_qnames"] = arrow_dictionary_encode(pc.binary_join_element_wise(qt, qr, pa.scalar("_", qt.type)))
+    F["_ip_ids"], F["_ip_names"] = arrow_dictionary_encode(tab.column("ip_dst", n))
+    return F
+

@@ -40,7 +40,7 @@ def run(cfg, dist=None, device=None, log=print) -> dict:
             got = prefetch.take(prefetch.dns_key(cfg))
             res["prefetched"] = got is not None
             if got is not None:
-                tab, top = got
+                tab, top, pre_host = got
             else:
                 tab = FD.load_dns(cfg.dns_path, cfg.feedback_path(), cfg.dupfactor, strict=cfg.strict)
                 top = FD.load_top_domains(cfg.top1m)
@@ -52,7 +52,7 @@ def run(cfg, dist=None, device=None, log=print) -> dict:
     if need_pre:
         if rank == 0:
             with R.stage("dns_pre") as res:
-                feat = FD.featurize(tab, device, top, threads=cfg.threads)
+                feat = FD.featurize(tab, device, top, threads=cfg.threads, host=pre_host)
                 pre_host = feat.host
                 wsp = FD.DnsWordSpace(feat.cuts, feat.qpairs)
                 dwc = count_pairs(feat.ip, feat.word_key, feat.weight)

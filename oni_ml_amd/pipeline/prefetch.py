@@ -2,15 +2,17 @@
 
 A cold `ml_ops` process spends ~0.7 s importing torch (libtorch's dlopen and static initialisers)
 before any stage runs, and the first stage only reads the day's inputs: the 27-column flow CSV into
-the native table, or the DNS parquet through Arrow -- neither needs torch, and both do their work
-with the GIL released.  `cli.cmd_ml_ops` therefore starts that read on a thread before it imports
-torch (single-process runs, fresh work directory), and the load stage takes the result if it was
-started for the same inputs; otherwise, or if the prefetch failed, the stage reads the inputs itself
-(so an input error is raised and recorded inside the stage, as before).  ``ONI_PREFETCH=0`` turns it
-off.  Imports nothing heavy: this module is loaded before torch.
+the native table, or the DNS parquet through Arrow (plus dns_pre's torch-free name features) -- none of
+it needs torch.  `cli.cmd_ml_ops` therefore starts that work before it imports torch (single-process
+runs, fresh work directory): the flow read on a thread (native, GIL released), the DNS read in a forked
+child (below), and the load stage takes the result if it was started for the same inputs; otherwise,
+or if the prefetch failed, the stage reads the inputs itself (so an input error is raised and
+recorded inside the stage, as before).  ``ONI_PREFETCH=0`` turns it off.  Imports nothing heavy: this
+module is loaded before torch.
 """
 from __future__ import annotations
 
+import os
 import threading
 from typing import Callable, Dict, Optional, Tuple
 
@@ -22,7 +24,7 @@ def flow_key(cfg) -> tuple:
 
 
 def dns_key(cfg) -> tuple:
-    return ("dns", cfg.dns_path, cfg.feedback_path(), cfg.dupfactor, cfg.strict, cfg.top1m)
+    return ("dns", cfg.dns_path, cfg.feedback_path(), cfg.dupfactor, cfg.strict, cfg.top1m, cfg.threads)
 
 
 def start(key: tuple, fn: Callable, *args) -> None:
@@ -43,17 +45,108 @@ def take(key: tuple) -> Optional[object]:
     """The prefetched value for ``key`` (waits for it), or None: nothing started for these inputs, or
     the prefetch raised.  Every other prefetch is dropped (its thread finishes on its own)."""
     job = _JOBS.pop(key, None)
+    for t, box in _JOBS.values():      # dropped: a forked child is still reaped and its files removed
+        if t is None:
+            box["collect"]()
     _JOBS.clear()
     if job is None:
         return None
     t, box = job
+    if t is None:                      # a forked prefetch (DNS): wait for the child, map its result
+        return box["collect"]()
     t.join()
     return box.get("value")
 
 
-def load_dns_inputs(dns_path, feedback_path, dupfactor, strict, top1m):
+def load_dns_inputs(dns_path, feedback_path, dupfactor, strict, top1m, threads=8):
+    """(table, top-1m list, dns_pre's torch-free host features) -- the name parse and the two dictionary
+    encodes run here too, beside the torch import (dns_pre 0.41 s, 0.25 s of it these; profiles/r5_cold_start.md)."""
     from ..features import dns_io
-    return dns_io.load_dns(dns_path, feedback_path, dupfactor, strict=strict), dns_io.load_top_domains(top1m)
+    tab = dns_io.load_dns(dns_path, feedback_path, dupfactor, strict=strict)
+    top = dns_io.load_top_domains(top1m)
+    return tab, top, dns_io.host_features(tab, top, threads)
+
+
+# ---- DNS: a forked child process -------------------------------------------------------------------
+# On a thread the DNS read cost the torch import 0.3 s (1.0-1.1 s against 0.7-0.8 alone, at any thread
+# count: pyarrow's own import and its Python-side glue hold the GIL and the import lock beside torch's),
+# where the flow CSV ingest (native, GIL released) costs it nothing.  So the DNS prefetch runs in a child
+# forked before anything but the standard library, numpy and this package is loaded (no GPU, no
+# threads): it reads the parquet, computes the host features and hands them back through /dev/shm --
+# the string columns as one Arrow IPC file (memory-mapped by the parent, zero copy), the per-row arrays
+# as .npy files (memory-mapped), the name lists and scalars pickled (this process's own data).
+
+def _dns_child(args, out_dir) -> None:
+    import pickle
+    import numpy as np
+    tab, top, F = load_dns_inputs(*args)
+    from ..features import dns_io
+    pa, _, _ = dns_io._pa()
+    names = list(tab.arrays)
+    batch = pa.record_batch([tab.arrays[c] for c in names], names=names)
+    with pa.OSFile(os.path.join(out_dir, "cols.arrow"), "wb") as f, pa.ipc.new_file(f, batch.schema) as w:
+        w.write_batch(batch)
+    arrays = dict(frame_len=tab.frame_len, unix_tstamp=tab.unix_tstamp, weight=tab.weight)
+    arrays.update({"F_" + k: v for k, v in F.items() if isinstance(v, np.ndarray)})
+    for k, v in arrays.items():
+        np.save(os.path.join(out_dir, k + ".npy"), np.ascontiguousarray(v))
+    meta = dict(n_raw=tab.n_raw, n_feedback=tab.n_feedback, dropped=tab.dropped, top=list(top),
+                F_lists={k: v for k, v in F.items() if not isinstance(v, np.ndarray)}, arrays=list(arrays))
+    with open(os.path.join(out_dir, "meta.pkl"), "wb") as f:
+        pickle.dump(meta, f, protocol=pickle.HIGHEST_PROTOCOL)
+
+
+def _dns_collect(pid, rfd, out_dir):
+    """The child's result as (DnsTable, top list, host features); None if it failed."""
+    import pickle
+    import shutil
+    try:
+        ok = os.read(rfd, 2) == b"OK"
+        os.close(rfd)
+        os.waitpid(pid, 0)
+        if not ok:
+            return None
+        import numpy as np
+        from ..features import dns_io
+        pa, _, _ = dns_io._pa()
+        with open(os.path.join(out_dir, "meta.pkl"), "rb") as f:
+            meta = pickle.load(f)   # written by this process's own fork (_dns_child)
+        src = pa.memory_map(os.path.join(out_dir, "cols.arrow"))
+        batch = pa.ipc.open_file(src).get_batch(0)
+        # copy-on-write mappings: writable like the arrays a read in this process returns
+        arr = {k: np.load(os.path.join(out_dir, k + ".npy"), mmap_mode="c") for k in meta["arrays"]}
+        tab = dns_io.DnsTable({c: batch.column(c) for c in batch.schema.names}, arr["frame_len"], arr["unix_tstamp"],
+                              arr["weight"], meta["n_raw"], meta["n_feedback"], dropped=meta["dropped"])
+        F = {k[2:]: v for k, v in arr.items() if k.startswith("F_")}
+        F.update(meta["F_lists"])
+        return tab, meta["top"], F
+    finally:
+        shutil.rmtree(out_dir, ignore_errors=True)   # the mappings stay valid after the unlink
+
+
+def _start_dns_fork(key, args) -> bool:
+    import tempfile
+    if threading.active_count() > 1 or not os.path.isdir("/dev/shm"):
+        return False
+    out_dir = tempfile.mkdtemp(prefix="oni_prefetch_", dir="/dev/shm")
+    rfd, wfd = os.pipe()
+    pid = os.fork()
+    if pid == 0:                       # child: no GPU, no threads; never returns
+        code = b"ER"
+        try:
+            os.close(rfd)
+            _dns_child(args, out_dir)
+            code = b"OK"
+        except BaseException:  # noqa: BLE001 -- the parent's load stage re-reads and raises it there
+            pass
+        finally:
+            try:
+                os.write(wfd, code)
+            finally:
+                os._exit(0)
+    os.close(wfd)
+    _JOBS[key] = (None, dict(collect=lambda: _dns_collect(pid, rfd, out_dir)))
+    return True
 
 
 def start_for(cfg) -> None:
@@ -62,5 +155,6 @@ def start_for(cfg) -> None:
         from ..features import flow_io
         start(flow_key(cfg), flow_io.load_flow, cfg.flow_path, cfg.feedback_path(), cfg.dupfactor, cfg.threads)
     elif cfg.dsource == "dns":
-        start(dns_key(cfg), load_dns_inputs, cfg.dns_path, cfg.feedback_path(), cfg.dupfactor, cfg.strict,
-              cfg.top1m)
+        args = (cfg.dns_path, cfg.feedback_path(), cfg.dupfactor, cfg.strict, cfg.top1m, cfg.threads)
+        if not _start_dns_fork(dns_key(cfg), args):
+            start(dns_key(cfg), load_dns_inputs, *args)
