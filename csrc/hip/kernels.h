@@ -93,6 +93,8 @@ enum GsVariant : int {
   kGsTeam8 = 3,    // one 8-wave workgroup per document (8 prefetched words per slot and chunk)
   kGsSmall = 4,    // 16 lanes per document: KS <= 32 tiny < n <= 64 words (register state); KS > 32 the
                    // one-wave range (gs_smallw, chunk tables in the c*phi rows)
+  kGsChain = 5,    // KS > 32, U > 32: one wave per document, a topic per lane, rows of the next 8 words in
+                   // flight (chunks of <= 4 words: lda-c's per-word schedule)
 };
 struct GSArgs {
   const int* doc_ptr;     // [D+1]

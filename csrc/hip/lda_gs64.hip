@@ -368,6 +368,198 @@ __global__ __launch_bounds__(256) void gs_small(GSArgs a) {
   }
 }
 
+// ----------------------------------------------------------------- chain ----
+// lda-c's per-word schedule and chunks of a few words at K > 32 (U > 32): one wave per document, lane l
+// holding topics l and l + 64 (TC = ceil(KS / 64)).  A chunk's P is a full-wave sum, the refresh TC
+// digamma/exp chains per lane with E, gamma, psi in registers: no LDS, no barrier.  At U = 1024 a document of
+// 257-4,096 words is a chain of up to 1,024 refreshes per sweep; the one-wave team paid an LDS round trip
+// each way per chunk and waited on the row of the next word, gathered one chunk (= one word) ahead (r5h:
+// 3.9 k cycles per chunk).  Here the rows of the next D words are in flight in a register ring (their ids D
+// words further ahead), so a chunk costs its arithmetic.  Chunk tables in the document's own c*phi rows:
+// C_j in row j W, the E chunk j used in row j W + 1 (chunks of >= 2 words); every row access is by the lane
+// owning the topic.  Words wrap into the next sweep (a stopped run discards D prefetched rows).
+template <int KS, int D>
+__global__ __launch_bounds__(256) void gs_chain(GSArgs a) {
+  static_assert(KS > 32 && KS <= 128, "gs_chain: 32 < KS <= 128");
+  constexpr int TC = (KS + 63) / 64;
+  if (a.params[kParamDone] != 0.0) return;
+  const int lane = threadIdx.x & 63;
+  const int item = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (item >= a.n_items) return;   // whole waves leave together
+  const double alpha = a.params[0], lik_const = a.params[1];
+  const int vmi = (int)a.params[2];
+  const double vconv = params_vconv(a.params);
+  const int K = a.K;
+  const int d = a.order[item];
+  if (d < 0) return;
+  const int s0 = a.doc_ptr[d], n = a.doc_ptr[d + 1] - s0;
+  if (n <= 0) return;              // (the planner never sends an empty document)
+  const int U = a.gs_updates;
+  const int W = (n + U - 1) / U;
+  const int nch = (n + W - 1) / W;
+  const int* __restrict__ wrow = a.word_idx + s0;
+  const float* __restrict__ crow = a.counts + s0;
+  double* __restrict__ rows = a.cphi + (size_t)s0 * KS;
+  auto owned = [&](int o) { return 64 * (o + 1) <= KS || lane + 64 * o < KS; };   // static but the last group
+  double total = 0.0;
+  for (int j = 0; j < nch; ++j) {
+    const int n0 = j * W, n1 = min(n, n0 + W);
+    double cs = 0.0;
+    for (int p = n0; p < n1; ++p) cs += (double)crow[p];   // integer counts: exact
+    total += cs;
+#pragma unroll
+    for (int o = 0; o < TC; ++o)
+      if (owned(o)) rows[(size_t)n0 * KS + lane + 64 * o] = lane + 64 * o < K ? cs / K : 0.0;
+  }
+  const double g0 = alpha + total / K;
+  const double m = psi_only(g0);
+  double gam[TC], psi[TC], E[TC], Cn[TC], acc[TC];
+#pragma unroll
+  for (int o = 0; o < TC; ++o) {
+    const int k = lane + 64 * o;
+    gam[o] = k < K ? g0 : 0.0;
+    psi[o] = m;
+    E[o] = k < K ? 1.0 : 0.0;
+    Cn[o] = owned(o) ? rows[k] : 0.0;   // C_0 (this lane's own store)
+    acc[o] = 0.0;
+  }
+  // rings: rb / rc the rows and counts of words g .. g + D - 1, wi / wc the ids and counts of words
+  // g + D .. g + 2D - 1 (word g in slot g mod D); beta's pad row covers the lanes past KS
+  double rb[D][TC], rc[D];
+  int wi[D];
+  float wc[D];
+#pragma unroll
+  for (int t = 0; t < D; ++t) {
+    const int p = t % n;
+    const double* brow = a.beta + (size_t)wrow[p] * KS + lane;
+#pragma unroll
+    for (int o = 0; o < TC; ++o) rb[t][o] = brow[64 * o];
+    rc[t] = (double)crow[p];
+    const int p2 = (t + D) % n;
+    wi[t] = wrow[p2];
+    wc[t] = crow[p2];
+  }
+  double L = 0.0, L_old = 0.0, conv = 1.0, GS = 0.0;
+  double lw = 0.0, lp = 0.0;
+  int pw = 0, j = 0;               // word of the sweep, its chunk
+  int cend = min(n, W);            // end of chunk j
+  int g2 = 2 * D;                  // the word whose id the slot being consumed loads next (mod n)
+  bool run = var_continue(conv, vconv, 0, vmi);
+  int it = run ? 1 : 0;            // sweeps begun
+  while (run) {
+#pragma unroll
+    for (int t = 0; t < D; ++t) {
+      if (run) {
+        // word pw: P over the whole wave, then its contribution to the chunk
+        double pp = 0.0;
+#pragma unroll
+        for (int o = 0; o < TC; ++o) pp = fma(E[o], rb[t][o], pp);
+        const double P = group_sum<64>(pp);
+        const double c = rc[t];
+        const double r = c * drcp(P);
+        lw = fma(c, flog(P), lw);
+#pragma unroll
+        for (int o = 0; o < TC; ++o) acc[o] = fma(r, rb[t][o], acc[o]);
+        // the slot's next row (word pw + D) and the id D words beyond it
+        {
+          const double* brow = a.beta + (size_t)wi[t] * KS + lane;
+#pragma unroll
+          for (int o = 0; o < TC; ++o) rb[t][o] = brow[64 * o];
+          rc[t] = (double)wc[t];
+          const int p2 = g2 % n;
+          wi[t] = wrow[p2];
+          wc[t] = crow[p2];
+          ++g2;
+        }
+        if (++pw == cend) {
+          // chunk j ends: its tables, then the refresh (branch-free: padding topics keep E = 0)
+          const int n0 = j * W;
+          const bool two = cend - n0 >= 2;
+#pragma unroll
+          for (int o = 0; o < TC; ++o) {
+            if (owned(o)) {
+              rows[(size_t)n0 * KS + lane + 64 * o] = E[o] * acc[o];
+              if (two) rows[(size_t)(n0 + 1) * KS + lane + 64 * o] = E[o];
+            }
+          }
+#pragma unroll
+          for (int o = 0; o < TC; ++o) {
+            const bool real = lane + 64 * o < K;
+            const double nw = E[o] * acc[o];
+            lp = fma(psi[o], nw, lp);
+            gam[o] = real ? gam[o] + (nw - Cn[o]) : gam[o];
+            double pn, en;
+            psi_exp(real ? gam[o] : 1.0, m, pn, en);
+            psi[o] = real ? pn : psi[o];
+            E[o] = real ? en : 0.0;
+            acc[o] = 0.0;
+          }
+          j = j + 1 < nch ? j + 1 : 0;
+          cend = min(n, (j + 1) * W);
+#pragma unroll
+          for (int o = 0; o < TC; ++o) Cn[o] = owned(o) ? rows[(size_t)j * W * KS + lane + 64 * o] : 0.0;
+          if (pw == n) {
+            // sweep end: lda-c's likelihood and convergence test
+            double gs = 0.0, lg = 0.0;
+#pragma unroll
+            for (int o = 0; o < TC; ++o) {
+              const bool real = lane + 64 * o < K;
+              const double l = lgamma_pos(real ? gam[o] : 1.0);
+              gs += real ? gam[o] : 0.0;
+              lg += real ? l : 0.0;
+            }
+            GS = group_sum<64>(gs);
+            const double LG = group_sum<64>(lg), LP = group_sum<64>(lp);
+            L = lik_const - lgamma_pos(GS) + LG + fma(m, total, lw) - LP;
+            conv = (L_old - L) / L_old;
+            L_old = L;
+            run = var_continue(conv, vconv, it, vmi);
+            it += run ? 1 : 0;
+            pw = 0;
+            lw = 0.0;
+            lp = 0.0;
+          }
+        }
+      }
+    }
+  }
+  double ps = 0.0;
+#pragma unroll
+  for (int o = 0; o < TC; ++o) {
+    const int k = lane + 64 * o;
+    if (k < K) ps += psi[o];
+    if (owned(o)) a.gamma[(size_t)d * KS + k] = gam[o];
+  }
+  ps = group_sum<64>(ps);
+  if (lane == 0) {
+    a.lik[d] = L;
+    a.alpha_ss[d] = ps - K * psi_only(GS);
+    a.iters[d] = it;
+  }
+  // final pass over chunks of >= 2 words: c_n phi_nk = E_jk b_nk r_n with the final sweep's chunk E
+  if (W < 2) return;
+  for (int jj = 0; jj < nch; ++jj) {
+    const int n0 = jj * W, n1 = min(n, n0 + W);
+    if (n1 - n0 < 2) continue;
+    double Ej[TC];
+#pragma unroll
+    for (int o = 0; o < TC; ++o) Ej[o] = owned(o) ? rows[(size_t)(n0 + 1) * KS + lane + 64 * o] : 0.0;
+    for (int p = n0; p < n1; ++p) {
+      const double* brow = a.beta + (size_t)wrow[p] * KS + lane;
+      double b[TC], pp = 0.0;
+#pragma unroll
+      for (int o = 0; o < TC; ++o) {
+        b[o] = brow[64 * o];
+        pp = fma(Ej[o], b[o], pp);
+      }
+      const double rr = (double)crow[p] * drcp(group_sum<64>(pp));
+#pragma unroll
+      for (int o = 0; o < TC; ++o)
+        if (owned(o)) __builtin_nontemporal_store(Ej[o] * b[o] * rr, &rows[(size_t)p * KS + lane + 64 * o]);
+    }
+  }
+}
+
 // ---------------------------------------------------------- small, K > 32 ----
 // The one-wave range at K > 32 (short documents; at lda-c's per-word schedule every document whose chunks
 // hold <= 2 words): 16 lanes per document, KPL = ceil(KS / 16) topics per lane, four documents per wave,
@@ -2436,6 +2628,12 @@ static void gs_estep_ks(const GSArgs& a, int variant, hipStream_t s) {
         hipLaunchKernelGGL((gs::gs_smallw<KS, 2, 2>), dim3((a.n_items + 15) / 16), dim3(256), 0, s, a);
       break;
     }
+    case kGsChain:
+      if constexpr (KS > 32)
+        hipLaunchKernelGGL((gs::gs_chain<KS, 8>), dim3((a.n_items + 3) / 4), dim3(256), 0, s, a);
+      else
+        throw std::runtime_error("gs_estep: the chain kernel needs KS > 32");
+      break;
     case kGsTeam1: {
       // one wave per document (<= 256 words, chunks of <= 8 words): the topic-group layout keeps
       // more lanes busy than one word per lane (measured 0.90 vs 1.13 ms on the headline corpus)

@@ -1,0 +1,57 @@
+"""The ECDF cut rule of features/quantiles.py on the host, without torch (numpy only): the DNS prefetch
+child computes dns_pre's and dns_post's cuts while the parent imports torch (pipeline/prefetch.py).
+
+Same arithmetic as ``quantiles.ecdf_cuts``: sorted distinct values with exact integer (weighted)
+counts, F = cumulative count / total in double, cut_q = max({0} U {v : F(v) < q}) -- identical bits.
+"""
+from __future__ import annotations
+
+from typing import Optional, Sequence
+
+import numpy as np
+
+
+def ecdf_cuts_np(values: np.ndarray, quantiles: Sequence[float], weights: Optional[np.ndarray] = None) -> np.ndarray:
+    v = np.asarray(values, np.float64).reshape(-1)
+    q = np.asarray(list(quantiles), np.float64)
+    if v.size == 0:
+        return np.zeros_like(q)
+    uniq, inv = np.unique(v, return_inverse=True)
+    if weights is None:
+        counts = np.bincount(inv, minlength=uniq.size).astype(np.int64)
+    else:
+        # integer weights: an exact int64 sum per distinct value (bincount's float64 sum is exact below 2^53,
+        # the int64 path keeps it exact everywhere)
+        counts = np.zeros(uniq.size, np.int64)
+        np.add.at(counts, inv, np.asarray(weights, np.int64).reshape(-1))
+    cum = np.cumsum(counts)
+    F = cum.astype(np.float64) / np.float64(cum[-1])
+    idx = np.searchsorted(F, q, side="left") - 1
+    cand = np.where(idx >= 0, uniq[np.clip(idx, 0, None)], 0.0)
+    return np.maximum(cand, 0.0)
+
+
+# dns_pre_lda.scala's cuts: deciles of unix_tstamp and frame_len over every row, quintiles of the subdomain
+# length, entropy and label count over the rows with a value > 0 (features/dns.py featurize)
+DNS_CUT_COLUMNS = (("unix_tstamp", "deciles", False), ("frame_len", "deciles", False),
+                   ("subdomain_length", "quintiles", True), ("entropy", "quintiles", True),
+                   ("num_periods", "quintiles", True))
+
+
+def dns_cuts_np(values: dict, weight: np.ndarray, n: int, threads: int = 8) -> dict:
+    """{column: cuts} over the first n rows (np.unique releases the GIL: the five columns on threads)."""
+    from concurrent.futures import ThreadPoolExecutor
+    from .quantile_levels import DECILES, QUINTILES
+    w = np.asarray(weight[:n], np.int64)
+
+    def one(spec):
+        name, levels, positive = spec
+        v = np.asarray(values[name][:n], np.float64)
+        q = DECILES if levels == "deciles" else QUINTILES
+        if positive:
+            m = v > 0
+            return name, ecdf_cuts_np(v[m], q, w[m])
+        return name, ecdf_cuts_np(v, q, w)
+
+    with ThreadPoolExecutor(max(1, min(threads, len(DNS_CUT_COLUMNS)))) as ex:
+        return dict(ex.map(one, DNS_CUT_COLUMNS))

@@ -87,7 +87,10 @@ def featurize(tab: DnsTable, device, top_domains: Sequence[str], cuts: Optional[
         entropy=torch.from_numpy(F["entropy"]).to(device),
         num_periods=torch.from_numpy(F["num_periods"].astype(np.float64)).to(device),
     )
-    if cuts is None:
+    if cuts is None and host is not None and n in host.get("_cuts", {}):
+        # the prefetch child's host cuts for these rows (features/cuts_host.py: the same rule, same bits)
+        cuts_t = {k: torch.as_tensor(np.asarray(v, np.float64), device=device) for k, v in host["_cuts"][n].items()}
+    elif cuts is None:
         cuts_t = {}
         for k, q in (("unix_tstamp", DECILES), ("frame_len", DECILES)):
             cuts_t[k] = ecdf_cuts(vals[k], q, w)

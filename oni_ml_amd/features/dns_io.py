@@ -266,7 +266,7 @@ def arrow_dictionary_encode(arr):
     return d.indices.to_numpy(zero_copy_only=False).astype(np.int32), d.dictionary.to_pylist()
 
 
-def host_features(tab: DnsTable, top_domains, threads: int = 8, n: Optional[int] = None) -> dict:
+def host_features(tab: DnsTable, top_domains, threads: int = 8, n: Optional[int] = None, cuts: bool = False) -> dict:
     """The torch-free part of dns_pre over every row of ``tab``: the C++ name features (domain, subdomain,
     lengths, entropy, top-1m flag), and the first-appearance dictionaries of "qry_type_qry_rcode" and of
     ip_dst.  `pipeline/prefetch.py` runs it on the input thread while torch imports; features/dns.py's
@@ -281,5 +281,11 @@ def host_features(tab: DnsTable, top_domains, threads: int = 8, n: Optional[int]
     # the separator must have the columns' type (large_string once feedback rows are appended)
     F["_qid"], F["_qnames"] = arrow_dictionary_encode(pc.binary_join_element_wise(qt, qr, pa.scalar("_", qt.type)))
     F["_ip_ids"], F["_ip_names"] = arrow_dictionary_encode(tab.column("ip_dst", n))
+    if cuts:
+        # dns_pre's cuts (every row) and dns_post's (the raw rows: the reference recomputes them there)
+        from .cuts_host import dns_cuts_np
+        vals = dict(unix_tstamp=tab.unix_tstamp, frame_len=tab.frame_len, subdomain_length=F["subdomain_length"],
+                    entropy=F["entropy"], num_periods=F["num_periods"])
+        F["_cuts"] = {m: dns_cuts_np(vals, tab.weight, m, threads) for m in sorted({n, min(n, tab.n_raw)})}
     return F
 

@@ -20,8 +20,7 @@ from typing import Optional, Sequence
 import numpy as np
 import torch
 
-DECILES = (0.0, 0.1, 0.2, 0.3, 0.4, 0.5, 0.6, 0.7, 0.8, 0.9)
-QUINTILES = (0.0, 0.2, 0.4, 0.6, 0.8)
+from .quantile_levels import DECILES, QUINTILES  # noqa: F401  (re-exported)
 
 
 def ecdf_cuts(values: torch.Tensor, quantiles: Sequence[float], weights: Optional[torch.Tensor] = None) -> torch.Tensor:

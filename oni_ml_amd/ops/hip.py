@@ -304,7 +304,7 @@ def bin_columns(values, cuts):
 # ------------------------------------------------------- fp64 block Gauss-Seidel ---
 # lda-c-faithful E-step (csrc/hip/lda_gs64.hip): double everywhere, gamma refreshed after every
 # chunk of ceil(n / gs_updates) words (documents of <= gs_updates words: lda-c's per-word schedule).
-GS_TINY, GS_TEAM1, GS_TEAM4, GS_TEAM8, GS_SMALL = range(5)
+GS_TINY, GS_TEAM1, GS_TEAM4, GS_TEAM8, GS_SMALL, GS_CHAIN = range(6)
 GS_SMALL_MAX = 64   # csrc/hip/lda_gs64.hip kGsSmallMax
 
 
@@ -418,7 +418,7 @@ def gs_estep(doc_ptr, word_idx, counts, order, beta, K, gs_updates, params, gamm
         raise ValueError("K out of range")
     if not (1 <= int(gs_updates) <= gs_umax(KS)):
         raise ValueError(f"gs_updates must be in [1, {gs_umax(KS)}] at KS {KS}")
-    if variant not in (GS_TINY, GS_TEAM1, GS_TEAM4, GS_TEAM8, GS_SMALL):
+    if variant not in (GS_TINY, GS_TEAM1, GS_TEAM4, GS_TEAM8, GS_SMALL, GS_CHAIN):
         raise ValueError(f"unknown gs variant {variant}")
     dev = beta.device
     args = [
@@ -867,15 +867,15 @@ class GSPlan:
         split a chunk's W = ceil(n / U) words, so at lda-c's per-word schedule (U = 1024: W = 1 for every
         document up to 1,024 words) a 4- or 8-wave team idles all but one word slot and pays two
         workgroup barriers per word, where one wave per document refreshes in-wave with no barrier.
-        One wave per document up to W = 2, four up to W = 16, eight beyond (never below the U = 32 edges).
-        K = 100 shard at U = 1024 (profiles/r4_tuning_log.md): fixed length edges 172.4 ms per EM iteration,
-        (8, 64) 133.2, (4, 32) 107.3, (2, 16) 106.7.  Documents of <= 256 words keep the 16-lane kernel
-        (gs_smallw: throughput); above, the one-wave range is a per-word chain of up to U refreshes per sweep,
-        where the 16-lane kernel's 7 digamma/exp chains per lane cost more latency per refresh than one wave's
-        2 (r5g: the bucket 66.4 ms on 16 lanes per document vs 43.1 ms on one wave)."""
-        w1, w4 = 2, 16
-        e1, e4 = max(256, w1 * U), max(2048, w4 * U)
-        return ((GS_TEAM8, e4, None), (GS_TEAM4, e1, e4), (GS_TEAM1, 256, e1), (GS_SMALL, None, 256))
+        Documents of <= 256 words keep the 16-lane kernel (gs_smallw: throughput); above, up to W = 4 words per
+        chunk, a per-word chain of up to U refreshes per sweep runs on one wave per document with a topic per
+        lane (gs_chain); four waves up to W = 16, eight beyond (never below the U = 32 edges).  K = 100 shard at
+        U = 1024 (profiles/r4_tuning_log.md): fixed length edges 172.4 ms per EM iteration, (8, 64) 133.2,
+        (4, 32) 107.3, (2, 16) 106.7 with the one-wave team as the first range; the 16-lane kernel's 7
+        digamma/exp chains per lane cost more latency per refresh than one wave's 2 (r5g: 66.4 vs 43.1 ms)."""
+        wc, w4 = 2, 16
+        ec, e4 = max(256, wc * U), max(2048, w4 * U)
+        return ((GS_TEAM8, e4, None), (GS_TEAM4, ec, e4), (GS_CHAIN, 256, ec), (GS_SMALL, None, 256))
 
     @staticmethod
     def isolate_longest(o, m: int, xcds: int = 8):

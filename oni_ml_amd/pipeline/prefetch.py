@@ -59,12 +59,14 @@ def take(key: tuple) -> Optional[object]:
 
 
 def load_dns_inputs(dns_path, feedback_path, dupfactor, strict, top1m, threads=8):
-    """(table, top-1m list, dns_pre's torch-free host features) -- the name parse and the two dictionary
-    encodes run here too, beside the torch import (dns_pre 0.41 s, 0.25 s of it these; profiles/r5_cold_start.md)."""
+    """(table, top-1m list, dns_pre's torch-free host features) -- the name parse, the two dictionary
+    encodes and the ECDF cuts of dns_pre and dns_post run here too, beside the torch import (dns_pre
+    0.41 s, 0.25 s of it the first three; the cuts 0.13 s on the device, first-use kernels included;
+    profiles/r5_cold_start.md)."""
     from ..features import dns_io
     tab = dns_io.load_dns(dns_path, feedback_path, dupfactor, strict=strict)
     top = dns_io.load_top_domains(top1m)
-    return tab, top, dns_io.host_features(tab, top, threads)
+    return tab, top, dns_io.host_features(tab, top, threads, cuts=True)
 
 
 # ---- DNS: a forked child process -------------------------------------------------------------------

@@ -61,7 +61,8 @@ def main():
     dc = eng.dc
     lens = c.lengths()
     its = eng.iters.cpu().numpy()
-    names = {H.GS_TINY: "tiny", H.GS_TEAM1: "team1", H.GS_TEAM4: "team4", H.GS_TEAM8: "team8", H.GS_SMALL: "small"}
+    names = {H.GS_TINY: "tiny", H.GS_TEAM1: "team1", H.GS_TEAM4: "team4", H.GS_TEAM8: "team8", H.GS_SMALL: "small",
+             H.GS_CHAIN: "chain"}
     out = dict(docs=c.num_docs, nnz=c.nnz, U=eng._U, buckets=[])
 
     def launch(var, order, dbg=None):
@@ -130,7 +131,7 @@ def main():
                                    entries=int(L.sum()), sweeps_mean=round(float(it.mean()), 2),
                                    sweeps_max=int(it.max()), ms=round(ms, 4),
                                    word_sweeps=int((L * it).sum())))
-        if a.phases and var not in (H.GS_TINY, H.GS_SMALL):
+        if a.phases and var not in (H.GS_TINY, H.GS_SMALL, H.GS_CHAIN):
             dbg = torch.zeros(16, dtype=torch.int64, device="cuda")
             launch(var, order, dbg)
             v = dbg.cpu().tolist()

@@ -198,3 +198,21 @@ def test_dns_post_features_reuse_pre_host(tmp_path):
         assert np.array_equal(np.asarray(a.host[k]), np.asarray(b.host[k])), k
     assert list(a.host["domains"]) == list(b.host["domains"])[:len(a.host["domains"])]
     assert list(a.host["subdomains"]) == list(b.host["subdomains"])[:len(a.host["subdomains"])]
+
+
+def test_host_cuts_match_device_rule():
+    """features/cuts_host.py (the DNS prefetch child's numpy cuts) == quantiles.ecdf_cuts == the literal
+    reference transcription, bit for bit, weighted and unweighted."""
+    import torch
+    from oni_ml_amd.features.cuts_host import ecdf_cuts_np
+    from oni_ml_amd.features.quantiles import DECILES, QUINTILES, ecdf_cuts, ecdf_cuts_reference
+    rng = np.random.default_rng(3)
+    for trial in range(12):
+        v = np.round(rng.random(3000) * rng.integers(1, 40), int(rng.integers(0, 3)))
+        w = rng.integers(1, 1000, v.size)
+        for q in (DECILES, QUINTILES):
+            a = ecdf_cuts_np(v, q, w)
+            assert np.array_equal(a, ecdf_cuts(torch.from_numpy(v), q, torch.from_numpy(w)).numpy())
+            assert np.array_equal(a, ecdf_cuts_reference(v, q, w))
+            assert np.array_equal(ecdf_cuts_np(v, q), ecdf_cuts(torch.from_numpy(v), q).numpy())
+    assert np.array_equal(ecdf_cuts_np(np.zeros(0), DECILES), np.zeros(len(DECILES)))
