@@ -820,13 +820,40 @@ template <int KS, int NW>
 struct TeamShape {
   static constexpr int DPB = (NW == 1 && KS <= 32) ? 4 : 1;   // documents per workgroup
   static constexpr int NTD = NW * 64;                          // threads per document
-  static constexpr int TG = tg_of(KS), KPL = kpl_of(KS);
+  static constexpr int TG = tg_of(KS);
+  // PAIR (TG = 16, KS > 64): a lane holds topic PAIRS 2q, 2q + 1 (+ 32 per pair) and loads each pair with one
+  // 16-byte load -- half the load instructions of one topic per 8-byte lane; the row gathers of the K = 100
+  // team kernels are issue-bound (a chunk's prefetch issue 2.5-4.5 k cycles, profiles/r5_k100.md)
+  static constexpr bool PAIR = TG == 16;
+  static constexpr int KPL = PAIR ? 2 * ((KS + 2 * TG - 1) / (2 * TG)) : kpl_of(KS);
   static constexpr int NSW = 64 / TG;                          // word slots per wave
   static constexpr int LSW = ilog2(NSW);
   static constexpr int NS = NW * NSW;                          // word slots per document
   static constexpr int TO = (KS + NTD - 1) / NTD;              // topics owned per thread
   static constexpr int RMAX = NW >= 8 ? (KPL <= 5 ? 8 : 4) : 1; // prefetched words per slot per chunk (even)
 };
+
+// topic of a lane's i-th value in the team layouts (TeamShape::PAIR: consecutive pairs)
+template <int TG, bool PAIR>
+__device__ __forceinline__ int tk(int q, int i) { return PAIR ? 2 * q + (i & 1) + 2 * TG * (i >> 1) : q + TG * i; }
+
+// a word's KPL values of this lane at constant offsets (lanes past KS read into the next row: beta's pad row)
+template <int KS, int KPL, int TG, bool PAIR>
+__device__ __forceinline__ void load_row(const double* __restrict__ beta, int w, int q, double (&b)[KPL]) {
+  if constexpr (PAIR) {
+    const dvec2* r = reinterpret_cast<const dvec2*>(beta + (size_t)w * KS + 2 * q);
+#pragma unroll
+    for (int ii = 0; ii < KPL / 2; ++ii) {
+      const dvec2 v = r[TG * ii];
+      b[2 * ii] = v.x;
+      b[2 * ii + 1] = v.y;
+    }
+  } else {
+    const double* brow = beta + (size_t)w * KS + q;
+#pragma unroll
+    for (int i = 0; i < KPL; ++i) b[i] = brow[TG * i];
+  }
+}
 
 // N words of the word phase, interleaved (independent dependency chains): P = sum_k E_k b_k over
 // the TG lanes of each slot, r = c / P, acc += r b, lw += c log P.  A word with c == 0 (no word in
@@ -856,7 +883,7 @@ __device__ __forceinline__ void word_steps(const double (&E)[KPL], const double 
 
 // RMAX streamed words of one slot (p0, p0 + NS, ...; past `end` counts 0 and re-reads a valid row):
 // ids, then rows, then the word steps, so a batch costs about one gather latency
-template <int RMAX, int KS, int KPL, int TG, int LSW>
+template <int RMAX, int KS, int KPL, int TG, int LSW, bool PAIR>
 __device__ __forceinline__ void stream_batch(const double* __restrict__ beta, const int* __restrict__ wrow,
                                              const float* __restrict__ crow, int p0, int end, int NS, int q,
                                              const double (&E)[KPL], double (&b)[RMAX][KPL], double (&acc)[KPL],
@@ -871,26 +898,23 @@ __device__ __forceinline__ void stream_batch(const double* __restrict__ beta, co
     c[r] = p < end ? (double)crow[pc] : 0.0;
   }
 #pragma unroll
-  for (int r = 0; r < RMAX; ++r) {
-    const double* brow = beta + (size_t)w[r] * KS + q;   // constant offsets (beta's pad row: gs_smallw)
-#pragma unroll
-    for (int i = 0; i < KPL; ++i) b[r][i] = brow[TG * i];
-  }
+  for (int r = 0; r < RMAX; ++r) load_row<KS, KPL, TG, PAIR>(beta, w[r], q, b[r]);
   word_steps<RMAX, KPL, LSW>(E, b, c, acc, lw);
 }
 
 // the streamed tail of one slot: full batches while >= 2 rounds remain, the last round alone (a
 // lone word in a full batch paid RMAX rows and word steps; measured on the split kernel)
-template <int RMAX, int KS, int KPL, int TG, int LSW>
+template <int RMAX, int KS, int KPL, int TG, int LSW, bool PAIR>
 __device__ __forceinline__ void stream_tail(const double* __restrict__ beta, const int* __restrict__ wrow,
                                             const float* __restrict__ crow, int p0, int end, int NS, int q,
                                             const double (&E)[KPL], double (&b)[RMAX][KPL], double (&acc)[KPL],
                                             double& lw) {
   int p = p0;
-  for (; p + NS < end; p += RMAX * NS) stream_batch<RMAX, KS, KPL, TG, LSW>(beta, wrow, crow, p, end, NS, q, E, b, acc, lw);
+  for (; p + NS < end; p += RMAX * NS)
+    stream_batch<RMAX, KS, KPL, TG, LSW, PAIR>(beta, wrow, crow, p, end, NS, q, E, b, acc, lw);
   if (p < end) {
     double b1[1][KPL];
-    stream_batch<1, KS, KPL, TG, LSW>(beta, wrow, crow, p, end, NS, q, E, b1, acc, lw);
+    stream_batch<1, KS, KPL, TG, LSW, PAIR>(beta, wrow, crow, p, end, NS, q, E, b1, acc, lw);
   }
 }
 
@@ -902,6 +926,7 @@ __global__ __launch_bounds__(team_threads(KS, NW), MINW) void gs_team(GSArgs a) 
   using T = TeamShape<KS, NW>;
   constexpr int DPB = T::DPB, NTD = T::NTD, TG = T::TG, KPL = T::KPL, NSW = T::NSW, LSW = T::LSW, NS = T::NS,
                 TO = T::TO, RMAX = T::RMAX;
+  constexpr bool PAIR = T::PAIR;
   // GM (one-wave documents at KS > 32, and every team size when GMT: U > kGsUMax refreshes per
   // sweep): the chunk tables live in the document's own c*phi rows instead of LDS (2 x 32 x KS
   // doubles of LDS held one wave per CU to ~3 waves; U chunks of them do not fit at all): C_j in
@@ -1027,9 +1052,7 @@ __global__ __launch_bounds__(team_threads(KS, NW), MINW) void gs_team(GSArgs a) 
     if (!active) return;   // wave-uniform: waves without words of a chunk gather no rows
 #pragma unroll
     for (int r = 0; r < RMAX; ++r) {
-      const double* brow = a.beta + (size_t)w[r] * KS + q;   // constant offsets (beta's pad row: gs_smallw)
-#pragma unroll
-      for (int i = 0; i < KPL; ++i) bc[r][i] = brow[TG * i];
+      load_row<KS, KPL, TG, PAIR>(a.beta, w[r], q, bc[r]);   // constant offsets (beta's pad row: gs_smallw)
     }
   };
   if (nch > 0) {
@@ -1066,7 +1089,7 @@ __global__ __launch_bounds__(team_threads(KS, NW), MINW) void gs_team(GSArgs a) 
         double E[KPL], acc[KPL];
 #pragma unroll
         for (int i = 0; i < KPL; ++i) {
-          E[i] = (q + TG * i < KS) ? E_[q + TG * i] : 0.0;
+          E[i] = (tk<TG, PAIR>(q, i) < KS) ? E_[tk<TG, PAIR>(q, i)] : 0.0;
           acc[i] = 0.0;
         }
         // rounds of this chunk (team-uniform): pairs of words in flight per slot
@@ -1081,7 +1104,7 @@ __global__ __launch_bounds__(team_threads(KS, NW), MINW) void gs_team(GSArgs a) 
         // words beyond the prefetched rounds (documents longer than RMAX * NS * U): streamed in
         // batches of RMAX rows per slot with a batch's loads in flight together (bc is free until
         // the next chunk's prefetch below); one row at a time left the word phase latency-bound
-        stream_tail<RMAX, KS, KPL, TG, LSW>(a.beta, wrow, crow, n0 + slot + RMAX * NS, n1, NS, q, E, bc, acc, lw);
+        stream_tail<RMAX, KS, KPL, TG, LSW, PAIR>(a.beta, wrow, crow, n0 + slot + RMAX * NS, n1, NS, q, E, bc, acc, lw);
         // next chunk's rows (its ids landed during the word phase)
         load_rows(wc);
         tick(0);
@@ -1094,7 +1117,7 @@ __global__ __launch_bounds__(team_threads(KS, NW), MINW) void gs_team(GSArgs a) 
         if (sl == 0) {
 #pragma unroll
           for (int i = 0; i < KPL; ++i)
-            if (q + TG * i < KS) sRed[ds][wv][q + TG * i] = acc[i];
+            if (tk<TG, PAIR>(q, i) < KS) sRed[ds][wv][tk<TG, PAIR>(q, i)] = acc[i];
         }
         tick(1);
       }
@@ -1209,7 +1232,7 @@ __global__ __launch_bounds__(team_threads(KS, NW), MINW) void gs_team(GSArgs a) 
       const double* er = a.cphi + (size_t)(s0 + n0 + 1) * KS;
       double E[KPL];
 #pragma unroll
-      for (int i = 0; i < KPL; ++i) E[i] = (q + TG * i < KS) ? er[q + TG * i] : 0.0;
+      for (int i = 0; i < KPL; ++i) E[i] = (tk<TG, PAIR>(q, i) < KS) ? er[tk<TG, PAIR>(q, i)] : 0.0;
       __syncthreads();
       if (active) {
         for (int p = n0 + slot; p < n1; p += NS) {
@@ -1217,7 +1240,7 @@ __global__ __launch_bounds__(team_threads(KS, NW), MINW) void gs_team(GSArgs a) 
           const double c = (double)crow[p];
           double b[KPL];
 #pragma unroll
-          for (int i = 0; i < KPL; ++i) b[i] = (q + TG * i < KS) ? brow[q + TG * i] : 0.0;
+          for (int i = 0; i < KPL; ++i) b[i] = (tk<TG, PAIR>(q, i) < KS) ? brow[tk<TG, PAIR>(q, i)] : 0.0;
           double pp = 0.0;
 #pragma unroll
           for (int i = 0; i < KPL; ++i) pp = fma(E[i], b[i], pp);
@@ -1225,7 +1248,7 @@ __global__ __launch_bounds__(team_threads(KS, NW), MINW) void gs_team(GSArgs a) 
           double* row = a.cphi + (size_t)(s0 + p) * KS;
 #pragma unroll
           for (int i = 0; i < KPL; ++i)
-            if (q + TG * i < KS) __builtin_nontemporal_store(E[i] * b[i] * r, &row[q + TG * i]);
+            if (tk<TG, PAIR>(q, i) < KS) __builtin_nontemporal_store(E[i] * b[i] * r, &row[tk<TG, PAIR>(q, i)]);
         }
       }
     }
@@ -1241,17 +1264,17 @@ __global__ __launch_bounds__(team_threads(KS, NW), MINW) void gs_team(GSArgs a) 
       if (n1 - n0 < 2) continue;
       const double* er = a.cphi + (size_t)(s0 + n0 + 1) * KS;
 #pragma unroll
-      for (int i = 0; i < KPL; ++i) E[i] = (q + TG * i < KS) ? er[q + TG * i] : 0.0;
+      for (int i = 0; i < KPL; ++i) E[i] = (tk<TG, PAIR>(q, i) < KS) ? er[tk<TG, PAIR>(q, i)] : 0.0;
     } else {
 #pragma unroll
-      for (int i = 0; i < KPL; ++i) E[i] = (q + TG * i < KS) ? Et[j][q + TG * i] : 0.0;
+      for (int i = 0; i < KPL; ++i) E[i] = (tk<TG, PAIR>(q, i) < KS) ? Et[j][tk<TG, PAIR>(q, i)] : 0.0;
     }
     for (int p = n0 + slot; p < n1; p += NS) {
       const double* brow = a.beta + (size_t)wrow[p] * KS;
       const double c = (double)crow[p];
       double b[KPL];
 #pragma unroll
-      for (int i = 0; i < KPL; ++i) b[i] = (q + TG * i < KS) ? brow[q + TG * i] : 0.0;
+      for (int i = 0; i < KPL; ++i) b[i] = (tk<TG, PAIR>(q, i) < KS) ? brow[tk<TG, PAIR>(q, i)] : 0.0;
       double pp = 0.0;
 #pragma unroll
       for (int i = 0; i < KPL; ++i) pp = fma(E[i], b[i], pp);
@@ -1259,7 +1282,7 @@ __global__ __launch_bounds__(team_threads(KS, NW), MINW) void gs_team(GSArgs a) 
       double* row = a.cphi + (size_t)(s0 + p) * KS;
 #pragma unroll
       for (int i = 0; i < KPL; ++i)
-        if (q + TG * i < KS) __builtin_nontemporal_store(E[i] * b[i] * r, &row[q + TG * i]);
+        if (tk<TG, PAIR>(q, i) < KS) __builtin_nontemporal_store(E[i] * b[i] * r, &row[tk<TG, PAIR>(q, i)]);
     }
   }
 }
@@ -1349,6 +1372,7 @@ __global__ __launch_bounds__(512) void gs_splitw(GSArgs a, SplitArgs sp) {
   using T = TeamShape<KS, 8>;   // word-slot geometry and prefetch depth of the 8-wave team
   constexpr int NW = 7, NTD = (NW + 1) * 64, TG = T::TG, KPL = T::KPL, NSW = T::NSW, LSW = T::LSW, NS = NW * NSW,
                 RMAX = T::RMAX;
+  constexpr bool PAIR = T::PAIR;
   constexpr int NC = KS + 1;                 // exchanged columns: KS topic sums + the log-sum
   constexpr int GR = 2 * NC;                 // granules per segment row
   constexpr int TC = (NC + 63) / 64;         // columns per topic-wave lane
@@ -1622,9 +1646,7 @@ __global__ __launch_bounds__(512) void gs_splitw(GSArgs a, SplitArgs sp) {
     for (int r = 0; r < RMAX; ++r) {
       // unconditional, constant offsets: a round past the range re-reads a valid row of the document
       // and carries count 0 (beta's pad row covers topic lanes past KS: gs_smallw)
-      const double* brow = a.beta + (size_t)w[r] * KS + q;
-#pragma unroll
-      for (int i = 0; i < KPL; ++i) bc[r][i] = brow[TG * i];
+      load_row<KS, KPL, TG, PAIR>(a.beta, w[r], q, bc[r]);
     }
   };
   load_ids(0, wc, cc, vc);
@@ -1640,7 +1662,7 @@ __global__ __launch_bounds__(512) void gs_splitw(GSArgs a, SplitArgs sp) {
         double E[KPL], acc[KPL], lw = 0.0;
 #pragma unroll
         for (int i = 0; i < KPL; ++i) {
-          E[i] = (q + TG * i < KS) ? sE[q + TG * i] : 0.0;
+          E[i] = (tk<TG, PAIR>(q, i) < KS) ? sE[tk<TG, PAIR>(q, i)] : 0.0;
           acc[i] = 0.0;
         }
         double cr[RMAX];
@@ -1656,14 +1678,14 @@ __global__ __launch_bounds__(512) void gs_splitw(GSArgs a, SplitArgs sp) {
         } else {
           word_steps<RMAX, KPL, LSW>(E, bc, cr, acc, lw);
         }
-        stream_tail<RMAX, KS, KPL, TG, LSW>(a.beta, wrow, crow, m0 + slot + RMAX * NS, m1, NS, q, E, bc, acc, lw);
+        stream_tail<RMAX, KS, KPL, TG, LSW, PAIR>(a.beta, wrow, crow, m0 + slot + RMAX * NS, m1, NS, q, E, bc, acc, lw);
 #pragma unroll
         for (int i = 0; i < KPL; ++i) acc[i] = bits_sum<0, LSW, false>(acc[i]);
         lw = group_sum<64>(q == 0 ? lw : 0.0);
         if (sl == 0) {
 #pragma unroll
           for (int i = 0; i < KPL; ++i)
-            if (q + TG * i < KS) sRed[wv][q + TG * i] = acc[i];
+            if (tk<TG, PAIR>(q, i) < KS) sRed[wv][tk<TG, PAIR>(q, i)] = acc[i];
         }
         if (lane == 0) sRedL[wv] = lw;
         // arrival (LDS only: no vmcnt wait), then the next chunk's rows -- beside the exchange
@@ -1705,7 +1727,7 @@ __global__ __launch_bounds__(512) void gs_splitw(GSArgs a, SplitArgs sp) {
     double E[KPL];
 #pragma unroll
     for (int i = 0; i < KPL; ++i) {
-      const int k = q + TG * i;
+      const int k = tk<TG, PAIR>(q, i);
       E[i] = k < KS ? (GM ? tab[(size_t)j * 2 * KS + KS + k] : sEt[j][kc_(k)]) : 0.0;
     }
     for (int p = m0 + slot; p < m1; p += NS) {
@@ -1713,7 +1735,7 @@ __global__ __launch_bounds__(512) void gs_splitw(GSArgs a, SplitArgs sp) {
       const double c = (double)crow[p];
       double bv[KPL];
 #pragma unroll
-      for (int i = 0; i < KPL; ++i) bv[i] = (q + TG * i < KS) ? brow[q + TG * i] : 0.0;
+      for (int i = 0; i < KPL; ++i) bv[i] = (tk<TG, PAIR>(q, i) < KS) ? brow[tk<TG, PAIR>(q, i)] : 0.0;
       double pp = 0.0;
 #pragma unroll
       for (int i = 0; i < KPL; ++i) pp = fma(E[i], bv[i], pp);
@@ -1721,7 +1743,7 @@ __global__ __launch_bounds__(512) void gs_splitw(GSArgs a, SplitArgs sp) {
       double* row = a.cphi + (size_t)(s0 + p) * KS;
 #pragma unroll
       for (int i = 0; i < KPL; ++i)
-        if (q + TG * i < KS) __builtin_nontemporal_store(E[i] * bv[i] * r, &row[q + TG * i]);
+        if (tk<TG, PAIR>(q, i) < KS) __builtin_nontemporal_store(E[i] * bv[i] * r, &row[tk<TG, PAIR>(q, i)]);
     }
   }
 }
