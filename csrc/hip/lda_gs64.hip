@@ -57,6 +57,28 @@ constexpr int tiny_tg(int KS) { return KS <= 32 ? 8 : 16; }
 constexpr int tiny_kpl(int KS) { return (KS + tiny_tg(KS) - 1) / tiny_tg(KS); }
 constexpr int tiny_max(int KS) { return tiny_kpl(KS) <= 4 ? 8 : 4; }
 
+// topic of a lane's i-th value in the team layouts (TeamShape::PAIR: consecutive pairs)
+template <int TG, bool PAIR>
+__device__ __forceinline__ int tk(int q, int i) { return PAIR ? 2 * q + (i & 1) + 2 * TG * (i >> 1) : q + TG * i; }
+
+// a word's KPL values of this lane at constant offsets (lanes past KS read into the next row: beta's pad row)
+template <int KS, int KPL, int TG, bool PAIR>
+__device__ __forceinline__ void load_row(const double* __restrict__ beta, int w, int q, double (&b)[KPL]) {
+  if constexpr (PAIR) {
+    const dvec2* r = reinterpret_cast<const dvec2*>(beta + (size_t)w * KS + 2 * q);
+#pragma unroll
+    for (int ii = 0; ii < KPL / 2; ++ii) {
+      const dvec2 v = r[TG * ii];
+      b[2 * ii] = v.x;
+      b[2 * ii + 1] = v.y;
+    }
+  } else {
+    const double* brow = beta + (size_t)w * KS + q;
+#pragma unroll
+    for (int i = 0; i < KPL; ++i) b[i] = brow[TG * i];
+  }
+}
+
 // ------------------------------------------------------------------ tiny ----
 // C[j][.] (the current contribution of word j) is a register queue: word j always
 // uses C[0], then the queue rotates left by one with the new value at the back, so
@@ -600,7 +622,10 @@ __device__ __forceinline__ void quad_word_steps(const double (&E)[KPL], const do
 template <int KS, int RQ, int MINW = 1>
 __global__ __launch_bounds__(256, MINW) void gs_smallw(GSArgs a) {
   static_assert(KS > 32, "gs_smallw: KS > 32 (gs_small covers KS <= 32)");
-  constexpr int TG = 16, KPL = (KS + TG - 1) / TG;
+  // topic pairs per lane with 16-byte row loads (TeamShape::PAIR): KPL = 2 ceil(KS / 32)
+  constexpr bool PAIR = KS % 32 != 0;   // KS = 128: the same 8 topics per lane either way, and the pair
+                                        // layout spilled at 2 waves per SIMD
+  constexpr int TG = 16, KPL = PAIR ? 2 * ((KS + 2 * TG - 1) / (2 * TG)) : (KS + TG - 1) / TG;
   if (a.params[kParamDone] != 0.0) return;
   const int t = threadIdx.x, q = t & (TG - 1);
   const int item = blockIdx.x * (256 / TG) + t / TG;
@@ -634,7 +659,7 @@ __global__ __launch_bounds__(256, MINW) void gs_smallw(GSArgs a) {
     total += cs;
 #pragma unroll
     for (int i = 0; i < KPL; ++i) {
-      const int k = q + TG * i;
+      const int k = tk<TG, PAIR>(q, i);
       if (k < KS) rows[(size_t)n0 * KS + k] = k < K ? cs / K : 0.0;
     }
   }
@@ -643,7 +668,7 @@ __global__ __launch_bounds__(256, MINW) void gs_smallw(GSArgs a) {
   double gam[KPL], psi[KPL], E[KPL], Cn[KPL];
 #pragma unroll
   for (int i = 0; i < KPL; ++i) {
-    const int k = q + TG * i;
+    const int k = tk<TG, PAIR>(q, i);
     gam[i] = k < K ? g0 : 0.0;
     psi[i] = m;
     E[i] = k < K ? 1.0 : 0.0;
@@ -665,10 +690,8 @@ __global__ __launch_bounds__(256, MINW) void gs_smallw(GSArgs a) {
   auto head_rows = [&]() {
 #pragma unroll
     for (int r = 0; r < RQ; ++r) {
-      const double* brow = a.beta + (size_t)wn[r] * KS + q;
       cq[r] = (double)cn[r];
-#pragma unroll
-      for (int i = 0; i < KPL; ++i) bq[r][i] = brow[TG * i];
+      load_row<KS, KPL, TG, PAIR>(a.beta, wn[r], q, bq[r]);
     }
   };
   head_ids(0);
@@ -691,10 +714,8 @@ __global__ __launch_bounds__(256, MINW) void gs_smallw(GSArgs a) {
 #pragma unroll
         for (int r = 0; r < RQ; ++r) {
           const int pc = min(p0 + r, n1 - 1);
-          const double* brow = a.beta + (size_t)wrow[pc] * KS + q;
           c[r] = p0 + r < n1 ? (double)crow[pc] : 0.0;
-#pragma unroll
-          for (int i = 0; i < KPL; ++i) bq[r][i] = brow[TG * i];
+          load_row<KS, KPL, TG, PAIR>(a.beta, wrow[pc], q, bq[r]);
         }
         quad_word_steps<RQ, KPL>(E, bq, c, acc, lw);
       }
@@ -706,8 +727,8 @@ __global__ __launch_bounds__(256, MINW) void gs_smallw(GSArgs a) {
       // this chunk's C_j (and E_j) rows; lanes past KS exist only in the last topic group (static test)
 #pragma unroll
       for (int i = 0; i < KPL; ++i) {
-        const int k = q + TG * i;
-        if (TG * (i + 1) <= KS || k < KS) {
+        const int k = tk<TG, PAIR>(q, i);
+        if (k < KS) {
           rows[(size_t)n0 * KS + k] = E[i] * acc[i];
           if (two) rows[(size_t)(n0 + 1) * KS + k] = E[i];
         }
@@ -717,7 +738,7 @@ __global__ __launch_bounds__(256, MINW) void gs_smallw(GSArgs a) {
       // keep psi = m, E = 0, gamma = 0: nw = 0 there)
 #pragma unroll
       for (int i = 0; i < KPL; ++i) {
-        const bool real = q + TG * i < K;
+        const bool real = tk<TG, PAIR>(q, i) < K;
         const double nw = E[i] * acc[i];
         lp = fma(psi[i], nw, lp);
         gam[i] += nw - Cn[i];
@@ -729,14 +750,14 @@ __global__ __launch_bounds__(256, MINW) void gs_smallw(GSArgs a) {
       // C of the next chunk, after this chunk's row stores (nch == 1: the same row)
 #pragma unroll
       for (int i = 0; i < KPL; ++i) {
-        const int k = q + TG * i;
-        Cn[i] = (TG * (i + 1) <= KS || k < KS) ? rows[(size_t)j1 * W * KS + k] : 0.0;
+        const int k = tk<TG, PAIR>(q, i);
+        Cn[i] = (k < KS) ? rows[(size_t)j1 * W * KS + k] : 0.0;
       }
     }
     double gs = 0.0, lg = 0.0;
 #pragma unroll
     for (int i = 0; i < KPL; ++i) {
-      const bool real = q + TG * i < K;
+      const bool real = tk<TG, PAIR>(q, i) < K;
       const double l = lgamma_pos(real ? gam[i] : 1.0);
       gs += real ? gam[i] : 0.0;
       lg += real ? l : 0.0;
@@ -751,7 +772,7 @@ __global__ __launch_bounds__(256, MINW) void gs_smallw(GSArgs a) {
   double ps = 0.0;
 #pragma unroll
   for (int i = 0; i < KPL; ++i) {
-    const int k = q + TG * i;
+    const int k = tk<TG, PAIR>(q, i);
     if (k < K) ps += psi[i];
     if (k < KS) a.gamma[(size_t)d * KS + k] = gam[i];
   }
@@ -770,7 +791,7 @@ __global__ __launch_bounds__(256, MINW) void gs_smallw(GSArgs a) {
     double Ej[KPL];
 #pragma unroll
     for (int i = 0; i < KPL; ++i) {
-      const int k = q + TG * i;
+      const int k = tk<TG, PAIR>(q, i);
       Ej[i] = k < KS ? rows[(size_t)(n0 + 1) * KS + k] : 0.0;
     }
     for (int p0 = n0; p0 < n1; p0 += RQ) {
@@ -778,10 +799,8 @@ __global__ __launch_bounds__(256, MINW) void gs_smallw(GSArgs a) {
 #pragma unroll
       for (int r = 0; r < RQ; ++r) {
         const int pc = min(p0 + r, n1 - 1);
-        const double* brow = a.beta + (size_t)wrow[pc] * KS + q;
         c[r] = (double)crow[pc];
-#pragma unroll
-        for (int i = 0; i < KPL; ++i) b[r][i] = brow[TG * i];
+        load_row<KS, KPL, TG, PAIR>(a.beta, wrow[pc], q, b[r]);
       }
 #pragma unroll
       for (int r = 0; r < RQ; ++r) {
@@ -795,7 +814,7 @@ __global__ __launch_bounds__(256, MINW) void gs_smallw(GSArgs a) {
         double* row = rows + (size_t)(p0 + r) * KS;
 #pragma unroll
         for (int i = 0; i < KPL; ++i) {
-          const int k = q + TG * i;
+          const int k = tk<TG, PAIR>(q, i);
           if (k < KS) __builtin_nontemporal_store(Ej[i] * b[r][i] * rr, &row[k]);
         }
       }
@@ -821,10 +840,10 @@ struct TeamShape {
   static constexpr int DPB = (NW == 1 && KS <= 32) ? 4 : 1;   // documents per workgroup
   static constexpr int NTD = NW * 64;                          // threads per document
   static constexpr int TG = tg_of(KS);
-  // PAIR (TG = 16, KS > 64): a lane holds topic PAIRS 2q, 2q + 1 (+ 32 per pair) and loads each pair with one
+  // PAIR (TG >= 8, KS > 32): a lane holds topic PAIRS 2q, 2q + 1 (+ 2 TG per pair) and loads each pair with one
   // 16-byte load -- half the load instructions of one topic per 8-byte lane; the row gathers of the K = 100
   // team kernels are issue-bound (a chunk's prefetch issue 2.5-4.5 k cycles, profiles/r5_k100.md)
-  static constexpr bool PAIR = TG == 16;
+  static constexpr bool PAIR = TG >= 8;
   static constexpr int KPL = PAIR ? 2 * ((KS + 2 * TG - 1) / (2 * TG)) : kpl_of(KS);
   static constexpr int NSW = 64 / TG;                          // word slots per wave
   static constexpr int LSW = ilog2(NSW);
@@ -832,28 +851,6 @@ struct TeamShape {
   static constexpr int TO = (KS + NTD - 1) / NTD;              // topics owned per thread
   static constexpr int RMAX = NW >= 8 ? (KPL <= 5 ? 8 : 4) : 1; // prefetched words per slot per chunk (even)
 };
-
-// topic of a lane's i-th value in the team layouts (TeamShape::PAIR: consecutive pairs)
-template <int TG, bool PAIR>
-__device__ __forceinline__ int tk(int q, int i) { return PAIR ? 2 * q + (i & 1) + 2 * TG * (i >> 1) : q + TG * i; }
-
-// a word's KPL values of this lane at constant offsets (lanes past KS read into the next row: beta's pad row)
-template <int KS, int KPL, int TG, bool PAIR>
-__device__ __forceinline__ void load_row(const double* __restrict__ beta, int w, int q, double (&b)[KPL]) {
-  if constexpr (PAIR) {
-    const dvec2* r = reinterpret_cast<const dvec2*>(beta + (size_t)w * KS + 2 * q);
-#pragma unroll
-    for (int ii = 0; ii < KPL / 2; ++ii) {
-      const dvec2 v = r[TG * ii];
-      b[2 * ii] = v.x;
-      b[2 * ii + 1] = v.y;
-    }
-  } else {
-    const double* brow = beta + (size_t)w * KS + q;
-#pragma unroll
-    for (int i = 0; i < KPL; ++i) b[i] = brow[TG * i];
-  }
-}
 
 // N words of the word phase, interleaved (independent dependency chains): P = sum_k E_k b_k over
 // the TG lanes of each slot, r = c / P, acc += r b, lw += c log P.  A word with c == 0 (no word in
@@ -2647,7 +2644,7 @@ static void gs_estep_ks(const GSArgs& a, int variant, hipStream_t s) {
       if constexpr (KS <= 32)
         hipLaunchKernelGGL((gs::gs_small<KS>), dim3((a.n_items + 15) / 16), dim3(256), 0, s, a);
       else
-        hipLaunchKernelGGL((gs::gs_smallw<KS, 2, 2>), dim3((a.n_items + 15) / 16), dim3(256), 0, s, a);
+        hipLaunchKernelGGL((gs::gs_smallw<KS, 2, (KS > 100 ? 1 : 2)>), dim3((a.n_items + 15) / 16), dim3(256), 0, s, a);
       break;
     }
     case kGsChain:
