@@ -404,6 +404,8 @@ template <int KS, int D>
 __global__ __launch_bounds__(256) void gs_chain(GSArgs a) {
   static_assert(KS > 32 && KS <= 128, "gs_chain: 32 < KS <= 128");
   constexpr int TC = (KS + 63) / 64;
+  // TC = 2: lane l holds the topic pair 2l, 2l + 1 and loads it with one 16-byte load (KS even)
+  constexpr bool PAIR = TC == 2;
   if (a.params[kParamDone] != 0.0) return;
   const int lane = threadIdx.x & 63;
   const int item = blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -422,7 +424,18 @@ __global__ __launch_bounds__(256) void gs_chain(GSArgs a) {
   const int* __restrict__ wrow = a.word_idx + s0;
   const float* __restrict__ crow = a.counts + s0;
   double* __restrict__ rows = a.cphi + (size_t)s0 * KS;
-  auto owned = [&](int o) { return 64 * (o + 1) <= KS || lane + 64 * o < KS; };   // static but the last group
+  auto topic = [&](int o) -> int { return PAIR ? 2 * lane + o : lane + 64 * o; };
+  auto owned = [&](int o) { return topic(o) < KS; };
+  // a word's TC values of this lane (lanes past KS read into the next row: beta's pad row)
+  auto row_of = [&](int w, double (&v)[TC]) {
+    if constexpr (PAIR) {
+      const dvec2 x = *reinterpret_cast<const dvec2*>(a.beta + (size_t)w * KS + 2 * lane);
+      v[0] = x.x;
+      v[1] = x.y;
+    } else {
+      v[0] = a.beta[(size_t)w * KS + lane];
+    }
+  };
   double total = 0.0;
   for (int j = 0; j < nch; ++j) {
     const int n0 = j * W, n1 = min(n, n0 + W);
@@ -431,14 +444,14 @@ __global__ __launch_bounds__(256) void gs_chain(GSArgs a) {
     total += cs;
 #pragma unroll
     for (int o = 0; o < TC; ++o)
-      if (owned(o)) rows[(size_t)n0 * KS + lane + 64 * o] = lane + 64 * o < K ? cs / K : 0.0;
+      if (owned(o)) rows[(size_t)n0 * KS + topic(o)] = topic(o) < K ? cs / K : 0.0;
   }
   const double g0 = alpha + total / K;
   const double m = psi_only(g0);
   double gam[TC], psi[TC], E[TC], Cn[TC], acc[TC];
 #pragma unroll
   for (int o = 0; o < TC; ++o) {
-    const int k = lane + 64 * o;
+    const int k = topic(o);
     gam[o] = k < K ? g0 : 0.0;
     psi[o] = m;
     E[o] = k < K ? 1.0 : 0.0;
@@ -453,9 +466,7 @@ __global__ __launch_bounds__(256) void gs_chain(GSArgs a) {
 #pragma unroll
   for (int t = 0; t < D; ++t) {
     const int p = t % n;
-    const double* brow = a.beta + (size_t)wrow[p] * KS + lane;
-#pragma unroll
-    for (int o = 0; o < TC; ++o) rb[t][o] = brow[64 * o];
+    row_of(wrow[p], rb[t]);
     rc[t] = (double)crow[p];
     const int p2 = (t + D) % n;
     wi[t] = wrow[p2];
@@ -484,9 +495,7 @@ __global__ __launch_bounds__(256) void gs_chain(GSArgs a) {
         for (int o = 0; o < TC; ++o) acc[o] = fma(r, rb[t][o], acc[o]);
         // the slot's next row (word pw + D) and the id D words beyond it
         {
-          const double* brow = a.beta + (size_t)wi[t] * KS + lane;
-#pragma unroll
-          for (int o = 0; o < TC; ++o) rb[t][o] = brow[64 * o];
+          row_of(wi[t], rb[t]);
           rc[t] = (double)wc[t];
           const int p2 = g2 % n;
           wi[t] = wrow[p2];
@@ -500,13 +509,13 @@ __global__ __launch_bounds__(256) void gs_chain(GSArgs a) {
 #pragma unroll
           for (int o = 0; o < TC; ++o) {
             if (owned(o)) {
-              rows[(size_t)n0 * KS + lane + 64 * o] = E[o] * acc[o];
-              if (two) rows[(size_t)(n0 + 1) * KS + lane + 64 * o] = E[o];
+              rows[(size_t)n0 * KS + topic(o)] = E[o] * acc[o];
+              if (two) rows[(size_t)(n0 + 1) * KS + topic(o)] = E[o];
             }
           }
 #pragma unroll
           for (int o = 0; o < TC; ++o) {
-            const bool real = lane + 64 * o < K;
+            const bool real = topic(o) < K;
             const double nw = E[o] * acc[o];
             lp = fma(psi[o], nw, lp);
             gam[o] = real ? gam[o] + (nw - Cn[o]) : gam[o];
@@ -519,13 +528,13 @@ __global__ __launch_bounds__(256) void gs_chain(GSArgs a) {
           j = j + 1 < nch ? j + 1 : 0;
           cend = min(n, (j + 1) * W);
 #pragma unroll
-          for (int o = 0; o < TC; ++o) Cn[o] = owned(o) ? rows[(size_t)j * W * KS + lane + 64 * o] : 0.0;
+          for (int o = 0; o < TC; ++o) Cn[o] = owned(o) ? rows[(size_t)j * W * KS + topic(o)] : 0.0;
           if (pw == n) {
             // sweep end: lda-c's likelihood and convergence test
             double gs = 0.0, lg = 0.0;
 #pragma unroll
             for (int o = 0; o < TC; ++o) {
-              const bool real = lane + 64 * o < K;
+              const bool real = topic(o) < K;
               const double l = lgamma_pos(real ? gam[o] : 1.0);
               gs += real ? gam[o] : 0.0;
               lg += real ? l : 0.0;
@@ -548,7 +557,7 @@ __global__ __launch_bounds__(256) void gs_chain(GSArgs a) {
   double ps = 0.0;
 #pragma unroll
   for (int o = 0; o < TC; ++o) {
-    const int k = lane + 64 * o;
+    const int k = topic(o);
     if (k < K) ps += psi[o];
     if (owned(o)) a.gamma[(size_t)d * KS + k] = gam[o];
   }
@@ -565,19 +574,16 @@ __global__ __launch_bounds__(256) void gs_chain(GSArgs a) {
     if (n1 - n0 < 2) continue;
     double Ej[TC];
 #pragma unroll
-    for (int o = 0; o < TC; ++o) Ej[o] = owned(o) ? rows[(size_t)(n0 + 1) * KS + lane + 64 * o] : 0.0;
+    for (int o = 0; o < TC; ++o) Ej[o] = owned(o) ? rows[(size_t)(n0 + 1) * KS + topic(o)] : 0.0;
     for (int p = n0; p < n1; ++p) {
-      const double* brow = a.beta + (size_t)wrow[p] * KS + lane;
       double b[TC], pp = 0.0;
+      row_of(wrow[p], b);
 #pragma unroll
-      for (int o = 0; o < TC; ++o) {
-        b[o] = brow[64 * o];
-        pp = fma(Ej[o], b[o], pp);
-      }
+      for (int o = 0; o < TC; ++o) pp = fma(Ej[o], b[o], pp);
       const double rr = (double)crow[p] * drcp(group_sum<64>(pp));
 #pragma unroll
       for (int o = 0; o < TC; ++o)
-        if (owned(o)) __builtin_nontemporal_store(Ej[o] * b[o] * rr, &rows[(size_t)p * KS + lane + 64 * o]);
+        if (owned(o)) __builtin_nontemporal_store(Ej[o] * b[o] * rr, &rows[(size_t)p * KS + topic(o)]);
     }
   }
 }
@@ -622,9 +628,9 @@ __device__ __forceinline__ void quad_word_steps(const double (&E)[KPL], const do
 template <int KS, int RQ, int MINW = 1>
 __global__ __launch_bounds__(256, MINW) void gs_smallw(GSArgs a) {
   static_assert(KS > 32, "gs_smallw: KS > 32 (gs_small covers KS <= 32)");
-  // topic pairs per lane with 16-byte row loads (TeamShape::PAIR): KPL = 2 ceil(KS / 32)
-  constexpr bool PAIR = KS % 32 != 0;   // KS = 128: the same 8 topics per lane either way, and the pair
-                                        // layout spilled at 2 waves per SIMD
+  // one topic per 8-byte lane: the pair layout (TeamShape::PAIR) measured slower here (K = 100 bucket 9.48 vs
+  // 8.99 ms, r5s: 8 topics per lane instead of 7 and 235 vs 196 VGPRs), the 16-lane kernel being refresh-bound
+  constexpr bool PAIR = false;
   constexpr int TG = 16, KPL = PAIR ? 2 * ((KS + 2 * TG - 1) / (2 * TG)) : (KS + TG - 1) / TG;
   if (a.params[kParamDone] != 0.0) return;
   const int t = threadIdx.x, q = t & (TG - 1);

@@ -6,4 +6,5 @@ timeout -k 10 300 python -u bench.py --topics 100 --events 12500000 --steps 10 -
 timeout -k 10 300 python -u bench.py --topics 50 --steps 20 --warmup 5 --converge 0 > gpurun_out/r5s/bench_k50.json 2> gpurun_out/r5s/bench_k50.err && \
 timeout -k 10 300 python -u bench.py --topics 50 --gs-updates 64 --steps 20 --warmup 5 --converge 0 > gpurun_out/r5s/bench_k50_u64.json 2> gpurun_out/r5s/bench_k50_u64.err && \
 TAG=r5s KEEP_GOING=0 PMC="SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_WAIT_INST_ANY GRBM_GUI_ACTIVE;TCC_HIT_sum TCC_MISS_sum" \
-PMC_MATCH="gs_" PMC_ARGS="--topics 100 --events 12500000 --steps 3 --warmup 1 --converge 0" bash scripts/gpu.sh pmc > gpurun_out/r5s/pmc.log 2>&1
+PMC_MATCH="gs_" PMC_ARGS="--topics 100 --events 12500000 --steps 3 --warmup 1 --converge 0" bash scripts/gpu.sh pmc > gpurun_out/r5s/pmc.log 2>&1 && \
+timeout -k 10 300 python -u scripts/bench_gs64.py --topics 100 --events 12500000 --gs-updates 1024 > gpurun_out/r5s/k100_u1024.log 2>&1
