@@ -447,10 +447,11 @@ class LDAEngine:
         gp, dc, dev = self.gs_plan, self.dc, self.device
         if len(gp.plan) + (gp.split is not None) < 2:
             return None
-        if gp.split is not None:
+        key = self._late_key(gp)
+        if key == "split":
             late = np.asarray(sorted(gp.split.segments), np.int64)
         else:
-            o = gp.plan[0][1].cpu().numpy()
+            o = gp.plan[key][1].cpu().numpy()
             late = o[o >= 0].astype(np.int64)
         force = self.suff_split == "force"
         if late.size == 0 or (not force and dc.doc_len[late].sum() > 0.6 * max(1, int(dc.doc_len.sum()))):
@@ -465,6 +466,21 @@ class LDAEngine:
             self._suff_part = torch.zeros(need, self._suff_part.shape[1], dtype=torch.float64, device=dev)
         return dict(wpE=wpE, ceE=ceE, planE=planE, wpL=wpL, ceL=ceL, planL=planL,
                     cw_early=torch.zeros_like(self.cw), late_docs=int(late.size))
+
+    @staticmethod
+    def _late_key(gp):
+        """The bucket the late suff-stats pass waits for (it runs alone on streams[1]; the early pass covers
+        every other bucket's words): the one expected to finish last.  At K > 32 that is the 8-wave team
+        when there is one -- the split documents (dispatched first, co-resident) finished at 9.9 ms of a
+        30.6 ms K = 100 iteration and the 8-wave team last, so with the split as the late bucket both passes
+        ran after everything (profiles/r5q_k100_timeline.txt) -- else the split, else plan[0] (the
+        longest-document bucket at K <= 32)."""
+        from ...ops import hip as H
+        if gp.KS > 32:
+            for i, (var, _) in enumerate(gp.plan):
+                if var == H.GS_TEAM8:
+                    return i
+        return "split" if gp.split is not None else 0
 
     def _launch_estep64(self, newton_key=None, phase: str = "all"):
         """fp64 E-step: length buckets on 4 streams (longest first), one join, then the CSC
@@ -555,16 +571,25 @@ class LDAEngine:
         work = list(gp.plan)
         if gp.split is not None:
             work.insert(0, ("split", gp.split.batches))
-        # no other bucket may share late_s (with 6 work items the round robin would put item 4 there
-        # and the early pass would read its cphi rows before they are written)
+        # the late bucket (_late_key) runs alone on late_s = streams[1]: no other bucket may share it (the
+        # early pass would read their cphi rows before they are written); the others round-robin over the
+        # remaining streams in dispatch order
         late_s = streams[1] if late else None
+        key = self._late_key(gp)
+        late_i = 0 if key == "split" else key + (gp.split is not None)
+        others = [x for x in streams[1:] if x is not late_s] + [main]
         # a c.phi window: the buffer's first e1 - e0 rows hold the window's entries
         cphi = self.cphi if win is None else self.cphi[:win["e1"] - win["e0"]]
         ent_base = None if win is None else win["e0"]
+        oi = 0
         for si, (var, order) in zip(range(len(work)), work):
-            s = streams[(si + 1) % len(streams)] if si < len(work) - 1 else main
-            if si > 0 and s is late_s:
-                s = streams[2]
+            if late and si == late_i:
+                s = late_s
+            else:
+                # the tiny bucket (last) follows the split / first side-stream bucket instead of queueing
+                # behind the 16-lane bucket on the main stream: K = 100 shard 29.4 -> see r5u
+                s = others[oi % len(others)]
+                oi += 1
             if s is not main and s not in used:
                 s.wait_event(self._ev_fork)
                 used.append(s)

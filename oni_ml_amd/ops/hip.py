@@ -794,6 +794,7 @@ class GSPlan:
     def __init__(self, lengths, KS: int, gs_updates: int, device, split_min: Optional[int] = None,
                  doc_range=None, xsplit: Optional[dict] = None):
         import numpy as np
+        self.KS = int(KS)
         L = np.asarray(lengths, dtype=np.int64)
         # doc_range (d0, d1): only documents d0 <= d < d1 (one c.phi window of the engine); the stable
         # sort of the range equals the range's documents in the stable sort of all of them
