@@ -2397,7 +2397,11 @@ __global__ __launch_bounds__(256) void gs_suff64(const int* __restrict__ word_pt
                                                  const double* __restrict__ lik, const double* __restrict__ ass,
                                                  int lo, int hi, const double* gate,
                                                  const double* cw_base) {
-  constexpr int TG = tg_of(KS), KPL = kpl_of(KS), NSLOT = 256 / TG;
+  // one topic per lane: the paired 16-byte loads of the team kernels measured slower here (K = 100 early
+  // pass 2.06 -> 2.62 ms, r5v); the c.phi pad row (em.py) is kept so PAIR stays a one-line switch
+  constexpr int TG = tg_of(KS), NSLOT = 256 / TG;
+  constexpr bool PAIR = false;
+  constexpr int KPL = PAIR ? 2 * ((KS + 2 * TG - 1) / (2 * TG)) : kpl_of(KS);
   __shared__ double sAcc[NSLOT][KS];
   __shared__ double sRow[16][KS];
   if (gated(gate)) return;
@@ -2441,29 +2445,24 @@ __global__ __launch_bounds__(256) void gs_suff64(const int* __restrict__ word_pt
     int e = word_ptr[w] + sidx;
     const int end = word_ptr[w + 1];
     for (; e + 3 * S < end; e += 4 * S) {
-      const double* rr[4];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) rr[u] = cphi + (size_t)csc_ent[e + u * S] * KS;
       double v[4][KPL];
 #pragma unroll
-      for (int u = 0; u < 4; ++u)
-#pragma unroll
-        for (int i = 0; i < KPL; ++i) v[u][i] = (q + TG * i < KS) ? rr[u][q + TG * i] : 0.0;
+      for (int u = 0; u < 4; ++u) load_row<KS, KPL, TG, PAIR>(cphi, csc_ent[e + u * S], q, v[u]);
 #pragma unroll
       for (int u = 0; u < 4; ++u)
 #pragma unroll
         for (int i = 0; i < KPL; ++i) acc[i] += v[u][i];
     }
     for (; e < end; e += S) {
-      const double* rr = cphi + (size_t)csc_ent[e] * KS;
+      double v[KPL];
+      load_row<KS, KPL, TG, PAIR>(cphi, csc_ent[e], q, v);
 #pragma unroll
-      for (int i = 0; i < KPL; ++i)
-        if (q + TG * i < KS) acc[i] += rr[q + TG * i];
+      for (int i = 0; i < KPL; ++i) acc[i] += v[i];
     }
   }
 #pragma unroll
   for (int i = 0; i < KPL; ++i)
-    if (q + TG * i < KS) sAcc[t / TG][q + TG * i] = acc[i];
+    if (tk<TG, PAIR>(q, i) < KS) sAcc[t / TG][tk<TG, PAIR>(q, i)] = acc[i];
   __syncthreads();
   const int ngroups = 256 / G;
   for (int idx = t; idx < ngroups * KS; idx += 256) {

@@ -324,7 +324,8 @@ class LDAEngine:
         self._stages = self._build_stages(corpus, KS)
         self.cw = torch.zeros(V, KS, dtype=f64, device=dev)
         self.gamma = torch.zeros(D, KS, dtype=f64, device=dev)
-        self.cphi = torch.zeros(max(rows, 1), KS, dtype=f64, device=dev)[:rows]
+        # one pad row past the last entry: the suff-stats kernel's paired row loads (KS > 32) may read into it
+        self.cphi = torch.zeros(rows + 1, KS, dtype=f64, device=dev)[:rows]
         self.lik = torch.zeros(D, dtype=f64, device=dev)
         self.ass = torch.zeros(D, dtype=f64, device=dev)
         self.iters = torch.zeros(D, dtype=torch.int32, device=dev)

@@ -395,12 +395,13 @@ def gs_stage(beta, word_idx, st: "GSStage", gate=None):
                    _chk(st.buf, torch.float64, "stage", None, dev), int(KS), _gate_ptr(gate, dev), _stream())
 
 
-def _need_pad_row(beta):
+def _need_pad_row(t):
     """The E-step kernels load a row's topic lanes at constant offsets: lanes past KS read into the next
-    row, the last row's into one zero pad row past the vocabulary (LDAEngine allocates [V + 1, KS])."""
-    V, KS = beta.shape
-    if beta.untyped_storage().nbytes() < (beta.storage_offset() + (V + 1) * KS) * beta.element_size():
-        raise ValueError("beta needs a zero pad row past its last row ([V + 1, KS] storage, view [:V])")
+    row, the last row's into one pad row past the table (LDAEngine allocates beta as [V + 1, KS] and the
+    c.phi rows as [nnz + 1, KS], and hands the kernels the views without it)."""
+    V, KS = t.shape
+    if t.untyped_storage().nbytes() < (t.storage_offset() + (V + 1) * KS) * t.element_size():
+        raise ValueError("the table needs a pad row past its last row ([n + 1, KS] storage, view [:n])")
 
 
 def gs_estep(doc_ptr, word_idx, counts, order, beta, K, gs_updates, params, gamma, cphi, lik, alpha_ss, iters, variant,
@@ -460,6 +461,8 @@ def gs_suff64(word_ptr, csc_ent, plan: "SuffPlan", cphi, cw, part, gate=None, sc
         raise ValueError("csc_ent longer than the corpus")
     if part.dim() != 2 or part.shape[1] != KS + 2 or part.shape[0] < max(plan.n_blocks, 1):
         raise ValueError(f"part: shape {tuple(part.shape)}, expected [>= {plan.n_blocks}, {KS + 2}]")
+    if KS > 32:
+        _need_pad_row(cphi)        # paired row loads read up to one row past the last entry
     if scalars is None:
         lik = ass = 0
         lo = hi = 0

@@ -1,0 +1,6 @@
+# suff-stats back to one topic per lane: gs64 tests; K = 100 shard and 100 M-event benches; K = 50 flow day; headline bench
+mkdir -p gpurun_out/r5w
+timeout -k 10 500 python -u -m pytest tests/test_gs64.py -x -v --timeout 120 --timeout-method thread > gpurun_out/r5w/pytest.log 2>&1 && \
+timeout -k 10 300 python -u bench.py --topics 100 --events 12500000 --steps 10 --warmup 3 --converge 0 > gpurun_out/r5w/bench_k100.json 2> gpurun_out/r5w/bench_k100.err && \
+timeout -k 10 500 python -u bench.py --topics 100 --events 100000000 --steps 5 --warmup 2 --converge 0 > gpurun_out/r5w/bench_k100_100m.json 2> gpurun_out/r5w/bench_k100_100m.err && \
+timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 > gpurun_out/r5w/bench_k20.json 2> gpurun_out/r5w/bench_k20.err
