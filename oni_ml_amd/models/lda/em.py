@@ -448,6 +448,8 @@ class LDAEngine:
         gp, dc, dev = self.gs_plan, self.dc, self.device
         if len(gp.plan) + (gp.split is not None) < 2:
             return None
+        if gp.KS > 32:
+            return self._build_suff_groups()
         key = self._late_key(gp)
         if key == "split":
             late = np.asarray(sorted(gp.split.segments), np.int64)
@@ -468,6 +470,116 @@ class LDAEngine:
         return dict(wpE=wpE, ceE=ceE, planE=planE, wpL=wpL, ceL=ceL, planL=planL,
                     cw_early=torch.zeros_like(self.cw), late_docs=int(late.size))
 
+    def _stream_slots(self, gp, late: bool) -> list:
+        """Stream of every work item ([split] + gp.plan) as _launch_buckets dispatches them: 0 = the current
+        stream, i >= 1 = self._streams[i - 1].  late: the _late_key bucket alone on stream 1, the others
+        round-robin over the remaining side streams and then the current stream."""
+        n = len(gp.plan) + (gp.split is not None)
+        key = self._late_key(gp)
+        late_i = 0 if key == "split" else key + (gp.split is not None)
+        others = [i for i in range(1, len(self._streams) + 1) if not (late and i == 1)] + [0]
+        out, oi = [], 0
+        for si in range(n):
+            if late and si == late_i:
+                out.append(1)
+            else:
+                out.append(others[oi % len(others)])
+                oi += 1
+        return out
+
+    def _build_suff_groups(self):
+        """Per-stream sufficient statistics (KS > 32): each stream's suff-stats pass runs on that stream as
+        soon as its own buckets are done, so only the last-finishing stream's pass (and a short combine)
+        follows the E-step, whichever stream that is (the K = 100 shard: the 8-wave team; 100 M events:
+        the tiny bucket, which waits behind the split documents: 18.5 ms of suff-stats after the E-step,
+        profiles/r5y_100m/timeline.txt).
+
+        A word whose entries all lie in one stream's documents gets its class_word row from that stream's
+        pass directly; the other words' per-stream rows go to a scratch (compact CSC per stream) and the
+        combine pass -- one more gs_suff64 over a CSC of scratch rows in stream order -- sums them.  The
+        sum order is fixed by the plan, never by which stream finishes first: bitwise reproducible.
+        class_total's partial rows come from the direct rows and the combine only."""
+        import numpy as np
+        from ...ops import hip as H
+        gp, dc, dev = self.gs_plan, self.dc, self.device
+        slots = self._stream_slots(gp, late=True)
+        work_docs = []
+        if gp.split is not None:
+            work_docs.append(np.asarray(sorted(gp.split.segments), np.int64))
+        for _, order in gp.plan:
+            o = order.cpu().numpy()
+            work_docs.append(o[o >= 0].astype(np.int64))
+        keys = sorted(set(slots))
+        if len(keys) < 2:
+            return None
+        V = self.V
+        groups, lens = [], []
+        for k in keys:
+            docs = np.concatenate([d for d, sl in zip(work_docs, slots) if sl == k])
+            mask = torch.zeros(self.D, dtype=torch.bool, device=dev)
+            mask[torch.from_numpy(docs).to(dev)] = True
+            wp, ce, ln = H.csc_subset(dc.word_ptr, dc.csc_ent, dc.csc_doc, mask)
+            groups.append(dict(slot=k, wp=wp, ce=ce))
+            lens.append(ln.astype(np.int64))
+        present = np.stack([ln > 0 for ln in lens])
+        nper = present.sum(0)
+        multi = nper > 1
+        rows_off = 0
+        wcat, gcat, rcat = [], [], []
+        for gi, (g, ln) in enumerate(zip(groups, lens)):
+            uw = np.flatnonzero(present[gi] & ~multi)
+            if gi == 0:                                # words with no entry at all: zero rows, written once
+                uw = np.union1d(uw, np.flatnonzero(nper == 0))
+            g["plan_u"] = H.SuffPlan(ln, dev, words=uw) if uw.size else None
+            mw = np.flatnonzero(present[gi] & multi)
+            g["m"] = int(mw.size)
+            if mw.size:
+                g["wp_m"], g["ce_m"] = H.csc_compact(g["wp"], g["ce"], mw)
+                g["plan_m"] = H.SuffPlan(ln[mw], dev)
+                g["off"] = rows_off
+                wcat.append(mw), gcat.append(np.full(mw.size, gi)), rcat.append(rows_off + np.arange(mw.size))
+                rows_off += int(mw.size)
+            else:
+                g["plan_m"] = None
+        if rows_off == 0:
+            return None                                  # no word shared between streams: nothing to combine
+        w_all, g_all, r_all = np.concatenate(wcat), np.concatenate(gcat), np.concatenate(rcat)
+        o = np.lexsort((g_all, w_all))                   # by word, then stream order
+        cnt = np.bincount(w_all, minlength=V).astype(np.int64)
+        wp_c = np.zeros(V + 1, np.int64)
+        wp_c[1:] = np.cumsum(cnt)
+        comb = dict(wp=torch.from_numpy(wp_c.astype(np.int32)).to(dev),
+                    ce=torch.from_numpy(r_all[o].astype(np.int32)).to(dev),
+                    plan=H.SuffPlan(cnt, dev, words=np.flatnonzero(multi)))
+        # scratch rows of the shared words, one pad row past the last (KS > 32 row loads)
+        xs = torch.zeros(rows_off + 1, self.KS, dtype=torch.float64, device=dev)[:rows_off]
+        # partial rows: [direct passes | combine] are summed into class_total; the scratch passes' after them
+        nb = 0
+        for g in groups:
+            g["pu0"] = nb
+            nb += g["plan_u"].n_blocks if g["plan_u"] is not None else 0
+        comb["p0"] = nb
+        nsum = nb + comb["plan"].n_blocks
+        nb = nsum
+        for g in groups:
+            g["pm0"] = nb
+            nb += g["plan_m"].n_blocks if g["plan_m"] is not None else 0
+        if self._suff_part.shape[0] < nb:
+            self._suff_part = torch.zeros(nb, self._suff_part.shape[1], dtype=torch.float64, device=dev)
+        return dict(mode="groups", groups=groups, comb=comb, xs=xs, n_sum=nsum)
+
+    def _suff_group_passes(self, g, ss):
+        """One stream's suff-stats passes (on the current stream): its direct rows, then its shared words'
+        rows into the scratch."""
+        from ...ops import hip as H
+        gate, part = self._gate, self._suff_part
+        if g["plan_u"] is not None:
+            H.gs_suff64(g["wp"], g["ce"], g["plan_u"], self.cphi, self._cw_local,
+                        part[g["pu0"]:g["pu0"] + max(g["plan_u"].n_blocks, 1)], gate=gate)
+        if g["plan_m"] is not None:
+            H.gs_suff64(g["wp_m"], g["ce_m"], g["plan_m"], self.cphi, ss["xs"][g["off"]:g["off"] + g["m"]],
+                        part[g["pm0"]:g["pm0"] + max(g["plan_m"].n_blocks, 1)], gate=gate)
+
     @staticmethod
     def _late_key(gp):
         """The bucket the late suff-stats pass waits for (it runs alone on streams[1]; the early pass covers
@@ -478,9 +590,10 @@ class LDAEngine:
         longest-document bucket at K <= 32)."""
         from ...ops import hip as H
         if gp.KS > 32:
-            for i, (var, _) in enumerate(gp.plan):
-                if var == H.GS_TEAM8:
-                    return i
+            for want in (H.GS_TEAM8, H.GS_TEAM4):
+                for i, (var, _) in enumerate(gp.plan):
+                    if var == want:
+                        return i
         return "split" if gp.split is not None else 0
 
     def _launch_estep64(self, newton_key=None, phase: str = "all"):
@@ -509,10 +622,18 @@ class LDAEngine:
         # one rank, fused EM iteration: this launch's M-step refills the staged rows for the next E-step,
         # and this E-step uses the rows the previous M-step (or the batch's opening refill) left
         fused = newton_key is not None and phase == "all" and bool(self._fused_stages(gp))
-        used, late_s = self._launch_buckets(gp, ss is not None, fused_stage=fused)
+        grp = ss if (ss is not None and ss.get("mode") == "groups" and phase == "all") else None
+        used, late_s = self._launch_buckets(gp, ss is not None, fused_stage=fused, groups=grp)
         if phase == "estep":             # the document kernels only (final inference pass)
             return
         scal = (self.lik, self.ass, 0, self.lik.numel())
+        if grp is not None:
+            c = grp["comb"]
+            H.gs_suff64(c["wp"], c["ce"], c["plan"], grp["xs"], self._cw_local,
+                        self._suff_part[c["p0"]:c["p0"] + max(c["plan"].n_blocks, 1)], gate=gate, scalars=scal)
+            H.colsum_partials(self._suff_part, grp["n_sum"], self._red_local, gate=gate)
+            self._finish_suff64(newton_key, stages=self._fused_stages(gp) if fused else ())
+            return
         if late_s is not None:
             H.gs_suff64(ss["wpE"], ss["ceE"], ss["planE"], self.cphi, ss["cw_early"], self._suff_part, gate=gate)
             main.wait_event(self._ev_join[used.index(late_s)])
@@ -548,7 +669,7 @@ class LDAEngine:
         for st in self._fused_stages(self.gs_plan):
             H.gs_stage(self.beta, self.dc.word_idx, st, gate=self._gate)
 
-    def _launch_buckets(self, gp, late: bool = False, win=None, fused_stage: bool = False):
+    def _launch_buckets(self, gp, late: bool = False, win=None, fused_stage: bool = False, groups=None):
         """The document kernels of GSPlan ``gp`` on 4 streams, joined back into the current stream.
         late: work[0] (the longest-document bucket) stays un-joined on streams[1], returned as late_s,
         for the early / late suff-stats; win: one of the c.phi windows (``_cphi_windows``) -- the document
@@ -575,22 +696,16 @@ class LDAEngine:
         # the late bucket (_late_key) runs alone on late_s = streams[1]: no other bucket may share it (the
         # early pass would read their cphi rows before they are written); the others round-robin over the
         # remaining streams in dispatch order
-        late_s = streams[1] if late else None
-        key = self._late_key(gp)
-        late_i = 0 if key == "split" else key + (gp.split is not None)
-        others = [x for x in streams[1:] if x is not late_s] + [main]
+        # groups (the per-stream suff-stats, _build_suff_groups): every stream is joined after its passes
+        late_s = streams[1] if (late and groups is None) else None
+        # (the tiny bucket, last, follows the split / first side-stream bucket instead of queueing behind the
+        # 16-lane bucket on the main stream: K = 100 shard 29.4 -> see r5u)
+        slots = self._stream_slots(gp, late)
         # a c.phi window: the buffer's first e1 - e0 rows hold the window's entries
         cphi = self.cphi if win is None else self.cphi[:win["e1"] - win["e0"]]
         ent_base = None if win is None else win["e0"]
-        oi = 0
         for si, (var, order) in zip(range(len(work)), work):
-            if late and si == late_i:
-                s = late_s
-            else:
-                # the tiny bucket (last) follows the split / first side-stream bucket instead of queueing
-                # behind the 16-lane bucket on the main stream: K = 100 shard 29.4 -> see r5u
-                s = others[oi % len(others)]
-                oi += 1
+            s = streams[slots[si]]
             if s is not main and s not in used:
                 s.wait_event(self._ev_fork)
                 used.append(s)
@@ -604,6 +719,10 @@ class LDAEngine:
                     st = self._stages.get(id(order))
                     H.gs_estep(dc.doc_ptr, dc.word_idx, dc.counts, order, self.beta, self.K, self._U, prm,
                                self.gamma, cphi, self.lik, self.ass, self.iters, var, ent_base=ent_base, stage=st)
+        if groups is not None:
+            for g in groups["groups"]:
+                with torch.cuda.stream(streams[g["slot"]]):
+                    self._suff_group_passes(g, groups)
         # every bucket but work[0] is joined first and the early pass overlaps work[0]
         for j, s in enumerate(used):
             self._ev_join[j].record(s)

@@ -490,6 +490,21 @@ def csc_subset(word_ptr, csc_ent, csc_doc, doc_mask):
     return ptr.to(torch.int32), csc_ent[keep].contiguous(), cnt.cpu().numpy()
 
 
+def csc_compact(word_ptr, csc_ent, words):
+    """(word_ptr, csc_ent) of the CSC columns ``words`` (host ids), renumbered 0 .. len(words) - 1, slot
+    order kept (a compact sub-CSC for a gs_suff64 pass into a scratch of len(words) rows)."""
+    import numpy as np
+    dev = word_ptr.device
+    w = torch.from_numpy(np.asarray(words, np.int64)).to(dev)
+    st = word_ptr[w].long()
+    ln = word_ptr[w + 1].long() - st
+    ptr = torch.zeros(w.numel() + 1, dtype=torch.int64, device=dev)
+    ptr[1:] = torch.cumsum(ln, 0)
+    tot = int(ptr[-1])
+    idx = torch.repeat_interleave(st - ptr[:-1], ln) + torch.arange(tot, device=dev)
+    return ptr.to(torch.int32), csc_ent[idx].contiguous()
+
+
 def gs_mstep_control(cw, class_total, beta, K, scalars, params, ctl, hist, done_count, rows=None, newton=None,
                      stages=(), word_idx=None):
     """fp64 M-step (beta = cw / class_total, exp(-100) floor) + alpha Newton + device EM control step.

@@ -306,10 +306,11 @@ def test_split_documents_match_oracle(K, env, U, monkeypatch):
     assert torch.equal(g1, eng.gamma)
 
 
-@pytest.mark.parametrize("K,split_min", [(20, None), (100, None), (20, "3000")])
+@pytest.mark.parametrize("K,split_min", [(20, None), (100, None), (20, "3000"), (50, "3000")])
 def test_suff_split_matches_single_pass(K, split_min, monkeypatch):
     """Early / late sufficient statistics (the early pass overlaps the longest-document bucket, the late
-    pass adds its rows first) against the single CSC pass: class_word, class totals and likelihood.
+    pass adds its rows first; at KS > 32 one pass per stream plus the combine of the shared words) against
+    the single CSC pass: class_word, class totals and likelihood.
     split_min: split documents plus all five length buckets = 6 work items, more than the 4 streams
     (the case where a round-robin stream choice would put a bucket beside the late pass's stream)."""
     if split_min:
@@ -320,8 +321,10 @@ def test_suff_split_matches_single_pass(K, split_min, monkeypatch):
     for mode in ("off", "force"):
         eng, sc = _gpu_estep(c, K, lb, 0.45, LDASettings(var_max_iter=4), 32, suff_split=mode)
         assert (eng._suff_split is None) == (mode == "off")
+        if mode == "force" and K > 32:   # KS > 32: one pass per stream, shared words combined after
+            assert eng._suff_split["mode"] == "groups" and len(eng._suff_split["groups"]) >= 2
         if split_min:
-            assert eng.gs_plan.split is not None and len(eng.gs_plan.plan) + 1 >= 6, \
+            assert eng.gs_plan.split is not None and len(eng.gs_plan.plan) + 1 >= (6 if K <= 32 else 5), \
                 [v for v, _ in eng.gs_plan.plan]
         eng.e_step()                                   # graph replay of the same launch sequence
         torch.cuda.synchronize()
@@ -369,7 +372,7 @@ def test_final_pass_word_assignments_match_oracle(vconv):
         assert (z == ref).mean() > 0.999
 
 
-@pytest.mark.parametrize("K,split_min", [(20, None), (100, None), (20, "3000")])
+@pytest.mark.parametrize("K,split_min", [(20, None), (100, None), (20, "3000"), (50, "3000")])
 def test_cphi_windows_match_one_buffer(K, split_min, monkeypatch):
     """c.phi windows (the E-step in contiguous document windows sharing one small c.phi buffer, each
     window's suff-stats added in place) against the one-buffer engine: gamma bitwise (the document
@@ -379,7 +382,7 @@ def test_cphi_windows_match_one_buffer(K, split_min, monkeypatch):
         monkeypatch.setenv("ONI_GS_SPLIT_MIN", split_min)
     c = _edge_corpus(seed=5, max_len=9000)
     lb = _log_beta(c.num_terms, K, seed=9)
-    KS = 24 if K == 20 else 104
+    KS = {20: 24, 50: 52}.get(K, 104)
     budget_gb = (c.nnz // 3) * KS * 8 / 2**30          # ~3-4 windows
     out = []
     for gb in (None, budget_gb):
