@@ -521,36 +521,19 @@ class LDAEngine:
             wp, ce, ln = H.csc_subset(dc.word_ptr, dc.csc_ent, dc.csc_doc, mask)
             groups.append(dict(slot=k, wp=wp, ce=ce))
             lens.append(ln.astype(np.int64))
-        present = np.stack([ln > 0 for ln in lens])
-        nper = present.sum(0)
-        multi = nper > 1
-        rows_off = 0
-        wcat, gcat, rcat = [], [], []
-        for gi, (g, ln) in enumerate(zip(groups, lens)):
-            uw = np.flatnonzero(present[gi] & ~multi)
-            if gi == 0:                                # words with no entry at all: zero rows, written once
-                uw = np.union1d(uw, np.flatnonzero(nper == 0))
-            g["plan_u"] = H.SuffPlan(ln, dev, words=uw) if uw.size else None
-            mw = np.flatnonzero(present[gi] & multi)
-            g["m"] = int(mw.size)
+        gpl = H.suff_group_plan(lens, V)
+        if gpl is None:
+            return None                                  # no word shared between streams: nothing to combine
+        for g, ln, u, mw, off in zip(groups, lens, gpl["unique"], gpl["multi"], gpl["off"]):
+            g["plan_u"] = H.SuffPlan(ln, dev, words=u) if u.size else None
+            g["m"], g["off"], g["plan_m"] = int(mw.size), off, None
             if mw.size:
                 g["wp_m"], g["ce_m"] = H.csc_compact(g["wp"], g["ce"], mw)
                 g["plan_m"] = H.SuffPlan(ln[mw], dev)
-                g["off"] = rows_off
-                wcat.append(mw), gcat.append(np.full(mw.size, gi)), rcat.append(rows_off + np.arange(mw.size))
-                rows_off += int(mw.size)
-            else:
-                g["plan_m"] = None
-        if rows_off == 0:
-            return None                                  # no word shared between streams: nothing to combine
-        w_all, g_all, r_all = np.concatenate(wcat), np.concatenate(gcat), np.concatenate(rcat)
-        o = np.lexsort((g_all, w_all))                   # by word, then stream order
-        cnt = np.bincount(w_all, minlength=V).astype(np.int64)
-        wp_c = np.zeros(V + 1, np.int64)
-        wp_c[1:] = np.cumsum(cnt)
-        comb = dict(wp=torch.from_numpy(wp_c.astype(np.int32)).to(dev),
-                    ce=torch.from_numpy(r_all[o].astype(np.int32)).to(dev),
-                    plan=H.SuffPlan(cnt, dev, words=np.flatnonzero(multi)))
+        rows_off = gpl["rows"]
+        comb = dict(wp=torch.from_numpy(gpl["wp"].astype(np.int32)).to(dev),
+                    ce=torch.from_numpy(gpl["ce"].astype(np.int32)).to(dev),
+                    plan=H.SuffPlan(gpl["cnt"], dev, words=gpl["shared"]))
         # scratch rows of the shared words, one pad row past the last (KS > 32 row loads)
         xs = torch.zeros(rows_off + 1, self.KS, dtype=torch.float64, device=dev)[:rows_off]
         # partial rows: [direct passes | combine] are summed into class_total; the scratch passes' after them

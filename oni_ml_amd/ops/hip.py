@@ -490,6 +490,39 @@ def csc_subset(word_ptr, csc_ent, csc_doc, doc_mask):
     return ptr.to(torch.int32), csc_ent[keep].contiguous(), cnt.cpu().numpy()
 
 
+def suff_group_plan(lens, V: int):
+    """Host plan of the per-stream suff-stats (LDAEngine._build_suff_groups).  lens[g]: entries of each word
+    in stream g's documents.  Per stream: ``unique`` -- words whose entries all lie in g (stream 0 also
+    takes the words with no entry, written as zero rows), ``multi`` -- words shared with another stream,
+    whose rows go to scratch rows off[g] + i; the combine CSC (wp, ce) lists, per shared word, its scratch
+    rows in stream order.  None when no word is shared."""
+    import numpy as np
+    present = np.stack([np.asarray(ln) > 0 for ln in lens])
+    nper = present.sum(0)
+    multi = nper > 1
+    unique, mlist, off = [], [], []
+    rows = 0
+    wcat, gcat, rcat = [], [], []
+    for gi in range(len(lens)):
+        u = np.flatnonzero(present[gi] & ~multi)
+        if gi == 0:
+            u = np.union1d(u, np.flatnonzero(nper == 0))
+        mw = np.flatnonzero(present[gi] & multi)
+        unique.append(u), mlist.append(mw), off.append(rows)
+        if mw.size:
+            wcat.append(mw), gcat.append(np.full(mw.size, gi)), rcat.append(rows + np.arange(mw.size))
+            rows += int(mw.size)
+    if rows == 0:
+        return None
+    w_all, g_all, r_all = np.concatenate(wcat), np.concatenate(gcat), np.concatenate(rcat)
+    o = np.lexsort((g_all, w_all))                   # by word, then stream order
+    cnt = np.bincount(w_all, minlength=V).astype(np.int64)
+    wp = np.zeros(V + 1, np.int64)
+    wp[1:] = np.cumsum(cnt)
+    return dict(unique=unique, multi=mlist, off=off, rows=rows, wp=wp, ce=r_all[o], cnt=cnt,
+                shared=np.flatnonzero(multi))
+
+
 def csc_compact(word_ptr, csc_ent, words):
     """(word_ptr, csc_ent) of the CSC columns ``words`` (host ids), renumbered 0 .. len(words) - 1, slot
     order kept (a compact sub-CSC for a gs_suff64 pass into a scratch of len(words) rows)."""
