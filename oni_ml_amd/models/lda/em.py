@@ -121,6 +121,7 @@ class LDAEngine:
         if suff_split not in ("auto", "off", "force"):
             raise ValueError(f"suff_split must be auto | off | force, got {suff_split!r}")
         self.suff_split = suff_split
+        self.n_streams = max(2, int(streams))     # the E-step buckets' streams, the current one included
         self.xsplit = xsplit          # experimental XCD-split plan of the longest documents (ops/hip.py GSPlan)
         # the fused EM iteration's M-step launch refills the next E-step's staged rows (one rank); False: a
         # gs_stage launch before every E-step (tests/test_gs64.py pins the two bitwise equal)
@@ -331,7 +332,7 @@ class LDAEngine:
         self.iters = torch.zeros(D, dtype=torch.int32, device=dev)
         # (high-priority side streams for the longest-document buckets measured slower: 2.13 -> 2.40 ms
         # per EM iteration at K = 20, 3.33 -> 3.84 at K = 50; profiles/r3_tuning_log.md)
-        self._streams = [torch.cuda.Stream(device=dev) for _ in range(3)]
+        self._streams = [torch.cuda.Stream(device=dev) for _ in range(max(1, self.n_streams - 1))]
         self._red = torch.zeros(2 + KS, dtype=f64, device=dev)
         self._scalars = self._red[:2]
         self.class_total = self._red[2:]
@@ -349,7 +350,7 @@ class LDAEngine:
         self._ctlhist = torch.zeros(8 + H.HIST_COLS * self._hist_cap, dtype=f64, device=dev)
         self._ctl, self._hist = self._ctlhist[:8], self._ctlhist[8:]
         self._ev_fork = torch.cuda.Event()
-        self._ev_join = [torch.cuda.Event() for _ in range(4)]
+        self._ev_join = [torch.cuda.Event() for _ in range(len(self._streams) + 1)]
         self._graph = None
         self._mgraph, self._mgraph_key = None, None
         self._fgraphs, self._fgraph_key = {}, None
