@@ -4,6 +4,7 @@
 #pragma once
 #include "common.h"
 #include "kernels.h"
+#include "log_table.h"
 
 namespace oni {
 namespace gs {
@@ -66,11 +67,36 @@ __device__ __forceinline__ double fexp(double x) {
   return __builtin_amdgcn_ldexp(fma(c1, r8, c0), (int)k);
 }
 
+// Natural log of a positive normal double by table: y = 2^e m, m in [1, 2), i = the top 7 bits of m's
+// fraction, log y = e ln 2 + L_i + log1p(r), r = m inv_i - 1 (one fma, |r| <= 2^-8), log1p by a degree-6
+// polynomial (truncation < 3e-18).  inv_i / L_i = -log(inv_i): log_table.h (scripts/gen_log_table.py),
+// copied into the workgroup's LDS by log_table_fill.  <= 1 ulp for y >= 2 (host emulation with exact fma
+// over 6 .. 1e4: 0.65 ulp); near y = 1 the e ln 2 + L cancellation leaves ~1e-16 absolute error (flog keeps
+// the relative accuracy there).  17 VALU instructions and one ds_read_b128 against flog's ~36.
+__device__ __forceinline__ void log_table_fill(dvec2* __restrict__ s) {
+  for (int i = threadIdx.x; i < 128; i += blockDim.x) s[i] = dvec2{kLogTab[i][0], kLogTab[i][1]};
+}
+__device__ __forceinline__ double flog_t(double y, const dvec2* __restrict__ tab) {
+  const unsigned long long b = (unsigned long long)__double_as_longlong(y);
+  const unsigned hi = (unsigned)(b >> 32);
+  const dvec2 c = tab[(hi >> 13) & 127u];
+  const double mt = __longlong_as_double((long long)(((unsigned long long)((hi & 0x000FFFFFu) | 0x3FF00000u) << 32) |
+                                                     (b & 0xFFFFFFFFull)));
+  const double de = (double)((int)(hi >> 20) - 1023);
+  const double r = fma(mt, c.x, -1.0);
+  const double r2 = r * r;
+  const double q1 = fma(r, 0.33333333333333333, -0.5);
+  const double q3 = fma(r2, -0.16666666666666667, fma(r, 0.2, -0.25));
+  const double p = fma(r2 * r2, q3, fma(r2, q1, r));
+  return fma(de, 6.93147180369123816490e-01, fma(de, 1.90821492927058770002e-10, c.y + p));
+}
+
 // lda-c digamma (x + 6 shift, 4-term series, six recurrence terms) and
 // E = exp(psi - m).  The six reciprocals 1/(x+i) are (dA B + dB A) / (A B) with
 // A = x(x+1)(x+2), B = (x+3)(x+4)(x+5) (one reciprocal; A B < 1e54 for x < 1e9);
 // E = (x+6) exp(rest - m) does not wait on the log.
-__device__ __forceinline__ void psi_exp(double x, double m, double& psi, double& e) {
+template <bool TAB = false>
+__device__ __forceinline__ void psi_exp(double x, double m, double& psi, double& e, const dvec2* tab = nullptr) {
   const double y = x + 6.0;
   const double iy = drcp(y);
   const double z = iy * iy;
@@ -80,7 +106,7 @@ __device__ __forceinline__ void psi_exp(double x, double m, double& psi, double&
   const double ser = fma(fma(0.004166666666667, z, -0.003968253986254), z * z,
                          fma(0.008333333333333, z, -0.083333333333333)) * z;
   const double rest = fma(-0.5, iy, ser) - fma(dA, B, dB * A) * drcp(A * B);
-  psi = flog(y) + rest;
+  psi = (TAB ? flog_t(y, tab) : flog(y)) + rest;
   e = y * fexp(rest - m);
 }
 

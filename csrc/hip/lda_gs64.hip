@@ -118,7 +118,10 @@ __global__ __launch_bounds__(256) void gs_tiny(GSArgs a) {
   constexpr int BST = NMAX * KS + 1;   // odd stride in doubles: groups of a wave hit different banks
   __shared__ double sB[DPB][BST];
   __shared__ double sN[DPB][NMAX];
+  __shared__ dvec2 sLog[128];          // flog_t's table
   if (a.params[kParamDone] != 0.0) return;
+  log_table_fill(sLog);
+  __syncthreads();
   const int t = threadIdx.x, q = t & (TG - 1), g = t / TG;
   const int item = blockIdx.x * DPB + g;
   if (item >= a.n_items) return;   // whole TG groups leave together
@@ -173,7 +176,7 @@ __global__ __launch_bounds__(256) void gs_tiny(GSArgs a) {
       for (int i = 0; i < KPL; ++i) pp = fma(E[i], b[i], pp);
       const double P = bits_sum<0, LTG, false>(pp);
       const double r = c * drcp(P);
-      lw = fma(c, flog(P), lw);
+      lw = fma(c, flog_t(P, sLog), lw);
       // branch-free refresh: the KPL digamma/exp chains interleave (a topic-guarded psi_exp is a basic block
       // of its own and the chains ran one after another); padding topics have E = 0, so nw = 0, and keep
       // gamma = 0, psi = m, E = 0
@@ -185,7 +188,7 @@ __global__ __launch_bounds__(256) void gs_tiny(GSArgs a) {
         gam[i] += nw - C[0][i];
         C[0][i] = nw;
         double pn, en;
-        psi_exp(real ? gam[i] : 1.0, m, pn, en);
+        psi_exp<true>(real ? gam[i] : 1.0, m, pn, en, sLog);
         psi[i] = real ? pn : psi[i];
         E[i] = real ? en : 0.0;
       }
@@ -604,7 +607,7 @@ __global__ __launch_bounds__(256) void gs_chain(GSArgs a) {
 // meet E = 0 / are never stored -- the clamped index held two address VGPRs per load.
 template <int N, int KPL>
 __device__ __forceinline__ void quad_word_steps(const double (&E)[KPL], const double (*b)[KPL], const double* c,
-                                                double (&acc)[KPL], double& lw) {
+                                                double (&acc)[KPL], double& lw, const dvec2* __restrict__ tab) {
   double P[N];
 #pragma unroll
   for (int u = 0; u < N; ++u) {
@@ -619,7 +622,7 @@ __device__ __forceinline__ void quad_word_steps(const double (&E)[KPL], const do
   for (int u = 0; u < N; ++u) {
     const double Pu = c[u] > 0.0 ? P[u] : 1.0;
     const double r = c[u] * drcp(Pu);
-    lw = fma(c[u], flog(Pu), lw);
+    lw = fma(c[u], flog_t(Pu, tab), lw);
 #pragma unroll
     for (int i = 0; i < KPL; ++i) acc[i] = fma(r, b[u][i], acc[i]);
   }
@@ -632,7 +635,10 @@ __global__ __launch_bounds__(256, MINW) void gs_smallw(GSArgs a) {
   // 8.99 ms, r5s: 8 topics per lane instead of 7 and 235 vs 196 VGPRs), the 16-lane kernel being refresh-bound
   constexpr bool PAIR = false;
   constexpr int TG = 16, KPL = PAIR ? 2 * ((KS + 2 * TG - 1) / (2 * TG)) : (KS + TG - 1) / TG;
+  __shared__ dvec2 sLog[128];          // flog_t's table
   if (a.params[kParamDone] != 0.0) return;
+  log_table_fill(sLog);
+  __syncthreads();
   const int t = threadIdx.x, q = t & (TG - 1);
   const int item = blockIdx.x * (256 / TG) + t / TG;
   if (item >= a.n_items) return;   // whole 16-lane groups leave together
@@ -713,7 +719,7 @@ __global__ __launch_bounds__(256, MINW) void gs_smallw(GSArgs a) {
       double acc[KPL];
 #pragma unroll
       for (int i = 0; i < KPL; ++i) acc[i] = 0.0;
-      quad_word_steps<RQ, KPL>(E, bq, cq, acc, lw);
+      quad_word_steps<RQ, KPL>(E, bq, cq, acc, lw, sLog);
       // the rest of the chunk: batches of RQ rows, a batch's loads in flight together
       for (int p0 = n0 + RQ; p0 < n1; p0 += RQ) {
         double c[RQ];
@@ -723,7 +729,7 @@ __global__ __launch_bounds__(256, MINW) void gs_smallw(GSArgs a) {
           c[r] = p0 + r < n1 ? (double)crow[pc] : 0.0;
           load_row<KS, KPL, TG, PAIR>(a.beta, wrow[pc], q, bq[r]);
         }
-        quad_word_steps<RQ, KPL>(E, bq, c, acc, lw);
+        quad_word_steps<RQ, KPL>(E, bq, c, acc, lw, sLog);
       }
       // next chunk's head rows in flight during the refresh; ids of the one after
       const int j1 = j + 1 < nch ? j + 1 : 0;
@@ -749,7 +755,7 @@ __global__ __launch_bounds__(256, MINW) void gs_smallw(GSArgs a) {
         lp = fma(psi[i], nw, lp);
         gam[i] += nw - Cn[i];
         double p, e;
-        psi_exp(real ? gam[i] : 1.0, m, p, e);
+        psi_exp<true>(real ? gam[i] : 1.0, m, p, e, sLog);
         psi[i] = real ? p : psi[i];
         E[i] = real ? e : 0.0;
       }
