@@ -867,9 +867,9 @@ struct TeamShape {
 // N words of the word phase, interleaved (independent dependency chains): P = sum_k E_k b_k over
 // the TG lanes of each slot, r = c / P, acc += r b, lw += c log P.  A word with c == 0 (no word in
 // that round) contributes nothing (its P is replaced by 1 before the reciprocal).
-template <int N, int KPL, int LSW>
+template <int N, int KPL, int LSW, bool TAB = false>
 __device__ __forceinline__ void word_steps(const double (&E)[KPL], const double (*b)[KPL], const double* c,
-                                           double (&acc)[KPL], double& lw) {
+                                           double (&acc)[KPL], double& lw, const dvec2* tab = nullptr) {
   double P[N];
 #pragma unroll
   for (int u = 0; u < N; ++u) {
@@ -884,7 +884,7 @@ __device__ __forceinline__ void word_steps(const double (&E)[KPL], const double 
   for (int u = 0; u < N; ++u) {
     const double Pu = c[u] > 0.0 ? P[u] : 1.0;
     const double r = c[u] * drcp(Pu);
-    lw = fma(c[u], flog(Pu), lw);
+    lw = fma(c[u], TAB ? flog_t(Pu, tab) : flog(Pu), lw);
 #pragma unroll
     for (int i = 0; i < KPL; ++i) acc[i] = fma(r, b[u][i], acc[i]);
   }
@@ -892,11 +892,11 @@ __device__ __forceinline__ void word_steps(const double (&E)[KPL], const double 
 
 // RMAX streamed words of one slot (p0, p0 + NS, ...; past `end` counts 0 and re-reads a valid row):
 // ids, then rows, then the word steps, so a batch costs about one gather latency
-template <int RMAX, int KS, int KPL, int TG, int LSW, bool PAIR>
+template <int RMAX, int KS, int KPL, int TG, int LSW, bool PAIR, bool TAB = false>
 __device__ __forceinline__ void stream_batch(const double* __restrict__ beta, const int* __restrict__ wrow,
                                              const float* __restrict__ crow, int p0, int end, int NS, int q,
                                              const double (&E)[KPL], double (&b)[RMAX][KPL], double (&acc)[KPL],
-                                             double& lw) {
+                                             double& lw, const dvec2* tab = nullptr) {
   int w[RMAX];
   double c[RMAX];
 #pragma unroll
@@ -908,22 +908,22 @@ __device__ __forceinline__ void stream_batch(const double* __restrict__ beta, co
   }
 #pragma unroll
   for (int r = 0; r < RMAX; ++r) load_row<KS, KPL, TG, PAIR>(beta, w[r], q, b[r]);
-  word_steps<RMAX, KPL, LSW>(E, b, c, acc, lw);
+  word_steps<RMAX, KPL, LSW, TAB>(E, b, c, acc, lw, tab);
 }
 
 // the streamed tail of one slot: full batches while >= 2 rounds remain, the last round alone (a
 // lone word in a full batch paid RMAX rows and word steps; measured on the split kernel)
-template <int RMAX, int KS, int KPL, int TG, int LSW, bool PAIR>
+template <int RMAX, int KS, int KPL, int TG, int LSW, bool PAIR, bool TAB = false>
 __device__ __forceinline__ void stream_tail(const double* __restrict__ beta, const int* __restrict__ wrow,
                                             const float* __restrict__ crow, int p0, int end, int NS, int q,
                                             const double (&E)[KPL], double (&b)[RMAX][KPL], double (&acc)[KPL],
-                                            double& lw) {
+                                            double& lw, const dvec2* tab = nullptr) {
   int p = p0;
   for (; p + NS < end; p += RMAX * NS)
-    stream_batch<RMAX, KS, KPL, TG, LSW, PAIR>(beta, wrow, crow, p, end, NS, q, E, b, acc, lw);
+    stream_batch<RMAX, KS, KPL, TG, LSW, PAIR, TAB>(beta, wrow, crow, p, end, NS, q, E, b, acc, lw, tab);
   if (p < end) {
     double b1[1][KPL];
-    stream_batch<1, KS, KPL, TG, LSW, PAIR>(beta, wrow, crow, p, end, NS, q, E, b1, acc, lw);
+    stream_batch<1, KS, KPL, TG, LSW, PAIR, TAB>(beta, wrow, crow, p, end, NS, q, E, b1, acc, lw, tab);
   }
 }
 
@@ -950,7 +950,15 @@ __global__ __launch_bounds__(team_threads(KS, NW), MINW) void gs_team(GSArgs a) 
   __shared__ double sRed[DPB][NW][KS];       // per-wave slot sums
   __shared__ double sCs[DPB][UT];            // chunk count sums (GM: straight into the C_j rows)
   __shared__ double sScal[DPB][NW][4];       // per-wave sweep partials
+  // KS > 32: flog_t's table for the per-word log and the refresh (DPB == 1 there: the workgroup is one
+  // document, so every early return below is workgroup-uniform)
+  constexpr bool TAB = KS > 32;
+  __shared__ dvec2 sLog[TAB ? 128 : 1];
   if (a.params[kParamDone] != 0.0) return;
+  if constexpr (TAB) {
+    log_table_fill(sLog);
+    __syncthreads();
+  }
   const int t = threadIdx.x % NTD, ds = threadIdx.x / NTD;
   const int item = blockIdx.x * DPB + ds;
   if (item >= a.n_items) return;             // NW == 1: one wave per document (no block barriers)
@@ -1104,16 +1112,17 @@ __global__ __launch_bounds__(team_threads(KS, NW), MINW) void gs_team(GSArgs a) 
         // rounds of this chunk (team-uniform): pairs of words in flight per slot
         const int R = (n1 - n0 + NS - 1) / NS;
         if constexpr (RMAX == 1) {
-          word_steps<1, KPL, LSW>(E, bc, cr, acc, lw);
+          word_steps<1, KPL, LSW, TAB>(E, bc, cr, acc, lw, sLog);
         } else if (R > 2) {
-          word_steps<RMAX, KPL, LSW>(E, bc, cr, acc, lw);    // every round in flight at once
+          word_steps<RMAX, KPL, LSW, TAB>(E, bc, cr, acc, lw, sLog);    // every round in flight at once
         } else {
-          word_steps<2, KPL, LSW>(E, bc, cr, acc, lw);
+          word_steps<2, KPL, LSW, TAB>(E, bc, cr, acc, lw, sLog);
         }
         // words beyond the prefetched rounds (documents longer than RMAX * NS * U): streamed in
         // batches of RMAX rows per slot with a batch's loads in flight together (bc is free until
         // the next chunk's prefetch below); one row at a time left the word phase latency-bound
-        stream_tail<RMAX, KS, KPL, TG, LSW, PAIR>(a.beta, wrow, crow, n0 + slot + RMAX * NS, n1, NS, q, E, bc, acc, lw);
+        stream_tail<RMAX, KS, KPL, TG, LSW, PAIR, TAB>(a.beta, wrow, crow, n0 + slot + RMAX * NS, n1, NS, q, E, bc, acc,
+                                                        lw, sLog);
         // next chunk's rows (its ids landed during the word phase)
         load_rows(wc);
         tick(0);
@@ -1151,7 +1160,7 @@ __global__ __launch_bounds__(team_threads(KS, NW), MINW) void gs_team(GSArgs a) 
         lps[o] = fma(psi[o], nwv[o], lps[o]);
         gam[o] = real ? gam[o] + (nwv[o] - Cj) : gam[o];
         double pn, en;
-        psi_exp(real ? gam[o] : 1.0, m, pn, en);
+        psi_exp<TAB>(real ? gam[o] : 1.0, m, pn, en, sLog);
         psi[o] = real ? pn : psi[o];
         Env[o] = real ? en : 0.0;
       }
