@@ -409,7 +409,10 @@ __global__ __launch_bounds__(256) void gs_chain(GSArgs a) {
   constexpr int TC = (KS + 63) / 64;
   // TC = 2: lane l holds the topic pair 2l, 2l + 1 and loads it with one 16-byte load (KS even)
   constexpr bool PAIR = TC == 2;
+  __shared__ dvec2 sLog[128];      // flog_t's table
   if (a.params[kParamDone] != 0.0) return;
+  log_table_fill(sLog);
+  __syncthreads();
   const int lane = threadIdx.x & 63;
   const int item = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (item >= a.n_items) return;   // whole waves leave together
@@ -493,7 +496,7 @@ __global__ __launch_bounds__(256) void gs_chain(GSArgs a) {
         const double P = group_sum<64>(pp);
         const double c = rc[t];
         const double r = c * drcp(P);
-        lw = fma(c, flog(P), lw);
+        lw = fma(c, flog_t(P, sLog), lw);
 #pragma unroll
         for (int o = 0; o < TC; ++o) acc[o] = fma(r, rb[t][o], acc[o]);
         // the slot's next row (word pw + D) and the id D words beyond it
@@ -523,7 +526,7 @@ __global__ __launch_bounds__(256) void gs_chain(GSArgs a) {
             lp = fma(psi[o], nw, lp);
             gam[o] = real ? gam[o] + (nw - Cn[o]) : gam[o];
             double pn, en;
-            psi_exp(real ? gam[o] : 1.0, m, pn, en);
+            psi_exp<true>(real ? gam[o] : 1.0, m, pn, en, sLog);
             psi[o] = real ? pn : psi[o];
             E[o] = real ? en : 0.0;
             acc[o] = 0.0;
