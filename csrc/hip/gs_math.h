@@ -113,7 +113,8 @@ __device__ __forceinline__ void psi_exp(double x, double m, double& psi, double&
 // ln Gamma(x), x > 0: Stirling series at y = x + 6 (terms through 1/y^13, truncation
 // < 1e-13 absolute) and the recurrence lnG(x) = lnG(x + 6) - ln(x (x+1) ... (x+5)).
 // Same accuracy class as the libm lgamma lda-c calls, at a fraction of OCML's cost.
-__device__ __forceinline__ double lgamma_pos(double x) {
+template <bool TAB = false>
+__device__ __forceinline__ double lgamma_pos(double x, const dvec2* tab = nullptr) {
   const double y = x + 6.0;
   const double iy = drcp(y);
   const double z = iy * iy;
@@ -121,7 +122,10 @@ __device__ __forceinline__ double lgamma_pos(double x) {
                          0.00059523809523809524) * z + 0.00079365079365079365) * z - 0.0027777777777777778) * z +
                       0.083333333333333333) * iy;
   const double p = x * (x + 1.0) * (x + 2.0) * ((x + 3.0) * (x + 4.0) * (x + 5.0));
-  return (y - 0.5) * flog(y) - y + 0.91893853320467274 + ser - flog(p);
+  if constexpr (TAB)
+    return (y - 0.5) * flog_t(y, tab) - y + 0.91893853320467274 + ser - flog_t(p, tab);
+  else
+    return (y - 0.5) * flog(y) - y + 0.91893853320467274 + ser - flog(p);
 }
 
 __device__ __forceinline__ double psi_only(double x) {

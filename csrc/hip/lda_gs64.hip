@@ -204,7 +204,7 @@ __global__ __launch_bounds__(256) void gs_tiny(GSArgs a) {
     for (int i = 0; i < KPL; ++i) {
       if (q + TG * i < K) {
         gs += gam[i];
-        lg += lgamma_pos(gam[i]);
+        lg += lgamma_pos<true>(gam[i], sLog);
       }
     }
     GS = bits_sum<0, LTG, false>(gs);
@@ -541,7 +541,7 @@ __global__ __launch_bounds__(256) void gs_chain(GSArgs a) {
 #pragma unroll
             for (int o = 0; o < TC; ++o) {
               const bool real = topic(o) < K;
-              const double l = lgamma_pos(real ? gam[o] : 1.0);
+              const double l = lgamma_pos<true>(real ? gam[o] : 1.0, sLog);
               gs += real ? gam[o] : 0.0;
               lg += real ? l : 0.0;
             }
@@ -773,7 +773,7 @@ __global__ __launch_bounds__(256, MINW) void gs_smallw(GSArgs a) {
 #pragma unroll
     for (int i = 0; i < KPL; ++i) {
       const bool real = tk<TG, PAIR>(q, i) < K;
-      const double l = lgamma_pos(real ? gam[i] : 1.0);
+      const double l = lgamma_pos<true>(real ? gam[i] : 1.0, sLog);
       gs += real ? gam[i] : 0.0;
       lg += real ? l : 0.0;
     }
@@ -1194,7 +1194,7 @@ __global__ __launch_bounds__(team_threads(KS, NW), MINW) void gs_team(GSArgs a) 
     for (int o = 0; o < TO; ++o) {
       if (t + NTD * o < K) {
         gs += gam[o];
-        lg += lgamma_pos(gam[o]);
+        lg += lgamma_pos<TAB>(gam[o], sLog);
         lp += lps[o];
       }
     }
