@@ -188,7 +188,7 @@ __global__ __launch_bounds__(256) void gs_tiny(GSArgs a) {
         gam[i] += nw - C[0][i];
         C[0][i] = nw;
         double pn, en;
-        psi_exp<true>(real ? gam[i] : 1.0, m, pn, en, sLog);
+        psi_exp<true, true>(real ? gam[i] : 1.0, m, pn, en, sLog);
         psi[i] = real ? pn : psi[i];
         E[i] = real ? en : 0.0;
       }
@@ -758,7 +758,7 @@ __global__ __launch_bounds__(256, MINW) void gs_smallw(GSArgs a) {
         lp = fma(psi[i], nw, lp);
         gam[i] += nw - Cn[i];
         double p, e;
-        psi_exp<true>(real ? gam[i] : 1.0, m, p, e, sLog);
+        psi_exp<true, true>(real ? gam[i] : 1.0, m, p, e, sLog);
         psi[i] = real ? p : psi[i];
         E[i] = real ? e : 0.0;
       }
