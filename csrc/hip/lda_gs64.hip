@@ -922,8 +922,34 @@ __device__ __forceinline__ void stream_tail(const double* __restrict__ beta, con
                                             const double (&E)[KPL], double (&b)[RMAX][KPL], double (&acc)[KPL],
                                             double& lw, const dvec2* tab = nullptr) {
   int p = p0;
-  for (; p + NS < end; p += RMAX * NS)
-    stream_batch<RMAX, KS, KPL, TG, LSW, PAIR, TAB>(beta, wrow, crow, p, end, NS, q, E, b, acc, lw, tab);
+  if (p + NS < end) {
+    // the ids of batch i + 1 load while batch i's rows are in flight: a batch then waits one memory latency
+    // (its rows), not two (ids, then rows)
+    int w[RMAX];
+    double c[RMAX];
+#pragma unroll
+    for (int r = 0; r < RMAX; ++r) {
+      const int pr = p + r * NS;
+      const int pc = min(pr, end - 1);
+      w[r] = wrow[pc];
+      c[r] = pr < end ? (double)crow[pc] : 0.0;
+    }
+    for (; p + NS < end; p += RMAX * NS) {
+#pragma unroll
+      for (int r = 0; r < RMAX; ++r) load_row<KS, KPL, TG, PAIR>(beta, w[r], q, b[r]);
+      double cb[RMAX];
+      const int pn = p + RMAX * NS;
+#pragma unroll
+      for (int r = 0; r < RMAX; ++r) {
+        cb[r] = c[r];
+        const int pr = pn + r * NS;
+        const int pc = max(0, min(pr, end - 1));
+        w[r] = wrow[pc];
+        c[r] = pr < end ? (double)crow[pc] : 0.0;
+      }
+      word_steps<RMAX, KPL, LSW, TAB>(E, b, cb, acc, lw, tab);
+    }
+  }
   if (p < end) {
     double b1[1][KPL];
     stream_batch<1, KS, KPL, TG, LSW, PAIR, TAB>(beta, wrow, crow, p, end, NS, q, E, b1, acc, lw, tab);
