@@ -79,3 +79,22 @@ def test_group_plan_covers_every_word_once():
 def test_group_plan_none_without_shared_words():
     lens = [np.array([2, 0, 1, 0]), np.array([0, 3, 0, 0])]
     assert H.suff_group_plan(lens, 4) is None
+
+
+def test_stream_slots_late_bucket_alone():
+    """LDAEngine._stream_slots (the bucket -> stream map shared by _launch_buckets and the per-stream
+    suff-stats plan): at KS > 32 the 8-wave team alone on stream 1, the others round-robin over the
+    remaining side streams, then the current stream (0)."""
+    from types import SimpleNamespace
+    from oni_ml_amd.models.lda.em import LDAEngine
+    plan = [(H.GS_TEAM8, None), (H.GS_TEAM4, None), (H.GS_SMALL, None), (H.GS_TINY, None)]
+    gp = SimpleNamespace(KS=104, plan=plan, split=object())       # work = [split, team8, team4, small, tiny]
+    eng = SimpleNamespace(_streams=[None] * 3, _late_key=LDAEngine._late_key)
+    slots = LDAEngine._stream_slots(eng, gp, late=True)
+    assert slots == [2, 1, 3, 0, 2]
+    assert slots.count(1) == 1
+    # no late bucket: plain round-robin over the side streams, then the current one
+    assert LDAEngine._stream_slots(eng, gp, late=False) == [1, 2, 3, 0, 1]
+    # five streams (LDAEngine(streams=5)): four side streams
+    eng5 = SimpleNamespace(_streams=[None] * 4, _late_key=LDAEngine._late_key)
+    assert LDAEngine._stream_slots(eng5, gp, late=True) == [2, 1, 3, 4, 0]
