@@ -73,8 +73,11 @@ __device__ __forceinline__ double fexp(double x) {
 // copied into the workgroup's LDS by log_table_fill.  <= 1 ulp for y >= 2 (host emulation with exact fma
 // over 6 .. 1e4: 0.65 ulp); near y = 1 the e ln 2 + L cancellation leaves ~1e-16 absolute error (flog keeps
 // the relative accuracy there).  17 VALU instructions and one ds_read_b128 against flog's ~36.
+// LDS image: [0, 128) the log table {inv_i, L_i}, [128, 160) the exp table kExpTab as pairs
+constexpr int kMathTabN = 160;
 __device__ __forceinline__ void log_table_fill(dvec2* __restrict__ s) {
-  for (int i = threadIdx.x; i < 128; i += blockDim.x) s[i] = dvec2{kLogTab[i][0], kLogTab[i][1]};
+  for (int i = threadIdx.x; i < kMathTabN; i += blockDim.x)
+    s[i] = i < 128 ? dvec2{kLogTab[i][0], kLogTab[i][1]} : dvec2{kExpTab[2 * (i - 128)], kExpTab[2 * (i - 128) + 1]};
 }
 __device__ __forceinline__ double flog_t(double y, const dvec2* __restrict__ tab) {
   const unsigned long long b = (unsigned long long)__double_as_longlong(y);
@@ -91,6 +94,21 @@ __device__ __forceinline__ double flog_t(double y, const dvec2* __restrict__ tab
   return fma(de, 6.93147180369123816490e-01, fma(de, 1.90821492927058770002e-10, c.y + p));
 }
 
+// exp(x) for |x| < 700 by table: x = (64 e + j) ln 2 / 64 + r, |r| <= ln 2 / 128, exp x = 2^e T_j (1 + q(r)),
+// q of degree 6 (truncation < 3e-20), T_j = RN(2^(j/64)) from the LDS image (log_table_fill).  <= 1 ulp
+// (host emulation with exact fma over [-700, 10]); 17 VALU instructions against fexp's 21.
+__device__ __forceinline__ double fexp_t(double x, const dvec2* __restrict__ tab) {
+  const double kf = __builtin_rint(x * 92.332482616893657);
+  const double r = fma(-kf, 0x1.a39ef35793c76p-39, fma(-kf, 0x1.62e42fee00000p-7, x));
+  const int ki = (int)kf;
+  const double T = reinterpret_cast<const double*>(tab + 128)[ki & 63];
+  const double r2 = r * r;
+  const double a = fma(r, 0.16666666666666667, 0.5);
+  const double c = fma(r2, 0.0013888888888888889, fma(r, 0.0083333333333333333, 0.041666666666666667));
+  const double q = fma(r2 * r2, c, fma(r2, a, r));
+  return __builtin_amdgcn_ldexp(fma(T, q, T), ki >> 6);
+}
+
 // lda-c digamma (x + 6 shift, 4-term series, six recurrence terms) and
 // E = exp(psi - m).  The six reciprocals 1/(x+i) are (dA B + dB A) / (A B) with
 // A = x(x+1)(x+2), B = (x+3)(x+4)(x+5) (one reciprocal; A B < 1e54 for x < 1e9);
@@ -98,7 +116,8 @@ __device__ __forceinline__ double flog_t(double y, const dvec2* __restrict__ tab
 // R1 (the throughput-bound kernels): one reciprocal R = 1 / (A B y) for both 1/y = A B R and the six terms
 // (dA B + dB A) y R -- 3 instructions fewer, ~4 more dependent steps before the series (A B y < 1e63 for
 // x < 1e9), a few ulp on terms that are not the log
-template <bool TAB = false, bool R1 = false>
+// ET: exp by table too (off in the 16-lane kernel: 211 -> 243 VGPRs there and 2.5 % slower, r5ao)
+template <bool TAB = false, bool R1 = false, bool ET = TAB>
 __device__ __forceinline__ void psi_exp(double x, double m, double& psi, double& e, const dvec2* tab = nullptr) {
   const double y = x + 6.0;
   const double x1 = x + 1.0, x2 = x + 2.0, x3 = x + 3.0, x4 = x + 4.0, x5 = x + 5.0;
@@ -119,7 +138,7 @@ __device__ __forceinline__ void psi_exp(double x, double m, double& psi, double&
                          fma(0.008333333333333, z, -0.083333333333333)) * z;
   const double rest = fma(-0.5, iy, ser) - S;
   psi = (TAB ? flog_t(y, tab) : flog(y)) + rest;
-  e = y * fexp(rest - m);
+  e = y * (ET ? fexp_t(rest - m, tab) : fexp(rest - m));
 }
 
 // ln Gamma(x), x > 0: Stirling series at y = x + 6 (terms through 1/y^13, truncation

@@ -118,7 +118,7 @@ __global__ __launch_bounds__(256) void gs_tiny(GSArgs a) {
   constexpr int BST = NMAX * KS + 1;   // odd stride in doubles: groups of a wave hit different banks
   __shared__ double sB[DPB][BST];
   __shared__ double sN[DPB][NMAX];
-  __shared__ dvec2 sLog[128];          // flog_t's table
+  __shared__ dvec2 sLog[kMathTabN];          // flog_t's table
   if (a.params[kParamDone] != 0.0) return;
   log_table_fill(sLog);
   __syncthreads();
@@ -409,7 +409,7 @@ __global__ __launch_bounds__(256) void gs_chain(GSArgs a) {
   constexpr int TC = (KS + 63) / 64;
   // TC = 2: lane l holds the topic pair 2l, 2l + 1 and loads it with one 16-byte load (KS even)
   constexpr bool PAIR = TC == 2;
-  __shared__ dvec2 sLog[128];      // flog_t's table
+  __shared__ dvec2 sLog[kMathTabN];      // flog_t's table
   if (a.params[kParamDone] != 0.0) return;
   log_table_fill(sLog);
   __syncthreads();
@@ -638,7 +638,7 @@ __global__ __launch_bounds__(256, MINW) void gs_smallw(GSArgs a) {
   // 8.99 ms, r5s: 8 topics per lane instead of 7 and 235 vs 196 VGPRs), the 16-lane kernel being refresh-bound
   constexpr bool PAIR = false;
   constexpr int TG = 16, KPL = PAIR ? 2 * ((KS + 2 * TG - 1) / (2 * TG)) : (KS + TG - 1) / TG;
-  __shared__ dvec2 sLog[128];          // flog_t's table
+  __shared__ dvec2 sLog[kMathTabN];          // flog_t's table
   if (a.params[kParamDone] != 0.0) return;
   log_table_fill(sLog);
   __syncthreads();
@@ -758,7 +758,7 @@ __global__ __launch_bounds__(256, MINW) void gs_smallw(GSArgs a) {
         lp = fma(psi[i], nw, lp);
         gam[i] += nw - Cn[i];
         double p, e;
-        psi_exp<true, true>(real ? gam[i] : 1.0, m, p, e, sLog);
+        psi_exp<true, true, false>(real ? gam[i] : 1.0, m, p, e, sLog);
         psi[i] = real ? p : psi[i];
         E[i] = real ? e : 0.0;
       }
@@ -982,7 +982,7 @@ __global__ __launch_bounds__(team_threads(KS, NW), MINW) void gs_team(GSArgs a) 
   // KS > 32: flog_t's table for the per-word log and the refresh (DPB == 1 there: the workgroup is one
   // document, so every early return below is workgroup-uniform)
   constexpr bool TAB = KS > 32;
-  __shared__ dvec2 sLog[TAB ? 128 : 1];
+  __shared__ dvec2 sLog[TAB ? kMathTabN : 1];
   if (a.params[kParamDone] != 0.0) return;
   if constexpr (TAB) {
     log_table_fill(sLog);
