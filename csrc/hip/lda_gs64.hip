@@ -188,7 +188,7 @@ __global__ __launch_bounds__(256) void gs_tiny(GSArgs a) {
         gam[i] += nw - C[0][i];
         C[0][i] = nw;
         double pn, en;
-        psi_exp<true, true>(real ? gam[i] : 1.0, m, pn, en, sLog);
+        psi_exp<true, true, (KS > 32)>(real ? gam[i] : 1.0, m, pn, en, sLog);   // table exp: K > 32 only (r5aq)
         psi[i] = real ? pn : psi[i];
         E[i] = real ? en : 0.0;
       }
