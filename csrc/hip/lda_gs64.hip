@@ -149,7 +149,7 @@ __global__ __launch_bounds__(256) void gs_tiny(GSArgs a) {
 #pragma unroll
   for (int i = 0; i < KPL; ++i) {
     const bool real = q + TG * i < K;
-    gam[i] = real ? g0 : 0.0;
+    gam[i] = real ? g0 : 1.0;   // padding topics hold gamma = 1 (finite refresh, never summed or stored)
     psi[i] = m;
     E[i] = real ? 1.0 : 0.0;
   }
@@ -179,7 +179,7 @@ __global__ __launch_bounds__(256) void gs_tiny(GSArgs a) {
       lw = fma(c, flog_t(P, sLog), lw);
       // branch-free refresh: the KPL digamma/exp chains interleave (a topic-guarded psi_exp is a basic block
       // of its own and the chains ran one after another); padding topics have E = 0, so nw = 0, and keep
-      // gamma = 0, psi = m, E = 0
+      // gamma = 1, E = 0
 #pragma unroll
       for (int i = 0; i < KPL; ++i) {
         const bool real = q + TG * i < K;
@@ -188,8 +188,9 @@ __global__ __launch_bounds__(256) void gs_tiny(GSArgs a) {
         gam[i] += nw - C[0][i];
         C[0][i] = nw;
         double pn, en;
-        psi_exp<true, true, (KS > 32)>(real ? gam[i] : 1.0, m, pn, en, sLog);   // table exp: K > 32 only (r5aq)
-        psi[i] = real ? pn : psi[i];
+        // padding topics: gamma stays 1 (nw = 0, C = 0), psi finite and only ever multiplied by nw = 0
+        psi_exp<true, true, (KS > 32)>(gam[i], m, pn, en, sLog);   // table exp: K > 32 only (r5aq)
+        psi[i] = pn;
         E[i] = real ? en : 0.0;
       }
       rotl1(C);
@@ -219,7 +220,7 @@ __global__ __launch_bounds__(256) void gs_tiny(GSArgs a) {
   for (int i = 0; i < KPL; ++i) {
     const int k = q + TG * i;
     if (k < K) ps += psi[i];
-    if (k < KS) a.gamma[(size_t)d * KS + k] = gam[i];
+    if (k < KS) a.gamma[(size_t)d * KS + k] = k < K ? gam[i] : 0.0;
   }
   ps = bits_sum<0, LTG, false>(ps);
 #pragma unroll
@@ -684,7 +685,7 @@ __global__ __launch_bounds__(256, MINW) void gs_smallw(GSArgs a) {
 #pragma unroll
   for (int i = 0; i < KPL; ++i) {
     const int k = tk<TG, PAIR>(q, i);
-    gam[i] = k < K ? g0 : 0.0;
+    gam[i] = k < K ? g0 : 1.0;   // padding topics hold gamma = 1 (finite refresh, never summed or stored)
     psi[i] = m;
     E[i] = k < K ? 1.0 : 0.0;
     Cn[i] = k < KS ? rows[k] : 0.0;   // C_0 (this lane's own stores above)
@@ -749,8 +750,8 @@ __global__ __launch_bounds__(256, MINW) void gs_smallw(GSArgs a) {
         }
       }
       // the refresh without branches: a topic-guarded psi_exp is a basic block of its own, so the KPL
-      // chains would run one after another instead of interleaved (padding topics compute psi_exp(1) and
-      // keep psi = m, E = 0, gamma = 0: nw = 0 there)
+      // chains would run one after another instead of interleaved (padding topics keep gamma = 1
+      // and E = 0: nw = 0 there)
 #pragma unroll
       for (int i = 0; i < KPL; ++i) {
         const bool real = tk<TG, PAIR>(q, i) < K;
@@ -758,8 +759,9 @@ __global__ __launch_bounds__(256, MINW) void gs_smallw(GSArgs a) {
         lp = fma(psi[i], nw, lp);
         gam[i] += nw - Cn[i];
         double p, e;
-        psi_exp<true, true, false>(real ? gam[i] : 1.0, m, p, e, sLog);
-        psi[i] = real ? p : psi[i];
+        // padding topics: gamma stays 1 (nw = 0, C = 0), psi finite and only ever multiplied by nw = 0
+        psi_exp<true, true, false>(gam[i], m, p, e, sLog);
+        psi[i] = p;
         E[i] = real ? e : 0.0;
       }
       // C of the next chunk, after this chunk's row stores (nch == 1: the same row)
@@ -789,7 +791,7 @@ __global__ __launch_bounds__(256, MINW) void gs_smallw(GSArgs a) {
   for (int i = 0; i < KPL; ++i) {
     const int k = tk<TG, PAIR>(q, i);
     if (k < K) ps += psi[i];
-    if (k < KS) a.gamma[(size_t)d * KS + k] = gam[i];
+    if (k < KS) a.gamma[(size_t)d * KS + k] = k < K ? gam[i] : 0.0;
   }
   ps = bits_sum<0, 4, false>(ps);
   if (q == 0) {
