@@ -90,14 +90,16 @@ PYBIND11_MODULE(_onihip, m) {
   m.def("gs_split_lds_umax", [](int KS) { return oni::gs_split_lds_umax(KS); });
   m.def("gs_split", [](u doc_ptr, u word_idx, u counts, u beta, int K, int KS, int gs_updates, u params, u gamma,
                        u cphi, u lik, u alpha_ss, u iters, u seg_doc, u seg_index, u seg_count, u seg_base,
-                       u doc_slot, int n_blocks, u xchg, u counter, int n_docs, u error, u stream, u dbg, u tab) {
+                       u doc_slot, int n_blocks, u xchg, u counter, int n_docs, u error, u stream, u dbg, u tab,
+                       int tab_rows, u csum, int csum_stride) {
     oni::GSArgs a{P<const int>(doc_ptr), P<const int>(word_idx), P<const float>(counts), nullptr,
                   n_blocks,              P<const double>(beta),  K,                      gs_updates,
                   P<const double>(params), P<double>(gamma),     P<double>(cphi),        P<double>(lik),
                   P<double>(alpha_ss),   P<int>(iters),         P<long long>(dbg)};
     oni::SplitArgs s{P<const int>(seg_doc), P<const int>(seg_index), P<const int>(seg_count),
-                     P<const int>(seg_base), P<const int>(doc_slot), n_blocks, 0,
-                     P<unsigned long long>(xchg), P<int>(counter), n_docs, P<int>(error), P<double>(tab)};
+                     P<const int>(seg_base), P<const int>(doc_slot), n_blocks, tab_rows,
+                     P<unsigned long long>(xchg), P<int>(counter), n_docs, P<int>(error), P<double>(tab),
+                     P<const double>(csum), csum_stride};
     oni::launch_gs_split(a, s, KS, S(stream));
   });
   m.def("gs_suff64", [](u word_ptr, u csc_ent, u order, int n_heavy, int n_medium, int n_light, u cphi, u cw, u part,

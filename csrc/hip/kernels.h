@@ -28,13 +28,16 @@ struct SplitArgs {
   const int* seg_base;    // [n_blocks] block id of the document's segment 0
   const int* doc_slot;    // [n_blocks] counter slot of the document
   int n_blocks;
-  int seg_words;          // unused by the fp64 kernels
-  unsigned long long* xchg;  // tagged granules (parity double-buffer), layout per kernel
+  int tab_rows;           // rows per workgroup of `tab` (>= nch of every document of the launch)
+  unsigned long long* xchg;  // tagged granules (parity double-buffer), layout per kernel; gs_splitw:
+                             // [2][n_blocks][2 (KS + 1)] partials, then [2][n_docs][2 (KS + 1)] totals
   int* counter;           // [2][n_docs] per document: launch epoch (tags of different launches never
                           // match), exit count (the last segment out bumps the epoch, resets the count)
   int n_docs;             // documents in this launch
   int* error;             // set to 1 if a wait times out (never hangs the GPU)
-  double* tab = nullptr;  // U > the LDS table rows (KS > 32): per-segment chunk tables [n_blocks][U][2][KS]
+  double* tab = nullptr;  // U > the LDS table rows (KS > 32): per-segment chunk tables [n_blocks][tab_rows][2][KS]
+  const double* csum = nullptr;  // [n_docs][csum_stride] chunk count sums of each document (nullptr: the
+  int csum_stride = 0;           // kernel sums the counts itself)
 };
 
 // Sufficient-statistic launches: workgroups for [heavy | medium | light] word lists
@@ -94,7 +97,8 @@ enum GsVariant : int {
   kGsSmall = 4,    // 16 lanes per document: KS <= 32 tiny < n <= 64 words (register state); KS > 32 the
                    // one-wave range (gs_smallw, chunk tables in the c*phi rows)
   kGsChain = 5,    // KS > 32, U > 32: one wave per document, a topic per lane, rows of the next 8 words in
-                   // flight (chunks of <= 4 words: lda-c's per-word schedule)
+                   // flight (the planner routes chunks of W <= GSPlan.CHAIN_MAX_W = 2 words here:
+                   // lda-c's per-word schedule, ops/hip.py wide_u_edges)
 };
 struct GSArgs {
   const int* doc_ptr;     // [D+1]

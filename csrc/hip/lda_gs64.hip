@@ -1360,7 +1360,7 @@ __device__ __forceinline__ void put_tagged_bits(unsigned long long* p, unsigned 
 // round trip per granule group; the round-3 form polled 4 segments per round trip, 2 x 4 serial round
 // trips per chunk at G = 16, K = 100 (12.8 k cycles per chunk, profiles/r5f) -- and the microbenchmark
 // (scripts/micro/xcd_exchange.hip) measured batched polls at half the per-granule form.  False on a timeout.
-constexpr int kSplitMaxSeg = 16;   // GMX: segments per document (GSSplitPlan caps G)
+constexpr int kSplitMaxSeg = 16;   // GMX of the single-round gather (more: split_allreduce2)
 template <int TC, int GMX, int NC>
 __device__ __forceinline__ bool tagged_gather(const unsigned long long* x, int G, int stride, int lane, unsigned tag,
                                               double (&out)[TC]) {
@@ -1403,6 +1403,75 @@ __device__ __forceinline__ bool tagged_gather(const unsigned long long* x, int G
   return true;
 }
 
+// Two-phase exchange for G > kSplitMaxSeg segments (up to kSplitMaxSeg2): a single-round gather reads
+// G x NC x 2 granules per segment -- linear in G, and past 16 segments more than the topic wave's registers
+// can keep in flight -- so the columns are owned instead: segment g reduces columns c = g + G x (x < nown)
+// over the G published partials (reduce-scatter: ~NC x 2 granules per segment, <= 4 per lane, all in one
+// batched poll), publishes each owned total once with the chunk's tag into the document's totals row, and
+// every segment then gathers the NC totals (all-gather: NC x 2 granules).  Two round trips whatever G is;
+// each total is computed by exactly one segment, so every replica reads the same bits.  Buffer reuse: the
+// totals row (seq & 1) is rewritten at seq + 2 only after its owner has read every segment's seq + 2
+// partial, which a segment publishes only after it has gathered the seq + 1 totals, i.e. after it has
+// finished reading seq's.  sPair: LDS scratch of >= NC + kSplitMaxSeg2 doubles (the topic wave only).
+constexpr int kSplitMaxSeg2 = 128;   // two-phase exchange: two segments per topic-wave lane
+template <int TC, int NC, int GR>
+__device__ __forceinline__ bool split_allreduce2(const unsigned long long* __restrict__ xs, unsigned long long* xt,
+                                                 int G, int g, int lane, unsigned tag, double* sPair,
+                                                 double (&out)[TC]) {
+  // pairs (column, segment) per lane: nown x G < NC + G when G < NC, = G <= kSplitMaxSeg2 otherwise, and
+  // < 2 NC when NC / 2 < G < NC (nown = 2)
+  constexpr int PMAX = ((2 * NC > kSplitMaxSeg2 ? 2 * NC : kSplitMaxSeg2) + 63) / 64;
+  const int nown = g < NC ? (NC - 1 - g) / G + 1 : 0;        // uniform across the wave
+  const int npair = nown * G;
+  if (npair > 0) {
+    int off[PMAX];
+#pragma unroll
+    for (int o = 0; o < PMAX; ++o) {
+      const int i = min(lane + 64 * o, npair - 1);
+      const int x = i / G, u = i - x * G;
+      off[o] = u * GR + 2 * (g + G * x);
+    }
+    unsigned long long v[PMAX][2];
+    long spins = 0;
+    for (;;) {
+#pragma unroll
+      for (int o = 0; o < PMAX; ++o) {
+        v[o][0] = __hip_atomic_load(xs + off[o], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        v[o][1] = __hip_atomic_load(xs + off[o] + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      bool ok = true;
+#pragma unroll
+      for (int o = 0; o < PMAX; ++o)
+        ok &= lane + 64 * o >= npair || ((unsigned)(v[o][0] >> 32) == tag && (unsigned)(v[o][1] >> 32) == tag);
+      if (ok) break;
+      if (++spins > kSplitSpinLimit) {
+#pragma unroll
+        for (int o = 0; o < TC; ++o) out[o] = __builtin_nan("");
+        return false;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+#pragma unroll
+    for (int o = 0; o < PMAX; ++o)
+      if (lane + 64 * o < npair)
+        sPair[lane + 64 * o] =
+            __longlong_as_double((long long)(((v[o][1] & 0xffffffffull) << 32) | (v[o][0] & 0xffffffffull)));
+    wave_lds_sync();
+    for (int x = 0; x < nown; ++x) {
+      double s = (lane < G ? sPair[x * G + lane] : 0.0) + (lane + 64 < G ? sPair[x * G + lane + 64] : 0.0);
+      s = group_sum<64>(s);   // fixed DPP tree: computed once, by this owner
+      if (lane == 0) {
+        const unsigned long long bits = (unsigned long long)__double_as_longlong(s);
+        unsigned long long* row = xt + 2 * (g + G * x);
+        put_tagged_bits(row, (unsigned)(bits & 0xffffffffull), tag);
+        put_tagged_bits(row + 1, (unsigned)(bits >> 32), tag);
+      }
+    }
+    wave_lds_sync();
+  }
+  return tagged_gather<TC, 1, NC>(xt, 1, GR, lane, tag, out);
+}
+
 // ------------------------------------------------------------ split kernel ----
 // 7 word waves + 1 topic wave: the word waves leave their chunk partials in LDS, signal an LDS arrival
 // counter and issue the NEXT chunk's row prefetch at once; the topic wave sums the waves, publishes the
@@ -1435,10 +1504,12 @@ __global__ __launch_bounds__(512) void gs_splitw(GSArgs a, SplitArgs sp) {
   __shared__ double sScal[4];
   __shared__ int arrive[NW];   // per word wave: chunks whose partial sums it has left in sRed / sRedL
   __shared__ int sFail;
+  __shared__ double sPair[KS > 32 ? 2 * NC + kSplitMaxSeg2 : 1];   // the two-phase exchange's values
   if (a.params[kParamDone] != 0.0) return;
   const int t = threadIdx.x, b = blockIdx.x;
   const int d = sp.seg_doc[b], g = sp.seg_index[b], G = sp.seg_count[b], base = sp.seg_base[b];
-  int* counter = sp.counter + sp.doc_slot[b];
+  const int dslot = sp.doc_slot[b];
+  int* counter = sp.counter + dslot;
   const int epoch = __hip_atomic_load(counter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const double alpha = a.params[0], lik_const = a.params[1];
   const int vmi = (int)a.params[2];
@@ -1458,17 +1529,31 @@ __global__ __launch_bounds__(512) void gs_splitw(GSArgs a, SplitArgs sp) {
   const bool active = wv < nact;              // never the topic wave
   const int* __restrict__ wrow = a.word_idx + s0;
   const float* __restrict__ crow = a.counts + s0;
-  double* __restrict__ tab = GM ? sp.tab + (size_t)b * U * 2 * KS : nullptr;   // row j: C_j, then E_j
+  // row j: C_j, then E_j; sp.tab_rows >= every batch document's nch (GSSplitPlan)
+  double* __restrict__ tab = GM ? sp.tab + (size_t)b * sp.tab_rows * 2 * KS : nullptr;
   auto range = [&](int j, int& m0, int& m1) {
     const int n1 = min(n, (j + 1) * W);
     m0 = min(n1, j * W + g * WG);
     m1 = min(n1, m0 + WG);
   };
-  for (int j = t; j < nch; j += NTD) sCs[j] = 0.0;
-  if (t == 0) sFail = 0;
-  if (t < NW) arrive[t] = 0;
-  lds_barrier();
-  for (int p = t; p < n; p += NTD) atomicAdd(&sCs[p / W], (double)crow[p]);   // integer counts: exact
+  if (GM && nch > sp.tab_rows) {   // a host plan error: every segment of d leaves (same nch), none waits
+    if (t == 0) __hip_atomic_store(sp.error, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return;
+  }
+  if (sp.csum) {
+    // the chunk count sums the plan computed once (GSSplitPlan.chunk_sums): no pass over the whole
+    // document's counts in every segment (443 k words x 124 segments at config 5)
+    const double* cs = sp.csum + (size_t)dslot * sp.csum_stride;
+    for (int j = t; j < nch; j += NTD) sCs[j] = cs[j];
+    if (t == 0) sFail = 0;
+    if (t < NW) arrive[t] = 0;
+  } else {
+    for (int j = t; j < nch; j += NTD) sCs[j] = 0.0;
+    if (t == 0) sFail = 0;
+    if (t < NW) arrive[t] = 0;
+    lds_barrier();
+    for (int p = t; p < n; p += NTD) atomicAdd(&sCs[p / W], (double)crow[p]);   // integer counts: exact
+  }
   lds_barrier();
   double total = 0.0;
   for (int j = 0; j < nch; ++j) total += sCs[j];
@@ -1578,13 +1663,21 @@ __global__ __launch_bounds__(512) void gs_splitw(GSArgs a, SplitArgs sp) {
           ok = tagged_gather<TC, 4, NC>(xs, G, GR, lane, tag, tot);
         } else if (G <= 8) {
           ok = tagged_gather<TC, 8, NC>(xs, G, GR, lane, tag, tot);
-        } else {
+        } else if (G <= kSplitMaxSeg) {
 #pragma unroll
           for (int o = 0; o < TC; ++o) {
             double t1[1];
             ok &= tagged_gather<1, kSplitMaxSeg, NC>(xs, G, GR, lane + 64 * o, tag, t1);
             tot[o] = t1[0];
           }
+        } else if constexpr (KS > 32) {
+          // the document's totals row, after the launch's 2 x n_blocks partial rows (KS <= 32 splits take at
+          // most kSplitMaxSeg segments: GSSplitPlan; the narrow word layout has no registers to spare for it)
+          unsigned long long* xt = sp.xchg + (size_t)2 * sp.n_blocks * GR +
+                                   ((size_t)(seq & 1) * sp.n_docs + dslot) * GR;
+          ok = split_allreduce2<TC, NC, GR>(xs, xt, G, g, lane, tag, sPair, tot);
+        } else {
+          ok = false;
         }
         tick(4);
         if (!ok) {

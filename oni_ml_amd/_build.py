@@ -229,7 +229,9 @@ def build_sanitized(kind: str = "thread", verbose=False) -> Path:
     return exe
 
 
-def build_all(verbose=False, hip=True, native=True):
+def build_all(verbose=False, hip=True, native=True, experimental=False):
+    """experimental: also build csrc/hip/experimental/ (only on request: ``python -m oni_ml_amd._build exp``;
+    ml_ops never loads it, and its tests skip without it)."""
     with _lock:
         RECORD.clear()
         outs = []
@@ -241,7 +243,12 @@ def build_all(verbose=False, hip=True, native=True):
             if not Path(HIPCC).exists():
                 raise RuntimeError(f"hipcc not found at {HIPCC}")
             outs.append(build_hip(verbose))
-            outs.append(build_hip_exp(verbose))
+            if experimental:
+                outs.append(build_hip_exp(verbose))
+            else:
+                # a stale experimental module would travel with the tree and be mapped by its tests
+                for p in LIB.glob("_onihip_exp*"):
+                    p.unlink()
         return outs
 
 
@@ -256,4 +263,4 @@ if __name__ == "__main__":
     v = "-v" in sys.argv
     if "clean" in sys.argv:
         clean()
-    print(build_all(verbose=v))
+    print(build_all(verbose=v, experimental="exp" in sys.argv))

@@ -119,7 +119,8 @@ def cmd_ml_ops(argv):
     ap.add_argument("--no-word-assignments", dest="word_assignments", action="store_false")
     ap.add_argument("--rank-gamma", action="store_true", default=None,
                     help="write <rank>.gamma / <rank>.beta per GPU (default: on when running on several GPUs and K x V <= 2^26)")
-    ap.add_argument("--threads", type=int, default=8)
+    ap.add_argument("--threads", type=int, default=None,
+                    help="host threads of the stage pools (default: min(8, this rank's CPU budget))")
     ap.add_argument("--deliver", action="store_true", help="scp -r LPATH UINODE:RPATH (ml_ops.sh:121)")
     ap.add_argument("--cuts", help="fixed flow cuts: a flow_qtiles file or its text (the reference's CUT)")
     ap.add_argument("--hdfs", action="store_true",
@@ -146,13 +147,20 @@ def cmd_ml_ops(argv):
                            hadoop=a.hadoop)
     # one process, fresh run: the day's inputs are read on a thread while torch imports
     # (pipeline/prefetch.py); the load stage takes the result
+    from .pipeline import prefetch
     if (knobs.get("ONI_PREFETCH", "1") != "0" and a.gpus <= 1 and int(os.environ.get("WORLD_SIZE", "1")) == 1
             and not a.resume and not a.hdfs):
         try:
-            from .pipeline import prefetch
-            prefetch.start_for(resolve(1))
+            prefetch.start_for(resolve(1), fork=not _tool_attached())
         except Exception:  # noqa: BLE001 -- a bad configuration is reported by the resolve below
             pass
+    try:
+        return _ml_ops_body(a, resolve)
+    finally:
+        prefetch.drop_all()   # a run that failed before its load stage: no forked child or /dev/shm files left
+
+
+def _ml_ops_body(a, resolve):
     import torch  # noqa: F401  (its import time is a start-up mark of its own)
     MARKS["torch_imported"] = time.time()
     from .models.lda.settings import LDASettings

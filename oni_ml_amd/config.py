@@ -92,7 +92,7 @@ class RunConfig:
     seed: int = 0
     start: str = "random"                 # random | seeded | <model prefix>
     resume: bool = False
-    threads: int = 8
+    threads: int = 0      # host threads of the stage pools; 0: knobs.threads(8), this rank's CPU budget
     write_doc_wc: bool = True
     word_assignments: bool = True          # lda-c writes word-assignments.dat on every `lda est`
     rank_gamma: Optional[bool] = None      # <rank>.gamma / <rank>.beta; None: multi-rank runs of K x V <= 2^26
@@ -166,6 +166,9 @@ def resolve(fdate: str, dsource: str, tol: Optional[float] = None, conf_path: Op
         if not hasattr(cfg, k):
             raise TypeError(f"unknown config key {k}")
         setattr(cfg, k, v)
+    if cfg.threads <= 0:
+        from . import knobs
+        cfg.threads = knobs.threads(8)
     return cfg
 
 

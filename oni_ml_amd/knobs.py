@@ -18,7 +18,9 @@ KNOBS = {
     "ONI_GPUS": "scripts/ml_ops.sh: GPUs to launch one process each on under torchrun (default 1)",
     # --- host resources
     "ONI_THREADS": "host threads of the native pools: CSV/parquet ingest, the C++ LDA engine, writers "
-                   "(default: min(16, CPUs); the `lda` binary: all hardware threads)",
+                   "(default: min(16, the rank's CPU budget = its bound CPUs, or CPUs / LOCAL_WORLD_SIZE); "
+                   "the `lda` binary: all hardware threads); set, it also turns off the per-rank CPU binding "
+                   "(utils/hostres.py)",
     "ONI_SEED": "seed of the `lda` binary's random start (default 4357)",
     # --- device memory
     "ONI_CPHI_GB": "HBM budget of the per-entry c.phi rows; larger corpora run the E-step in document "
@@ -64,6 +66,10 @@ def profile(token: str):
 
 
 def threads(default: int = 16) -> int:
-    """ONI_THREADS, else min(default, CPUs)."""
+    """ONI_THREADS, else min(default, this rank's CPU budget): the CPUs bound to it (utils/hostres.py
+    bind_rank), or the allowed CPUs divided by LOCAL_WORLD_SIZE."""
     v = get("ONI_THREADS")
-    return max(1, int(v)) if v else max(1, min(default, os.cpu_count() or 1))
+    if v:
+        return max(1, int(v))
+    from .utils import hostres
+    return max(1, min(default, hostres.cpu_budget()))

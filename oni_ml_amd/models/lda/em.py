@@ -97,6 +97,18 @@ def _hbm_total(device) -> int:
     return int(torch.cuda.mem_get_info(device)[1])
 
 
+def _stage_budget_gb(v: str) -> float:
+    """ONI_GS_STAGE: the staged-rows budget in GB.  Until round 5 it was an on/off flag (1 = staged,
+    4 GB cap): a value in (0, 1] is read as that flag, with a warning."""
+    gb = float(v)
+    if 0 < gb <= 1:
+        import warnings
+        warnings.warn(f"ONI_GS_STAGE={v}: read as the old on/off flag (4 GB budget); give the budget in GB > 1",
+                      stacklevel=3)
+        return 4.0
+    return gb
+
+
 class LDAEngine:
     def __init__(self, corpus: Corpus, num_topics: int, settings: Optional[LDASettings] = None,
                  alpha_init: float = 2.5, backend: str = "auto", device=None, dist=None, seed: int = 0,
@@ -215,7 +227,9 @@ class LDAEngine:
             private = np.setdiff1d(local, shared, assume_unique=True)
             self._plan_a = H.SuffPlan(self.dc.word_len, self.device, words=shared)
             self._plan_b = H.SuffPlan(self.dc.word_len, self.device, words=private)
-            nb = max(self._plan_a.n_blocks + self._plan_b.n_blocks, self.suff_plan.n_blocks, 1)
+            # never below the rows _init_gs64 sized for the K > 32 per-stream groups (e_step()'s phase='all')
+            nb = max(self._plan_a.n_blocks + self._plan_b.n_blocks, self.suff_plan.n_blocks, 1,
+                     int(self._suff_part.shape[0]))
             self._suff_part = torch.zeros(nb, 2 + self.KS, dtype=torch.float64, device=self.device)
             self._graph_a = self._graph_b = None
 
@@ -314,11 +328,13 @@ class LDAEngine:
         self._cwin = self._cphi_windows(corpus, KS)
         if self._cwin is None:
             self.gs_plan = H.GSPlan(self.dc.doc_len, KS, self._U, dev, xsplit=self.xsplit)
+            self._split_sums(self.gs_plan, corpus)
             rows = nnz
         else:
             self.gs_plan = None
             for w in self._cwin:
                 w["gp"] = H.GSPlan(self.dc.doc_len, KS, self._U, dev, doc_range=(w["d0"], w["d1"]))
+                self._split_sums(w["gp"], corpus)
             rows = max(w["e1"] - w["e0"] for w in self._cwin)
         # one zero pad row past the vocabulary: gs_smallw's constant-offset row loads may read past row V - 1
         self.beta = torch.zeros(V + 1, KS, dtype=f64, device=dev)[:V]
@@ -362,12 +378,19 @@ class LDAEngine:
         elif self.suff_split != "off":
             self._suff_split = self._build_suff_split()
 
+    @staticmethod
+    def _split_sums(gp, corpus: Corpus) -> None:
+        """The split batches' chunk count sums, once per plan (ops/hip.py GSSplitPlan.chunk_sums)."""
+        from ...ops import hip as H
+        if isinstance(gp.split, H.GSSplitPlan):
+            gp.split.chunk_sums(corpus.doc_ptr, corpus.counts)
+
     def _build_stages(self, corpus: Corpus, KS: int) -> dict:
         """Staged beta rows (ops/hip.py GSStage) of every kGsTeam8 launch at KS <= 32, keyed by the id of
         the launch's order tensor.  ONI_GS_STAGE = the budget in GB (default 4; 0 turns them off): a plan
         whose copies would exceed it is left unstaged."""
         from ...ops import hip as H
-        gb = float(knobs.get("ONI_GS_STAGE", "4"))
+        gb = _stage_budget_gb(knobs.get("ONI_GS_STAGE", "4"))
         if KS > 32 or gb <= 0:
             return {}
         cap = gb * 2**30

@@ -63,8 +63,14 @@ def exp_lib():
             _EXP = importlib.import_module("_onihip_exp")
         except Exception as e:  # pragma: no cover - depends on build state
             raise RuntimeError(f"oni_ml_amd experimental HIP extension (_onihip_exp) failed to load: {e!r}. "
-                               "Run `python -m oni_ml_amd._build`.") from e
+                               "It is built only on request: `python -m oni_ml_amd._build exp`.") from e
     return _EXP
+
+
+def exp_available() -> bool:
+    """Whether the opt-in experimental module was built (its tests skip otherwise)."""
+    import glob
+    return bool(glob.glob(os.path.join(os.path.dirname(os.path.dirname(__file__)), "_lib", "_onihip_exp*.so")))
 
 
 def compiled_ks():
@@ -582,10 +588,11 @@ def gs_mstep(cw, class_total, beta, K, gate=None):
 def split_spec(KS: int) -> dict:
     """The split-document plan of ONI_GS_SPLIT_MIN = 'N[,g=G][,batches=B][,words=W]': documents longer
     than N words split (default 2048 at KS > 32, 0 = off at KS <= 32), at most G workgroups per document
-    (16), B launch batches (1), W words of a chunk per workgroup (0: the 8-wave team's prefetch)."""
+    (SPLIT_MAX_SEG), B launch batches (1), W words of a chunk per workgroup (0: the split kernel's
+    prefetched rounds, split_seg_words)."""
     from .. import knobs
     spec = (knobs.get("ONI_GS_SPLIT_MIN") or "").strip()
-    out = dict(min=2048 if KS > 32 else 0, g=16, batches=1, words=0)
+    out = dict(min=2048 if KS > 32 else 0, g=SPLIT_MAX_SEG, batches=1, words=0)
     if spec:
         head, *rest = [x.strip() for x in spec.split(",")]
         if head:
@@ -610,62 +617,132 @@ def gs_split_launch_cap(KS: int) -> int:
     return cap
 
 
-SPLIT_MAX_SEG = 16   # csrc/hip/lda_gs64.hip kSplitMaxSeg
+SPLIT_MAX_SEG = 128        # csrc/hip/lda_gs64.hip kSplitMaxSeg2 (segments per document)
+SPLIT_MAX_SEG_GATHER = 16  # kSplitMaxSeg: up to here one batched gather per chunk, above it the two-phase exchange
 
 
 def gs_team8_words(KS: int) -> int:
     """Words of a chunk one 8-wave fp64 workgroup holds in its prefetched rounds (TeamShape<KS, 8>:
-    slots x RMAX); the split kernel sizes segments to this."""
+    slots x RMAX)."""
     tg = 4 if KS <= 32 else (8 if KS <= 64 else 16)
     kpl = -(-KS // tg)
     return 8 * (64 // tg) * (8 if kpl <= 5 else 4)
 
 
+def split_seg_words(KS: int) -> int:
+    """Words of a chunk one split segment holds in its prefetched rounds: the split kernel's 7 word waves
+    (gs_splitw: TeamShape<KS, 8> slots and RMAX) -- a segment past it streams the rest one gather latency
+    per round."""
+    return gs_team8_words(KS) * 7 // 8
+
+
+def split_chain_cycles(n: int, U: int, G: int, KS: int) -> float:
+    """Modelled cycles of one chunk of an n-word document on G segments (G = 1: the 8-wave team kernel),
+    for the plan's segment allocation only (profiles/r6_split.md): a word-phase term per word of the
+    segment's share plus the exchange (one batched gather up to 16 segments, two round trips beyond)."""
+    W = -(-n // U)
+    per = -(-W // G)
+    sw = split_seg_words(KS)
+    # prefetched rounds cost ~issue + compute; streamed rounds a gather latency each
+    word = 40.0 * min(per, sw) + (1800.0 * -(-(per - sw) // sw) if per > sw else 0.0) + 2000.0
+    if G == 1:
+        return word
+    xch = 4000.0 + (0.0 if G <= 4 else 2500.0 if G <= 8 else 8000.0 if G <= SPLIT_MAX_SEG_GATHER else 6000.0)
+    return word + xch + 1500.0
+
+
 class GSSplitPlan:
-    """Launch batches of the fp64 split-document kernel (gs_split): document d of n words gets
-    G = clamp(ceil(ceil(n / U) / seg_words), 2, max_seg) workgroups, each taking 1/G of every chunk;
-    a batch holds <= gs_split_launch_cap(KS) workgroups (co-resident, so the per-chunk exchange
-    cannot deadlock).  Documents are taken longest first into at most `max_batches` batches (batches
-    run back to back on one stream, so a second batch lengthens the critical path); documents that
-    do not fit stay with the one-workgroup team (``leftover``)."""
+    """Launch batches of the fp64 split-document kernel (gs_split): document d of n words (W = ceil(n / U)
+    words per chunk) gets G workgroups, each taking 1/G of every chunk; a batch holds
+    <= gs_split_launch_cap(KS) workgroups (co-resident, so the per-chunk exchange cannot deadlock).
+
+    G per document is water-filled over the launch cap: every candidate starts at G = 1 (the 8-wave team
+    kernel), and the document whose modelled chunk time (split_chain_cycles) is the largest gets more
+    segments, until the cap is spent or that document is at its most useful G = ceil(W / seg_words) (at most
+    SPLIT_MAX_SEG): the launch shortens the longest chain first; the budget left gives the other candidates
+    two segments each, longest first.  Documents still at G = 1 stay with the team kernel (``leftover``),
+    unless ``max_batches`` > 1 (ONI_GS_SPLIT_MIN batches=B, default 1) allows more batches of the rest
+    (back to back on one stream: a later batch lengthens the critical path)."""
 
     def __init__(self, doc_ids, lengths, KS: int, gs_updates: int, device, seg_words: int = 0,
                  max_seg: int = 0, max_batches: int = 0):
+        import heapq
         import numpy as np
         self.KS = int(KS)
         self.max_blocks = gs_split_launch_cap(KS)
         sp = split_spec(KS)
-        self.seg_words = int(seg_words) or sp["words"] or min(128, gs_team8_words(KS))
-        # the kernel's exchange polls at most SPLIT_MAX_SEG segments per document (lda_gs64.hip kSplitMaxSeg)
-        max_seg = min(int(max_seg) or sp["g"], self.max_blocks, SPLIT_MAX_SEG)
+        # an explicit segment size (ONI_GS_SPLIT_MIN words=W, or the argument) fixes G = clamp(ceil(W / words),
+        # 2, max_seg) per document, longest first; otherwise the modelled water-filling (_allocate)
+        self.fixed = bool(int(seg_words) or sp["words"])
+        self.seg_words = int(seg_words) or sp["words"] or split_seg_words(KS)
+        # KS <= 32: the single-round gather only (gs_splitw has no two-phase exchange in the narrow layout)
+        max_seg = min(int(max_seg) or sp["g"], self.max_blocks,
+                      SPLIT_MAX_SEG if self.KS > 32 else SPLIT_MAX_SEG_GATHER)
         max_batches = int(max_batches) or sp["batches"]
         U = int(gs_updates)
         self.U = U
-        # U past the LDS chunk tables: per-segment tables in a scratch ([n_blocks][U][2][KS] doubles)
-        self.tab_rows = U if U > gs_split_lds_umax(self.KS) else 0
+        self.tab_lds = U <= gs_split_lds_umax(self.KS)
         self.segments = {}
         self.batches = []
         self.leftover = []
-        cur, used = [], 0
-        for d in doc_ids:
-            n = int(lengths[d])
-            W = -(-n // U)
-            G = max(2, min(max_seg, -(-W // self.seg_words)))
-            G = min(G, max(1, W))
-            if used + G > self.max_blocks:
-                if len(self.batches) + 1 >= max_batches:
-                    self.leftover.append(int(d))
-                    continue
-                self.batches.append(self._make(cur, device))
-                cur, used = [], 0
-            self.segments[int(d)] = G
-            cur.append((int(d), G))
-            used += G
-        if cur:
-            self.batches.append(self._make(cur, device))
+        todo = [int(d) for d in doc_ids]
+        while todo and len(self.batches) < max_batches:
+            G = self._allocate(todo, lengths, U, max_seg)
+            docs = [(d, G[d]) for d in todo if G[d] >= 2]
+            if not docs:
+                break
+            for d, g in docs:
+                self.segments[d] = g
+            self.batches.append(self._make(docs, lengths, device))
+            done = {d for d, _ in docs}
+            todo = [d for d in todo if d not in done]
+        self.leftover = todo
         self.n_docs = len(self.segments)
 
-    def _make(self, docs, device):
+    def _allocate(self, docs, lengths, U, max_seg):
+        """Water-filling: segments to the document with the longest modelled chunk, within the cap."""
+        import heapq
+        G = {d: 1 for d in docs}
+        if self.fixed:
+            used = 0
+            for d in docs:
+                W = -(-int(lengths[d]) // U)
+                g = min(max(2, -(-W // self.seg_words)), max_seg, W)
+                if g >= 2 and used + g <= self.max_blocks:
+                    G[d] = g
+                    used += g
+            return G
+        gmax = {}
+        for d in docs:
+            W = -(-int(lengths[d]) // U)
+            # a document with W >= 2 words per chunk can always take two segments
+            gmax[d] = 1 if W < 2 else max(2, min(max_seg, W, -(-W // self.seg_words)))
+        t = lambda d, g: split_chain_cycles(int(lengths[d]), U, g, self.KS)   # noqa: E731
+        heap = [(-t(d, 1), d) for d in docs if gmax[d] >= 2]
+        heapq.heapify(heap)
+        used = 0
+        while heap:
+            tc, d = heapq.heappop(heap)
+            g = G[d]
+            # the fewest more segments that shorten it (the exchange's cost steps up at 5, 9 and 17 segments);
+            # one workgroup -> G segments costs G launch slots
+            gn = next((x for x in range(max(2, g + 1), gmax[d] + 1)
+                       if used + x - (g if g > 1 else 0) <= self.max_blocks and t(d, x) < -tc), None)
+            if gn is None:
+                break     # the longest chain cannot shorten further: the rest cannot set the launch time
+            used += gn - (g if g > 1 else 0)
+            G[d] = gn
+            heapq.heappush(heap, (-t(d, gn), d))
+        # the budget left: two segments for each remaining candidate, longest first -- a co-resident split
+        # launch is dispatched ahead of the short-document floods, where a 512-thread team workgroup can
+        # queue behind them (K = 50: 4.5 -> 3.4 ms per EM iteration, profiles/r3_tuning_log.md)
+        for d in docs:
+            if G[d] == 1 and gmax[d] >= 2 and used + 2 <= self.max_blocks:
+                G[d] = 2
+                used += 2
+        return G
+
+    def _make(self, docs, lengths, device):
         import numpy as np
         sd, si, sc, sb, slot = [], [], [], [], []
         for j, (d, G) in enumerate(docs):
@@ -674,15 +751,49 @@ class GSSplitPlan:
                 sd.append(d), si.append(q), sc.append(G), sb.append(base), slot.append(j)
         t = lambda a: torch.tensor(np.asarray(a, np.int32), device=device)
         nb = len(sd)
-        if sc and max(sc) > SPLIT_MAX_SEG:
-            raise ValueError(f"gs_split: {max(sc)} segments per document > {SPLIT_MAX_SEG}")
+        gmx = SPLIT_MAX_SEG if self.KS > 32 else SPLIT_MAX_SEG_GATHER
+        if sc and max(sc) > gmx:
+            raise ValueError(f"gs_split: {max(sc)} segments per document > {gmx} at KS {self.KS}")
+        if nb > self.max_blocks:
+            raise ValueError(f"gs_split: {nb} workgroups > the launch cap {self.max_blocks}")
+        # U past the LDS chunk tables: per-segment tables in a scratch ([n_blocks][tab_rows][2][KS] doubles),
+        # tab_rows = the batch's largest chunk count (<= U)
+        tab_rows = 0 if self.tab_lds else max(-(-int(lengths[d]) // -(-int(lengths[d]) // self.U)) for d, _ in docs)
+        gr = 2 * (self.KS + 1)
         return dict(seg_doc=t(sd), seg_index=t(si), seg_count=t(sc), seg_base=t(sb), doc_slot=t(slot), n_blocks=nb,
-                    # tagged granules {uint32 half of a double, uint32 tag}: [2][n_blocks][2 (KS + 1)]
-                    xchg=torch.zeros(2 * nb * 2 * (self.KS + 1), dtype=torch.int64, device=device),
+                    # tagged granules {uint32 half of a double, uint32 tag}: [2][n_blocks][2 (KS + 1)] partials,
+                    # then [2][docs][2 (KS + 1)] totals (the two-phase exchange past 16 segments)
+                    xchg=torch.zeros(2 * nb * gr + 2 * len(docs) * gr, dtype=torch.int64, device=device),
                     counter=torch.zeros(2 * len(docs), dtype=torch.int32, device=device),
-                    error=torch.zeros(1, dtype=torch.int32, device=device), docs=len(docs),
-                    tab=(torch.empty(nb * self.tab_rows * 2 * self.KS, dtype=torch.float64, device=device)
-                         if self.tab_rows else None))
+                    error=torch.zeros(1, dtype=torch.int32, device=device), docs=len(docs), tab_rows=tab_rows,
+                    tab=(torch.empty(nb * tab_rows * 2 * self.KS, dtype=torch.float64, device=device)
+                         if tab_rows else None))
+
+    def chunk_sums(self, doc_ptr, counts) -> None:
+        """Each batch document's chunk count sums ([docs][max nch] doubles, exact: integer counts) from the
+        corpus' host doc_ptr / counts, for the kernel's C_j initialisation (built once per plan)."""
+        import numpy as np
+        for b in self.batches:
+            docs = b["seg_doc"].cpu().numpy()[b["seg_base"].cpu().numpy() == np.arange(b["n_blocks"])]
+            rows = []
+            for d in docs:
+                s0, s1 = int(doc_ptr[d]), int(doc_ptr[d + 1])
+                n = s1 - s0
+                W = -(-n // self.U)
+                c = np.asarray(counts[s0:s1], np.float64)
+                nch = -(-n // W)
+                rows.append(np.add.reduceat(c, np.arange(0, n, W)) if n else np.zeros(0))
+                assert rows[-1].size == nch
+            width = max(1, max(r.size for r in rows))
+            cs = np.zeros((len(rows), width), np.float64)
+            for i, r in enumerate(rows):
+                cs[i, :r.size] = r
+            b["csum"] = torch.from_numpy(cs).to(b["seg_doc"].device)
+            b["csum_u"] = self.U
+
+    def scratch_bytes(self) -> int:
+        """Device bytes of the batches' chunk-table scratch (counted in the c.phi budget)."""
+        return sum(b["tab"].numel() * 8 for b in self.batches if b.get("tab") is not None)
 
 
 def gs_split(doc_ptr, word_idx, counts, beta, K, gs_updates, params, gamma, cphi, lik, alpha_ss, iters, batch,
@@ -711,21 +822,34 @@ def gs_split(doc_ptr, word_idx, counts, beta, K, gs_updates, params, gamma, cphi
         _chk(iters, torch.int32, "iters", (D,), dev),
         batch["seg_doc"].data_ptr(), batch["seg_index"].data_ptr(), batch["seg_count"].data_ptr(),
         batch["seg_base"].data_ptr(), batch["doc_slot"].data_ptr(), int(nb),
-        _chk(batch["xchg"], torch.int64, "xchg", (2 * nb * 2 * (KS + 1),), dev),
+        _chk(batch["xchg"], torch.int64, "xchg", (2 * (nb + batch["docs"]) * 2 * (KS + 1),), dev),
         _chk(batch["counter"], torch.int32, "counter", (2 * batch["docs"],), dev), int(batch["docs"]),
         _chk(batch["error"], torch.int32, "error", (1,), dev), _stream(),
         0 if dbg is None else _chk(dbg, torch.int64, "dbg", (8,), dev),
-        _split_tab(batch, nb, int(gs_updates), KS, dev))
+        *_split_tab(batch, nb, int(gs_updates), KS, dev, doc_ptr), *_split_csum(batch, int(gs_updates), dev))
 
 
-def _split_tab(batch, nb, U, KS, dev) -> int:
-    """The split batch's chunk-table scratch (required past the LDS tables' U)."""
+def _split_csum(batch, U, dev):
+    """(address, stride) of the batch's chunk count sums (GSSplitPlan.chunk_sums), (0, 0) if not built."""
+    cs = batch.get("csum")
+    if cs is None:
+        return 0, 0
+    if batch.get("csum_u") != U:
+        raise ValueError(f"gs_split: chunk sums built for U = {batch.get('csum_u')}, launched with U = {U}")
+    _chk(cs, torch.float64, "csum", (batch["docs"], cs.shape[1]), dev)
+    return cs.data_ptr(), int(cs.shape[1])
+
+
+def _split_tab(batch, nb, U, KS, dev, doc_ptr):
+    """(scratch address, rows per workgroup) of the split batch's chunk tables (required past the LDS
+    tables' U); the rows must cover every document's chunk count (the kernel also checks)."""
     tab = batch.get("tab")
     if U > gs_split_lds_umax(KS):
-        if tab is None or tab.numel() < nb * U * 2 * KS:
-            raise ValueError(f"gs_split: U = {U} needs a chunk-table scratch of {nb} x {U} x 2 x {KS} doubles")
-        return _chk(tab, torch.float64, "tab", None, dev)
-    return 0
+        rows = int(batch.get("tab_rows") or 0)
+        if tab is None or rows <= 0 or tab.numel() < nb * rows * 2 * KS:
+            raise ValueError(f"gs_split: U = {U} needs a chunk-table scratch of {nb} x rows x 2 x {KS} doubles")
+        return _chk(tab, torch.float64, "tab", None, dev), rows
+    return 0, 0
 
 
 def gs_xsplit_rows(KS: int) -> int:
@@ -913,6 +1037,8 @@ class GSPlan:
         # 2.20 / 2.27 vs 2.18 / 2.18 ms, then 1.746 / 1.742 / 1.761 vs 1.734 / 1.733 / 1.739 ms per EM
         # iteration; profiles/r2_tuning_log.md, r3_tuning_log.md)
 
+    CHAIN_MAX_W = 2   # widest chunk (words) the one-wave per-word chain kernel takes (csrc/hip/kernels.h kGsChain)
+
     @classmethod
     def wide_u_edges(cls, U: int):
         """Team sizes by CHUNK WIDTH at K > 32 and U > 32 (the c.phi-table team kernels): a team's waves
@@ -925,7 +1051,7 @@ class GSPlan:
         U = 1024 (profiles/r4_tuning_log.md): fixed length edges 172.4 ms per EM iteration, (8, 64) 133.2,
         (4, 32) 107.3, (2, 16) 106.7 with the one-wave team as the first range; the 16-lane kernel's 7
         digamma/exp chains per lane cost more latency per refresh than one wave's 2 (r5g: 66.4 vs 43.1 ms)."""
-        wc, w4 = 2, 16
+        wc, w4 = cls.CHAIN_MAX_W, 16
         ec, e4 = max(256, wc * U), max(2048, w4 * U)
         return ((GS_TEAM8, e4, None), (GS_TEAM4, ec, e4), (GS_CHAIN, 256, ec), (GS_SMALL, None, 256))
 

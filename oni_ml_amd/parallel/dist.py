@@ -472,6 +472,9 @@ def init_from_env(expected_world: int = None, backend: str = None, timeout_s: fl
         dev = torch.device("cuda", local % max(1, torch.cuda.device_count()))
     else:
         dev = torch.device("cpu")
+    if not knobs.get("ONI_THREADS"):       # an explicit ONI_THREADS: the operator sizes the host
+        from ..utils import hostres
+        hostres.bind_rank(local, dev)      # the GPU's NUMA node CPUs, a per-rank thread budget
     forced = knobs.get("ONI_DIST_FORCE_GROUP", "0") == "1"
     ctx = DistContext(rank=rank, world_size=world, local_rank=local, device=dev, backend=backend,
                       deterministic=knobs.get("ONI_DIST_DETERMINISTIC", "0") == "1", forced=forced)

@@ -45,10 +45,7 @@ def take(key: tuple) -> Optional[object]:
     """The prefetched value for ``key`` (waits for it), or None: nothing started for these inputs, or
     the prefetch raised.  Every other prefetch is dropped (its thread finishes on its own)."""
     job = _JOBS.pop(key, None)
-    for t, box in _JOBS.values():      # dropped: a forked child is still reaped and its files removed
-        if t is None:
-            box["collect"]()
-    _JOBS.clear()
+    drop_all()
     if job is None:
         return None
     t, box = job
@@ -56,6 +53,17 @@ def take(key: tuple) -> Optional[object]:
         return box["collect"]()
     t.join()
     return box.get("value")
+
+
+def drop_all() -> None:
+    """Drop every pending prefetch: a forked child is killed, reaped and its /dev/shm directory removed
+    (cmd_ml_ops calls this in a ``finally``, so a run that fails before its load stage leaves no tmpfs
+    files behind; also registered with atexit when a child is forked); a thread finishes on its own."""
+    jobs = list(_JOBS.values())
+    _JOBS.clear()
+    for t, box in jobs:
+        if t is None:
+            box["drop"]()
 
 
 def load_dns_inputs(dns_path, feedback_path, dupfactor, strict, top1m, threads=8):
@@ -98,6 +106,25 @@ def _dns_child(args, out_dir) -> None:
         pickle.dump(meta, f, protocol=pickle.HIGHEST_PROTOCOL)
 
 
+def _dns_drop(pid, rfd, out_dir) -> None:
+    """Kill and reap an uncollected child, remove its files (idempotent)."""
+    import shutil
+    import signal
+    try:
+        os.kill(pid, signal.SIGKILL)
+    except OSError:
+        pass
+    try:
+        os.waitpid(pid, 0)
+    except ChildProcessError:
+        pass
+    try:
+        os.close(rfd)
+    except OSError:
+        pass
+    shutil.rmtree(out_dir, ignore_errors=True)
+
+
 def _dns_collect(pid, rfd, out_dir):
     """The child's result as (DnsTable, top list, host features); None if it failed."""
     import pickle
@@ -126,7 +153,11 @@ def _dns_collect(pid, rfd, out_dir):
         shutil.rmtree(out_dir, ignore_errors=True)   # the mappings stay valid after the unlink
 
 
+_ATEXIT = []
+
+
 def _start_dns_fork(key, args) -> bool:
+    import atexit
     import tempfile
     if threading.active_count() > 1 or not os.path.isdir("/dev/shm"):
         return False
@@ -147,16 +178,20 @@ def _start_dns_fork(key, args) -> bool:
             finally:
                 os._exit(0)
     os.close(wfd)
-    _JOBS[key] = (None, dict(collect=lambda: _dns_collect(pid, rfd, out_dir)))
+    _JOBS[key] = (None, dict(collect=lambda: _dns_collect(pid, rfd, out_dir),
+                             drop=lambda: _dns_drop(pid, rfd, out_dir)))
+    if not _ATEXIT:
+        _ATEXIT.append(atexit.register(drop_all))
     return True
 
 
-def start_for(cfg) -> None:
-    """Start the read of ``cfg``'s inputs (flow or dns)."""
+def start_for(cfg, fork: bool = True) -> None:
+    """Start the read of ``cfg``'s inputs (flow or dns).  ``fork=False`` (a profiler or tracer whose
+    preloaded library may already hold the GPU, cli._tool_attached): the DNS read runs on a thread."""
     if cfg.dsource == "flow":
         from ..features import flow_io
         start(flow_key(cfg), flow_io.load_flow, cfg.flow_path, cfg.feedback_path(), cfg.dupfactor, cfg.threads)
     elif cfg.dsource == "dns":
         args = (cfg.dns_path, cfg.feedback_path(), cfg.dupfactor, cfg.strict, cfg.top1m, cfg.threads)
-        if not _start_dns_fork(dns_key(cfg), args):
+        if not (fork and _start_dns_fork(dns_key(cfg), args)):
             start(dns_key(cfg), load_dns_inputs, *args)

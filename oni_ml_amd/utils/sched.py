@@ -17,10 +17,7 @@ def background_priority() -> None:
     """Raise the calling thread's nice value by BG_NICE (10).  Linux
     applies PRIO_PROCESS with a thread id to that thread only; raising a nice value needs no
     privilege.  Best effort: other platforms or a refused call leave the priority as it is."""
-    try:
-        n = BG_NICE
-    except ValueError:
-        n = 10
+    n = BG_NICE
     if n <= 0 or not hasattr(os, "setpriority"):
         return
     try:

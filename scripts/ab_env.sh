@@ -1,7 +1,7 @@
 #!/bin/bash
 # A/B of bench.py's ms per EM iteration under environment variants, interleaved to cancel drift:
 #   bash scripts/ab_env.sh ROUNDS "ENV_A" "ENV_B" ... -- [bench args]
-#   bash scripts/ab_env.sh 3 "ONI_GS_STAGE=1" "ONI_GS_STAGE=0" -- --steps 20 --warmup 5
+#   bash scripts/ab_env.sh 3 "ONI_GS_STAGE=4" "ONI_GS_STAGE=0" -- --steps 20 --warmup 5
 set -u -o pipefail
 rounds=$1; shift
 variants=()

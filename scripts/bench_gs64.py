@@ -45,12 +45,25 @@ def main():
     ap.add_argument("--prefixes", default="", help="also time the team8 bucket on its N longest documents, e.g. 1,2,8")
     ap.add_argument("--xsplit", type=int, default=0, help="the N longest documents on the XCD-split kernel (gs_xsplit)")
     ap.add_argument("--xsplit-g", type=int, default=0, help="gs_xsplit members per document (0: the LDS minimum)")
+    ap.add_argument("--long", default="", help="a synthetic corpus of only these document lengths (e.g. 443426: "
+                                               "config 5's longest document alone), distinct random words")
+    ap.add_argument("--vocab", type=int, default=4_536_586, help="--long: vocabulary (config 5's month)")
+    ap.add_argument("--sweeps", type=int, default=0, help="timed launches run exactly this many sweeps (no "
+                                                           "convergence test), e.g. 20: a long document's real count")
     a = ap.parse_args()
     from oni_ml_amd.models.lda.em import LDAEngine
     from oni_ml_amd.models.lda.settings import LDASettings
     from oni_ml_amd.ops import hip as H
     from oni_ml_amd.pipeline.flow import synthetic_flow_corpus
-    c, _ = synthetic_flow_corpus(events=a.events, seed=0, device="cuda")
+    if a.long:
+        from oni_ml_amd.corpus.csr import Corpus
+        rng = np.random.default_rng(0)
+        lens = np.asarray([int(x) for x in a.long.split(",")], np.int64)
+        ptr = np.concatenate([[0], np.cumsum(lens)])
+        words = np.concatenate([np.sort(rng.choice(a.vocab, n, replace=False)) for n in lens]).astype(np.int32)
+        c = Corpus(ptr, words, rng.integers(1, 4, words.size).astype(np.int64), a.vocab)
+    else:
+        c, _ = synthetic_flow_corpus(events=a.events, seed=0, device="cuda")
     st = LDASettings()
     st.gs_updates = a.gs_updates
     xs = dict(docs=a.xsplit, members=a.xsplit_g) if a.xsplit else None
@@ -58,6 +71,10 @@ def main():
     eng.init_random()
     eng.em_iterations(a.warm_em, True, c.num_docs, stop=False)
     torch.cuda.synchronize()
+    if a.sweeps:
+        # params {alpha, lgamma const, VAR_MAX_ITER, VAR_CONVERGED, ...}: fixed sweeps for the timed launches
+        eng._params[2] = float(a.sweeps)
+        eng._params[3] = -1e30
     dc = eng.dc
     lens = c.lengths()
     its = eng.iters.cpu().numpy()

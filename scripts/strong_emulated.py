@@ -131,7 +131,7 @@ def main():
                    full_ms=round(t_full * 1e3, 4), chain_floor_ms=round(t_chain * 1e3, 4), ranks={})
         bytes_ = K * c.num_terms * 8
         for n in [int(x) for x in a.ranks.split(",")]:
-            def shard_times(bounds):
+            def shard_times(bounds, chains=None):
                 per = []
                 for d0, d1 in bounds:
                     sh = c.slice_docs(d0, d1)
@@ -140,8 +140,17 @@ def main():
                     per.append(_time_iteration(e, lb, alpha, vmi, D, reps))
                     del e
                     torch.cuda.empty_cache()
+                    if chains is not None:
+                        # the shard's longest document alone: its chain, the floor of that rank
+                        dl_ = d0 + int(np.argmax(lens[d0:d1]))
+                        o1 = c.slice_docs(dl_, dl_ + 1)
+                        e = LDAEngine(Corpus(o1.doc_ptr, o1.word_idx, o1.counts, c.num_terms), K, LDASettings(),
+                                      backend="hip", seed=0, precision="fp64", local_shard=True)
+                        chains.append((int(lens[dl_]), _time_iteration(e, lb, alpha, vmi, D, reps)))
+                        del e
                 return per
-            per = [t_full] if n == 1 else shard_times(shard_bounds(c.doc_ptr, n))
+            chains = []
+            per = [t_full] if n == 1 else shard_times(shard_bounds(c.doc_ptr, n), chains)
             # chain-aware shards (parallel/dist.py chain_bounds, ONI_SHARD_CHAIN=1): the longest document alone
             cb = shard_bounds(c.doc_ptr, n, chain=True, K=K) if n > 1 else None
             per_chain = shard_times(cb) if cb is not None and cb != shard_bounds(c.doc_ptr, n) else None
@@ -155,6 +164,8 @@ def main():
             else:
                 xrows, xms = 0, 0.0
             rec["ranks"][n] = dict(per_rank_ms=[round(x * 1e3, 4) for x in per], max_ms=round(mx * 1e3, 4),
+                                   per_rank_longest_words=[w for w, _ in chains],
+                                   per_rank_chain_ms=[round(t * 1e3, 4) for _, t in chains],
                                    chain_aware_per_rank_ms=None if per_chain is None else [round(x * 1e3, 4) for x in per_chain],
                                    chain_aware_max_ms=None if mc is None else round(mc * 1e3, 4),
                                    chain_aware_speedup_mesh=None if mc is None else round(t_full / (mc + mesh), 3),
@@ -178,6 +189,13 @@ def main():
             L.append(f"docs {rec['docs']}, nnz {rec['nnz']}, V {rec['vocab']}; longest document {rec['longest_doc']} "
                      f"words; one GPU {rec['full_ms']} ms / EM iteration; **chain floor** (longest document alone) "
                      f"{rec['chain_floor_ms']} ms = at most {rec['full_ms'] / max(rec['chain_floor_ms'], 1e-9):.2f}x")
+            L.append("")
+            L.append("Per-rank longest document (words) and its chain alone (ms), plain cuts:")
+            L.append("")
+            for n, r in rec["ranks"].items():
+                if r.get("per_rank_chain_ms"):
+                    L.append(f"- N = {n}: " + ", ".join(f"{w} w / {t} ms" for w, t in zip(r["per_rank_longest_words"],
+                                                                                        r["per_rank_chain_ms"])))
             L.append("")
             L.append("| N | max shard ms | per-rank ms | all-reduce ring / mesh ms | iteration ms (ring / mesh) | speedup (ring / mesh) | chain-aware: max shard ms, per-rank ms, speedup (mesh) | sparse exchange: rows, ms, iteration ms, speedup |")
             L.append("|---|---|---|---|---|---|---|---|")

@@ -253,19 +253,26 @@ def test_staged_rows_bitwise_equal_beta_rows(monkeypatch):
         assert np.array_equal(a, b)
 
 
-@pytest.mark.parametrize("K,env,U", [
-    (100, {}, 32),                                                      # default split for KS > 32
-    (100, {"ONI_GS_SPLIT_MIN": "4000"}, 32),
-    (100, {"ONI_GS_SPLIT_MIN": "4000,g=3,batches=8", "ONI_SPLIT_MAX_BLOCKS": "9"}, 32),
-    (20, {"ONI_GS_SPLIT_MIN": "3000,g=5"}, 32),                         # forced on a narrow KS
-    (52, {"ONI_GS_SPLIT_MIN": "2500"}, 32),
-    (50, {}, 64),                                                       # 64-row LDS tables (KS 52, U = 64)
-    (50, {"ONI_GS_SPLIT_MIN": "2500,g=3"}, 48),
-    # 16 / 6-8 / 2-4 segments: the exchange's per-column, 8- and 4-segment batched polls
-    (100, {"ONI_GS_SPLIT_MIN": "2500,g=16,words=16"}, 32),
-    (20, {"ONI_GS_SPLIT_MIN": "2500,g=12,words=24"}, 32),
+@pytest.mark.parametrize("K,env,U,gmin", [
+    (100, {}, 32, 2),                                                   # default split for KS > 32
+    (100, {"ONI_GS_SPLIT_MIN": "4000"}, 32, 2),
+    (100, {"ONI_GS_SPLIT_MIN": "4000,g=3,batches=8", "ONI_SPLIT_MAX_BLOCKS": "9"}, 32, 2),
+    (20, {"ONI_GS_SPLIT_MIN": "3000,g=5"}, 32, 2),                      # forced on a narrow KS
+    (52, {"ONI_GS_SPLIT_MIN": "2500"}, 32, 2),
+    (50, {}, 64, 2),                                                    # 64-row LDS tables (KS 52, U = 64)
+    (50, {"ONI_GS_SPLIT_MIN": "2500,g=3"}, 48, 2),
+    # the single-round gathers: per-column passes up to 16 segments, batched at <= 8
+    (100, {"ONI_GS_SPLIT_MIN": "2500,g=16,words=16"}, 32, 9),
+    (100, {"ONI_GS_SPLIT_MIN": "2500,g=8,words=16"}, 32, 5),
+    (20, {"ONI_GS_SPLIT_MIN": "2500,g=12,words=24"}, 32, 9),
+    # the two-phase exchange (reduce-scatter of owned columns + all-gather of the totals) past 16 segments
+    (100, {"ONI_GS_SPLIT_MIN": "2500,g=32,words=8"}, 32, 32),
+    (100, {"ONI_GS_SPLIT_MIN": "2500,g=64,words=8"}, 32, 64),
+    (100, {"ONI_GS_SPLIT_MIN": "2500,words=4"}, 32, 100),              # G > NC: segments owning no column
+    (50, {"ONI_GS_SPLIT_MIN": "2500,g=64,words=4"}, 64, 64),
+    (50, {"ONI_GS_SPLIT_MIN": "2500,g=32,words=4"}, 64, 32),
 ])
-def test_split_documents_match_oracle(K, env, U, monkeypatch):
+def test_split_documents_match_oracle(K, env, U, gmin, monkeypatch):
     """gs_split (one document over G workgroups exchanging tagged per-chunk partials) against the
     oracle: every replica runs the same refresh, so gamma / likelihood / class_word match at 1e-10."""
     for k, v in env.items():
@@ -275,6 +282,23 @@ def test_split_documents_match_oracle(K, env, U, monkeypatch):
     lens = np.minimum(rng.zipf(1.5, D), 200)
     lens[:7] = [30000, 20000, 12000, 9100, 5000, 3100, 2600]
     lens[9] = 0
+    _check_split(K, U, lens, V, env, gmin, rng)
+
+
+@pytest.mark.parametrize("K,U,g", [(100, 1024, 32), (100, 1024, 64), (50, 64, 64)])
+def test_split_wide_u_two_phase_match_oracle(K, U, g, monkeypatch):
+    """The two-phase exchange with the chunk tables past LDS (U = 1024, lda-c's per-word schedule at K = 100:
+    a 70 k-word document has W = 69 words per chunk, so up to 64 segments) and at K = 50, U = 64."""
+    monkeypatch.setenv("ONI_GS_SPLIT_MIN", f"2500,g={g},words=1")
+    rng = np.random.default_rng(K + U)
+    V, D = 90000, 200
+    lens = np.minimum(rng.zipf(1.5, D), 200)
+    lens[:4] = [70000, 33000, 9000, 3000]
+    _check_split(K, U, lens, V, {"ONI_GS_SPLIT_MIN": "x"}, g, rng)
+
+
+def _check_split(K, U, lens, V, env, gmin, rng):
+    D = lens.size
     ptr = np.concatenate([[0], np.cumsum(lens)])
     words = np.concatenate([rng.choice(V, n, replace=False) for n in lens]).astype(np.int32)
     counts = rng.integers(1, 4, words.size)
@@ -285,10 +309,7 @@ def test_split_documents_match_oracle(K, env, U, monkeypatch):
     eng, sc = _gpu_estep(c, K, lb, 0.33, LDASettings(var_max_iter=5, var_converged=-1e30), U)
     sp = eng.gs_plan.split
     assert sp is not None and sp.n_docs >= (4 if "ONI_GS_SPLIT_MIN" in env else 2)
-    assert max(sp.segments.values()) >= 2
-    if "words=" in env.get("ONI_GS_SPLIT_MIN", ""):
-        G = sorted(sp.segments.values())
-        assert G[-1] > 8 and any(4 < g <= 8 for g in G), G
+    assert max(sp.segments.values()) >= max(2, gmin), sp.segments
     if "ONI_SPLIT_MAX_BLOCKS" in env:
         assert len(sp.batches) >= 2
     assert int(sum(b["error"].item() for b in sp.batches)) == 0
@@ -465,7 +486,11 @@ def test_large_u_needs_wide_topics():
 def test_xsplit_documents_match_oracle(K, xs):
     """gs_xsplit (csrc/hip/experimental/lda_xsplit.hip: one document over one-wave members of one XCD, beta rows resident
     in LDS, 16-byte self-tagged granules) against the oracle at 1e-10, every member replaying the same
-    refresh; graph replay moves the launch epoch on."""
+    refresh; graph replay moves the launch epoch on.  The experimental module is built only on request
+    (`python -m oni_ml_amd._build exp`; measured not faster, profiles/r5_xcd_split.md)."""
+    from oni_ml_amd.ops import hip as H
+    if not H.exp_available():
+        pytest.skip("experimental module _onihip_exp not built (python -m oni_ml_amd._build exp)")
     rng = np.random.default_rng(K + 7)
     V, D = 40000, 260
     lens = np.minimum(rng.zipf(1.5, D), 200)

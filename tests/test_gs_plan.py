@@ -22,30 +22,60 @@ def test_isolate_longest_short_lists():
     assert GSPlan.isolate_longest(np.array([5], dtype=np.int32), 2).tolist() == [5]
 
 
-def test_split_plan_one_batch_longest_first(monkeypatch):
-    """GSSplitPlan: G = clamp(ceil(ceil(n / U) / seg_words), 2, max_seg); longest documents first into
-    one co-resident batch, the rest left to the one-workgroup team; batch arrays consistent."""
+def test_split_plan_water_fills_the_longest_chain(monkeypatch):
+    """GSSplitPlan: segments go to the document with the longest modelled chunk (split_chain_cycles) until the
+    cap is spent or that document is at its most useful G = ceil(W / seg_words); the rest stay with the
+    one-workgroup team; batch arrays consistent; the exchange buffer holds the partials and the totals rows."""
     from oni_ml_amd.ops import hip as H
     monkeypatch.setattr(H, "gs_split_launch_cap", lambda KS: 20)
     lens = np.array([82418, 5000, 30000, 4200, 9100, 100, 12000], dtype=np.int64)
     order = np.argsort(-lens, kind="stable")
     cand = order[lens[order] > 4096]
-    sp = H.GSSplitPlan(cand, lens, 100, 32, "cpu", seg_words=128, max_seg=16)
-    # 82418 -> W 2576 -> 16 segments; 30000 -> 938 -> 8 does not fit (16 + 8 > 20); 12000 -> 375 -> 3;
-    # 9100 -> 285 -> 3 does not fit (19 + 3); 5000 -> 157 -> 2 does not fit
-    assert sp.segments == {0: 16, 6: 3}
-    assert sorted(sp.leftover) == [1, 2, 3, 4]      # 4200 -> 132 -> 2 does not fit either
-    assert len(sp.batches) == 1
+    U, KS = 32, 100
+    sp = H.GSSplitPlan(cand, lens, KS, U, "cpu", max_seg=16)
+    assert len(sp.batches) == 1 and not sp.fixed
     b = sp.batches[0]
-    assert b["n_blocks"] == 19 and b["docs"] == 2
-    assert b["seg_doc"].tolist() == [0] * 16 + [6] * 3
-    assert b["seg_index"].tolist() == list(range(16)) + [0, 1, 2]
-    assert b["seg_base"].tolist() == [0] * 16 + [16] * 3
-    assert b["xchg"].numel() == 2 * 19 * 2 * 101
-    # several batches when allowed
-    sp2 = H.GSSplitPlan(cand, lens, 100, 32, "cpu", seg_words=128, max_seg=16, max_batches=8)
-    assert sp2.leftover == [] and len(sp2.batches) >= 2
-    assert all(bb["n_blocks"] <= 20 for bb in sp2.batches)
+    assert b["n_blocks"] == sum(sp.segments.values()) <= 20
+    sw = H.split_seg_words(KS)
+    gmax = {int(d): max(2, min(16, -(-(-(-int(lens[d]) // U)) // sw))) for d in cand}
+    assert all(2 <= g <= gmax[d] for d, g in sp.segments.items())
+    assert sp.segments[0] == max(sp.segments.values())            # the longest document the most
+    assert sorted(sp.leftover + list(sp.segments)) == sorted(cand.tolist())
+    t = {int(d): H.split_chain_cycles(int(lens[d]), U, sp.segments.get(int(d), 1), KS) for d in cand}
+    top = max(t, key=t.get)
+    # the longest modelled chain cannot shorten: at its useful maximum, or no room for its next segment
+    g = sp.segments.get(top, 1)
+    free = 20 - b["n_blocks"]
+    assert not any(x - (g if g > 1 else 0) <= free and H.split_chain_cycles(int(lens[top]), U, x, KS) < t[top]
+                   for x in range(max(2, g + 1), gmax[top] + 1))
+    base = 0
+    for j, (d, g) in enumerate(sp.segments.items()):
+        sl = slice(base, base + g)
+        assert b["seg_doc"][sl].tolist() == [d] * g and b["seg_index"][sl].tolist() == list(range(g))
+        assert b["seg_base"][sl].tolist() == [base] * g and b["doc_slot"][sl].tolist() == [j] * g
+        base += g
+    assert b["xchg"].numel() == 2 * (b["n_blocks"] + b["docs"]) * 2 * (KS + 1)
+    assert b["tab"] is None and b["tab_rows"] == 0
+    # past 16 segments (the two-phase exchange) and past the LDS chunk tables: a scratch per workgroup of
+    # the batch's largest chunk count
+    monkeypatch.setattr(H, "gs_split_launch_cap", lambda KS: 192)
+    big = np.array([443426, 54924, 30000, 9000], dtype=np.int64)
+    sp = H.GSSplitPlan(np.arange(4), big, KS, 32, "cpu")
+    assert sp.segments[0] == -(-(-(-443426 // 32)) // H.split_seg_words(KS)) > 100
+    assert sum(sp.segments.values()) <= 192 and sp.segments.get(1, 1) >= 2
+    sp = H.GSSplitPlan(np.arange(2), big, KS, 1024, "cpu")
+    (b,) = sp.batches
+    assert b["tab_rows"] == max(-(-n // -(-n // 1024)) for n in big[:2]) and \
+        b["tab"].numel() == b["n_blocks"] * b["tab_rows"] * 2 * KS
+    # several batches when allowed: the rest of the candidates in later batches
+    monkeypatch.setattr(H, "gs_split_launch_cap", lambda KS: 9)
+    sp2 = H.GSSplitPlan(cand, lens, KS, U, "cpu", seg_words=128, max_seg=3, max_batches=8)
+    assert all(bb["n_blocks"] <= 9 for bb in sp2.batches)
+    assert len(sp2.batches) >= 2 and sp2.leftover == [] and set(sp2.segments) == set(cand.tolist())
+    # an explicit segment size: G = clamp(ceil(W / words), 2, max_seg), longest first, while the cap allows
+    monkeypatch.setattr(H, "gs_split_launch_cap", lambda KS: 20)
+    sp3 = H.GSSplitPlan(cand, lens, KS, U, "cpu", seg_words=128, max_seg=16)
+    assert sp3.fixed and sp3.segments == {0: 16, 6: 3} and sorted(sp3.leftover) == [1, 2, 3, 4]
 
 
 def test_csc_subset_partitions_each_word_in_order():

@@ -76,3 +76,32 @@ def test_input_prefetch_keeps_outputs(tmp_path):
             assert load and load[0]["prefetched"] is (v == "1")
             outs[v] = {f: (lp / f).read_bytes() for f in files[src]}
         assert outs["1"] == outs["0"], src
+
+
+def test_dns_prefetch_dropped_on_failure(tmp_path):
+    """A forked DNS prefetch that no load stage collects (a run failing before its load stage) is killed,
+    reaped and its /dev/shm directory removed by prefetch.drop_all (cmd_ml_ops' finally) -- ADVICE r5."""
+    from oni_ml_amd.synth.dns import generate_dns_day
+    g = generate_dns_day(str(tmp_path / "dns"), events=2000, seed=1, files=2)
+    code = f"""
+import glob, os
+from oni_ml_amd.pipeline import prefetch
+before = set(glob.glob('/dev/shm/oni_prefetch_*'))
+args = ({g['dns_path']!r}, None, 1000, True, {g['top1m']!r}, 2)
+assert prefetch._start_dns_fork(('dns',), args)
+(_, box), = prefetch._JOBS.values()
+made = set(glob.glob('/dev/shm/oni_prefetch_*')) - before
+assert len(made) == 1, made
+prefetch.drop_all()
+assert not prefetch._JOBS
+assert not (set(glob.glob('/dev/shm/oni_prefetch_*')) - before)
+try:
+    os.waitpid(-1, os.WNOHANG)
+    raise SystemExit('a child is left')
+except ChildProcessError:
+    pass
+print('ok')
+"""
+    r = subprocess.run([sys.executable, "-c", code], cwd=ROOT, env=dict(os.environ, PYTHONPATH=ROOT),
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and r.stdout.strip() == "ok", r.stderr[-2000:]
