@@ -175,7 +175,9 @@ def _e2e_warm(args, ctx, dev, tmp):
     wall = ctx.allreduce_max(time.perf_counter() - t0)
     out = dict(e2e_wall_s=round(wall, 3), e2e_stage_s={k: round(v, 3) for k, v in s.get("stage_seconds", {}).items()},
                e2e_em_iters=s.get("lda", {}).get("em_iterations"), e2e_flagged=s.get("scored"),
-               e2e_corpus=s.get("corpus"))
+               e2e_corpus=s.get("corpus"),
+               # the lda stage's own breakdown (estimate(): engine setup, EM loop, model copies, final pass)
+               e2e_lda_timing=s.get("lda", {}).get("timing"))
     return out
 
 
@@ -224,6 +226,7 @@ def _e2e_cold(args, ctx, tmp):
             out["e2e_cold_inprocess_wall_s"] = round(float(sm.get("wall_seconds", 0.0)), 3)
             out["e2e_cold_startup_s"] = round(wall - float(sm.get("wall_seconds", 0.0)), 3)
             out["e2e_cold_flagged"] = sm.get("scored")
+            out["e2e_cold_lda_timing"] = sm.get("lda", {}).get("timing")
             out["e2e_cold_startup_marks"] = sm.get("startup_marks")
         except (OSError, ValueError):
             pass
@@ -335,10 +338,12 @@ def main():
         _log("weak scaling: one day per rank")
         cw, _, wnames = build_corpus(args, args.seed + 1000 * rank, dev)
         from oni_ml_amd.pipeline.flow import unify_vocabulary
-        cw, _ = unify_vocabulary(ctx, cw, wnames)
+        cw, vocab = unify_vocabulary(ctx, cw, wnames)
         value_weak, wrec = _to_convergence(args, cw, ctx, dev, args.seed + 1, local=True)
+        import hashlib
         extra.update(weak_em_iters=wrec["em_iters"], weak_seconds=wrec["seconds"], weak_docs=wrec["docs"],
-                     weak_exchange=wrec["exchange"])
+                     weak_exchange=wrec["exchange"], weak_vocab=len(vocab),
+                     weak_vocab_sha16=hashlib.sha256("\n".join(vocab).encode()).hexdigest()[:16])
         del cw
     extra["weak_docs_per_sec"] = round(value_weak, 1)
 

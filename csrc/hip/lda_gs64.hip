@@ -406,7 +406,7 @@ __global__ __launch_bounds__(256) void gs_small(GSArgs a) {
 // owning the topic.  Words wrap into the next sweep (a stopped run discards D prefetched rows).
 template <int KS, int D>
 __global__ __launch_bounds__(256) void gs_chain(GSArgs a) {
-  static_assert(KS > 32 && KS <= 128, "gs_chain: 32 < KS <= 128");
+  static_assert(KS <= 128, "gs_chain: KS <= 128");
   constexpr int TC = (KS + 63) / 64;
   // TC = 2: lane l holds the topic pair 2l, 2l + 1 and loads it with one 16-byte load (KS even)
   constexpr bool PAIR = TC == 2;
@@ -439,8 +439,12 @@ __global__ __launch_bounds__(256) void gs_chain(GSArgs a) {
       const dvec2 x = *reinterpret_cast<const dvec2*>(a.beta + (size_t)w * KS + 2 * lane);
       v[0] = x.x;
       v[1] = x.y;
-    } else {
+    } else if constexpr (KS >= 64) {
       v[0] = a.beta[(size_t)w * KS + lane];
+    } else {
+      // KS <= 32 (lda-c's per-word schedule at K <= 32): lanes past KS hold no topic and read nothing
+      // (64 - KS of them would run past beta's one pad row)
+      v[0] = lane < KS ? a.beta[(size_t)w * KS + lane] : 0.0;
     }
   };
   double total = 0.0;
@@ -964,8 +968,10 @@ __device__ __forceinline__ void stream_tail(const double* __restrict__ beta, con
 template <int KS, int NW, int MINW = 1, bool GMT = false>
 __global__ __launch_bounds__(team_threads(KS, NW), MINW) void gs_team(GSArgs a) {
   using T = TeamShape<KS, NW>;
+  // (KS <= 32 GMT, the parity mode: 4 / 2 prefetched rounds -- 8 spilled 284 bytes at KS = 20, 4 at KS 24-32)
   constexpr int DPB = T::DPB, NTD = T::NTD, TG = T::TG, KPL = T::KPL, NSW = T::NSW, LSW = T::LSW, NS = T::NS,
-                TO = T::TO, RMAX = T::RMAX;
+                TO = T::TO, RMAX = (GMT && KS <= 32) ? (T::RMAX < (KS <= 20 ? 4 : 2) ? T::RMAX : (KS <= 20 ? 4 : 2))
+                                                         : T::RMAX;
   constexpr bool PAIR = T::PAIR;
   // GM (one-wave documents at KS > 32, and every team size when GMT: U > kGsUMax refreshes per
   // sweep): the chunk tables live in the document's own c*phi rows instead of LDS (2 x 32 x KS
@@ -973,7 +979,9 @@ __global__ __launch_bounds__(team_threads(KS, NW), MINW) void gs_team(GSArgs a) 
   // row j W, the E chunk j used in row j W + 1 (chunks of >= 2 words).  A one-word chunk's C_j IS
   // that word's c*phi (E_j r b), so documents of <= U words need no final pass at all.
   constexpr bool GM = GMT || (NW == 1 && KS > 32);
-  static_assert(!GMT || KS > 32, "U > kGsUMax: KS > 32 team kernels only");
+  // KS <= 32 with U > kGsUMax (lda-c's per-word schedule at K <= 32): the 4- and 8-wave teams only (DPB == 1,
+  // so the early returns stay workgroup-uniform); the one-wave range goes to gs_chain there
+  static_assert(!GMT || KS > 32 || NW > 1, "U > kGsUMax at KS <= 32: 4- and 8-wave team kernels only");
   constexpr int UT = GM ? 1 : kGsUMax;
   __shared__ double sC[DPB][UT][KS];         // chunk contributions (previous sweep)
   __shared__ double sEt[DPB][UT][KS];        // E each chunk used (final pass)
@@ -2785,6 +2793,8 @@ static void gs_estep_ks(const GSArgs& a, int variant, hipStream_t s) {
       break;
     }
     case kGsSmall: {
+      if (KS <= 32 && a.gs_updates > kGsUMax)
+        throw std::runtime_error("gs_estep: gs_small keeps its chunk tables in LDS (U <= 32 at KS <= 32)");
       if constexpr (KS <= 32)
         hipLaunchKernelGGL((gs::gs_small<KS>), dim3((a.n_items + 15) / 16), dim3(256), 0, s, a);
       else
@@ -2792,12 +2802,11 @@ static void gs_estep_ks(const GSArgs& a, int variant, hipStream_t s) {
       break;
     }
     case kGsChain:
-      if constexpr (KS > 32)
-        hipLaunchKernelGGL((gs::gs_chain<KS, 8>), dim3((a.n_items + 3) / 4), dim3(256), 0, s, a);
-      else
-        throw std::runtime_error("gs_estep: the chain kernel needs KS > 32");
+      hipLaunchKernelGGL((gs::gs_chain<KS, 8>), dim3((a.n_items + 3) / 4), dim3(256), 0, s, a);
       break;
     case kGsTeam1: {
+      if (KS <= 32 && a.gs_updates > kGsUMax)
+        throw std::runtime_error("gs_estep: the one-wave team keeps its chunk tables in LDS (U <= 32 at KS <= 32)");
       // one wave per document (<= 256 words, chunks of <= 8 words): the topic-group layout keeps
       // more lanes busy than one word per lane (measured 0.90 vs 1.13 ms on the headline corpus)
       constexpr int dpb = gs::TeamShape<KS, 1>::DPB;
@@ -2812,7 +2821,10 @@ static void gs_estep_ks(const GSArgs& a, int variant, hipStream_t s) {
       break;
     }
     case kGsTeam4:
-      if constexpr (KS <= 32) {
+      if (KS <= 32 && a.gs_updates > kGsUMax) {
+        // lda-c's per-word schedule at K <= 32: the topic-group team with its chunk tables in the c*phi rows
+        hipLaunchKernelGGL((gs::gs_team<KS, 4, 1, true>), dim3(a.n_items), dim3(256), 0, s, a);
+      } else if constexpr (KS <= 32) {
         // one wave per document, a word per lane, in-wave refresh: 2.128 / 2.129 / 2.143 vs 2.136 / 2.141 /
         // 2.144 ms per EM iteration for 3 word waves + a topic wave (3 A/B rounds, profiles/r3_tuning_log.md):
         // a quarter of the waves for the same chains leaves the CUs to the other buckets
@@ -2824,7 +2836,10 @@ static void gs_estep_ks(const GSArgs& a, int variant, hipStream_t s) {
         hipLaunchKernelGGL((gs::gs_team<KS, 4>), dim3(a.n_items), dim3(256), 0, s, a);
       break;
     case kGsTeam8:
-      if constexpr (KS <= 32) {
+      if (KS <= 32 && a.gs_updates > kGsUMax) {
+        if (a.stage != nullptr) throw std::runtime_error("gs_estep: no staged rows past U = 32 at KS <= 32");
+        hipLaunchKernelGGL((gs::gs_team<KS, 8, 1, true>), dim3(a.n_items), dim3(512), 0, s, a);
+      } else if constexpr (KS <= 32) {
         // longest documents: 7 word waves x 2 prefetched words per lane + a topic wave (5 x 3: 2.64 ms, 3 x 4:
         // 2.06 ms vs 1.74 per headline EM iteration; profiles/r4_tuning_log.md).  Staged rows (GSStage): every
         // next-chunk round gathered after the arrival (1.726-1.740 vs 1.824-1.833 ms for an early round-0
@@ -2846,7 +2861,8 @@ static void gs_estep_ks(const GSArgs& a, int variant, hipStream_t s) {
   ONI_HIP_CHECK(hipGetLastError());
 }
 
-int gs_umax(int KS) { return KS > 32 ? kGsUMaxWide : kGsUMax; }
+// every KS: U > kGsUMax keeps the chunk tables in the c*phi rows (gs_team GMT, gs_chain, gs_smallw at KS > 32)
+int gs_umax(int KS) { (void)KS; return kGsUMaxWide; }
 
 void launch_gs_stage(const double* beta, const int* word_idx, const int* tile_ent, const int* tile_cnt, int n_tiles,
                      double* stage, int KS, const double* gate, hipStream_t s) {

@@ -312,8 +312,7 @@ class LDAEngine:
             u = parity_gs_updates(self.K)
         u = u or min(32, H.gs_umax(KS))
         if not 1 <= u <= H.gs_umax(KS):
-            raise ValueError(f"gs_updates={u}: the GPU engine supports 1..{H.gs_umax(KS)} at K={self.K} "
-                             f"(more than {H.gs_umax()} needs K > 32)")
+            raise ValueError(f"gs_updates={u}: the GPU engine supports 1..{H.gs_umax(KS)} at K={self.K}")
         return u
 
     def _init_gs64(self, corpus: Corpus):
@@ -391,7 +390,7 @@ class LDAEngine:
         whose copies would exceed it is left unstaged."""
         from ...ops import hip as H
         gb = _stage_budget_gb(knobs.get("ONI_GS_STAGE", "4"))
-        if KS > 32 or gb <= 0:
+        if KS > 32 or gb <= 0 or self._U > 32:   # U > 32: the topic-group team reads beta (no gs_wsteam)
             return {}
         cap = gb * 2**30
         plans = [self.gs_plan] if self._cwin is None else [w["gp"] for w in self._cwin]

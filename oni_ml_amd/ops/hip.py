@@ -315,8 +315,8 @@ GS_SMALL_MAX = 64   # csrc/hip/lda_gs64.hip kGsSmallMax
 
 
 def gs_umax(KS: int = 0) -> int:
-    """Largest U (gamma refreshes per sweep) of the fp64 engine: 32 with the chunk tables in LDS
-    (KS <= 32, and the split-document kernel), more at KS > 32 (tables in the c.phi rows)."""
+    """Largest U (gamma refreshes per sweep) of the fp64 engine: 4096 at every KS -- past 32 the chunk
+    tables live in the c.phi rows (gs_team GMT, gs_chain; at KS > 32 also gs_smallw)."""
     return int(lib().gs_umax(int(KS)))
 
 
@@ -1018,8 +1018,8 @@ class GSPlan:
         # under round-robin dispatch (isolate_longest, a speed hint)
         iso = 1 if KS <= 32 else 0
         edges = self.EDGES_NARROW if KS <= 32 else self.EDGES
-        if KS > 32 and int(gs_updates) > 32:
-            edges = self.wide_u_edges(int(gs_updates))
+        if int(gs_updates) > 32:
+            edges = self.wide_u_edges(int(gs_updates)) if KS > 32 else self.narrow_wide_u_edges(int(gs_updates))
         for var, lo, hi in edges:
             lo_ = tiny if lo is None else lo
             m = (Ls > lo_) if hi is None else ((Ls > lo_) & (Ls <= hi))
@@ -1054,6 +1054,17 @@ class GSPlan:
         wc, w4 = cls.CHAIN_MAX_W, 16
         ec, e4 = max(256, wc * U), max(2048, w4 * U)
         return ((GS_TEAM8, e4, None), (GS_TEAM4, ec, e4), (GS_CHAIN, 256, ec), (GS_SMALL, None, 256))
+
+    @classmethod
+    def narrow_wide_u_edges(cls, U: int):
+        """KS <= 32 at U > 32 (lda-c's per-word schedule at K = 20, an opt-in parity mode): the LDS-table
+        kernels (gs_small, the one-wave and word-per-lane teams, gs_wsteam) cannot hold U chunk tables, so
+        every document past the tiny kernel's range runs with its tables in the c.phi rows: the per-word chain
+        kernel (one wave per document, a topic per lane) up to chunks of CHAIN_MAX_W words, then the 4- and
+        8-wave topic-group teams (gs_team GMT) by chunk width as at KS > 32."""
+        wc, w4 = cls.CHAIN_MAX_W, 16
+        ec, e4 = wc * U, max(2048, w4 * U)
+        return ((GS_TEAM8, e4, None), (GS_TEAM4, ec, e4), (GS_CHAIN, None, ec))
 
     @staticmethod
     def isolate_longest(o, m: int, xcds: int = 8):

@@ -73,6 +73,18 @@ def _exchange_model(c, bounds, K):
     return mx, t, dense
 
 
+def _local(sh, V, lb, compact):
+    """(corpus, model) of one rank's documents: with ``compact`` the vocabulary is the shard's own words
+    (renumbered, beta columns sliced), as a rank's real iteration touches them -- the sparse exchange
+    engine's M-step and suff-stats cover only its local rows (parallel/dist.py VocabExchange, em.py
+    _overlap); without, a full-V M-step per rank (~4.5 ms at config 5) is charged to every shard."""
+    from oni_ml_amd.corpus.csr import Corpus
+    if not compact:
+        return Corpus(sh.doc_ptr, sh.word_idx, sh.counts, V), lb
+    words, inv = np.unique(sh.word_idx, return_inverse=True)
+    return Corpus(sh.doc_ptr, inv.astype(np.int32), sh.counts, int(words.size)), np.ascontiguousarray(lb[:, words])
+
+
 def _time_iteration(eng, lb, alpha, vmi, D, reps):
     ts = []
     for _ in range(reps):
@@ -92,6 +104,8 @@ def main():
     ap.add_argument("--ranks", default="1,2,4,8")
     ap.add_argument("--warm-em", type=int, default=6)
     ap.add_argument("--reps", type=int, default=7)
+    ap.add_argument("--compact", type=int, default=1,
+                    help="1: each shard on its own words (the sparse-exchange engine's local M-step); 0: full V")
     ap.add_argument("--json")
     ap.add_argument("--md")
     a = ap.parse_args()
@@ -123,9 +137,9 @@ def main():
         lens = c.lengths()
         dl = int(np.argmax(lens))
         one = c.slice_docs(dl, dl + 1)
-        e1 = LDAEngine(Corpus(one.doc_ptr, one.word_idx, one.counts, c.num_terms), K, LDASettings(), backend="hip",
-                       seed=0, precision="fp64", local_shard=True)
-        t_chain = _time_iteration(e1, lb, alpha, vmi, D, reps)
+        c1, lb1 = _local(one, c.num_terms, lb, a.compact)
+        e1 = LDAEngine(c1, K, LDASettings(), backend="hip", seed=0, precision="fp64", local_shard=True)
+        t_chain = _time_iteration(e1, lb1, alpha, vmi, D, reps)
         del e1
         rec = dict(label=cfg["label"], docs=D, nnz=c.nnz, vocab=c.num_terms, K=K, longest_doc=int(lens[dl]),
                    full_ms=round(t_full * 1e3, 4), chain_floor_ms=round(t_chain * 1e3, 4), ranks={})
@@ -135,18 +149,18 @@ def main():
                 per = []
                 for d0, d1 in bounds:
                     sh = c.slice_docs(d0, d1)
-                    e = LDAEngine(Corpus(sh.doc_ptr, sh.word_idx, sh.counts, c.num_terms), K, LDASettings(),
-                                  backend="hip", seed=0, precision="fp64", local_shard=True)
-                    per.append(_time_iteration(e, lb, alpha, vmi, D, reps))
+                    cs_, lbs = _local(sh, c.num_terms, lb, a.compact)
+                    e = LDAEngine(cs_, K, LDASettings(), backend="hip", seed=0, precision="fp64", local_shard=True)
+                    per.append(_time_iteration(e, lbs, alpha, vmi, D, reps))
                     del e
                     torch.cuda.empty_cache()
                     if chains is not None:
                         # the shard's longest document alone: its chain, the floor of that rank
                         dl_ = d0 + int(np.argmax(lens[d0:d1]))
                         o1 = c.slice_docs(dl_, dl_ + 1)
-                        e = LDAEngine(Corpus(o1.doc_ptr, o1.word_idx, o1.counts, c.num_terms), K, LDASettings(),
-                                      backend="hip", seed=0, precision="fp64", local_shard=True)
-                        chains.append((int(lens[dl_]), _time_iteration(e, lb, alpha, vmi, D, reps)))
+                        co, lbo = _local(o1, c.num_terms, lb, a.compact)
+                        e = LDAEngine(co, K, LDASettings(), backend="hip", seed=0, precision="fp64", local_shard=True)
+                        chains.append((int(lens[dl_]), _time_iteration(e, lbo, alpha, vmi, D, reps)))
                         del e
                 return per
             chains = []
@@ -163,7 +177,15 @@ def main():
                 xrows, xms, _ = _exchange_model(c, xb, K)
             else:
                 xrows, xms = 0, 0.0
+            # entries of each plain-cut shard by document length (<= 4, 5-256, 257-2048, > 2048 words): the data
+            # a cost-weighted cut is fitted to (parallel/dist.py doc_cost)
+            edges = [0, 4, 256, 2048, 1 << 40]
+            buckets = []
+            for d0, d1 in (shard_bounds(c.doc_ptr, n) if n > 1 else [(0, D)]):
+                ln = lens[d0:d1]
+                buckets.append([int(ln[(ln > lo) & (ln <= hi)].sum()) for lo, hi in zip(edges[:-1], edges[1:])])
             rec["ranks"][n] = dict(per_rank_ms=[round(x * 1e3, 4) for x in per], max_ms=round(mx * 1e3, 4),
+                                   per_rank_entries_by_len=buckets,
                                    per_rank_longest_words=[w for w, _ in chains],
                                    per_rank_chain_ms=[round(t * 1e3, 4) for _, t in chains],
                                    chain_aware_per_rank_ms=None if per_chain is None else [round(x * 1e3, 4) for x in per_chain],

@@ -107,3 +107,49 @@ def test_bench_strong_scaling_cpu_rehearsal(world):
     out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
     assert out["n_gpus"] == world and out["scaling"] == "strong" and out["config"]["parallelism"] == f"dp{world}"
     assert out["value"] > 0
+
+
+def test_bench_world8_gloo_shards_chain_and_weak_vocabulary():
+    """bench.py at N = 8 over gloo (the RCCL code paths rehearsed on the CPU; no hardware claim):
+    the strong-scaling shards tile the one-day corpus and are the engine's chain-aware cut
+    (dist.engine_bounds: the longest document's rank carries no more than the cut's modelled share), and
+    the weak run's union vocabulary (one day per rank, seeds 1000 r) equals a one-process union of the
+    same eight days (reference: ml_ops.sh:73-80, one model.dat over the MPI ranks)."""
+    import hashlib
+    from oni_ml_amd.parallel.dist import chain_kappa, engine_bounds
+    from oni_ml_amd.pipeline.flow import synthetic_flow_corpus
+    world, events = 8, 3000
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(world),
+                        "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "bench.py", "--gpus",
+                        str(world), "--steps", "1", "--warmup", "1", "--events", str(events), "--device", "cpu",
+                        "--e2e", "0", "--e2e-cold", "0"],
+                       cwd=ROOT, capture_output=True, text=True, timeout=1200,
+                       env=dict(os.environ, OMP_NUM_THREADS="1"))
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    assert out["n_gpus"] == world and out["scaling"] == "strong"
+    # strong: one corpus, its documents tiled by the ranks' contiguous shards -- the engine's cut
+    c, _, _ = synthetic_flow_corpus(events=events, seed=0, device="cpu", return_names=True)
+    sh = out["shards"]
+    assert len(sh) == world and sh[0]["doc_range"][0] == 0 and sh[-1]["doc_range"][1] == c.num_docs
+    assert all(sh[i]["doc_range"][1] == sh[i + 1]["doc_range"][0] for i in range(world - 1))
+    assert sum(s["nnz"] for s in sh) == c.nnz
+    assert [tuple(s["doc_range"]) for s in sh] == [tuple(b) for b in engine_bounds(c.doc_ptr, world, K=20)]
+    lens = np.diff(c.doc_ptr)
+    p = int(np.argmax(lens))
+    rank_p = next(i for i, s in enumerate(sh) if s["doc_range"][0] <= p < s["doc_range"][1])
+    assert sh[rank_p]["max_doc_len"] == int(lens[p])
+    # the chain rule's cost of the longest document's rank is no worse than a plain nnz cut's
+    others = sh[rank_p]["nnz"] - int(lens[p])
+    kap = chain_kappa(20)
+    plain = max(s["nnz"] for s in sh)
+    assert kap * lens[p] + others <= max(kap * lens[p] + plain, plain) + 1e-9
+    # weak: the union vocabulary of eight days equals the one-process union
+    names = set()
+    for rk in range(world):
+        _, _, nm = synthetic_flow_corpus(events=events, seed=1000 * rk, device="cpu", return_names=True)
+        names |= set(nm)
+    union = sorted(names)
+    assert out["weak_vocab"] == len(union)
+    assert out["weak_vocab_sha16"] == hashlib.sha256("\n".join(union).encode()).hexdigest()[:16]
+    assert out["weak_docs"] > c.num_docs
