@@ -374,52 +374,85 @@ def chain_kappa(K: int = None) -> float:
     return CHAIN_KAPPA * (20.0 / float(K)) ** 0.74
 
 
+# Per-entry cost of a document by its length, ns at K = 100 (documents of <= 4 | 5-256 | 257-2048 | > 2048
+# words): a least-squares fit of 14 measured config-5 shard iterations at N = 2 / 4 / 8 (plus 3.2 ms per
+# rank), residual 2.3 ms rms (profiles/r6_strong_emulated.md).  Short documents converge in ~3 sweeps,
+# long ones run all 20: entries are not the unit of work, so nnz-balanced cuts left the ranks of the
+# month's long documents at 2x the others (38.5 vs 17.1 ms at N = 8).
+COST_EDGES = (4, 256, 2048)
+COST_NS_K100 = (2.27, 1.30, 1.79, 3.17)
+CHAIN_NS_PER_WORD = 72.0   # one-workgroup chain (gs_wsteam / gs_team): ~72 ns per word, K = 20 and 100 alike
+SPLIT_CHAIN_NS = 6.0e6     # K > 32: a split document's chain is ~U x sweeps chunk exchanges (443 k words: 6.0 ms)
+
+
+def doc_costs(lens, K: int = None) -> np.ndarray:
+    """Modelled E-step cost (ns) of each document: its entries x the per-entry cost of its length class,
+    scaled from K = 100 as an entry's throughput cost scales (~K^0.74, chain_kappa)."""
+    lens = np.asarray(lens, np.int64)
+    w = np.asarray(COST_NS_K100, np.float64) * ((float(K) / 100.0) ** 0.74 if K else 1.0)
+    return lens * w[np.searchsorted(np.asarray(COST_EDGES), lens, side="left")]
+
+
+def chain_ns(L: int, K: int = None) -> float:
+    """Modelled serial chain (ns) of an L-word document: one workgroup's chunk refreshes, or at K > 32 past
+    the split threshold the split kernel's exchange-bound chain."""
+    t = CHAIN_NS_PER_WORD * float(L)
+    if K and K > 32 and L > 2048:
+        t = min(t, SPLIT_CHAIN_NS)
+    return t
+
+
 def chain_bounds(doc_ptr: np.ndarray, world: int, kappa: float = None, K: int = None):
-    """Chain-aware contiguous shards.  The longest document's block Gauss-Seidel sweeps are a serial
-    chain that no sharding shortens (profiles/r3_strong_emulated.md), and every other document on its
-    GPU lengthens it: modelled, a rank costs its entries, and the rank holding the longest document
-    costs kappa x its length plus its other entries.  Candidates: the plain nnz-balanced cut, and every
-    split of the other world - 1 ranks between the documents left and right of the longest one (a side
-    given no rank shares the longest document's rank); the cheapest wins (largest rank, then the largest
-    of the other ranks).  Config 5 (a 443 k-word document, 90 M entries) at 8 ranks: the side-proportional
-    rule gave its 3 % left side a rank of its own, 69 ms vs 57 ms for plain cuts (r4_strong_emulated.md).
-    Plain cuts when the chain does not bound the shards (kappa x longest <= nnz / world).  ``kappa``
-    defaults to ``chain_kappa(K)``."""
-    if kappa is None:
-        kappa = chain_kappa(K)
+    """Chain- and cost-aware contiguous shards.  A rank costs the modelled E-step cost of its documents
+    (``doc_costs``: entries weighted by length class); the rank holding the longest document costs that
+    document's serial chain (``chain_ns``) plus its other documents.  Candidates: the cost-balanced cut,
+    and every split of the other world - 1 ranks between the documents left and right of the longest one
+    (a side given no rank shares the longest document's rank); the cheapest wins (largest rank, then the
+    largest of the other ranks).  Cost-balanced cuts alone when the chain does not bound the shards
+    (chain <= total / world).  ``kappa`` (tests): the chain as kappa x length in entry units, unweighted --
+    the round-4 rule."""
     D = len(doc_ptr) - 1
-    nnz = int(doc_ptr[-1])
     if world < 2 or D < world:
         return shard_bounds(doc_ptr, world)
     ptr = np.asarray(doc_ptr, np.int64)
     lens = np.diff(ptr)
+    if kappa is not None:
+        cost = lens.astype(np.float64)
+        chain_of = lambda L: kappa * L   # noqa: E731
+    else:
+        cost = doc_costs(lens, K)
+        chain_of = lambda L: chain_ns(L, K)   # noqa: E731
+    cptr = np.concatenate([[0.0], np.cumsum(cost)])
+    total = float(cptr[-1])
     p = int(np.argmax(lens))
     L = int(lens[p])
-    if kappa * L <= nnz / world:
-        return shard_bounds(doc_ptr, world)
+    chain = chain_of(L)
+    base = shard_bounds(cptr, world)
+    if chain <= total / world:
+        return base
 
-    def cost(bounds):
+    def rank_cost(bounds):
         worst, other = 0.0, 0.0
         for a, b in bounds:
-            e = float(ptr[b] - ptr[a])
+            e = float(cptr[b] - cptr[a])
             if a <= p < b:
-                worst = max(worst, kappa * L + e - L)
+                worst = max(worst, chain + e - float(cost[p]))
             else:
                 worst, other = max(worst, e), max(other, e)
         return worst, other
 
-    cands = [shard_bounds(doc_ptr, world)]
+    cands = [base]
     for kl in range(world):
         kr = world - 1 - kl
         if (kl and p == 0) or (kr and p == D - 1) or kl > p or kr > D - 1 - p:
             continue                    # a rank for a side without (enough) documents
-        out = list(shard_bounds(ptr[:p + 1], kl)) if kl else []
+        out = list(shard_bounds(cptr[:p + 1], kl)) if kl else []
         out.append((0 if not kl else p, D if not kr else p + 1))
         if kr:
-            sub = ptr[p + 1:] - ptr[p + 1]
+            sub = cptr[p + 1:] - cptr[p + 1]
             out += [(p + 1 + a, p + 1 + b) for a, b in shard_bounds(sub, kr)]
         cands.append(out)
-    return min(cands, key=cost)
+    return min(cands, key=rank_cost)
 
 
 def chain_default() -> bool:
@@ -437,12 +470,13 @@ def engine_bounds(doc_ptr: np.ndarray, world: int, K: int = None):
 
 
 def shard_bounds(doc_ptr: np.ndarray, world: int, chain: bool = False, K: int = None):
-    """Contiguous [d0, d1) ranges with ~equal nnz (ties broken toward equal doc counts).
+    """Contiguous [d0, d1) ranges with ~equal nnz (ties broken toward equal doc counts); ``doc_ptr`` may be
+    any cumulative weight (chain_bounds passes the modelled costs).
     ``chain``: ``chain_bounds`` instead (``engine_bounds``, the default rule of the engine's shards)."""
     if chain:
         return chain_bounds(doc_ptr, world, K=K)
     D = len(doc_ptr) - 1
-    nnz = int(doc_ptr[-1])
+    nnz = doc_ptr[-1]
     if world <= 1 or D == 0:
         return [(0, D)]
     bounds = [0]

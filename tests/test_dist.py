@@ -203,3 +203,22 @@ def test_chain_bounds_isolate_the_longest_document():
     edge = np.concatenate([[0], np.cumsum(np.r_[9000, np.full(999, 5)])])   # longest first
     b = chain_bounds(edge, 4)
     assert b[0] == (0, 1) and b[-1][1] == 1000 and len(b) == 4
+
+
+def test_engine_bounds_balance_modelled_cost_not_entries():
+    """The engine's cut balances the modelled E-step cost (dist.doc_costs: entries weighted by length class,
+    fitted to the config-5 shards), not entries: ranks of long documents (all 20 sweeps) take fewer entries
+    than ranks of short ones; at K > 32 a split document's chain is capped (SPLIT_CHAIN_NS)."""
+    from oni_ml_amd.parallel.dist import SPLIT_CHAIN_NS, chain_ns, doc_costs, engine_bounds
+    rng = np.random.default_rng(1)
+    lens = np.r_[rng.integers(2100, 5000, 400), rng.integers(5, 200, 20000)]
+    ptr = np.concatenate([[0], np.cumsum(lens)])
+    b = engine_bounds(ptr, 4, K=100)
+    cost = doc_costs(lens, 100)
+    per_cost = [cost[s:e].sum() for s, e in b]
+    per_nnz = [int(ptr[e] - ptr[s]) for s, e in b]
+    assert max(per_cost) < 1.05 * sum(per_cost) / 4                   # cost-balanced
+    assert per_nnz[0] < 0.8 * per_nnz[-1]                              # the long-document rank: fewer entries
+    assert chain_ns(443_000, 100) == SPLIT_CHAIN_NS < chain_ns(443_000, 20)
+    assert doc_costs(np.array([4, 5, 256, 257, 2048, 2049]), 100).tolist() == pytest.approx(
+        [4 * 2.27, 5 * 1.30, 256 * 1.30, 257 * 1.79, 2048 * 1.79, 2049 * 3.17])
