@@ -177,15 +177,23 @@ def main():
                 xrows, xms, _ = _exchange_model(c, xb, K)
             else:
                 xrows, xms = 0, 0.0
-            # entries of each plain-cut shard by document length (<= 4, 5-256, 257-2048, > 2048 words): the data
-            # a cost-weighted cut is fitted to (parallel/dist.py doc_cost)
-            edges = [0, 4, 256, 2048, 1 << 40]
-            buckets = []
-            for d0, d1 in (shard_bounds(c.doc_ptr, n) if n > 1 else [(0, D)]):
-                ln = lens[d0:d1]
-                buckets.append([int(ln[(ln > lo) & (ln <= hi)].sum()) for lo, hi in zip(edges[:-1], edges[1:])])
+            # entries of each shard by document length class, and its distinct words: the data the engine's
+            # cost-weighted cut is fitted to (parallel/dist.py doc_costs)
+            edges = [0, 1, 4, 16, 64, 256, 1024, 2048, 8192, 1 << 40]
+
+            def shard_stats(bounds):
+                out_b, out_v = [], []
+                for d0, d1 in bounds:
+                    ln = lens[d0:d1]
+                    out_b.append([int(ln[(ln > lo) & (ln <= hi)].sum()) for lo, hi in zip(edges[:-1], edges[1:])])
+                    out_v.append(int(np.unique(c.word_idx[c.doc_ptr[d0]:c.doc_ptr[d1]]).size))
+                return out_b, out_v
+            buckets, vocab = shard_stats(shard_bounds(c.doc_ptr, n) if n > 1 else [(0, D)])
+            cbuckets, cvocab = shard_stats(cb) if per_chain else (None, None)
             rec["ranks"][n] = dict(per_rank_ms=[round(x * 1e3, 4) for x in per], max_ms=round(mx * 1e3, 4),
-                                   per_rank_entries_by_len=buckets,
+                                   len_class_edges=edges[1:-1], per_rank_entries_by_len=buckets,
+                                   per_rank_vocab=vocab, chain_aware_entries_by_len=cbuckets,
+                                   chain_aware_vocab=cvocab,
                                    per_rank_longest_words=[w for w, _ in chains],
                                    per_rank_chain_ms=[round(t * 1e3, 4) for _, t in chains],
                                    chain_aware_per_rank_ms=None if per_chain is None else [round(x * 1e3, 4) for x in per_chain],
