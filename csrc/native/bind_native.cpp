@@ -73,10 +73,20 @@ static py::array_t<uint8_t> join_chunks(const std::vector<std::string>& chunks) 
   return out;
 }
 
+// Host threads a native call takes when the caller passes none (threads <= 0), resolved at CALL time:
+// the calling thread's own setting (set_default_threads(n, this_thread=True): a background writer leaves
+// the rank's GPU-driving thread some CPUs), else the process setting (the rank's budget, oni_ml_amd/
+// ops/native.py from knobs.threads / utils/hostres.py), else min(hardware threads, 16).
+static std::atomic<int> g_default_threads{0};
+static thread_local int t_default_threads = 0;
 static int default_threads() {
+  if (t_default_threads > 0) return t_default_threads;
+  const int g = g_default_threads.load(std::memory_order_relaxed);
+  if (g > 0) return g;
   unsigned n = std::thread::hardware_concurrency();
   return n ? (int)std::min(n, 16u) : 4;
 }
+static int resolve_threads(int threads) { return threads > 0 ? threads : default_threads(); }
 
 // Keeps numpy arrays / name lists alive while the writer runs.
 struct ColHolder {
@@ -179,13 +189,24 @@ PYBIND11_MODULE(_oninative, m) {
   py::class_<TextTable>(m, "TextTable")
       .def(py::init<int, std::vector<int>, std::vector<std::vector<int>>>(), py::arg("ncols"),
            py::arg("numeric_cols"), py::arg("dict_groups"))
-      .def("load_files", &TextTable::load_files, py::arg("paths"), py::arg("drop_header") = true,
-           py::arg("threads") = default_threads(), py::call_guard<py::gil_scoped_release>())
-      .def("load_range", &TextTable::load_range, py::arg("path"), py::arg("begin"), py::arg("end"),
-           py::arg("header"), py::arg("drop_header") = true, py::arg("threads") = default_threads(),
+      .def("load_files",
+           [](TextTable& t, const std::vector<std::string>& paths, bool drop_header, int threads) {
+             return t.load_files(paths, drop_header, resolve_threads(threads));
+           },
+           py::arg("paths"), py::arg("drop_header") = true, py::arg("threads") = 0,
            py::call_guard<py::gil_scoped_release>())
-      .def("append_text", &TextTable::append_text, py::arg("text"), py::arg("weight") = 1,
-           py::arg("threads") = default_threads(), py::call_guard<py::gil_scoped_release>())
+      .def("load_range",
+           [](TextTable& t, const std::string& path, int64_t begin, int64_t end, const std::string& header,
+              bool drop_header, int threads) {
+             return t.load_range(path, begin, end, header, drop_header, resolve_threads(threads));
+           },
+           py::arg("path"), py::arg("begin"), py::arg("end"), py::arg("header"), py::arg("drop_header") = true,
+           py::arg("threads") = 0, py::call_guard<py::gil_scoped_release>())
+      .def("append_text",
+           [](TextTable& t, const std::string& text, int64_t weight, int threads) {
+             return t.append_text(text, weight, resolve_threads(threads));
+           },
+           py::arg("text"), py::arg("weight") = 1, py::arg("threads") = 0, py::call_guard<py::gil_scoped_release>())
       .def_property_readonly("num_rows", [](const TextTable& t) { return (int64_t)t.rows.size(); })
       .def_readonly("header", &TextTable::header)
       .def_readonly("n_bad_fields", &TextTable::n_bad_fields)
@@ -246,11 +267,19 @@ PYBIND11_MODULE(_oninative, m) {
         for (auto& c : cols)
           if (c.kind == OutCol::kTable && !c.rowmap && max_row >= (int64_t)c.table->rows.size())
             throw std::invalid_argument("row index beyond table");
+        threads = resolve_threads(threads);
         py::gil_scoped_release rel;
         return write_rows(path, ord, n, cols, sep, append, threads);
       },
       py::arg("path"), py::arg("order"), py::arg("cols"), py::arg("sep") = ",", py::arg("append") = false,
-      py::arg("threads") = default_threads(), py::arg("n") = -1);
+      py::arg("threads") = 0, py::arg("n") = -1);
+  m.def("set_default_threads", [](int n, bool this_thread) {
+    if (this_thread)
+      t_default_threads = n;
+    else
+      g_default_threads.store(n, std::memory_order_relaxed);
+  }, py::arg("n"), py::arg("this_thread") = false);
+  m.def("get_default_threads", []() { return default_threads(); });
 
   m.def(
       "format_rows",
@@ -301,7 +330,7 @@ PYBIND11_MODULE(_oninative, m) {
         DnsFeatures F;
         {
           py::gil_scoped_release rel;
-          F = dns_features((const char*)bi.ptr, off, n, cc, top, special, threads);
+          F = dns_features((const char*)bi.ptr, off, n, cc, top, special, resolve_threads(threads));
         }
         py::dict d;
         d["domain_id"] = to_np(F.domain_id);
@@ -315,7 +344,7 @@ PYBIND11_MODULE(_oninative, m) {
         return d;
       },
       py::arg("data"), py::arg("offsets"), py::arg("country_codes"), py::arg("top_domains"),
-      py::arg("special") = "intel", py::arg("threads") = default_threads());
+      py::arg("special") = "intel", py::arg("threads") = 0);
 
   // Concatenate byte spans of one buffer in the given order (the result-file merge: rows received
   // from every rank, put in global sort order).

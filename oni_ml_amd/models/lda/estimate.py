@@ -57,8 +57,10 @@ class AsyncWriter:
             t.start()
 
     def _loop(self, q):
+        from ...ops import native
         from ...utils.sched import background_priority
         background_priority()
+        native.background_thread_budget(len(self._qs))   # the writers share the rank's budget
         while True:
             job = q.get()
             if job is None:

@@ -22,7 +22,32 @@ def lib():
             raise RuntimeError(
                 f"oni_ml_amd native runtime (_oninative) is not built or failed to load: {e!r}. "
                 "Run `python -m oni_ml_amd._build`.") from e
+        apply_thread_budget()
     return _LIB
+
+
+def apply_thread_budget() -> None:
+    """The native pools' default thread count (a call that passes no ``threads``) = this rank's budget
+    (knobs.threads: ONI_THREADS, else the CPUs bound to the rank within the cgroup quota); re-applied by
+    utils/hostres.bind_rank once the rank is pinned."""
+    if _LIB is None or not hasattr(_LIB, "set_default_threads"):
+        return
+    from .. import knobs
+    _LIB.set_default_threads(int(knobs.threads(16)), False)
+
+
+# CPUs a background writer leaves to the rank's other threads (the one driving the GPU, the HIP runtime's):
+# a writer that takes the whole cgroup quota throttles the GPU-driving thread with it
+WRITER_RESERVE = 2
+
+
+def background_thread_budget(share: int = 1) -> None:
+    """Called on a background writer thread: its native calls default to (the rank's budget minus
+    WRITER_RESERVE) / ``share`` threads (``share`` writers running side by side)."""
+    if _LIB is None:
+        lib()
+    from .. import knobs
+    _LIB.set_default_threads(max(1, (int(knobs.threads(16)) - WRITER_RESERVE) // max(1, share)), True)
 
 
 def available() -> bool:

@@ -160,8 +160,10 @@ def background(fn, name: str = "oni-writer"):
     box = {}
 
     def body():
+        from ..ops import native
         from ..utils.sched import background_priority
         background_priority()
+        native.background_thread_budget()   # leaves the GPU-driving thread CPUs within the quota
         try:
             fn()
         except BaseException as e:  # noqa: BLE001 -- handed to the joiner

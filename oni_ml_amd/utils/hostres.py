@@ -15,7 +15,7 @@ the whole host, N x oversubscribed, and float over sockets away from its GPU.
   cut into LOCAL_WORLD_SIZE contiguous slices, slice ``local_rank``;
 - planned over the host's CPUs (cgroup cpuset), then intersected with the process's affinity, so a
   child of a bound rank that binds again keeps its parent's set;
-- ``torch.set_num_threads`` to that CPU count.
+- ``torch.set_num_threads`` to that CPU count (at most its share of the cgroup's CPU quota).
 
 ``cpu_budget()`` is what every pool sizes itself from (knobs.threads): the bound set's size, or the
 allowed CPUs divided by LOCAL_WORLD_SIZE when nothing was bound.  An explicit ONI_THREADS wins and
@@ -56,11 +56,34 @@ def host_cpus() -> List[int]:
     return list(range(os.cpu_count() or 1))
 
 
+def quota_cpus() -> Optional[float]:
+    """CPUs the cgroup's CFS quota allows (cgroup v2 cpu.max, v1 cpu.cfs_quota_us / cpu.cfs_period_us), or
+    None without a quota.  A container can see every CPU of the host in its cpuset and still run on a
+    fraction of them (the GPU boxes: the whole machine visible, a 16-CPU share)."""
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        return None if q == "max" else float(q) / float(per)
+    except (OSError, ValueError):
+        pass
+    try:
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") as f:
+            q = float(f.read())
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as f:
+            per = float(f.read())
+        return None if q <= 0 or per <= 0 else q / per
+    except (OSError, ValueError):
+        return None
+
+
 def cpu_budget() -> int:
-    """Host threads this rank's pools may use."""
-    if _BOUND is not None:
-        return max(1, len(_BOUND))
-    return max(1, len(allowed_cpus()) // local_world())
+    """Host threads this rank's pools may use: its bound CPUs (else the allowed CPUs / LOCAL_WORLD_SIZE),
+    at most its share of the cgroup's CPU quota."""
+    n = len(_BOUND) if _BOUND is not None else len(allowed_cpus()) // local_world()
+    q = quota_cpus()
+    if q is not None:
+        n = min(n, int(q // local_world()))
+    return max(1, n)
 
 
 def parse_cpulist(text: str) -> List[int]:
@@ -135,9 +158,11 @@ def bind_rank(local_rank: int, device=None) -> List[int]:
     except (AttributeError, OSError):
         pass
     _BOUND = list(cpus)
+    from ..ops import native
+    native.apply_thread_budget()             # the native pools' default, if the module is loaded
     try:
         import torch
-        torch.set_num_threads(max(1, len(cpus)))
+        torch.set_num_threads(cpu_budget())
     except Exception:  # noqa: BLE001 -- torch's pool may already be running; the budget still applies
         pass
     return _BOUND

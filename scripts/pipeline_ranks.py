@@ -52,7 +52,11 @@ def main():
     ap.add_argument("--days", type=int, default=1, help="flow: part files (one per day) of the generated input")
     ap.add_argument("--topics", type=int, default=20)
     ap.add_argument("--compat", default=None, help="strict | fixed (default: strict at K = 20, else fixed)")
-    ap.add_argument("--threads", type=int, default=8, help="native threads per rank")
+    ap.add_argument("--threads", type=int, default=8, help="native threads per rank (0: no --threads, the "
+                                                               "rank's CPU budget decides, utils/hostres.py)")
+    ap.add_argument("--env", action="append", default=[], help="KEY=VALUE set for the ml_ops processes")
+    ap.add_argument("--variants", default="", help="';'-separated env variants (KEY=VAL,KEY=VAL) run back to back "
+                                                   "at every N on the same input (e.g. 'ONI_THREADS=16;')")
     ap.add_argument("--split-threads", action="store_true", help="--threads is the box's share: N ranks get threads / N each")
     ap.add_argument("--cphi-gb", default=None, help="per-rank HBM budget of the c.phi rows")
     ap.add_argument("--no-word-assignments", action="store_true")
@@ -88,13 +92,15 @@ def main():
                                  with_edge_rows=False)
             inp = ["--dns-path", g["dns_path"], "--top1m", g["top1m"]]
         ns = [int(x) for x in a.ranks.split(",")]
-        plan = ([("calibration", ns[0])] if a.tol_quantile else []) + [("run", n) for n in ns]
-        for kind, n in plan:
+        variants = a.variants.split(";") if a.variants else [""]
+        plan = ([("calibration", ns[0], "")] if a.tol_quantile else []) + [("run", n, v) for n in ns for v in variants]
+        for kind, n, variant in plan:
             lp = os.path.join(tmp, f"ml{n}")
             compat = a.compat or ("strict" if a.topics == 20 else "fixed")
             cli = ["-m", "oni_ml_amd", "ml_ops", "20160122", a.source, tol, "--lpath", lp, "--gpus", str(n),
                    "--conf", "/nonexistent", "--quiet", "--backend", a.lda_backend, "--topics", str(a.topics),
-                   "--compat", compat, "--threads", str(max(1, a.threads // n) if a.split_threads else a.threads)] + inp
+                   "--compat", compat] + (["--threads", str(max(1, a.threads // n) if a.split_threads else a.threads)]
+                                          if a.threads > 0 else []) + inp
             if a.cphi_gb:
                 cli += ["--cphi-gb", str(a.cphi_gb)]
             if a.no_word_assignments:
@@ -107,6 +113,8 @@ def main():
                                       ["-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n),
                                        "--master-addr", "127.0.0.1", "--master-port", str(_port())] + cli)
             env = dict(os.environ, ONI_DIST_BACKEND=a.backend)
+            env.update(dict(kv.split("=", 1) for kv in a.env))
+            env.update(dict(kv.split("=", 1) for kv in variant.split(",") if kv))
             if a.cprofile:
                 env["ONI_FAST_EXIT"] = "0"
             t0 = time.perf_counter()
@@ -139,7 +147,7 @@ def main():
                     for k, v in rec.items() if k.startswith("key_q")}
             out_gb = sum(os.path.getsize(os.path.join(d, f)) for d, _, fs in os.walk(lp) for f in fs) / 1e9
             shutil.rmtree(lp, ignore_errors=True)       # (config 5 writes ~50 GB of text per run)
-            run = dict(kind=kind, tol=tol, ranks=n, process_wall_s=round(wall, 3), pipeline_wall_s=round(pw, 3),
+            run = dict(kind=kind, variant=variant, tol=tol, ranks=n, process_wall_s=round(wall, 3), pipeline_wall_s=round(pw, 3),
                        flagged=summ.get("scored"), rank0_key_quantiles=keyq, startup_marks=summ.get("startup_marks"), corpus=summ.get("corpus"),
                        em_iterations=summ.get("lda", {}).get("em_iterations"),
                        lda_seconds=summ.get("lda", {}).get("seconds"), lda_timing=summ.get("lda", {}).get("timing"),
@@ -159,7 +167,8 @@ def main():
     if a.md:
         lines = [f"# Per-rank stage seconds, {a.source} day of {a.events} events (collectives: {a.backend})", ""]
         for run in out["runs"]:
-            lines.append(f"## N = {run['ranks']}: pipeline wall {run['pipeline_wall_s']} s, TOL {run['tol']}, "
+            lines.append(f"## N = {run['ranks']}{' [' + run['variant'] + ']' if run.get('variant') else ''}: "
+                         f"pipeline wall {run['pipeline_wall_s']} s, TOL {run['tol']}, "
                          f"flagged {run['flagged']}, "
                          f"EM iterations {run['em_iterations']}"
                          + (f", rank 0 serial {run['rank0_serial_s']} s = {100 * run['rank0_serial_share']:.1f} % of the wall"

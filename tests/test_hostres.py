@@ -102,3 +102,20 @@ print(subprocess.run([sys.executable, '-c', {code!r}], capture_output=True, text
     assert out.returncode == 0, out.stderr[-2000:]
     g = json.loads(out.stdout.strip().splitlines()[-1])
     assert g["aff"] == allowed and g["t16"] == 3 and g["cfg"] == 3
+
+
+def test_cpu_quota_caps_the_budget(monkeypatch):
+    """A cgroup CPU quota smaller than the visible CPUs (the GPU boxes) caps every rank's share."""
+    monkeypatch.setattr(hostres, "quota_cpus", lambda: 16.0)
+    monkeypatch.setattr(hostres, "allowed_cpus", lambda: list(range(192)))
+    monkeypatch.setenv("LOCAL_WORLD_SIZE", "8")
+    monkeypatch.setattr(hostres, "_BOUND", None)
+    assert hostres.cpu_budget() == 2
+    monkeypatch.setattr(hostres, "_BOUND", list(range(24)))
+    assert hostres.cpu_budget() == 2
+    monkeypatch.setattr(hostres, "quota_cpus", lambda: None)
+    assert hostres.cpu_budget() == 24
+    monkeypatch.setenv("LOCAL_WORLD_SIZE", "1")
+    monkeypatch.setattr(hostres, "_BOUND", None)
+    monkeypatch.setattr(hostres, "quota_cpus", lambda: 16.0)
+    assert hostres.cpu_budget() == 16
