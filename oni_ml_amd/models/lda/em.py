@@ -1388,6 +1388,69 @@ class LDAEngine:
             return self.dist.gather_rows(g, self.global_docs)
         return g
 
+    # ----------------------------------------------------- LAG saves, pipelined
+    SNAPSHOT_BYTES = 1 << 30     # device snapshots of the LAG state (2 sets) only below this size
+
+    def _snapshot_saves_ok(self) -> bool:
+        """One rank, fp64 HIP engine, graphs: LAG saves from device snapshots (2 x (cw + gamma) bytes)."""
+        if self.backend != "hip" or self._distributed or not self.use_graph or self._cwin is not None:
+            return False
+        return 2 * (self.cw.numel() + self.gamma.numel()) * 8 <= self.SNAPSHOT_BYTES
+
+    def _em_with_snapshots(self, on_save, on_iteration, i, L_old, hist, stats, lag, n_docs_global):
+        """EM iterations with LAG saves and one batch queued ahead: a batch ending on a LAG boundary is
+        followed on the stream by copies of class_word, the class totals and gamma into one of two
+        snapshot sets; once its history is read back (the next batch already queued) the save runs from
+        the snapshot, with the host scalars of that iteration.  A batch the device loop stopped early (the
+        loop converged before the boundary) saves nothing, exactly as the draining loop would not."""
+        st = self.settings
+        # lda-c's loop test runs after each iteration while i <= EM_MAX_ITER: up to EM_MAX_ITER + 1 iterations
+        batches = _lag_batches(i, st.em_max_iter + 1, lag, self.max_batch)
+        if not batches:
+            return i, L_old, 1.0
+        if getattr(self, "_snaps", None) is None:
+            self._snaps = [tuple(torch.empty_like(x) for x in (self.cw, self.class_total, self.gamma))
+                           for _ in range(2)]
+        emc, emx = st.em_converged, st.em_max_iter
+        bufs = [self._out_host, torch.zeros_like(self._out_host).pin_memory()]
+        conv = 1.0
+        pending = None          # (ticket, batch size, snapshot set or None)
+        it_q = i
+
+        def collect(p):
+            nonlocal i, L_old, conv
+            ticket, n, snap = p
+            recs = self._collect_batch(ticket)
+            for lik, c, alpha, vmi, _ass in recs:
+                i += 1
+                L_old, conv = lik, c
+                hist.append((lik, c))
+                stats.append(EMIterStats(i, lik, c, alpha, 0.0, -1.0, -1, vmi))
+                if on_iteration is not None:
+                    on_iteration(self, i, lik, c)
+            if snap is not None and len(recs) == n and i % lag == 0:
+                view = _Snapshot(self, *snap)
+                on_save(f"{i:03d}", view)
+            return len(recs) < n
+
+        for j, n in enumerate(batches):
+            t = self._enqueue_batch(n, st.estimate_alpha, n_docs_global, L_old, it_q, True, emc, emx,
+                                    cont=j > 0, buf=bufs[j % 2])
+            it_q += n
+            snap = None
+            if it_q % lag == 0:
+                snap = self._snaps[j % 2]
+                for dst, src in zip(snap, (self.cw, self.class_total, self.gamma)):
+                    dst.copy_(src, non_blocking=True)
+            if pending is not None:
+                if collect(pending):     # the device loop ended in that batch: this one is a no-op
+                    pending = (t, n, snap)
+                    break
+            pending = (t, n, snap)
+        if pending is not None:
+            collect(pending)
+        return i, L_old, conv
+
     # ----------------------------------------------------------------- driver
     def run(self, start: str = "random", corpus_global: Optional[Corpus] = None,
             on_iteration: Optional[Callable] = None, on_save: Optional[Callable] = None,
@@ -1430,6 +1493,12 @@ class LDAEngine:
                 if on_iteration is not None:
                     on_iteration(self, i, lik, conv)
             conv = 0.0 if not recs else conv
+        if on_save is not None and lag > 0 and not per_iter_stats and self._snapshot_saves_ok() and \
+                _em_continue(conv, i, st.em_converged, st.em_max_iter):
+            # LAG saves without draining the device: batches end on LAG boundaries, each followed by an
+            # on-device snapshot of the saved state, one batch always queued ahead (_em_with_snapshots)
+            i, L_old, conv = self._em_with_snapshots(on_save, on_iteration, i, L_old, hist, stats, lag,
+                                                     n_docs_global)
         while on_save is not None or per_iter_stats or self.backend != "hip":
             if not _em_continue(conv, i, st.em_converged, st.em_max_iter):
                 break
@@ -1471,6 +1540,38 @@ class LDAEngine:
         res = LDAResult(log_beta=None, gamma=None, alpha=self.alpha, num_topics=self.K, num_terms=self.V,
                         likelihoods=hist, stats=stats, em_iterations=i, seconds=time.perf_counter() - t0)
         return res
+
+
+class _Snapshot:
+    """The saved state of one LAG iteration, copied on the device behind that iteration's batch (class_word,
+    class totals, gamma) plus its host scalars; duck-types the engine for estimate()'s on_save (the state
+    methods read the snapshot, everything else falls through to the engine)."""
+
+    def __init__(self, eng, cw, class_total, gamma):
+        self._eng, self.cw, self._cw_local, self.class_total, self.gamma = eng, cw, cw, class_total, gamma
+        self.alpha, self.var_max_iter = eng.alpha, eng.var_max_iter
+
+    def __getattr__(self, name):
+        return getattr(self._eng, name)
+
+    def global_cw(self):
+        return self.cw
+
+    log_beta_deferred = LDAEngine.log_beta_deferred
+    host_copy_deferred = LDAEngine.host_copy_deferred
+    local_gamma_deferred = LDAEngine.local_gamma_deferred
+    local_gamma = LDAEngine.local_gamma
+
+
+def _lag_batches(i: int, last: int, lag: int, cap: int) -> List[int]:
+    """Batch sizes covering iterations i + 1 .. last, each ending at a multiple of ``lag`` or the end,
+    at most ``cap`` long."""
+    out = []
+    while i < last:
+        n = min(cap, lag - (i % lag), last - i)
+        out.append(n)
+        i += n
+    return out
 
 
 def resolved_gs_updates(settings, K: int) -> int:

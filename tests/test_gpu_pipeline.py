@@ -120,3 +120,34 @@ def _inf_case():
     rng = np.random.default_rng(2)
     b = rng.random((12, 300)) ** 3 + 1e-3
     return c, np.log(b / b.sum(1, keepdims=True))
+
+
+@pytest.mark.parametrize("conv", [1e-12, 3e-4])
+def test_lag_saves_from_snapshots_match_draining_loop(tmp_path, monkeypatch, conv):
+    """LAG saves from on-device snapshots with one batch queued ahead (LDAEngine._em_with_snapshots) write
+    the same files, byte for byte, as the loop that drains the device at every LAG boundary: the %03d
+    models, the checkpoint's statistics, likelihood.dat, final.* (conv 3e-4: the device loop stops before
+    the last boundary, which then saves nothing)."""
+    from oni_ml_amd.models.lda.em import LDAEngine
+    from oni_ml_amd.models.lda.estimate import estimate
+    from oni_ml_amd.synth.corpus import planted_corpus
+    c = planted_corpus(num_docs=3000, num_terms=800, num_topics=6, seed=4)
+    out = {}
+    for mode in ("snap", "drain"):
+        if mode == "drain":
+            monkeypatch.setattr(LDAEngine, "_snapshot_saves_ok", lambda self: False)
+        st = LDASettings(em_max_iter=23, em_converged=conv)
+        st.lag = 3
+        d = tmp_path / mode
+        res = estimate(c, 20, 2.5, st, "random", str(d), backend="hip", device="cuda", seed=5)
+        files = sorted(p.name for p in d.iterdir() if p.is_file() and p.suffix not in (".json", ".npz"))
+        npz = {p.name: dict(np.load(p)) for p in d.iterdir() if p.suffix == ".npz"}   # (zip entries carry times)
+        out[mode] = (res.em_iterations, {f: (d / f).read_bytes() for f in files}, npz)
+    (n1, f1, c1), (n2, f2, c2) = out["snap"], out["drain"]
+    assert n1 == n2 and sorted(f1) == sorted(f2)
+    assert any(f.endswith(".beta") and f[:3].isdigit() and f != "000.beta" for f in f1)
+    for f in f1:
+        assert f1[f] == f2[f], f
+    assert sorted(c1) == sorted(c2) and "checkpoint.npz" in c1
+    for name in c1:
+        assert sorted(c1[name]) == sorted(c2[name]) and all(np.array_equal(c1[name][k], c2[name][k]) for k in c1[name])
