@@ -88,6 +88,30 @@ static int default_threads() {
 }
 static int resolve_threads(int threads) { return threads > 0 ? threads : default_threads(); }
 
+// Background writers (threads marked by set_default_threads(n, this_thread=True)) draw their worker
+// threads from ONE process-wide pool (set_background_pool): the lda_pre writer and the model writers
+// running side by side share the rank's budget instead of each taking it whole -- more runnable threads
+// than the cgroup's CPU quota throttle the whole process, the thread driving the GPU with it.
+static std::atomic<int> g_bg_free{-1};   // free tokens; -1: no pool configured (no limit)
+struct BgThreads {
+  int n = 0, taken = 0;
+  explicit BgThreads(int want) {
+    n = want;
+    if (t_default_threads <= 0 || g_bg_free.load() < 0) return;   // not a background writer / no pool
+    int cur = g_bg_free.load();
+    while (taken < want && cur > 0) {
+      if (g_bg_free.compare_exchange_weak(cur, cur - 1)) {
+        ++taken;
+        cur = g_bg_free.load();
+      }
+    }
+    n = std::max(1, taken);   // an exhausted pool still makes progress on one thread
+  }
+  ~BgThreads() {
+    if (taken) g_bg_free.fetch_add(taken);
+  }
+};
+
 // Keeps numpy arrays / name lists alive while the writer runs.
 struct ColHolder {
   std::vector<py::object> keep;
@@ -268,8 +292,9 @@ PYBIND11_MODULE(_oninative, m) {
           if (c.kind == OutCol::kTable && !c.rowmap && max_row >= (int64_t)c.table->rows.size())
             throw std::invalid_argument("row index beyond table");
         threads = resolve_threads(threads);
+        BgThreads bg(threads);
         py::gil_scoped_release rel;
-        return write_rows(path, ord, n, cols, sep, append, threads);
+        return write_rows(path, ord, n, cols, sep, append, bg.n);
       },
       py::arg("path"), py::arg("order"), py::arg("cols"), py::arg("sep") = ",", py::arg("append") = false,
       py::arg("threads") = 0, py::arg("n") = -1);
@@ -280,6 +305,8 @@ PYBIND11_MODULE(_oninative, m) {
       g_default_threads.store(n, std::memory_order_relaxed);
   }, py::arg("n"), py::arg("this_thread") = false);
   m.def("get_default_threads", []() { return default_threads(); });
+  m.def("set_background_pool", [](int n) { g_bg_free.store(n); }, py::arg("n"));
+  m.def("background_pool_free", []() { return g_bg_free.load(); });
 
   m.def(
       "format_rows",
@@ -547,11 +574,12 @@ PYBIND11_MODULE(_oninative, m) {
         for (int64_t d = 0; d < D; ++d)
           if (p[d] > p[d + 1]) throw std::invalid_argument("non-monotone doc_ptr");
         if (threads <= 0) threads = default_threads();
+        BgThreads bg(threads);
         py::gil_scoped_release rel;
         if (assignments)
           for (int64_t i = 0; i < (int64_t)counts.size(); ++i)
             if (counts.data()[i] < 0 || words.data()[i] < 0) throw std::invalid_argument("negative word or topic");
-        return write_corpus_text(path, p, D, words.data(), counts.data(), threads, assignments);
+        return write_corpus_text(path, p, D, words.data(), counts.data(), bg.n, assignments);
       },
       py::arg("path"), py::arg("doc_ptr"), py::arg("words"), py::arg("counts"), py::arg("threads") = 0,
       py::arg("assignments") = false);

@@ -33,7 +33,10 @@ def apply_thread_budget() -> None:
     if _LIB is None or not hasattr(_LIB, "set_default_threads"):
         return
     from .. import knobs
-    _LIB.set_default_threads(int(knobs.threads(16)), False)
+    n = int(knobs.threads(16))
+    _LIB.set_default_threads(n, False)
+    if hasattr(_LIB, "set_background_pool"):
+        _LIB.set_background_pool(max(1, n - WRITER_RESERVE))   # every background writer's threads, together
 
 
 # CPUs a background writer leaves to the rank's other threads (the one driving the GPU, the HIP runtime's):
@@ -42,8 +45,9 @@ WRITER_RESERVE = 2
 
 
 def background_thread_budget(share: int = 1) -> None:
-    """Called on a background writer thread: its native calls default to (the rank's budget minus
-    WRITER_RESERVE) / ``share`` threads (``share`` writers running side by side)."""
+    """Called on a background writer thread: marks it as one (its native calls then draw their worker
+    threads from the process-wide background pool of budget - WRITER_RESERVE tokens, shared by every
+    writer running at the time) and asks for at most (budget - WRITER_RESERVE) / ``share`` of them."""
     if _LIB is None:
         lib()
     from .. import knobs

@@ -119,3 +119,35 @@ def test_cpu_quota_caps_the_budget(monkeypatch):
     monkeypatch.setattr(hostres, "_BOUND", None)
     monkeypatch.setattr(hostres, "quota_cpus", lambda: 16.0)
     assert hostres.cpu_budget() == 16
+
+
+def test_background_writers_share_one_thread_pool(tmp_path):
+    """Native calls on background writer threads (ops/native.background_thread_budget) draw their worker
+    threads from one process-wide pool of budget - WRITER_RESERVE tokens; every token comes back, and the
+    files are the same as a foreground write's."""
+    import threading
+    import numpy as np
+    from oni_ml_amd.io import ldac
+    from oni_ml_amd.ops import native
+    L = native.lib()
+    native.apply_thread_budget()
+    free0 = L.background_pool_free()
+    assert free0 >= 1
+    g = np.random.default_rng(0).random((20000, 24))
+    ldac.save_gamma(str(tmp_path / "fg.gamma"), g)
+    errs = []
+
+    def writer(i):
+        try:
+            native.background_thread_budget(2)
+            ldac.save_gamma(str(tmp_path / f"bg{i}.gamma"), g)
+        except Exception as e:  # noqa: BLE001
+            errs.append(e)
+    ts = [threading.Thread(target=writer, args=(i,)) for i in range(3)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    assert not errs and L.background_pool_free() == free0
+    ref = (tmp_path / "fg.gamma").read_bytes()
+    assert all((tmp_path / f"bg{i}.gamma").read_bytes() == ref for i in range(3))
