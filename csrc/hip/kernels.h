@@ -99,10 +99,7 @@ enum GsVariant : int {
   kGsChain = 5,    // KS > 32, U > 32: one wave per document, a topic per lane, rows of the next 8 words in
                    // flight (the planner routes chunks of W <= GSPlan.CHAIN_MAX_W = 2 words here:
                    // lda-c's per-word schedule, ops/hip.py wide_u_edges)
-  kGsTeam8W = 6,   // KS <= 32, staged rows, chunks of <= kTeam8WMaxW words: 11 word waves + a topic wave,
-                   // the chunk's E in SGPRs (gs_wsteam SE), 3 waves per SIMD
 };
-constexpr int kTeam8WMaxW = 11 * 64 * 2;   // words of a chunk the 11 word waves hold in their 2 rounds
 struct GSArgs {
   const int* doc_ptr;     // [D+1]
   const int* word_idx;    // [nnz]

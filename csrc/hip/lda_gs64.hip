@@ -2205,17 +2205,7 @@ __global__ __launch_bounds__(wteam_threads(NW)) void gs_wteam(GSArgs a) {
 // arrival -- so the address unit works beside the reduction; the other rounds after the arrival.
 // (Measured slower and removed in round 5, records in profiles/r4_tuning_log.md: the topic wave summing
 // the word waves' lane partials, 5 or 3 word waves, two early rounds, the LDS-ring loader variant.)
-// SE (scalar E): the word waves hold the chunk's E (the same for every lane) in SGPRs (readfirstlane of the
-// LDS broadcast), so KS x 2 VGPRs go to more word waves: NW = 15, one prefetched word per lane, 4 waves per
-// SIMD within 128 VGPRs instead of 7 word waves at 2 waves per SIMD.
-__device__ __forceinline__ double wave_uniform(double x) {
-  const long long b = __double_as_longlong(x);
-  const int lo = __builtin_amdgcn_readfirstlane((int)(b & 0xffffffffLL));
-  const int hi = __builtin_amdgcn_readfirstlane((int)(b >> 32));
-  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
-}
-
-template <int KS, int NW, int RMAX, int EP = 0, bool STG = false, bool SE = false, bool STREAM = true>
+template <int KS, int NW, int RMAX, int EP = 0, bool STG = false>
 __global__ __launch_bounds__((NW + 1) * 64) void gs_wsteam(GSArgs a) {
   static_assert(KS <= 32 && KS % 2 == 0, "word team: KS <= 32");
   constexpr int NTD = (NW + 1) * 64, NS = NW * 64;
@@ -2422,7 +2412,7 @@ __global__ __launch_bounds__((NW + 1) * 64) void gs_wsteam(GSArgs a) {
         double E[KS], acc[KS];
 #pragma unroll
         for (int kk = 0; kk < KS; ++kk) {
-          E[kk] = SE ? wave_uniform(E_[kk]) : E_[kk];
+          E[kk] = E_[kk];
           acc[kk] = 0.0;
         }
 #pragma unroll
@@ -2461,13 +2451,11 @@ __global__ __launch_bounds__((NW + 1) * 64) void gs_wsteam(GSArgs a) {
             }
           }
         }
-        if constexpr (STREAM) {
-          for (int p = n0 + t + RMAX * NS; p < n1; p += NS) {   // beyond the prefetched rounds
-            double b[1][KS];
-            load_row(row_of(p), b[0]);
-            const double cp = (double)crow[p];
-            wword_steps<KS, 1>(E, b, &cp, acc, lw);
-          }
+        for (int p = n0 + t + RMAX * NS; p < n1; p += NS) {   // beyond the prefetched rounds
+          double b[1][KS];
+          load_row(row_of(p), b[0]);
+          const double cp = (double)crow[p];
+          wword_steps<KS, 1>(E, b, &cp, acc, lw);
         }
         tick(0);
         wave_topic_sums<KS>(acc, lane, sRed[wv]);
@@ -2866,16 +2854,6 @@ static void gs_estep_ks(const GSArgs& a, int variant, hipStream_t s) {
         hipLaunchKernelGGL((gs::gs_team<KS, 8, 1, true>), dim3(a.n_items), dim3(512), 0, s, a);
       else
         hipLaunchKernelGGL((gs::gs_team<KS, 8>), dim3(a.n_items), dim3(512), 0, s, a);
-      break;
-    case kGsTeam8W:
-      // the planner sends only documents with W = ceil(n / U) <= kTeam8WMaxW (no streamed tail)
-      if constexpr (KS <= 32 && KS % 2 == 0) {
-        if (a.stage == nullptr || a.gs_updates > kGsUMax)
-          throw std::runtime_error("gs_estep: the 11-wave team needs staged rows and U <= 32");
-        hipLaunchKernelGGL((gs::gs_wsteam<KS, 11, 2, 0, true, true, false>), dim3(a.n_items), dim3(768), 0, s, a);
-      } else {
-        throw std::runtime_error("gs_estep: the 11-wave team needs an even KS <= 32");
-      }
       break;
     default:
       throw std::runtime_error("gs_estep: unknown variant");

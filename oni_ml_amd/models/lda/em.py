@@ -391,16 +391,13 @@ class LDAEngine:
         from ...ops import hip as H
         gb = _stage_budget_gb(knobs.get("ONI_GS_STAGE", "4"))
         if KS > 32 or gb <= 0 or self._U > 32:   # U > 32: the topic-group team reads beta (no gs_wsteam)
-            for gp in ([self.gs_plan] if self._cwin is None else [w["gp"] for w in self._cwin]):
-                if gp is not None:
-                    gp.plan[:] = [(H.GS_TEAM8 if v == H.GS_TEAM8W else v, o) for v, o in gp.plan]
             return {}
         cap = gb * 2**30
         plans = [self.gs_plan] if self._cwin is None else [w["gp"] for w in self._cwin]
         out = {}
         for gp in plans:
             for var, order in gp.plan:
-                if var not in (H.GS_TEAM8, H.GS_TEAM8W):
+                if var != H.GS_TEAM8:
                     continue
                 o = order.cpu().numpy()
                 o = o[o >= 0]
@@ -410,8 +407,6 @@ class LDAEngine:
                     continue
                 cap -= need
                 out[id(order)] = H.GSStage(order, corpus.doc_ptr, KS, self.device)
-            # the 11-wave team reads only staged rows: an unstaged plan keeps the 7-wave kernel
-            gp.plan[:] = [(H.GS_TEAM8 if v == H.GS_TEAM8W and id(o) not in out else v, o) for v, o in gp.plan]
         return out
 
     def _cphi_windows(self, corpus: Corpus, KS: int):

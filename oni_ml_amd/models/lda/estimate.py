@@ -92,6 +92,11 @@ class AsyncWriter:
             raise self._err
 
 
+def _append_text(path: str, text: str):
+    with open(path, "a") as f:
+        f.write(text)
+
+
 def _after(event, fn):
     """fn, run once ``event`` (a queued device-to-host copy of its inputs, or None) has completed."""
     if event is None:
@@ -254,14 +259,26 @@ def estimate(corpus: Corpus, num_topics: int, alpha_init: float, settings: LDASe
 
     history = list(hist)
 
+    writer = AsyncWriter()
+    lik_path = os.path.join(outdir, "likelihood.dat")
+    lik_lines = []      # likelihood.dat lines not yet handed to the writer
+
+    def flush_likelihood():
+        # appended by the writer thread (one file, one key: in order), not by the thread driving the GPU:
+        # an open/append/close per EM iteration waited on the filesystem behind the lda_pre text files
+        # (profiles/r6_lda_stage.md); a resume rewrites the file from the checkpoint's history anyway
+        if rank0 and lik_lines:
+            text = "".join(lik_lines)
+            lik_lines.clear()
+            writer.submit(_append_text, lik_path, text, key="likelihood")
+
     def on_iteration(e, i, lik, conv):
         history.append((lik, conv))
         if rank0:
-            ldac.append_likelihood(os.path.join(outdir, "likelihood.dat"), lik, conv)
+            lik_lines.append(ldac.format_likelihood_line(lik, conv))
         if fault_at_iteration is not None and i >= fault_at_iteration:
+            flush_likelihood()
             raise RuntimeError(f"injected fault after EM iteration {i}")
-
-    writer = AsyncWriter()
     # this rank's exact gamma block of an earlier run (load_final_rows) is stale from here on
     stale = os.path.join(outdir, f"final_gamma.rank{r}.npz")
     if os.path.exists(stale):
@@ -270,6 +287,7 @@ def estimate(corpus: Corpus, num_topics: int, alpha_init: float, settings: LDASe
     saved = {}          # the final save's host copies, reused for the result
 
     def on_save(tag, e):
+        flush_likelihood()
         # collectives first, on every rank: global class_word (sparse exchange)
         ckpt = tag not in ("000", "final")
         cwg = e.global_cw()

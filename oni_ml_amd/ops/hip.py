@@ -310,8 +310,7 @@ def bin_columns(values, cuts):
 # ------------------------------------------------------- fp64 block Gauss-Seidel ---
 # lda-c-faithful E-step (csrc/hip/lda_gs64.hip): double everywhere, gamma refreshed after every
 # chunk of ceil(n / gs_updates) words (documents of <= gs_updates words: lda-c's per-word schedule).
-GS_TINY, GS_TEAM1, GS_TEAM4, GS_TEAM8, GS_SMALL, GS_CHAIN, GS_TEAM8W = range(7)
-TEAM8W_MAX_W = 11 * 64 * 2   # csrc/hip/kernels.h kTeam8WMaxW
+GS_TINY, GS_TEAM1, GS_TEAM4, GS_TEAM8, GS_SMALL, GS_CHAIN = range(6)
 GS_SMALL_MAX = 64   # csrc/hip/lda_gs64.hip kGsSmallMax
 
 
@@ -426,7 +425,7 @@ def gs_estep(doc_ptr, word_idx, counts, order, beta, K, gs_updates, params, gamm
         raise ValueError("K out of range")
     if not (1 <= int(gs_updates) <= gs_umax(KS)):
         raise ValueError(f"gs_updates must be in [1, {gs_umax(KS)}] at KS {KS}")
-    if variant not in (GS_TINY, GS_TEAM1, GS_TEAM4, GS_TEAM8, GS_SMALL, GS_CHAIN, GS_TEAM8W):
+    if variant not in (GS_TINY, GS_TEAM1, GS_TEAM4, GS_TEAM8, GS_SMALL, GS_CHAIN):
         raise ValueError(f"unknown gs variant {variant}")
     dev = beta.device
     args = [
@@ -446,11 +445,8 @@ def gs_estep(doc_ptr, word_idx, counts, order, beta, K, gs_updates, params, gamm
         0 if stage is None else _chk(stage.stage_off, torch.int64, "stage_off", (order.numel(),), dev),
     ]
     _need_pad_row(beta)
-    if stage is not None and (variant not in (GS_TEAM8, GS_TEAM8W) or KS != stage.KS):
+    if stage is not None and (variant != GS_TEAM8 or KS != stage.KS):
         raise ValueError("staged rows: kGsTeam8 launches of the stage's KS only")
-    if variant == GS_TEAM8W:
-        if stage is None or KS > 32 or KS % 2 or int(gs_updates) > 32:
-            raise ValueError("GS_TEAM8W: staged rows, an even KS <= 32 and U <= 32")
     if order.numel() == 0:
         return
     lib().gs_estep(*args)
@@ -1032,9 +1028,6 @@ class GSPlan:
             o = order[m].copy()
             if var == GS_TEAM8 and iso > 0:
                 o = self.isolate_longest(o, min(iso, 8))
-            if var == GS_TEAM8 and self.TEAM8W and KS <= 32 and KS % 2 == 0 and int(gs_updates) <= 32 and \
-                    -(-int(L[o[o >= 0]].max()) // int(gs_updates)) <= TEAM8W_MAX_W:
-                var = GS_TEAM8W        # 11 word waves (needs the staged rows: LDAEngine falls back without)
             self.plan.append((var, torch.from_numpy(o).to(device)))
         m = Ls <= tiny
         if m.any():
@@ -1045,7 +1038,6 @@ class GSPlan:
         # iteration; profiles/r2_tuning_log.md, r3_tuning_log.md)
 
     CHAIN_MAX_W = 2   # widest chunk (words) the one-wave per-word chain kernel takes (csrc/hip/kernels.h kGsChain)
-    TEAM8W = False    # KS <= 32: the longest documents on 11 word waves (GS_TEAM8W) instead of 7
 
     @classmethod
     def wide_u_edges(cls, U: int):

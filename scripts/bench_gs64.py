@@ -48,7 +48,6 @@ def main():
     ap.add_argument("--long", default="", help="a synthetic corpus of only these document lengths (e.g. 443426: "
                                                "config 5's longest document alone), distinct random words")
     ap.add_argument("--vocab", type=int, default=4_536_586, help="--long: vocabulary (config 5's month)")
-    ap.add_argument("--team8w", type=int, default=0, help="1: the longest documents on the 11-word-wave team")
     ap.add_argument("--sweeps", type=int, default=0, help="timed launches run exactly this many sweeps (no "
                                                            "convergence test), e.g. 20: a long document's real count")
     a = ap.parse_args()
@@ -56,7 +55,6 @@ def main():
     from oni_ml_amd.models.lda.settings import LDASettings
     from oni_ml_amd.ops import hip as H
     from oni_ml_amd.pipeline.flow import synthetic_flow_corpus
-    H.GSPlan.TEAM8W = bool(a.team8w)
     if a.long:
         from oni_ml_amd.corpus.csr import Corpus
         rng = np.random.default_rng(0)
@@ -81,7 +79,7 @@ def main():
     lens = c.lengths()
     its = eng.iters.cpu().numpy()
     names = {H.GS_TINY: "tiny", H.GS_TEAM1: "team1", H.GS_TEAM4: "team4", H.GS_TEAM8: "team8", H.GS_SMALL: "small",
-             H.GS_TEAM8W: "team8w",
+
              H.GS_CHAIN: "chain"}
     out = dict(docs=c.num_docs, nnz=c.nnz, U=eng._U, buckets=[])
 
@@ -138,7 +136,7 @@ def main():
             continue
         o = order.cpu().numpy()
         o = o[o >= 0]   # XCD placement gaps
-        if a.first and var in (H.GS_TEAM1, H.GS_TEAM4, H.GS_TEAM8, H.GS_TEAM8W):
+        if a.first and var in (H.GS_TEAM1, H.GS_TEAM4, H.GS_TEAM8):
             o = o[:a.first]
             keep = eng._stages.pop(id(order), None)
             order = torch.from_numpy(o.astype(np.int32)).to(order.device)

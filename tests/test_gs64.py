@@ -188,7 +188,7 @@ def test_gs64_graph_replay_and_gate():
     assert eng.gamma.abs().max().item() == 0
 
 
-@pytest.mark.parametrize("stage", ["1", "0", "w"])
+@pytest.mark.parametrize("stage", ["1", "0"])
 @pytest.mark.parametrize("head", [
     # longest chunk 938 words: past the two prefetched rounds (7 waves x 64 lanes x 2), streamed remainder
     [30000, 20000, 15000, 9000, 6000, 5000, 4000, 3500, 3000, 2500, 2200, 2100],
@@ -200,9 +200,7 @@ def test_longest_documents_match_oracle(head, stage, monkeypatch):
     holds empty slots (GSPlan.isolate_longest); with the staged row copies (GSStage, default) and
     gathering from beta."""
     from oni_ml_amd.ops import hip as H
-    # "w": the 11-word-wave team (GS_TEAM8W, staged rows, the chunk's E in SGPRs)
-    monkeypatch.setattr(H.GSPlan, "TEAM8W", stage == "w")
-    monkeypatch.setenv("ONI_GS_STAGE", "1" if stage == "w" else stage)
+    monkeypatch.setenv("ONI_GS_STAGE", stage)
     rng = np.random.default_rng(11)
     V, D = 40000, 300
     lens = np.minimum(rng.zipf(1.5, D), 200)
@@ -217,9 +215,8 @@ def test_longest_documents_match_oracle(head, stage, monkeypatch):
     ref = _oracle(c, lb, 0.41, st, U)
     eng, sc = _gpu_estep(c, K, lb, 0.41, LDASettings(var_max_iter=4, var_converged=-1e30), U)
     launches = {v: o.cpu().numpy() for v, o in eng.gs_plan.plan}
-    t8 = H.GS_TEAM8W if stage == "w" else H.GS_TEAM8
-    assert (launches[t8] < 0).any() and launches[t8][0] == 0   # placement gaps
-    assert len(eng._stages) == (0 if stage == "0" else 1)
+    assert (launches[H.GS_TEAM8] < 0).any() and launches[H.GS_TEAM8][0] == 0   # placement gaps
+    assert len(eng._stages) == (1 if stage == "1" else 0)
     assert np.array_equal(eng.iters.cpu().numpy(), ref["iters"])
     assert _rel(eng.gamma[:, :K].cpu().numpy(), ref["gamma"], 1e-12) < 1e-10
     assert _rel(eng.lik.cpu().numpy(), ref["doc_likelihood"], 1.0) < 1e-10
