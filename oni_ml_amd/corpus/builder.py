@@ -40,6 +40,13 @@ class DocWordCounts:
     def n(self) -> int:
         return int(self.doc.numel())
 
+    def to_host(self) -> "DocWordCounts":
+        """The same counts as host tensors.  The lda_pre text writer runs on a thread beside the EM; a
+        device-to-host copy issued from that thread waited for the EM batch in flight and held up the
+        enqueue of the next one (the lda stage 69 -> 114 ms, profiles/r6m_lda_stage_ab.json), so the
+        pipeline copies on its own thread before it starts the writer."""
+        return DocWordCounts(self.doc.cpu(), self.word.cpu(), self.count.cpu())
+
 
 def count_pairs(doc: torch.Tensor, word: torch.Tensor, weight: Optional[torch.Tensor] = None) -> DocWordCounts:
     """reduceByKey((doc, word), +weight) with output sorted by (doc, word)."""

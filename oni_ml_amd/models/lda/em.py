@@ -1197,7 +1197,9 @@ class LDAEngine:
     def _collect_batch(self, ticket) -> List[tuple]:
         from ...ops import hip as H
         ev, buf, n = ticket
+        t0 = time.perf_counter()
         ev.synchronize()
+        self._hphase("wait", t0)
         m = 8 + H.HIST_COLS * n
         out = buf[:m].tolist()
         done = int(out[2])
@@ -1388,6 +1390,12 @@ class LDAEngine:
             return self.dist.gather_rows(g, self.global_docs)
         return g
 
+    def _hphase(self, name: str, t0: float):
+        """Host seconds of one EM-loop phase since ``t0`` (init / enqueue / wait / save / save_final), summed
+        per run into ``host_phases``: where the thread driving the GPU spends the lda stage."""
+        hp = self.__dict__.setdefault("host_phases", {})
+        hp[name] = hp.get(name, 0.0) + time.perf_counter() - t0
+
     # ----------------------------------------------------- LAG saves, pipelined
     SNAPSHOT_BYTES = 1 << 30     # device snapshots of the LAG state (2 sets) only below this size
 
@@ -1430,12 +1438,16 @@ class LDAEngine:
                     on_iteration(self, i, lik, c)
             if snap is not None and len(recs) == n and i % lag == 0:
                 view = _Snapshot(self, *snap)
+                t0 = time.perf_counter()
                 on_save(f"{i:03d}", view)
+                self._hphase("save", t0)
             return len(recs) < n
 
         for j, n in enumerate(batches):
+            t0 = time.perf_counter()
             t = self._enqueue_batch(n, st.estimate_alpha, n_docs_global, L_old, it_q, True, emc, emx,
                                     cont=j > 0, buf=bufs[j % 2])
+            self._hphase("enqueue", t0)
             it_q += n
             snap = None
             if it_q % lag == 0:
@@ -1459,6 +1471,7 @@ class LDAEngine:
         st = self.settings
         lag = st.lag
         t0 = time.perf_counter()
+        self.host_phases = {}
         if start == "random":
             self.init_random()
         elif start == "seeded":
@@ -1467,8 +1480,11 @@ class LDAEngine:
             pass  # state restored by caller (checkpoint.restore)
         else:
             raise ValueError(start)
+        self._hphase("init", t0)
         if on_save is not None and start_iteration == 0:
+            ts = time.perf_counter()
             on_save("000", self)
+            self._hphase("save", ts)
         i = start_iteration
         L_old = likelihood_old
         conv = 1.0
@@ -1536,7 +1552,9 @@ class LDAEngine:
             if on_save is not None and lag > 0 and (i % lag) == 0:
                 on_save(f"{i:03d}", self)
         if on_save is not None:
+            ts = time.perf_counter()
             on_save("final", self)
+            self._hphase("save_final", ts)
         res = LDAResult(log_beta=None, gamma=None, alpha=self.alpha, num_topics=self.K, num_terms=self.V,
                         likelihoods=hist, stats=stats, em_iterations=i, seconds=time.perf_counter() - t0)
         return res

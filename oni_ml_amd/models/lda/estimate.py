@@ -362,6 +362,8 @@ def estimate(corpus: Corpus, num_topics: int, alpha_init: float, settings: LDASe
         if not (ok and defer_files):
             writer.close()
     timing["em_s"] = round(res.seconds, 4)
+    # where the GPU-driving thread spent the EM loop (em.py _hphase): init, enqueue, wait, save, save_final
+    timing["em_host"] = {k: round(v, 4) for k, v in getattr(eng, "host_phases", {}).items()}
     t_out = _now()
     res.likelihoods = history
     # this rank's documents (all of them with one rank); the final save already copied both

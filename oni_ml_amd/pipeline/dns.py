@@ -65,10 +65,13 @@ def run(cfg, dist=None, device=None, log=print) -> dict:
                 word_names = wsp.decode(built.word_keys)
                 lp, b_, dn_, wn_, ipn = cfg.lpath, built, doc_names, word_names, feat.ip_names
 
+                # host copies here, not on the writer thread (DocWordCounts.to_host)
+                dwc_h = dwc.to_host() if cfg.write_doc_wc else None
+
                 def write_files():
-                    if cfg.write_doc_wc:
+                    if dwc_h is not None:
                         from ..corpus.builder import write_doc_wc
-                        write_doc_wc(os.path.join(lp, "doc_wc.dat"), dwc, ipn, C.vocab_lookup(b_.word_keys, wn_))
+                        write_doc_wc(os.path.join(lp, "doc_wc.dat"), dwc_h, ipn, C.vocab_lookup(b_.word_keys, wn_))
                     C.write_corpus_files(lp, b_, dn_, wn_)
                 # as in the flow pipeline: the text files on a thread during EM, the marker waits for them
                 if True:   # text files on a thread beside the EM (pipeline/flow.py)

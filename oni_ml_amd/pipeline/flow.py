@@ -74,10 +74,13 @@ def run(cfg, dist=None, device=None, log=print) -> dict:
                 word_names = _word_names(ws, built.word_keys)
                 lp, b_, dn_, wn_ = cfg.lpath, built, doc_names, word_names
 
+                # host copies here, not on the writer thread (DocWordCounts.to_host)
+                dwc_h = dwc.to_host() if cfg.write_doc_wc else None
+
                 def write_files():
-                    if cfg.write_doc_wc:
+                    if dwc_h is not None:
                         from ..corpus.builder import write_doc_wc
-                        write_doc_wc(os.path.join(lp, "doc_wc.dat"), dwc, ipn, C.vocab_lookup(b_.word_keys, wn_))
+                        write_doc_wc(os.path.join(lp, "doc_wc.dat"), dwc_h, ipn, C.vocab_lookup(b_.word_keys, wn_))
                     C.write_corpus_files(lp, b_, dn_, wn_)
                 # the text files are the stage contract, not an input of the in-memory lda stage: written
                 # on a thread while the GPU runs EM; the lda_pre marker waits for them (finish_deferred)

@@ -6,6 +6,8 @@ synthetic headline day, in this process, under variants that remove one suspect 
   sync_pre     lda_pre's text files written before the lda stage (no writer thread beside the EM)
   lag0         no LAG model files inside the EM loop (only 000 and final)
   threads4     the background writers on 4 threads
+  nowc         no doc_wc.dat (the lda_pre writer's one job that copies device tensors to the host)
+  switch       the interpreter's GIL switch interval at 0.2 ms instead of 5 ms
 
 Each variant runs --reps times after one untimed warm-up run; prints the median stage seconds and the
 lda stage's own breakdown (estimate(): setup, EM loop, final pass).
@@ -53,6 +55,9 @@ def main():
                                   threads=4 if v == "threads4" else None)
                 if v == "lag0":
                     cfg.settings.lag = 0
+                if v == "nowc":
+                    cfg.write_doc_wc = False
+                sys.setswitchinterval(2e-4 if v == "switch" else 5e-3)
                 C.background = (lambda fn, name="": (fn(), (lambda: None))[1]) if v == "sync_pre" else real_bg
                 if dev.type == "cuda":
                     torch.cuda.synchronize()
@@ -61,7 +66,9 @@ def main():
                 if dev.type == "cuda":
                     torch.cuda.synchronize()
                 wall = time.perf_counter() - t0
-                recs.append(dict(wall=wall, stages=s.get("stage_seconds", {}), lda=s.get("lda", {}).get("timing", {})))
+                tm = dict(s.get("lda", {}).get("timing", {}))
+                tm.update({"host_" + k: x for k, x in tm.pop("em_host", {}).items()})
+                recs.append(dict(wall=wall, stages=s.get("stage_seconds", {}), lda=tm))
                 shutil.rmtree(lp, ignore_errors=True)
             C.background = real_bg
             if v == "warmup":
