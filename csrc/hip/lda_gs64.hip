@@ -61,21 +61,39 @@ constexpr int tiny_max(int KS) { return tiny_kpl(KS) <= 4 ? 8 : 4; }
 template <int TG, bool PAIR>
 __device__ __forceinline__ int tk(int q, int i) { return PAIR ? 2 * q + (i & 1) + 2 * TG * (i >> 1) : q + TG * i; }
 
-// a word's KPL values of this lane at constant offsets (lanes past KS read into the next row: beta's pad row)
+// a word's KPL values of this lane at constant offsets.  The row's last, partial topic group: lanes past KS
+// re-read the group's last valid topic (the cache line a valid lane already fetches), so a row gather touches
+// only the row's own lines -- reading on into the next row touched ~1.75 extra 128-B lines per 800-B row at
+// KS = 100 (8.75 instead of 7).  Measured at 100 M events: team8 0.147 -> 0.141 ns per word-sweep (-4 %), team4
+// -1 % (profiles/r6p_team4_rmax.md): these gathers are not bound by the lines they fetch.
+// Those lanes' values only ever meet E = 0 or are never stored (every consumer guards tk < KS).
 template <int KS, int KPL, int TG, bool PAIR>
 __device__ __forceinline__ void load_row(const double* __restrict__ beta, int w, int q, double (&b)[KPL]) {
+  const double* rb = beta + (size_t)w * KS;
   if constexpr (PAIR) {
-    const dvec2* r = reinterpret_cast<const dvec2*>(beta + (size_t)w * KS + 2 * q);
+    static_assert(KS % 2 == 0, "pair rows: even KS");
+    const dvec2* r = reinterpret_cast<const dvec2*>(rb + 2 * q);
 #pragma unroll
     for (int ii = 0; ii < KPL / 2; ++ii) {
-      const dvec2 v = r[TG * ii];
+      dvec2 v;
+      if (2 * TG * (ii + 1) <= KS) {
+        v = r[TG * ii];
+      } else {
+        const int last = (KS - 2 * TG * ii) / 2 - 1;     // the group's last valid pair (compile-time)
+        v = *reinterpret_cast<const dvec2*>(rb + 2 * TG * ii + 2 * min(q, last));
+      }
       b[2 * ii] = v.x;
       b[2 * ii + 1] = v.y;
     }
   } else {
-    const double* brow = beta + (size_t)w * KS + q;
+    const double* brow = rb + q;
 #pragma unroll
-    for (int i = 0; i < KPL; ++i) b[i] = brow[TG * i];
+    for (int i = 0; i < KPL; ++i) {
+      if (TG * (i + 1) <= KS)
+        b[i] = brow[TG * i];
+      else
+        b[i] = rb[TG * i + min(q, KS - TG * i - 1)];
+    }
   }
 }
 
@@ -870,7 +888,10 @@ struct TeamShape {
   static constexpr int LSW = ilog2(NSW);
   static constexpr int NS = NW * NSW;                          // word slots per document
   static constexpr int TO = (KS + NTD - 1) / NTD;              // topics owned per thread
-  static constexpr int RMAX = NW >= 8 ? (KPL <= 5 ? 8 : 4) : 1; // prefetched words per slot per chunk (even)
+  // prefetched words per slot per chunk (even).  The 4-wave team keeps one round at KS > 32 too, although it runs
+  // 2 waves per SIMD at any VGPR count up to 256 (171 with one round): 2 or 3 rounds (205 / 230 VGPRs) measured
+  // slower on the K = 100 shard (team4 bucket 5.89 ms at 1, 6.01 at 2, 6.28 at 3; profiles/r6p_team4_rmax.md)
+  static constexpr int RMAX = NW >= 8 ? (KPL <= 5 ? 8 : 4) : 1;
 };
 
 // N words of the word phase, interleaved (independent dependency chains): P = sum_k E_k b_k over
