@@ -405,6 +405,7 @@ def main(argv=None):
         return 1
     prof = knobs.profile("cprofile")
     if isinstance(prof, str):
+        prof = prof.replace("{rank}", os.environ.get("RANK", "0"))   # one file per rank under torchrun
         # host profile of a whole command (cold-start analysis, scripts/cold_start.py)
         import cProfile
         pr = cProfile.Profile()

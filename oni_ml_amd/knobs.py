@@ -41,7 +41,7 @@ KNOBS = {
     "ONI_SHARD_CHAIN": "0: plain nnz-balanced document shards instead of the chain-aware cut",
     # --- observability / process
     "ONI_ROCTX": "1: roctx ranges per stage and EM iteration (rocprofv3 --marker-trace)",
-    "ONI_PROFILE": "comma list: cprofile:FILE (the command under cProfile, stats to FILE), table (native "
+    "ONI_PROFILE": "comma list: cprofile:FILE (the command under cProfile, stats to FILE; {rank} in FILE: the rank), table (native "
                    "ingest / writer timings on stderr)",
     "ONI_FAST_EXIT": "0: full interpreter and HIP teardown after a completed ml_ops (default: os._exit)",
     "ONI_PREFETCH": "0: do not read the day's inputs on a thread while torch imports",

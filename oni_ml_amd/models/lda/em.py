@@ -25,7 +25,9 @@ from __future__ import annotations
 
 import math
 import os
+import threading
 import time
+import weakref
 from dataclasses import dataclass, field
 from typing import Callable, List, Optional
 
@@ -107,6 +109,40 @@ def _stage_budget_gb(v: str) -> float:
                       stacklevel=3)
         return 4.0
     return gb
+
+
+
+class PinnedPool:
+    """Pinned host buffers of the LAG saves' deferred device-to-host copies, reused once the file writer has
+    let go of them.  A fresh process pins ~1.1 ms per 10 MB (profiles/r6q_pinned_probe.log); the headline
+    day's six LAG saves (log beta, gamma, the checkpoint's class_word) took a new ~40 MB set each, ~42 ms of
+    a cold ml_ops lda stage.  ``take`` returns a (tensor, ndarray) pair; when the ndarray and every view of
+    it are gone (the writer's jobs finished), the tensor goes back to the free list of its shape."""
+
+    def __init__(self, alloc: Optional[Callable] = None):
+        self._free = {}
+        self._lock = threading.Lock()
+        self._alloc = alloc or (lambda shape, dtype: torch.empty(shape, dtype=dtype, pin_memory=True))
+        self.allocated = 0           # buffers pinned so far (tests, records)
+
+    def take(self, shape, dtype):
+        key = (tuple(int(x) for x in shape), dtype)
+        with self._lock:
+            lst = self._free.get(key)
+            t = lst.pop() if lst else None
+        if t is None:
+            t = self._alloc(key[0], dtype)
+            self.allocated += 1
+        arr = t.numpy()
+        weakref.finalize(arr, self._give, key, t)
+        return t, arr
+
+    def _give(self, key, t):
+        with self._lock:
+            self._free.setdefault(key, []).append(t)
+
+
+_PINNED = PinnedPool()
 
 
 class LDAEngine:
@@ -1292,10 +1328,12 @@ class LDAEngine:
     # *_deferred variants; larger ones take the blocking, chunked path
     DEFER_BYTES = 256 << 20
 
-    def log_beta_deferred(self, cw: Optional[torch.Tensor] = None):
+    def log_beta_deferred(self, cw: Optional[torch.Tensor] = None, reuse: bool = False):
         """(host [K, V] array, event or None): ``log_beta`` whose device-to-host copy is queued on the
         current stream into a pinned buffer; the array is valid once ``event`` completed.  The LAG saves
-        hand both to the file writer, so an EM run with saves does not wait for each copy."""
+        hand both to the file writer, so an EM run with saves does not wait for each copy.  ``reuse``: the
+        buffer comes from the process's PinnedPool (the caller must not keep the array past its writer
+        jobs' use -- the LAG saves; the final save's arrays are returned to the caller and stay fresh)."""
         full = self.global_cw() if cw is None else cw
         c = full[:, :self.K]
         V, K = c.shape
@@ -1304,33 +1342,33 @@ class LDAEngine:
         cT = c.T.to(torch.float64).contiguous()
         lct = torch.log(self.class_total[:K].to(torch.float64))
         lb = torch.where(cT > 0, torch.log(cT) - lct[:, None], torch.full_like(cT, LOG_FLOOR))
-        host = torch.empty((K, V), dtype=torch.float64, pin_memory=True)
+        host, arr = _pinned(reuse, (K, V), torch.float64)
         host.copy_(lb, non_blocking=True)
         ev = torch.cuda.Event()
         ev.record()
-        return host.numpy(), ev
+        return arr, ev
 
-    def host_copy_deferred(self, t: torch.Tensor):
+    def host_copy_deferred(self, t: torch.Tensor, reuse: bool = False):
         """(host array, event or None): a copy of device tensor ``t`` queued on the current stream into a
         pinned buffer (valid once ``event`` completed); blocking for host tensors or above DEFER_BYTES."""
         if t.device.type != "cuda" or t.numel() * t.element_size() > self.DEFER_BYTES:
             return t.to("cpu", copy=True).numpy(), None
-        host = torch.empty(tuple(t.shape), dtype=t.dtype, pin_memory=True)
+        host, arr = _pinned(reuse, tuple(t.shape), t.dtype)
         host.copy_(t if t.is_contiguous() else t.contiguous(), non_blocking=True)
         ev = torch.cuda.Event()
         ev.record()
-        return host.numpy(), ev
+        return arr, ev
 
-    def local_gamma_deferred(self):
+    def local_gamma_deferred(self, reuse: bool = False):
         """(host [D_local, K] gamma, event or None): ``local_gamma`` with a queued pinned copy."""
         g = self.gamma[:, :self.K]
         if self.device.type != "cuda" or g.numel() * 8 > self.DEFER_BYTES:
             return self.local_gamma(), None
-        host = torch.empty(tuple(g.shape), dtype=torch.float64, pin_memory=True)
+        host, arr = _pinned(reuse, tuple(g.shape), torch.float64)
         host.copy_(g if g.is_contiguous() else g.contiguous(), non_blocking=True)
         ev = torch.cuda.Event()
         ev.record()
-        return host.numpy(), ev
+        return arr, ev
 
     def local_log_beta(self) -> np.ndarray:
         """[K, V] log of this rank's own class_word rows over the GLOBAL class totals (-100 floor):
@@ -1579,6 +1617,14 @@ class _Snapshot:
     host_copy_deferred = LDAEngine.host_copy_deferred
     local_gamma_deferred = LDAEngine.local_gamma_deferred
     local_gamma = LDAEngine.local_gamma
+
+
+def _pinned(reuse: bool, shape, dtype):
+    """(pinned tensor, its ndarray): from the PinnedPool when ``reuse``, else a fresh buffer."""
+    if reuse:
+        return _PINNED.take(shape, dtype)
+    t = torch.empty(shape, dtype=dtype, pin_memory=True)
+    return t, t.numpy()
 
 
 def _lag_batches(i: int, last: int, lag: int, cap: int) -> List[int]:

@@ -70,6 +70,7 @@ class AsyncWriter:
                     job()
                 except BaseException as e:  # surfaced by close()
                     self._err = e
+            job = None      # drop the job's arrays now (pooled pinned buffers go back to the pool)
 
     def submit(self, fn, *args, key: Optional[str] = None, **kw):
         """``key``: jobs with the same key run on one thread in submission order (one file rewritten
@@ -293,13 +294,16 @@ def estimate(corpus: Corpus, num_topics: int, alpha_init: float, settings: LDASe
         cwg = e.global_cw()
         ev_st = None
         st = None
+        # LAG saves take their pinned buffers from the process's pool (the writer's jobs are their only
+        # users); the final save's arrays are returned to the caller and get fresh ones
+        reuse = tag != "final"
         if ckpt:   # the checkpoint's exact statistics, copied behind the device work like the model
-            cw_h, _ = e.host_copy_deferred(cwg)
-            ct_h, ev_st = e.host_copy_deferred(e.class_total)     # queued after cw: its event covers both
+            cw_h, _ = e.host_copy_deferred(cwg, reuse=reuse)
+            ct_h, ev_st = e.host_copy_deferred(e.class_total, reuse=reuse)   # queued after cw: its event covers both
             st = dict(cw=cw_h, class_total=ct_h)
         # host copies queued behind the device work; the writer waits for their events
-        lb, ev_lb = e.log_beta_deferred(cwg)
-        g, ev_g = e.local_gamma_deferred() if tag != "000" else (None, None)
+        lb, ev_lb = e.log_beta_deferred(cwg, reuse=reuse)
+        g, ev_g = e.local_gamma_deferred(reuse=reuse) if tag != "000" else (None, None)
         if tag == "final":
             for ev in (ev_lb, ev_g):
                 if ev is not None:

@@ -21,6 +21,11 @@ def variants():
         # the 8-wave team only past 4,096 words
         "t8_4k": ((H.GS_TEAM8, 4096, None), (H.GS_TEAM4, 256, 4096), (H.GS_SMALL, None, 256)),
         "t8_8k": ((H.GS_TEAM8, 8192, None), (H.GS_TEAM4, 256, 8192), (H.GS_SMALL, None, 256)),
+        # the 16-lane kernel (no barrier, four documents per wave) up to 512 / 1,024 words instead of 256
+        "s512": ((H.GS_TEAM8, 2048, None), (H.GS_TEAM4, 512, 2048), (H.GS_SMALL, None, 512)),
+        "s1024": ((H.GS_TEAM8, 2048, None), (H.GS_TEAM4, 1024, 2048), (H.GS_SMALL, None, 1024)),
+        # the 16-lane kernel only up to 128 words (the 4-wave team from 129)
+        "s128": ((H.GS_TEAM8, 2048, None), (H.GS_TEAM4, 128, 2048), (H.GS_SMALL, None, 128)),
     }
 
 
