@@ -49,6 +49,9 @@ PYBIND11_MODULE(_onihip, m) {
     oni::launch_rows_accumulate(P<const int>(rows), P<const int>(ptr), P<const int>(src), P<const double>(own),
                                 P<const double>(recv), P<double>(out), n_rows, width, S(stream));
   });
+  m.def("log_beta_t", [](u cw, int V, int K, int ld, u ct, double floor_v, u out, u stream) {
+    oni::launch_log_beta_t(P<const double>(cw), V, K, ld, P<const double>(ct), floor_v, P<double>(out), S(stream));
+  });
   m.def("colsum_partials", [](u part, int nb, int cols, u out, u gate, u stream) {
     oni::launch_colsum_partials(P<const double>(part), nb, cols, P<double>(out), P<const double>(gate), S(stream));
   });

@@ -198,6 +198,9 @@ void launch_gs_mstep(const double* cw, const double* class_total, double* beta, 
 // Deterministic reductions (reduce.hip).  gate (nullable): skip when *gate != 0.
 // out[k] = sum_b part[b][k] (b in order), the second pass of the fused suff-stats.
 void launch_colsum_partials(const double* part, int nb, int cols, double* out, const double* gate, hipStream_t s);
+// out [K][V] = log(cw[v][k]) - log(ct[k]) (floor_v where cw == 0): the saved log beta in file order.
+void launch_log_beta_t(const double* cw, int V, int K, int ld, const double* ct, double floor_v, double* out,
+                       hipStream_t s);
 // Sparse class_word exchange: out[rows[i]] = 0 + src_0 + src_1 + ... over row i's sources
 // (CSR ptr/src; src >= 0: recv row, src < 0: the rank's own row own[rows[i]]), fp64, double2 granules.
 void launch_rows_accumulate(const int* rows, const int* ptr, const int* src, const double* own, const double* recv,

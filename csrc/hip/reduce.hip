@@ -90,3 +90,31 @@ void launch_rows_accumulate(const int* rows, const int* ptr, const int* src, con
 }
 
 }  // namespace oni
+
+namespace oni {
+
+// Model files (LAG saves, final.beta): out[k][v] = log(cw[v][k]) - log(ct[k]), or `floor` where cw[v][k] == 0 --
+// lda-c's saved log beta, transposed to its [K][V] file order.  One thread per (k, v), v fastest: the [K][V]
+// writes coalesce, the cw reads stride KS doubles (the whole matrix is read once).  Replaces torch's transpose /
+// log / where chain on the save path: the same ocml log in the same order (bitwise the torch result), and no
+// first use of torch's elementwise kernels inside the EM loop of a fresh process.
+__global__ __launch_bounds__(kRT) void log_beta_t_kernel(const double* __restrict__ cw, int V, int K, int ld,
+                                                         const double* __restrict__ ct, double floor_v,
+                                                         double* __restrict__ out) {
+  const long long i = (long long)blockIdx.x * kRT + threadIdx.x;
+  if (i >= (long long)V * K) return;
+  const int k = (int)(i / V), v = (int)(i - (long long)k * V);
+  const double c = cw[(size_t)v * ld + k];
+  out[i] = c > 0.0 ? log(c) - log(ct[k]) : floor_v;
+}
+
+void launch_log_beta_t(const double* cw, int V, int K, int ld, const double* ct, double floor_v, double* out,
+                       hipStream_t s) {
+  const long long n = (long long)V * K;
+  if (n <= 0) return;
+  hipLaunchKernelGGL(log_beta_t_kernel, dim3((unsigned)((n + kRT - 1) / kRT)), dim3(kRT), 0, s, cw, V, K, ld, ct,
+                     floor_v, out);
+  ONI_HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace oni

@@ -145,6 +145,43 @@ class PinnedPool:
 _PINNED = PinnedPool()
 
 
+class DeviceHandoff:
+    """A device tensor of a LAG save handed to a file-writer thread.  The thread driving the GPU only queues a
+    device copy of the saved state and records ``event``; the writer's first ``get()`` copies the tensor to a
+    pooled pinned host buffer on a side stream of its own (behind ``event``), waits for that stream only, and
+    drops the device tensor.  The host buffers are then pinned and taken by the writer when it is ready to
+    format, not by the EM loop at every save (profiles/r6_lda_stage.md)."""
+    _streams = {}
+    _slock = threading.Lock()
+
+    def __init__(self, t: torch.Tensor, event):
+        self._t, self._ev = t, event
+        self.shape, self.dtype = tuple(t.shape), t.dtype
+        self._lock = threading.Lock()
+        self._host = None
+
+    @classmethod
+    def _stream(cls, device):
+        with cls._slock:
+            s = cls._streams.get(device)
+            if s is None:
+                s = cls._streams[device] = torch.cuda.Stream(device=device)
+            return s
+
+    def get(self) -> np.ndarray:
+        with self._lock:
+            if self._host is None:
+                t = self._t
+                s = self._stream(t.device)
+                s.wait_event(self._ev)
+                h, arr = _PINNED.take(self.shape, self.dtype)
+                with torch.cuda.stream(s):
+                    h.copy_(t, non_blocking=True)
+                s.synchronize()
+                self._host, self._t = arr, None
+            return self._host
+
+
 class LDAEngine:
     def __init__(self, corpus: Corpus, num_topics: int, settings: Optional[LDASettings] = None,
                  alpha_init: float = 2.5, backend: str = "auto", device=None, dist=None, seed: int = 0,
@@ -1180,6 +1217,8 @@ class LDAEngine:
                 m = min(cap, left)
                 g = self._fgraphs.get(m)
                 if g is None:
+                    # (one more direct launch ahead of the capture, so two iterations are queued while the host
+                    # records: measured no faster to convergence, 52.96 vs 53.00 ms median of 7, r6w)
                     self._fgraphs[m] = self._capture(
                         lambda: [self._launch_estep(newton_key=key) for _ in range(m)])
                 else:
@@ -1339,14 +1378,46 @@ class LDAEngine:
         V, K = c.shape
         if self.device.type != "cuda" or K * V * 8 > self.DEFER_BYTES:
             return _log_beta_host(c, self.class_total[:K]), None
-        cT = c.T.to(torch.float64).contiguous()
-        lct = torch.log(self.class_total[:K].to(torch.float64))
-        lb = torch.where(cT > 0, torch.log(cT) - lct[:, None], torch.full_like(cT, LOG_FLOOR))
+        lb = self._log_beta_device(full, K)
         host, arr = _pinned(reuse, (K, V), torch.float64)
         host.copy_(lb, non_blocking=True)
         ev = torch.cuda.Event()
         ev.record()
         return arr, ev
+
+    def _log_beta_device(self, full: torch.Tensor, K: int) -> torch.Tensor:
+        """[K, V] saved log beta on the device: the HIP kernel (ops/hip.py log_beta_t) where the engine is the HIP
+        one and the statistics are plain contiguous fp64, else torch's transpose / log / where (the same bits)."""
+        ct = self.class_total
+        if self.backend == "hip" and full.dtype == torch.float64 and full.is_contiguous() and \
+                ct.dtype == torch.float64 and ct.is_contiguous():
+            from ...ops import hip as H
+            return H.log_beta_t(full, ct, K, LOG_FLOOR)
+        cT = full[:, :K].T.to(torch.float64).contiguous()
+        lct = torch.log(ct[:K].to(torch.float64))
+        return torch.where(cT > 0, torch.log(cT) - lct[:, None], torch.full_like(cT, LOG_FLOOR))
+
+    def save_handoff(self, cw: torch.Tensor, gamma: bool, checkpoint: bool) -> Optional[dict]:
+        """A LAG save's state as DeviceHandoffs -- log_beta [K, V], gamma [D, K] (``gamma``), the checkpoint's
+        class_word and class totals (``checkpoint``) -- copied on the device behind the work already queued, one
+        event for all; None where the handoff does not apply (not the one-rank HIP engine on a GPU, or a save
+        larger than SNAPSHOT_BYTES: those keep the pinned-copy path)."""
+        if self.backend != "hip" or self.device.type != "cuda" or self._distributed:
+            return None
+        K = self.K
+        nbytes = (K * cw.shape[0] + (self.gamma.shape[0] * K if gamma else 0) +
+                  (cw.numel() + self.class_total.numel() if checkpoint else 0)) * 8
+        if nbytes > self.SNAPSHOT_BYTES:
+            return None
+        out = dict(log_beta=self._log_beta_device(cw, K))
+        if gamma:
+            out["gamma"] = self.gamma[:, :K].contiguous() if self.gamma.shape[1] != K else self.gamma.clone()
+        if checkpoint:
+            out["cw"] = cw.clone()
+            out["class_total"] = self.class_total.clone()
+        ev = torch.cuda.Event()
+        ev.record()
+        return {k: DeviceHandoff(v, ev) for k, v in out.items()}
 
     def host_copy_deferred(self, t: torch.Tensor, reuse: bool = False):
         """(host array, event or None): a copy of device tensor ``t`` queued on the current stream into a
@@ -1614,6 +1685,8 @@ class _Snapshot:
         return self.cw
 
     log_beta_deferred = LDAEngine.log_beta_deferred
+    _log_beta_device = LDAEngine._log_beta_device
+    save_handoff = LDAEngine.save_handoff
     host_copy_deferred = LDAEngine.host_copy_deferred
     local_gamma_deferred = LDAEngine.local_gamma_deferred
     local_gamma = LDAEngine.local_gamma

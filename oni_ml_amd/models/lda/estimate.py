@@ -31,7 +31,7 @@ import torch
 
 from ...corpus.csr import Corpus
 from ...io import ldac
-from .em import LDAEngine, LDAResult
+from .em import DeviceHandoff, LDAEngine, LDAResult
 from .settings import LAG, LDASettings
 
 CKPT = "checkpoint.npz"
@@ -96,6 +96,22 @@ class AsyncWriter:
 def _append_text(path: str, text: str):
     with open(path, "a") as f:
         f.write(text)
+
+
+def _host(x):
+    """A DeviceHandoff's host array (copied on the calling writer thread), dict values resolved, else x."""
+    if isinstance(x, DeviceHandoff):
+        return x.get()
+    if isinstance(x, dict):
+        return {k: _host(v) for k, v in x.items()}
+    return x
+
+
+def _resolved(fn):
+    """fn with every DeviceHandoff argument (and dict value) replaced by its host array, in the writer thread."""
+    def run(*args, **kw):
+        return fn(*[_host(a) for a in args], **{k: _host(v) for k, v in kw.items()})
+    return run
 
 
 def _after(event, fn):
@@ -297,6 +313,22 @@ def estimate(corpus: Corpus, num_topics: int, alpha_init: float, settings: LDASe
         # LAG saves take their pinned buffers from the process's pool (the writer's jobs are their only
         # users); the final save's arrays are returned to the caller and get fresh ones
         reuse = tag != "final"
+        ho = e.save_handoff(cwg, gamma=tag != "000", checkpoint=ckpt) if reuse and not multi else None
+        if ho is not None:
+            # one rank on the GPU: device copies + one event here, the host copies on the writer threads
+            if not rank0:
+                return
+            writer.submit(_resolved(ldac.save_model), os.path.join(outdir, tag), ho["log_beta"], e.alpha)
+            if "gamma" in ho:
+                writer.submit(_resolved(ldac.save_gamma), os.path.join(outdir, f"{tag}.gamma"), ho["gamma"])
+            if ckpt:
+                ck = dict(log_beta=ho["log_beta"], alpha=np.float64(e.alpha), iteration=np.int64(int(tag)),
+                          likelihood_old=np.float64(history[-1][0] if history else 0.0),
+                          var_max_iter=np.int64(e.var_max_iter),
+                          history=np.asarray(history, np.float64).reshape(-1, 2),
+                          cw=ho["cw"], class_total=ho["class_total"])
+                writer.submit(_resolved(_write_checkpoint), outdir, ck, key="checkpoint")
+            return
         if ckpt:   # the checkpoint's exact statistics, copied behind the device work like the model
             cw_h, _ = e.host_copy_deferred(cwg, reuse=reuse)
             ct_h, ev_st = e.host_copy_deferred(e.class_total, reuse=reuse)   # queued after cw: its event covers both

@@ -192,6 +192,24 @@ def init_random_ss(cw, K, seed):
                          int(seed) & 0xFFFFFFFFFFFFFFFF, _stream())
 
 
+def log_beta_t(cw, class_total, K: int, floor: float, out=None):
+    """[K, V] float64 log(cw[:, k]) - log(class_total[k]) (``floor`` where cw == 0) of a [V, KS] class_word: the
+    saved log beta in file order (csrc/hip/reduce.hip log_beta_t_kernel; bitwise torch's transpose / log / where)."""
+    dev = cw.device
+    V, KS = cw.shape
+    if not (0 < K <= KS):
+        raise ValueError(f"log_beta_t: K={K} outside 1..{KS}")
+    p_cw = _chk(cw, torch.float64, "cw", (V, KS), dev)
+    p_ct = _chk(class_total, torch.float64, "class_total", None, dev)
+    if class_total.numel() < K:
+        raise ValueError(f"log_beta_t: class_total holds {class_total.numel()} < K = {K} values")
+    if out is None:
+        out = torch.empty((K, V), dtype=torch.float64, device=dev)
+    p_out = _chk(out, torch.float64, "out", (K, V), dev)
+    lib().log_beta_t(p_cw, int(V), int(K), int(KS), p_ct, float(floor), p_out, _stream())
+    return out
+
+
 def colsum_partials(part, n_blocks, out, gate=None):
     """out[k] = sum_b part[b, k] for b < n_blocks (deterministic order)."""
     dev = part.device

@@ -1,0 +1,6 @@
+# strong-scaling emulation of the 1-day configs on round-6 kernels (headline K = 20, config 3 K = 50, config 4 DNS)
+set -u -o pipefail
+cd /tmp && export TMPDIR=/tmp
+cd "$GRAFT_REPO_ROOT"
+export TAG=r6v STRONG_ARGS="--configs headline,k50,dns"
+bash scripts/gpu.sh strong

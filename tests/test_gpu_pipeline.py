@@ -128,14 +128,20 @@ def test_lag_saves_from_snapshots_match_draining_loop(tmp_path, monkeypatch, con
     the same files, byte for byte, as the loop that drains the device at every LAG boundary: the %03d
     models, the checkpoint's statistics, likelihood.dat, final.* (conv 3e-4: the device loop stops before
     the last boundary, which then saves nothing)."""
+    from oni_ml_amd.models.lda import em as EM
     from oni_ml_amd.models.lda.em import LDAEngine
     from oni_ml_amd.models.lda.estimate import estimate
     from oni_ml_amd.synth.corpus import planted_corpus
     c = planted_corpus(num_docs=3000, num_terms=800, num_topics=6, seed=4)
     out = {}
-    for mode in ("snap", "drain"):
+    # snap / drain: the LAG state handed to the writer threads as device copies (LDAEngine.save_handoff);
+    # pinned: the round-5 path (pinned host copies queued by the EM loop itself)
+    for mode in ("snap", "drain", "pinned"):
         if mode == "drain":
             monkeypatch.setattr(LDAEngine, "_snapshot_saves_ok", lambda self: False)
+        if mode == "pinned":
+            monkeypatch.setattr(LDAEngine, "save_handoff", lambda self, *a, **k: None)
+            monkeypatch.setattr(EM._Snapshot, "save_handoff", lambda self, *a, **k: None)
         st = LDASettings(em_max_iter=23, em_converged=conv)
         st.lag = 3
         d = tmp_path / mode
@@ -143,11 +149,13 @@ def test_lag_saves_from_snapshots_match_draining_loop(tmp_path, monkeypatch, con
         files = sorted(p.name for p in d.iterdir() if p.is_file() and p.suffix not in (".json", ".npz"))
         npz = {p.name: dict(np.load(p)) for p in d.iterdir() if p.suffix == ".npz"}   # (zip entries carry times)
         out[mode] = (res.em_iterations, {f: (d / f).read_bytes() for f in files}, npz)
-    (n1, f1, c1), (n2, f2, c2) = out["snap"], out["drain"]
-    assert n1 == n2 and sorted(f1) == sorted(f2)
-    assert any(f.endswith(".beta") and f[:3].isdigit() and f != "000.beta" for f in f1)
-    for f in f1:
-        assert f1[f] == f2[f], f
-    assert sorted(c1) == sorted(c2) and "checkpoint.npz" in c1
-    for name in c1:
-        assert sorted(c1[name]) == sorted(c2[name]) and all(np.array_equal(c1[name][k], c2[name][k]) for k in c1[name])
+    for other in ("drain", "pinned"):
+        (n1, f1, c1), (n2, f2, c2) = out["snap"], out[other]
+        assert n1 == n2 and sorted(f1) == sorted(f2)
+        assert any(f.endswith(".beta") and f[:3].isdigit() and f != "000.beta" for f in f1)
+        for f in f1:
+            assert f1[f] == f2[f], (other, f)
+        assert sorted(c1) == sorted(c2) and "checkpoint.npz" in c1
+        for name in c1:
+            assert sorted(c1[name]) == sorted(c2[name]) and \
+                all(np.array_equal(c1[name][k], c2[name][k]) for k in c1[name]), (other, name)

@@ -72,3 +72,20 @@ def test_alpha_newton_device_matches_host(K):
         a = float(out.item())
         assert a == pytest.approx(host, rel=1e-9), (astar, a, host)
         assert float(params[1].item()) == pytest.approx(special.lik_const(a, K), rel=1e-9, abs=1e-9)
+
+
+@pytest.mark.parametrize("V,K,KS", [(1000, 20, 20), (777, 50, 52), (4097, 100, 100), (3, 7, 8)])
+def test_log_beta_kernel_bitwise(hip, V, K, KS):
+    """The saved log beta's HIP kernel (ops/hip.py log_beta_t) against torch's transpose / log / where chain on
+    the device, bit for bit, including the -100 floor of zero counts and padding columns past K."""
+    from oni_ml_amd.ops import hip as H
+    g = torch.Generator().manual_seed(V + K)
+    cw = torch.rand((V, KS), generator=g, dtype=torch.float64) * 50
+    cw[torch.rand((V, KS), generator=g) < 0.2] = 0.0
+    cw = cw.cuda()
+    ct = cw.sum(0) + 1.0
+    got = H.log_beta_t(cw, ct, K, -100.0)
+    cT = cw[:, :K].T.contiguous()
+    want = torch.where(cT > 0, torch.log(cT) - torch.log(ct[:K])[:, None], torch.full_like(cT, -100.0))
+    assert got.shape == (K, V)
+    assert torch.equal(got.view(torch.int64), want.view(torch.int64))
