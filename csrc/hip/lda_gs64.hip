@@ -2851,10 +2851,13 @@ static void gs_estep_ks(const GSArgs& a, int variant, hipStream_t s) {
         // a quarter of the waves for the same chains leaves the CUs to the other buckets
         hipLaunchKernelGGL((gs::gs_wteam<KS, 1, 1>), dim3(a.n_items), dim3(64), 0, s, a);
       }
-      else if (a.gs_updates > kGsUMax)
-        hipLaunchKernelGGL((gs::gs_team<KS, 4, 1, true>), dim3(a.n_items), dim3(256), 0, s, a);
       else
-        hipLaunchKernelGGL((gs::gs_team<KS, 4>), dim3(a.n_items), dim3(256), 0, s, a);
+        // KS > 32, any U: the chunk tables in the c*phi rows (GM) and 3 waves per SIMD.  The LDS-table form
+        // (2 x 32 x KS doubles: 58 KB at K = 100) fits two workgroups per CU; this one (6.7 KB, 166 VGPRs, 12 B
+        // spilled) three: team4 bucket 5.88 -> 4.78 ms on the 12.5 M-event shard, 38.1 -> 30.7 ms at 100 M
+        // events (E-step graph 170.0 -> 167.1 ms); 4 waves per SIMD spill 160 B and gain less
+        // (profiles/r6z_team4_gm.md)
+        hipLaunchKernelGGL((gs::gs_team<KS, 4, 3, true>), dim3(a.n_items), dim3(256), 0, s, a);
       break;
     case kGsTeam8:
       if (KS <= 32 && a.gs_updates > kGsUMax) {

@@ -654,6 +654,15 @@ def split_seg_words(KS: int) -> int:
     return gs_team8_words(KS) * 7 // 8
 
 
+def split_seg_target(KS: int) -> int:
+    """Smallest useful share of a chunk per split segment (words), the water-filling's cap on a document's
+    segments (G <= ceil(W / target)): the split kernel's prefetched rounds at K = 100 (112 words); at KS <= 64
+    (8-lane topic groups, 224 prefetched words) 96 -- the 1-day corpus at K = 50 per EM iteration: 3.15 ms with
+    the prefetch-sized cap (its longest document on 4 segments), 2.94 / 2.58 / 2.88 / 3.6 ms with fixed
+    shares of 128 / 96 / 64 / 48 words (profiles/r6z_split_k50.md)."""
+    return 96 if KS <= 64 else split_seg_words(KS)
+
+
 def split_chain_cycles(n: int, U: int, G: int, KS: int) -> float:
     """Modelled cycles of one chunk of an n-word document on G segments (G = 1: the 8-wave team kernel),
     for the plan's segment allocation only (profiles/r6_split.md): a word-phase term per word of the
@@ -665,7 +674,11 @@ def split_chain_cycles(n: int, U: int, G: int, KS: int) -> float:
     word = 40.0 * min(per, sw) + (1800.0 * -(-(per - sw) // sw) if per > sw else 0.0) + 2000.0
     if G == 1:
         return word
-    xch = 4000.0 + (0.0 if G <= 4 else 2500.0 if G <= 8 else 8000.0 if G <= SPLIT_MAX_SEG_GATHER else 6000.0)
+    # the exchange's steps past 4 segments grow with the granules a segment reads: (KS + 1) columns each.
+    # Fitted at K = 100; at K = 50 the unscaled steps stopped the 1-day corpus' longest document at 4 segments,
+    # 3.15 ms per EM iteration against 2.58 with 8 (profiles/r6z_split_k50.md)
+    step = 0.0 if G <= 4 else 2500.0 if G <= 8 else 8000.0 if G <= SPLIT_MAX_SEG_GATHER else 6000.0
+    xch = 4000.0 + step * (KS + 1) / 101.0
     return word + xch + 1500.0
 
 
@@ -691,8 +704,10 @@ class GSSplitPlan:
         sp = split_spec(KS)
         # an explicit segment size (ONI_GS_SPLIT_MIN words=W, or the argument) fixes G = clamp(ceil(W / words),
         # 2, max_seg) per document, longest first; otherwise the modelled water-filling (_allocate)
-        self.fixed = bool(int(seg_words) or sp["words"])
-        self.seg_words = int(seg_words) or sp["words"] or split_seg_words(KS)
+        # KS <= 64: fixed 96-word shares by default -- measured ahead of the water-filling there (2.58 vs 2.74 ms
+        # per EM iteration at K = 50, profiles/r6z_split_k50.md), where the model was fitted at K = 100
+        self.fixed = bool(int(seg_words) or sp["words"]) or self.KS <= 64
+        self.seg_words = int(seg_words) or sp["words"] or split_seg_target(KS)
         # KS <= 32: the single-round gather only (gs_splitw has no two-phase exchange in the narrow layout)
         max_seg = min(int(max_seg) or sp["g"], self.max_blocks,
                       SPLIT_MAX_SEG if self.KS > 32 else SPLIT_MAX_SEG_GATHER)
