@@ -209,7 +209,8 @@ def _e2e_cold(args, ctx, tmp):
     for _ in range(2):
         ctx.barrier()
         t0 = time.perf_counter()
-        env["ONI_T_SPAWN"] = repr(time.time())
+        t_spawn = time.time()
+        env["ONI_T_SPAWN"] = repr(t_spawn)
         r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=args.e2e_timeout)
         wall = time.perf_counter() - t0
         if r.returncode != 0:
@@ -228,7 +229,9 @@ def _e2e_cold(args, ctx, tmp):
             out["e2e_cold_flagged"] = sm.get("scored")
             out["e2e_cold_lda_timing"] = sm.get("lda", {}).get("timing")
             out["e2e_cold_startup_marks"] = sm.get("startup_marks")
-        except (OSError, ValueError):
+            with open(os.path.join(lpath, ".exit_mark")) as f:   # the child's os._exit call: the rest is process teardown
+                out["e2e_cold_startup_marks"]["exit_call"] = round(float(f.read()) - t_spawn, 4)
+        except (OSError, ValueError, TypeError):
             pass
     return out
 

@@ -34,6 +34,8 @@ from . import knobs
 MARKS = {}
 # set by a completed ml_ops when ONI_FAST_EXIT (default 1) allows `python -m oni_ml_amd` to skip teardown
 FAST_EXIT = False
+# <LPATH>/.exit_mark when a timing parent set ONI_T_SPAWN: __main__ writes the time of its exit call there
+EXIT_MARK = None
 
 
 def _tool_attached() -> bool:
@@ -206,8 +208,10 @@ def _ml_ops_body(a, resolve):
             if ui and rp:
                 subprocess.run(["scp", "-r", cfg.lpath, f"{ui}:{rp}"], check=True)
     ctx.shutdown()
-    global FAST_EXIT
+    global FAST_EXIT, EXIT_MARK
     FAST_EXIT = knobs.get("ONI_FAST_EXIT", "1") != "0" and not _tool_attached()
+    if ctx.rank == 0 and knobs.get("ONI_T_SPAWN", ""):
+        EXIT_MARK = os.path.join(cfg.lpath, ".exit_mark")
     return 0
 
 

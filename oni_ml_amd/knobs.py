@@ -45,7 +45,7 @@ KNOBS = {
                    "ingest / writer timings on stderr)",
     "ONI_FAST_EXIT": "0: full interpreter and HIP teardown after a completed ml_ops (default: os._exit)",
     "ONI_PREFETCH": "0: do not read the day's inputs on a thread while torch imports",
-    "ONI_T_SPAWN": "internal: spawn time a parent (bench.py, scripts/cold_start.py) hands a child process",
+    "ONI_T_SPAWN": "internal: spawn time a parent (bench.py, scripts/cold_start.py) hands a child process (the child then also writes the time of its exit call to <LPATH>/.exit_mark)",
 }
 
 
