@@ -230,7 +230,9 @@ def _e2e_cold(args, ctx, tmp):
             out["e2e_cold_lda_timing"] = sm.get("lda", {}).get("timing")
             out["e2e_cold_startup_marks"] = sm.get("startup_marks")
             with open(os.path.join(lpath, ".exit_mark")) as f:   # the child's os._exit call: the rest is process teardown
-                out["e2e_cold_startup_marks"]["exit_call"] = round(float(f.read()) - t_spawn, 4)
+                ex = f.read().split()
+            out["e2e_cold_startup_marks"]["exit_call"] = round(float(ex[0]) - t_spawn, 4)
+            out["e2e_cold_exit_status"] = dict(kv.split("=", 1) for kv in ex[1:])
         except (OSError, ValueError, TypeError):
             pass
     return out

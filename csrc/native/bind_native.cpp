@@ -422,6 +422,54 @@ PYBIND11_MODULE(_oninative, m) {
     return out;
   });
 
+  // Flow word strings of integer word keys (features/flow.py FlowWordSpace.decode):
+  // key = (((port * NT + tb) * NB + bb) * NP + pb) * 2 + prefix -> "[-1_]<port>_<tb>_<bb>_<pb>", every
+  // number in Java Double.toString form (flow_pre_lda.scala:349).  Heads (one per port and side) and
+  // tails (one per bin triple) are formatted once; the words are concatenated without the GIL into
+  // one buffer, then turned into str objects.
+  m.def("flow_word_names", [](py::array_t<double, py::array::c_style | py::array::forcecast> ports, int NT, int NB,
+                              int NP, py::array_t<int64_t, py::array::c_style | py::array::forcecast> keys) {
+    const int64_t np_ = ports.size(), nk = keys.size();
+    const int64_t nt = (int64_t)NT * NB * NP;
+    if (NT <= 0 || NB <= 0 || NP <= 0) throw std::invalid_argument("flow_word_names: empty bin range");
+    std::vector<std::string> heads(2 * np_), tails(nt);
+    const int nb = std::max(NT, std::max(NB, NP));
+    std::vector<std::string> bstr(nb);
+    for (int i = 0; i < nb; ++i) bstr[i] = java_double((double)i);
+    for (int64_t p = 0; p < np_; ++p) {
+      const std::string ps = java_double(ports.data()[p]);
+      heads[2 * p] = ps + "_";
+      heads[2 * p + 1] = "-1_" + ps + "_";
+    }
+    for (int t = 0; t < NT; ++t)
+      for (int b = 0; b < NB; ++b)
+        for (int q = 0; q < NP; ++q) tails[((int64_t)t * NB + b) * NP + q] = bstr[t] + "_" + bstr[b] + "_" + bstr[q];
+    std::string buf;
+    std::vector<int64_t> ends(nk);
+    const int64_t* k = keys.data();
+    {
+      py::gil_scoped_release rel;
+      buf.reserve((size_t)nk * 24);
+      for (int64_t i = 0; i < nk; ++i) {
+        const int64_t key = k[i];
+        const int64_t rest = key >> 1, tail = rest % nt, port = rest / nt;
+        if (key < 0 || port >= np_) throw std::out_of_range("flow_word_names: key outside the word space");
+        buf += heads[2 * port + (key & 1)];
+        buf += tails[tail];
+        ends[i] = (int64_t)buf.size();
+      }
+    }
+    py::list out(nk);
+    int64_t s = 0;
+    for (int64_t i = 0; i < nk; ++i) {
+      PyObject* o = PyUnicode_FromStringAndSize(buf.data() + s, (Py_ssize_t)(ends[i] - s));
+      if (!o) throw py::error_already_set();
+      PyList_SET_ITEM(out.ptr(), (Py_ssize_t)i, o);
+      s = ends[i];
+    }
+    return out;
+  });
+
   // Value round trips through the reference's text hand-offs: "%5.10f"
   // (final.gamma / final.beta read back by lda_post.py) and Python-2 str
   // (doc_results.csv / word_results.csv read back by the Scala scorers).

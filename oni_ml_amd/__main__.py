@@ -20,7 +20,15 @@ if cli.FAST_EXIT:
     sys.stdout.flush()
     sys.stderr.flush()
     if cli.EXIT_MARK:   # a timing parent (ONI_T_SPAWN): wall-clock time of the exit call, the rest is teardown
+        t_exit = time.time()
+        st = {}
+        try:
+            with open("/proc/self/status") as f:
+                st = {k: v.split()[0] for k, v in (ln.split(":", 1) for ln in f if ":" in ln)
+                      if k in ("VmRSS", "VmHWM", "RssAnon", "RssFile", "RssShmem", "VmPin", "Threads")}
+        except OSError:
+            pass
         with open(cli.EXIT_MARK, "w") as f:
-            f.write(repr(time.time()))
+            f.write(repr(t_exit) + " " + " ".join(f"{k}={v}" for k, v in sorted(st.items())))
     os._exit(rc or 0)
 sys.exit(rc)

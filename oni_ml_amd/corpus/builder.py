@@ -24,6 +24,7 @@ from typing import List, Optional, Sequence, Tuple
 import numpy as np
 import torch
 
+from ..ops import sortgroup as SG
 from .csr import Corpus
 
 _SHIFT = 32
@@ -54,8 +55,7 @@ def count_pairs(doc: torch.Tensor, word: torch.Tensor, weight: Optional[torch.Te
         raise ValueError("word keys must fit in 32 bits")
     pk = (doc.to(torch.int64) << _SHIFT) | word.to(torch.int64)
     if weight is None:
-        uniq, cnt = torch.unique(pk, sorted=True, return_counts=True)
-        cnt = cnt.to(torch.int64)
+        uniq, cnt = SG.unique(pk, return_counts=True)
     else:
         uniq, cnt = segment_sums(pk, weight.to(device=pk.device, dtype=torch.int64))
     return DocWordCounts(uniq >> _SHIFT, uniq & ((1 << _SHIFT) - 1), cnt)
@@ -64,13 +64,8 @@ def count_pairs(doc: torch.Tensor, word: torch.Tensor, weight: Optional[torch.Te
 def segment_sums(keys: torch.Tensor, w: torch.Tensor):
     """(sorted distinct keys, sum of w per key) by a radix sort and a prefix sum -- no atomics, so
     heavily repeated keys (a handful of port words, hour-of-day values) cost nothing extra; an
-    int64 index_add_ over them serialises on a few contended addresses."""
-    sk, perm = torch.sort(keys)
-    uniq, counts = torch.unique_consecutive(sk, return_counts=True)
-    cw = torch.cumsum(w[perm], 0)
-    ends = torch.cumsum(counts, 0) - 1
-    tot = cw[ends]
-    return uniq, torch.diff(tot, prepend=tot.new_zeros(1))
+    int64 index_add_ over them serialises on a few contended addresses (ops/sortgroup.py)."""
+    return SG.segment_sums(keys, w)
 
 
 def concat(parts: Sequence[DocWordCounts], merge: bool = False) -> DocWordCounts:
@@ -86,16 +81,17 @@ def concat(parts: Sequence[DocWordCounts], merge: bool = False) -> DocWordCounts
 def _first_appearance_ids(keys: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
     """ids[i] = rank of keys[i]'s first appearance; returns (ids, distinct keys in rank order)."""
     # stable sort: the first element of each run of equal keys is the key's first appearance
-    sk, perm = torch.sort(keys, stable=True)
-    uniq, counts = torch.unique_consecutive(sk, return_counts=True)
-    starts = torch.cumsum(counts, 0) - counts
-    first = perm[starts]
+    # (ops/sortgroup.py: the group of every sorted position from a prefix sum, no repeat_interleave)
+    sk, perm = SG.sort_stable(keys)
+    grp, G = SG.run_ids(sk)
+    st = SG.run_starts(grp, G)[:-1]
+    first = SG.gather(perm, st)
     inv = torch.empty_like(perm)
-    inv[perm] = torch.repeat_interleave(torch.arange(uniq.numel(), device=keys.device), counts)
-    order = torch.argsort(first)
+    inv[perm] = grp
+    order = torch.sort(first).indices          # first appearances are distinct: any sort is the stable one
     rank = torch.empty_like(order)
     rank[order] = torch.arange(order.numel(), device=keys.device)
-    return rank[inv], uniq[order]
+    return SG.gather(rank, inv), SG.gather(SG.gather(sk, st), order)
 
 
 @dataclass
@@ -112,15 +108,15 @@ def lda_pre(dwc: DocWordCounts) -> BuiltCorpus:
     wid, wkeys = _first_appearance_ids(dwc.word)
     did, dkeys = _first_appearance_ids(dwc.doc)
     order = torch.sort(did, stable=True).indices
-    d_sorted = did[order]
+    d_sorted = SG.gather(did, order)
     D = int(dkeys.numel())
     # d_sorted is sorted: the CSR offsets are a binary search per document (a bincount would be
     # an atomic histogram over the entries)
     ptr = torch.searchsorted(d_sorted, torch.arange(D + 1, device=d_sorted.device, dtype=d_sorted.dtype))
     corpus = Corpus(
         doc_ptr=ptr.cpu().numpy(),
-        word_idx=wid[order].to(torch.int32).cpu().numpy(),
-        counts=dwc.count[order].cpu().numpy(),
+        word_idx=SG.gather(wid, order).to(torch.int32).cpu().numpy(),
+        counts=SG.gather(dwc.count, order).cpu().numpy(),
         num_terms=int(wkeys.numel()),
     )
     return BuiltCorpus(corpus, dkeys.cpu().numpy(), wkeys.cpu().numpy())

@@ -131,11 +131,11 @@ class DeviceCorpus:
         cnt = torch.from_numpy(c.counts).to(dev).to(torch.float32)
         ws, perm = torch.sort(w, stable=True)
         wptr = torch.searchsorted(ws, torch.arange(V + 1, device=dev, dtype=ws.dtype))
-        doc_of = torch.repeat_interleave(torch.arange(D, device=dev, dtype=torch.int32),
-                                         (ptr[1:] - ptr[:-1]), output_size=c.nnz)
-        wlen = torch.diff(wptr).cpu().numpy().astype(np.int64)
+        from ..ops import sortgroup as SG
+        doc_of = SG.segment_ids(ptr[1:] - ptr[:-1], total=c.nnz).to(torch.int32)   # (no repeat_interleave)
+        wlen = (wptr[1:] - wptr[:-1]).cpu().numpy().astype(np.int64)
         return DeviceCorpus(
             doc_ptr=ptr.to(torch.int32), word_idx=w.to(torch.int32), counts=cnt,
-            word_ptr=wptr.to(torch.int32), csc_ent=perm.to(torch.int32), csc_doc=doc_of[perm],
+            word_ptr=wptr.to(torch.int32), csc_ent=perm.to(torch.int32), csc_doc=SG.gather(doc_of, perm),
             num_docs=D, num_terms=V, nnz=c.nnz, doc_len=lens.astype(np.int64), word_len=wlen,
         )

@@ -53,12 +53,18 @@ class FlowWordSpace:
         """Index of each value in `ports` (-1 if absent)."""
         p = torch.from_numpy(self.ports).to(word_port.device)
         i = torch.searchsorted(p, word_port).clamp_max(max(p.numel() - 1, 0))
-        ok = p[i] == word_port if p.numel() else torch.zeros_like(word_port, dtype=torch.bool)
+        ok = p.index_select(0, i) == word_port if p.numel() else torch.zeros_like(word_port, dtype=torch.bool)
         return torch.where(ok, i, torch.full_like(i, -1))
 
     def decode(self, keys: np.ndarray) -> List[str]:
         """Word strings of ``keys``: one concatenation per word of a head ("[-1_]<port>_", one per
-        (port, side)) and a tail ("<time>_<ibyt>_<ipkt>", one per bin triple), both built once."""
+        (port, side)) and a tail ("<time>_<ibyt>_<ipkt>", one per bin triple), both built once
+        (csrc/native/bind_native.cpp flow_word_names; ``decode_py`` is the Python form, its test oracle)."""
+        from ..ops import native
+        return native.lib().flow_word_names(np.asarray(self.ports, np.float64), self.NT, self.NB, self.NP,
+                                            np.asarray(keys, np.int64))
+
+    def decode_py(self, keys: np.ndarray) -> List[str]:
         k = np.asarray(keys, np.int64)
         prefix = k % 2
         k = k // 2
@@ -130,7 +136,8 @@ def featurize(ft: FlowTable, device, cuts: Optional[Dict[str, np.ndarray]] = Non
 
 
 def word_space_for(feat: FlowFeatures) -> FlowWordSpace:
-    ports = torch.unique(feat.word_port).cpu().numpy()
+    from ..ops import sortgroup as SG
+    ports = SG.unique(feat.word_port).cpu().numpy()
     return FlowWordSpace(ports, len(feat.cuts["time"]) + 1, len(feat.cuts["ibyt"]) + 1, len(feat.cuts["ipkt"]) + 1)
 
 

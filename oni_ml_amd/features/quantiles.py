@@ -29,12 +29,11 @@ def ecdf_cuts(values: torch.Tensor, quantiles: Sequence[float], weights: Optiona
     q = torch.tensor(list(quantiles), dtype=torch.float64, device=v.device)
     if v.numel() == 0:
         return torch.zeros_like(q)
+    from ..ops import sortgroup as SG
     if weights is None:
-        uniq, counts = torch.unique(v, sorted=True, return_counts=True)
-        counts = counts.to(torch.int64)
+        uniq, counts = SG.unique(v, return_counts=True)
     else:
-        from ..corpus.builder import segment_sums
-        uniq, counts = segment_sums(v, weights.to(device=v.device, dtype=torch.int64).reshape(-1))
+        uniq, counts = SG.segment_sums(v, weights.to(device=v.device, dtype=torch.int64).reshape(-1))
     return ecdf_cuts_from_hist(uniq, counts, quantiles)
 
 
@@ -49,8 +48,10 @@ def ecdf_cuts_from_hist(uniq: torch.Tensor, counts: torch.Tensor, quantiles: Seq
     F = cum.to(torch.float64) / cum[-1].to(torch.float64)
     # largest index with F < q  (F is non-decreasing)
     idx = torch.searchsorted(F, q, right=False) - 1
-    cand = torch.where(idx >= 0, uniq[idx.clamp_min(0)], torch.zeros_like(q))
-    return torch.maximum(cand, torch.zeros_like(q))
+    cand = torch.where(idx >= 0, uniq.index_select(0, idx.clamp_min(0)), torch.zeros_like(q))
+    # max(cand, 0) as a select: torch.maximum's first call costs a cold process 120 ms (ops/sortgroup.py);
+    # the same bits (+0.0 for cand <= 0, -0.0 included; cand is never NaN: F(NaN) = 1 >= q)
+    return torch.where(cand > 0, cand, torch.zeros_like(q))
 
 
 def ecdf_cuts_reference(values, quantiles, weights=None) -> np.ndarray:

@@ -504,14 +504,11 @@ def gs_suff64(word_ptr, csc_ent, plan: "SuffPlan", cphi, cw, part, gate=None, sc
 def csc_subset(word_ptr, csc_ent, csc_doc, doc_mask):
     """(word_ptr, csc_ent) of the CSC slots whose document is in ``doc_mask`` (bool [D], device), slot
     order kept; plus the per-word entry counts on the host (for a SuffPlan)."""
-    V = word_ptr.numel() - 1
-    keep = doc_mask[csc_doc.long()]
-    wlen = (word_ptr[1:] - word_ptr[:-1]).long()
-    word_of = torch.repeat_interleave(torch.arange(V, device=word_ptr.device), wlen)
-    cnt = torch.bincount(word_of[keep], minlength=V)
-    ptr = torch.zeros(V + 1, dtype=torch.int64, device=word_ptr.device)
-    ptr[1:] = torch.cumsum(cnt, 0)
-    return ptr.to(torch.int32), csc_ent[keep].contiguous(), cnt.cpu().numpy()
+    from . import sortgroup as SG
+    keep = SG.gather(doc_mask, csc_doc)
+    ce, before = SG.compact(csc_ent, keep)       # before[s]: kept slots ahead of slot s
+    ptr = SG.gather(before, word_ptr)            # word w's kept slots start where its slots do
+    return ptr.to(torch.int32), ce.contiguous(), (ptr[1:] - ptr[:-1]).cpu().numpy()
 
 
 def suff_group_plan(lens, V: int):
@@ -551,15 +548,16 @@ def csc_compact(word_ptr, csc_ent, words):
     """(word_ptr, csc_ent) of the CSC columns ``words`` (host ids), renumbered 0 .. len(words) - 1, slot
     order kept (a compact sub-CSC for a gs_suff64 pass into a scratch of len(words) rows)."""
     import numpy as np
+    from . import sortgroup as SG
     dev = word_ptr.device
     w = torch.from_numpy(np.asarray(words, np.int64)).to(dev)
-    st = word_ptr[w].long()
-    ln = word_ptr[w + 1].long() - st
+    st = SG.gather(word_ptr, w).long()
+    ln = SG.gather(word_ptr, w + 1).long() - st
     ptr = torch.zeros(w.numel() + 1, dtype=torch.int64, device=dev)
     ptr[1:] = torch.cumsum(ln, 0)
     tot = int(ptr[-1])
-    idx = torch.repeat_interleave(st - ptr[:-1], ln) + torch.arange(tot, device=dev)
-    return ptr.to(torch.int32), csc_ent[idx].contiguous()
+    idx = SG.gather(st - ptr[:-1], SG.segment_ids(ln, tot)) + torch.arange(tot, device=dev)
+    return ptr.to(torch.int32), SG.gather(csc_ent, idx).contiguous()
 
 
 def gs_mstep_control(cw, class_total, beta, K, scalars, params, ctl, hist, done_count, rows=None, newton=None,

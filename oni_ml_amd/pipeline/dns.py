@@ -151,7 +151,8 @@ def score_dns(cfg, tab: FD.DnsTable, top, tables: C.ModelTables, device, log=pri
         cuts = FDD.global_cuts(ctx, tab, top, device, raw_only=True, threads=cfg.threads)
     feat = FD.featurize(tab, device, top, cuts=cuts, raw_only=True, threads=cfg.threads, host=host)
     wsp = FD.DnsWordSpace(feat.cuts, feat.qpairs)
-    uk, inv = torch.unique(feat.word_key, return_inverse=True)
+    from ..ops import sortgroup as SG
+    uk, inv = SG.unique(feat.word_key, return_inverse=True)
     unames = wsp.decode(uk.cpu().numpy())
     if ip_map is not None:
         m = np.asarray(ip_map, np.int64)[:len(feat.ip_names)]
@@ -160,8 +161,8 @@ def score_dns(cfg, tab: FD.DnsTable, top, tables: C.ModelTables, device, log=pri
         m = np.fromiter((di.get(n, -1) for n in feat.ip_names), dtype=np.int64, count=len(feat.ip_names))
     # the rows these queries reference: the whole tables (one process) or fetched from their ranks
     th, ph, drow, wrow = tables.compact(m, tables.word_rows(unames))
-    widx = torch.from_numpy(wrow).to(device)[inv]
-    didx = torch.from_numpy(drow).to(device)[feat.ip]
+    widx = SG.gather(torch.from_numpy(wrow).to(device), inv)
+    didx = SG.gather(torch.from_numpy(drow).to(device), feat.ip)
     K = tables.K
     if cfg.strict and K != 20:
         raise ValueError("compat=strict scores over exactly 20 topics (dns_post_lda.scala:316)")

@@ -21,6 +21,7 @@ import torch
 
 from ..corpus.builder import concat, count_pairs, lda_pre
 from ..features import flow as FF
+from ..ops import sortgroup as SG
 from ..score import scorer as S
 from . import common as C
 from . import prefetch
@@ -200,7 +201,7 @@ def score_flow(cfg, ft: FF.FlowTable, tables: C.ModelTables, device, log=print, 
     ws = tables.key_space if fast else FF.word_space_for(feat)
     src, dst = FF.word_keys(feat, ws)
     both = torch.cat([src, dst])
-    uk, inv = torch.unique(both, return_inverse=True)
+    uk, inv = SG.unique(both, return_inverse=True)
     uk_np = uk.cpu().numpy()
     if fast:
         wk = np.asarray(tables.word_keys, np.int64)
@@ -216,28 +217,28 @@ def score_flow(cfg, ft: FF.FlowTable, tables: C.ModelTables, device, log=print, 
         ip_rows = np.fromiter((tables.doc_index().get(n, -1) for n in ipn), dtype=np.int64, count=len(ipn))
     # the rows these events reference: the whole tables (one process) or fetched from their ranks
     th, ph, drow, wrow = tables.compact(ip_rows, word_rows)
-    widx = torch.from_numpy(wrow).to(device)[inv]
+    widx = SG.gather(torch.from_numpy(wrow).to(device), inv)
     w_src, w_dst = widx[: src.numel()], widx[src.numel():]
     didx = torch.from_numpy(drow).to(device)
     K = tables.K
     if cfg.strict and K != 20:
         raise ValueError("compat=strict scores over exactly 20 topics (flow_post_lda.scala:232)")
     model = S.TopicModel.build(th, ph, S.default_value("flow", K, cfg.strict), device)
-    sa, sb, key, flag = S.score(model, didx[feat.sip.long()], w_src, didx[feat.dip.long()], w_dst, cfg.tol)
+    sa, sb, key, flag = S.score(model, SG.gather(didx, feat.sip), w_src, SG.gather(didx, feat.dip), w_dst, cfg.tol)
     qs = S.key_quantiles(key)
     order = S.rank_flagged(key, flag)
     n = int(order.size)
     out = os.path.join(cfg.lpath, "flow_results.csv")
     # output columns: 27 raw + time + ibyt_bin + ipkt_bin + time_bin + word_port + ip_pair + src/dest word + scores
     o_t = torch.from_numpy(order).to(device)
-    inv_src = inv[: src.numel()][o_t].cpu().numpy().astype(np.int32)
-    inv_dst = inv[src.numel():][o_t].cpu().numpy().astype(np.int32)
+    inv_src = SG.gather(inv[: src.numel()], o_t).cpu().numpy().astype(np.int32)
+    inv_dst = SG.gather(inv[src.numel():], o_t).cpu().numpy().astype(np.int32)
     if unames is None:      # names only for the words of the flagged rows
         need = np.unique(np.concatenate([inv_src, inv_dst]))
         unames = ws.decode(uk_np[need])
         inv_src = np.searchsorted(need, inv_src).astype(np.int32)
         inv_dst = np.searchsorted(need, inv_dst).astype(np.int32)
-    sel = lambda t: t[o_t].cpu().numpy()
+    sel = lambda t: SG.gather(t, o_t).cpu().numpy()
     cols = [
         ("table", ft.table, order),
         ("java", sel(feat.time)),

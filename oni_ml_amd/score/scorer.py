@@ -69,11 +69,12 @@ def key_quantiles(key: torch.Tensor, qs=(1e-4, 1e-3, 1e-2, 0.1, 0.5), sample: in
 
 def rank_flagged(key: torch.Tensor, flag: torch.Tensor) -> torch.Tensor:
     """Indices of flagged rows in ascending key order (stable) as an int64 host array."""
-    sel = torch.nonzero(flag.to(torch.bool), as_tuple=False).reshape(-1)
+    from ..ops import sortgroup as SG
+    sel, _ = SG.compact(torch.arange(flag.numel(), device=flag.device), flag.reshape(-1).to(torch.bool))
     if sel.numel() == 0:
         return np.zeros(0, np.int64)
-    order = torch.sort(key[sel], stable=True).indices
-    return sel[order].cpu().numpy().astype(np.int64)
+    order = SG.sort_stable(SG.gather(key, sel))[1]
+    return SG.gather(sel, order).cpu().numpy().astype(np.int64)
 
 
 def lookup_sorted(keys_sorted: torch.Tensor, values_idx: torch.Tensor, query: torch.Tensor) -> torch.Tensor:

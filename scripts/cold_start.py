@@ -33,7 +33,9 @@ INPUT = []     # the source's input flags (main)
 
 def _child(tmp, tag, tol, extra_env=None, pyflags=(), source="flow"):
     lpath = os.path.join(tmp, tag)
-    env = dict(os.environ, PYTHONPATH=ROOT, **(extra_env or {}))
+    extra_env = dict(extra_env or {})
+    root = os.path.abspath(extra_env.pop("ROOT", ROOT))   # a variant's own copy of the package (A/B of host code)
+    env = dict(os.environ, PYTHONPATH=root, **extra_env)
     for k in ("FLOW_PATH", "DNS_PATH", "LPATH", "TOL"):
         env.pop(k, None)
     cmd = [sys.executable, *pyflags, "-m", "oni_ml_amd", "ml_ops", "20160122", source, repr(tol), "--lpath", lpath,
@@ -42,7 +44,7 @@ def _child(tmp, tag, tol, extra_env=None, pyflags=(), source="flow"):
     t_spawn = time.time()
     env["ONI_T_SPAWN"] = repr(t_spawn)
     t0 = time.perf_counter()
-    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
+    r = subprocess.run(cmd, cwd=root, env=env, capture_output=True, text=True, timeout=600)
     wall = time.perf_counter() - t0
     if r.returncode != 0:
         raise RuntimeError(f"{tag}: rc {r.returncode}\n{r.stderr[-3000:]}")
@@ -50,7 +52,9 @@ def _child(tmp, tag, tol, extra_env=None, pyflags=(), source="flow"):
         sm = json.load(f)
     try:   # the os._exit call (FAST_EXIT): what is left of the wall after it is process teardown
         with open(mark) as f:
-            sm.setdefault("startup_marks", {})["exit_call"] = round(float(f.read()) - t_spawn, 4)
+            ex = f.read().split()
+        sm.setdefault("startup_marks", {})["exit_call"] = round(float(ex[0]) - t_spawn, 4)
+        sm["exit_status"] = dict(kv.split("=", 1) for kv in ex[1:])
     except (OSError, ValueError):
         pass
     return wall, sm, r.stderr
@@ -60,6 +64,7 @@ def _variants(spec):
     out = []
     for v in spec.split(";"):
         v = v.strip()
+        # KEY=VALUE settings; ROOT=<dir>: run that directory's copy of the package
         env = {} if v in ("", "default") else dict(kv.split("=", 1) for kv in v.split())
         out.append((v or "default", env))
     return out
@@ -113,7 +118,7 @@ def main():
         for i, (tag, env) in enumerate(variants):
             wall, sm, _ = _child(tmp, f"run{i}", a.tol, extra_env=env, source=a.source)
             runs.append(dict(variant=tag, wall_s=round(wall, 3), inprocess_s=round(sm["wall_seconds"], 3),
-                             marks=sm.get("startup_marks"),
+                             marks=sm.get("startup_marks"), exit=sm.get("exit_status"),
                              stages={k: round(v, 3) for k, v in sm["stage_seconds"].items()},
                              flagged=sm.get("scored")))
             print(json.dumps(runs[-1]), flush=True)
@@ -137,11 +142,11 @@ def main():
             json.dump(rec, f, indent=1)
     if a.md:
         L = [f"# Cold `ml_ops` process, 1-day {a.source} ({a.events} events)", "",
-             "| run | variant | spawn -> exit s | in-process s | start-up marks (s after spawn) | stages s | flagged |",
-             "|---|---|---|---|---|---|---|"]
+             "| run | variant | spawn -> exit s | in-process s | start-up marks (s after spawn) | stages s | flagged | at exit (kB) |",
+             "|---|---|---|---|---|---|---|---|"]
         for i, r in enumerate(runs):
             L.append(f"| {i} | {r['variant']} | {r['wall_s']} | {r['inprocess_s']} | {r['marks']} | {r['stages']} | "
-                     f"{r['flagged']} |")
+                     f"{r['flagged']} | {r.get('exit')} |")
         for v in dict.fromkeys(r["variant"] for r in runs):
             w = sorted(r["wall_s"] for r in runs if r["variant"] == v)
             L.append(f"\nmedian spawn -> exit, {v}: {w[len(w) // 2]} s ({len(w)} runs)")

@@ -54,6 +54,20 @@ def test_qtiles_roundtrip():
 PORTS = [0, 1, 22, 53, 80, 443, 1023, 1024, 1025, 8080, 49152, 65535]
 
 
+def test_flow_word_names_native_matches_python():
+    """FlowWordSpace.decode (native flow_word_names) against its Python form: ports with Java formatting
+    edge cases (negative, -0.0, exponent forms, fractions), every prefix / bin, a key past the space refused."""
+    ports = np.unique(np.array([-1.0, -0.0, 0.0, 0.5, 3.0, 80.0, 443.0, 65535.0, 1e7, 1.5e-3, 123456789.0]))
+    ports = np.concatenate([ports, [-0.0]]) if not np.signbit(ports).any() else ports
+    ws = FF.FlowWordSpace(np.sort(ports), 11, 11, 6)
+    keys = np.arange(ports.size * 11 * 11 * 6 * 2, dtype=np.int64)
+    assert ws.decode(keys) == ws.decode_py(keys)
+    assert ws.decode(keys[::-7]) == ws.decode_py(keys[::-7])
+    assert ws.decode(np.zeros(0, np.int64)) == []
+    with pytest.raises(IndexError):
+        ws.decode(np.array([keys.size], np.int64))
+
+
 def test_flow_words_all_port_cases():
     a, b = np.meshgrid(np.array(PORTS, np.float64), np.array(PORTS, np.float64))
     a, b = a.ravel(), b.ravel()
