@@ -197,7 +197,9 @@ def _e2e_cold(args, ctx, tmp):
                MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), PYTHONPATH=ROOT + os.pathsep + env.get("PYTHONPATH", ""))
     if args.device == "cpu":
         env["ONI_DIST_BACKEND"] = "gloo"
-    cmd = [sys.executable, "-m", "oni_ml_amd", "ml_ops", "20160122", "flow", repr(float(args.e2e_tol)),
+    # through the deployment launcher (scripts/ml_ops.sh: the reference's ml_ops.sh entry point and its
+    # process environment), which execs `python -m oni_ml_amd ml_ops ...`
+    cmd = ["bash", os.path.join(ROOT, "scripts", "ml_ops.sh"), "20160122", "flow", repr(float(args.e2e_tol)),
            "--lpath", lpath, "--flow-path", os.path.join(tmp, "in"), "--conf", os.path.join(tmp, "no-duxbay.conf"),
            "--gpus", str(ctx.world_size), "--topics", str(args.topics), "--backend", args.backend, "--quiet"]
     if args.device == "cuda":
@@ -218,7 +220,7 @@ def _e2e_cold(args, ctx, tmp):
         ctx.barrier()
         walls.append(ctx.allreduce_max(wall))
     first, wall = walls
-    out = dict(e2e_cold_wall_s=round(wall, 3), e2e_cold_first_wall_s=round(first, 3), e2e_cold_cmd=" ".join(cmd[1:6]))
+    out = dict(e2e_cold_wall_s=round(wall, 3), e2e_cold_first_wall_s=round(first, 3), e2e_cold_cmd=" ".join(["scripts/ml_ops.sh"] + cmd[2:5]))
     if ctx.rank == 0:
         try:
             with open(os.path.join(lpath, "run_summary.json")) as f:

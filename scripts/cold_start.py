@@ -38,8 +38,12 @@ def _child(tmp, tag, tol, extra_env=None, pyflags=(), source="flow"):
     env = dict(os.environ, PYTHONPATH=root, **extra_env)
     for k in ("FLOW_PATH", "DNS_PATH", "LPATH", "TOL"):
         env.pop(k, None)
-    cmd = [sys.executable, *pyflags, "-m", "oni_ml_amd", "ml_ops", "20160122", source, repr(tol), "--lpath", lpath,
-           "--conf", os.path.join(tmp, "none.conf"), "--quiet"] + INPUT
+    args = ["20160122", source, repr(tol), "--lpath", lpath, "--conf", os.path.join(tmp, "none.conf"), "--quiet"] + INPUT
+    launcher = os.path.join(root, "scripts", "ml_ops.sh")
+    if pyflags or not os.path.exists(launcher):
+        cmd = [sys.executable, *pyflags, "-m", "oni_ml_amd", "ml_ops"] + args
+    else:   # the deployment launcher (its process environment included), as bench.py's cold leg
+        cmd = ["bash", launcher] + args
     mark = os.path.join(lpath, ".exit_mark")
     t_spawn = time.time()
     env["ONI_T_SPAWN"] = repr(t_spawn)

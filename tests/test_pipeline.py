@@ -154,6 +154,22 @@ def test_cli_syntax_error():
     assert "ml_ops.sh syntax error" in r.stdout
 
 
+def test_launcher_environment(tmp_path):
+    """scripts/ml_ops.sh (bench.py's cold leg goes through it) execs the package with THP-backed malloc
+    (glibc.malloc.hugetlb=1, prepended to any GLIBC_TUNABLES already set) and reports the reference's
+    syntax error."""
+    shim = tmp_path / "python"
+    shim.write_text('#!/bin/bash\necho "TUNABLES=${GLIBC_TUNABLES}"\n')
+    shim.chmod(0o755)
+    env = dict(os.environ, PATH=f"{tmp_path}:{os.environ['PATH']}", GLIBC_TUNABLES="glibc.malloc.arena_max=2")
+    r = subprocess.run(["bash", os.path.join(ROOT, "scripts", "ml_ops.sh"), "20160122", "flow"], env=env,
+                       capture_output=True, text=True)
+    assert r.stdout.strip() == "TUNABLES=glibc.malloc.hugetlb=1:glibc.malloc.arena_max=2"
+    r = subprocess.run(["bash", os.path.join(ROOT, "scripts", "ml_ops.sh"), "2016", "flow"], capture_output=True,
+                       text=True)
+    assert "ml_ops.sh syntax error" in r.stdout
+
+
 def test_cli_end_to_end_and_lda_est(tmp_path):
     from oni_ml_amd.synth.flow import generate_flow_day
     generate_flow_day(str(tmp_path / "in") + "/", events=3000, seed=2, n_internal=200, n_external=300)
