@@ -20,15 +20,19 @@ def ecdf_cuts_np(values: np.ndarray, quantiles: Sequence[float], weights: Option
     if weights is None:
         counts = np.bincount(inv, minlength=uniq.size).astype(np.int64)
     else:
-        # integer weights: an exact int64 sum per distinct value (bincount's float64 sum is exact below 2^53,
-        # the int64 path keeps it exact everywhere)
-        counts = np.zeros(uniq.size, np.int64)
-        np.add.at(counts, inv, np.asarray(weights, np.int64).reshape(-1))
+        # integer weights: an exact sum per distinct value (bincount's float64 sum is exact while the day's
+        # total stays below 2^53; np.add.at, exact everywhere, takes ~10x longer)
+        w = np.asarray(weights, np.int64).reshape(-1)
+        if int(w.sum()) < (1 << 53):
+            counts = np.bincount(inv.reshape(-1), weights=w, minlength=uniq.size).astype(np.int64)
+        else:
+            counts = np.zeros(uniq.size, np.int64)
+            np.add.at(counts, inv, w)
     cum = np.cumsum(counts)
     F = cum.astype(np.float64) / np.float64(cum[-1])
     idx = np.searchsorted(F, q, side="left") - 1
     cand = np.where(idx >= 0, uniq[np.clip(idx, 0, None)], 0.0)
-    return np.maximum(cand, 0.0)
+    return np.where(cand > 0, cand, 0.0)     # max(cand, 0) as quantiles.ecdf_cuts takes it (-0.0 -> +0.0)
 
 
 # dns_pre_lda.scala's cuts: deciles of unix_tstamp and frame_len over every row, quintiles of the subdomain
@@ -55,3 +59,16 @@ def dns_cuts_np(values: dict, weight: np.ndarray, n: int, threads: int = 8) -> d
 
     with ThreadPoolExecutor(max(1, min(threads, len(DNS_CUT_COLUMNS)))) as ex:
         return dict(ex.map(one, DNS_CUT_COLUMNS))
+
+
+def flow_cuts_np(table, n: int) -> dict:
+    """flow_pre's cuts of the first ``n`` rows of a flow TextTable (features/flow.py featurize): deciles of
+    the time column (hour + minute / 60) + second / 3600 and of ibyt, quintiles of ipkt, weighted by the rows'
+    weights -- the same rule and bits as the device ``ecdf_cuts``."""
+    from .flow_io import C_HOUR, C_IBYT, C_IPKT, C_MIN, C_SEC
+    from .quantile_levels import DECILES, QUINTILES
+    w = np.asarray(table.weights()[:n], np.int64)
+    col = lambda c: np.asarray(table.numeric(c)[:n], np.float64)
+    time = (col(C_HOUR) + col(C_MIN) / 60) + col(C_SEC) / 3600
+    return dict(time=ecdf_cuts_np(time, DECILES, w), ibyt=ecdf_cuts_np(col(C_IBYT), DECILES, w),
+                ipkt=ecdf_cuts_np(col(C_IPKT), QUINTILES, w))

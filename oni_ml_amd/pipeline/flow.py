@@ -28,6 +28,13 @@ from . import prefetch
 from .runner import StageRunner
 
 
+def _host_cuts(ft, which: str):
+    """flow_pre's ("all") or flow_post's ("raw") cuts computed by the input prefetch (pipeline/prefetch.py
+    load_flow_inputs), or None."""
+    hc = getattr(ft, "host_cuts", None) if ft is not None else None
+    return hc.get(which) if hc else None
+
+
 def _word_names(ws: FF.FlowWordSpace, keys: np.ndarray):
     return ws.decode(keys)
 
@@ -58,7 +65,9 @@ def run(cfg, dist=None, device=None, log=print) -> dict:
     if need_pre:
         if rank == 0:
             with R.stage("flow_pre") as res:
-                feat = FF.featurize(ft, device, cuts=cfg.fixed_cuts())
+                # cuts: CUT, else those the input prefetch computed on the host, else the device ECDF
+                cuts = cfg.fixed_cuts()
+                feat = FF.featurize(ft, device, cuts=cuts if cuts is not None else _host_cuts(ft, "all"))
                 ws = FF.word_space_for(feat)
                 src, dst = FF.word_keys(feat, ws)
                 dwc = concat([count_pairs(feat.sip, src, feat.weight), count_pairs(feat.dip, dst, feat.weight)],
@@ -191,6 +200,8 @@ def score_flow(cfg, ft: FF.FlowTable, tables: C.ModelTables, device, log=print, 
         from ..features import flow_dist as FDS
         cols, w = FDS.table_columns(ft, ft.n_raw, torch.device(device))
         cuts = {k: v.cpu().numpy() for k, v in FDS.global_cuts(ctx, cols, w, device).items()}
+    if cuts is None and not multi:
+        cuts = _host_cuts(ft, "raw")
     feat = FF.featurize(ft, device, cuts=cuts, raw_only=True)
     # keys straight to φ rows when the tables carry this process's vocabulary (compat=fixed: names are
     # untruncated and unique, so key -> name -> row is key -> row; the cuts are the pre stage's, so the

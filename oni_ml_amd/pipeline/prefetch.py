@@ -185,12 +185,26 @@ def _start_dns_fork(key, args) -> bool:
     return True
 
 
+def load_flow_inputs(flow_path, feedback_path, dupfactor, threads=8, fixed_cuts=False):
+    """The flow table and, unless the run has fixed cuts (CUT), flow_pre's ECDF cuts of every row and
+    flow_post's of the raw rows computed on the host (features/cuts_host.py; the same bits as the device
+    rule): the stages then skip the device ECDF, whose first run in a process loaded ~0.2 s of torch kernels
+    (profiles/r6aj_cold_flow_pre.md).  Kept on ``FlowTable.host_cuts``."""
+    from ..features import cuts_host, flow_io
+    ft = flow_io.load_flow(flow_path, feedback_path, dupfactor, threads)
+    if not fixed_cuts:
+        cut_all = cuts_host.flow_cuts_np(ft.table, ft.n)
+        cut_raw = cut_all if ft.n_feedback == 0 else cuts_host.flow_cuts_np(ft.table, ft.n_raw)
+        ft.host_cuts = dict(all=cut_all, raw=cut_raw)
+    return ft
+
+
 def start_for(cfg, fork: bool = True) -> None:
     """Start the read of ``cfg``'s inputs (flow or dns).  ``fork=False`` (a profiler or tracer whose
     preloaded library may already hold the GPU, cli._tool_attached): the DNS read runs on a thread."""
     if cfg.dsource == "flow":
-        from ..features import flow_io
-        start(flow_key(cfg), flow_io.load_flow, cfg.flow_path, cfg.feedback_path(), cfg.dupfactor, cfg.threads)
+        start(flow_key(cfg), load_flow_inputs, cfg.flow_path, cfg.feedback_path(), cfg.dupfactor, cfg.threads,
+              cfg.fixed_cuts() is not None)
     elif cfg.dsource == "dns":
         args = (cfg.dns_path, cfg.feedback_path(), cfg.dupfactor, cfg.strict, cfg.top1m, cfg.threads)
         if not (fork and _start_dns_fork(dns_key(cfg), args)):

@@ -94,6 +94,43 @@ def test_flow_feedback_changes_corpus_weights(tmp_path):
     assert max(counts) >= 1000
 
 
+def test_prefetched_host_cuts_equal_device_rule(tmp_path):
+    """The input prefetch's host cuts (pipeline/prefetch.py load_flow_inputs) are bit for bit the stages'
+    own ECDF (quantiles.ecdf_cuts): every row weighted (feedback x DUPFACTOR) for flow_pre, the raw rows for
+    flow_post; and the pipeline's outputs are the same files with and without them."""
+    import torch
+    from oni_ml_amd.features import flow as FF
+    from oni_ml_amd.pipeline import prefetch
+    from oni_ml_amd.synth.flow import generate_flow_day, generate_flow_feedback
+    r = generate_flow_day(str(tmp_path / "in") + "/", events=4000, seed=9, n_internal=200, n_external=300)
+    rows = open(r["paths"][0]).read().splitlines()[1:]
+    os.makedirs(tmp_path / "ml", exist_ok=True)
+    generate_flow_feedback(str(tmp_path / "ml" / "flow_scores.csv"), rows, n=5)
+    ft = prefetch.load_flow_inputs(str(tmp_path / "in"), str(tmp_path / "ml" / "flow_scores.csv"), 1000, 2)
+    assert ft.n_feedback == 5
+    dev = FF.featurize(ft, torch.device("cpu"))
+    raw = FF.featurize(ft, torch.device("cpu"), raw_only=True)
+    for k in ("time", "ibyt", "ipkt"):
+        assert ft.host_cuts["all"][k].tobytes() == dev.cuts[k].tobytes(), k
+        assert ft.host_cuts["raw"][k].tobytes() == raw.cuts[k].tobytes(), k
+    assert any(ft.host_cuts["all"][k].tobytes() != ft.host_cuts["raw"][k].tobytes() for k in ("time", "ibyt", "ipkt"))
+    # the whole pipeline with the prefetched table (host cuts) and with its own read: the same files
+    outs = []
+    for tag, use in (("pre", True), ("own", False)):
+        lp = tmp_path / tag
+        os.makedirs(lp, exist_ok=True)
+        import shutil
+        shutil.copy(tmp_path / "ml" / "flow_scores.csv", lp / "flow_scores.csv")
+        cfg = CFG.resolve("20160122", "flow", tol=1e-2, conf_path=None, environ={}, lpath=str(lp),
+                          flow_path=str(tmp_path / "in"), backend="torch", threads=2, verbose=False)
+        cfg.settings = LDASettings(em_max_iter=2)
+        if use:
+            prefetch.start_for(cfg)
+        run(cfg, device="cpu", log=lambda *a, **k: None)
+        outs.append({f: (lp / f).read_bytes() for f in ("flow_results.csv", "model.dat", "words.dat", "flow_cuts.json")})
+    assert outs[0] == outs[1]
+
+
 def test_dns_pipeline(tmp_path):
     from oni_ml_amd.synth.dns import generate_dns_day
     r = generate_dns_day(str(tmp_path / "in"), events=6000, seed=3, files=3, n_names=800, n_clients=300)
