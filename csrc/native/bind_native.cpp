@@ -470,6 +470,56 @@ PYBIND11_MODULE(_oninative, m) {
     return out;
   });
 
+  // DNS word strings of mixed-radix word keys (features/dns.py DnsWordSpace.decode):
+  // key = ((top * r0 + d0) * r1 + d1 ...) * len(tail) + q -> "<top>_<d0>_<d1>..._<tail[q]>" (dns_pre_lda.scala's
+  // word: the top-domain flag, the five bins, the query-type / response-code pair).
+  m.def("radix_word_names", [](py::array_t<int64_t, py::array::c_style | py::array::forcecast> keys,
+                               std::vector<int64_t> radix, std::vector<std::string> tail) {
+    const int64_t nk = keys.size(), nq = std::max<int64_t>(1, (int64_t)tail.size());
+    for (int64_t r : radix)
+      if (r <= 0) throw std::invalid_argument("radix_word_names: radix must be positive");
+    const int64_t* k = keys.data();
+    std::string buf;
+    std::vector<int64_t> ends(nk);
+    {
+      py::gil_scoped_release rel;
+      buf.reserve((size_t)nk * 24);
+      std::vector<int64_t> d(radix.size());
+      char tmp[24];
+      for (int64_t i = 0; i < nk; ++i) {
+        int64_t x = k[i];
+        if (x < 0) throw std::out_of_range("radix_word_names: negative key");
+        const int64_t q = x % nq;
+        x /= nq;
+        for (size_t j = radix.size(); j-- > 0;) {
+          d[j] = x % radix[j];
+          x /= radix[j];
+        }
+        auto put = [&](int64_t v) {
+          auto r = std::to_chars(tmp, tmp + sizeof(tmp), v);
+          buf.append(tmp, r.ptr);
+        };
+        put(x);
+        for (int64_t v : d) {
+          buf += '_';
+          put(v);
+        }
+        buf += '_';
+        buf += tail.at((size_t)q);   // (no tail: out_of_range, as the Python form's IndexError)
+        ends[i] = (int64_t)buf.size();
+      }
+    }
+    py::list out(nk);
+    int64_t s = 0;
+    for (int64_t i = 0; i < nk; ++i) {
+      PyObject* o = PyUnicode_FromStringAndSize(buf.data() + s, (Py_ssize_t)(ends[i] - s));
+      if (!o) throw py::error_already_set();
+      PyList_SET_ITEM(out.ptr(), (Py_ssize_t)i, o);
+      s = ends[i];
+    }
+    return out;
+  });
+
   // Value round trips through the reference's text hand-offs: "%5.10f"
   // (final.gamma / final.beta read back by lda_post.py) and Python-2 str
   // (doc_results.csv / word_results.csv read back by the Scala scorers).

@@ -125,6 +125,13 @@ class DnsWordSpace:
         self.qpairs = list(qpairs)
 
     def decode(self, keys: np.ndarray) -> List[str]:
+        """Word strings of ``keys`` (csrc/native/bind_native.cpp radix_word_names; ``decode_py`` is the
+        Python form, its test oracle)."""
+        from ..ops import native
+        return native.lib().radix_word_names(np.asarray(keys, np.int64), [int(r) for r in self.radix],
+                                             list(self.qpairs))
+
+    def decode_py(self, keys: np.ndarray) -> List[str]:
         k = np.asarray(keys, np.int64)
         nq = max(1, len(self.qpairs))
         q = k % nq

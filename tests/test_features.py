@@ -68,6 +68,18 @@ def test_flow_word_names_native_matches_python():
         ws.decode(np.array([keys.size], np.int64))
 
 
+def test_dns_word_names_native_matches_python():
+    """DnsWordSpace.decode (native radix_word_names) against its Python form over the whole key space."""
+    from oni_ml_amd.features.dns import DnsWordSpace
+    cuts = {k: np.arange(n, dtype=np.float64) for k, n in (("frame_len", 9), ("unix_tstamp", 9),
+                                                            ("subdomain_length", 4), ("entropy", 3), ("num_periods", 4))}
+    ws = DnsWordSpace(cuts, ["1_0", "28_0", "1_3", "255_2"])
+    keys = np.arange(3 * 10 * 10 * 5 * 4 * 5 * 4, dtype=np.int64)
+    assert ws.decode(keys) == ws.decode_py(keys)
+    assert ws.decode(keys[::-13]) == ws.decode_py(keys[::-13])
+    assert ws.decode(np.zeros(0, np.int64)) == []
+
+
 def test_flow_words_all_port_cases():
     a, b = np.meshgrid(np.array(PORTS, np.float64), np.array(PORTS, np.float64))
     a, b = a.ravel(), b.ravel()
