@@ -8,8 +8,11 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
+#include <algorithm>
 #include <atomic>
 #include <charconv>
+#include <cstring>
+#include <limits>
 #include <thread>
 
 #include "corpus_io.h"
@@ -466,6 +469,82 @@ PYBIND11_MODULE(_oninative, m) {
       if (!o) throw py::error_already_set();
       PyList_SET_ITEM(out.ptr(), (Py_ssize_t)i, o);
       s = ends[i];
+    }
+    return out;
+  });
+
+  // ECDF cuts of float64 columns on the host, without the GIL (the flow input prefetch runs them while the
+  // main thread imports torch; numpy's unique held the GIL long enough to slow the import, r6ak):
+  // the rule and bits of features/quantiles.py ecdf_cuts -- values ordered by their int64 radix keys
+  // (-0.0 below +0.0, every NaN canonical and last, ties in row order), runs of equal values under
+  // `!=` (NaN never equal), exact int64 weight sums, F = cum / total in double, cut_q = the last run
+  // value with F < q, max(cut, 0) taken as a select.  One thread per column.
+  m.def("ecdf_cuts_cols", [](std::vector<py::array_t<double, py::array::c_style | py::array::forcecast>> cols,
+                             py::object weights, std::vector<std::vector<double>> levels) {
+    if (cols.size() != levels.size()) throw std::invalid_argument("ecdf_cuts_cols: one level list per column");
+    const size_t nc = cols.size();
+    std::vector<const double*> vp(nc);
+    std::vector<int64_t> n(nc);
+    for (size_t c = 0; c < nc; ++c) vp[c] = cols[c].data(), n[c] = cols[c].size();
+    const int64_t* w = nullptr;
+    py::array_t<int64_t, py::array::c_style | py::array::forcecast> wa;
+    if (!weights.is_none()) {
+      wa = py::array_t<int64_t, py::array::c_style | py::array::forcecast>::ensure(weights);
+      if (!wa) throw std::invalid_argument("ecdf_cuts_cols: int64 weights expected");
+      w = wa.data();
+      for (size_t c = 0; c < nc; ++c)
+        if (wa.size() < n[c]) throw std::invalid_argument("ecdf_cuts_cols: weights shorter than a column");
+    }
+    std::vector<std::vector<double>> out(nc);
+    {
+      py::gil_scoped_release rel;
+      auto one = [&](size_t c) {
+        const double* v = vp[c];
+        const int64_t N = n[c];
+        const std::vector<double>& q = levels[c];
+        std::vector<double>& res = out[c];
+        res.assign(q.size(), 0.0);
+        if (N == 0) return;
+        // (key, row) pairs: the stable order of the keys is the device sort's
+        std::vector<std::pair<int64_t, int64_t>> kr((size_t)N);
+        for (int64_t i = 0; i < N; ++i) {
+          double x = v[i];
+          if (x != x) x = std::numeric_limits<double>::quiet_NaN();
+          int64_t k;
+          std::memcpy(&k, &x, 8);
+          kr[(size_t)i] = {k < 0 ? (k ^ INT64_MAX) : k, i};
+        }
+        std::sort(kr.begin(), kr.end());
+        std::vector<double> uv;
+        std::vector<int64_t> cum;
+        int64_t acc = 0;
+        for (int64_t i = 0; i < N; ++i) {
+          const double x = v[kr[(size_t)i].second];
+          const bool fresh = i == 0 || x != v[kr[(size_t)i - 1].second];
+          if (fresh) {
+            if (i) cum.push_back(acc);
+            uv.push_back(x);
+          }
+          acc += w ? w[kr[(size_t)i].second] : 1;
+        }
+        cum.push_back(acc);
+        const double tot = (double)acc;
+        for (size_t j = 0; j < q.size(); ++j) {
+          // searchsorted(F, q, left) - 1: the last run with F < q
+          int64_t lo = 0, hi = (int64_t)cum.size();
+          while (lo < hi) {
+            const int64_t mid = (lo + hi) / 2;
+            if ((double)cum[(size_t)mid] / tot < q[j]) lo = mid + 1;
+            else hi = mid;
+          }
+          const double cand = lo - 1 >= 0 ? uv[(size_t)(lo - 1)] : 0.0;
+          res[j] = cand > 0 ? cand : 0.0;
+        }
+      };
+      std::vector<std::thread> th;
+      for (size_t c = 1; c < nc; ++c) th.emplace_back(one, c);
+      if (nc) one(0);
+      for (auto& t : th) t.join();
     }
     return out;
   });

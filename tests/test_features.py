@@ -68,6 +68,29 @@ def test_flow_word_names_native_matches_python():
         ws.decode(np.array([keys.size], np.int64))
 
 
+def test_native_ecdf_cuts_match_device_rule():
+    """native ecdf_cuts_cols (the flow prefetch's host cuts) against quantiles.ecdf_cuts bit for bit: ties,
+    NaN rows (each its own run, last), -0.0 / +0.0, weighted and unweighted, and the numpy oracle."""
+    from oni_ml_amd.features.cuts_host import ecdf_cuts_np
+    rng = np.random.default_rng(4)
+    for trial in range(4):
+        n = 20000
+        v = np.round(rng.normal(0, 3, n), 1)
+        if trial % 2:
+            v[rng.integers(0, n, 300)] = np.nan
+        v[:40], v[40:80] = -0.0, 0.0
+        w = rng.integers(1, 5, n).astype(np.int64)
+        w[:25] = 1000
+        c = native.lib().ecdf_cuts_cols([v, np.abs(v)], w, [list(DECILES), list(QUINTILES)])
+        assert np.asarray(c[0]).tobytes() == ecdf_cuts(torch.from_numpy(v), DECILES, torch.from_numpy(w)).numpy().tobytes()
+        assert np.asarray(c[1]).tobytes() == ecdf_cuts(torch.from_numpy(np.abs(v)), QUINTILES,
+                                                       torch.from_numpy(w)).numpy().tobytes()
+        assert np.asarray(c[0]).tobytes() == ecdf_cuts_np(v, DECILES, w).tobytes()
+        u = native.lib().ecdf_cuts_cols([v], None, [list(DECILES)])
+        assert np.asarray(u[0]).tobytes() == ecdf_cuts(torch.from_numpy(v), DECILES).numpy().tobytes()
+    assert list(native.lib().ecdf_cuts_cols([np.zeros(0)], None, [[0.5]])[0]) == [0.0]
+
+
 def test_dns_word_names_native_matches_python():
     """DnsWordSpace.decode (native radix_word_names) against its Python form over the whole key space."""
     from oni_ml_amd.features.dns import DnsWordSpace
