@@ -505,29 +505,71 @@ PYBIND11_MODULE(_oninative, m) {
         std::vector<double>& res = out[c];
         res.assign(q.size(), 0.0);
         if (N == 0) return;
-        // (key, row) pairs: the stable order of the keys is the device sort's
-        std::vector<std::pair<int64_t, int64_t>> kr((size_t)N);
+        // the runs of the device's sorted order without a sort of the rows: distinct values by hashing their
+        // int64 order keys (+0.0 and -0.0 one run under `!=`; the cut of either is +0.0), the distinct keys
+        // sorted, then every NaN row a run of its own, last, in row order (NaN != NaN)
+        // (open addressing, grown at half load: the table follows the distinct count, not the rows)
+        size_t cap = 1 << 12, used = 0;
+        int sh = 64 - __builtin_ctzll(cap);
+        std::vector<int64_t> hk(cap, INT64_MIN), hw(cap, 0);
+        auto slot = [&](int64_t k) {
+          size_t h = (size_t)(((uint64_t)k * 0x9E3779B97F4A7C15ull) >> sh);
+          while (hk[h] != INT64_MIN && hk[h] != k) h = (h + 1) & (cap - 1);
+          return h;
+        };
+        std::vector<int64_t> nan_w;
         for (int64_t i = 0; i < N; ++i) {
           double x = v[i];
-          if (x != x) x = std::numeric_limits<double>::quiet_NaN();
+          const int64_t wi = w ? w[i] : 1;
+          if (x != x) {
+            nan_w.push_back(wi);
+            continue;
+          }
+          if (x == 0.0) x = 0.0;
           int64_t k;
           std::memcpy(&k, &x, 8);
-          kr[(size_t)i] = {k < 0 ? (k ^ INT64_MAX) : k, i};
+          k = k < 0 ? (k ^ INT64_MAX) : k;
+          size_t h = slot(k);
+          if (hk[h] == INT64_MIN) {
+            if (2 * (used + 1) > cap) {   // grow, re-insert, and find k's slot again
+              std::vector<int64_t> ok(std::move(hk)), ow(std::move(hw));
+              cap <<= 1;
+              sh = 64 - __builtin_ctzll(cap);
+              hk.assign(cap, INT64_MIN);
+              hw.assign(cap, 0);
+              for (size_t j = 0; j < ok.size(); ++j)
+                if (ok[j] != INT64_MIN) {
+                  const size_t g = slot(ok[j]);
+                  hk[g] = ok[j];
+                  hw[g] = ow[j];
+                }
+              h = slot(k);
+            }
+            hk[h] = k;
+            ++used;
+          }
+          hw[h] += wi;
         }
-        std::sort(kr.begin(), kr.end());
+        std::vector<std::pair<int64_t, int64_t>> kw;
+        for (size_t h = 0; h < cap; ++h)
+          if (hk[h] != INT64_MIN) kw.emplace_back(hk[h], hw[h]);
+        std::sort(kw.begin(), kw.end());
         std::vector<double> uv;
         std::vector<int64_t> cum;
+        uv.reserve(kw.size() + nan_w.size());
+        cum.reserve(kw.size() + nan_w.size());
         int64_t acc = 0;
-        for (int64_t i = 0; i < N; ++i) {
-          const double x = v[kr[(size_t)i].second];
-          const bool fresh = i == 0 || x != v[kr[(size_t)i - 1].second];
-          if (fresh) {
-            if (i) cum.push_back(acc);
-            uv.push_back(x);
-          }
-          acc += w ? w[kr[(size_t)i].second] : 1;
+        for (const auto& e : kw) {
+          int64_t k = e.first < 0 ? (e.first ^ INT64_MAX) : e.first;
+          double x;
+          std::memcpy(&x, &k, 8);
+          uv.push_back(x);
+          cum.push_back(acc += e.second);
         }
-        cum.push_back(acc);
+        for (int64_t wi : nan_w) {
+          uv.push_back(std::numeric_limits<double>::quiet_NaN());
+          cum.push_back(acc += wi);
+        }
         const double tot = (double)acc;
         for (size_t j = 0; j < q.size(); ++j) {
           // searchsorted(F, q, left) - 1: the last run with F < q

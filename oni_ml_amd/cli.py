@@ -153,7 +153,7 @@ def cmd_ml_ops(argv):
     if (knobs.get("ONI_PREFETCH", "1") != "0" and a.gpus <= 1 and int(os.environ.get("WORLD_SIZE", "1")) == 1
             and not a.resume and not a.hdfs):
         try:
-            prefetch.start_for(resolve(1), fork=not _tool_attached())
+            prefetch.start_for(resolve(1), fork=not _tool_attached(), after_import=True)
         except Exception:  # noqa: BLE001 -- a bad configuration is reported by the resolve below
             pass
     try:
@@ -165,6 +165,8 @@ def cmd_ml_ops(argv):
 def _ml_ops_body(a, resolve):
     import torch  # noqa: F401  (its import time is a start-up mark of its own)
     MARKS["torch_imported"] = time.time()
+    from .pipeline import prefetch
+    prefetch.imported()
     from .models.lda.settings import LDASettings
     from .parallel import dist as D
     MARKS["package_imported"] = time.time()

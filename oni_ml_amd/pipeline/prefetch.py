@@ -17,6 +17,14 @@ import threading
 from typing import Callable, Dict, Optional, Tuple
 
 _JOBS: Dict[tuple, Tuple[threading.Thread, dict]] = {}
+# set by cli once `import torch` is done: host work beside the import slows it (its page faults and
+# allocations contend with the import's; the flow cuts beside it cost the import ~0.1 s, r6am), so the
+# flow cuts wait for it and overlap the HIP runtime's start instead
+_IMPORTED = threading.Event()
+
+
+def imported() -> None:
+    _IMPORTED.set()
 
 
 def flow_key(cfg) -> tuple:
@@ -185,13 +193,15 @@ def _start_dns_fork(key, args) -> bool:
     return True
 
 
-def load_flow_inputs(flow_path, feedback_path, dupfactor, threads=8, fixed_cuts=False):
+def load_flow_inputs(flow_path, feedback_path, dupfactor, threads=8, fixed_cuts=False, after_import=False):
     """The flow table and, unless the run has fixed cuts (CUT), flow_pre's ECDF cuts of every row and
     flow_post's of the raw rows computed on the host (features/cuts_host.py; the same bits as the device
     rule): the stages then skip the device ECDF, whose first run in a process loaded ~0.2 s of torch kernels
     (profiles/r6aj_cold_flow_pre.md).  Kept on ``FlowTable.host_cuts``."""
     from ..features import cuts_host, flow_io
     ft = flow_io.load_flow(flow_path, feedback_path, dupfactor, threads)
+    if after_import:
+        _IMPORTED.wait(timeout=60.0)
     if not fixed_cuts:
         cut_all = cuts_host.flow_cuts_np(ft.table, ft.n)
         cut_raw = cut_all if ft.n_feedback == 0 else cuts_host.flow_cuts_np(ft.table, ft.n_raw)
@@ -199,12 +209,13 @@ def load_flow_inputs(flow_path, feedback_path, dupfactor, threads=8, fixed_cuts=
     return ft
 
 
-def start_for(cfg, fork: bool = True) -> None:
+def start_for(cfg, fork: bool = True, after_import: bool = False) -> None:
     """Start the read of ``cfg``'s inputs (flow or dns).  ``fork=False`` (a profiler or tracer whose
-    preloaded library may already hold the GPU, cli._tool_attached): the DNS read runs on a thread."""
+    preloaded library may already hold the GPU, cli._tool_attached): the DNS read runs on a thread.
+    ``after_import``: the flow cuts wait for ``imported()`` (the caller imports torch meanwhile)."""
     if cfg.dsource == "flow":
         start(flow_key(cfg), load_flow_inputs, cfg.flow_path, cfg.feedback_path(), cfg.dupfactor, cfg.threads,
-              cfg.fixed_cuts() is not None)
+              cfg.fixed_cuts() is not None, after_import)
     elif cfg.dsource == "dns":
         args = (cfg.dns_path, cfg.feedback_path(), cfg.dupfactor, cfg.strict, cfg.top1m, cfg.threads)
         if not (fork and _start_dns_fork(dns_key(cfg), args)):

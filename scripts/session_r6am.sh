@@ -1,0 +1,17 @@
+# final-tree record: all GPU tests, smoke, default bench (cold leg through scripts/ml_ops.sh), rocprof of the
+# headline; then the cold ml_ops A/B: native host cuts / numpy host cuts (abvar/base) / device cuts (abvar/nocuts)
+set -u -o pipefail
+cd /tmp && export TMPDIR=/tmp
+cd "$GRAFT_REPO_ROOT"
+export TAG=r6am
+bash scripts/gpu.sh tests smoke bench prof || exit $?
+O=gpurun_out/r6am
+timeout -k 10 700 python -u scripts/cold_start.py --reps 4 --variants "default;ROOT=abvar/base;ROOT=abvar/nocuts" --md $O/cold_ab.md --json $O/cold_ab.json > $O/cold_ab.log 2>&1 || exit 1
+grep median $O/cold_ab.md
+python - <<'PY'
+import json
+d = json.load(open("gpurun_out/r6am/cold_ab.json"))
+for r in d["runs"]:
+    m = r["marks"]
+    print(f'{r["variant"][:18]:20s} wall {r["wall_s"]} torch {m["torch_imported"]} pipe {m["pipeline_end"]-m["pipeline_start"]:.3f} exit+{r["wall_s"]-m.get("exit_call",0):.3f}', r["stages"])
+PY
