@@ -3,6 +3,7 @@ import importlib.util
 import os
 import subprocess
 import sys
+import time
 
 from oni_ml_amd.utils import pycache
 
@@ -42,8 +43,15 @@ def test_fast_exit_keeps_outputs(tmp_path):
         lp = tmp_path / f"out{v}"
         r = subprocess.run([sys.executable, "-m", "oni_ml_amd", "ml_ops", "20160122", "flow", "1e-3", "--lpath", str(lp),
                             "--flow-path", str(inp), "--conf", str(tmp_path / "none.conf"), "--quiet", "--backend", "cpu"],
-                           cwd=ROOT, env=dict(env, ONI_FAST_EXIT=v), capture_output=True, text=True, timeout=600)
+                           cwd=ROOT, env=dict(env, ONI_FAST_EXIT=v, ONI_T_SPAWN=repr(time.time())), capture_output=True,
+                           text=True, timeout=600)
         assert r.returncode == 0, r.stderr[-2000:]
+        # a timing parent (ONI_T_SPAWN) gets the time of the fast exit call and the memory then resident
+        mark = lp / ".exit_mark"
+        assert mark.exists() == (v == "1")
+        if v == "1":
+            t, *kv = mark.read_text().split()
+            assert float(t) > 0 and "RssAnon" in dict(x.split("=", 1) for x in kv)
         outs[v] = {f: (lp / f).read_bytes() for f in ("flow_results.csv", "doc_results.csv", "word_results.csv",
                                                       "final.gamma", "final.beta", "word-assignments.dat")}
     assert outs["1"] == outs["0"]
