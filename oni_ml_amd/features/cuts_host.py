@@ -43,19 +43,19 @@ DNS_CUT_COLUMNS = (("unix_tstamp", "deciles", False), ("frame_len", "deciles", F
 
 
 def dns_cuts_np(values: dict, weight: np.ndarray, n: int, threads: int = 8) -> dict:
-    """{column: cuts} over the first n rows (np.unique releases the GIL: the five columns on threads)."""
+    """{column: cuts} over the first n rows: the five columns on threads, each through the native
+    ``ecdf_cuts_cols`` (no GIL; bitwise ecdf_cuts_np, which took ~0.15 s a column at 2 M rows)."""
     from concurrent.futures import ThreadPoolExecutor
     from .quantile_levels import DECILES, QUINTILES
+    from ..ops import native
     w = np.asarray(weight[:n], np.int64)
 
     def one(spec):
         name, levels, positive = spec
         v = np.asarray(values[name][:n], np.float64)
-        q = DECILES if levels == "deciles" else QUINTILES
-        if positive:
-            m = v > 0
-            return name, ecdf_cuts_np(v[m], q, w[m])
-        return name, ecdf_cuts_np(v, q, w)
+        q = list(DECILES if levels == "deciles" else QUINTILES)
+        vv, ww = (v[v > 0], w[v > 0]) if positive else (v, w)
+        return name, np.asarray(native.lib().ecdf_cuts_cols([vv], ww, [q])[0], np.float64)
 
     with ThreadPoolExecutor(max(1, min(threads, len(DNS_CUT_COLUMNS)))) as ex:
         return dict(ex.map(one, DNS_CUT_COLUMNS))
