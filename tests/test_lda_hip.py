@@ -22,7 +22,7 @@ def test_device_convergence_matches_host_loop():
     res = []
     for batch in (1, 8):
         eng = LDAEngine(c, 20, LDASettings(em_max_iter=60, em_converged=2e-4), backend="hip", seed=9)
-        eng.max_batch = batch
+        eng.max_batch = eng.pipe_batch = batch   # (run() without saves batches by pipe_batch)
         r = eng.run()
         res.append((r.likelihoods, eng.alpha, eng.gather_gamma(), r.em_iterations))
     (L1, a1, g1, n1), (L8, a8, g8, n8) = res
