@@ -193,6 +193,11 @@ def _start_dns_fork(key, args) -> bool:
     return True
 
 
+# host cuts only for days up to this many rows: a cold start matters for a day's run; on a month (config 5,
+# 100 M rows) the device ECDF over the GPU's bandwidth beats hashing 100 M values per column on the host
+HOST_CUT_ROWS = 1 << 22
+
+
 def load_flow_inputs(flow_path, feedback_path, dupfactor, threads=8, fixed_cuts=False, after_import=False):
     """The flow table and, unless the run has fixed cuts (CUT), flow_pre's ECDF cuts of every row and
     flow_post's of the raw rows computed on the host (features/cuts_host.py; the same bits as the device
@@ -202,7 +207,7 @@ def load_flow_inputs(flow_path, feedback_path, dupfactor, threads=8, fixed_cuts=
     ft = flow_io.load_flow(flow_path, feedback_path, dupfactor, threads)
     if after_import:
         _IMPORTED.wait(timeout=60.0)
-    if not fixed_cuts:
+    if not fixed_cuts and ft.n <= HOST_CUT_ROWS:
         cut_all = cuts_host.flow_cuts_np(ft.table, ft.n)
         cut_raw = cut_all if ft.n_feedback == 0 else cuts_host.flow_cuts_np(ft.table, ft.n_raw)
         ft.host_cuts = dict(all=cut_all, raw=cut_raw)

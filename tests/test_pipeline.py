@@ -114,6 +114,14 @@ def test_prefetched_host_cuts_equal_device_rule(tmp_path):
         assert ft.host_cuts["all"][k].tobytes() == dev.cuts[k].tobytes(), k
         assert ft.host_cuts["raw"][k].tobytes() == raw.cuts[k].tobytes(), k
     assert any(ft.host_cuts["all"][k].tobytes() != ft.host_cuts["raw"][k].tobytes() for k in ("time", "ibyt", "ipkt"))
+    # a month-sized input keeps the device ECDF (HOST_CUT_ROWS)
+    lim = prefetch.HOST_CUT_ROWS
+    try:
+        prefetch.HOST_CUT_ROWS = ft.n - 1
+        big = prefetch.load_flow_inputs(str(tmp_path / "in"), str(tmp_path / "ml" / "flow_scores.csv"), 1000, 2)
+        assert getattr(big, "host_cuts", None) is None
+    finally:
+        prefetch.HOST_CUT_ROWS = lim
     # the whole pipeline with the prefetched table (host cuts) and with its own read: the same files
     outs = []
     for tag, use in (("pre", True), ("own", False)):
